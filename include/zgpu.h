@@ -1,0 +1,160 @@
+/*
+ * zgpu.h — C ABI of the MI355X-native Zarr chunk-decode codec pipeline (libzgpu.so).
+ *
+ * This is the drop-in boundary that a zarrs runtime codec plugin binds (see INTEGRATION.md for
+ * the Rust FFI stub). Plain pointers and sizes only; no torch or HIP types in any signature.
+ * Reference interfaces replaced (paths relative to the zarrs workspace root):
+ *
+ *   zgpu_chain_create   <- CodecChain::from_metadata + CodecChain::with_context
+ *                          (zarrs/src/array/codec/array_to_bytes/codec_chain.rs:105-169,192-229),
+ *                          Codec::from_metadata via the runtime registry
+ *                          (zarrs_codec/src/lib.rs:279-318,372-449)
+ *   zgpu_decode_batch   <- CodecChainBound::decode_into (codec_chain.rs:592-646) for full chunks and
+ *                          ArrayPartialDecoderTraits::partial_decode_into
+ *                          (zarrs_codec/src/codec_traits/array_partial_sync.rs:66-129) for partial
+ *                          selections; for a sharding_indexed chain, ShardingCodecBound::decode_into
+ *                          (sharding/sharding_codec.rs:617-707) and ShardingPartialDecoder
+ *                          (sharding/sharding_partial_decoder_sync.rs:311-400). Batched: one call
+ *                          decodes many chunks (per-chunk calls are a degenerate batch).
+ *   zgpu_retrieve_array_subset
+ *                       <- Array::retrieve_array_subset_into (zarrs/src/array/array_ops/
+ *                          array_read_ops_common.rs:20-179, array_read_ops_array.rs:231-375):
+ *                          the array-level batched driver that feeds zgpu_decode_batch.
+ *   status codes        <- CodecError variants (zarrs_codec/src/lib.rs:617-686), 1:1 (see below).
+ *
+ * Threading: every entry point is thread-safe; calls on one context are serialised internally
+ * (they share the context's device scratch), calls on different contexts run concurrently.
+ * Memory: the caller owns every encoded input and the output; the library owns its scratch.
+ */
+#ifndef ZGPU_H
+#define ZGPU_H
+
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define ZGPU_MAX_DIMS 8
+
+/* Status codes (per chunk and per call). Mapping onto zarrs_codec::CodecError:
+ *  ZGPU_INVALID_CHECKSUM       -> CodecError::InvalidChecksum            (crc32c_codec.rs:130-133)
+ *  ZGPU_DECODED_SIZE_MISMATCH  -> CodecError::UnexpectedChunkDecodedSize / InvalidBytesLength
+ *                                 (ArrayBytes::validate, zarrs_codec/src/array_bytes.rs:376-386)
+ *  ZGPU_SHARD_INDEX_OOB        -> CodecError::Other("The shard index references out-of-bounds
+ *                                 bytes. The chunk may be corrupted.") (sharding_codec.rs:682-686)
+ *  ZGPU_CORRUPT_STREAM         -> CodecError::IOError (gzip_codec.rs:116-118, zstd_codec.rs:119-128)
+ *  ZGPU_INVALID_BYTE_RANGE     -> CodecError::InvalidByteRangeError
+ *  ZGPU_UNSUPPORTED            -> CodecError::UnsupportedDataType / unsupported codec
+ *  ZGPU_CRC_INPUT_TOO_SHORT    -> CodecError::Other("crc32c decoder expects a 32 bit input")
+ *  ZGPU_SHARD_TOO_SMALL        -> CodecError::Other("The encoded shard is smaller than the
+ *                                 expected size of its index.") (sharding_codec.rs:1277-1281)
+ *  ZGPU_SHUFFLE_LENGTH         -> CodecError::Other("the shuffle codec expects the input byte
+ *                                 length to be an integer multiple of the elementsize")
+ *  ZGPU_INVALID_ARGUMENT       -> bad metadata / geometry (CodecCreateError, InvalidArraySubset)
+ *  ZGPU_HIP_ERROR              -> device runtime failure (no zarrs equivalent)
+ */
+enum {
+  ZGPU_OK = 0,
+  ZGPU_INVALID_CHECKSUM = 1,
+  ZGPU_DECODED_SIZE_MISMATCH = 2,
+  ZGPU_SHARD_INDEX_OOB = 3,
+  ZGPU_CORRUPT_STREAM = 4,
+  ZGPU_INVALID_BYTE_RANGE = 5,
+  ZGPU_UNSUPPORTED = 6,
+  ZGPU_CRC_INPUT_TOO_SHORT = 7,
+  ZGPU_SHARD_TOO_SMALL = 8,
+  ZGPU_SHUFFLE_LENGTH = 9,
+  ZGPU_INVALID_ARGUMENT = 10,
+  ZGPU_HIP_ERROR = 11,
+};
+
+/* decode flags */
+#define ZGPU_ENC_DEVICE 0x1u  /* desc.enc / chunk_ptrs are device pointers (else host memory)  */
+#define ZGPU_OUT_DEVICE 0x2u  /* out is a device pointer (else host memory)                    */
+#define ZGPU_NO_VALIDATE 0x4u /* override: CodecOptions::validate_checksums = false for the call */
+
+typedef struct zgpu_ctx zgpu_ctx;
+typedef struct zgpu_chain zgpu_chain;
+typedef struct zgpu_plan zgpu_plan;
+
+/* One context per GPU: owns a HIP stream, device scratch and pinned staging. */
+int zgpu_ctx_create(int hip_device, zgpu_ctx **out);
+void zgpu_ctx_destroy(zgpu_ctx *ctx);
+/* Last error message of the calling thread on this context ("" if none). */
+const char *zgpu_last_error(const zgpu_ctx *ctx);
+const char *zgpu_status_name(int status);
+/* Library version string, and the device kernels' ISA ("gfx950"). */
+const char *zgpu_version(void);
+
+/*
+ * Parse and bind a codec chain.
+ *  codecs_json : the Zarr V3 "codecs" JSON array (nested sharding_indexed configs included).
+ *                Supported: transpose, bytes, sharding_indexed, crc32c (+numcodecs.crc32c),
+ *                gzip, zstd, numcodecs.shuffle. Others -> ZGPU_UNSUPPORTED.
+ *  data_type   : Zarr V3 data type name ("float32", "uint16", ...); fixed-size types only.
+ *  fill        : native-endian fill value bytes (FillValue::as_ne_bytes), fill_len == dtype size.
+ *  validate_checksums : CodecOptions::validate_checksums (zarrs default true, options.rs:24-33).
+ */
+int zgpu_chain_create(zgpu_ctx *ctx, const char *codecs_json, const char *data_type,
+                      const void *fill, uint32_t fill_len, int validate_checksums,
+                      zgpu_chain **out);
+void zgpu_chain_destroy(zgpu_chain *chain);
+/* Bytes per element of the bound data type. */
+uint32_t zgpu_chain_element_size(const zgpu_chain *chain);
+
+/* One chunk (or shard) to decode into the output array. */
+typedef struct {
+  const void *enc;                      /* encoded bytes; NULL = missing chunk -> fill value     */
+  uint64_t enc_len;
+  uint64_t chunk_shape[ZGPU_MAX_DIMS];  /* decoded chunk (shard) shape                          */
+  uint64_t sel_start[ZGPU_MAX_DIMS];    /* wanted region of the chunk (chunk-relative)          */
+  uint64_t sel_shape[ZGPU_MAX_DIMS];    /*   == chunk_shape & start 0 -> full decode path       */
+  uint64_t out_start[ZGPU_MAX_DIMS];    /* where the region lands in the output array           */
+} zgpu_chunk_desc;
+
+/*
+ * Decode n chunks into one C-order output array of shape out_shape[ndim].
+ * A selection covering the whole chunk takes the full decode path (checksums verified);
+ * a partial selection takes the partial-decoder path (crc32c stripped, not verified; for
+ * sharding only the intersecting inner chunks are decoded), exactly as zarrs'
+ * retrieve_chunk_subset_into does (array_read_ops_array.rs:346-375).
+ * Output regions of different descriptors must be disjoint (ArrayBytesFixedDisjointView).
+ * status[n] (optional) receives each chunk's status. Returns the first non-zero chunk status
+ * (zarrs' try_for_each semantics) or a call-level error. hip_stream NULL = context stream.
+ * The call is synchronous with respect to the host (statuses are final on return).
+ */
+int zgpu_decode_batch(zgpu_chain *chain, uint32_t ndim, const zgpu_chunk_desc *descs,
+                      uint64_t n, void *out, const uint64_t *out_shape, uint32_t flags,
+                      int32_t *status, void *hip_stream);
+
+/*
+ * Prepared form of zgpu_decode_batch for device-resident inputs that are decoded repeatedly
+ * (benchmarks, hipGraph capture): the descriptor table is planned and uploaded once.
+ * zgpu_plan_execute enqueues the decode on the stream and, if status != NULL, waits and returns
+ * per-chunk statuses; with status == NULL it returns immediately after enqueue.
+ */
+int zgpu_plan_create(zgpu_chain *chain, uint32_t ndim, const zgpu_chunk_desc *descs, uint64_t n,
+                     const uint64_t *out_shape, uint32_t flags, zgpu_plan **out);
+int zgpu_plan_execute(zgpu_plan *plan, void *out, int32_t *status, void *hip_stream);
+void zgpu_plan_destroy(zgpu_plan *plan);
+/* Algorithmic HBM bytes of one execute (encoded bytes read + index bytes + decoded bytes
+ * written), the figure bench.py prices the roofline with. */
+uint64_t zgpu_plan_algorithmic_bytes(const zgpu_plan *plan);
+
+/*
+ * Array::retrieve_array_subset_into over a regular chunk grid. chunk_ptrs/chunk_lens are
+ * indexed by the C-order linear chunk-grid index (grid = ceil(array_shape/chunk_shape));
+ * chunk_ptrs[i] == NULL means the key is missing (fill value). out holds prod(sel_shape)
+ * elements in C order. Returns the first failing chunk's status.
+ */
+int zgpu_retrieve_array_subset(zgpu_chain *chain, uint32_t ndim, const uint64_t *array_shape,
+                               const uint64_t *chunk_shape, const void *const *chunk_ptrs,
+                               const uint64_t *chunk_lens, const uint64_t *sel_start,
+                               const uint64_t *sel_shape, void *out, uint32_t flags,
+                               void *hip_stream);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* ZGPU_H */

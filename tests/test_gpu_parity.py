@@ -1,0 +1,184 @@
+"""GPU parity: the HIP pipeline (libzgpu.so through the C ABI) against the committed goldens, the
+reference's own fixtures, and the CPU oracle on seeded inputs. Bit-exact everywhere (every stage on
+this path is lossless: SURVEY 8(a))."""
+import json
+import os
+
+import numpy as np
+import pytest
+
+import fixtures as F
+import oracle as O
+
+pytestmark = pytest.mark.gpu
+
+CASES = json.load(open(os.path.join(F.GOLDEN, "cases.json")))
+
+
+@pytest.fixture(scope="module")
+def torch_cuda():
+    import torch
+    return torch
+
+
+@pytest.fixture(scope="module")
+def ctx():
+    from zarrs_amd import Context
+    return Context(0)
+
+
+def _gpu_decode(ctx, case, enc: bytes, device_input: bool, torch):
+    from zarrs_amd import CodecChain, make_desc
+    ch = CodecChain.from_metadata(case["codecs"], case["data_type"], case["fill_value"], ctx)
+    shape = case["shape"]
+    sel = case["sel"] or [[0] * len(shape), shape]
+    src = torch.frombuffer(bytearray(enc), dtype=torch.uint8).cuda() if (device_input and len(enc)) else enc
+    out = np.zeros(sel[1], dtype=ch.dtype)
+    d = make_desc(src, shape, sel[0], sel[1])
+    return ch.decode_batch([d], out, list(sel[1]), enc_device=device_input and len(enc) > 0), out
+
+
+@pytest.mark.parametrize("device_input", [True, False], ids=["hbm", "host"])
+@pytest.mark.parametrize("case", CASES, ids=[c["name"] for c in CASES])
+def test_golden(ctx, torch_cuda, case, device_input):
+    from zarrs_amd import ZgpuError
+    g = np.load(os.path.join(F.GOLDEN, "synthetic.npz"), allow_pickle=False)
+    enc = g[case["name"] + "/enc"].tobytes()
+    if case["status"]:
+        with pytest.raises(ZgpuError) as ei:
+            _gpu_decode(ctx, case, enc, device_input, torch_cuda)
+        assert ei.value.status == case["status"]
+        return
+    st, out = _gpu_decode(ctx, case, enc, device_input, torch_cuda)
+    assert st == [0]
+    assert out.tobytes() == g[case["name"] + "/dec"].tobytes()
+
+
+@pytest.mark.parametrize("fixture", F.FLOAT_0_99 + [F.SHARDED])
+@pytest.mark.parametrize("store", ["host", "hbm"])
+def test_reference_fixture_array(ctx, torch_cuda, fixture, store):
+    from zarrs_amd import Array, DeviceStore, MemoryStore
+    m, chunks = F.load_array(fixture)
+    meta = {"shape": m["shape"], "data_type": m["data_type"], "fill_value": m["fill_value"],
+            "chunk_grid": {"name": "regular", "configuration": {"chunk_shape": m["chunk_shape"]}},
+            "chunk_key_encoding": {"name": "default", "configuration": {"separator": "/"}},
+            "codecs": m["codecs"]}
+    ms = MemoryStore({"c/" + "/".join(map(str, k)): v for k, v in chunks.items()})
+    st = DeviceStore.from_store(ms) if store == "hbm" else ms
+    arr = Array(st, meta, ctx)
+    exp = np.arange(int(np.prod(m["shape"]))).reshape(m["shape"]).astype(arr.dtype)
+    assert np.array_equal(arr.retrieve_array_subset(), exp)
+    # partial subsets crossing chunk boundaries (partial-decoder path)
+    assert np.array_equal(arr.retrieve_array_subset([1, 2], [6, 5]), exp[1:7, 2:7])
+    assert np.array_equal(arr.retrieve_chunk([1, 0]), exp[m["chunk_shape"][0]:2 * m["chunk_shape"][0],
+                                                          :m["chunk_shape"][1]])
+
+
+def _encode_grid(chain_o, a, cs, drop=()):
+    chunks = {}
+    grid = [-(-s // c) for s, c in zip(a.shape, cs)]
+    for idx in np.ndindex(*grid):
+        if idx in drop:
+            continue
+        blk = np.zeros(cs, a.dtype)
+        sl = tuple(slice(i * c, min((i + 1) * c, s)) for i, c, s in zip(idx, cs, a.shape))
+        src = a[sl]
+        blk[tuple(slice(0, n) for n in src.shape)] = src
+        chunks[idx] = chain_o.encode(blk)
+    return chunks
+
+
+CHAINS = {
+    "c2_transpose_be": ([{"name": "transpose", "configuration": {"order": [2, 1, 0]}},
+                         {"name": "bytes", "configuration": {"endian": "big"}}], "float32"),
+    "bytes_le": ([{"name": "bytes", "configuration": {"endian": "little"}}], "float32"),
+    "transpose_021_u16": ([{"name": "transpose", "configuration": {"order": [0, 2, 1]}},
+                           {"name": "bytes", "configuration": {"endian": "big"}}], "uint16"),
+    "crc_shuffle": ([{"name": "bytes", "configuration": {"endian": "little"}},
+                     {"name": "numcodecs.shuffle", "configuration": {"elementsize": 8}},
+                     {"name": "crc32c"}], "float64"),
+    "sharded_crc": ([{"name": "sharding_indexed", "configuration": {
+        "chunk_shape": [8, 8, 8], "codecs": [{"name": "bytes", "configuration": {"endian": "little"}},
+                                             {"name": "crc32c"}],
+        "index_codecs": [{"name": "bytes", "configuration": {"endian": "little"}}, {"name": "crc32c"}],
+        "index_location": "end"}}], "float32"),
+    "sharded_transpose_inner": ([{"name": "sharding_indexed", "configuration": {
+        "chunk_shape": [8, 4, 16], "codecs": [{"name": "transpose", "configuration": {"order": [2, 0, 1]}},
+                                              {"name": "bytes", "configuration": {"endian": "big"}}],
+        "index_codecs": [{"name": "bytes", "configuration": {"endian": "big"}}, {"name": "crc32c"}],
+        "index_location": "start"}}], "int32"),
+}
+
+
+@pytest.mark.parametrize("name", list(CHAINS))
+@pytest.mark.parametrize("store", ["host", "hbm"])
+def test_random_arrays_vs_oracle(ctx, torch_cuda, name, store):
+    from zarrs_amd import Array, DeviceStore, MemoryStore
+    codecs, dt = CHAINS[name]
+    rng = np.random.default_rng(abs(hash(name)) % 2**32)
+    shape, cs = [45, 70, 33], [16, 32, 32]
+    npdt = np.dtype(O.DTYPES[dt][0])
+    a = (rng.standard_normal(shape) * 100).astype(npdt)
+    co = O.OracleChain.from_metadata(codecs, dt, 3, 3)
+    chunks = _encode_grid(co, a, cs, drop={(1, 1, 0)})
+    ms = MemoryStore({"c/" + "/".join(map(str, k)): v for k, v in chunks.items()})
+    meta = {"shape": shape, "data_type": dt, "fill_value": 3, "codecs": codecs,
+            "chunk_grid": {"name": "regular", "configuration": {"chunk_shape": cs}}}
+    arr = Array(DeviceStore.from_store(ms) if store == "hbm" else ms, meta, ctx)
+    for start, sub in (([0, 0, 0], shape), ([5, 17, 3], [30, 40, 29]), ([16, 32, 0], [16, 32, 32]),
+                       ([44, 69, 32], [1, 1, 1])):
+        exp = O.retrieve_array_subset(co, shape, cs, chunks, start, sub, nthreads=4)
+        got = arr.retrieve_array_subset(start, sub)
+        assert got.tobytes() == exp.tobytes(), (start, sub)
+
+
+def test_device_output_and_plan(ctx, torch_cuda):
+    """Device-resident encoded chunks -> device output through the prepared-plan API (bench path)."""
+    import ctypes as C
+    torch = torch_cuda
+    from zarrs_amd import CodecChain, make_desc
+    from zarrs_amd import _lib as L
+    codecs, dt = CHAINS["c2_transpose_be"]
+    rng = np.random.default_rng(5)
+    cs, grid = [64, 64, 64], [2, 3, 2]
+    a = rng.standard_normal([g * c for g, c in zip(grid, cs)]).astype(np.float32)
+    co = O.OracleChain.from_metadata(codecs, dt, 0, 3)
+    chunks = _encode_grid(co, a, cs)
+    dev = {k: torch.frombuffer(bytearray(v), dtype=torch.uint8).cuda() for k, v in chunks.items()}
+    ch = CodecChain.from_metadata(codecs, dt, 0, ctx)
+    descs = [make_desc(dev[k], cs, out_start=[i * c for i, c in zip(k, cs)]) for k in sorted(dev)]
+    out = torch.empty(a.shape, dtype=torch.float32, device="cuda")
+    arr = (L.ChunkDesc * len(descs))(*descs)
+    plan = C.c_void_p()
+    L.check(L.load().zgpu_plan_create(ch._h, 3, arr, len(descs), L.u64s(a.shape),
+                                      L.ENC_DEVICE | L.OUT_DEVICE, C.byref(plan)))
+    st = (C.c_int32 * len(descs))()
+    for _ in range(3):
+        out.zero_()
+        L.check(L.load().zgpu_plan_execute(plan, out.data_ptr(), st, None))
+        assert np.array_equal(out.cpu().numpy(), a)
+    assert L.load().zgpu_plan_algorithmic_bytes(plan) == 2 * a.nbytes
+    L.load().zgpu_plan_destroy(plan)
+
+
+def test_error_first_status_per_descriptor(ctx, torch_cuda):
+    """A corrupt chunk reports INVALID_CHECKSUM for its descriptor only; the others decode."""
+    from zarrs_amd import CodecChain, ZgpuError, make_desc
+    codecs = [{"name": "bytes", "configuration": {"endian": "little"}}, {"name": "crc32c"}]
+    co = O.OracleChain.from_metadata(codecs, "uint16", 0, 1)
+    a = np.arange(300, dtype=np.uint16)
+    encs = [co.encode(a[i * 100:(i + 1) * 100]) for i in range(3)]
+    bad = bytearray(encs[1])
+    bad[10] ^= 1
+    encs[1] = bytes(bad)
+    ch = CodecChain.from_metadata(codecs, "uint16", 0, ctx)
+    out = np.zeros(300, np.uint16)
+    descs = [make_desc(e, [100], out_start=[100 * i]) for i, e in enumerate(encs)]
+    with pytest.raises(ZgpuError) as ei:
+        ch.decode_batch(descs, out, [300], enc_device=False)
+    assert ei.value.status == 1
+    assert np.array_equal(out[:100], a[:100]) and np.array_equal(out[200:], a[200:])
+    # validate_checksums = false -> decodes (the flipped byte shows through)
+    ch2 = CodecChain.from_metadata(codecs, "uint16", 0, ctx, validate_checksums=False)
+    out2 = np.zeros(300, np.uint16)
+    assert ch2.decode_batch(descs, out2, [300], enc_device=False) == [0, 0, 0]

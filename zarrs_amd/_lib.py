@@ -1,0 +1,104 @@
+"""ctypes binding of libzgpu.so (the C ABI declared in include/zgpu.h).
+
+The product path has no CPU fallback: if the HIP library is missing this module raises, and every
+decode runs the gfx950 kernels.
+"""
+from __future__ import annotations
+
+import ctypes as C
+import os
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.path.join(HERE, "lib", "libzgpu.so")
+MAX_DIMS = 8
+
+STATUS_NAMES = [
+    "OK", "INVALID_CHECKSUM", "DECODED_SIZE_MISMATCH", "SHARD_INDEX_OOB", "CORRUPT_STREAM",
+    "INVALID_BYTE_RANGE", "UNSUPPORTED", "CRC_INPUT_TOO_SHORT", "SHARD_TOO_SMALL", "SHUFFLE_LENGTH",
+    "INVALID_ARGUMENT", "HIP_ERROR",
+]
+OK, INVALID_CHECKSUM, DECODED_SIZE_MISMATCH, SHARD_INDEX_OOB, CORRUPT_STREAM, INVALID_BYTE_RANGE, \
+    UNSUPPORTED, CRC_INPUT_TOO_SHORT, SHARD_TOO_SMALL, SHUFFLE_LENGTH, INVALID_ARGUMENT, HIP_ERROR = range(12)
+
+ENC_DEVICE = 0x1
+OUT_DEVICE = 0x2
+NO_VALIDATE = 0x4
+
+# every symbol include/zgpu.h declares (tests/test_abi.py checks the .so exports all of them)
+EXPORTS = [
+    "zgpu_ctx_create", "zgpu_ctx_destroy", "zgpu_last_error", "zgpu_status_name", "zgpu_version",
+    "zgpu_chain_create", "zgpu_chain_destroy", "zgpu_chain_element_size", "zgpu_decode_batch",
+    "zgpu_plan_create", "zgpu_plan_execute", "zgpu_plan_destroy", "zgpu_plan_algorithmic_bytes",
+    "zgpu_retrieve_array_subset",
+]
+
+
+class ChunkDesc(C.Structure):
+    _fields_ = [
+        ("enc", C.c_void_p),
+        ("enc_len", C.c_uint64),
+        ("chunk_shape", C.c_uint64 * MAX_DIMS),
+        ("sel_start", C.c_uint64 * MAX_DIMS),
+        ("sel_shape", C.c_uint64 * MAX_DIMS),
+        ("out_start", C.c_uint64 * MAX_DIMS),
+    ]
+
+
+class ZgpuError(RuntimeError):
+    """Maps zgpu status codes onto the reference's CodecError variants (zarrs_codec/src/lib.rs:617-686)."""
+
+    def __init__(self, status: int, message: str = ""):
+        self.status = status
+        name = STATUS_NAMES[status] if 0 <= status < len(STATUS_NAMES) else str(status)
+        super().__init__(f"{name}{': ' + message if message and message != name else ''}")
+
+
+_lib = None
+
+
+def load() -> C.CDLL:
+    global _lib
+    if _lib is not None:
+        return _lib
+    if not os.path.exists(LIB_PATH):
+        raise ImportError(f"{LIB_PATH} is missing: build it with `make -C zarrs_amd/csrc` "
+                          "(or __graft_entry__.build()); there is no CPU fallback")
+    L = C.CDLL(LIB_PATH)
+    vp, u32, u64, i32 = C.c_void_p, C.c_uint32, C.c_uint64, C.c_int
+    P64 = C.POINTER(C.c_uint64)
+    L.zgpu_ctx_create.argtypes = [i32, C.POINTER(vp)]
+    L.zgpu_ctx_destroy.argtypes = [vp]
+    L.zgpu_last_error.restype = C.c_char_p
+    L.zgpu_last_error.argtypes = [vp]
+    L.zgpu_status_name.restype = C.c_char_p
+    L.zgpu_status_name.argtypes = [i32]
+    L.zgpu_version.restype = C.c_char_p
+    L.zgpu_chain_create.argtypes = [vp, C.c_char_p, C.c_char_p, vp, u32, i32, C.POINTER(vp)]
+    L.zgpu_chain_destroy.argtypes = [vp]
+    L.zgpu_chain_element_size.restype = u32
+    L.zgpu_chain_element_size.argtypes = [vp]
+    L.zgpu_decode_batch.argtypes = [vp, u32, C.POINTER(ChunkDesc), u64, vp, P64, u32,
+                                    C.POINTER(C.c_int32), vp]
+    L.zgpu_plan_create.argtypes = [vp, u32, C.POINTER(ChunkDesc), u64, P64, u32, C.POINTER(vp)]
+    L.zgpu_plan_execute.argtypes = [vp, vp, C.POINTER(C.c_int32), vp]
+    L.zgpu_plan_destroy.argtypes = [vp]
+    L.zgpu_plan_algorithmic_bytes.restype = u64
+    L.zgpu_plan_algorithmic_bytes.argtypes = [vp]
+    L.zgpu_retrieve_array_subset.argtypes = [vp, u32, P64, P64, C.POINTER(vp), P64, P64, P64, vp,
+                                             u32, vp]
+    _lib = L
+    return L
+
+
+def last_error() -> str:
+    return (load().zgpu_last_error(None) or b"").decode()
+
+
+def check(status: int) -> None:
+    if status:
+        raise ZgpuError(status, last_error())
+
+
+def u64s(vals, n=None):
+    vals = [int(v) for v in vals]
+    return (C.c_uint64 * (n or max(len(vals), 1)))(*vals)

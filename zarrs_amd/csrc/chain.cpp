@@ -1,0 +1,149 @@
+// Codec chain parsing (see chain.hpp). Reference: codec_chain.rs:192-229 (from_metadata: exactly one
+// array->bytes codec, error otherwise), zarrs_codec/src/lib.rs:372-449 (name -> codec lookup), and the
+// per-codec configurations in zarrs_metadata_ext/src/codec/registered/{transpose,bytes,sharding,
+// crc32c,gzip,zstd,shuffle}.rs.
+#include "chain.hpp"
+
+#include <cstring>
+
+#include "../../include/zgpu.h"
+
+namespace zgpu {
+
+bool data_type_info(const std::string &n, uint32_t &es, uint32_t &comp) {
+  struct E { const char *name; uint32_t es, comp; };
+  static const E tab[] = {
+      {"bool", 1, 1},    {"int8", 1, 1},    {"uint8", 1, 1},    {"int16", 2, 2},     {"uint16", 2, 2},
+      {"float16", 2, 2}, {"bfloat16", 2, 2}, {"int32", 4, 4},   {"uint32", 4, 4},    {"float32", 4, 4},
+      {"int64", 8, 8},   {"uint64", 8, 8},  {"float64", 8, 8},  {"complex64", 8, 4}, {"complex128", 16, 8},
+  };
+  for (const E &e : tab)
+    if (n == e.name) {
+      es = e.es;
+      comp = e.comp;
+      return true;
+    }
+  return false;
+}
+
+static std::shared_ptr<Chain> parse(const Json &codecs, const std::string &dt, uint32_t es, uint32_t comp,
+                                    const uint8_t *fill) {
+  if (codecs.kind != Json::Arr) throw ChainError{ZGPU_INVALID_ARGUMENT, "codecs must be a JSON array"};
+  auto c = std::make_shared<Chain>();
+  c->es = es;
+  c->comp = comp;
+  c->data_type = dt;
+  if (fill) std::memcpy(c->fill, fill, es);
+  bool have_a2b = false;
+  for (const Json &m : codecs.arr) {
+    Codec k;
+    const Json *cfg = nullptr;
+    if (m.kind == Json::Str) {
+      k.name = m.s;
+    } else if (m.kind == Json::Obj && m.get("name")) {
+      k.name = m.get("name")->as_str();
+      cfg = m.get("configuration");
+    } else {
+      throw ChainError{ZGPU_INVALID_ARGUMENT, "codec metadata must be {name, configuration}"};
+    }
+    auto cfg_get = [&](const char *key) -> const Json * { return cfg ? cfg->get(key) : nullptr; };
+    if (k.name == "transpose") {
+      k.kind = CodecKind::Transpose;
+      const Json *o = cfg_get("order");
+      if (!o || o->kind != Json::Arr) throw ChainError{ZGPU_INVALID_ARGUMENT, "transpose: missing order"};
+      uint32_t seen = 0;
+      for (const Json &v : o->arr) {
+        int64_t a = v.as_int();
+        if (a < 0 || a >= (int64_t)o->arr.size() || a >= ZGPU_MAX_DIMS || ((seen >> a) & 1))
+          throw ChainError{ZGPU_INVALID_ARGUMENT, "transpose: order is not a permutation"};
+        seen |= 1u << a;
+        k.order.push_back((uint32_t)a);
+      }
+      if (have_a2b) throw ChainError{ZGPU_INVALID_ARGUMENT, "array->array codec after array->bytes codec"};
+      c->a2a.push_back(k);
+      continue;
+    }
+    if (k.name == "bytes" || k.name == "sharding_indexed") {
+      if (have_a2b) throw ChainError{ZGPU_INVALID_ARGUMENT, "multiple array->bytes codecs"};
+      if (k.name == "bytes") {
+        k.kind = CodecKind::Bytes;
+        const Json *e = cfg_get("endian");
+        if (e && e->kind == Json::Str) {
+          if (e->s == "big") k.big_endian = true;
+          else if (e->s != "little") throw ChainError{ZGPU_INVALID_ARGUMENT, "bytes: bad endian"};
+        } else if (comp > 1) {
+          // BytesCodecEndiannessMissingError (zarrs_data_type/src/codec_traits/bytes.rs:109-110)
+          throw ChainError{ZGPU_INVALID_ARGUMENT, "bytes: endian required for multi-byte data types"};
+        }
+      } else {
+        k.kind = CodecKind::Sharding;
+        const Json *cs = cfg_get("chunk_shape");
+        if (!cs || cs->kind != Json::Arr) throw ChainError{ZGPU_INVALID_ARGUMENT, "sharding: missing chunk_shape"};
+        for (const Json &v : cs->arr) {
+          int64_t s = v.as_int();
+          if (s <= 0) throw ChainError{ZGPU_INVALID_ARGUMENT, "sharding: chunk_shape must be positive"};
+          k.inner_shape.push_back((uint64_t)s);
+        }
+        const Json *ic = cfg_get("codecs");
+        if (!ic) throw ChainError{ZGPU_INVALID_ARGUMENT, "sharding: missing codecs"};
+        k.inner = parse(*ic, dt, es, comp, c->fill);
+        Json defidx = Json::parse(R"([{"name":"bytes","configuration":{"endian":"little"}},{"name":"crc32c"}])");
+        const Json *xc = cfg_get("index_codecs");
+        const uint8_t ffill[8] = {0xff, 0xff, 0xff, 0xff, 0xff, 0xff, 0xff, 0xff};
+        k.index = parse(xc ? *xc : defidx, "uint64", 8, 8, ffill);
+        const Json *loc = cfg_get("index_location");
+        if (loc && loc->kind == Json::Str) {
+          if (loc->s == "start") k.at_start = true;
+          else if (loc->s != "end") throw ChainError{ZGPU_INVALID_ARGUMENT, "sharding: bad index_location"};
+        }
+      }
+      c->a2b = k;
+      have_a2b = true;
+      continue;
+    }
+    if (!have_a2b) throw ChainError{ZGPU_INVALID_ARGUMENT, "bytes->bytes codec before the array->bytes codec"};
+    if (k.name == "crc32c" || k.name == "numcodecs.crc32c") {
+      k.kind = CodecKind::Crc32c;
+      const Json *loc = cfg_get("location");
+      if (loc && loc->kind == Json::Str && loc->s == "start") k.at_start = true;
+    } else if (k.name == "gzip") {
+      k.kind = CodecKind::Gzip;
+      const Json *l = cfg_get("level");
+      k.level = l ? (int)l->as_int() : 5;
+    } else if (k.name == "zstd" || k.name == "numcodecs.zstd") {
+      k.kind = CodecKind::Zstd;
+      const Json *l = cfg_get("level");
+      k.level = l ? (int)l->as_int() : 0;
+      const Json *cs = cfg_get("checksum");
+      k.checksum = cs && cs->kind == Json::Bool && cs->b;
+    } else if (k.name == "numcodecs.shuffle" || k.name == "shuffle") {
+      k.kind = CodecKind::Shuffle;
+      const Json *e = cfg_get("elementsize");
+      k.elementsize = e ? (uint32_t)e->as_int() : 4;
+      if (k.elementsize == 0) throw ChainError{ZGPU_INVALID_ARGUMENT, "shuffle: elementsize must be > 0"};
+    } else {
+      throw ChainError{ZGPU_UNSUPPORTED, "codec '" + k.name + "' is not supported by the GPU pipeline"};
+    }
+    c->b2b.push_back(k);
+  }
+  if (!have_a2b) throw ChainError{ZGPU_INVALID_ARGUMENT, "missing array->bytes codec"};
+  return c;
+}
+
+std::shared_ptr<Chain> parse_chain(const Json &codecs, const std::string &dt, const uint8_t *fill) {
+  uint32_t es, comp;
+  if (!data_type_info(dt, es, comp)) throw ChainError{ZGPU_UNSUPPORTED, "data type '" + dt + "'"};
+  return parse(codecs, dt, es, comp, fill);
+}
+
+int64_t chain_fixed_encoded_size(const Chain &c, uint64_t nelem) {
+  if (c.a2b.kind != CodecKind::Bytes) return -1;
+  int64_t n = (int64_t)(nelem * c.es);
+  for (const Codec &k : c.b2b) {
+    if (k.kind == CodecKind::Crc32c) n += 4;
+    else if (k.kind != CodecKind::Shuffle) return -1;
+  }
+  return n;
+}
+
+}  // namespace zgpu

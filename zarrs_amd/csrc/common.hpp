@@ -1,0 +1,60 @@
+// Shared host/device definitions for the zgpu decode pipeline (gfx950).
+//
+// Device data layout (one "plan" = one batch of chunk descriptors):
+//   Item[n_items]      leaf chunk work items (a plain chunk, or one inner chunk of a shard):
+//                      current encoded byte range {src,len} that each b2b stage rewrites in place
+//   geom[n_items][3*nd] u64: sel_start (leaf-chunk relative), sel_shape, out_start (output array)
+//   status[n_items]    u32 per-item status (0 = ok; first error sticks, later stages skip)
+//   Shard[n_shards]    sharded descriptors: encoded shard {ptr,len}; index decoded into
+//   index[n_shards][n_inner*2] u64 (offset, nbytes) per inner chunk, C order of inner coords
+#pragma once
+#include <stdint.h>
+
+#define ZG_MAXD 8
+
+// item flags
+#define ZG_ITEM_FILL 0x1u     // write the fill value (missing chunk / empty inner chunk)
+#define ZG_ITEM_PARTIAL 0x2u  // partial-decoder path: crc32c strips without verifying
+#define ZG_ITEM_SHARDED 0x4u  // src/len resolved on device from the shard index
+
+struct ZgItem {
+  uint64_t src;    // device address of the current encoded bytes
+  uint64_t len;    // current byte length
+  uint32_t desc;   // owning descriptor
+  uint32_t flags;  // ZG_ITEM_*
+  uint32_t shard;  // shard slot (sharded items)
+  uint32_t inner;  // inner chunk linear index inside the shard
+};
+
+struct ZgShard {
+  uint64_t ptr;  // device address of the encoded shard
+  uint64_t len;
+};
+
+// Parameters of the final fused stage: bytes codec (endianness) + transpose(s) + scatter
+// into the output subset (+ an innermost numcodecs.shuffle when it sits directly above bytes).
+struct ZgScatter {
+  uint32_t nd;
+  uint32_t es;        // element size (bytes)
+  uint32_t comp;      // component size for endianness swap
+  uint32_t swap;      // 1: stored big-endian -> reverse each component
+  uint32_t shuffle;   // 1: fused unshuffle with elementsize == es
+  uint32_t tile_a;    // decoded axis that is innermost in the encoded layout (tiled kernel)
+  uint64_t chunk_shape[ZG_MAXD];  // leaf decoded shape
+  uint64_t enc_stride[ZG_MAXD];   // encoded linear stride (elements) of each decoded axis
+  uint64_t out_stride[ZG_MAXD];   // output array C strides (elements)
+  uint64_t nelem;                 // elements per leaf chunk
+  uint8_t fill[16];
+};
+
+// device status codes (== zgpu.h)
+#define ZG_OK 0u
+#define ZG_INVALID_CHECKSUM 1u
+#define ZG_DECODED_SIZE_MISMATCH 2u
+#define ZG_SHARD_INDEX_OOB 3u
+#define ZG_CORRUPT_STREAM 4u
+#define ZG_INVALID_BYTE_RANGE 5u
+#define ZG_UNSUPPORTED 6u
+#define ZG_CRC_INPUT_TOO_SHORT 7u
+#define ZG_SHARD_TOO_SMALL 8u
+#define ZG_SHUFFLE_LENGTH 9u

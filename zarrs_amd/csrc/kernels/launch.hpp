@@ -1,0 +1,53 @@
+// Host-callable launchers of the gfx950 kernels (defined in the .hip translation units).
+#pragma once
+#include <hip/hip_runtime.h>
+
+#include "../common.hpp"
+
+namespace zgpu {
+
+enum ScatterMode : uint32_t { SCATTER_ROWS = 0, SCATTER_TILED = 1, SCATTER_GENERIC = 2 };
+
+hipError_t launch_scatter(const ZgItem *items, const uint64_t *geom, uint32_t *status, const ZgScatter &P,
+                          uint8_t *out, uint32_t n_items, uint32_t mode, uint64_t units_per_item,
+                          hipStream_t s);
+uint64_t scatter_units_per_item(uint32_t mode, const ZgScatter &P, const uint64_t *max_sel_shape);
+
+// crc32c (Castagnoli) verify + strip of a 4-byte LE checksum at the start or end of each item.
+// verify: 0 never, 1 unless the item is on the partial path.
+hipError_t launch_crc32c_strip(ZgItem *items, uint32_t *status, uint32_t n_items, int at_start, int verify,
+                               hipStream_t s);
+
+// Shard index: decode every shard's index (bytes{endian} + optional crc32c chain), then resolve
+// each sharded item's {src,len} or fill flag.  index_crc: 0 none, 1 end, 2 start.
+struct ZgIndexSpec {
+  uint64_t n_inner;      // inner chunks per shard
+  uint64_t index_bytes;  // encoded index size (incl. checksums)
+  uint32_t at_start;     // sharding index_location
+  uint32_t big_endian;   // index bytes codec endianness
+  uint32_t n_crc;        // number of crc32c codecs in the index chain (<= 4)
+  uint32_t crc_at_start[4];
+  uint32_t verify;       // validate_checksums
+};
+hipError_t launch_shard_index(const ZgShard *shards, uint32_t n_shards, const ZgIndexSpec &spec,
+                              uint64_t *index, uint32_t *shard_status, hipStream_t s);
+hipError_t launch_item_resolve(ZgItem *items, uint32_t *status, uint32_t n_items, const ZgShard *shards,
+                               const uint64_t *index, const uint32_t *shard_status, uint64_t n_inner,
+                               unsigned long long *enc_bytes, hipStream_t s);
+
+// gzip trailer check: CRC-32 (IEEE) and ISIZE of each item's inflated bytes vs aux[i] = {crc, isize}
+hipError_t launch_crc32_check(const ZgItem *items, uint32_t *status, uint32_t n_items, const uint2 *aux,
+                              hipStream_t s);
+
+// gzip (RFC 1952) member decode: header parse, DEFLATE inflate into dst slots, CRC-32 + ISIZE check.
+// On return items[i] points at its slot; aux[i] receives the trailer {crc32, isize} for launch_crc32_check.
+hipError_t launch_gzip(ZgItem *items, uint32_t *status, uint32_t n_items, uint8_t *dst, uint64_t slot_bytes,
+                       uint2 *aux, hipStream_t s);
+// zstd (RFC 8878) frame decode into dst slots.
+hipError_t launch_zstd(ZgItem *items, uint32_t *status, uint32_t n_items, uint8_t *dst, uint64_t slot_bytes,
+                       hipStream_t s);
+// standalone unshuffle (when shuffle is not directly above the bytes codec)
+hipError_t launch_unshuffle(ZgItem *items, uint32_t *status, uint32_t n_items, uint8_t *dst, uint64_t slot_bytes,
+                            uint32_t elementsize, hipStream_t s);
+
+}  // namespace zgpu

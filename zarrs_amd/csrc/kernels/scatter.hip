@@ -1,0 +1,407 @@
+// Fused final decode stage for gfx950: bytes codec (endianness swap) + transpose codec(s) +
+// numcodecs.shuffle (innermost position only) + scatter of the chunk selection into the output
+// array (ArrayBytesFixedDisjointView::copy_from_slice / fill).
+//
+// Reference semantics restated (paths relative to the zarrs workspace root):
+//   endianness   zarrs_data_type/src/codec_traits/bytes.rs:97-131 (reverse each component)
+//   transpose    zarrs/src/array/codec/array_to_array/transpose.rs:110-135,223-266
+//                (decoded dec[c] = enc[e], e_a = c[order[a]]; composed over all a2a codecs)
+//   unshuffle    zarrs/src/array/codec/bytes_to_bytes/shuffle/shuffle_codec.rs:109-129
+//   scatter/fill zarrs_codec/src/array_bytes_fixed_disjoint_view.rs:144-206
+//   size check   zarrs_codec/src/array_bytes.rs:376-386 (UnexpectedChunkDecodedSize)
+//
+// Three kernels, chosen per batch on the host from the chain's composed permutation:
+//   k_scatter_rows   the encoded innermost axis is the decoded innermost axis: contiguous rows,
+//                    16-B vector copy when every row is 16-B aligned, element copy otherwise.
+//   k_scatter_tiled  a true innermost transpose: 64x64-element tiles staged through LDS so both
+//                    the encoded read and the output write are row-contiguous (HBM bound).
+//   k_scatter_generic anything else (fused shuffle + transpose, odd element sizes): one thread
+//                    per output element, coalesced writes.
+#include <hip/hip_runtime.h>
+
+#include "../common.hpp"
+#include "launch.hpp"
+
+namespace zgpu {
+
+__device__ __forceinline__ uint32_t swap_word(uint32_t x, uint32_t comp) {
+  if (comp == 4) return __builtin_bswap32(x);
+  if (comp == 2) return ((x >> 8) & 0x00FF00FFu) | ((x << 8) & 0xFF00FF00u);
+  return x;
+}
+
+__device__ __forceinline__ uint4 swap_vec(uint4 v, uint32_t comp) {
+  if (comp == 8) return make_uint4(__builtin_bswap32(v.y), __builtin_bswap32(v.x),
+                                   __builtin_bswap32(v.w), __builtin_bswap32(v.z));
+  return make_uint4(swap_word(v.x, comp), swap_word(v.y, comp), swap_word(v.z, comp),
+                    swap_word(v.w, comp));
+}
+
+// Load one element of `es` bytes (es <= 16) from a possibly unaligned address, apply the
+// endianness reversal of each `comp`-byte component, and return it in a 16-byte register.
+__device__ __forceinline__ uint4 load_elem(const uint8_t *p, uint32_t es, uint32_t comp, uint32_t swap) {
+  uint8_t b[16];
+  uintptr_t a = (uintptr_t)p;
+  if (es == 4 && (a & 3) == 0) {
+    uint32_t w = *(const uint32_t *)p;
+    if (swap) w = swap_word(w, comp);
+    return make_uint4(w, 0, 0, 0);
+  }
+  if (es == 2 && (a & 1) == 0) {
+    uint32_t w = *(const uint16_t *)p;
+    if (swap) w = ((w >> 8) | (w << 8)) & 0xFFFFu;
+    return make_uint4(w, 0, 0, 0);
+  }
+  if (es == 8 && (a & 7) == 0) {
+    uint2 w = *(const uint2 *)p;
+    uint4 v = make_uint4(w.x, w.y, 0, 0);
+    if (swap) {
+      if (comp == 8) v = make_uint4(__builtin_bswap32(w.y), __builtin_bswap32(w.x), 0, 0);
+      else v = make_uint4(swap_word(w.x, comp), swap_word(w.y, comp), 0, 0);
+    }
+    return v;
+  }
+  for (uint32_t i = 0; i < es; i++) b[i] = p[i];
+  if (swap && comp > 1)
+    for (uint32_t c0 = 0; c0 < es; c0 += comp)
+      for (uint32_t x = 0, y = comp - 1; x < y; x++, y--) {
+        uint8_t t = b[c0 + x]; b[c0 + x] = b[c0 + y]; b[c0 + y] = t;
+      }
+  for (uint32_t i = es; i < 16; i++) b[i] = 0;
+  uint4 v;
+  v.x = b[0] | b[1] << 8 | b[2] << 16 | (uint32_t)b[3] << 24;
+  v.y = b[4] | b[5] << 8 | b[6] << 16 | (uint32_t)b[7] << 24;
+  v.z = b[8] | b[9] << 8 | b[10] << 16 | (uint32_t)b[11] << 24;
+  v.w = b[12] | b[13] << 8 | b[14] << 16 | (uint32_t)b[15] << 24;
+  return v;
+}
+
+__device__ __forceinline__ void store_elem(uint8_t *p, uint4 v, uint32_t es) {
+  uintptr_t a = (uintptr_t)p;
+  if (es == 4 && (a & 3) == 0) { *(uint32_t *)p = v.x; return; }
+  if (es == 2 && (a & 1) == 0) { *(uint16_t *)p = (uint16_t)v.x; return; }
+  if (es == 8 && (a & 7) == 0) { *(uint2 *)p = make_uint2(v.x, v.y); return; }
+  if (es == 1) { *p = (uint8_t)v.x; return; }
+  const uint32_t w[4] = {v.x, v.y, v.z, v.w};
+  for (uint32_t i = 0; i < es; i++) p[i] = (uint8_t)(w[i >> 2] >> (8 * (i & 3)));
+}
+
+__device__ __forceinline__ uint4 fill_elem(const ZgScatter &P) {
+  uint4 v;
+  v.x = P.fill[0] | P.fill[1] << 8 | P.fill[2] << 16 | (uint32_t)P.fill[3] << 24;
+  v.y = P.fill[4] | P.fill[5] << 8 | P.fill[6] << 16 | (uint32_t)P.fill[7] << 24;
+  v.z = P.fill[8] | P.fill[9] << 8 | P.fill[10] << 16 | (uint32_t)P.fill[11] << 24;
+  v.w = P.fill[12] | P.fill[13] << 8 | P.fill[14] << 16 | (uint32_t)P.fill[15] << 24;
+  return v;
+}
+
+// Validate the decoded byte count of a non-fill item; returns false if the item is dead.
+__device__ __forceinline__ bool item_live(const ZgItem &it, uint32_t *status, uint32_t i,
+                                          const ZgScatter &P) {
+  if (status[i]) return false;
+  if (!(it.flags & ZG_ITEM_FILL) && it.len != P.nelem * P.es) {
+    if (threadIdx.x == 0) status[i] = ZG_DECODED_SIZE_MISMATCH;
+    return false;
+  }
+  return true;
+}
+
+// ---------------------------------------------------------------------------------------------
+// Rows: block = (item, group of ROWS rows). Row offsets are computed once per row into LDS.
+// ---------------------------------------------------------------------------------------------
+constexpr int ROWS_PER_BLOCK = 64;
+constexpr int SCATTER_THREADS = 256;
+
+__global__ __launch_bounds__(SCATTER_THREADS) void k_scatter_rows(
+    const ZgItem *__restrict__ items, const uint64_t *__restrict__ geom, uint32_t *__restrict__ status,
+    ZgScatter P, uint8_t *__restrict__ out, uint32_t blocks_per_item) {
+  const uint32_t item = blockIdx.x / blocks_per_item;
+  const uint32_t blk = blockIdx.x % blocks_per_item;
+  const ZgItem it = items[item];
+  if (!item_live(it, status, item, P)) return;
+  const uint32_t nd = P.nd;
+  const uint64_t *g = geom + (uint64_t)item * 3 * nd;  // sel_start | sel_shape | out_start
+  uint64_t nrows = 1;
+  for (uint32_t d = 0; d + 1 < nd; d++) nrows *= g[nd + d];
+  const uint64_t row0 = (uint64_t)blk * ROWS_PER_BLOCK;
+  if (row0 >= nrows) return;
+  const uint32_t nr = (uint32_t)min<uint64_t>(ROWS_PER_BLOCK, nrows - row0);
+  const uint64_t L = g[nd + nd - 1];  // row length (elements)
+  const uint32_t es = P.es;
+
+  __shared__ uint64_t s_src[ROWS_PER_BLOCK], s_dst[ROWS_PER_BLOCK];
+  __shared__ int s_misaligned;
+  if (threadIdx.x == 0) s_misaligned = 0;
+  __syncthreads();
+  const bool fill = it.flags & ZG_ITEM_FILL;
+  if (threadIdx.x < nr) {
+    uint64_t r = row0 + threadIdx.x, so = g[nd - 1] * P.enc_stride[nd - 1], dof = g[2 * nd + nd - 1];
+    for (int d = (int)nd - 2; d >= 0; d--) {
+      const uint64_t ext = g[nd + d], c = r % ext;
+      r /= ext;
+      so += (g[d] + c) * P.enc_stride[d];
+      dof += (g[2 * nd + d] + c) * P.out_stride[d];
+    }
+    const uint64_t sb = it.src + so * es, db = (uint64_t)out + dof * es;
+    s_src[threadIdx.x] = sb;
+    s_dst[threadIdx.x] = db;
+    if (((fill ? 0 : sb) | db | (L * es)) & 15) s_misaligned = 1;
+  }
+  __syncthreads();
+  const uint32_t swap = P.swap && P.comp > 1;
+  if (!s_misaligned && !P.shuffle) {
+    // 16-B vectors: every row start and length is 16-B aligned.
+    const uint32_t vpr = (uint32_t)(L * es / 16);
+    const uint32_t total = nr * vpr;
+    const uint4 fv = fill ? fill_elem(P) : make_uint4(0, 0, 0, 0);
+    uint4 fvec = fv;
+    if (fill) {  // replicate the element over 16 bytes
+      uint8_t b[16];
+      for (int i = 0; i < 16; i++) b[i] = P.fill[i % es];
+      fvec.x = b[0] | b[1] << 8 | b[2] << 16 | (uint32_t)b[3] << 24;
+      fvec.y = b[4] | b[5] << 8 | b[6] << 16 | (uint32_t)b[7] << 24;
+      fvec.z = b[8] | b[9] << 8 | b[10] << 16 | (uint32_t)b[11] << 24;
+      fvec.w = b[12] | b[13] << 8 | b[14] << 16 | (uint32_t)b[15] << 24;
+    }
+    for (uint32_t v = threadIdx.x; v < total; v += SCATTER_THREADS) {
+      const uint32_t r = v / vpr, c = v % vpr;
+      uint4 x;
+      if (fill) {
+        x = fvec;
+      } else {
+        x = *(const uint4 *)(s_src[r] + (uint64_t)c * 16);
+        if (swap) x = swap_vec(x, P.comp);
+      }
+      *(uint4 *)(s_dst[r] + (uint64_t)c * 16) = x;
+    }
+    return;
+  }
+  // Element path (unaligned rows, odd sizes, fused unshuffle).
+  const uint64_t total = (uint64_t)nr * L;
+  const uint4 fv = fill_elem(P);
+  for (uint64_t v = threadIdx.x; v < total; v += SCATTER_THREADS) {
+    const uint32_t r = (uint32_t)(v / L);
+    const uint64_t c = v % L;
+    uint4 x;
+    if (fill) {
+      x = fv;
+    } else if (P.shuffle) {
+      // element s of the chunk: byte b lives at src[b * nelem + s]
+      const uint64_t s = (s_src[r] - it.src) / es + c;
+      const uint8_t *base = (const uint8_t *)it.src;
+      uint8_t b[16];
+      for (uint32_t k = 0; k < es; k++) b[k] = base[(uint64_t)k * P.nelem + s];
+      if (swap)
+        for (uint32_t c0 = 0; c0 < es; c0 += P.comp)
+          for (uint32_t a = 0, bb = P.comp - 1; a < bb; a++, bb--) {
+            uint8_t t = b[c0 + a]; b[c0 + a] = b[c0 + bb]; b[c0 + bb] = t;
+          }
+      uint32_t w[4] = {0, 0, 0, 0};
+      for (uint32_t k = 0; k < es; k++) w[k >> 2] |= (uint32_t)b[k] << (8 * (k & 3));
+      x = make_uint4(w[0], w[1], w[2], w[3]);
+    } else {
+      x = load_elem((const uint8_t *)(s_src[r] + c * es), es, P.comp, swap);
+    }
+    store_elem((uint8_t *)(s_dst[r] + c * es), x, es);
+  }
+}
+
+// ---------------------------------------------------------------------------------------------
+// Tiled transpose: decoded axis A = P.tile_a is innermost (stride 1) in the encoded layout,
+// decoded axis Lx = nd-1 is innermost in the output. A tile is TA x TL elements for fixed values
+// of the other axes; loaded along A (contiguous), stored along Lx (contiguous) via LDS.
+// ---------------------------------------------------------------------------------------------
+constexpr int TILE = 64;
+
+template <int ES>
+__global__ __launch_bounds__(SCATTER_THREADS) void k_scatter_tiled(
+    const ZgItem *__restrict__ items, const uint64_t *__restrict__ geom, uint32_t *__restrict__ status,
+    ZgScatter P, uint8_t *__restrict__ out, uint32_t tiles_per_item) {
+  using T = typename std::conditional<ES == 1, uint8_t, typename std::conditional<ES == 2, uint16_t,
+            typename std::conditional<ES == 4, uint32_t, uint2>::type>::type>::type;
+  // one padded row per L index; +1 element pad keeps column reads at 2-way conflicts at most
+  __shared__ T tile[TILE][TILE + (ES >= 4 ? 1 : 4 / ES)];
+  const uint32_t item = blockIdx.x / tiles_per_item;
+  uint32_t t = blockIdx.x % tiles_per_item;
+  const ZgItem it = items[item];
+  if (!item_live(it, status, item, P)) return;
+  const uint32_t nd = P.nd, A = P.tile_a, Lx = nd - 1;
+  const uint64_t *g = geom + (uint64_t)item * 3 * nd;
+  const uint64_t *ss = g, *sh = g + nd, *os = g + 2 * nd;
+  const uint32_t nta = (uint32_t)((sh[A] + TILE - 1) / TILE), ntl = (uint32_t)((sh[Lx] + TILE - 1) / TILE);
+  const uint32_t ta = t % nta; t /= nta;
+  const uint32_t tl = t % ntl; t /= ntl;
+  // remaining index enumerates the other axes (row-major over axes != A, Lx)
+  uint64_t so = 0, dof = 0, rem = t;
+  for (int d = (int)nd - 1; d >= 0; d--) {
+    if ((uint32_t)d == A || (uint32_t)d == Lx) continue;
+    const uint64_t c = rem % sh[d];
+    rem /= sh[d];
+    so += (ss[d] + c) * P.enc_stride[d];
+    dof += (os[d] + c) * P.out_stride[d];
+  }
+  if (rem) return;  // beyond this item's selection
+  const uint64_t a0 = (uint64_t)ta * TILE, l0 = (uint64_t)tl * TILE;
+  const uint32_t na = (uint32_t)min<uint64_t>(TILE, sh[A] - a0), nl = (uint32_t)min<uint64_t>(TILE, sh[Lx] - l0);
+  so += (ss[A] + a0) * P.enc_stride[A] + (ss[Lx] + l0) * P.enc_stride[Lx];
+  dof += (os[A] + a0) * P.out_stride[A] + (os[Lx] + l0);
+  const bool fill = it.flags & ZG_ITEM_FILL;
+  T *dst = (T *)(out) + dof;
+  if (fill) {
+    T fv;
+    __builtin_memcpy(&fv, P.fill, ES);
+    for (uint32_t e = threadIdx.x; e < na * TILE; e += SCATTER_THREADS) {
+      const uint32_t a = e / TILE, l = e % TILE;
+      if (l < nl) dst[(uint64_t)a * P.out_stride[A] + l] = fv;
+    }
+    return;
+  }
+  const T *src = (const T *)(it.src) + so;
+  const uint64_t sL = P.enc_stride[Lx], dA = P.out_stride[A];
+  const uint32_t swap = P.swap && P.comp > 1;
+  const bool aligned = ((it.src & 15) == 0) && ((sL * ES) % 16 == 0) && (((so + 0) * ES) % 16 == 0) &&
+                       na == TILE;
+  constexpr int VPR = TILE * ES / 16;          // 16-B vectors per tile row
+  constexpr int EPV = 16 / ES;                  // elements per vector
+  if (aligned) {
+    constexpr int RPP = SCATTER_THREADS / VPR;  // rows per pass
+#pragma unroll
+    for (int p = 0; p < TILE / RPP; p++) {
+      const uint32_t l = p * RPP + threadIdx.x / VPR, v = threadIdx.x % VPR;
+      if (l < nl) {
+        uint4 x = *(const uint4 *)(src + (uint64_t)l * sL + v * EPV);
+        if (swap) x = swap_vec(x, P.comp);
+        const T *xe = (const T *)&x;
+#pragma unroll
+        for (int k = 0; k < EPV; k++) tile[l][v * EPV + k] = xe[k];
+      }
+    }
+  } else {
+    for (uint32_t e = threadIdx.x; e < TILE * TILE; e += SCATTER_THREADS) {
+      const uint32_t l = e / TILE, a = e % TILE;
+      if (l < nl && a < na) {
+        uint4 x = load_elem((const uint8_t *)(src + (uint64_t)l * sL + a), ES, P.comp, swap);
+        T v;
+        __builtin_memcpy(&v, &x, ES);
+        tile[l][a] = v;
+      }
+    }
+  }
+  __syncthreads();
+  const bool oaligned = (((uint64_t)dst & 15) == 0) && ((dA * ES) % 16 == 0) && nl == TILE;
+  if (oaligned) {
+    constexpr int RPP = SCATTER_THREADS / VPR;
+#pragma unroll
+    for (int p = 0; p < TILE / RPP; p++) {
+      const uint32_t a = p * RPP + threadIdx.x / VPR, v = threadIdx.x % VPR;
+      if (a < na) {
+        uint4 x;
+        T *xe = (T *)&x;
+#pragma unroll
+        for (int k = 0; k < EPV; k++) xe[k] = tile[v * EPV + k][a];
+        *(uint4 *)(dst + (uint64_t)a * dA + v * EPV) = x;
+      }
+    }
+  } else {
+    for (uint32_t e = threadIdx.x; e < TILE * TILE; e += SCATTER_THREADS) {
+      const uint32_t a = e / TILE, l = e % TILE;
+      if (a < na && l < nl) dst[(uint64_t)a * dA + l] = tile[l][a];
+    }
+  }
+}
+
+// ---------------------------------------------------------------------------------------------
+// Generic element gather: one thread per selected element.
+// ---------------------------------------------------------------------------------------------
+__global__ __launch_bounds__(SCATTER_THREADS) void k_scatter_generic(
+    const ZgItem *__restrict__ items, const uint64_t *__restrict__ geom, uint32_t *__restrict__ status,
+    ZgScatter P, uint8_t *__restrict__ out, uint32_t blocks_per_item) {
+  const uint32_t item = blockIdx.x / blocks_per_item;
+  const uint32_t blk = blockIdx.x % blocks_per_item;
+  const ZgItem it = items[item];
+  if (!item_live(it, status, item, P)) return;
+  const uint32_t nd = P.nd, es = P.es;
+  const uint64_t *g = geom + (uint64_t)item * 3 * nd;
+  uint64_t n = 1;
+  for (uint32_t d = 0; d < nd; d++) n *= g[nd + d];
+  const uint64_t e = (uint64_t)blk * SCATTER_THREADS + threadIdx.x;
+  if (e >= n) return;
+  uint64_t rem = e, so = 0, dof = 0;
+  for (int d = (int)nd - 1; d >= 0; d--) {
+    const uint64_t c = rem % g[nd + d];
+    rem /= g[nd + d];
+    so += (g[d] + c) * P.enc_stride[d];
+    dof += (g[2 * nd + d] + c) * P.out_stride[d];
+  }
+  const uint32_t swap = P.swap && P.comp > 1;
+  uint4 x;
+  if (it.flags & ZG_ITEM_FILL) {
+    x = fill_elem(P);
+  } else if (P.shuffle) {
+    const uint8_t *base = (const uint8_t *)it.src;
+    uint8_t b[16];
+    for (uint32_t k = 0; k < es; k++) b[k] = base[(uint64_t)k * P.nelem + so];
+    if (swap)
+      for (uint32_t c0 = 0; c0 < es; c0 += P.comp)
+        for (uint32_t a = 0, bb = P.comp - 1; a < bb; a++, bb--) {
+          uint8_t t = b[c0 + a]; b[c0 + a] = b[c0 + bb]; b[c0 + bb] = t;
+        }
+    uint32_t w[4] = {0, 0, 0, 0};
+    for (uint32_t k = 0; k < es; k++) w[k >> 2] |= (uint32_t)b[k] << (8 * (k & 3));
+    x = make_uint4(w[0], w[1], w[2], w[3]);
+  } else {
+    x = load_elem((const uint8_t *)it.src + so * es, es, P.comp, swap);
+  }
+  store_elem(out + dof * es, x, es);
+}
+
+// ---------------------------------------------------------------------------------------------
+hipError_t launch_scatter(const ZgItem *items, const uint64_t *geom, uint32_t *status, const ZgScatter &P,
+                          uint8_t *out, uint32_t n_items, uint32_t mode, uint64_t units_per_item,
+                          hipStream_t s) {
+  if (n_items == 0 || units_per_item == 0) return hipSuccess;
+  const uint64_t grid = (uint64_t)n_items * units_per_item;
+  if (grid > 0x7fffffffull) return hipErrorInvalidConfiguration;
+  const uint32_t u = (uint32_t)units_per_item;
+  switch (mode) {
+    case SCATTER_ROWS:
+      hipLaunchKernelGGL(k_scatter_rows, dim3((uint32_t)grid), dim3(SCATTER_THREADS), 0, s, items, geom,
+                         status, P, out, u);
+      break;
+    case SCATTER_TILED:
+      switch (P.es) {
+        case 1: hipLaunchKernelGGL(k_scatter_tiled<1>, dim3((uint32_t)grid), dim3(SCATTER_THREADS), 0, s, items, geom, status, P, out, u); break;
+        case 2: hipLaunchKernelGGL(k_scatter_tiled<2>, dim3((uint32_t)grid), dim3(SCATTER_THREADS), 0, s, items, geom, status, P, out, u); break;
+        case 4: hipLaunchKernelGGL(k_scatter_tiled<4>, dim3((uint32_t)grid), dim3(SCATTER_THREADS), 0, s, items, geom, status, P, out, u); break;
+        case 8: hipLaunchKernelGGL(k_scatter_tiled<8>, dim3((uint32_t)grid), dim3(SCATTER_THREADS), 0, s, items, geom, status, P, out, u); break;
+        default: return hipErrorInvalidValue;
+      }
+      break;
+    default:
+      hipLaunchKernelGGL(k_scatter_generic, dim3((uint32_t)grid), dim3(SCATTER_THREADS), 0, s, items, geom,
+                         status, P, out, u);
+  }
+  return hipGetLastError();
+}
+
+uint64_t scatter_units_per_item(uint32_t mode, const ZgScatter &P, const uint64_t *max_sel_shape) {
+  const uint32_t nd = P.nd;
+  if (mode == SCATTER_ROWS) {
+    uint64_t rows = 1;
+    for (uint32_t d = 0; d + 1 < nd; d++) rows *= max_sel_shape[d];
+    return (rows + ROWS_PER_BLOCK - 1) / ROWS_PER_BLOCK;
+  }
+  if (mode == SCATTER_TILED) {
+    uint64_t t = 1;
+    for (uint32_t d = 0; d < nd; d++) {
+      if (d == P.tile_a || d == nd - 1) t *= (max_sel_shape[d] + TILE - 1) / TILE;
+      else t *= max_sel_shape[d];
+    }
+    return t;
+  }
+  uint64_t n = 1;
+  for (uint32_t d = 0; d < nd; d++) n *= max_sel_shape[d];
+  return (n + SCATTER_THREADS - 1) / SCATTER_THREADS;
+}
+
+}  // namespace zgpu

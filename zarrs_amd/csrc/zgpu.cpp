@@ -1,0 +1,730 @@
+// libzgpu: host orchestration of the MI355X chunk-decode pipeline behind the C ABI of include/zgpu.h.
+//
+// A batch of chunk descriptors is planned on the host into leaf work items (a plain chunk, or one
+// inner chunk of a shard that intersects the selection), uploaded once, and decoded by a short
+// sequence of batched kernels, each over ALL items of the batch:
+//   [sharded]  k_shard_index (index chain decode + crc32c verify per shard)
+//              k_item_resolve (index lookup per item: byte range, empty -> fill, out-of-bounds)
+//   b2b stages in reverse metadata order (codec_chain.rs:612-617):
+//              crc32c verify+strip (pointer arithmetic, no copy) | gzip | zstd | unshuffle
+//   final      fused bytes(endian) + transpose + (innermost shuffle) + scatter/fill into the output
+// Per-item statuses come back in one D2H copy; the first failing item of a descriptor gives that
+// descriptor's status (try_for_each semantics, sharding_codec.rs:702-704).
+#include <hip/hip_runtime.h>
+
+#include <algorithm>
+#include <cstdio>
+#include <cstring>
+#include <map>
+#include <memory>
+#include <mutex>
+#include <string>
+#include <vector>
+
+#include "../../include/zgpu.h"
+#include "chain.hpp"
+#include "common.hpp"
+#include "kernels/launch.hpp"
+
+using namespace zgpu;
+
+namespace {
+
+thread_local std::string g_last_error;
+
+struct HipFail {
+  hipError_t e;
+  const char *what;
+};
+#define HIPCHK(x)                                   \
+  do {                                              \
+    hipError_t _e = (x);                            \
+    if (_e != hipSuccess) throw HipFail{_e, #x};    \
+  } while (0)
+
+}  // namespace
+
+// ------------------------------------------------------------------------------------------------
+// Context: one per GPU. Owns a stream and a caching device allocator (grow-only pools reused across
+// calls so a steady-state decode performs no hipMalloc).
+// ------------------------------------------------------------------------------------------------
+struct zgpu_ctx {
+  int device = 0;
+  hipStream_t stream = nullptr;
+  std::mutex mu;
+  std::multimap<size_t, void *> free_dev;  // size -> ptr
+  std::map<void *, size_t> live_dev;
+  std::multimap<size_t, void *> free_host;
+  std::map<void *, size_t> live_host;
+
+  void *dev_alloc(size_t bytes) {
+    bytes = std::max<size_t>(256, (bytes + 255) & ~(size_t)255);
+    auto it = free_dev.lower_bound(bytes);
+    if (it != free_dev.end() && it->first <= bytes * 2 + (1u << 20)) {
+      void *p = it->second;
+      live_dev[p] = it->first;
+      free_dev.erase(it);
+      return p;
+    }
+    void *p = nullptr;
+    hipError_t e = hipMalloc(&p, bytes);
+    if (e != hipSuccess) {  // release the cache and retry once
+      for (auto &kv : free_dev) (void)hipFree(kv.second);
+      free_dev.clear();
+      HIPCHK(hipMalloc(&p, bytes));
+    }
+    live_dev[p] = bytes;
+    return p;
+  }
+  void dev_free(void *p) {
+    if (!p) return;
+    auto it = live_dev.find(p);
+    if (it == live_dev.end()) return;
+    free_dev.emplace(it->second, p);
+    live_dev.erase(it);
+  }
+  void *host_alloc(size_t bytes) {
+    bytes = std::max<size_t>(4096, (bytes + 4095) & ~(size_t)4095);
+    auto it = free_host.lower_bound(bytes);
+    if (it != free_host.end() && it->first <= bytes * 2 + (1u << 20)) {
+      void *p = it->second;
+      live_host[p] = it->first;
+      free_host.erase(it);
+      return p;
+    }
+    void *p = nullptr;
+    HIPCHK(hipHostMalloc(&p, bytes, hipHostMallocDefault));
+    live_host[p] = bytes;
+    return p;
+  }
+  void host_free(void *p) {
+    if (!p) return;
+    auto it = live_host.find(p);
+    if (it == live_host.end()) return;
+    free_host.emplace(it->second, p);
+    live_host.erase(it);
+  }
+  ~zgpu_ctx() {
+    (void)hipSetDevice(device);
+    if (stream) (void)hipStreamSynchronize(stream);
+    for (auto &kv : free_dev) (void)hipFree(kv.second);
+    for (auto &kv : live_dev) (void)hipFree(kv.first);
+    for (auto &kv : free_host) (void)hipHostFree(kv.second);
+    for (auto &kv : live_host) (void)hipHostFree(kv.first);
+    if (stream) (void)hipStreamDestroy(stream);
+  }
+};
+
+struct zgpu_chain {
+  zgpu_ctx *ctx;
+  std::shared_ptr<Chain> chain;
+  bool validate;
+};
+
+// ------------------------------------------------------------------------------------------------
+// Plan
+// ------------------------------------------------------------------------------------------------
+enum StageKind { ST_CRC32C, ST_GZIP, ST_ZSTD, ST_UNSHUFFLE };
+struct Stage {
+  StageKind kind;
+  int at_start = 0;
+  uint32_t elementsize = 0;
+  int pool = 0;  // destination slot pool for materialising stages
+};
+
+struct zgpu_plan {
+  zgpu_ctx *ctx = nullptr;
+  std::shared_ptr<Chain> chain;
+  const Chain *leaf = nullptr;
+  bool validate = true;
+  uint32_t nd = 0;
+  uint64_t n_desc = 0;
+  uint32_t flags = 0;
+  std::vector<uint64_t> out_shape;
+  // host tables
+  std::vector<ZgItem> items;
+  std::vector<uint64_t> geom;
+  std::vector<uint32_t> item_desc_status;  // plan-time per-desc status
+  std::vector<ZgShard> shards;
+  std::vector<Stage> stages;
+  ZgScatter scatter{};
+  uint32_t scatter_mode = SCATTER_GENERIC;
+  uint64_t scatter_units = 0;
+  bool sharded = false;
+  ZgIndexSpec ispec{};
+  uint64_t slot_bytes = 0;
+  int n_pools = 0;
+  uint64_t alg_bytes_static = 0;  // decoded bytes written + (unsharded) encoded bytes + index bytes
+  // device buffers
+  ZgItem *d_items = nullptr, *d_items_init = nullptr;
+  uint64_t *d_geom = nullptr;
+  uint32_t *d_status = nullptr;
+  ZgShard *d_shards = nullptr;
+  uint64_t *d_index = nullptr;
+  uint32_t *d_shard_status = nullptr;
+  uint8_t *d_pool[2] = {nullptr, nullptr};
+  uint2 *d_aux = nullptr;
+  unsigned long long *d_counter = nullptr;
+  // host-input staging
+  uint8_t *d_enc_stage = nullptr;
+  uint64_t last_enc_bytes = 0;
+
+  ~zgpu_plan() {
+    if (!ctx) return;
+    void *bufs[] = {d_items, d_items_init, d_geom, d_status, d_shards, d_index, d_shard_status,
+                    d_pool[0], d_pool[1], d_aux, d_counter, d_enc_stage};
+    for (void *b : bufs) ctx->dev_free(b);
+  }
+};
+
+static int set_err(int st, const std::string &m) {
+  g_last_error = m;
+  return st;
+}
+
+// composed permutation of all array->array codecs: encoded axis a <-> decoded axis m[a]
+static void composed_axes(const Chain &c, uint32_t nd, uint32_t *m) {
+  for (uint32_t a = 0; a < nd; a++) m[a] = a;
+  for (const Codec &k : c.a2a) {  // E_{k} axis a <-> E_{k-1} axis order[a]
+    uint32_t t[ZG_MAXD];
+    for (uint32_t a = 0; a < nd; a++) t[a] = m[k.order[a]];
+    std::memcpy(m, t, nd * sizeof(uint32_t));
+  }
+}
+
+static void build_leaf_stages(zgpu_plan &P, const Chain &leaf, uint64_t nelem) {
+  // decode order: last b2b first
+  const int nb = (int)leaf.b2b.size();
+  int pool = 0;
+  uint64_t max_slot = 0;
+  bool fused_shuffle = false;
+  for (int i = nb - 1; i >= 0; i--) {
+    const Codec &k = leaf.b2b[i];
+    Stage s;
+    if (k.kind == CodecKind::Crc32c) {
+      s.kind = ST_CRC32C;
+      s.at_start = k.at_start;
+      P.stages.push_back(s);
+      continue;
+    }
+    if (k.kind == CodecKind::Shuffle && i == 0 && k.elementsize == leaf.es) {
+      fused_shuffle = true;  // fused into the scatter stage
+      continue;
+    }
+    // materialising stage: its output is the encoded representation of codecs [bytes, b2b_0..i-1]
+    int64_t out_size = (int64_t)(nelem * leaf.es);
+    for (int j = 0; j < i; j++) {
+      if (leaf.b2b[j].kind == CodecKind::Crc32c) out_size += 4;
+      else if (leaf.b2b[j].kind != CodecKind::Shuffle) out_size = -1;
+      if (out_size < 0) break;
+    }
+    if (out_size < 0) throw ChainError{ZGPU_UNSUPPORTED, "a compressor nested inside another variable-size codec"};
+    s.kind = k.kind == CodecKind::Gzip ? ST_GZIP : k.kind == CodecKind::Zstd ? ST_ZSTD : ST_UNSHUFFLE;
+    s.elementsize = k.elementsize;
+    s.pool = pool;
+    pool ^= 1;
+    max_slot = std::max<uint64_t>(max_slot, (uint64_t)out_size);
+    P.stages.push_back(s);
+    P.n_pools = std::min(2, P.n_pools + 1);
+  }
+  P.slot_bytes = (max_slot + 255) & ~(uint64_t)255;
+  P.scatter.shuffle = fused_shuffle;
+}
+
+static void plan_build(zgpu_plan &P, const zgpu_chunk_desc *descs) {
+  const Chain &top = *P.chain;
+  const uint32_t nd = P.nd;
+  P.item_desc_status.assign(P.n_desc, 0);
+  const bool shard_chain = top.a2b.kind == CodecKind::Sharding;
+  if (shard_chain) {
+    if (!top.a2a.empty()) throw ChainError{ZGPU_UNSUPPORTED, "array->array codecs before sharding_indexed"};
+    if (top.a2b.inner->a2b.kind == CodecKind::Sharding) throw ChainError{ZGPU_UNSUPPORTED, "nested sharding"};
+    if (!top.b2b.empty()) throw ChainError{ZGPU_UNSUPPORTED, "bytes->bytes codecs after sharding_indexed"};
+    if (top.a2b.inner_shape.size() != nd) throw ChainError{ZGPU_INVALID_ARGUMENT, "sharding chunk_shape rank"};
+  }
+  const Chain &leaf = shard_chain ? *top.a2b.inner : top;
+  P.leaf = &leaf;
+  P.sharded = shard_chain;
+  for (const Codec &k : leaf.a2a)
+    if (k.order.size() != nd) throw ChainError{ZGPU_INVALID_ARGUMENT, "transpose order rank != array rank"};
+
+  // leaf chunk shape
+  uint64_t leaf_shape[ZG_MAXD];
+  if (shard_chain) {
+    for (uint32_t d = 0; d < nd; d++) leaf_shape[d] = top.a2b.inner_shape[d];
+  } else if (P.n_desc) {
+    for (uint32_t d = 0; d < nd; d++) leaf_shape[d] = descs[0].chunk_shape[d];
+  } else {
+    for (uint32_t d = 0; d < nd; d++) leaf_shape[d] = 1;
+  }
+  uint64_t nelem = 1;
+  for (uint32_t d = 0; d < nd; d++) nelem *= leaf_shape[d];
+
+  uint64_t out_strides[ZG_MAXD], s = 1;
+  for (int d = (int)nd - 1; d >= 0; d--) {
+    out_strides[d] = s;
+    s *= P.out_shape[d];
+  }
+  const uint64_t es = top.es;
+  uint64_t max_sel[ZG_MAXD] = {0};
+  uint64_t n_inner = 1, cps[ZG_MAXD];
+  if (shard_chain) {
+    int64_t isz = -1;
+    for (uint32_t d = 0; d < nd; d++) cps[d] = 0;
+    (void)isz;
+  }
+
+  for (uint64_t i = 0; i < P.n_desc; i++) {
+    const zgpu_chunk_desc &D = descs[i];
+    bool ok = true, full = true;
+    for (uint32_t d = 0; d < nd; d++) {
+      if (D.chunk_shape[d] == 0 || D.sel_start[d] + D.sel_shape[d] > D.chunk_shape[d] ||
+          D.out_start[d] + D.sel_shape[d] > P.out_shape[d])
+        ok = false;
+      if (D.sel_start[d] != 0 || D.sel_shape[d] != D.chunk_shape[d]) full = false;
+      if (!shard_chain && D.chunk_shape[d] != leaf_shape[d]) ok = false;
+    }
+    if (!ok) {
+      P.item_desc_status[i] = ZGPU_INVALID_ARGUMENT;
+      continue;
+    }
+    uint64_t vol = 1;
+    for (uint32_t d = 0; d < nd; d++) vol *= D.sel_shape[d];
+    if (vol == 0) continue;
+    P.alg_bytes_static += vol * es;
+    if (!shard_chain) {
+      ZgItem it{};
+      it.src = (uint64_t)D.enc;
+      it.len = D.enc_len;
+      it.desc = (uint32_t)i;
+      it.flags = (D.enc ? 0u : ZG_ITEM_FILL) | (full ? 0u : ZG_ITEM_PARTIAL);
+      if (D.enc) P.alg_bytes_static += D.enc_len;
+      P.items.push_back(it);
+      for (uint32_t d = 0; d < nd; d++) P.geom.push_back(D.sel_start[d]);
+      for (uint32_t d = 0; d < nd; d++) P.geom.push_back(D.sel_shape[d]);
+      for (uint32_t d = 0; d < nd; d++) P.geom.push_back(D.out_start[d]);
+      for (uint32_t d = 0; d < nd; d++) max_sel[d] = std::max(max_sel[d], D.sel_shape[d]);
+      continue;
+    }
+    // sharded descriptor: one item per intersecting inner chunk
+    n_inner = 1;
+    for (uint32_t d = 0; d < nd; d++) {
+      if (D.chunk_shape[d] % leaf_shape[d]) ok = false;
+      cps[d] = D.chunk_shape[d] / leaf_shape[d];
+      n_inner *= cps[d];
+    }
+    if (!ok) {  // calculate_chunks_per_shard error (sharding.rs:136-154)
+      P.item_desc_status[i] = ZGPU_INVALID_ARGUMENT;
+      continue;
+    }
+    if (P.ispec.n_inner && P.ispec.n_inner != n_inner) {
+      P.item_desc_status[i] = ZGPU_UNSUPPORTED;  // mixed shard shapes in one batch
+      continue;
+    }
+    P.ispec.n_inner = n_inner;
+    const uint32_t shard_slot = (uint32_t)P.shards.size();
+    P.shards.push_back(ZgShard{(uint64_t)D.enc, D.enc ? D.enc_len : 0});
+    uint64_t lo[ZG_MAXD], hi[ZG_MAXD], idx[ZG_MAXD];
+    for (uint32_t d = 0; d < nd; d++) {
+      lo[d] = D.sel_start[d] / leaf_shape[d];
+      hi[d] = (D.sel_start[d] + D.sel_shape[d] - 1) / leaf_shape[d] + 1;
+      idx[d] = lo[d];
+    }
+    for (;;) {
+      uint64_t lin = 0;
+      ZgItem it{};
+      it.desc = (uint32_t)i;
+      it.shard = shard_slot;
+      it.flags = D.enc ? (ZG_ITEM_SHARDED | (full ? 0u : ZG_ITEM_PARTIAL)) : ZG_ITEM_FILL;
+      uint64_t g[3 * ZG_MAXD];
+      for (uint32_t d = 0; d < nd; d++) {
+        lin = lin * cps[d] + idx[d];
+        const uint64_t cs = idx[d] * leaf_shape[d], ce = cs + leaf_shape[d];
+        const uint64_t s0 = std::max(D.sel_start[d], cs), s1 = std::min(D.sel_start[d] + D.sel_shape[d], ce);
+        g[d] = s0 - cs;
+        g[nd + d] = s1 - s0;
+        g[2 * nd + d] = D.out_start[d] + (s0 - D.sel_start[d]);
+        max_sel[d] = std::max(max_sel[d], s1 - s0);
+      }
+      it.inner = (uint32_t)lin;
+      P.items.push_back(it);
+      P.geom.insert(P.geom.end(), g, g + 3 * nd);
+      int d = (int)nd - 1;
+      for (; d >= 0; d--) {
+        if (++idx[d] < hi[d]) break;
+        idx[d] = lo[d];
+      }
+      if (d < 0) break;
+    }
+  }
+
+  if (shard_chain) {
+    const Chain &xc = *top.a2b.index;
+    if (xc.a2b.kind != CodecKind::Bytes || !xc.a2a.empty())
+      throw ChainError{ZGPU_UNSUPPORTED, "index_codecs must be bytes (+crc32c)"};
+    for (const Codec &k : xc.b2b)
+      if (k.kind != CodecKind::Crc32c) throw ChainError{ZGPU_UNSUPPORTED, "index_codecs must be bytes (+crc32c)"};
+    if (xc.b2b.size() > 4) throw ChainError{ZGPU_UNSUPPORTED, "too many index crc32c codecs"};
+    const int64_t isz = chain_fixed_encoded_size(xc, P.ispec.n_inner * 2);
+    P.ispec.index_bytes = (uint64_t)isz;
+    P.ispec.at_start = top.a2b.at_start;
+    P.ispec.big_endian = xc.a2b.big_endian;
+    P.ispec.n_crc = (uint32_t)xc.b2b.size();
+    for (size_t k = 0; k < xc.b2b.size(); k++) P.ispec.crc_at_start[k] = xc.b2b[k].at_start;
+    P.ispec.verify = P.validate;
+    for (const ZgShard &sh : P.shards)
+      if (sh.ptr) P.alg_bytes_static += P.ispec.index_bytes;
+  }
+
+  build_leaf_stages(P, leaf, nelem);
+
+  // scatter parameters
+  ZgScatter &S = P.scatter;
+  S.nd = nd;
+  S.es = leaf.es;
+  S.comp = leaf.comp;
+  S.swap = leaf.a2b.big_endian && leaf.comp > 1;
+  S.nelem = nelem;
+  std::memcpy(S.fill, leaf.fill, 16);
+  uint32_t m[ZG_MAXD];
+  composed_axes(leaf, nd, m);
+  uint64_t eshape[ZG_MAXD], est[ZG_MAXD];
+  for (uint32_t a = 0; a < nd; a++) eshape[a] = leaf_shape[m[a]];
+  s = 1;
+  for (int a = (int)nd - 1; a >= 0; a--) {
+    est[a] = s;
+    s *= eshape[a];
+  }
+  for (uint32_t a = 0; a < nd; a++) S.enc_stride[m[a]] = est[a];
+  for (uint32_t d = 0; d < nd; d++) {
+    S.chunk_shape[d] = leaf_shape[d];
+    S.out_stride[d] = out_strides[d];
+  }
+  S.tile_a = m[nd - 1];
+  if (S.tile_a == nd - 1) {
+    P.scatter_mode = SCATTER_ROWS;
+  } else if (!S.shuffle && (S.es == 1 || S.es == 2 || S.es == 4 || S.es == 8)) {
+    P.scatter_mode = SCATTER_TILED;
+  } else {
+    P.scatter_mode = SCATTER_GENERIC;
+  }
+  P.scatter_units = P.items.empty() ? 0 : scatter_units_per_item(P.scatter_mode, S, max_sel);
+}
+
+static void plan_upload(zgpu_plan &P) {
+  zgpu_ctx &C = *P.ctx;
+  const size_t ni = P.items.size();
+  if (ni) {
+    P.d_items = (ZgItem *)C.dev_alloc(ni * sizeof(ZgItem));
+    P.d_items_init = (ZgItem *)C.dev_alloc(ni * sizeof(ZgItem));
+    P.d_geom = (uint64_t *)C.dev_alloc(P.geom.size() * 8);
+    P.d_status = (uint32_t *)C.dev_alloc(ni * 4);
+    HIPCHK(hipMemcpyAsync(P.d_items_init, P.items.data(), ni * sizeof(ZgItem), hipMemcpyHostToDevice, C.stream));
+    HIPCHK(hipMemcpyAsync(P.d_geom, P.geom.data(), P.geom.size() * 8, hipMemcpyHostToDevice, C.stream));
+    for (int k = 0; k < P.n_pools; k++) P.d_pool[k] = (uint8_t *)C.dev_alloc(ni * P.slot_bytes);
+    for (const Stage &s : P.stages)
+      if (s.kind == ST_GZIP && !P.d_aux) P.d_aux = (uint2 *)C.dev_alloc(ni * sizeof(uint2));
+  }
+  P.d_counter = (unsigned long long *)C.dev_alloc(256);
+  if (!P.shards.empty()) {
+    P.d_shards = (ZgShard *)C.dev_alloc(P.shards.size() * sizeof(ZgShard));
+    P.d_index = (uint64_t *)C.dev_alloc(P.shards.size() * P.ispec.n_inner * 16);
+    P.d_shard_status = (uint32_t *)C.dev_alloc(P.shards.size() * 4);
+    HIPCHK(hipMemcpyAsync(P.d_shards, P.shards.data(), P.shards.size() * sizeof(ZgShard), hipMemcpyHostToDevice,
+                          C.stream));
+  }
+}
+
+// Enqueue the decode of an uploaded plan on stream s.
+static void plan_enqueue(zgpu_plan &P, uint8_t *out, hipStream_t s) {
+  const uint32_t ni = (uint32_t)P.items.size();
+  HIPCHK(hipMemsetAsync(P.d_counter, 0, 256, s));
+  if (!ni) return;
+  HIPCHK(hipMemcpyAsync(P.d_items, P.d_items_init, ni * sizeof(ZgItem), hipMemcpyDeviceToDevice, s));
+  HIPCHK(hipMemsetAsync(P.d_status, 0, (size_t)ni * 4, s));
+  if (P.sharded) {
+    HIPCHK(launch_shard_index(P.d_shards, (uint32_t)P.shards.size(), P.ispec, P.d_index, P.d_shard_status, s));
+    HIPCHK(launch_item_resolve(P.d_items, P.d_status, ni, P.d_shards, P.d_index, P.d_shard_status, P.ispec.n_inner,
+                               P.d_counter, s));
+  }
+  for (const Stage &st : P.stages) {
+    switch (st.kind) {
+      case ST_CRC32C:
+        HIPCHK(launch_crc32c_strip(P.d_items, P.d_status, ni, st.at_start, P.validate ? 1 : 0, s));
+        break;
+      case ST_GZIP:
+        HIPCHK(launch_gzip(P.d_items, P.d_status, ni, P.d_pool[st.pool], P.slot_bytes, P.d_aux, s));
+        HIPCHK(launch_crc32_check(P.d_items, P.d_status, ni, P.d_aux, s));
+        break;
+      case ST_ZSTD:
+        HIPCHK(launch_zstd(P.d_items, P.d_status, ni, P.d_pool[st.pool], P.slot_bytes, s));
+        break;
+      case ST_UNSHUFFLE:
+        HIPCHK(launch_unshuffle(P.d_items, P.d_status, ni, P.d_pool[st.pool], P.slot_bytes, st.elementsize, s));
+        break;
+    }
+  }
+  HIPCHK(launch_scatter(P.d_items, P.d_geom, P.d_status, P.scatter, out, ni, P.scatter_mode, P.scatter_units, s));
+}
+
+// Read back per-item statuses and reduce them to per-descriptor statuses. Returns the first
+// non-zero descriptor status.
+static int plan_statuses(zgpu_plan &P, int32_t *status, hipStream_t s) {
+  const size_t ni = P.items.size();
+  std::vector<uint32_t> st(ni);
+  unsigned long long counter = 0;
+  if (ni) HIPCHK(hipMemcpyAsync(st.data(), P.d_status, ni * 4, hipMemcpyDeviceToHost, s));
+  HIPCHK(hipMemcpyAsync(&counter, P.d_counter, 8, hipMemcpyDeviceToHost, s));
+  HIPCHK(hipStreamSynchronize(s));
+  P.last_enc_bytes = counter;
+  std::vector<int32_t> ds(P.item_desc_status.begin(), P.item_desc_status.end());
+  for (size_t i = 0; i < ni; i++) {
+    const uint32_t d = P.items[i].desc;
+    if (st[i] && ds[d] == 0) ds[d] = (int32_t)st[i];
+  }
+  int first = 0;
+  for (uint64_t d = 0; d < P.n_desc; d++) {
+    if (status) status[d] = ds[d];
+    if (!first && ds[d]) first = ds[d];
+  }
+  return first;
+}
+
+static zgpu_plan *plan_new(zgpu_chain *ch, uint32_t nd, const zgpu_chunk_desc *descs, uint64_t n,
+                           const uint64_t *out_shape, uint32_t flags) {
+  auto P = std::make_unique<zgpu_plan>();
+  P->ctx = ch->ctx;
+  P->chain = ch->chain;
+  P->validate = ch->validate && !(flags & ZGPU_NO_VALIDATE);
+  P->nd = nd;
+  P->n_desc = n;
+  P->flags = flags;
+  P->out_shape.assign(out_shape, out_shape + nd);
+  plan_build(*P, descs);
+  return P.release();
+}
+
+static hipStream_t pick_stream(zgpu_ctx *c, void *s) { return s ? (hipStream_t)s : c->stream; }
+
+// ------------------------------------------------------------------------------------------------
+// C ABI
+// ------------------------------------------------------------------------------------------------
+#define ABI_GUARD_BEGIN try {
+#define ABI_GUARD_END                                                                          \
+  }                                                                                            \
+  catch (const ChainError &e) {                                                                \
+    return set_err(e.status, e.msg);                                                           \
+  }                                                                                            \
+  catch (const HipFail &e) {                                                                   \
+    return set_err(ZGPU_HIP_ERROR, std::string(e.what) + ": " + hipGetErrorString(e.e));       \
+  }                                                                                            \
+  catch (const std::exception &e) {                                                            \
+    return set_err(ZGPU_INVALID_ARGUMENT, e.what());                                           \
+  }
+
+extern "C" {
+
+const char *zgpu_version(void) { return "zgpu 0.1.0 (gfx950)"; }
+
+const char *zgpu_status_name(int s) {
+  static const char *names[] = {"OK", "INVALID_CHECKSUM", "DECODED_SIZE_MISMATCH", "SHARD_INDEX_OOB",
+                                "CORRUPT_STREAM", "INVALID_BYTE_RANGE", "UNSUPPORTED", "CRC_INPUT_TOO_SHORT",
+                                "SHARD_TOO_SMALL", "SHUFFLE_LENGTH", "INVALID_ARGUMENT", "HIP_ERROR"};
+  return (s >= 0 && s <= 11) ? names[s] : "UNKNOWN";
+}
+
+const char *zgpu_last_error(const zgpu_ctx *) { return g_last_error.c_str(); }
+
+int zgpu_ctx_create(int dev, zgpu_ctx **out) {
+  ABI_GUARD_BEGIN
+  if (!out) return set_err(ZGPU_INVALID_ARGUMENT, "out is NULL");
+  int n = 0;
+  HIPCHK(hipGetDeviceCount(&n));
+  if (dev < 0 || dev >= n) return set_err(ZGPU_INVALID_ARGUMENT, "no such HIP device");
+  HIPCHK(hipSetDevice(dev));
+  auto c = std::make_unique<zgpu_ctx>();
+  c->device = dev;
+  HIPCHK(hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking));
+  *out = c.release();
+  return ZGPU_OK;
+  ABI_GUARD_END
+}
+
+void zgpu_ctx_destroy(zgpu_ctx *c) { delete c; }
+
+int zgpu_chain_create(zgpu_ctx *ctx, const char *codecs_json, const char *data_type, const void *fill,
+                      uint32_t fill_len, int validate, zgpu_chain **out) {
+  ABI_GUARD_BEGIN
+  if (!ctx || !codecs_json || !data_type || !out) return set_err(ZGPU_INVALID_ARGUMENT, "NULL argument");
+  uint32_t es, comp;
+  if (!data_type_info(data_type, es, comp)) return set_err(ZGPU_UNSUPPORTED, std::string("data type ") + data_type);
+  if (fill && fill_len != es) return set_err(ZGPU_INVALID_ARGUMENT, "fill_len != element size");
+  uint8_t f[16] = {0};
+  if (fill) std::memcpy(f, fill, es);
+  Json j = Json::parse(codecs_json);
+  auto ch = std::make_unique<zgpu_chain>();
+  ch->ctx = ctx;
+  ch->chain = parse_chain(j, data_type, f);
+  ch->validate = validate != 0;
+  *out = ch.release();
+  return ZGPU_OK;
+  ABI_GUARD_END
+}
+
+void zgpu_chain_destroy(zgpu_chain *c) { delete c; }
+
+uint32_t zgpu_chain_element_size(const zgpu_chain *c) { return c ? c->chain->es : 0; }
+
+int zgpu_plan_create(zgpu_chain *ch, uint32_t nd, const zgpu_chunk_desc *descs, uint64_t n, const uint64_t *out_shape,
+                     uint32_t flags, zgpu_plan **out) {
+  ABI_GUARD_BEGIN
+  if (!ch || !out || !out_shape || (n && !descs)) return set_err(ZGPU_INVALID_ARGUMENT, "NULL argument");
+  if (nd == 0 || nd > ZGPU_MAX_DIMS) return set_err(ZGPU_INVALID_ARGUMENT, "ndim out of range");
+  if (!(flags & ZGPU_ENC_DEVICE)) return set_err(ZGPU_INVALID_ARGUMENT, "plans need device-resident inputs");
+  std::lock_guard<std::mutex> lk(ch->ctx->mu);
+  HIPCHK(hipSetDevice(ch->ctx->device));
+  std::unique_ptr<zgpu_plan> P(plan_new(ch, nd, descs, n, out_shape, flags));
+  plan_upload(*P);
+  HIPCHK(hipStreamSynchronize(ch->ctx->stream));
+  *out = P.release();
+  return ZGPU_OK;
+  ABI_GUARD_END
+}
+
+int zgpu_plan_execute(zgpu_plan *P, void *out, int32_t *status, void *stream) {
+  ABI_GUARD_BEGIN
+  if (!P || !out) return set_err(ZGPU_INVALID_ARGUMENT, "NULL argument");
+  std::lock_guard<std::mutex> lk(P->ctx->mu);
+  HIPCHK(hipSetDevice(P->ctx->device));
+  hipStream_t s = pick_stream(P->ctx, stream);
+  plan_enqueue(*P, (uint8_t *)out, s);
+  if (!status) return ZGPU_OK;
+  return plan_statuses(*P, status, s);
+  ABI_GUARD_END
+}
+
+void zgpu_plan_destroy(zgpu_plan *P) {
+  if (!P) return;
+  std::lock_guard<std::mutex> lk(P->ctx->mu);
+  delete P;
+}
+
+uint64_t zgpu_plan_algorithmic_bytes(const zgpu_plan *P) { return P ? P->alg_bytes_static + P->last_enc_bytes : 0; }
+
+int zgpu_decode_batch(zgpu_chain *ch, uint32_t nd, const zgpu_chunk_desc *descs, uint64_t n, void *out,
+                      const uint64_t *out_shape, uint32_t flags, int32_t *status, void *stream) {
+  ABI_GUARD_BEGIN
+  if (!ch || !out_shape || (n && !descs) || !out) return set_err(ZGPU_INVALID_ARGUMENT, "NULL argument");
+  if (nd == 0 || nd > ZGPU_MAX_DIMS) return set_err(ZGPU_INVALID_ARGUMENT, "ndim out of range");
+  zgpu_ctx *C = ch->ctx;
+  std::lock_guard<std::mutex> lk(C->mu);
+  HIPCHK(hipSetDevice(C->device));
+  hipStream_t s = pick_stream(C, stream);
+  std::vector<zgpu_chunk_desc> local;
+  const zgpu_chunk_desc *dd = descs;
+  uint8_t *enc_stage = nullptr;
+  if (!(flags & ZGPU_ENC_DEVICE)) {  // host inputs: one packed H2D copy through pinned staging
+    uint64_t total = 0;
+    for (uint64_t i = 0; i < n; i++)
+      if (descs[i].enc) total += (descs[i].enc_len + 255) & ~(uint64_t)255;
+    local.assign(descs, descs + n);
+    if (total) {
+      enc_stage = (uint8_t *)C->dev_alloc(total);
+      uint8_t *pin = (uint8_t *)C->host_alloc(total);
+      uint64_t off = 0;
+      for (uint64_t i = 0; i < n; i++) {
+        if (!descs[i].enc) continue;
+        std::memcpy(pin + off, descs[i].enc, descs[i].enc_len);
+        local[i].enc = enc_stage + off;
+        off += (descs[i].enc_len + 255) & ~(uint64_t)255;
+      }
+      HIPCHK(hipMemcpyAsync(enc_stage, pin, total, hipMemcpyHostToDevice, s));
+      HIPCHK(hipStreamSynchronize(s));
+      C->host_free(pin);
+    }
+    dd = local.data();
+  }
+  uint64_t out_elems = 1;
+  for (uint32_t d = 0; d < nd; d++) out_elems *= out_shape[d];
+  const uint64_t out_bytes = out_elems * ch->chain->es;
+  uint8_t *dout = (uint8_t *)out;
+  bool host_out = !(flags & ZGPU_OUT_DEVICE);
+  if (host_out) {
+    dout = (uint8_t *)C->dev_alloc(out_bytes ? out_bytes : 1);
+    // regions not covered by any descriptor keep the caller's bytes
+    HIPCHK(hipMemcpyAsync(dout, out, out_bytes, hipMemcpyHostToDevice, s));
+  }
+  std::unique_ptr<zgpu_plan> P;
+  int rc = 0;
+  try {
+    P.reset(plan_new(ch, nd, dd, n, out_shape, flags | ZGPU_ENC_DEVICE));
+    plan_upload(*P);
+    plan_enqueue(*P, dout, s);
+    rc = plan_statuses(*P, status, s);
+    if (host_out) {
+      HIPCHK(hipMemcpyAsync(out, dout, out_bytes, hipMemcpyDeviceToHost, s));
+      HIPCHK(hipStreamSynchronize(s));
+    }
+  } catch (...) {
+    if (host_out) C->dev_free(dout);
+    C->dev_free(enc_stage);
+    throw;
+  }
+  if (host_out) C->dev_free(dout);
+  C->dev_free(enc_stage);
+  P.reset();
+  if (rc) set_err(rc, zgpu_status_name(rc));
+  return rc;
+  ABI_GUARD_END
+}
+
+int zgpu_retrieve_array_subset(zgpu_chain *ch, uint32_t nd, const uint64_t *array_shape, const uint64_t *chunk_shape,
+                               const void *const *chunk_ptrs, const uint64_t *chunk_lens, const uint64_t *sel_start,
+                               const uint64_t *sel_shape, void *out, uint32_t flags, void *stream) {
+  ABI_GUARD_BEGIN
+  if (!ch || !array_shape || !chunk_shape || !chunk_ptrs || !chunk_lens || !sel_start || !sel_shape || !out)
+    return set_err(ZGPU_INVALID_ARGUMENT, "NULL argument");
+  if (nd == 0 || nd > ZGPU_MAX_DIMS) return set_err(ZGPU_INVALID_ARGUMENT, "ndim out of range");
+  // array_read_ops_common.rs:20-109: subset -> intersecting chunks -> one descriptor per chunk
+  uint64_t grid[ZG_MAXD], lo[ZG_MAXD], hi[ZG_MAXD], idx[ZG_MAXD];
+  uint64_t nchunks = 1;
+  for (uint32_t d = 0; d < nd; d++) {
+    if (chunk_shape[d] == 0) return set_err(ZGPU_INVALID_ARGUMENT, "zero chunk extent");
+    if (sel_start[d] + sel_shape[d] > array_shape[d])
+      return set_err(ZGPU_INVALID_ARGUMENT, "array subset out of bounds");
+    grid[d] = (array_shape[d] + chunk_shape[d] - 1) / chunk_shape[d];
+    if (sel_shape[d] == 0) return ZGPU_OK;  // nothing to do
+    lo[d] = sel_start[d] / chunk_shape[d];
+    hi[d] = (sel_start[d] + sel_shape[d] - 1) / chunk_shape[d] + 1;
+    nchunks *= hi[d] - lo[d];
+    idx[d] = lo[d];
+  }
+  std::vector<zgpu_chunk_desc> descs;
+  descs.reserve(nchunks);
+  for (;;) {
+    zgpu_chunk_desc D{};
+    uint64_t lin = 0;
+    for (uint32_t d = 0; d < nd; d++) {
+      lin = lin * grid[d] + idx[d];
+      const uint64_t cs = idx[d] * chunk_shape[d], ce = cs + chunk_shape[d];
+      const uint64_t s0 = std::max(sel_start[d], cs), s1 = std::min(sel_start[d] + sel_shape[d], ce);
+      D.chunk_shape[d] = chunk_shape[d];
+      D.sel_start[d] = s0 - cs;
+      D.sel_shape[d] = s1 - s0;
+      D.out_start[d] = s0 - sel_start[d];
+    }
+    D.enc = chunk_ptrs[lin];
+    D.enc_len = D.enc ? chunk_lens[lin] : 0;
+    descs.push_back(D);
+    int d = (int)nd - 1;
+    for (; d >= 0; d--) {
+      if (++idx[d] < hi[d]) break;
+      idx[d] = lo[d];
+    }
+    if (d < 0) break;
+  }
+  return zgpu_decode_batch(ch, nd, descs.data(), descs.size(), out, sel_shape, flags, nullptr, stream);
+  ABI_GUARD_END
+}
+
+}  // extern "C"
