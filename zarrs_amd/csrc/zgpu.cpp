@@ -278,7 +278,7 @@ static void plan_build(zgpu_plan &P, const zgpu_chunk_desc *descs) {
     const zgpu_chunk_desc &D = descs[i];
     bool ok = true, full = true;
     for (uint32_t d = 0; d < nd; d++) {
-      if (D.chunk_shape[d] == 0 || D.sel_start[d] + D.sel_shape[d] > D.chunk_shape[d] ||
+      if (D.sel_start[d] + D.sel_shape[d] > D.chunk_shape[d] ||
           D.out_start[d] + D.sel_shape[d] > P.out_shape[d])
         ok = false;
       if (D.sel_start[d] != 0 || D.sel_shape[d] != D.chunk_shape[d]) full = false;
@@ -290,7 +290,7 @@ static void plan_build(zgpu_plan &P, const zgpu_chunk_desc *descs) {
     }
     uint64_t vol = 1;
     for (uint32_t d = 0; d < nd; d++) vol *= D.sel_shape[d];
-    if (vol == 0) continue;
+    if (vol == 0 && (!full || shard_chain)) continue;  // a zero-extent full chunk still runs its checks
     P.alg_bytes_static += vol * es;
     if (!shard_chain) {
       ZgItem it{};
