@@ -1,4 +1,26 @@
-// gzip member decode (RFC 1952) — placeholder until the device decoder lands: marks items UNSUPPORTED.
+// gzip member decode (RFC 1952 header/trailer + RFC 1951 DEFLATE) for gfx950.
+//
+// Reference behaviour restated: zarrs/src/array/codec/bytes_to_bytes/gzip/gzip_codec.rs:110-120 —
+// flate2 1.1 `bufread::GzDecoder::read_to_end` (miniz_oxide backend): parse the first member's
+// header, inflate its DEFLATE stream, check the trailer CRC-32 and ISIZE (the CRC check itself runs
+// in k_crc32_check, crc.hip); any malformed input -> io::Error -> CodecError::IOError
+// (ZG_CORRUPT_STREAM here). Bytes after the first member are ignored, as GzDecoder does.
+//
+// Design (one 64-lane wavefront = one workgroup = one gzip stream):
+//  * Symbol decode is inherently serial, so every lane runs the same decode loop on wave-uniform
+//    values (readfirstlane keeps them in SGPRs); there is no divergence and no broadcast step.
+//  * Bit reader: the compressed stream is read as aligned 32-bit words through two 256-byte register
+//    windows (one word per lane, one coalesced load each); a refill is a v_readlane, and the next
+//    window is loaded a full window ahead, so the decode loop never waits on HBM.
+//  * Huffman tables live in LDS: a 10-bit root table for literal/length and an 8-bit one for
+//    distances, each entry already holding the decoded meaning (literal byte, or length/distance base
+//    + extra-bit count). Longer codes (rare) take a canonical count/first slow path. Tables are built
+//    cooperatively by the 64 lanes (ballot ranks + parallel root fill).
+//  * Decoded symbols are recorded one per lane (up to 64 per batch), then executed in parallel:
+//    a wave prefix sum places them, literals are written at once, each match is copied by all lanes
+//    (out[p+i] = out[p-d+(i mod d)], so overlapping copies need no serialisation), through a 16 KiB
+//    LDS ring that holds the recent output; sources older than the ring come from the flushed output
+//    in HBM. Each batch is flushed to the item's slot with 16-byte stores.
 #include <hip/hip_runtime.h>
 
 #include "../common.hpp"
@@ -6,15 +28,543 @@
 
 namespace zgpu {
 
-__global__ void k_gzip_unsupported(const ZgItem *items, uint32_t *status, uint32_t n) {
-  const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
-  if (i < n && !status[i] && !(items[i].flags & ZG_ITEM_FILL)) status[i] = ZG_UNSUPPORTED;
+namespace {
+
+constexpr int RING = 16384;  // LDS ring of recent output (power of two)
+constexpr int RMASK = RING - 1;
+constexpr int BATCH_CAP = 4096;  // max output bytes decoded into one batch (<= RING/2)
+constexpr int LROOT = 10, DROOT = 8;
+
+// table entry: bits 0-3 code length (0 = longer than the root: slow path), 4-5 kind,
+// 6-9 extra bits, 16-31 value (literal byte / length base / distance base)
+constexpr uint32_t K_LIT = 0, K_LEN = 1, K_EOB = 2, K_BAD = 3;
+
+__constant__ uint16_t c_len_base[29] = {3,  4,  5,  6,  7,  8,  9,  10, 11,  13,  15,  17,  19,  23, 27,
+                                        31, 35, 43, 51, 59, 67, 83, 99, 115, 131, 163, 195, 227, 258};
+__constant__ uint8_t c_len_extra[29] = {0, 0, 0, 0, 0, 0, 0, 0, 1, 1, 1, 1, 2, 2, 2,
+                                        2, 3, 3, 3, 3, 4, 4, 4, 4, 5, 5, 5, 5, 0};
+__constant__ uint16_t c_dist_base[30] = {1,   2,   3,   4,   5,   7,    9,    13,   17,   25,
+                                         33,  49,  65,  97,  129, 193,  257,  385,  513,  769,
+                                         1025, 1537, 2049, 3073, 4097, 6145, 8193, 12289, 16385, 24577};
+__constant__ uint8_t c_dist_extra[30] = {0, 0, 0, 0, 1, 1, 2, 2, 3, 3, 4, 4, 5, 5, 6,
+                                         6, 7, 7, 8, 8, 9, 9, 10, 10, 11, 11, 12, 12, 13, 13};
+__constant__ uint8_t c_clen_order[19] = {16, 17, 18, 0, 8, 7, 9, 6, 10, 5, 11, 4, 12, 3, 13, 2, 14, 1, 15};
+
+struct HuffMeta {  // canonical code description for the slow path
+  uint16_t count[16];
+  uint16_t first[16];
+  uint16_t offs[16];
+  uint16_t maxlen;
+};
+
+struct Smem {
+  uint8_t ring[RING];
+  uint32_t ltab[1 << LROOT];
+  uint32_t dtab[1 << DROOT];
+  uint16_t lsorted[288];
+  uint16_t dsorted[32];
+  uint8_t lens[320];  // code lengths: 0..HLIT-1 literal/length, then distances
+  uint8_t clens[20];
+  uint16_t csorted[20];
+  HuffMeta lm, dm, cm;
+  uint32_t tmp[16];
+};
+
+__device__ __forceinline__ uint32_t U(uint32_t x) { return __builtin_amdgcn_readfirstlane(x); }
+__device__ __forceinline__ int lane_id() { return __lane_id(); }
+
+// ---------------------------------------------------------------------------------------------
+// Bit reader over aligned 32-bit words held in two per-lane register windows.
+// ---------------------------------------------------------------------------------------------
+struct Bits {
+  const uint32_t *base;  // aligned word stream
+  uint32_t nwords;       // words that may be loaded (covering the item)
+  uint32_t wcur;         // index of the first word of the current window
+  uint32_t win0, win1;   // current / next window (lane l holds word wcur + l / wcur + 64 + l)
+  uint32_t wnext;        // next word to append to the bit buffer
+  uint64_t bb;           // bit buffer (LSB first)
+  uint32_t nb;           // valid bits in bb
+  uint64_t consumed;     // bits consumed from the start of the aligned stream
+};
+
+__device__ __forceinline__ uint32_t load_word(const Bits &B, uint32_t w) {
+  return w < B.nwords ? B.base[w] : 0u;
 }
 
-hipError_t launch_gzip(ZgItem *items, uint32_t *status, uint32_t n_items, uint8_t *dst, uint64_t slot_bytes, uint2 *aux,
-                       hipStream_t s) {
+__device__ __forceinline__ void bits_seek(Bits &B, uint64_t bitpos) {
+  // position the reader at an absolute bit offset of the aligned stream
+  const uint32_t w = (uint32_t)(bitpos >> 5);
+  B.wcur = w & ~63u;
+  B.win0 = load_word(B, B.wcur + lane_id());
+  B.win1 = load_word(B, B.wcur + 64 + lane_id());
+  B.wnext = w;
+  B.bb = 0;
+  B.nb = 0;
+  B.consumed = (uint64_t)w * 32;
+  // fill and drop the leading bits
+  const uint32_t skip = (uint32_t)(bitpos & 31);
+  // append one word
+  {
+    const uint32_t word = U(__builtin_amdgcn_readlane(B.win0, (int)(B.wnext - B.wcur)));
+    B.bb = word;
+    B.nb = 32;
+    B.wnext++;
+  }
+  B.bb >>= skip;
+  B.nb -= skip;
+  B.consumed += skip;
+}
+
+__device__ __forceinline__ void bits_refill(Bits &B) {
+  if (B.nb <= 32) {
+    uint32_t idx = B.wnext - B.wcur;
+    if (idx >= 64) {  // advance the window pair; keep one window of lookahead in flight
+      B.wcur += 64;
+      B.win0 = B.win1;
+      B.win1 = load_word(B, B.wcur + 64 + lane_id());
+      idx -= 64;
+    }
+    const uint32_t word = U(__builtin_amdgcn_readlane(B.win0, (int)idx));
+    B.bb |= (uint64_t)word << B.nb;
+    B.nb += 32;
+    B.wnext++;
+  }
+}
+
+__device__ __forceinline__ uint32_t bits_peek(const Bits &B, uint32_t n) { return (uint32_t)B.bb & ((1u << n) - 1); }
+__device__ __forceinline__ void bits_drop(Bits &B, uint32_t n) {
+  B.bb >>= n;
+  B.nb -= n;
+  B.consumed += n;
+}
+__device__ __forceinline__ uint32_t bits_get(Bits &B, uint32_t n) {
+  bits_refill(B);
+  const uint32_t v = bits_peek(B, n);
+  bits_drop(B, n);
+  return v;
+}
+
+__device__ __forceinline__ uint32_t rev_bits(uint32_t v, uint32_t n) { return __builtin_bitreverse32(v) >> (32 - n); }
+
+// ---------------------------------------------------------------------------------------------
+// Cooperative canonical-Huffman table build. lens[n] code lengths (LDS). kind: 0 litlen, 1 dist,
+// 2 code-length codes (root 7 = max length: no slow path). Returns false on an invalid code set
+// (over-subscribed, or incomplete with more than one code: zlib inflate_table rules).
+// ---------------------------------------------------------------------------------------------
+__device__ bool build_table(const uint8_t *lens, uint32_t n, uint32_t root, uint32_t *tab, uint16_t *sorted,
+                            HuffMeta &M, int kind, uint32_t *tmp) {
+  const int lane = lane_id();
+  if (lane < 16) tmp[lane] = 0;
+  __syncthreads();
+  for (uint32_t s = lane; s < n; s += 64) {
+    const uint32_t l = lens[s];
+    if (l) atomicAdd(&tmp[l], 1u);
+  }
+  __syncthreads();
+  // uniform: counts, validity, first codes, offsets
+  uint32_t cnt[16];
+  for (int l = 0; l < 16; l++) cnt[l] = U(tmp[l]);
+  int left = 1;
+  uint32_t maxlen = 0;
+  for (int l = 1; l < 16; l++) {
+    left <<= 1;
+    left -= (int)cnt[l];
+    if (cnt[l]) maxlen = l;
+    if (left < 0) return false;  // over-subscribed
+  }
+  if (left > 0 && maxlen != 1 && maxlen != 0) return false;  // incomplete set (zlib inflate_table)
+  if (kind == 2 && (left > 0 || maxlen == 0)) return false;    // code-length codes must be complete
+  // canonical first codes (RFC 1951 3.2.2): next_code[l] = (next_code[l-1] + count[l-1]) << 1
+  uint32_t first[16];
+  {
+    uint32_t code = 0;
+    first[0] = 0;
+    for (int l = 1; l < 16; l++) {
+      code = (code + (l > 1 ? cnt[l - 1] : 0)) << 1;
+      first[l] = code;
+    }
+  }
+  if (lane == 0) {
+    uint32_t off = 0;
+    for (int l = 1; l < 16; l++) {
+      M.count[l] = (uint16_t)cnt[l];
+      M.first[l] = (uint16_t)first[l];
+      M.offs[l] = (uint16_t)off;
+      off += cnt[l];
+    }
+    M.maxlen = (uint16_t)maxlen;
+  }
+  __syncthreads();
+  // sorted symbols (by length, then symbol) via ballot ranks
+  uint32_t base[16];
+  {
+    uint32_t off = 0;
+    for (int l = 0; l < 16; l++) {
+      base[l] = off;
+      off += (l ? cnt[l] : 0);
+    }
+  }
+  for (uint32_t s0 = 0; s0 < n; s0 += 64) {
+    const uint32_t s = s0 + lane;
+    const uint32_t l = s < n ? lens[s] : 0;
+    for (int L = 1; L <= (int)maxlen; L++) {
+      const uint64_t m = __ballot(l == (uint32_t)L);
+      if (l == (uint32_t)L) {
+        const uint32_t rank = __builtin_popcountll(m & ((1ull << lane) - 1));
+        sorted[base[L] + rank] = (uint16_t)s;
+      }
+      base[L] += __builtin_popcountll(m);
+    }
+  }
+  __syncthreads();
+  // root table fill: entry e <-> R-bit MSB-first prefix v = reverse(e)
+  const uint32_t size = 1u << root;
+  for (uint32_t e = lane; e < size; e += 64) {
+    const uint32_t v = rev_bits(e, root);
+    uint32_t entry = (K_BAD << 4) | 0xF;  // invalid code marker (len 15 so it is consumed; flagged bad)
+    bool found = false;
+    for (uint32_t L = 1; L <= root && L <= maxlen && !found; L++) {
+      const uint32_t c = v >> (root - L);
+      if (c - first[L] < cnt[L]) {
+        const uint32_t sym = sorted[M.offs[L] + c - first[L]];
+        found = true;
+        if (kind == 0) {
+          if (sym < 256) entry = (sym << 16) | (K_LIT << 4) | L;
+          else if (sym == 256) entry = (K_EOB << 4) | L;
+          else if (sym < 286) entry = ((uint32_t)c_len_base[sym - 257] << 16) | ((uint32_t)c_len_extra[sym - 257] << 6) | (K_LEN << 4) | L;
+          else entry = (K_BAD << 4) | L;
+        } else if (kind == 1) {
+          if (sym < 30) entry = ((uint32_t)c_dist_base[sym] << 16) | ((uint32_t)c_dist_extra[sym] << 6) | (K_LEN << 4) | L;
+          else entry = (K_BAD << 4) | L;
+        } else {
+          entry = (sym << 16) | L;
+        }
+      }
+    }
+    if (!found && maxlen > root) entry = 0;  // longer code: slow path
+    tab[e] = entry;
+  }
+  __syncthreads();
+  return true;
+}
+
+// Decode one symbol with a root table; returns the table-style entry (slow path resolves long codes).
+__device__ __forceinline__ uint32_t decode_sym(Bits &B, const uint32_t *tab, uint32_t root, const uint16_t *sorted,
+                                               const HuffMeta &M, int kind) {
+  bits_refill(B);
+  uint32_t e = U(tab[bits_peek(B, root)]);
+  if (e & 15) {
+    bits_drop(B, e & 15);
+    return e;
+  }
+  // slow path: codes longer than the root, canonical walk from length root+1
+  uint32_t v = rev_bits(bits_peek(B, root), root);
+  uint32_t L = root;
+  const uint32_t maxlen = U(M.maxlen);
+  uint32_t sym = 0xFFFF;
+  uint64_t bb = B.bb >> root;
+  while (L < maxlen) {
+    L++;
+    v = (v << 1) | (uint32_t)(bb & 1);
+    bb >>= 1;
+    const uint32_t first = U(M.first[L]), cnt = U(M.count[L]);
+    if (v - first < cnt) {
+      sym = U(sorted[U(M.offs[L]) + v - first]);
+      break;
+    }
+  }
+  if (sym == 0xFFFF) return (K_BAD << 4) | 15;
+  bits_drop(B, L);
+  if (kind == 0) {
+    if (sym < 256) return (sym << 16) | (K_LIT << 4) | 15;
+    if (sym == 256) return (K_EOB << 4) | 15;
+    if (sym < 286) return ((uint32_t)c_len_base[sym - 257] << 16) | ((uint32_t)c_len_extra[sym - 257] << 6) | (K_LEN << 4) | 15;
+    return (K_BAD << 4) | 15;
+  }
+  if (sym < 30) return ((uint32_t)c_dist_base[sym] << 16) | ((uint32_t)c_dist_extra[sym] << 6) | (K_LEN << 4) | 15;
+  return (K_BAD << 4) | 15;
+}
+
+__device__ __forceinline__ void build_fixed_lens(uint8_t *lens) {
+  for (uint32_t s = lane_id(); s < 320; s += 64) {
+    uint8_t l;
+    if (s < 144) l = 8;
+    else if (s < 256) l = 9;
+    else if (s < 280) l = 7;
+    else if (s < 288) l = 8;
+    else l = 5;  // 30 distance codes (+2 invalid) of length 5, stored at 288..319
+    lens[s] = l;
+  }
+  __syncthreads();
+}
+
+// Flush output bytes [from, to) (absolute positions) from the ring to the slot with 16-B stores.
+// Words straddling `to` are rewritten by the next flush.
+__device__ __forceinline__ void flush(const Smem &S, uint8_t *out, uint64_t cap, uint64_t from, uint64_t to) {
+  const uint64_t a = from & ~(uint64_t)15, b = (to + 15) & ~(uint64_t)15;
+  for (uint64_t p = a + (uint64_t)lane_id() * 16; p < b; p += 64 * 16) {
+    if (p + 16 <= cap) {
+      const uint4 v = *(const uint4 *)&S.ring[p & RMASK];
+      *(uint4 *)(out + p) = v;
+    } else {
+      for (uint64_t q = p; q < cap && q < p + 16; q++) out[q] = S.ring[q & RMASK];
+    }
+  }
+}
+
+}  // namespace
+
+// One wave per item. aux[i] = {trailer CRC-32, trailer ISIZE}.
+__global__ __launch_bounds__(64) void k_gzip(ZgItem *items, uint32_t *status, uint8_t *dst, uint64_t slot_bytes,
+                                             uint2 *aux) {
+  __shared__ Smem S;
+  const uint32_t item = blockIdx.x;
+  const ZgItem it = items[item];
+  if (status[item] || (it.flags & ZG_ITEM_FILL)) return;
+  const int lane = lane_id();
+  uint8_t *out = dst + (uint64_t)item * slot_bytes;
+  const uint64_t cap = slot_bytes;
+  const uint8_t *in = (const uint8_t *)it.src;
+  const uint64_t in_len = it.len;
+  uint32_t err = 0;
+
+  // ---- RFC 1952 header (uniform byte reads) ----
+  uint64_t hp = 10;
+  if (in_len < 18) err = ZG_CORRUPT_STREAM;
+  uint32_t flg = 0;
+  if (!err) {
+    if (U(in[0]) != 0x1f || U(in[1]) != 0x8b || U(in[2]) != 8) err = ZG_CORRUPT_STREAM;
+    flg = U(in[3]);
+    if (flg & 0xE0) err = ZG_CORRUPT_STREAM;  // reserved flag bits
+  }
+  if (!err && (flg & 4)) {  // FEXTRA
+    const uint32_t xlen = U(in[hp]) | (U(in[hp + 1]) << 8);  // hp + 2 <= 18 <= in_len
+    hp += 2 + xlen;
+    if (hp > in_len) err = ZG_CORRUPT_STREAM;
+  }
+  if (!err && (flg & 8)) {  // FNAME
+    while (hp < in_len && U(in[hp]) != 0) hp++;
+    hp++;
+  }
+  if (!err && (flg & 16)) {  // FCOMMENT
+    while (hp < in_len && U(in[hp]) != 0) hp++;
+    hp++;
+  }
+  if (!err && (flg & 2)) hp += 2;  // FHCRC
+  if (!err && hp + 8 > in_len) err = ZG_CORRUPT_STREAM;
+  if (err) {
+    if (lane == 0) status[item] = err;
+    return;
+  }
+
+  // ---- bit reader over the aligned stream ----
+  Bits B;
+  const uintptr_t mis = (uintptr_t)in & 3;
+  B.base = (const uint32_t *)((uintptr_t)in - mis);
+  B.nwords = (uint32_t)((in_len + mis + 3) / 4);
+  const uint64_t end_bits = (in_len + mis) * 8;
+  bits_seek(B, (hp + mis) * 8);
+
+  uint64_t pos = 0;        // output bytes produced (absolute)
+  uint64_t flushed = 0;    // output bytes flushed to the slot
+  bool last = false;
+  while (!last && !err) {
+    bits_refill(B);
+    last = bits_get(B, 1);
+    const uint32_t type = bits_get(B, 2);
+    if (type == 0) {  // ---- stored block ----
+      const uint32_t r = (uint32_t)(B.consumed & 7);
+      bits_drop(B, r ? 8 - r : 0);  // to a byte boundary (nb is a multiple of 8 here)
+      bits_refill(B);
+      const uint32_t ln = bits_get(B, 16), nln = bits_get(B, 16);
+      if ((ln ^ 0xFFFF) != nln) { err = ZG_CORRUPT_STREAM; break; }
+      const uint64_t byte0 = B.consumed / 8 - mis;  // byte offset in `in`
+      if (byte0 + ln > in_len) { err = ZG_CORRUPT_STREAM; break; }
+      if (pos + ln > cap) { err = ZG_DECODED_SIZE_MISMATCH; break; }
+      for (uint32_t done = 0; done < ln;) {
+        const uint32_t n = min<uint32_t>(ln - done, BATCH_CAP);
+        for (uint32_t k = lane; k < n; k += 64) S.ring[(pos + k) & RMASK] = in[byte0 + done + k];
+        __syncthreads();
+        flush(S, out, cap, flushed, pos + n);
+        pos += n;
+        flushed = pos;
+        done += n;
+        __syncthreads();
+      }
+      bits_seek(B, (byte0 + ln + mis) * 8);
+      continue;
+    }
+    if (type == 3) { err = ZG_CORRUPT_STREAM; break; }
+    uint32_t hlit = 288, hdist = 32;
+    if (type == 1) {
+      build_fixed_lens(S.lens);
+    } else {  // ---- dynamic header ----
+      hlit = bits_get(B, 5) + 257;
+      hdist = bits_get(B, 5) + 1;
+      const uint32_t hclen = bits_get(B, 4) + 4;
+      if (hlit > 286 || hdist > 30) { err = ZG_CORRUPT_STREAM; break; }
+      uint32_t cl[19];
+      for (int k = 0; k < 19; k++) cl[k] = 0;
+      for (uint32_t k = 0; k < hclen; k++) cl[k] = bits_get(B, 3);
+      if (lane == 0)
+        for (int k = 0; k < 19; k++) S.clens[c_clen_order[k]] = (uint8_t)cl[k];
+      __syncthreads();
+      if (!build_table(S.clens, 19, 7, S.ltab, S.csorted, S.cm, 2, S.tmp)) { err = ZG_CORRUPT_STREAM; break; }
+      // code lengths for literal/length + distance alphabets (ltab used as a 128-entry 7-bit table)
+      uint32_t n = 0, prev = 0;
+      const uint32_t total = hlit + hdist;
+      while (n < total) {
+        bits_refill(B);
+        const uint32_t e = U(S.ltab[bits_peek(B, 7)]);
+        bits_drop(B, e & 15);
+        const uint32_t sym = e >> 16;
+        uint32_t rep = 0, val = 0;
+        if (sym < 16) {
+          val = sym;
+          rep = 1;
+          prev = sym;
+        } else if (sym == 16) {
+          if (n == 0) { err = ZG_CORRUPT_STREAM; break; }
+          val = prev;
+          rep = 3 + bits_get(B, 2);
+        } else if (sym == 17) {
+          rep = 3 + bits_get(B, 3);
+          val = 0;
+          prev = 0;
+        } else {
+          rep = 11 + bits_get(B, 7);
+          val = 0;
+          prev = 0;
+        }
+        if (n + rep > total) { err = ZG_CORRUPT_STREAM; break; }
+        for (uint32_t k = lane; k < rep; k += 64) {
+          const uint32_t s = n + k;
+          S.lens[s < hlit ? s : 288 + (s - hlit)] = (uint8_t)val;
+        }
+        n += rep;
+      }
+      if (err) break;
+      // zero the unused tails so the table builders see exactly hlit / hdist symbols
+      for (uint32_t s = lane; s < 320; s += 64) {
+        if ((s >= hlit && s < 288) || s >= 288 + hdist) S.lens[s] = 0;
+      }
+      __syncthreads();
+      if (U(S.lens[256]) == 0) { err = ZG_CORRUPT_STREAM; break; }  // missing end-of-block code
+    }
+    if (!build_table(S.lens, 288, LROOT, S.ltab, S.lsorted, S.lm, 0, S.tmp)) { err = ZG_CORRUPT_STREAM; break; }
+    if (!build_table(S.lens + 288, 32, DROOT, S.dtab, S.dsorted, S.dm, 1, S.tmp)) { err = ZG_CORRUPT_STREAM; break; }
+    (void)hlit;
+    (void)hdist;
+
+    // ---- symbol batches ----
+    bool eob = false;
+    while (!eob && !err) {
+      uint32_t rec = 0;  // this lane's symbol: literal byte, or (1<<31)|(dist<<9)|len
+      uint32_t cnt = 0, bytes = 0;
+      while (cnt < 64 && bytes < BATCH_CAP) {
+        const uint32_t e = decode_sym(B, S.ltab, LROOT, S.lsorted, S.lm, 0);
+        const uint32_t kind = (e >> 4) & 3;
+        if (kind == K_LIT) {
+          if (lane == (int)cnt) rec = e >> 16;
+          cnt++;
+          bytes++;
+          continue;
+        }
+        if (kind == K_EOB) { eob = true; break; }
+        if (kind == K_BAD) { err = ZG_CORRUPT_STREAM; break; }
+        bits_refill(B);
+        const uint32_t lx = (e >> 6) & 15;
+        const uint32_t len = (e >> 16) + bits_peek(B, lx);
+        bits_drop(B, lx);
+        const uint32_t de = decode_sym(B, S.dtab, DROOT, S.dsorted, S.dm, 1);
+        if (((de >> 4) & 3) != K_LEN) { err = ZG_CORRUPT_STREAM; break; }
+        bits_refill(B);
+        const uint32_t dx = (de >> 6) & 15;
+        const uint32_t dist = (de >> 16) + bits_peek(B, dx);
+        bits_drop(B, dx);
+        if (dist > pos + bytes) { err = ZG_CORRUPT_STREAM; break; }  // distance too far back
+        if (lane == (int)cnt) rec = 0x80000000u | (dist << 9) | len;
+        cnt++;
+        bytes += len;
+      }
+      if (B.consumed > end_bits) err = ZG_CORRUPT_STREAM;  // ran past the input
+      if (err) break;
+      if (pos + bytes > cap) { err = ZG_DECODED_SIZE_MISMATCH; break; }
+      // ---- execute the batch ----
+      const bool mine = lane < (int)cnt;
+      const bool is_match = mine && (rec >> 31);
+      uint32_t ln = mine ? (is_match ? (rec & 511) : 1u) : 0u;
+      // inclusive wave scan of lengths
+      uint32_t inc = ln;
+      for (int o = 1; o < 64; o <<= 1) {
+        const uint32_t t = __shfl_up(inc, o, 64);
+        if (lane >= o) inc += t;
+      }
+      const uint64_t mypos = pos + inc - ln;
+      if (mine && !is_match) S.ring[mypos & RMASK] = (uint8_t)rec;
+      const uint64_t batch_end = pos + bytes;
+      uint64_t mm = __ballot(is_match);
+      bool need_global = false;
+      {
+        // any source older than batch_end - RING must be read from the flushed slot
+        const uint32_t d = (rec >> 9) & 0xFFFF;
+        need_global = __ballot(is_match && mypos - d + RING < batch_end) != 0;
+      }
+      if (need_global) __threadfence_block();  // earlier flushes visible to this wave's loads
+      while (mm) {
+        const int j = __builtin_ctzll(mm);
+        mm &= mm - 1;
+        const uint32_t r = U(__builtin_amdgcn_readlane(rec, j));
+        const uint64_t p = ((uint64_t)U(__builtin_amdgcn_readlane((uint32_t)mypos, j))) |
+                           ((uint64_t)U(__builtin_amdgcn_readlane((uint32_t)(mypos >> 32), j)) << 32);
+        const uint32_t len = r & 511, d = (r >> 9) & 0xFFFF;
+        const float inv = 1.0f / (float)d;
+        for (uint32_t i = lane; i < len; i += 64) {
+          uint32_t q = (uint32_t)((float)i * inv);
+          int32_t rm = (int32_t)i - (int32_t)(q * d);
+          if (rm < 0) rm += d;
+          if (rm >= (int32_t)d) rm -= d;
+          const uint64_t src = p - d + (uint32_t)rm;
+          uint8_t v;
+          if (src + RING >= batch_end) v = S.ring[src & RMASK];
+          else v = __builtin_nontemporal_load(out + src);  // nt: bypass a possibly stale L1 line
+          S.ring[(p + i) & RMASK] = v;
+        }
+      }
+      __syncthreads();
+      flush(S, out, cap, flushed, batch_end);
+      pos = batch_end;
+      flushed = pos;
+      __syncthreads();
+    }
+  }
+  if (!err) {
+    // trailer: byte-align, CRC-32 then ISIZE (little endian)
+    const uint32_t r = (uint32_t)(B.consumed & 7);
+    bits_drop(B, r ? 8 - r : 0);
+    bits_refill(B);
+    const uint32_t crc_lo = bits_get(B, 16);
+    const uint32_t crc_hi = bits_get(B, 16);
+    const uint32_t isz_lo = bits_get(B, 16);
+    const uint32_t isz_hi = bits_get(B, 16);
+    const uint32_t crc = crc_lo | (crc_hi << 16), isz = isz_lo | (isz_hi << 16);
+    if (B.consumed > end_bits) err = ZG_CORRUPT_STREAM;
+    if (lane == 0 && !err) aux[item] = make_uint2(crc, isz);
+  }
+  if (lane == 0) {
+    if (err) {
+      status[item] = err;
+    } else {
+      items[item].src = (uint64_t)out;
+      items[item].len = pos;
+    }
+  }
+}
+
+hipError_t launch_gzip(ZgItem *items, uint32_t *status, uint32_t n_items, uint8_t *dst, uint64_t slot_bytes,
+                       uint2 *aux, hipStream_t s) {
   if (!n_items) return hipSuccess;
-  hipLaunchKernelGGL(k_gzip_unsupported, dim3((n_items + 255) / 256), dim3(256), 0, s, items, status, n_items);
+  hipLaunchKernelGGL(k_gzip, dim3(n_items), dim3(64), 0, s, items, status, dst, slot_bytes, aux);
   return hipGetLastError();
 }
 
