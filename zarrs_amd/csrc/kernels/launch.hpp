@@ -43,9 +43,10 @@ hipError_t launch_crc32_check(const ZgItem *items, uint32_t *status, uint32_t n_
 // On return items[i] points at its slot; aux[i] receives the trailer {crc32, isize} for launch_crc32_check.
 hipError_t launch_gzip(ZgItem *items, uint32_t *status, uint32_t n_items, uint8_t *dst, uint64_t slot_bytes,
                        uint2 *aux, hipStream_t s);
-// zstd (RFC 8878) frame decode into dst slots.
+// zstd (RFC 8878) frame decode into dst slots; lit_scratch holds zstd_lit_scratch_per_item() bytes per item.
 hipError_t launch_zstd(ZgItem *items, uint32_t *status, uint32_t n_items, uint8_t *dst, uint64_t slot_bytes,
-                       hipStream_t s);
+                       uint8_t *lit_scratch, hipStream_t s);
+uint64_t zstd_lit_scratch_per_item();
 // standalone unshuffle (when shuffle is not directly above the bytes codec)
 hipError_t launch_unshuffle(ZgItem *items, uint32_t *status, uint32_t n_items, uint8_t *dst, uint64_t slot_bytes,
                             uint32_t elementsize, hipStream_t s);

@@ -164,6 +164,7 @@ struct zgpu_plan {
   uint32_t *d_shard_status = nullptr;
   uint8_t *d_pool[2] = {nullptr, nullptr};
   uint2 *d_aux = nullptr;
+  uint8_t *d_zlit = nullptr;
   unsigned long long *d_counter = nullptr;
   // host-input staging
   uint8_t *d_enc_stage = nullptr;
@@ -172,7 +173,7 @@ struct zgpu_plan {
   ~zgpu_plan() {
     if (!ctx) return;
     void *bufs[] = {d_items, d_items_init, d_geom, d_status, d_shards, d_index, d_shard_status,
-                    d_pool[0], d_pool[1], d_aux, d_counter, d_enc_stage};
+                    d_pool[0], d_pool[1], d_aux, d_zlit, d_counter, d_enc_stage};
     for (void *b : bufs) ctx->dev_free(b);
   }
 };
@@ -422,8 +423,10 @@ static void plan_upload(zgpu_plan &P) {
     HIPCHK(hipMemcpyAsync(P.d_items_init, P.items.data(), ni * sizeof(ZgItem), hipMemcpyHostToDevice, C.stream));
     HIPCHK(hipMemcpyAsync(P.d_geom, P.geom.data(), P.geom.size() * 8, hipMemcpyHostToDevice, C.stream));
     for (int k = 0; k < P.n_pools; k++) P.d_pool[k] = (uint8_t *)C.dev_alloc(ni * P.slot_bytes);
-    for (const Stage &s : P.stages)
+    for (const Stage &s : P.stages) {
       if (s.kind == ST_GZIP && !P.d_aux) P.d_aux = (uint2 *)C.dev_alloc(ni * sizeof(uint2));
+      if (s.kind == ST_ZSTD && !P.d_zlit) P.d_zlit = (uint8_t *)C.dev_alloc(ni * zstd_lit_scratch_per_item());
+    }
   }
   P.d_counter = (unsigned long long *)C.dev_alloc(256);
   if (!P.shards.empty()) {
@@ -457,7 +460,7 @@ static void plan_enqueue(zgpu_plan &P, uint8_t *out, hipStream_t s) {
         HIPCHK(launch_crc32_check(P.d_items, P.d_status, ni, P.d_aux, s));
         break;
       case ST_ZSTD:
-        HIPCHK(launch_zstd(P.d_items, P.d_status, ni, P.d_pool[st.pool], P.slot_bytes, s));
+        HIPCHK(launch_zstd(P.d_items, P.d_status, ni, P.d_pool[st.pool], P.slot_bytes, P.d_zlit, s));
         break;
       case ST_UNSHUFFLE:
         HIPCHK(launch_unshuffle(P.d_items, P.d_status, ni, P.d_pool[st.pool], P.slot_bytes, st.elementsize, s));
