@@ -77,7 +77,7 @@ def run_gpu(args, rank, world, dev):
     L.check(lib.zgpu_plan_create(chain._h, 3, arr, n_chunks, L.u64s(shape), L.ENC_DEVICE | L.OUT_DEVICE,
                                  C.byref(plan)))
     status = (C.c_int32 * n_chunks)()
-    stream = torch.cuda.current_stream(dev)
+    stream = torch.cuda.Stream(dev)  # the library launches on this stream; events are recorded on it
     sp = C.c_void_p(stream.cuda_stream)
 
     def step():
@@ -93,17 +93,27 @@ def run_gpu(args, rank, world, dev):
     if world > 1:
         torch.distributed.barrier()
     torch.cuda.synchronize()
-    ev0 = torch.cuda.Event(enable_timing=True)
-    ev1 = torch.cuda.Event(enable_timing=True)
     t0 = time.perf_counter()
-    ev0.record(stream)
     for _ in range(args.steps):
         step()
-    ev1.record(stream)
     torch.cuda.synchronize()
     if world > 1:
         torch.distributed.barrier()
     elapsed = time.perf_counter() - t0
+    if args.child:  # rocprofv3 --pmc pass: only the dispatches matter
+        lib.zgpu_plan_destroy(plan)
+        return None
+    # Device time of one decode launch sequence (ctl memset + k_scatter_tiled), HIP events on the
+    # stream the library launches on; enqueue-only executes (status=NULL), back to back.
+    ev0 = torch.cuda.Event(enable_timing=True)
+    ev1 = torch.cuda.Event(enable_timing=True)
+    ev0.record(stream)
+    for _ in range(args.steps):
+        rc = lib.zgpu_plan_execute(plan, out.data_ptr(), None, sp)
+        if rc:
+            raise RuntimeError(f"decode failed: {L.STATUS_NAMES[rc]} {L.last_error()}")
+    ev1.record(stream)
+    torch.cuda.synchronize()
     ev_ms = ev0.elapsed_time(ev1) / args.steps
     # algorithmic bytes per launch of the dominant kernel: 1 MiB read + 1 MiB written per chunk
     alg_bytes = lib.zgpu_plan_algorithmic_bytes(plan)
@@ -115,8 +125,88 @@ def run_gpu(args, rank, world, dev):
     torch.cuda.synchronize()
     batch_ms = (time.perf_counter() - t1) / reps * 1e3
     lib.zgpu_plan_destroy(plan)
+    host = None
+    if args.host_leg and rank == 0:
+        host = host_leg(chain, enc, shape, grid, chunk_bytes, n_chunks, dec_ref, sp)
     return dict(elapsed=elapsed, ev_ms=ev_ms, alg_bytes=alg_bytes, ok=ok, n_chunks=n_chunks,
-                decoded_bytes=n_chunks * chunk_bytes, batch_ms=batch_ms)
+                decoded_bytes=n_chunks * chunk_bytes, batch_ms=batch_ms, host=host)
+
+
+def host_leg(chain, enc, shape, grid, chunk_bytes, n_chunks, dec_ref, sp):
+    """PCIe-inclusive rates: encoded chunks in pinned host memory -> zgpu_decode_batch
+    (H2D + decode) -> device array, and -> host array (+ D2H). Not the headline value."""
+    from zarrs_amd import make_desc
+    h_enc = enc.cpu().pin_memory()
+    base = h_enc.data_ptr()
+    descs = []
+    for c in range(n_chunks):
+        i, r = divmod(c, grid[1] * grid[2])
+        j, k = divmod(r, grid[2])
+        descs.append(make_desc((base + c * chunk_bytes, chunk_bytes), [CHUNK] * 3,
+                               out_start=[i * CHUNK, j * CHUNK, k * CHUNK]))
+    out = torch.empty(shape, dtype=torch.float32, device=enc.device)
+    res = {}
+    chain.decode_batch(descs, out, shape, enc_device=False, stream=sp)  # warm-up
+    torch.cuda.synchronize()
+    reps = 3
+    t0 = time.perf_counter()
+    for _ in range(reps):
+        chain.decode_batch(descs, out, shape, enc_device=False, stream=sp)
+    torch.cuda.synchronize()
+    t = (time.perf_counter() - t0) / reps
+    res["host_enc_to_device_out_GiBps"] = round(n_chunks * chunk_bytes / t / 2 ** 30, 2)
+    ok = bool(torch.equal(out.view(torch.int32), dec_ref.view(torch.int32)))
+    h_out = torch.empty(shape, dtype=torch.float32).pin_memory()
+    chain.decode_batch(descs, h_out.numpy(), shape, enc_device=False, stream=sp)
+    t0 = time.perf_counter()
+    for _ in range(reps):
+        chain.decode_batch(descs, h_out.numpy(), shape, enc_device=False, stream=sp)
+    t = (time.perf_counter() - t0) / reps
+    res["host_enc_to_host_out_GiBps"] = round(n_chunks * chunk_bytes / t / 2 ** 30, 2)
+    res["roundtrip_ok"] = ok and bool(torch.equal(h_out.view(torch.int32), dec_ref.cpu().view(torch.int32)))
+    return res
+
+
+KERNEL = "k_scatter_tiled"
+
+
+def pmc_traffic(args):
+    """HBM traffic of the dominant kernel per launch from rocprofv3 PMC counters, in two separate
+    passes (FETCH_SIZE and WRITE_SIZE cannot share one pass on gfx950), corrected as
+    /opt/skills/guides/MI355X_MICROARCH.md (HBM) prescribes: counters are in KiB; FETCH_SIZE counts
+    exactly half the bytes of a wide (16 B/lane) coalesced streaming read on gfx950 -> x2;
+    WRITE_SIZE is exact for 16-B streaming stores. Runs bench.py itself as a child under rocprofv3."""
+    import csv
+    import glob
+    import shutil
+    import subprocess
+    import tempfile
+    if not shutil.which("rocprofv3"):
+        return None, "rocprofv3 not found"
+    vals = {}
+    tmp = tempfile.mkdtemp(prefix="zgpu_pmc_")
+    try:
+        for ctr in ("FETCH_SIZE", "WRITE_SIZE"):
+            d = os.path.join(tmp, ctr)
+            cmd = ["rocprofv3", "--pmc", ctr, "--kernel-include-regex", KERNEL, "-d", d, "-o", "pmc",
+                   "--output-format", "csv", "--", sys.executable, os.path.abspath(__file__), "--child",
+                   "--steps", "2", "--warmup", "1", "--no-cpu", "--grid", *map(str, args.grid)]
+            r = subprocess.run(cmd, stdout=subprocess.DEVNULL, stderr=subprocess.PIPE, timeout=240)
+            if r.returncode:
+                return None, f"rocprofv3 --pmc {ctr} rc={r.returncode}: {r.stderr.decode()[-200:]}"
+            files = glob.glob(os.path.join(d, "**", "*counter_collection.csv"), recursive=True)
+            v = [float(row["Counter_Value"]) for f in files for row in csv.DictReader(open(f))
+                 if KERNEL in row["Kernel_Name"] and row["Counter_Name"] == ctr]
+            if not v:
+                return None, f"no {ctr} samples for {KERNEL}"
+            vals[ctr] = sum(v) / len(v)
+    except Exception as e:  # noqa: BLE001 - report, never fail the bench line on the profiler
+        return None, f"pmc pass failed: {e}"
+    finally:
+        shutil.rmtree(tmp, ignore_errors=True)
+    fetch = vals["FETCH_SIZE"] * 1024 * 2
+    write = vals["WRITE_SIZE"] * 1024
+    return {"bytes": int(fetch + write), "fetch_bytes": int(fetch), "write_bytes": int(write)}, None
 
 
 def cpu_baseline(args):
@@ -161,6 +251,10 @@ def main():
     ap.add_argument("--cpu-grid", type=int, nargs=3, default=[8, 8, 8], help="CPU baseline sample grid")
     ap.add_argument("--cpu-seconds", type=float, default=15.0)
     ap.add_argument("--no-cpu", action="store_true")
+    ap.add_argument("--no-pmc", action="store_true", help="skip the rocprofv3 PMC traffic passes")
+    ap.add_argument("--no-host-leg", dest="host_leg", action="store_false",
+                    help="skip the PCIe-inclusive (host input/output) leg")
+    ap.add_argument("--child", action="store_true", help=argparse.SUPPRESS)
     args = ap.parse_args()
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
@@ -172,6 +266,8 @@ def main():
         torch.distributed.init_process_group("nccl", device_id=torch.device("cuda", local))
     dev = torch.device("cuda", local)
     r = run_gpu(args, rank, world, dev)
+    if args.child:
+        return
 
     elapsed = torch.tensor([r["elapsed"]], dtype=torch.float64, device=dev)
     ok = torch.tensor([1 if r["ok"] else 0], dtype=torch.int32, device=dev)
@@ -184,6 +280,9 @@ def main():
     cpu = None
     if rank == 0 and not args.no_cpu:
         cpu = cpu_baseline(args)
+    traffic, traffic_note = None, "skipped (--no-pmc or N>1)"
+    if rank == 0 and world == 1 and not args.no_pmc:
+        traffic, traffic_note = pmc_traffic(args)
     if rank == 0:
         achieved = r["alg_bytes"] / (r["ev_ms"] * 1e-3) / 1e9
         line = {
@@ -196,12 +295,16 @@ def main():
                        "chunks_per_gpu": r["n_chunks"], "array_shape_per_gpu": [g * CHUNK for g in args.grid],
                        "parallelism": f"chunk-partitioned x{world}"},
             "roofline": {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS,
-                         "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": None,
+                         "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBS, 4),
+                         "traffic": traffic["bytes"] if traffic else None,
+                         "traffic_detail": traffic or traffic_note,
                          "kernel": "k_scatter_tiled<4>",
-                         "alg_bytes_per_launch": r["alg_bytes"], "avg_step_ms_hip_events": round(r["ev_ms"], 4)},
+                         "alg_bytes_per_launch": r["alg_bytes"],
+                         "avg_launch_ms_hip_events": round(r["ev_ms"], 4)},
             "cpu_baseline": cpu,
             "roundtrip_ok": bool(ok.item()),
             "decode_batch_ms_incl_host_planning": round(r["batch_ms"], 3),
+            "host_leg": r["host"],
         }
         print(json.dumps(line), flush=True)
     if world > 1:

@@ -182,3 +182,38 @@ def test_error_first_status_per_descriptor(ctx, torch_cuda):
     ch2 = CodecChain.from_metadata(codecs, "uint16", 0, ctx, validate_checksums=False)
     out2 = np.zeros(300, np.uint16)
     assert ch2.decode_batch(descs, out2, [300], enc_device=False) == [0, 0, 0]
+
+
+TILED = [  # (data type, transpose order, chunk shape, array shape): full 64-wide tiles, ragged slab groups
+    ("float32", [2, 1, 0], [64, 6, 64], [128, 12, 192]),
+    ("float64", [2, 1, 0], [64, 5, 64], [128, 10, 128]),
+    ("uint16", [2, 1, 0], [64, 7, 64], [192, 14, 128]),
+    ("uint8", [1, 2, 0], [64, 3, 64], [128, 6, 128]),
+    ("float32", [1, 0], [64, 128], [128, 256]),
+    ("int32", [3, 1, 0, 2], [2, 64, 5, 64], [4, 128, 10, 128]),
+]
+
+
+@pytest.mark.parametrize("dt,order,cs,shape", TILED, ids=[f"{t[0]}_{''.join(map(str, t[1]))}" for t in TILED])
+def test_tiled_transpose_paths(ctx, torch_cuda, dt, order, cs, shape):
+    """The slab-batched LDS transpose (k_scatter_tiled): aligned 16-B paths, ragged slab groups,
+    fill (missing chunk), partial selections, unaligned output offsets -- vs the oracle."""
+    from zarrs_amd import Array, DeviceStore, MemoryStore
+    codecs = [{"name": "transpose", "configuration": {"order": order}},
+              {"name": "bytes", "configuration": {"endian": "big"}}]
+    rng = np.random.default_rng(len(shape) * 100 + cs[1])
+    npdt = np.dtype(O.DTYPES[dt][0])
+    a = (rng.standard_normal(shape) * 1000).astype(npdt)
+    co = O.OracleChain.from_metadata(codecs, dt, 7, len(shape))
+    chunks = _encode_grid(co, a, cs, drop={tuple([1] + [0] * (len(shape) - 1))})
+    ms = MemoryStore({"c/" + "/".join(map(str, k)): v for k, v in chunks.items()})
+    meta = {"shape": shape, "data_type": dt, "fill_value": 7, "codecs": codecs,
+            "chunk_grid": {"name": "regular", "configuration": {"chunk_shape": cs}}}
+    arr = Array(DeviceStore.from_store(ms), meta, ctx)
+    subsets = [([0] * len(shape), shape),
+               ([1] * len(shape), [s - 2 for s in shape]),
+               ([c // 2 for c in cs], [max(1, c) for c in cs])]
+    for start, sub in subsets:
+        exp = O.retrieve_array_subset(co, shape, cs, chunks, start, sub, nthreads=4)
+        got = arr.retrieve_array_subset(start, sub)
+        assert got.tobytes() == exp.tobytes(), (start, sub)

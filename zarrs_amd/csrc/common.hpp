@@ -40,6 +40,9 @@ struct ZgScatter {
   uint32_t swap;      // 1: stored big-endian -> reverse each component
   uint32_t shuffle;   // 1: fused unshuffle with elementsize == es
   uint32_t tile_a;    // decoded axis that is innermost in the encoded layout (tiled kernel)
+  uint32_t tile_b;    // tiled kernel: axis batched TJ slabs per block (smallest encoded stride
+                      // among the other axes: adjacent slabs are adjacent encoded rows); ZG_MAXD = none
+  uint32_t pad0;
   uint64_t chunk_shape[ZG_MAXD];  // leaf decoded shape
   uint64_t enc_stride[ZG_MAXD];   // encoded linear stride (elements) of each decoded axis
   uint64_t out_stride[ZG_MAXD];   // output array C strides (elements)

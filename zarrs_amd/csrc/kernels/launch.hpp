@@ -7,6 +7,8 @@
 namespace zgpu {
 
 enum ScatterMode : uint32_t { SCATTER_ROWS = 0, SCATTER_TILED = 1, SCATTER_GENERIC = 2 };
+// slabs (TILE x TILE tiles at consecutive values of ZgScatter::tile_b) per tiled-scatter block
+constexpr __host__ __device__ int tiled_slabs(uint32_t es) { return es == 8 ? 2 : 4; }
 
 hipError_t launch_scatter(const ZgItem *items, const uint64_t *geom, uint32_t *status, const ZgScatter &P,
                           uint8_t *out, uint32_t n_items, uint32_t mode, uint64_t units_per_item,

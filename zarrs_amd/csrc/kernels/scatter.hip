@@ -208,10 +208,26 @@ __global__ __launch_bounds__(SCATTER_THREADS) void k_scatter_rows(
 
 // ---------------------------------------------------------------------------------------------
 // Tiled transpose: decoded axis A = P.tile_a is innermost (stride 1) in the encoded layout,
-// decoded axis Lx = nd-1 is innermost in the output. A tile is TA x TL elements for fixed values
-// of the other axes; loaded along A (contiguous), stored along Lx (contiguous) via LDS.
+// decoded axis Lx = nd-1 is innermost in the output. A slab is a TILE x TILE tile over (A, Lx) for
+// fixed values of the other axes; loaded along A (contiguous), stored along Lx (contiguous) via
+// LDS. One block moves TJ slabs at consecutive values of axis B = P.tile_b (the other axis with the
+// smallest encoded stride), so for a full chunk the TJ encoded rows of one Lx index are ONE
+// contiguous run (TJ x 256 B for f32 64^3) and every thread keeps TJ*4 16-B loads in flight.
+// Every byte is touched once, so loads and stores are non-temporal (no L2 retention).
+// Measured on MI355X (tools/lab/scatter_lab.hip, 4096 x 64^3 f32 chunks): TJ 1 -> 5.19 TB/s,
+// TJ 2 -> 5.48, TJ 4 -> 5.81, TJ 4 + nt -> 5.98 TB/s; TJ 8 (1 block/CU) is slower again.
 // ---------------------------------------------------------------------------------------------
 constexpr int TILE = 64;
+
+typedef unsigned int zg_v4u __attribute__((ext_vector_type(4)));
+__device__ __forceinline__ uint4 nt_load16(const void *p) {
+  const zg_v4u x = __builtin_nontemporal_load((const zg_v4u *)p);
+  return make_uint4(x.x, x.y, x.z, x.w);
+}
+__device__ __forceinline__ void nt_store16(void *p, uint4 v) {
+  const zg_v4u x = {v.x, v.y, v.z, v.w};
+  __builtin_nontemporal_store(x, (zg_v4u *)p);
+}
 
 template <int ES>
 __global__ __launch_bounds__(SCATTER_THREADS) void k_scatter_tiled(
@@ -219,93 +235,121 @@ __global__ __launch_bounds__(SCATTER_THREADS) void k_scatter_tiled(
     ZgScatter P, uint8_t *__restrict__ out, uint32_t tiles_per_item) {
   using T = typename std::conditional<ES == 1, uint8_t, typename std::conditional<ES == 2, uint16_t,
             typename std::conditional<ES == 4, uint32_t, uint2>::type>::type>::type;
-  // one padded row per L index; +1 element pad keeps column reads at 2-way conflicts at most
-  __shared__ T tile[TILE][TILE + (ES >= 4 ? 1 : 4 / ES)];
+  constexpr int TJ = tiled_slabs(ES);
+  constexpr int PITCH = TILE + (ES >= 4 ? 1 : 4 / ES);  // +1 word: column reads conflict-free
+  constexpr int SLAB = TILE * PITCH + (ES >= 4 ? 1 : 4 / ES);  // +1 word: slabs on distinct banks
+  __shared__ T tile[TJ * SLAB];
   const uint32_t item = blockIdx.x / tiles_per_item;
   uint32_t t = blockIdx.x % tiles_per_item;
   const ZgItem it = items[item];
   if (!item_live(it, status, item, P)) return;
-  const uint32_t nd = P.nd, A = P.tile_a, Lx = nd - 1;
+  const uint32_t nd = P.nd, A = P.tile_a, Lx = nd - 1, B = P.tile_b;
   const uint64_t *g = geom + (uint64_t)item * 3 * nd;
   const uint64_t *ss = g, *sh = g + nd, *os = g + 2 * nd;
+  const bool hasB = B < nd;
+  const uint64_t bext = hasB ? sh[B] : 1;
   const uint32_t nta = (uint32_t)((sh[A] + TILE - 1) / TILE), ntl = (uint32_t)((sh[Lx] + TILE - 1) / TILE);
+  const uint32_t nbg = (uint32_t)((bext + TJ - 1) / TJ);
   const uint32_t ta = t % nta; t /= nta;
   const uint32_t tl = t % ntl; t /= ntl;
-  // remaining index enumerates the other axes (row-major over axes != A, Lx)
+  const uint32_t tb = t % nbg; t /= nbg;
+  // remaining index enumerates the other axes (row-major over axes != A, Lx, B)
   uint64_t so = 0, dof = 0, rem = t;
   for (int d = (int)nd - 1; d >= 0; d--) {
-    if ((uint32_t)d == A || (uint32_t)d == Lx) continue;
+    if ((uint32_t)d == A || (uint32_t)d == Lx || (uint32_t)d == B) continue;
     const uint64_t c = rem % sh[d];
     rem /= sh[d];
     so += (ss[d] + c) * P.enc_stride[d];
     dof += (os[d] + c) * P.out_stride[d];
   }
   if (rem) return;  // beyond this item's selection
-  const uint64_t a0 = (uint64_t)ta * TILE, l0 = (uint64_t)tl * TILE;
+  const uint64_t a0 = (uint64_t)ta * TILE, l0 = (uint64_t)tl * TILE, b0 = (uint64_t)tb * TJ;
   const uint32_t na = (uint32_t)min<uint64_t>(TILE, sh[A] - a0), nl = (uint32_t)min<uint64_t>(TILE, sh[Lx] - l0);
-  so += (ss[A] + a0) * P.enc_stride[A] + (ss[Lx] + l0) * P.enc_stride[Lx];
-  dof += (os[A] + a0) * P.out_stride[A] + (os[Lx] + l0);
-  const bool fill = it.flags & ZG_ITEM_FILL;
+  const uint32_t nb = (uint32_t)min<uint64_t>(TJ, bext - b0);
+  const uint64_t sL = P.enc_stride[Lx], dA = P.out_stride[A];
+  const uint64_t sB = hasB ? P.enc_stride[B] : 0, dB = hasB ? P.out_stride[B] : 0;
+  so += (ss[A] + a0) * P.enc_stride[A] + (ss[Lx] + l0) * sL + (hasB ? (ss[B] + b0) * sB : 0);
+  dof += (os[A] + a0) * dA + (os[Lx] + l0) + (hasB ? (os[B] + b0) * dB : 0);
   T *dst = (T *)(out) + dof;
-  if (fill) {
+  constexpr int VPR = TILE * ES / 16;  // 16-B vectors per tile row
+  constexpr int EPV = 16 / ES;         // elements per vector
+  constexpr int NV = TJ * TILE * VPR;  // vectors per block
+  const bool oaligned = (((uint64_t)dst & 15) == 0) && ((dA * ES) % 16 == 0) && ((dB * ES) % 16 == 0) &&
+                        nl == TILE;
+  if (it.flags & ZG_ITEM_FILL) {
     T fv;
     __builtin_memcpy(&fv, P.fill, ES);
-    for (uint32_t e = threadIdx.x; e < na * TILE; e += SCATTER_THREADS) {
-      const uint32_t a = e / TILE, l = e % TILE;
-      if (l < nl) dst[(uint64_t)a * P.out_stride[A] + l] = fv;
+    if (oaligned) {
+      uint4 x;
+      T *xe = (T *)&x;
+#pragma unroll
+      for (int k = 0; k < EPV; k++) xe[k] = fv;
+      for (uint32_t e = threadIdx.x; e < (uint32_t)NV; e += SCATTER_THREADS) {
+        const uint32_t a = e / (TJ * VPR), jj = (e / VPR) % TJ, v = e % VPR;
+        if (a < na && jj < nb) nt_store16(dst + jj * dB + (uint64_t)a * dA + v * EPV, x);
+      }
+    } else {
+      for (uint32_t e = threadIdx.x; e < (uint32_t)(TJ * TILE * TILE); e += SCATTER_THREADS) {
+        const uint32_t a = e / (TJ * TILE), jj = (e / TILE) % TJ, l = e % TILE;
+        if (a < na && jj < nb && l < nl) dst[jj * dB + (uint64_t)a * dA + l] = fv;
+      }
     }
     return;
   }
   const T *src = (const T *)(it.src) + so;
-  const uint64_t sL = P.enc_stride[Lx], dA = P.out_stride[A];
   const uint32_t swap = P.swap && P.comp > 1;
-  const bool aligned = ((it.src & 15) == 0) && ((sL * ES) % 16 == 0) && (((so + 0) * ES) % 16 == 0) &&
+  const bool aligned = (((uint64_t)src & 15) == 0) && ((sL * ES) % 16 == 0) && ((sB * ES) % 16 == 0) &&
                        na == TILE;
-  constexpr int VPR = TILE * ES / 16;          // 16-B vectors per tile row
-  constexpr int EPV = 16 / ES;                  // elements per vector
   if (aligned) {
-    constexpr int RPP = SCATTER_THREADS / VPR;  // rows per pass
+    // e -> (row l, slab jj, vector v): a wave reads TJ adjacent encoded rows = one contiguous run
+    constexpr int PER = NV / SCATTER_THREADS;
+    uint4 x[PER];
 #pragma unroll
-    for (int p = 0; p < TILE / RPP; p++) {
-      const uint32_t l = p * RPP + threadIdx.x / VPR, v = threadIdx.x % VPR;
-      if (l < nl) {
-        uint4 x = *(const uint4 *)(src + (uint64_t)l * sL + v * EPV);
-        if (swap) x = swap_vec(x, P.comp);
-        const T *xe = (const T *)&x;
+    for (int p = 0; p < PER; p++) {
+      const uint32_t e = p * SCATTER_THREADS + threadIdx.x;
+      const uint32_t l = e / (TJ * VPR), jj = (e / VPR) % TJ, v = e % VPR;
+      if (l < nl && jj < nb) x[p] = nt_load16(src + jj * sB + (uint64_t)l * sL + v * EPV);
+    }
 #pragma unroll
-        for (int k = 0; k < EPV; k++) tile[l][v * EPV + k] = xe[k];
+    for (int p = 0; p < PER; p++) {
+      const uint32_t e = p * SCATTER_THREADS + threadIdx.x;
+      const uint32_t l = e / (TJ * VPR), jj = (e / VPR) % TJ, v = e % VPR;
+      if (l < nl && jj < nb) {
+        uint4 y = swap ? swap_vec(x[p], P.comp) : x[p];
+        const T *ye = (const T *)&y;
+#pragma unroll
+        for (int k = 0; k < EPV; k++) tile[jj * SLAB + l * PITCH + v * EPV + k] = ye[k];
       }
     }
   } else {
-    for (uint32_t e = threadIdx.x; e < TILE * TILE; e += SCATTER_THREADS) {
-      const uint32_t l = e / TILE, a = e % TILE;
-      if (l < nl && a < na) {
-        uint4 x = load_elem((const uint8_t *)(src + (uint64_t)l * sL + a), ES, P.comp, swap);
+    for (uint32_t e = threadIdx.x; e < (uint32_t)(TJ * TILE * TILE); e += SCATTER_THREADS) {
+      const uint32_t l = e / (TJ * TILE), jj = (e / TILE) % TJ, a = e % TILE;
+      if (l < nl && jj < nb && a < na) {
+        uint4 y = load_elem((const uint8_t *)(src + jj * sB + (uint64_t)l * sL + a), ES, P.comp, swap);
         T v;
-        __builtin_memcpy(&v, &x, ES);
-        tile[l][a] = v;
+        __builtin_memcpy(&v, &y, ES);
+        tile[jj * SLAB + l * PITCH + a] = v;
       }
     }
   }
   __syncthreads();
-  const bool oaligned = (((uint64_t)dst & 15) == 0) && ((dA * ES) % 16 == 0) && nl == TILE;
   if (oaligned) {
-    constexpr int RPP = SCATTER_THREADS / VPR;
 #pragma unroll
-    for (int p = 0; p < TILE / RPP; p++) {
-      const uint32_t a = p * RPP + threadIdx.x / VPR, v = threadIdx.x % VPR;
-      if (a < na) {
-        uint4 x;
-        T *xe = (T *)&x;
+    for (int p = 0; p < NV / SCATTER_THREADS; p++) {
+      const uint32_t e = p * SCATTER_THREADS + threadIdx.x;
+      const uint32_t a = e / (TJ * VPR), jj = (e / VPR) % TJ, v = e % VPR;
+      if (a < na && jj < nb) {
+        uint4 y;
+        T *ye = (T *)&y;
 #pragma unroll
-        for (int k = 0; k < EPV; k++) xe[k] = tile[v * EPV + k][a];
-        *(uint4 *)(dst + (uint64_t)a * dA + v * EPV) = x;
+        for (int k = 0; k < EPV; k++) ye[k] = tile[jj * SLAB + (v * EPV + k) * PITCH + a];
+        nt_store16(dst + jj * dB + (uint64_t)a * dA + v * EPV, y);
       }
     }
   } else {
-    for (uint32_t e = threadIdx.x; e < TILE * TILE; e += SCATTER_THREADS) {
-      const uint32_t a = e / TILE, l = e % TILE;
-      if (a < na && l < nl) dst[(uint64_t)a * dA + l] = tile[l][a];
+    for (uint32_t e = threadIdx.x; e < (uint32_t)(TJ * TILE * TILE); e += SCATTER_THREADS) {
+      const uint32_t a = e / (TJ * TILE), jj = (e / TILE) % TJ, l = e % TILE;
+      if (a < na && jj < nb && l < nl) dst[jj * dB + (uint64_t)a * dA + l] = tile[jj * SLAB + l * PITCH + a];
     }
   }
 }
@@ -392,9 +436,11 @@ uint64_t scatter_units_per_item(uint32_t mode, const ZgScatter &P, const uint64_
     return (rows + ROWS_PER_BLOCK - 1) / ROWS_PER_BLOCK;
   }
   if (mode == SCATTER_TILED) {
+    const uint64_t tj = tiled_slabs(P.es);
     uint64_t t = 1;
     for (uint32_t d = 0; d < nd; d++) {
       if (d == P.tile_a || d == nd - 1) t *= (max_sel_shape[d] + TILE - 1) / TILE;
+      else if (d == P.tile_b) t *= (max_sel_shape[d] + tj - 1) / tj;
       else t *= max_sel_shape[d];
     }
     return t;

@@ -166,15 +166,20 @@ struct zgpu_plan {
   uint2 *d_aux = nullptr;
   uint8_t *d_zlit = nullptr;
   unsigned long long *d_counter = nullptr;
+  // control block: [counter (256 B) | per-item status (4 B each)], cleared by ONE memset and read
+  // back by ONE D2H copy into pinned memory (h_ctl) per execute
+  uint8_t *d_ctl = nullptr, *h_ctl = nullptr;
+  size_t ctl_bytes = 0;
   // host-input staging
   uint8_t *d_enc_stage = nullptr;
   uint64_t last_enc_bytes = 0;
 
   ~zgpu_plan() {
     if (!ctx) return;
-    void *bufs[] = {d_items, d_items_init, d_geom, d_status, d_shards, d_index, d_shard_status,
-                    d_pool[0], d_pool[1], d_aux, d_zlit, d_counter, d_enc_stage};
+    void *bufs[] = {d_items, d_items_init, d_geom, d_shards, d_index, d_shard_status,
+                    d_pool[0], d_pool[1], d_aux, d_zlit, d_ctl, d_enc_stage};
     for (void *b : bufs) ctx->dev_free(b);
+    ctx->host_free(h_ctl);
   }
 };
 
@@ -402,6 +407,11 @@ static void plan_build(zgpu_plan &P, const zgpu_chunk_desc *descs) {
     S.out_stride[d] = out_strides[d];
   }
   S.tile_a = m[nd - 1];
+  S.tile_b = ZG_MAXD;
+  for (uint32_t d = 0; d + 1 < nd; d++) {
+    if (d == S.tile_a) continue;
+    if (S.tile_b == ZG_MAXD || S.enc_stride[d] <= S.enc_stride[S.tile_b]) S.tile_b = d;
+  }
   if (S.tile_a == nd - 1) {
     P.scatter_mode = SCATTER_ROWS;
   } else if (!S.shuffle && (S.es == 1 || S.es == 2 || S.es == 4 || S.es == 8)) {
@@ -419,7 +429,6 @@ static void plan_upload(zgpu_plan &P) {
     P.d_items = (ZgItem *)C.dev_alloc(ni * sizeof(ZgItem));
     P.d_items_init = (ZgItem *)C.dev_alloc(ni * sizeof(ZgItem));
     P.d_geom = (uint64_t *)C.dev_alloc(P.geom.size() * 8);
-    P.d_status = (uint32_t *)C.dev_alloc(ni * 4);
     HIPCHK(hipMemcpyAsync(P.d_items_init, P.items.data(), ni * sizeof(ZgItem), hipMemcpyHostToDevice, C.stream));
     HIPCHK(hipMemcpyAsync(P.d_geom, P.geom.data(), P.geom.size() * 8, hipMemcpyHostToDevice, C.stream));
     for (int k = 0; k < P.n_pools; k++) P.d_pool[k] = (uint8_t *)C.dev_alloc(ni * P.slot_bytes);
@@ -428,7 +437,11 @@ static void plan_upload(zgpu_plan &P) {
       if (s.kind == ST_ZSTD && !P.d_zlit) P.d_zlit = (uint8_t *)C.dev_alloc(ni * zstd_lit_scratch_per_item());
     }
   }
-  P.d_counter = (unsigned long long *)C.dev_alloc(256);
+  P.ctl_bytes = 256 + ni * 4;
+  P.d_ctl = (uint8_t *)C.dev_alloc(P.ctl_bytes);
+  P.h_ctl = (uint8_t *)C.host_alloc(P.ctl_bytes);
+  P.d_counter = (unsigned long long *)P.d_ctl;
+  P.d_status = (uint32_t *)(P.d_ctl + 256);
   if (!P.shards.empty()) {
     P.d_shards = (ZgShard *)C.dev_alloc(P.shards.size() * sizeof(ZgShard));
     P.d_index = (uint64_t *)C.dev_alloc(P.shards.size() * P.ispec.n_inner * 16);
@@ -441,10 +454,13 @@ static void plan_upload(zgpu_plan &P) {
 // Enqueue the decode of an uploaded plan on stream s.
 static void plan_enqueue(zgpu_plan &P, uint8_t *out, hipStream_t s) {
   const uint32_t ni = (uint32_t)P.items.size();
-  HIPCHK(hipMemsetAsync(P.d_counter, 0, 256, s));
+  HIPCHK(hipMemsetAsync(P.d_ctl, 0, P.ctl_bytes, s));
   if (!ni) return;
-  HIPCHK(hipMemcpyAsync(P.d_items, P.d_items_init, ni * sizeof(ZgItem), hipMemcpyDeviceToDevice, s));
-  HIPCHK(hipMemsetAsync(P.d_status, 0, (size_t)ni * 4, s));
+  // stages rewrite each item's {src,len} in place; a chain with none reads the uploaded table as is
+  const bool mutates = P.sharded || !P.stages.empty();
+  ZgItem *items = mutates ? P.d_items : P.d_items_init;
+  if (mutates)
+    HIPCHK(hipMemcpyAsync(P.d_items, P.d_items_init, ni * sizeof(ZgItem), hipMemcpyDeviceToDevice, s));
   if (P.sharded) {
     HIPCHK(launch_shard_index(P.d_shards, (uint32_t)P.shards.size(), P.ispec, P.d_index, P.d_shard_status, s));
     HIPCHK(launch_item_resolve(P.d_items, P.d_status, ni, P.d_shards, P.d_index, P.d_shard_status, P.ispec.n_inner,
@@ -467,18 +483,18 @@ static void plan_enqueue(zgpu_plan &P, uint8_t *out, hipStream_t s) {
         break;
     }
   }
-  HIPCHK(launch_scatter(P.d_items, P.d_geom, P.d_status, P.scatter, out, ni, P.scatter_mode, P.scatter_units, s));
+  HIPCHK(launch_scatter(items, P.d_geom, P.d_status, P.scatter, out, ni, P.scatter_mode, P.scatter_units, s));
 }
 
 // Read back per-item statuses and reduce them to per-descriptor statuses. Returns the first
 // non-zero descriptor status.
 static int plan_statuses(zgpu_plan &P, int32_t *status, hipStream_t s) {
   const size_t ni = P.items.size();
-  std::vector<uint32_t> st(ni);
-  unsigned long long counter = 0;
-  if (ni) HIPCHK(hipMemcpyAsync(st.data(), P.d_status, ni * 4, hipMemcpyDeviceToHost, s));
-  HIPCHK(hipMemcpyAsync(&counter, P.d_counter, 8, hipMemcpyDeviceToHost, s));
+  HIPCHK(hipMemcpyAsync(P.h_ctl, P.d_ctl, P.ctl_bytes, hipMemcpyDeviceToHost, s));
   HIPCHK(hipStreamSynchronize(s));
+  unsigned long long counter;
+  std::memcpy(&counter, P.h_ctl, sizeof(counter));
+  const uint32_t *st = (const uint32_t *)(P.h_ctl + 256);
   P.last_enc_bytes = counter;
   std::vector<int32_t> ds(P.item_desc_status.begin(), P.item_desc_status.end());
   for (size_t i = 0; i < ni; i++) {
@@ -654,8 +670,15 @@ int zgpu_decode_batch(zgpu_chain *ch, uint32_t nd, const zgpu_chunk_desc *descs,
   bool host_out = !(flags & ZGPU_OUT_DEVICE);
   if (host_out) {
     dout = (uint8_t *)C->dev_alloc(out_bytes ? out_bytes : 1);
-    // regions not covered by any descriptor keep the caller's bytes
-    HIPCHK(hipMemcpyAsync(dout, out, out_bytes, hipMemcpyHostToDevice, s));
+    // regions not covered by any descriptor keep the caller's bytes; the regions are disjoint
+    // (ArrayBytesFixedDisjointView contract), so equal volumes mean full coverage: no upload
+    uint64_t covered = 0;
+    for (uint64_t i = 0; i < n; i++) {
+      uint64_t v = 1;
+      for (uint32_t d = 0; d < nd; d++) v *= descs[i].sel_shape[d];
+      covered += v;
+    }
+    if (covered != out_elems) HIPCHK(hipMemcpyAsync(dout, out, out_bytes, hipMemcpyHostToDevice, s));
   }
   std::unique_ptr<zgpu_plan> P;
   int rc = 0;
