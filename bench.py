@@ -1,18 +1,26 @@
 #!/usr/bin/env python3
 """bench.py — decoded-array GiB/s of the MI355X chunk-decode pipeline on device-resident chunks.
 
-Workload (BASELINE.json configs[1]): 4096 independent 64^3 float32 chunks per GPU
-(a [1024,1024,1024] array, 4 GiB encoded + 4 GiB decoded), codecs
+Default workload (BASELINE.json configs[1]): 4096 independent 64^3 float32
+chunks per GPU (a [1024,1024,1024] array, 4 GiB encoded + 4 GiB decoded), codecs
 [transpose{order:[2,1,0]}, bytes{endian:big}], encoded chunks resident in HBM, decoded into one
-device output array. One step = one zgpu_plan_execute over the whole 4096-chunk batch, per-chunk
-statuses read back (the full decode, nothing skipped). N GPUs: one process per GPU, each decodes its
-own 4096 chunks (weak scaling, no data-path collective); time = max over ranks.
+device output array. One step = one zgpu_plan_execute over the whole batch with per-chunk statuses
+read back (the full decode, nothing skipped). N GPUs: one process per GPU, each decodes its own
+4096 chunks (chunks are independent: weak scaling, no data-path collective); time = max over ranks.
+
+--workload c3: sharded [2048]^3 f32 array, 256^3 shards of 32^3 inner chunks,
+[bytes, gzip 1, crc32c] + [bytes, crc32c] index; read the subset [200:968, 300:1068, 1000:1768]
+(64 shards touched, 8 fully covered, 56 partial). With N GPUs the subset is split into N slabs along
+axis 0 (each rank decodes the inner chunks its slab touches) and gathered to rank 0 over RCCL
+inside the timed step (C4).
 
 Prints ONE JSON line (rank 0). Extra objects:
-  roofline      dominant kernel (k_scatter_tiled<4>): algorithmic bytes per launch / average step
-                time from HIP events on the launch stream, against 8.0 TB/s HBM3E
-  cpu_baseline  the oracle (C restatement of zarrs' per-chunk pipeline, oracle/) on the host cores,
+  roofline      dominant kernel: algorithmic bytes per launch / device time per launch (HIP events on
+                the stream the library launches on), against 8.0 TB/s HBM3E; traffic = HBM bytes
+                per launch from rocprofv3 PMC passes (FETCH_SIZE, WRITE_SIZE) of this same script
+  cpu_baseline  the oracle (oracle/, C restatement of zarrs' per-chunk pipeline) on the host cores,
                 rank 0 only, on a bounded sample of the same workload
+  host_leg      (C2) PCIe-inclusive rates: encoded chunks in pinned host memory
 """
 from __future__ import annotations
 
@@ -31,65 +39,303 @@ import torch  # noqa: E402
 
 HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec, /opt/skills/guides/MI355X_MICROARCH.md
 METRIC = "decoded-array GiB/s, device-resident chunks, 1/2/4/8 MI355X; % HBM roofline"
-CODECS = [{"name": "transpose", "configuration": {"order": [2, 1, 0]}},
-          {"name": "bytes", "configuration": {"endian": "big"}}]
-CHUNK = 64
 
 
-def gen_decoded(shape, seed, device):
-    g = torch.Generator(device=device)
-    g.manual_seed(seed)
-    return torch.rand(shape, generator=g, device=device, dtype=torch.float32) * 2 - 1
+def _threads():
+    return int(os.environ.get("OMP_NUM_THREADS", "0") or 0) or os.cpu_count() or 1
 
 
-def encode_c2(dec: torch.Tensor) -> torch.Tensor:
-    """[G0*64, G1*64, G2*64] f32 -> encoded chunks [n_chunks, 64,64,64] (transpose [2,1,0], big endian),
-    chunk-major in C order of the chunk grid, as uint8 [n_chunks * 1 MiB]."""
-    g0, g1, g2 = (s // CHUNK for s in dec.shape)
-    t = dec.view(g0, CHUNK, g1, CHUNK, g2, CHUNK).permute(0, 2, 4, 5, 3, 1)  # chunk(i,j,k), enc(k,j,i)
-    t = t.contiguous().view(torch.uint8).view(-1, 4).flip(1)  # big endian
-    return t.contiguous().view(-1)
+def _synth():
+    path = os.path.join(ROOT, "tools", "synth", "libsynth.so")
+    if not os.path.exists(path):
+        raise RuntimeError(f"{path} missing: make -C tools/synth (or __graft_entry__.build())")
+    L = C.CDLL(path)
+    P64 = C.POINTER(C.c_uint64)
+    L.synth_c3_values.argtypes = [P64, P64, C.c_void_p, C.c_int]
+    L.synth_gzip_crc_shard.argtypes = [C.c_void_p, C.c_uint64, P64, P64, C.c_int, C.c_int,
+                                       C.POINTER(C.c_void_p), P64]
+    L.synth_free.argtypes = [C.c_void_p]
+    return L
 
 
+def _u64(v):
+    return (C.c_uint64 * len(v))(*[int(x) for x in v])
+
+
+# ------------------------------------------------------------------------------------------------
+# C2
+# ------------------------------------------------------------------------------------------------
+class C2:
+    CODECS = [{"name": "transpose", "configuration": {"order": [2, 1, 0]}},
+              {"name": "bytes", "configuration": {"endian": "big"}}]
+    CHUNK = 64
+    kernel = "k_scatter_tiled"
+    dtype = "f32"
+
+    def __init__(self, args, rank, world, dev):
+        from zarrs_amd import CodecChain, make_desc
+        self.args, self.rank, self.world, self.dev = args, rank, world, dev
+        grid = args.grid
+        K = self.CHUNK
+        self.shape = [g * K for g in grid]
+        self.n_chunks = grid[0] * grid[1] * grid[2]
+        self.chunk_bytes = K ** 3 * 4
+        g = torch.Generator(device=dev)
+        g.manual_seed(1234 + rank)
+        self.dec_ref = torch.rand(self.shape, generator=g, device=dev, dtype=torch.float32) * 2 - 1
+        self.enc = self.encode(self.dec_ref)
+        self.chain = CodecChain.from_metadata(self.CODECS, "float32", 0.0, args.ctx)
+        base = self.enc.data_ptr()
+        self.descs = []
+        for c in range(self.n_chunks):
+            i, r = divmod(c, grid[1] * grid[2])
+            j, k = divmod(r, grid[2])
+            self.descs.append(make_desc((base + c * self.chunk_bytes, self.chunk_bytes), [K] * 3,
+                                        out_start=[i * K, j * K, k * K]))
+        self.out = torch.empty(self.shape, dtype=torch.float32, device=dev)
+        self.out_shape = self.shape
+        self.decoded_bytes = self.n_chunks * self.chunk_bytes  # per rank per step
+        self.config = {"workload": "C2: 4096 independent 64^3 f32 chunks per GPU, "
+                                   "[transpose{order:[2,1,0]}, bytes{endian:big}], device-resident",
+                       "chunks_per_gpu": self.n_chunks, "array_shape_per_gpu": self.shape,
+                       "parallelism": f"chunk-partitioned x{world}"}
+        self.data = "synthetic (uniform [-1,1) f32, encoded on device; decode(encode(x)) == x checked)"
+        self.scaling = "weak"
+
+    @classmethod
+    def encode(cls, dec: torch.Tensor) -> torch.Tensor:
+        """[G0*64, G1*64, G2*64] f32 -> encoded chunks (transpose [2,1,0], big endian), chunk-major
+        in C order of the chunk grid, as uint8 [n_chunks * 1 MiB]."""
+        K = cls.CHUNK
+        g0, g1, g2 = (s // K for s in dec.shape)
+        t = dec.view(g0, K, g1, K, g2, K).permute(0, 2, 4, 5, 3, 1)  # chunk(i,j,k), enc(k,j,i)
+        t = t.contiguous().view(torch.uint8).view(-1, 4).flip(1)  # big endian
+        return t.contiguous().view(-1)
+
+    def after_decode(self):
+        pass
+
+    def check(self) -> bool:
+        return bool(torch.equal(self.out.view(torch.int32), self.dec_ref.view(torch.int32)))
+
+    def cpu_baseline(self):
+        """Oracle (C restatement of zarrs' per-chunk pipeline) on host cores, bounded sample."""
+        sys.path.insert(0, os.path.join(ROOT, "oracle"))
+        import oracle as O
+        K, threads, g = self.CHUNK, _threads(), self.args.cpu_grid
+        shape = [x * K for x in g]
+        n = g[0] * g[1] * g[2]
+        rng = np.random.default_rng(7)
+        dec = (rng.random(shape, dtype=np.float32) * 2 - 1)
+        enc = np.ascontiguousarray(dec.reshape(g[0], K, g[1], K, g[2], K)
+                                   .transpose(0, 2, 4, 5, 3, 1)).astype(">f4").reshape(n, -1)
+        chain = O.OracleChain.from_metadata(self.CODECS, "float32", 0.0, 3)
+        ptrs = (C.c_void_p * n)(*[enc[c].ctypes.data for c in range(n)])
+        lens = (C.c_uint64 * n)(*([K ** 3 * 4] * n))
+        out = np.empty(shape, np.float32)
+        O.retrieve_ptrs(chain, shape, [K] * 3, ptrs, lens, [0, 0, 0], shape, out, threads)
+        assert np.array_equal(out, dec)
+        times = _time_reps(lambda: O.retrieve_ptrs(chain, shape, [K] * 3, ptrs, lens, [0, 0, 0], shape,
+                                                   out, threads), self.args.cpu_seconds)
+        t = float(np.median(times))
+        return {"value": round(n * K ** 3 * 4 / t / 2 ** 30, 3), "unit": "GiB/s", "cores": threads,
+                "kind": "port",
+                "sample": f"{n} of the 4096 chunks ({shape[0]}x{shape[1]}x{shape[2]} f32 subset), median of "
+                          f"{len(times)} reps, oracle retrieve_array_subset with {threads} threads"}
+
+    def host_leg(self, sp):
+        """PCIe-inclusive rates: encoded chunks in pinned host memory -> zgpu_decode_batch
+        (H2D + decode) -> device array, and -> host array (+ D2H). Not the headline value."""
+        from zarrs_amd import make_desc
+        K, grid = self.CHUNK, self.args.grid
+        h_enc = self.enc.cpu().pin_memory()
+        base = h_enc.data_ptr()
+        descs = []
+        for c in range(self.n_chunks):
+            i, r = divmod(c, grid[1] * grid[2])
+            j, k = divmod(r, grid[2])
+            descs.append(make_desc((base + c * self.chunk_bytes, self.chunk_bytes), [K] * 3,
+                                   out_start=[i * K, j * K, k * K]))
+        res = {}
+        out = self.out
+        self.chain.decode_batch(descs, out, self.shape, enc_device=False, stream=sp)  # warm-up
+        torch.cuda.synchronize()
+        reps = 3
+        t0 = time.perf_counter()
+        for _ in range(reps):
+            self.chain.decode_batch(descs, out, self.shape, enc_device=False, stream=sp)
+        torch.cuda.synchronize()
+        t = (time.perf_counter() - t0) / reps
+        res["host_enc_to_device_out_GiBps"] = round(self.decoded_bytes / t / 2 ** 30, 2)
+        ok = self.check()
+        h_out = torch.empty(self.shape, dtype=torch.float32).pin_memory()
+        self.chain.decode_batch(descs, h_out, self.shape, enc_device=False, stream=sp)
+        t0 = time.perf_counter()
+        for _ in range(reps):
+            self.chain.decode_batch(descs, h_out, self.shape, enc_device=False, stream=sp)
+        t = (time.perf_counter() - t0) / reps
+        res["host_enc_to_host_out_GiBps"] = round(self.decoded_bytes / t / 2 ** 30, 2)
+        res["roundtrip_ok"] = ok and bool(torch.equal(h_out.view(torch.int32), self.dec_ref.cpu().view(torch.int32)))
+        return res
+
+
+# ------------------------------------------------------------------------------------------------
+# C3 / C4
+# ------------------------------------------------------------------------------------------------
+class C3:
+    SHARD, INNER = 256, 32
+    ARRAY = [2048, 2048, 2048]
+    SUB_START, SUB_SHAPE = [200, 300, 1000], [768, 768, 768]
+    CODECS = [{"name": "sharding_indexed", "configuration": {
+        "chunk_shape": [32, 32, 32],
+        "codecs": [{"name": "bytes", "configuration": {"endian": "little"}},
+                   {"name": "gzip", "configuration": {"level": 1}}, {"name": "crc32c"}],
+        "index_codecs": [{"name": "bytes", "configuration": {"endian": "little"}}, {"name": "crc32c"}],
+        "index_location": "end"}}]
+    kernel = "k_gzip"
+    dtype = "f32"
+
+    def __init__(self, args, rank, world, dev):
+        from zarrs_amd import CodecChain, make_desc
+        self.args, self.rank, self.world, self.dev = args, rank, world, dev
+        S = self.SHARD
+        if self.SUB_SHAPE[0] % world:
+            raise ValueError("the subset's axis-0 extent must divide by the GPU count")
+        slab = self.SUB_SHAPE[0] // world
+        # this rank's slab of the subset (array coordinates)
+        self.start = [self.SUB_START[0] + rank * slab] + self.SUB_START[1:]
+        self.shape = [slab] + self.SUB_SHAPE[1:]
+        syn = _synth()
+        self.chain = CodecChain.from_metadata(self.CODECS, "float32", 0.0, args.ctx)
+        lo = [s // S for s in self.start]
+        hi = [(s + n - 1) // S + 1 for s, n in zip(self.start, self.shape)]
+        self.shards, self.descs, enc_total = {}, [], 0
+        dec = np.empty([S] * 3, np.float32)
+        nt = _threads()
+        for si in range(lo[0], hi[0]):
+            for sj in range(lo[1], hi[1]):
+                for sk in range(lo[2], hi[2]):
+                    org = [si * S, sj * S, sk * S]
+                    syn.synth_c3_values(_u64(org), _u64([S] * 3), dec.ctypes.data, nt)
+                    p, n = C.c_void_p(), C.c_uint64()
+                    if syn.synth_gzip_crc_shard(dec.ctypes.data, 4, _u64([S] * 3), _u64([self.INNER] * 3), 1,
+                                                nt, C.byref(p), C.byref(n)):
+                        raise RuntimeError("shard encode failed")
+                    host = np.ctypeslib.as_array((C.c_uint8 * n.value).from_address(p.value)).copy()
+                    syn.synth_free(p)
+                    t = torch.from_numpy(host).to(dev)
+                    self.shards[(si, sj, sk)] = (t, host)
+                    enc_total += n.value
+                    s0 = [max(a, o) for a, o in zip(self.start, org)]
+                    s1 = [min(a + b, o + S) for a, b, o in zip(self.start, self.shape, org)]
+                    self.descs.append(make_desc((t.data_ptr(), n.value), [S] * 3,
+                                                sel_start=[a - o for a, o in zip(s0, org)],
+                                                sel_shape=[b - a for a, b in zip(s0, s1)],
+                                                out_start=[a - b for a, b in zip(s0, self.start)]))
+        self.enc_total = enc_total
+        n_sh = len(self.shards)
+        self.ratio = n_sh * S ** 3 * 4 / enc_total
+        exp = np.empty(self.shape, np.float32)
+        syn.synth_c3_values(_u64(self.start), _u64(self.shape), exp.ctypes.data, nt)
+        self.expected = torch.from_numpy(exp).to(dev)
+        self.out = torch.empty(self.shape, dtype=torch.float32, device=dev)
+        self.out_shape = self.shape
+        self.decoded_bytes = int(np.prod(self.shape)) * 4  # per rank per step
+        self.gathered = None
+        if world > 1 and rank == 0:
+            self.gathered = [torch.empty(self.shape, dtype=torch.float32, device=dev) for _ in range(world)]
+        self.config = {"workload": "C3" + ("/C4" if world > 1 else "") +
+                                   ": sharded [2048]^3 f32, 256^3 shards / 32^3 inner chunks, "
+                                   "[bytes, gzip 1, crc32c] + [bytes, crc32c] index at end, read subset "
+                                   "[200:968, 300:1068, 1000:1768]",
+                       "shards_touched_per_gpu": n_sh, "subset_shape": self.SUB_SHAPE,
+                       "slab_per_gpu": self.shape, "gzip_ratio": round(self.ratio, 3),
+                       "encoded_bytes_resident_per_gpu": enc_total,
+                       "parallelism": f"axis-0 slabs x{world}" + (", RCCL gather to rank 0 in the step"
+                                                                   if world > 1 else "")}
+        self.data = ("synthetic (round(256*(sin(.05x)+cos(.03y)+.5sin(.07z))+N(0,1))/256 f32, shards "
+                     "written by tools/synth; decode(encode(x)) == x checked on device)")
+        self.scaling = "strong"
+
+    def after_decode(self):
+        if self.world > 1:  # C4: the requested subset spans GPUs -> one gather to the root
+            torch.distributed.gather(self.out, self.gathered, dst=0)
+
+    def check(self) -> bool:
+        ok = bool(torch.equal(self.out.view(torch.int32), self.expected.view(torch.int32)))
+        if self.gathered is not None:
+            ok = ok and bool(torch.equal(self.gathered[0], self.out))
+        return ok
+
+    def cpu_baseline(self):
+        sys.path.insert(0, os.path.join(ROOT, "oracle"))
+        import oracle as O
+        threads = _threads()
+        chain = O.OracleChain.from_metadata(self.CODECS, "float32", 0.0, 3)
+        # sample: the first 2x2x2 shards' worth of the subset (a [256-56, 256-44, 256-232]... box
+        # anchored at the subset start, clipped to 256^3)
+        sub = [min(256, n) for n in self.shape]
+        grid = [a // self.SHARD for a in self.ARRAY]
+        ptrs = (C.c_void_p * int(np.prod(grid)))()
+        lens = (C.c_uint64 * int(np.prod(grid)))()
+        for (si, sj, sk), (_, host) in self.shards.items():
+            lin = (si * grid[1] + sj) * grid[2] + sk
+            ptrs[lin] = host.ctypes.data
+            lens[lin] = host.nbytes
+        out = np.empty(sub, np.float32)
+        O.retrieve_ptrs(chain, self.ARRAY, [self.SHARD] * 3, ptrs, lens, self.start, sub, out, threads)
+        assert np.array_equal(out, self.expected[:sub[0], :sub[1], :sub[2]].cpu().numpy())
+        times = _time_reps(lambda: O.retrieve_ptrs(chain, self.ARRAY, [self.SHARD] * 3, ptrs, lens,
+                                                   self.start, sub, out, threads), self.args.cpu_seconds)
+        t = float(np.median(times))
+        return {"value": round(out.nbytes / t / 2 ** 30, 3), "unit": "GiB/s", "cores": threads, "kind": "port",
+                "sample": f"subset {sub} at {self.start} of the same shards, median of {len(times)} reps, "
+                          f"oracle retrieve_array_subset (zlib inflate) with {threads} threads"}
+
+    def host_leg(self, sp):
+        return None
+
+
+WORKLOADS = {"c2": C2, "c3": C3}
+
+
+def _time_reps(fn, seconds):
+    times = []
+    t_end = time.perf_counter() + seconds
+    while len(times) < 5 or (time.perf_counter() < t_end and len(times) < 50):
+        t0 = time.perf_counter()
+        fn()
+        times.append(time.perf_counter() - t0)
+    return times
+
+
+# ------------------------------------------------------------------------------------------------
 def run_gpu(args, rank, world, dev):
-    from zarrs_amd import CodecChain, Context, make_desc
+    from zarrs_amd import Context
     from zarrs_amd import _lib as L
-    grid = args.grid
-    shape = [g * CHUNK for g in grid]
-    n_chunks = grid[0] * grid[1] * grid[2]
-    chunk_bytes = CHUNK ** 3 * 4
-    dec_ref = gen_decoded(shape, 1234 + rank, dev)
-    enc = encode_c2(dec_ref)
-    torch.cuda.synchronize()
-    ctx = Context(dev.index)
-    chain = CodecChain.from_metadata(CODECS, "float32", 0.0, ctx)
-    descs = []
-    base = enc.data_ptr()
-    for c in range(n_chunks):
-        i, r = divmod(c, grid[1] * grid[2])
-        j, k = divmod(r, grid[2])
-        descs.append(make_desc((base + c * chunk_bytes, chunk_bytes), [CHUNK] * 3,
-                               out_start=[i * CHUNK, j * CHUNK, k * CHUNK]))
-    arr = (L.ChunkDesc * n_chunks)(*descs)
-    out = torch.empty(shape, dtype=torch.float32, device=dev)
+    args.ctx = Context(dev.index)
+    W = WORKLOADS[args.workload](args, rank, world, dev)
+    n = len(W.descs)
+    arr = (L.ChunkDesc * n)(*W.descs)
     plan = C.c_void_p()
     lib = L.load()
-    L.check(lib.zgpu_plan_create(chain._h, 3, arr, n_chunks, L.u64s(shape), L.ENC_DEVICE | L.OUT_DEVICE,
+    L.check(lib.zgpu_plan_create(W.chain._h, 3, arr, n, L.u64s(W.out_shape), L.ENC_DEVICE | L.OUT_DEVICE,
                                  C.byref(plan)))
-    status = (C.c_int32 * n_chunks)()
+    status = (C.c_int32 * n)()
     stream = torch.cuda.Stream(dev)  # the library launches on this stream; events are recorded on it
     sp = C.c_void_p(stream.cuda_stream)
 
     def step():
-        rc = lib.zgpu_plan_execute(plan, out.data_ptr(), status, sp)
+        rc = lib.zgpu_plan_execute(plan, W.out.data_ptr(), status, sp)
         if rc:
             raise RuntimeError(f"decode failed: {L.STATUS_NAMES[rc]} {L.last_error()}")
+        W.after_decode()
 
+    torch.cuda.synchronize()
     for _ in range(args.warmup):
         step()
     torch.cuda.synchronize()
-    # round-trip property at full size: decode(encode(x)) == x, bit for bit
-    ok = bool(torch.equal(out.view(torch.int32), dec_ref.view(torch.int32)))
+    ok = W.check()  # decode(encode(x)) == x, bit for bit, at full size
     if world > 1:
         torch.distributed.barrier()
     torch.cuda.synchronize()
@@ -103,74 +349,32 @@ def run_gpu(args, rank, world, dev):
     if args.child:  # rocprofv3 --pmc pass: only the dispatches matter
         lib.zgpu_plan_destroy(plan)
         return None
-    # Device time of one decode launch sequence (ctl memset + k_scatter_tiled), HIP events on the
-    # stream the library launches on; enqueue-only executes (status=NULL), back to back.
+    # Device time of one decode launch sequence, HIP events on the stream the library launches on;
+    # enqueue-only executes (status=NULL), back to back.
     ev0 = torch.cuda.Event(enable_timing=True)
     ev1 = torch.cuda.Event(enable_timing=True)
     ev0.record(stream)
     for _ in range(args.steps):
-        rc = lib.zgpu_plan_execute(plan, out.data_ptr(), None, sp)
+        rc = lib.zgpu_plan_execute(plan, W.out.data_ptr(), None, sp)
         if rc:
             raise RuntimeError(f"decode failed: {L.STATUS_NAMES[rc]} {L.last_error()}")
     ev1.record(stream)
     torch.cuda.synchronize()
     ev_ms = ev0.elapsed_time(ev1) / args.steps
-    # algorithmic bytes per launch of the dominant kernel: 1 MiB read + 1 MiB written per chunk
     alg_bytes = lib.zgpu_plan_algorithmic_bytes(plan)
     # host planning + upload included (zgpu_decode_batch form), for DESIGN.md
     t1 = time.perf_counter()
     reps = max(1, min(5, args.steps))
     for _ in range(reps):
-        chain.decode_batch(descs, out, shape, enc_device=True, stream=sp)
+        W.chain.decode_batch(W.descs, W.out, W.out_shape, enc_device=True, stream=sp)
     torch.cuda.synchronize()
     batch_ms = (time.perf_counter() - t1) / reps * 1e3
     lib.zgpu_plan_destroy(plan)
-    host = None
-    if args.host_leg and rank == 0:
-        host = host_leg(chain, enc, shape, grid, chunk_bytes, n_chunks, dec_ref, sp)
-    return dict(elapsed=elapsed, ev_ms=ev_ms, alg_bytes=alg_bytes, ok=ok, n_chunks=n_chunks,
-                decoded_bytes=n_chunks * chunk_bytes, batch_ms=batch_ms, host=host)
+    host = W.host_leg(sp) if (args.host_leg and rank == 0) else None
+    return dict(W=W, elapsed=elapsed, ev_ms=ev_ms, alg_bytes=alg_bytes, ok=ok, batch_ms=batch_ms, host=host)
 
 
-def host_leg(chain, enc, shape, grid, chunk_bytes, n_chunks, dec_ref, sp):
-    """PCIe-inclusive rates: encoded chunks in pinned host memory -> zgpu_decode_batch
-    (H2D + decode) -> device array, and -> host array (+ D2H). Not the headline value."""
-    from zarrs_amd import make_desc
-    h_enc = enc.cpu().pin_memory()
-    base = h_enc.data_ptr()
-    descs = []
-    for c in range(n_chunks):
-        i, r = divmod(c, grid[1] * grid[2])
-        j, k = divmod(r, grid[2])
-        descs.append(make_desc((base + c * chunk_bytes, chunk_bytes), [CHUNK] * 3,
-                               out_start=[i * CHUNK, j * CHUNK, k * CHUNK]))
-    out = torch.empty(shape, dtype=torch.float32, device=enc.device)
-    res = {}
-    chain.decode_batch(descs, out, shape, enc_device=False, stream=sp)  # warm-up
-    torch.cuda.synchronize()
-    reps = 3
-    t0 = time.perf_counter()
-    for _ in range(reps):
-        chain.decode_batch(descs, out, shape, enc_device=False, stream=sp)
-    torch.cuda.synchronize()
-    t = (time.perf_counter() - t0) / reps
-    res["host_enc_to_device_out_GiBps"] = round(n_chunks * chunk_bytes / t / 2 ** 30, 2)
-    ok = bool(torch.equal(out.view(torch.int32), dec_ref.view(torch.int32)))
-    h_out = torch.empty(shape, dtype=torch.float32).pin_memory()
-    chain.decode_batch(descs, h_out.numpy(), shape, enc_device=False, stream=sp)
-    t0 = time.perf_counter()
-    for _ in range(reps):
-        chain.decode_batch(descs, h_out.numpy(), shape, enc_device=False, stream=sp)
-    t = (time.perf_counter() - t0) / reps
-    res["host_enc_to_host_out_GiBps"] = round(n_chunks * chunk_bytes / t / 2 ** 30, 2)
-    res["roundtrip_ok"] = ok and bool(torch.equal(h_out.view(torch.int32), dec_ref.cpu().view(torch.int32)))
-    return res
-
-
-KERNEL = "k_scatter_tiled"
-
-
-def pmc_traffic(args):
+def pmc_traffic(args, kernel):
     """HBM traffic of the dominant kernel per launch from rocprofv3 PMC counters, in two separate
     passes (FETCH_SIZE and WRITE_SIZE cannot share one pass on gfx950), corrected as
     /opt/skills/guides/MI355X_MICROARCH.md (HBM) prescribes: counters are in KiB; FETCH_SIZE counts
@@ -188,17 +392,18 @@ def pmc_traffic(args):
     try:
         for ctr in ("FETCH_SIZE", "WRITE_SIZE"):
             d = os.path.join(tmp, ctr)
-            cmd = ["rocprofv3", "--pmc", ctr, "--kernel-include-regex", KERNEL, "-d", d, "-o", "pmc",
+            cmd = ["rocprofv3", "--pmc", ctr, "--kernel-include-regex", kernel, "-d", d, "-o", "pmc",
                    "--output-format", "csv", "--", sys.executable, os.path.abspath(__file__), "--child",
-                   "--steps", "2", "--warmup", "1", "--no-cpu", "--grid", *map(str, args.grid)]
-            r = subprocess.run(cmd, stdout=subprocess.DEVNULL, stderr=subprocess.PIPE, timeout=240)
+                   "--workload", args.workload, "--steps", "2", "--warmup", "1", "--no-cpu",
+                   "--grid", *map(str, args.grid)]
+            r = subprocess.run(cmd, stdout=subprocess.DEVNULL, stderr=subprocess.PIPE, timeout=300)
             if r.returncode:
                 return None, f"rocprofv3 --pmc {ctr} rc={r.returncode}: {r.stderr.decode()[-200:]}"
             files = glob.glob(os.path.join(d, "**", "*counter_collection.csv"), recursive=True)
             v = [float(row["Counter_Value"]) for f in files for row in csv.DictReader(open(f))
-                 if KERNEL in row["Kernel_Name"] and row["Counter_Name"] == ctr]
+                 if kernel in row["Kernel_Name"] and row["Counter_Name"] == ctr]
             if not v:
-                return None, f"no {ctr} samples for {KERNEL}"
+                return None, f"no {ctr} samples for {kernel}"
             vals[ctr] = sum(v) / len(v)
     except Exception as e:  # noqa: BLE001 - report, never fail the bench line on the profiler
         return None, f"pmc pass failed: {e}"
@@ -206,40 +411,8 @@ def pmc_traffic(args):
         shutil.rmtree(tmp, ignore_errors=True)
     fetch = vals["FETCH_SIZE"] * 1024 * 2
     write = vals["WRITE_SIZE"] * 1024
-    return {"bytes": int(fetch + write), "fetch_bytes": int(fetch), "write_bytes": int(write)}, None
-
-
-def cpu_baseline(args):
-    """Oracle (oracle/, C restatement of zarrs' per-chunk pipeline) on host cores, bounded sample."""
-    sys.path.insert(0, os.path.join(ROOT, "oracle"))
-    import oracle as O
-    threads = int(os.environ.get("OMP_NUM_THREADS", "0") or 0) or os.cpu_count() or 1
-    g = args.cpu_grid
-    shape = [x * CHUNK for x in g]
-    n = g[0] * g[1] * g[2]
-    rng = np.random.default_rng(7)
-    dec = (rng.random(shape, dtype=np.float32) * 2 - 1)
-    # encode exactly as the GPU workload: transpose [2,1,0] + big endian, chunk-major
-    enc = np.ascontiguousarray(dec.reshape(g[0], CHUNK, g[1], CHUNK, g[2], CHUNK)
-                               .transpose(0, 2, 4, 5, 3, 1)).astype(">f4")
-    enc = enc.reshape(n, -1)
-    chain = O.OracleChain.from_metadata(CODECS, "float32", 0.0, 3)
-    ptrs = (C.c_void_p * n)(*[enc[c].ctypes.data for c in range(n)])
-    lens = (C.c_uint64 * n)(*([CHUNK ** 3 * 4] * n))
-    out = np.empty(shape, np.float32)
-    O.retrieve_ptrs(chain, shape, [CHUNK] * 3, ptrs, lens, [0, 0, 0], shape, out, threads)  # warm-up
-    assert np.array_equal(out, dec)
-    times = []
-    t_end = time.perf_counter() + args.cpu_seconds
-    while len(times) < 5 or (time.perf_counter() < t_end and len(times) < 50):
-        t0 = time.perf_counter()
-        O.retrieve_ptrs(chain, shape, [CHUNK] * 3, ptrs, lens, [0, 0, 0], shape, out, threads)
-        times.append(time.perf_counter() - t0)
-    t = float(np.median(times))
-    return {"value": round(n * CHUNK ** 3 * 4 / t / 2 ** 30, 3), "unit": "GiB/s", "cores": threads,
-            "kind": "port",
-            "sample": f"{n} of the 4096 chunks ({shape[0]}x{shape[1]}x{shape[2]} f32 subset), "
-                      f"median of {len(times)} reps, oracle retrieve_array_subset with {threads} threads"}
+    return {"bytes": int(fetch + write), "fetch_bytes": int(fetch), "write_bytes": int(write),
+            "source": "rocprofv3 --pmc FETCH_SIZE / WRITE_SIZE passes (KiB; FETCH x2 on gfx950)"}, None
 
 
 def main():
@@ -247,8 +420,9 @@ def main():
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=20)
     ap.add_argument("--warmup", type=int, default=3)
-    ap.add_argument("--grid", type=int, nargs=3, default=[16, 16, 16], help="chunk grid per GPU")
-    ap.add_argument("--cpu-grid", type=int, nargs=3, default=[8, 8, 8], help="CPU baseline sample grid")
+    ap.add_argument("--workload", choices=sorted(WORKLOADS), default="c2")
+    ap.add_argument("--grid", type=int, nargs=3, default=[16, 16, 16], help="C2 chunk grid per GPU")
+    ap.add_argument("--cpu-grid", type=int, nargs=3, default=[8, 8, 8], help="C2 CPU baseline sample grid")
     ap.add_argument("--cpu-seconds", type=float, default=15.0)
     ap.add_argument("--no-cpu", action="store_true")
     ap.add_argument("--no-pmc", action="store_true", help="skip the rocprofv3 PMC traffic passes")
@@ -268,37 +442,30 @@ def main():
     r = run_gpu(args, rank, world, dev)
     if args.child:
         return
-
+    W = r["W"]
     elapsed = torch.tensor([r["elapsed"]], dtype=torch.float64, device=dev)
     ok = torch.tensor([1 if r["ok"] else 0], dtype=torch.int32, device=dev)
     if world > 1:
         torch.distributed.all_reduce(elapsed, op=torch.distributed.ReduceOp.MAX)
         torch.distributed.all_reduce(ok, op=torch.distributed.ReduceOp.MIN)
     t = float(elapsed.item())
-    total_bytes = r["decoded_bytes"] * world * args.steps
-    value = total_bytes / t / 2 ** 30
-    cpu = None
-    if rank == 0 and not args.no_cpu:
-        cpu = cpu_baseline(args)
+    value = W.decoded_bytes * world * args.steps / t / 2 ** 30
+    cpu = W.cpu_baseline() if (rank == 0 and not args.no_cpu) else None
     traffic, traffic_note = None, "skipped (--no-pmc or N>1)"
     if rank == 0 and world == 1 and not args.no_pmc:
-        traffic, traffic_note = pmc_traffic(args)
+        traffic, traffic_note = pmc_traffic(args, W.kernel)
     if rank == 0:
         achieved = r["alg_bytes"] / (r["ev_ms"] * 1e-3) / 1e9
         line = {
             "metric": METRIC, "value": round(value, 2), "unit": "GiB/s", "n_gpus": world,
             "steps": args.steps, "warmup": args.warmup, "ms_per_step": round(t / args.steps * 1e3, 4),
-            "higher_is_better": True, "scaling": "weak", "vs_baseline": None, "dtype": "f32",
-            "data": "synthetic (uniform [-1,1) f32, encoded on device; decode(encode(x)) == x checked)",
-            "config": {"workload": "C2: 4096 independent 64^3 f32 chunks per GPU, "
-                                   "[transpose{order:[2,1,0]}, bytes{endian:big}], device-resident",
-                       "chunks_per_gpu": r["n_chunks"], "array_shape_per_gpu": [g * CHUNK for g in args.grid],
-                       "parallelism": f"chunk-partitioned x{world}"},
+            "higher_is_better": True, "scaling": W.scaling, "vs_baseline": None, "dtype": W.dtype,
+            "data": W.data, "config": W.config,
             "roofline": {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS,
                          "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBS, 4),
                          "traffic": traffic["bytes"] if traffic else None,
                          "traffic_detail": traffic or traffic_note,
-                         "kernel": "k_scatter_tiled<4>",
+                         "kernel": W.kernel,
                          "alg_bytes_per_launch": r["alg_bytes"],
                          "avg_launch_ms_hip_events": round(r["ev_ms"], 4)},
             "cpu_baseline": cpu,

@@ -28,11 +28,34 @@
 
 namespace zgpu {
 
+#ifdef ZG_PROFILE
+// lab builds only (tools/lab): per-phase shader-clock totals, summed over waves
+__device__ unsigned long long g_prof[8];
+// per-wave accumulators (prof_acc[], declared by PROF_DECL), flushed once per wave by PROF_FLUSH
+#define PROF_DECL uint64_t prof_acc[5] = {0, 0, 0, 0, 0}
+#define PROF_T(v) const uint64_t v = clock64()
+#define PROF_ADD(slot, t0) prof_acc[slot] += clock64() - (t0)
+#define PROF_FLUSH do { if (__lane_id() == 0) for (int k_ = 0; k_ < 5; k_++) atomicAdd(&g_prof[k_], (unsigned long long)prof_acc[k_]); } while (0)
+#else
+#define PROF_DECL
+#define PROF_FLUSH
+#define PROF_T(v)
+#define PROF_ADD(slot, t0)
+#endif
+
 namespace {
 
-constexpr int RING = 16384;  // LDS ring of recent output (power of two)
+#ifndef ZG_INFLATE_RING
+#define ZG_INFLATE_RING 4096
+#endif
+// LDS ring of recent output (power of two). Small on purpose: LDS per wave sets how many streams a
+// CU decodes at once, and sources older than the ring are read back from the flushed output.
+constexpr int RING = ZG_INFLATE_RING;
 constexpr int RMASK = RING - 1;
-constexpr int BATCH_CAP = 4096;  // max output bytes decoded into one batch (<= RING/2)
+constexpr int BATCH_CAP = RING / 2;  // max output bytes decoded into one batch
+constexpr int FLUSH_MIN = RING / 4;  // flush the ring to the slot once this many bytes are pending
+// unflushed bytes stay below FLUSH_MIN + BATCH_CAP + 258 < RING: every source older than the ring
+// has been flushed
 constexpr int LROOT = 10, DROOT = 8;
 
 // table entry: bits 0-3 code length (0 = longer than the root: slow path), 4-5 kind,
@@ -71,6 +94,10 @@ struct Smem {
 };
 
 __device__ __forceinline__ uint32_t U(uint32_t x) { return __builtin_amdgcn_readfirstlane(x); }
+// lane k of v := x (x, k uniform)
+__device__ __forceinline__ uint32_t put_lane(uint32_t v, uint32_t x, uint32_t k) {
+  return __lane_id() == (int)k ? x : v;
+}
 __device__ __forceinline__ int lane_id() { return __lane_id(); }
 
 // ---------------------------------------------------------------------------------------------
@@ -115,16 +142,49 @@ __device__ __forceinline__ void bits_seek(Bits &B, uint64_t bitpos) {
   B.consumed += skip;
 }
 
+// Move the window pair forward until word w is in the first window.
+__device__ __forceinline__ void bits_advance_to(Bits &B, uint32_t w) {
+  while ((int32_t)(w - B.wcur) >= 64) {  // forward only
+    B.wcur += 64;
+    B.win0 = B.win1;
+    B.win1 = load_word(B, B.wcur + 64 + lane_id());
+  }
+}
+
+// word wcur + k (k < 128) of the window pair, as a uniform value
+__device__ __forceinline__ uint32_t win_word(const Bits &B, uint32_t k) {
+  return k < 64 ? U(__builtin_amdgcn_readlane(B.win0, (int)k)) : U(__builtin_amdgcn_readlane(B.win1, (int)(k - 64)));
+}
+
+// The four aligned words w..w+3 (128 bits) as uniform values.
+__device__ __forceinline__ void bits_words(Bits &B, uint32_t w, uint32_t &W0, uint32_t &W1, uint32_t &W2,
+                                           uint32_t &W3) {
+  bits_advance_to(B, w);
+  const uint32_t k = w - B.wcur;
+  W0 = win_word(B, k);
+  W1 = win_word(B, k + 1);
+  W2 = win_word(B, k + 2);
+  W3 = win_word(B, k + 3);
+}
+
+// Re-position the reader at an absolute (forward) bit offset without reloading the windows.
+__device__ __forceinline__ void bits_seek_in(Bits &B, uint64_t bitpos) {
+  const uint32_t w = (uint32_t)(bitpos >> 5);
+  bits_advance_to(B, w);
+  const uint32_t k = w - B.wcur;
+  const uint32_t a = win_word(B, k), b = win_word(B, k + 1);
+  const uint32_t sk = (uint32_t)(bitpos & 31);
+  B.bb = (((uint64_t)b << 32) | a) >> sk;
+  B.nb = 64 - sk;
+  B.wnext = w + 2;
+  B.consumed = bitpos;
+}
+
 __device__ __forceinline__ void bits_refill(Bits &B) {
   if (B.nb <= 32) {
-    uint32_t idx = B.wnext - B.wcur;
-    if (idx >= 64) {  // advance the window pair; keep one window of lookahead in flight
-      B.wcur += 64;
-      B.win0 = B.win1;
-      B.win1 = load_word(B, B.wcur + 64 + lane_id());
-      idx -= 64;
-    }
-    const uint32_t word = U(__builtin_amdgcn_readlane(B.win0, (int)idx));
+    // windows only ever advance past words already consumed (the walk re-reads from `consumed`)
+    bits_advance_to(B, (uint32_t)(B.consumed >> 5));
+    const uint32_t word = win_word(B, B.wnext - B.wcur);  // wnext <= consumed word + 3: < 128
     B.bb |= (uint64_t)word << B.nb;
     B.nb += 32;
     B.wnext++;
@@ -318,6 +378,8 @@ __device__ __forceinline__ void flush(const Smem &S, uint8_t *out, uint64_t cap,
 __global__ __launch_bounds__(64) void k_gzip(ZgItem *items, uint32_t *status, uint8_t *dst, uint64_t slot_bytes,
                                              uint2 *aux) {
   __shared__ Smem S;
+  PROF_DECL;
+  PROF_T(t_all);
   const uint32_t item = blockIdx.x;
   const ZgItem it = items[item];
   if (status[item] || (it.flags & ZG_ITEM_FILL)) return;
@@ -369,6 +431,7 @@ __global__ __launch_bounds__(64) void k_gzip(ZgItem *items, uint32_t *status, ui
   uint64_t flushed = 0;    // output bytes flushed to the slot
   bool last = false;
   while (!last && !err) {
+    PROF_T(t_hdr);
     bits_refill(B);
     last = bits_get(B, 1);
     const uint32_t type = bits_get(B, 2);
@@ -453,90 +516,184 @@ __global__ __launch_bounds__(64) void k_gzip(ZgItem *items, uint32_t *status, ui
     }
     if (!build_table(S.lens, 288, LROOT, S.ltab, S.lsorted, S.lm, 0, S.tmp)) { err = ZG_CORRUPT_STREAM; break; }
     if (!build_table(S.lens + 288, 32, DROOT, S.dtab, S.dsorted, S.dm, 1, S.tmp)) { err = ZG_CORRUPT_STREAM; break; }
+    PROF_ADD(0, t_hdr);
     (void)hlit;
     (void)hdist;
 
     // ---- symbol batches ----
     bool eob = false;
     while (!eob && !err) {
-      uint32_t rec = 0;  // this lane's symbol: literal byte, or (1<<31)|(dist<<9)|len
+      PROF_T(t_dec);
+      uint32_t rec = 0;  // lane k's symbol: literal byte, or (1<<31)|(dist<<9)|len
       uint32_t cnt = 0, bytes = 0;
-      while (cnt < 64 && bytes < BATCH_CAP) {
-        const uint32_t e = decode_sym(B, S.ltab, LROOT, S.lsorted, S.lm, 0);
-        const uint32_t kind = (e >> 4) & 3;
-        if (kind == K_LIT) {
-          if (lane == (int)cnt) rec = e >> 16;
+      uint64_t bp = B.consumed;  // absolute bit position of the next symbol
+      while (cnt < 64 && bytes < BATCH_CAP && !eob && !err) {
+        // Lane-parallel lookahead: lane l looks both tables up at bit bp + l, so one LDS round trip
+        // serves every symbol that starts inside the next 64 bits; a scalar walk then chains them
+        // (readlane at the running offset) until a symbol no longer fits the window.
+        uint32_t W0, W1, W2, W3;
+        bits_words(B, (uint32_t)(bp >> 5), W0, W1, W2, W3);
+        const uint32_t bit = (uint32_t)(bp & 31) + (uint32_t)lane;
+        const uint32_t wi = bit >> 5;
+        const uint32_t lo = wi == 0 ? W0 : (wi == 1 ? W1 : W2);
+        const uint32_t hi = wi == 0 ? W1 : (wi == 1 ? W2 : W3);
+        const uint32_t V = __builtin_amdgcn_alignbit(hi, lo, bit & 31);
+        const uint32_t E = S.ltab[V & ((1u << LROOT) - 1)];
+        const uint32_t D = S.dtab[V & ((1u << DROOT) - 1)];
+        uint32_t o = 0;
+        bool slow = false;
+        while (cnt < 64 && bytes < BATCH_CAP) {
+          const uint32_t e = __builtin_amdgcn_readlane(E, o);
+          const uint32_t L = e & 15;
+          if (L == 0) { slow = true; break; }  // code longer than the root table
+          const uint32_t kind = (e >> 4) & 3;
+          if (kind == K_LIT) {
+            rec = put_lane(rec, e >> 16, cnt);
+            cnt++;
+            bytes++;
+            o += L;
+            if (o > 63) break;
+            continue;
+          }
+          if (kind == K_EOB) { o += L; eob = true; break; }
+          if (kind == K_BAD) { err = ZG_CORRUPT_STREAM; break; }
+          const uint32_t lx = (e >> 6) & 15;
+          const uint32_t o1 = o + L, o2 = o1 + lx;
+          if (o2 > 63) break;  // the distance code starts beyond the window: next window
+          const uint32_t len = (e >> 16) + (__builtin_amdgcn_readlane(V, o1) & ((1u << lx) - 1));
+          const uint32_t de = __builtin_amdgcn_readlane(D, o2);
+          const uint32_t DL = de & 15;
+          if (DL == 0) { slow = true; break; }
+          if (((de >> 4) & 3) != K_LEN) { err = ZG_CORRUPT_STREAM; break; }
+          const uint32_t dx = (de >> 6) & 15, o3 = o2 + DL;
+          if (o3 > 63) break;
+          const uint32_t dist = (de >> 16) + (__builtin_amdgcn_readlane(V, o3) & ((1u << dx) - 1));
+          if (dist > pos + bytes) { err = ZG_CORRUPT_STREAM; break; }  // distance too far back
+          rec = put_lane(rec, 0x80000000u | (dist << 9) | len, cnt);
           cnt++;
-          bytes++;
-          continue;
+          bytes += len;
+          o = o3 + dx;
+          if (o > 63) break;
         }
-        if (kind == K_EOB) { eob = true; break; }
-        if (kind == K_BAD) { err = ZG_CORRUPT_STREAM; break; }
-        bits_refill(B);
-        const uint32_t lx = (e >> 6) & 15;
-        const uint32_t len = (e >> 16) + bits_peek(B, lx);
-        bits_drop(B, lx);
-        const uint32_t de = decode_sym(B, S.dtab, DROOT, S.dsorted, S.dm, 1);
-        if (((de >> 4) & 3) != K_LEN) { err = ZG_CORRUPT_STREAM; break; }
-        bits_refill(B);
-        const uint32_t dx = (de >> 6) & 15;
-        const uint32_t dist = (de >> 16) + bits_peek(B, dx);
-        bits_drop(B, dx);
-        if (dist > pos + bytes) { err = ZG_CORRUPT_STREAM; break; }  // distance too far back
-        if (lane == (int)cnt) rec = 0x80000000u | (dist << 9) | len;
-        cnt++;
-        bytes += len;
+        bp += o;
+        if (slow && !err && cnt < 64 && bytes < BATCH_CAP) {
+          // one symbol through the canonical slow path (codes longer than the root)
+          bits_seek_in(B, bp);
+          const uint32_t e = decode_sym(B, S.ltab, LROOT, S.lsorted, S.lm, 0);
+          const uint32_t kind = (e >> 4) & 3;
+          if (kind == K_LIT) {
+            rec = put_lane(rec, e >> 16, cnt);
+            cnt++;
+            bytes++;
+          } else if (kind == K_EOB) {
+            eob = true;
+          } else if (kind == K_BAD) {
+            err = ZG_CORRUPT_STREAM;
+          } else {
+            bits_refill(B);
+            const uint32_t lx = (e >> 6) & 15;
+            const uint32_t len = (e >> 16) + bits_peek(B, lx);
+            bits_drop(B, lx);
+            const uint32_t de = decode_sym(B, S.dtab, DROOT, S.dsorted, S.dm, 1);
+            if (((de >> 4) & 3) != K_LEN) {
+              err = ZG_CORRUPT_STREAM;
+            } else {
+              bits_refill(B);
+              const uint32_t dx = (de >> 6) & 15;
+              const uint32_t dist = (de >> 16) + bits_peek(B, dx);
+              bits_drop(B, dx);
+              if (dist > pos + bytes) err = ZG_CORRUPT_STREAM;
+              rec = put_lane(rec, 0x80000000u | (dist << 9) | len, cnt);
+              cnt++;
+              bytes += len;
+            }
+          }
+          bp = B.consumed;
+        }
+        if (bp > end_bits) err = ZG_CORRUPT_STREAM;  // ran past the input
       }
-      if (B.consumed > end_bits) err = ZG_CORRUPT_STREAM;  // ran past the input
+      bits_seek_in(B, bp);
       if (err) break;
       if (pos + bytes > cap) { err = ZG_DECODED_SIZE_MISMATCH; break; }
       // ---- execute the batch ----
+      PROF_ADD(1, t_dec);
+      PROF_T(t_exe);
       const bool mine = lane < (int)cnt;
       const bool is_match = mine && (rec >> 31);
-      uint32_t ln = mine ? (is_match ? (rec & 511) : 1u) : 0u;
-      // inclusive wave scan of lengths
-      uint32_t inc = ln;
-      for (int o = 1; o < 64; o <<= 1) {
-        const uint32_t t = __shfl_up(inc, o, 64);
-        if (lane >= o) inc += t;
+      const uint32_t ln = mine ? (is_match ? (rec & 511) : 1u) : 0u;
+      uint32_t inc = ln;  // inclusive wave scan of output lengths
+      for (int off = 1; off < 64; off <<= 1) {
+        const uint32_t t = __shfl_up(inc, off, 64);
+        if (lane >= off) inc += t;
       }
       const uint64_t mypos = pos + inc - ln;
       if (mine && !is_match) S.ring[mypos & RMASK] = (uint8_t)rec;
       const uint64_t batch_end = pos + bytes;
-      uint64_t mm = __ballot(is_match);
-      bool need_global = false;
-      {
-        // any source older than batch_end - RING must be read from the flushed slot
-        const uint32_t d = (rec >> 9) & 0xFFFF;
-        need_global = __ballot(is_match && mypos - d + RING < batch_end) != 0;
-      }
-      if (need_global) __threadfence_block();  // earlier flushes visible to this wave's loads
-      while (mm) {
-        const int j = __builtin_ctzll(mm);
-        mm &= mm - 1;
-        const uint32_t r = U(__builtin_amdgcn_readlane(rec, j));
-        const uint64_t p = ((uint64_t)U(__builtin_amdgcn_readlane((uint32_t)mypos, j))) |
-                           ((uint64_t)U(__builtin_amdgcn_readlane((uint32_t)(mypos >> 32), j)) << 32);
-        const uint32_t len = r & 511, d = (r >> 9) & 0xFFFF;
-        const float inv = 1.0f / (float)d;
-        for (uint32_t i = lane; i < len; i += 64) {
-          uint32_t q = (uint32_t)((float)i * inv);
-          int32_t rm = (int32_t)i - (int32_t)(q * d);
-          if (rm < 0) rm += d;
-          if (rm >= (int32_t)d) rm -= d;
-          const uint64_t src = p - d + (uint32_t)rm;
-          uint8_t v;
-          if (src + RING >= batch_end) v = S.ring[src & RMASK];
-          else v = __builtin_nontemporal_load(out + src);  // nt: bypass a possibly stale L1 line
-          S.ring[(p + i) & RMASK] = v;
+      const uint32_t mlen = rec & 511, md = (rec >> 9) & 0xFFFF;
+      const uint64_t msrc = mypos - md;
+      // sources older than the ring are read back from the flushed output
+      if (__ballot(is_match && msrc + RING < batch_end)) __threadfence_block();
+      // Matches resolve in rounds: every pending match whose source lies entirely before the first
+      // pending match (or that IS the first one) copies its bytes itself; dest byte i takes source
+      // byte msrc + (i mod d), which is always final, so a lane's copy has no inner dependency.
+      bool pending = is_match;
+      uint64_t pm;
+      while ((pm = __ballot(pending)) != 0) {
+        const int first = __builtin_ctzll(pm);
+        const uint32_t F_lo = __builtin_amdgcn_readlane((uint32_t)mypos, first);
+        const uint32_t F_hi = __builtin_amdgcn_readlane((uint32_t)(mypos >> 32), first);
+        const uint64_t F = ((uint64_t)F_hi << 32) | F_lo;
+        const uint32_t flen = __builtin_amdgcn_readlane(mlen, first);
+        if (flen > 32) {  // a long match: copied by the whole wave once it is the first pending
+          const uint32_t fd = __builtin_amdgcn_readlane(md, first);
+          const float inv = 1.0f / (float)fd;
+          for (uint32_t i = lane; i < flen; i += 64) {
+            uint32_t q = (uint32_t)((float)i * inv);
+            int32_t rm = (int32_t)i - (int32_t)(q * fd);
+            if (rm < 0) rm += fd;
+            if (rm >= (int32_t)fd) rm -= fd;
+            const uint64_t src = F - fd + (uint32_t)rm;
+            const uint8_t v = (src + RING >= batch_end) ? S.ring[src & RMASK] : __builtin_nontemporal_load(out + src);
+            S.ring[(F + i) & RMASK] = v;
+          }
+          if (lane == first) pending = false;
+          continue;
+        }
+        const bool ready = pending && mlen <= 32 && (lane == first || msrc + mlen <= F);
+        if (ready) {
+          const bool in_ring = msrc + RING >= batch_end;
+          for (uint32_t i0 = 0; i0 < mlen; i0 += 4) {
+            uint8_t v[4];
+#pragma unroll
+            for (int k = 0; k < 4; k++) {
+              const uint32_t i = i0 + k;
+              const uint32_t r = i < md ? i : i % md;
+              const uint64_t src = msrc + r;
+              v[k] = (i < mlen) ? (in_ring ? S.ring[src & RMASK] : __builtin_nontemporal_load(out + src)) : 0;
+            }
+#pragma unroll
+            for (int k = 0; k < 4; k++)
+              if (i0 + k < mlen) S.ring[(mypos + i0 + k) & RMASK] = v[k];
+          }
+          pending = false;
         }
       }
-      __syncthreads();
-      flush(S, out, cap, flushed, batch_end);
+      PROF_ADD(2, t_exe);
+      PROF_T(t_fl);
       pos = batch_end;
-      flushed = pos;
-      __syncthreads();
+      if (pos - flushed >= FLUSH_MIN) {
+        __syncthreads();
+        flush(S, out, cap, flushed, pos);
+        flushed = pos;
+        __syncthreads();
+      }
+      PROF_ADD(3, t_fl);
     }
+  }
+  if (!err && flushed < pos) {
+    __syncthreads();
+    flush(S, out, cap, flushed, pos);
+    flushed = pos;
   }
   if (!err) {
     // trailer: byte-align, CRC-32 then ISIZE (little endian)
@@ -559,6 +716,8 @@ __global__ __launch_bounds__(64) void k_gzip(ZgItem *items, uint32_t *status, ui
       items[item].len = pos;
     }
   }
+  PROF_ADD(4, t_all);
+  PROF_FLUSH;
 }
 
 hipError_t launch_gzip(ZgItem *items, uint32_t *status, uint32_t n_items, uint8_t *dst, uint64_t slot_bytes,
