@@ -198,13 +198,11 @@ class C3:
     def __init__(self, args, rank, world, dev):
         from zarrs_amd import CodecChain, make_desc
         self.args, self.rank, self.world, self.dev = args, rank, world, dev
+        from zarrs_amd.distributed import slab_partition
         S = self.SHARD
-        if self.SUB_SHAPE[0] % world:
-            raise ValueError("the subset's axis-0 extent must divide by the GPU count")
-        slab = self.SUB_SHAPE[0] // world
-        # this rank's slab of the subset (array coordinates)
-        self.start = [self.SUB_START[0] + rank * slab] + self.SUB_START[1:]
-        self.shape = [slab] + self.SUB_SHAPE[1:]
+        # this rank's axis-0 slab of the subset (array coordinates)
+        self.slabs = slab_partition(self.SUB_START, self.SUB_SHAPE, world)
+        self.start, self.shape = self.slabs[rank]
         syn = _synth()
         self.chain = CodecChain.from_metadata(self.CODECS, "float32", 0.0, args.ctx)
         lo = [s // S for s in self.start]
@@ -242,8 +240,6 @@ class C3:
         self.out_shape = self.shape
         self.decoded_bytes = int(np.prod(self.shape)) * 4  # per rank per step
         self.gathered = None
-        if world > 1 and rank == 0:
-            self.gathered = [torch.empty(self.shape, dtype=torch.float32, device=dev) for _ in range(world)]
         self.config = {"workload": "C3" + ("/C4" if world > 1 else "") +
                                    ": sharded [2048]^3 f32, 256^3 shards / 32^3 inner chunks, "
                                    "[bytes, gzip 1, crc32c] + [bytes, crc32c] index at end, read subset "
@@ -259,12 +255,13 @@ class C3:
 
     def after_decode(self):
         if self.world > 1:  # C4: the requested subset spans GPUs -> one gather to the root
-            torch.distributed.gather(self.out, self.gathered, dst=0)
+            from zarrs_amd.distributed import gather_slabs
+            self.gathered = gather_slabs(self.out, self.slabs, dst=0)
 
     def check(self) -> bool:
         ok = bool(torch.equal(self.out.view(torch.int32), self.expected.view(torch.int32)))
-        if self.gathered is not None:
-            ok = ok and bool(torch.equal(self.gathered[0], self.out))
+        if self.gathered is not None:  # rank 0 holds the whole subset: its first slab is its own
+            ok = ok and bool(torch.equal(self.gathered[:self.shape[0]], self.out))
         return ok
 
     def cpu_baseline(self):
