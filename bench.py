@@ -95,6 +95,8 @@ class C2:
         self.out = torch.empty(self.shape, dtype=torch.float32, device=dev)
         self.out_shape = self.shape
         self.decoded_bytes = self.n_chunks * self.chunk_bytes  # per rank per step
+        self.parts = [(self.chain, self.descs, self.out, self.out_shape)]
+        self.step_bytes = self.decoded_bytes * world  # all ranks, one step
         self.config = {"workload": "C2: 4096 independent 64^3 f32 chunks per GPU, "
                                    "[transpose{order:[2,1,0]}, bytes{endian:big}], device-resident",
                        "chunks_per_gpu": self.n_chunks, "array_shape_per_gpu": self.shape,
@@ -239,6 +241,8 @@ class C3:
         self.out = torch.empty(self.shape, dtype=torch.float32, device=dev)
         self.out_shape = self.shape
         self.decoded_bytes = int(np.prod(self.shape)) * 4  # per rank per step
+        self.parts = [(self.chain, self.descs, self.out, self.out_shape)]
+        self.step_bytes = int(np.prod(self.SUB_SHAPE)) * 4  # the whole subset, all ranks
         self.gathered = None
         self.config = {"workload": "C3" + ("/C4" if world > 1 else "") +
                                    ": sharded [2048]^3 f32, 256^3 shards / 32^3 inner chunks, "
@@ -293,7 +297,159 @@ class C3:
         return None
 
 
-WORKLOADS = {"c2": C2, "c3": C3}
+# ------------------------------------------------------------------------------------------------
+# C5
+# ------------------------------------------------------------------------------------------------
+class C5:
+    """OME-Zarr-style uint16 pyramid: five levels, each the 2x2x2 mean of the one
+    above, chunk shapes per level as listed there, [bytes, numcodecs.shuffle{2}, zstd{3}] chunks.
+    The y/x extents are divided by --c5-scale (default 4: L0 [512,1024,1024], 1 GiB) so the host can
+    generate and zstd-encode the pyramid in seconds; chunk shapes are unchanged. N GPUs: the chunks
+    of all levels are LPT-partitioned by encoded size (strong scaling, no collective)."""
+    L0 = [512, 4096, 4096]
+    CHUNKS = [[32, 512, 512], [64, 256, 256], [64, 128, 128], [64, 64, 64], [32, 64, 64]]
+    CODECS = [{"name": "bytes", "configuration": {"endian": "little"}},
+              {"name": "numcodecs.shuffle", "configuration": {"elementsize": 2}},
+              {"name": "zstd", "configuration": {"level": 3, "checksum": False}}]
+    kernel = "k_zstd"
+    dtype = "u16"
+
+    def __init__(self, args, rank, world, dev):
+        from zarrs_amd import CodecChain, make_desc
+        from zarrs_amd.distributed import lpt_partition
+        self.args, self.rank, self.world, self.dev = args, rank, world, dev
+        sc = args.c5_scale
+        shape0 = [self.L0[0], self.L0[1] // sc, self.L0[2] // sc]
+        syn = _synth()
+        syn.synth_c5_level0.argtypes = [C.c_uint64] * 3 + [C.c_int] + [C.c_void_p] * 5 + [C.c_uint64, C.c_void_p,
+                                                                                         C.c_int]
+        syn.synth_shuffle_zstd_chunks.argtypes = [C.c_void_p, C.c_uint64, C.c_void_p, C.c_void_p, C.c_uint64,
+                                                  C.c_int, C.c_int, C.c_int, C.c_void_p, C.c_void_p]
+        rng = np.random.default_rng(42)
+        nb = 64
+        cz = rng.uniform(0, shape0[0], nb).astype(np.float32)
+        cy = rng.uniform(0, shape0[1], nb).astype(np.float32)
+        cx = rng.uniform(0, shape0[2], nb).astype(np.float32)
+        sg = rng.uniform(4, 40, nb).astype(np.float32)
+        amp = rng.uniform(300, 4000, nb).astype(np.float32)
+        lvl = np.empty(shape0, np.uint16)
+        nt = _threads()
+        syn.synth_c5_level0(*shape0, nb, cz.ctypes.data, cy.ctypes.data, cx.ctypes.data, sg.ctypes.data,
+                            amp.ctypes.data, 42, lvl.ctypes.data, nt)
+        levels = [lvl]
+        for _ in range(4):  # 2x2x2 mean (rounded half up), the usual OME-Zarr downsampling
+            a = levels[-1].astype(np.uint32)
+            z, y, x = a.shape
+            m = a.reshape(z // 2, 2, y // 2, 2, x // 2, 2).sum(axis=(1, 3, 5))
+            levels.append(((m + 4) // 8).astype(np.uint16))
+        # every chunk of every level, zero-padded to the full chunk shape (zarrs writes edge chunks whole)
+        chunks = []  # (level, chunk index, decoded bytes)
+        for li, (a, cs) in enumerate(zip(levels, self.CHUNKS)):
+            grid = [-(-s // c) for s, c in zip(a.shape, cs)]
+            for idx in np.ndindex(*grid):
+                blk = np.zeros(cs, np.uint16)
+                sl = tuple(slice(i * c, min((i + 1) * c, s)) for i, c, s in zip(idx, cs, a.shape))
+                src = a[sl]
+                blk[tuple(slice(0, n) for n in src.shape)] = src
+                chunks.append((li, idx, blk))
+        n = len(chunks)
+        flat = np.concatenate([b.reshape(-1).view(np.uint8) for _, _, b in chunks])
+        offs = np.zeros(n, np.uint64)
+        lens = np.array([b.nbytes for _, _, b in chunks], np.uint64)
+        offs[1:] = np.cumsum(lens)[:-1]
+        outs = (C.c_void_p * n)()
+        olens = (C.c_uint64 * n)()
+        if syn.synth_shuffle_zstd_chunks(flat.ctypes.data, 2, offs.ctypes.data, lens.ctypes.data, n, 3, 0, nt,
+                                         outs, olens):
+            raise RuntimeError("zstd encode failed")
+        enc_sizes = [olens[i] for i in range(n)]
+        mine = lpt_partition(enc_sizes, world)[rank]
+        self.chain = CodecChain.from_metadata(self.CODECS, "uint16", 0, args.ctx)
+        self.outs = [torch.zeros(a.shape, dtype=torch.int16, device=dev) for a in levels]
+        self.expected = [torch.from_numpy(a.view(np.int16)).to(dev) for a in levels]
+        self.masks = [torch.zeros(a.shape, dtype=torch.bool, device=dev) for a in levels]
+        per_level = [[] for _ in levels]
+        # host copies of every encoded chunk (the CPU baseline decodes them all)
+        self.enc_host = [np.ctypeslib.as_array((C.c_uint8 * olens[i]).from_address(outs[i])).copy()
+                         for i in range(n)]
+        for i in range(n):
+            syn.synth_free(C.c_void_p(outs[i]))
+        mine = set(mine)
+        self.enc_bufs, enc_total, dec_total, all_bytes = [], 0, 0, 0
+        for i, (li, idx, blk) in enumerate(chunks):
+            cs, a = self.CHUNKS[li], levels[li]
+            start = [k * c for k, c in zip(idx, cs)]
+            sel = [min(c, s - st) for c, s, st in zip(cs, a.shape, start)]
+            all_bytes += int(np.prod(sel)) * 2
+            if i not in mine:
+                continue
+            t = torch.from_numpy(self.enc_host[i]).to(dev)
+            self.enc_bufs.append(t)
+            enc_total += olens[i]
+            dec_total += int(np.prod(sel)) * 2
+            per_level[li].append(make_desc((t.data_ptr(), olens[i]), cs, [0, 0, 0], sel, start))
+            self.masks[li][tuple(slice(st, st + n_) for st, n_ in zip(start, sel))] = True
+        self.parts = [(self.chain, d, o, list(o.shape)) for d, o in zip(per_level, self.outs)]
+        self.decoded_bytes = dec_total
+        self.step_bytes = all_bytes
+        self.ratio = sum(int(x) for x in lens) / max(1, sum(enc_sizes))
+        self.levels_host = levels
+        self.all_chunks = chunks
+        self.config = {"workload": f"C5: OME-Zarr-style u16 pyramid, 5 levels, L0 {shape0} (y/x scaled 1/{sc}), "
+                                   "chunks [32,512,512] [64,256,256] [64,128,128] [64,64,64] [32,64,64], "
+                                   "[bytes, numcodecs.shuffle{2}, zstd{3}]",
+                       "chunks_total": n, "chunks_this_gpu": len(mine), "zstd_ratio": round(self.ratio, 3),
+                       "encoded_bytes_this_gpu": enc_total,
+                       "parallelism": f"LPT chunk partition x{world}"}
+        self.data = ("synthetic (background 100 + 64 Gaussian blobs amplitude <= 4000 + sqrt(mean)*N(0,1) noise, "
+                     "u16, seed 42; 2x2x2 mean pyramid; decode(encode(x)) == x checked on device)")
+        self.scaling = "strong"
+
+    def after_decode(self):
+        pass
+
+    def check(self) -> bool:
+        ok = True
+        for o, e, m in zip(self.outs, self.expected, self.masks):
+            ok = ok and bool(torch.equal(o[m], e[m]))
+        return ok
+
+    def cpu_baseline(self):
+        sys.path.insert(0, os.path.join(ROOT, "oracle"))
+        import oracle as O
+        threads = _threads()
+        chain = O.OracleChain.from_metadata(self.CODECS, "uint16", 0, 3)
+        # sample: all levels' chunks through the oracle's retrieve (chunk-parallel, libzstd)
+        tables = []
+        for li, (a, cs) in enumerate(zip(self.levels_host, self.CHUNKS)):
+            grid = [-(-s // c) for s, c in zip(a.shape, cs)]
+            ptrs = (C.c_void_p * int(np.prod(grid)))()
+            lens = (C.c_uint64 * int(np.prod(grid)))()
+            tables.append((li, a.shape, cs, ptrs, lens))
+        for i, (li, idx, blk) in enumerate(self.all_chunks):
+            _, shp, cs, ptrs, lens = tables[li]
+            grid = [-(-s // c) for s, c in zip(shp, cs)]
+            lin = int(np.ravel_multi_index(idx, grid))
+            ptrs[lin] = self.enc_host[i].ctypes.data
+            lens[lin] = self.enc_host[i].nbytes
+        outs_np = [np.empty(a.shape, np.uint16) for a in self.levels_host]
+
+        def run():
+            for (li, shp, cs, ptrs, lens), o in zip(tables, outs_np):
+                O.retrieve_ptrs(chain, list(shp), cs, ptrs, lens, [0, 0, 0], list(shp), o, threads)
+        run()
+        assert all(np.array_equal(o, a) for o, a in zip(outs_np, self.levels_host))
+        times = _time_reps(run, self.args.cpu_seconds)
+        t = float(np.median(times))
+        return {"value": round(self.step_bytes / t / 2 ** 30, 3), "unit": "GiB/s", "cores": threads, "kind": "port",
+                "sample": f"the whole pyramid ({len(self.all_chunks)} chunks), median of {len(times)} reps, "
+                          f"oracle retrieve_array_subset per level (libzstd) with {threads} threads"}
+
+    def host_leg(self, sp):
+        return None
+
+
+WORKLOADS = {"c2": C2, "c3": C3, "c5": C5}
 
 
 def _time_reps(fn, seconds):
@@ -312,20 +468,25 @@ def run_gpu(args, rank, world, dev):
     from zarrs_amd import _lib as L
     args.ctx = Context(dev.index)
     W = WORKLOADS[args.workload](args, rank, world, dev)
-    n = len(W.descs)
-    arr = (L.ChunkDesc * n)(*W.descs)
-    plan = C.c_void_p()
     lib = L.load()
-    L.check(lib.zgpu_plan_create(W.chain._h, 3, arr, n, L.u64s(W.out_shape), L.ENC_DEVICE | L.OUT_DEVICE,
-                                 C.byref(plan)))
-    status = (C.c_int32 * n)()
+    plans = []  # one prepared plan per part (e.g. per pyramid level: one chunk shape per plan)
+    for chain, descs, out, out_shape in W.parts:
+        n = len(descs)
+        if not n:
+            continue
+        arr = (L.ChunkDesc * n)(*descs)
+        plan = C.c_void_p()
+        L.check(lib.zgpu_plan_create(chain._h, len(out_shape), arr, n, L.u64s(out_shape),
+                                     L.ENC_DEVICE | L.OUT_DEVICE, C.byref(plan)))
+        plans.append((plan, out, (C.c_int32 * n)()))
     stream = torch.cuda.Stream(dev)  # the library launches on this stream; events are recorded on it
     sp = C.c_void_p(stream.cuda_stream)
 
     def step():
-        rc = lib.zgpu_plan_execute(plan, W.out.data_ptr(), status, sp)
-        if rc:
-            raise RuntimeError(f"decode failed: {L.STATUS_NAMES[rc]} {L.last_error()}")
+        for plan, out, status in plans:
+            rc = lib.zgpu_plan_execute(plan, out.data_ptr(), status, sp)
+            if rc:
+                raise RuntimeError(f"decode failed: {L.STATUS_NAMES[rc]} {L.last_error()}")
         W.after_decode()
 
     torch.cuda.synchronize()
@@ -344,7 +505,8 @@ def run_gpu(args, rank, world, dev):
         torch.distributed.barrier()
     elapsed = time.perf_counter() - t0
     if args.child:  # rocprofv3 --pmc pass: only the dispatches matter
-        lib.zgpu_plan_destroy(plan)
+        for plan, _, _ in plans:
+            lib.zgpu_plan_destroy(plan)
         return None
     # Device time of one decode launch sequence, HIP events on the stream the library launches on;
     # enqueue-only executes (status=NULL), back to back.
@@ -352,21 +514,25 @@ def run_gpu(args, rank, world, dev):
     ev1 = torch.cuda.Event(enable_timing=True)
     ev0.record(stream)
     for _ in range(args.steps):
-        rc = lib.zgpu_plan_execute(plan, W.out.data_ptr(), None, sp)
-        if rc:
-            raise RuntimeError(f"decode failed: {L.STATUS_NAMES[rc]} {L.last_error()}")
+        for plan, out, _ in plans:
+            rc = lib.zgpu_plan_execute(plan, out.data_ptr(), None, sp)
+            if rc:
+                raise RuntimeError(f"decode failed: {L.STATUS_NAMES[rc]} {L.last_error()}")
     ev1.record(stream)
     torch.cuda.synchronize()
     ev_ms = ev0.elapsed_time(ev1) / args.steps
-    alg_bytes = lib.zgpu_plan_algorithmic_bytes(plan)
+    alg_bytes = sum(lib.zgpu_plan_algorithmic_bytes(plan) for plan, _, _ in plans)
     # host planning + upload included (zgpu_decode_batch form), for DESIGN.md
     t1 = time.perf_counter()
     reps = max(1, min(5, args.steps))
     for _ in range(reps):
-        W.chain.decode_batch(W.descs, W.out, W.out_shape, enc_device=True, stream=sp)
+        for chain, descs, out, out_shape in W.parts:
+            if descs:
+                chain.decode_batch(descs, out, out_shape, enc_device=True, stream=sp)
     torch.cuda.synchronize()
     batch_ms = (time.perf_counter() - t1) / reps * 1e3
-    lib.zgpu_plan_destroy(plan)
+    for plan, _, _ in plans:
+        lib.zgpu_plan_destroy(plan)
     host = W.host_leg(sp) if (args.host_leg and rank == 0) else None
     return dict(W=W, elapsed=elapsed, ev_ms=ev_ms, alg_bytes=alg_bytes, ok=ok, batch_ms=batch_ms, host=host)
 
@@ -421,6 +587,7 @@ def main():
     ap.add_argument("--grid", type=int, nargs=3, default=[16, 16, 16], help="C2 chunk grid per GPU")
     ap.add_argument("--cpu-grid", type=int, nargs=3, default=[8, 8, 8], help="C2 CPU baseline sample grid")
     ap.add_argument("--cpu-seconds", type=float, default=15.0)
+    ap.add_argument("--c5-scale", type=int, default=4, help="C5: divide the L0 y/x extents by this")
     ap.add_argument("--no-cpu", action="store_true")
     ap.add_argument("--no-pmc", action="store_true", help="skip the rocprofv3 PMC traffic passes")
     ap.add_argument("--no-host-leg", dest="host_leg", action="store_false",
@@ -446,7 +613,7 @@ def main():
         torch.distributed.all_reduce(elapsed, op=torch.distributed.ReduceOp.MAX)
         torch.distributed.all_reduce(ok, op=torch.distributed.ReduceOp.MIN)
     t = float(elapsed.item())
-    value = W.decoded_bytes * world * args.steps / t / 2 ** 30
+    value = W.step_bytes * args.steps / t / 2 ** 30
     cpu = W.cpu_baseline() if (rank == 0 and not args.no_cpu) else None
     traffic, traffic_note = None, "skipped (--no-pmc or N>1)"
     if rank == 0 and world == 1 and not args.no_pmc:

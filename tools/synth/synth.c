@@ -274,3 +274,67 @@ int synth_shuffle_zstd_chunks(const void *dec, uint64_t es, const uint64_t *offs
 }
 
 void synth_free(void *p) { free(p); }
+
+/* ---------------------------------------------------------------------------------------------
+ * C5: OME-Zarr-style uint16 level 0: background 100 + K Gaussian blobs (amplitude <= 4000) +
+ * noise ~ sqrt(mean) * N(0,1) (Poisson approximation), clipped to u16. Blobs are separable
+ * (gx[x] * gy[y] * gz[z]) and evaluated only inside their 4-sigma boxes.
+ * ------------------------------------------------------------------------------------------- */
+typedef struct {
+  uint64_t nz, ny, nx;
+  int nblobs;
+  const float *cz, *cy, *cx, *sg, *amp;
+  uint16_t *out;
+  int t, nt;
+  uint64_t seed;
+} c5_job;
+
+static void *c5_worker(void *arg) {
+  c5_job *J = (c5_job *)arg;
+  float *acc = (float *)malloc(J->nx * sizeof(float));
+  float *gy = (float *)malloc(J->nblobs * sizeof(float));
+  for (uint64_t z = J->t; z < J->nz; z += J->nt) {
+    for (uint64_t y = 0; y < J->ny; y++) {
+      for (uint64_t x = 0; x < J->nx; x++) acc[x] = 100.0f;
+      for (int b = 0; b < J->nblobs; b++) {
+        const float s = J->sg[b], dz = (float)z - J->cz[b], dy = (float)y - J->cy[b];
+        if (fabsf(dz) > 4 * s || fabsf(dy) > 4 * s) continue;
+        const float gzy = J->amp[b] * expf(-(dz * dz + dy * dy) / (2 * s * s));
+        long x0 = (long)(J->cx[b] - 4 * s), x1 = (long)(J->cx[b] + 4 * s) + 1;
+        if (x0 < 0) x0 = 0;
+        if (x1 > (long)J->nx) x1 = (long)J->nx;
+        for (long x = x0; x < x1; x++) {
+          const float dx = (float)x - J->cx[b];
+          acc[x] += gzy * expf(-dx * dx / (2 * s * s));
+        }
+      }
+      uint16_t *row = J->out + (z * J->ny + y) * J->nx;
+      for (uint64_t x = 0; x < J->nx; x++) {
+        const float m = acc[x];
+        float v = m + sqrtf(m) * hnorm(((z * J->ny + y) * J->nx + x) ^ J->seed);
+        v = rintf(v);
+        if (v < 0) v = 0;
+        if (v > 65535.0f) v = 65535.0f;
+        row[x] = (uint16_t)v;
+      }
+    }
+  }
+  free(acc);
+  free(gy);
+  return NULL;
+}
+
+/* blobs: nblobs entries of (cz, cy, cx, sigma, amplitude) each */
+void synth_c5_level0(uint64_t nz, uint64_t ny, uint64_t nx, int nblobs, const float *cz, const float *cy,
+                     const float *cx, const float *sg, const float *amp, uint64_t seed, uint16_t *out,
+                     int nthreads) {
+  if (nthreads < 1) nthreads = 1;
+  if (nthreads > 256) nthreads = 256;
+  pthread_t th[256];
+  c5_job jobs[256];
+  for (int t = 0; t < nthreads; t++) {
+    jobs[t] = (c5_job){nz, ny, nx, nblobs, cz, cy, cx, sg, amp, out, t, nthreads, seed};
+    pthread_create(&th[t], NULL, c5_worker, &jobs[t]);
+  }
+  for (int t = 0; t < nthreads; t++) pthread_join(th[t], NULL);
+}

@@ -25,6 +25,7 @@
 #include "chain.hpp"
 #include "common.hpp"
 #include "kernels/launch.hpp"
+#include "xfer.hpp"
 
 using namespace zgpu;
 
@@ -642,24 +643,51 @@ int zgpu_decode_batch(zgpu_chain *ch, uint32_t nd, const zgpu_chunk_desc *descs,
   std::vector<zgpu_chunk_desc> local;
   const zgpu_chunk_desc *dd = descs;
   uint8_t *enc_stage = nullptr;
-  if (!(flags & ZGPU_ENC_DEVICE)) {  // host inputs: one packed H2D copy through pinned staging
-    uint64_t total = 0;
-    for (uint64_t i = 0; i < n; i++)
-      if (descs[i].enc) total += (descs[i].enc_len + 255) & ~(uint64_t)255;
+  const uint64_t slab = 64ull << 20;
+  uint8_t *pin_stage = nullptr;  // 2 slabs of pinned staging, only for pageable host buffers
+  auto stage = [&]() {
+    if (!pin_stage) pin_stage = (uint8_t *)C->host_alloc(2 * slab);
+    return pin_stage;
+  };
+  if (!(flags & ZGPU_ENC_DEVICE)) {
+    // host inputs: chunks sorted by address, touching/overlapping ones merged into ranges; pinned
+    // ranges are DMA'd directly (one copy per range), pageable ones through the staging slabs
     local.assign(descs, descs + n);
+    std::vector<uint64_t> order;
+    for (uint64_t i = 0; i < n; i++)
+      if (descs[i].enc && descs[i].enc_len) order.push_back(i);
+    std::sort(order.begin(), order.end(),
+              [&](uint64_t a, uint64_t b) { return (uintptr_t)descs[a].enc < (uintptr_t)descs[b].enc; });
+    std::vector<HostRange> ranges;
+    std::vector<uint64_t> range_of(n, 0);
+    uint64_t total = 0;
+    for (uint64_t i : order) {
+      const uint8_t *p = (const uint8_t *)descs[i].enc;
+      if (!ranges.empty() && p <= ranges.back().src + ranges.back().len) {
+        HostRange &r = ranges.back();
+        const uint64_t end = std::max<uint64_t>((uint64_t)(p - r.src) + descs[i].enc_len, r.len);
+        total += end - r.len;
+        r.len = end;
+      } else {
+        total = (total + 255) & ~(uint64_t)255;
+        ranges.push_back(HostRange{p, descs[i].enc_len, total});
+        total += descs[i].enc_len;
+      }
+      range_of[i] = ranges.size() - 1;
+    }
     if (total) {
       enc_stage = (uint8_t *)C->dev_alloc(total);
-      uint8_t *pin = (uint8_t *)C->host_alloc(total);
-      uint64_t off = 0;
-      for (uint64_t i = 0; i < n; i++) {
-        if (!descs[i].enc) continue;
-        std::memcpy(pin + off, descs[i].enc, descs[i].enc_len);
-        local[i].enc = enc_stage + off;
-        off += (descs[i].enc_len + 255) & ~(uint64_t)255;
+      bool pinned = true;
+      for (const HostRange &r : ranges)
+        if (!host_is_pinned(r.src) || !host_is_pinned(r.src + r.len - 1)) {
+          pinned = false;
+          break;
+        }
+      HIPCHK(h2d_ranges(enc_stage, ranges, pinned, pinned ? nullptr : stage(), slab, host_copy_threads(), s));
+      for (uint64_t i : order) {
+        const HostRange &r = ranges[range_of[i]];
+        local[i].enc = enc_stage + r.dev_off + ((const uint8_t *)descs[i].enc - r.src);
       }
-      HIPCHK(hipMemcpyAsync(enc_stage, pin, total, hipMemcpyHostToDevice, s));
-      HIPCHK(hipStreamSynchronize(s));
-      C->host_free(pin);
     }
     dd = local.data();
   }
@@ -678,7 +706,8 @@ int zgpu_decode_batch(zgpu_chain *ch, uint32_t nd, const zgpu_chunk_desc *descs,
       for (uint32_t d = 0; d < nd; d++) v *= descs[i].sel_shape[d];
       covered += v;
     }
-    if (covered != out_elems) HIPCHK(hipMemcpyAsync(dout, out, out_bytes, hipMemcpyHostToDevice, s));
+    if (covered != out_elems)
+      HIPCHK(h2d_bytes(dout, (const uint8_t *)out, out_bytes, stage(), slab, host_copy_threads(), s));
   }
   std::unique_ptr<zgpu_plan> P;
   int rc = 0;
@@ -687,17 +716,16 @@ int zgpu_decode_batch(zgpu_chain *ch, uint32_t nd, const zgpu_chunk_desc *descs,
     plan_upload(*P);
     plan_enqueue(*P, dout, s);
     rc = plan_statuses(*P, status, s);
-    if (host_out) {
-      HIPCHK(hipMemcpyAsync(out, dout, out_bytes, hipMemcpyDeviceToHost, s));
-      HIPCHK(hipStreamSynchronize(s));
-    }
+    if (host_out) HIPCHK(d2h_bytes((uint8_t *)out, dout, out_bytes, stage(), slab, host_copy_threads(), s));
   } catch (...) {
     if (host_out) C->dev_free(dout);
     C->dev_free(enc_stage);
+    C->host_free(pin_stage);
     throw;
   }
   if (host_out) C->dev_free(dout);
   C->dev_free(enc_stage);
+  C->host_free(pin_stage);
   P.reset();
   if (rc) set_err(rc, zgpu_status_name(rc));
   return rc;
