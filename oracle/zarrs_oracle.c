@@ -417,6 +417,41 @@ static int decode_region(const orc_chain *c, const uint8_t *enc, uint64_t len, u
                          const uint64_t *sel_shape, int partial, int validate, uint8_t *out,
                          const uint64_t *out_shape, const uint64_t *out_start);
 
+/* Inner (codec) concurrency of the calling chunk task: zarrs splits its thread budget into outer
+ * (chunks) x inner (subchunks of a shard), concurrency.rs:23-69 / sharding_codec.rs:648-655. */
+static __thread int g_inner_threads = 1;
+
+typedef struct {
+  const orc_chain *ic;
+  const uint8_t *enc;
+  uint64_t len;
+  uint32_t nd;
+  const uint64_t *inner, *out_shape;
+  uint8_t *out;
+  int partial, validate;
+  uint64_t n;
+  const uint64_t *work;  /* per item: off, size, cst[nd], osh[nd], opos[nd] */
+  atomic_ullong next;
+  atomic_int err;
+} inner_job_t;
+
+static void *inner_worker(void *arg) {
+  inner_job_t *J = arg;
+  const uint32_t nd = J->nd, stride = 2 + 3 * nd;
+  for (;;) {
+    uint64_t t = atomic_fetch_add(&J->next, 1);
+    if (t >= J->n) break;
+    const uint64_t *w = J->work + t * stride;
+    int st = decode_region(J->ic, J->enc + w[0], w[1], nd, J->inner, w + 2, w + 2 + nd, J->partial, J->validate,
+                           J->out, J->out_shape, w + 2 + 2 * nd);
+    if (st) {
+      int z = 0;
+      atomic_compare_exchange_strong(&J->err, &z, st);
+    }
+  }
+  return NULL;
+}
+
 /* Shard decode into an output region. Full path: SC:617-707 (all subchunks, crc verified);
  * partial path: SP:311-400 (intersecting subchunks, inner partial decoders, crc stripped only).
  * Index: SH:178-194, SC:1262-1298 (index chain fully decoded, crc verified in both paths). */
@@ -447,6 +482,58 @@ static int shard_region(const orc_chain *c, const uint8_t *enc, uint64_t len, ui
     hi[d] = sel_shape[d] ? (sel_start[d] + sel_shape[d] - 1) / k->inner[d] + 1 : lo[d];
     if (hi[d] == lo[d]) { free(index); return ORC_OK; }
     idx[d] = lo[d];
+  }
+  if (g_inner_threads > 1) {
+    /* collect the intersecting subchunks, fill/validate serially, decode on inner threads */
+    const uint32_t stride = 2 + 3 * nd;
+    uint64_t cap = 1;
+    for (uint32_t d = 0; d < nd; d++) cap *= hi[d] - lo[d];
+    uint64_t *work = malloc(cap * stride * 8), nw = 0;
+    for (;;) {
+      uint64_t lin = 0, *w = work + nw * stride;
+      for (uint32_t d = 0; d < nd; d++) {
+        lin = lin * cps[d] + idx[d];
+        uint64_t cs = idx[d] * k->inner[d], ce = cs + k->inner[d];
+        uint64_t s0 = sel_start[d] > cs ? sel_start[d] : cs;
+        uint64_t s1 = sel_start[d] + sel_shape[d] < ce ? sel_start[d] + sel_shape[d] : ce;
+        w[2 + d] = s0 - cs;
+        w[2 + nd + d] = s1 - s0;
+        w[2 + 2 * nd + d] = out_start[d] + (s0 - sel_start[d]);
+      }
+      uint64_t off = index[2 * lin], size = index[2 * lin + 1];
+      if (off == UINT64_MAX && size == UINT64_MAX) {
+        fill_region(nd, c->es, c->fill, out, out_shape, w + 2 + 2 * nd, w + 2 + nd);
+      } else if (off > len || size > len - off) {
+        free(work);
+        free(index);
+        return ORC_SHARD_INDEX_OOB;
+      } else {
+        w[0] = off;
+        w[1] = size;
+        nw++;
+      }
+      int d = (int)nd - 1;
+      for (; d >= 0; d--) {
+        if (++idx[d] < hi[d]) break;
+        idx[d] = lo[d];
+      }
+      if (d < 0) break;
+    }
+    inner_job_t J;
+    memset(&J, 0, sizeof(J));
+    J.ic = k->inner_chain; J.enc = enc; J.len = len; J.nd = nd; J.inner = k->inner;
+    J.out_shape = out_shape; J.out = out; J.partial = partial; J.validate = validate; J.n = nw; J.work = work;
+    atomic_init(&J.next, 0);
+    atomic_init(&J.err, 0);
+    int nt = g_inner_threads < 64 ? g_inner_threads : 64;
+    if ((uint64_t)nt > nw) nt = nw ? (int)nw : 1;
+    pthread_t th[64];
+    for (int i = 1; i < nt; i++) pthread_create(&th[i], NULL, inner_worker, &J);
+    inner_worker(&J);
+    for (int i = 1; i < nt; i++) pthread_join(th[i], NULL);
+    free(work);
+    free(index);
+    return atomic_load(&J.err);
   }
   for (;;) {
     uint64_t lin = 0, cst[MAXD], ost[MAXD], osh[MAXD], opos[MAXD];
@@ -726,6 +813,7 @@ typedef struct {
   uint64_t lo[MAXD], hi[MAXD], ngrid[MAXD], n;
   atomic_ullong next;
   int *status;
+  int inner_threads;
 } job_t;
 
 /* RO:111-179 retrieve_chunk closure + RA:346-375 full-vs-partial branch */
@@ -760,6 +848,7 @@ static int do_chunk(job_t *j, uint64_t t) {
 
 static void *worker(void *arg) {
   job_t *j = arg;
+  g_inner_threads = j->inner_threads;
   for (;;) {
     uint64_t t = atomic_fetch_add(&j->next, 1);
     if (t >= j->n) break;
@@ -791,12 +880,16 @@ int orc_retrieve_array_subset(const orc_chain *c, uint32_t nd, const uint64_t *a
   atomic_init(&j->next, 0);
   j->status = calloc(j->n ? j->n : 1, sizeof(int));
   if (nthreads < 1) nthreads = 1;
+  /* outer x inner split of the thread budget (concurrency.rs:23-48) */
+  j->inner_threads = j->n ? nthreads / (int)((uint64_t)nthreads < j->n ? (uint64_t)nthreads : j->n) : 1;
+  if (j->inner_threads < 1) j->inner_threads = 1;
   if ((uint64_t)nthreads > j->n) nthreads = (int)(j->n ? j->n : 1);
   pthread_t th[256];
   if (nthreads > 256) nthreads = 256;
   for (int i = 1; i < nthreads; i++) pthread_create(&th[i], NULL, worker, j);
   worker(j);
   for (int i = 1; i < nthreads; i++) pthread_join(th[i], NULL);
+  g_inner_threads = 1;
   /* deterministic "first error" (try_for_each): the lowest chunk index wins */
   int st = ORC_OK;
   for (uint64_t t = 0; t < j->n && !st; t++) st = j->status[t];
