@@ -115,3 +115,83 @@ def test_zstd_batch_vs_libzstd(level):
     got = out.cpu().numpy().reshape(len(encs), n)
     for i, d in enumerate(data):
         assert np.array_equal(got[i], d), (i, kinds[i])
+
+
+def _zstd_batch(codecs, encs, n_each, nd_shape=None):
+    from zarrs_amd import CodecChain, Context, make_desc
+    import torch
+    blob = b"".join(encs)
+    dev = torch.frombuffer(bytearray(blob), dtype=torch.uint8).cuda()
+    descs, off = [], 0
+    for i, e in enumerate(encs):
+        descs.append(make_desc((dev.data_ptr() + off, len(e)), [n_each], out_start=[i * n_each]))
+        off += len(e)
+    ch = CodecChain.from_metadata(codecs, "uint8", 0, Context.default())
+    out = torch.zeros(len(encs) * n_each, dtype=torch.uint8, device="cuda")
+    try:
+        st = ch.decode_batch(descs, out, [len(encs) * n_each], enc_device=True)
+    except Exception as e:  # noqa: BLE001
+        return getattr(e, "status", -1), None
+    return st, out.cpu().numpy().reshape(len(encs), n_each)
+
+
+@pytest.mark.parametrize("level", [1, 3, 19])
+def test_zstd_multiblock_frames(level):
+    """MiB-sized frames: many blocks per frame, treeless literals and repeat-mode FSE tables that
+    the block-parallel path resolves to earlier blocks, repeat offsets across block boundaries."""
+    rng = np.random.default_rng(200 + level)
+    codecs = [BYTES_LE, {"name": "zstd", "configuration": {"level": level, "checksum": level != 1}}]
+    oc = O.OracleChain.from_metadata(codecs, "uint8", 0, 1)
+    n = 3 << 20
+    kinds = ["random", "text", "smooth", "runs", "far"]
+    data = [_content(rng, n, k) for k in kinds]
+    # C5-like: byte-shuffled u16 blobs + noise
+    z = np.arange(n // 2, dtype=np.float32)
+    u16 = np.clip(100 + 3000 * np.exp(-((z % 65536) - 30000) ** 2 / 2e7) + rng.normal(0, 10, n // 2), 0,
+                  65535).astype(np.uint16)
+    data.append(np.concatenate([u16.view(np.uint8)[0::2], u16.view(np.uint8)[1::2]]))
+    kinds.append("shuffled_u16")
+    encs = [oc.encode(d) for d in data]
+    st, got = _zstd_batch(codecs, encs, n)
+    assert st == [0] * len(encs)
+    for i, d in enumerate(data):
+        assert np.array_equal(got[i], d), (i, kinds[i])
+
+
+def test_zstd_concatenated_and_skippable_frames():
+    """Several frames (and a skippable frame) in one chunk decode to the concatenation
+    (zstd bulk decompress semantics, zstd_codec.rs:113-130)."""
+    import struct
+    rng = np.random.default_rng(5)
+    codecs = [BYTES_LE, {"name": "zstd", "configuration": {"level": 3, "checksum": True}}]
+    oc = O.OracleChain.from_metadata(codecs, "uint8", 0, 1)
+    parts = [_content(rng, 300000, "text"), _content(rng, 70000, "smooth"), _content(rng, 500000, "runs")]
+    skip = struct.pack("<II", 0x184D2A53, 7) + b"ignored"
+    enc = oc.encode(parts[0]) + skip + oc.encode(parts[1]) + oc.encode(parts[2])
+    n = sum(len(p) for p in parts)
+    st, got = _zstd_batch(codecs, [enc], n)
+    assert st == [0]
+    assert np.array_equal(got[0], np.concatenate(parts))
+
+
+def test_zstd_corruption_detected():
+    """A flipped byte inside a checksummed multi-block frame is reported as CORRUPT_STREAM, and the
+    other chunks of the batch still decode."""
+    rng = np.random.default_rng(6)
+    codecs = [BYTES_LE, {"name": "zstd", "configuration": {"level": 3, "checksum": True}}]
+    oc = O.OracleChain.from_metadata(codecs, "uint8", 0, 1)
+    n = 1 << 20
+    data = [_content(rng, n, "text"), _content(rng, n, "smooth")]
+    encs = [oc.encode(d) for d in data]
+    bad = bytearray(encs[0])
+    bad[len(bad) // 2] ^= 0x40
+    from zarrs_amd import CodecChain, Context, make_desc
+    import torch
+    ch = CodecChain.from_metadata(codecs, "uint8", 0, Context.default())
+    out = np.zeros(2 * n, np.uint8)
+    descs = [make_desc(bytes(bad), [n], out_start=[0]), make_desc(encs[1], [n], out_start=[n])]
+    from zarrs_amd import ZgpuError
+    with pytest.raises(ZgpuError) as ei:
+        ch.decode_batch(descs, out, [2 * n], enc_device=False)
+    assert ei.value.status in (2, 4)  # CORRUPT_STREAM (or a size mismatch it causes)
+    assert np.array_equal(out[n:], data[1])

@@ -45,10 +45,21 @@ hipError_t launch_crc32_check(const ZgItem *items, uint32_t *status, uint32_t n_
 // On return items[i] points at its slot; aux[i] receives the trailer {crc32, isize} for launch_crc32_check.
 hipError_t launch_gzip(ZgItem *items, uint32_t *status, uint32_t n_items, uint8_t *dst, uint64_t slot_bytes,
                        uint2 *aux, hipStream_t s);
-// zstd (RFC 8878) frame decode into dst slots; lit_scratch holds zstd_lit_scratch_per_item() bytes per item.
+// zstd (RFC 8878) frame decode into dst slots: block-parallel (scan, per-block entropy decode,
+// per-item execution) with the serial one-wave-per-item decoder as the fallback.
+struct ZstdScratch {
+  void *blks;            // n_items * blk_cap block records
+  uint32_t *nblk, *mode;  // per item
+  uint8_t *lit;          // n_items * lit_stride literal scratch
+  uint64_t lit_stride;
+  uint32_t *seq;         // n_items * seq_cap sequences of 3 u32
+  uint64_t seq_cap;
+  uint32_t blk_cap;
+};
+void zstd_scratch_layout(uint64_t slot_bytes, uint32_t &blk_cap, uint64_t &blk_bytes, uint64_t &lit_stride,
+                         uint64_t &seq_cap);
 hipError_t launch_zstd(ZgItem *items, uint32_t *status, uint32_t n_items, uint8_t *dst, uint64_t slot_bytes,
-                       uint8_t *lit_scratch, hipStream_t s);
-uint64_t zstd_lit_scratch_per_item();
+                       const ZstdScratch &Z, hipStream_t s);
 // standalone unshuffle (when shuffle is not directly above the bytes codec)
 hipError_t launch_unshuffle(ZgItem *items, uint32_t *status, uint32_t n_items, uint8_t *dst, uint64_t slot_bytes,
                             uint32_t elementsize, hipStream_t s);

@@ -17,6 +17,8 @@
 //    older match sources are read back from the flushed output (zstd windows exceed the ring).
 #include <hip/hip_runtime.h>
 
+#include <algorithm>
+
 #include "../common.hpp"
 #include "launch.hpp"
 
@@ -29,6 +31,8 @@ constexpr int ZBATCH = 4096;         // max output span of one sequence batch
 constexpr uint32_t ZBIG = 2048;      // sequences with a longer run are executed alone, chunked
 constexpr uint32_t BLOCK_MAX = 131072;
 constexpr uint32_t MAX_HUF_LOG = 12;
+// per-item decode mode chosen by k_zstd_scan
+constexpr uint32_t ZMODE_PARALLEL = 0, ZMODE_SERIAL = 1, ZMODE_SKIP = 2;
 
 struct Fse {  // FSE decoding table entry
   uint16_t base;
@@ -270,7 +274,8 @@ __device__ void build_fse_default(Fse *T, const int16_t *def, uint32_t nsym, uin
 
 // ---- Huffman (literals) ----
 // Parse the tree description and build the decoding table. Returns bytes consumed, 0 on error.
-__device__ uint32_t read_huffman(const In &I, uint64_t off, uint64_t avail, ZSmem &S, uint32_t &table_log,
+template <class SM>
+__device__ uint32_t read_huffman(const In &I, uint64_t off, uint64_t avail, SM &S, uint32_t &table_log,
                                  const uint8_t *item, uint64_t item_len) {
   const int lane = lane_id();
   if (avail < 1) return 0;
@@ -591,16 +596,17 @@ __device__ void out_match(ZSmem &S, Out &O, uint32_t d, uint64_t n) {
 
 // One wave per item. lit: per-item literal scratch (BLOCK_MAX + 64 bytes each).
 __global__ __launch_bounds__(64) void k_zstd(ZgItem *items, uint32_t *status, uint8_t *dst, uint64_t slot_bytes,
-                                             uint8_t *lit_scratch) {
+                                             uint8_t *lit_scratch, uint64_t lit_stride, const uint32_t *zmode) {
   __shared__ ZSmem S;
   const uint32_t item = blockIdx.x;
   const ZgItem it = items[item];
   if (status[item] || (it.flags & ZG_ITEM_FILL)) return;
+  if (zmode && zmode[item] != ZMODE_SERIAL) return;  // decoded by the block-parallel path
   const int lane = lane_id();
   const uint8_t *in = (const uint8_t *)it.src;
   const In I{in, it.len};
   Out O{dst + (uint64_t)item * slot_bytes, slot_bytes, 0, 0, false};
-  uint8_t *lit = lit_scratch + (uint64_t)item * (BLOCK_MAX + 64);
+  uint8_t *lit = lit_scratch + (uint64_t)item * lit_stride;
   uint32_t err = 0;
   uint64_t ip = 0;
   bool any_frame = false;
@@ -982,12 +988,641 @@ __global__ __launch_bounds__(64) void k_zstd(ZgItem *items, uint32_t *status, ui
   }
 }
 
-uint64_t zstd_lit_scratch_per_item() { return BLOCK_MAX + 64; }
+// =================================================================================================
+// Block-parallel path (items whose blocks fit the scratch; k_zstd above is the fallback).
+//
+// A zstd frame is a chain of blocks whose sizes are in their 3-byte headers, so the expensive part,
+// entropy decoding, parallelises over blocks once the per-block table sources are known:
+//   k_zstd_scan    one wave per item: walk frames and block headers, parse each compressed block's
+//                  literal / sequence section headers, resolve "treeless" literals and "repeat" FSE
+//                  modes to the block that defined the table, and write one ZBlk record per block
+//   k_zstd_blocks  one wave per block (grid-stride over all records): build the Huffman and FSE
+//                  tables, decode the literals into the item's literal scratch and the sequences
+//                  (literal length, match length, raw Offset_Value) into its sequence scratch
+//   k_zstd_exec    one wave per item: walk its blocks in order, resolve repeat offsets, and
+//                  execute literal copies and matches through the LDS ring (matches resolve in rounds:
+//                  every match whose source lies before the first unresolved one copies itself)
+// =================================================================================================
+namespace {
+
+constexpr uint32_t ZB_RAW = 0, ZB_RLE = 1, ZB_CMP = 2;
+constexpr uint32_t ZBF_FIRST = 1u << 8, ZBF_LAST = 1u << 9, ZBF_FCS = 1u << 10, ZBF_CK = 1u << 11;
+
+struct ZBlk {
+  uint32_t flags;             // bits 0-1 block type, 2-3 literal type, 4 four streams, ZBF_*
+  uint32_t in_off, in_size;   // block content (raw data / rle byte / compressed content), item-relative
+  uint32_t out_size;          // decoded size: raw/rle from the header, compressed from k_zstd_blocks
+  uint32_t regen;             // literal count
+  uint32_t lit_off, lit_end;  // raw literals: data; rle: the byte; huffman: streams (jump table first)
+  uint32_t huf_off;           // Huffman tree description in effect
+  uint32_t nseq, seq_off, seq_end;  // sequence bitstream
+  uint32_t tab_off[3];        // LL / OF / ML table source (rle: symbol byte; fse: NCount)
+  uint32_t tab_mode;          // 2 bits per table: 0 predefined, 1 rle, 2 fse
+  uint32_t lit_buf;           // literal scratch offset (huffman / rle literals)
+  uint32_t seq_buf;           // first sequence in the item's sequence scratch
+  uint32_t pad;
+  uint64_t fcs;               // frame content size (first block of a frame with one)
+  uint32_t ck, pad2;          // frame checksum (last block of a frame with one)
+};
+
+struct ZScanSmem {
+  int16_t norm[64];
+};
+
+struct ZDecSmem {
+  uint16_t huf[1 << MAX_HUF_LOG];
+  Fse ll[512], ml[512], of[256], wt[64];
+  int16_t norm[64];
+  uint8_t weights[256];
+  uint16_t hsorted[256];
+  uint32_t tmp[32];
+};
+
+}  // namespace
+
+__global__ __launch_bounds__(64) void k_zstd_scan(const ZgItem *items, uint32_t *status, ZBlk *blks,
+                                                  uint32_t blk_cap, uint32_t *nblk, uint32_t *zmode,
+                                                  uint64_t lit_stride, uint64_t seq_cap) {
+  __shared__ ZScanSmem S;
+  const uint32_t item = blockIdx.x;
+  const ZgItem it = items[item];
+  const int lane = lane_id();
+  if (status[item] || (it.flags & ZG_ITEM_FILL)) {
+    if (lane == 0) { nblk[item] = 0; zmode[item] = ZMODE_SKIP; }
+    return;
+  }
+  if (it.len >= 0xFFFFFFF0ull) {  // 32-bit record offsets: decode such items serially
+    if (lane == 0) { nblk[item] = 0; zmode[item] = ZMODE_SERIAL; }
+    return;
+  }
+  const uint8_t *in = (const uint8_t *)it.src;
+  const In I{in, it.len};
+  ZBlk *B = blks + (uint64_t)item * blk_cap;
+  uint32_t nb = 0, err = 0;
+  bool serial = false, any_frame = false;
+  uint64_t ip = 0, lit_used = 0, seq_used = 0;
+#define SFAIL(code) { err = (code); break; }
+  while (!err && !serial && ip < it.len) {
+    const uint32_t magic = I.le32(ip);
+    if (ip + 4 > it.len) SFAIL(ZG_CORRUPT_STREAM);
+    if ((magic & 0xFFFFFFF0u) == 0x184D2A50u) {  // skippable frame
+      if (ip + 8 > it.len) SFAIL(ZG_CORRUPT_STREAM);
+      ip += 8 + (uint64_t)I.le32(ip + 4);
+      if (ip > it.len) SFAIL(ZG_CORRUPT_STREAM);
+      continue;
+    }
+    if (magic != 0xFD2FB528u) SFAIL(ZG_CORRUPT_STREAM);
+    ip += 4;
+    any_frame = true;
+    const uint32_t fhd = I.b(ip++);
+    const uint32_t fcs_flag = fhd >> 6, single = (fhd >> 5) & 1, has_ck = (fhd >> 2) & 1, did_flag = fhd & 3;
+    if (fhd & 8) SFAIL(ZG_CORRUPT_STREAM);
+    if (!single) ip++;
+    const uint32_t did_sz = did_flag == 3 ? 4 : did_flag;
+    uint32_t did = 0;
+    for (uint32_t k = 0; k < did_sz; k++) did |= I.b(ip + k) << (8 * k);
+    ip += did_sz;
+    if (did != 0) SFAIL(ZG_CORRUPT_STREAM);
+    const uint32_t fcs_sz = fcs_flag == 0 ? (single ? 1 : 0) : (fcs_flag == 1 ? 2 : fcs_flag == 2 ? 4 : 8);
+    uint64_t fcs = 0;
+    for (uint32_t k = 0; k < fcs_sz; k++) fcs |= (uint64_t)I.b(ip + k) << (8 * k);
+    if (fcs_sz == 2) fcs += 256;
+    ip += fcs_sz;
+    if (ip > it.len) SFAIL(ZG_CORRUPT_STREAM);
+    bool first = true, last = false;
+    uint32_t huf_src = 0xFFFFFFFFu;                      // tree in effect (treeless literals reuse it)
+    uint32_t tmode[3] = {3, 3, 3}, toff[3] = {0, 0, 0};  // 3 = no table yet
+    while (!last && !err) {
+      if (nb == blk_cap) { serial = true; break; }
+      if (ip + 3 > it.len) SFAIL(ZG_CORRUPT_STREAM);
+      const uint32_t bh = I.le24(ip);
+      ip += 3;
+      last = bh & 1;
+      const uint32_t btype = (bh >> 1) & 3, bsize = bh >> 3;
+      if (btype == 3) SFAIL(ZG_CORRUPT_STREAM);
+      ZBlk R{};
+      R.flags = btype | (first ? ZBF_FIRST : 0u) | (last ? ZBF_LAST : 0u);
+      if (first && fcs_sz) { R.flags |= ZBF_FCS; R.fcs = fcs; }
+      first = false;
+      R.in_off = (uint32_t)ip;
+      if (btype == 0) {
+        if (ip + bsize > it.len) SFAIL(ZG_CORRUPT_STREAM);
+        R.in_size = bsize;
+        R.out_size = bsize;
+        ip += bsize;
+      } else if (btype == 1) {
+        if (ip + 1 > it.len) SFAIL(ZG_CORRUPT_STREAM);
+        R.in_size = 1;
+        R.out_size = bsize;
+        ip += 1;
+      } else {
+        if (bsize > BLOCK_MAX || ip + bsize > it.len) SFAIL(ZG_CORRUPT_STREAM);
+        const uint64_t bend = ip + bsize;
+        R.in_size = bsize;
+        uint64_t p = ip;
+        const uint32_t b0 = I.b(p);
+        const uint32_t ltype = b0 & 3, sfmt = (b0 >> 2) & 3;
+        uint32_t regen = 0, csize = 0, lhdr = 0, four = 0;
+        if (ltype <= 1) {
+          if (sfmt == 0 || sfmt == 2) { regen = b0 >> 3; lhdr = 1; }
+          else if (sfmt == 1) { regen = (b0 >> 4) | (I.b(p + 1) << 4); lhdr = 2; }
+          else { regen = (b0 >> 4) | (I.b(p + 1) << 4) | (I.b(p + 2) << 12); lhdr = 3; }
+        } else {
+          four = sfmt == 0 ? 0 : 1;
+          if (sfmt <= 1) { const uint32_t v = I.le24(p); regen = (v >> 4) & 0x3FF; csize = (v >> 14) & 0x3FF; lhdr = 3; }
+          else if (sfmt == 2) { const uint32_t v = I.le32(p); regen = (v >> 4) & 0x3FFF; csize = (v >> 18) & 0x3FFF; lhdr = 4; }
+          else {
+            const uint64_t v = (uint64_t)I.le32(p) | ((uint64_t)I.b(p + 4) << 32);
+            regen = (uint32_t)(v >> 4) & 0x3FFFF; csize = (uint32_t)(v >> 22) & 0x3FFFF; lhdr = 5;
+          }
+        }
+        if (regen > BLOCK_MAX) SFAIL(ZG_CORRUPT_STREAM);
+        p += lhdr;
+        R.flags |= (ltype << 2) | (four << 4);
+        R.regen = regen;
+        if (ltype == 0) {
+          if (p + regen > bend) SFAIL(ZG_CORRUPT_STREAM);
+          R.lit_off = (uint32_t)p;
+          R.lit_end = (uint32_t)(p + regen);
+          p += regen;
+        } else if (ltype == 1) {
+          if (p + 1 > bend) SFAIL(ZG_CORRUPT_STREAM);
+          R.lit_off = (uint32_t)p;
+          p += 1;
+        } else {
+          if (p + csize > bend) SFAIL(ZG_CORRUPT_STREAM);
+          uint64_t q = p;
+          if (ltype == 2) {  // tree description: FSE-compressed weights (hb < 128) or 4-bit weights
+            const uint32_t hb = I.b(q);
+            const uint32_t tsz = hb < 128 ? 1 + hb : 1 + (hb - 127 + 1) / 2;
+            if (hb == 0 || tsz > csize) SFAIL(ZG_CORRUPT_STREAM);
+            huf_src = (uint32_t)q;
+            q += tsz;
+          } else if (huf_src == 0xFFFFFFFFu) {
+            SFAIL(ZG_CORRUPT_STREAM);  // treeless without a previous table
+          }
+          R.huf_off = huf_src;
+          R.lit_off = (uint32_t)q;
+          R.lit_end = (uint32_t)(p + csize);
+          p += csize;
+        }
+        if (ltype != 0) {  // rle / huffman literals are materialised in the literal scratch
+          R.lit_buf = (uint32_t)lit_used;
+          lit_used += regen;
+          if (lit_used > lit_stride) { serial = true; break; }
+        }
+        // sequences section header
+        if (p >= bend) SFAIL(ZG_CORRUPT_STREAM);
+        uint32_t nseq = 0;
+        const uint32_t c0 = I.b(p);
+        if (c0 < 128) { nseq = c0; p += 1; }
+        else if (c0 < 255) { nseq = ((c0 - 128) << 8) + I.b(p + 1); p += 2; }
+        else { nseq = I.le16(p + 1) + 0x7F00; p += 3; }
+        R.nseq = nseq;
+        if (nseq) {
+          if (p >= bend) SFAIL(ZG_CORRUPT_STREAM);
+          const uint32_t modes = I.b(p++);
+          if (modes & 3) SFAIL(ZG_CORRUPT_STREAM);
+          const uint32_t mm[3] = {modes >> 6, (modes >> 4) & 3, (modes >> 2) & 3};  // LL, OF, ML
+          bool ok = true;
+          for (int t = 0; t < 3 && ok; t++) {
+            const uint32_t maxs = t == 0 ? 35 : t == 1 ? 31 : 52, maxl = t == 0 ? 9 : t == 1 ? 8 : 9;
+            if (mm[t] == 0) {
+              tmode[t] = 0;
+              toff[t] = 0;
+            } else if (mm[t] == 1) {
+              if (p >= bend || I.b(p) > maxs) { ok = false; break; }
+              tmode[t] = 1;
+              toff[t] = (uint32_t)p;
+              p += 1;
+            } else if (mm[t] == 2) {
+              uint32_t acc, ns;
+              const uint32_t used = read_ncount(I, p, bend - p, S.norm, maxs, maxl, acc, ns);
+              if (!used) { ok = false; break; }
+              tmode[t] = 2;
+              toff[t] = (uint32_t)p;
+              p += used;
+            } else if (tmode[t] == 3) {
+              ok = false;  // repeat mode without a previous table
+            }
+          }
+          if (!ok) SFAIL(ZG_CORRUPT_STREAM);
+          R.tab_mode = tmode[0] | (tmode[1] << 2) | (tmode[2] << 4);
+          R.tab_off[0] = toff[0];
+          R.tab_off[1] = toff[1];
+          R.tab_off[2] = toff[2];
+          R.seq_off = (uint32_t)p;
+          R.seq_end = (uint32_t)bend;
+          R.seq_buf = (uint32_t)seq_used;
+          seq_used += nseq;
+          if (seq_used > seq_cap) { serial = true; break; }
+        } else if (p != bend) {
+          SFAIL(ZG_CORRUPT_STREAM);
+        }
+        ip = bend;
+      }
+      if (last && has_ck) {
+        if (ip + 4 > it.len) SFAIL(ZG_CORRUPT_STREAM);
+        R.flags |= ZBF_CK;
+        R.ck = I.le32(ip);
+        ip += 4;
+      }
+      if (lane == 0) B[nb] = R;
+      nb++;
+    }
+  }
+#undef SFAIL
+  if (!err && !serial && !any_frame) err = ZG_CORRUPT_STREAM;
+  if (lane == 0) {
+    nblk[item] = serial ? 0u : nb;
+    zmode[item] = serial ? ZMODE_SERIAL : (err ? ZMODE_SKIP : ZMODE_PARALLEL);
+    if (err && !serial) status[item] = err;
+  }
+}
+
+// One wave per (item, block) record, grid-stride. Sequences land as {ll, ml, Offset_Value}.
+__global__ __launch_bounds__(64) void k_zstd_blocks(const ZgItem *items, uint32_t *status, ZBlk *blks,
+                                                    uint32_t blk_cap, const uint32_t *nblk,
+                                                    const uint32_t *zmode, uint32_t n_items, uint8_t *lit_scratch,
+                                                    uint64_t lit_stride, uint32_t *seq_scratch, uint64_t seq_cap) {
+  __shared__ ZDecSmem S;
+  const int lane = lane_id();
+  const uint64_t total = (uint64_t)n_items * blk_cap;
+  for (uint64_t g = blockIdx.x; g < total; g += gridDim.x) {
+    const uint32_t item = (uint32_t)(g / blk_cap), bi = (uint32_t)(g % blk_cap);
+    if (bi >= nblk[item] || zmode[item] != ZMODE_PARALLEL) continue;
+    ZBlk *Bp = blks + g;
+    const uint32_t flags = U(Bp->flags);
+    if ((flags & 3) != ZB_CMP) continue;
+    const ZgItem it = items[item];
+    const uint8_t *in = (const uint8_t *)it.src;
+    const In I{in, it.len};
+    const uint32_t ltype = (flags >> 2) & 3, regen = U(Bp->regen);
+    uint8_t *lit = lit_scratch + (uint64_t)item * lit_stride + U(Bp->lit_buf);
+    bool bad = false;
+    // ---- literals ----
+    if (ltype == 1) {
+      const uint8_t v = (uint8_t)I.b(U(Bp->lit_off));
+      for (uint32_t k = lane; k < regen; k += 64) lit[k] = v;
+    } else if (ltype >= 2) {
+      const uint32_t huf_off = U(Bp->huf_off), lo0 = U(Bp->lit_off), lend = U(Bp->lit_end);
+      uint32_t tl = 0;
+      if (!read_huffman(I, huf_off, it.len - huf_off, S, tl, in, it.len)) {
+        bad = true;
+      } else {
+        const uint32_t nstreams = (flags >> 4) & 1 ? 4 : 1;
+        uint64_t s_lo[4], s_hi[4];
+        uint32_t s_n[4];
+        if (nstreams == 1) {
+          s_lo[0] = lo0; s_hi[0] = lend; s_n[0] = regen;
+        } else {
+          const uint64_t q = lo0;
+          if (q + 6 > lend) bad = true;
+          const uint32_t l1 = I.le16(q), l2 = I.le16(q + 2), l3 = I.le16(q + 4);
+          const uint64_t b = q + 6;
+          if (b + l1 + l2 + l3 > lend) bad = true;
+          s_lo[0] = b; s_hi[0] = b + l1;
+          s_lo[1] = s_hi[0]; s_hi[1] = s_lo[1] + l2;
+          s_lo[2] = s_hi[1]; s_hi[2] = s_lo[2] + l3;
+          s_lo[3] = s_hi[2]; s_hi[3] = lend;
+          const uint32_t seg = (regen + 3) / 4;
+          if (3 * seg > regen) bad = true;
+          s_n[0] = s_n[1] = s_n[2] = seg;
+          s_n[3] = regen - 3 * seg;
+        }
+        uint32_t lbad = 0;
+        if (!bad && lane < (int)nstreams) {
+          const uint64_t lo = lane == 0 ? s_lo[0] : lane == 1 ? s_lo[1] : lane == 2 ? s_lo[2] : s_lo[3];
+          const uint64_t hi = lane == 0 ? s_hi[0] : lane == 1 ? s_hi[1] : lane == 2 ? s_hi[2] : s_hi[3];
+          const uint32_t ns = lane == 0 ? s_n[0] : lane == 1 ? s_n[1] : lane == 2 ? s_n[2] : s_n[3];
+          const uint32_t out0 = nstreams == 4 ? lane * ((regen + 3) / 4) : 0u;
+          const uintptr_t mis = (uintptr_t)in & 3;
+          LaneBits L;
+          L.words = (const uint32_t *)((uintptr_t)in - mis);
+          L.nwords = (uint32_t)((it.len + mis + 3) / 4);
+          const uint32_t lastb = hi > lo ? in[hi - 1] : 0u;
+          if (lastb == 0) {
+            lbad = 1;
+          } else {
+            L.cur = (int64_t)(hi - 1 + mis) * 8 + (31 - __builtin_clz(lastb));
+            L.lo_bit = (int64_t)(lo + mis) * 8;
+            lane_bits_init(L);
+            for (uint32_t k = 0; k < ns; k++) {
+              const uint32_t e = S.huf[lane_peek(L, tl)];
+              L.cur -= e >> 8;
+              lit[out0 + k] = (uint8_t)e;
+              if (L.cur < L.lo_bit) { lbad = 1; break; }
+            }
+            if (L.cur != L.lo_bit) lbad = 1;
+          }
+        }
+        if (__ballot(lbad != 0)) bad = true;
+      }
+    }
+    // ---- sequences ----
+    const uint32_t nseq = U(Bp->nseq);
+    uint64_t sum_ll = 0, sum_ml = 0;
+    if (!bad && nseq) {
+      const uint32_t tm = U(Bp->tab_mode);
+      uint32_t lg[3] = {0, 0, 0};
+      for (int t = 0; t < 3 && !bad; t++) {
+        const uint32_t mode = (tm >> (2 * t)) & 3, off = U(Bp->tab_off[t]);
+        Fse *T = t == 0 ? S.ll : t == 1 ? S.of : S.ml;
+        const uint32_t maxs = t == 0 ? 35 : t == 1 ? 31 : 52, maxl = t == 0 ? 9 : t == 1 ? 8 : 9;
+        if (mode == 0) {
+          if (t == 0) { build_fse_default(T, c_ll_def, 36, 6, S.norm, S.tmp); lg[t] = 6; }
+          else if (t == 1) { build_fse_default(T, c_of_def, 29, 5, S.norm, S.tmp); lg[t] = 5; }
+          else { build_fse_default(T, c_ml_def, 53, 6, S.norm, S.tmp); lg[t] = 6; }
+        } else if (mode == 1) {
+          build_fse_rle(T, I.b(off));
+          lg[t] = 0;
+        } else {
+          uint32_t acc, ns;
+          if (!read_ncount(I, off, it.len - off, S.norm, maxs, maxl, acc, ns)) { bad = true; break; }
+          __syncthreads();
+          build_fse(T, S.norm, ns, acc, S.tmp);
+          lg[t] = acc;
+        }
+      }
+      BitsBack R;
+      if (!bad && !bb_init(R, in, it.len, U(Bp->seq_off), U(Bp->seq_end))) bad = true;
+      if (!bad) {
+        uint32_t sll = bb_read(R, lg[0]), sof = bb_read(R, lg[1]), sml = bb_read(R, lg[2]);
+        uint32_t *out = seq_scratch + ((uint64_t)item * seq_cap + U(Bp->seq_buf)) * 3;
+        uint32_t remaining = nseq, done = 0;
+        while (remaining && !bad) {
+          uint32_t r_ll = 0, r_ml = 0, r_of = 0, cnt = 0;
+          while (cnt < 64 && remaining) {
+            const Fse eo = S.of[sof], em = S.ml[sml], el = S.ll[sll];
+            const uint32_t ofc = U(eo.sym), mlc = U(em.sym), llc = U(el.sym);
+            if (ofc > 31 || mlc > 52 || llc > 35) { bad = true; break; }
+            uint32_t ofv;
+            if (ofc <= 25) {
+              ofv = (1u << ofc) + bb_read(R, ofc);
+            } else {
+              const uint32_t hi = bb_read(R, ofc - 16);
+              const uint32_t lo = bb_read(R, 16);
+              ofv = (1u << ofc) + ((hi << 16) | lo);
+            }
+            const uint32_t ml = c_ml_base[mlc] + bb_read(R, c_ml_bits[mlc]);
+            const uint32_t ll = c_ll_base[llc] + bb_read(R, c_ll_bits[llc]);
+            remaining--;
+            if (remaining) {
+              sll = U(el.base) + bb_read(R, U(el.nb));
+              sml = U(em.base) + bb_read(R, U(em.nb));
+              sof = U(eo.base) + bb_read(R, U(eo.nb));
+            }
+            if (lane == (int)cnt) { r_ll = ll; r_ml = ml; r_of = ofv; }
+            sum_ll += ll;
+            sum_ml += ml;
+            cnt++;
+          }
+          if (bad) break;
+          if (lane < (int)cnt) {
+            uint32_t *o = out + (uint64_t)(done + lane) * 3;
+            o[0] = r_ll;
+            o[1] = r_ml;
+            o[2] = r_of;
+          }
+          done += cnt;
+        }
+        if (!bad && (bb_overflow(R) || !bb_exact_end(R))) bad = true;
+      }
+    }
+    if (!bad && sum_ll > regen) bad = true;
+    if (lane == 0) {
+      if (bad) status[item] = ZG_CORRUPT_STREAM;
+      else Bp->out_size = (uint32_t)min<uint64_t>(regen + sum_ml, 0xFFFFFFFFull);
+    }
+  }
+}
+
+// One wave per item: execute the decoded blocks in order.
+__global__ __launch_bounds__(64) void k_zstd_exec(ZgItem *items, uint32_t *status, const ZBlk *blks,
+                                                  uint32_t blk_cap, const uint32_t *nblk, const uint32_t *zmode,
+                                                  uint8_t *dst, uint64_t slot_bytes, const uint8_t *lit_scratch,
+                                                  uint64_t lit_stride, const uint32_t *seq_scratch, uint64_t seq_cap) {
+  __shared__ ZSmem S;
+  const uint32_t item = blockIdx.x;
+  const int lane = lane_id();
+  if (zmode[item] != ZMODE_PARALLEL || status[item]) return;
+  const ZgItem it = items[item];
+  const uint8_t *in = (const uint8_t *)it.src;
+  Out O{dst + (uint64_t)item * slot_bytes, slot_bytes, 0, 0, false};
+  const uint32_t nb = nblk[item];
+  const ZBlk *B = blks + (uint64_t)item * blk_cap;
+  uint32_t err = 0;
+  uint64_t frame_start = 0, fcs = 0;
+  bool has_fcs = false;
+  uint32_t rep0 = 1, rep1 = 4, rep2 = 8;
+  for (uint32_t bi = 0; bi < nb && !err; bi++) {
+    const uint32_t flags = U(B[bi].flags);
+    if (flags & ZBF_FIRST) {
+      frame_start = O.pos;
+      rep0 = 1; rep1 = 4; rep2 = 8;
+      has_fcs = flags & ZBF_FCS;
+      fcs = U64(B[bi].fcs);
+      if (has_fcs && O.pos + fcs > O.cap) { err = ZG_DECODED_SIZE_MISMATCH; break; }
+    }
+    const uint32_t type = flags & 3;
+    const uint32_t in_off = U(B[bi].in_off), out_size = U(B[bi].out_size);
+    if (O.pos + out_size > O.cap) { err = ZG_DECODED_SIZE_MISMATCH; break; }
+    if (type == ZB_RAW) {
+      out_copy_global(S, O, in + in_off, out_size);
+    } else if (type == ZB_RLE) {
+      out_rle(S, O, (uint8_t)U(in[in_off]), out_size);
+    } else {
+      const uint32_t ltype = (flags >> 2) & 3, regen = U(B[bi].regen), nseq = U(B[bi].nseq);
+      const uint8_t *lsrc = ltype == 0 ? in + U(B[bi].lit_off)
+                                       : lit_scratch + (uint64_t)item * lit_stride + U(B[bi].lit_buf);
+      const uint32_t *seqs = seq_scratch + ((uint64_t)item * seq_cap + U(B[bi].seq_buf)) * 3;
+      uint64_t litpos = 0;
+      uint32_t base = 0;
+      while (base < nseq && !err) {
+        // load up to 64 sequences, resolve repeat offsets in order, stop at ZBATCH / big sequences
+        const uint32_t avail = min<uint32_t>(64, nseq - base);
+        uint32_t r_ll = 0, r_ml = 0, r_ov = 0;
+        if (lane < (int)avail) {
+          const uint32_t *q = seqs + (uint64_t)(base + lane) * 3;
+          r_ll = q[0];
+          r_ml = q[1];
+          r_ov = q[2];
+        }
+        uint32_t cnt = 0, r_of = 0;
+        uint64_t span = 0, lspan = 0;
+        bool big = false;
+        uint32_t big_ll = 0, big_ml = 0, big_of = 0;
+        while (cnt < avail) {
+          const uint32_t ll = __builtin_amdgcn_readlane(r_ll, cnt), ml = __builtin_amdgcn_readlane(r_ml, cnt);
+          const uint32_t ofv = __builtin_amdgcn_readlane(r_ov, cnt);
+          const bool is_big = ll >= ZBIG || ml >= ZBIG;
+          if (!is_big && span + ll + ml > ZBATCH) break;  // ll, ml < ZBIG <= ZBATCH: fits alone
+          uint32_t off;
+          if (ofv > 3) {
+            off = ofv - 3;
+            rep2 = rep1; rep1 = rep0; rep0 = off;
+          } else {
+            const uint32_t idx = ofv - 1 + (ll == 0 ? 1 : 0);
+            if (idx == 0) {
+              off = rep0;
+            } else if (idx == 1) {
+              off = rep1; rep1 = rep0; rep0 = off;
+            } else if (idx == 2) {
+              off = rep2; rep2 = rep1; rep1 = rep0; rep0 = off;
+            } else {
+              off = rep0 - 1; rep2 = rep1; rep1 = rep0; rep0 = off;
+            }
+          }
+          if (is_big) {  // executed alone after this batch
+            big = true;
+            big_ll = ll; big_ml = ml; big_of = off;
+            break;
+          }
+          if (lane == (int)cnt) r_of = off;
+          cnt++;
+          span += ll + ml;
+          lspan += ll;
+        }
+        // ---- execute the batch ----
+        if (cnt) {
+          const uint64_t out_base = O.pos;
+          if (out_base + span > O.cap) { err = ZG_DECODED_SIZE_MISMATCH; break; }
+          if (litpos + lspan > regen) { err = ZG_CORRUPT_STREAM; break; }
+          out_reserve(S, O, span);
+          const bool mine = lane < (int)cnt;
+          const uint32_t sll = mine ? r_ll : 0u, sml = mine ? r_ml : 0u;
+          uint32_t a = sll, b = sll + sml;
+          for (int o = 1; o < 64; o <<= 1) {
+            const uint32_t ta = __shfl_up(a, o, 64), tb = __shfl_up(b, o, 64);
+            if (lane >= o) { a += ta; b += tb; }
+          }
+          S.pfx_lit[lane] = a;
+          S.pfx_out[lane] = b;
+          const uint64_t mstart = out_base + b - sml;  // this lane's match start
+          const bool badoff = mine && sml && (r_of == 0 || (uint64_t)r_of > mstart - frame_start);
+          if (__ballot(badoff)) { err = ZG_CORRUPT_STREAM; break; }
+          __syncthreads();
+          const uint32_t Lb = (uint32_t)lspan;
+          for (uint32_t k = lane; k < Lb; k += 64) {
+            uint32_t lo2 = 0, hi2 = cnt - 1;  // first sequence with pfx_lit > k
+            while (lo2 < hi2) {
+              const uint32_t mid = (lo2 + hi2) >> 1;
+              if (S.pfx_lit[mid] > k) hi2 = mid; else lo2 = mid + 1;
+            }
+            const uint32_t prev_lit = lo2 ? S.pfx_lit[lo2 - 1] : 0u, prev_out = lo2 ? S.pfx_out[lo2 - 1] : 0u;
+            S.ring[(out_base + prev_out + (k - prev_lit)) & ZRMASK] = __builtin_nontemporal_load(lsrc + litpos + k);
+          }
+          const uint64_t wend = out_base + span;
+          if (__ballot(mine && sml > 0 && mstart - r_of + ZRING < wend)) out_fence(O);
+          // matches resolve in rounds (see k_gzip)
+          const uint64_t msrc = mstart - r_of;
+          bool pending = mine && sml > 0;
+          uint64_t pm;
+          while ((pm = __ballot(pending)) != 0) {
+            const int first = __builtin_ctzll(pm);
+            const uint32_t F_lo = __builtin_amdgcn_readlane((uint32_t)mstart, first);
+            const uint32_t F_hi = __builtin_amdgcn_readlane((uint32_t)(mstart >> 32), first);
+            const uint64_t F = ((uint64_t)F_hi << 32) | F_lo;
+            const uint32_t flen = __builtin_amdgcn_readlane(sml, first);
+            if (flen > 32) {
+              const uint32_t fd = __builtin_amdgcn_readlane(r_of, first);
+              const float inv = 1.0f / (float)fd;
+              for (uint32_t i = lane; i < flen; i += 64) {
+                uint32_t rm = i;
+                if (fd < flen) {
+                  uint32_t q = (uint32_t)((float)i * inv);
+                  int32_t r = (int32_t)i - (int32_t)(q * fd);
+                  if (r < 0) r += fd;
+                  if (r >= (int32_t)fd) r -= fd;
+                  rm = (uint32_t)r;
+                }
+                S.ring[(F + i) & ZRMASK] = src_byte(S, O, F - fd + rm, wend);
+              }
+              if (lane == first) pending = false;
+              continue;
+            }
+            const bool ready = pending && sml <= 32 && (lane == first || msrc + sml <= F);
+            if (ready) {
+              for (uint32_t i0 = 0; i0 < sml; i0 += 4) {
+                uint8_t v[4];
+#pragma unroll
+                for (int k = 0; k < 4; k++) {
+                  const uint32_t i = i0 + k;
+                  const uint32_t r = i < r_of ? i : i % r_of;
+                  v[k] = i < sml ? src_byte(S, O, msrc + r, wend) : (uint8_t)0;
+                }
+#pragma unroll
+                for (int k = 0; k < 4; k++)
+                  if (i0 + k < sml) S.ring[(mstart + i0 + k) & ZRMASK] = v[k];
+              }
+              pending = false;
+            }
+          }
+          __syncthreads();
+          O.pos = wend;
+          litpos += lspan;
+        }
+        base += cnt;
+        if (big) {
+          if (O.pos + big_ll + big_ml > O.cap) { err = ZG_DECODED_SIZE_MISMATCH; break; }
+          if (litpos + big_ll > regen) { err = ZG_CORRUPT_STREAM; break; }
+          out_copy_global(S, O, lsrc + litpos, big_ll);
+          litpos += big_ll;
+          if (big_ml) {
+            if (big_of == 0 || (uint64_t)big_of > O.pos - frame_start) { err = ZG_CORRUPT_STREAM; break; }
+            out_match(S, O, big_of, big_ml);
+          }
+          base += 1;
+        }
+      }
+      if (err) break;
+      if (litpos > regen) { err = ZG_CORRUPT_STREAM; break; }
+      out_copy_global(S, O, lsrc + litpos, regen - litpos);
+    }
+    if (flags & ZBF_LAST) {
+      if (has_fcs && O.pos - frame_start != fcs) { err = ZG_CORRUPT_STREAM; break; }
+      if (flags & ZBF_CK) {
+        out_flush(S, O);
+        out_fence(O);
+        const uint64_t h = xxh64(O.out + frame_start, O.pos - frame_start);
+        if ((uint32_t)h != U(B[bi].ck)) { err = ZG_CORRUPT_STREAM; break; }
+      }
+    }
+  }
+  if (!err) out_flush(S, O);
+  if (lane == 0) {
+    if (err) {
+      status[item] = err;
+    } else {
+      items[item].src = (uint64_t)O.out;
+      items[item].len = O.pos;
+    }
+  }
+}
+
+void zstd_scratch_layout(uint64_t slot_bytes, uint32_t &blk_cap, uint64_t &blk_bytes, uint64_t &lit_stride,
+                         uint64_t &seq_cap) {
+  blk_cap = (uint32_t)std::min<uint64_t>(slot_bytes / 32768 + 64, 1u << 20);
+  blk_bytes = sizeof(ZBlk);
+  lit_stride = std::max<uint64_t>(slot_bytes, BLOCK_MAX + 64);
+  lit_stride = (lit_stride + 255) & ~(uint64_t)255;
+  seq_cap = slot_bytes / 4 + 1024;  // sequences per item (each decodes >= 3 bytes; typical >= 8)
+}
 
 hipError_t launch_zstd(ZgItem *items, uint32_t *status, uint32_t n_items, uint8_t *dst, uint64_t slot_bytes,
-                       uint8_t *lit_scratch, hipStream_t s) {
+                       const ZstdScratch &Z, hipStream_t s) {
   if (!n_items) return hipSuccess;
-  hipLaunchKernelGGL(k_zstd, dim3(n_items), dim3(64), 0, s, items, status, dst, slot_bytes, lit_scratch);
+  ZBlk *blks = (ZBlk *)Z.blks;
+  hipLaunchKernelGGL(k_zstd_scan, dim3(n_items), dim3(64), 0, s, items, status, blks, Z.blk_cap, Z.nblk, Z.mode,
+                     Z.lit_stride, Z.seq_cap);
+  const uint64_t recs = (uint64_t)n_items * Z.blk_cap;
+  const uint32_t grid = (uint32_t)std::min<uint64_t>(recs, 256 * 16);
+  hipLaunchKernelGGL(k_zstd_blocks, dim3(grid), dim3(64), 0, s, items, status, blks, Z.blk_cap, Z.nblk, Z.mode,
+                     n_items, Z.lit, Z.lit_stride, Z.seq, Z.seq_cap);
+  hipLaunchKernelGGL(k_zstd_exec, dim3(n_items), dim3(64), 0, s, items, status, blks, Z.blk_cap, Z.nblk, Z.mode,
+                     dst, slot_bytes, Z.lit, Z.lit_stride, Z.seq, Z.seq_cap);
+  hipLaunchKernelGGL(k_zstd, dim3(n_items), dim3(64), 0, s, items, status, dst, slot_bytes, Z.lit, Z.lit_stride,
+                     Z.mode);
   return hipGetLastError();
 }
 

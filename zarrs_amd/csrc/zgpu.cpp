@@ -165,7 +165,7 @@ struct zgpu_plan {
   uint32_t *d_shard_status = nullptr;
   uint8_t *d_pool[2] = {nullptr, nullptr};
   uint2 *d_aux = nullptr;
-  uint8_t *d_zlit = nullptr;
+  ZstdScratch zs{};  // block-parallel zstd scratch (allocated when the chain has zstd)
   unsigned long long *d_counter = nullptr;
   // control block: [counter (256 B) | per-item status (4 B each)], cleared by ONE memset and read
   // back by ONE D2H copy into pinned memory (h_ctl) per execute
@@ -178,7 +178,8 @@ struct zgpu_plan {
   ~zgpu_plan() {
     if (!ctx) return;
     void *bufs[] = {d_items, d_items_init, d_geom, d_shards, d_index, d_shard_status,
-                    d_pool[0], d_pool[1], d_aux, d_zlit, d_ctl, d_enc_stage};
+                    d_pool[0], d_pool[1], d_aux, zs.blks, zs.nblk, zs.mode, zs.lit, zs.seq, d_ctl,
+                    d_enc_stage};
     for (void *b : bufs) ctx->dev_free(b);
     ctx->host_free(h_ctl);
   }
@@ -435,7 +436,15 @@ static void plan_upload(zgpu_plan &P) {
     for (int k = 0; k < P.n_pools; k++) P.d_pool[k] = (uint8_t *)C.dev_alloc(ni * P.slot_bytes);
     for (const Stage &s : P.stages) {
       if (s.kind == ST_GZIP && !P.d_aux) P.d_aux = (uint2 *)C.dev_alloc(ni * sizeof(uint2));
-      if (s.kind == ST_ZSTD && !P.d_zlit) P.d_zlit = (uint8_t *)C.dev_alloc(ni * zstd_lit_scratch_per_item());
+      if (s.kind == ST_ZSTD && !P.zs.blks) {
+        uint64_t blk_bytes;
+        zstd_scratch_layout(P.slot_bytes, P.zs.blk_cap, blk_bytes, P.zs.lit_stride, P.zs.seq_cap);
+        P.zs.blks = C.dev_alloc(ni * (uint64_t)P.zs.blk_cap * blk_bytes);
+        P.zs.nblk = (uint32_t *)C.dev_alloc(ni * 4);
+        P.zs.mode = (uint32_t *)C.dev_alloc(ni * 4);
+        P.zs.lit = (uint8_t *)C.dev_alloc(ni * P.zs.lit_stride);
+        P.zs.seq = (uint32_t *)C.dev_alloc(ni * P.zs.seq_cap * 12);
+      }
     }
   }
   P.ctl_bytes = 256 + ni * 4;
@@ -477,7 +486,7 @@ static void plan_enqueue(zgpu_plan &P, uint8_t *out, hipStream_t s) {
         HIPCHK(launch_crc32_check(P.d_items, P.d_status, ni, P.d_aux, s));
         break;
       case ST_ZSTD:
-        HIPCHK(launch_zstd(P.d_items, P.d_status, ni, P.d_pool[st.pool], P.slot_bytes, P.d_zlit, s));
+        HIPCHK(launch_zstd(P.d_items, P.d_status, ni, P.d_pool[st.pool], P.slot_bytes, P.zs, s));
         break;
       case ST_UNSHUFFLE:
         HIPCHK(launch_unshuffle(P.d_items, P.d_status, ni, P.d_pool[st.pool], P.slot_bytes, st.elementsize, s));
