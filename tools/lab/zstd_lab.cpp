@@ -1,0 +1,149 @@
+// Lab harness (not product code): the block-parallel zstd path on C5-like chunks (byte-shuffled
+// uint16 blob field + noise, zstd level 3), per-kernel times and, in a ZG_PROFILE build, the
+// per-phase shader-clock profile of k_zstd_exec.
+// Build: hipcc --offload-arch=gfx950 -O3 -std=c++17 -fopenmp [-DZG_PROFILE] -I../../zarrs_amd/csrc \
+//        -x hip -o zstd_lab zstd_lab.cpp -l:libzstd.so.1
+#include <hip/hip_runtime.h>
+
+#include <cmath>
+#include <cstdio>
+#include <cstdlib>
+#include <cstring>
+#include <random>
+#include <vector>
+
+#include "common.hpp"
+#include "kernels/zstd.hip"
+
+typedef struct ZSTD_CCtx_s ZSTD_CCtx;
+extern "C" {
+unsigned ZSTD_isError(size_t code);
+ZSTD_CCtx *ZSTD_createCCtx(void);
+size_t ZSTD_freeCCtx(ZSTD_CCtx *);
+size_t ZSTD_CCtx_setParameter(ZSTD_CCtx *, int param, int value);
+size_t ZSTD_compress2(ZSTD_CCtx *, void *dst, size_t cap, const void *src, size_t n);
+size_t ZSTD_compressBound(size_t srcSize);
+}
+
+#define CK(x) do { hipError_t e = (x); if (e != hipSuccess) { printf("HIP %s at %d\n", hipGetErrorString(e), __LINE__); exit(1);} } while (0)
+
+int main(int argc, char **argv) {
+  setvbuf(stdout, NULL, _IOLBF, 0);
+  const int n = argc > 1 ? atoi(argv[1]) : 64;
+  const uint64_t chunk = (argc > 2 ? atoll(argv[2]) : 16) << 20;  // bytes
+  const int level = argc > 3 ? atoi(argv[3]) : 3;
+  std::vector<std::vector<uint8_t>> dec(n), enc(n);
+#pragma omp parallel for
+  for (int c = 0; c < n; c++) {
+    std::mt19937_64 rng(1234 + c);
+    std::normal_distribution<float> nd(0.f, 1.f);
+    const uint64_t cnt = chunk / 2;
+    std::vector<uint16_t> v(cnt);
+    for (uint64_t i = 0; i < cnt; i++) {
+      const float x = (float)(i % 512), y = (float)((i / 512) % 512);
+      const float m = 100.f + 3000.f * expf(-((x - 200) * (x - 200) + (y - 300) * (y - 300)) / (2 * 40.f * 40.f));
+      float val = rintf(m + sqrtf(m) * nd(rng));
+      v[i] = (uint16_t)fminf(fmaxf(val, 0.f), 65535.f);
+    }
+    dec[c].resize(chunk);
+    const uint8_t *b = (const uint8_t *)v.data();
+    for (uint64_t i = 0; i < cnt; i++) { dec[c][i] = b[2 * i]; dec[c][cnt + i] = b[2 * i + 1]; }
+    ZSTD_CCtx *cc = ZSTD_createCCtx();
+    ZSTD_CCtx_setParameter(cc, 100, level);
+    enc[c].resize(ZSTD_compressBound(chunk));
+    size_t r = ZSTD_compress2(cc, enc[c].data(), enc[c].size(), dec[c].data(), chunk);
+    enc[c].resize(r);
+    ZSTD_freeCCtx(cc);
+  }
+  uint64_t total = 0;
+  std::vector<uint64_t> off(n);
+  for (int c = 0; c < n; c++) { off[c] = total; total += (enc[c].size() + 255) & ~255ull; }
+  printf("%d chunks of %.1f MiB, %.1f MiB encoded (ratio %.3f)\n", n, chunk / 1048576.0, total / 1048576.0,
+         (double)n * chunk / total);
+  std::vector<uint8_t> packed(total);
+  for (int c = 0; c < n; c++) memcpy(&packed[off[c]], enc[c].data(), enc[c].size());
+  uint8_t *d_enc, *d_out;
+  CK(hipMalloc(&d_enc, total));
+  CK(hipMemcpy(d_enc, packed.data(), total, hipMemcpyHostToDevice));
+  CK(hipMalloc(&d_out, (size_t)n * chunk));
+  std::vector<ZgItem> items(n);
+  for (int c = 0; c < n; c++) items[c] = ZgItem{(uint64_t)(d_enc + off[c]), enc[c].size(), (uint32_t)c, 0, 0, 0};
+  ZgItem *d_items;
+  uint32_t *d_status;
+  CK(hipMalloc(&d_items, n * sizeof(ZgItem)));
+  CK(hipMalloc(&d_status, n * 4));
+  zgpu::ZstdScratch Z{};
+  uint64_t blk_bytes;
+  zgpu::zstd_scratch_layout(chunk, Z.blk_cap, blk_bytes, Z.lit_stride, Z.seq_cap);
+  CK(hipMalloc(&Z.blks, n * (uint64_t)Z.blk_cap * blk_bytes));
+  CK(hipMalloc(&Z.nblk, n * 4));
+  CK(hipMalloc(&Z.mode, n * 4));
+  CK(hipMalloc(&Z.lit, n * Z.lit_stride));
+  CK(hipMalloc(&Z.seq, n * Z.seq_cap * 12));
+  constexpr int NK = 6;
+  const char *kn[NK] = {"scan", "blocks", "plan", "exec_blocks", "fixup", "serial"};
+  hipEvent_t ev[NK + 1];
+  for (auto &evk : ev) CK(hipEventCreate(&evk));
+  float best[NK];
+  for (auto &bk : best) bk = 1e30f;
+  for (int rep = 0; rep < 3; rep++) {
+    CK(hipMemcpy(d_items, items.data(), n * sizeof(ZgItem), hipMemcpyHostToDevice));
+    CK(hipMemset(d_status, 0, n * 4));
+    zgpu::ZBlk *blks = (zgpu::ZBlk *)Z.blks;
+    const uint32_t grid = (uint32_t)std::min<uint64_t>((uint64_t)n * Z.blk_cap, 256 * 16);
+    CK(hipEventRecord(ev[0]));
+    hipLaunchKernelGGL(zgpu::k_zstd_scan, dim3(n), dim3(64), 0, 0, d_items, d_status, blks, Z.blk_cap, Z.nblk, Z.mode,
+                       Z.lit_stride, Z.seq_cap);
+    CK(hipEventRecord(ev[1]));
+    hipLaunchKernelGGL(zgpu::k_zstd_blocks, dim3(grid), dim3(64), 0, 0, d_items, d_status, blks, Z.blk_cap, Z.nblk,
+                       Z.mode, (uint32_t)n, Z.lit, Z.lit_stride, Z.seq, Z.seq_cap);
+    CK(hipEventRecord(ev[2]));
+    hipLaunchKernelGGL(zgpu::k_zstd_plan, dim3(n), dim3(64), 0, 0, d_items, d_status, blks, Z.blk_cap, Z.nblk, Z.mode,
+                       chunk);
+    CK(hipEventRecord(ev[3]));
+    hipLaunchKernelGGL(zgpu::k_zstd_exec_blocks, dim3(grid), dim3(64), 0, 0, d_items, d_status, blks, Z.blk_cap,
+                       Z.nblk, Z.mode, (uint32_t)n, d_out, chunk, Z.lit, Z.lit_stride, Z.seq, Z.seq_cap);
+    CK(hipEventRecord(ev[4]));
+    hipLaunchKernelGGL(zgpu::k_zstd_fixup, dim3(n), dim3(64), 0, 0, d_items, d_status, blks, Z.blk_cap, Z.nblk,
+                       Z.mode, d_out, chunk, Z.seq, Z.seq_cap);
+    CK(hipEventRecord(ev[5]));
+    hipLaunchKernelGGL(zgpu::k_zstd, dim3(n), dim3(64), 0, 0, d_items, d_status, d_out, chunk, Z.lit, Z.lit_stride,
+                       Z.mode);
+    CK(hipEventRecord(ev[6]));
+    CK(hipEventSynchronize(ev[6]));
+    for (int k = 0; k < NK; k++) {
+      float ms;
+      CK(hipEventElapsedTime(&ms, ev[k], ev[k + 1]));
+      best[k] = std::min(best[k], ms);
+    }
+  }
+  std::vector<uint32_t> st(n), nblk(n), mode(n);
+  CK(hipMemcpy(st.data(), d_status, n * 4, hipMemcpyDeviceToHost));
+  CK(hipMemcpy(nblk.data(), Z.nblk, n * 4, hipMemcpyDeviceToHost));
+  CK(hipMemcpy(mode.data(), Z.mode, n * 4, hipMemcpyDeviceToHost));
+  int bad = 0;
+  std::vector<uint8_t> out(chunk);
+  uint64_t blocks = 0;
+  for (int c = 0; c < n; c++) {
+    CK(hipMemcpy(out.data(), d_out + (uint64_t)c * chunk, chunk, hipMemcpyDeviceToHost));
+    if (st[c] || memcmp(out.data(), dec[c].data(), chunk)) bad++;
+    blocks += nblk[c];
+  }
+  double tot = 0;
+  for (int k = 0; k < NK; k++) tot += best[k];
+  // deferred-match statistics
+  std::vector<uint8_t> hb((uint64_t)n * Z.blk_cap * blk_bytes);
+  CK(hipMemcpy(hb.data(), Z.blks, hb.size(), hipMemcpyDeviceToHost));
+  uint64_t ndef = 0, nserial = 0;
+  for (int c = 0; c < n; c++)
+    for (uint32_t b = 0; b < nblk[c]; b++) {
+      const zgpu::ZBlk &B = ((const zgpu::ZBlk *)hb.data())[(uint64_t)c * Z.blk_cap + b];
+      if ((B.flags & 3) == 2) { ndef += B.def_n; nserial += B.def_n ? 1 : 0; }
+    }
+  printf("blocks %llu (%.1f/chunk), mode[0]=%u, deferred matches %llu in %llu blocks, bad=%d\n",
+         (unsigned long long)blocks, (double)blocks / n, mode[0], (unsigned long long)ndef,
+         (unsigned long long)nserial, bad);
+  for (int k = 0; k < NK; k++) printf("  %-12s %8.3f ms\n", kn[k], best[k]);
+  printf("total %.3f ms -> %.2f GB/s decoded\n", tot, (double)n * chunk / tot / 1e6);
+  return bad ? 1 : 0;
+}

@@ -24,6 +24,20 @@
 
 namespace zgpu {
 
+#ifdef ZG_PROFILE
+// lab builds only (tools/lab/zstd_lab.cpp): k_zstd_exec per-phase shader-clock totals
+__device__ unsigned long long g_zprof[8];
+#define ZP_DECL uint64_t zp_acc[8] = {0, 0, 0, 0, 0, 0, 0, 0}
+#define ZP_T(v) const uint64_t v = clock64()
+#define ZP_ADD(slot, t0) zp_acc[slot] += clock64() - (t0)
+#define ZP_FLUSH do { if (__lane_id() == 0) for (int k_ = 0; k_ < 8; k_++) atomicAdd(&g_zprof[k_], (unsigned long long)zp_acc[k_]); } while (0)
+#else
+#define ZP_DECL
+#define ZP_T(v)
+#define ZP_ADD(slot, t0)
+#define ZP_FLUSH
+#endif
+
 namespace {
 
 constexpr int ZRING = 16384, ZRMASK = ZRING - 1;
@@ -516,9 +530,13 @@ struct Out {
   bool dirty;        // flushed stores not yet fenced for this wave's loads
 };
 
-__device__ __forceinline__ void out_flush(ZSmem &S, Out &O) {
+template <class SM>
+__device__ __forceinline__ void out_flush(SM &S, Out &O) {
   __syncthreads();
-  const uint64_t a = O.flushed & ~(uint64_t)15, b = (O.pos + 15) & ~(uint64_t)15;
+  // the partial 16-B word at `flushed` is written byte by byte: the bytes before `flushed` may
+  // belong to someone else (k_zstd_exec_blocks writes neighbouring blocks concurrently)
+  const uint64_t a = (O.flushed + 15) & ~(uint64_t)15, b = (O.pos + 15) & ~(uint64_t)15;
+  for (uint64_t q = O.flushed + lane_id(); q < a && q < O.pos; q += 64) O.out[q] = S.ring[q & ZRMASK];
   for (uint64_t p = a + (uint64_t)lane_id() * 16; p < b; p += 64 * 16) {
     if (p + 16 <= O.cap) {
       *(uint4 *)(O.out + p) = *(const uint4 *)&S.ring[p & ZRMASK];
@@ -531,7 +549,8 @@ __device__ __forceinline__ void out_flush(ZSmem &S, Out &O) {
   __syncthreads();
 }
 // make room for n more bytes in the ring (n <= ZBATCH)
-__device__ __forceinline__ void out_reserve(ZSmem &S, Out &O, uint64_t n) {
+template <class SM>
+__device__ __forceinline__ void out_reserve(SM &S, Out &O, uint64_t n) {
   if (O.pos + n > O.flushed + ZRING - 1024) out_flush(S, O);
 }
 __device__ __forceinline__ void out_fence(Out &O) {
@@ -540,20 +559,56 @@ __device__ __forceinline__ void out_fence(Out &O) {
     O.dirty = false;
   }
 }
-__device__ __forceinline__ uint8_t src_byte(ZSmem &S, const Out &O, uint64_t s, uint64_t wend) {
-  return (s + ZRING >= wend) ? S.ring[s & ZRMASK] : __builtin_nontemporal_load(O.out + s);
+template <class SM>
+__device__ __forceinline__ uint8_t src_byte(SM &S, const Out &O, uint64_t s, uint64_t wend) {
+  if (s + ZRING >= wend) return S.ring[s & ZRMASK];
+  // flushed output of this wave: an sc1 load (bypasses L1) after out_fence
+  const uint32_t *w = (const uint32_t *)((uintptr_t)(O.out + s) & ~(uintptr_t)3);
+  return (uint8_t)(__hip_atomic_load(w, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) >> (8 * ((uintptr_t)(O.out + s) & 3)));
 }
+typedef unsigned int zv4u __attribute__((ext_vector_type(4)));
+// Copy n <= ZBATCH bytes of global memory into LDS bytes dst[(pos + k) & mask] with 16-byte loads,
+// every load issued before the first LDS write (a byte loop would pay the memory latency per step).
+// The aligned 16-B blocks never extend past the 16-B block holding the last wanted byte.
+__device__ __forceinline__ void lds_copy_in(uint8_t *dst, uint64_t mask, uint64_t pos, const uint8_t *src,
+                                            uint32_t n) {
+  const uintptr_t base = (uintptr_t)src & ~(uintptr_t)15;
+  const uint32_t head = (uint32_t)((uintptr_t)src - base);
+  const uint32_t nvec = (head + n + 15) >> 4;  // <= 257 for n <= 4096
+  constexpr int R = ZBATCH / 16 / 64 + 1;
+  zv4u v[R];
+#pragma unroll
+  for (int r = 0; r < R; r++) {
+    const uint32_t idx = lane_id() + 64 * r;
+    if (idx < nvec) v[r] = __builtin_nontemporal_load((const zv4u *)(base + 16ull * idx));
+  }
+#pragma unroll
+  for (int r = 0; r < R; r++) {
+    const uint32_t idx = lane_id() + 64 * r;
+    if (idx < nvec) {
+      const uint32_t w[4] = {v[r].x, v[r].y, v[r].z, v[r].w};
+#pragma unroll
+      for (int j = 0; j < 16; j++) {
+        const int32_t k = (int32_t)(16 * idx + j) - (int32_t)head;
+        if (k >= 0 && (uint32_t)k < n) dst[(pos + (uint32_t)k) & mask] = (uint8_t)(w[j >> 2] >> (8 * (j & 3)));
+      }
+    }
+  }
+}
+
 // copy n bytes from global memory (raw block / literals) to the output
-__device__ void out_copy_global(ZSmem &S, Out &O, const uint8_t *src, uint64_t n) {
+template <class SM>
+__device__ void out_copy_global(SM &S, Out &O, const uint8_t *src, uint64_t n) {
   for (uint64_t done = 0; done < n;) {
     const uint64_t c = min<uint64_t>(n - done, ZBATCH);
     out_reserve(S, O, c);
-    for (uint64_t k = lane_id(); k < c; k += 64) S.ring[(O.pos + k) & ZRMASK] = __builtin_nontemporal_load(src + done + k);
+    lds_copy_in(S.ring, ZRMASK, O.pos, src + done, (uint32_t)c);
     O.pos += c;
     done += c;
   }
 }
-__device__ void out_rle(ZSmem &S, Out &O, uint8_t v, uint64_t n) {
+template <class SM>
+__device__ void out_rle(SM &S, Out &O, uint8_t v, uint64_t n) {
   for (uint64_t done = 0; done < n;) {
     const uint64_t c = min<uint64_t>(n - done, ZBATCH);
     out_reserve(S, O, c);
@@ -563,7 +618,8 @@ __device__ void out_rle(ZSmem &S, Out &O, uint8_t v, uint64_t n) {
   }
 }
 // match of length n at distance d (d <= pos - frame_start, checked by the caller)
-__device__ void out_match(ZSmem &S, Out &O, uint32_t d, uint64_t n) {
+template <class SM>
+__device__ void out_match(SM &S, Out &O, uint32_t d, uint64_t n) {
   const uint64_t p = O.pos;
   const float inv = 1.0f / (float)d;
   for (uint64_t done = 0; done < n;) {
@@ -991,22 +1047,33 @@ __global__ __launch_bounds__(64) void k_zstd(ZgItem *items, uint32_t *status, ui
 // =================================================================================================
 // Block-parallel path (items whose blocks fit the scratch; k_zstd above is the fallback).
 //
-// A zstd frame is a chain of blocks whose sizes are in their 3-byte headers, so the expensive part,
-// entropy decoding, parallelises over blocks once the per-block table sources are known:
+// A zstd frame is a chain of blocks whose sizes are in their 3-byte headers, so both the entropy
+// decoding and most of the sequence execution parallelise over blocks:
 //   k_zstd_scan    one wave per item: walk frames and block headers, parse each compressed block's
 //                  literal / sequence section headers, resolve "treeless" literals and "repeat" FSE
-//                  modes to the block that defined the table, and write one ZBlk record per block
-//   k_zstd_blocks  one wave per block (grid-stride over all records): build the Huffman and FSE
-//                  tables, decode the literals into the item's literal scratch and the sequences
-//                  (literal length, match length, raw Offset_Value) into its sequence scratch
-//   k_zstd_exec    one wave per item: walk its blocks in order, resolve repeat offsets, and
-//                  execute literal copies and matches through the LDS ring (matches resolve in rounds:
-//                  every match whose source lies before the first unresolved one copies itself)
+//                  modes to the block that defined the table; one ZBlk record per block
+//   k_zstd_blocks  one wave per block: Huffman literals into the literal scratch, FSE sequences into
+//                  the sequence scratch. Repeat offsets are resolved symbolically ("incoming rep k,
+//                  minus j"), so no block waits for its predecessor; the block's outgoing rep state
+//                  is kept in the same symbolic form
+//   k_zstd_plan    one wave per item: block output offsets (prefix sum), concrete incoming rep state
+//                  per block (composing the symbolic transforms), frame content size checks
+//   k_zstd_exec_blocks  one wave per block: executes the block into its own output range. A match
+//                  whose source lies in an earlier block, or touches bytes deferred before it (an
+//                  exact per-byte taint bitmap in LDS), is deferred: recorded in place of the
+//                  consumed sequences; everything else is final. Matches of a batch resolve in rounds
+//                  (see k_gzip)
+//   k_zstd_fixup   one wave per item, blocks in order: a block with deferred matches is loaded whole
+//                  into LDS (<= 128 KiB), its deferred matches run there (sources in earlier blocks
+//                  are final by then), and it is written back; then the frame checksums.
+//                  Deferral chains can span a whole frame (a run continuing across blocks), so this
+//                  pass is serial per frame, but it touches only the deferred matches, in LDS
 // =================================================================================================
 namespace {
 
 constexpr uint32_t ZB_RAW = 0, ZB_RLE = 1, ZB_CMP = 2;
 constexpr uint32_t ZBF_FIRST = 1u << 8, ZBF_LAST = 1u << 9, ZBF_FCS = 1u << 10, ZBF_CK = 1u << 11;
+constexpr uint32_t ZSYM = 0x80000000u;      // symbolic offset: ZSYM | slot << 24 | minus
 
 struct ZBlk {
   uint32_t flags;             // bits 0-1 block type, 2-3 literal type, 4 four streams, ZBF_*
@@ -1020,23 +1087,100 @@ struct ZBlk {
   uint32_t tab_mode;          // 2 bits per table: 0 predefined, 1 rle, 2 fse
   uint32_t lit_buf;           // literal scratch offset (huffman / rle literals)
   uint32_t seq_buf;           // first sequence in the item's sequence scratch
-  uint32_t pad;
+  uint32_t ck;                // frame checksum (last block of a frame with one)
   uint64_t fcs;               // frame content size (first block of a frame with one)
-  uint32_t ck, pad2;          // frame checksum (last block of a frame with one)
+  uint32_t rep_out[3];        // outgoing rep offsets (symbolic in the incoming ones)
+  uint32_t rep_in[3];         // incoming rep offsets (concrete, from k_zstd_plan)
+  uint32_t out_off;           // item-relative output offset (k_zstd_plan)
+  uint32_t frame_off;         // output offset of the block's frame
+  uint32_t def_n;             // deferred matches recorded by k_zstd_exec_blocks
+  uint32_t def_done;          // deferred matches resolved so far
 };
 
 struct ZScanSmem {
   int16_t norm[64];
 };
 
+// literals (Huffman table) and sequences (FSE tables) are decoded one after the other: the two
+// table sets share LDS
 struct ZDecSmem {
-  uint16_t huf[1 << MAX_HUF_LOG];
-  Fse ll[512], ml[512], of[256], wt[64];
+  union {
+    uint16_t huf[1 << MAX_HUF_LOG];
+    struct {
+      Fse ll[512], ml[512], of[256];
+    };
+  };
+  Fse wt[64];
   int16_t norm[64];
   uint8_t weights[256];
   uint16_t hsorted[256];
   uint32_t tmp[32];
 };
+
+struct ZExecSmem {
+  uint8_t ring[ZRING];
+  uint32_t taint[BLOCK_MAX / 32];  // one bit per output byte of the block: deferred (not yet final)
+  uint8_t lit_stage[ZBATCH];       // the batch's literals, staged with 16-B loads
+  uint32_t pfx_lit[64], pfx_out[64];
+};
+
+// coherent byte read of output this wave (or an earlier kernel) wrote: an agent-scope relaxed
+// atomic load is an sc1 load that bypasses the CU's L1 (MI355X_MICROARCH.md, hand-off table)
+__device__ __forceinline__ uint8_t load_out_byte(const uint8_t *p) {
+  const uint32_t *w = (const uint32_t *)((uintptr_t)p & ~(uintptr_t)3);
+  const uint32_t v = __hip_atomic_load(w, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  return (uint8_t)(v >> (8 * ((uintptr_t)p & 3)));
+}
+
+__device__ __forceinline__ uint32_t sym_dec(uint32_t x) { return (x & ZSYM) ? x + 1 : x - 1; }
+__device__ __forceinline__ uint32_t sym_eval(uint32_t x, uint32_t r0, uint32_t r1, uint32_t r2) {
+  if (!(x & ZSYM)) return x;
+  const uint32_t slot = (x >> 24) & 3, minus = x & 0xFFFFFF;
+  return (slot == 0 ? r0 : slot == 1 ? r1 : r2) - minus;
+}
+
+// exact-range output flush for a block (its neighbours belong to other waves): bytes [from, to)
+template <class SM>
+__device__ __forceinline__ void blk_flush(SM &S, uint8_t *out, uint64_t from, uint64_t to) {
+  __syncthreads();
+  const uint64_t a = (from + 15) & ~(uint64_t)15, b = to & ~(uint64_t)15;
+  if (a >= b) {
+    for (uint64_t p = from + lane_id(); p < to; p += 64) out[p] = S.ring[p & ZRMASK];
+  } else {
+    for (uint64_t p = from + lane_id(); p < a; p += 64) out[p] = S.ring[p & ZRMASK];
+    for (uint64_t p = a + (uint64_t)lane_id() * 16; p < b; p += 64 * 16)
+      *(uint4 *)(out + p) = *(const uint4 *)&S.ring[p & ZRMASK];
+    for (uint64_t p = b + lane_id(); p < to; p += 64) out[p] = S.ring[p & ZRMASK];
+  }
+  __syncthreads();
+}
+
+// exact-range write-back of a block image img[0, to - from) to out[from, to)
+__device__ __forceinline__ void blk_flush_img(const uint8_t *img, uint8_t *out, uint64_t from, uint64_t to) {
+  __syncthreads();
+  const uint64_t a = (from + 15) & ~(uint64_t)15, b = to & ~(uint64_t)15;
+  if (a >= b) {
+    for (uint64_t p = from + lane_id(); p < to; p += 64) out[p] = img[p - from];
+  } else {
+    for (uint64_t p = from + lane_id(); p < a; p += 64) out[p] = img[p - from];
+    for (uint64_t p = a + (uint64_t)lane_id() * 16; p < b; p += 64 * 16) {
+      const uint8_t *q = img + (p - from);
+      uint4 v;
+      if (((p - from) & 3) == 0) {
+        v = make_uint4(*(const uint32_t *)q, *(const uint32_t *)(q + 4), *(const uint32_t *)(q + 8),
+                       *(const uint32_t *)(q + 12));
+      } else {
+        uint32_t w[4];
+        for (int j = 0; j < 4; j++)
+          w[j] = q[4 * j] | (q[4 * j + 1] << 8) | (q[4 * j + 2] << 16) | ((uint32_t)q[4 * j + 3] << 24);
+        v = make_uint4(w[0], w[1], w[2], w[3]);
+      }
+      *(uint4 *)(out + p) = v;
+    }
+    for (uint64_t p = b + lane_id(); p < to; p += 64) out[p] = img[p - from];
+  }
+  __syncthreads();
+}
 
 }  // namespace
 
@@ -1240,7 +1384,7 @@ __global__ __launch_bounds__(64) void k_zstd_scan(const ZgItem *items, uint32_t 
   }
 }
 
-// One wave per (item, block) record, grid-stride. Sequences land as {ll, ml, Offset_Value}.
+// One wave per (item, block) record, grid-stride. Sequences land as {ll, ml, offset symbol}.
 __global__ __launch_bounds__(64) void k_zstd_blocks(const ZgItem *items, uint32_t *status, ZBlk *blks,
                                                     uint32_t blk_cap, const uint32_t *nblk,
                                                     const uint32_t *zmode, uint32_t n_items, uint8_t *lit_scratch,
@@ -1260,6 +1404,7 @@ __global__ __launch_bounds__(64) void k_zstd_blocks(const ZgItem *items, uint32_
     const uint32_t ltype = (flags >> 2) & 3, regen = U(Bp->regen);
     uint8_t *lit = lit_scratch + (uint64_t)item * lit_stride + U(Bp->lit_buf);
     bool bad = false;
+    __syncthreads();  // the previous record's table reads are done before they are rebuilt
     // ---- literals ----
     if (ltype == 1) {
       const uint8_t v = (uint8_t)I.b(U(Bp->lit_off));
@@ -1319,9 +1464,11 @@ __global__ __launch_bounds__(64) void k_zstd_blocks(const ZgItem *items, uint32_
         if (__ballot(lbad != 0)) bad = true;
       }
     }
+    __syncthreads();  // Huffman table reads done: the FSE tables reuse its LDS
     // ---- sequences ----
     const uint32_t nseq = U(Bp->nseq);
     uint64_t sum_ll = 0, sum_ml = 0;
+    uint32_t r0 = ZSYM | (0u << 24), r1 = ZSYM | (1u << 24), r2 = ZSYM | (2u << 24);
     if (!bad && nseq) {
       const uint32_t tm = U(Bp->tab_mode);
       uint32_t lg[3] = {0, 0, 0};
@@ -1372,7 +1519,25 @@ __global__ __launch_bounds__(64) void k_zstd_blocks(const ZgItem *items, uint32_
               sml = U(em.base) + bb_read(R, U(em.nb));
               sof = U(eo.base) + bb_read(R, U(eo.nb));
             }
-            if (lane == (int)cnt) { r_ll = ll; r_ml = ml; r_of = ofv; }
+            // repeat offsets, symbolically in the block's incoming rep state (RFC 8878 3.1.1.5)
+            uint32_t off;
+            if (ofv > 3) {
+              off = ofv - 3;
+              if (off & ZSYM) { bad = true; break; }  // beyond any window we decode
+              r2 = r1; r1 = r0; r0 = off;
+            } else {
+              const uint32_t idx = ofv - 1 + (ll == 0 ? 1 : 0);
+              if (idx == 0) {
+                off = r0;
+              } else if (idx == 1) {
+                off = r1; r1 = r0; r0 = off;
+              } else if (idx == 2) {
+                off = r2; r2 = r1; r1 = r0; r0 = off;
+              } else {
+                off = sym_dec(r0); r2 = r1; r1 = r0; r0 = off;
+              }
+            }
+            if (lane == (int)cnt) { r_ll = ll; r_ml = ml; r_of = off; }
             sum_ll += ll;
             sum_ml += ml;
             cnt++;
@@ -1390,212 +1555,436 @@ __global__ __launch_bounds__(64) void k_zstd_blocks(const ZgItem *items, uint32_
       }
     }
     if (!bad && sum_ll > regen) bad = true;
+    if (!bad && regen + sum_ml > BLOCK_MAX) bad = true;  // a block decodes to at most 128 KiB
     if (lane == 0) {
-      if (bad) status[item] = ZG_CORRUPT_STREAM;
-      else Bp->out_size = (uint32_t)min<uint64_t>(regen + sum_ml, 0xFFFFFFFFull);
+      if (bad) {
+        status[item] = ZG_CORRUPT_STREAM;
+      } else {
+        Bp->out_size = (uint32_t)(regen + sum_ml);
+        Bp->rep_out[0] = r0;
+        Bp->rep_out[1] = r1;
+        Bp->rep_out[2] = r2;
+      }
     }
   }
 }
 
-// One wave per item: execute the decoded blocks in order.
-__global__ __launch_bounds__(64) void k_zstd_exec(ZgItem *items, uint32_t *status, const ZBlk *blks,
+// One wave per item: output offsets, incoming rep offsets, frame size checks.
+__global__ __launch_bounds__(64) void k_zstd_plan(const ZgItem *items, uint32_t *status, ZBlk *blks,
                                                   uint32_t blk_cap, const uint32_t *nblk, const uint32_t *zmode,
-                                                  uint8_t *dst, uint64_t slot_bytes, const uint8_t *lit_scratch,
-                                                  uint64_t lit_stride, const uint32_t *seq_scratch, uint64_t seq_cap) {
-  __shared__ ZSmem S;
+                                                  uint64_t slot_bytes) {
   const uint32_t item = blockIdx.x;
-  const int lane = lane_id();
   if (zmode[item] != ZMODE_PARALLEL || status[item]) return;
-  const ZgItem it = items[item];
-  const uint8_t *in = (const uint8_t *)it.src;
-  Out O{dst + (uint64_t)item * slot_bytes, slot_bytes, 0, 0, false};
+  const int lane = lane_id();
+  ZBlk *B = blks + (uint64_t)item * blk_cap;
   const uint32_t nb = nblk[item];
-  const ZBlk *B = blks + (uint64_t)item * blk_cap;
-  uint32_t err = 0;
-  uint64_t frame_start = 0, fcs = 0;
-  bool has_fcs = false;
-  uint32_t rep0 = 1, rep1 = 4, rep2 = 8;
-  for (uint32_t bi = 0; bi < nb && !err; bi++) {
+  uint64_t pos = 0, frame_off = 0;
+  uint32_t r0 = 1, r1 = 4, r2 = 8, err = 0;
+  for (uint32_t bi = 0; bi < nb; bi++) {
     const uint32_t flags = U(B[bi].flags);
     if (flags & ZBF_FIRST) {
-      frame_start = O.pos;
-      rep0 = 1; rep1 = 4; rep2 = 8;
-      has_fcs = flags & ZBF_FCS;
-      fcs = U64(B[bi].fcs);
-      if (has_fcs && O.pos + fcs > O.cap) { err = ZG_DECODED_SIZE_MISMATCH; break; }
+      frame_off = pos;
+      r0 = 1; r1 = 4; r2 = 8;
     }
-    const uint32_t type = flags & 3;
-    const uint32_t in_off = U(B[bi].in_off), out_size = U(B[bi].out_size);
-    if (O.pos + out_size > O.cap) { err = ZG_DECODED_SIZE_MISMATCH; break; }
-    if (type == ZB_RAW) {
-      out_copy_global(S, O, in + in_off, out_size);
-    } else if (type == ZB_RLE) {
-      out_rle(S, O, (uint8_t)U(in[in_off]), out_size);
-    } else {
-      const uint32_t ltype = (flags >> 2) & 3, regen = U(B[bi].regen), nseq = U(B[bi].nseq);
-      const uint8_t *lsrc = ltype == 0 ? in + U(B[bi].lit_off)
-                                       : lit_scratch + (uint64_t)item * lit_stride + U(B[bi].lit_buf);
-      const uint32_t *seqs = seq_scratch + ((uint64_t)item * seq_cap + U(B[bi].seq_buf)) * 3;
-      uint64_t litpos = 0;
-      uint32_t base = 0;
-      while (base < nseq && !err) {
-        // load up to 64 sequences, resolve repeat offsets in order, stop at ZBATCH / big sequences
-        const uint32_t avail = min<uint32_t>(64, nseq - base);
-        uint32_t r_ll = 0, r_ml = 0, r_ov = 0;
-        if (lane < (int)avail) {
-          const uint32_t *q = seqs + (uint64_t)(base + lane) * 3;
-          r_ll = q[0];
-          r_ml = q[1];
-          r_ov = q[2];
-        }
-        uint32_t cnt = 0, r_of = 0;
-        uint64_t span = 0, lspan = 0;
-        bool big = false;
-        uint32_t big_ll = 0, big_ml = 0, big_of = 0;
-        while (cnt < avail) {
-          const uint32_t ll = __builtin_amdgcn_readlane(r_ll, cnt), ml = __builtin_amdgcn_readlane(r_ml, cnt);
-          const uint32_t ofv = __builtin_amdgcn_readlane(r_ov, cnt);
-          const bool is_big = ll >= ZBIG || ml >= ZBIG;
-          if (!is_big && span + ll + ml > ZBATCH) break;  // ll, ml < ZBIG <= ZBATCH: fits alone
-          uint32_t off;
-          if (ofv > 3) {
-            off = ofv - 3;
-            rep2 = rep1; rep1 = rep0; rep0 = off;
-          } else {
-            const uint32_t idx = ofv - 1 + (ll == 0 ? 1 : 0);
-            if (idx == 0) {
-              off = rep0;
-            } else if (idx == 1) {
-              off = rep1; rep1 = rep0; rep0 = off;
-            } else if (idx == 2) {
-              off = rep2; rep2 = rep1; rep1 = rep0; rep0 = off;
-            } else {
-              off = rep0 - 1; rep2 = rep1; rep1 = rep0; rep0 = off;
-            }
-          }
-          if (is_big) {  // executed alone after this batch
-            big = true;
-            big_ll = ll; big_ml = ml; big_of = off;
-            break;
-          }
-          if (lane == (int)cnt) r_of = off;
-          cnt++;
-          span += ll + ml;
-          lspan += ll;
-        }
-        // ---- execute the batch ----
-        if (cnt) {
-          const uint64_t out_base = O.pos;
-          if (out_base + span > O.cap) { err = ZG_DECODED_SIZE_MISMATCH; break; }
-          if (litpos + lspan > regen) { err = ZG_CORRUPT_STREAM; break; }
-          out_reserve(S, O, span);
-          const bool mine = lane < (int)cnt;
-          const uint32_t sll = mine ? r_ll : 0u, sml = mine ? r_ml : 0u;
-          uint32_t a = sll, b = sll + sml;
-          for (int o = 1; o < 64; o <<= 1) {
-            const uint32_t ta = __shfl_up(a, o, 64), tb = __shfl_up(b, o, 64);
-            if (lane >= o) { a += ta; b += tb; }
-          }
-          S.pfx_lit[lane] = a;
-          S.pfx_out[lane] = b;
-          const uint64_t mstart = out_base + b - sml;  // this lane's match start
-          const bool badoff = mine && sml && (r_of == 0 || (uint64_t)r_of > mstart - frame_start);
-          if (__ballot(badoff)) { err = ZG_CORRUPT_STREAM; break; }
-          __syncthreads();
-          const uint32_t Lb = (uint32_t)lspan;
-          for (uint32_t k = lane; k < Lb; k += 64) {
-            uint32_t lo2 = 0, hi2 = cnt - 1;  // first sequence with pfx_lit > k
-            while (lo2 < hi2) {
-              const uint32_t mid = (lo2 + hi2) >> 1;
-              if (S.pfx_lit[mid] > k) hi2 = mid; else lo2 = mid + 1;
-            }
-            const uint32_t prev_lit = lo2 ? S.pfx_lit[lo2 - 1] : 0u, prev_out = lo2 ? S.pfx_out[lo2 - 1] : 0u;
-            S.ring[(out_base + prev_out + (k - prev_lit)) & ZRMASK] = __builtin_nontemporal_load(lsrc + litpos + k);
-          }
-          const uint64_t wend = out_base + span;
-          if (__ballot(mine && sml > 0 && mstart - r_of + ZRING < wend)) out_fence(O);
-          // matches resolve in rounds (see k_gzip)
-          const uint64_t msrc = mstart - r_of;
-          bool pending = mine && sml > 0;
-          uint64_t pm;
-          while ((pm = __ballot(pending)) != 0) {
-            const int first = __builtin_ctzll(pm);
-            const uint32_t F_lo = __builtin_amdgcn_readlane((uint32_t)mstart, first);
-            const uint32_t F_hi = __builtin_amdgcn_readlane((uint32_t)(mstart >> 32), first);
-            const uint64_t F = ((uint64_t)F_hi << 32) | F_lo;
-            const uint32_t flen = __builtin_amdgcn_readlane(sml, first);
-            if (flen > 32) {
-              const uint32_t fd = __builtin_amdgcn_readlane(r_of, first);
-              const float inv = 1.0f / (float)fd;
-              for (uint32_t i = lane; i < flen; i += 64) {
-                uint32_t rm = i;
-                if (fd < flen) {
-                  uint32_t q = (uint32_t)((float)i * inv);
-                  int32_t r = (int32_t)i - (int32_t)(q * fd);
-                  if (r < 0) r += fd;
-                  if (r >= (int32_t)fd) r -= fd;
-                  rm = (uint32_t)r;
-                }
-                S.ring[(F + i) & ZRMASK] = src_byte(S, O, F - fd + rm, wend);
-              }
-              if (lane == first) pending = false;
-              continue;
-            }
-            const bool ready = pending && sml <= 32 && (lane == first || msrc + sml <= F);
-            if (ready) {
-              for (uint32_t i0 = 0; i0 < sml; i0 += 4) {
-                uint8_t v[4];
-#pragma unroll
-                for (int k = 0; k < 4; k++) {
-                  const uint32_t i = i0 + k;
-                  const uint32_t r = i < r_of ? i : i % r_of;
-                  v[k] = i < sml ? src_byte(S, O, msrc + r, wend) : (uint8_t)0;
-                }
-#pragma unroll
-                for (int k = 0; k < 4; k++)
-                  if (i0 + k < sml) S.ring[(mstart + i0 + k) & ZRMASK] = v[k];
-              }
-              pending = false;
-            }
-          }
-          __syncthreads();
-          O.pos = wend;
-          litpos += lspan;
-        }
-        base += cnt;
-        if (big) {
-          if (O.pos + big_ll + big_ml > O.cap) { err = ZG_DECODED_SIZE_MISMATCH; break; }
-          if (litpos + big_ll > regen) { err = ZG_CORRUPT_STREAM; break; }
-          out_copy_global(S, O, lsrc + litpos, big_ll);
-          litpos += big_ll;
-          if (big_ml) {
-            if (big_of == 0 || (uint64_t)big_of > O.pos - frame_start) { err = ZG_CORRUPT_STREAM; break; }
-            out_match(S, O, big_of, big_ml);
-          }
-          base += 1;
-        }
+    if (lane == 0) {
+      B[bi].out_off = (uint32_t)pos;
+      B[bi].frame_off = (uint32_t)frame_off;
+      B[bi].rep_in[0] = r0;
+      B[bi].rep_in[1] = r1;
+      B[bi].rep_in[2] = r2;
+    }
+    if ((flags & 3) == ZB_CMP && U(B[bi].nseq)) {
+      const uint32_t o0 = U(B[bi].rep_out[0]), o1 = U(B[bi].rep_out[1]), o2 = U(B[bi].rep_out[2]);
+      const uint32_t n0 = sym_eval(o0, r0, r1, r2), n1 = sym_eval(o1, r0, r1, r2), n2 = sym_eval(o2, r0, r1, r2);
+      r0 = n0; r1 = n1; r2 = n2;
+    }
+    pos += U(B[bi].out_size);
+    if (pos > slot_bytes || pos >= 0xFFFFFFF0ull) { err = ZG_DECODED_SIZE_MISMATCH; break; }
+  }
+  // frame content sizes: every frame whose first block has ZBF_FCS
+  if (!err) {
+    uint64_t fstart = 0, fcs = 0;
+    bool has = false;
+    for (uint32_t bi = 0; bi < nb; bi++) {
+      const uint32_t flags = U(B[bi].flags);
+      if (flags & ZBF_FIRST) {
+        fstart = U(B[bi].out_off);
+        has = flags & ZBF_FCS;
+        fcs = (uint64_t)U((uint32_t)B[bi].fcs) | ((uint64_t)U((uint32_t)(B[bi].fcs >> 32)) << 32);
       }
-      if (err) break;
-      if (litpos > regen) { err = ZG_CORRUPT_STREAM; break; }
-      out_copy_global(S, O, lsrc + litpos, regen - litpos);
-    }
-    if (flags & ZBF_LAST) {
-      if (has_fcs && O.pos - frame_start != fcs) { err = ZG_CORRUPT_STREAM; break; }
-      if (flags & ZBF_CK) {
-        out_flush(S, O);
-        out_fence(O);
-        const uint64_t h = xxh64(O.out + frame_start, O.pos - frame_start);
-        if ((uint32_t)h != U(B[bi].ck)) { err = ZG_CORRUPT_STREAM; break; }
+      if ((flags & ZBF_LAST) && has && (uint64_t)U(B[bi].out_off) + U(B[bi].out_size) - fstart != fcs) {
+        err = ZG_CORRUPT_STREAM;
+        break;
       }
     }
   }
-  if (!err) out_flush(S, O);
+  if (lane == 0 && err) status[item] = err;
+}
+
+// One wave per (item, block) record, grid-stride: execute the block into its output range.
+__global__ __launch_bounds__(64) void k_zstd_exec_blocks(const ZgItem *items, uint32_t *status, ZBlk *blks,
+                                                         uint32_t blk_cap, const uint32_t *nblk,
+                                                         const uint32_t *zmode, uint32_t n_items, uint8_t *dst,
+                                                         uint64_t slot_bytes, const uint8_t *lit_scratch,
+                                                         uint64_t lit_stride, const uint32_t *seq_scratch,
+                                                         uint64_t seq_cap) {
+  __shared__ ZExecSmem S;
+  const int lane = lane_id();
+  const uint64_t total = (uint64_t)n_items * blk_cap;
+  for (uint64_t g = blockIdx.x; g < total; g += gridDim.x) {
+    const uint32_t item = (uint32_t)(g / blk_cap), bi = (uint32_t)(g % blk_cap);
+    if (bi >= nblk[item] || zmode[item] != ZMODE_PARALLEL || status[item]) continue;
+    ZBlk *Bp = blks + g;
+    const ZgItem it = items[item];
+    const uint8_t *in = (const uint8_t *)it.src;
+    uint8_t *out = dst + (uint64_t)item * slot_bytes;
+    const uint32_t flags = U(Bp->flags), type = flags & 3;
+    const uint64_t bstart = U(Bp->out_off);
+    const uint32_t out_size = U(Bp->out_size);
+    __syncthreads();  // the previous record's LDS use is over
+    if (type != ZB_CMP) {  // raw / rle: no dependencies
+      Out O{out, bstart + out_size, bstart, bstart, false};
+      if (type == ZB_RAW) out_copy_global(S, O, in + U(Bp->in_off), out_size);
+      else if (type == ZB_RLE) out_rle(S, O, (uint8_t)U(in[U(Bp->in_off)]), out_size);
+      blk_flush(S, out, O.flushed, O.pos);
+      continue;
+    }
+    uint32_t err = 0;
+    const uint32_t ltype = (flags >> 2) & 3, regen = U(Bp->regen), nseq = U(Bp->nseq);
+    const uint8_t *lsrc = ltype == 0 ? in + U(Bp->lit_off) : lit_scratch + (uint64_t)item * lit_stride + U(Bp->lit_buf);
+    const uint32_t *seqs = seq_scratch + ((uint64_t)item * seq_cap + U(Bp->seq_buf)) * 3;
+    // deferred matches {pos, distance, length} overwrite the block's already consumed sequences
+    uint32_t *defl = const_cast<uint32_t *>(seqs);
+    const uint32_t ri0 = U(Bp->rep_in[0]), ri1 = U(Bp->rep_in[1]), ri2 = U(Bp->rep_in[2]);
+    const uint64_t frame_off = U(Bp->frame_off);
+    for (uint32_t k = lane; k < BLOCK_MAX / 32; k += 64) S.taint[k] = 0;
+    __syncthreads();
+    Out O{out, bstart + out_size, bstart, bstart, false};
+    uint32_t ndef = 0;
+    uint64_t litpos = 0;
+    uint32_t base = 0;
+    // taint test of block-relative byte range [a, b) (a < b): any deferred byte in it?
+    auto tainted = [&](uint64_t a, uint64_t b) -> bool {
+      for (uint64_t w = a >> 5; w <= (b - 1) >> 5; w++) {
+        uint32_t m = S.taint[w];
+        const uint32_t lo = w == (a >> 5) ? (uint32_t)(a & 31) : 0u;
+        const uint32_t hi = w == ((b - 1) >> 5) ? (uint32_t)((b - 1) & 31) : 31u;
+        m &= (hi == 31 ? 0xFFFFFFFFu : ((1u << (hi + 1)) - 1)) & ~((1u << lo) - 1);
+        if (m) return true;
+      }
+      return false;
+    };
+    auto mark = [&](uint64_t a, uint64_t b) {  // block-relative [a, b), this lane only
+      for (uint64_t w = a >> 5; w <= (b - 1) >> 5; w++) {
+        const uint32_t lo = w == (a >> 5) ? (uint32_t)(a & 31) : 0u;
+        const uint32_t hi = w == ((b - 1) >> 5) ? (uint32_t)((b - 1) & 31) : 31u;
+        atomicOr(&S.taint[w], (hi == 31 ? 0xFFFFFFFFu : ((1u << (hi + 1)) - 1)) & ~((1u << lo) - 1));
+      }
+    };
+    while (base < nseq && !err) {
+      const uint32_t avail = min<uint32_t>(64, nseq - base);
+      uint32_t r_ll = 0, r_ml = 0, r_of = 0;
+      if (lane < (int)avail) {
+        const uint32_t *q = seqs + (uint64_t)(base + lane) * 3;
+        r_ll = q[0];
+        r_ml = q[1];
+        r_of = sym_eval(q[2], ri0, ri1, ri2);
+      }
+      // batch: consecutive sequences up to ZBATCH bytes; a big one (>= ZBIG) goes alone
+      uint32_t cnt = 0;
+      uint64_t span = 0, lspan = 0;
+      bool big = false;
+      while (cnt < avail) {
+        const uint32_t ll = __builtin_amdgcn_readlane(r_ll, cnt), ml = __builtin_amdgcn_readlane(r_ml, cnt);
+        if (ll >= ZBIG || ml >= ZBIG) {
+          big = cnt == 0;
+          if (big) cnt = 1;
+          break;
+        }
+        if (span + ll + ml > ZBATCH) break;
+        cnt++;
+        span += ll + ml;
+        lspan += ll;
+      }
+      if (big) {
+        span = (uint64_t)__builtin_amdgcn_readlane(r_ll, 0) + __builtin_amdgcn_readlane(r_ml, 0);
+        lspan = __builtin_amdgcn_readlane(r_ll, 0);
+      }
+      const uint64_t out_base = O.pos;
+      if (out_base + span > O.cap) { err = ZG_CORRUPT_STREAM; break; }
+      if (litpos + lspan > regen) { err = ZG_CORRUPT_STREAM; break; }
+      const bool mine = lane < (int)cnt;
+      const uint32_t sll = mine ? r_ll : 0u, sml = mine ? r_ml : 0u;
+      uint32_t a = sll, b = sll + sml;
+      for (int o = 1; o < 64; o <<= 1) {
+        const uint32_t ta = __shfl_up(a, o, 64), tb = __shfl_up(b, o, 64);
+        if (lane >= o) { a += ta; b += tb; }
+      }
+      const uint64_t mstart = out_base + b - sml;
+      if (__ballot(mine && sml && (r_of == 0 || (uint64_t)r_of > mstart - frame_off))) { err = ZG_CORRUPT_STREAM; break; }
+      if (big) {
+        // literal run then a long match, each through the ring in ZBATCH pieces
+        const uint32_t bll = __builtin_amdgcn_readlane(r_ll, 0), bml = __builtin_amdgcn_readlane(r_ml, 0);
+        const uint32_t bof = __builtin_amdgcn_readlane(r_of, 0);
+        out_copy_global(S, O, lsrc + litpos, bll);
+        litpos += bll;
+        if (bml) {
+          const uint64_t p = O.pos, src = p - bof;
+          bool tnt = src < bstart;
+          if (!tnt) {
+            const uint64_t ra = src - bstart, rb = ra + min<uint64_t>(bml, bof);
+            bool t = false;
+            for (uint64_t w0 = (ra >> 5) + lane; w0 <= ((rb - 1) >> 5); w0 += 64) t |= tainted(max<uint64_t>(ra, w0 << 5), min<uint64_t>(rb, (w0 + 1) << 5));
+            tnt = __ballot(t) != 0;
+          }
+          if (tnt) {  // defer the whole match
+            for (uint64_t w0 = ((p - bstart) >> 5) + lane; w0 <= ((p - bstart + bml - 1) >> 5); w0 += 64)
+              mark(max<uint64_t>(p - bstart, w0 << 5), min<uint64_t>(p - bstart + bml, (w0 + 1) << 5));
+            if (lane == 0) { defl[3 * ndef] = (uint32_t)p; defl[3 * ndef + 1] = bof; defl[3 * ndef + 2] = bml; }
+            ndef++;
+            for (uint64_t done = 0; done < bml;) {  // keep the ring positions consistent (garbage)
+              const uint64_t c = min<uint64_t>(bml - done, ZBATCH);
+              out_reserve(S, O, c);
+              O.pos += c;
+              done += c;
+            }
+            __syncthreads();
+          } else {
+            out_match(S, O, bof, bml);
+          }
+        }
+        base += 1;
+        continue;
+      }
+      // ---- regular batch ----
+      out_reserve(S, O, span);
+      S.pfx_lit[lane] = a;
+      S.pfx_out[lane] = b;
+      const uint32_t Lb = (uint32_t)lspan;
+      lds_copy_in(S.lit_stage, ~0ull, 0, lsrc + litpos, Lb);
+      __syncthreads();
+      for (uint32_t k = lane; k < Lb; k += 64) {
+        uint32_t lo2 = 0, hi2 = cnt - 1;  // first sequence with pfx_lit > k
+        while (lo2 < hi2) {
+          const uint32_t mid = (lo2 + hi2) >> 1;
+          if (S.pfx_lit[mid] > k) hi2 = mid; else lo2 = mid + 1;
+        }
+        const uint32_t prev_lit = lo2 ? S.pfx_lit[lo2 - 1] : 0u, prev_out = lo2 ? S.pfx_out[lo2 - 1] : 0u;
+        S.ring[(out_base + prev_out + (k - prev_lit)) & ZRMASK] = S.lit_stage[k];
+      }
+      const uint64_t wend = out_base + span;
+      const uint64_t msrc = mstart - r_of;
+      if (__ballot(mine && sml > 0 && msrc + ZRING < wend)) out_fence(O);
+      bool pending = mine && sml > 0, deferred = false;
+      uint64_t pm;
+      while ((pm = __ballot(pending)) != 0) {
+        const int first = __builtin_ctzll(pm);
+        const uint32_t F_lo = __builtin_amdgcn_readlane((uint32_t)mstart, first);
+        const uint32_t F_hi = __builtin_amdgcn_readlane((uint32_t)(mstart >> 32), first);
+        const uint64_t F = ((uint64_t)F_hi << 32) | F_lo;
+        const uint32_t flen = __builtin_amdgcn_readlane(sml, first);
+        const bool ready = pending && (lane == first || (sml <= 32 && msrc + sml <= F));
+        // taint: source in an earlier block, or touching a deferred byte
+        bool tnt = false;
+        if (ready) {
+          if (msrc < bstart) {
+            tnt = true;
+          } else if (sml <= 32 || lane != first) {
+            tnt = tainted(msrc - bstart, msrc - bstart + min<uint32_t>(sml, r_of));
+          }
+        }
+        if (flen > 32) {  // the first pending match is long: taint-check and copy cooperatively
+          const uint32_t fd = __builtin_amdgcn_readlane(r_of, first);
+          bool ft = __builtin_amdgcn_readlane((uint32_t)tnt, first) != 0;
+          if (!ft) {
+            const uint64_t ra = F - fd - bstart, rb = ra + min<uint32_t>(flen, fd);
+            bool t = false;
+            for (uint64_t w0 = (ra >> 5) + lane; w0 <= ((rb - 1) >> 5); w0 += 64)
+              t |= tainted(max<uint64_t>(ra, w0 << 5), min<uint64_t>(rb, (w0 + 1) << 5));
+            ft = __ballot(t) != 0;
+          }
+          if (ft) {
+            for (uint64_t w0 = ((F - bstart) >> 5) + lane; w0 <= ((F - bstart + flen - 1) >> 5); w0 += 64)
+              mark(max<uint64_t>(F - bstart, w0 << 5), min<uint64_t>(F - bstart + flen, (w0 + 1) << 5));
+            if (lane == first) deferred = true;
+          } else {
+            const float inv = 1.0f / (float)fd;
+            for (uint32_t i = lane; i < flen; i += 64) {
+              uint32_t rm = i;
+              if (fd < flen) {
+                uint32_t q = (uint32_t)((float)i * inv);
+                int32_t r = (int32_t)i - (int32_t)(q * fd);
+                if (r < 0) r += fd;
+                if (r >= (int32_t)fd) r -= fd;
+                rm = (uint32_t)r;
+              }
+              S.ring[(F + i) & ZRMASK] = src_byte(S, O, F - fd + rm, wend);
+            }
+          }
+          if (lane == first) pending = false;
+          __syncthreads();
+          continue;
+        }
+        if (ready) {
+          if (tnt) {
+            mark(mstart - bstart, mstart - bstart + sml);
+            deferred = true;
+          } else {
+            for (uint32_t i0 = 0; i0 < sml; i0 += 4) {
+              uint8_t v[4];
+#pragma unroll
+              for (int k = 0; k < 4; k++) {
+                const uint32_t i = i0 + k;
+                const uint32_t r = i < r_of ? i : i % r_of;
+                v[k] = i < sml ? src_byte(S, O, msrc + r, wend) : (uint8_t)0;
+              }
+#pragma unroll
+              for (int k = 0; k < 4; k++)
+                if (i0 + k < sml) S.ring[(mstart + i0 + k) & ZRMASK] = v[k];
+            }
+          }
+          pending = false;
+        }
+        __syncthreads();
+      }
+      // record this batch's deferred matches in output order
+      const uint64_t dm = __ballot(deferred);
+      const uint32_t nd = __builtin_popcountll(dm);
+      if (nd) {
+        if (deferred) {  // ndef + k <= base + lane: a consumed sequence slot
+          const uint32_t k = ndef + __builtin_popcountll(dm & ((1ull << lane) - 1));
+          defl[3 * k] = (uint32_t)mstart;
+          defl[3 * k + 1] = r_of;
+          defl[3 * k + 2] = sml;
+        }
+        ndef += nd;
+      }
+      __syncthreads();
+      O.pos = wend;
+      litpos += lspan;
+      base += cnt;
+    }
+    if (!err) {
+      if (litpos > regen) {
+        err = ZG_CORRUPT_STREAM;
+      } else {
+        out_copy_global(S, O, lsrc + litpos, regen - litpos);
+        if (O.pos != bstart + out_size) err = ZG_CORRUPT_STREAM;
+      }
+    }
+    if (!err) blk_flush(S, out, O.flushed, O.pos);
+    if (lane == 0) {
+      if (err) status[item] = err;
+      Bp->def_n = err ? 0u : ndef;
+      Bp->def_done = 0;
+    }
+    __syncthreads();
+  }
+}
+
+// One wave per item, 128 KiB of LDS: blocks in order; a block with deferred matches is loaded into
+// LDS, its deferred matches (in output order) run there, and it is written back.
+__global__ __launch_bounds__(64) void k_zstd_fixup(ZgItem *items, uint32_t *status, const ZBlk *blks,
+                                                   uint32_t blk_cap, const uint32_t *nblk, const uint32_t *zmode,
+                                                   uint8_t *dst, uint64_t slot_bytes, const uint32_t *seq_scratch,
+                                                   uint64_t seq_cap) {
+  __shared__ uint8_t img[BLOCK_MAX];
+  const uint32_t item = blockIdx.x;
+  const int lane = lane_id();
+  if (zmode[item] != ZMODE_PARALLEL || status[item]) return;
+  uint8_t *out = dst + (uint64_t)item * slot_bytes;
+  const ZBlk *B = blks + (uint64_t)item * blk_cap;
+  const uint32_t nb = nblk[item];
+  uint32_t err = 0;
+  uint64_t end = 0, fstart = 0;
+  bool wrote = false;  // this wave has written output: its later loads of earlier blocks use sc1
+  for (uint32_t bi = 0; bi < nb && !err; bi++) {
+    const uint32_t flags = U(B[bi].flags);
+    const uint64_t bstart = U(B[bi].out_off);
+    const uint32_t bsize = U(B[bi].out_size);
+    if (flags & ZBF_FIRST) fstart = bstart;
+    end = bstart + bsize;
+    const uint32_t ndef = (flags & 3) == ZB_CMP ? U(B[bi].def_n) : 0u;
+    if (ndef) {
+      const uint32_t *defl = seq_scratch + ((uint64_t)item * seq_cap + U(B[bi].seq_buf)) * 3;
+      for (uint32_t o = 0; o < bsize; o += ZBATCH)
+        lds_copy_in(img, ~0ull, o, out + bstart + o, min<uint32_t>(ZBATCH, bsize - o));
+      __syncthreads();
+      for (uint32_t k0 = 0; k0 < ndef; k0 += 64) {
+        const uint32_t k = k0 + lane;
+        const bool valid = k < ndef;
+        uint64_t p = 0;
+        uint32_t d = 1, len = 0;
+        if (valid) {
+          p = defl[3 * k];
+          d = defl[3 * k + 1];
+          len = defl[3 * k + 2];
+        }
+        const uint64_t src = p - d;
+        bool pending = valid;
+        uint64_t pm;
+        while ((pm = __ballot(pending)) != 0) {
+          const int first = __builtin_ctzll(pm);
+          const uint32_t F_lo = __builtin_amdgcn_readlane((uint32_t)p, first);
+          const uint32_t F_hi = __builtin_amdgcn_readlane((uint32_t)(p >> 32), first);
+          const uint64_t F = ((uint64_t)F_hi << 32) | F_lo;
+          const uint32_t flen = __builtin_amdgcn_readlane(len, first);
+          if (flen > 32) {  // long: the whole wave copies it
+            const uint32_t fd = __builtin_amdgcn_readlane(d, first);
+            const float inv = 1.0f / (float)fd;
+            for (uint32_t i = lane; i < flen; i += 64) {
+              uint32_t rm = i;
+              if (fd < flen) {
+                uint32_t q = (uint32_t)((float)i * inv);
+                int32_t r = (int32_t)i - (int32_t)(q * fd);
+                if (r < 0) r += fd;
+                if (r >= (int32_t)fd) r -= fd;
+                rm = (uint32_t)r;
+              }
+              const uint64_t sb = F - fd + rm;
+              img[F - bstart + i] = sb >= bstart ? img[sb - bstart] : (wrote ? load_out_byte(out + sb) : out[sb]);
+            }
+            if (lane == first) pending = false;
+            __syncthreads();
+            continue;
+          }
+          const bool ready = pending && len <= 32 && (lane == first || src + len <= F);
+          if (ready) {
+            for (uint32_t i0 = 0; i0 < len; i0 += 4) {
+              uint8_t v[4];
+#pragma unroll
+              for (int j = 0; j < 4; j++) {
+                const uint32_t i = i0 + j;
+                const uint64_t sb = src + (i < d ? i : i % d);
+                v[j] = i < len ? (sb >= bstart ? img[sb - bstart] : (wrote ? load_out_byte(out + sb) : out[sb]))
+                               : (uint8_t)0;
+              }
+#pragma unroll
+              for (int j = 0; j < 4; j++)
+                if (i0 + j < len) img[p - bstart + i0 + j] = v[j];
+            }
+            pending = false;
+          }
+          __syncthreads();
+        }
+      }
+      blk_flush_img(img, out, bstart, bstart + bsize);
+      __builtin_amdgcn_s_waitcnt(0);  // written back before any later load of it
+      __threadfence_block();
+      wrote = true;
+    }
+    if ((flags & ZBF_LAST) && (flags & ZBF_CK)) {
+      __threadfence();
+      const uint64_t h = xxh64(out + fstart, end - fstart);
+      if ((uint32_t)h != U(B[bi].ck)) err = ZG_CORRUPT_STREAM;
+    }
+  }
   if (lane == 0) {
     if (err) {
       status[item] = err;
     } else {
-      items[item].src = (uint64_t)O.out;
-      items[item].len = O.pos;
+      items[item].src = (uint64_t)out;
+      items[item].len = end;
     }
   }
 }
@@ -1608,7 +1997,6 @@ void zstd_scratch_layout(uint64_t slot_bytes, uint32_t &blk_cap, uint64_t &blk_b
   lit_stride = (lit_stride + 255) & ~(uint64_t)255;
   seq_cap = slot_bytes / 4 + 1024;  // sequences per item (each decodes >= 3 bytes; typical >= 8)
 }
-
 hipError_t launch_zstd(ZgItem *items, uint32_t *status, uint32_t n_items, uint8_t *dst, uint64_t slot_bytes,
                        const ZstdScratch &Z, hipStream_t s) {
   if (!n_items) return hipSuccess;
@@ -1619,8 +2007,12 @@ hipError_t launch_zstd(ZgItem *items, uint32_t *status, uint32_t n_items, uint8_
   const uint32_t grid = (uint32_t)std::min<uint64_t>(recs, 256 * 16);
   hipLaunchKernelGGL(k_zstd_blocks, dim3(grid), dim3(64), 0, s, items, status, blks, Z.blk_cap, Z.nblk, Z.mode,
                      n_items, Z.lit, Z.lit_stride, Z.seq, Z.seq_cap);
-  hipLaunchKernelGGL(k_zstd_exec, dim3(n_items), dim3(64), 0, s, items, status, blks, Z.blk_cap, Z.nblk, Z.mode,
-                     dst, slot_bytes, Z.lit, Z.lit_stride, Z.seq, Z.seq_cap);
+  hipLaunchKernelGGL(k_zstd_plan, dim3(n_items), dim3(64), 0, s, items, status, blks, Z.blk_cap, Z.nblk, Z.mode,
+                     slot_bytes);
+  hipLaunchKernelGGL(k_zstd_exec_blocks, dim3(grid), dim3(64), 0, s, items, status, blks, Z.blk_cap, Z.nblk, Z.mode,
+                     n_items, dst, slot_bytes, Z.lit, Z.lit_stride, Z.seq, Z.seq_cap);
+  hipLaunchKernelGGL(k_zstd_fixup, dim3(n_items), dim3(64), 0, s, items, status, blks, Z.blk_cap, Z.nblk, Z.mode,
+                     dst, slot_bytes, Z.seq, Z.seq_cap);
   hipLaunchKernelGGL(k_zstd, dim3(n_items), dim3(64), 0, s, items, status, dst, slot_bytes, Z.lit, Z.lit_stride,
                      Z.mode);
   return hipGetLastError();
