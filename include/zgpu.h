@@ -137,6 +137,10 @@ int zgpu_decode_batch(zgpu_chain *chain, uint32_t ndim, const zgpu_chunk_desc *d
 int zgpu_plan_create(zgpu_chain *chain, uint32_t ndim, const zgpu_chunk_desc *descs, uint64_t n,
                      const uint64_t *out_shape, uint32_t flags, zgpu_plan **out);
 int zgpu_plan_execute(zgpu_plan *plan, void *out, int32_t *status, void *hip_stream);
+/* Wait for the plan's last execute on hip_stream and return its per-chunk statuses (first non-zero
+ * status as the return value): lets independent plans (e.g. the levels of a multiscale pyramid)
+ * run concurrently on separate streams. */
+int zgpu_plan_status(zgpu_plan *plan, int32_t *status, void *hip_stream);
 void zgpu_plan_destroy(zgpu_plan *plan);
 /* Algorithmic HBM bytes of one execute (encoded bytes read + index bytes + decoded bytes
  * written), the figure bench.py prices the roofline with. */

@@ -1,0 +1,51 @@
+// Lab (not product code): cost of 16-B LDS moves on gfx950 by alignment and active lanes, and the
+// clock64 tick rate.
+#include <hip/hip_runtime.h>
+#include <cstdio>
+typedef unsigned int v4u __attribute__((ext_vector_type(4)));
+__global__ void k(int mis_src, int mis_dst, int iters, int active, int pieces, unsigned long long *cyc, unsigned *sink) {
+  __shared__ unsigned char ring[65536];
+  for (int i = threadIdx.x; i < 65536; i += 64) ring[i] = (unsigned char)i;
+  __syncthreads();
+  const unsigned lane = threadIdx.x;
+  const unsigned long long t0 = clock64();
+  for (int it = 0; it < iters; it++) {
+    if ((int)lane < active) {
+      const unsigned so = ((it * 2048 + lane * 128) & 16383) + mis_src;
+      const unsigned dof = 32768 + ((it * 2048 + lane * 128) & 16383) + mis_dst;
+      v4u v[8];
+#pragma unroll
+      for (int j = 0; j < 8; j++) if (j < pieces) __builtin_memcpy(&v[j], &ring[so + 16 * j], 16);
+#pragma unroll
+      for (int j = 0; j < 8; j++) if (j < pieces) __builtin_memcpy(&ring[dof + 16 * j], &v[j], 16);
+    }
+    __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
+  }
+  __syncthreads();
+  const unsigned long long t1 = clock64();
+  if (lane == 0) *cyc = t1 - t0;
+  sink[lane] = ring[lane * 7];
+}
+__global__ void spin(unsigned long long n, unsigned long long *cyc) {
+  const unsigned long long t0 = clock64();
+  unsigned long long t = t0;
+  while (t - t0 < n) t = clock64();
+  if (threadIdx.x == 0) *cyc = t - t0;
+}
+int main() {
+  unsigned long long *c; unsigned *s;
+  hipMalloc(&c, 8); hipMalloc(&s, 256);
+  int cases[][4] = {{0, 0, 64, 1}, {1, 3, 64, 1}, {0, 0, 64, 8}, {1, 3, 64, 8}, {1, 3, 5, 8}, {1, 3, 1, 8}, {0, 0, 1, 8}, {1, 3, 5, 1}};
+  for (auto &cs : cases) {
+    hipLaunchKernelGGL(k, dim3(1), dim3(64), 0, 0, cs[0], cs[1], 1000, cs[2], cs[3], c, s);
+    unsigned long long h; hipMemcpy(&h, c, 8, hipMemcpyDeviceToHost);
+    printf("src+%d dst+%d lanes %d pieces %d: %.1f ticks per iteration\n", cs[0], cs[1], cs[2], cs[3], h / 1000.0);
+  }
+  hipEvent_t e0, e1; hipEventCreate(&e0); hipEventCreate(&e1);
+  hipEventRecord(e0);
+  hipLaunchKernelGGL(spin, dim3(1), dim3(64), 0, 0, 100000000ull, c);
+  hipEventRecord(e1); hipEventSynchronize(e1);
+  float ms; hipEventElapsedTime(&ms, e0, e1);
+  printf("clock64: 1e8 ticks in %.3f ms -> %.3f GHz\n", ms, 1e8 / ms / 1e6);
+  return 0;
+}

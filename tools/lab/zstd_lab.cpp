@@ -2,7 +2,8 @@
 // uint16 blob field + noise, zstd level 3), per-kernel times and, in a ZG_PROFILE build, the
 // per-phase shader-clock profile of k_zstd_exec.
 // Build: hipcc --offload-arch=gfx950 -O3 -std=c++17 -fopenmp [-DZG_PROFILE] -I../../zarrs_amd/csrc \
-//        -x hip -o zstd_lab zstd_lab.cpp -l:libzstd.so.1
+//        -x hip -o zstd_lab zstd_lab.cpp -L../synth -lsynth -Wl,-rpath,'$ORIGIN/../synth' -l:libzstd.so.1
+// Run: ./zstd_lab <chunks> <MiB per chunk> [level] [c5]   (c5: bench-like data, 16 MiB chunks)
 #include <hip/hip_runtime.h>
 
 #include <cmath>
@@ -17,6 +18,8 @@
 
 typedef struct ZSTD_CCtx_s ZSTD_CCtx;
 extern "C" {
+void synth_c5_level0(uint64_t nz, uint64_t ny, uint64_t nx, int nblobs, const float *cz, const float *cy,
+                     const float *cx, const float *sg, const float *amp, uint64_t seed, uint16_t *out, int nthreads);
 unsigned ZSTD_isError(size_t code);
 ZSTD_CCtx *ZSTD_createCCtx(void);
 size_t ZSTD_freeCCtx(ZSTD_CCtx *);
@@ -32,9 +35,42 @@ int main(int argc, char **argv) {
   const int n = argc > 1 ? atoi(argv[1]) : 64;
   const uint64_t chunk = (argc > 2 ? atoll(argv[2]) : 16) << 20;  // bytes
   const int level = argc > 3 ? atoi(argv[3]) : 3;
+  // argv[4] == "c5": chunks [32,512,512] of a bench-like C5 level 0 ([512,1024,1024], 64 blobs)
+  const bool c5 = argc > 4 && !strcmp(argv[4], "c5");
+  std::vector<uint16_t> lvl;
+  if (c5) {
+    std::mt19937_64 g(42);
+    std::uniform_real_distribution<float> u(0.f, 1.f);
+    float cz[64], cy[64], cx[64], sg[64], amp[64];
+    for (int b = 0; b < 64; b++) {
+      cz[b] = 512 * u(g); cy[b] = 1024 * u(g); cx[b] = 1024 * u(g);
+      sg[b] = 4 + 36 * u(g); amp[b] = 300 + 3700 * u(g);
+    }
+    lvl.resize((size_t)512 * 1024 * 1024);
+    synth_c5_level0(512, 1024, 1024, 64, cz, cy, cx, sg, amp, 42, lvl.data(), 16);
+  }
   std::vector<std::vector<uint8_t>> dec(n), enc(n);
 #pragma omp parallel for
   for (int c = 0; c < n; c++) {
+    if (c5) {
+      const int z0 = (c / 4) * 32, y0 = ((c / 2) % 2) * 512, x0 = (c % 2) * 512;
+      const uint64_t cnt = (uint64_t)32 * 512 * 512;
+      dec[c].resize(2 * cnt);
+      uint64_t i = 0;
+      for (int z = 0; z < 32; z++)
+        for (int y = 0; y < 512; y++)
+          for (int x = 0; x < 512; x++, i++) {
+            const uint16_t v = lvl[((uint64_t)(z0 + z) * 1024 + (y0 + y)) * 1024 + (x0 + x)];
+            dec[c][i] = (uint8_t)v;
+            dec[c][cnt + i] = (uint8_t)(v >> 8);
+          }
+      ZSTD_CCtx *cc = ZSTD_createCCtx();
+      ZSTD_CCtx_setParameter(cc, 100, level);
+      enc[c].resize(ZSTD_compressBound(2 * cnt));
+      enc[c].resize(ZSTD_compress2(cc, enc[c].data(), enc[c].size(), dec[c].data(), 2 * cnt));
+      ZSTD_freeCCtx(cc);
+      continue;
+    }
     std::mt19937_64 rng(1234 + c);
     std::normal_distribution<float> nd(0.f, 1.f);
     const uint64_t cnt = chunk / 2;
@@ -81,11 +117,17 @@ int main(int argc, char **argv) {
   CK(hipMalloc(&Z.lit, n * Z.lit_stride));
   CK(hipMalloc(&Z.seq, n * Z.seq_cap * 12));
   constexpr int NK = 6;
-  const char *kn[NK] = {"scan", "blocks", "plan", "exec_blocks", "fixup", "serial"};
+  const char *kn[NK] = {"scan", "lits", "blocks", "plan", "exec_item", "serial"};
   hipEvent_t ev[NK + 1];
   for (auto &evk : ev) CK(hipEventCreate(&evk));
   float best[NK];
   for (auto &bk : best) bk = 1e30f;
+#ifdef ZG_PROFILE
+  {
+    unsigned long long z[8] = {0};
+    CK(hipMemcpyToSymbol(HIP_SYMBOL(zgpu::g_zprof), z, sizeof(z)));
+  }
+#endif
   for (int rep = 0; rep < 3; rep++) {
     CK(hipMemcpy(d_items, items.data(), n * sizeof(ZgItem), hipMemcpyHostToDevice));
     CK(hipMemset(d_status, 0, n * 4));
@@ -95,17 +137,18 @@ int main(int argc, char **argv) {
     hipLaunchKernelGGL(zgpu::k_zstd_scan, dim3(n), dim3(64), 0, 0, d_items, d_status, blks, Z.blk_cap, Z.nblk, Z.mode,
                        Z.lit_stride, Z.seq_cap);
     CK(hipEventRecord(ev[1]));
+    hipLaunchKernelGGL(zgpu::k_zstd_lits, dim3(std::min<uint64_t>((uint64_t)n * Z.blk_cap, 512)),
+                       dim3(zgpu::LIT_THREADS), 0, 0, d_items, d_status, blks, Z.blk_cap, Z.nblk, Z.mode, (uint32_t)n,
+                       Z.lit, Z.lit_stride);
+    CK(hipEventRecord(ev[2]));
     hipLaunchKernelGGL(zgpu::k_zstd_blocks, dim3(grid), dim3(64), 0, 0, d_items, d_status, blks, Z.blk_cap, Z.nblk,
                        Z.mode, (uint32_t)n, Z.lit, Z.lit_stride, Z.seq, Z.seq_cap);
-    CK(hipEventRecord(ev[2]));
+    CK(hipEventRecord(ev[3]));
     hipLaunchKernelGGL(zgpu::k_zstd_plan, dim3(n), dim3(64), 0, 0, d_items, d_status, blks, Z.blk_cap, Z.nblk, Z.mode,
                        chunk);
-    CK(hipEventRecord(ev[3]));
-    hipLaunchKernelGGL(zgpu::k_zstd_exec_blocks, dim3(grid), dim3(64), 0, 0, d_items, d_status, blks, Z.blk_cap,
-                       Z.nblk, Z.mode, (uint32_t)n, d_out, chunk, Z.lit, Z.lit_stride, Z.seq, Z.seq_cap);
     CK(hipEventRecord(ev[4]));
-    hipLaunchKernelGGL(zgpu::k_zstd_fixup, dim3(n), dim3(64), 0, 0, d_items, d_status, blks, Z.blk_cap, Z.nblk,
-                       Z.mode, d_out, chunk, Z.seq, Z.seq_cap);
+    hipLaunchKernelGGL(zgpu::k_zstd_exec_item, dim3(n), dim3(64), 0, 0, d_items, d_status, blks, Z.blk_cap, Z.nblk,
+                       Z.mode, d_out, chunk, Z.lit, Z.lit_stride, Z.seq, Z.seq_cap);
     CK(hipEventRecord(ev[5]));
     hipLaunchKernelGGL(zgpu::k_zstd, dim3(n), dim3(64), 0, 0, d_items, d_status, d_out, chunk, Z.lit, Z.lit_stride,
                        Z.mode);
@@ -131,19 +174,18 @@ int main(int argc, char **argv) {
   }
   double tot = 0;
   for (int k = 0; k < NK; k++) tot += best[k];
-  // deferred-match statistics
-  std::vector<uint8_t> hb((uint64_t)n * Z.blk_cap * blk_bytes);
-  CK(hipMemcpy(hb.data(), Z.blks, hb.size(), hipMemcpyDeviceToHost));
-  uint64_t ndef = 0, nserial = 0;
-  for (int c = 0; c < n; c++)
-    for (uint32_t b = 0; b < nblk[c]; b++) {
-      const zgpu::ZBlk &B = ((const zgpu::ZBlk *)hb.data())[(uint64_t)c * Z.blk_cap + b];
-      if ((B.flags & 3) == 2) { ndef += B.def_n; nserial += B.def_n ? 1 : 0; }
-    }
-  printf("blocks %llu (%.1f/chunk), mode[0]=%u, deferred matches %llu in %llu blocks, bad=%d\n",
-         (unsigned long long)blocks, (double)blocks / n, mode[0], (unsigned long long)ndef,
-         (unsigned long long)nserial, bad);
+  printf("blocks %llu (%.1f/chunk), mode[0]=%u, bad=%d\n", (unsigned long long)blocks, (double)blocks / n, mode[0], bad);
   for (int k = 0; k < NK; k++) printf("  %-12s %8.3f ms\n", kn[k], best[k]);
+#ifdef ZG_PROFILE
+  {
+    unsigned long long z[8];
+    CK(hipMemcpyFromSymbol(z, HIP_SYMBOL(zgpu::g_zprof), sizeof(z)));
+    const double nb = z[4] ? (double)z[4] : 1.0;
+    const double nbt = z[6] ? (double)z[6] : 1.0;
+    printf("exec_item slow matches per batch: n>128 %.2f d<n %.2f d<16 %.2f other %.2f | resolve %.0f rounds %.2f | (other total %llu) | batches %llu"
+           " seqs/batch %.1f\n", z[0] / nbt, z[1] / nbt, z[2] / nbt, z[5] / nbt, z[3] / nbt, z[4] / nbt, z[5], z[6], z[7] / nbt);
+  }
+#endif
   printf("total %.3f ms -> %.2f GB/s decoded\n", tot, (double)n * chunk / tot / 1e6);
   return bad ? 1 : 0;
 }

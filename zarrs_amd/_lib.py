@@ -28,7 +28,7 @@ NO_VALIDATE = 0x4
 EXPORTS = [
     "zgpu_ctx_create", "zgpu_ctx_destroy", "zgpu_last_error", "zgpu_status_name", "zgpu_version",
     "zgpu_chain_create", "zgpu_chain_destroy", "zgpu_chain_element_size", "zgpu_decode_batch",
-    "zgpu_plan_create", "zgpu_plan_execute", "zgpu_plan_destroy", "zgpu_plan_algorithmic_bytes",
+    "zgpu_plan_create", "zgpu_plan_execute", "zgpu_plan_status", "zgpu_plan_destroy", "zgpu_plan_algorithmic_bytes",
     "zgpu_retrieve_array_subset",
 ]
 
@@ -81,6 +81,7 @@ def load() -> C.CDLL:
                                     C.POINTER(C.c_int32), vp]
     L.zgpu_plan_create.argtypes = [vp, u32, C.POINTER(ChunkDesc), u64, P64, u32, C.POINTER(vp)]
     L.zgpu_plan_execute.argtypes = [vp, vp, C.POINTER(C.c_int32), vp]
+    L.zgpu_plan_status.argtypes = [vp, C.POINTER(C.c_int32), vp]
     L.zgpu_plan_destroy.argtypes = [vp]
     L.zgpu_plan_algorithmic_bytes.restype = u64
     L.zgpu_plan_algorithmic_bytes.argtypes = [vp]

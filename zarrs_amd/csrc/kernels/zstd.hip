@@ -91,6 +91,17 @@ __device__ __forceinline__ uint64_t U64(uint64_t x) {
 }
 __device__ __forceinline__ int lane_id() { return __lane_id(); }
 __device__ __forceinline__ uint32_t highbit(uint32_t v) { return 31 - __builtin_clz(v); }  // v > 0
+// LDS hand-off between the lanes of ONE wave (LDS operations of a wave complete in order): a compiler
+// fence and a wave barrier. WS=false keeps the workgroup barrier (1-wave workgroups: the same thing).
+template <bool WS>
+__device__ __forceinline__ void zsync() {
+  if (WS) {
+    __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+  } else {
+    __syncthreads();
+  }
+}
 
 // ---- uniform forward byte access (headers) ----
 struct In {
@@ -100,6 +111,49 @@ struct In {
   __device__ __forceinline__ uint32_t le16(uint64_t i) const { return b(i) | (b(i + 1) << 8); }
   __device__ __forceinline__ uint32_t le24(uint64_t i) const { return le16(i) | (b(i + 2) << 16); }
   __device__ __forceinline__ uint32_t le32(uint64_t i) const { return le24(i) | (b(i + 3) << 24); }
+  __device__ __forceinline__ uint64_t le40(uint64_t i) const { return (uint64_t)le32(i) | ((uint64_t)b(i + 4) << 32); }
+};
+
+// ---- uniform forward byte access through a 256-byte register window (one load per window, not
+// one dependent load per header byte): lane l holds word wk + l of the aligned item buffer ----
+struct InW {
+  const uint32_t *words;
+  uint64_t n, nwords;
+  uint32_t mis;
+  int64_t wk;
+  uint32_t w;
+  __device__ InW(const uint8_t *p, uint64_t n_) : n(n_), wk(-1000000), w(0) {
+    mis = (uint32_t)((uintptr_t)p & 3);
+    words = (const uint32_t *)((uintptr_t)p - mis);
+    nwords = (n_ + mis + 3) / 4;
+  }
+  __device__ __forceinline__ uint32_t b(uint64_t i) {
+    if (i >= n) return 0u;
+    const int64_t k = (int64_t)((i + mis) >> 2);
+    if (k < wk || k >= wk + 64) {
+      wk = k;
+      const uint64_t kl = (uint64_t)k + lane_id();
+      w = kl < nwords ? words[kl] : 0u;
+    }
+    const uint32_t word = U(__builtin_amdgcn_readlane(w, (int)(k - wk)));
+    return (word >> (8 * ((i + mis) & 3))) & 0xFFu;
+  }
+  __device__ __forceinline__ uint32_t le16(uint64_t i) { return b(i) | (b(i + 1) << 8); }
+  __device__ __forceinline__ uint32_t le24(uint64_t i) { return le16(i) | (b(i + 2) << 16); }
+  __device__ __forceinline__ uint32_t le32(uint64_t i) { return le24(i) | (b(i + 3) << 24); }
+  // bytes [i, i + 5) in one go (two readlanes), zero past the item
+  __device__ __forceinline__ uint64_t le40(uint64_t i) {
+    if (i + 5 > n) return (uint64_t)le32(i) | ((uint64_t)b(i + 4) << 32);
+    const int64_t k = (int64_t)((i + mis) >> 2);
+    if (k < wk || k + 1 >= wk + 64) {
+      wk = k;
+      const uint64_t kl = (uint64_t)k + lane_id();
+      w = kl < nwords ? words[kl] : 0u;
+    }
+    const uint64_t v = (uint64_t)U(__builtin_amdgcn_readlane(w, (int)(k - wk))) |
+                       ((uint64_t)U(__builtin_amdgcn_readlane(w, (int)(k - wk + 1))) << 32);
+    return v >> (8 * ((i + mis) & 3));
+  }
 };
 
 // ---- uniform backward bit reader over [lo, hi) bytes of the item input ----
@@ -164,13 +218,13 @@ __device__ __forceinline__ bool bb_overflow(const BitsBack &R) { return R.cur < 
 
 // ---- FSE ----
 // Parse an FSE table description (FSE_readNCount semantics). Returns bytes consumed, 0 on error.
-__device__ uint32_t read_ncount(const In &I, uint64_t off, uint64_t avail, int16_t *norm, uint32_t max_sym,
+template <class IN>
+__device__ uint32_t read_ncount(IN &I, uint64_t off, uint64_t avail, int16_t *norm, uint32_t max_sym,
                                 uint32_t max_log, uint32_t &acc_log, uint32_t &nsym) {
   uint64_t bit = 0;
   auto peek32 = [&](uint64_t b) -> uint32_t {
     const uint64_t byte = off + (b >> 3);
-    const uint64_t w = (uint64_t)I.le32(byte) | ((uint64_t)I.b(byte + 4) << 32);
-    return (uint32_t)(w >> (b & 7));
+    return (uint32_t)(I.le40(byte) >> (b & 7));
   };
   uint32_t bs = peek32(0);
   acc_log = (bs & 15) + 5;
@@ -225,6 +279,7 @@ __device__ uint32_t read_ncount(const In &I, uint64_t off, uint64_t avail, int16
 }
 
 // Build an FSE decoding table from normalized counts (FSE_buildDTable).
+template <bool WS = false>
 __device__ void build_fse(Fse *T, const int16_t *norm, uint32_t nsym, uint32_t acc_log, uint32_t *tmp) {
   const uint32_t size = 1u << acc_log, mask = size - 1;
   const int lane = lane_id();
@@ -249,7 +304,7 @@ __device__ void build_fse(Fse *T, const int16_t *norm, uint32_t nsym, uint32_t a
       } while (pos > high);
     }
   }
-  __syncthreads();
+  zsync<WS>();
   // state info: lane s owns symbol s (nsym <= 64); symbols' next-state counters start at norm[s]
   // (1 for -1 symbols) and advance in increasing table position.
   uint32_t next = 0;
@@ -266,29 +321,31 @@ __device__ void build_fse(Fse *T, const int16_t *norm, uint32_t nsym, uint32_t a
       next++;
     }
   }
-  __syncthreads();
+  zsync<WS>();
   (void)tmp;
 }
 
+template <bool WS = false>
 __device__ void build_fse_rle(Fse *T, uint32_t sym) {
   if (lane_id() == 0) {
     T[0].sym = (uint8_t)sym;
     T[0].nb = 0;
     T[0].base = 0;
   }
-  __syncthreads();
+  zsync<WS>();
 }
 
+template <bool WS = false>
 __device__ void build_fse_default(Fse *T, const int16_t *def, uint32_t nsym, uint32_t acc_log, int16_t *norm,
                                   uint32_t *tmp) {
   for (uint32_t s = lane_id(); s < nsym; s += 64) norm[s] = def[s];
-  __syncthreads();
-  build_fse(T, norm, nsym, acc_log, tmp);
+  zsync<WS>();
+  build_fse<WS>(T, norm, nsym, acc_log, tmp);
 }
 
 // ---- Huffman (literals) ----
 // Parse the tree description and build the decoding table. Returns bytes consumed, 0 on error.
-template <class SM>
+template <class SM, bool WS = false>
 __device__ uint32_t read_huffman(const In &I, uint64_t off, uint64_t avail, SM &S, uint32_t &table_log,
                                  const uint8_t *item, uint64_t item_len) {
   const int lane = lane_id();
@@ -303,15 +360,16 @@ __device__ uint32_t read_huffman(const In &I, uint64_t off, uint64_t avail, SM &
       const uint32_t byte = item[off + 1 + n / 2];
       S.weights[n] = (uint8_t)((n & 1) ? (byte & 15) : (byte >> 4));
     }
-    __syncthreads();
+    zsync<WS>();
   } else {
     used = 1 + hb;
     if (used > avail || hb == 0) return 0;
     uint32_t acc, ns;
-    const uint32_t h = read_ncount(I, off + 1, hb, S.norm, 15, 6, acc, ns);
+    In Ic = I;
+    const uint32_t h = read_ncount(Ic, off + 1, hb, S.norm, 15, 6, acc, ns);
     if (!h) return 0;
-    __syncthreads();
-    build_fse(S.wt, S.norm, ns, acc, S.tmp);
+    zsync<WS>();
+    build_fse<WS>(S.wt, S.norm, ns, acc, S.tmp);
     BitsBack R;
     if (!bb_init(R, item, item_len, off + 1 + h, off + 1 + hb)) return 0;
     uint32_t s1 = bb_read(R, acc), s2 = bb_read(R, acc);
@@ -343,11 +401,11 @@ __device__ uint32_t read_huffman(const In &I, uint64_t off, uint64_t avail, SM &
         break;
       }
     }
-    __syncthreads();
+    zsync<WS>();
   }
   // weights -> table log, implied last weight
   if (lane < 16) S.tmp[lane] = 0;
-  __syncthreads();
+  zsync<WS>();
   uint32_t wsum = 0;
   for (uint32_t n0 = 0; n0 < nw; n0 += 64) {
     const uint32_t n = n0 + lane;
@@ -364,14 +422,14 @@ __device__ uint32_t read_huffman(const In &I, uint64_t off, uint64_t avail, SM &
   if (rest == 0 || (rest & (rest - 1))) return 0;
   const uint32_t last_w = highbit(rest) + 1;
   if (lane == 0) S.weights[nw] = (uint8_t)last_w;
-  __syncthreads();
+  zsync<WS>();
   const uint32_t nsym = nw + 1;
   // rank counts
   for (uint32_t n = lane; n < nsym; n += 64) {
     const uint32_t w = S.weights[n];
     if (w) atomicAdd(&S.tmp[w], 1u);
   }
-  __syncthreads();
+  zsync<WS>();
   uint32_t cnt[13];
   for (int w = 0; w < 13; w++) cnt[w] = w < 16 ? U(S.tmp[w]) : 0u;
   if (cnt[1] < 2 || (cnt[1] & 1)) return 0;
@@ -399,7 +457,7 @@ __device__ uint32_t read_huffman(const In &I, uint64_t off, uint64_t avail, SM &
       }
     }
   }
-  __syncthreads();
+  zsync<WS>();
   // fill: entries of weight class W occupy [start[W], start[W] + cnt[W] * 2^(W-1))
   const uint32_t size = 1u << tl;
   for (uint32_t e = lane; e < size; e += 64) {
@@ -409,7 +467,7 @@ __device__ uint32_t read_huffman(const In &I, uint64_t off, uint64_t avail, SM &
     const uint32_t sym = S.hsorted[sbase[W] + (e - start[W]) / len];
     S.huf[e] = (uint16_t)(((tl + 1 - W) << 8) | sym);
   }
-  __syncthreads();
+  zsync<WS>();
   table_log = tl;
   return used;
 }
@@ -567,6 +625,7 @@ __device__ __forceinline__ uint8_t src_byte(SM &S, const Out &O, uint64_t s, uin
   return (uint8_t)(__hip_atomic_load(w, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) >> (8 * ((uintptr_t)(O.out + s) & 3)));
 }
 typedef unsigned int zv4u __attribute__((ext_vector_type(4)));
+typedef __attribute__((address_space(1))) uint32_t gu32;  // global-memory word (no flat access)
 // Copy n <= ZBATCH bytes of global memory into LDS bytes dst[(pos + k) & mask] with 16-byte loads,
 // every load issued before the first LDS write (a byte loop would pay the memory latency per step).
 // The aligned 16-B blocks never extend past the 16-B block holding the last wanted byte.
@@ -1047,27 +1106,21 @@ __global__ __launch_bounds__(64) void k_zstd(ZgItem *items, uint32_t *status, ui
 // =================================================================================================
 // Block-parallel path (items whose blocks fit the scratch; k_zstd above is the fallback).
 //
-// A zstd frame is a chain of blocks whose sizes are in their 3-byte headers, so both the entropy
-// decoding and most of the sequence execution parallelise over blocks:
+// A zstd frame is a chain of blocks whose sizes are in their 3-byte headers, so the entropy decoding
+// parallelises over blocks; the sequence execution (LZ77 copies, which in real data reach across
+// blocks all the time) runs per item:
 //   k_zstd_scan    one wave per item: walk frames and block headers, parse each compressed block's
 //                  literal / sequence section headers, resolve "treeless" literals and "repeat" FSE
 //                  modes to the block that defined the table; one ZBlk record per block
-//   k_zstd_blocks  one wave per block: Huffman literals into the literal scratch, FSE sequences into
-//                  the sequence scratch. Repeat offsets are resolved symbolically ("incoming rep k,
-//                  minus j"), so no block waits for its predecessor; the block's outgoing rep state
-//                  is kept in the same symbolic form
+//   k_zstd_lits    256 threads per block: Huffman literals into the literal scratch (all lanes
+//                  decode, see the kernel)
+//   k_zstd_blocks  one wave per block: FSE sequences into the sequence scratch. Repeat offsets are
+//                  resolved symbolically ("incoming rep k, minus j"), so no block waits for its
+//                  predecessor; the block's outgoing rep state is kept in the same symbolic form
 //   k_zstd_plan    one wave per item: block output offsets (prefix sum), concrete incoming rep state
 //                  per block (composing the symbolic transforms), frame content size checks
-//   k_zstd_exec_blocks  one wave per block: executes the block into its own output range. A match
-//                  whose source lies in an earlier block, or touches bytes deferred before it (an
-//                  exact per-byte taint bitmap in LDS), is deferred: recorded in place of the
-//                  consumed sequences; everything else is final. Matches of a batch resolve in rounds
-//                  (see k_gzip)
-//   k_zstd_fixup   one wave per item, blocks in order: a block with deferred matches is loaded whole
-//                  into LDS (<= 128 KiB), its deferred matches run there (sources in earlier blocks
-//                  are final by then), and it is written back; then the frame checksums.
-//                  Deferral chains can span a whole frame (a run continuing across blocks), so this
-//                  pass is serial per frame, but it touches only the deferred matches, in LDS
+//   k_zstd_exec_item  one wave per item: sequence execution through a 64 KiB LDS ring, far match
+//                  sources staged per batch; frame checksums
 // =================================================================================================
 namespace {
 
@@ -1093,8 +1146,6 @@ struct ZBlk {
   uint32_t rep_in[3];         // incoming rep offsets (concrete, from k_zstd_plan)
   uint32_t out_off;           // item-relative output offset (k_zstd_plan)
   uint32_t frame_off;         // output offset of the block's frame
-  uint32_t def_n;             // deferred matches recorded by k_zstd_exec_blocks
-  uint32_t def_done;          // deferred matches resolved so far
 };
 
 struct ZScanSmem {
@@ -1117,69 +1168,13 @@ struct ZDecSmem {
   uint32_t tmp[32];
 };
 
-struct ZExecSmem {
-  uint8_t ring[ZRING];
-  uint32_t taint[BLOCK_MAX / 32];  // one bit per output byte of the block: deferred (not yet final)
-  uint8_t lit_stage[ZBATCH];       // the batch's literals, staged with 16-B loads
-  uint32_t pfx_lit[64], pfx_out[64];
-};
 
-// coherent byte read of output this wave (or an earlier kernel) wrote: an agent-scope relaxed
-// atomic load is an sc1 load that bypasses the CU's L1 (MI355X_MICROARCH.md, hand-off table)
-__device__ __forceinline__ uint8_t load_out_byte(const uint8_t *p) {
-  const uint32_t *w = (const uint32_t *)((uintptr_t)p & ~(uintptr_t)3);
-  const uint32_t v = __hip_atomic_load(w, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-  return (uint8_t)(v >> (8 * ((uintptr_t)p & 3)));
-}
 
 __device__ __forceinline__ uint32_t sym_dec(uint32_t x) { return (x & ZSYM) ? x + 1 : x - 1; }
 __device__ __forceinline__ uint32_t sym_eval(uint32_t x, uint32_t r0, uint32_t r1, uint32_t r2) {
   if (!(x & ZSYM)) return x;
   const uint32_t slot = (x >> 24) & 3, minus = x & 0xFFFFFF;
   return (slot == 0 ? r0 : slot == 1 ? r1 : r2) - minus;
-}
-
-// exact-range output flush for a block (its neighbours belong to other waves): bytes [from, to)
-template <class SM>
-__device__ __forceinline__ void blk_flush(SM &S, uint8_t *out, uint64_t from, uint64_t to) {
-  __syncthreads();
-  const uint64_t a = (from + 15) & ~(uint64_t)15, b = to & ~(uint64_t)15;
-  if (a >= b) {
-    for (uint64_t p = from + lane_id(); p < to; p += 64) out[p] = S.ring[p & ZRMASK];
-  } else {
-    for (uint64_t p = from + lane_id(); p < a; p += 64) out[p] = S.ring[p & ZRMASK];
-    for (uint64_t p = a + (uint64_t)lane_id() * 16; p < b; p += 64 * 16)
-      *(uint4 *)(out + p) = *(const uint4 *)&S.ring[p & ZRMASK];
-    for (uint64_t p = b + lane_id(); p < to; p += 64) out[p] = S.ring[p & ZRMASK];
-  }
-  __syncthreads();
-}
-
-// exact-range write-back of a block image img[0, to - from) to out[from, to)
-__device__ __forceinline__ void blk_flush_img(const uint8_t *img, uint8_t *out, uint64_t from, uint64_t to) {
-  __syncthreads();
-  const uint64_t a = (from + 15) & ~(uint64_t)15, b = to & ~(uint64_t)15;
-  if (a >= b) {
-    for (uint64_t p = from + lane_id(); p < to; p += 64) out[p] = img[p - from];
-  } else {
-    for (uint64_t p = from + lane_id(); p < a; p += 64) out[p] = img[p - from];
-    for (uint64_t p = a + (uint64_t)lane_id() * 16; p < b; p += 64 * 16) {
-      const uint8_t *q = img + (p - from);
-      uint4 v;
-      if (((p - from) & 3) == 0) {
-        v = make_uint4(*(const uint32_t *)q, *(const uint32_t *)(q + 4), *(const uint32_t *)(q + 8),
-                       *(const uint32_t *)(q + 12));
-      } else {
-        uint32_t w[4];
-        for (int j = 0; j < 4; j++)
-          w[j] = q[4 * j] | (q[4 * j + 1] << 8) | (q[4 * j + 2] << 16) | ((uint32_t)q[4 * j + 3] << 24);
-        v = make_uint4(w[0], w[1], w[2], w[3]);
-      }
-      *(uint4 *)(out + p) = v;
-    }
-    for (uint64_t p = b + lane_id(); p < to; p += 64) out[p] = img[p - from];
-  }
-  __syncthreads();
 }
 
 }  // namespace
@@ -1200,7 +1195,7 @@ __global__ __launch_bounds__(64) void k_zstd_scan(const ZgItem *items, uint32_t 
     return;
   }
   const uint8_t *in = (const uint8_t *)it.src;
-  const In I{in, it.len};
+  InW I(in, it.len);
   ZBlk *B = blks + (uint64_t)item * blk_cap;
   uint32_t nb = 0, err = 0;
   bool serial = false, any_frame = false;
@@ -1405,65 +1400,10 @@ __global__ __launch_bounds__(64) void k_zstd_blocks(const ZgItem *items, uint32_
     uint8_t *lit = lit_scratch + (uint64_t)item * lit_stride + U(Bp->lit_buf);
     bool bad = false;
     __syncthreads();  // the previous record's table reads are done before they are rebuilt
-    // ---- literals ----
-    if (ltype == 1) {
-      const uint8_t v = (uint8_t)I.b(U(Bp->lit_off));
-      for (uint32_t k = lane; k < regen; k += 64) lit[k] = v;
-    } else if (ltype >= 2) {
-      const uint32_t huf_off = U(Bp->huf_off), lo0 = U(Bp->lit_off), lend = U(Bp->lit_end);
-      uint32_t tl = 0;
-      if (!read_huffman(I, huf_off, it.len - huf_off, S, tl, in, it.len)) {
-        bad = true;
-      } else {
-        const uint32_t nstreams = (flags >> 4) & 1 ? 4 : 1;
-        uint64_t s_lo[4], s_hi[4];
-        uint32_t s_n[4];
-        if (nstreams == 1) {
-          s_lo[0] = lo0; s_hi[0] = lend; s_n[0] = regen;
-        } else {
-          const uint64_t q = lo0;
-          if (q + 6 > lend) bad = true;
-          const uint32_t l1 = I.le16(q), l2 = I.le16(q + 2), l3 = I.le16(q + 4);
-          const uint64_t b = q + 6;
-          if (b + l1 + l2 + l3 > lend) bad = true;
-          s_lo[0] = b; s_hi[0] = b + l1;
-          s_lo[1] = s_hi[0]; s_hi[1] = s_lo[1] + l2;
-          s_lo[2] = s_hi[1]; s_hi[2] = s_lo[2] + l3;
-          s_lo[3] = s_hi[2]; s_hi[3] = lend;
-          const uint32_t seg = (regen + 3) / 4;
-          if (3 * seg > regen) bad = true;
-          s_n[0] = s_n[1] = s_n[2] = seg;
-          s_n[3] = regen - 3 * seg;
-        }
-        uint32_t lbad = 0;
-        if (!bad && lane < (int)nstreams) {
-          const uint64_t lo = lane == 0 ? s_lo[0] : lane == 1 ? s_lo[1] : lane == 2 ? s_lo[2] : s_lo[3];
-          const uint64_t hi = lane == 0 ? s_hi[0] : lane == 1 ? s_hi[1] : lane == 2 ? s_hi[2] : s_hi[3];
-          const uint32_t ns = lane == 0 ? s_n[0] : lane == 1 ? s_n[1] : lane == 2 ? s_n[2] : s_n[3];
-          const uint32_t out0 = nstreams == 4 ? lane * ((regen + 3) / 4) : 0u;
-          const uintptr_t mis = (uintptr_t)in & 3;
-          LaneBits L;
-          L.words = (const uint32_t *)((uintptr_t)in - mis);
-          L.nwords = (uint32_t)((it.len + mis + 3) / 4);
-          const uint32_t lastb = hi > lo ? in[hi - 1] : 0u;
-          if (lastb == 0) {
-            lbad = 1;
-          } else {
-            L.cur = (int64_t)(hi - 1 + mis) * 8 + (31 - __builtin_clz(lastb));
-            L.lo_bit = (int64_t)(lo + mis) * 8;
-            lane_bits_init(L);
-            for (uint32_t k = 0; k < ns; k++) {
-              const uint32_t e = S.huf[lane_peek(L, tl)];
-              L.cur -= e >> 8;
-              lit[out0 + k] = (uint8_t)e;
-              if (L.cur < L.lo_bit) { lbad = 1; break; }
-            }
-            if (L.cur != L.lo_bit) lbad = 1;
-          }
-        }
-        if (__ballot(lbad != 0)) bad = true;
-      }
-    }
+    // literals: k_zstd_lits
+    (void)ltype;
+    (void)regen;
+    (void)lit;
     __syncthreads();  // Huffman table reads done: the FSE tables reuse its LDS
     // ---- sequences ----
     const uint32_t nseq = U(Bp->nseq);
@@ -1485,7 +1425,8 @@ __global__ __launch_bounds__(64) void k_zstd_blocks(const ZgItem *items, uint32_
           lg[t] = 0;
         } else {
           uint32_t acc, ns;
-          if (!read_ncount(I, off, it.len - off, S.norm, maxs, maxl, acc, ns)) { bad = true; break; }
+          In Ic = I;
+          if (!read_ncount(Ic, off, it.len - off, S.norm, maxs, maxl, acc, ns)) { bad = true; break; }
           __syncthreads();
           build_fse(T, S.norm, ns, acc, S.tmp);
           lg[t] = acc;
@@ -1569,6 +1510,268 @@ __global__ __launch_bounds__(64) void k_zstd_blocks(const ZgItem *items, uint32_
   }
 }
 
+// -------------------------------------------------------------------------------------------------
+// Huffman literals, 256 threads per block record. One symbol costs a wave ~15 instructions whoever
+// decodes it, so the four streams are decoded by all 256 lanes: every stream is cut into equal bit
+// segments (64 per stream with 4 streams, 256 with 1), each lane decodes one. A lane that does not
+// start at a known symbol boundary starts LIT_WARM bits early: Huffman decoding self-synchronises,
+// and the lane is known to be right once the first boundary it reaches inside its segment equals the
+// exit boundary of the lane before it (decoding from a boundary is deterministic). Lanes that do not
+// meet are re-decoded from their predecessor's exit (repair rounds). Pass 1 finds every segment's
+// entry, exit and symbol count; pass 2 decodes again and writes the symbols at the prefix-summed
+// offsets. The compressed literal section is staged in LDS first (sections over LIT_LDS read global).
+// -------------------------------------------------------------------------------------------------
+constexpr uint32_t LIT_LDS = 64 * 1024;
+constexpr int32_t LIT_WARM = 128;
+constexpr uint32_t LIT_THREADS = 256;
+
+struct ZLitSmem {
+  uint16_t huf[1 << MAX_HUF_LOG];
+  Fse wt[64];
+  int16_t norm[64];
+  uint8_t weights[256];
+  uint16_t hsorted[256];
+  uint32_t tmp[32];
+  int32_t entry[LIT_THREADS], exit_[LIT_THREADS];
+  uint32_t cnt[LIT_THREADS], wsum[4];
+  uint32_t ctl[4];  // table log, flags
+  uint32_t lin[LIT_LDS / 4 + 8];
+};
+
+// backward bit container: C holds bits [lp, p) of the word array, bit p-1 at C bit 63
+struct HufLane {
+  uint64_t C;
+  int32_t v, lp;
+};
+template <class Wd>
+__device__ __forceinline__ void hl_init(HufLane &H, int32_t p, const Wd &word) {
+  const int32_t k = (p - 1) >> 5;
+  const uint64_t V = ((uint64_t)word(k) << 32) | word(k - 1);
+  H.lp = (k - 1) * 32;
+  H.v = p - H.lp;  // (32, 64]
+  H.C = V << (64 - H.v);
+}
+// decode symbols while p > stop (at most maxn); WRITE: out[k] = symbol k
+template <bool WRITE, class Wd>
+__device__ __forceinline__ uint32_t hl_run(HufLane &H, int32_t &p, int32_t stop, uint32_t tl, const uint16_t *huf,
+                                           const Wd &word, uint8_t *out, uint32_t maxn) {
+  uint32_t n = 0;
+  const uint32_t sh = 64 - tl;
+  while (p > stop && n < maxn) {
+    if (H.v <= 32) {
+      H.C |= (uint64_t)word((H.lp >> 5) - 1) << (32 - H.v);
+      H.v += 32;
+      H.lp -= 32;
+    }
+    const uint32_t e = huf[(uint32_t)(H.C >> sh)];
+    const uint32_t nb = e >> 8;
+    H.C <<= nb;
+    H.v -= (int32_t)nb;
+    p -= (int32_t)nb;
+    if (WRITE) out[n] = (uint8_t)e;
+    n++;
+  }
+  return n;
+}
+
+template <class Wd>
+__device__ bool lits_decode(ZLitSmem &S, const Wd &word, uint32_t nstreams, const int32_t *top, const int32_t *lob,
+                            const uint32_t *nsym, uint32_t tl, uint8_t *lit, uint32_t seg) {
+  const uint32_t t = threadIdx.x;
+  const uint32_t G = LIT_THREADS / nstreams;
+  const uint32_t s = t / G, j = t % G;
+  const int32_t T0 = s == 0 ? top[0] : s == 1 ? top[1] : s == 2 ? top[2] : top[3];
+  const int32_t L0 = s == 0 ? lob[0] : s == 1 ? lob[1] : s == 2 ? lob[2] : lob[3];
+  const uint32_t NS = s == 0 ? nsym[0] : s == 1 ? nsym[1] : s == 2 ? nsym[2] : nsym[3];
+  const int64_t len = (int64_t)T0 - L0;
+  const int32_t tj = T0 - (int32_t)(len * j / G), tj1 = T0 - (int32_t)(len * (j + 1) / G);
+  const uint32_t maxn = NS + 1;  // a segment never holds more symbols than its stream
+  // pass 1: entry / exit / count
+  {
+    HufLane H;
+    int32_t p = j == 0 ? T0 : min(T0, tj + LIT_WARM);
+    hl_init(H, p, word);
+    if (j) hl_run<false>(H, p, tj, tl, S.huf, word, nullptr, 0xFFFFFFFFu);
+    S.entry[t] = p;
+    S.cnt[t] = hl_run<false>(H, p, tj1, tl, S.huf, word, nullptr, maxn);
+    S.exit_[t] = p;
+  }
+  __syncthreads();
+  // repair rounds: a lane whose entry is not its predecessor's exit re-decodes from that exit once
+  // the predecessor is right (a lane is right when its entry is right)
+  for (uint32_t round = 0; round < G; round++) {
+    const bool wrong = j != 0 && S.entry[t] != S.exit_[t - 1];
+    const bool pred_ok = j <= 1 || S.entry[t - 1] == S.exit_[t - 2];
+    __syncthreads();
+    int32_t ne = 0, nx = 0;
+    uint32_t nc = 0;
+    const bool fix = wrong && pred_ok;
+    if (fix) {
+      HufLane H;
+      int32_t p = S.exit_[t - 1];
+      ne = p;
+      hl_init(H, p, word);
+      nc = hl_run<false>(H, p, tj1, tl, S.huf, word, nullptr, maxn);
+      nx = p;
+    }
+    if (__syncthreads_or(wrong) == 0) break;
+    if (fix) {
+      S.entry[t] = ne;
+      S.exit_[t] = nx;
+      S.cnt[t] = nc;
+    }
+    __syncthreads();
+  }
+  // every lane right now; per-stream symbol count and exact end
+  uint32_t c = S.cnt[t];
+  const uint32_t lane = lane_id();
+  uint32_t incl = c;
+  for (int o = 1; o < 64; o <<= 1) {
+    const uint32_t u = __shfl_up(incl, o, 64);
+    if ((int)lane >= o) incl += u;
+  }
+  if (lane == 63) S.wsum[t >> 6] = incl;
+  __syncthreads();
+  uint32_t base = 0;
+  if (nstreams == 1)
+    for (uint32_t w = 0; w < (t >> 6); w++) base += S.wsum[w];
+  const uint32_t off = base + incl - c;
+  uint32_t total = 0;
+  if (nstreams == 1) total = S.wsum[0] + S.wsum[1] + S.wsum[2] + S.wsum[3];
+  else total = S.wsum[s];
+  bool bad = total != NS || S.entry[t] != (j == 0 ? T0 : S.exit_[t - 1]);
+  if (j == G - 1 && S.exit_[t] != L0) bad = true;
+  if (__syncthreads_or(bad)) return false;
+  // pass 2: decode again, writing
+  if (c) {
+    HufLane H;
+    int32_t p = S.entry[t];
+    hl_init(H, p, word);
+    hl_run<true>(H, p, tj1, tl, S.huf, word, lit + (uint64_t)s * seg + off, c);
+  }
+  return true;
+}
+
+__global__ __launch_bounds__(LIT_THREADS) void k_zstd_lits(const ZgItem *items, uint32_t *status, const ZBlk *blks,
+                                                           uint32_t blk_cap, const uint32_t *nblk,
+                                                           const uint32_t *zmode, uint32_t n_items,
+                                                           uint8_t *lit_scratch, uint64_t lit_stride) {
+  __shared__ ZLitSmem S;
+  const uint32_t t = threadIdx.x;
+  const uint64_t total = (uint64_t)n_items * blk_cap;
+  for (uint64_t g = blockIdx.x; g < total; g += gridDim.x) {
+    const uint32_t item = (uint32_t)(g / blk_cap), bi = (uint32_t)(g % blk_cap);
+    if (bi >= nblk[item] || zmode[item] != ZMODE_PARALLEL) continue;
+    const ZBlk *Bp = blks + g;
+    const uint32_t flags = Bp->flags;
+    const uint32_t ltype = (flags >> 2) & 3;
+    if ((flags & 3) != ZB_CMP || ltype == 0) continue;
+    const ZgItem it = items[item];
+    const uint8_t *in = (const uint8_t *)it.src;
+    const uint32_t regen = Bp->regen;
+    uint8_t *lit = lit_scratch + (uint64_t)item * lit_stride + Bp->lit_buf;
+    __syncthreads();  // the previous record's LDS use is over
+    if (ltype == 1) {  // RLE literals
+      const uint8_t v = in[Bp->lit_off];
+      for (uint32_t k = t; k < regen; k += LIT_THREADS) lit[k] = v;
+      continue;
+    }
+    const uint32_t huf_off = Bp->huf_off, lo0 = Bp->lit_off, lend = Bp->lit_end;
+    if (t < 64) {  // wave 0 builds the table
+      const In I{in, it.len};
+      uint32_t tl = 0;
+      const uint32_t ok = read_huffman<ZLitSmem, true>(I, huf_off, it.len - huf_off, S, tl, in, it.len);
+      if (t == 0) {
+        S.ctl[0] = ok ? tl : 0u;
+      }
+    }
+    __syncthreads();
+    const uint32_t tl = S.ctl[0];
+    bool bad = tl == 0;
+    const uint32_t nstreams = (flags >> 4) & 1 ? 4 : 1;
+    uint64_t s_lo[4] = {lo0, 0, 0, 0}, s_hi[4] = {lend, 0, 0, 0};
+    uint32_t s_n[4] = {regen, 0, 0, 0};
+    const uint32_t seg = (regen + 3) / 4;
+    if (!bad && nstreams == 4) {
+      const uint64_t q = lo0;
+      if (q + 6 > lend) bad = true;
+      const uint32_t l1 = in[q] | (in[q + 1] << 8), l2 = in[q + 2] | (in[q + 3] << 8), l3 = in[q + 4] | (in[q + 5] << 8);
+      const uint64_t b = q + 6;
+      if (b + l1 + l2 + l3 > lend) bad = true;
+      s_lo[0] = b; s_hi[0] = b + l1;
+      s_lo[1] = s_hi[0]; s_hi[1] = s_lo[1] + l2;
+      s_lo[2] = s_hi[1]; s_hi[2] = s_lo[2] + l3;
+      s_lo[3] = s_hi[2]; s_hi[3] = lend;
+      if (3 * seg > regen) bad = true;
+      s_n[0] = s_n[1] = s_n[2] = seg;
+      s_n[3] = regen - 3 * seg;
+    }
+    // bit positions relative to the staged (or global) word base
+    const uintptr_t mis = (uintptr_t)in & 3;
+    const uint32_t *words = (const uint32_t *)((uintptr_t)in - mis);
+    const int64_t nwords_item = (int64_t)((it.len + mis + 3) / 4);
+    const int64_t wbase = (int64_t)((s_lo[0] + mis) >> 2);          // first word of the section
+    const int64_t wend = (int64_t)(((nstreams == 4 ? s_hi[3] : s_hi[0]) + mis + 3) >> 2);  // one past its last word
+    int32_t top[4] = {0, 0, 0, 0}, lob[4] = {0, 0, 0, 0};
+#pragma unroll
+    for (uint32_t k = 0; k < 4; k++) {
+      if (k < nstreams && !bad) {
+        const uint32_t lastb = s_hi[k] > s_lo[k] ? in[s_hi[k] - 1] : 0u;
+        if (lastb == 0) bad = true;
+        top[k] = (int32_t)((int64_t)(s_hi[k] - 1 + mis) * 8 + (lastb ? highbit(lastb) : 0u) - wbase * 32);
+        lob[k] = (int32_t)((int64_t)(s_lo[k] + mis) * 8 - wbase * 32);
+      }
+    }
+    bool ok = false;
+    if (!bad) {
+      const int64_t nw = wend - wbase;
+      if (nw * 4 <= (int64_t)LIT_LDS) {
+        // 16-B loads, 8 per thread in flight before the first LDS write
+        const int64_t a16 = wbase & ~(int64_t)3, n16 = (wend - a16 + 3) >> 2;
+        const uint32_t sh = (uint32_t)(wbase - a16);  // words of the first vector before the section
+        for (int64_t v0 = 0; v0 < n16; v0 += 8 * LIT_THREADS) {
+          zv4u r[8];
+#pragma unroll
+          for (int q = 0; q < 8; q++) {
+            const int64_t v = v0 + q * LIT_THREADS + t;
+            if (v < n16) {
+              const gu32 *src = (const gu32 *)(words + a16 + 4 * v);
+              if (a16 + 4 * v + 4 <= nwords_item) {
+                r[q] = *(const __attribute__((address_space(1))) zv4u *)src;
+              } else {  // the item's last words: never read past its end
+                const int64_t lim = nwords_item - (a16 + 4 * v);
+                r[q] = zv4u{src[0], lim > 1 ? src[1] : 0u, lim > 2 ? src[2] : 0u, 0u};
+              }
+            }
+          }
+#pragma unroll
+          for (int q = 0; q < 8; q++) {
+            const int64_t v = v0 + q * LIT_THREADS + t;
+            if (v < n16) {
+              const uint32_t w4[4] = {r[q].x, r[q].y, r[q].z, r[q].w};
+#pragma unroll
+              for (int e = 0; e < 4; e++) {
+                const int64_t k = 4 * v + e - sh;
+                if (k >= 0 && k < nw) S.lin[k] = w4[e];
+              }
+            }
+          }
+        }
+        __syncthreads();
+        const int32_t n32 = (int32_t)nw;
+        auto word = [n32](int32_t k) -> uint32_t { return (k >= 0 && k < n32) ? S.lin[k] : 0u; };
+        ok = lits_decode(S, word, nstreams, top, lob, s_n, tl, lit, seg);
+      } else {
+        const gu32 *Wp = (const gu32 *)(words + wbase);
+        const int64_t lim = nwords_item - wbase;
+        auto word = [Wp, lim](int32_t k) -> uint32_t { return (k >= 0 && k < lim) ? Wp[k] : 0u; };
+        ok = lits_decode(S, word, nstreams, top, lob, s_n, tl, lit, seg);
+      }
+    }
+    if (!ok && t == 0) status[item] = ZG_CORRUPT_STREAM;
+  }
+}
+
 // One wave per item: output offsets, incoming rep offsets, frame size checks.
 __global__ __launch_bounds__(64) void k_zstd_plan(const ZgItem *items, uint32_t *status, ZBlk *blks,
                                                   uint32_t blk_cap, const uint32_t *nblk, const uint32_t *zmode,
@@ -1621,370 +1824,560 @@ __global__ __launch_bounds__(64) void k_zstd_plan(const ZgItem *items, uint32_t 
   if (lane == 0 && err) status[item] = err;
 }
 
-// One wave per (item, block) record, grid-stride: execute the block into its output range.
-__global__ __launch_bounds__(64) void k_zstd_exec_blocks(const ZgItem *items, uint32_t *status, ZBlk *blks,
-                                                         uint32_t blk_cap, const uint32_t *nblk,
-                                                         const uint32_t *zmode, uint32_t n_items, uint8_t *dst,
-                                                         uint64_t slot_bytes, const uint8_t *lit_scratch,
-                                                         uint64_t lit_stride, const uint32_t *seq_scratch,
-                                                         uint64_t seq_cap) {
-  __shared__ ZExecSmem S;
+namespace {
+// -------------------------------------------------------------------------------------------------
+// k_zstd_exec_item: one wave per item executes its blocks in order from the decoded sequences and
+// literals. A 64 KiB LDS ring holds the recent output; a match reaching further back reads output
+// this wave already flushed, staged into LDS per batch by 16-B loads issued together with the
+// batch's literal loads: one memory round trip per batch, not one per match. A batch is up to 64
+// sequences spanning <= ZBATCH bytes; its matches resolve in rounds: every pending match whose
+// source lies before the first unresolved one is copied by the whole wave, one after another.
+// (Matches crossing block boundaries are the rule in real data, e.g. byte-shuffled u16 images
+// whose high-byte plane is a chain of row- and plane-periodic copies, so there is no block-level
+// parallelism to take here; it is taken in k_zstd_lits / k_zstd_blocks, and across items.)
+// -------------------------------------------------------------------------------------------------
+constexpr uint32_t XRING = 65536, XRMASK = XRING - 1;
+constexpr uint32_t XSTAGE_V = 512;  // staged far-source vectors (16 B) per batch
+constexpr int XR_LIT = ZBATCH / 16 / 64 + 1, XR_FAR = XSTAGE_V / 64;
+
+struct XReady {
+  uint64_t ms, fe;
+  int64_t sb;
+  uint32_t d, n;
+};
+struct ZXSmem {
+  uint8_t ring[XRING];
+  zv4u stage[XSTAGE_V];
+  uint8_t lit_stage[ZBATCH + 16];
+  uint32_t pfx_lit[64], pfx_out[64], pfx_nv[64], own_pv[64];
+  uint64_t own_v0[64];
+  XReady rq[64];        // the round's ready matches
+  uint32_t rq_pfx[64];  // their inclusive 16-B piece counts
+};
+
+struct XOut {
+  uint8_t *out;
+  uint64_t pos, flushed;
+};
+
+__device__ __forceinline__ uint64_t rl64(uint64_t v, int i) {
+  return (uint64_t)U(__builtin_amdgcn_readlane((uint32_t)v, i)) |
+         ((uint64_t)U(__builtin_amdgcn_readlane((uint32_t)(v >> 32), i)) << 32);
+}
+
+// ring bytes [flushed, pos) -> the item slot
+__device__ __forceinline__ void x_flush(ZXSmem &S, XOut &O) {
+  __syncthreads();
+  const uint64_t from = O.flushed, to = O.pos;
+  const uint64_t a = min<uint64_t>((from + 15) & ~(uint64_t)15, to), b = max<uint64_t>(to & ~(uint64_t)15, a);
+  for (uint64_t p = from + lane_id(); p < a; p += 64) O.out[p] = S.ring[p & XRMASK];
+  for (uint64_t p = a + (uint64_t)lane_id() * 16; p < b; p += 64 * 16)
+    *(zv4u *)(O.out + p) = *(const zv4u *)&S.ring[p & XRMASK];
+  for (uint64_t p = b + lane_id(); p < to; p += 64) O.out[p] = S.ring[p & XRMASK];
+  O.flushed = to;
+  __syncthreads();
+}
+// before producing output up to wend: at most half the ring stays unflushed
+__device__ __forceinline__ void x_reserve(ZXSmem &S, XOut &O, uint64_t wend) {
+  if (wend - O.flushed > XRING / 2) x_flush(S, O);
+}
+// Sources below the bound are read from the slot: flushed, in whole 128-B lines (so no L1 line can
+// hold a byte written after the line was loaded). Sources at or above it are still in the ring and
+// are not overwritten by a batch ending at wend (<= ZBATCH past the current position).
+__device__ __forceinline__ uint64_t x_far_bound(const XOut &O, uint64_t wend) {
+  const uint64_t lim = wend + ZBATCH > XRING ? wend + ZBATCH - XRING : 0;
+  return min<uint64_t>(lim, O.flushed) & ~(uint64_t)127;
+}
+// n bytes of global memory into the ring at the output position, 8 KiB pieces (every load of a
+// piece in flight before its first LDS write)
+constexpr uint32_t XPIECE = 8192;
+__device__ __forceinline__ void x_copy(ZXSmem &S, XOut &O, const uint8_t *src, uint64_t n) {
+  constexpr int R = XPIECE / 16 / 64 + 1;
+  for (uint64_t done = 0; done < n;) {
+    const uint32_t c = (uint32_t)min<uint64_t>(n - done, XPIECE);
+    x_reserve(S, O, O.pos + c);
+    const uint8_t *sp = src + done;
+    const uintptr_t base = (uintptr_t)sp & ~(uintptr_t)15;
+    const uint32_t head = (uint32_t)((uintptr_t)sp - base);
+    const uint32_t nvec = (head + c + 15) >> 4;
+    zv4u v[R];
+#pragma unroll
+    for (int r = 0; r < R; r++) {
+      const uint32_t idx = lane_id() + 64 * r;
+      if (idx < nvec) v[r] = __builtin_nontemporal_load((const zv4u *)(base + 16ull * idx));
+    }
+#pragma unroll
+    for (int r = 0; r < R; r++) {
+      const uint32_t idx = lane_id() + 64 * r;
+      if (idx < nvec) {
+        const int64_t k0 = (int64_t)(16 * idx) - head;  // output byte of the vector's first byte
+        const uint64_t q = O.pos + k0;
+        if (k0 >= 0 && k0 + 16 <= (int64_t)c && (q & XRMASK) <= XRING - 16) {
+          __builtin_memcpy(&S.ring[q & XRMASK], &v[r], 16);
+        } else {
+          const uint32_t w[4] = {v[r].x, v[r].y, v[r].z, v[r].w};
+#pragma unroll
+          for (int j = 0; j < 16; j++) {
+            const int64_t k = k0 + j;
+            if (k >= 0 && k < (int64_t)c) S.ring[(O.pos + k) & XRMASK] = (uint8_t)(w[j >> 2] >> (8 * (j & 3)));
+          }
+        }
+      }
+    }
+    O.pos += c;
+    done += c;
+  }
+  __syncthreads();
+}
+__device__ __forceinline__ void x_fill(ZXSmem &S, XOut &O, uint8_t v, uint64_t n) {
+  for (uint64_t done = 0; done < n;) {
+    const uint64_t c = min<uint64_t>(n - done, ZBATCH);
+    x_reserve(S, O, O.pos + c);
+    for (uint64_t k = lane_id(); k < c; k += 64) S.ring[(O.pos + k) & XRMASK] = v;
+    O.pos += c;
+    done += c;
+  }
+  __syncthreads();
+}
+
+// The lanes with n > 0 hold matches {ms, d, n} (sources before ms). Stage their far parts (below fb)
+// and the batch's n_lit literals from lit, all loads in flight together. Returns false (nothing
+// staged) if the far parts exceed the stage. fe / sb: the lane's far end and stage byte offset.
+__device__ __forceinline__ bool x_stage(ZXSmem &S, const uint8_t *out, uint64_t fb, uint64_t ms, uint32_t d,
+                                        uint32_t n, const uint8_t *lit, uint32_t n_lit, uint64_t &fe, int64_t &sb) {
   const int lane = lane_id();
-  const uint64_t total = (uint64_t)n_items * blk_cap;
-  for (uint64_t g = blockIdx.x; g < total; g += gridDim.x) {
-    const uint32_t item = (uint32_t)(g / blk_cap), bi = (uint32_t)(g % blk_cap);
-    if (bi >= nblk[item] || zmode[item] != ZMODE_PARALLEL || status[item]) continue;
-    ZBlk *Bp = blks + g;
-    const ZgItem it = items[item];
-    const uint8_t *in = (const uint8_t *)it.src;
-    uint8_t *out = dst + (uint64_t)item * slot_bytes;
-    const uint32_t flags = U(Bp->flags), type = flags & 3;
-    const uint64_t bstart = U(Bp->out_off);
-    const uint32_t out_size = U(Bp->out_size);
-    __syncthreads();  // the previous record's LDS use is over
-    if (type != ZB_CMP) {  // raw / rle: no dependencies
-      Out O{out, bstart + out_size, bstart, bstart, false};
-      if (type == ZB_RAW) out_copy_global(S, O, in + U(Bp->in_off), out_size);
-      else if (type == ZB_RLE) out_rle(S, O, (uint8_t)U(in[U(Bp->in_off)]), out_size);
-      blk_flush(S, out, O.flushed, O.pos);
-      continue;
-    }
-    uint32_t err = 0;
-    const uint32_t ltype = (flags >> 2) & 3, regen = U(Bp->regen), nseq = U(Bp->nseq);
-    const uint8_t *lsrc = ltype == 0 ? in + U(Bp->lit_off) : lit_scratch + (uint64_t)item * lit_stride + U(Bp->lit_buf);
-    const uint32_t *seqs = seq_scratch + ((uint64_t)item * seq_cap + U(Bp->seq_buf)) * 3;
-    // deferred matches {pos, distance, length} overwrite the block's already consumed sequences
-    uint32_t *defl = const_cast<uint32_t *>(seqs);
-    const uint32_t ri0 = U(Bp->rep_in[0]), ri1 = U(Bp->rep_in[1]), ri2 = U(Bp->rep_in[2]);
-    const uint64_t frame_off = U(Bp->frame_off);
-    for (uint32_t k = lane; k < BLOCK_MAX / 32; k += 64) S.taint[k] = 0;
-    __syncthreads();
-    Out O{out, bstart + out_size, bstart, bstart, false};
-    uint32_t ndef = 0;
-    uint64_t litpos = 0;
-    uint32_t base = 0;
-    // taint test of block-relative byte range [a, b) (a < b): any deferred byte in it?
-    auto tainted = [&](uint64_t a, uint64_t b) -> bool {
-      for (uint64_t w = a >> 5; w <= (b - 1) >> 5; w++) {
-        uint32_t m = S.taint[w];
-        const uint32_t lo = w == (a >> 5) ? (uint32_t)(a & 31) : 0u;
-        const uint32_t hi = w == ((b - 1) >> 5) ? (uint32_t)((b - 1) & 31) : 31u;
-        m &= (hi == 31 ? 0xFFFFFFFFu : ((1u << (hi + 1)) - 1)) & ~((1u << lo) - 1);
-        if (m) return true;
-      }
-      return false;
-    };
-    auto mark = [&](uint64_t a, uint64_t b) {  // block-relative [a, b), this lane only
-      for (uint64_t w = a >> 5; w <= (b - 1) >> 5; w++) {
-        const uint32_t lo = w == (a >> 5) ? (uint32_t)(a & 31) : 0u;
-        const uint32_t hi = w == ((b - 1) >> 5) ? (uint32_t)((b - 1) & 31) : 31u;
-        atomicOr(&S.taint[w], (hi == 31 ? 0xFFFFFFFFu : ((1u << (hi + 1)) - 1)) & ~((1u << lo) - 1));
-      }
-    };
-    while (base < nseq && !err) {
-      const uint32_t avail = min<uint32_t>(64, nseq - base);
-      uint32_t r_ll = 0, r_ml = 0, r_of = 0;
-      if (lane < (int)avail) {
-        const uint32_t *q = seqs + (uint64_t)(base + lane) * 3;
-        r_ll = q[0];
-        r_ml = q[1];
-        r_of = sym_eval(q[2], ri0, ri1, ri2);
-      }
-      // batch: consecutive sequences up to ZBATCH bytes; a big one (>= ZBIG) goes alone
-      uint32_t cnt = 0;
-      uint64_t span = 0, lspan = 0;
-      bool big = false;
-      while (cnt < avail) {
-        const uint32_t ll = __builtin_amdgcn_readlane(r_ll, cnt), ml = __builtin_amdgcn_readlane(r_ml, cnt);
-        if (ll >= ZBIG || ml >= ZBIG) {
-          big = cnt == 0;
-          if (big) cnt = 1;
-          break;
-        }
-        if (span + ll + ml > ZBATCH) break;
-        cnt++;
-        span += ll + ml;
-        lspan += ll;
-      }
-      if (big) {
-        span = (uint64_t)__builtin_amdgcn_readlane(r_ll, 0) + __builtin_amdgcn_readlane(r_ml, 0);
-        lspan = __builtin_amdgcn_readlane(r_ll, 0);
-      }
-      const uint64_t out_base = O.pos;
-      if (out_base + span > O.cap) { err = ZG_CORRUPT_STREAM; break; }
-      if (litpos + lspan > regen) { err = ZG_CORRUPT_STREAM; break; }
-      const bool mine = lane < (int)cnt;
-      const uint32_t sll = mine ? r_ll : 0u, sml = mine ? r_ml : 0u;
-      uint32_t a = sll, b = sll + sml;
-      for (int o = 1; o < 64; o <<= 1) {
-        const uint32_t ta = __shfl_up(a, o, 64), tb = __shfl_up(b, o, 64);
-        if (lane >= o) { a += ta; b += tb; }
-      }
-      const uint64_t mstart = out_base + b - sml;
-      if (__ballot(mine && sml && (r_of == 0 || (uint64_t)r_of > mstart - frame_off))) { err = ZG_CORRUPT_STREAM; break; }
-      if (big) {
-        // literal run then a long match, each through the ring in ZBATCH pieces
-        const uint32_t bll = __builtin_amdgcn_readlane(r_ll, 0), bml = __builtin_amdgcn_readlane(r_ml, 0);
-        const uint32_t bof = __builtin_amdgcn_readlane(r_of, 0);
-        out_copy_global(S, O, lsrc + litpos, bll);
-        litpos += bll;
-        if (bml) {
-          const uint64_t p = O.pos, src = p - bof;
-          bool tnt = src < bstart;
-          if (!tnt) {
-            const uint64_t ra = src - bstart, rb = ra + min<uint64_t>(bml, bof);
-            bool t = false;
-            for (uint64_t w0 = (ra >> 5) + lane; w0 <= ((rb - 1) >> 5); w0 += 64) t |= tainted(max<uint64_t>(ra, w0 << 5), min<uint64_t>(rb, (w0 + 1) << 5));
-            tnt = __ballot(t) != 0;
-          }
-          if (tnt) {  // defer the whole match
-            for (uint64_t w0 = ((p - bstart) >> 5) + lane; w0 <= ((p - bstart + bml - 1) >> 5); w0 += 64)
-              mark(max<uint64_t>(p - bstart, w0 << 5), min<uint64_t>(p - bstart + bml, (w0 + 1) << 5));
-            if (lane == 0) { defl[3 * ndef] = (uint32_t)p; defl[3 * ndef + 1] = bof; defl[3 * ndef + 2] = bml; }
-            ndef++;
-            for (uint64_t done = 0; done < bml;) {  // keep the ring positions consistent (garbage)
-              const uint64_t c = min<uint64_t>(bml - done, ZBATCH);
-              out_reserve(S, O, c);
-              O.pos += c;
-              done += c;
-            }
-            __syncthreads();
-          } else {
-            out_match(S, O, bof, bml);
-          }
-        }
-        base += 1;
-        continue;
-      }
-      // ---- regular batch ----
-      out_reserve(S, O, span);
-      S.pfx_lit[lane] = a;
-      S.pfx_out[lane] = b;
-      const uint32_t Lb = (uint32_t)lspan;
-      lds_copy_in(S.lit_stage, ~0ull, 0, lsrc + litpos, Lb);
-      __syncthreads();
-      for (uint32_t k = lane; k < Lb; k += 64) {
-        uint32_t lo2 = 0, hi2 = cnt - 1;  // first sequence with pfx_lit > k
-        while (lo2 < hi2) {
-          const uint32_t mid = (lo2 + hi2) >> 1;
-          if (S.pfx_lit[mid] > k) hi2 = mid; else lo2 = mid + 1;
-        }
-        const uint32_t prev_lit = lo2 ? S.pfx_lit[lo2 - 1] : 0u, prev_out = lo2 ? S.pfx_out[lo2 - 1] : 0u;
-        S.ring[(out_base + prev_out + (k - prev_lit)) & ZRMASK] = S.lit_stage[k];
-      }
-      const uint64_t wend = out_base + span;
-      const uint64_t msrc = mstart - r_of;
-      if (__ballot(mine && sml > 0 && msrc + ZRING < wend)) out_fence(O);
-      bool pending = mine && sml > 0, deferred = false;
-      uint64_t pm;
-      while ((pm = __ballot(pending)) != 0) {
-        const int first = __builtin_ctzll(pm);
-        const uint32_t F_lo = __builtin_amdgcn_readlane((uint32_t)mstart, first);
-        const uint32_t F_hi = __builtin_amdgcn_readlane((uint32_t)(mstart >> 32), first);
-        const uint64_t F = ((uint64_t)F_hi << 32) | F_lo;
-        const uint32_t flen = __builtin_amdgcn_readlane(sml, first);
-        const bool ready = pending && (lane == first || (sml <= 32 && msrc + sml <= F));
-        // taint: source in an earlier block, or touching a deferred byte
-        bool tnt = false;
-        if (ready) {
-          if (msrc < bstart) {
-            tnt = true;
-          } else if (sml <= 32 || lane != first) {
-            tnt = tainted(msrc - bstart, msrc - bstart + min<uint32_t>(sml, r_of));
-          }
-        }
-        if (flen > 32) {  // the first pending match is long: taint-check and copy cooperatively
-          const uint32_t fd = __builtin_amdgcn_readlane(r_of, first);
-          bool ft = __builtin_amdgcn_readlane((uint32_t)tnt, first) != 0;
-          if (!ft) {
-            const uint64_t ra = F - fd - bstart, rb = ra + min<uint32_t>(flen, fd);
-            bool t = false;
-            for (uint64_t w0 = (ra >> 5) + lane; w0 <= ((rb - 1) >> 5); w0 += 64)
-              t |= tainted(max<uint64_t>(ra, w0 << 5), min<uint64_t>(rb, (w0 + 1) << 5));
-            ft = __ballot(t) != 0;
-          }
-          if (ft) {
-            for (uint64_t w0 = ((F - bstart) >> 5) + lane; w0 <= ((F - bstart + flen - 1) >> 5); w0 += 64)
-              mark(max<uint64_t>(F - bstart, w0 << 5), min<uint64_t>(F - bstart + flen, (w0 + 1) << 5));
-            if (lane == first) deferred = true;
-          } else {
-            const float inv = 1.0f / (float)fd;
-            for (uint32_t i = lane; i < flen; i += 64) {
-              uint32_t rm = i;
-              if (fd < flen) {
-                uint32_t q = (uint32_t)((float)i * inv);
-                int32_t r = (int32_t)i - (int32_t)(q * fd);
-                if (r < 0) r += fd;
-                if (r >= (int32_t)fd) r -= fd;
-                rm = (uint32_t)r;
-              }
-              S.ring[(F + i) & ZRMASK] = src_byte(S, O, F - fd + rm, wend);
-            }
-          }
-          if (lane == first) pending = false;
-          __syncthreads();
-          continue;
-        }
-        if (ready) {
-          if (tnt) {
-            mark(mstart - bstart, mstart - bstart + sml);
-            deferred = true;
-          } else {
-            for (uint32_t i0 = 0; i0 < sml; i0 += 4) {
-              uint8_t v[4];
+  const uint64_t src = ms - d;
+  const uint32_t cl = min(n, d);
+  fe = n ? min<uint64_t>(src + cl, fb) : 0;
+  const bool far = n && fe > src;
+  const uint64_t v0 = src >> 4;
+  const uint32_t nv = far ? (uint32_t)(((fe + 15) >> 4) - v0) : 0u;
+  uint32_t incl = nv;
+  for (int o = 1; o < 64; o <<= 1) {
+    const uint32_t u = __shfl_up(incl, o, 64);
+    if (lane >= o) incl += u;
+  }
+  const uint32_t total = U(__builtin_amdgcn_readlane(incl, 63));
+  if (total > XSTAGE_V) return false;
+  const uint32_t pv = incl - nv;
+  sb = (int64_t)pv * 16 - (int64_t)v0 * 16;
+  S.pfx_nv[lane] = incl;
+  S.own_pv[lane] = pv;
+  S.own_v0[lane] = v0;
+  __syncthreads();
+  const uintptr_t lbase = (uintptr_t)lit & ~(uintptr_t)15;
+  const uint32_t lhead = (uint32_t)((uintptr_t)lit - lbase);
+  const uint32_t lvec = n_lit ? (lhead + n_lit + 15) >> 4 : 0u;
+  zv4u lv[XR_LIT], fv[XR_FAR];
 #pragma unroll
-              for (int k = 0; k < 4; k++) {
-                const uint32_t i = i0 + k;
-                const uint32_t r = i < r_of ? i : i % r_of;
-                v[k] = i < sml ? src_byte(S, O, msrc + r, wend) : (uint8_t)0;
-              }
+  for (int r = 0; r < XR_LIT; r++) {
+    const uint32_t idx = lane + 64 * r;
+    if (idx < lvec) lv[r] = __builtin_nontemporal_load((const zv4u *)(lbase + 16ull * idx));
+  }
 #pragma unroll
-              for (int k = 0; k < 4; k++)
-                if (i0 + k < sml) S.ring[(mstart + i0 + k) & ZRMASK] = v[k];
-            }
-          }
-          pending = false;
-        }
-        __syncthreads();
+  for (int r = 0; r < XR_FAR; r++) {
+    const uint32_t f = lane + 64 * r;
+    if (f < total) {
+      uint32_t lo = 0, hi = 63;  // the lane whose vectors hold f: first with pfx_nv > f
+      while (lo < hi) {
+        const uint32_t mid = (lo + hi) >> 1;
+        if (S.pfx_nv[mid] > f) hi = mid; else lo = mid + 1;
       }
-      // record this batch's deferred matches in output order
-      const uint64_t dm = __ballot(deferred);
-      const uint32_t nd = __builtin_popcountll(dm);
-      if (nd) {
-        if (deferred) {  // ndef + k <= base + lane: a consumed sequence slot
-          const uint32_t k = ndef + __builtin_popcountll(dm & ((1ull << lane) - 1));
-          defl[3 * k] = (uint32_t)mstart;
-          defl[3 * k + 1] = r_of;
-          defl[3 * k + 2] = sml;
-        }
-        ndef += nd;
-      }
-      __syncthreads();
-      O.pos = wend;
-      litpos += lspan;
-      base += cnt;
+      fv[r] = *(const zv4u *)(out + 16 * (S.own_v0[lo] + (f - S.own_pv[lo])));
     }
-    if (!err) {
-      if (litpos > regen) {
-        err = ZG_CORRUPT_STREAM;
-      } else {
-        out_copy_global(S, O, lsrc + litpos, regen - litpos);
-        if (O.pos != bstart + out_size) err = ZG_CORRUPT_STREAM;
+  }
+#pragma unroll
+  for (int r = 0; r < XR_LIT; r++) {
+    const uint32_t idx = lane + 64 * r;
+    if (idx < lvec) {
+      const uint32_t w[4] = {lv[r].x, lv[r].y, lv[r].z, lv[r].w};
+#pragma unroll
+      for (int j = 0; j < 16; j++) {
+        const int32_t k = (int32_t)(16 * idx + j) - (int32_t)lhead;
+        if (k >= 0 && (uint32_t)k < n_lit) S.lit_stage[k] = (uint8_t)(w[j >> 2] >> (8 * (j & 3)));
       }
     }
-    if (!err) blk_flush(S, out, O.flushed, O.pos);
-    if (lane == 0) {
-      if (err) status[item] = err;
-      Bp->def_n = err ? 0u : ndef;
-      Bp->def_done = 0;
+  }
+#pragma unroll
+  for (int r = 0; r < XR_FAR; r++) {
+    const uint32_t f = lane + 64 * r;
+    if (f < total) S.stage[f] = fv[r];
+  }
+  __syncthreads();
+  return true;
+}
+
+// unaligned 16-B LDS moves by value (an address-taken vector array would live in scratch)
+__device__ __forceinline__ zv4u ld16(const uint8_t *p) {
+  zv4u v;
+  __builtin_memcpy(&v, p, 16);
+  return v;
+}
+__device__ __forceinline__ void st16(uint8_t *p, zv4u v) { __builtin_memcpy(p, &v, 16); }
+
+// Gather e <= 16 bytes, byte j from source offset (r + j) mod d of s (stage below fe, else ring),
+// all loads issued before the first store, then store them at o.
+__device__ __forceinline__ void x_gather(ZXSmem &S, const uint8_t *stg, uint64_t o, uint64_t s, uint32_t r,
+                                         uint32_t d, uint32_t e, uint64_t fe, int64_t sb) {
+  uint32_t w[4] = {0, 0, 0, 0};
+  uint32_t rr = r;
+#pragma unroll
+  for (int j = 0; j < 16; j++) {
+    if ((uint32_t)j < e) {
+      const uint64_t q = s + rr;
+      const uint32_t v = q < fe ? stg[(int64_t)q + sb] : S.ring[q & XRMASK];
+      w[j >> 2] |= v << (8 * (j & 3));
     }
-    __syncthreads();
+    rr = rr + 1 == d ? 0u : rr + 1;
+  }
+  if (e == 16 && (o & XRMASK) <= XRING - 16) {
+    st16(&S.ring[o & XRMASK], zv4u{w[0], w[1], w[2], w[3]});
+  } else {
+#pragma unroll
+    for (int j = 0; j < 16; j++)
+      if ((uint32_t)j < e) S.ring[(o + j) & XRMASK] = (uint8_t)(w[j >> 2] >> (8 * (j & 3)));
   }
 }
 
-// One wave per item, 128 KiB of LDS: blocks in order; a block with deferred matches is loaded into
-// LDS, its deferred matches (in output order) run there, and it is written back.
-__global__ __launch_bounds__(64) void k_zstd_fixup(ZgItem *items, uint32_t *status, const ZBlk *blks,
-                                                   uint32_t blk_cap, const uint32_t *nblk, const uint32_t *zmode,
-                                                   uint8_t *dst, uint64_t slot_bytes, const uint32_t *seq_scratch,
-                                                   uint64_t seq_cap) {
-  __shared__ uint8_t img[BLOCK_MAX];
+// Copy len <= 16 bytes whose source [q, q + len) is contiguous (no period wrap) and entirely before
+// the destination o: ring or stage (below fe) to ring, as one 16-B move or two overlapping 8-B / 4-B
+// moves; bytes only where a move would straddle the ring end or the stage / ring split.
+template <int W>
+__device__ __forceinline__ void x_mv(ZXSmem &S, const uint8_t *stg, uint64_t o, uint64_t q, uint64_t fe, int64_t sb) {
+  typedef __attribute__((ext_vector_type(W / 4))) unsigned int vt;
+  vt v;
+  if (q < fe) __builtin_memcpy(&v, stg + ((int64_t)q + sb), W);
+  else __builtin_memcpy(&v, &S.ring[q & XRMASK], W);
+  __builtin_memcpy(&S.ring[o & XRMASK], &v, W);
+}
+__device__ __forceinline__ void x_run(ZXSmem &S, const uint8_t *stg, uint64_t o, uint64_t q, uint32_t len, uint64_t fe,
+                                      int64_t sb) {
+  const uint32_t w = len >= 16 ? 16u : len >= 8 ? 8u : len >= 4 ? 4u : 0u;
+  const bool ok = w && (o & XRMASK) <= XRING - 16 && (q + len <= fe || (q >= fe && (q & XRMASK) <= XRING - 16));
+  if (ok) {
+    const uint64_t o2 = o + len - w, q2 = q + len - w;
+    if (w == 16) {
+      x_mv<16>(S, stg, o, q, fe, sb);
+    } else if (w == 8) {
+      x_mv<8>(S, stg, o, q, fe, sb);
+      x_mv<8>(S, stg, o2, q2, fe, sb);
+    } else {
+      x_mv<4>(S, stg, o, q, fe, sb);
+      x_mv<4>(S, stg, o2, q2, fe, sb);
+    }
+  } else {
+    x_gather(S, stg, o, q, 0, 0xFFFFFFFFu, len, fe, sb);
+  }
+}
+
+// Resolve the staged matches (see x_stage) in rounds. A round takes every pending match whose source
+// lies before the first unresolved one (nothing it reads is still to be written). A short match
+// (<= 128 bytes, not overlapping its source, source wholly in the stage or the ring) is copied by its
+// own lane: all its 16-byte pieces loaded, then stored (the last piece ends at the match end,
+// rewriting its neighbour's bytes with the same values). Other matches are copied by the whole wave,
+// one after another: byte k is byte (k mod d) of the first period [ms - d, ms - d + min(n, d)),
+// which precedes the match, so no lane reads what another writes. LDS operations of a wave complete
+// in issue order, so a round reads what the previous one wrote without waiting for it.
+__device__ uint32_t x_resolve(ZXSmem &S, uint64_t ms, uint32_t d, uint32_t n, uint64_t fe, int64_t sb,
+                              uint64_t *prof = nullptr) {
+  const int lane = lane_id();
+  const uint8_t *stg = (const uint8_t *)S.stage;
+  const uint64_t src = ms - d;
+  const uint32_t cl = min(n, d);
+  bool pending = n > 0;
+  // the short-match path: source and destination contiguous in one buffer each
+  const bool in_stage = src + n <= fe, in_ring = src >= fe && (src & XRMASK) + n <= XRING;
+  const bool dst_ok = (ms & XRMASK) + n <= XRING;
+  const bool splat = n > 16 && n <= 512 && d < n && (d == 1 || d == 2 || d == 4 || d == 8) && dst_ok &&
+                     (src + d <= fe || (src >= fe && (src & XRMASK) + d <= XRING));
+  const bool fast = splat || (n > 0 && n <= 512 && d >= n && dst_ok && (in_stage || in_ring));
+  const uint8_t *sp = in_stage ? stg + ((int64_t)src + sb) : &S.ring[src & XRMASK];
+  uint8_t *dp = &S.ring[ms & XRMASK];
+  uint32_t rounds = 0;
+  uint64_t pm;
+  while ((pm = __ballot(pending)) != 0) {
+    const int first = __builtin_ctzll(pm);
+    const uint64_t F = rl64(ms, first);
+    const bool ready = pending && (lane == first || src + cl <= F);
+#ifdef ZG_PROFILE
+    const uint64_t c0 = clock64();
+#endif
+    if (ready && splat) {
+      // period 1, 2, 4 or 8: every 16-byte piece is the period repeated
+      const uint8_t *pp = src + d <= fe ? stg + ((int64_t)src + sb) : &S.ring[src & XRMASK];
+      uint64_t pat = 0;
+      for (uint32_t j = 0; j < d; j++) pat |= (uint64_t)pp[j] << (8 * j);
+      if (d == 1) pat *= 0x0101010101010101ull;
+      else if (d == 2) pat *= 0x0001000100010001ull;
+      else if (d == 4) pat |= pat << 32;
+      const zv4u v = zv4u{(uint32_t)pat, (uint32_t)(pat >> 32), (uint32_t)pat, (uint32_t)(pat >> 32)};
+      for (uint32_t k = 0; k + 16 <= n; k += 16) st16(dp + k, v);
+      if (n & 15) {  // the last 16 bytes start at phase (n - 16) mod d of the period
+        const uint32_t sh = 8 * ((n - 16) & (d - 1));
+        const uint64_t rp = sh ? (pat >> sh) | (pat << (64 - sh)) : pat;
+        st16(dp + n - 16, zv4u{(uint32_t)rp, (uint32_t)(rp >> 32), (uint32_t)rp, (uint32_t)(rp >> 32)});
+      }
+    } else if (ready && fast) {
+      if (n >= 16) {
+        // groups of up to 8 pieces: all loads of a group, then its stores; a piece never starts
+        // after n - 16 (the last one rewrites its neighbour's bytes with the same values)
+        const uint32_t lim = n - 16;
+        for (uint32_t g0 = 0; g0 < n; g0 += 128) {
+          const uint32_t np = min((n - g0 + 15) >> 4, 8u);
+          zv4u v0, v1, v2, v3, v4, v5, v6, v7;
+          v0 = ld16(sp + min(g0, lim));
+          if (np > 1) v1 = ld16(sp + min(g0 + 16, lim));
+          if (np > 2) v2 = ld16(sp + min(g0 + 32, lim));
+          if (np > 3) v3 = ld16(sp + min(g0 + 48, lim));
+          if (np > 4) v4 = ld16(sp + min(g0 + 64, lim));
+          if (np > 5) v5 = ld16(sp + min(g0 + 80, lim));
+          if (np > 6) v6 = ld16(sp + min(g0 + 96, lim));
+          if (np > 7) v7 = ld16(sp + min(g0 + 112, lim));
+          st16(dp + min(g0, lim), v0);
+          if (np > 1) st16(dp + min(g0 + 16, lim), v1);
+          if (np > 2) st16(dp + min(g0 + 32, lim), v2);
+          if (np > 3) st16(dp + min(g0 + 48, lim), v3);
+          if (np > 4) st16(dp + min(g0 + 64, lim), v4);
+          if (np > 5) st16(dp + min(g0 + 80, lim), v5);
+          if (np > 6) st16(dp + min(g0 + 96, lim), v6);
+          if (np > 7) st16(dp + min(g0 + 112, lim), v7);
+        }
+      } else if (n >= 8) {
+        uint64_t a0, a1;
+        __builtin_memcpy(&a0, sp, 8);
+        __builtin_memcpy(&a1, sp + n - 8, 8);
+        __builtin_memcpy(dp, &a0, 8);
+        __builtin_memcpy(dp + n - 8, &a1, 8);
+      } else if (n >= 4) {
+        uint32_t a0, a1;
+        __builtin_memcpy(&a0, sp, 4);
+        __builtin_memcpy(&a1, sp + n - 4, 4);
+        __builtin_memcpy(dp, &a0, 4);
+        __builtin_memcpy(dp + n - 4, &a1, 4);
+      } else {
+        for (uint32_t j = 0; j < n; j++) dp[j] = sp[j];
+      }
+    }
+    uint64_t sm = __ballot(ready && !fast);
+#ifdef ZG_PROFILE
+    const uint64_t c1 = clock64();
+    (void)c0;
+    if (prof) {
+      const bool sl = ready && !fast;
+      prof[0] += __builtin_popcountll(__ballot(sl && n > 128));
+      prof[1] += __builtin_popcountll(__ballot(sl && d < n));
+      prof[2] += __builtin_popcountll(__ballot(sl && d < 16));
+      prof[3] += __builtin_popcountll(__ballot(sl && n <= 128 && d >= n));
+    }
+#endif
+    while (sm) {
+      const int i = __builtin_ctzll(sm);
+      sm &= sm - 1;
+      const uint64_t ms_i = rl64(ms, i), fe_i = rl64(fe, i);
+      const int64_t sb_i = (int64_t)rl64((uint64_t)sb, i);
+      uint32_t d_i = U(__builtin_amdgcn_readlane(d, i));
+      const uint32_t n_i = U(__builtin_amdgcn_readlane(n, i));
+      uint64_t s_i = ms_i - d_i;
+      const uint32_t k0 = 0;
+      const float inv = __builtin_amdgcn_rcpf((float)d_i);
+      for (uint32_t k = k0 + 16 * lane; k < n_i; k += 1024) {
+        const uint32_t kk = (n_i - k < 16 && n_i >= 16) ? n_i - 16 : k;
+        const uint32_t e = min(n_i - kk, 16u);
+        uint32_t r = kk;
+        if (kk >= d_i) {
+          const uint32_t q = (uint32_t)((float)kk * inv);
+          int32_t rr = (int32_t)kk - (int32_t)(q * d_i);
+          while (rr < 0) rr += d_i;
+          while (rr >= (int32_t)d_i) rr -= d_i;
+          r = (uint32_t)rr;
+        }
+        const uint64_t o = ms_i + kk;
+        if (r + e <= d_i) x_run(S, stg, o, s_i + r, e, fe_i, sb_i);
+        else x_gather(S, stg, o, s_i, r, d_i, e, fe_i, sb_i);  // the piece wraps the period
+      }
+      __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
+    }
+#ifdef ZG_PROFILE
+    (void)c1;
+#endif
+    pending = pending && !ready;
+    __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
+    rounds++;
+  }
+  __syncthreads();
+  return rounds;
+}
+
+// one long match (or one whose far part does not fit a batch), in ZBATCH chunks; false if corrupt
+__device__ __forceinline__ bool x_long_match(ZXSmem &S, XOut &O, uint64_t fstart, uint32_t off, uint64_t ml, uint64_t bend) {
+  const uint64_t p = O.pos;
+  if (off == 0 || off > p - fstart || p + ml > bend) return false;
+  for (uint64_t c0 = 0; c0 < ml; c0 += ZBATCH) {
+    const uint32_t c = (uint32_t)min<uint64_t>(ZBATCH, ml - c0);
+    x_reserve(S, O, p + c0 + c);
+    const uint64_t fb = x_far_bound(O, p + c0 + c);
+    const uint32_t n = lane_id() == 0 ? c : 0u;
+    uint64_t fe;
+    int64_t sb;
+    x_stage(S, O.out, fb, p + c0, off, n, nullptr, 0, fe, sb);  // <= 258 vectors: always fits
+    x_resolve(S, p + c0, off, n, fe, sb);
+    O.pos = p + c0 + c;
+  }
+  return true;
+}
+
+}  // namespace
+
+__global__ __launch_bounds__(64) void k_zstd_exec_item(ZgItem *items, uint32_t *status, const ZBlk *blks,
+                                                       uint32_t blk_cap, const uint32_t *nblk, const uint32_t *zmode,
+                                                       uint8_t *dst, uint64_t slot_bytes, const uint8_t *lit_scratch,
+                                                       uint64_t lit_stride, const uint32_t *seq_scratch,
+                                                       uint64_t seq_cap) {
+  __shared__ ZXSmem S;
   const uint32_t item = blockIdx.x;
   const int lane = lane_id();
+  ZP_DECL;
   if (zmode[item] != ZMODE_PARALLEL || status[item]) return;
+  const ZgItem it = items[item];
+  const uint8_t *in = (const uint8_t *)it.src;
   uint8_t *out = dst + (uint64_t)item * slot_bytes;
   const ZBlk *B = blks + (uint64_t)item * blk_cap;
   const uint32_t nb = nblk[item];
+  XOut O{out, 0, 0};
   uint32_t err = 0;
-  uint64_t end = 0, fstart = 0;
-  bool wrote = false;  // this wave has written output: its later loads of earlier blocks use sc1
+  uint64_t fstart = 0;
   for (uint32_t bi = 0; bi < nb && !err; bi++) {
-    const uint32_t flags = U(B[bi].flags);
+    const uint32_t flags = U(B[bi].flags), type = flags & 3;
     const uint64_t bstart = U(B[bi].out_off);
     const uint32_t bsize = U(B[bi].out_size);
     if (flags & ZBF_FIRST) fstart = bstart;
-    end = bstart + bsize;
-    const uint32_t ndef = (flags & 3) == ZB_CMP ? U(B[bi].def_n) : 0u;
-    if (ndef) {
-      const uint32_t *defl = seq_scratch + ((uint64_t)item * seq_cap + U(B[bi].seq_buf)) * 3;
-      for (uint32_t o = 0; o < bsize; o += ZBATCH)
-        lds_copy_in(img, ~0ull, o, out + bstart + o, min<uint32_t>(ZBATCH, bsize - o));
-      __syncthreads();
-      for (uint32_t k0 = 0; k0 < ndef; k0 += 64) {
-        const uint32_t k = k0 + lane;
-        const bool valid = k < ndef;
-        uint64_t p = 0;
-        uint32_t d = 1, len = 0;
-        if (valid) {
-          p = defl[3 * k];
-          d = defl[3 * k + 1];
-          len = defl[3 * k + 2];
+    if (bstart != O.pos) { err = ZG_CORRUPT_STREAM; break; }
+    const uint64_t bend = bstart + bsize;
+    if (type == ZB_RAW) {
+      x_copy(S, O, in + U(B[bi].in_off), bsize);
+    } else if (type == ZB_RLE) {
+      x_fill(S, O, (uint8_t)U(in[U(B[bi].in_off)]), bsize);
+    } else {
+      const uint32_t ltype = (flags >> 2) & 3, regen = U(B[bi].regen), nseq = U(B[bi].nseq);
+      const uint8_t *lsrc =
+          ltype == 0 ? in + U(B[bi].lit_off) : lit_scratch + (uint64_t)item * lit_stride + U(B[bi].lit_buf);
+      const uint32_t *seqs = seq_scratch + ((uint64_t)item * seq_cap + U(B[bi].seq_buf)) * 3;
+      const uint32_t ri0 = U(B[bi].rep_in[0]), ri1 = U(B[bi].rep_in[1]), ri2 = U(B[bi].rep_in[2]);
+      uint64_t litpos = 0;
+      uint32_t base = 0;
+      while (base < nseq && !err) {
+        ZP_T(th);
+        const uint32_t avail = min<uint32_t>(64, nseq - base);
+        const bool have = lane < (int)avail;
+        uint32_t r_ll = 0, r_ml = 0, r_of = 1;
+        if (have) {
+          const uint32_t *q = seqs + (uint64_t)(base + lane) * 3;
+          r_ll = q[0];
+          r_ml = q[1];
+          r_of = sym_eval(q[2], ri0, ri1, ri2);
         }
-        const uint64_t src = p - d;
-        bool pending = valid;
-        uint64_t pm;
-        while ((pm = __ballot(pending)) != 0) {
-          const int first = __builtin_ctzll(pm);
-          const uint32_t F_lo = __builtin_amdgcn_readlane((uint32_t)p, first);
-          const uint32_t F_hi = __builtin_amdgcn_readlane((uint32_t)(p >> 32), first);
-          const uint64_t F = ((uint64_t)F_hi << 32) | F_lo;
-          const uint32_t flen = __builtin_amdgcn_readlane(len, first);
-          if (flen > 32) {  // long: the whole wave copies it
-            const uint32_t fd = __builtin_amdgcn_readlane(d, first);
-            const float inv = 1.0f / (float)fd;
-            for (uint32_t i = lane; i < flen; i += 64) {
-              uint32_t rm = i;
-              if (fd < flen) {
-                uint32_t q = (uint32_t)((float)i * inv);
-                int32_t r = (int32_t)i - (int32_t)(q * fd);
-                if (r < 0) r += fd;
-                if (r >= (int32_t)fd) r -= fd;
-                rm = (uint32_t)r;
-              }
-              const uint64_t sb = F - fd + rm;
-              img[F - bstart + i] = sb >= bstart ? img[sb - bstart] : (wrote ? load_out_byte(out + sb) : out[sb]);
-            }
-            if (lane == first) pending = false;
-            __syncthreads();
-            continue;
-          }
-          const bool ready = pending && len <= 32 && (lane == first || src + len <= F);
-          if (ready) {
-            for (uint32_t i0 = 0; i0 < len; i0 += 4) {
-              uint8_t v[4];
-#pragma unroll
-              for (int j = 0; j < 4; j++) {
-                const uint32_t i = i0 + j;
-                const uint64_t sb = src + (i < d ? i : i % d);
-                v[j] = i < len ? (sb >= bstart ? img[sb - bstart] : (wrote ? load_out_byte(out + sb) : out[sb]))
-                               : (uint8_t)0;
-              }
-#pragma unroll
-              for (int j = 0; j < 4; j++)
-                if (i0 + j < len) img[p - bstart + i0 + j] = v[j];
-            }
-            pending = false;
-          }
-          __syncthreads();
+        uint32_t a = r_ll, b = r_ll + r_ml;  // inclusive prefix sums (literals, output)
+        for (int o = 1; o < 64; o <<= 1) {
+          const uint32_t ta = __shfl_up(a, o, 64), tb = __shfl_up(b, o, 64);
+          if (lane >= o) { a += ta; b += tb; }
         }
+        const uint64_t bigm = __ballot(have && (r_ll >= ZBIG || r_ml >= ZBIG));
+        const uint32_t fit = __builtin_popcountll(__ballot(have && b <= ZBATCH));
+        uint32_t cnt = min<uint32_t>(fit, bigm ? (uint32_t)__builtin_ctzll(bigm) : 64u);
+        const uint64_t out_base = O.pos;
+        bool staged = false;
+        uint64_t fe = 0;
+        int64_t sb = 0;
+        uint32_t span = 0, lspan = 0;
+        bool mine = false;
+        uint64_t mstart = 0;
+        uint32_t sml = 0;
+        if (cnt) {
+          span = U(__builtin_amdgcn_readlane(b, cnt - 1));
+          lspan = U(__builtin_amdgcn_readlane(a, cnt - 1));
+          if (out_base + span > bend || litpos + lspan > regen) { err = ZG_CORRUPT_STREAM; break; }
+          mine = lane < (int)cnt;
+          sml = mine ? r_ml : 0u;
+          mstart = out_base + b - sml;
+          if (__ballot(mine && sml && (r_of == 0 || (uint64_t)r_of > mstart - fstart))) {
+            err = ZG_CORRUPT_STREAM;
+            break;
+          }
+          x_reserve(S, O, out_base + span);
+          const uint64_t fb = x_far_bound(O, out_base + span);
+          staged = x_stage(S, O.out, fb, mstart, r_of, sml, lsrc + litpos, lspan, fe, sb);
+        }
+#ifdef ZG_PROFILE
+        zp_acc[6] += 1;
+        zp_acc[7] += cnt;
+#endif
+        if (!staged) {  // one sequence alone: its literal run, then its match in chunks
+          const uint32_t ll = U(__builtin_amdgcn_readlane(r_ll, 0)), ml = U(__builtin_amdgcn_readlane(r_ml, 0));
+          const uint32_t of = U(__builtin_amdgcn_readlane(r_of, 0));
+          if (litpos + ll > regen || O.pos + ll + ml > bend) { err = ZG_CORRUPT_STREAM; break; }
+          x_copy(S, O, lsrc + litpos, ll);
+          litpos += ll;
+          if (ml && !x_long_match(S, O, fstart, of, ml, bend)) { err = ZG_CORRUPT_STREAM; break; }
+          base += 1;
+          continue;
+        }
+        // literals of the batch into place
+        ZP_T(tl);
+        S.pfx_lit[lane] = a;
+        S.pfx_out[lane] = b;
+        __syncthreads();
+        for (uint32_t k = lane; k < lspan; k += 64) {
+          uint32_t lo = 0, hi = cnt - 1;  // first sequence with pfx_lit > k
+          while (lo < hi) {
+            const uint32_t mid = (lo + hi) >> 1;
+            if (S.pfx_lit[mid] > k) hi = mid; else lo = mid + 1;
+          }
+          const uint32_t prev_lit = lo ? S.pfx_lit[lo - 1] : 0u, prev_out = lo ? S.pfx_out[lo - 1] : 0u;
+          S.ring[(out_base + prev_out + (k - prev_lit)) & XRMASK] = S.lit_stage[k];
+        }
+        __syncthreads();
+        ZP_T(t3);
+#ifdef ZG_PROFILE
+        uint64_t rp[4] = {0, 0, 0, 0};
+        const uint32_t nr = x_resolve(S, mstart, r_of, sml, fe, sb, rp);
+        zp_acc[0] += rp[0];
+        zp_acc[1] += rp[1];
+        zp_acc[2] += rp[2];
+        zp_acc[5] += rp[3];
+#else
+        const uint32_t nr = x_resolve(S, mstart, r_of, sml, fe, sb);
+#endif
+        ZP_ADD(3, t3);
+#ifdef ZG_PROFILE
+        zp_acc[4] += nr;
+#endif
+        (void)nr;
+        O.pos = out_base + span;
+        litpos += lspan;
+        base += cnt;
       }
-      blk_flush_img(img, out, bstart, bstart + bsize);
-      __builtin_amdgcn_s_waitcnt(0);  // written back before any later load of it
-      __threadfence_block();
-      wrote = true;
+      if (!err) {
+        if (litpos > regen || O.pos + (regen - litpos) != bend) err = ZG_CORRUPT_STREAM;
+        else x_copy(S, O, lsrc + litpos, regen - litpos);
+      }
     }
-    if ((flags & ZBF_LAST) && (flags & ZBF_CK)) {
+    if (!err && O.pos != bend) err = ZG_CORRUPT_STREAM;
+    if (!err && (flags & ZBF_LAST) && (flags & ZBF_CK)) {
+      x_flush(S, O);
+      __builtin_amdgcn_s_waitcnt(0);
       __threadfence();
-      const uint64_t h = xxh64(out + fstart, end - fstart);
+      const uint64_t h = xxh64(out + fstart, O.pos - fstart);
       if ((uint32_t)h != U(B[bi].ck)) err = ZG_CORRUPT_STREAM;
     }
   }
+  if (!err) x_flush(S, O);
+  ZP_FLUSH;
   if (lane == 0) {
     if (err) {
       status[item] = err;
     } else {
       items[item].src = (uint64_t)out;
-      items[item].len = end;
+      items[item].len = O.pos;
     }
   }
 }
@@ -2005,14 +2398,15 @@ hipError_t launch_zstd(ZgItem *items, uint32_t *status, uint32_t n_items, uint8_
                      Z.lit_stride, Z.seq_cap);
   const uint64_t recs = (uint64_t)n_items * Z.blk_cap;
   const uint32_t grid = (uint32_t)std::min<uint64_t>(recs, 256 * 16);
+  const uint32_t lgrid = (uint32_t)std::min<uint64_t>(recs, 256 * 2);
+  hipLaunchKernelGGL(k_zstd_lits, dim3(lgrid), dim3(LIT_THREADS), 0, s, items, status, blks, Z.blk_cap, Z.nblk,
+                     Z.mode, n_items, Z.lit, Z.lit_stride);
   hipLaunchKernelGGL(k_zstd_blocks, dim3(grid), dim3(64), 0, s, items, status, blks, Z.blk_cap, Z.nblk, Z.mode,
                      n_items, Z.lit, Z.lit_stride, Z.seq, Z.seq_cap);
   hipLaunchKernelGGL(k_zstd_plan, dim3(n_items), dim3(64), 0, s, items, status, blks, Z.blk_cap, Z.nblk, Z.mode,
                      slot_bytes);
-  hipLaunchKernelGGL(k_zstd_exec_blocks, dim3(grid), dim3(64), 0, s, items, status, blks, Z.blk_cap, Z.nblk, Z.mode,
-                     n_items, dst, slot_bytes, Z.lit, Z.lit_stride, Z.seq, Z.seq_cap);
-  hipLaunchKernelGGL(k_zstd_fixup, dim3(n_items), dim3(64), 0, s, items, status, blks, Z.blk_cap, Z.nblk, Z.mode,
-                     dst, slot_bytes, Z.seq, Z.seq_cap);
+  hipLaunchKernelGGL(k_zstd_exec_item, dim3(n_items), dim3(64), 0, s, items, status, blks, Z.blk_cap, Z.nblk, Z.mode,
+                     dst, slot_bytes, Z.lit, Z.lit_stride, Z.seq, Z.seq_cap);
   hipLaunchKernelGGL(k_zstd, dim3(n_items), dim3(64), 0, s, items, status, dst, slot_bytes, Z.lit, Z.lit_stride,
                      Z.mode);
   return hipGetLastError();

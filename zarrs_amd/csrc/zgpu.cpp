@@ -632,6 +632,17 @@ int zgpu_plan_execute(zgpu_plan *P, void *out, int32_t *status, void *stream) {
   ABI_GUARD_END
 }
 
+int zgpu_plan_status(zgpu_plan *P, int32_t *status, void *stream) {
+  ABI_GUARD_BEGIN
+  if (!P) return set_err(ZGPU_INVALID_ARGUMENT, "NULL argument");
+  std::lock_guard<std::mutex> lk(P->ctx->mu);
+  HIPCHK(hipSetDevice(P->ctx->device));
+  const int rc = plan_statuses(*P, status, pick_stream(P->ctx, stream));
+  if (rc) set_err(rc, zgpu_status_name(rc));
+  return rc;
+  ABI_GUARD_END
+}
+
 void zgpu_plan_destroy(zgpu_plan *P) {
   if (!P) return;
   std::lock_guard<std::mutex> lk(P->ctx->mu);
