@@ -13,11 +13,23 @@ __global__ void k(int mis_src, int mis_dst, int iters, int active, int pieces, u
     if ((int)lane < active) {
       const unsigned so = ((it * 2048 + lane * 128) & 16383) + mis_src;
       const unsigned dof = 32768 + ((it * 2048 + lane * 128) & 16383) + mis_dst;
-      v4u v[8];
-#pragma unroll
-      for (int j = 0; j < 8; j++) if (j < pieces) __builtin_memcpy(&v[j], &ring[so + 16 * j], 16);
-#pragma unroll
-      for (int j = 0; j < 8; j++) if (j < pieces) __builtin_memcpy(&ring[dof + 16 * j], &v[j], 16);
+      v4u v0, v1, v2, v3, v4, v5, v6, v7;
+      __builtin_memcpy(&v0, &ring[so + 0], 16);
+      if (pieces > 1) __builtin_memcpy(&v1, &ring[so + 16], 16);
+      if (pieces > 2) __builtin_memcpy(&v2, &ring[so + 32], 16);
+      if (pieces > 3) __builtin_memcpy(&v3, &ring[so + 48], 16);
+      if (pieces > 4) __builtin_memcpy(&v4, &ring[so + 64], 16);
+      if (pieces > 5) __builtin_memcpy(&v5, &ring[so + 80], 16);
+      if (pieces > 6) __builtin_memcpy(&v6, &ring[so + 96], 16);
+      if (pieces > 7) __builtin_memcpy(&v7, &ring[so + 112], 16);
+      __builtin_memcpy(&ring[dof + 0], &v0, 16);
+      if (pieces > 1) __builtin_memcpy(&ring[dof + 16], &v1, 16);
+      if (pieces > 2) __builtin_memcpy(&ring[dof + 32], &v2, 16);
+      if (pieces > 3) __builtin_memcpy(&ring[dof + 48], &v3, 16);
+      if (pieces > 4) __builtin_memcpy(&ring[dof + 64], &v4, 16);
+      if (pieces > 5) __builtin_memcpy(&ring[dof + 80], &v5, 16);
+      if (pieces > 6) __builtin_memcpy(&ring[dof + 96], &v6, 16);
+      if (pieces > 7) __builtin_memcpy(&ring[dof + 112], &v7, 16);
     }
     __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
   }

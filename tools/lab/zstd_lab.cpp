@@ -182,7 +182,7 @@ int main(int argc, char **argv) {
     CK(hipMemcpyFromSymbol(z, HIP_SYMBOL(zgpu::g_zprof), sizeof(z)));
     const double nb = z[4] ? (double)z[4] : 1.0;
     const double nbt = z[6] ? (double)z[6] : 1.0;
-    printf("exec_item slow matches per batch: n>128 %.2f d<n %.2f d<16 %.2f other %.2f | resolve %.0f rounds %.2f | (other total %llu) | batches %llu"
+    printf("exec_item slow matches per batch: n>512 %.2f 16<=d<n %.2f d<16 %.2f other(split src) %.2f | resolve %.0f rounds %.2f | (other total %llu) | batches %llu"
            " seqs/batch %.1f\n", z[0] / nbt, z[1] / nbt, z[2] / nbt, z[5] / nbt, z[3] / nbt, z[4] / nbt, z[5], z[6], z[7] / nbt);
   }
 #endif

@@ -1154,6 +1154,13 @@ struct ZScanSmem {
 
 // literals (Huffman table) and sequences (FSE tables) are decoded one after the other: the two
 // table sets share LDS
+// sequence decoding table entry: the code's value base and extra-bit count with the FSE transition
+// (one 8-byte LDS read per table per sequence); nbx == 0xFF marks a code outside the format
+struct SeqX {
+  uint32_t base;
+  uint16_t next;
+  uint8_t nb, nbx;
+};
 struct ZDecSmem {
   union {
     uint16_t huf[1 << MAX_HUF_LOG];
@@ -1161,6 +1168,7 @@ struct ZDecSmem {
       Fse ll[512], ml[512], of[256];
     };
   };
+  SeqX xl[512], xm[512], xo[256];
   Fse wt[64];
   int16_t norm[64];
   uint8_t weights[256];
@@ -1432,33 +1440,80 @@ __global__ __launch_bounds__(64) void k_zstd_blocks(const ZgItem *items, uint32_
           lg[t] = acc;
         }
       }
+      // value bases / extra bits folded into the decoding tables
+      if (!bad) {
+        __syncthreads();
+        for (uint32_t u = lane; u < (1u << lg[0]); u += 64) {
+          const Fse e = S.ll[u];
+          const bool ok = e.sym <= 35;
+          S.xl[u] = SeqX{ok ? c_ll_base[e.sym] : 0u, e.base, e.nb, (uint8_t)(ok ? c_ll_bits[e.sym] : 0xFF)};
+        }
+        for (uint32_t u = lane; u < (1u << lg[2]); u += 64) {
+          const Fse e = S.ml[u];
+          const bool ok = e.sym <= 52;
+          S.xm[u] = SeqX{ok ? c_ml_base[e.sym] : 0u, e.base, e.nb, (uint8_t)(ok ? c_ml_bits[e.sym] : 0xFF)};
+        }
+        for (uint32_t u = lane; u < (1u << lg[1]); u += 64) {
+          const Fse e = S.of[u];
+          const bool ok = e.sym <= 31;
+          S.xo[u] = SeqX{ok ? (1u << e.sym) : 0u, e.base, e.nb, (uint8_t)(ok ? e.sym : 0xFF)};
+        }
+        __syncthreads();
+      }
+      // Backward bit container in SGPRs: C holds bits [32 * lw, 32 * lw + have) of the aligned item
+      // words, the next unread bit at bit 63; refilled a word at a time from the BitsBack register
+      // window (readlane), so a field read is three scalar operations.
       BitsBack R;
       if (!bad && !bb_init(R, in, it.len, U(Bp->seq_off), U(Bp->seq_end))) bad = true;
       if (!bad) {
-        uint32_t sll = bb_read(R, lg[0]), sof = bb_read(R, lg[1]), sml = bb_read(R, lg[2]);
+        auto word = [&](int32_t k) -> uint32_t {
+          if (k < R.wb - 16) {  // slide the window pair down, prefetching the next lower window
+            R.wb -= 64;
+            R.wcur = R.wprev;
+            R.wprev = ldw(R, R.wb - 64 + lane_id());
+          }
+          return wget(R, k);
+        };
+        const int64_t p0 = R.cur;
+        int32_t lw = (int32_t)((p0 - 1) >> 5) - 1;
+        int32_t have = (int32_t)(p0 - 32 * (int64_t)lw);  // (32, 64]
+        uint64_t C = (((uint64_t)word(lw + 1) << 32) | word(lw)) << (64 - have);
+        auto refill = [&]() {
+          if (have <= 32) {
+            lw--;
+            C |= (uint64_t)word(lw) << (32 - have);
+            have += 32;
+          }
+        };
+        auto rd = [&](uint32_t n) -> uint32_t {  // n <= 31 bits
+          const uint32_t v = (uint32_t)((C >> 1) >> (63 - n));
+          C <<= n;
+          have -= (int32_t)n;
+          return v;
+        };
+        uint32_t sll = rd(lg[0]), sof = rd(lg[1]);
+        refill();
+        uint32_t sml = rd(lg[2]);
         uint32_t *out = seq_scratch + ((uint64_t)item * seq_cap + U(Bp->seq_buf)) * 3;
         uint32_t remaining = nseq, done = 0;
+        const uint2 *XO = (const uint2 *)S.xo, *XM = (const uint2 *)S.xm, *XL = (const uint2 *)S.xl;
         while (remaining && !bad) {
           uint32_t r_ll = 0, r_ml = 0, r_of = 0, cnt = 0;
           while (cnt < 64 && remaining) {
-            const Fse eo = S.of[sof], em = S.ml[sml], el = S.ll[sll];
-            const uint32_t ofc = U(eo.sym), mlc = U(em.sym), llc = U(el.sym);
-            if (ofc > 31 || mlc > 52 || llc > 35) { bad = true; break; }
-            uint32_t ofv;
-            if (ofc <= 25) {
-              ofv = (1u << ofc) + bb_read(R, ofc);
-            } else {
-              const uint32_t hi = bb_read(R, ofc - 16);
-              const uint32_t lo = bb_read(R, 16);
-              ofv = (1u << ofc) + ((hi << 16) | lo);
-            }
-            const uint32_t ml = c_ml_base[mlc] + bb_read(R, c_ml_bits[mlc]);
-            const uint32_t ll = c_ll_base[llc] + bb_read(R, c_ll_bits[llc]);
+            const uint2 eo = XO[sof], em = XM[sml], el = XL[sll];
+            const uint32_t ob = U(eo.x), ow = U(eo.y), mb = U(em.x), mw = U(em.y), lb = U(el.x), lwd = U(el.y);
+            if ((ow | mw | lwd) & 0x80000000u) { bad = true; break; }
+            refill();
+            const uint32_t ofv = ob + rd(ow >> 24);
+            refill();
+            const uint32_t ml = mb + rd(mw >> 24);
+            const uint32_t ll = lb + rd(lwd >> 24);
             remaining--;
             if (remaining) {
-              sll = U(el.base) + bb_read(R, U(el.nb));
-              sml = U(em.base) + bb_read(R, U(em.nb));
-              sof = U(eo.base) + bb_read(R, U(eo.nb));
+              refill();
+              sll = (lwd & 0xFFFF) + rd((lwd >> 16) & 0xFF);
+              sml = (mw & 0xFFFF) + rd((mw >> 16) & 0xFF);
+              sof = (ow & 0xFFFF) + rd((ow >> 16) & 0xFF);
             }
             // repeat offsets, symbolically in the block's incoming rep state (RFC 8878 3.1.1.5)
             uint32_t off;
@@ -1492,7 +1547,8 @@ __global__ __launch_bounds__(64) void k_zstd_blocks(const ZgItem *items, uint32_
           }
           done += cnt;
         }
-        if (!bad && (bb_overflow(R) || !bb_exact_end(R))) bad = true;
+        // the stream must end exactly on its first bit
+        if (!bad && (int64_t)lw * 32 + have != R.lo_bit) bad = true;
       }
     }
     if (!bad && sum_ll > regen) bad = true;
@@ -2265,12 +2321,20 @@ __global__ __launch_bounds__(64) void k_zstd_exec_item(ZgItem *items, uint32_t *
       const uint32_t ri0 = U(B[bi].rep_in[0]), ri1 = U(B[bi].rep_in[1]), ri2 = U(B[bi].rep_in[2]);
       uint64_t litpos = 0;
       uint32_t base = 0;
+      // the next batch's sequences are loaded while this batch executes
+      uint32_t nx_base = 0xFFFFFFFFu, nx_ll = 0, nx_ml = 0, nx_of = 0;
       while (base < nseq && !err) {
         ZP_T(th);
         const uint32_t avail = min<uint32_t>(64, nseq - base);
         const bool have = lane < (int)avail;
         uint32_t r_ll = 0, r_ml = 0, r_of = 1;
-        if (have) {
+        if (nx_base == base) {
+          if (have) {
+            r_ll = nx_ll;
+            r_ml = nx_ml;
+            r_of = sym_eval(nx_of, ri0, ri1, ri2);
+          }
+        } else if (have) {
           const uint32_t *q = seqs + (uint64_t)(base + lane) * 3;
           r_ll = q[0];
           r_ml = q[1];
@@ -2311,6 +2375,13 @@ __global__ __launch_bounds__(64) void k_zstd_exec_item(ZgItem *items, uint32_t *
         zp_acc[6] += 1;
         zp_acc[7] += cnt;
 #endif
+        nx_base = base + (staged ? cnt : 1u);
+        if (nx_base < nseq && lane < (int)(nseq - nx_base)) {
+          const uint32_t *q = seqs + (uint64_t)(nx_base + lane) * 3;
+          nx_ll = q[0];
+          nx_ml = q[1];
+          nx_of = q[2];
+        }
         if (!staged) {  // one sequence alone: its literal run, then its match in chunks
           const uint32_t ll = U(__builtin_amdgcn_readlane(r_ll, 0)), ml = U(__builtin_amdgcn_readlane(r_ml, 0));
           const uint32_t of = U(__builtin_amdgcn_readlane(r_of, 0));
@@ -2321,19 +2392,29 @@ __global__ __launch_bounds__(64) void k_zstd_exec_item(ZgItem *items, uint32_t *
           base += 1;
           continue;
         }
-        // literals of the batch into place
+        // literals of the batch into place: every lane moves its own run, 16 bytes at a time (loads
+        // of a group of four before its stores), bytes where the run wraps the ring
         ZP_T(tl);
-        S.pfx_lit[lane] = a;
-        S.pfx_out[lane] = b;
-        __syncthreads();
-        for (uint32_t k = lane; k < lspan; k += 64) {
-          uint32_t lo = 0, hi = cnt - 1;  // first sequence with pfx_lit > k
-          while (lo < hi) {
-            const uint32_t mid = (lo + hi) >> 1;
-            if (S.pfx_lit[mid] > k) hi = mid; else lo = mid + 1;
+        if (mine && r_ll) {
+          const uint32_t ll = r_ll, o = (uint32_t)out_base + b - r_ml - ll;
+          const uint8_t *ls = S.lit_stage + (a - ll);
+          if (ll >= 16 && (o & XRMASK) + ll <= XRING) {
+            uint8_t *dq = &S.ring[o & XRMASK];
+            for (uint32_t k0 = 0; k0 < ll; k0 += 64) {
+              const uint32_t lim = ll - 16;
+              const zv4u v0 = ld16(ls + min(k0, lim));
+              zv4u v1, v2, v3;
+              if (k0 + 16 < ll) v1 = ld16(ls + min(k0 + 16, lim));
+              if (k0 + 32 < ll) v2 = ld16(ls + min(k0 + 32, lim));
+              if (k0 + 48 < ll) v3 = ld16(ls + min(k0 + 48, lim));
+              st16(dq + min(k0, lim), v0);
+              if (k0 + 16 < ll) st16(dq + min(k0 + 16, lim), v1);
+              if (k0 + 32 < ll) st16(dq + min(k0 + 32, lim), v2);
+              if (k0 + 48 < ll) st16(dq + min(k0 + 48, lim), v3);
+            }
+          } else {
+            for (uint32_t k = 0; k < ll; k++) S.ring[(o + k) & XRMASK] = ls[k];
           }
-          const uint32_t prev_lit = lo ? S.pfx_lit[lo - 1] : 0u, prev_out = lo ? S.pfx_out[lo - 1] : 0u;
-          S.ring[(out_base + prev_out + (k - prev_lit)) & XRMASK] = S.lit_stage[k];
         }
         __syncthreads();
         ZP_T(t3);
