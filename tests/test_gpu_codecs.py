@@ -29,6 +29,19 @@ def _content(rng, n, kind):
     if kind == "far":  # repeats at distances near the 32 KiB window limit
         blk = rng.integers(0, 256, 30000, dtype=np.uint8)
         return np.tile(blk, n // 30000 + 1)[:n].copy()
+    if kind == "vfar":  # repeats 100,000 bytes back: zstd sources beyond the 64 KiB LDS ring
+        blk = rng.integers(0, 256, 100000, dtype=np.uint8)
+        return np.tile(blk, n // 100000 + 1)[:n].copy()
+    if kind == "periods":  # runs of short odd / even periods and lengths: overlapping copies
+        out, size = [], 0
+        while size < n:
+            p = int(rng.choice([1, 2, 3, 5, 7, 12, 17, 24, 40]))
+            ln = int(rng.integers(20, 3000))
+            pat = rng.integers(0, 256, p, dtype=np.uint8)
+            out.append(np.tile(pat, ln // p + 1)[:ln])
+            out.append(rng.integers(0, 256, int(rng.integers(0, 40)), dtype=np.uint8))
+            size += ln + len(out[-1])
+        return np.concatenate(out)[:n].copy()
     raise ValueError(kind)
 
 
@@ -143,7 +156,7 @@ def test_zstd_multiblock_frames(level):
     codecs = [BYTES_LE, {"name": "zstd", "configuration": {"level": level, "checksum": level != 1}}]
     oc = O.OracleChain.from_metadata(codecs, "uint8", 0, 1)
     n = 3 << 20
-    kinds = ["random", "text", "smooth", "runs", "far"]
+    kinds = ["random", "text", "smooth", "runs", "far", "vfar", "periods"]
     data = [_content(rng, n, k) for k in kinds]
     # C5-like: byte-shuffled u16 blobs + noise
     z = np.arange(n // 2, dtype=np.float32)

@@ -97,6 +97,14 @@ CHAINS = {
     "crc_shuffle": ([{"name": "bytes", "configuration": {"endian": "little"}},
                      {"name": "numcodecs.shuffle", "configuration": {"elementsize": 8}},
                      {"name": "crc32c"}], "float64"),
+    "shuffle2_zstd_u16": ([{"name": "bytes", "configuration": {"endian": "little"}},
+                           {"name": "numcodecs.shuffle", "configuration": {"elementsize": 2}},
+                           {"name": "zstd", "configuration": {"level": 3, "checksum": False}}], "uint16"),
+    "shuffle4_be_f32": ([{"name": "bytes", "configuration": {"endian": "big"}},
+                         {"name": "numcodecs.shuffle", "configuration": {"elementsize": 4}}], "float32"),
+    "shuffle2_be_gzip_i16": ([{"name": "bytes", "configuration": {"endian": "big"}},
+                              {"name": "numcodecs.shuffle", "configuration": {"elementsize": 2}},
+                              {"name": "gzip", "configuration": {"level": 1}}], "int16"),
     "sharded_crc": ([{"name": "sharding_indexed", "configuration": {
         "chunk_shape": [8, 8, 8], "codecs": [{"name": "bytes", "configuration": {"endian": "little"}},
                                              {"name": "crc32c"}],

@@ -176,6 +176,56 @@ __global__ __launch_bounds__(SCATTER_THREADS) void k_scatter_rows(
     }
     return;
   }
+  if (P.shuffle && !fill && (es == 2 || es == 4)) {
+    // Fused unshuffle, 16 output bytes per thread: byte plane k of the chunk holds byte k of every
+    // element (shuffle_codec.rs:109-129), so 16/es consecutive elements take 16/es bytes from each
+    // plane (one 8- or 4-byte load per plane) and are interleaved with byte permutes into one
+    // 16-byte store. Needs rows of whole vectors on aligned plane and output addresses.
+    const uint32_t epv = 16 / es;  // elements per vector
+    const uint64_t s0 = (s_src[0] - it.src) / es;
+    bool vec_ok = (L % epv) == 0 && (P.nelem % epv) == 0 && ((it.src & 15) == 0);
+    for (uint32_t r = 0; r < nr && vec_ok; r++)
+      vec_ok = (((s_src[r] - it.src) / es) % epv) == 0 && (s_dst[r] & 15) == 0;
+    (void)s0;
+    if (vec_ok) {
+      const uint32_t vpr = (uint32_t)(L / epv);
+      const uint32_t total = nr * vpr;
+      const uint8_t *base = (const uint8_t *)it.src;
+      for (uint32_t v = threadIdx.x; v < total; v += SCATTER_THREADS) {
+        const uint32_t r = v / vpr, c = v % vpr;
+        const uint64_t e0 = (s_src[r] - it.src) / es + (uint64_t)c * epv;  // first element
+        uint32_t w[4];
+        if (es == 2) {
+          const uint2 a = *(const uint2 *)(base + e0), b = *(const uint2 *)(base + P.nelem + e0);
+          // bytes of element j: plane 0 byte j, plane 1 byte j (swapped for big-endian u16)
+          const uint2 lo = swap ? b : a, hi = swap ? a : b;
+          w[0] = __builtin_amdgcn_perm(hi.x, lo.x, 0x05010400u);
+          w[1] = __builtin_amdgcn_perm(hi.x, lo.x, 0x07030602u);
+          w[2] = __builtin_amdgcn_perm(hi.y, lo.y, 0x05010400u);
+          w[3] = __builtin_amdgcn_perm(hi.y, lo.y, 0x07030602u);
+        } else {
+          uint32_t pl[4];
+#pragma unroll
+          for (int k = 0; k < 4; k++) pl[k] = *(const uint32_t *)(base + (uint64_t)k * P.nelem + e0);
+          // element j = bytes j of planes 0..3; a 4x4 byte transpose
+          const uint32_t t0 = __builtin_amdgcn_perm(pl[1], pl[0], 0x05010400u);  // p0b0 p1b0 p0b1 p1b1
+          const uint32_t t1 = __builtin_amdgcn_perm(pl[1], pl[0], 0x07030602u);  // p0b2 p1b2 p0b3 p1b3
+          const uint32_t t2 = __builtin_amdgcn_perm(pl[3], pl[2], 0x05010400u);
+          const uint32_t t3 = __builtin_amdgcn_perm(pl[3], pl[2], 0x07030602u);
+          w[0] = __builtin_amdgcn_perm(t2, t0, 0x05040100u);  // e0: p0b0 p1b0 p2b0 p3b0
+          w[1] = __builtin_amdgcn_perm(t2, t0, 0x07060302u);  // e1
+          w[2] = __builtin_amdgcn_perm(t3, t1, 0x05040100u);  // e2
+          w[3] = __builtin_amdgcn_perm(t3, t1, 0x07060302u);  // e3
+          if (swap) {
+#pragma unroll
+            for (int k = 0; k < 4; k++) w[k] = swap_word(w[k], P.comp);
+          }
+        }
+        *(uint4 *)(s_dst[r] + (uint64_t)c * 16) = make_uint4(w[0], w[1], w[2], w[3]);
+      }
+      return;
+    }
+  }
   // Element path (unaligned rows, odd sizes, fused unshuffle).
   const uint64_t total = (uint64_t)nr * L;
   const uint4 fv = fill_elem(P);
