@@ -479,9 +479,11 @@ def run_gpu(args, rank, world, dev):
         L.check(lib.zgpu_plan_create(chain._h, len(out_shape), arr, n, L.u64s(out_shape),
                                      L.ENC_DEVICE | L.OUT_DEVICE, C.byref(plan)))
         plans.append((plan, out, (C.c_int32 * n)()))
-    stream = torch.cuda.Stream(dev)  # the library launches on this stream; events are recorded on it
+    # the library launches on this stream; events are recorded on it. Independent parts (pyramid
+    # levels) run concurrently, one stream each: part 0 (the largest level, the longest serial chain)
+    # on `stream` at high priority, so its kernels take CUs first
+    stream = torch.cuda.Stream(dev, priority=-1) if len(plans) > 1 else torch.cuda.Stream(dev)
     sp = C.c_void_p(stream.cuda_stream)
-    # independent parts (pyramid levels) run concurrently, one stream each; part 0 on `stream`
     side = [torch.cuda.Stream(dev) for _ in plans[1:]]
     part_streams = [stream] + side
     part_sp = [C.c_void_p(st.cuda_stream) for st in part_streams]
