@@ -182,8 +182,10 @@ int main(int argc, char **argv) {
     CK(hipMemcpyFromSymbol(z, HIP_SYMBOL(zgpu::g_zprof), sizeof(z)));
     const double nb = z[4] ? (double)z[4] : 1.0;
     const double nbt = z[6] ? (double)z[6] : 1.0;
-    printf("exec_item slow matches per batch: n>512 %.2f 16<=d<n %.2f d<16 %.2f other(split src) %.2f | resolve %.0f rounds %.2f | (other total %llu) | batches %llu"
-           " seqs/batch %.1f\n", z[0] / nbt, z[1] / nbt, z[2] / nbt, z[5] / nbt, z[3] / nbt, z[4] / nbt, z[5], z[6], z[7] / nbt);
+    const double per = (double)n * 3;  // per frame (3 reps)
+    printf("exec_item per frame (Mticks): head %.2f stage %.2f lits %.2f resolve %.2f singles %.2f raw/rle/tail %.2f | total %.2f | batches %.0f\n",
+           z[0] / per / 1e6, z[1] / per / 1e6, z[2] / per / 1e6, z[3] / per / 1e6, z[4] / per / 1e6, z[5] / per / 1e6,
+           z[6] / per / 1e6, z[7] / per);
   }
 #endif
   printf("total %.3f ms -> %.2f GB/s decoded\n", tot, (double)n * chunk / tot / 1e6);

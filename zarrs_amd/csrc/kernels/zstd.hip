@@ -1944,44 +1944,63 @@ __device__ __forceinline__ uint64_t x_far_bound(const XOut &O, uint64_t wend) {
   const uint64_t lim = wend + ZBATCH > XRING ? wend + ZBATCH - XRING : 0;
   return min<uint64_t>(lim, O.flushed) & ~(uint64_t)127;
 }
-// n bytes of global memory into the ring at the output position, 8 KiB pieces (every load of a
+// n bytes of global memory into the ring at the output position, 16 KiB pieces (every load of a
 // piece in flight before its first LDS write)
-constexpr uint32_t XPIECE = 8192;
 __device__ __forceinline__ void x_copy(ZXSmem &S, XOut &O, const uint8_t *src, uint64_t n) {
-  constexpr int R = XPIECE / 16 / 64 + 1;
-  for (uint64_t done = 0; done < n;) {
-    const uint32_t c = (uint32_t)min<uint64_t>(n - done, XPIECE);
-    x_reserve(S, O, O.pos + c);
-    const uint8_t *sp = src + done;
-    const uintptr_t base = (uintptr_t)sp & ~(uintptr_t)15;
-    const uint32_t head = (uint32_t)((uintptr_t)sp - base);
-    const uint32_t nvec = (head + c + 15) >> 4;
-    zv4u v[R];
+  const int lane = lane_id();
+  if (!n) return;
+  // bytes up to the ring's next 16-B boundary, then 16-B chunks stored aligned (unaligned 16-B LDS
+  // accesses are replayed, cdna_hip_programming.md Guideline 17): every chunk's source is
+  // misaligned by the same m, so a chunk is two aligned global vectors and four byte-aligns
+  uint64_t done = min<uint64_t>(n, (16 - (O.pos & 15)) & 15);
+  if (done) {
+    x_reserve(S, O, O.pos + done);
+    if (lane < (int)done) S.ring[(O.pos + lane) & XRMASK] = src[lane];
+    O.pos += done;
+  }
+  const uintptr_t s0 = (uintptr_t)(src + done);
+  const uint32_t m = (uint32_t)(s0 & 15), mq = m >> 2, mr = m & 3;
+  const zv4u *sa = (const zv4u *)(s0 & ~(uintptr_t)15);
+  const uint64_t nch = (n - done) >> 4;
+  constexpr uint32_t R = 16, PC = 64 * R;  // chunks per piece: 16 KiB (one wave per CU: VGPRs are free)
+  for (uint64_t c0 = 0; c0 < nch; c0 += PC) {
+    const uint32_t cn = (uint32_t)min<uint64_t>(PC, nch - c0);
+    x_reserve(S, O, O.pos + 16ull * cn);
+    zv4u lo[R], hi[R];
 #pragma unroll
-    for (int r = 0; r < R; r++) {
-      const uint32_t idx = lane_id() + 64 * r;
-      if (idx < nvec) v[r] = __builtin_nontemporal_load((const zv4u *)(base + 16ull * idx));
-    }
-#pragma unroll
-    for (int r = 0; r < R; r++) {
-      const uint32_t idx = lane_id() + 64 * r;
-      if (idx < nvec) {
-        const int64_t k0 = (int64_t)(16 * idx) - head;  // output byte of the vector's first byte
-        const uint64_t q = O.pos + k0;
-        if (k0 >= 0 && k0 + 16 <= (int64_t)c && (q & XRMASK) <= XRING - 16) {
-          __builtin_memcpy(&S.ring[q & XRMASK], &v[r], 16);
-        } else {
-          const uint32_t w[4] = {v[r].x, v[r].y, v[r].z, v[r].w};
-#pragma unroll
-          for (int j = 0; j < 16; j++) {
-            const int64_t k = k0 + j;
-            if (k >= 0 && k < (int64_t)c) S.ring[(O.pos + k) & XRMASK] = (uint8_t)(w[j >> 2] >> (8 * (j & 3)));
-          }
-        }
+    for (uint32_t r = 0; r < R; r++) {
+      const uint32_t i = lane + 64 * r;
+      if (i < cn) {
+        lo[r] = __builtin_nontemporal_load(sa + c0 + i);
+        hi[r] = m ? __builtin_nontemporal_load(sa + c0 + i + 1) : lo[r];
       }
     }
-    O.pos += c;
-    done += c;
+#pragma unroll
+    for (uint32_t r = 0; r < R; r++) {
+      const uint32_t i = lane + 64 * r;
+      if (i < cn) {
+        const uint32_t w[8] = {lo[r].x, lo[r].y, lo[r].z, lo[r].w, hi[r].x, hi[r].y, hi[r].z, hi[r].w};
+        zv4u v;
+        // m is uniform: one branch taken by the whole wave
+        if (mq == 0) v = zv4u{__builtin_amdgcn_alignbyte(w[1], w[0], mr), __builtin_amdgcn_alignbyte(w[2], w[1], mr),
+                              __builtin_amdgcn_alignbyte(w[3], w[2], mr), __builtin_amdgcn_alignbyte(w[4], w[3], mr)};
+        else if (mq == 1) v = zv4u{__builtin_amdgcn_alignbyte(w[2], w[1], mr), __builtin_amdgcn_alignbyte(w[3], w[2], mr),
+                                   __builtin_amdgcn_alignbyte(w[4], w[3], mr), __builtin_amdgcn_alignbyte(w[5], w[4], mr)};
+        else if (mq == 2) v = zv4u{__builtin_amdgcn_alignbyte(w[3], w[2], mr), __builtin_amdgcn_alignbyte(w[4], w[3], mr),
+                                   __builtin_amdgcn_alignbyte(w[5], w[4], mr), __builtin_amdgcn_alignbyte(w[6], w[5], mr)};
+        else v = zv4u{__builtin_amdgcn_alignbyte(w[4], w[3], mr), __builtin_amdgcn_alignbyte(w[5], w[4], mr),
+                      __builtin_amdgcn_alignbyte(w[6], w[5], mr), __builtin_amdgcn_alignbyte(w[7], w[6], mr)};
+        *(zv4u *)&S.ring[(O.pos + 16ull * i) & XRMASK] = v;
+      }
+    }
+    O.pos += 16ull * cn;
+  }
+  done += 16 * nch;
+  const uint32_t tail = (uint32_t)(n - done);
+  if (tail) {
+    x_reserve(S, O, O.pos + tail);
+    if (lane < (int)tail) S.ring[(O.pos + lane) & XRMASK] = src[done + lane];
+    O.pos += tail;
   }
   __syncthreads();
 }
@@ -2293,6 +2312,7 @@ __global__ __launch_bounds__(64) void k_zstd_exec_item(ZgItem *items, uint32_t *
   const uint32_t item = blockIdx.x;
   const int lane = lane_id();
   ZP_DECL;
+  ZP_T(t_all);
   if (zmode[item] != ZMODE_PARALLEL || status[item]) return;
   const ZgItem it = items[item];
   const uint8_t *in = (const uint8_t *)it.src;
@@ -2309,10 +2329,13 @@ __global__ __launch_bounds__(64) void k_zstd_exec_item(ZgItem *items, uint32_t *
     if (flags & ZBF_FIRST) fstart = bstart;
     if (bstart != O.pos) { err = ZG_CORRUPT_STREAM; break; }
     const uint64_t bend = bstart + bsize;
+    ZP_T(t5);
     if (type == ZB_RAW) {
       x_copy(S, O, in + U(B[bi].in_off), bsize);
+      ZP_ADD(5, t5);
     } else if (type == ZB_RLE) {
       x_fill(S, O, (uint8_t)U(in[U(B[bi].in_off)]), bsize);
+      ZP_ADD(5, t5);
     } else {
       const uint32_t ltype = (flags >> 2) & 3, regen = U(B[bi].regen), nseq = U(B[bi].nseq);
       const uint8_t *lsrc =
@@ -2367,13 +2390,15 @@ __global__ __launch_bounds__(64) void k_zstd_exec_item(ZgItem *items, uint32_t *
             err = ZG_CORRUPT_STREAM;
             break;
           }
+          ZP_ADD(0, th);
+          ZP_T(ts);
           x_reserve(S, O, out_base + span);
           const uint64_t fb = x_far_bound(O, out_base + span);
           staged = x_stage(S, O.out, fb, mstart, r_of, sml, lsrc + litpos, lspan, fe, sb);
+          ZP_ADD(1, ts);
         }
 #ifdef ZG_PROFILE
-        zp_acc[6] += 1;
-        zp_acc[7] += cnt;
+        zp_acc[7] += 1;
 #endif
         nx_base = base + (staged ? cnt : 1u);
         if (nx_base < nseq && lane < (int)(nseq - nx_base)) {
@@ -2383,6 +2408,7 @@ __global__ __launch_bounds__(64) void k_zstd_exec_item(ZgItem *items, uint32_t *
           nx_of = q[2];
         }
         if (!staged) {  // one sequence alone: its literal run, then its match in chunks
+          ZP_T(t4);
           const uint32_t ll = U(__builtin_amdgcn_readlane(r_ll, 0)), ml = U(__builtin_amdgcn_readlane(r_ml, 0));
           const uint32_t of = U(__builtin_amdgcn_readlane(r_of, 0));
           if (litpos + ll > regen || O.pos + ll + ml > bend) { err = ZG_CORRUPT_STREAM; break; }
@@ -2390,11 +2416,12 @@ __global__ __launch_bounds__(64) void k_zstd_exec_item(ZgItem *items, uint32_t *
           litpos += ll;
           if (ml && !x_long_match(S, O, fstart, of, ml, bend)) { err = ZG_CORRUPT_STREAM; break; }
           base += 1;
+          ZP_ADD(4, t4);
           continue;
         }
         // literals of the batch into place: every lane moves its own run, 16 bytes at a time (loads
         // of a group of four before its stores), bytes where the run wraps the ring
-        ZP_T(tl);
+        ZP_T(tl2);
         if (mine && r_ll) {
           const uint32_t ll = r_ll, o = (uint32_t)out_base + b - r_ml - ll;
           const uint8_t *ls = S.lit_stage + (a - ll);
@@ -2417,29 +2444,20 @@ __global__ __launch_bounds__(64) void k_zstd_exec_item(ZgItem *items, uint32_t *
           }
         }
         __syncthreads();
+        ZP_ADD(2, tl2);
         ZP_T(t3);
-#ifdef ZG_PROFILE
-        uint64_t rp[4] = {0, 0, 0, 0};
-        const uint32_t nr = x_resolve(S, mstart, r_of, sml, fe, sb, rp);
-        zp_acc[0] += rp[0];
-        zp_acc[1] += rp[1];
-        zp_acc[2] += rp[2];
-        zp_acc[5] += rp[3];
-#else
         const uint32_t nr = x_resolve(S, mstart, r_of, sml, fe, sb);
-#endif
         ZP_ADD(3, t3);
-#ifdef ZG_PROFILE
-        zp_acc[4] += nr;
-#endif
         (void)nr;
         O.pos = out_base + span;
         litpos += lspan;
         base += cnt;
       }
       if (!err) {
+        ZP_T(t5b);
         if (litpos > regen || O.pos + (regen - litpos) != bend) err = ZG_CORRUPT_STREAM;
         else x_copy(S, O, lsrc + litpos, regen - litpos);
+        ZP_ADD(5, t5b);
       }
     }
     if (!err && O.pos != bend) err = ZG_CORRUPT_STREAM;
@@ -2452,6 +2470,7 @@ __global__ __launch_bounds__(64) void k_zstd_exec_item(ZgItem *items, uint32_t *
     }
   }
   if (!err) x_flush(S, O);
+  ZP_ADD(6, t_all);
   ZP_FLUSH;
   if (lane == 0) {
     if (err) {
