@@ -183,9 +183,10 @@ int main(int argc, char **argv) {
     const double nb = z[4] ? (double)z[4] : 1.0;
     const double nbt = z[6] ? (double)z[6] : 1.0;
     const double per = (double)n * 3;  // per frame (3 reps)
-    printf("exec_item per frame (Mticks): head %.2f stage %.2f lits %.2f resolve %.2f singles %.2f raw/rle/tail %.2f | total %.2f | batches %.0f\n",
+    printf("exec_item per frame (Mticks): single-lits %.2f stage %.2f single-matches %.2f resolve %.2f singles %.2f raw/rle/tail %.2f | total %.2f | batches %.0f\n",
            z[0] / per / 1e6, z[1] / per / 1e6, z[2] / per / 1e6, z[3] / per / 1e6, z[4] / per / 1e6, z[5] / per / 1e6,
-           z[6] / per / 1e6, z[7] / per);
+           z[6] / per / 1e6, (double)(z[7] & 0xFFFFFFFFu) / per);
+    printf("single matches with d < 16 per frame: %.0f\n", (double)(z[7] >> 32) / per);
   }
 #endif
   printf("total %.3f ms -> %.2f GB/s decoded\n", tot, (double)n * chunk / tot / 1e6);

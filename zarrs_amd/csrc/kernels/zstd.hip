@@ -2283,20 +2283,90 @@ __device__ uint32_t x_resolve(ZXSmem &S, uint64_t ms, uint32_t d, uint32_t n, ui
   return rounds;
 }
 
-// one long match (or one whose far part does not fit a batch), in ZBATCH chunks; false if corrupt
+// n <= d bytes from ring position spos to ring position dpos = spos + d (the source precedes the
+// destination entirely): bytes up to dpos's 16-B boundary, then aligned 16-B stores, each built from
+// two aligned ring vectors with byte-aligns (the ring size is a multiple of 16: no vector wraps)
+__device__ __forceinline__ void x_ring_copy(ZXSmem &S, uint64_t dpos, uint64_t spos, uint32_t n) {
+  const int lane = lane_id();
+  const uint32_t head = min<uint32_t>(n, (uint32_t)((16 - (dpos & 15)) & 15));
+  if (lane < (int)head) S.ring[(dpos + lane) & XRMASK] = S.ring[(spos + lane) & XRMASK];
+  const uint64_t s1 = spos + head;
+  const uint32_t m = (uint32_t)(s1 & 15), mq = m >> 2, mr = m & 3;
+  const uint32_t nch = (n - head) >> 4;
+  for (uint32_t i = lane; i < nch; i += 64) {
+    const uint64_t sv = (s1 + 16ull * i) & ~(uint64_t)15;
+    const zv4u lo = *(const zv4u *)&S.ring[sv & XRMASK];
+    const zv4u hi = m ? *(const zv4u *)&S.ring[(sv + 16) & XRMASK] : lo;
+    const uint32_t w[8] = {lo.x, lo.y, lo.z, lo.w, hi.x, hi.y, hi.z, hi.w};
+    zv4u v;
+    if (mq == 0) v = zv4u{__builtin_amdgcn_alignbyte(w[1], w[0], mr), __builtin_amdgcn_alignbyte(w[2], w[1], mr),
+                          __builtin_amdgcn_alignbyte(w[3], w[2], mr), __builtin_amdgcn_alignbyte(w[4], w[3], mr)};
+    else if (mq == 1) v = zv4u{__builtin_amdgcn_alignbyte(w[2], w[1], mr), __builtin_amdgcn_alignbyte(w[3], w[2], mr),
+                               __builtin_amdgcn_alignbyte(w[4], w[3], mr), __builtin_amdgcn_alignbyte(w[5], w[4], mr)};
+    else if (mq == 2) v = zv4u{__builtin_amdgcn_alignbyte(w[3], w[2], mr), __builtin_amdgcn_alignbyte(w[4], w[3], mr),
+                               __builtin_amdgcn_alignbyte(w[5], w[4], mr), __builtin_amdgcn_alignbyte(w[6], w[5], mr)};
+    else v = zv4u{__builtin_amdgcn_alignbyte(w[4], w[3], mr), __builtin_amdgcn_alignbyte(w[5], w[4], mr),
+                  __builtin_amdgcn_alignbyte(w[6], w[5], mr), __builtin_amdgcn_alignbyte(w[7], w[6], mr)};
+    *(zv4u *)&S.ring[(dpos + head + 16ull * i) & XRMASK] = v;
+  }
+  const uint32_t t0 = head + 16 * nch, tail = n - t0;
+  if (lane < (int)tail) S.ring[(dpos + t0 + lane) & XRMASK] = S.ring[(spos + t0 + lane) & XRMASK];
+  __syncthreads();
+}
+
+// One long match (or one whose far part does not fit a batch); false if corrupt. Periods 1/2/4/8 are
+// pattern stores; other distances copy chunks whose source lies wholly before them: from the ring
+// (x_ring_copy) or, below the far bound, from the flushed output (x_copy).
 __device__ __forceinline__ bool x_long_match(ZXSmem &S, XOut &O, uint64_t fstart, uint32_t off, uint64_t ml, uint64_t bend) {
+  const int lane = lane_id();
   const uint64_t p = O.pos;
   if (off == 0 || off > p - fstart || p + ml > bend) return false;
-  for (uint64_t c0 = 0; c0 < ml; c0 += ZBATCH) {
-    const uint32_t c = (uint32_t)min<uint64_t>(ZBATCH, ml - c0);
+  if (off == 1 || off == 2 || off == 4 || off == 8) {
+    uint64_t pat = 0;
+    for (uint32_t j = 0; j < off; j++) pat |= (uint64_t)S.ring[(p - off + j) & XRMASK] << (8 * j);
+    if (off == 1) pat *= 0x0101010101010101ull;
+    else if (off == 2) pat *= 0x0001000100010001ull;
+    else if (off == 4) pat |= pat << 32;
+    for (uint64_t c0 = 0; c0 < ml;) {
+      const uint32_t c = (uint32_t)min<uint64_t>(ZBATCH, ml - c0);
+      x_reserve(S, O, O.pos + c);
+      // byte k of the match is pat byte (k mod 8)
+      const uint32_t head = min<uint32_t>(c, (uint32_t)((16 - (O.pos & 15)) & 15));
+      if (lane < (int)head) S.ring[(O.pos + lane) & XRMASK] = (uint8_t)(pat >> (8 * ((c0 + lane) & 7)));
+      const uint32_t sh = 8 * ((c0 + head) & 7);
+      const uint64_t rp = sh ? (pat >> sh) | (pat << (64 - sh)) : pat;
+      const zv4u v = zv4u{(uint32_t)rp, (uint32_t)(rp >> 32), (uint32_t)rp, (uint32_t)(rp >> 32)};
+      const uint32_t nch = (c - head) >> 4;
+      for (uint32_t i = lane; i < nch; i += 64) *(zv4u *)&S.ring[(O.pos + head + 16ull * i) & XRMASK] = v;
+      const uint32_t t0 = head + 16 * nch, tail = c - t0;
+      if (lane < (int)tail) S.ring[(O.pos + t0 + lane) & XRMASK] = (uint8_t)(pat >> (8 * ((c0 + t0 + lane) & 7)));
+      __syncthreads();
+      O.pos += c;
+      c0 += c;
+    }
+    return true;
+  }
+  for (uint64_t c0 = 0; c0 < ml;) {
+    // copy from D bytes back, D the largest multiple of the distance not beyond the match start:
+    // the chunk's source is then contiguous, wholly before the chunk and final (chunks double
+    // until ZBATCH for short distances)
+    const uint64_t D = (uint64_t)off * ((c0 + off) / off);
+    const uint32_t c = (uint32_t)min<uint64_t>(min<uint64_t>(ZBATCH, ml - c0), D);
+    const uint64_t src = p + c0 - D;
     x_reserve(S, O, p + c0 + c);
     const uint64_t fb = x_far_bound(O, p + c0 + c);
-    const uint32_t n = lane_id() == 0 ? c : 0u;
-    uint64_t fe;
-    int64_t sb;
-    x_stage(S, O.out, fb, p + c0, off, n, nullptr, 0, fe, sb);  // <= 258 vectors: always fits
-    x_resolve(S, p + c0, off, n, fe, sb);
-    O.pos = p + c0 + c;
+    if (src >= fb) {
+      x_ring_copy(S, p + c0, src, c);
+      O.pos = p + c0 + c;
+    } else if (src + c <= fb) {
+      x_copy(S, O, O.out + src, c);  // flushed, whole 128-B lines: no stale L1 line (x_far_bound)
+    } else {
+      const uint32_t c1 = (uint32_t)(fb - src);
+      x_copy(S, O, O.out + src, c1);
+      x_ring_copy(S, p + c0 + c1, src + c1, c - c1);
+      O.pos = p + c0 + c;
+    }
+    c0 += c;
   }
   return true;
 }
@@ -2390,7 +2460,6 @@ __global__ __launch_bounds__(64) void k_zstd_exec_item(ZgItem *items, uint32_t *
             err = ZG_CORRUPT_STREAM;
             break;
           }
-          ZP_ADD(0, th);
           ZP_T(ts);
           x_reserve(S, O, out_base + span);
           const uint64_t fb = x_far_bound(O, out_base + span);
@@ -2414,7 +2483,13 @@ __global__ __launch_bounds__(64) void k_zstd_exec_item(ZgItem *items, uint32_t *
           if (litpos + ll > regen || O.pos + ll + ml > bend) { err = ZG_CORRUPT_STREAM; break; }
           x_copy(S, O, lsrc + litpos, ll);
           litpos += ll;
+          ZP_ADD(0, t4);
+          ZP_T(t4m);
           if (ml && !x_long_match(S, O, fstart, of, ml, bend)) { err = ZG_CORRUPT_STREAM; break; }
+          ZP_ADD(2, t4m);
+#ifdef ZG_PROFILE
+          if (of < 16) zp_acc[7] += 1ull << 32;
+#endif
           base += 1;
           ZP_ADD(4, t4);
           continue;
@@ -2444,7 +2519,6 @@ __global__ __launch_bounds__(64) void k_zstd_exec_item(ZgItem *items, uint32_t *
           }
         }
         __syncthreads();
-        ZP_ADD(2, tl2);
         ZP_T(t3);
         const uint32_t nr = x_resolve(S, mstart, r_of, sml, fe, sb);
         ZP_ADD(3, t3);
