@@ -1905,6 +1905,7 @@ struct ZXSmem {
   uint8_t ring[XRING];
   zv4u stage[XSTAGE_V];
   uint8_t lit_stage[ZBATCH + 16];
+  uint8_t vown[XSTAGE_V];  // staged far vector -> the lane (match) it belongs to
   uint32_t pfx_lit[64], pfx_out[64], pfx_nv[64], own_pv[64];
   uint64_t own_v0[64];
   XReady rq[64];        // the round's ready matches
@@ -2036,9 +2037,9 @@ __device__ __forceinline__ bool x_stage(ZXSmem &S, const uint8_t *out, uint64_t 
   if (total > XSTAGE_V) return false;
   const uint32_t pv = incl - nv;
   sb = (int64_t)pv * 16 - (int64_t)v0 * 16;
-  S.pfx_nv[lane] = incl;
   S.own_pv[lane] = pv;
   S.own_v0[lane] = v0;
+  for (uint32_t j = 0; j < nv; j++) S.vown[pv + j] = (uint8_t)lane;  // stage vector -> its lane
   __syncthreads();
   const uintptr_t lbase = (uintptr_t)lit & ~(uintptr_t)15;
   const uint32_t lhead = (uint32_t)((uintptr_t)lit - lbase);
@@ -2053,11 +2054,7 @@ __device__ __forceinline__ bool x_stage(ZXSmem &S, const uint8_t *out, uint64_t 
   for (int r = 0; r < XR_FAR; r++) {
     const uint32_t f = lane + 64 * r;
     if (f < total) {
-      uint32_t lo = 0, hi = 63;  // the lane whose vectors hold f: first with pfx_nv > f
-      while (lo < hi) {
-        const uint32_t mid = (lo + hi) >> 1;
-        if (S.pfx_nv[mid] > f) hi = mid; else lo = mid + 1;
-      }
+      const uint32_t lo = S.vown[f];
       fv[r] = *(const zv4u *)(out + 16 * (S.own_v0[lo] + (f - S.own_pv[lo])));
     }
   }
