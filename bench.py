@@ -389,7 +389,21 @@ class C5:
             dec_total += int(np.prod(sel)) * 2
             per_level[li].append(make_desc((t.data_ptr(), olens[i]), cs, [0, 0, 0], sel, start))
             self.masks[li][tuple(slice(st, st + n_) for st, n_ in zip(start, sel))] = True
-        self.parts = [(self.chain, d, o, list(o.shape)) for d, o in zip(per_level, self.outs)]
+        # plans (chunk batches) and the streams they run on: the largest level is split in two halves
+        # on streams of their own (its entropy-decode kernels are throughput-bound, its per-chunk
+        # sequence execution is not, so halving the batch shortens its chain), the next level on a
+        # third stream, the small levels one after another on a fourth (GPU_MAX_HW_QUEUES is 4)
+        l0 = per_level[0]
+        halves = lpt_partition([int(dsc.enc_len) for dsc in l0], 2)  # balanced by encoded size
+        groups = [[l0[i] for i in hv] for hv in halves] + per_level[1:]
+        outs_g = [self.outs[0], self.outs[0]] + self.outs[1:]
+        self.parts, lane_of = [], []
+        for gi, (d, o) in enumerate(zip(groups, outs_g)):
+            if d:
+                self.parts.append((self.chain, d, o, list(o.shape)))
+                lane_of.append(min(gi, 3))
+        self.lanes = [[p for p, l in enumerate(lane_of) if l == k] for k in range(4)]
+        self.lanes = [ln for ln in self.lanes if ln]
         self.decoded_bytes = dec_total
         self.step_bytes = all_bytes
         self.ratio = sum(int(x) for x in lens) / max(1, sum(enc_sizes))
@@ -470,7 +484,8 @@ def run_gpu(args, rank, world, dev):
     W = WORKLOADS[args.workload](args, rank, world, dev)
     lib = L.load()
     plans = []  # one prepared plan per part (e.g. per pyramid level: one chunk shape per plan)
-    for chain, descs, out, out_shape in W.parts:
+    part_plan = {}
+    for pi, (chain, descs, out, out_shape) in enumerate(W.parts):
         n = len(descs)
         if not n:
             continue
@@ -478,25 +493,32 @@ def run_gpu(args, rank, world, dev):
         plan = C.c_void_p()
         L.check(lib.zgpu_plan_create(chain._h, len(out_shape), arr, n, L.u64s(out_shape),
                                      L.ENC_DEVICE | L.OUT_DEVICE, C.byref(plan)))
+        part_plan[pi] = len(plans)
         plans.append((plan, out, (C.c_int32 * n)()))
+    # stream lanes: lists of plans executed in order on one stream; lanes run concurrently
+    lanes = getattr(W, "lanes", [[i] for i in range(len(W.parts))])
+    lanes = [[part_plan[i] for i in ln if i in part_plan] for ln in lanes]
+    lanes = [ln for ln in lanes if ln]
     # the library launches on this stream; events are recorded on it. Independent parts (pyramid
     # levels) run concurrently, one stream each: part 0 (the largest level, the longest serial chain)
     # on `stream` at high priority, so its kernels take CUs first
-    stream = torch.cuda.Stream(dev, priority=-1) if len(plans) > 1 else torch.cuda.Stream(dev)
+    stream = torch.cuda.Stream(dev, priority=-1) if len(lanes) > 1 else torch.cuda.Stream(dev)
     sp = C.c_void_p(stream.cuda_stream)
-    side = [torch.cuda.Stream(dev) for _ in plans[1:]]
-    part_streams = [stream] + side
-    part_sp = [C.c_void_p(st.cuda_stream) for st in part_streams]
+    side = [torch.cuda.Stream(dev, priority=-1 if li < 2 else 0) for li in range(1, len(lanes))]
+    lane_sp = [sp] + [C.c_void_p(st.cuda_stream) for st in side]
+    plan_sp = {pi: lane_sp[li] for li, ln in enumerate(lanes) for pi in ln}
 
     def enqueue_all():
         start = torch.cuda.Event()
         start.record(stream)
         for st in side:
             st.wait_event(start)
-        for (plan, out, _), s_ in zip(plans, part_sp):
-            rc = lib.zgpu_plan_execute(plan, out.data_ptr(), None, s_)
-            if rc:
-                raise RuntimeError(f"decode failed: {L.STATUS_NAMES[rc]} {L.last_error()}")
+        for li, ln in enumerate(lanes):
+            for pi in ln:
+                plan, out, _ = plans[pi]
+                rc = lib.zgpu_plan_execute(plan, out.data_ptr(), None, lane_sp[li])
+                if rc:
+                    raise RuntimeError(f"decode failed: {L.STATUS_NAMES[rc]} {L.last_error()}")
         for st in side:
             done = torch.cuda.Event()
             done.record(st)
@@ -509,12 +531,21 @@ def run_gpu(args, rank, world, dev):
         else:
             enqueue_all()
             rc = 0
-            for (plan, _, status), s_ in zip(plans, part_sp):
-                rc = rc or lib.zgpu_plan_status(plan, status, s_)
+            for pi, (plan, _, status) in enumerate(plans):
+                rc = rc or lib.zgpu_plan_status(plan, status, plan_sp[pi])
         if rc:
             raise RuntimeError(f"decode failed: {L.STATUS_NAMES[rc]} {L.last_error()}")
         W.after_decode()
 
+    if args.lane_times and len(lanes) > 1:  # diagnostics: each lane alone (stderr)
+        for li, ln in enumerate(lanes):
+            for _ in range(2):
+                t0 = time.perf_counter()
+                for pi in ln:
+                    plan, out, status = plans[pi]
+                    lib.zgpu_plan_execute(plan, out.data_ptr(), status, sp)
+                dt = time.perf_counter() - t0
+            print(f"lane {li} (plans {ln}) alone: {dt * 1e3:.2f} ms", file=sys.stderr)
     torch.cuda.synchronize()
     for _ in range(args.warmup):
         step()
@@ -612,6 +643,7 @@ def main():
     ap.add_argument("--cpu-seconds", type=float, default=15.0)
     ap.add_argument("--c5-scale", type=int, default=4, help="C5: divide the L0 y/x extents by this")
     ap.add_argument("--no-cpu", action="store_true")
+    ap.add_argument("--lane-times", action="store_true", help="print each stream lane's solo time (stderr)")
     ap.add_argument("--no-pmc", action="store_true", help="skip the rocprofv3 PMC traffic passes")
     ap.add_argument("--no-host-leg", dest="host_leg", action="store_false",
                     help="skip the PCIe-inclusive (host input/output) leg")
