@@ -1886,8 +1886,8 @@ namespace {
 // literals. A 64 KiB LDS ring holds the recent output; a match reaching further back reads output
 // this wave already flushed, staged into LDS per batch by 16-B loads issued together with the
 // batch's literal loads: one memory round trip per batch, not one per match. A batch is up to 64
-// sequences spanning <= ZBATCH bytes; its matches resolve in rounds: every pending match whose
-// source lies before the first unresolved one is copied by the whole wave, one after another.
+// sequences spanning <= ZBATCH bytes; its matches resolve in rounds: every pending match none of
+// whose source bytes is still to be written by another pending match is copied in the round.
 // (Matches crossing block boundaries are the rule in real data, e.g. byte-shuffled u16 images
 // whose high-byte plane is a chain of row- and plane-periodic copies, so there is no block-level
 // parallelism to take here; it is taken in k_zstd_lits / k_zstd_blocks, and across items.)
@@ -2143,8 +2143,9 @@ __device__ __forceinline__ void x_run(ZXSmem &S, const uint8_t *stg, uint64_t o,
 }
 
 // Resolve the staged matches (see x_stage) in rounds. A round takes every pending match whose source
-// lies before the first unresolved one (nothing it reads is still to be written). A short match
-// (<= 128 bytes, not overlapping its source, source wholly in the stage or the ring) is copied by its
+// bytes outside itself overlap no pending match's destination (exact dependencies: the rounds are the
+// depth of the batch's copy chain, about half the count of a first-unresolved frontier on C5's
+// high-byte planes, tools/lab/zstd_taint.cpp). A short match (<= 512 bytes, not overlapping its source, source wholly in the stage or the ring) is copied by its
 // own lane: all its 16-byte pieces loaded, then stored (the last piece ends at the match end,
 // rewriting its neighbour's bytes with the same values). Other matches are copied by the whole wave,
 // one after another: byte k is byte (k mod d) of the first period [ms - d, ms - d + min(n, d)),
@@ -2165,12 +2166,30 @@ __device__ uint32_t x_resolve(ZXSmem &S, uint64_t ms, uint32_t d, uint32_t n, ui
   const bool fast = splat || (n > 0 && n <= 512 && d >= n && dst_ok && (in_stage || in_ring));
   const uint8_t *sp = in_stage ? stg + ((int64_t)src + sb) : &S.ring[src & XRMASK];
   uint8_t *dp = &S.ring[ms & XRMASK];
+  // exact dependencies: the batch's matches whose destination overlaps the bytes this one reads
+  // from outside itself, [src, src + cl). Match starts ascend with the lane, so the first and last
+  // such match come from two binary searches over the lanes' starts (relative to lane 0's).
+  uint64_t dep = 0;
+  {
+    const uint64_t base0 = rl64(ms, 0);
+    const int32_t rm = (int32_t)(ms - base0), ra = (int32_t)(src - base0), rb = ra + (int32_t)cl - 1;
+    int ja = -1, jb = -1;
+#pragma unroll
+    for (int st = 64; st; st >>= 1) {
+      const int ca = ja + st, cb = jb + st;
+      const int32_t va = __shfl(rm, min(ca, 63), 64), vb = __shfl(rm, min(cb, 63), 64);
+      if (ca <= 63 && va <= ra) ja = ca;
+      if (cb <= 63 && vb <= rb) jb = cb;
+    }
+    const int32_t ea = __shfl(rm + (int32_t)n, max(ja, 0), 64);  // end of the match holding src
+    const int lo = ja < 0 ? 0 : (ea <= ra ? ja + 1 : ja);
+    if (pending && jb >= lo)
+      dep = (jb >= 63 ? ~0ull : ((2ull << jb) - 1)) & ~((1ull << lo) - 1);
+  }
   uint32_t rounds = 0;
   uint64_t pm;
   while ((pm = __ballot(pending)) != 0) {
-    const int first = __builtin_ctzll(pm);
-    const uint64_t F = rl64(ms, first);
-    const bool ready = pending && (lane == first || src + cl <= F);
+    const bool ready = pending && !(pm & dep);
 #ifdef ZG_PROFILE
     const uint64_t c0 = clock64();
 #endif
