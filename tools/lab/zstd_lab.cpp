@@ -124,7 +124,7 @@ int main(int argc, char **argv) {
   for (auto &bk : best) bk = 1e30f;
 #ifdef ZG_PROFILE
   {
-    unsigned long long z[8] = {0};
+    unsigned long long z[12] = {0};
     CK(hipMemcpyToSymbol(HIP_SYMBOL(zgpu::g_zprof), z, sizeof(z)));
   }
 #endif
@@ -178,7 +178,7 @@ int main(int argc, char **argv) {
   for (int k = 0; k < NK; k++) printf("  %-12s %8.3f ms\n", kn[k], best[k]);
 #ifdef ZG_PROFILE
   {
-    unsigned long long z[8];
+    unsigned long long z[12];
     CK(hipMemcpyFromSymbol(z, HIP_SYMBOL(zgpu::g_zprof), sizeof(z)));
     const double nb = z[4] ? (double)z[4] : 1.0;
     const double nbt = z[6] ? (double)z[6] : 1.0;
@@ -187,6 +187,8 @@ int main(int argc, char **argv) {
            z[0] / per / 1e6, z[1] / per / 1e6, z[2] / per / 1e6, z[3] / per / 1e6, z[4] / per / 1e6, z[5] / per / 1e6,
            z[6] / per / 1e6, (double)(z[7] & 0xFFFFFFFFu) / per);
     printf("single matches with d < 16 per frame: %.0f\n", (double)(z[7] >> 32) / per);
+    printf("resolve per frame (Mticks): ready %.2f fast copies %.2f slow copies %.2f | rounds %.0f\n", z[8] / per / 1e6,
+           z[9] / per / 1e6, z[10] / per / 1e6, (double)z[11] / per);
   }
 #endif
   printf("total %.3f ms -> %.2f GB/s decoded\n", tot, (double)n * chunk / tot / 1e6);

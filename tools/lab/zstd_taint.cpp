@@ -119,6 +119,17 @@ int main(int argc, char **argv) {
         rp++;
       }
     }
+    {
+      uint64_t c[5] = {}, bsum[5] = {};
+      for (size_t q = 0; q < ns; q++) {
+        const unsigned n = s[q].matchLength, d = s[q].offset;
+        if (!n) continue;
+        const int cls = n > 512 ? 4 : (d < n && n > 16 && (d == 1 || d == 2 || d == 4 || d == 8)) ? 0 : d >= n ? 1 : d < 16 ? 2 : 3;
+        c[cls]++; bsum[cls] += n;
+      }
+      printf("  matches: splat %lu (%lu B), straight %lu (%lu B), overlap d<16 %lu (%lu B), overlap d>=16 %lu (%lu B), >512 B %lu (%lu B)\n",
+             c[0], bsum[0], c[1], bsum[1], c[2], bsum[2], c[3], bsum[3], c[4], bsum[4]);
+    }
     printf("  batches %lu, rounds: frontier rule %lu, exact dependencies %lu\n", nbat, rf, rp);
   }
   for (int S : {2, 4, 8, 16, 32, 128}) {

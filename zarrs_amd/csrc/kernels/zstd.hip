@@ -26,11 +26,11 @@ namespace zgpu {
 
 #ifdef ZG_PROFILE
 // lab builds only (tools/lab/zstd_lab.cpp): k_zstd_exec per-phase shader-clock totals
-__device__ unsigned long long g_zprof[8];
-#define ZP_DECL uint64_t zp_acc[8] = {0, 0, 0, 0, 0, 0, 0, 0}
+__device__ unsigned long long g_zprof[12];
+#define ZP_DECL uint64_t zp_acc[12] = {0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0}
 #define ZP_T(v) const uint64_t v = clock64()
 #define ZP_ADD(slot, t0) zp_acc[slot] += clock64() - (t0)
-#define ZP_FLUSH do { if (__lane_id() == 0) for (int k_ = 0; k_ < 8; k_++) atomicAdd(&g_zprof[k_], (unsigned long long)zp_acc[k_]); } while (0)
+#define ZP_FLUSH do { if (__lane_id() == 0) for (int k_ = 0; k_ < 12; k_++) atomicAdd(&g_zprof[k_], (unsigned long long)zp_acc[k_]); } while (0)
 #else
 #define ZP_DECL
 #define ZP_T(v)
@@ -2161,7 +2161,8 @@ __device__ uint32_t x_resolve(ZXSmem &S, uint64_t ms, uint32_t d, uint32_t n, ui
   // the short-match path: source and destination contiguous in one buffer each
   const bool in_stage = src + n <= fe, in_ring = src >= fe && (src & XRMASK) + n <= XRING;
   const bool dst_ok = (ms & XRMASK) + n <= XRING;
-  const bool splat = n > 16 && n <= 512 && d < n && (d == 1 || d == 2 || d == 4 || d == 8) && dst_ok &&
+  // period < 16 overlapping its own output: stores of the period repeated (see below)
+  const bool splat = n <= 512 && d < n && d < 16 && dst_ok &&
                      (src + d <= fe || (src >= fe && (src & XRMASK) + d <= XRING));
   const bool fast = splat || (n > 0 && n <= 512 && d >= n && dst_ok && (in_stage || in_ring));
   const uint8_t *sp = in_stage ? stg + ((int64_t)src + sb) : &S.ring[src & XRMASK];
@@ -2188,26 +2189,42 @@ __device__ uint32_t x_resolve(ZXSmem &S, uint64_t ms, uint32_t d, uint32_t n, ui
   }
   uint32_t rounds = 0;
   uint64_t pm;
-  while ((pm = __ballot(pending)) != 0) {
+  while (true) {
+#ifdef ZG_PROFILE
+    const uint64_t cr = clock64();
+#endif
+    if ((pm = __ballot(pending)) == 0) break;
     const bool ready = pending && !(pm & dep);
 #ifdef ZG_PROFILE
     const uint64_t c0 = clock64();
 #endif
     if (ready && splat) {
-      // period 1, 2, 4 or 8: every 16-byte piece is the period repeated
+      // period d < 16: P = the first 16 bytes of the periodic extension (the period doubled until
+      // it fills 16 bytes). With L = d * floor(16 / d), byte j of every 16-byte store at a multiple
+      // of L is byte j of P -- the bytes past L included, so consecutive stores overlap with equal
+      // values. The last < 16 bytes, from the next multiple of L, are P's first bytes, stored 8/4/2/1.
       const uint8_t *pp = src + d <= fe ? stg + ((int64_t)src + sb) : &S.ring[src & XRMASK];
-      uint64_t pat = 0;
-      for (uint32_t j = 0; j < d; j++) pat |= (uint64_t)pp[j] << (8 * j);
-      if (d == 1) pat *= 0x0101010101010101ull;
-      else if (d == 2) pat *= 0x0001000100010001ull;
-      else if (d == 4) pat |= pat << 32;
-      const zv4u v = zv4u{(uint32_t)pat, (uint32_t)(pat >> 32), (uint32_t)pat, (uint32_t)(pat >> 32)};
-      for (uint32_t k = 0; k + 16 <= n; k += 16) st16(dp + k, v);
-      if (n & 15) {  // the last 16 bytes start at phase (n - 16) mod d of the period
-        const uint32_t sh = 8 * ((n - 16) & (d - 1));
-        const uint64_t rp = sh ? (pat >> sh) | (pat << (64 - sh)) : pat;
-        st16(dp + n - 16, zv4u{(uint32_t)rp, (uint32_t)(rp >> 32), (uint32_t)rp, (uint32_t)(rp >> 32)});
-      }
+      const zv4u v = ld16(pp);  // bytes past the period are garbage, masked off
+      unsigned __int128 P = ((unsigned __int128)(((uint64_t)v[3] << 32) | v[2]) << 64) | (((uint64_t)v[1] << 32) | v[0]);
+      P &= (((unsigned __int128)1) << (8 * d)) - 1;
+      for (uint32_t len = d; len < 16; len *= 2) P |= P << (8 * len);
+      const uint64_t p0 = (uint64_t)P, p1 = (uint64_t)(P >> 64);
+      const zv4u pv = zv4u{(uint32_t)p0, (uint32_t)(p0 >> 32), (uint32_t)p1, (uint32_t)(p1 >> 32)};
+      const uint32_t L = d * (16 / d);
+      uint32_t t = 0;
+      if (n >= 16)
+        for (; t + 16 <= n; t += L) st16(dp + t, pv);
+      const uint32_t r = n - t;  // < 16, phase 0
+      uint32_t o = 0;
+      if (r & 8) { __builtin_memcpy(dp + t, &p0, 8); o = 8; }
+      const unsigned __int128 Q = P >> (8 * o);
+      const uint64_t q0 = (uint64_t)Q;
+      if (r & 4) { const uint32_t w = (uint32_t)q0; __builtin_memcpy(dp + t + o, &w, 4); }
+      const uint64_t q1 = (r & 4) ? q0 >> 32 : q0;
+      const uint32_t o2 = o + (r & 4);
+      if (r & 2) { const uint16_t w = (uint16_t)q1; __builtin_memcpy(dp + t + o2, &w, 2); }
+      const uint64_t q2 = (r & 2) ? q1 >> 16 : q1;
+      if (r & 1) dp[t + o2 + (r & 2)] = (uint8_t)q2;
     } else if (ready && fast) {
       if (n >= 16) {
         // groups of up to 8 pieces: all loads of a group, then its stores; a piece never starts
@@ -2252,13 +2269,10 @@ __device__ uint32_t x_resolve(ZXSmem &S, uint64_t ms, uint32_t d, uint32_t n, ui
     uint64_t sm = __ballot(ready && !fast);
 #ifdef ZG_PROFILE
     const uint64_t c1 = clock64();
-    (void)c0;
     if (prof) {
-      const bool sl = ready && !fast;
-      prof[0] += __builtin_popcountll(__ballot(sl && n > 128));
-      prof[1] += __builtin_popcountll(__ballot(sl && d < n));
-      prof[2] += __builtin_popcountll(__ballot(sl && d < 16));
-      prof[3] += __builtin_popcountll(__ballot(sl && n <= 128 && d >= n));
+      prof[0] += c0 - cr;
+      prof[1] += c1 - c0;
+      prof[3] += 1;
     }
 #endif
     while (sm) {
@@ -2289,7 +2303,7 @@ __device__ uint32_t x_resolve(ZXSmem &S, uint64_t ms, uint32_t d, uint32_t n, ui
       __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
     }
 #ifdef ZG_PROFILE
-    (void)c1;
+    if (prof) prof[2] += clock64() - c1;
 #endif
     pending = pending && !ready;
     __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
@@ -2536,7 +2550,11 @@ __global__ __launch_bounds__(64) void k_zstd_exec_item(ZgItem *items, uint32_t *
         }
         __syncthreads();
         ZP_T(t3);
+#ifdef ZG_PROFILE
+        const uint32_t nr = x_resolve(S, mstart, r_of, sml, fe, sb, zp_acc + 8);
+#else
         const uint32_t nr = x_resolve(S, mstart, r_of, sml, fe, sb);
+#endif
         ZP_ADD(3, t3);
         (void)nr;
         O.pos = out_base + span;
