@@ -61,7 +61,7 @@ int main(int argc, char **argv) {
   }
   {  // resolution rounds of k_zstd_exec_item's batches: the frontier rule vs exact dependencies
     const uint32_t ZB = 4096, BIG = 2048;
-    uint64_t rf = 0, rp = 0, nbat = 0, pos = 0;
+    uint64_t rf = 0, rp = 0, nbat = 0, pos = 0, maxp = 0, maxs = 0, rsp = 0, hist[5] = {};
     size_t k = 0;
     while (k < ns) {
       // one batch: up to 64 sequences, output span <= ZB, stopping before a big one / block end
@@ -115,6 +115,14 @@ int main(int argc, char **argv) {
           for (int i = 0; i < j; i++) if (pe[i] && ms[i] < b && ms[i] + n[i] > a) ok = false;
           rdy[j] = ok;
         }
+        uint32_t mx = 0, ms_ = 0; bool sp = false;
+        for (int j = 0; j < m; j++) if (rdy[j]) {
+          const uint32_t d = (uint32_t)(ms[j] - src[j]);
+          if (d < n[j] && d < 16) { sp = true; ms_ = std::max(ms_, (n[j] + 15) / 16); }
+          else mx = std::max(mx, (n[j] + 15) / 16);
+        }
+        maxp += mx; maxs += ms_; rsp += sp;
+        hist[std::min<uint32_t>(mx, 32) / 8]++;
         for (int j = 0; j < m; j++) if (rdy[j]) pe[j] = false;
         rp++;
       }
@@ -131,6 +139,8 @@ int main(int argc, char **argv) {
              c[0], bsum[0], c[1], bsum[1], c[2], bsum[2], c[3], bsum[3], c[4], bsum[4]);
     }
     printf("  batches %lu, rounds: frontier rule %lu, exact dependencies %lu\n", nbat, rf, rp);
+    printf("  exact rounds: sum of max straight pieces %lu, sum of max period pieces %lu, rounds with a period copy %lu; max pieces <8 %lu, <16 %lu, <24 %lu, <32 %lu, 32 %lu\n",
+           maxp, maxs, rsp, hist[0], hist[1], hist[2], hist[3], hist[4]);
   }
   for (int S : {2, 4, 8, 16, 32, 128}) {
     const uint64_t seg = N / S;

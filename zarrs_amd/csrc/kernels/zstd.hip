@@ -1894,6 +1894,7 @@ namespace {
 // -------------------------------------------------------------------------------------------------
 constexpr uint32_t XRING = 65536, XRMASK = XRING - 1;
 constexpr uint32_t XSTAGE_V = 512;  // staged far-source vectors (16 B) per batch
+constexpr uint32_t XPL = 128;       // bytes of a short match its own lane copies (the rest: the wave)
 constexpr int XR_LIT = ZBATCH / 16 / 64 + 1, XR_FAR = XSTAGE_V / 64;
 
 struct XReady {
@@ -2198,6 +2199,8 @@ __device__ uint32_t x_resolve(ZXSmem &S, uint64_t ms, uint32_t d, uint32_t n, ui
 #ifdef ZG_PROFILE
     const uint64_t c0 = clock64();
 #endif
+    uint32_t L = 16, te = 0;
+    zv4u pat = zv4u{0, 0, 0, 0};
     if (ready && splat) {
       // period d < 16: P = the first 16 bytes of the periodic extension (the period doubled until
       // it fills 16 bytes). With L = d * floor(16 / d), byte j of every 16-byte store at a multiple
@@ -2210,10 +2213,17 @@ __device__ uint32_t x_resolve(ZXSmem &S, uint64_t ms, uint32_t d, uint32_t n, ui
       for (uint32_t len = d; len < 16; len *= 2) P |= P << (8 * len);
       const uint64_t p0 = (uint64_t)P, p1 = (uint64_t)(P >> 64);
       const zv4u pv = zv4u{(uint32_t)p0, (uint32_t)(p0 >> 32), (uint32_t)p1, (uint32_t)(p1 >> 32)};
-      const uint32_t L = d * (16 / d);
-      uint32_t t = 0;
-      if (n >= 16)
-        for (; t + 16 <= n; t += L) st16(dp + t, pv);
+      L = d * (16 / d);
+      pat = pv;
+      // te: the first multiple of L with te + 16 > n; this lane stores below XPL, the wave the rest
+      if (n >= 16) {
+        uint32_t q = (uint32_t)((float)(n - 16) * __builtin_amdgcn_rcpf((float)L));
+        if ((q + 1) * L + 16 <= n) q++;
+        if (q * L + 16 > n) q--;
+        te = (q + 1) * L;
+      }
+      for (uint32_t u = 0; u < min(te, XPL); u += L) st16(dp + u, pv);
+      const uint32_t t = te;
       const uint32_t r = n - t;  // < 16, phase 0
       uint32_t o = 0;
       if (r & 8) { __builtin_memcpy(dp + t, &p0, 8); o = 8; }
@@ -2230,7 +2240,8 @@ __device__ uint32_t x_resolve(ZXSmem &S, uint64_t ms, uint32_t d, uint32_t n, ui
         // groups of up to 8 pieces: all loads of a group, then its stores; a piece never starts
         // after n - 16 (the last one rewrites its neighbour's bytes with the same values)
         const uint32_t lim = n - 16;
-        for (uint32_t g0 = 0; g0 < n; g0 += 128) {
+        {  // bytes from XPL = 128 on: the whole wave, below
+          const uint32_t g0 = 0;
           const uint32_t np = min((n - g0 + 15) >> 4, 8u);
           zv4u v0, v1, v2, v3, v4, v5, v6, v7;
           v0 = ld16(sp + min(g0, lim));
@@ -2264,6 +2275,31 @@ __device__ uint32_t x_resolve(ZXSmem &S, uint64_t ms, uint32_t d, uint32_t n, ui
         __builtin_memcpy(dp + n - 4, &a1, 4);
       } else {
         for (uint32_t j = 0; j < n; j++) dp[j] = sp[j];
+      }
+    }
+    // long matches past their first XPL bytes: the whole wave, one match after another -- a straight
+    // copy as one 16-B piece per lane (the last one ending at the match end), a period as its
+    // pattern stored at the multiples of L from the first one >= XPL up to te
+    {
+      const uint8_t *lb = (const uint8_t *)&S;
+      const uint32_t so = (uint32_t)(sp - lb), dof = (uint32_t)(dp - lb);
+      uint64_t bm = __ballot(ready && ((splat && te > XPL) || (fast && !splat && n > XPL)));
+      while (bm) {
+        const int i = __builtin_ctzll(bm);
+        bm &= bm - 1;
+        const uint32_t n_i = U(__builtin_amdgcn_readlane(n, i)), do_i = U(__builtin_amdgcn_readlane(dof, i));
+        const uint32_t te_i = U(__builtin_amdgcn_readlane(te, i));
+        if (te_i) {
+          const uint32_t L_i = U(__builtin_amdgcn_readlane(L, i));
+          const zv4u pv_i = zv4u{U(__builtin_amdgcn_readlane(pat[0], i)), U(__builtin_amdgcn_readlane(pat[1], i)),
+                                 U(__builtin_amdgcn_readlane(pat[2], i)), U(__builtin_amdgcn_readlane(pat[3], i))};
+          const uint32_t t = ((XPL + L_i - 1) / L_i + lane) * L_i;
+          if (t < te_i) st16((uint8_t *)lb + do_i + t, pv_i);
+        } else {
+          const uint32_t so_i = U(__builtin_amdgcn_readlane(so, i));
+          const uint32_t k = min(XPL + 16 * lane, n_i - 16);
+          if (XPL + 16 * lane < n_i) st16((uint8_t *)lb + do_i + k, ld16(lb + so_i + k));
+        }
       }
     }
     uint64_t sm = __ballot(ready && !fast);
