@@ -116,8 +116,8 @@ int main(int argc, char **argv) {
   CK(hipMalloc(&Z.mode, n * 4));
   CK(hipMalloc(&Z.lit, n * Z.lit_stride));
   CK(hipMalloc(&Z.seq, n * Z.seq_cap * 12));
-  constexpr int NK = 6;
-  const char *kn[NK] = {"scan", "lits", "blocks", "plan", "exec_item", "serial"};
+  constexpr int NK = 7;
+  const char *kn[NK] = {"scan", "lits", "blocks", "plan", "direct", "exec_item", "serial"};
   hipEvent_t ev[NK + 1];
   for (auto &evk : ev) CK(hipEventCreate(&evk));
   float best[NK];
@@ -131,6 +131,7 @@ int main(int argc, char **argv) {
   for (int rep = 0; rep < 3; rep++) {
     CK(hipMemcpy(d_items, items.data(), n * sizeof(ZgItem), hipMemcpyHostToDevice));
     CK(hipMemset(d_status, 0, n * 4));
+    CK(hipMemset(d_out, 0xA5, (size_t)n * chunk));
     zgpu::ZBlk *blks = (zgpu::ZBlk *)Z.blks;
     const uint32_t grid = (uint32_t)std::min<uint64_t>((uint64_t)n * Z.blk_cap, 256 * 16);
     CK(hipEventRecord(ev[0]));
@@ -147,13 +148,16 @@ int main(int argc, char **argv) {
     hipLaunchKernelGGL(zgpu::k_zstd_plan, dim3(n), dim3(64), 0, 0, d_items, d_status, blks, Z.blk_cap, Z.nblk, Z.mode,
                        chunk);
     CK(hipEventRecord(ev[4]));
+    hipLaunchKernelGGL(zgpu::k_zstd_direct, dim3(grid), dim3(256), 0, 0, d_items, d_status, blks, Z.blk_cap, Z.nblk,
+                       Z.mode, (uint32_t)n, d_out, chunk, Z.lit, Z.lit_stride);
+    CK(hipEventRecord(ev[5]));
     hipLaunchKernelGGL(zgpu::k_zstd_exec_item, dim3(n), dim3(64), 0, 0, d_items, d_status, blks, Z.blk_cap, Z.nblk,
                        Z.mode, d_out, chunk, Z.lit, Z.lit_stride, Z.seq, Z.seq_cap);
-    CK(hipEventRecord(ev[5]));
+    CK(hipEventRecord(ev[6]));
     hipLaunchKernelGGL(zgpu::k_zstd, dim3(n), dim3(64), 0, 0, d_items, d_status, d_out, chunk, Z.lit, Z.lit_stride,
                        Z.mode);
-    CK(hipEventRecord(ev[6]));
-    CK(hipEventSynchronize(ev[6]));
+    CK(hipEventRecord(ev[7]));
+    CK(hipEventSynchronize(ev[7]));
     for (int k = 0; k < NK; k++) {
       float ms;
       CK(hipEventElapsedTime(&ms, ev[k], ev[k + 1]));

@@ -1894,7 +1894,7 @@ namespace {
 // -------------------------------------------------------------------------------------------------
 constexpr uint32_t XRING = 65536, XRMASK = XRING - 1;
 constexpr uint32_t XSTAGE_V = 512;  // staged far-source vectors (16 B) per batch
-constexpr uint32_t XPL = 128;       // bytes of a short match its own lane copies (the rest: the wave)
+constexpr uint32_t XPL = 32;        // bytes of a short match its own lane copies (the rest: the wave)
 constexpr int XR_LIT = ZBATCH / 16 / 64 + 1, XR_FAR = XSTAGE_V / 64;
 
 struct XReady {
@@ -1916,6 +1916,7 @@ struct ZXSmem {
 struct XOut {
   uint8_t *out;
   uint64_t pos, flushed;
+  uint64_t rv;  // the ring holds no output below rv (a block written by k_zstd_direct precedes it)
 };
 
 __device__ __forceinline__ uint64_t rl64(uint64_t v, int i) {
@@ -1943,7 +1944,7 @@ __device__ __forceinline__ void x_reserve(ZXSmem &S, XOut &O, uint64_t wend) {
 // hold a byte written after the line was loaded). Sources at or above it are still in the ring and
 // are not overwritten by a batch ending at wend (<= ZBATCH past the current position).
 __device__ __forceinline__ uint64_t x_far_bound(const XOut &O, uint64_t wend) {
-  const uint64_t lim = wend + ZBATCH > XRING ? wend + ZBATCH - XRING : 0;
+  const uint64_t lim = max<uint64_t>(wend + ZBATCH > XRING ? wend + ZBATCH - XRING : 0, O.rv);  // rv: 128-B aligned
   return min<uint64_t>(lim, O.flushed) & ~(uint64_t)127;
 }
 // n bytes of global memory into the ring at the output position, 16 KiB pieces (every load of a
@@ -2242,7 +2243,7 @@ __device__ uint32_t x_resolve(ZXSmem &S, uint64_t ms, uint32_t d, uint32_t n, ui
         const uint32_t lim = n - 16;
         {  // bytes from XPL = 128 on: the whole wave, below
           const uint32_t g0 = 0;
-          const uint32_t np = min((n - g0 + 15) >> 4, 8u);
+          const uint32_t np = min((n - g0 + 15) >> 4, XPL / 16);
           zv4u v0, v1, v2, v3, v4, v5, v6, v7;
           v0 = ld16(sp + min(g0, lim));
           if (np > 1) v1 = ld16(sp + min(g0 + 16, lim));
@@ -2439,6 +2440,73 @@ __device__ __forceinline__ bool x_long_match(ZXSmem &S, XOut &O, uint64_t fstart
 
 }  // namespace
 
+// Blocks whose output is their literals alone (raw, rle, or compressed without sequences) depend on
+// nothing before them: k_zstd_direct writes them into the slot with the whole GPU ahead of the
+// per-item execution, which only flushes up to them and steps over (at least XDIRECT bytes: a
+// shorter block costs the executor less than the restart of its ring).
+constexpr uint32_t XDIRECT = 4096;
+__device__ __forceinline__ bool x_direct_block(uint32_t flags, uint32_t nseq, uint32_t out_size) {
+  const uint32_t type = flags & 3;
+  return out_size >= XDIRECT && (type == ZB_RAW || type == ZB_RLE || (type == ZB_CMP && nseq == 0));
+}
+
+__global__ __launch_bounds__(256) void k_zstd_direct(const ZgItem *items, const uint32_t *status, const ZBlk *blks,
+                                                    uint32_t blk_cap, const uint32_t *nblk, const uint32_t *zmode,
+                                                    uint32_t n_items, uint8_t *dst, uint64_t slot_bytes,
+                                                    const uint8_t *lit_scratch, uint64_t lit_stride) {
+  const uint64_t recs = (uint64_t)n_items * blk_cap;
+  const uint32_t tid = threadIdx.x;
+  for (uint64_t rec = blockIdx.x; rec < recs; rec += gridDim.x) {
+    const uint32_t item = (uint32_t)(rec / blk_cap), bi = (uint32_t)(rec % blk_cap);
+    if (zmode[item] != ZMODE_PARALLEL || status[item] || bi >= nblk[item]) continue;
+    const ZBlk &b = blks[rec];
+    const uint32_t flags = b.flags, type = flags & 3, n = b.out_size;
+    if (!x_direct_block(flags, b.nseq, n)) continue;
+    if (type == ZB_CMP && b.regen != n) continue;  // corrupt: k_zstd_exec_item reports it
+    const uint8_t *in = (const uint8_t *)items[item].src;
+    uint8_t *o = dst + (uint64_t)item * slot_bytes + b.out_off;
+    if (type == ZB_RLE) {
+      const uint8_t v = in[b.in_off];
+      const uint32_t w = v * 0x01010101u;
+      const uint32_t head = min<uint32_t>(n, (16 - ((uintptr_t)o & 15)) & 15);
+      if (tid < head) o[tid] = v;
+      const uint32_t nv = (n - head) / 16;
+      for (uint32_t k = tid; k < nv; k += 256) *(zv4u *)(o + head + 16 * k) = zv4u{w, w, w, w};
+      for (uint32_t k = head + 16 * nv + tid; k < n; k += 256) o[k] = v;
+      continue;
+    }
+    const uint8_t *src = type == ZB_RAW ? in + b.in_off
+                         : ((flags >> 2) & 3) == 0 ? in + b.lit_off
+                                                   : lit_scratch + (uint64_t)item * lit_stride + b.lit_buf;
+    // destination-aligned 16-B vectors, each from two aligned source vectors and byte-aligns
+    const uint32_t head = min<uint32_t>(n, (16 - ((uintptr_t)o & 15)) & 15);
+    if (tid < head) o[tid] = src[tid];
+    const uint32_t nv = (n - head) / 16;
+    const uintptr_t s0 = (uintptr_t)(src + head);
+    const uint32_t m = (uint32_t)(s0 & 15);
+    const zv4u *sv = (const zv4u *)(s0 & ~(uintptr_t)15);
+    for (uint32_t k = tid; k < nv; k += 256) {
+      const zv4u lo = __builtin_nontemporal_load(sv + k);
+      zv4u r = lo;
+      if (m) {
+        const zv4u hi = __builtin_nontemporal_load(sv + k + 1);
+        const uint32_t sh = m & 3;  // bytes
+        const uint32_t q = m >> 2;
+        const uint32_t w0 = lo[0], w1 = lo[1], w2 = lo[2], w3 = lo[3], w4 = hi[0], w5 = hi[1], w6 = hi[2];
+        const uint32_t c0 = q == 0 ? w0 : q == 1 ? w1 : q == 2 ? w2 : w3;
+        const uint32_t c1 = q == 0 ? w1 : q == 1 ? w2 : q == 2 ? w3 : w4;
+        const uint32_t c2 = q == 0 ? w2 : q == 1 ? w3 : q == 2 ? w4 : w5;
+        const uint32_t c3 = q == 0 ? w3 : q == 1 ? w4 : q == 2 ? w5 : w6;
+        const uint32_t c4 = q == 0 ? w4 : q == 1 ? w5 : q == 2 ? w6 : hi[3];
+        r = zv4u{__builtin_amdgcn_alignbyte(c1, c0, sh), __builtin_amdgcn_alignbyte(c2, c1, sh),
+                 __builtin_amdgcn_alignbyte(c3, c2, sh), __builtin_amdgcn_alignbyte(c4, c3, sh)};
+      }
+      __builtin_nontemporal_store(r, (zv4u *)(o + head) + k);
+    }
+    for (uint32_t k = head + 16 * nv + tid; k < n; k += 256) o[k] = src[k];
+  }
+}
+
 __global__ __launch_bounds__(64) void k_zstd_exec_item(ZgItem *items, uint32_t *status, const ZBlk *blks,
                                                        uint32_t blk_cap, const uint32_t *nblk, const uint32_t *zmode,
                                                        uint8_t *dst, uint64_t slot_bytes, const uint8_t *lit_scratch,
@@ -2455,7 +2523,7 @@ __global__ __launch_bounds__(64) void k_zstd_exec_item(ZgItem *items, uint32_t *
   uint8_t *out = dst + (uint64_t)item * slot_bytes;
   const ZBlk *B = blks + (uint64_t)item * blk_cap;
   const uint32_t nb = nblk[item];
-  XOut O{out, 0, 0};
+  XOut O{out, 0, 0, 0};
   uint32_t err = 0;
   uint64_t fstart = 0;
   for (uint32_t bi = 0; bi < nb && !err; bi++) {
@@ -2466,7 +2534,18 @@ __global__ __launch_bounds__(64) void k_zstd_exec_item(ZgItem *items, uint32_t *
     if (bstart != O.pos) { err = ZG_CORRUPT_STREAM; break; }
     const uint64_t bend = bstart + bsize;
     ZP_T(t5);
-    if (type == ZB_RAW) {
+    if (x_direct_block(flags, U(B[bi].nseq), bsize)) {
+      // written by k_zstd_direct: everything before it to the slot, then the ring restarts at the
+      // block's last 128-B line boundary (sources below it are staged from the slot)
+      if (type == ZB_CMP && U(B[bi].regen) != bsize) { err = ZG_CORRUPT_STREAM; break; }
+      x_flush(S, O);
+      const uint64_t a = bend & ~(uint64_t)127;
+      for (uint64_t p = a + lane; p < bend; p += 64) S.ring[p & XRMASK] = out[p];
+      O.pos = O.flushed = bend;
+      O.rv = a;
+      __syncthreads();
+      ZP_ADD(5, t5);
+    } else if (type == ZB_RAW) {
       x_copy(S, O, in + U(B[bi].in_off), bsize);
       ZP_ADD(5, t5);
     } else if (type == ZB_RLE) {
@@ -2649,6 +2728,8 @@ hipError_t launch_zstd(ZgItem *items, uint32_t *status, uint32_t n_items, uint8_
                      n_items, Z.lit, Z.lit_stride, Z.seq, Z.seq_cap);
   hipLaunchKernelGGL(k_zstd_plan, dim3(n_items), dim3(64), 0, s, items, status, blks, Z.blk_cap, Z.nblk, Z.mode,
                      slot_bytes);
+  hipLaunchKernelGGL(k_zstd_direct, dim3(grid), dim3(256), 0, s, items, status, blks, Z.blk_cap, Z.nblk, Z.mode,
+                     n_items, dst, slot_bytes, Z.lit, Z.lit_stride);
   hipLaunchKernelGGL(k_zstd_exec_item, dim3(n_items), dim3(64), 0, s, items, status, blks, Z.blk_cap, Z.nblk, Z.mode,
                      dst, slot_bytes, Z.lit, Z.lit_stride, Z.seq, Z.seq_cap);
   hipLaunchKernelGGL(k_zstd, dim3(n_items), dim3(64), 0, s, items, status, dst, slot_bytes, Z.lit, Z.lit_stride,
