@@ -42,6 +42,13 @@ def _content(rng, n, kind):
             out.append(rng.integers(0, 256, int(rng.integers(0, 40)), dtype=np.uint8))
             size += ln + len(out[-1])
         return np.concatenate(out)[:n].copy()
+    if kind == "direct":  # raw, rle and literal-only blocks, then matches reaching back into them
+        r = rng.integers(0, 256, 150000, dtype=np.uint8)
+        sk = np.minimum(rng.geometric(0.3, 150000), 255).astype(np.uint8)  # skewed: Huffman literals
+        parts = [r, r[-5000:], r[60000:61000], np.zeros(300000, np.uint8), sk, sk[-3000:], r[:2000],
+                 sk[1000:1500], r[140000:149000]]
+        out = np.concatenate(parts)
+        return np.tile(out, n // len(out) + 1)[:n].copy()
     raise ValueError(kind)
 
 
@@ -156,7 +163,7 @@ def test_zstd_multiblock_frames(level):
     codecs = [BYTES_LE, {"name": "zstd", "configuration": {"level": level, "checksum": level != 1}}]
     oc = O.OracleChain.from_metadata(codecs, "uint8", 0, 1)
     n = 3 << 20
-    kinds = ["random", "text", "smooth", "runs", "far", "vfar", "periods"]
+    kinds = ["random", "text", "smooth", "runs", "far", "vfar", "periods", "direct"]
     data = [_content(rng, n, k) for k in kinds]
     # C5-like: byte-shuffled u16 blobs + noise
     z = np.arange(n // 2, dtype=np.float32)
