@@ -36,7 +36,9 @@ int main(int argc, char **argv) {
   const uint64_t chunk = (argc > 2 ? atoll(argv[2]) : 16) << 20;  // bytes
   const int level = argc > 3 ? atoi(argv[3]) : 3;
   // argv[4] == "c5": chunks [32,512,512] of a bench-like C5 level 0 ([512,1024,1024], 64 blobs)
-  const bool c5 = argc > 4 && !strcmp(argv[4], "c5");
+  // argv[4] == "c5l1": chunks [64,256,256] of the 2x2x2 mean of that level (8 MiB each)
+  const bool l1 = argc > 4 && !strcmp(argv[4], "c5l1");
+  const bool c5 = l1 || (argc > 4 && !strcmp(argv[4], "c5"));
   std::vector<uint16_t> lvl;
   if (c5) {
     std::mt19937_64 g(42);
@@ -53,14 +55,23 @@ int main(int argc, char **argv) {
 #pragma omp parallel for
   for (int c = 0; c < n; c++) {
     if (c5) {
-      const int z0 = (c / 4) * 32, y0 = ((c / 2) % 2) * 512, x0 = (c % 2) * 512;
-      const uint64_t cnt = (uint64_t)32 * 512 * 512;
+      const int ncz = l1 ? 64 : 32, ncy = l1 ? 256 : 512;
+      const int z0 = (c / 4) * ncz, y0 = ((c / 2) % 2) * ncy, x0 = (c % 2) * ncy;
+      const uint64_t cnt = (uint64_t)ncz * ncy * ncy;
       dec[c].resize(2 * cnt);
       uint64_t i = 0;
-      for (int z = 0; z < 32; z++)
-        for (int y = 0; y < 512; y++)
-          for (int x = 0; x < 512; x++, i++) {
-            const uint16_t v = lvl[((uint64_t)(z0 + z) * 1024 + (y0 + y)) * 1024 + (x0 + x)];
+      for (int z = 0; z < ncz; z++)
+        for (int y = 0; y < ncy; y++)
+          for (int x = 0; x < ncy; x++, i++) {
+            uint32_t v = 0;
+            if (!l1) {
+              v = lvl[((uint64_t)(z0 + z) * 1024 + (y0 + y)) * 1024 + (x0 + x)];
+            } else {
+              for (int k = 0; k < 8; k++)
+                v += lvl[((uint64_t)(2 * (z0 + z) + (k >> 2)) * 1024 + (2 * (y0 + y) + ((k >> 1) & 1))) * 1024 +
+                         (2 * (x0 + x) + (k & 1))];
+              v /= 8;
+            }
             dec[c][i] = (uint8_t)v;
             dec[c][cnt + i] = (uint8_t)(v >> 8);
           }
@@ -124,7 +135,7 @@ int main(int argc, char **argv) {
   for (auto &bk : best) bk = 1e30f;
 #ifdef ZG_PROFILE
   {
-    unsigned long long z[12] = {0};
+    unsigned long long z[13] = {0};
     CK(hipMemcpyToSymbol(HIP_SYMBOL(zgpu::g_zprof), z, sizeof(z)));
   }
 #endif
@@ -151,7 +162,7 @@ int main(int argc, char **argv) {
     hipLaunchKernelGGL(zgpu::k_zstd_direct, dim3(grid), dim3(256), 0, 0, d_items, d_status, blks, Z.blk_cap, Z.nblk,
                        Z.mode, (uint32_t)n, d_out, chunk, Z.lit, Z.lit_stride);
     CK(hipEventRecord(ev[5]));
-    hipLaunchKernelGGL(zgpu::k_zstd_exec_item, dim3(n), dim3(64), 0, 0, d_items, d_status, blks, Z.blk_cap, Z.nblk,
+    hipLaunchKernelGGL(zgpu::k_zstd_exec_item, dim3(n * zgpu::XSEG), dim3(64), 0, 0, d_items, d_status, blks, Z.blk_cap, Z.nblk,
                        Z.mode, d_out, chunk, Z.lit, Z.lit_stride, Z.seq, Z.seq_cap);
     CK(hipEventRecord(ev[6]));
     hipLaunchKernelGGL(zgpu::k_zstd, dim3(n), dim3(64), 0, 0, d_items, d_status, d_out, chunk, Z.lit, Z.lit_stride,
@@ -182,7 +193,7 @@ int main(int argc, char **argv) {
   for (int k = 0; k < NK; k++) printf("  %-12s %8.3f ms\n", kn[k], best[k]);
 #ifdef ZG_PROFILE
   {
-    unsigned long long z[12];
+    unsigned long long z[13];
     CK(hipMemcpyFromSymbol(z, HIP_SYMBOL(zgpu::g_zprof), sizeof(z)));
     const double nb = z[4] ? (double)z[4] : 1.0;
     const double nbt = z[6] ? (double)z[6] : 1.0;
@@ -193,6 +204,7 @@ int main(int argc, char **argv) {
     printf("single matches with d < 16 per frame: %.0f\n", (double)(z[7] >> 32) / per);
     printf("resolve per frame (Mticks): ready %.2f fast copies %.2f slow copies %.2f | rounds %.0f\n", z[8] / per / 1e6,
            z[9] / per / 1e6, z[10] / per / 1e6, (double)z[11] / per);
+    printf("batches with far sources per frame: %.0f\n", z[12] / per);
   }
 #endif
   printf("total %.3f ms -> %.2f GB/s decoded\n", tot, (double)n * chunk / tot / 1e6);

@@ -28,14 +28,26 @@ int main(int argc, char **argv) {
   }
   std::vector<uint16_t> lvl((size_t)512 * 1024 * 1024);
   synth_c5_level0(512, 1024, 1024, 64, cz, cy, cx, sg, amp, 42, lvl.data(), 8);
-  const int c = chunk, z0 = (c / 4) * 32, y0 = ((c / 2) % 2) * 512, x0 = (c % 2) * 512;
-  const uint64_t cnt = (uint64_t)32 * 512 * 512, N = 2 * cnt;
+  const int level = argc > 2 ? atoi(argv[2]) : 0;  // 1: a chunk [64,256,256] of the 2x2x2 mean level
+  const int c = chunk;
+  const int ncz = level ? 64 : 32, ncy = level ? 256 : 512;
+  const int z0 = (c / 4) * ncz, y0 = ((c / 2) % 2) * ncy, x0 = (c % 2) * ncy;
+  const uint64_t cnt = (uint64_t)ncz * ncy * ncy, N = 2 * cnt;
   std::vector<uint8_t> d(N);
   uint64_t i = 0;
-  for (int z = 0; z < 32; z++)
-    for (int y = 0; y < 512; y++)
-      for (int x = 0; x < 512; x++, i++) {
-        const uint16_t v = lvl[((uint64_t)(z0 + z) * 1024 + (y0 + y)) * 1024 + (x0 + x)];
+  for (int z = 0; z < ncz; z++)
+    for (int y = 0; y < ncy; y++)
+      for (int x = 0; x < ncy; x++, i++) {
+        uint32_t v;
+        if (!level) {
+          v = lvl[((uint64_t)(z0 + z) * 1024 + (y0 + y)) * 1024 + (x0 + x)];
+        } else {
+          uint32_t sum = 0;
+          for (int k = 0; k < 8; k++)
+            sum += lvl[((uint64_t)(2 * (z0 + z) + (k >> 2)) * 1024 + (2 * (y0 + y) + ((k >> 1) & 1))) * 1024 +
+                       (2 * (x0 + x) + (k & 1))];
+          v = sum / 8;
+        }
         d[i] = (uint8_t)v; d[cnt + i] = (uint8_t)(v >> 8);
       }
   ZSTD_CCtx *cc = ZSTD_createCCtx();
@@ -45,6 +57,16 @@ int main(int argc, char **argv) {
   if (ZSTD_isError(ns)) { printf("generateSequences failed\n"); return 1; }
   uint64_t nm = 0, mb = 0, lb = 0;
   for (size_t k = 0; k < ns; k++) { lb += s[k].litLength; if (s[k].matchLength) { nm++; mb += s[k].matchLength; } }
+  {
+    uint64_t p = 0, lo_seq = 0, cross = 0;
+    for (size_t k = 0; k < ns; k++) {
+      p += s[k].litLength;
+      if (p < N / 2) lo_seq++;
+      if (s[k].matchLength && p >= N / 2 && p - s[k].offset < N / 2) cross++;
+      p += s[k].matchLength;
+    }
+    printf("sequences starting in the low plane %lu of %zu; matches crossing into it from the high plane %lu\n", lo_seq, ns, cross);
+  }
   printf("chunk %d: %zu sequences, %lu matches, match bytes %lu, literal bytes %lu (total %lu)\n", c, ns, nm, mb, lb, N);
   {  // offset / length histogram of the matches
     const uint64_t lim[] = {1, 2, 4, 8, 16, 64, 256, 511, 512, 513, 1024, 4096, 65536, 262144, 1ull << 40};

@@ -26,11 +26,11 @@ namespace zgpu {
 
 #ifdef ZG_PROFILE
 // lab builds only (tools/lab/zstd_lab.cpp): k_zstd_exec per-phase shader-clock totals
-__device__ unsigned long long g_zprof[12];
-#define ZP_DECL uint64_t zp_acc[12] = {0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0}
+__device__ unsigned long long g_zprof[13];
+#define ZP_DECL uint64_t zp_acc[13] = {0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0}
 #define ZP_T(v) const uint64_t v = clock64()
 #define ZP_ADD(slot, t0) zp_acc[slot] += clock64() - (t0)
-#define ZP_FLUSH do { if (__lane_id() == 0) for (int k_ = 0; k_ < 12; k_++) atomicAdd(&g_zprof[k_], (unsigned long long)zp_acc[k_]); } while (0)
+#define ZP_FLUSH do { if (__lane_id() == 0) for (int k_ = 0; k_ < 13; k_++) atomicAdd(&g_zprof[k_], (unsigned long long)zp_acc[k_]); } while (0)
 #else
 #define ZP_DECL
 #define ZP_T(v)
@@ -1146,6 +1146,11 @@ struct ZBlk {
   uint32_t rep_in[3];         // incoming rep offsets (concrete, from k_zstd_plan)
   uint32_t out_off;           // item-relative output offset (k_zstd_plan)
   uint32_t frame_off;         // output offset of the block's frame
+  // how far the block's matches reach back from its start (k_zstd_blocks): max(offset - position)
+  // over concrete offsets, min(minus + position) per rep slot over symbolic ones
+  int32_t reach_c;
+  uint32_t reach_m[3];
+  uint32_t seg;               // 1: an executor segment starts at this block (k_zstd_plan)
 };
 
 struct ZScanSmem {
@@ -1417,6 +1422,8 @@ __global__ __launch_bounds__(64) void k_zstd_blocks(const ZgItem *items, uint32_
     const uint32_t nseq = U(Bp->nseq);
     uint64_t sum_ll = 0, sum_ml = 0;
     uint32_t r0 = ZSYM | (0u << 24), r1 = ZSYM | (1u << 24), r2 = ZSYM | (2u << 24);
+    int32_t reach_c = INT32_MIN;
+    uint32_t reach_m0 = ~0u, reach_m1 = ~0u, reach_m2 = ~0u;
     if (!bad && nseq) {
       const uint32_t tm = U(Bp->tab_mode);
       uint32_t lg[3] = {0, 0, 0};
@@ -1539,6 +1546,38 @@ __global__ __launch_bounds__(64) void k_zstd_blocks(const ZgItem *items, uint32_
             cnt++;
           }
           if (bad) break;
+          {  // the batch's reach back from the block start (exact, per match)
+            const uint64_t bpos = sum_ll + sum_ml;  // block position after the batch
+            uint32_t inc = lane < (int)cnt ? r_ll + r_ml : 0u;
+            for (int o = 1; o < 64; o <<= 1) {
+              const uint32_t t = __shfl_up(inc, o, 64);
+              if (lane >= o) inc += t;
+            }
+            const uint32_t tot = __shfl(inc, 63, 64);
+            const int32_t p = (int32_t)(bpos - tot + inc - r_ml);  // this lane's match start
+            int32_t rc = INT32_MIN;
+            uint32_t m0 = ~0u, m1 = ~0u, m2 = ~0u;
+            if (lane < (int)cnt && r_ml) {
+              if (!(r_of & ZSYM)) {
+                rc = (int32_t)r_of - p;
+              } else {
+                const uint32_t slot = (r_of >> 24) & 3, mv = (r_of & 0xFFFFFF) + (uint32_t)p;
+                if (slot == 0) m0 = mv;
+                else if (slot == 1) m1 = mv;
+                else m2 = mv;
+              }
+            }
+            for (int o = 32; o; o >>= 1) {
+              rc = max(rc, __shfl_xor(rc, o, 64));
+              m0 = min(m0, __shfl_xor(m0, o, 64));
+              m1 = min(m1, __shfl_xor(m1, o, 64));
+              m2 = min(m2, __shfl_xor(m2, o, 64));
+            }
+            reach_c = max(reach_c, rc);
+            reach_m0 = min(reach_m0, m0);
+            reach_m1 = min(reach_m1, m1);
+            reach_m2 = min(reach_m2, m2);
+          }
           if (lane < (int)cnt) {
             uint32_t *o = out + (uint64_t)(done + lane) * 3;
             o[0] = r_ll;
@@ -1558,6 +1597,10 @@ __global__ __launch_bounds__(64) void k_zstd_blocks(const ZgItem *items, uint32_
         status[item] = ZG_CORRUPT_STREAM;
       } else {
         Bp->out_size = (uint32_t)(regen + sum_ml);
+        Bp->reach_c = reach_c;
+        Bp->reach_m[0] = reach_m0;
+        Bp->reach_m[1] = reach_m1;
+        Bp->reach_m[2] = reach_m2;
         Bp->rep_out[0] = r0;
         Bp->rep_out[1] = r1;
         Bp->rep_out[2] = r2;
@@ -1829,6 +1872,21 @@ __global__ __launch_bounds__(LIT_THREADS) void k_zstd_lits(const ZgItem *items, 
 }
 
 // One wave per item: output offsets, incoming rep offsets, frame size checks.
+// Blocks whose output is their literals alone (raw, rle, or compressed without sequences) depend on
+// nothing before them: k_zstd_direct writes them into the slot with the whole GPU ahead of the
+// per-item execution, which only flushes up to them and steps over (at least XDIRECT bytes: a
+// shorter block costs the executor less than the restart of its ring).
+constexpr uint32_t XDIRECT = 4096;
+__device__ __forceinline__ bool x_direct_block(uint32_t flags, uint32_t nseq, uint32_t out_size) {
+  const uint32_t type = flags & 3;
+  return out_size >= XDIRECT && (type == ZB_RAW || type == ZB_RLE || (type == ZB_CMP && nseq == 0));
+}
+
+// Executor segments: an item's blocks are cut where no later match reaches back before the cut (and
+// not inside a checksummed frame); each segment gets its own k_zstd_exec_item wave. Byte-shuffled
+// images cut at their byte planes (tools/lab/zstd_taint.cpp: no match crosses the plane boundary).
+constexpr uint32_t XSEG = 4;
+
 __global__ __launch_bounds__(64) void k_zstd_plan(const ZgItem *items, uint32_t *status, ZBlk *blks,
                                                   uint32_t blk_cap, const uint32_t *nblk, const uint32_t *zmode,
                                                   uint64_t slot_bytes) {
@@ -1877,6 +1935,46 @@ __global__ __launch_bounds__(64) void k_zstd_plan(const ZgItem *items, uint32_t 
       }
     }
   }
+  if (!err) {
+    // valid cuts (backward: the least source position of the matches from the block on), then up to
+    // XSEG - 1 of them chosen forward at equal shares of the estimated execution cost
+    uint64_t smin = ~0ull, total_w = 0, vmask = 0;  // vmask: lane l holds the cuts at blocks 64 l ..
+    bool ck = false;
+    const bool cuts = nb <= 64 * 64;
+    for (uint32_t bi = nb; cuts && bi-- > 0;) {
+      const uint32_t flags = U(B[bi].flags), type = flags & 3, nsq = U(B[bi].nseq), osz = U(B[bi].out_size);
+      if (flags & ZBF_LAST) ck = flags & ZBF_CK;
+      const uint64_t off = U(B[bi].out_off);
+      if (type == ZB_CMP && nsq) {
+        int64_t reach = (int32_t)U((uint32_t)B[bi].reach_c);
+        for (int k = 0; k < 3; k++) {
+          const uint32_t m = U(B[bi].reach_m[k]);
+          if (m != ~0u) reach = max<int64_t>(reach, (int64_t)U(B[bi].rep_in[k]) - (int64_t)m);
+        }
+        const int64_t ms = (int64_t)off - reach;
+        smin = min<uint64_t>(smin, ms < 0 ? 0ull : (uint64_t)ms);
+      }
+      const bool valid = bi > 0 && smin >= off && (!ck || (flags & ZBF_FIRST));
+      total_w += (type == ZB_CMP ? 8ull * nsq : 0ull) + (x_direct_block(flags, nsq, osz) ? 0u : osz / 16);
+      if (valid && lane == (int)(bi >> 6)) vmask |= 1ull << (bi & 63);
+    }
+    uint64_t acc = 0;
+    uint32_t k = 1;
+    for (uint32_t bi = 0; bi < nb; bi++) {
+      uint32_t seg = bi == 0;
+      if (cuts) {
+        const uint32_t flags = U(B[bi].flags), type = flags & 3, nsq = U(B[bi].nseq), osz = U(B[bi].out_size);
+        const uint64_t vm = (uint64_t)U(__builtin_amdgcn_readlane((uint32_t)vmask, (int)(bi >> 6))) |
+                            ((uint64_t)U(__builtin_amdgcn_readlane((uint32_t)(vmask >> 32), (int)(bi >> 6))) << 32);
+        if (((vm >> (bi & 63)) & 1) && k < XSEG && acc * XSEG >= total_w * k) {
+          seg = 1;
+          k++;
+        }
+        acc += (type == ZB_CMP ? 8ull * nsq : 0ull) + (x_direct_block(flags, nsq, osz) ? 0u : osz / 16);
+      }
+      if (lane == 0) B[bi].seg = seg;
+    }
+  }
   if (lane == 0 && err) status[item] = err;
 }
 
@@ -1905,7 +2003,7 @@ struct XReady {
 struct ZXSmem {
   uint8_t ring[XRING];
   zv4u stage[XSTAGE_V];
-  uint8_t lit_stage[ZBATCH + 16];
+  uint8_t lit_stage[ZBATCH + 32];  // the batch's literals at their 16-B phase in memory
   uint8_t vown[XSTAGE_V];  // staged far vector -> the lane (match) it belongs to
   uint32_t pfx_lit[64], pfx_out[64], pfx_nv[64], own_pv[64];
   uint64_t own_v0[64];
@@ -2061,16 +2159,9 @@ __device__ __forceinline__ bool x_stage(ZXSmem &S, const uint8_t *out, uint64_t 
     }
   }
 #pragma unroll
-  for (int r = 0; r < XR_LIT; r++) {
+  for (int r = 0; r < XR_LIT; r++) {  // aligned as in memory: literal k is lit_stage[lhead + k]
     const uint32_t idx = lane + 64 * r;
-    if (idx < lvec) {
-      const uint32_t w[4] = {lv[r].x, lv[r].y, lv[r].z, lv[r].w};
-#pragma unroll
-      for (int j = 0; j < 16; j++) {
-        const int32_t k = (int32_t)(16 * idx + j) - (int32_t)lhead;
-        if (k >= 0 && (uint32_t)k < n_lit) S.lit_stage[k] = (uint8_t)(w[j >> 2] >> (8 * (j & 3)));
-      }
-    }
+    if (idx < lvec) *(zv4u *)&S.lit_stage[16 * idx] = lv[r];
   }
 #pragma unroll
   for (int r = 0; r < XR_FAR; r++) {
@@ -2440,15 +2531,6 @@ __device__ __forceinline__ bool x_long_match(ZXSmem &S, XOut &O, uint64_t fstart
 
 }  // namespace
 
-// Blocks whose output is their literals alone (raw, rle, or compressed without sequences) depend on
-// nothing before them: k_zstd_direct writes them into the slot with the whole GPU ahead of the
-// per-item execution, which only flushes up to them and steps over (at least XDIRECT bytes: a
-// shorter block costs the executor less than the restart of its ring).
-constexpr uint32_t XDIRECT = 4096;
-__device__ __forceinline__ bool x_direct_block(uint32_t flags, uint32_t nseq, uint32_t out_size) {
-  const uint32_t type = flags & 3;
-  return out_size >= XDIRECT && (type == ZB_RAW || type == ZB_RLE || (type == ZB_CMP && nseq == 0));
-}
 
 __global__ __launch_bounds__(256) void k_zstd_direct(const ZgItem *items, const uint32_t *status, const ZBlk *blks,
                                                     uint32_t blk_cap, const uint32_t *nblk, const uint32_t *zmode,
@@ -2513,7 +2595,7 @@ __global__ __launch_bounds__(64) void k_zstd_exec_item(ZgItem *items, uint32_t *
                                                        uint64_t lit_stride, const uint32_t *seq_scratch,
                                                        uint64_t seq_cap) {
   __shared__ ZXSmem S;
-  const uint32_t item = blockIdx.x;
+  const uint32_t item = blockIdx.x / XSEG, sg = blockIdx.x % XSEG;
   const int lane = lane_id();
   ZP_DECL;
   ZP_T(t_all);
@@ -2523,10 +2605,24 @@ __global__ __launch_bounds__(64) void k_zstd_exec_item(ZgItem *items, uint32_t *
   uint8_t *out = dst + (uint64_t)item * slot_bytes;
   const ZBlk *B = blks + (uint64_t)item * blk_cap;
   const uint32_t nb = nblk[item];
-  XOut O{out, 0, 0, 0};
+  // this wave's segment: blocks [b0, b1) between the sg-th and the next segment start (k_zstd_plan)
+  uint32_t b0 = nb, b1 = nb, count = 0;
+  for (uint32_t base = 0; base < nb && count <= sg + 1; base += 64) {
+    uint64_t m = __ballot(base + lane < nb && B[base + lane].seg);
+    while (m && count <= sg + 1) {
+      const uint32_t i = __builtin_ctzll(m);
+      m &= m - 1;
+      if (count == sg) b0 = base + i;
+      else if (count == sg + 1) b1 = base + i;
+      count++;
+    }
+  }
+  if (b0 >= nb) return;  // fewer segments
+  const uint64_t p0 = U(B[b0].out_off);
+  XOut O{out, p0, p0, p0};
   uint32_t err = 0;
-  uint64_t fstart = 0;
-  for (uint32_t bi = 0; bi < nb && !err; bi++) {
+  uint64_t fstart = U(B[b0].frame_off);
+  for (uint32_t bi = b0; bi < b1 && !err; bi++) {
     const uint32_t flags = U(B[bi].flags), type = flags & 3;
     const uint64_t bstart = U(B[bi].out_off);
     const uint32_t bsize = U(B[bi].out_size);
@@ -2609,6 +2705,9 @@ __global__ __launch_bounds__(64) void k_zstd_exec_item(ZgItem *items, uint32_t *
           x_reserve(S, O, out_base + span);
           const uint64_t fb = x_far_bound(O, out_base + span);
           staged = x_stage(S, O.out, fb, mstart, r_of, sml, lsrc + litpos, lspan, fe, sb);
+#ifdef ZG_PROFILE
+          zp_acc[12] += __ballot(mine && sml && fe > mstart - r_of) != 0;
+#endif
           ZP_ADD(1, ts);
         }
 #ifdef ZG_PROFILE
@@ -2644,7 +2743,7 @@ __global__ __launch_bounds__(64) void k_zstd_exec_item(ZgItem *items, uint32_t *
         ZP_T(tl2);
         if (mine && r_ll) {
           const uint32_t ll = r_ll, o = (uint32_t)out_base + b - r_ml - ll;
-          const uint8_t *ls = S.lit_stage + (a - ll);
+          const uint8_t *ls = S.lit_stage + (((uintptr_t)(lsrc + litpos)) & 15) + (a - ll);
           if (ll >= 16 && (o & XRMASK) + ll <= XRING) {
             uint8_t *dq = &S.ring[o & XRMASK];
             for (uint32_t k0 = 0; k0 < ll; k0 += 64) {
@@ -2698,7 +2797,7 @@ __global__ __launch_bounds__(64) void k_zstd_exec_item(ZgItem *items, uint32_t *
   if (lane == 0) {
     if (err) {
       status[item] = err;
-    } else {
+    } else if (b1 == nb) {  // the last segment
       items[item].src = (uint64_t)out;
       items[item].len = O.pos;
     }
@@ -2730,7 +2829,7 @@ hipError_t launch_zstd(ZgItem *items, uint32_t *status, uint32_t n_items, uint8_
                      slot_bytes);
   hipLaunchKernelGGL(k_zstd_direct, dim3(grid), dim3(256), 0, s, items, status, blks, Z.blk_cap, Z.nblk, Z.mode,
                      n_items, dst, slot_bytes, Z.lit, Z.lit_stride);
-  hipLaunchKernelGGL(k_zstd_exec_item, dim3(n_items), dim3(64), 0, s, items, status, blks, Z.blk_cap, Z.nblk, Z.mode,
+  hipLaunchKernelGGL(k_zstd_exec_item, dim3(n_items * XSEG), dim3(64), 0, s, items, status, blks, Z.blk_cap, Z.nblk, Z.mode,
                      dst, slot_bytes, Z.lit, Z.lit_stride, Z.seq, Z.seq_cap);
   hipLaunchKernelGGL(k_zstd, dim3(n_items), dim3(64), 0, s, items, status, dst, slot_bytes, Z.lit, Z.lit_stride,
                      Z.mode);
