@@ -192,6 +192,46 @@ def test_error_first_status_per_descriptor(ctx, torch_cuda):
     assert ch2.decode_batch(descs, out2, [300], enc_device=False) == [0, 0, 0]
 
 
+def test_pipelined_host_to_host(ctx, torch_cuda):
+    """Pinned host chunks -> pinned host array covering it: the overlapped sub-batch path (H2D,
+    decode and D2H of axis-0 row ranges on three streams). Bit-exact vs the oracle; a corrupt chunk
+    in a middle sub-batch fails its descriptor only; a partial cover falls back to the serial path."""
+    import torch
+    from zarrs_amd import CodecChain, ZgpuError, make_desc
+    codecs = [{"name": "transpose", "configuration": {"order": [2, 1, 0]}},
+              {"name": "bytes", "configuration": {"endian": "big"}}, {"name": "crc32c"}]
+    cs, grid = [16, 32, 32], [16, 2, 2]
+    rng = np.random.default_rng(11)
+    a = rng.standard_normal([g * c for g, c in zip(grid, cs)]).astype(np.float32)
+    co = O.OracleChain.from_metadata(codecs, "float32", 0, 3)
+    chunks = _encode_grid(co, a, cs)
+    keys = sorted(chunks)
+    offs = np.cumsum([0] + [len(chunks[k]) for k in keys])
+    host = torch.from_numpy(np.frombuffer(b"".join(chunks[k] for k in keys), np.uint8).copy()).pin_memory()
+    base = host.data_ptr()
+    descs = [make_desc((base + int(offs[j]), len(chunks[k])), cs, out_start=[i * c for i, c in zip(k, cs)])
+             for j, k in enumerate(keys)]
+    ch = CodecChain.from_metadata(codecs, "float32", 0, ctx)
+    out = torch.zeros(a.shape, dtype=torch.float32).pin_memory()
+    assert ch.decode_batch(descs, out, list(a.shape), enc_device=False) == [0] * len(descs)
+    assert np.array_equal(out.numpy(), a)
+    # a flipped byte in the chunk at rows 128..143 (sub-batch 5 of 8)
+    bad = keys.index((8, 1, 0))
+    host[int(offs[bad]) + 7] ^= 1
+    out.zero_()
+    with pytest.raises(ZgpuError) as ei:
+        ch.decode_batch(descs, out, list(a.shape), enc_device=False)
+    assert ei.value.status == 1
+    got = out.numpy()
+    assert np.array_equal(got[:128], a[:128]) and np.array_equal(got[144:], a[144:])
+    host[int(offs[bad]) + 7] ^= 1
+    # partial cover (the last chunk row left out): serial path, uncovered bytes keep their values
+    part = [d for d, k in zip(descs, keys) if k[0] < 15]
+    out.fill_(7.0)
+    ch.decode_batch(part, out, list(a.shape), enc_device=False)
+    assert np.array_equal(out.numpy()[:240], a[:240]) and bool((out[240:] == 7.0).all())
+
+
 TILED = [  # (data type, transpose order, chunk shape, array shape): full 64-wide tiles, ragged slab groups
     ("float32", [2, 1, 0], [64, 6, 64], [128, 12, 192]),
     ("float64", [2, 1, 0], [64, 5, 64], [128, 10, 128]),

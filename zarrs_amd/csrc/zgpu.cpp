@@ -52,6 +52,7 @@ struct HipFail {
 struct zgpu_ctx {
   int device = 0;
   hipStream_t stream = nullptr;
+  hipStream_t copy[2] = {nullptr, nullptr};  // H2D / D2H streams of the pipelined host path (lazy)
   std::mutex mu;
   std::multimap<size_t, void *> free_dev;  // size -> ptr
   std::map<void *, size_t> live_dev;
@@ -113,6 +114,8 @@ struct zgpu_ctx {
     for (auto &kv : free_host) (void)hipHostFree(kv.second);
     for (auto &kv : live_host) (void)hipHostFree(kv.first);
     if (stream) (void)hipStreamDestroy(stream);
+    for (hipStream_t cs : copy)
+      if (cs) (void)hipStreamDestroy(cs);
   }
 };
 
@@ -424,15 +427,16 @@ static void plan_build(zgpu_plan &P, const zgpu_chunk_desc *descs) {
   P.scatter_units = P.items.empty() ? 0 : scatter_units_per_item(P.scatter_mode, S, max_sel);
 }
 
-static void plan_upload(zgpu_plan &P) {
+static void plan_upload(zgpu_plan &P, hipStream_t us = nullptr) {
   zgpu_ctx &C = *P.ctx;
+  if (!us) us = C.stream;
   const size_t ni = P.items.size();
   if (ni) {
     P.d_items = (ZgItem *)C.dev_alloc(ni * sizeof(ZgItem));
     P.d_items_init = (ZgItem *)C.dev_alloc(ni * sizeof(ZgItem));
     P.d_geom = (uint64_t *)C.dev_alloc(P.geom.size() * 8);
-    HIPCHK(hipMemcpyAsync(P.d_items_init, P.items.data(), ni * sizeof(ZgItem), hipMemcpyHostToDevice, C.stream));
-    HIPCHK(hipMemcpyAsync(P.d_geom, P.geom.data(), P.geom.size() * 8, hipMemcpyHostToDevice, C.stream));
+    HIPCHK(hipMemcpyAsync(P.d_items_init, P.items.data(), ni * sizeof(ZgItem), hipMemcpyHostToDevice, us));
+    HIPCHK(hipMemcpyAsync(P.d_geom, P.geom.data(), P.geom.size() * 8, hipMemcpyHostToDevice, us));
     for (int k = 0; k < P.n_pools; k++) P.d_pool[k] = (uint8_t *)C.dev_alloc(ni * P.slot_bytes);
     for (const Stage &s : P.stages) {
       if (s.kind == ST_GZIP && !P.d_aux) P.d_aux = (uint2 *)C.dev_alloc(ni * sizeof(uint2));
@@ -457,7 +461,7 @@ static void plan_upload(zgpu_plan &P) {
     P.d_index = (uint64_t *)C.dev_alloc(P.shards.size() * P.ispec.n_inner * 16);
     P.d_shard_status = (uint32_t *)C.dev_alloc(P.shards.size() * 4);
     HIPCHK(hipMemcpyAsync(P.d_shards, P.shards.data(), P.shards.size() * sizeof(ZgShard), hipMemcpyHostToDevice,
-                          C.stream));
+                          us));
   }
 }
 
@@ -651,6 +655,129 @@ void zgpu_plan_destroy(zgpu_plan *P) {
 
 uint64_t zgpu_plan_algorithmic_bytes(const zgpu_plan *P) { return P ? P->alg_bytes_static + P->last_enc_bytes : 0; }
 
+// Host input and host output, both pinned, descriptors covering the whole output: the batch is cut
+// into sub-batches of whole axis-0 row ranges (no descriptor straddles a cut), and sub-batch k's H2D
+// (copy stream 0), decode (s) and D2H of its rows (copy stream 1) overlap with its neighbours' --
+// PCIe is full duplex, so the host-to-host rate approaches the one-direction bound instead of half
+// of it. Returns false (nothing done) when the batch does not cut into at least two sub-batches.
+static bool decode_pipelined(zgpu_chain *ch, uint32_t nd, const zgpu_chunk_desc *descs, uint64_t n, uint8_t *out,
+                             const uint64_t *out_shape, uint32_t flags, int32_t *status, hipStream_t s, int &rc) {
+  constexpr uint64_t K = 16;  // target sub-batches
+  zgpu_ctx *C = ch->ctx;
+  uint64_t row_bytes = ch->chain->es;
+  for (uint32_t d = 1; d < nd; d++) row_bytes *= out_shape[d];
+  std::vector<uint64_t> ord(n);
+  for (uint64_t i = 0; i < n; i++) ord[i] = i;
+  std::sort(ord.begin(), ord.end(), [&](uint64_t a, uint64_t b) {
+    return descs[a].out_start[0] != descs[b].out_start[0] ? descs[a].out_start[0] < descs[b].out_start[0] : a < b;
+  });
+  struct Group { uint64_t b, e, r0, r1; };
+  std::vector<Group> groups;
+  const uint64_t rows_per = std::max<uint64_t>(1, (out_shape[0] + K - 1) / K);
+  uint64_t reach = 0, gb = 0, gr = 0;
+  for (uint64_t k = 0; k < n; k++) {
+    const zgpu_chunk_desc &d = descs[ord[k]];
+    if (k > gb && d.out_start[0] >= reach && d.out_start[0] - gr >= rows_per) {
+      groups.push_back(Group{gb, k, gr, d.out_start[0]});
+      gb = k;
+      gr = d.out_start[0];
+    }
+    reach = std::max<uint64_t>(reach, d.out_start[0] + d.sel_shape[0]);
+  }
+  if (groups.empty() || gr != groups.back().r1 || reach != out_shape[0]) return false;
+  groups.push_back(Group{gb, n, gr, reach});
+  if (groups.front().r0 != 0) return false;
+  for (hipStream_t &cs : C->copy)
+    if (!cs) HIPCHK(hipStreamCreateWithFlags(&cs, hipStreamNonBlocking));
+  // encoded bytes: per sub-batch, address-sorted and merged ranges in one device staging buffer
+  std::vector<size_t> range_of(n, SIZE_MAX);  // descriptor -> its merged range in its sub-batch
+  std::vector<std::vector<HostRange>> granges(groups.size());
+  uint64_t total = 0;
+  for (size_t g = 0; g < groups.size(); g++) {
+    std::vector<uint64_t> idx(ord.begin() + groups[g].b, ord.begin() + groups[g].e);
+    std::sort(idx.begin(), idx.end(),
+              [&](uint64_t a, uint64_t b) { return (uintptr_t)descs[a].enc < (uintptr_t)descs[b].enc; });
+    std::vector<HostRange> &R = granges[g];
+    for (uint64_t i : idx) {
+      if (!descs[i].enc || !descs[i].enc_len) continue;
+      const uint8_t *p = (const uint8_t *)descs[i].enc;
+      if (!R.empty() && p <= R.back().src + R.back().len) {
+        HostRange &r = R.back();
+        const uint64_t end = std::max<uint64_t>((uint64_t)(p - r.src) + descs[i].enc_len, r.len);
+        total += end - r.len;
+        r.len = end;
+      } else {
+        total = (total + 255) & ~(uint64_t)255;
+        R.push_back(HostRange{p, descs[i].enc_len, total});
+        total += descs[i].enc_len;
+      }
+      range_of[i] = R.size() - 1;
+    }
+  }
+  uint8_t *enc_dev = (uint8_t *)C->dev_alloc(total ? total : 1);
+  uint8_t *dout = (uint8_t *)C->dev_alloc(out_shape[0] * row_bytes);
+  std::vector<hipEvent_t> ev(2 * groups.size(), nullptr);
+  std::vector<std::unique_ptr<zgpu_plan>> plans(groups.size());
+  auto cleanup = [&]() {
+    for (hipEvent_t e : ev)
+      if (e) (void)hipEventDestroy(e);
+    C->dev_free(enc_dev);
+    C->dev_free(dout);
+  };
+  try {
+    for (hipEvent_t &e : ev) HIPCHK(hipEventCreateWithFlags(&e, hipEventDisableTiming));
+    for (size_t g = 0; g < groups.size(); g++) {
+      const Group &G = groups[g];
+      for (const HostRange &r : granges[g])
+        HIPCHK(hipMemcpyAsync(enc_dev + r.dev_off, r.src, r.len, hipMemcpyHostToDevice, C->copy[0]));
+      HIPCHK(hipEventRecord(ev[2 * g], C->copy[0]));
+      std::vector<zgpu_chunk_desc> gd;
+      gd.reserve(G.e - G.b);
+      for (uint64_t k = G.b; k < G.e; k++) {
+        const uint64_t i = ord[k];
+        zgpu_chunk_desc d = descs[i];
+        const size_t r = range_of[i];
+        if (r != SIZE_MAX) {
+          const HostRange &hr = granges[g][r];
+          d.enc = enc_dev + hr.dev_off + ((const uint8_t *)descs[i].enc - hr.src);
+        } else {
+          d.enc = nullptr;
+        }
+        gd.push_back(d);
+      }
+      plans[g].reset(plan_new(ch, nd, gd.data(), gd.size(), out_shape, flags | ZGPU_ENC_DEVICE | ZGPU_OUT_DEVICE));
+      plan_upload(*plans[g], s);
+      HIPCHK(hipStreamWaitEvent(s, ev[2 * g], 0));
+      plan_enqueue(*plans[g], dout, s);
+      HIPCHK(hipEventRecord(ev[2 * g + 1], s));
+      HIPCHK(hipStreamWaitEvent(C->copy[1], ev[2 * g + 1], 0));
+      HIPCHK(hipMemcpyAsync(out + G.r0 * row_bytes, dout + G.r0 * row_bytes, (G.r1 - G.r0) * row_bytes,
+                            hipMemcpyDeviceToHost, C->copy[1]));
+    }
+    std::vector<int32_t> all(n, 0);
+    for (size_t g = 0; g < groups.size(); g++) {
+      const Group &G = groups[g];
+      std::vector<int32_t> st(G.e - G.b, 0);
+      plan_statuses(*plans[g], st.data(), s);
+      for (uint64_t k = G.b; k < G.e; k++) all[ord[k]] = st[k - G.b];
+    }
+    rc = 0;  // the first failing descriptor in the caller's order
+    for (uint64_t i = 0; i < n; i++) {
+      if (status) status[i] = all[i];
+      if (!rc) rc = all[i];
+    }
+    HIPCHK(hipStreamSynchronize(C->copy[1]));
+  } catch (...) {
+    (void)hipDeviceSynchronize();
+    plans.clear();
+    cleanup();
+    throw;
+  }
+  plans.clear();
+  cleanup();
+  return true;
+}
+
 int zgpu_decode_batch(zgpu_chain *ch, uint32_t nd, const zgpu_chunk_desc *descs, uint64_t n, void *out,
                       const uint64_t *out_shape, uint32_t flags, int32_t *status, void *stream) {
   ABI_GUARD_BEGIN
@@ -660,6 +787,26 @@ int zgpu_decode_batch(zgpu_chain *ch, uint32_t nd, const zgpu_chunk_desc *descs,
   std::lock_guard<std::mutex> lk(C->mu);
   HIPCHK(hipSetDevice(C->device));
   hipStream_t s = pick_stream(C, stream);
+  if (!(flags & ZGPU_ENC_DEVICE) && !(flags & ZGPU_OUT_DEVICE) && n >= 2) {
+    // pinned host in and out, full coverage: the overlapped sub-batch pipeline
+    uint64_t out_elems = 1, covered = 0, out_b;
+    for (uint32_t d = 0; d < nd; d++) out_elems *= out_shape[d];
+    out_b = out_elems * ch->chain->es;
+    bool pinned = out_b && host_is_pinned(out) && host_is_pinned((const uint8_t *)out + out_b - 1);
+    for (uint64_t i = 0; i < n && pinned; i++) {
+      uint64_t v = 1;
+      for (uint32_t d = 0; d < nd; d++) v *= descs[i].sel_shape[d];
+      covered += v;
+      const uint8_t *e = (const uint8_t *)descs[i].enc;
+      if (e && descs[i].enc_len && (!host_is_pinned(e) || !host_is_pinned(e + descs[i].enc_len - 1))) pinned = false;
+    }
+    int rc = 0;
+    if (pinned && covered == out_elems &&
+        decode_pipelined(ch, nd, descs, n, (uint8_t *)out, out_shape, flags, status, s, rc)) {
+      if (rc) set_err(rc, zgpu_status_name(rc));
+      return rc;
+    }
+  }
   std::vector<zgpu_chunk_desc> local;
   const zgpu_chunk_desc *dd = descs;
   uint8_t *enc_stage = nullptr;
@@ -733,7 +880,7 @@ int zgpu_decode_batch(zgpu_chain *ch, uint32_t nd, const zgpu_chunk_desc *descs,
   int rc = 0;
   try {
     P.reset(plan_new(ch, nd, dd, n, out_shape, flags | ZGPU_ENC_DEVICE));
-    plan_upload(*P);
+    plan_upload(*P, s);
     plan_enqueue(*P, dout, s);
     rc = plan_statuses(*P, status, s);
     if (host_out) HIPCHK(d2h_bytes((uint8_t *)out, dout, out_bytes, stage(), slab, host_copy_threads(), s));
