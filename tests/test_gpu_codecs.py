@@ -49,6 +49,12 @@ def _content(rng, n, kind):
                  sk[1000:1500], r[140000:149000]]
         out = np.concatenate(parts)
         return np.tile(out, n // len(out) + 1)[:n].copy()
+    if kind == "direct_period":  # a raw block ending a block boundary, then a long period-2/1 run from it
+        r = rng.integers(0, 256, 131072, dtype=np.uint8)
+        parts = [r, np.tile(r[-2:], 3000), rng.integers(0, 256, 131072 - 6000, dtype=np.uint8),
+                 np.full(5000, r[-1], np.uint8), rng.integers(0, 256, 200000, dtype=np.uint8)]
+        out = np.concatenate(parts)
+        return np.tile(out, n // len(out) + 1)[:n].copy()
     raise ValueError(kind)
 
 
@@ -163,7 +169,7 @@ def test_zstd_multiblock_frames(level):
     codecs = [BYTES_LE, {"name": "zstd", "configuration": {"level": level, "checksum": level != 1}}]
     oc = O.OracleChain.from_metadata(codecs, "uint8", 0, 1)
     n = 3 << 20
-    kinds = ["random", "text", "smooth", "runs", "far", "vfar", "periods", "direct"]
+    kinds = ["random", "text", "smooth", "runs", "far", "vfar", "periods", "direct", "direct_period"]
     data = [_content(rng, n, k) for k in kinds]
     # C5-like: byte-shuffled u16 blobs + noise
     z = np.arange(n // 2, dtype=np.float32)

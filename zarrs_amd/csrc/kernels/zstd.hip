@@ -2481,7 +2481,10 @@ __device__ __forceinline__ bool x_long_match(ZXSmem &S, XOut &O, uint64_t fstart
   if (off == 0 || off > p - fstart || p + ml > bend) return false;
   if (off == 1 || off == 2 || off == 4 || off == 8) {
     uint64_t pat = 0;
-    for (uint32_t j = 0; j < off; j++) pat |= (uint64_t)S.ring[(p - off + j) & XRMASK] << (8 * j);
+    for (uint32_t j = 0; j < off; j++) {  // the period: from the slot where the ring holds nothing
+      const uint64_t q = p - off + j;
+      pat |= (uint64_t)(q >= O.rv ? S.ring[q & XRMASK] : O.out[q]) << (8 * j);
+    }
     if (off == 1) pat *= 0x0101010101010101ull;
     else if (off == 2) pat *= 0x0001000100010001ull;
     else if (off == 4) pat |= pat << 32;
