@@ -35,6 +35,9 @@ for _ in range(2):
     m = a.reshape(z // 2, 2, y // 2, 2, x // 2, 2).sum(axis=(1, 3, 5))
     levels.append(((m + 4) // 8).astype(np.uint16))
 cases = [(0, (7, 0, 1)), (0, (8, 0, 1)), (0, (11, 3, 1)), (2, (1, 1, 2)), (2, (1, 0, 1)), (0, (0, 0, 0))]
+if os.environ.get("C5_CASES"):  # "level:i,j,k;level:i,j,k..."
+    cases = [(int(c.split(":")[0]), tuple(int(x) for x in c.split(":")[1].split(",")))
+             for c in os.environ["C5_CASES"].split(";")]
 blks, encs = [], []
 for li, idx in cases:
     cs = CHUNKS[li]
@@ -62,7 +65,8 @@ for v in variants:
     ch = CodecChain.from_metadata(bench.C5.CODECS, "uint16", 0, ctx)
     devs = [torch.frombuffer(bytearray(e), dtype=torch.uint8).cuda() for e in encs]
     res = []
-    for (li, idx), blk, d in zip(cases, blks, devs):
+    reps = int(os.environ.get("C5_REPS", "1"))
+    for (li, idx), blk, d in [c for c in zip(cases, blks, devs) for _ in range(reps)]:
         out = torch.zeros(blk.shape, dtype=torch.int16, device="cuda")
         st = ch.decode_batch([make_desc(d, list(blk.shape))], out, list(blk.shape), enc_device=True)
         got = out.cpu().numpy().view(np.uint16)
@@ -71,6 +75,8 @@ for v in variants:
     # all cases of one level in one batch, side by side along axis 0
     for li0 in (0, 2):
         sel = [k for k, (li, _) in enumerate(cases) if li == li0]
+        if not sel:
+            continue
         cs = CHUNKS[li0]
         out = torch.zeros([cs[0] * len(sel)] + cs[1:], dtype=torch.int16, device="cuda")
         descs = [make_desc(devs[k], cs, out_start=[j * cs[0], 0, 0]) for j, k in enumerate(sel)]

@@ -1151,6 +1151,8 @@ struct ZBlk {
   int32_t reach_c;
   uint32_t reach_m[3];
   uint32_t seg;               // 1: an executor segment starts at this block (k_zstd_plan)
+  uint64_t in_src;            // record 0: the item's encoded bytes (k_zstd_plan; the executor's
+                              // last segment rewrites the item record while others may still start)
 };
 
 struct ZScanSmem {
@@ -1895,6 +1897,7 @@ __global__ __launch_bounds__(64) void k_zstd_plan(const ZgItem *items, uint32_t 
   const int lane = lane_id();
   ZBlk *B = blks + (uint64_t)item * blk_cap;
   const uint32_t nb = nblk[item];
+  if (lane == 0 && nb) B[0].in_src = items[item].src;
   uint64_t pos = 0, frame_off = 0;
   uint32_t r0 = 1, r1 = 4, r2 = 8, err = 0;
   for (uint32_t bi = 0; bi < nb; bi++) {
@@ -2603,11 +2606,18 @@ __global__ __launch_bounds__(64) void k_zstd_exec_item(ZgItem *items, uint32_t *
   ZP_DECL;
   ZP_T(t_all);
   if (zmode[item] != ZMODE_PARALLEL || status[item]) return;
-  const ZgItem it = items[item];
-  const uint8_t *in = (const uint8_t *)it.src;
   uint8_t *out = dst + (uint64_t)item * slot_bytes;
   const ZBlk *B = blks + (uint64_t)item * blk_cap;
   const uint32_t nb = nblk[item];
+  if (!nb) {  // no blocks: an empty output
+    if (sg == 0 && lane == 0) {
+      items[item].src = (uint64_t)out;
+      items[item].len = 0;
+    }
+    return;
+  }
+  // the input pointer from the plan's copy: the item record is rewritten by the last segment
+  const uint8_t *in = (const uint8_t *)U64(B[0].in_src);
   // this wave's segment: blocks [b0, b1) between the sg-th and the next segment start (k_zstd_plan)
   uint32_t b0 = nb, b1 = nb, count = 0;
   for (uint32_t base = 0; base < nb && count <= sg + 1; base += 64) {
