@@ -303,8 +303,9 @@ class C3:
 class C5:
     """OME-Zarr-style uint16 pyramid: five levels, each the 2x2x2 mean of the one
     above, chunk shapes per level as listed there, [bytes, numcodecs.shuffle{2}, zstd{3}] chunks.
-    The y/x extents are divided by --c5-scale (default 4: L0 [512,1024,1024], 1 GiB) so the host can
-    generate and zstd-encode the pyramid in seconds; chunk shapes are unchanged. N GPUs: the chunks
+    --c5-scale divides the L0 y/x extents (default 1: the full L0 [512,4096,4096], 16 GiB, 1488 chunks,
+    ~1.5 min with data generation; 4: L0 [512,1024,1024], 93 chunks, for quick iterations); chunk
+    shapes are unchanged. N GPUs: the chunks
     of all levels are LPT-partitioned by encoded size (strong scaling, no collective)."""
     L0 = [512, 4096, 4096]
     CHUNKS = [[32, 512, 512], [64, 256, 256], [64, 128, 128], [64, 64, 64], [32, 64, 64]]
@@ -660,7 +661,7 @@ def main():
     ap.add_argument("--grid", type=int, nargs=3, default=[16, 16, 16], help="C2 chunk grid per GPU")
     ap.add_argument("--cpu-grid", type=int, nargs=3, default=[8, 8, 8], help="C2 CPU baseline sample grid")
     ap.add_argument("--cpu-seconds", type=float, default=15.0)
-    ap.add_argument("--c5-scale", type=int, default=4, help="C5: divide the L0 y/x extents by this")
+    ap.add_argument("--c5-scale", type=int, default=1, help="C5: divide the L0 y/x extents by this (1: the full [512,4096,4096] L0)")
     ap.add_argument("--no-cpu", action="store_true")
     ap.add_argument("--lane-times", action="store_true", help="print each stream lane's solo time (stderr)")
     ap.add_argument("--no-pmc", action="store_true", help="skip the rocprofv3 PMC traffic passes")

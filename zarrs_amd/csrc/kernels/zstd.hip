@@ -1998,11 +1998,6 @@ constexpr uint32_t XSTAGE_V = 512;  // staged far-source vectors (16 B) per batc
 constexpr uint32_t XPL = 32;        // bytes of a short match its own lane copies (the rest: the wave)
 constexpr int XR_LIT = ZBATCH / 16 / 64 + 1, XR_FAR = XSTAGE_V / 64;
 
-struct XReady {
-  uint64_t ms, fe;
-  int64_t sb;
-  uint32_t d, n;
-};
 struct ZXSmem {
   uint8_t ring[XRING];
   zv4u stage[XSTAGE_V];
@@ -2010,8 +2005,6 @@ struct ZXSmem {
   uint8_t vown[XSTAGE_V];  // staged far vector -> the lane (match) it belongs to
   uint32_t pfx_lit[64], pfx_out[64], pfx_nv[64], own_pv[64];
   uint64_t own_v0[64];
-  XReady rq[64];        // the round's ready matches
-  uint32_t rq_pfx[64];  // their inclusive 16-B piece counts
 };
 
 struct XOut {
