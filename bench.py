@@ -178,6 +178,45 @@ class C2:
         t = (time.perf_counter() - t0) / reps
         res["host_enc_to_host_out_GiBps"] = round(self.decoded_bytes / t / 2 ** 30, 2)
         res["roundtrip_ok"] = ok and bool(torch.equal(h_out.view(torch.int32), self.dec_ref.cpu().view(torch.int32)))
+        res.update(self.fs_leg(h_enc))
+        return res
+
+    def fs_leg(self, h_enc):
+        """Filesystem store -> device array: the 4096 chunks as files c/i/j/k
+        of a FilesystemStore, read by zgpu_retrieve_array_subset_files (host-thread preads into
+        pinned staging overlapped with H2D + decode). Buffered reads hit the page cache (the files
+        were just written); direct_io reads the device (O_DIRECT, buffered where unsupported)."""
+        import shutil
+        import tempfile
+        from zarrs_amd import Array, FilesystemStore
+        K, grid = self.CHUNK, self.args.grid
+        root = tempfile.mkdtemp(prefix="zgpu_fs_", dir=os.environ.get("TMPDIR", "/tmp"))
+        res = {}
+        try:
+            raw = h_enc.numpy()
+            st = FilesystemStore(root)
+            for c in range(self.n_chunks):
+                i, r = divmod(c, grid[1] * grid[2])
+                j, k = divmod(r, grid[2])
+                st[f"c/{i}/{j}/{k}"] = raw[c * self.chunk_bytes:(c + 1) * self.chunk_bytes].tobytes()
+            meta = {"shape": self.shape, "data_type": "float32", "fill_value": 0.0, "codecs": self.CODECS,
+                    "chunk_grid": {"name": "regular", "configuration": {"chunk_shape": [K] * 3}}}
+            for name, direct in (("fs_enc_to_device_out_GiBps", False),
+                                 ("fs_direct_enc_to_device_out_GiBps", True)):
+                arr = Array(FilesystemStore(root, direct_io=direct), meta, self.args.ctx)
+                self.out.zero_()
+                arr.retrieve_array_subset_into([0, 0, 0], self.shape, self.out)  # warm-up
+                torch.cuda.synchronize()
+                ok = self.check()
+                reps = 3
+                t0 = time.perf_counter()
+                for _ in range(reps):
+                    arr.retrieve_array_subset_into([0, 0, 0], self.shape, self.out)
+                torch.cuda.synchronize()
+                t = (time.perf_counter() - t0) / reps
+                res[name] = round(self.decoded_bytes / t / 2 ** 30, 2) if ok else "MISMATCH"
+        finally:
+            shutil.rmtree(root, ignore_errors=True)
         return res
 
 

@@ -20,6 +20,11 @@
  *                       <- Array::retrieve_array_subset_into (zarrs/src/array/array_ops/
  *                          array_read_ops_common.rs:20-179, array_read_ops_array.rs:231-375):
  *                          the array-level batched driver that feeds zgpu_decode_batch.
+ *   zgpu_decode_files / zgpu_retrieve_array_subset_files
+ *                       <- the same, with the encoded chunks read from a filesystem store:
+ *                          FilesystemStore::get / get_partial_many (zarrs_filesystem/src/lib.rs:
+ *                          323-470) feeding array_read_ops_array.rs:290-300, with the reads of
+ *                          one sub-batch overlapped with the H2D copy and decode of the previous.
  *   status codes        <- CodecError variants (zarrs_codec/src/lib.rs:617-686), 1:1 (see below).
  *
  * Threading: every entry point is thread-safe; calls on one context are serialised internally
@@ -53,6 +58,8 @@ extern "C" {
  *                                 length to be an integer multiple of the elementsize")
  *  ZGPU_INVALID_ARGUMENT       -> bad metadata / geometry (CodecCreateError, InvalidArraySubset)
  *  ZGPU_HIP_ERROR              -> device runtime failure (no zarrs equivalent)
+ *  ZGPU_STORAGE_ERROR          -> StorageError::IOError from the filesystem store (open/read
+ *                                 failures other than a missing key; zarrs_storage/src/lib.rs)
  */
 enum {
   ZGPU_OK = 0,
@@ -67,12 +74,14 @@ enum {
   ZGPU_SHUFFLE_LENGTH = 9,
   ZGPU_INVALID_ARGUMENT = 10,
   ZGPU_HIP_ERROR = 11,
+  ZGPU_STORAGE_ERROR = 12,
 };
 
 /* decode flags */
 #define ZGPU_ENC_DEVICE 0x1u  /* desc.enc / chunk_ptrs are device pointers (else host memory)  */
 #define ZGPU_OUT_DEVICE 0x2u  /* out is a device pointer (else host memory)                    */
 #define ZGPU_NO_VALIDATE 0x4u /* override: CodecOptions::validate_checksums = false for the call */
+#define ZGPU_DIRECT_IO 0x8u   /* filesystem reads: FilesystemStoreOptions::direct_io (O_DIRECT)   */
 
 typedef struct zgpu_ctx zgpu_ctx;
 typedef struct zgpu_chain zgpu_chain;
@@ -157,6 +166,40 @@ int zgpu_retrieve_array_subset(zgpu_chain *chain, uint32_t ndim, const uint64_t 
                                const uint64_t *chunk_lens, const uint64_t *sel_start,
                                const uint64_t *sel_shape, void *out, uint32_t flags,
                                void *hip_stream);
+
+/*
+ * Encoded chunks in a filesystem store. One byte range of one file per descriptor:
+ * path = FilesystemStore::key_to_fspath(key) (zarrs_filesystem/src/lib.rs:173-179); path NULL or a
+ * file that does not exist = missing key -> fill value (lib.rs:339-343,428-430); len == UINT64_MAX
+ * reads from offset to the end of the file (ByteRange::FromStart(offset, None)); a range past the
+ * end of the file gives that descriptor ZGPU_INVALID_BYTE_RANGE (lib.rs:437-447).
+ */
+typedef struct {
+  const char *path;
+  uint64_t offset;
+  uint64_t len;
+} zgpu_file_range;
+
+/*
+ * zgpu_decode_batch with descs[i].enc/enc_len taken from files[i] (the caller's enc fields are
+ * ignored). The batch is cut into sub-batches (in descriptor order); a pool of host threads reads
+ * sub-batch k+1 with positional reads (O_DIRECT page reads with ZGPU_DIRECT_IO, falling back to
+ * buffered reads where the filesystem has no O_DIRECT) into pinned staging while sub-batch k is
+ * copied to HBM and decoded. out is device memory (ZGPU_OUT_DEVICE) or host memory.
+ * Hard I/O errors (not ENOENT) fail the call with ZGPU_STORAGE_ERROR.
+ */
+int zgpu_decode_files(zgpu_chain *chain, uint32_t ndim, const zgpu_chunk_desc *descs,
+                      const zgpu_file_range *files, uint64_t n, void *out, const uint64_t *out_shape,
+                      uint32_t flags, int32_t *status, void *hip_stream);
+
+/*
+ * zgpu_retrieve_array_subset over a filesystem store: chunk_paths[i] is the path of the chunk with
+ * C-order linear grid index i (NULL or nonexistent = missing key); each chunk file is read whole.
+ */
+int zgpu_retrieve_array_subset_files(zgpu_chain *chain, uint32_t ndim, const uint64_t *array_shape,
+                                     const uint64_t *chunk_shape, const char *const *chunk_paths,
+                                     const uint64_t *sel_start, const uint64_t *sel_shape, void *out,
+                                     uint32_t flags, void *hip_stream);
 
 #ifdef __cplusplus
 }

@@ -15,21 +15,24 @@ MAX_DIMS = 8
 STATUS_NAMES = [
     "OK", "INVALID_CHECKSUM", "DECODED_SIZE_MISMATCH", "SHARD_INDEX_OOB", "CORRUPT_STREAM",
     "INVALID_BYTE_RANGE", "UNSUPPORTED", "CRC_INPUT_TOO_SHORT", "SHARD_TOO_SMALL", "SHUFFLE_LENGTH",
-    "INVALID_ARGUMENT", "HIP_ERROR",
+    "INVALID_ARGUMENT", "HIP_ERROR", "STORAGE_ERROR",
 ]
 OK, INVALID_CHECKSUM, DECODED_SIZE_MISMATCH, SHARD_INDEX_OOB, CORRUPT_STREAM, INVALID_BYTE_RANGE, \
-    UNSUPPORTED, CRC_INPUT_TOO_SHORT, SHARD_TOO_SMALL, SHUFFLE_LENGTH, INVALID_ARGUMENT, HIP_ERROR = range(12)
+    UNSUPPORTED, CRC_INPUT_TOO_SHORT, SHARD_TOO_SMALL, SHUFFLE_LENGTH, INVALID_ARGUMENT, HIP_ERROR, \
+    STORAGE_ERROR = range(13)
 
 ENC_DEVICE = 0x1
 OUT_DEVICE = 0x2
 NO_VALIDATE = 0x4
+DIRECT_IO = 0x8
+WHOLE = (1 << 64) - 1  # zgpu_file_range.len: to the end of the file
 
 # every symbol include/zgpu.h declares (tests/test_abi.py checks the .so exports all of them)
 EXPORTS = [
     "zgpu_ctx_create", "zgpu_ctx_destroy", "zgpu_last_error", "zgpu_status_name", "zgpu_version",
     "zgpu_chain_create", "zgpu_chain_destroy", "zgpu_chain_element_size", "zgpu_decode_batch",
     "zgpu_plan_create", "zgpu_plan_execute", "zgpu_plan_status", "zgpu_plan_destroy", "zgpu_plan_algorithmic_bytes",
-    "zgpu_retrieve_array_subset",
+    "zgpu_retrieve_array_subset", "zgpu_decode_files", "zgpu_retrieve_array_subset_files",
 ]
 
 
@@ -42,6 +45,10 @@ class ChunkDesc(C.Structure):
         ("sel_shape", C.c_uint64 * MAX_DIMS),
         ("out_start", C.c_uint64 * MAX_DIMS),
     ]
+
+
+class FileRange(C.Structure):
+    _fields_ = [("path", C.c_char_p), ("offset", C.c_uint64), ("len", C.c_uint64)]
 
 
 class ZgpuError(RuntimeError):
@@ -87,6 +94,10 @@ def load() -> C.CDLL:
     L.zgpu_plan_algorithmic_bytes.argtypes = [vp]
     L.zgpu_retrieve_array_subset.argtypes = [vp, u32, P64, P64, C.POINTER(vp), P64, P64, P64, vp,
                                              u32, vp]
+    L.zgpu_decode_files.argtypes = [vp, u32, C.POINTER(ChunkDesc), C.POINTER(FileRange), u64, vp, P64,
+                                    u32, C.POINTER(C.c_int32), vp]
+    L.zgpu_retrieve_array_subset_files.argtypes = [vp, u32, P64, P64, C.POINTER(C.c_char_p), P64, P64,
+                                                   vp, u32, vp]
     _lib = L
     return L
 

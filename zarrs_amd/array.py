@@ -7,6 +7,11 @@
   Array.retrieve_chunk         <- Array::retrieve_chunk (array_read_ops_array.rs:265-272)
   MemoryStore                  <- zarrs_storage MemoryStore (encoded chunks in host memory)
   DeviceStore                  <- encoded chunks resident in HBM (torch uint8 tensors)
+  FilesystemStore              <- zarrs_filesystem FilesystemStore (zarrs_filesystem/src/lib.rs):
+                                  key_to_fspath (:173-179), get / get_partial_many (:323-470);
+                                  Array reads it through zgpu_retrieve_array_subset_files (chunk
+                                  files read by host threads into pinned staging, overlapped with
+                                  the H2D copy and decode of the previous sub-batch)
 Chunk keys use the default encoding "c/i/j/k" (chunk_key_encoding/default.rs:79-102) or v2 "i.j".
 """
 from __future__ import annotations
@@ -37,6 +42,76 @@ class DeviceStore(dict):
             d[k] = torch.frombuffer(bytearray(v), dtype=torch.uint8).to(device) if len(v) else \
                 torch.empty(0, dtype=torch.uint8, device=device)
         return d
+
+
+class FilesystemStore:
+    """A directory of Zarr keys. ``direct_io`` mirrors FilesystemStoreOptions::direct_io
+    (zarrs_filesystem/src/lib.rs:74-77): O_DIRECT page reads (buffered where unsupported)."""
+    device = False
+
+    def __init__(self, base_path, direct_io: bool = False):
+        import os
+        self.base_path = os.fspath(base_path)
+        self.direct_io = direct_io
+
+    def key_to_fspath(self, key: str) -> str:
+        import os
+        return os.path.join(self.base_path, key.lstrip("/")) if key else self.base_path
+
+    def get(self, key: str):
+        try:
+            with open(self.key_to_fspath(key), "rb") as f:
+                return f.read()
+        except (FileNotFoundError, NotADirectoryError):
+            return None
+
+    def __getitem__(self, key):
+        v = self.get(key)
+        if v is None:
+            raise KeyError(key)
+        return v
+
+    def __contains__(self, key):
+        import os
+        return os.path.isfile(self.key_to_fspath(key))
+
+    def set(self, key: str, value: bytes) -> None:
+        import os
+        path = self.key_to_fspath(key)
+        os.makedirs(os.path.dirname(path), exist_ok=True)
+        with open(path, "wb") as f:
+            f.write(value)
+
+    __setitem__ = set
+
+    def decode_files(self, chain, descs, ranges, out, out_shape, status=None):
+        """zgpu_decode_files: descs (ChunkDesc array) with their (key, offset, length) ranges
+        (length None = to the end of the file)."""
+        n = len(ranges)
+        fr = (L.FileRange * max(n, 1))()
+        keep = []
+        for i, (key, off, ln) in enumerate(ranges):
+            p = None if key is None else self.key_to_fspath(key).encode()
+            keep.append(p)
+            fr[i].path, fr[i].offset, fr[i].len = p, int(off), L.WHOLE if ln is None else int(ln)
+        odev, op = _out_ptr(out)
+        st = (C.c_int32 * max(n, 1))()
+        flags = (L.OUT_DEVICE if odev else 0) | (L.DIRECT_IO if self.direct_io else 0)
+        rc = L.load().zgpu_decode_files(chain._h, len(out_shape), descs, fr, n, op, L.u64s(out_shape),
+                                        flags, st, None)
+        if status is not None:
+            status[:] = list(st)[:n]
+        return rc, list(st)[:n]
+
+
+def _out_ptr(out):
+    try:
+        import torch
+        if isinstance(out, torch.Tensor):
+            return out.is_cuda, out.data_ptr()
+    except ImportError:  # pragma: no cover
+        pass
+    return False, out.ctypes.data
 
 
 class Array:
@@ -97,6 +172,19 @@ class Array:
         return ptrs, lens, keep
 
     def retrieve_array_subset_into(self, start, shape, out) -> None:
+        if isinstance(self.store, FilesystemStore):
+            grid = self.chunk_grid_shape()
+            n = int(np.prod(grid))
+            paths = (C.c_char_p * n)()
+            for lin in range(n):
+                paths[lin] = self.store.key_to_fspath(self.chunk_key(np.unravel_index(lin, grid))).encode()
+            odev, op = _out_ptr(out)
+            flags = (L.OUT_DEVICE if odev else 0) | (L.DIRECT_IO if self.store.direct_io else 0)
+            rc = L.load().zgpu_retrieve_array_subset_files(
+                self.codecs._h, self.ndim, L.u64s(self.shape), L.u64s(self.chunk_shape), paths,
+                L.u64s(start), L.u64s(shape), op, flags, None)
+            L.check(rc)
+            return
         ptrs, lens, keep = self._tables()
         try:
             import torch

@@ -14,6 +14,7 @@
 
 #include <algorithm>
 #include <cstdio>
+#include <cstdlib>
 #include <cstring>
 #include <map>
 #include <memory>
@@ -25,6 +26,7 @@
 #include "chain.hpp"
 #include "common.hpp"
 #include "kernels/launch.hpp"
+#include "fsstore.hpp"
 #include "xfer.hpp"
 
 using namespace zgpu;
@@ -562,8 +564,9 @@ const char *zgpu_version(void) { return "zgpu 0.1.0 (gfx950)"; }
 const char *zgpu_status_name(int s) {
   static const char *names[] = {"OK", "INVALID_CHECKSUM", "DECODED_SIZE_MISMATCH", "SHARD_INDEX_OOB",
                                 "CORRUPT_STREAM", "INVALID_BYTE_RANGE", "UNSUPPORTED", "CRC_INPUT_TOO_SHORT",
-                                "SHARD_TOO_SMALL", "SHUFFLE_LENGTH", "INVALID_ARGUMENT", "HIP_ERROR"};
-  return (s >= 0 && s <= 11) ? names[s] : "UNKNOWN";
+                                "SHARD_TOO_SMALL", "SHUFFLE_LENGTH", "INVALID_ARGUMENT", "HIP_ERROR",
+                                "STORAGE_ERROR"};
+  return (s >= 0 && s <= 12) ? names[s] : "UNKNOWN";
 }
 
 const char *zgpu_last_error(const zgpu_ctx *) { return g_last_error.c_str(); }
@@ -899,29 +902,32 @@ int zgpu_decode_batch(zgpu_chain *ch, uint32_t nd, const zgpu_chunk_desc *descs,
   ABI_GUARD_END
 }
 
-int zgpu_retrieve_array_subset(zgpu_chain *ch, uint32_t nd, const uint64_t *array_shape, const uint64_t *chunk_shape,
-                               const void *const *chunk_ptrs, const uint64_t *chunk_lens, const uint64_t *sel_start,
-                               const uint64_t *sel_shape, void *out, uint32_t flags, void *stream) {
-  ABI_GUARD_BEGIN
-  if (!ch || !array_shape || !chunk_shape || !chunk_ptrs || !chunk_lens || !sel_start || !sel_shape || !out)
-    return set_err(ZGPU_INVALID_ARGUMENT, "NULL argument");
-  if (nd == 0 || nd > ZGPU_MAX_DIMS) return set_err(ZGPU_INVALID_ARGUMENT, "ndim out of range");
-  // array_read_ops_common.rs:20-109: subset -> intersecting chunks -> one descriptor per chunk
+// array_read_ops_common.rs:20-109: subset -> intersecting chunks -> one descriptor per chunk, in
+// C order of the chunk grid; lins[k] = descriptor k's C-order linear chunk-grid index.
+// Returns ZGPU_OK, -1 for an empty subset (nothing to do), or an error status.
+static int subset_descs(uint32_t nd, const uint64_t *array_shape, const uint64_t *chunk_shape,
+                        const uint64_t *sel_start, const uint64_t *sel_shape, std::vector<zgpu_chunk_desc> &descs,
+                        std::vector<uint64_t> &lins) {
   uint64_t grid[ZG_MAXD], lo[ZG_MAXD], hi[ZG_MAXD], idx[ZG_MAXD];
   uint64_t nchunks = 1;
+  bool empty = false;
   for (uint32_t d = 0; d < nd; d++) {
     if (chunk_shape[d] == 0) return set_err(ZGPU_INVALID_ARGUMENT, "zero chunk extent");
     if (sel_start[d] + sel_shape[d] > array_shape[d])
       return set_err(ZGPU_INVALID_ARGUMENT, "array subset out of bounds");
     grid[d] = (array_shape[d] + chunk_shape[d] - 1) / chunk_shape[d];
-    if (sel_shape[d] == 0) return ZGPU_OK;  // nothing to do
+    if (sel_shape[d] == 0) {
+      empty = true;
+      continue;
+    }
     lo[d] = sel_start[d] / chunk_shape[d];
     hi[d] = (sel_start[d] + sel_shape[d] - 1) / chunk_shape[d] + 1;
     nchunks *= hi[d] - lo[d];
     idx[d] = lo[d];
   }
-  std::vector<zgpu_chunk_desc> descs;
+  if (empty) return -1;
   descs.reserve(nchunks);
+  lins.reserve(nchunks);
   for (;;) {
     zgpu_chunk_desc D{};
     uint64_t lin = 0;
@@ -934,9 +940,8 @@ int zgpu_retrieve_array_subset(zgpu_chain *ch, uint32_t nd, const uint64_t *arra
       D.sel_shape[d] = s1 - s0;
       D.out_start[d] = s0 - sel_start[d];
     }
-    D.enc = chunk_ptrs[lin];
-    D.enc_len = D.enc ? chunk_lens[lin] : 0;
     descs.push_back(D);
+    lins.push_back(lin);
     int d = (int)nd - 1;
     for (; d >= 0; d--) {
       if (++idx[d] < hi[d]) break;
@@ -944,7 +949,185 @@ int zgpu_retrieve_array_subset(zgpu_chain *ch, uint32_t nd, const uint64_t *arra
     }
     if (d < 0) break;
   }
+  return ZGPU_OK;
+}
+
+int zgpu_retrieve_array_subset(zgpu_chain *ch, uint32_t nd, const uint64_t *array_shape, const uint64_t *chunk_shape,
+                               const void *const *chunk_ptrs, const uint64_t *chunk_lens, const uint64_t *sel_start,
+                               const uint64_t *sel_shape, void *out, uint32_t flags, void *stream) {
+  ABI_GUARD_BEGIN
+  if (!ch || !array_shape || !chunk_shape || !chunk_ptrs || !chunk_lens || !sel_start || !sel_shape || !out)
+    return set_err(ZGPU_INVALID_ARGUMENT, "NULL argument");
+  if (nd == 0 || nd > ZGPU_MAX_DIMS) return set_err(ZGPU_INVALID_ARGUMENT, "ndim out of range");
+  std::vector<zgpu_chunk_desc> descs;
+  std::vector<uint64_t> lins;
+  const int r = subset_descs(nd, array_shape, chunk_shape, sel_start, sel_shape, descs, lins);
+  if (r) return r < 0 ? ZGPU_OK : r;
+  for (size_t k = 0; k < descs.size(); k++) {
+    descs[k].enc = chunk_ptrs[lins[k]];
+    descs[k].enc_len = descs[k].enc ? chunk_lens[lins[k]] : 0;
+  }
   return zgpu_decode_batch(ch, nd, descs.data(), descs.size(), out, sel_shape, flags, nullptr, stream);
+  ABI_GUARD_END
+}
+
+// Filesystem store -> HBM -> decode, pipelined over sub-batches in descriptor order: host threads
+// read sub-batch g into pinned slab g%2 (positional reads, O_DIRECT pages with ZGPU_DIRECT_IO) while
+// sub-batch g-1's H2D (copy stream 0) and decode (the call's stream) run; slab g%2 is reused once
+// sub-batch g-2's H2D has completed.
+int zgpu_decode_files(zgpu_chain *ch, uint32_t nd, const zgpu_chunk_desc *descs, const zgpu_file_range *files,
+                      uint64_t n, void *out, const uint64_t *out_shape, uint32_t flags, int32_t *status,
+                      void *stream) {
+  ABI_GUARD_BEGIN
+  if (!ch || !out_shape || (n && (!descs || !files)) || !out) return set_err(ZGPU_INVALID_ARGUMENT, "NULL argument");
+  if (nd == 0 || nd > ZGPU_MAX_DIMS) return set_err(ZGPU_INVALID_ARGUMENT, "ndim out of range");
+  zgpu_ctx *C = ch->ctx;
+  std::lock_guard<std::mutex> lk(C->mu);
+  HIPCHK(hipSetDevice(C->device));
+  hipStream_t s = pick_stream(C, stream);
+  const int threads = host_copy_threads();
+  std::vector<FileRange> fr(n);
+  for (uint64_t i = 0; i < n; i++) {
+    fr[i].path = files[i].path;
+    fr[i].offset = files[i].offset;
+    fr[i].len = files[i].len;
+  }
+  struct Closer {
+    std::vector<FileRange> &r;
+    ~Closer() { fs_close_all(r); }
+  } closer{fr};
+  std::string err = fs_open_all(fr, (flags & ZGPU_DIRECT_IO) != 0, threads);
+  if (!err.empty()) return set_err(ZGPU_STORAGE_ERROR, err);
+  // sub-batches: ~8 of them, 32-512 MiB of reads each
+  auto readable = [&](uint64_t i) { return !fr[i].missing && !fr[i].bad_range; };
+  uint64_t total = 0;
+  for (uint64_t i = 0; i < n; i++)
+    if (readable(i)) total += (fr[i].rd_len + 4095) & ~(uint64_t)4095;
+  uint64_t target = std::min<uint64_t>(512ull << 20, std::max<uint64_t>(32ull << 20, total / 8));
+  if (const char *e = std::getenv("ZGPU_FS_GROUP_BYTES")) target = std::max<uint64_t>(1, std::strtoull(e, nullptr, 10));
+  struct Group { uint64_t b, e, base, bytes; };
+  std::vector<Group> groups;
+  {
+    Group g{0, 0, 0, 0};
+    for (uint64_t i = 0; i < n; i++) {
+      const uint64_t sz = readable(i) ? ((fr[i].rd_len + 4095) & ~(uint64_t)4095) : 0;
+      if (i > g.b && g.bytes + sz > target) {
+        g.e = i;
+        groups.push_back(g);
+        g = Group{i, 0, g.base + g.bytes, 0};
+      }
+      fr[i].slab_off = g.bytes;  // page-aligned (O_DIRECT buffers)
+      g.bytes += sz;
+    }
+    g.e = n;
+    if (n) groups.push_back(g);
+  }
+  uint64_t max_g = 4096;
+  for (const Group &g : groups) max_g = std::max(max_g, g.bytes);
+  uint64_t out_elems = 1;
+  for (uint32_t d = 0; d < nd; d++) out_elems *= out_shape[d];
+  const uint64_t out_bytes = out_elems * ch->chain->es;
+  const bool host_out = !(flags & ZGPU_OUT_DEVICE);
+  for (hipStream_t &cs : C->copy)
+    if (!cs) HIPCHK(hipStreamCreateWithFlags(&cs, hipStreamNonBlocking));
+  uint8_t *enc_dev = nullptr, *dout = (uint8_t *)out, *slab[2] = {nullptr, nullptr}, *pin_stage = nullptr;
+  const uint64_t stage_slab = 64ull << 20;
+  std::vector<hipEvent_t> ev(groups.size(), nullptr);
+  std::vector<std::unique_ptr<zgpu_plan>> plans(groups.size());
+  auto cleanup = [&]() {
+    (void)hipStreamSynchronize(C->copy[0]);
+    (void)hipStreamSynchronize(s);
+    plans.clear();
+    for (hipEvent_t e : ev)
+      if (e) (void)hipEventDestroy(e);
+    C->dev_free(enc_dev);
+    if (host_out) C->dev_free(dout);
+    C->host_free(slab[0]);
+    C->host_free(slab[1]);
+    C->host_free(pin_stage);
+  };
+  int rc = 0;
+  try {
+    enc_dev = (uint8_t *)C->dev_alloc(total ? total : 1);
+    if (host_out) {
+      dout = (uint8_t *)C->dev_alloc(out_bytes ? out_bytes : 1);
+      uint64_t covered = 0;  // disjoint regions: equal volumes mean full coverage (no upload)
+      for (uint64_t i = 0; i < n; i++) {
+        uint64_t v = 1;
+        for (uint32_t d = 0; d < nd; d++) v *= descs[i].sel_shape[d];
+        covered += v;
+      }
+      if (covered != out_elems) {
+        pin_stage = (uint8_t *)C->host_alloc(2 * stage_slab);
+        HIPCHK(h2d_bytes(dout, (const uint8_t *)out, out_bytes, pin_stage, stage_slab, threads, s));
+      }
+    }
+    for (int k = 0; k < 2 && k < (int)groups.size(); k++) slab[k] = (uint8_t *)C->host_alloc(max_g);
+    for (hipEvent_t &e : ev) HIPCHK(hipEventCreateWithFlags(&e, hipEventDisableTiming));
+    for (size_t g = 0; g < groups.size(); g++) {
+      const Group &G = groups[g];
+      if (g >= 2) HIPCHK(hipEventSynchronize(ev[g - 2]));  // slab g%2 free again
+      uint8_t *sl = slab[g & 1];
+      std::vector<uint64_t> idx;
+      for (uint64_t i = G.b; i < G.e; i++)
+        if (readable(i)) idx.push_back(i);
+      err = fs_read_into(fr, idx, sl, threads);
+      if (!err.empty()) throw ChainError{ZGPU_STORAGE_ERROR, err};
+      if (G.bytes) HIPCHK(hipMemcpyAsync(enc_dev + G.base, sl, G.bytes, hipMemcpyHostToDevice, C->copy[0]));
+      HIPCHK(hipEventRecord(ev[g], C->copy[0]));
+      std::vector<zgpu_chunk_desc> gd(descs + G.b, descs + G.e);
+      for (uint64_t i = G.b; i < G.e; i++) {
+        zgpu_chunk_desc &d = gd[i - G.b];
+        if (readable(i)) {  // an empty object still has a (valid) address
+          d.enc = enc_dev + G.base + fr[i].slab_off + (fr[i].offset - fr[i].rd_off);
+          d.enc_len = fr[i].len;
+        } else {
+          d.enc = nullptr;
+          d.enc_len = 0;
+        }
+      }
+      plans[g].reset(plan_new(ch, nd, gd.data(), gd.size(), out_shape, flags | ZGPU_ENC_DEVICE | ZGPU_OUT_DEVICE));
+      plan_upload(*plans[g], s);
+      HIPCHK(hipStreamWaitEvent(s, ev[g], 0));
+      plan_enqueue(*plans[g], dout, s);
+    }
+    std::vector<int32_t> all(n, 0);
+    for (size_t g = 0; g < groups.size(); g++)
+      plan_statuses(*plans[g], all.data() + groups[g].b, s);
+    for (uint64_t i = 0; i < n; i++) {
+      if (fr[i].bad_range) all[i] = ZGPU_INVALID_BYTE_RANGE;
+      if (status) status[i] = all[i];
+      if (!rc) rc = all[i];
+    }
+    if (host_out) {
+      if (!pin_stage) pin_stage = (uint8_t *)C->host_alloc(2 * stage_slab);
+      HIPCHK(d2h_bytes((uint8_t *)out, dout, out_bytes, pin_stage, stage_slab, threads, s));
+    }
+  } catch (...) {
+    cleanup();
+    throw;
+  }
+  cleanup();
+  if (rc) set_err(rc, zgpu_status_name(rc));
+  return rc;
+  ABI_GUARD_END
+}
+
+int zgpu_retrieve_array_subset_files(zgpu_chain *ch, uint32_t nd, const uint64_t *array_shape,
+                                     const uint64_t *chunk_shape, const char *const *chunk_paths,
+                                     const uint64_t *sel_start, const uint64_t *sel_shape, void *out, uint32_t flags,
+                                     void *stream) {
+  ABI_GUARD_BEGIN
+  if (!ch || !array_shape || !chunk_shape || !chunk_paths || !sel_start || !sel_shape || !out)
+    return set_err(ZGPU_INVALID_ARGUMENT, "NULL argument");
+  if (nd == 0 || nd > ZGPU_MAX_DIMS) return set_err(ZGPU_INVALID_ARGUMENT, "ndim out of range");
+  std::vector<zgpu_chunk_desc> descs;
+  std::vector<uint64_t> lins;
+  const int r = subset_descs(nd, array_shape, chunk_shape, sel_start, sel_shape, descs, lins);
+  if (r) return r < 0 ? ZGPU_OK : r;
+  std::vector<zgpu_file_range> files(descs.size());
+  for (size_t k = 0; k < descs.size(); k++) files[k] = zgpu_file_range{chunk_paths[lins[k]], 0, UINT64_MAX};
+  return zgpu_decode_files(ch, nd, descs.data(), files.data(), descs.size(), out, sel_shape, flags, nullptr, stream);
   ABI_GUARD_END
 }
 
