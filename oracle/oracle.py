@@ -72,6 +72,7 @@ def lib():
         L.orc_chain_add_gzip.argtypes = [vp, i32]
         L.orc_chain_add_zstd.argtypes = [vp, i32, i32]
         L.orc_chain_add_shuffle.argtypes = [vp, u32]
+        L.orc_chain_add_blosc.argtypes = [vp, C.c_char_p, i32, i32, u32, C.c_uint64]
         L.orc_decode_chunk.argtypes = [vp, vp, u64, u32, P64, i32, vp]
         L.orc_encode_chunk.argtypes = [vp, vp, u32, P64, C.POINTER(vp), P64]
         L.orc_free.argtypes = [vp]
@@ -153,6 +154,10 @@ class OracleChain:
                 st = L.orc_chain_add_gzip(h, int(cfg.get("level", 5)))
             elif name == "zstd":
                 st = L.orc_chain_add_zstd(h, int(cfg.get("level", 0)), 1 if cfg.get("checksum") else 0)
+            elif name == "blosc":
+                sh = {"noshuffle": 0, "shuffle": 1, "bitshuffle": 2}[cfg.get("shuffle", "noshuffle")]
+                st = L.orc_chain_add_blosc(h, cfg.get("cname", "lz4").encode(), int(cfg.get("clevel", 5)), sh,
+                                           int(cfg.get("typesize") or 0), int(cfg.get("blocksize") or 0))
             elif name in ("numcodecs.shuffle", "shuffle"):
                 st = L.orc_chain_add_shuffle(h, int(cfg.get("elementsize", 4)))
             else:

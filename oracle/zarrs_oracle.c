@@ -40,12 +40,18 @@ extern ZSTD_DStream *ZSTD_createDStream(void);
 extern size_t ZSTD_freeDStream(ZSTD_DStream *);
 extern size_t ZSTD_initDStream(ZSTD_DStream *);
 extern size_t ZSTD_decompressStream(ZSTD_DStream *, ZSTD_outBuffer *, ZSTD_inBuffer *);
+/* ---- c-blosc 1.21 public ABI (blosc-src 0.3.6 vendors c-blosc 1.21.x; zarrs/Cargo.toml:103) ---- */
+extern int blosc_cbuffer_validate(const void *cbuffer, size_t cbytes, size_t *nbytes);
+extern int blosc_decompress_ctx(const void *src, void *dest, size_t destsize, int numinternalthreads);
+extern int blosc_compress_ctx(int clevel, int doshuffle, size_t typesize, size_t nbytes, const void *src,
+                              void *dest, size_t destsize, const char *compressor, size_t blocksize,
+                              int numinternalthreads);
 #define ZSTD_c_compressionLevel 100
 #define ZSTD_c_checksumFlag 201
 #define ZSTD_CONTENTSIZE_ERROR (0ULL - 2)
 
 #define MAXD 8
-enum { K_TRANSPOSE = 1, K_BYTES, K_SHARDING, K_CRC32C, K_GZIP, K_ZSTD, K_SHUFFLE };
+enum { K_TRANSPOSE = 1, K_BYTES, K_SHARDING, K_CRC32C, K_GZIP, K_ZSTD, K_SHUFFLE, K_BLOSC };
 
 typedef struct {
   int kind;
@@ -54,6 +60,10 @@ typedef struct {
   int big_endian;            /* bytes */
   int at_start;              /* crc32c location / sharding index_location */
   int level, checksum;       /* gzip / zstd */
+  int bl_shuffle;            /* blosc: 0 noshuffle, 1 shuffle, 2 bitshuffle */
+  uint32_t bl_typesize;      /* blosc */
+  uint64_t bl_blocksize;     /* blosc (0 = automatic) */
+  char bl_cname[16];         /* blosc compressor name */
   uint32_t elementsize;      /* shuffle */
   uint64_t inner[MAXD];      /* sharding subchunk shape */
   orc_chain *inner_chain, *index_chain;
@@ -203,6 +213,16 @@ int orc_chain_add_zstd(orc_chain *c, int level, int checksum) {
   k->level = level; k->checksum = checksum;
   return ORC_OK;
 }
+/* BL = zarrs/src/array/codec/bytes_to_bytes/blosc/{blosc_codec_via_blosc_src.rs,blosc_via_blosc_src.rs} */
+int orc_chain_add_blosc(orc_chain *c, const char *cname, int clevel, int shuffle, uint32_t typesize,
+                        uint64_t blocksize) {
+  if (!cname || strlen(cname) >= 16 || shuffle < 0 || shuffle > 2) return ORC_INVALID_ARGUMENT;
+  codec_t *k = add_b2b(c, K_BLOSC);
+  if (!k) return ORC_INVALID_ARGUMENT;
+  k->level = clevel; k->bl_shuffle = shuffle; k->bl_typesize = typesize; k->bl_blocksize = blocksize;
+  strcpy(k->bl_cname, cname);
+  return ORC_OK;
+}
 int orc_chain_add_shuffle(orc_chain *c, uint32_t es) {
   if (es == 0) return ORC_INVALID_ARGUMENT;
   codec_t *k = add_b2b(c, K_SHUFFLE);
@@ -275,6 +295,18 @@ static int gzip_decode(buf_t *b, uint64_t hint) {
   if (r != Z_STREAM_END) { free(o); return ORC_CORRUPT_STREAM; }
   buf_drop(b);
   b->p = o; b->n = len; b->owned = 1;
+  return ORC_OK;
+}
+
+/* BL blosc_codec_via_blosc_src.rs:132-142 (do_decode): blosc_validate -> destsize, then
+ * blosc_decompress_ctx (blosc_via_blosc_src.rs:115-121,162-191); invalid -> CodecError::Other */
+static int blosc_decode(buf_t *b) {
+  size_t dest = 0;
+  if (blosc_cbuffer_validate(b->p, b->n, &dest) != 0) return ORC_CORRUPT_STREAM;
+  uint8_t *o = malloc(dest ? dest : 1);
+  int r = blosc_decompress_ctx(b->p, o, dest, 1);
+  if (r < 0 || (size_t)r != dest || (r == 0 && dest != 0)) { free(o); return ORC_CORRUPT_STREAM; }
+  buf_drop(b); b->p = o; b->n = dest; b->owned = 1;
   return ORC_OK;
 }
 
@@ -593,6 +625,7 @@ static int decode_region(const orc_chain *c, const uint8_t *enc, uint64_t len, u
       case K_GZIP: st = gzip_decode(&b, i == 0 ? nbytes : 0); break;
       case K_ZSTD: st = zstd_decode(&b); break;
       case K_SHUFFLE: st = shuffle_decode(k, &b); break;
+      case K_BLOSC: st = blosc_decode(&b); break;
       default: st = ORC_UNSUPPORTED;
     }
     if (st) { buf_drop(&b); return st; }
@@ -690,6 +723,15 @@ static int b2b_encode(const codec_t *k, buf_t *b) {
       ZSTD_freeCCtx(cc);
       if (ZSTD_isError(r)) { free(o); return ORC_CORRUPT_STREAM; }
       buf_drop(b); b->p = o; b->n = r; b->owned = 1;
+      return ORC_OK;
+    }
+    case K_BLOSC: { /* BL blosc_via_blosc_src.rs:64-110 (blosc_compress_bytes) */
+      size_t cap = b->n + 16;
+      uint8_t *o = malloc(cap);
+      int r = blosc_compress_ctx(k->level, k->bl_shuffle, k->bl_typesize ? k->bl_typesize : 1, b->n, b->p, o, cap,
+                                 k->bl_cname, k->bl_blocksize, 1);
+      if (r <= 0) { free(o); return ORC_CORRUPT_STREAM; }
+      buf_drop(b); b->p = o; b->n = (uint64_t)r; b->owned = 1;
       return ORC_OK;
     }
     case K_SHUFFLE: { /* SF:86-107 */

@@ -54,6 +54,8 @@ int orc_chain_add_sharding(orc_chain *c, uint32_t ndim, const uint64_t *inner_sh
 int orc_chain_add_crc32c(orc_chain *c, int at_start);
 int orc_chain_add_gzip(orc_chain *c, int level);
 int orc_chain_add_zstd(orc_chain *c, int level, int checksum);
+int orc_chain_add_blosc(orc_chain *c, const char *cname, int clevel, int shuffle, uint32_t typesize,
+                        uint64_t blocksize);
 int orc_chain_add_shuffle(orc_chain *c, uint32_t elementsize);
 
 /* Full chunk decode (CodecChainBound::decode, codec_chain.rs:557-590). out must hold

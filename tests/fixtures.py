@@ -45,6 +45,11 @@ def load_array(rel: str):
             elif comp["id"] == "zstd":
                 codecs.append({"name": "zstd", "configuration": {"level": comp.get("level", 0),
                                                                  "checksum": False}})
+            elif comp["id"] == "blosc":  # zarrs_metadata_ext v2->v3 blosc: shuffle 0/1/2, typesize = dtype
+                codecs.append({"name": "blosc", "configuration": {
+                    "cname": comp["cname"], "clevel": comp["clevel"],
+                    "shuffle": ["noshuffle", "shuffle", "bitshuffle"][comp.get("shuffle", 1)],
+                    "typesize": int(z["dtype"][2:]), "blocksize": comp.get("blocksize", 0)}})
             else:
                 raise ValueError(comp)
     grid = [-(-s // c) for s, c in zip(shape, chunk_shape)]
@@ -66,3 +71,6 @@ FLOAT_0_99 = [
     "v2/array_none_C.zarr", "v2/array_none_F.zarr", "v2/array_gzip_C.zarr", "v2/array_zstd_C.zarr",
 ]
 SHARDED = "sharded_array_write_read.zarr/group/array"
+# blosc fixtures (zstd + bitshuffle, typesize 4), also float32 0..99 (zarrs/src/array.rs:1684-1788)
+BLOSC = ["v3/array_blosc.zarr", "v3/array_blosc_transpose.zarr", "v3_zarr_python/array_blosc.zarr",
+         "v2/array_blosc_C.zarr", "v2/array_blosc_F.zarr"]

@@ -16,6 +16,9 @@ ARRAYS = [
     "v2/array_none_C.zarr", "v2/array_none_F.zarr", "v2/array_gzip_C.zarr",
     "v2/array_zstd_C.zarr",
     "sharded_array_write_read.zarr/group/array",
+    # blosc (c-blosc 1.21 via blosc-src): zstd + bitshuffle, float32 0..99
+    "v3/array_blosc.zarr", "v3/array_blosc_transpose.zarr", "v3_zarr_python/array_blosc.zarr",
+    "v2/array_blosc_C.zarr", "v2/array_blosc_F.zarr",
 ]
 
 if __name__ == "__main__":

@@ -1,0 +1,150 @@
+"""GPU parity of the blosc codec against the reference's blosc fixtures
+(zstd + bitshuffle, written by zarrs and zarr-python) and the CPU oracle (c-blosc 1.21, the library
+zarrs' blosc-src binds) on seeded inputs: lz4 / lz4hc / zstd streams, byte shuffle / bitshuffle /
+none, typesizes 1-8, forced block sizes (split streams, leftover blocks, bitshuffle skipped for
+element counts that are not a multiple of 8), memcpyed frames, blosc inside sharding. Bit-exact."""
+import numpy as np
+import pytest
+
+import fixtures as F
+import oracle as O
+
+pytestmark = pytest.mark.gpu
+
+
+@pytest.fixture(scope="module")
+def torch_cuda():
+    import torch
+    return torch
+
+
+@pytest.fixture(scope="module")
+def ctx():
+    from zarrs_amd import Context
+    return Context(0)
+
+
+@pytest.mark.parametrize("store", ["host", "hbm"])
+@pytest.mark.parametrize("fixture", F.BLOSC)
+def test_blosc_reference_fixture(ctx, torch_cuda, fixture, store):
+    from zarrs_amd import Array, DeviceStore, MemoryStore
+    m, chunks = F.load_array(fixture)
+    meta = {"shape": m["shape"], "data_type": m["data_type"], "fill_value": m["fill_value"],
+            "chunk_grid": {"name": "regular", "configuration": {"chunk_shape": m["chunk_shape"]}},
+            "codecs": m["codecs"]}
+    ms = MemoryStore({"c/" + "/".join(map(str, k)): v for k, v in chunks.items()})
+    arr = Array(DeviceStore.from_store(ms) if store == "hbm" else ms, meta, ctx)
+    exp = np.arange(100).reshape(10, 10).astype(np.float32)
+    assert np.array_equal(arr.retrieve_array_subset(), exp)
+    assert np.array_equal(arr.retrieve_array_subset([1, 2], [6, 5]), exp[1:7, 2:7])
+
+
+def _blosc(cname, shuffle, ts, blocksize=0, clevel=5):
+    return {"name": "blosc", "configuration": {"cname": cname, "clevel": clevel, "shuffle": shuffle,
+                                               "typesize": ts, "blocksize": blocksize}}
+
+
+DT = {1: "uint8", 2: "uint16", 4: "float32", 8: "float64"}
+CASES = []
+for cname in ("lz4", "zstd", "lz4hc"):
+    for sh in ("noshuffle", "shuffle", "bitshuffle"):
+        for ts in (1, 2, 4, 8):
+            CASES.append((cname, sh, ts))
+
+
+def _data(rng, n, ts):
+    a = rng.standard_normal(n) * 40
+    a[: n // 2] = np.round(a[: n // 2])  # half compressible
+    if ts == 1:
+        return (a % 200).astype(np.uint8)
+    if ts == 2:
+        return np.abs(a).astype(np.uint16)
+    return a.astype(DT[ts])
+
+
+@pytest.mark.parametrize("cname,shuffle,ts", CASES, ids=[f"{c}-{s}-{t}" for c, s, t in CASES])
+def test_blosc_batch_vs_oracle(ctx, torch_cuda, cname, shuffle, ts):
+    """Batches of 3 chunks (one decode call per chunk shape: a plan has one leaf chunk shape)
+    through the GPU stage, bytes vs the c-blosc oracle, device-resident inputs."""
+    from zarrs_amd import CodecChain, make_desc
+    rng = np.random.default_rng(ts * 7 + len(cname) + len(shuffle))
+    # (elements, blocksize): single block, forced small blocks with a leftover, element counts that
+    # are not a multiple of 8, a large chunk with automatic blocks
+    specs = [(1, 0), (100, 0), (1000, 256), (4099, 1024), (33333, 0), (262147, 0), (5000, 4096)]
+    # the GPU chain is parsed once; the decoder reads cname/shuffle/blocksize from each frame
+    ch = CodecChain.from_metadata([{"name": "bytes", "configuration": {"endian": "little"}},
+                                   _blosc(cname, shuffle, ts)], DT[ts], 0, ctx)
+    for n, bsz in specs:
+        codecs = [{"name": "bytes", "configuration": {"endian": "little"}}, _blosc(cname, shuffle, ts, bsz)]
+        co = O.OracleChain.from_metadata(codecs, DT[ts], 0, 1)
+        descs, keep, exp = [], [], []
+        for k in range(3):
+            a = _data(rng, n, ts)
+            enc = co.encode(a)
+            assert np.array_equal(co.decode(enc, (n,)), a)
+            d = torch_cuda.frombuffer(bytearray(enc), dtype=torch_cuda.uint8).cuda()
+            keep.append(d)
+            descs.append(make_desc(d, [n], out_start=[k * n]))
+            exp.append(a)
+        out = np.zeros(3 * n, DT[ts])
+        st = ch.decode_batch(descs, out, [3 * n], enc_device=True)
+        assert st == [0] * 3, (n, bsz)
+        assert out.tobytes() == np.concatenate(exp).tobytes(), (n, bsz)
+
+
+def test_blosc_memcpyed_and_errors(ctx, torch_cuda):
+    from zarrs_amd import CodecChain, ZgpuError, make_desc
+    from zarrs_amd import _lib as L
+    rng = np.random.default_rng(5)
+    a = rng.random(3000).astype(np.float32)  # clevel 0 -> memcpyed frame
+    codecs0 = [{"name": "bytes", "configuration": {"endian": "little"}}, _blosc("lz4", "shuffle", 4, clevel=0)]
+    enc0 = O.OracleChain.from_metadata(codecs0, "float32", 0, 1).encode(a)
+    assert enc0[2] & 0x2  # memcpyed
+    ch = CodecChain.from_metadata(codecs0, "float32", 0, ctx)
+    out = np.zeros(3000, np.float32)
+    assert ch.decode_batch([make_desc(enc0, [3000])], out, [3000], enc_device=False) == [0]
+    assert np.array_equal(out, a)
+    # blosclz is not decoded on the GPU: UNSUPPORTED, loudly
+    codecs1 = [{"name": "bytes", "configuration": {"endian": "little"}}, _blosc("blosclz", "shuffle", 4)]
+    enc1 = O.OracleChain.from_metadata(codecs1, "float32", 0, 1).encode(np.zeros(3000, np.float32) + 1)
+    with pytest.raises(ZgpuError) as ei:
+        ch.decode_batch([make_desc(enc1, [3000])], out, [3000], enc_device=False)
+    assert ei.value.status == L.UNSUPPORTED
+    # corrupt lz4 stream / truncated frame / wrong decoded size
+    codecs2 = [{"name": "bytes", "configuration": {"endian": "little"}}, _blosc("lz4", "shuffle", 4)]
+    b = np.round(rng.standard_normal(3000) * 10).astype(np.float32)
+    enc2 = bytearray(O.OracleChain.from_metadata(codecs2, "float32", 0, 1).encode(b))
+    assert not enc2[2] & 0x2
+    bad = bytearray(enc2)  # the first stream's compressed size points past the frame
+    p0 = int.from_bytes(enc2[16:20], "little")
+    bad[p0:p0 + 4] = (0x7FFFFFF0).to_bytes(4, "little")
+    for e, want in ((bytes(bad), (L.CORRUPT_STREAM,)), (bytes(enc2[:10]), (L.CORRUPT_STREAM,)),
+                    (bytes(enc2[:-5]), (L.CORRUPT_STREAM,))):
+        with pytest.raises(ZgpuError) as ei:
+            ch.decode_batch([make_desc(e, [3000])], out, [3000], enc_device=False)
+        assert ei.value.status in want
+    with pytest.raises(ZgpuError) as ei:
+        ch.decode_batch([make_desc(bytes(enc2), [2000])], out[:2000], [2000], enc_device=False)
+    assert ei.value.status == L.DECODED_SIZE_MISMATCH
+
+
+@pytest.mark.parametrize("cname", ["lz4", "zstd"])
+def test_blosc_inside_sharding_vs_oracle(ctx, torch_cuda, cname):
+    from zarrs_amd import Array, DeviceStore, MemoryStore
+    from test_gpu_parity import _encode_grid
+    codecs = [{"name": "sharding_indexed", "configuration": {
+        "chunk_shape": [16, 16, 16],
+        "codecs": [{"name": "bytes", "configuration": {"endian": "little"}}, _blosc(cname, "shuffle", 2)],
+        "index_codecs": [{"name": "bytes", "configuration": {"endian": "little"}}, {"name": "crc32c"}]}}]
+    rng = np.random.default_rng(11)
+    shape, cs = [70, 64, 50], [32, 32, 32]
+    a = (np.abs(rng.standard_normal(shape)) * 300).astype(np.uint16)
+    co = O.OracleChain.from_metadata(codecs, "uint16", 7, 3)
+    chunks = _encode_grid(co, a, cs, drop={(1, 1, 0)})
+    ms = MemoryStore({"c/" + "/".join(map(str, k)): v for k, v in chunks.items()})
+    meta = {"shape": shape, "data_type": "uint16", "fill_value": 7, "codecs": codecs,
+            "chunk_grid": {"name": "regular", "configuration": {"chunk_shape": cs}}}
+    arr = Array(DeviceStore.from_store(ms), meta, ctx)
+    for start, sub in (([0, 0, 0], shape), ([5, 17, 3], [60, 40, 29])):
+        exp = O.retrieve_array_subset(co, shape, cs, chunks, start, sub, nthreads=4)
+        assert arr.retrieve_array_subset(start, sub).tobytes() == exp.tobytes(), (start, sub)

@@ -20,7 +20,7 @@ def test_crc32c_kat():
     assert O.crc32c(b"123456789") == 0xE3069283
 
 
-@pytest.mark.parametrize("fixture", F.FLOAT_0_99)
+@pytest.mark.parametrize("fixture", F.FLOAT_0_99 + F.BLOSC)
 def test_reference_fixture_float(fixture):
     # zarrs/src/array.rs:1684-1788: every array_* fixture decodes to float32 0..99
     m, chunks = F.load_array(fixture)

@@ -116,6 +116,20 @@ static std::shared_ptr<Chain> parse(const Json &codecs, const std::string &dt, u
       k.level = l ? (int)l->as_int() : 0;
       const Json *cs = cfg_get("checksum");
       k.checksum = cs && cs->kind == Json::Bool && cs->b;
+    } else if (k.name == "blosc" || k.name == "numcodecs.blosc") {
+      // blosc_codec_via_blosc_src.rs: cname / clevel / shuffle / typesize / blocksize; the decoder
+      // reads everything it needs (compressor, shuffle, typesize, block size) from the frame header
+      k.kind = CodecKind::Blosc;
+      const Json *cn = cfg_get("cname");
+      k.cname = cn && cn->kind == Json::Str ? cn->s : "lz4";
+      static const char *known[] = {"blosclz", "lz4", "lz4hc", "snappy", "zlib", "zstd"};
+      bool ok = false;
+      for (const char *n : known) ok = ok || k.cname == n;
+      if (!ok) throw ChainError{ZGPU_INVALID_ARGUMENT, "blosc: unknown cname '" + k.cname + "'"};
+      const Json *l = cfg_get("clevel");
+      k.level = l ? (int)l->as_int() : 5;
+      const Json *t = cfg_get("typesize");
+      k.elementsize = t && t->kind != Json::Null ? (uint32_t)t->as_int() : 0;
     } else if (k.name == "numcodecs.shuffle" || k.name == "shuffle") {
       k.kind = CodecKind::Shuffle;
       const Json *e = cfg_get("elementsize");

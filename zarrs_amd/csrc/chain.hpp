@@ -12,7 +12,7 @@
 
 namespace zgpu {
 
-enum class CodecKind { Transpose, Bytes, Sharding, Crc32c, Gzip, Zstd, Shuffle };
+enum class CodecKind { Transpose, Bytes, Sharding, Crc32c, Gzip, Zstd, Shuffle, Blosc };
 
 struct Chain;
 
@@ -24,7 +24,8 @@ struct Codec {
   bool at_start = false;              // crc32c location / sharding index_location
   int level = 0;                      // gzip / zstd
   bool checksum = false;              // zstd
-  uint32_t elementsize = 4;           // shuffle
+  uint32_t elementsize = 4;           // shuffle; blosc typesize
+  std::string cname;                  // blosc compressor (decode reads the compressor from the header)
   std::vector<uint64_t> inner_shape;  // sharding
   std::shared_ptr<Chain> inner, index;
 };

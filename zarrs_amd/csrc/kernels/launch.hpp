@@ -64,4 +64,35 @@ hipError_t launch_zstd(ZgItem *items, uint32_t *status, uint32_t n_items, uint8_
 hipError_t launch_unshuffle(ZgItem *items, uint32_t *status, uint32_t n_items, uint8_t *dst, uint64_t slot_bytes,
                             uint32_t elementsize, hipStream_t s);
 
+// blosc (c-blosc 1.x frames): stream table built on the device, sized on the host from BlInfo
+enum : uint32_t { BL_COMP_LZ4 = 1, BL_COMP_ZSTD = 4, BL_COMP_MEMCPY = 0x100, BL_COMP_SKIP = 0xFFFFFFFFu };
+enum : uint32_t { BL_KIND_RAW = 0, BL_KIND_LZ4 = 1, BL_KIND_ZSTD = 4 };
+struct BlInfo {     // per item (read back)
+  uint32_t nsub;    // compressed streams
+  uint32_t nblk;    // blocks
+  uint32_t comp;    // BL_COMP_*
+  uint32_t max_ne;  // largest stream decoded size
+  uint32_t nbytes;  // decoded size
+  uint32_t ver;     // frame format version
+};
+struct BlBlock {
+  uint32_t item, bsize;
+  uint64_t out_off;  // in the item's decoded bytes
+  uint32_t first_sub, nsplit, ne, mode, ts, ver;  // mode 0 none, 1 byte unshuffle, 2 bitunshuffle
+};
+struct BlDecode {
+  const uint64_t *bases;  // per item {first stream, first block}
+  ZgItem *subs;
+  uint32_t *sub_status, *sub_kind;
+  BlBlock *blocks;
+  uint8_t *tmp;           // n_sub * sub_slot decoded streams
+  uint64_t sub_slot;
+  ZstdScratch zs;
+  uint64_t n_sub, n_blk, n_zstd, n_lz4;
+};
+hipError_t launch_blosc_info(const ZgItem *items, uint32_t *status, uint32_t n_items, uint64_t slot_bytes,
+                             BlInfo *info, hipStream_t s);
+hipError_t launch_blosc_decode(ZgItem *items, uint32_t *status, uint32_t n_items, const BlInfo *info,
+                               const BlDecode &D, uint8_t *dst, uint64_t slot_bytes, hipStream_t s);
+
 }  // namespace zgpu

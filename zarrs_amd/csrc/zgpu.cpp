@@ -130,7 +130,7 @@ struct zgpu_chain {
 // ------------------------------------------------------------------------------------------------
 // Plan
 // ------------------------------------------------------------------------------------------------
-enum StageKind { ST_CRC32C, ST_GZIP, ST_ZSTD, ST_UNSHUFFLE };
+enum StageKind { ST_CRC32C, ST_GZIP, ST_ZSTD, ST_UNSHUFFLE, ST_BLOSC };
 struct Stage {
   StageKind kind;
   int at_start = 0;
@@ -171,6 +171,23 @@ struct zgpu_plan {
   uint8_t *d_pool[2] = {nullptr, nullptr};
   uint2 *d_aux = nullptr;
   ZstdScratch zs{};  // block-parallel zstd scratch (allocated when the chain has zstd)
+  // blosc stage scratch (grown on demand; the stream table is sized from the frame headers)
+  struct Grow {
+    void *p = nullptr;
+    size_t n = 0;
+  };
+  Grow bl_info, bl_bases, bl_subs, bl_sub_status, bl_sub_kind, bl_blocks, bl_tmp, bl_zblks, bl_znblk, bl_zmode,
+      bl_zlit, bl_zseq;
+  uint8_t *bl_h = nullptr;  // pinned: BlInfo read-back, then the bases upload
+  size_t bl_h_n = 0;
+  void *grow(Grow &g, size_t bytes) {
+    if (g.n < bytes) {
+      ctx->dev_free(g.p);
+      g.p = ctx->dev_alloc(bytes);
+      g.n = bytes;
+    }
+    return g.p;
+  }
   unsigned long long *d_counter = nullptr;
   // control block: [counter (256 B) | per-item status (4 B each)], cleared by ONE memset and read
   // back by ONE D2H copy into pinned memory (h_ctl) per execute
@@ -186,6 +203,10 @@ struct zgpu_plan {
                     d_pool[0], d_pool[1], d_aux, zs.blks, zs.nblk, zs.mode, zs.lit, zs.seq, d_ctl,
                     d_enc_stage};
     for (void *b : bufs) ctx->dev_free(b);
+    for (Grow *g : {&bl_info, &bl_bases, &bl_subs, &bl_sub_status, &bl_sub_kind, &bl_blocks, &bl_tmp, &bl_zblks,
+                    &bl_znblk, &bl_zmode, &bl_zlit, &bl_zseq})
+      ctx->dev_free(g->p);
+    ctx->host_free(bl_h);
     ctx->host_free(h_ctl);
   }
 };
@@ -232,7 +253,10 @@ static void build_leaf_stages(zgpu_plan &P, const Chain &leaf, uint64_t nelem) {
       if (out_size < 0) break;
     }
     if (out_size < 0) throw ChainError{ZGPU_UNSUPPORTED, "a compressor nested inside another variable-size codec"};
-    s.kind = k.kind == CodecKind::Gzip ? ST_GZIP : k.kind == CodecKind::Zstd ? ST_ZSTD : ST_UNSHUFFLE;
+    s.kind = k.kind == CodecKind::Gzip    ? ST_GZIP
+             : k.kind == CodecKind::Zstd  ? ST_ZSTD
+             : k.kind == CodecKind::Blosc ? ST_BLOSC
+                                          : ST_UNSHUFFLE;
     s.elementsize = k.elementsize;
     s.pool = pool;
     pool ^= 1;
@@ -467,6 +491,62 @@ static void plan_upload(zgpu_plan &P, hipStream_t us = nullptr) {
   }
 }
 
+// blosc stage: frame headers -> (host read-back) stream table sizes -> streams + blocks on the device
+// -> zstd / lz4 stream decode -> per-block gather + unshuffle into the item slots. The read-back makes
+// this stage synchronous with the host (the only stage that is).
+static void blosc_stage(zgpu_plan &P, const Stage &st, hipStream_t s) {
+  zgpu_ctx &C = *P.ctx;
+  const uint32_t ni = (uint32_t)P.items.size();
+  uint8_t *dst = P.d_pool[st.pool];
+  BlInfo *info = (BlInfo *)P.grow(P.bl_info, ni * sizeof(BlInfo));
+  const size_t hbytes = std::max<size_t>(ni * sizeof(BlInfo), ni * 16);
+  if (P.bl_h_n < hbytes) {
+    C.host_free(P.bl_h);
+    P.bl_h = (uint8_t *)C.host_alloc(hbytes);
+    P.bl_h_n = hbytes;
+  }
+  HIPCHK(launch_blosc_info(P.d_items, P.d_status, ni, P.slot_bytes, info, s));
+  HIPCHK(hipMemcpyAsync(P.bl_h, info, ni * sizeof(BlInfo), hipMemcpyDeviceToHost, s));
+  HIPCHK(hipStreamSynchronize(s));
+  std::vector<BlInfo> hi(ni);
+  std::memcpy(hi.data(), P.bl_h, ni * sizeof(BlInfo));
+  BlDecode D{};
+  uint64_t *bases = (uint64_t *)P.bl_h;
+  uint64_t max_ne = 0;
+  for (uint32_t i = 0; i < ni; i++) {
+    bases[2 * i] = D.n_sub;
+    bases[2 * i + 1] = D.n_blk;
+    if (hi[i].comp == BL_COMP_SKIP) continue;
+    D.n_sub += hi[i].nsub;
+    D.n_blk += hi[i].nblk;
+    if (hi[i].comp == BL_COMP_ZSTD) D.n_zstd += hi[i].nsub;
+    if (hi[i].comp == BL_COMP_LZ4) D.n_lz4 += hi[i].nsub;
+    max_ne = std::max<uint64_t>(max_ne, hi[i].max_ne);
+  }
+  uint64_t *d_bases = (uint64_t *)P.grow(P.bl_bases, ni * 16);
+  HIPCHK(hipMemcpyAsync(d_bases, bases, ni * 16, hipMemcpyHostToDevice, s));
+  D.bases = d_bases;
+  const uint64_t ns = std::max<uint64_t>(D.n_sub, 1);
+  D.subs = (ZgItem *)P.grow(P.bl_subs, ns * sizeof(ZgItem));
+  D.sub_status = (uint32_t *)P.grow(P.bl_sub_status, ns * 4);
+  D.sub_kind = (uint32_t *)P.grow(P.bl_sub_kind, ns * 4);
+  D.blocks = (BlBlock *)P.grow(P.bl_blocks, std::max<uint64_t>(D.n_blk, 1) * sizeof(BlBlock));
+  if (D.n_zstd + D.n_lz4) {
+    D.sub_slot = (max_ne + 255) & ~(uint64_t)255;
+    D.tmp = (uint8_t *)P.grow(P.bl_tmp, D.n_sub * D.sub_slot);
+  }
+  if (D.n_zstd) {
+    uint64_t blk_bytes;
+    zstd_scratch_layout(D.sub_slot, D.zs.blk_cap, blk_bytes, D.zs.lit_stride, D.zs.seq_cap);
+    D.zs.blks = P.grow(P.bl_zblks, D.n_sub * (uint64_t)D.zs.blk_cap * blk_bytes);
+    D.zs.nblk = (uint32_t *)P.grow(P.bl_znblk, D.n_sub * 4);
+    D.zs.mode = (uint32_t *)P.grow(P.bl_zmode, D.n_sub * 4);
+    D.zs.lit = (uint8_t *)P.grow(P.bl_zlit, D.n_sub * D.zs.lit_stride);
+    D.zs.seq = (uint32_t *)P.grow(P.bl_zseq, D.n_sub * D.zs.seq_cap * 12);
+  }
+  HIPCHK(launch_blosc_decode(P.d_items, P.d_status, ni, info, D, dst, P.slot_bytes, s));
+}
+
 // Enqueue the decode of an uploaded plan on stream s.
 static void plan_enqueue(zgpu_plan &P, uint8_t *out, hipStream_t s) {
   const uint32_t ni = (uint32_t)P.items.size();
@@ -493,6 +573,9 @@ static void plan_enqueue(zgpu_plan &P, uint8_t *out, hipStream_t s) {
         break;
       case ST_ZSTD:
         HIPCHK(launch_zstd(P.d_items, P.d_status, ni, P.d_pool[st.pool], P.slot_bytes, P.zs, s));
+        break;
+      case ST_BLOSC:
+        blosc_stage(P, st, s);
         break;
       case ST_UNSHUFFLE:
         HIPCHK(launch_unshuffle(P.d_items, P.d_status, ni, P.d_pool[st.pool], P.slot_bytes, st.elementsize, s));
