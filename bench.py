@@ -522,7 +522,109 @@ class C5:
         return None
 
 
-WORKLOADS = {"c2": C2, "c3": C3, "c5": C5}
+# ------------------------------------------------------------------------------------------------
+# blosc
+# ------------------------------------------------------------------------------------------------
+class Blosc:
+    """u16 microscopy-style volume [256,1024,1024], chunks [64,256,256] (64 chunks of 8 MiB), codecs
+    [bytes, blosc{lz4, clevel 5, shuffle, typesize 2}] -- numcodecs' Blosc defaults, the most common
+    compressor in existing OME-Zarr data. Chunks encoded on the host by c-blosc 1.21 (the oracle's
+    library), decoded on the GPU from HBM; per-rank chunk partition, no collective."""
+    SHAPE, CHUNK = [256, 1024, 1024], [64, 256, 256]
+    CNAME = "lz4"
+    kernel = "k_lz4"
+    dtype = "u16"
+
+    def codecs(self):
+        return [{"name": "bytes", "configuration": {"endian": "little"}},
+                {"name": "blosc", "configuration": {"cname": self.CNAME, "clevel": 5, "shuffle": "shuffle",
+                                                    "typesize": 2, "blocksize": 0}}]
+
+    def __init__(self, args, rank, world, dev):
+        from concurrent.futures import ThreadPoolExecutor
+        from zarrs_amd import CodecChain, make_desc
+        sys.path.insert(0, os.path.join(ROOT, "oracle"))
+        import oracle as O
+        self.args, self.rank, self.world, self.dev = args, rank, world, dev
+        shape, cs = self.SHAPE, self.CHUNK
+        g = torch.Generator(device=dev)
+        g.manual_seed(42 + rank)
+        z, y, x = (torch.arange(n, device=dev, dtype=torch.float32) for n in shape)
+        img = 100 + 900 * (torch.sin(z[:, None, None] * 0.05) * torch.cos(y[None, :, None] * 0.013)
+                           * torch.sin(x[None, None, :] * 0.021)).abs()
+        img = img + torch.randn(shape, generator=g, device=dev) * img.sqrt()
+        self.dec_ref = img.clamp(0, 65535).to(torch.int32).to(torch.uint16)
+        host = self.dec_ref.cpu().numpy()
+        grid = [s_ // c for s_, c in zip(shape, cs)]
+        idxs = list(np.ndindex(*grid))
+        co = O.OracleChain.from_metadata(self.codecs(), "uint16", 0, 3)
+
+        def enc(idx):
+            sl = tuple(slice(i * c, (i + 1) * c) for i, c in zip(idx, cs))
+            return co.encode(np.ascontiguousarray(host[sl]))
+        with ThreadPoolExecutor(_threads()) as ex:
+            self.enc_host = list(ex.map(enc, idxs))
+        self.host = host
+        self.idxs = idxs
+        self.chain = CodecChain.from_metadata(self.codecs(), "uint16", 0, args.ctx)
+        self.enc_bufs, descs = [], []
+        for idx, e in zip(idxs, self.enc_host):
+            t = torch.frombuffer(bytearray(e), dtype=torch.uint8).to(dev)
+            self.enc_bufs.append(t)
+            descs.append(make_desc((t.data_ptr(), len(e)), cs, out_start=[i * c for i, c in zip(idx, cs)]))
+        self.out = torch.empty(shape, dtype=torch.uint16, device=dev)
+        self.parts = [(self.chain, descs, self.out, shape)]
+        self.decoded_bytes = int(np.prod(shape)) * 2
+        self.step_bytes = self.decoded_bytes * world
+        enc_total = sum(len(e) for e in self.enc_host)
+        self.config = {"workload": f"blosc: u16 volume {shape} per GPU, chunks {cs}, [bytes, blosc{{{self.CNAME}, "
+                                   "clevel 5, shuffle, typesize 2, blocksize auto}] (numcodecs Blosc defaults)",
+                       "chunks_per_gpu": len(idxs), "blosc_ratio": round(self.decoded_bytes / enc_total, 3),
+                       "parallelism": f"chunk-partitioned x{world}"}
+        self.data = ("synthetic (100 + 900|sin z cos y sin x| + sqrt-scaled N(0,1) noise, u16, seed 42; "
+                     "encoded by c-blosc 1.21; decode(encode(x)) == x checked on device)")
+        self.scaling = "weak"
+
+    def after_decode(self):
+        pass
+
+    def check(self) -> bool:
+        return bool(torch.equal(self.out, self.dec_ref))
+
+    def cpu_baseline(self):
+        sys.path.insert(0, os.path.join(ROOT, "oracle"))
+        import oracle as O
+        threads = _threads()
+        chain = O.OracleChain.from_metadata(self.codecs(), "uint16", 0, 3)
+        grid = [s_ // c for s_, c in zip(self.SHAPE, self.CHUNK)]
+        n = int(np.prod(grid))
+        ptrs = (C.c_void_p * n)()
+        lens = (C.c_uint64 * n)()
+        bufs = [np.frombuffer(e, np.uint8) for e in self.enc_host]
+        for idx, b in zip(self.idxs, bufs):
+            lin = int(np.ravel_multi_index(idx, grid))
+            ptrs[lin], lens[lin] = b.ctypes.data, b.nbytes
+        out = np.empty(self.SHAPE, np.uint16)
+        O.retrieve_ptrs(chain, self.SHAPE, self.CHUNK, ptrs, lens, [0, 0, 0], self.SHAPE, out, threads)
+        assert np.array_equal(out, self.host)
+        times = _time_reps(lambda: O.retrieve_ptrs(chain, self.SHAPE, self.CHUNK, ptrs, lens, [0, 0, 0],
+                                                   self.SHAPE, out, threads), self.args.cpu_seconds)
+        t = float(np.median(times))
+        return {"value": round(out.nbytes / t / 2 ** 30, 3), "unit": "GiB/s", "cores": threads, "kind": "port",
+                "sample": f"the whole volume ({n} chunks), median of {len(times)} reps, oracle "
+                          f"retrieve_array_subset (c-blosc 1.21 blosc_decompress_ctx) with {threads} threads"}
+
+    def host_leg(self, sp):
+        return None
+
+
+class BloscZstd(Blosc):
+    """Same volume, blosc{zstd, clevel 5, shuffle}: zarr-python 3's BloscCodec default compressor."""
+    CNAME = "zstd"
+    kernel = "k_zstd_exec_item"
+
+
+WORKLOADS = {"c2": C2, "c3": C3, "c5": C5, "blosc": Blosc, "blosc-zstd": BloscZstd}
 
 
 def _time_reps(fn, seconds):

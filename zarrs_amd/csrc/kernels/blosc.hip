@@ -196,11 +196,14 @@ __global__ __launch_bounds__(64) void k_lz4(ZgItem *subs, uint32_t *sub_status, 
     }
     ml += 4;
     if (op + ml > slot) { err = 1; break; }
-    __threadfence();  // the match reads bytes this wave just stored (agent-scope acquire: fresh lines)
+    // the match reads bytes this wave just stored: wait for the stores (workgroup scope = this CU's
+    // L1, which the wave's own write-through stores keep coherent; an agent-scope fence would write
+    // back / invalidate L2 across XCDs every sequence)
+    __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "workgroup");
     const uint8_t *src = out + op - off;
     for (uint64_t i = lane; i < ml; i += 64) out[op + i] = src[off >= ml ? i : i % off];
     op += ml;
-    __threadfence();
+    __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "workgroup");
   }
   if (lane == 0) {
     sub_status[s] = err ? ZG_CORRUPT_STREAM : 0u;
