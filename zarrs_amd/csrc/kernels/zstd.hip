@@ -22,6 +22,8 @@
 #include "../common.hpp"
 #include "launch.hpp"
 
+#include <cstdlib>
+
 namespace zgpu {
 
 #ifdef ZG_PROFILE
@@ -1403,9 +1405,11 @@ __global__ __launch_bounds__(64) void k_zstd_blocks(const ZgItem *items, uint32_
   const int lane = lane_id();
   const uint64_t total = (uint64_t)n_items * blk_cap;
   for (uint64_t g = blockIdx.x; g < total; g += gridDim.x) {
-    const uint32_t item = (uint32_t)(g / blk_cap), bi = (uint32_t)(g % blk_cap);
+    // block-major record order: block bi of every item before block bi+1 of any, so that items
+    // with few blocks (many small frames, e.g. blosc streams) spread over all workgroups
+    const uint32_t item = (uint32_t)(g % n_items), bi = (uint32_t)(g / n_items);
     if (bi >= nblk[item] || zmode[item] != ZMODE_PARALLEL) continue;
-    ZBlk *Bp = blks + g;
+    ZBlk *Bp = blks + (uint64_t)item * blk_cap + bi;
     const uint32_t flags = U(Bp->flags);
     if ((flags & 3) != ZB_CMP) continue;
     const ZgItem it = items[item];
@@ -1761,9 +1765,9 @@ __global__ __launch_bounds__(LIT_THREADS) void k_zstd_lits(const ZgItem *items, 
   const uint32_t t = threadIdx.x;
   const uint64_t total = (uint64_t)n_items * blk_cap;
   for (uint64_t g = blockIdx.x; g < total; g += gridDim.x) {
-    const uint32_t item = (uint32_t)(g / blk_cap), bi = (uint32_t)(g % blk_cap);
+    const uint32_t item = (uint32_t)(g % n_items), bi = (uint32_t)(g / n_items);  // block-major order
     if (bi >= nblk[item] || zmode[item] != ZMODE_PARALLEL) continue;
-    const ZBlk *Bp = blks + g;
+    const ZBlk *Bp = blks + (uint64_t)item * blk_cap + bi;
     const uint32_t flags = Bp->flags;
     const uint32_t ltype = (flags >> 2) & 3;
     if ((flags & 3) != ZB_CMP || ltype == 0) continue;
@@ -2538,9 +2542,9 @@ __global__ __launch_bounds__(256) void k_zstd_direct(const ZgItem *items, const 
   const uint64_t recs = (uint64_t)n_items * blk_cap;
   const uint32_t tid = threadIdx.x;
   for (uint64_t rec = blockIdx.x; rec < recs; rec += gridDim.x) {
-    const uint32_t item = (uint32_t)(rec / blk_cap), bi = (uint32_t)(rec % blk_cap);
+    const uint32_t item = (uint32_t)(rec % n_items), bi = (uint32_t)(rec / n_items);  // block-major order
     if (zmode[item] != ZMODE_PARALLEL || status[item] || bi >= nblk[item]) continue;
-    const ZBlk &b = blks[rec];
+    const ZBlk &b = blks[(uint64_t)item * blk_cap + bi];
     const uint32_t flags = b.flags, type = flags & 3, n = b.out_size;
     if (!x_direct_block(flags, b.nseq, n)) continue;
     if (type == ZB_CMP && b.regen != n) continue;  // corrupt: k_zstd_exec_item reports it
@@ -2825,8 +2829,17 @@ hipError_t launch_zstd(ZgItem *items, uint32_t *status, uint32_t n_items, uint8_
   hipLaunchKernelGGL(k_zstd_scan, dim3(n_items), dim3(64), 0, s, items, status, blks, Z.blk_cap, Z.nblk, Z.mode,
                      Z.lit_stride, Z.seq_cap);
   const uint64_t recs = (uint64_t)n_items * Z.blk_cap;
-  const uint32_t grid = (uint32_t)std::min<uint64_t>(recs, 256 * 16);
-  const uint32_t lgrid = (uint32_t)std::min<uint64_t>(recs, 256 * 2);
+  // grids of the record-strided entropy kernels (overridable for tuning: ZGPU_ZSTD_GRID, ZGPU_ZSTD_LGRID)
+  static const uint64_t g_cap = [] {
+    const char *e = std::getenv("ZGPU_ZSTD_GRID");
+    return e ? std::max<uint64_t>(1, std::strtoull(e, nullptr, 10)) : (uint64_t)256 * 16;
+  }();
+  static const uint64_t l_cap = [] {
+    const char *e = std::getenv("ZGPU_ZSTD_LGRID");
+    return e ? std::max<uint64_t>(1, std::strtoull(e, nullptr, 10)) : (uint64_t)256 * 2;
+  }();
+  const uint32_t grid = (uint32_t)std::min<uint64_t>(recs, g_cap);
+  const uint32_t lgrid = (uint32_t)std::min<uint64_t>(recs, l_cap);
   hipLaunchKernelGGL(k_zstd_lits, dim3(lgrid), dim3(LIT_THREADS), 0, s, items, status, blks, Z.blk_cap, Z.nblk,
                      Z.mode, n_items, Z.lit, Z.lit_stride);
   hipLaunchKernelGGL(k_zstd_blocks, dim3(grid), dim3(64), 0, s, items, status, blks, Z.blk_cap, Z.nblk, Z.mode,
