@@ -25,6 +25,7 @@
  *                          FilesystemStore::get / get_partial_many (zarrs_filesystem/src/lib.rs:
  *                          323-470) feeding array_read_ops_array.rs:290-300, with the reads of
  *                          one sub-batch overlapped with the H2D copy and decode of the previous.
+ *   zgpu_encode_batch   <- CodecChain::encode (codec_chain.rs:528-555), fixed-size chains
  *   status codes        <- CodecError variants (zarrs_codec/src/lib.rs:617-686), 1:1 (see below).
  *
  * Threading: every entry point is thread-safe; calls on one context are serialised internally
@@ -200,6 +201,28 @@ int zgpu_retrieve_array_subset_files(zgpu_chain *chain, uint32_t ndim, const uin
                                      const uint64_t *chunk_shape, const char *const *chunk_paths,
                                      const uint64_t *sel_start, const uint64_t *sel_shape, void *out,
                                      uint32_t flags, void *hip_stream);
+
+/*
+ * Write path: CodecChain::encode (zarrs/src/array/codec/array_to_bytes/
+ * codec_chain.rs:528-555) for fixed-size chains -- transpose, bytes (endianness), numcodecs.shuffle
+ * (innermost, elementsize = data type size), crc32c (end or start, any number). Compressing codecs
+ * and sharding return ZGPU_UNSUPPORTED.
+ * zgpu_chain_encoded_size: encoded bytes of one chunk of chunk_shape (BytesRepresentation::FixedSize),
+ * -1 if the chain's encoded size is not fixed.
+ * zgpu_encode_batch: encode the chunks whose origins are descs[i].chunk_start (in elements) of the
+ * device-resident C-order array (array_shape) into descs[i].dst (device memory, >= encoded size).
+ * Chunk regions past the array edge encode the fill value. flags must be
+ * ZGPU_ENC_DEVICE | ZGPU_OUT_DEVICE.
+ */
+typedef struct {
+  void *dst;
+  uint64_t dst_cap;
+  uint64_t chunk_start[ZGPU_MAX_DIMS];
+} zgpu_encode_desc;
+int64_t zgpu_chain_encoded_size(const zgpu_chain *chain, uint32_t ndim, const uint64_t *chunk_shape);
+int zgpu_encode_batch(zgpu_chain *chain, uint32_t ndim, const uint64_t *chunk_shape, const void *array,
+                      const uint64_t *array_shape, const zgpu_encode_desc *descs, uint64_t n, uint32_t flags,
+                      void *hip_stream);
 
 #ifdef __cplusplus
 }

@@ -33,6 +33,7 @@ EXPORTS = [
     "zgpu_chain_create", "zgpu_chain_destroy", "zgpu_chain_element_size", "zgpu_decode_batch",
     "zgpu_plan_create", "zgpu_plan_execute", "zgpu_plan_status", "zgpu_plan_destroy", "zgpu_plan_algorithmic_bytes",
     "zgpu_retrieve_array_subset", "zgpu_decode_files", "zgpu_retrieve_array_subset_files",
+    "zgpu_chain_encoded_size", "zgpu_encode_batch",
 ]
 
 
@@ -49,6 +50,10 @@ class ChunkDesc(C.Structure):
 
 class FileRange(C.Structure):
     _fields_ = [("path", C.c_char_p), ("offset", C.c_uint64), ("len", C.c_uint64)]
+
+
+class EncodeDesc(C.Structure):
+    _fields_ = [("dst", C.c_void_p), ("dst_cap", C.c_uint64), ("chunk_start", C.c_uint64 * MAX_DIMS)]
 
 
 class ZgpuError(RuntimeError):
@@ -98,6 +103,9 @@ def load() -> C.CDLL:
                                     u32, C.POINTER(C.c_int32), vp]
     L.zgpu_retrieve_array_subset_files.argtypes = [vp, u32, P64, P64, C.POINTER(C.c_char_p), P64, P64,
                                                    vp, u32, vp]
+    L.zgpu_chain_encoded_size.restype = C.c_int64
+    L.zgpu_chain_encoded_size.argtypes = [vp, u32, P64]
+    L.zgpu_encode_batch.argtypes = [vp, u32, P64, vp, P64, C.POINTER(EncodeDesc), u64, u32, vp]
     _lib = L
     return L
 

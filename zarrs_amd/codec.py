@@ -170,6 +170,32 @@ class CodecChain:
         dev = _ptr_len(encoded)[2]
         self.decode_batch([make_desc(encoded, shape, out_start=out_start)], out, list(out.shape), dev)
 
+    def encoded_size(self, chunk_shape) -> int:
+        """Encoded bytes of one chunk (fixed-size chains), -1 if variable (zgpu_chain_encoded_size)."""
+        return int(L.load().zgpu_chain_encoded_size(self._h, len(chunk_shape), L.u64s(chunk_shape)))
+
+    def encode_chunks(self, array, chunk_shape, chunk_starts, stream=None) -> list:
+        """CodecChain::encode of the chunks of a device-resident torch array whose origins are
+        chunk_starts (zgpu_encode_batch). Returns one uint8 device tensor per chunk."""
+        import torch
+        assert array.is_cuda and array.is_contiguous()
+        size = self.encoded_size(chunk_shape)
+        if size < 0:
+            raise L.ZgpuError(L.UNSUPPORTED, "encode: the chain's encoded size is not fixed")
+        n = len(chunk_starts)
+        flat = torch.empty(max(n, 1) * ((size + 255) // 256 * 256), dtype=torch.uint8, device=array.device)
+        pitch = (size + 255) // 256 * 256
+        descs = (L.EncodeDesc * max(n, 1))()
+        for i, st in enumerate(chunk_starts):
+            descs[i].dst = flat.data_ptr() + i * pitch
+            descs[i].dst_cap = size
+            for d, v in enumerate(st):
+                descs[i].chunk_start[d] = int(v)
+        rc = L.load().zgpu_encode_batch(self._h, len(chunk_shape), L.u64s(chunk_shape), array.data_ptr(),
+                                       L.u64s(list(array.shape)), descs, n, L.ENC_DEVICE | L.OUT_DEVICE, stream)
+        L.check(rc)
+        return [flat[i * pitch:i * pitch + size] for i in range(n)]
+
     def partial_decode(self, encoded, shape, subset_start, subset_shape) -> np.ndarray:
         out = np.empty([int(s) for s in subset_shape], dtype=self.dtype)
         dev = _ptr_len(encoded)[2]

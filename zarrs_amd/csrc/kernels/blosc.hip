@@ -160,7 +160,7 @@ __global__ __launch_bounds__(64) void k_lz4(ZgItem *subs, uint32_t *sub_status, 
   const uint8_t *in = (const uint8_t *)it.src;
   const uint64_t cs = it.len;
   uint8_t *out = dst + (uint64_t)s * slot;
-  uint64_t ip = 0, op = 0;
+  uint64_t ip = 0, op = 0, safe = 0;
   uint32_t err = 0;
   for (;;) {
     if (ip >= cs) { err = 1; break; }
@@ -196,14 +196,17 @@ __global__ __launch_bounds__(64) void k_lz4(ZgItem *subs, uint32_t *sub_status, 
     }
     ml += 4;
     if (op + ml > slot) { err = 1; break; }
-    // the match reads bytes this wave just stored: wait for the stores (workgroup scope = this CU's
-    // L1, which the wave's own write-through stores keep coherent; an agent-scope fence would write
-    // back / invalidate L2 across XCDs every sequence)
-    __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "workgroup");
+    // the match may read bytes this wave stored since its last wait: wait for the stores first
+    // (workgroup scope = this CU's L1, which the wave's own write-through stores keep coherent; an
+    // agent-scope fence would write back / invalidate L2 across XCDs). Bytes below `safe` are known
+    // complete, so far-back sources (the common case) need no wait at all.
+    if (op - off + (off < ml ? off : ml) > safe) {
+      __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "workgroup");
+      safe = op;
+    }
     const uint8_t *src = out + op - off;
     for (uint64_t i = lane; i < ml; i += 64) out[op + i] = src[off >= ml ? i : i % off];
     op += ml;
-    __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "workgroup");
   }
   if (lane == 0) {
     sub_status[s] = err ? ZG_CORRUPT_STREAM : 0u;

@@ -298,4 +298,29 @@ hipError_t launch_item_resolve(ZgItem *items, uint32_t *status, uint32_t n_items
   return hipGetLastError();
 }
 
+
+// ------------------------------- crc32c encode (write path) -----------------------------------
+// CodecChain::encode of a crc32c codec (crc32c_codec.rs:88-106): checksum of the bytes so far,
+// 4 bytes LE appended (End) or prepended (Start). Chunk c's bytes are dsts[c] + [lo, lo + len).
+__global__ __launch_bounds__(CRC_THREADS) void k_crc32c_encode(const uint64_t *dsts, uint64_t lo, uint64_t len,
+                                                               int at_start) {
+  __shared__ CrcTables T;
+  __shared__ uint64_t s_len[CRC_THREADS / 64];
+  __shared__ uint32_t s_crc[CRC_THREADS / 64];
+  uint8_t *p = (uint8_t *)dsts[blockIdx.x] + lo;
+  build_tables(T, POLY_CRC32C);
+  const uint32_t c = wg_crc(p, len, T, POLY_CRC32C, s_len, s_crc);
+  if (threadIdx.x < 4) {
+    uint8_t *w = at_start ? p - 4 : p + len;
+    w[threadIdx.x] = (uint8_t)(c >> (8 * threadIdx.x));
+  }
+}
+
+hipError_t launch_crc32c_encode(const uint64_t *dsts, uint32_t n, uint64_t lo, uint64_t len, int at_start,
+                                hipStream_t s) {
+  if (!n) return hipSuccess;
+  hipLaunchKernelGGL(k_crc32c_encode, dim3(n), dim3(CRC_THREADS), 0, s, dsts, lo, len, at_start);
+  return hipGetLastError();
+}
+
 }  // namespace zgpu

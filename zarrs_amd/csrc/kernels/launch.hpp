@@ -64,6 +64,22 @@ hipError_t launch_zstd(ZgItem *items, uint32_t *status, uint32_t n_items, uint8_
 hipError_t launch_unshuffle(ZgItem *items, uint32_t *status, uint32_t n_items, uint8_t *dst, uint64_t slot_bytes,
                             uint32_t elementsize, hipStream_t s);
 
+// encode (write path): array -> encoded chunk layouts (transposes, endianness, innermost shuffle)
+struct ZgEncode {
+  uint32_t nd, es, comp, swap, shuffle, aligned;
+  uint64_t nelem;                    // elements per chunk
+  uint64_t data_off;                 // bytes before the data in each chunk (crc32c at start)
+  uint64_t enc_shape[ZG_MAXD];       // encoded (transposed) chunk shape
+  uint32_t dec_axis[ZG_MAXD];        // encoded axis a is decoded axis dec_axis[a]
+  uint64_t array_shape[ZG_MAXD];
+  uint64_t array_stride[ZG_MAXD];    // elements
+  uint8_t fill[16];
+};
+hipError_t launch_encode_gather(const uint64_t *dsts, const uint64_t *starts, const uint8_t *array,
+                                const ZgEncode &P, uint32_t n_chunks, hipStream_t s);
+hipError_t launch_crc32c_encode(const uint64_t *dsts, uint32_t n, uint64_t lo, uint64_t len, int at_start,
+                                hipStream_t s);
+
 // blosc (c-blosc 1.x frames): stream table built on the device, sized on the host from BlInfo
 enum : uint32_t { BL_COMP_LZ4 = 1, BL_COMP_ZSTD = 4, BL_COMP_MEMCPY = 0x100, BL_COMP_SKIP = 0xFFFFFFFFu };
 enum : uint32_t { BL_KIND_RAW = 0, BL_KIND_LZ4 = 1, BL_KIND_ZSTD = 4 };

@@ -1196,6 +1196,102 @@ int zgpu_decode_files(zgpu_chain *ch, uint32_t nd, const zgpu_chunk_desc *descs,
   ABI_GUARD_END
 }
 
+// Encoded size of one chunk for a fixed-size chain (BytesRepresentation::FixedSize), -1 if variable.
+int64_t zgpu_chain_encoded_size(const zgpu_chain *ch, uint32_t nd, const uint64_t *chunk_shape) {
+  if (!ch || !chunk_shape || nd == 0 || nd > ZGPU_MAX_DIMS) return -1;
+  uint64_t n = 1;
+  for (uint32_t d = 0; d < nd; d++) n *= chunk_shape[d];
+  return chain_fixed_encoded_size(*ch->chain, n);
+}
+
+// CodecChain::encode (codec_chain.rs:528-555) of n chunks of one device-resident C-order array into
+// device buffers: one gather (transposes + endianness + innermost shuffle, fill past the array edge),
+// then one k_crc32c_encode launch per crc32c codec.
+int zgpu_encode_batch(zgpu_chain *ch, uint32_t nd, const uint64_t *chunk_shape, const void *array,
+                      const uint64_t *array_shape, const zgpu_encode_desc *descs, uint64_t n, uint32_t flags,
+                      void *stream) {
+  ABI_GUARD_BEGIN
+  if (!ch || !chunk_shape || !array || !array_shape || (n && !descs))
+    return set_err(ZGPU_INVALID_ARGUMENT, "NULL argument");
+  if (nd == 0 || nd > ZGPU_MAX_DIMS) return set_err(ZGPU_INVALID_ARGUMENT, "ndim out of range");
+  if ((flags & (ZGPU_ENC_DEVICE | ZGPU_OUT_DEVICE)) != (ZGPU_ENC_DEVICE | ZGPU_OUT_DEVICE))
+    return set_err(ZGPU_INVALID_ARGUMENT, "encode: array and destinations must be device memory");
+  const Chain &c = *ch->chain;
+  if (c.a2b.kind != CodecKind::Bytes) return set_err(ZGPU_UNSUPPORTED, "encode: array->bytes codec must be bytes");
+  for (const Codec &k : c.a2a)
+    if (k.order.size() != nd) return set_err(ZGPU_INVALID_ARGUMENT, "transpose order rank != ndim");
+  bool shuffle = false;
+  int n_start = 0;
+  for (size_t i = 0; i < c.b2b.size(); i++) {
+    const Codec &k = c.b2b[i];
+    if (k.kind == CodecKind::Shuffle && i == 0 && k.elementsize == c.es) shuffle = true;
+    else if (k.kind == CodecKind::Crc32c) n_start += k.at_start ? 1 : 0;
+    else return set_err(ZGPU_UNSUPPORTED, "encode: only transpose / bytes / numcodecs.shuffle (innermost, "
+                                          "elementsize = data type size) / crc32c run on the GPU write path");
+  }
+  ZgEncode P{};
+  P.nd = nd;
+  P.es = c.es;
+  P.comp = c.comp;
+  P.swap = (c.a2b.big_endian && c.comp > 1) ? 1 : 0;
+  P.shuffle = shuffle;
+  P.nelem = 1;
+  for (uint32_t d = 0; d < nd; d++) P.nelem *= chunk_shape[d];
+  P.data_off = 4ull * n_start;
+  uint32_t m[ZG_MAXD];
+  composed_axes(c, nd, m);
+  uint64_t stride = 1;
+  for (int d = (int)nd - 1; d >= 0; d--) {
+    P.array_shape[d] = array_shape[d];
+    P.array_stride[d] = stride;
+    stride *= array_shape[d];
+  }
+  for (uint32_t a = 0; a < nd; a++) {
+    P.dec_axis[a] = m[a];
+    P.enc_shape[a] = chunk_shape[m[a]];
+  }
+  std::memcpy(P.fill, c.fill, sizeof(P.fill));
+  const int64_t enc_size = chain_fixed_encoded_size(c, P.nelem);
+  bool aligned = (P.data_off % c.es) == 0;
+  std::vector<uint64_t> h(n * (1 + nd));
+  for (uint64_t i = 0; i < n; i++) {
+    if (!descs[i].dst || descs[i].dst_cap < (uint64_t)enc_size)
+      return set_err(ZGPU_INVALID_ARGUMENT, "encode: destination missing or smaller than the encoded size");
+    for (uint32_t d = 0; d < nd; d++)
+      if (descs[i].chunk_start[d] >= array_shape[d])
+        return set_err(ZGPU_INVALID_ARGUMENT, "encode: chunk origin outside the array");
+    h[i] = (uint64_t)descs[i].dst;
+    if (h[i] % 16) aligned = false;
+    for (uint32_t d = 0; d < nd; d++) h[n + i * nd + d] = descs[i].chunk_start[d];
+  }
+  P.aligned = aligned;
+  zgpu_ctx *C = ch->ctx;
+  std::lock_guard<std::mutex> lk(C->mu);
+  HIPCHK(hipSetDevice(C->device));
+  hipStream_t s = pick_stream(C, stream);
+  if (!n) return ZGPU_OK;
+  uint64_t *d = (uint64_t *)C->dev_alloc(h.size() * 8);
+  try {
+    HIPCHK(hipMemcpyAsync(d, h.data(), h.size() * 8, hipMemcpyHostToDevice, s));
+    HIPCHK(launch_encode_gather(d, d + n, (const uint8_t *)array, P, (uint32_t)n, s));
+    uint64_t lo = P.data_off, len = P.nelem * c.es;
+    for (const Codec &k : c.b2b) {
+      if (k.kind != CodecKind::Crc32c) continue;
+      HIPCHK(launch_crc32c_encode(d, (uint32_t)n, lo, len, k.at_start ? 1 : 0, s));
+      if (k.at_start) lo -= 4;
+      len += 4;
+    }
+    HIPCHK(hipStreamSynchronize(s));
+  } catch (...) {
+    (void)hipStreamSynchronize(s);
+    C->dev_free(d);
+    throw;
+  }
+  C->dev_free(d);
+  return ZGPU_OK;
+  ABI_GUARD_END
+}
+
 int zgpu_retrieve_array_subset_files(zgpu_chain *ch, uint32_t nd, const uint64_t *array_shape,
                                      const uint64_t *chunk_shape, const char *const *chunk_paths,
                                      const uint64_t *sel_start, const uint64_t *sel_shape, void *out, uint32_t flags,
