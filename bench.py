@@ -179,6 +179,53 @@ class C2:
         res["host_enc_to_host_out_GiBps"] = round(self.decoded_bytes / t / 2 ** 30, 2)
         res["roundtrip_ok"] = ok and bool(torch.equal(h_out.view(torch.int32), self.dec_ref.cpu().view(torch.int32)))
         res.update(self.fs_leg(h_enc))
+        res["encode"] = self.encode_leg(sp)
+        return res
+
+    def encode_leg(self, sp):
+        """Write path: zgpu_encode_batch of the same 4096 chunks from the
+        decoded device array into chunk buffers (transpose [2,1,0] + big endian), checked byte for
+        byte against the bench's own encoding; the oracle's per-chunk encoder on the host beside it."""
+        from concurrent.futures import ThreadPoolExecutor
+        from zarrs_amd import _lib as L
+        lib = L.load()
+        K, grid = self.CHUNK, self.args.grid
+        dst = torch.empty_like(self.enc)
+        descs = (L.EncodeDesc * self.n_chunks)()
+        for c in range(self.n_chunks):
+            i, r = divmod(c, grid[1] * grid[2])
+            j, k = divmod(r, grid[2])
+            descs[c].dst = dst.data_ptr() + c * self.chunk_bytes
+            descs[c].dst_cap = self.chunk_bytes
+            descs[c].chunk_start[0], descs[c].chunk_start[1], descs[c].chunk_start[2] = i * K, j * K, k * K
+
+        def run():
+            L.check(lib.zgpu_encode_batch(self.chain._h, 3, L.u64s([K] * 3), self.dec_ref.data_ptr(),
+                                          L.u64s(self.shape), descs, self.n_chunks, L.ENC_DEVICE | L.OUT_DEVICE, sp))
+        run()
+        ok = bool(torch.equal(dst, self.enc))
+        reps = 10
+        t0 = time.perf_counter()
+        for _ in range(reps):
+            run()
+        t = (time.perf_counter() - t0) / reps
+        res = {"gpu_GiBps": round(self.decoded_bytes / t / 2 ** 30, 1), "ms": round(t * 1e3, 3),
+               "hbm_frac_incl_launch": round(2 * self.decoded_bytes / t / 1e9 / HBM_PEAK_GBS, 3),
+               "bytes_equal_to_reference_encoding": ok}
+        if self.args.no_cpu:
+            return res
+        sys.path.insert(0, os.path.join(ROOT, "oracle"))
+        import oracle as O
+        co = O.OracleChain.from_metadata(self.CODECS, "float32", 0.0, 3)
+        host = self.dec_ref[:8 * K].cpu().numpy()  # 8 x 16 x 16 = 2048 chunk sample
+        blocks = [np.ascontiguousarray(host[i * K:(i + 1) * K, j * K:(j + 1) * K, k * K:(k + 1) * K])
+                  for i in range(8) for j in range(grid[1]) for k in range(grid[2])][:512]
+        with ThreadPoolExecutor(_threads()) as ex:
+            list(ex.map(co.encode, blocks))
+            times = _time_reps(lambda: list(ex.map(co.encode, blocks)), 3.0)
+        tc = float(np.median(times))
+        res["cpu_oracle_GiBps"] = round(len(blocks) * self.chunk_bytes / tc / 2 ** 30, 2)
+        res["cpu_cores"] = _threads()
         return res
 
     def fs_leg(self, h_enc):
