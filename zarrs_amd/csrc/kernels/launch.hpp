@@ -73,6 +73,8 @@ struct ZgEncode {
   uint32_t dec_axis[ZG_MAXD];        // encoded axis a is decoded axis dec_axis[a]
   uint64_t array_shape[ZG_MAXD];
   uint64_t array_stride[ZG_MAXD];    // elements
+  uint64_t dec_shape[ZG_MAXD];       // chunk shape (decoded axes)
+  uint64_t enc_stride_of_dec[ZG_MAXD];  // encoded linear stride (elements) of each decoded axis
   uint8_t fill[16];
 };
 hipError_t launch_encode_gather(const uint64_t *dsts, const uint64_t *starts, const uint8_t *array,

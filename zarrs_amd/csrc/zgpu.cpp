@@ -1250,6 +1250,14 @@ int zgpu_encode_batch(zgpu_chain *ch, uint32_t nd, const uint64_t *chunk_shape, 
     P.dec_axis[a] = m[a];
     P.enc_shape[a] = chunk_shape[m[a]];
   }
+  {
+    uint64_t es_ = 1;
+    for (int a = (int)nd - 1; a >= 0; a--) {
+      P.enc_stride_of_dec[m[a]] = es_;
+      es_ *= P.enc_shape[a];
+    }
+    for (uint32_t d = 0; d < nd; d++) P.dec_shape[d] = chunk_shape[d];
+  }
   std::memcpy(P.fill, c.fill, sizeof(P.fill));
   const int64_t enc_size = chain_fixed_encoded_size(c, P.nelem);
   bool aligned = (P.data_off % c.es) == 0;
