@@ -37,6 +37,7 @@ sys.path.insert(0, ROOT)
 import numpy as np  # noqa: E402
 import torch  # noqa: E402
 
+L_CTR_ZSTD_SERIAL, L_CTR_ZSTD_PARALLEL = 1, 2  # zgpu.h ZGPU_CTR_*
 HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec, /opt/skills/guides/MI355X_MICROARCH.md
 METRIC = "decoded-array GiB/s, device-resident chunks, 1/2/4/8 MI355X; % HBM roofline"
 
@@ -705,6 +706,8 @@ def run_gpu(args, rank, world, dev):
         plans.append((plan, out, (C.c_int32 * n)()))
     # stream lanes: lists of plans executed in order on one stream; lanes run concurrently
     lanes = getattr(W, "lanes", [[i] for i in range(len(W.parts))])
+    if args.serial_lanes:  # profiling: every plan on one stream, so kernel durations do not overlap
+        lanes = [[i for ln in lanes for i in ln]]
     lanes = [[part_plan[i] for i in ln if i in part_plan] for ln in lanes]
     lanes = [ln for ln in lanes if ln]
     # the library launches on this stream; events are recorded on it. Independent parts (pyramid
@@ -784,6 +787,11 @@ def run_gpu(args, rank, world, dev):
     torch.cuda.synchronize()
     ev_ms = ev0.elapsed_time(ev1) / args.steps
     alg_bytes = sum(lib.zgpu_plan_algorithmic_bytes(plan) for plan, _, _ in plans)
+    counters = [0] * L.N_COUNTERS
+    for plan, _, _ in plans:  # device counters of each plan's last execute (statuses read in step())
+        buf = (C.c_uint64 * L.N_COUNTERS)()
+        lib.zgpu_plan_counters(plan, buf, L.N_COUNTERS)
+        counters = [a + b for a, b in zip(counters, buf)]
     # host planning + upload included (zgpu_decode_batch form), for DESIGN.md
     t1 = time.perf_counter()
     reps = max(1, min(5, args.steps))
@@ -796,7 +804,8 @@ def run_gpu(args, rank, world, dev):
     for plan, _, _ in plans:
         lib.zgpu_plan_destroy(plan)
     host = W.host_leg(sp) if (args.host_leg and rank == 0) else None
-    return dict(W=W, elapsed=elapsed, ev_ms=ev_ms, alg_bytes=alg_bytes, ok=ok, batch_ms=batch_ms, host=host)
+    return dict(W=W, elapsed=elapsed, ev_ms=ev_ms, alg_bytes=alg_bytes, ok=ok, batch_ms=batch_ms, host=host,
+                counters=counters)
 
 
 def pmc_traffic(args, kernel):
@@ -853,6 +862,8 @@ def main():
     ap.add_argument("--no-cpu", action="store_true")
     ap.add_argument("--lane-times", action="store_true", help="print each stream lane's solo time (stderr)")
     ap.add_argument("--no-pmc", action="store_true", help="skip the rocprofv3 PMC traffic passes")
+    ap.add_argument("--serial-lanes", action="store_true",
+                    help="run every plan on one stream (profiling: per-kernel durations without overlap)")
     ap.add_argument("--no-host-leg", dest="host_leg", action="store_false",
                     help="skip the PCIe-inclusive (host input/output) leg")
     ap.add_argument("--child", action="store_true", help=argparse.SUPPRESS)
@@ -900,6 +911,9 @@ def main():
             "decode_batch_ms_incl_host_planning": round(r["batch_ms"], 3),
             "host_leg": r["host"],
         }
+        if r["counters"][L_CTR_ZSTD_SERIAL] or r["counters"][L_CTR_ZSTD_PARALLEL]:
+            line["zstd_items_per_step"] = {"block_parallel": r["counters"][L_CTR_ZSTD_PARALLEL],
+                                           "serial_fallback": r["counters"][L_CTR_ZSTD_SERIAL]}
         print(json.dumps(line), flush=True)
     if world > 1:
         torch.distributed.destroy_process_group()

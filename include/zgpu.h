@@ -30,6 +30,9 @@
  *
  * Threading: every entry point is thread-safe; calls on one context are serialised internally
  * (they share the context's device scratch), calls on different contexts run concurrently.
+ * Stream ordering: a call runs on the caller's hip_stream (device inputs/outputs must be ready in
+ * that stream's order), or with hip_stream NULL on the context's own stream, which first waits for
+ * all work queued so far on the legacy default stream.
  * Memory: the caller owns every encoded input and the output; the library owns its scratch.
  */
 #ifndef ZGPU_H
@@ -155,6 +158,23 @@ void zgpu_plan_destroy(zgpu_plan *plan);
 /* Algorithmic HBM bytes of one execute (encoded bytes read + index bytes + decoded bytes
  * written), the figure bench.py prices the roofline with. */
 uint64_t zgpu_plan_algorithmic_bytes(const zgpu_plan *plan);
+
+/* Device counters of a plan's last execute (after its statuses were read) or of the calling
+ * thread's last decode call (zgpu_decode_batch / zgpu_decode_files / zgpu_retrieve_*), summed over
+ * its sub-batches. Writes min(n, ZGPU_N_COUNTERS) values, returns how many were written. */
+#define ZGPU_CTR_ENC_BYTES 0     /* encoded bytes read (resolved inner-chunk ranges of sharded items) */
+#define ZGPU_CTR_ZSTD_SERIAL 1   /* zstd items decoded by the serial one-wave fallback decoder     */
+#define ZGPU_CTR_ZSTD_PARALLEL 2 /* zstd items decoded by the block-parallel pipeline              */
+#define ZGPU_N_COUNTERS 3
+uint32_t zgpu_plan_counters(const zgpu_plan *plan, uint64_t *out, uint32_t n);
+uint32_t zgpu_last_counters(uint64_t *out, uint32_t n);
+
+/* Detail of the calling thread's last call that returned ZGPU_DECODED_SIZE_MISMATCH, for
+ * CodecError::UnexpectedChunkDecodedSize(InvalidBytesLengthError::new(len, expected_len))
+ * (zarrs_codec/src/lib.rs:491-501,632): the failing descriptor, the decoded length the final stage
+ * saw and the expected length of the (inner) chunk. len == UINT64_MAX: a decompressor produced more
+ * than expected_len bytes and stopped (its total is not known). Returns 1 if a detail is available. */
+int zgpu_last_size_mismatch(uint64_t *desc, uint64_t *len, uint64_t *expected_len);
 
 /*
  * Array::retrieve_array_subset_into over a regular chunk grid. chunk_ptrs/chunk_lens are

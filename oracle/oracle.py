@@ -123,22 +123,49 @@ class OracleChain:
             _lib.orc_chain_free(self._h)
             self._h = None
 
+    A2A = ("transpose",)
+    A2B = ("bytes", "endian", "sharding_indexed")
+    B2B = ("crc32c", "numcodecs.crc32c", "gzip", "zstd", "numcodecs.zstd", "blosc", "numcodecs.blosc",
+           "numcodecs.shuffle", "shuffle")
+
+    @staticmethod
+    def _sorted(codecs):
+        """CodecChain::from_metadata (codec_chain.rs:192-229): entries sorted by kind (array->array,
+        array->bytes, bytes->bytes; metadata order within a kind); an entry whose codec cannot be
+        created is skipped if it has "must_understand": false (:197-206). Codec names this restatement
+        does not know are the "cannot be created" case."""
+        a2a, a2b, b2b = [], [], []
+        for m in codecs:
+            if isinstance(m, str):
+                m = {"name": m}
+            name = m["name"]
+            if name in OracleChain.A2A:
+                a2a.append(m)
+            elif name in OracleChain.A2B:
+                a2b.append(m)
+            elif name in OracleChain.B2B:
+                b2b.append(m)
+            elif m.get("must_understand", True):
+                raise OracleError(6, f"codec {name}")
+        if len(a2b) != 1:
+            raise OracleError(10, "exactly one array->bytes codec")
+        return a2a + a2b + b2b
+
     @staticmethod
     def _build(codecs, data_type: str, fill: bytes, ndim: int):
         L = lib()
         np_dt, comp = DTYPES[data_type]
         es = np.dtype(np_dt).itemsize
+        codecs = OracleChain._sorted(codecs)
         h = L.orc_chain_new(es, comp, fill)
         if not h:
             raise OracleError(10, "bad data type")
         for m in codecs:
-            if isinstance(m, str):
-                m = {"name": m}
             name, cfg = m["name"], m.get("configuration", {}) or {}
             if name == "transpose":
                 order = cfg["order"]
                 st = L.orc_chain_add_transpose(h, len(order), (C.c_uint32 * len(order))(*order))
-            elif name == "bytes":
+            elif name in ("bytes", "endian"):
                 st = L.orc_chain_add_bytes(h, 1 if cfg.get("endian", "little") == "big" else 0)
             elif name == "sharding_indexed":
                 inner_shape = cfg["chunk_shape"]
@@ -152,9 +179,9 @@ class OracleChain:
                 st = L.orc_chain_add_crc32c(h, 1 if cfg.get("location", "end") == "start" else 0)
             elif name == "gzip":
                 st = L.orc_chain_add_gzip(h, int(cfg.get("level", 5)))
-            elif name == "zstd":
+            elif name in ("zstd", "numcodecs.zstd"):
                 st = L.orc_chain_add_zstd(h, int(cfg.get("level", 0)), 1 if cfg.get("checksum") else 0)
-            elif name == "blosc":
+            elif name in ("blosc", "numcodecs.blosc"):
                 sh = {"noshuffle": 0, "shuffle": 1, "bitshuffle": 2}[cfg.get("shuffle", "noshuffle")]
                 st = L.orc_chain_add_blosc(h, cfg.get("cname", "lz4").encode(), int(cfg.get("clevel", 5)), sh,
                                            int(cfg.get("typesize") or 0), int(cfg.get("blocksize") or 0))

@@ -34,8 +34,8 @@ def add(name, codecs, data_type, shape, enc: bytes, dec: np.ndarray | None, stat
     cases.append(dict(name=name, codecs=codecs, data_type=data_type, shape=list(shape), status=status,
                       fill_value=fill, sel=sel))
     # self-check against the oracle
-    ch = O.OracleChain.from_metadata(codecs, data_type, fill, len(shape))
     try:
+        ch = O.OracleChain.from_metadata(codecs, data_type, fill, len(shape))
         if sel is None:
             got = ch.decode(enc, shape)
         else:
@@ -203,6 +203,18 @@ add("gzip_bad_trailer", [BYTES_LE, {"name": "gzip", "configuration": {"level": 6
 add("shuffle_len", [BYTES_LE, {"name": "numcodecs.shuffle", "configuration": {"elementsize": 4}}],
     "uint16", [3], b"\x00" * 6, None, status=9)
 add("size_mismatch", [BYTES_LE], "float32", [4], b"\x00" * 12, None, status=2)
+
+# 7. CodecChain::from_metadata (codec_chain.rs:192-229): a codec that cannot be created is skipped when
+# "must_understand": false, an error otherwise; entries are sorted by kind, not by position
+dec = np.arange(50, dtype=np.uint16) * 3
+raw = dec.tobytes()
+crc_enc = raw + O.crc32c(raw).to_bytes(4, "little")
+add("must_understand_false_skipped",
+    [BYTES_LE, {"name": "example.unknown_codec", "configuration": {"x": 1}, "must_understand": False},
+     {"name": "crc32c"}], "uint16", [50], crc_enc, dec)
+add("must_understand_default_true", [BYTES_LE, {"name": "example.unknown_codec"}], "uint16", [50], raw, None,
+    status=6)
+add("codecs_sorted_by_kind", [{"name": "crc32c"}, BYTES_LE], "uint16", [50], crc_enc, dec)
 
 if __name__ == "__main__":
     np.savez_compressed(os.path.join(HERE, "synthetic.npz"), **arrays)

@@ -1,6 +1,8 @@
-"""N>1 read path on CPU (gloo, world_size 2): slab partition + gather assemble exactly the subset
-rank 0 would have read alone; LPT partition is balanced and deterministic. The per-rank decode is
-a numpy stand-in here (the GPU decode itself is covered by the -m gpu parity tests)."""
+"""N>1 read path on CPU (gloo, world_size 2 and 3): slab partition + gather assemble exactly the
+subset rank 0 would have read alone (the root's slab decoded in place, peers received straight into
+their rows); the C5 pattern (chunks LPT-partitioned by encoded size, one cross-rank subset gathered)
+on zstd-shuffle chunks; gathers inside a process subgroup. The per-rank decode is the CPU oracle
+(the GPU decode itself is covered by the -m gpu parity tests)."""
 import os
 import socket
 
@@ -10,19 +12,40 @@ import torch
 import torch.distributed as dist
 import torch.multiprocessing as mp
 
-from zarrs_amd.distributed import (gather_slabs, lpt_partition, retrieve_array_subset_distributed,
-                                   slab_partition)
+import oracle as O
+from zarrs_amd.distributed import (chunk_boxes, gather_regions, gather_slabs, lpt_partition,
+                                   retrieve_array_subset_distributed, slab_partition)
+
+CODECS = [{"name": "bytes", "configuration": {"endian": "little"}}, {"name": "crc32c"}]
+C5_CODECS = [{"name": "bytes", "configuration": {"endian": "little"}},
+             {"name": "numcodecs.shuffle", "configuration": {"elementsize": 2}},
+             {"name": "zstd", "configuration": {"level": 3, "checksum": False}}]
 
 
-class FakeArray:
-    """retrieve_array_subset_into over an in-memory reference array (decode stand-in)."""
-    def __init__(self, a):
-        self.a = a
+def _encode_grid(co, a, cs):
+    chunks = {}
+    for idx in np.ndindex(*[-(-s // c) for s, c in zip(a.shape, cs)]):
+        blk = np.zeros(cs, a.dtype)
+        sl = tuple(slice(i * c, min((i + 1) * c, s)) for i, c, s in zip(idx, cs, a.shape))
+        blk[tuple(slice(0, n) for n in a[sl].shape)] = a[sl]
+        chunks[idx] = co.encode(blk)
+    return chunks
+
+
+class OracleArray:
+    """retrieve_array_subset_into through the CPU oracle (the per-rank decode stand-in), counting
+    the output buffers it was handed (the root must decode into its view of the gathered subset)."""
+    def __init__(self, a, cs, codecs, data_type):
+        self.shape, self.cs = list(a.shape), cs
+        self.co = O.OracleChain.from_metadata(codecs, data_type, 0, a.ndim)
+        self.chunks = _encode_grid(self.co, a, cs)
         self.dtype = a.dtype
+        self.outs = []
 
     def retrieve_array_subset_into(self, start, shape, out):
-        sl = tuple(slice(s, s + n) for s, n in zip(start, shape))
-        out.copy_(torch.from_numpy(np.ascontiguousarray(self.a[sl])))
+        self.outs.append(out)
+        got = O.retrieve_array_subset(self.co, self.shape, self.cs, self.chunks, start, shape)
+        out.copy_(torch.from_numpy(got))
 
 
 def _free_port():
@@ -37,7 +60,7 @@ def _worker(rank, world, port, q):
     dist.init_process_group("gloo", rank=rank, world_size=world)
     try:
         a = (np.arange(37 * 11 * 5, dtype=np.float32) * 1.5).reshape(37, 11, 5)
-        arr = FakeArray(a)
+        arr = OracleArray(a, [4, 4, 2], CODECS, "float32")
         res = {}
         for name, (start, shape) in {"even": ([2, 1, 0], [20, 9, 5]), "ragged": ([3, 0, 1], [31, 11, 3]),
                                      "tiny": ([5, 5, 2], [1, 2, 2])}.items():
@@ -45,11 +68,79 @@ def _worker(rank, world, port, q):
             if rank == 0:
                 sl = tuple(slice(s, s + n) for s, n in zip(start, shape))
                 res[name] = bool(np.array_equal(got.numpy(), a[sl]))
+                # the root's slab was decoded in place, inside the returned subset (no temporary)
+                own = arr.outs[-1] if arr.outs else None
+                res[name + "_inplace"] = own is None or own.data_ptr() == got.data_ptr()
             else:
                 res[name] = got is None
+        # C5 pattern: u16 chunks [bytes, shuffle 2, zstd 3] LPT-partitioned by encoded size; every rank
+        # decodes its chunks into its own level array; one subset spanning ranks gathered to rank 0
+        rng = np.random.default_rng(42)
+        lvl = (100 + rng.poisson(50, (8, 24, 40))).astype(np.uint16)
+        lvl[2:6, 4:20, 8:30] += 3000
+        cs = [4, 8, 8]
+        src = OracleArray(lvl, cs, C5_CODECS, "uint16")
+        keys = sorted(src.chunks)
+        parts = lpt_partition([len(src.chunks[k]) for k in keys], world)
+        owner = {keys[i]: r for r, p in enumerate(parts) for i in p}
+        local = torch.zeros(lvl.shape, dtype=torch.int16)
+        for k in keys:
+            if owner[k] != rank:
+                continue
+            st = [i * c for i, c in zip(k, cs)]
+            sh = [min(c, s - o) for c, s, o in zip(cs, lvl.shape, st)]
+            blk = src.co.decode(src.chunks[k], cs)
+            local[tuple(slice(o, o + n) for o, n in zip(st, sh))] = torch.from_numpy(
+                blk[tuple(slice(0, n) for n in sh)].view(np.int16))
+        sub0, subn = [1, 3, 5], [6, 19, 30]
+        boxes = [[] for _ in range(world)]
+        for idx, b0, bs in chunk_boxes(list(lvl.shape), cs, sub0, subn):
+            boxes[owner[idx]].append((b0, bs))
+        res["c5_spans_ranks"] = all(len(b) > 0 for b in boxes)
+        got = gather_regions(local, boxes, sub0, subn)
+        if rank == 0:
+            res["c5_gather"] = bool(np.array_equal(got.numpy().view(np.uint16), lvl[1:7, 3:22, 5:35]))
+        else:
+            res["c5_gather"] = got is None
         q.put((rank, res))
     finally:
         dist.destroy_process_group()
+
+
+def _subgroup_worker(rank, world, port, q):
+    """world 3, a subgroup of global ranks [1, 2]: group rank 0 (global 1) is the gather root."""
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        g = dist.new_group([1, 2])
+        res = {}
+        if rank in (1, 2):
+            a = (np.arange(19 * 6, dtype=np.float32) - 7).reshape(19, 6)
+            arr = OracleArray(a, [5, 4], CODECS, "float32")
+            got = retrieve_array_subset_distributed(arr, [2, 1], [15, 5], group=g, device="cpu")
+            if rank == 1:
+                res["root"] = got is not None and bool(np.array_equal(got.numpy(), a[2:17, 1:6]))
+            else:
+                res["peer"] = got is None
+        dist.barrier()
+        q.put((rank, res))
+    finally:
+        dist.destroy_process_group()
+
+
+def _spawn(target, world):
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=target, args=(r, world, port, q)) for r in range(world)]
+    for p in procs:
+        p.start()
+    out = dict(q.get(timeout=120) for _ in range(world))
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    return out
 
 
 def test_slab_partition_covers_subset():
@@ -78,16 +169,17 @@ def test_gather_single_rank_passthrough():
 
 
 def test_two_rank_gloo_gather():
-    world = 2
-    ctx = mp.get_context("spawn")
-    q = ctx.Queue()
-    port = _free_port()
-    procs = [ctx.Process(target=_worker, args=(r, world, port, q)) for r in range(world)]
-    for p in procs:
-        p.start()
-    out = dict(q.get(timeout=120) for _ in range(world))
-    for p in procs:
-        p.join(timeout=60)
-        assert p.exitcode == 0
+    out = _spawn(_worker, 2)
     assert all(out[0].values()), out
     assert all(out[1].values()), out
+
+
+def test_subgroup_gather_root_is_group_rank():
+    out = _spawn(_subgroup_worker, 3)
+    assert out[1] == {"root": True} and out[2] == {"peer": True}, out
+
+
+def test_chunk_boxes_cover_subset():
+    boxes = chunk_boxes([10, 13], [4, 5], [3, 2], [6, 11])
+    assert sum(bs[0] * bs[1] for _, _, bs in boxes) == 66
+    assert [i for i, _, _ in boxes] == [(0, 0), (0, 1), (0, 2), (1, 0), (1, 1), (1, 2), (2, 0), (2, 1), (2, 2)]

@@ -35,15 +35,25 @@ CHAINS = {
     "crc_start_end_i32": ([T([2, 0, 1]), B("little"), {"name": "crc32c", "configuration": {"location": "start"}},
                            {"name": "crc32c"}], "int32"),
     "complex64_be": ([B("big")], "complex64"),
+    # transposing chains through the LDS-tiled encoder's less common branches
+    "transpose_shuffle_crc_f32": ([T([2, 1, 0]), B("big"), {"name": "numcodecs.shuffle", "configuration":
+                                   {"elementsize": 4}}, {"name": "crc32c"}], "float32"),
+    "transpose_crc_start_f64": ([T([2, 1, 0]), B("little"), {"name": "crc32c", "configuration":
+                                 {"location": "start"}}], "float64"),
+    "transpose_complex64_be": ([T([1, 2, 0]), B("big")], "complex64"),
 }
+# (array shape, chunk shape): small ragged chunks, and 64-wide tiles (the vectorised tiled path)
+# whose edge chunks cross the array boundary (element path with fill)
+GEOMS = {"ragged": ([45, 70, 33], [16, 32, 32]), "tiles64": ([130, 12, 100], [64, 8, 64])}
 
 
+@pytest.mark.parametrize("geom", list(GEOMS))
 @pytest.mark.parametrize("name", list(CHAINS))
-def test_encode_vs_oracle(ctx, torch_cuda, name):
+def test_encode_vs_oracle(ctx, torch_cuda, name, geom):
     from zarrs_amd import CodecChain
     codecs, dt = CHAINS[name]
     rng = np.random.default_rng(3)
-    shape, cs = [45, 70, 33], [16, 32, 32]
+    shape, cs = GEOMS[geom]
     npdt = np.dtype(O.DTYPES[dt][0])
     a = (rng.standard_normal(shape) * 100).astype(npdt) if npdt.kind != "c" else \
         (rng.standard_normal(shape) + 1j * rng.standard_normal(shape)).astype(npdt)
@@ -55,7 +65,7 @@ def test_encode_vs_oracle(ctx, torch_cuda, name):
     arr = t.view(torch_cuda.uint8)
     # the library takes an untyped device array: pass the bytes with the element shape
     arr_t = arr.view(-1)
-    got = ch.encode_chunks(_Typed(arr_t, shape), cs, starts)
+    got = ch.encode_chunks(_Typed(arr_t, shape, npdt.itemsize), cs, starts)
     fill = np.array(5, npdt)
     for st, g in zip(starts, got):
         blk = np.full(cs, fill, npdt)
@@ -68,12 +78,19 @@ def test_encode_vs_oracle(ctx, torch_cuda, name):
 
 class _Typed:
     """A device byte buffer presented with the array's element shape (what encode_chunks reads)."""
-    def __init__(self, t, shape):
-        self._t, self.shape = t, shape
+    def __init__(self, t, shape, itemsize):
+        self._t, self.shape, self._itemsize = t, shape, itemsize
         self.is_cuda, self.device = True, t.device
+        assert t.numel() == int(np.prod(shape)) * itemsize
 
     def is_contiguous(self):
         return True
+
+    def numel(self):
+        return int(np.prod(self.shape))
+
+    def element_size(self):
+        return self._itemsize
 
     def data_ptr(self):
         return self._t.data_ptr()
@@ -95,3 +112,33 @@ def test_encode_round_trip_and_unsupported(ctx, torch_cuda):
     with pytest.raises(ZgpuError) as ei:
         gz.encode_chunks(x, [64, 64, 64], starts)
     assert ei.value.status == L.UNSUPPORTED
+    # a tensor whose element size does not match the chain's data type is refused up front
+    with pytest.raises(ZgpuError) as ei:
+        ch.encode_chunks(x.to(torch_cuda.float16), [64, 64, 64], starts)
+    assert ei.value.status == L.INVALID_ARGUMENT
+
+
+def test_sliced_launches(ctx, torch_cuda, monkeypatch):
+    """Block ranges beyond one launch's grid limit (gridDim.x * 256 < 2^32) run as several launches
+    with a block offset: forced here with a tiny ZGPU_MAX_GRID, for the tiled encoder and the
+    tiled / rows scatter kernels, bit-exact against the unsliced result."""
+    from zarrs_amd import CodecChain, make_desc
+    monkeypatch.setenv("ZGPU_MAX_GRID", "7")
+    for codecs in ([T([2, 1, 0]), B("big")], [B("big"), {"name": "crc32c"}]):
+        ch = CodecChain.from_metadata(codecs, "float32", 0, ctx)
+        x = torch_cuda.rand((128, 72, 128), device="cuda")
+        starts = [[i, j, k] for i in (0, 64) for j in (0, 64) for k in (0, 64)]
+        enc = ch.encode_chunks(x, [64, 64, 64], starts)
+        co = O.OracleChain.from_metadata(codecs, "float32", 0, 3)
+        xh = x.cpu().numpy()
+        for s, e in zip(starts, enc):
+            blk = np.zeros([64] * 3, np.float32)
+            src = xh[s[0]:s[0] + 64, s[1]:s[1] + 64, s[2]:s[2] + 64]
+            blk[:src.shape[0], :src.shape[1], :src.shape[2]] = src
+            assert e.cpu().numpy().tobytes() == co.encode(blk)
+        out = torch_cuda.empty_like(x)
+        descs = [make_desc((e.data_ptr(), e.numel()), [64] * 3, sel_shape=[min(64, n - s0) for n, s0 in
+                                                                            zip(x.shape, s)], out_start=s)
+                 for e, s in zip(enc, starts)]
+        assert ch.decode_batch(descs, out, list(x.shape), enc_device=True) == [0] * 8
+        assert torch_cuda.equal(out, x)

@@ -33,8 +33,11 @@ EXPORTS = [
     "zgpu_chain_create", "zgpu_chain_destroy", "zgpu_chain_element_size", "zgpu_decode_batch",
     "zgpu_plan_create", "zgpu_plan_execute", "zgpu_plan_status", "zgpu_plan_destroy", "zgpu_plan_algorithmic_bytes",
     "zgpu_retrieve_array_subset", "zgpu_decode_files", "zgpu_retrieve_array_subset_files",
-    "zgpu_chain_encoded_size", "zgpu_encode_batch",
+    "zgpu_chain_encoded_size", "zgpu_encode_batch", "zgpu_plan_counters", "zgpu_last_counters",
+    "zgpu_last_size_mismatch",
 ]
+CTR_ENC_BYTES, CTR_ZSTD_SERIAL, CTR_ZSTD_PARALLEL = range(3)
+N_COUNTERS = 3
 
 
 class ChunkDesc(C.Structure):
@@ -106,12 +109,33 @@ def load() -> C.CDLL:
     L.zgpu_chain_encoded_size.restype = C.c_int64
     L.zgpu_chain_encoded_size.argtypes = [vp, u32, P64]
     L.zgpu_encode_batch.argtypes = [vp, u32, P64, vp, P64, C.POINTER(EncodeDesc), u64, u32, vp]
+    L.zgpu_plan_counters.restype = u32
+    L.zgpu_plan_counters.argtypes = [vp, P64, u32]
+    L.zgpu_last_counters.restype = u32
+    L.zgpu_last_counters.argtypes = [P64, u32]
+    L.zgpu_last_size_mismatch.argtypes = [P64, P64, P64]
     _lib = L
     return L
 
 
 def last_error() -> str:
     return (load().zgpu_last_error(None) or b"").decode()
+
+
+def last_counters() -> dict:
+    """Device counters of this thread's last decode call (zgpu_last_counters)."""
+    buf = (C.c_uint64 * N_COUNTERS)()
+    load().zgpu_last_counters(buf, N_COUNTERS)
+    return {"enc_bytes": buf[0], "zstd_serial": buf[1], "zstd_parallel": buf[2]}
+
+
+def last_size_mismatch():
+    """(descriptor, len, expected_len) of the last DECODED_SIZE_MISMATCH, or None; len None when a
+    decompressor overflowed the expected size (InvalidBytesLengthError, zarrs_codec/src/lib.rs:491)."""
+    d, n, e = C.c_uint64(), C.c_uint64(), C.c_uint64()
+    if not load().zgpu_last_size_mismatch(C.byref(d), C.byref(n), C.byref(e)):
+        return None
+    return d.value, (None if n.value == (1 << 64) - 1 else n.value), e.value
 
 
 def check(status: int) -> None:

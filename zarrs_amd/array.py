@@ -17,12 +17,13 @@ Chunk keys use the default encoding "c/i/j/k" (chunk_key_encoding/default.rs:79-
 from __future__ import annotations
 
 import ctypes as C
+import itertools
 import json
 
 import numpy as np
 
 from . import _lib as L
-from .codec import CodecChain, Context
+from .codec import CodecChain, Context, default_stream
 
 
 class MemoryStore(dict):
@@ -145,29 +146,37 @@ class Array:
     def chunk_grid_shape(self):
         return [-(-s // c) for s, c in zip(self.shape, self.chunk_shape)]
 
-    def _tables(self):
+    def _tables(self, start, shape):
+        """Pointer tables indexed by the C-order linear chunk-grid index; only the chunks the subset
+        intersects are looked up in the store (chunks_in_array_subset, array_ops_array.rs:341-346),
+        the others stay NULL. Host bytes are passed zero-copy."""
         grid = self.chunk_grid_shape()
         n = int(np.prod(grid))
         ptrs = (C.c_void_p * n)()
         lens = (C.c_uint64 * n)()
         keep = []
-        for lin in range(n):
-            idx = np.unravel_index(lin, grid)
+        if any(int(s) == 0 for s in shape):
+            return ptrs, lens, keep
+        ranges = [range(int(st) // c, (int(st) + int(sh) - 1) // c + 1)
+                  for st, sh, c in zip(start, shape, self.chunk_shape)]
+        for idx in itertools.product(*ranges):
             v = self.store.get(self.chunk_key(idx))
             if v is None:
                 continue
+            lin = int(np.ravel_multi_index(idx, grid))
             if self.store.device:
                 ptrs[lin] = v.data_ptr() if v.numel() else None
                 lens[lin] = v.numel()
+                keep.append(v)
                 if not v.numel():  # an empty object is still present: give it a valid address
                     import torch
                     t = torch.empty(1, dtype=torch.uint8, device=v.device)
                     keep.append(t)
                     ptrs[lin] = t.data_ptr()
             else:
-                b = C.create_string_buffer(bytes(v), max(len(v), 1))
+                b = np.frombuffer(v, dtype=np.uint8) if len(v) else np.zeros(1, np.uint8)
                 keep.append(b)
-                ptrs[lin] = C.addressof(b)
+                ptrs[lin] = b.ctypes.data
                 lens[lin] = len(v)
         return ptrs, lens, keep
 
@@ -182,10 +191,10 @@ class Array:
             flags = (L.OUT_DEVICE if odev else 0) | (L.DIRECT_IO if self.store.direct_io else 0)
             rc = L.load().zgpu_retrieve_array_subset_files(
                 self.codecs._h, self.ndim, L.u64s(self.shape), L.u64s(self.chunk_shape), paths,
-                L.u64s(start), L.u64s(shape), op, flags, None)
+                L.u64s(start), L.u64s(shape), op, flags, default_stream(None, out))
             L.check(rc)
             return
-        ptrs, lens, keep = self._tables()
+        ptrs, lens, keep = self._tables(start, shape)
         try:
             import torch
             odev = isinstance(out, torch.Tensor) and out.is_cuda
@@ -195,7 +204,7 @@ class Array:
         flags = (L.ENC_DEVICE if self.store.device else 0) | (L.OUT_DEVICE if odev else 0)
         rc = L.load().zgpu_retrieve_array_subset(
             self.codecs._h, self.ndim, L.u64s(self.shape), L.u64s(self.chunk_shape), ptrs, lens,
-            L.u64s(start), L.u64s(shape), op, flags, None)
+            L.u64s(start), L.u64s(shape), op, flags, default_stream(None, out, *keep))
         del keep
         L.check(rc)
 

@@ -90,6 +90,23 @@ def _ptr_len(buf):
     return C.addressof(cb), len(b), False, cb
 
 
+def default_stream(stream, *bufs):
+    """The HIP stream a call runs on: the caller's, else torch's current stream of the first device
+    tensor among bufs (so the decode is ordered after the kernels that produced its inputs). A NULL
+    stream (torch's default stream) makes the library order its own stream after the legacy default
+    stream (zgpu.h)."""
+    if stream is not None:
+        return stream
+    try:
+        import torch
+    except ImportError:  # pragma: no cover
+        return None
+    for b in bufs:
+        if isinstance(b, torch.Tensor) and b.is_cuda:
+            return torch.cuda.current_stream(b.device).cuda_stream or None
+    return None
+
+
 def make_desc(enc, chunk_shape, sel_start=None, sel_shape=None, out_start=None) -> L.ChunkDesc:
     nd = len(chunk_shape)
     d = L.ChunkDesc()
@@ -153,6 +170,7 @@ class CodecChain:
         flags = (L.ENC_DEVICE if enc_device else 0) | (L.OUT_DEVICE if odev else 0)
         if validate_checksums is False:
             flags |= L.NO_VALIDATE
+        stream = default_stream(stream, out, *[getattr(d, "_keep", None) for d in descs])
         rc = L.load().zgpu_decode_batch(self._h, len(out_shape), arr, n, op, L.u64s(out_shape),
                                         flags, st, stream)
         statuses = [st[i] for i in range(n)]
@@ -179,6 +197,9 @@ class CodecChain:
         chunk_starts (zgpu_encode_batch). Returns one uint8 device tensor per chunk."""
         import torch
         assert array.is_cuda and array.is_contiguous()
+        if array.numel() * array.element_size() != int(np.prod(array.shape)) * self.dtype.itemsize or \
+                array.element_size() != self.dtype.itemsize:
+            raise L.ZgpuError(L.INVALID_ARGUMENT, f"encode: {array.dtype} tensor for a {self.data_type} chain")
         size = self.encoded_size(chunk_shape)
         if size < 0:
             raise L.ZgpuError(L.UNSUPPORTED, "encode: the chain's encoded size is not fixed")
@@ -191,6 +212,7 @@ class CodecChain:
             descs[i].dst_cap = size
             for d, v in enumerate(st):
                 descs[i].chunk_start[d] = int(v)
+        stream = default_stream(stream, array)
         rc = L.load().zgpu_encode_batch(self._h, len(chunk_shape), L.u64s(chunk_shape), array.data_ptr(),
                                        L.u64s(list(array.shape)), descs, n, L.ENC_DEVICE | L.OUT_DEVICE, stream)
         L.check(rc)

@@ -7,6 +7,10 @@
 // are one gather from the array into each chunk's encoded layout; crc32c codecs follow as
 // k_crc32c_encode launches. Chunk regions past the array edge encode the fill value (zarrs encodes
 // the whole chunk, filled: array_write_ops / ArrayBytes::new_fill_value).
+#include <algorithm>
+#include <type_traits>
+
+#include "dev.hpp"
 #include "launch.hpp"
 
 namespace zgpu {
@@ -76,79 +80,141 @@ __global__ __launch_bounds__(256) void k_encode_gather(const uint64_t *dsts, con
 
 
 // Transposing chains: the encoded innermost axis (decoded axis A = dec_axis[nd-1]) differs from the
-// array's innermost axis B = nd-1, so a plain gather reads the array with a stride. One workgroup
-// per (chunk, other coords, 64x64 tile of A x B): coalesced reads along B into a padded LDS tile,
-// coalesced writes along A out of it (the decode path's k_scatter_tiled, run backwards).
+// array's innermost axis Lx = nd-1, so a plain gather reads the array with a stride. The decode
+// path's k_scatter_tiled run backwards: a block moves TJ slabs of a 64x64 (A x Lx) tile at
+// consecutive values of axis B (the other axis with the smallest encoded stride, so the TJ encoded
+// rows of one Lx index are adjacent), reading array rows along Lx with 16-B non-temporal loads into
+// a padded LDS tile (row pitch 65 words: conflict-free column reads) and writing encoded rows along
+// A with 16-B non-temporal stores. Tiles that cross the array edge or unaligned layouts take an
+// element path (fill past the edge). Launched in slices of the block range (grid*256 < 2^32).
+constexpr int ETILE = 64;
+constexpr int ETHREADS = 256;
+
 template <int ES>
-__global__ __launch_bounds__(256) void k_encode_tiled(const uint64_t *dsts, const uint64_t *starts,
-                                                      const uint8_t *array, ZgEncode P, uint64_t n_other,
-                                                      uint32_t tiles_a, uint32_t tiles_b) {
-  __shared__ ElemA<ES> tile[64][65];
-  const uint32_t nd = P.nd, A = P.dec_axis[nd - 1], Bx = nd - 1;
-  uint64_t id = blockIdx.x;
-  const uint32_t tb = (uint32_t)(id % tiles_b);
-  id /= tiles_b;
-  const uint32_t ta = (uint32_t)(id % tiles_a);
-  id /= tiles_a;
-  const uint64_t o = id % n_other, c = id / n_other;
+__global__ __launch_bounds__(ETHREADS) void k_encode_tiled(const uint64_t *__restrict__ dsts,
+                                                           const uint64_t *__restrict__ starts,
+                                                           const uint8_t *__restrict__ array, ZgEncode P,
+                                                           uint64_t tiles_per_chunk, uint64_t block_base) {
+  using T = typename std::conditional<ES == 1, uint8_t, typename std::conditional<ES == 2, uint16_t,
+            typename std::conditional<ES == 4, uint32_t, uint2>::type>::type>::type;
+  constexpr int TJ = tiled_slabs(ES);
+  constexpr int PITCH = ETILE + (ES >= 4 ? 1 : 4 / ES);
+  constexpr int SLAB = ETILE * PITCH + (ES >= 4 ? 1 : 4 / ES);
+  __shared__ T tile[TJ * SLAB];
+  const uint64_t bid = block_base + blockIdx.x;
+  const uint64_t c = bid / tiles_per_chunk;
+  uint64_t t = bid % tiles_per_chunk;
+  const uint32_t nd = P.nd, A = P.dec_axis[nd - 1], Lx = nd - 1, B = P.tile_b;
+  const bool hasB = B < nd;
+  const uint64_t extA = P.dec_shape[A], extL = P.dec_shape[Lx], extB = hasB ? P.dec_shape[B] : 1;
+  const uint64_t nta = (extA + ETILE - 1) / ETILE, ntl = (extL + ETILE - 1) / ETILE, nbg = (extB + TJ - 1) / TJ;
+  const uint64_t ta = t % nta; t /= nta;
+  const uint64_t tl = t % ntl; t /= ntl;
+  const uint64_t tb = t % nbg; t /= nbg;
   const uint64_t *st = starts + c * nd;
-  // the other decoded coordinates (C order over the axes other than A and B)
-  uint64_t base_arr = 0, base_enc = 0, rem = o;
+  // the other decoded coordinates (C order over the axes other than A, Lx, B)
+  uint64_t arr = 0, enc = 0, rem = t;
   bool inside = true;
   for (int d = (int)nd - 1; d >= 0; d--) {
-    if ((uint32_t)d == A || (uint32_t)d == Bx) continue;
-    const uint64_t ext = P.dec_shape[d], x = rem % ext;
-    rem /= ext;
+    if ((uint32_t)d == A || (uint32_t)d == Lx || (uint32_t)d == B) continue;
+    const uint64_t x = rem % P.dec_shape[d];
+    rem /= P.dec_shape[d];
     const uint64_t ac = st[d] + x;
     inside = inside && ac < P.array_shape[d];
-    base_arr += ac * P.array_stride[d];
-    base_enc += x * P.enc_stride_of_dec[d];
+    arr += ac * P.array_stride[d];
+    enc += x * P.enc_stride_of_dec[d];
   }
-  const uint32_t t = threadIdx.x, lx = t & 63, ly = t >> 6;
-  const uint64_t extA = P.dec_shape[A], extB = P.dec_shape[Bx];
-  // read: rows along A, columns along B (array-contiguous)
-  for (uint32_t r = ly; r < 64; r += 4) {
-    const uint64_t a = (uint64_t)ta * 64 + r, b = (uint64_t)tb * 64 + lx;
-    if (a >= extA || b >= extB) continue;
-    const uint64_t aa = st[A] + a, ab = st[Bx] + b;
-    ElemA<ES> v;
-    if (inside && aa < P.array_shape[A] && ab < P.array_shape[Bx]) {
-      v = *(const ElemA<ES> *)(array + (base_arr + aa * P.array_stride[A] + ab * P.array_stride[Bx]) * ES);
-    } else {
+  const uint64_t a0 = ta * ETILE, l0 = tl * ETILE, b0 = tb * TJ;
+  const uint32_t na = (uint32_t)min<uint64_t>(ETILE, extA - a0), nl = (uint32_t)min<uint64_t>(ETILE, extL - l0);
+  const uint32_t nb = (uint32_t)min<uint64_t>(TJ, extB - b0);
+  const uint64_t sA = P.array_stride[A], sB = hasB ? P.array_stride[B] : 0;
+  const uint64_t eL = P.enc_stride_of_dec[Lx], eB = hasB ? P.enc_stride_of_dec[B] : 0;
+  // array-space origin of the tile and how much of it lies inside the array
+  const uint64_t oa = st[A] + a0, ol = st[Lx] + l0, ob = hasB ? st[B] + b0 : 0;
+  const bool whole = inside && oa + na <= P.array_shape[A] && ol + nl <= P.array_shape[Lx] &&
+                     (!hasB || ob + nb <= P.array_shape[B]);
+  const T *src = (const T *)array + arr + oa * sA + ol + (hasB ? ob * sB : 0);
+  uint8_t *dst8 = (uint8_t *)dsts[c] + P.data_off + (enc + a0 + l0 * eL + b0 * eB) * ES;
+  const uint32_t swap = P.swap && P.comp > 1;
+  constexpr int VPR = ETILE * ES / 16;  // 16-B vectors per tile row
+  constexpr int EPV = 16 / ES;          // elements per vector
+  constexpr int NV = TJ * ETILE * VPR;  // vectors per block
+  constexpr int PER = NV / ETHREADS;
+  const bool vload = whole && nl == ETILE && (((uint64_t)src & 15) == 0) && ((sA * ES) % 16 == 0) &&
+                     ((sB * ES) % 16 == 0);
+  if (vload) {
+    // e -> (row a, slab jj, vector v along Lx)
+    uint4 x[PER];
 #pragma unroll
-      for (int k = 0; k < ES; k++) v.b[k] = P.fill[k];
+    for (int p = 0; p < PER; p++) {
+      const uint32_t e = p * ETHREADS + threadIdx.x;
+      const uint32_t a = e / (TJ * VPR), jj = (e / VPR) % TJ, v = e % VPR;
+      if (a < na && jj < nb) x[p] = nt_load16(src + jj * sB + (uint64_t)a * sA + v * EPV);
     }
-    tile[r][lx] = v;
+#pragma unroll
+    for (int p = 0; p < PER; p++) {
+      const uint32_t e = p * ETHREADS + threadIdx.x;
+      const uint32_t a = e / (TJ * VPR), jj = (e / VPR) % TJ, v = e % VPR;
+      if (a < na && jj < nb) {
+        uint4 y = swap ? swap_vec(x[p], P.comp) : x[p];
+        const T *ye = (const T *)&y;
+#pragma unroll
+        for (int k = 0; k < EPV; k++) tile[jj * SLAB + a * PITCH + v * EPV + k] = ye[k];
+      }
+    }
+  } else {
+    T fv;
+    __builtin_memcpy(&fv, P.fill, ES);
+    if (swap) {  // the fill value is stored through the same endianness as the data
+      uint8_t b[ES], w[ES];
+      __builtin_memcpy(b, &fv, ES);
+      for (uint32_t c0 = 0; c0 < (uint32_t)ES; c0 += P.comp)
+        for (uint32_t k = 0; k < P.comp; k++) w[c0 + k] = b[c0 + P.comp - 1 - k];
+      __builtin_memcpy(&fv, w, ES);
+    }
+    for (uint32_t e = threadIdx.x; e < (uint32_t)(TJ * ETILE * ETILE); e += ETHREADS) {
+      const uint32_t a = e / (TJ * ETILE), jj = (e / ETILE) % TJ, l = e % ETILE;
+      if (a >= na || jj >= nb || l >= nl) continue;
+      T v = fv;
+      if (inside && oa + a < P.array_shape[A] && ol + l < P.array_shape[Lx] &&
+          (!hasB || ob + jj < P.array_shape[B])) {
+        v = src[jj * sB + (uint64_t)a * sA + l];
+        if (swap) {
+          uint8_t b[ES], w[ES];
+          __builtin_memcpy(b, &v, ES);
+          for (uint32_t c0 = 0; c0 < (uint32_t)ES; c0 += P.comp)
+            for (uint32_t k = 0; k < P.comp; k++) w[c0 + k] = b[c0 + P.comp - 1 - k];
+          __builtin_memcpy(&v, w, ES);
+        }
+      }
+      tile[jj * SLAB + a * PITCH + l] = v;
+    }
   }
   __syncthreads();
-  uint8_t *out = (uint8_t *)dsts[c] + P.data_off;
-  // write: for a fixed b, consecutive a are consecutive encoded elements
-  for (uint32_t r = ly; r < 64; r += 4) {
-    const uint64_t a = (uint64_t)ta * 64 + lx, b = (uint64_t)tb * 64 + r;
-    if (a >= extA || b >= extB) continue;
-    ElemA<ES> v = tile[lx][r];
-    if (P.swap) {
-      ElemA<ES> w = v;
-      if (P.comp == ES) {
+  const bool vstore = na == ETILE && (((uint64_t)dst8 & 15) == 0) && ((eL * ES) % 16 == 0) && ((eB * ES) % 16 == 0);
+  if (vstore) {
+    // e -> (row l, slab jj, vector v along A): TJ adjacent encoded rows per Lx index
 #pragma unroll
-        for (int k = 0; k < ES; k++) w.b[k] = v.b[ES - 1 - k];
-      } else {
-        for (uint32_t c0 = 0; c0 < ES; c0 += P.comp)
-          for (uint32_t k = 0; k < P.comp; k++) w.b[c0 + k] = v.b[c0 + P.comp - 1 - k];
+    for (int p = 0; p < PER; p++) {
+      const uint32_t e = p * ETHREADS + threadIdx.x;
+      const uint32_t l = e / (TJ * VPR), jj = (e / VPR) % TJ, v = e % VPR;
+      if (l < nl && jj < nb) {
+        uint4 y;
+        T *ye = (T *)&y;
+#pragma unroll
+        for (int k = 0; k < EPV; k++) ye[k] = tile[jj * SLAB + (v * EPV + k) * PITCH + l];
+        nt_store16(dst8 + (jj * eB + (uint64_t)l * eL + v * EPV) * ES, y);
       }
-      v = w;
     }
-    const uint64_t e = base_enc + a * P.enc_stride_of_dec[A] + b * P.enc_stride_of_dec[Bx];
-    if (P.shuffle) {
-#pragma unroll
-      for (int k = 0; k < ES; k++) out[(uint64_t)k * P.nelem + e] = v.b[k];
-    } else if (P.aligned) {
-      *(ElemA<ES> *)(out + e * ES) = v;
-    } else {
-      Elem<ES> w;
-#pragma unroll
-      for (int k = 0; k < ES; k++) w.b[k] = v.b[k];
-      *(Elem<ES> *)(out + e * ES) = w;
+  } else {
+    for (uint32_t e = threadIdx.x; e < (uint32_t)(TJ * ETILE * ETILE); e += ETHREADS) {
+      const uint32_t l = e / (TJ * ETILE), jj = (e / ETILE) % TJ, a = e % ETILE;
+      if (l < nl && jj < nb && a < na) {
+        const T v = tile[jj * SLAB + a * PITCH + l];
+        uint8_t *o = dst8 + (jj * eB + (uint64_t)l * eL + a) * ES;
+        if (P.aligned) *(T *)o = v;
+        else __builtin_memcpy(o, &v, ES);
+      }
     }
   }
 }
@@ -157,23 +223,29 @@ hipError_t launch_encode_gather(const uint64_t *dsts, const uint64_t *starts, co
                                 const ZgEncode &P, uint32_t n_chunks, hipStream_t s) {
   const uint64_t total = (uint64_t)n_chunks * P.nelem;
   if (!total) return hipSuccess;
-  const uint32_t A = P.dec_axis[P.nd - 1], Bx = P.nd - 1;
-  if (A != Bx && P.es <= 8) {  // transposing chain: LDS-tiled
-    const uint64_t extA = P.dec_shape[A], extB = P.dec_shape[Bx];
-    const uint32_t tiles_a = (uint32_t)((extA + 63) / 64), tiles_b = (uint32_t)((extB + 63) / 64);
-    const uint64_t n_other = P.nelem / (extA * extB);
-    const uint64_t blocks = (uint64_t)n_chunks * n_other * tiles_a * tiles_b;
-    if (blocks < (1ull << 31)) {
-      const dim3 g((uint32_t)blocks);
-      switch (P.es) {
-        case 1: hipLaunchKernelGGL(k_encode_tiled<1>, g, dim3(256), 0, s, dsts, starts, array, P, n_other, tiles_a, tiles_b); break;
-        case 2: hipLaunchKernelGGL(k_encode_tiled<2>, g, dim3(256), 0, s, dsts, starts, array, P, n_other, tiles_a, tiles_b); break;
-        case 4: hipLaunchKernelGGL(k_encode_tiled<4>, g, dim3(256), 0, s, dsts, starts, array, P, n_other, tiles_a, tiles_b); break;
-        case 8: hipLaunchKernelGGL(k_encode_tiled<8>, g, dim3(256), 0, s, dsts, starts, array, P, n_other, tiles_a, tiles_b); break;
-        default: return hipErrorInvalidValue;
-      }
-      return hipGetLastError();
+  const uint32_t A = P.dec_axis[P.nd - 1], Lx = P.nd - 1;
+  if (A != Lx && !P.shuffle && (P.es == 1 || P.es == 2 || P.es == 4 || P.es == 8)) {  // transposing: LDS-tiled
+    const uint64_t tj = tiled_slabs(P.es);
+    uint64_t tpc = 1;
+    for (uint32_t d = 0; d < P.nd; d++) {
+      if (d == A || d == Lx) tpc *= (P.dec_shape[d] + ETILE - 1) / ETILE;
+      else if (d == P.tile_b) tpc *= (P.dec_shape[d] + tj - 1) / tj;
+      else tpc *= P.dec_shape[d];
     }
+    const uint64_t blocks = (uint64_t)n_chunks * tpc;
+    const uint64_t MAXG = max_grid_blocks(ETHREADS);
+    for (uint64_t base = 0; base < blocks; base += MAXG) {
+      const dim3 g((uint32_t)std::min<uint64_t>(MAXG, blocks - base));
+      switch (P.es) {
+        case 1: hipLaunchKernelGGL(k_encode_tiled<1>, g, dim3(ETHREADS), 0, s, dsts, starts, array, P, tpc, base); break;
+        case 2: hipLaunchKernelGGL(k_encode_tiled<2>, g, dim3(ETHREADS), 0, s, dsts, starts, array, P, tpc, base); break;
+        case 4: hipLaunchKernelGGL(k_encode_tiled<4>, g, dim3(ETHREADS), 0, s, dsts, starts, array, P, tpc, base); break;
+        default: hipLaunchKernelGGL(k_encode_tiled<8>, g, dim3(ETHREADS), 0, s, dsts, starts, array, P, tpc, base); break;
+      }
+      const hipError_t e = hipGetLastError();
+      if (e != hipSuccess) return e;
+    }
+    return hipSuccess;
   }
   const uint32_t grid = (uint32_t)std::min<uint64_t>((total + 255) / 256, 256 * 64);
   switch (P.es) {

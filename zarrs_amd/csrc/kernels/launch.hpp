@@ -4,7 +4,21 @@
 
 #include "../common.hpp"
 
+#include <cstdlib>
+
 namespace zgpu {
+
+// Largest grid (in blocks of `threads`) one launch may use: gridDim.x * blockDim.x must stay below
+// 2^32 on HIP, so bigger block ranges are launched in slices. ZGPU_MAX_GRID lowers it (tests force
+// the sliced launches with it).
+inline uint64_t max_grid_blocks(uint32_t threads) {
+  uint64_t m = (0xFFFFFFFFull / threads) & ~(uint64_t)0xFFF;
+  if (const char *e = std::getenv("ZGPU_MAX_GRID")) {
+    const uint64_t v = std::strtoull(e, nullptr, 10);
+    if (v && v < m) m = v;
+  }
+  return m;
+}
 
 enum ScatterMode : uint32_t { SCATTER_ROWS = 0, SCATTER_TILED = 1, SCATTER_GENERIC = 2 };
 // slabs (TILE x TILE tiles at consecutive values of ZgScatter::tile_b) per tiled-scatter block
@@ -55,6 +69,8 @@ struct ZstdScratch {
   uint32_t *seq;         // n_items * seq_cap sequences of 3 u32
   uint64_t seq_cap;
   uint32_t blk_cap;
+  uint32_t force_serial = 0;               // every item on the serial one-wave decoder (tests, ZGPU_ZSTD_FORCE_SERIAL)
+  unsigned long long *counters = nullptr;  // [serial-fallback items, block-parallel items] (nullable)
 };
 void zstd_scratch_layout(uint64_t slot_bytes, uint32_t &blk_cap, uint64_t &blk_bytes, uint64_t &lit_stride,
                          uint64_t &seq_cap);
@@ -67,6 +83,7 @@ hipError_t launch_unshuffle(ZgItem *items, uint32_t *status, uint32_t n_items, u
 // encode (write path): array -> encoded chunk layouts (transposes, endianness, innermost shuffle)
 struct ZgEncode {
   uint32_t nd, es, comp, swap, shuffle, aligned;
+  uint32_t tile_b, pad0;             // tiled encode: decoded axis batched TJ slabs per block (ZG_MAXD: none)
   uint64_t nelem;                    // elements per chunk
   uint64_t data_off;                 // bytes before the data in each chunk (crc32c at start)
   uint64_t enc_shape[ZG_MAXD];       // encoded (transposed) chunk shape

@@ -19,23 +19,13 @@
 //                    per output element, coalesced writes.
 #include <hip/hip_runtime.h>
 
+#include <algorithm>
+
 #include "../common.hpp"
 #include "launch.hpp"
+#include "dev.hpp"
 
 namespace zgpu {
-
-__device__ __forceinline__ uint32_t swap_word(uint32_t x, uint32_t comp) {
-  if (comp == 4) return __builtin_bswap32(x);
-  if (comp == 2) return ((x >> 8) & 0x00FF00FFu) | ((x << 8) & 0xFF00FF00u);
-  return x;
-}
-
-__device__ __forceinline__ uint4 swap_vec(uint4 v, uint32_t comp) {
-  if (comp == 8) return make_uint4(__builtin_bswap32(v.y), __builtin_bswap32(v.x),
-                                   __builtin_bswap32(v.w), __builtin_bswap32(v.z));
-  return make_uint4(swap_word(v.x, comp), swap_word(v.y, comp), swap_word(v.z, comp),
-                    swap_word(v.w, comp));
-}
 
 // Load one element of `es` bytes (es <= 16) from a possibly unaligned address, apply the
 // endianness reversal of each `comp`-byte component, and return it in a 16-byte register.
@@ -114,9 +104,10 @@ constexpr int SCATTER_THREADS = 256;
 
 __global__ __launch_bounds__(SCATTER_THREADS) void k_scatter_rows(
     const ZgItem *__restrict__ items, const uint64_t *__restrict__ geom, uint32_t *__restrict__ status,
-    ZgScatter P, uint8_t *__restrict__ out, uint32_t blocks_per_item) {
-  const uint32_t item = blockIdx.x / blocks_per_item;
-  const uint32_t blk = blockIdx.x % blocks_per_item;
+    ZgScatter P, uint8_t *__restrict__ out, uint32_t blocks_per_item, uint64_t block_base) {
+  const uint64_t bid = block_base + blockIdx.x;
+  const uint32_t item = (uint32_t)(bid / blocks_per_item);
+  const uint32_t blk = (uint32_t)(bid % blocks_per_item);
   const ZgItem it = items[item];
   if (!item_live(it, status, item, P)) return;
   const uint32_t nd = P.nd;
@@ -269,28 +260,19 @@ __global__ __launch_bounds__(SCATTER_THREADS) void k_scatter_rows(
 // ---------------------------------------------------------------------------------------------
 constexpr int TILE = 64;
 
-typedef unsigned int zg_v4u __attribute__((ext_vector_type(4)));
-__device__ __forceinline__ uint4 nt_load16(const void *p) {
-  const zg_v4u x = __builtin_nontemporal_load((const zg_v4u *)p);
-  return make_uint4(x.x, x.y, x.z, x.w);
-}
-__device__ __forceinline__ void nt_store16(void *p, uint4 v) {
-  const zg_v4u x = {v.x, v.y, v.z, v.w};
-  __builtin_nontemporal_store(x, (zg_v4u *)p);
-}
-
 template <int ES>
 __global__ __launch_bounds__(SCATTER_THREADS) void k_scatter_tiled(
     const ZgItem *__restrict__ items, const uint64_t *__restrict__ geom, uint32_t *__restrict__ status,
-    ZgScatter P, uint8_t *__restrict__ out, uint32_t tiles_per_item) {
+    ZgScatter P, uint8_t *__restrict__ out, uint32_t tiles_per_item, uint64_t block_base) {
   using T = typename std::conditional<ES == 1, uint8_t, typename std::conditional<ES == 2, uint16_t,
             typename std::conditional<ES == 4, uint32_t, uint2>::type>::type>::type;
   constexpr int TJ = tiled_slabs(ES);
   constexpr int PITCH = TILE + (ES >= 4 ? 1 : 4 / ES);  // +1 word: column reads conflict-free
   constexpr int SLAB = TILE * PITCH + (ES >= 4 ? 1 : 4 / ES);  // +1 word: slabs on distinct banks
   __shared__ T tile[TJ * SLAB];
-  const uint32_t item = blockIdx.x / tiles_per_item;
-  uint32_t t = blockIdx.x % tiles_per_item;
+  const uint64_t bid = block_base + blockIdx.x;
+  const uint32_t item = (uint32_t)(bid / tiles_per_item);
+  uint32_t t = (uint32_t)(bid % tiles_per_item);
   const ZgItem it = items[item];
   if (!item_live(it, status, item, P)) return;
   const uint32_t nd = P.nd, A = P.tile_a, Lx = nd - 1, B = P.tile_b;
@@ -409,9 +391,10 @@ __global__ __launch_bounds__(SCATTER_THREADS) void k_scatter_tiled(
 // ---------------------------------------------------------------------------------------------
 __global__ __launch_bounds__(SCATTER_THREADS) void k_scatter_generic(
     const ZgItem *__restrict__ items, const uint64_t *__restrict__ geom, uint32_t *__restrict__ status,
-    ZgScatter P, uint8_t *__restrict__ out, uint32_t blocks_per_item) {
-  const uint32_t item = blockIdx.x / blocks_per_item;
-  const uint32_t blk = blockIdx.x % blocks_per_item;
+    ZgScatter P, uint8_t *__restrict__ out, uint32_t blocks_per_item, uint64_t block_base) {
+  const uint64_t bid = block_base + blockIdx.x;
+  const uint32_t item = (uint32_t)(bid / blocks_per_item);
+  const uint32_t blk = (uint32_t)(bid % blocks_per_item);
   const ZgItem it = items[item];
   if (!item_live(it, status, item, P)) return;
   const uint32_t nd = P.nd, es = P.es;
@@ -454,28 +437,33 @@ hipError_t launch_scatter(const ZgItem *items, const uint64_t *geom, uint32_t *s
                           uint8_t *out, uint32_t n_items, uint32_t mode, uint64_t units_per_item,
                           hipStream_t s) {
   if (n_items == 0 || units_per_item == 0) return hipSuccess;
-  const uint64_t grid = (uint64_t)n_items * units_per_item;
-  if (grid > 0x7fffffffull) return hipErrorInvalidConfiguration;
+  if (units_per_item > 0xFFFFFFFFull) return hipErrorInvalidConfiguration;
+  const uint64_t total = (uint64_t)n_items * units_per_item;
   const uint32_t u = (uint32_t)units_per_item;
-  switch (mode) {
-    case SCATTER_ROWS:
-      hipLaunchKernelGGL(k_scatter_rows, dim3((uint32_t)grid), dim3(SCATTER_THREADS), 0, s, items, geom,
-                         status, P, out, u);
-      break;
-    case SCATTER_TILED:
-      switch (P.es) {
-        case 1: hipLaunchKernelGGL(k_scatter_tiled<1>, dim3((uint32_t)grid), dim3(SCATTER_THREADS), 0, s, items, geom, status, P, out, u); break;
-        case 2: hipLaunchKernelGGL(k_scatter_tiled<2>, dim3((uint32_t)grid), dim3(SCATTER_THREADS), 0, s, items, geom, status, P, out, u); break;
-        case 4: hipLaunchKernelGGL(k_scatter_tiled<4>, dim3((uint32_t)grid), dim3(SCATTER_THREADS), 0, s, items, geom, status, P, out, u); break;
-        case 8: hipLaunchKernelGGL(k_scatter_tiled<8>, dim3((uint32_t)grid), dim3(SCATTER_THREADS), 0, s, items, geom, status, P, out, u); break;
-        default: return hipErrorInvalidValue;
-      }
-      break;
-    default:
-      hipLaunchKernelGGL(k_scatter_generic, dim3((uint32_t)grid), dim3(SCATTER_THREADS), 0, s, items, geom,
-                         status, P, out, u);
+  // gridDim.x * blockDim.x must stay below 2^32: launch the block range in slices
+  const uint64_t MAXG = max_grid_blocks(SCATTER_THREADS);
+  for (uint64_t base = 0; base < total; base += MAXG) {
+    const dim3 g((uint32_t)std::min<uint64_t>(MAXG, total - base));
+    switch (mode) {
+      case SCATTER_ROWS:
+        hipLaunchKernelGGL(k_scatter_rows, g, dim3(SCATTER_THREADS), 0, s, items, geom, status, P, out, u, base);
+        break;
+      case SCATTER_TILED:
+        switch (P.es) {
+          case 1: hipLaunchKernelGGL(k_scatter_tiled<1>, g, dim3(SCATTER_THREADS), 0, s, items, geom, status, P, out, u, base); break;
+          case 2: hipLaunchKernelGGL(k_scatter_tiled<2>, g, dim3(SCATTER_THREADS), 0, s, items, geom, status, P, out, u, base); break;
+          case 4: hipLaunchKernelGGL(k_scatter_tiled<4>, g, dim3(SCATTER_THREADS), 0, s, items, geom, status, P, out, u, base); break;
+          case 8: hipLaunchKernelGGL(k_scatter_tiled<8>, g, dim3(SCATTER_THREADS), 0, s, items, geom, status, P, out, u, base); break;
+          default: return hipErrorInvalidValue;
+        }
+        break;
+      default:
+        hipLaunchKernelGGL(k_scatter_generic, g, dim3(SCATTER_THREADS), 0, s, items, geom, status, P, out, u, base);
+    }
+    const hipError_t e = hipGetLastError();
+    if (e != hipSuccess) return e;
   }
-  return hipGetLastError();
+  return hipSuccess;
 }
 
 uint64_t scatter_units_per_item(uint32_t mode, const ZgScatter &P, const uint64_t *max_sel_shape) {

@@ -1198,7 +1198,8 @@ __device__ __forceinline__ uint32_t sym_eval(uint32_t x, uint32_t r0, uint32_t r
 
 __global__ __launch_bounds__(64) void k_zstd_scan(const ZgItem *items, uint32_t *status, ZBlk *blks,
                                                   uint32_t blk_cap, uint32_t *nblk, uint32_t *zmode,
-                                                  uint64_t lit_stride, uint64_t seq_cap) {
+                                                  uint64_t lit_stride, uint64_t seq_cap, uint32_t force_serial,
+                                                  unsigned long long *counters) {
   __shared__ ZScanSmem S;
   const uint32_t item = blockIdx.x;
   const ZgItem it = items[item];
@@ -1207,8 +1208,12 @@ __global__ __launch_bounds__(64) void k_zstd_scan(const ZgItem *items, uint32_t 
     if (lane == 0) { nblk[item] = 0; zmode[item] = ZMODE_SKIP; }
     return;
   }
-  if (it.len >= 0xFFFFFFF0ull) {  // 32-bit record offsets: decode such items serially
-    if (lane == 0) { nblk[item] = 0; zmode[item] = ZMODE_SERIAL; }
+  if (it.len >= 0xFFFFFFF0ull || force_serial) {  // 32-bit record offsets: decode such items serially
+    if (lane == 0) {
+      nblk[item] = 0;
+      zmode[item] = ZMODE_SERIAL;
+      if (counters) atomicAdd(&counters[0], 1ull);
+    }
     return;
   }
   const uint8_t *in = (const uint8_t *)it.src;
@@ -1393,6 +1398,7 @@ __global__ __launch_bounds__(64) void k_zstd_scan(const ZgItem *items, uint32_t 
     nblk[item] = serial ? 0u : nb;
     zmode[item] = serial ? ZMODE_SERIAL : (err ? ZMODE_SKIP : ZMODE_PARALLEL);
     if (err && !serial) status[item] = err;
+    if (counters && (serial || !err)) atomicAdd(&counters[serial ? 0 : 1], 1ull);  // serial / block-parallel items
   }
 }
 
@@ -2827,7 +2833,7 @@ hipError_t launch_zstd(ZgItem *items, uint32_t *status, uint32_t n_items, uint8_
   if (!n_items) return hipSuccess;
   ZBlk *blks = (ZBlk *)Z.blks;
   hipLaunchKernelGGL(k_zstd_scan, dim3(n_items), dim3(64), 0, s, items, status, blks, Z.blk_cap, Z.nblk, Z.mode,
-                     Z.lit_stride, Z.seq_cap);
+                     Z.lit_stride, Z.seq_cap, Z.force_serial, Z.counters);
   const uint64_t recs = (uint64_t)n_items * Z.blk_cap;
   // grids of the record-strided entropy kernels (overridable for tuning: ZGPU_ZSTD_GRID, ZGPU_ZSTD_LGRID)
   static const uint64_t g_cap = [] {

@@ -34,6 +34,15 @@ using namespace zgpu;
 namespace {
 
 thread_local std::string g_last_error;
+// device counters in the plan's control block (u64 each, cleared per execute)
+enum { CTR_ENC_BYTES = 0, CTR_ZSTD_SERIAL = 1, CTR_ZSTD_PARALLEL = 2, CTR_N = 3 };
+thread_local uint64_t g_last_counters[CTR_N];
+// UnexpectedChunkDecodedSize detail of the last call's first DECODED_SIZE_MISMATCH descriptor
+struct SizeDetail {
+  int valid = 0;
+  uint64_t desc = 0, len = 0, expected = 0;
+};
+thread_local SizeDetail g_size_detail;
 
 struct HipFail {
   hipError_t e;
@@ -55,6 +64,7 @@ struct zgpu_ctx {
   int device = 0;
   hipStream_t stream = nullptr;
   hipStream_t copy[2] = {nullptr, nullptr};  // H2D / D2H streams of the pipelined host path (lazy)
+  hipEvent_t order_ev = nullptr;              // legacy-stream -> context-stream ordering (pick_stream)
   std::mutex mu;
   std::multimap<size_t, void *> free_dev;  // size -> ptr
   std::map<void *, size_t> live_dev;
@@ -116,6 +126,7 @@ struct zgpu_ctx {
     for (auto &kv : free_host) (void)hipHostFree(kv.second);
     for (auto &kv : live_host) (void)hipHostFree(kv.first);
     if (stream) (void)hipStreamDestroy(stream);
+    if (order_ev) (void)hipEventDestroy(order_ev);
     for (hipStream_t cs : copy)
       if (cs) (void)hipStreamDestroy(cs);
   }
@@ -196,6 +207,7 @@ struct zgpu_plan {
   // host-input staging
   uint8_t *d_enc_stage = nullptr;
   uint64_t last_enc_bytes = 0;
+  uint64_t last_counters[CTR_N] = {0, 0, 0};
 
   ~zgpu_plan() {
     if (!ctx) return;
@@ -210,6 +222,11 @@ struct zgpu_plan {
     ctx->host_free(h_ctl);
   }
 };
+
+static void reset_call_state() {
+  for (uint64_t &c : g_last_counters) c = 0;
+  g_size_detail = SizeDetail{};
+}
 
 static int set_err(int st, const std::string &m) {
   g_last_error = m;
@@ -482,6 +499,8 @@ static void plan_upload(zgpu_plan &P, hipStream_t us = nullptr) {
   P.h_ctl = (uint8_t *)C.host_alloc(P.ctl_bytes);
   P.d_counter = (unsigned long long *)P.d_ctl;
   P.d_status = (uint32_t *)(P.d_ctl + 256);
+  P.zs.counters = P.d_counter + CTR_ZSTD_SERIAL;
+  if (const char *e = std::getenv("ZGPU_ZSTD_FORCE_SERIAL")) P.zs.force_serial = std::atoi(e) != 0;
   if (!P.shards.empty()) {
     P.d_shards = (ZgShard *)C.dev_alloc(P.shards.size() * sizeof(ZgShard));
     P.d_index = (uint64_t *)C.dev_alloc(P.shards.size() * P.ispec.n_inner * 16);
@@ -543,6 +562,8 @@ static void blosc_stage(zgpu_plan &P, const Stage &st, hipStream_t s) {
     D.zs.mode = (uint32_t *)P.grow(P.bl_zmode, D.n_sub * 4);
     D.zs.lit = (uint8_t *)P.grow(P.bl_zlit, D.n_sub * D.zs.lit_stride);
     D.zs.seq = (uint32_t *)P.grow(P.bl_zseq, D.n_sub * D.zs.seq_cap * 12);
+    D.zs.counters = P.zs.counters;
+    D.zs.force_serial = P.zs.force_serial;
   }
   HIPCHK(launch_blosc_decode(P.d_items, P.d_status, ni, info, D, dst, P.slot_bytes, s));
 }
@@ -585,26 +606,61 @@ static void plan_enqueue(zgpu_plan &P, uint8_t *out, hipStream_t s) {
   HIPCHK(launch_scatter(items, P.d_geom, P.d_status, P.scatter, out, ni, P.scatter_mode, P.scatter_units, s));
 }
 
+// InvalidBytesLengthError{len, expected_len} of descriptor d's first mismatching leaf item: the item's
+// current {src,len} is the decoded representation the final stage rejected. A materialising stage
+// that overflowed its slot leaves src on its input: the decoded length is then only known to exceed
+// the expected one (len = UINT64_MAX).
+static void size_detail(zgpu_plan &P, uint64_t d, const uint32_t *st, hipStream_t s) {
+  const size_t ni = P.items.size();
+  for (size_t i = 0; i < ni; i++) {
+    if (P.items[i].desc != d || st[i] != ZGPU_DECODED_SIZE_MISMATCH) continue;
+    const bool mutates = P.sharded || !P.stages.empty();
+    ZgItem it{};
+    HIPCHK(hipMemcpyAsync(&it, (mutates ? P.d_items : P.d_items_init) + i, sizeof(ZgItem), hipMemcpyDeviceToHost, s));
+    HIPCHK(hipStreamSynchronize(s));
+    bool materialised = false, exact = true;
+    for (const Stage &stg : P.stages)
+      if (stg.kind != ST_CRC32C) materialised = true;
+    if (materialised) {
+      exact = false;
+      for (int k = 0; k < P.n_pools; k++) {
+        const uint64_t lo = (uint64_t)P.d_pool[k], hi = lo + ni * P.slot_bytes;
+        if (it.src >= lo && it.src < hi) exact = true;
+      }
+    }
+    g_size_detail.valid = 1;
+    g_size_detail.desc = d;
+    g_size_detail.len = exact ? it.len : UINT64_MAX;
+    g_size_detail.expected = P.scatter.nelem * P.scatter.es;
+    return;
+  }
+}
+
 // Read back per-item statuses and reduce them to per-descriptor statuses. Returns the first
 // non-zero descriptor status.
 static int plan_statuses(zgpu_plan &P, int32_t *status, hipStream_t s) {
   const size_t ni = P.items.size();
   HIPCHK(hipMemcpyAsync(P.h_ctl, P.d_ctl, P.ctl_bytes, hipMemcpyDeviceToHost, s));
   HIPCHK(hipStreamSynchronize(s));
-  unsigned long long counter;
-  std::memcpy(&counter, P.h_ctl, sizeof(counter));
+  std::memcpy(P.last_counters, P.h_ctl, sizeof(P.last_counters));
+  for (int k = 0; k < CTR_N; k++) g_last_counters[k] += P.last_counters[k];
   const uint32_t *st = (const uint32_t *)(P.h_ctl + 256);
-  P.last_enc_bytes = counter;
+  P.last_enc_bytes = P.last_counters[CTR_ENC_BYTES];
   std::vector<int32_t> ds(P.item_desc_status.begin(), P.item_desc_status.end());
   for (size_t i = 0; i < ni; i++) {
     const uint32_t d = P.items[i].desc;
     if (st[i] && ds[d] == 0) ds[d] = (int32_t)st[i];
   }
   int first = 0;
+  uint64_t first_d = 0;
   for (uint64_t d = 0; d < P.n_desc; d++) {
     if (status) status[d] = ds[d];
-    if (!first && ds[d]) first = ds[d];
+    if (!first && ds[d]) {
+      first = ds[d];
+      first_d = d;
+    }
   }
+  if (first == ZGPU_DECODED_SIZE_MISMATCH && !g_size_detail.valid) size_detail(P, first_d, st, s);
   return first;
 }
 
@@ -622,7 +678,16 @@ static zgpu_plan *plan_new(zgpu_chain *ch, uint32_t nd, const zgpu_chunk_desc *d
   return P.release();
 }
 
-static hipStream_t pick_stream(zgpu_ctx *c, void *s) { return s ? (hipStream_t)s : c->stream; }
+// hip_stream NULL: the context's stream, ordered after all work already queued on the legacy
+// default stream (where torch's default stream and plain hipMemcpy/kernels land), so device buffers a
+// caller produced there are complete before the decode reads or writes them.
+static hipStream_t pick_stream(zgpu_ctx *c, void *s) {
+  if (s) return (hipStream_t)s;
+  if (!c->order_ev) HIPCHK(hipEventCreateWithFlags(&c->order_ev, hipEventDisableTiming));
+  HIPCHK(hipEventRecord(c->order_ev, nullptr));
+  HIPCHK(hipStreamWaitEvent(c->stream, c->order_ev, 0));
+  return c->stream;
+}
 
 // ------------------------------------------------------------------------------------------------
 // C ABI
@@ -716,6 +781,7 @@ int zgpu_plan_execute(zgpu_plan *P, void *out, int32_t *status, void *stream) {
   std::lock_guard<std::mutex> lk(P->ctx->mu);
   HIPCHK(hipSetDevice(P->ctx->device));
   hipStream_t s = pick_stream(P->ctx, stream);
+  reset_call_state();
   plan_enqueue(*P, (uint8_t *)out, s);
   if (!status) return ZGPU_OK;
   return plan_statuses(*P, status, s);
@@ -740,6 +806,28 @@ void zgpu_plan_destroy(zgpu_plan *P) {
 }
 
 uint64_t zgpu_plan_algorithmic_bytes(const zgpu_plan *P) { return P ? P->alg_bytes_static + P->last_enc_bytes : 0; }
+
+uint32_t zgpu_plan_counters(const zgpu_plan *P, uint64_t *out, uint32_t n) {
+  if (!P || !out) return 0;
+  const uint32_t k = std::min<uint32_t>(n, CTR_N);
+  std::memcpy(out, P->last_counters, k * sizeof(uint64_t));
+  return k;
+}
+
+int zgpu_last_size_mismatch(uint64_t *desc, uint64_t *len, uint64_t *expected_len) {
+  if (!g_size_detail.valid) return 0;
+  if (desc) *desc = g_size_detail.desc;
+  if (len) *len = g_size_detail.len;
+  if (expected_len) *expected_len = g_size_detail.expected;
+  return 1;
+}
+
+uint32_t zgpu_last_counters(uint64_t *out, uint32_t n) {
+  if (!out) return 0;
+  const uint32_t k = std::min<uint32_t>(n, CTR_N);
+  std::memcpy(out, g_last_counters, k * sizeof(uint64_t));
+  return k;
+}
 
 // Host input and host output, both pinned, descriptors covering the whole output: the batch is cut
 // into sub-batches of whole axis-0 row ranges (no descriptor straddles a cut), and sub-batch k's H2D
@@ -873,6 +961,7 @@ int zgpu_decode_batch(zgpu_chain *ch, uint32_t nd, const zgpu_chunk_desc *descs,
   std::lock_guard<std::mutex> lk(C->mu);
   HIPCHK(hipSetDevice(C->device));
   hipStream_t s = pick_stream(C, stream);
+  reset_call_state();
   if (!(flags & ZGPU_ENC_DEVICE) && !(flags & ZGPU_OUT_DEVICE) && n >= 2) {
     // pinned host in and out, full coverage: the overlapped sub-batch pipeline
     uint64_t out_elems = 1, covered = 0, out_b;
@@ -1068,6 +1157,7 @@ int zgpu_decode_files(zgpu_chain *ch, uint32_t nd, const zgpu_chunk_desc *descs,
   std::lock_guard<std::mutex> lk(C->mu);
   HIPCHK(hipSetDevice(C->device));
   hipStream_t s = pick_stream(C, stream);
+  reset_call_state();
   const int threads = host_copy_threads();
   std::vector<FileRange> fr(n);
   for (uint64_t i = 0; i < n; i++) {
@@ -1257,6 +1347,13 @@ int zgpu_encode_batch(zgpu_chain *ch, uint32_t nd, const uint64_t *chunk_shape, 
       es_ *= P.enc_shape[a];
     }
     for (uint32_t d = 0; d < nd; d++) P.dec_shape[d] = chunk_shape[d];
+    // tiled encode: the axis (other than the encoded and the array innermost) with the smallest
+    // encoded stride, so the TJ slabs of a block are adjacent encoded rows
+    P.tile_b = ZG_MAXD;
+    for (uint32_t d = 0; d + 1 < nd; d++) {
+      if (d == m[nd - 1]) continue;
+      if (P.tile_b == ZG_MAXD || P.enc_stride_of_dec[d] < P.enc_stride_of_dec[P.tile_b]) P.tile_b = d;
+    }
   }
   std::memcpy(P.fill, c.fill, sizeof(P.fill));
   const int64_t enc_size = chain_fixed_encoded_size(c, P.nelem);

@@ -9,8 +9,12 @@ read is partitioned and each rank decodes its share on its own GPU with no data-
                    straddle a slab boundary are decoded by both ranks (only their overlaps are written)
   lpt_partition    independent chunks assigned by longest-processing-time on encoded bytes (C2/C5
                    style batches with uneven compressed sizes)
-  gather_slabs     the only exchange step: every rank's slab to the root in one
-                   torch.distributed.gather (RCCL over xGMI on GPUs, gloo on CPU), skipped at N=1
+  gather_slabs     the only exchange step: every rank's slab to the root, received directly into
+                   its rows of the root's output (grouped send/recv: RCCL over xGMI on GPUs, gloo
+                   on CPU), skipped at N=1
+
+  gather_regions   chunk-partitioned ranks (LPT): every rank's chunk boxes of one subset packed into a
+                   single message each and unpacked on the root
 
 retrieve_array_subset_distributed ties them together for a zarrs_amd.Array (or anything with the
 same retrieve_array_subset_into(start, shape, out) method).
@@ -50,16 +54,46 @@ def lpt_partition(costs: Sequence[int], world: int):
     return [sorted(p) for p in parts]
 
 
-def gather_slabs(local, slabs, axis: int = 0, dst: int = 0, group=None):
-    """Gather every rank's slab (this rank's is `local`, shapes from `slab_partition`) to `dst`.
-    Returns the assembled subset on dst and None elsewhere. Unequal slabs are padded to the largest
-    one for the collective and trimmed after it."""
+def gather_slabs(local, slabs, axis: int = 0, dst: int = 0, group=None, out=None):
+    """Gather every rank's slab (this rank's is `local`, shapes from `slab_partition`) to group rank
+    `dst`. Returns the assembled subset on dst and None elsewhere.
+
+    Axis-0 slabs of a C-order subset are contiguous byte ranges of it, so on the root every peer's
+    slab is received straight into its place in the output (grouped point-to-point receives; RCCL
+    has no gather, and a root gather over xGMI should use the direct links, not a ring) and the
+    root's own slab is one device copy -- no padding, no temporaries, no concatenation. `out` may be
+    given (the root's preallocated subset; `local` may already be its own view into it). Other axes
+    fall back to a padded torch.distributed.gather. `dst` is a rank of `group`."""
     import torch
     import torch.distributed as dist
     world = len(slabs)
     if world == 1:
         return local
     rank = dist.get_rank(group)
+    g_dst = dist.get_global_rank(group, dst) if group is not None else dst
+    if axis == 0:
+        if rank != dst:
+            if local.numel():
+                dist.send(local.contiguous(), g_dst, group=group)
+            return None
+        if out is None:
+            shape = list(local.shape)
+            shape[0] = sum(sh[0] for _, sh in slabs)
+            out = torch.empty(shape, dtype=local.dtype, device=local.device)
+        ops, row = [], 0
+        for r, (_, sh) in enumerate(slabs):
+            part = out.narrow(0, row, sh[0])
+            row += sh[0]
+            if r == dst:
+                if part.data_ptr() != local.data_ptr():
+                    part.copy_(local)
+            elif part.numel():
+                g_r = dist.get_global_rank(group, r) if group is not None else r
+                ops.append(dist.P2POp(dist.irecv, part, g_r, group=group))
+        if ops:
+            for w in dist.batch_isend_irecv(ops):
+                w.wait()
+        return out
     mx = max(sh[axis] for _, sh in slabs)
     send = local
     if local.shape[axis] != mx:
@@ -68,11 +102,84 @@ def gather_slabs(local, slabs, axis: int = 0, dst: int = 0, group=None):
         send = torch.zeros(pad_shape, dtype=local.dtype, device=local.device)
         send.narrow(axis, 0, local.shape[axis]).copy_(local)
     bufs = [torch.empty_like(send) for _ in range(world)] if rank == dst else None
-    dist.gather(send.contiguous(), bufs, dst=dst, group=group)
+    dist.gather(send.contiguous(), bufs, dst=g_dst, group=group)
     if rank != dst:
         return None
     parts = [b.narrow(axis, 0, sh[axis]) for b, (_, sh) in zip(bufs, slabs)]
     return torch.cat(parts, dim=axis)
+
+
+def chunk_boxes(array_shape, chunk_shape, start, shape):
+    """[(chunk grid index, box start, box shape)] for every chunk of a regular grid that intersects
+    the subset (chunks_in_array_subset, array_ops_array.rs:341-346), boxes in array coordinates."""
+    import itertools
+    lo = [int(s) // c for s, c in zip(start, chunk_shape)]
+    hi = [(int(s) + int(n) - 1) // c + 1 for s, n, c in zip(start, shape, chunk_shape)]
+    out = []
+    if any(int(n) == 0 for n in shape):
+        return out
+    for idx in itertools.product(*[range(a, b) for a, b in zip(lo, hi)]):
+        b0 = [max(int(s), i * c) for s, i, c in zip(start, idx, chunk_shape)]
+        b1 = [min(int(s) + int(n), (i + 1) * c, a) for s, n, i, c, a in zip(start, shape, idx, chunk_shape,
+                                                                              array_shape)]
+        out.append((tuple(idx), b0, [e - b for b, e in zip(b0, b1)]))
+    return out
+
+
+def gather_regions(local, boxes_by_rank, sub_start, sub_shape, dst: int = 0, group=None, out=None):
+    """Assemble an array subset on group rank `dst` from chunk-partitioned ranks (C5: chunks
+    LPT-partitioned over the GPUs, one cross-GPU subset gathered). `local` is this
+    rank's copy of the whole array holding the chunks it decoded; boxes_by_rank[r] lists the
+    (start, shape) array boxes rank r contributes. Each peer packs its boxes into one contiguous
+    buffer and sends it with a single point-to-point message; the root receives every peer's buffer
+    (grouped receives, all links at once) and unpacks the boxes into the subset. Returns the subset
+    on dst and None elsewhere."""
+    import torch
+    import torch.distributed as dist
+    world = len(boxes_by_rank)
+    rank = dist.get_rank(group) if world > 1 else 0
+
+    def view(t, b0, bs, origin):
+        sl = tuple(slice(a - o, a - o + n) for a, n, o in zip(b0, bs, origin))
+        return t[sl]
+    zero = [0] * len(sub_start)
+    if rank != dst:
+        mine = boxes_by_rank[rank]
+        n = sum(int(torch.Size(bs).numel()) for _, bs in mine)
+        if n:
+            flat = torch.empty(n, dtype=local.dtype, device=local.device)
+            off = 0
+            for b0, bs in mine:
+                k = int(torch.Size(bs).numel())
+                flat.narrow(0, off, k).view(bs).copy_(view(local, b0, bs, zero))
+                off += k
+            dist.send(flat, dist.get_global_rank(group, dst) if group is not None else dst, group=group)
+        return None
+    if out is None:
+        out = torch.empty([int(x) for x in sub_shape], dtype=local.dtype, device=local.device)
+    for b0, bs in boxes_by_rank[dst]:
+        view(out, b0, bs, sub_start).copy_(view(local, b0, bs, zero))
+    ops, bufs = [], []
+    for r in range(world):
+        if r == dst:
+            continue
+        n = sum(int(torch.Size(bs).numel()) for _, bs in boxes_by_rank[r])
+        if not n:
+            continue
+        flat = torch.empty(n, dtype=local.dtype, device=local.device)
+        bufs.append((r, flat))
+        ops.append(dist.P2POp(dist.irecv, flat, dist.get_global_rank(group, r) if group is not None else r,
+                              group=group))
+    if ops:
+        for w in dist.batch_isend_irecv(ops):
+            w.wait()
+    for r, flat in bufs:
+        off = 0
+        for b0, bs in boxes_by_rank[r]:
+            k = int(torch.Size(bs).numel())
+            view(out, b0, bs, sub_start).copy_(flat.narrow(0, off, k).view(bs))
+            off += k
+    return out
 
 
 def retrieve_array_subset_distributed(array, start, shape, group=None, dst: int = 0, axis: int = 0,
@@ -89,7 +196,13 @@ def retrieve_array_subset_distributed(array, start, shape, group=None, dst: int 
     if device is None:
         device = torch.device("cuda", torch.cuda.current_device()) if torch.cuda.is_available() else "cpu"
     tdtype = torch.from_numpy(np.zeros(1, dtype=array.dtype)).dtype
-    local = torch.empty(sh, dtype=tdtype, device=device)
+    out = None
+    if rank == dst and axis == 0:  # the root decodes its slab in place inside the gathered subset
+        out = torch.empty([int(n) for n in shape], dtype=tdtype, device=device)
+        row0 = sum(slabs[r][1][0] for r in range(rank))
+        local = out.narrow(0, row0, sh[0])
+    else:
+        local = torch.empty(sh, dtype=tdtype, device=device)
     if all(n > 0 for n in sh):
         array.retrieve_array_subset_into(s, sh, local)
-    return gather_slabs(local, slabs, axis, dst, group)
+    return gather_slabs(local, slabs, axis, dst, group, out=out)
