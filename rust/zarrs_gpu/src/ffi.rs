@@ -1,0 +1,101 @@
+//! Raw bindings of include/zgpu.h (the C ABI of libzgpu.so). Keep in step with the header.
+#![allow(non_camel_case_types)]
+
+use std::ffi::{c_char, c_int, c_void};
+
+pub const ZGPU_MAX_DIMS: usize = 8;
+
+pub const ZGPU_OK: c_int = 0;
+pub const ZGPU_INVALID_CHECKSUM: c_int = 1;
+pub const ZGPU_DECODED_SIZE_MISMATCH: c_int = 2;
+pub const ZGPU_SHARD_INDEX_OOB: c_int = 3;
+pub const ZGPU_CORRUPT_STREAM: c_int = 4;
+pub const ZGPU_INVALID_BYTE_RANGE: c_int = 5;
+pub const ZGPU_UNSUPPORTED: c_int = 6;
+pub const ZGPU_CRC_INPUT_TOO_SHORT: c_int = 7;
+pub const ZGPU_SHARD_TOO_SMALL: c_int = 8;
+pub const ZGPU_SHUFFLE_LENGTH: c_int = 9;
+pub const ZGPU_INVALID_ARGUMENT: c_int = 10;
+pub const ZGPU_HIP_ERROR: c_int = 11;
+pub const ZGPU_STORAGE_ERROR: c_int = 12;
+
+pub const ZGPU_ENC_DEVICE: u32 = 0x1;
+pub const ZGPU_OUT_DEVICE: u32 = 0x2;
+pub const ZGPU_NO_VALIDATE: u32 = 0x4;
+pub const ZGPU_DIRECT_IO: u32 = 0x8;
+
+#[repr(C)]
+pub struct zgpu_ctx {
+    _opaque: [u8; 0],
+}
+#[repr(C)]
+pub struct zgpu_chain {
+    _opaque: [u8; 0],
+}
+
+#[repr(C)]
+#[derive(Clone, Copy)]
+pub struct zgpu_chunk_desc {
+    pub enc: *const c_void,
+    pub enc_len: u64,
+    pub chunk_shape: [u64; ZGPU_MAX_DIMS],
+    pub sel_start: [u64; ZGPU_MAX_DIMS],
+    pub sel_shape: [u64; ZGPU_MAX_DIMS],
+    pub out_start: [u64; ZGPU_MAX_DIMS],
+}
+
+impl Default for zgpu_chunk_desc {
+    fn default() -> Self {
+        Self {
+            enc: std::ptr::null(),
+            enc_len: 0,
+            chunk_shape: [0; ZGPU_MAX_DIMS],
+            sel_start: [0; ZGPU_MAX_DIMS],
+            sel_shape: [0; ZGPU_MAX_DIMS],
+            out_start: [0; ZGPU_MAX_DIMS],
+        }
+    }
+}
+
+unsafe extern "C" {
+    pub fn zgpu_ctx_create(hip_device: c_int, out: *mut *mut zgpu_ctx) -> c_int;
+    pub fn zgpu_ctx_destroy(ctx: *mut zgpu_ctx);
+    pub fn zgpu_last_error(ctx: *const zgpu_ctx) -> *const c_char;
+    pub fn zgpu_status_name(status: c_int) -> *const c_char;
+    pub fn zgpu_chain_create(
+        ctx: *mut zgpu_ctx,
+        codecs_json: *const c_char,
+        data_type: *const c_char,
+        fill: *const c_void,
+        fill_len: u32,
+        validate_checksums: c_int,
+        out: *mut *mut zgpu_chain,
+    ) -> c_int;
+    pub fn zgpu_chain_destroy(chain: *mut zgpu_chain);
+    pub fn zgpu_chain_element_size(chain: *const zgpu_chain) -> u32;
+    pub fn zgpu_decode_batch(
+        chain: *mut zgpu_chain,
+        ndim: u32,
+        descs: *const zgpu_chunk_desc,
+        n: u64,
+        out: *mut c_void,
+        out_shape: *const u64,
+        flags: u32,
+        status: *mut i32,
+        hip_stream: *mut c_void,
+    ) -> c_int;
+    pub fn zgpu_retrieve_array_subset(
+        chain: *mut zgpu_chain,
+        ndim: u32,
+        array_shape: *const u64,
+        chunk_shape: *const u64,
+        chunk_ptrs: *const *const c_void,
+        chunk_lens: *const u64,
+        sel_start: *const u64,
+        sel_shape: *const u64,
+        out: *mut c_void,
+        flags: u32,
+        hip_stream: *mut c_void,
+    ) -> c_int;
+    pub fn zgpu_last_size_mismatch(desc: *mut u64, len: *mut u64, expected_len: *mut u64) -> c_int;
+}

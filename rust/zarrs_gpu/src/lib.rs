@@ -1,0 +1,231 @@
+//! `zarrs_gpu`: the MI355X chunk-decode pipeline (libzgpu.so, include/zgpu.h) behind zarrs' own
+//! codec plugin surface, so that `zarrs/src`'s array read path runs unchanged.
+//!
+//! Two entry points, both over the C ABI:
+//!
+//! * [`register`] adds a runtime codec plugin for `sharding_indexed`
+//!   (`zarrs_codec::register_codec_v3`, zarrs_codec/src/lib.rs:279-318; runtime plugins are matched
+//!   before the compile-time ones, lib.rs:385-414). A shard is the natural GPU batch: its
+//!   `decode`/`decode_into` (ShardingCodecBound::decode_into, sharding_codec.rs:617-707) and its
+//!   partial decoder (ShardingPartialDecoder, sharding_partial_decoder_sync.rs:311-400) decode every
+//!   inner chunk of the shard in one `zgpu_decode_batch` call. Everything that is not decoding
+//!   (metadata, encoded representation, encode, partial encode, subchunk grids) is delegated to zarrs'
+//!   own `ShardingCodec`, which the plugin wraps. This is the pattern of
+//!   zarrs/tests/codec_runtime_registration.rs:92-183.
+//! * [`ArrayGpuExt`] adds a batched `retrieve_array_subset` for arrays of any supported chain
+//!   (unsharded C2/C5-style arrays): all intersecting chunks go to the GPU in one
+//!   `zgpu_retrieve_array_subset` call (Array::retrieve_array_subset_into,
+//!   array_read_ops_common.rs:20-179).
+//!
+//! Status codes map onto `CodecError` variants as include/zgpu.h documents.
+//!
+//! This crate is not compiled in the build container (no Rust toolchain there); its C side is tested
+//! from C++ (tests/c/abi_harness.cpp) and Python ctypes.
+
+mod array_ext;
+mod ffi;
+mod sharding;
+
+use std::collections::HashMap;
+use std::ffi::{CStr, CString, c_int, c_void};
+use std::ptr::NonNull;
+use std::sync::{Arc, LazyLock, Mutex};
+
+use zarrs_codec::{CodecCreateError, CodecError, InvalidBytesLengthError};
+use zarrs_data_type::{DataType, FillValue};
+use zarrs_plugin::{ExtensionName, ZarrVersion};
+
+pub use array_ext::ArrayGpuExt;
+pub use sharding::{GpuShardingCodec, GpuShardingCodecBound};
+
+/// Register the GPU `sharding_indexed` codec plugin. Keep the handle to unregister it.
+pub fn register() -> zarrs_codec::CodecRuntimeRegistryHandleV3 {
+    zarrs_codec::register_codec_v3(zarrs_codec::CodecRuntimePluginV3::new(
+        |name| name == "sharding_indexed",
+        GpuShardingCodec::create,
+    ))
+}
+
+/// Unregister a plugin registered by [`register`].
+pub fn unregister(handle: &zarrs_codec::CodecRuntimeRegistryHandleV3) -> bool {
+    zarrs_codec::unregister_codec_v3(handle)
+}
+
+/// The HIP device the plugin decodes on: `ZARRS_GPU_DEVICE` (default 0).
+fn device() -> c_int {
+    std::env::var("ZARRS_GPU_DEVICE").ok().and_then(|v| v.parse().ok()).unwrap_or(0)
+}
+
+/// One zgpu context per HIP device for the life of the process (zgpu.h: thread-safe, calls on one
+/// context are serialised internally).
+struct Ctx(NonNull<ffi::zgpu_ctx>);
+// SAFETY: every zgpu entry point is thread-safe (include/zgpu.h "Threading").
+unsafe impl Send for Ctx {}
+unsafe impl Sync for Ctx {}
+
+static CONTEXTS: LazyLock<Mutex<HashMap<c_int, Arc<Ctx>>>> = LazyLock::new(|| Mutex::new(HashMap::new()));
+
+fn context(dev: c_int) -> Result<Arc<Ctx>, String> {
+    let mut map = CONTEXTS.lock().map_err(|e| e.to_string())?;
+    if let Some(c) = map.get(&dev) {
+        return Ok(c.clone());
+    }
+    let mut p: *mut ffi::zgpu_ctx = std::ptr::null_mut();
+    // SAFETY: out-pointer to a local; the library fills it on success.
+    let rc = unsafe { ffi::zgpu_ctx_create(dev, &mut p) };
+    if rc != ffi::ZGPU_OK {
+        return Err(format!("zgpu_ctx_create({dev}): {}", last_error()));
+    }
+    let c = Arc::new(Ctx(NonNull::new(p).ok_or("zgpu_ctx_create returned NULL")?));
+    map.insert(dev, c.clone());
+    Ok(c)
+}
+
+fn last_error() -> String {
+    // SAFETY: zgpu_last_error returns a NUL-terminated thread-local string (never NULL).
+    unsafe { CStr::from_ptr(ffi::zgpu_last_error(std::ptr::null())) }.to_string_lossy().into_owned()
+}
+
+/// A bound codec chain on the GPU (`zgpu_chain`): CodecChain::from_metadata + with_context.
+pub(crate) struct Chain {
+    ptr: NonNull<ffi::zgpu_chain>,
+    _ctx: Arc<Ctx>,
+    pub(crate) element_size: usize,
+}
+// SAFETY: zgpu chains are immutable after creation and every call on them is thread-safe.
+unsafe impl Send for Chain {}
+unsafe impl Sync for Chain {}
+
+impl std::fmt::Debug for Chain {
+    fn fmt(&self, f: &mut std::fmt::Formatter<'_>) -> std::fmt::Result {
+        f.debug_struct("zgpu_chain").field("element_size", &self.element_size).finish()
+    }
+}
+
+impl Drop for Chain {
+    fn drop(&mut self) {
+        // SAFETY: created by zgpu_chain_create, destroyed once.
+        unsafe { ffi::zgpu_chain_destroy(self.ptr.as_ptr()) }
+    }
+}
+
+impl Chain {
+    /// `codecs_json` is the Zarr V3 "codecs" array; the chain is bound to `data_type` / `fill_value`.
+    pub(crate) fn new(codecs_json: &str, data_type: &DataType, fill_value: &FillValue) -> Result<Self, CodecCreateError> {
+        let ctx = context(device()).map_err(CodecCreateError::Other)?;
+        let name = data_type
+            .name(ZarrVersion::V3)
+            .ok_or_else(|| CodecCreateError::Other("data type has no Zarr V3 name".into()))?;
+        let json = CString::new(codecs_json).map_err(CodecCreateError::other)?;
+        let dt = CString::new(name.as_ref()).map_err(CodecCreateError::other)?;
+        let fill = fill_value.as_ne_bytes();
+        let mut p: *mut ffi::zgpu_chain = std::ptr::null_mut();
+        // SAFETY: valid C strings and fill buffer for the duration of the call; out-pointer to a local.
+        let rc = unsafe {
+            ffi::zgpu_chain_create(
+                ctx.0.as_ptr(),
+                json.as_ptr(),
+                dt.as_ptr(),
+                fill.as_ptr().cast(),
+                u32::try_from(fill.len()).map_err(CodecCreateError::other)?,
+                1,
+                &mut p,
+            )
+        };
+        if rc != ffi::ZGPU_OK {
+            return Err(CodecCreateError::Other(format!("zgpu_chain_create: {}", last_error())));
+        }
+        let ptr = NonNull::new(p).ok_or_else(|| CodecCreateError::Other("zgpu_chain_create returned NULL".into()))?;
+        // SAFETY: a live chain.
+        let element_size = unsafe { ffi::zgpu_chain_element_size(ptr.as_ptr()) } as usize;
+        Ok(Self { ptr, _ctx: ctx, element_size })
+    }
+
+    pub(crate) fn as_ptr(&self) -> *mut ffi::zgpu_chain {
+        self.ptr.as_ptr()
+    }
+
+    /// Decode the region `sel_start`/`sel_shape` of one encoded chunk (host bytes) of `chunk_shape`
+    /// into a new host buffer holding the region in C order. A region covering the whole chunk takes
+    /// the full decode path (checksums verified unless `validate` is false), any other region the
+    /// partial-decoder path (crc32c stripped, not verified), as zarrs does.
+    pub(crate) fn decode_region(
+        &self,
+        encoded: &[u8],
+        chunk_shape: &[u64],
+        sel_start: &[u64],
+        sel_shape: &[u64],
+        validate: bool,
+    ) -> Result<Vec<u8>, CodecError> {
+        let nd = chunk_shape.len();
+        if nd == 0 || nd > ffi::ZGPU_MAX_DIMS || sel_start.len() != nd || sel_shape.len() != nd {
+            return Err(CodecError::Other(format!("zgpu: unsupported dimensionality {nd}")));
+        }
+        let mut d = ffi::zgpu_chunk_desc {
+            enc: encoded.as_ptr().cast(),
+            enc_len: encoded.len() as u64,
+            ..Default::default()
+        };
+        d.chunk_shape[..nd].copy_from_slice(chunk_shape);
+        d.sel_start[..nd].copy_from_slice(sel_start);
+        d.sel_shape[..nd].copy_from_slice(sel_shape);
+        let n: u64 = sel_shape.iter().product();
+        let mut out = vec![0u8; usize::try_from(n).map_err(|e| CodecError::Other(e.to_string()))? * self.element_size];
+        let mut status = 0i32;
+        let flags = if validate { 0 } else { ffi::ZGPU_NO_VALIDATE };
+        // SAFETY: the descriptor points at `encoded` (host memory, flags without ZGPU_ENC_DEVICE) and
+        // `out` holds prod(sel_shape) elements; both outlive the synchronous call.
+        let rc = unsafe {
+            ffi::zgpu_decode_batch(
+                self.as_ptr(),
+                nd as u32,
+                &d,
+                1,
+                out.as_mut_ptr().cast::<c_void>(),
+                sel_shape.as_ptr(),
+                flags,
+                &mut status,
+                std::ptr::null_mut(),
+            )
+        };
+        if rc != ffi::ZGPU_OK {
+            return Err(status_error(rc));
+        }
+        Ok(out)
+    }
+}
+
+/// zgpu status -> CodecError (include/zgpu.h; zarrs_codec/src/lib.rs:617-686).
+pub(crate) fn status_error(status: c_int) -> CodecError {
+    match status {
+        ffi::ZGPU_INVALID_CHECKSUM => CodecError::InvalidChecksum,
+        ffi::ZGPU_DECODED_SIZE_MISMATCH => {
+            let (mut d, mut len, mut expected) = (0u64, 0u64, 0u64);
+            // SAFETY: out-pointers to locals.
+            if unsafe { ffi::zgpu_last_size_mismatch(&mut d, &mut len, &mut expected) } == 1 {
+                let len = if len == u64::MAX { usize::MAX } else { len as usize };
+                CodecError::UnexpectedChunkDecodedSize(InvalidBytesLengthError::new(len, expected as usize))
+            } else {
+                CodecError::Other(last_error())
+            }
+        }
+        ffi::ZGPU_SHARD_INDEX_OOB => {
+            CodecError::Other("The shard index references out-of-bounds bytes. The chunk may be corrupted.".into())
+        }
+        ffi::ZGPU_CORRUPT_STREAM => {
+            CodecError::IOError(Arc::new(std::io::Error::new(std::io::ErrorKind::InvalidData, last_error())))
+        }
+        ffi::ZGPU_CRC_INPUT_TOO_SHORT => CodecError::Other("crc32c decoder expects a 32 bit input".into()),
+        ffi::ZGPU_SHARD_TOO_SMALL => {
+            CodecError::Other("The encoded shard is smaller than the expected size of its index.".into())
+        }
+        ffi::ZGPU_SHUFFLE_LENGTH => CodecError::Other(
+            "the shuffle codec expects the input byte length to be an integer multiple of the elementsize".into(),
+        ),
+        _ => {
+            // SAFETY: zgpu_status_name returns a static string.
+            let name = unsafe { CStr::from_ptr(ffi::zgpu_status_name(status)) }.to_string_lossy();
+            CodecError::Other(format!("zgpu {name}: {}", last_error()))
+        }
+    }
+}

@@ -1,0 +1,52 @@
+//! The drop-in test, following zarrs/tests/codec_runtime_registration.rs:92-183: an array written by
+//! zarrs' own (CPU) sharding encoder is reopened with the GPU `sharding_indexed` plugin registered,
+//! and every read (whole array, partial shards, one element, the batched array extension) must equal
+//! what zarrs reads without the plugin. Needs a GPU (HIP device ZARRS_GPU_DEVICE, default 0).
+
+use std::sync::Arc;
+
+use zarrs::array::{Array, ArrayBuilder, ArraySubset, codec, data_type};
+use zarrs::storage::store::MemoryStore;
+use zarrs_gpu::ArrayGpuExt;
+
+fn write_array(store: Arc<MemoryStore>) -> Vec<u16> {
+    let array = ArrayBuilder::new(vec![64, 96], vec![32, 48], data_type::uint16(), 7u16)
+        .subchunk_shape(vec![8, 16])
+        .bytes_to_bytes_codecs(vec![
+            Arc::new(codec::GzipCodec::new(1).unwrap()),
+            Arc::new(codec::Crc32cCodec::new()),
+        ])
+        .build(store, "/array")
+        .unwrap();
+    array.store_metadata().unwrap();
+    let data: Vec<u16> = (0..64 * 96).map(|i| ((i * 37) % 4001) as u16).collect();
+    array.store_array_subset(&array.subset_all(), &data).unwrap();
+    data
+}
+
+#[test]
+fn gpu_sharding_plugin_matches_zarrs() {
+    let store = Arc::new(MemoryStore::default());
+    let data = write_array(store.clone());
+    let subsets = [
+        ArraySubset::new_with_ranges(&[0..64, 0..96]),  // whole shards: decode_into, crc32c verified
+        ArraySubset::new_with_ranges(&[5..40, 17..90]), // partial shards: the partial decoder
+        ArraySubset::new_with_ranges(&[33..34, 50..51]), // one element
+    ];
+    let cpu: Array<MemoryStore> = Array::open(store.clone(), "/array").unwrap();
+    let expected: Vec<Vec<u16>> = subsets.iter().map(|s| cpu.retrieve_array_subset(s).unwrap()).collect();
+    assert_eq!(expected[0], data);
+
+    let handle = zarrs_gpu::register();
+    let gpu: Array<MemoryStore> = Array::open(store.clone(), "/array").unwrap();
+    for (s, e) in subsets.iter().zip(&expected) {
+        let got: Vec<u16> = gpu.retrieve_array_subset(s).unwrap();
+        assert_eq!(&got, e);
+        // the batched extension (all shards of the subset in one call)
+        let raw = gpu.retrieve_array_subset_gpu(s).unwrap();
+        let got2: Vec<u16> = raw.chunks_exact(2).map(|b| u16::from_ne_bytes([b[0], b[1]])).collect();
+        assert_eq!(&got2, e);
+    }
+    assert!(zarrs_gpu::unregister(&handle));
+    assert!(!zarrs_gpu::unregister(&handle));
+}
