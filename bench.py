@@ -269,6 +269,78 @@ class C2:
 
 
 # ------------------------------------------------------------------------------------------------
+# C1 (BASELINE configs[0])
+# ------------------------------------------------------------------------------------------------
+class C1:
+    """Round trip of one 256^3 f32 chunk through the bytes-only chain: a step is
+    zgpu_encode_batch of the chunk from the device array into the device "store" buffer (the write
+    half, CodecChain::encode, codec_chain.rs:528-555) followed by its decode into the output array
+    (retrieve_chunk, array_read_ops_array.rs:265-310). On a little-endian host both halves are copies
+    (bytes codec passthrough, zarrs_data_type/src/codec_traits/bytes.rs:111-112): HBM-bound plumbing.
+    value = decoded bytes per step / step time."""
+    CODECS = [{"name": "bytes", "configuration": {"endian": "little"}}]
+    N = 256
+    kernel = "k_scatter_rows"
+    dtype = "f32"
+
+    def __init__(self, args, rank, world, dev):
+        from zarrs_amd import _lib as L
+        from zarrs_amd import CodecChain, make_desc
+        self.args, self.rank, self.world, self.dev = args, rank, world, dev
+        n = self.N
+        self.shape = [n, n, n]
+        g = torch.Generator(device=dev)
+        g.manual_seed(4321 + rank)
+        self.dec_ref = torch.rand(self.shape, generator=g, device=dev, dtype=torch.float32) * 2 - 1
+        self.chain = CodecChain.from_metadata(self.CODECS, "float32", 0.0, args.ctx)
+        self.nbytes = n ** 3 * 4
+        self.store = torch.empty(self.nbytes, dtype=torch.uint8, device=dev)  # the in-memory store
+        self.edesc = (L.EncodeDesc * 1)()
+        self.edesc[0].dst, self.edesc[0].dst_cap = self.store.data_ptr(), self.nbytes
+        self.out = torch.empty(self.shape, dtype=torch.float32, device=dev)
+        self.parts = [(self.chain, [make_desc((self.store.data_ptr(), self.nbytes), self.shape)], self.out,
+                       self.shape)]
+        self.decoded_bytes = self.nbytes
+        self.step_bytes = self.nbytes * world
+        self.extra_alg_bytes = 2 * self.nbytes  # the encode half: chunk read + encoded bytes written
+        self.config = {"workload": "C1: round trip (encode + decode) of one 256^3 f32 chunk, [bytes{endian:little}], "
+                                   "device-resident store", "chunk_shape": self.shape,
+                       "parallelism": f"one chunk per GPU x{world}"}
+        self.data = "synthetic (uniform [-1,1) f32 on device; decode(encode(x)) == x checked)"
+        self.scaling = "weak"
+
+    def pre_step(self, sp):
+        from zarrs_amd import _lib as L
+        L.check(L.load().zgpu_encode_batch(self.chain._h, 3, L.u64s(self.shape), self.dec_ref.data_ptr(),
+                                           L.u64s(self.shape), self.edesc, 1, L.ENC_DEVICE | L.OUT_DEVICE, sp))
+
+    def after_decode(self):
+        pass
+
+    def check(self) -> bool:
+        return bool(torch.equal(self.out.view(torch.int32), self.dec_ref.view(torch.int32)))
+
+    def cpu_baseline(self):
+        """The oracle's encode + decode of the chunk (one chunk: zarrs runs it on one thread)."""
+        sys.path.insert(0, os.path.join(ROOT, "oracle"))
+        import oracle as O
+        co = O.OracleChain.from_metadata(self.CODECS, "float32", 0.0, 3)
+        a = self.dec_ref.cpu().numpy()
+
+        def run():
+            return co.decode(co.encode(a), self.shape)
+        assert np.array_equal(run(), a)
+        times = _time_reps(run, min(self.args.cpu_seconds, 5.0))
+        t = float(np.median(times))
+        return {"value": round(self.nbytes / t / 2 ** 30, 3), "unit": "GiB/s", "cores": 1, "kind": "port",
+                "sample": f"the whole workload (one 256^3 f32 chunk encoded + decoded), median of {len(times)} reps, "
+                          "oracle encode/decode on one thread"}
+
+    def host_leg(self, sp):
+        return None
+
+
+# ------------------------------------------------------------------------------------------------
 # C3 / C4
 # ------------------------------------------------------------------------------------------------
 class C3:
@@ -672,7 +744,7 @@ class BloscZstd(Blosc):
     kernel = "k_zstd_exec_item"
 
 
-WORKLOADS = {"c2": C2, "c3": C3, "c5": C5, "blosc": Blosc, "blosc-zstd": BloscZstd}
+WORKLOADS = {"c1": C1, "c2": C2, "c3": C3, "c5": C5, "blosc": Blosc, "blosc-zstd": BloscZstd}
 
 
 def _time_reps(fn, seconds):
@@ -735,7 +807,11 @@ def run_gpu(args, rank, world, dev):
             done.record(st)
             stream.wait_event(done)
 
+    pre = getattr(W, "pre_step", None)
+
     def step():
+        if pre:
+            pre(sp)
         if len(plans) == 1:
             plan, out, status = plans[0]
             rc = lib.zgpu_plan_execute(plan, out.data_ptr(), status, sp)
@@ -782,11 +858,13 @@ def run_gpu(args, rank, world, dev):
     ev1 = torch.cuda.Event(enable_timing=True)
     ev0.record(stream)
     for _ in range(args.steps):
+        if pre:
+            pre(sp)
         enqueue_all()
     ev1.record(stream)
     torch.cuda.synchronize()
     ev_ms = ev0.elapsed_time(ev1) / args.steps
-    alg_bytes = sum(lib.zgpu_plan_algorithmic_bytes(plan) for plan, _, _ in plans)
+    alg_bytes = sum(lib.zgpu_plan_algorithmic_bytes(plan) for plan, _, _ in plans) + getattr(W, "extra_alg_bytes", 0)
     counters = [0] * L.N_COUNTERS
     for plan, _, _ in plans:  # device counters of each plan's last execute (statuses read in step())
         buf = (C.c_uint64 * L.N_COUNTERS)()

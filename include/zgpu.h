@@ -244,6 +244,55 @@ int zgpu_encode_batch(zgpu_chain *chain, uint32_t ndim, const uint64_t *chunk_sh
                       const uint64_t *array_shape, const zgpu_encode_desc *descs, uint64_t n, uint32_t flags,
                       void *hip_stream);
 
+/*
+ * HBM-resident decoded-chunk cache: ChunkCacheDecodedLruSizeLimit (zarrs/src/array/chunk_cache/
+ * chunk_cache_lru.rs:270) used through ArrayCached::retrieve_array_subset (zarrs/src/array/array_ops/
+ * array_read_ops_array_cached.rs:315-412). One cache per array (as an ArrayCached owns its cache):
+ * whole decoded chunks (full decode path, checksums verified) in a pool of floor(capacity / chunk
+ * bytes) HBM slots, keyed by the C-order chunk-grid index; a missing key is cached as "no chunk" (fill
+ * value); least recently used chunks are evicted. A read decodes all of its misses into their slots in
+ * one batch, then gathers the subset from HBM. A read touching more chunks than the cache holds is
+ * decoded directly (nothing new cached). Arguments as zgpu_retrieve_array_subset.
+ */
+typedef struct zgpu_cache zgpu_cache;
+int zgpu_cache_create(zgpu_ctx *ctx, uint64_t capacity_bytes, zgpu_cache **out);
+void zgpu_cache_destroy(zgpu_cache *cache);
+int zgpu_cache_clear(zgpu_cache *cache);
+int zgpu_cache_stats(zgpu_cache *cache, uint64_t *hits, uint64_t *misses, uint64_t *entries, uint64_t *bytes_used);
+int zgpu_cache_retrieve_array_subset(zgpu_cache *cache, zgpu_chain *chain, uint32_t ndim, const uint64_t *array_shape,
+                                     const uint64_t *chunk_shape, const void *const *chunk_ptrs,
+                                     const uint64_t *chunk_lens, const uint64_t *sel_start, const uint64_t *sel_shape,
+                                     void *out, uint32_t flags, void *hip_stream);
+
+/*
+ * DLPack export of a decoded subset left in HBM (the reference exports CPU tensors only:
+ * zarrs/src/array/array_dlpack_ext.rs:44-70, Device::CPU). The zgpu_dl_* types are layout-identical to
+ * DLPack's DLDevice / DLDataType / DLTensor / DLManagedTensor (dlpack.h, unversioned ABI, consumed
+ * through a PyCapsule named "dltensor"); device_type is kDLROCM (10). The library allocates the buffer
+ * on the chain's device; the consumer calls deleter(tensor) when done. cache may be NULL.
+ */
+#define ZGPU_DL_ROCM 10
+typedef struct { int32_t device_type; int32_t device_id; } zgpu_dl_device;
+typedef struct { uint8_t code; uint8_t bits; uint16_t lanes; } zgpu_dl_data_type;
+typedef struct {
+  void *data;
+  zgpu_dl_device device;
+  int32_t ndim;
+  zgpu_dl_data_type dtype;
+  int64_t *shape;
+  int64_t *strides; /* NULL: compact row-major */
+  uint64_t byte_offset;
+} zgpu_dl_tensor;
+typedef struct zgpu_dl_managed_tensor {
+  zgpu_dl_tensor dl_tensor;
+  void *manager_ctx;
+  void (*deleter)(struct zgpu_dl_managed_tensor *self);
+} zgpu_dl_managed_tensor;
+int zgpu_retrieve_array_subset_dlpack(zgpu_cache *cache, zgpu_chain *chain, uint32_t ndim, const uint64_t *array_shape,
+                                      const uint64_t *chunk_shape, const void *const *chunk_ptrs,
+                                      const uint64_t *chunk_lens, const uint64_t *sel_start, const uint64_t *sel_shape,
+                                      uint32_t flags, void *hip_stream, zgpu_dl_managed_tensor **out);
+
 #ifdef __cplusplus
 }
 #endif

@@ -1,8 +1,9 @@
 """GPU parity of the blosc codec against the reference's blosc fixtures
 (zstd + bitshuffle, written by zarrs and zarr-python) and the CPU oracle (c-blosc 1.21, the library
-zarrs' blosc-src binds) on seeded inputs: lz4 / lz4hc / zstd streams, byte shuffle / bitshuffle /
-none, typesizes 1-8, forced block sizes (split streams, leftover blocks, bitshuffle skipped for
-element counts that are not a multiple of 8), memcpyed frames, blosc inside sharding. Bit-exact."""
+zarrs' blosc-src binds) on seeded inputs: blosclz (c-blosc's default) / lz4 / lz4hc / zstd streams,
+byte shuffle / bitshuffle / none, typesizes 1-8, forced block sizes (split streams, leftover blocks,
+bitshuffle skipped for element counts that are not a multiple of 8), memcpyed frames, blosc inside
+sharding. Bit-exact."""
 import numpy as np
 import pytest
 
@@ -46,7 +47,7 @@ def _blosc(cname, shuffle, ts, blocksize=0, clevel=5):
 
 DT = {1: "uint8", 2: "uint16", 4: "float32", 8: "float64"}
 CASES = []
-for cname in ("lz4", "zstd", "lz4hc"):
+for cname in ("lz4", "zstd", "lz4hc", "blosclz"):
     for sh in ("noshuffle", "shuffle", "bitshuffle"):
         for ts in (1, 2, 4, 8):
             CASES.append((cname, sh, ts))
@@ -104,8 +105,8 @@ def test_blosc_memcpyed_and_errors(ctx, torch_cuda):
     out = np.zeros(3000, np.float32)
     assert ch.decode_batch([make_desc(enc0, [3000])], out, [3000], enc_device=False) == [0]
     assert np.array_equal(out, a)
-    # blosclz is not decoded on the GPU: UNSUPPORTED, loudly
-    codecs1 = [{"name": "bytes", "configuration": {"endian": "little"}}, _blosc("blosclz", "shuffle", 4)]
+    # zlib streams are not decoded on the GPU: UNSUPPORTED, loudly
+    codecs1 = [{"name": "bytes", "configuration": {"endian": "little"}}, _blosc("zlib", "shuffle", 4)]
     enc1 = O.OracleChain.from_metadata(codecs1, "float32", 0, 1).encode(np.zeros(3000, np.float32) + 1)
     with pytest.raises(ZgpuError) as ei:
         ch.decode_batch([make_desc(enc1, [3000])], out, [3000], enc_device=False)
@@ -128,7 +129,33 @@ def test_blosc_memcpyed_and_errors(ctx, torch_cuda):
     assert ei.value.status == L.DECODED_SIZE_MISMATCH
 
 
-@pytest.mark.parametrize("cname", ["lz4", "zstd"])
+@pytest.mark.parametrize("clevel", [1, 5, 9])
+def test_blosclz_streams_vs_cblosc(ctx, torch_cuda, clevel):
+    """blosclz (c-blosc's default compressor, the one zarrs benchmarks: benches/codecs.rs:52): long
+    runs, periodic data at distances past the 13-bit window (16-bit far matches, > 8191 back),
+    random literals, u16 image-like data; byte-exact vs c-blosc 1.21 through the oracle."""
+    from zarrs_amd import CodecChain, make_desc
+    rng = np.random.default_rng(clevel)
+    n = 1 << 20
+    datas = [np.repeat(rng.integers(0, 6, n // 64, dtype=np.uint8), 64),
+             np.tile(rng.integers(0, 256, 20000, dtype=np.uint8), n // 20000 + 1)[:n],
+             np.tile(rng.integers(0, 256, 9000, dtype=np.uint8), n // 9000 + 1)[:n],
+             rng.integers(0, 256, n, dtype=np.uint8),
+             (100 + rng.poisson(30, n // 2)).astype(np.uint16).view(np.uint8),
+             np.zeros(n, np.uint8)]
+    for sh in ("noshuffle", "shuffle"):
+        codecs = [{"name": "bytes", "configuration": {"endian": "little"}}, _blosc("blosclz", sh, 2, clevel=clevel)]
+        co = O.OracleChain.from_metadata(codecs, "uint16", 0, 1)
+        encs = [co.encode(d.view(np.uint16)) for d in datas]
+        ch = CodecChain.from_metadata(codecs, "uint16", 0, ctx)
+        devs = [torch_cuda.frombuffer(bytearray(e), dtype=torch_cuda.uint8).cuda() for e in encs]
+        descs = [make_desc(d, [n // 2], out_start=[k * (n // 2)]) for k, d in enumerate(devs)]
+        out = np.zeros(len(datas) * n // 2, np.uint16)
+        assert ch.decode_batch(descs, out, [out.size], enc_device=True) == [0] * len(datas)
+        assert out.view(np.uint8).tobytes() == np.concatenate(datas).tobytes(), sh
+
+
+@pytest.mark.parametrize("cname", ["lz4", "zstd", "blosclz"])
 def test_blosc_inside_sharding_vs_oracle(ctx, torch_cuda, cname):
     from zarrs_amd import Array, DeviceStore, MemoryStore
     from test_gpu_parity import _encode_grid

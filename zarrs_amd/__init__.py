@@ -5,6 +5,7 @@ This package is the host-side mirror of the zarrs read-path interface used by te
 """
 from ._lib import ZgpuError, load as load_library  # noqa: F401
 from .codec import CodecChain, Context, fill_value_bytes, make_desc  # noqa: F401
-from .array import Array, DeviceStore, FilesystemStore, MemoryStore  # noqa: F401
+from .array import (Array, ArrayCached, ChunkCacheDecodedLruSizeLimit, DeviceStore,  # noqa: F401
+                    FilesystemStore, MemoryStore)
 
 __version__ = "0.1.0"

@@ -9,7 +9,8 @@ import ctypes as C
 import os
 
 HERE = os.path.dirname(os.path.abspath(__file__))
-LIB_PATH = os.path.join(HERE, "lib", "libzgpu.so")
+# ZGPU_LIB: an alternative build of the same library (A/B measurements of kernel variants)
+LIB_PATH = os.environ.get("ZGPU_LIB") or os.path.join(HERE, "lib", "libzgpu.so")
 MAX_DIMS = 8
 
 STATUS_NAMES = [
@@ -34,7 +35,8 @@ EXPORTS = [
     "zgpu_plan_create", "zgpu_plan_execute", "zgpu_plan_status", "zgpu_plan_destroy", "zgpu_plan_algorithmic_bytes",
     "zgpu_retrieve_array_subset", "zgpu_decode_files", "zgpu_retrieve_array_subset_files",
     "zgpu_chain_encoded_size", "zgpu_encode_batch", "zgpu_plan_counters", "zgpu_last_counters",
-    "zgpu_last_size_mismatch",
+    "zgpu_last_size_mismatch", "zgpu_cache_create", "zgpu_cache_destroy", "zgpu_cache_clear", "zgpu_cache_stats",
+    "zgpu_cache_retrieve_array_subset", "zgpu_retrieve_array_subset_dlpack",
 ]
 CTR_ENC_BYTES, CTR_ZSTD_SERIAL, CTR_ZSTD_PARALLEL = range(3)
 N_COUNTERS = 3
@@ -57,6 +59,28 @@ class FileRange(C.Structure):
 
 class EncodeDesc(C.Structure):
     _fields_ = [("dst", C.c_void_p), ("dst_cap", C.c_uint64), ("chunk_start", C.c_uint64 * MAX_DIMS)]
+
+
+class DLDevice(C.Structure):
+    _fields_ = [("device_type", C.c_int32), ("device_id", C.c_int32)]
+
+
+class DLDataType(C.Structure):
+    _fields_ = [("code", C.c_uint8), ("bits", C.c_uint8), ("lanes", C.c_uint16)]
+
+
+class DLTensor(C.Structure):
+    _fields_ = [("data", C.c_void_p), ("device", DLDevice), ("ndim", C.c_int32), ("dtype", DLDataType),
+                ("shape", C.POINTER(C.c_int64)), ("strides", C.POINTER(C.c_int64)), ("byte_offset", C.c_uint64)]
+
+
+class DLManagedTensor(C.Structure):
+    pass
+
+
+DLManagedTensor._fields_ = [("dl_tensor", DLTensor), ("manager_ctx", C.c_void_p),
+                            ("deleter", C.CFUNCTYPE(None, C.POINTER(DLManagedTensor)))]
+DL_ROCM = 10
 
 
 class ZgpuError(RuntimeError):
@@ -114,6 +138,13 @@ def load() -> C.CDLL:
     L.zgpu_last_counters.restype = u32
     L.zgpu_last_counters.argtypes = [P64, u32]
     L.zgpu_last_size_mismatch.argtypes = [P64, P64, P64]
+    L.zgpu_cache_create.argtypes = [vp, u64, C.POINTER(vp)]
+    L.zgpu_cache_destroy.argtypes = [vp]
+    L.zgpu_cache_clear.argtypes = [vp]
+    L.zgpu_cache_stats.argtypes = [vp, P64, P64, P64, P64]
+    L.zgpu_cache_retrieve_array_subset.argtypes = [vp, vp, u32, P64, P64, C.POINTER(vp), P64, P64, P64, vp, u32, vp]
+    L.zgpu_retrieve_array_subset_dlpack.argtypes = [vp, vp, u32, P64, P64, C.POINTER(vp), P64, P64, P64, u32, vp,
+                                                    C.POINTER(C.POINTER(DLManagedTensor))]
     _lib = L
     return L
 

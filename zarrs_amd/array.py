@@ -208,6 +208,29 @@ class Array:
         del keep
         L.check(rc)
 
+    def retrieve_array_subset_dlpack(self, start=None, shape=None, cache=None):
+        """The subset decoded into HBM and handed over zero-copy as a DLPack kDLROCM tensor
+        (zgpu_retrieve_array_subset_dlpack; the reference's DLPack export, array_dlpack_ext.rs:44-70,
+        is CPU-only). Returns a torch tensor on the context's device that owns the library's buffer.
+        `cache`: an optional ChunkCacheDecodedLruSizeLimit. Encoded chunks from any store but the
+        filesystem one."""
+        import torch
+        start = [0] * self.ndim if start is None else [int(v) for v in start]
+        shape = list(self.shape) if shape is None else [int(v) for v in shape]
+        ptrs, lens, keep = self._tables(start, shape)
+        flags = L.ENC_DEVICE if self.store.device else 0
+        mt = C.POINTER(L.DLManagedTensor)()
+        rc = L.load().zgpu_retrieve_array_subset_dlpack(
+            cache._h if cache is not None else None, self.codecs._h, self.ndim, L.u64s(self.shape),
+            L.u64s(self.chunk_shape), ptrs, lens, L.u64s(start), L.u64s(shape), flags,
+            default_stream(None, *keep), C.byref(mt))
+        del keep
+        L.check(rc)
+        new_capsule = C.pythonapi.PyCapsule_New
+        new_capsule.restype = C.py_object
+        new_capsule.argtypes = [C.c_void_p, C.c_char_p, C.c_void_p]
+        return torch.utils.dlpack.from_dlpack(new_capsule(C.cast(mt, C.c_void_p), b"dltensor", None))
+
     def retrieve_array_subset(self, start=None, shape=None) -> np.ndarray:
         start = [0] * self.ndim if start is None else list(start)
         shape = self.shape if shape is None else list(shape)
@@ -218,4 +241,69 @@ class Array:
     def retrieve_chunk(self, idx) -> np.ndarray:
         start = [int(i) * c for i, c in zip(idx, self.chunk_shape)]
         shape = [min(c, s - st) for c, s, st in zip(self.chunk_shape, self.shape, start)]
+        return self.retrieve_array_subset(start, shape)
+
+
+class ChunkCacheDecodedLruSizeLimit:
+    """A decoded-chunk LRU cache of `capacity` bytes resident in HBM (zgpu_cache): the GPU form of
+    zarrs' ChunkCacheDecodedLruSizeLimit (zarrs/src/array/chunk_cache/chunk_cache_lru.rs:270)."""
+
+    def __init__(self, capacity: int, ctx: Context | None = None):
+        self.ctx = ctx or Context.default()
+        h = C.c_void_p()
+        L.check(L.load().zgpu_cache_create(self.ctx._h, int(capacity), C.byref(h)))
+        self._h = h
+        self.capacity = int(capacity)
+
+    def stats(self) -> dict:
+        v = [C.c_uint64() for _ in range(4)]
+        L.check(L.load().zgpu_cache_stats(self._h, *[C.byref(x) for x in v]))
+        return dict(zip(("hits", "misses", "entries", "bytes_used"), (x.value for x in v)))
+
+    def clear(self) -> None:
+        L.check(L.load().zgpu_cache_clear(self._h))
+
+    def __del__(self):
+        try:
+            if getattr(self, "_h", None):
+                L.load().zgpu_cache_destroy(self._h)
+                self._h = None
+        except Exception:
+            pass
+
+
+class ArrayCached:
+    """ArrayCached (zarrs/src/array/array_cached.rs:86-120): an Array with a chunk cache; reads go
+    through the HBM cache (ArrayCached::retrieve_array_subset, array_read_ops_array_cached.rs:315)."""
+
+    def __init__(self, array: Array, cache: ChunkCacheDecodedLruSizeLimit):
+        if isinstance(array.store, FilesystemStore):
+            raise NotImplementedError("ArrayCached over a FilesystemStore: read the chunks into a MemoryStore")
+        self.array, self.cache = array, cache
+
+    def retrieve_array_subset_into(self, start, shape, out) -> None:
+        a = self.array
+        ptrs, lens, keep = a._tables(start, shape)
+        odev, op = _out_ptr(out)
+        flags = (L.ENC_DEVICE if a.store.device else 0) | (L.OUT_DEVICE if odev else 0)
+        rc = L.load().zgpu_cache_retrieve_array_subset(
+            self.cache._h, a.codecs._h, a.ndim, L.u64s(a.shape), L.u64s(a.chunk_shape), ptrs, lens,
+            L.u64s(start), L.u64s(shape), op, flags, default_stream(None, out, *keep))
+        del keep
+        L.check(rc)
+
+    def retrieve_array_subset(self, start=None, shape=None) -> np.ndarray:
+        start = [0] * self.array.ndim if start is None else list(start)
+        shape = self.array.shape if shape is None else list(shape)
+        out = np.zeros([int(s) for s in shape], dtype=self.array.dtype)
+        self.retrieve_array_subset_into(start, shape, out)
+        return out
+
+    def retrieve_array_subset_dlpack(self, start=None, shape=None):
+        return self.array.retrieve_array_subset_dlpack(start, shape, cache=self.cache)
+
+    def retrieve_chunk(self, idx) -> np.ndarray:
+        a = self.array
+        start = [int(i) * c for i, c in zip(idx, a.chunk_shape)]
+        shape = [min(c, s - st) for c, s, st in zip(a.chunk_shape, a.shape, start)]
         return self.retrieve_array_subset(start, shape)

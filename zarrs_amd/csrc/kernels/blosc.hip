@@ -6,7 +6,7 @@
 //   16-B header {version, versionlz, flags, typesize, nbytes u32, blocksize u32, cbytes u32}
 //   flags: 0x1 byte shuffle, 0x2 memcpyed (raw payload after the header), 0x4 bitshuffle,
 //          0x10 blocks not split, bits 5-7 compressor format (0 blosclz, 1 lz4/lz4hc, 2 snappy,
-//          3 zlib, 4 zstd)
+//          3 zlib, 4 zstd); blosclz, lz4/lz4hc and zstd decode here, snappy / zlib -> UNSUPPORTED
 //   bstarts[nblocks] i32, then per block nsplit = (split && not the leftover block) ? typesize : 1
 //   streams of {csize i32, payload}; csize == neblock means stored.
 // A block's streams concatenate to the shuffled block, then unshuffle / bitunshuffle (format 2:
@@ -18,7 +18,7 @@
 //   k_blosc_streams  one wave per item: walks bstarts + split sizes in parallel over blocks, writes
 //                    one ZgItem per compressed stream (+ its kind) and one record per block
 //   zstd streams     the block-parallel zstd pipeline (launch_zstd) over the stream table
-//   k_lz4            one wave per lz4 stream
+//   k_lz4, k_blosclz one wave per lz4 / blosclz stream (input staged through an LDS window)
 //   k_blosc_finish   one workgroup per block: gathers the block's streams and unshuffles /
 //                    bitunshuffles them into the item's output slot (fused: no extra pass)
 #include "launch.hpp"
@@ -63,7 +63,7 @@ __global__ __launch_bounds__(64) void k_blosc_info(const ZgItem *items, uint32_t
   } else if (!err && nbytes) {
     const uint32_t comp = flags >> 5;
     if (ts == 0 || bs == 0) err = ZG_CORRUPT_STREAM;
-    else if (comp != BL_COMP_LZ4 && comp != BL_COMP_ZSTD) err = ZG_UNSUPPORTED;  // blosclz/snappy/zlib
+    else if (comp != BL_COMP_LZ4 && comp != BL_COMP_ZSTD && comp != BL_COMP_BLOSCLZ) err = ZG_UNSUPPORTED;  // snappy/zlib
     if (!err) {
       const uint32_t lo = nbytes % bs, nfull = nbytes / bs, nblk = nfull + (lo ? 1 : 0);
       const uint32_t nsplit = (flags & 0x10) ? 1 : ts;
@@ -128,7 +128,10 @@ __global__ __launch_bounds__(64) void k_blosc_streams(ZgItem *items, uint32_t *s
         }
         const bool raw = (uint64_t)cs == ne;
         subs[s0 + j] = ZgItem{it.src + (uint64_t)p, (uint64_t)cs, item, 0, 0, 0};
-        sub_kind[s0 + j] = raw ? BL_KIND_RAW : I.comp == BL_COMP_ZSTD ? BL_KIND_ZSTD : BL_KIND_LZ4;
+        sub_kind[s0 + j] = raw ? BL_KIND_RAW
+                           : I.comp == BL_COMP_ZSTD ? BL_KIND_ZSTD
+                           : I.comp == BL_COMP_LZ4  ? BL_KIND_LZ4
+                                                    : BL_KIND_BLOSCLZ;
         sub_status[s0 + j] = (!raw && I.comp == BL_COMP_ZSTD) ? 0u : BL_SKIP;
         p += cs;
       }
@@ -148,40 +151,103 @@ __global__ __launch_bounds__(64) void k_blosc_streams(ZgItem *items, uint32_t *s
   }
 }
 
+// ---------------------------------------------------------------------------------------------
+// Serial LZ77 stream decoders (lz4, blosclz), one wave per stream. The token parse is inherently
+// serial, so what bounds a wave is the latency of its dependent reads: every token / length / offset
+// byte comes from an LDS window of the compressed stream (LZW bytes, refilled with coalesced 16-B
+// loads when the parse leaves it), literal runs are copied from the window by all lanes, and a
+// match is one round trip to the already written output (all lanes' loads in flight together).
+// ---------------------------------------------------------------------------------------------
+constexpr uint32_t LZW = 8192;
+
+struct LzIn {
+  const uint8_t *in;  // the stream
+  uint64_t n;         // its length
+  uintptr_t a;        // absolute address of window byte 0 (16-B aligned)
+  uint8_t *w;         // LDS window
+
+  // load the window holding stream offset p (p < n); uniform across the wave
+  __device__ void fill(uint64_t p) {
+    __syncthreads();
+    a = ((uintptr_t)(in + p)) & ~(uintptr_t)15;
+    const uintptr_t lo = (uintptr_t)in, hi = (uintptr_t)(in + n);
+    for (uint32_t v = threadIdx.x; v < LZW / 16; v += 64) {
+      const uintptr_t q = a + 16ull * v;
+      if (q >= hi) break;
+      if (q >= lo && q + 16 <= hi) {
+        *(uint4 *)(w + 16 * v) = *(const uint4 *)q;
+      } else {  // the stream's first / last partial vector: bytes inside it only
+        for (uint32_t k = 0; k < 16; k++)
+          if (q + k >= lo && q + k < hi) w[16 * v + k] = *(const uint8_t *)(q + k);
+      }
+    }
+    __syncthreads();
+  }
+  __device__ __forceinline__ uint32_t b(uint64_t p) {
+    uint64_t k = (uintptr_t)(in + p) - a;
+    if (k >= LZW) {
+      fill(p);
+      k = (uintptr_t)(in + p) - a;
+    }
+    return w[k];
+  }
+  // out[op .. op+len) = stream[ip .. ip+len), by all lanes (window bytes from LDS, the rest global)
+  __device__ __forceinline__ void copy(uint8_t *out, uint64_t op, uint64_t ip, uint64_t len) {
+    for (uint64_t i = threadIdx.x; i < len; i += 64) {
+      const uint64_t k = (uintptr_t)(in + ip + i) - a;
+      out[op + i] = k < LZW ? w[k] : in[ip + i];
+    }
+  }
+};
+
+// A match of length ml at distance off (off <= op): byte i is out[op - off + (i mod off)], which
+// precedes the match, so lanes never read what another lane of this copy writes. The source may
+// hold bytes this wave stored since its last wait: wait for them first (workgroup scope = this CU's
+// L1, which the wave's own write-through stores keep coherent; an agent-scope fence would write back
+// / invalidate L2 across XCDs). Bytes below `safe` are known complete.
+__device__ __forceinline__ void lz_match(uint8_t *out, uint64_t op, uint64_t off, uint64_t ml, uint64_t &safe) {
+  if (op - off + (off < ml ? off : ml) > safe) {
+    __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "workgroup");
+    safe = op;
+  }
+  const uint8_t *src = out + op - off;
+  for (uint64_t i = threadIdx.x; i < ml; i += 64) out[op + i] = src[off >= ml ? i : i % off];
+}
+
 // LZ4 block format (lz4_Block_format.md): sequences {token, literal length, literals, offset u16,
-// match length}; the last sequence has literals only. One wave per stream; literal runs and
-// matches are copied by all lanes (a match of period d < its length reads only bytes before its
-// start: out[o + i] = out[o - d + i % d]).
+// match length}; the last sequence has literals only.
 __global__ __launch_bounds__(64) void k_lz4(ZgItem *subs, uint32_t *sub_status, const uint32_t *sub_kind,
                                             uint32_t n_sub, uint8_t *dst, uint64_t slot) {
+  __shared__ __attribute__((aligned(16))) uint8_t win[LZW];
   const uint32_t s = blockIdx.x, lane = threadIdx.x;
   if (sub_kind[s] != BL_KIND_LZ4 || sub_status[s] != BL_SKIP) return;
   const ZgItem it = subs[s];
-  const uint8_t *in = (const uint8_t *)it.src;
   const uint64_t cs = it.len;
+  LzIn I{(const uint8_t *)it.src, cs, 0, win};
   uint8_t *out = dst + (uint64_t)s * slot;
   uint64_t ip = 0, op = 0, safe = 0;
   uint32_t err = 0;
+  if (cs) I.fill(0);
   for (;;) {
     if (ip >= cs) { err = 1; break; }
-    const uint32_t token = in[ip++];
+    const uint32_t token = I.b(ip++);
     uint64_t ll = token >> 4;
     if (ll == 15) {
       uint32_t b;
       do {
         if (ip >= cs) { err = 1; break; }
-        b = in[ip++];
+        b = I.b(ip++);
         ll += b;
       } while (b == 255);
       if (err) break;
     }
     if (ip + ll > cs || op + ll > slot) { err = 1; break; }
-    for (uint64_t i = lane; i < ll; i += 64) out[op + i] = in[ip + i];
+    I.copy(out, op, ip, ll);
     ip += ll;
     op += ll;
     if (ip == cs) break;  // last sequence: literals only
     if (ip + 2 > cs) { err = 1; break; }
-    const uint64_t off = (uint64_t)in[ip] | ((uint64_t)in[ip + 1] << 8);
+    const uint64_t off = I.b(ip) | (I.b(ip + 1) << 8);
     ip += 2;
     if (off == 0 || off > op) { err = 1; break; }
     uint64_t ml = token & 15;
@@ -189,24 +255,82 @@ __global__ __launch_bounds__(64) void k_lz4(ZgItem *subs, uint32_t *sub_status, 
       uint32_t b;
       do {
         if (ip >= cs) { err = 1; break; }
-        b = in[ip++];
+        b = I.b(ip++);
         ml += b;
       } while (b == 255);
       if (err) break;
     }
     ml += 4;
     if (op + ml > slot) { err = 1; break; }
-    // the match may read bytes this wave stored since its last wait: wait for the stores first
-    // (workgroup scope = this CU's L1, which the wave's own write-through stores keep coherent; an
-    // agent-scope fence would write back / invalidate L2 across XCDs). Bytes below `safe` are known
-    // complete, so far-back sources (the common case) need no wait at all.
-    if (op - off + (off < ml ? off : ml) > safe) {
-      __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "workgroup");
-      safe = op;
-    }
-    const uint8_t *src = out + op - off;
-    for (uint64_t i = lane; i < ml; i += 64) out[op + i] = src[off >= ml ? i : i % off];
+    lz_match(out, op, off, ml, safe);
     op += ml;
+  }
+  if (lane == 0) {
+    sub_status[s] = err ? ZG_CORRUPT_STREAM : 0u;
+    subs[s].src = (uint64_t)out;
+    subs[s].len = op;
+  }
+}
+
+// blosclz (c-blosc 1.21 blosclz.c, blosclz_decompress; restated, checked against c-blosc in
+// tests/test_gpu_blosc.py): a FastLZ-style stream. The first control byte (low 5 bits) opens a
+// literal run; a control byte c < 32 is a run of c + 1 literals; c >= 32 is a match of length
+// (c >> 5) + 2 (7 -> extended by following bytes until one is not 255) whose distance is
+// ((c & 31) << 8) + next byte + 1, or, when that byte is 255 and c & 31 == 31, a 16-bit big-endian
+// value + 8192 (MAX_DISTANCE 8191 + 1). The stream ends when its bytes are consumed.
+__global__ __launch_bounds__(64) void k_blosclz(ZgItem *subs, uint32_t *sub_status, const uint32_t *sub_kind,
+                                                uint32_t n_sub, uint8_t *dst, uint64_t slot) {
+  __shared__ __attribute__((aligned(16))) uint8_t win[LZW];
+  const uint32_t s = blockIdx.x, lane = threadIdx.x;
+  if (sub_kind[s] != BL_KIND_BLOSCLZ || sub_status[s] != BL_SKIP) return;
+  const ZgItem it = subs[s];
+  const uint64_t n = it.len;
+  LzIn I{(const uint8_t *)it.src, n, 0, win};
+  uint8_t *out = dst + (uint64_t)s * slot;
+  uint64_t ip = 0, op = 0, safe = 0;
+  uint32_t err = 0;
+  if (n) {
+    I.fill(0);
+    uint32_t ctrl = I.b(ip++) & 31u;
+    for (;;) {
+      if (ctrl >= 32) {
+        uint64_t len = (ctrl >> 5) - 1;
+        uint64_t ofs = (uint64_t)(ctrl & 31u) << 8;
+        uint32_t code;
+        if (len == 6) {
+          do {
+            if (ip + 1 >= n) { err = 1; break; }
+            code = I.b(ip++);
+            len += code;
+          } while (code == 255);
+          if (err) break;
+        } else if (ip + 1 >= n) {
+          err = 1;
+          break;
+        }
+        code = I.b(ip++);
+        len += 3;
+        uint64_t dist = ofs + code + 1;
+        if (code == 255 && ofs == (31u << 8)) {
+          if (ip + 1 >= n) { err = 1; break; }
+          dist = ((uint64_t)I.b(ip) << 8) + I.b(ip + 1) + 8192;
+          ip += 2;
+        }
+        if (op + len > slot || dist > op) { err = 1; break; }
+        lz_match(out, op, dist, len, safe);
+        op += len;
+        if (ip >= n) break;
+        ctrl = I.b(ip++);
+      } else {
+        const uint64_t run = ctrl + 1;
+        if (op + run > slot || ip + run > n) { err = 1; break; }
+        I.copy(out, op, ip, run);
+        op += run;
+        ip += run;
+        if (ip >= n) break;
+        ctrl = I.b(ip++);
+      }
+    }
   }
   if (lane == 0) {
     sub_status[s] = err ? ZG_CORRUPT_STREAM : 0u;
@@ -300,6 +424,9 @@ hipError_t launch_blosc_decode(ZgItem *items, uint32_t *status, uint32_t n_items
   }
   if (D.n_lz4)
     hipLaunchKernelGGL(k_lz4, dim3((uint32_t)D.n_sub), dim3(64), 0, s, D.subs, D.sub_status, D.sub_kind,
+                       (uint32_t)D.n_sub, D.tmp, D.sub_slot);
+  if (D.n_blosclz)
+    hipLaunchKernelGGL(k_blosclz, dim3((uint32_t)D.n_sub), dim3(64), 0, s, D.subs, D.sub_status, D.sub_kind,
                        (uint32_t)D.n_sub, D.tmp, D.sub_slot);
   if (D.n_blk)
     hipLaunchKernelGGL(k_blosc_finish, dim3((uint32_t)D.n_blk), dim3(256), 0, s, D.blocks, D.subs, D.sub_status,

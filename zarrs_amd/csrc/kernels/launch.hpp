@@ -100,8 +100,8 @@ hipError_t launch_crc32c_encode(const uint64_t *dsts, uint32_t n, uint64_t lo, u
                                 hipStream_t s);
 
 // blosc (c-blosc 1.x frames): stream table built on the device, sized on the host from BlInfo
-enum : uint32_t { BL_COMP_LZ4 = 1, BL_COMP_ZSTD = 4, BL_COMP_MEMCPY = 0x100, BL_COMP_SKIP = 0xFFFFFFFFu };
-enum : uint32_t { BL_KIND_RAW = 0, BL_KIND_LZ4 = 1, BL_KIND_ZSTD = 4 };
+enum : uint32_t { BL_COMP_BLOSCLZ = 0, BL_COMP_LZ4 = 1, BL_COMP_ZSTD = 4, BL_COMP_MEMCPY = 0x100, BL_COMP_SKIP = 0xFFFFFFFFu };
+enum : uint32_t { BL_KIND_RAW = 0, BL_KIND_LZ4 = 1, BL_KIND_ZSTD = 4, BL_KIND_BLOSCLZ = 5 };
 struct BlInfo {     // per item (read back)
   uint32_t nsub;    // compressed streams
   uint32_t nblk;    // blocks
@@ -123,7 +123,7 @@ struct BlDecode {
   uint8_t *tmp;           // n_sub * sub_slot decoded streams
   uint64_t sub_slot;
   ZstdScratch zs;
-  uint64_t n_sub, n_blk, n_zstd, n_lz4;
+  uint64_t n_sub, n_blk, n_zstd, n_lz4, n_blosclz;
 };
 hipError_t launch_blosc_info(const ZgItem *items, uint32_t *status, uint32_t n_items, uint64_t slot_bytes,
                              BlInfo *info, hipStream_t s);

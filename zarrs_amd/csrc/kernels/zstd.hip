@@ -1632,7 +1632,10 @@ __global__ __launch_bounds__(64) void k_zstd_blocks(const ZgItem *items, uint32_
 // entry, exit and symbol count; pass 2 decodes again and writes the symbols at the prefix-summed
 // offsets. The compressed literal section is staged in LDS first (sections over LIT_LDS read global).
 // -------------------------------------------------------------------------------------------------
-constexpr uint32_t LIT_LDS = 64 * 1024;
+#ifndef ZG_LIT_LDS
+#define ZG_LIT_LDS (64 * 1024)
+#endif
+constexpr uint32_t LIT_LDS = ZG_LIT_LDS;
 constexpr int32_t LIT_WARM = 128;
 constexpr uint32_t LIT_THREADS = 256;
 
@@ -2003,7 +2006,10 @@ namespace {
 // whose high-byte plane is a chain of row- and plane-periodic copies, so there is no block-level
 // parallelism to take here; it is taken in k_zstd_lits / k_zstd_blocks, and across items.)
 // -------------------------------------------------------------------------------------------------
-constexpr uint32_t XRING = 65536, XRMASK = XRING - 1;
+#ifndef ZG_XRING
+#define ZG_XRING 65536
+#endif
+constexpr uint32_t XRING = ZG_XRING, XRMASK = XRING - 1;
 constexpr uint32_t XSTAGE_V = 512;  // staged far-source vectors (16 B) per batch
 constexpr uint32_t XPL = 32;        // bytes of a short match its own lane copies (the rest: the wave)
 constexpr int XR_LIT = ZBATCH / 16 / 64 + 1, XR_FAR = XSTAGE_V / 64;

@@ -27,6 +27,7 @@
 #include "common.hpp"
 #include "kernels/launch.hpp"
 #include "fsstore.hpp"
+#include "internal.hpp"
 #include "xfer.hpp"
 
 using namespace zgpu;
@@ -232,6 +233,12 @@ static int set_err(int st, const std::string &m) {
   g_last_error = m;
   return st;
 }
+
+int zgpu::set_last_error(int status, const std::string &msg) { return set_err(status, msg); }
+zgpu_ctx *zgpu::chain_ctx(const zgpu_chain *c) { return c->ctx; }
+const Chain &zgpu::chain_model(const zgpu_chain *c) { return *c->chain; }
+bool zgpu::chain_validates(const zgpu_chain *c) { return c->validate; }
+int zgpu::ctx_device(const zgpu_ctx *c) { return c->device; }
 
 // composed permutation of all array->array codecs: encoded axis a <-> decoded axis m[a]
 static void composed_axes(const Chain &c, uint32_t nd, uint32_t *m) {
@@ -540,6 +547,7 @@ static void blosc_stage(zgpu_plan &P, const Stage &st, hipStream_t s) {
     D.n_blk += hi[i].nblk;
     if (hi[i].comp == BL_COMP_ZSTD) D.n_zstd += hi[i].nsub;
     if (hi[i].comp == BL_COMP_LZ4) D.n_lz4 += hi[i].nsub;
+    if (hi[i].comp == BL_COMP_BLOSCLZ) D.n_blosclz += hi[i].nsub;
     max_ne = std::max<uint64_t>(max_ne, hi[i].max_ne);
   }
   uint64_t *d_bases = (uint64_t *)P.grow(P.bl_bases, ni * 16);
@@ -550,7 +558,7 @@ static void blosc_stage(zgpu_plan &P, const Stage &st, hipStream_t s) {
   D.sub_status = (uint32_t *)P.grow(P.bl_sub_status, ns * 4);
   D.sub_kind = (uint32_t *)P.grow(P.bl_sub_kind, ns * 4);
   D.blocks = (BlBlock *)P.grow(P.bl_blocks, std::max<uint64_t>(D.n_blk, 1) * sizeof(BlBlock));
-  if (D.n_zstd + D.n_lz4) {
+  if (D.n_zstd + D.n_lz4 + D.n_blosclz) {
     D.sub_slot = (max_ne + 255) & ~(uint64_t)255;
     D.tmp = (uint8_t *)P.grow(P.bl_tmp, D.n_sub * D.sub_slot);
   }
@@ -704,6 +712,56 @@ static hipStream_t pick_stream(zgpu_ctx *c, void *s) {
   catch (const std::exception &e) {                                                            \
     return set_err(ZGPU_INVALID_ARGUMENT, e.what());                                           \
   }
+
+// array_read_ops_common.rs:20-109: subset -> intersecting chunks -> one descriptor per chunk, in
+// C order of the chunk grid; lins[k] = descriptor k's C-order linear chunk-grid index.
+// Returns ZGPU_OK, -1 for an empty subset (nothing to do), or an error status.
+int zgpu::subset_descs(uint32_t nd, const uint64_t *array_shape, const uint64_t *chunk_shape,
+                       const uint64_t *sel_start, const uint64_t *sel_shape, std::vector<zgpu_chunk_desc> &descs,
+                       std::vector<uint64_t> &lins) {
+  uint64_t grid[ZG_MAXD], lo[ZG_MAXD], hi[ZG_MAXD], idx[ZG_MAXD];
+  uint64_t nchunks = 1;
+  bool empty = false;
+  for (uint32_t d = 0; d < nd; d++) {
+    if (chunk_shape[d] == 0) return set_err(ZGPU_INVALID_ARGUMENT, "zero chunk extent");
+    if (sel_start[d] + sel_shape[d] > array_shape[d])
+      return set_err(ZGPU_INVALID_ARGUMENT, "array subset out of bounds");
+    grid[d] = (array_shape[d] + chunk_shape[d] - 1) / chunk_shape[d];
+    if (sel_shape[d] == 0) {
+      empty = true;
+      continue;
+    }
+    lo[d] = sel_start[d] / chunk_shape[d];
+    hi[d] = (sel_start[d] + sel_shape[d] - 1) / chunk_shape[d] + 1;
+    nchunks *= hi[d] - lo[d];
+    idx[d] = lo[d];
+  }
+  if (empty) return -1;
+  descs.reserve(nchunks);
+  lins.reserve(nchunks);
+  for (;;) {
+    zgpu_chunk_desc D{};
+    uint64_t lin = 0;
+    for (uint32_t d = 0; d < nd; d++) {
+      lin = lin * grid[d] + idx[d];
+      const uint64_t cs = idx[d] * chunk_shape[d], ce = cs + chunk_shape[d];
+      const uint64_t s0 = std::max(sel_start[d], cs), s1 = std::min(sel_start[d] + sel_shape[d], ce);
+      D.chunk_shape[d] = chunk_shape[d];
+      D.sel_start[d] = s0 - cs;
+      D.sel_shape[d] = s1 - s0;
+      D.out_start[d] = s0 - sel_start[d];
+    }
+    descs.push_back(D);
+    lins.push_back(lin);
+    int d = (int)nd - 1;
+    for (; d >= 0; d--) {
+      if (++idx[d] < hi[d]) break;
+      idx[d] = lo[d];
+    }
+    if (d < 0) break;
+  }
+  return ZGPU_OK;
+}
 
 extern "C" {
 
@@ -1072,56 +1130,6 @@ int zgpu_decode_batch(zgpu_chain *ch, uint32_t nd, const zgpu_chunk_desc *descs,
   if (rc) set_err(rc, zgpu_status_name(rc));
   return rc;
   ABI_GUARD_END
-}
-
-// array_read_ops_common.rs:20-109: subset -> intersecting chunks -> one descriptor per chunk, in
-// C order of the chunk grid; lins[k] = descriptor k's C-order linear chunk-grid index.
-// Returns ZGPU_OK, -1 for an empty subset (nothing to do), or an error status.
-static int subset_descs(uint32_t nd, const uint64_t *array_shape, const uint64_t *chunk_shape,
-                        const uint64_t *sel_start, const uint64_t *sel_shape, std::vector<zgpu_chunk_desc> &descs,
-                        std::vector<uint64_t> &lins) {
-  uint64_t grid[ZG_MAXD], lo[ZG_MAXD], hi[ZG_MAXD], idx[ZG_MAXD];
-  uint64_t nchunks = 1;
-  bool empty = false;
-  for (uint32_t d = 0; d < nd; d++) {
-    if (chunk_shape[d] == 0) return set_err(ZGPU_INVALID_ARGUMENT, "zero chunk extent");
-    if (sel_start[d] + sel_shape[d] > array_shape[d])
-      return set_err(ZGPU_INVALID_ARGUMENT, "array subset out of bounds");
-    grid[d] = (array_shape[d] + chunk_shape[d] - 1) / chunk_shape[d];
-    if (sel_shape[d] == 0) {
-      empty = true;
-      continue;
-    }
-    lo[d] = sel_start[d] / chunk_shape[d];
-    hi[d] = (sel_start[d] + sel_shape[d] - 1) / chunk_shape[d] + 1;
-    nchunks *= hi[d] - lo[d];
-    idx[d] = lo[d];
-  }
-  if (empty) return -1;
-  descs.reserve(nchunks);
-  lins.reserve(nchunks);
-  for (;;) {
-    zgpu_chunk_desc D{};
-    uint64_t lin = 0;
-    for (uint32_t d = 0; d < nd; d++) {
-      lin = lin * grid[d] + idx[d];
-      const uint64_t cs = idx[d] * chunk_shape[d], ce = cs + chunk_shape[d];
-      const uint64_t s0 = std::max(sel_start[d], cs), s1 = std::min(sel_start[d] + sel_shape[d], ce);
-      D.chunk_shape[d] = chunk_shape[d];
-      D.sel_start[d] = s0 - cs;
-      D.sel_shape[d] = s1 - s0;
-      D.out_start[d] = s0 - sel_start[d];
-    }
-    descs.push_back(D);
-    lins.push_back(lin);
-    int d = (int)nd - 1;
-    for (; d >= 0; d--) {
-      if (++idx[d] < hi[d]) break;
-      idx[d] = lo[d];
-    }
-    if (d < 0) break;
-  }
-  return ZGPU_OK;
 }
 
 int zgpu_retrieve_array_subset(zgpu_chain *ch, uint32_t nd, const uint64_t *array_shape, const uint64_t *chunk_shape,
