@@ -397,7 +397,12 @@ class C3:
         exp = np.empty(self.shape, np.float32)
         syn.synth_c3_values(_u64(self.start), _u64(self.shape), exp.ctypes.data, nt)
         self.expected = torch.from_numpy(exp).to(dev)
-        self.out = torch.empty(self.shape, dtype=torch.float32, device=dev)
+        self.full = None
+        if world > 1 and rank == 0:  # the root decodes its slab in place inside the gathered subset
+            self.full = torch.empty(self.SUB_SHAPE, dtype=torch.float32, device=dev)
+            self.out = self.full.narrow(0, 0, self.shape[0])
+        else:
+            self.out = torch.empty(self.shape, dtype=torch.float32, device=dev)
         self.out_shape = self.shape
         self.decoded_bytes = int(np.prod(self.shape)) * 4  # per rank per step
         self.parts = [(self.chain, self.descs, self.out, self.out_shape)]
@@ -410,8 +415,8 @@ class C3:
                        "shards_touched_per_gpu": n_sh, "subset_shape": self.SUB_SHAPE,
                        "slab_per_gpu": self.shape, "gzip_ratio": round(self.ratio, 3),
                        "encoded_bytes_resident_per_gpu": enc_total,
-                       "parallelism": f"axis-0 slabs x{world}" + (", RCCL gather to rank 0 in the step"
-                                                                   if world > 1 else "")}
+                       "parallelism": f"axis-0 slabs x{world}" + (", peers' slabs received straight into rank 0's "
+                                                                   "output over RCCL in the step" if world > 1 else "")}
         self.data = ("synthetic (round(256*(sin(.05x)+cos(.03y)+.5sin(.07z))+N(0,1))/256 f32, shards "
                      "written by tools/synth; decode(encode(x)) == x checked on device)")
         self.scaling = "strong"
@@ -419,7 +424,7 @@ class C3:
     def after_decode(self):
         if self.world > 1:  # C4: the requested subset spans GPUs -> one gather to the root
             from zarrs_amd.distributed import gather_slabs
-            self.gathered = gather_slabs(self.out, self.slabs, dst=0)
+            self.gathered = gather_slabs(self.out, self.slabs, dst=0, out=self.full)
 
     def check(self) -> bool:
         ok = bool(torch.equal(self.out.view(torch.int32), self.expected.view(torch.int32)))
@@ -428,13 +433,13 @@ class C3:
         return ok
 
     def cpu_baseline(self):
+        """The oracle's retrieve_array_subset of this rank's whole slab (the full C3 subset at N=1, all
+        64 shards): shards fan out over the host threads (16 threads -> 16 shards in flight, one thread
+        each: zarrs' outer/inner split, concurrency.rs:23-48, with no thread spawned per shard)."""
         sys.path.insert(0, os.path.join(ROOT, "oracle"))
         import oracle as O
         threads = _threads()
         chain = O.OracleChain.from_metadata(self.CODECS, "float32", 0.0, 3)
-        # sample: the first 2x2x2 shards' worth of the subset (a [256-56, 256-44, 256-232]... box
-        # anchored at the subset start, clipped to 256^3)
-        sub = [min(256, n) for n in self.shape]
         grid = [a // self.SHARD for a in self.ARRAY]
         ptrs = (C.c_void_p * int(np.prod(grid)))()
         lens = (C.c_uint64 * int(np.prod(grid)))()
@@ -442,15 +447,16 @@ class C3:
             lin = (si * grid[1] + sj) * grid[2] + sk
             ptrs[lin] = host.ctypes.data
             lens[lin] = host.nbytes
-        out = np.empty(sub, np.float32)
-        O.retrieve_ptrs(chain, self.ARRAY, [self.SHARD] * 3, ptrs, lens, self.start, sub, out, threads)
-        assert np.array_equal(out, self.expected[:sub[0], :sub[1], :sub[2]].cpu().numpy())
+        out = np.empty(self.shape, np.float32)
+        O.retrieve_ptrs(chain, self.ARRAY, [self.SHARD] * 3, ptrs, lens, self.start, self.shape, out, threads)
+        assert np.array_equal(out, self.expected.cpu().numpy())
         times = _time_reps(lambda: O.retrieve_ptrs(chain, self.ARRAY, [self.SHARD] * 3, ptrs, lens,
-                                                   self.start, sub, out, threads), self.args.cpu_seconds)
+                                                   self.start, self.shape, out, threads), self.args.cpu_seconds)
         t = float(np.median(times))
         return {"value": round(out.nbytes / t / 2 ** 30, 3), "unit": "GiB/s", "cores": threads, "kind": "port",
-                "sample": f"subset {sub} at {self.start} of the same shards, median of {len(times)} reps, "
-                          f"oracle retrieve_array_subset (zlib inflate) with {threads} threads"}
+                "sample": f"the whole workload: subset {self.shape} at {self.start} ({len(self.shards)} shards), "
+                          f"median of {len(times)} reps, oracle retrieve_array_subset (zlib inflate) with "
+                          f"{threads} threads"}
 
     def host_leg(self, sp):
         return None
@@ -471,7 +477,10 @@ class C5:
     CODECS = [{"name": "bytes", "configuration": {"endian": "little"}},
               {"name": "numcodecs.shuffle", "configuration": {"elementsize": 2}},
               {"name": "zstd", "configuration": {"level": 3, "checksum": False}}]
-    kernel = "k_zstd_exec_item"
+    # a step is a kernel pipeline on 4 streams: the roofline covers the whole step (HIP events around
+    # it; PMC counters summed over its dispatches). DESIGN.md §3 has the per-kernel split.
+    kernel = "zstd decode step (k_zstd_scan/lits/blocks/plan/direct/exec_item + k_scatter_rows)"
+    pmc_regex = "k_zstd|k_scatter"
     dtype = "u16"
 
     def __init__(self, args, rank, world, dev):
@@ -578,12 +587,34 @@ class C5:
         self.data = ("synthetic (background 100 + 64 Gaussian blobs amplitude <= 4000 + sqrt(mean)*N(0,1) noise, "
                      "u16, seed 42; 2x2x2 mean pyramid; decode(encode(x)) == x checked on device)")
         self.scaling = "strong"
+        # N > 1: one cross-GPU L0 subset gathered to rank 0 in every step: the middle
+        # [64, H/2, W/2] box of L0, whose chunks the LPT partition spreads over the ranks
+        self.gathered = None
+        if world > 1:
+            from zarrs_amd.distributed import chunk_boxes
+            owner = {}
+            for r, part in enumerate(lpt_partition(enc_sizes, world)):
+                for i in part:
+                    owner[i] = r
+            lin0 = {idx: i for i, (li, idx, _) in enumerate(chunks) if li == 0}
+            self.g_start = [0, shape0[1] // 4, shape0[2] // 4]
+            self.g_shape = [min(64, shape0[0]), shape0[1] // 2, shape0[2] // 2]
+            self.g_boxes = [[] for _ in range(world)]
+            for idx, b0, bs in chunk_boxes(shape0, self.CHUNKS[0], self.g_start, self.g_shape):
+                self.g_boxes[owner[lin0[idx]]].append((b0, bs))
+            self.config["gather"] = {"l0_subset_start": self.g_start, "l0_subset_shape": self.g_shape,
+                                     "bytes": int(np.prod(self.g_shape)) * 2}
 
     def after_decode(self):
-        pass
+        if self.world > 1:
+            from zarrs_amd.distributed import gather_regions
+            self.gathered = gather_regions(self.outs[0], self.g_boxes, self.g_start, self.g_shape)
 
     def check(self) -> bool:
         ok = True
+        if self.gathered is not None:
+            sl = tuple(slice(a, a + n) for a, n in zip(self.g_start, self.g_shape))
+            ok = bool(torch.equal(self.gathered, self.expected[0][sl]))
         for o, e, m in zip(self.outs, self.expected, self.masks):
             if bool(m.all()):
                 ok = ok and bool(torch.equal(o, e))
@@ -652,7 +683,8 @@ class Blosc:
     library), decoded on the GPU from HBM; per-rank chunk partition, no collective."""
     SHAPE, CHUNK = [256, 1024, 1024], [64, 256, 256]
     CNAME = "lz4"
-    kernel = "k_lz4"
+    kernel = "blosc decode step (k_blosc_info/streams, stream decoders, k_blosc_finish, k_scatter_rows)"
+    pmc_regex = "k_blosc|k_lz4|k_zstd|k_scatter"
     dtype = "u16"
 
     def codecs(self):
@@ -741,7 +773,6 @@ class Blosc:
 class BloscZstd(Blosc):
     """Same volume, blosc{zstd, clevel 5, shuffle}: zarr-python 3's BloscCodec default compressor."""
     CNAME = "zstd"
-    kernel = "k_zstd_exec_item"
 
 
 WORKLOADS = {"c1": C1, "c2": C2, "c3": C3, "c5": C5, "blosc": Blosc, "blosc-zstd": BloscZstd}
@@ -886,12 +917,14 @@ def run_gpu(args, rank, world, dev):
                 counters=counters)
 
 
-def pmc_traffic(args, kernel):
-    """HBM traffic of the dominant kernel per launch from rocprofv3 PMC counters, in two separate
-    passes (FETCH_SIZE and WRITE_SIZE cannot share one pass on gfx950), corrected as
+def pmc_traffic(args, W):
+    """HBM traffic of the dominant kernel from rocprofv3 PMC counters, in two separate passes
+    (FETCH_SIZE and WRITE_SIZE cannot share one pass on gfx950), corrected as
     /opt/skills/guides/MI355X_MICROARCH.md (HBM) prescribes: counters are in KiB; FETCH_SIZE counts
-    exactly half the bytes of a wide (16 B/lane) coalesced streaming read on gfx950 -> x2;
-    WRITE_SIZE is exact for 16-B streaming stores. Runs bench.py itself as a child under rocprofv3."""
+    exactly half the bytes of a wide (16 B/lane) coalesced streaming read on gfx950 -> x2; WRITE_SIZE
+    is exact for 16-B streaming stores. Runs bench.py itself as a child under rocprofv3. A workload
+    whose step is a kernel pipeline (W.pmc_regex, e.g. C5) reports the sum over one step's dispatches;
+    otherwise the average per launch of W.kernel."""
     import csv
     import glob
     import shutil
@@ -899,32 +932,44 @@ def pmc_traffic(args, kernel):
     import tempfile
     if not shutil.which("rocprofv3"):
         return None, "rocprofv3 not found"
+    regex = getattr(W, "pmc_regex", W.kernel)
+    per_step = hasattr(W, "pmc_regex")
+    warm, steps = 1, 2
     vals = {}
     tmp = tempfile.mkdtemp(prefix="zgpu_pmc_")
     try:
         for ctr in ("FETCH_SIZE", "WRITE_SIZE"):
             d = os.path.join(tmp, ctr)
-            cmd = ["rocprofv3", "--pmc", ctr, "--kernel-include-regex", kernel, "-d", d, "-o", "pmc",
+            cmd = ["rocprofv3", "--pmc", ctr, "--kernel-include-regex", regex, "-d", d, "-o", "pmc",
                    "--output-format", "csv", "--", sys.executable, os.path.abspath(__file__), "--child",
-                   "--workload", args.workload, "--steps", "2", "--warmup", "1", "--no-cpu",
-                   "--grid", *map(str, args.grid)]
-            r = subprocess.run(cmd, stdout=subprocess.DEVNULL, stderr=subprocess.PIPE, timeout=300)
+                   "--workload", args.workload, "--steps", str(steps), "--warmup", str(warm), "--no-cpu",
+                   "--grid", *map(str, args.grid), "--c5-scale", str(args.c5_scale)]
+            r = subprocess.run(cmd, stdout=subprocess.DEVNULL, stderr=subprocess.PIPE, timeout=600)
             if r.returncode:
-                return None, f"rocprofv3 --pmc {ctr} rc={r.returncode}: {r.stderr.decode()[-200:]}"
+                err = [ln for ln in r.stderr.decode(errors="replace").splitlines()
+                       if "simple_timer" not in ln and ln.strip()]
+                return None, f"rocprofv3 --pmc {ctr} rc={r.returncode}: {' | '.join(err[-6:])[-600:]}"
             files = glob.glob(os.path.join(d, "**", "*counter_collection.csv"), recursive=True)
+            import re
+            rx = re.compile(regex)
             v = [float(row["Counter_Value"]) for f in files for row in csv.DictReader(open(f))
-                 if kernel in row["Kernel_Name"] and row["Counter_Name"] == ctr]
+                 if rx.search(row["Kernel_Name"]) and row["Counter_Name"] == ctr]
             if not v:
-                return None, f"no {ctr} samples for {kernel}"
-            vals[ctr] = sum(v) / len(v)
+                return None, f"no {ctr} samples for {regex}"
+            vals[ctr] = sum(v) / (warm + steps) if per_step else sum(v) / len(v)
     except Exception as e:  # noqa: BLE001 - report, never fail the bench line on the profiler
         return None, f"pmc pass failed: {e}"
     finally:
         shutil.rmtree(tmp, ignore_errors=True)
     fetch = vals["FETCH_SIZE"] * 1024 * 2
     write = vals["WRITE_SIZE"] * 1024
-    return {"bytes": int(fetch + write), "fetch_bytes": int(fetch), "write_bytes": int(write),
-            "source": "rocprofv3 --pmc FETCH_SIZE / WRITE_SIZE passes (KiB; FETCH x2 on gfx950)"}, None
+    out = {"bytes": int(fetch + write), "fetch_bytes": int(fetch), "write_bytes": int(write),
+           "per": "step (all dispatches matching " + regex + ")" if per_step else "launch of " + regex,
+           "source": "rocprofv3 --pmc FETCH_SIZE / WRITE_SIZE passes (KiB; FETCH x2 on gfx950)"}
+    if per_step:
+        out["note"] = ("the x2 FETCH correction is calibrated for 16-B/lane streaming reads only; the entropy "
+                       "kernels also read with narrower loads (uncalibrated), so fetch_bytes may be overstated")
+    return out, None
 
 
 def main():
@@ -969,7 +1014,7 @@ def main():
     cpu = W.cpu_baseline() if (rank == 0 and not args.no_cpu) else None
     traffic, traffic_note = None, "skipped (--no-pmc or N>1)"
     if rank == 0 and world == 1 and not args.no_pmc:
-        traffic, traffic_note = pmc_traffic(args, W.kernel)
+        traffic, traffic_note = pmc_traffic(args, W)
     if rank == 0:
         achieved = r["alg_bytes"] / (r["ev_ms"] * 1e-3) / 1e9
         line = {

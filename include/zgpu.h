@@ -226,7 +226,7 @@ int zgpu_retrieve_array_subset_files(zgpu_chain *chain, uint32_t ndim, const uin
  * Write path: CodecChain::encode (zarrs/src/array/codec/array_to_bytes/
  * codec_chain.rs:528-555) for fixed-size chains -- transpose, bytes (endianness), numcodecs.shuffle
  * (innermost, elementsize = data type size), crc32c (end or start, any number). Compressing codecs
- * and sharding return ZGPU_UNSUPPORTED.
+ * return ZGPU_UNSUPPORTED; sharding_indexed goes through zgpu_encode_chunks (variable lengths).
  * zgpu_chain_encoded_size: encoded bytes of one chunk of chunk_shape (BytesRepresentation::FixedSize),
  * -1 if the chain's encoded size is not fixed.
  * zgpu_encode_batch: encode the chunks whose origins are descs[i].chunk_start (in elements) of the
@@ -243,6 +243,18 @@ int64_t zgpu_chain_encoded_size(const zgpu_chain *chain, uint32_t ndim, const ui
 int zgpu_encode_batch(zgpu_chain *chain, uint32_t ndim, const uint64_t *chunk_shape, const void *array,
                       const uint64_t *array_shape, const zgpu_encode_desc *descs, uint64_t n, uint32_t flags,
                       void *hip_stream);
+/*
+ * zgpu_encode_batch plus sharding_indexed over a fixed-size inner chain (ShardingCodecBound::
+ * encode_bounded, sharding_codec.rs:924-1085, with SubchunkWriteOrder::C: inner chunks in C order of
+ * the inner grid, an inner chunk equal to the fill value everywhere omitted, index bytes{endian} +
+ * crc32c at the start or end). enc_lens[n] receives each chunk's encoded length (variable for shards);
+ * descs[i].dst_cap must be >= zgpu_chain_encoded_bound. zgpu_chain_encoded_bound: the fixed size, or a
+ * shard's bounded size (every inner chunk present + index), -1 if unbounded.
+ */
+int64_t zgpu_chain_encoded_bound(const zgpu_chain *chain, uint32_t ndim, const uint64_t *chunk_shape);
+int zgpu_encode_chunks(zgpu_chain *chain, uint32_t ndim, const uint64_t *chunk_shape, const void *array,
+                       const uint64_t *array_shape, const zgpu_encode_desc *descs, uint64_t n, uint32_t flags,
+                       uint64_t *enc_lens, void *hip_stream);
 
 /*
  * HBM-resident decoded-chunk cache: ChunkCacheDecodedLruSizeLimit (zarrs/src/array/chunk_cache/

@@ -192,17 +192,22 @@ class CodecChain:
         """Encoded bytes of one chunk (fixed-size chains), -1 if variable (zgpu_chain_encoded_size)."""
         return int(L.load().zgpu_chain_encoded_size(self._h, len(chunk_shape), L.u64s(chunk_shape)))
 
+    def encoded_bound(self, chunk_shape) -> int:
+        """Upper bound of one chunk's encoded size (zgpu_chain_encoded_bound), -1 if unbounded."""
+        return int(L.load().zgpu_chain_encoded_bound(self._h, len(chunk_shape), L.u64s(chunk_shape)))
+
     def encode_chunks(self, array, chunk_shape, chunk_starts, stream=None) -> list:
         """CodecChain::encode of the chunks of a device-resident torch array whose origins are
-        chunk_starts (zgpu_encode_batch). Returns one uint8 device tensor per chunk."""
+        chunk_starts (zgpu_encode_chunks; sharding_indexed over a fixed-size inner chain included).
+        Returns one uint8 device tensor per chunk."""
         import torch
         assert array.is_cuda and array.is_contiguous()
         if array.numel() * array.element_size() != int(np.prod(array.shape)) * self.dtype.itemsize or \
                 array.element_size() != self.dtype.itemsize:
             raise L.ZgpuError(L.INVALID_ARGUMENT, f"encode: {array.dtype} tensor for a {self.data_type} chain")
-        size = self.encoded_size(chunk_shape)
+        size = self.encoded_bound(chunk_shape)
         if size < 0:
-            raise L.ZgpuError(L.UNSUPPORTED, "encode: the chain's encoded size is not fixed")
+            raise L.ZgpuError(L.UNSUPPORTED, "encode: the chain's encoded size is not bounded")
         n = len(chunk_starts)
         flat = torch.empty(max(n, 1) * ((size + 255) // 256 * 256), dtype=torch.uint8, device=array.device)
         pitch = (size + 255) // 256 * 256
@@ -213,10 +218,12 @@ class CodecChain:
             for d, v in enumerate(st):
                 descs[i].chunk_start[d] = int(v)
         stream = default_stream(stream, array)
-        rc = L.load().zgpu_encode_batch(self._h, len(chunk_shape), L.u64s(chunk_shape), array.data_ptr(),
-                                       L.u64s(list(array.shape)), descs, n, L.ENC_DEVICE | L.OUT_DEVICE, stream)
+        lens = (C.c_uint64 * max(n, 1))()
+        rc = L.load().zgpu_encode_chunks(self._h, len(chunk_shape), L.u64s(chunk_shape), array.data_ptr(),
+                                        L.u64s(list(array.shape)), descs, n, L.ENC_DEVICE | L.OUT_DEVICE, lens,
+                                        stream)
         L.check(rc)
-        return [flat[i * pitch:i * pitch + size] for i in range(n)]
+        return [flat[i * pitch:i * pitch + lens[i]] for i in range(n)]
 
     def partial_decode(self, encoded, shape, subset_start, subset_shape) -> np.ndarray:
         out = np.empty([int(s) for s in subset_shape], dtype=self.dtype)

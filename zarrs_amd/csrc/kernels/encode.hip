@@ -219,6 +219,157 @@ __global__ __launch_bounds__(ETHREADS) void k_encode_tiled(const uint64_t *__res
   }
 }
 
+// ---------------------------------------------------------------------------------------------
+// sharding_indexed encode for fixed-size inner chains (ShardingCodecBound::encode_bounded,
+// zarrs/src/array/codec/array_to_bytes/sharding/sharding_codec.rs:924-1085 with
+// SubchunkWriteOrder::C): every inner chunk is encoded by the inner chain (launch_encode_gather +
+// crc32c above) into a temporary slot of E bytes; an inner chunk whose decoded values all equal the
+// fill value is omitted (index entry (u64::MAX, u64::MAX), encode_inner_by_chunk_index :883-920);
+// the present ones are laid out back to back in C order of the inner grid after (index at start) or
+// before (index at end) the encoded index (bytes{endian} + crc32c codecs, compute_index_encoded_size).
+// ---------------------------------------------------------------------------------------------
+template <int ES>
+__global__ __launch_bounds__(256) void k_fill_check(const uint64_t *__restrict__ starts,
+                                                    const uint8_t *__restrict__ array, ZgEncode P,
+                                                    uint32_t *__restrict__ nonfill) {
+  using T = typename std::conditional<ES == 1, uint8_t, typename std::conditional<ES == 2, uint16_t,
+            typename std::conditional<ES == 4, uint32_t, typename std::conditional<ES == 8, uint2,
+            uint4>::type>::type>::type>::type;
+  const uint64_t c = blockIdx.x;
+  const uint64_t *st = starts + c * P.nd;
+  T fv;
+  __builtin_memcpy(&fv, P.fill, ES);
+  const uint32_t nd = P.nd, L = nd - 1;
+  const uint64_t ext = P.dec_shape[L], rows = P.nelem / ext;
+  bool differs = false;
+  for (uint64_t r0 = 0; r0 < rows && !differs; r0 += 256 / 64) {
+    // a wave per row (64 lanes along the innermost axis), 4 rows per pass
+    const uint64_t r = r0 + threadIdx.x / 64;
+    if (r < rows) {
+      uint64_t rem = r, off = 0;
+      bool inside = true;
+      for (int d = (int)nd - 2; d >= 0; d--) {
+        const uint64_t x = rem % P.dec_shape[d];
+        rem /= P.dec_shape[d];
+        const uint64_t ac = st[d] + x;
+        inside = inside && ac < P.array_shape[d];
+        off += ac * P.array_stride[d];
+      }
+      if (inside)
+        for (uint64_t x = threadIdx.x & 63; x < ext; x += 64) {
+          if (st[L] + x >= P.array_shape[L]) break;  // past the array edge: fill
+          const T v = *(const T *)(array + (off + st[L] + x) * ES);
+          uint32_t a[(ES + 3) / 4] = {}, b[(ES + 3) / 4] = {};
+          __builtin_memcpy(a, &v, ES);
+          __builtin_memcpy(b, &fv, ES);
+          bool ne = false;
+#pragma unroll
+          for (int w = 0; w < (ES + 3) / 4; w++) ne = ne || a[w] != b[w];
+          if (ne) {
+            differs = true;
+            break;
+          }
+        }
+    }
+    if (__syncthreads_or(differs)) differs = true;
+  }
+  if (threadIdx.x == 0) nonfill[c] = differs ? 1u : 0u;
+}
+
+struct ZgShardLayout {
+  uint64_t n_inner, E, E_pitch;  // inner chunks per shard, encoded inner size, temp slot pitch
+  uint64_t index_bytes, pre;     // encoded index size; crc32c bytes before the raw index (start crcs)
+  uint32_t at_start, big_endian;
+};
+
+// One workgroup per shard: C-order prefix sum of the present inner chunks, index entries written
+// (raw u64 pairs, endianness of the index bytes codec) into the shard at the index position; the
+// shard's length and the position of its encoded index (for the index crc32c launches) returned.
+__global__ __launch_bounds__(256) void k_shard_layout(const uint32_t *__restrict__ nonfill, ZgShardLayout Lo,
+                                                      const uint64_t *__restrict__ shard_dst,
+                                                      uint64_t *__restrict__ inner_off,
+                                                      uint64_t *__restrict__ index_ptr, uint64_t *__restrict__ shard_len) {
+  __shared__ uint64_t s_base, s_wsum[4];
+  const uint64_t sh = blockIdx.x, n = Lo.n_inner;
+  const uint32_t *nf = nonfill + sh * n;
+  uint64_t *off = inner_off + sh * n;
+  const uint64_t body0 = Lo.at_start ? Lo.index_bytes : 0;
+  if (threadIdx.x == 0) s_base = 0;
+  __syncthreads();
+  for (uint64_t k0 = 0; k0 < n; k0 += 256) {
+    const uint64_t k = k0 + threadIdx.x;
+    const uint32_t f = k < n ? nf[k] : 0u;
+    // block exclusive scan of f
+    uint32_t incl = f;
+    const uint32_t lane = threadIdx.x & 63;
+    for (int o = 1; o < 64; o <<= 1) {
+      const uint32_t u = __shfl_up(incl, o, 64);
+      if ((int)lane >= o) incl += u;
+    }
+    if (lane == 63) s_wsum[threadIdx.x / 64] = incl;
+    __syncthreads();
+    uint64_t before = s_base;
+    for (uint32_t w = 0; w < threadIdx.x / 64; w++) before += s_wsum[w];
+    before += incl - f;
+    if (k < n) off[k] = f ? body0 + before * Lo.E : ~0ull;
+    __syncthreads();
+    if (threadIdx.x == 0) s_base += s_wsum[0] + s_wsum[1] + s_wsum[2] + s_wsum[3];
+    __syncthreads();
+  }
+  const uint64_t body = s_base * Lo.E;
+  const uint64_t idx0 = Lo.at_start ? 0 : body0 + body;  // encoded index position in the shard
+  uint8_t *raw = (uint8_t *)shard_dst[sh] + idx0 + Lo.pre;
+  for (uint64_t q = threadIdx.x; q < 2 * n; q += 256) {
+    const uint64_t o = off[q / 2];
+    const uint64_t v = o == ~0ull ? ~0ull : (q & 1 ? Lo.E : o);
+#pragma unroll
+    for (int b = 0; b < 8; b++) raw[q * 8 + b] = (uint8_t)(v >> (8 * (Lo.big_endian ? 7 - b : b)));
+  }
+  if (threadIdx.x == 0) {
+    index_ptr[sh] = shard_dst[sh] + idx0;
+    shard_len[sh] = body0 + body + (Lo.at_start ? 0 : Lo.index_bytes);
+  }
+}
+
+// The present inner chunks from their temporary slots to their shard offsets: a workgroup per
+// (shard, inner chunk); dword moves when both sides allow, bytes otherwise.
+__global__ __launch_bounds__(256) void k_shard_copy(const uint8_t *__restrict__ tmp, ZgShardLayout Lo,
+                                                    const uint64_t *__restrict__ shard_dst,
+                                                    const uint64_t *__restrict__ inner_off) {
+  const uint64_t g = blockIdx.x, sh = g / Lo.n_inner;
+  const uint64_t o = inner_off[g];
+  if (o == ~0ull) return;
+  const uint8_t *src = tmp + g * Lo.E_pitch;
+  uint8_t *dst = (uint8_t *)shard_dst[sh] + o;
+  if ((((uintptr_t)dst | Lo.E) & 3) == 0) {
+    const uint32_t *s4 = (const uint32_t *)src;
+    uint32_t *d4 = (uint32_t *)dst;
+    for (uint64_t k = threadIdx.x; k < Lo.E / 4; k += 256) d4[k] = s4[k];
+  } else {
+    for (uint64_t k = threadIdx.x; k < Lo.E; k += 256) dst[k] = src[k];
+  }
+}
+
+hipError_t launch_shard_encode(const uint64_t *starts, const uint8_t *array, const ZgEncode &inner, uint32_t n_chunks,
+                               uint32_t *nonfill, const uint8_t *tmp, const ZgShardLayoutArgs &A,
+                               const uint64_t *shard_dst, uint64_t *inner_off, uint64_t *index_ptr,
+                               uint64_t *shard_len, uint32_t n_shards, hipStream_t s) {
+  if (!n_chunks) return hipSuccess;
+  switch (inner.es) {
+    case 1: hipLaunchKernelGGL(k_fill_check<1>, dim3(n_chunks), dim3(256), 0, s, starts, array, inner, nonfill); break;
+    case 2: hipLaunchKernelGGL(k_fill_check<2>, dim3(n_chunks), dim3(256), 0, s, starts, array, inner, nonfill); break;
+    case 4: hipLaunchKernelGGL(k_fill_check<4>, dim3(n_chunks), dim3(256), 0, s, starts, array, inner, nonfill); break;
+    case 8: hipLaunchKernelGGL(k_fill_check<8>, dim3(n_chunks), dim3(256), 0, s, starts, array, inner, nonfill); break;
+    case 16: hipLaunchKernelGGL(k_fill_check<16>, dim3(n_chunks), dim3(256), 0, s, starts, array, inner, nonfill); break;
+    default: return hipErrorInvalidValue;
+  }
+  const ZgShardLayout Lo{A.n_inner, A.E, A.E_pitch, A.index_bytes, A.pre, A.at_start, A.big_endian};
+  hipLaunchKernelGGL(k_shard_layout, dim3(n_shards), dim3(256), 0, s, nonfill, Lo, shard_dst, inner_off, index_ptr,
+                     shard_len);
+  hipLaunchKernelGGL(k_shard_copy, dim3(n_chunks), dim3(256), 0, s, tmp, Lo, shard_dst, inner_off);
+  return hipGetLastError();
+}
+
 hipError_t launch_encode_gather(const uint64_t *dsts, const uint64_t *starts, const uint8_t *array,
                                 const ZgEncode &P, uint32_t n_chunks, hipStream_t s) {
   const uint64_t total = (uint64_t)n_chunks * P.nelem;

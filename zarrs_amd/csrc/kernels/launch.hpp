@@ -98,6 +98,18 @@ hipError_t launch_encode_gather(const uint64_t *dsts, const uint64_t *starts, co
                                 const ZgEncode &P, uint32_t n_chunks, hipStream_t s);
 hipError_t launch_crc32c_encode(const uint64_t *dsts, uint32_t n, uint64_t lo, uint64_t len, int at_start,
                                 hipStream_t s);
+// sharding_indexed encode of fixed-size inner chains: fill check of every inner chunk (geometry of
+// `inner`, origins `starts`), C-order layout + raw index per shard, copy of the encoded inner chunks
+// (temporary slots of E_pitch bytes) into the shards. The index crc32c codecs run afterwards
+// (launch_crc32c_encode over index_ptr).
+struct ZgShardLayoutArgs {
+  uint64_t n_inner, E, E_pitch, index_bytes, pre;
+  uint32_t at_start, big_endian;
+};
+hipError_t launch_shard_encode(const uint64_t *starts, const uint8_t *array, const ZgEncode &inner, uint32_t n_chunks,
+                               uint32_t *nonfill, const uint8_t *tmp, const ZgShardLayoutArgs &A,
+                               const uint64_t *shard_dst, uint64_t *inner_off, uint64_t *index_ptr,
+                               uint64_t *shard_len, uint32_t n_shards, hipStream_t s);
 
 // blosc (c-blosc 1.x frames): stream table built on the device, sized on the host from BlInfo
 enum : uint32_t { BL_COMP_BLOSCLZ = 0, BL_COMP_LZ4 = 1, BL_COMP_ZSTD = 4, BL_COMP_MEMCPY = 0x100, BL_COMP_SKIP = 0xFFFFFFFFu };

@@ -2010,7 +2010,10 @@ namespace {
 #define ZG_XRING 65536
 #endif
 constexpr uint32_t XRING = ZG_XRING, XRMASK = XRING - 1;
-constexpr uint32_t XSTAGE_V = 512;  // staged far-source vectors (16 B) per batch
+#ifndef ZG_XSTAGE_V
+#define ZG_XSTAGE_V 512
+#endif
+constexpr uint32_t XSTAGE_V = ZG_XSTAGE_V;  // staged far-source vectors (16 B) per batch
 constexpr uint32_t XPL = 32;        // bytes of a short match its own lane copies (the rest: the wave)
 constexpr int XR_LIT = ZBATCH / 16 / 64 + 1, XR_FAR = XSTAGE_V / 64;
 

@@ -1302,19 +1302,36 @@ int64_t zgpu_chain_encoded_size(const zgpu_chain *ch, uint32_t nd, const uint64_
   return chain_fixed_encoded_size(*ch->chain, n);
 }
 
-// CodecChain::encode (codec_chain.rs:528-555) of n chunks of one device-resident C-order array into
-// device buffers: one gather (transposes + endianness + innermost shuffle, fill past the array edge),
-// then one k_crc32c_encode launch per crc32c codec.
-int zgpu_encode_batch(zgpu_chain *ch, uint32_t nd, const uint64_t *chunk_shape, const void *array,
-                      const uint64_t *array_shape, const zgpu_encode_desc *descs, uint64_t n, uint32_t flags,
-                      void *stream) {
-  ABI_GUARD_BEGIN
-  if (!ch || !chunk_shape || !array || !array_shape || (n && !descs))
-    return set_err(ZGPU_INVALID_ARGUMENT, "NULL argument");
-  if (nd == 0 || nd > ZGPU_MAX_DIMS) return set_err(ZGPU_INVALID_ARGUMENT, "ndim out of range");
-  if ((flags & (ZGPU_ENC_DEVICE | ZGPU_OUT_DEVICE)) != (ZGPU_ENC_DEVICE | ZGPU_OUT_DEVICE))
-    return set_err(ZGPU_INVALID_ARGUMENT, "encode: array and destinations must be device memory");
+// Upper bound of one chunk's encoded size: the fixed size, or for sharding_indexed over a fixed-size
+// inner chain every inner chunk present plus the index (ShardingCodec::encoded_shard_bounded_size,
+// sharding_codec.rs:924-945, BytesRepresentation::BoundedSize); -1 if unbounded.
+int64_t zgpu_chain_encoded_bound(const zgpu_chain *ch, uint32_t nd, const uint64_t *chunk_shape) {
+  if (!ch || !chunk_shape || nd == 0 || nd > ZGPU_MAX_DIMS) return -1;
   const Chain &c = *ch->chain;
+  if (c.a2b.kind != CodecKind::Sharding) return zgpu_chain_encoded_size(ch, nd, chunk_shape);
+  if (!c.a2a.empty() || !c.b2b.empty() || c.a2b.inner_shape.size() != nd) return -1;
+  uint64_t n_inner = 1, inner_n = 1;
+  for (uint32_t d = 0; d < nd; d++) {
+    const uint64_t is = c.a2b.inner_shape[d];
+    if (chunk_shape[d] % is) return -1;
+    n_inner *= chunk_shape[d] / is;
+    inner_n *= is;
+  }
+  const int64_t E = chain_fixed_encoded_size(*c.a2b.inner, inner_n);
+  const int64_t X = chain_fixed_encoded_size(*c.a2b.index, n_inner * 2);
+  if (E < 0 || X < 0) return -1;
+  return (int64_t)n_inner * E + X;
+}
+
+}  // extern "C"
+
+// CodecChain::encode (codec_chain.rs:528-555) of a fixed-size chain for n chunks of a device array
+// into device buffers h_dst[i] (chunk origins h_starts[i*nd..]): one gather (transposes + endianness +
+// innermost shuffle, fill past the array edge), then one k_crc32c_encode launch per crc32c codec.
+// Enqueues only (no synchronisation); d_tab: device table of n dst pointers + n*nd origins.
+static int encode_fixed(zgpu_ctx *C, const Chain &c, uint32_t nd, const uint64_t *chunk_shape, const void *array,
+                        const uint64_t *array_shape, const std::vector<uint64_t> &h_tab, uint64_t n,
+                        std::vector<void *> &owned, hipStream_t s, ZgEncode *out_P = nullptr) {
   if (c.a2b.kind != CodecKind::Bytes) return set_err(ZGPU_UNSUPPORTED, "encode: array->bytes codec must be bytes");
   for (const Codec &k : c.a2a)
     if (k.order.size() != nd) return set_err(ZGPU_INVALID_ARGUMENT, "transpose order rank != ndim");
@@ -1364,45 +1381,171 @@ int zgpu_encode_batch(zgpu_chain *ch, uint32_t nd, const uint64_t *chunk_shape, 
     }
   }
   std::memcpy(P.fill, c.fill, sizeof(P.fill));
-  const int64_t enc_size = chain_fixed_encoded_size(c, P.nelem);
   bool aligned = (P.data_off % c.es) == 0;
-  std::vector<uint64_t> h(n * (1 + nd));
-  for (uint64_t i = 0; i < n; i++) {
-    if (!descs[i].dst || descs[i].dst_cap < (uint64_t)enc_size)
-      return set_err(ZGPU_INVALID_ARGUMENT, "encode: destination missing or smaller than the encoded size");
+  for (uint64_t i = 0; i < n; i++)
+    if (h_tab[i] % 16) aligned = false;
+  P.aligned = aligned;
+  if (out_P) *out_P = P;
+  if (!n) return ZGPU_OK;
+  uint64_t *d = (uint64_t *)C->dev_alloc(h_tab.size() * 8);
+  owned.push_back(d);
+  HIPCHK(hipMemcpyAsync(d, h_tab.data(), h_tab.size() * 8, hipMemcpyHostToDevice, s));
+  HIPCHK(launch_encode_gather(d, d + n, (const uint8_t *)array, P, (uint32_t)n, s));
+  uint64_t lo = P.data_off, len = P.nelem * c.es;
+  for (const Codec &k : c.b2b) {
+    if (k.kind != CodecKind::Crc32c) continue;
+    HIPCHK(launch_crc32c_encode(d, (uint32_t)n, lo, len, k.at_start ? 1 : 0, s));
+    if (k.at_start) lo -= 4;
+    len += 4;
+  }
+  return ZGPU_OK;
+}
+
+// sharding_indexed over a fixed-size inner chain (ShardingCodecBound::encode_bounded,
+// sharding_codec.rs:924-1085, SubchunkWriteOrder::C): all inner chunks of all shards encoded into
+// temporary slots in one batch, all-fill inner chunks omitted, the rest laid out in C order with the
+// encoded index at the start or the end; shard lengths to enc_lens.
+static int encode_sharded(zgpu_ctx *C, const Chain &top, uint32_t nd, const uint64_t *shard_shape, const void *array,
+                          const uint64_t *array_shape, const zgpu_encode_desc *descs, uint64_t n, uint64_t *enc_lens,
+                          std::vector<void *> &owned, hipStream_t s) {
+  const Chain &inner = *top.a2b.inner, &xc = *top.a2b.index;
+  if (!top.a2a.empty() || !top.b2b.empty())
+    return set_err(ZGPU_UNSUPPORTED, "encode: codecs around sharding_indexed");
+  if (top.a2b.inner_shape.size() != nd) return set_err(ZGPU_INVALID_ARGUMENT, "sharding chunk_shape rank");
+  if (xc.a2b.kind != CodecKind::Bytes || !xc.a2a.empty())
+    return set_err(ZGPU_UNSUPPORTED, "index_codecs must be bytes (+crc32c)");
+  for (const Codec &k : xc.b2b)
+    if (k.kind != CodecKind::Crc32c) return set_err(ZGPU_UNSUPPORTED, "index_codecs must be bytes (+crc32c)");
+  uint64_t cps[ZG_MAXD], n_inner = 1, inner_n = 1;
+  for (uint32_t d = 0; d < nd; d++) {
+    const uint64_t is = top.a2b.inner_shape[d];
+    if (shard_shape[d] % is) return set_err(ZGPU_INVALID_ARGUMENT, "shard shape not a multiple of chunk_shape");
+    cps[d] = shard_shape[d] / is;
+    n_inner *= cps[d];
+    inner_n *= is;
+  }
+  const int64_t E = chain_fixed_encoded_size(inner, inner_n);
+  if (E < 0) return set_err(ZGPU_UNSUPPORTED, "encode: the inner chain of sharding_indexed must be fixed-size");
+  const int64_t X = chain_fixed_encoded_size(xc, n_inner * 2);
+  const uint64_t bound = n_inner * (uint64_t)E + (uint64_t)X;
+  for (uint64_t i = 0; i < n; i++)
+    if (!descs[i].dst || descs[i].dst_cap < bound)
+      return set_err(ZGPU_INVALID_ARGUMENT, "encode: destination missing or smaller than the shard's bounded size");
+  const uint64_t pitch = ((uint64_t)E + 255) & ~(uint64_t)255, n_chunks = n * n_inner;
+  uint8_t *tmp = (uint8_t *)C->dev_alloc(std::max<uint64_t>(n_chunks * pitch, 1));
+  owned.push_back(tmp);
+  // inner chunk k of shard i: dst slot, origin in the array
+  std::vector<uint64_t> tab(n_chunks * (1 + nd));
+  for (uint64_t i = 0; i < n; i++)
+    for (uint64_t k = 0; k < n_inner; k++) {
+      const uint64_t g = i * n_inner + k;
+      tab[g] = (uint64_t)(tmp + g * pitch);
+      uint64_t rem = k;
+      for (int d = (int)nd - 1; d >= 0; d--) {
+        tab[n_chunks + g * nd + d] = descs[i].chunk_start[d] + (rem % cps[d]) * top.a2b.inner_shape[d];
+        rem /= cps[d];
+      }
+    }
+  ZgEncode IP{};
+  int rc = encode_fixed(C, inner, nd, top.a2b.inner_shape.data(), array, array_shape, tab, n_chunks, owned, s, &IP);
+  if (rc) return rc;
+  const uint64_t *d_tab = (const uint64_t *)owned.back();  // [dst slots | origins] on the device
+  // per-shard tables: dst pointers, inner offsets, index positions, lengths; fill flags
+  uint64_t *d_sh = (uint64_t *)C->dev_alloc(8 * (3 * n + n_chunks));
+  uint32_t *d_nf = (uint32_t *)C->dev_alloc(4 * std::max<uint64_t>(n_chunks, 1));
+  owned.push_back(d_sh);
+  owned.push_back(d_nf);
+  std::vector<uint64_t> hd(n);
+  for (uint64_t i = 0; i < n; i++) hd[i] = (uint64_t)descs[i].dst;
+  HIPCHK(hipMemcpyAsync(d_sh, hd.data(), 8 * n, hipMemcpyHostToDevice, s));
+  uint64_t *d_index_ptr = d_sh + n, *d_len = d_sh + 2 * n, *d_off = d_sh + 3 * n;
+  int n_pre = 0;
+  for (const Codec &k : xc.b2b) n_pre += k.at_start ? 1 : 0;
+  ZgShardLayoutArgs A{n_inner, (uint64_t)E, pitch, (uint64_t)X, 4ull * n_pre, top.a2b.at_start ? 1u : 0u,
+                      xc.a2b.big_endian ? 1u : 0u};
+  HIPCHK(launch_shard_encode(d_tab + n_chunks, (const uint8_t *)array, IP, (uint32_t)n_chunks, d_nf, tmp, A, d_sh, d_off,
+                             d_index_ptr, d_len, (uint32_t)n, s));
+  uint64_t lo = 4ull * n_pre, len = n_inner * 16;
+  for (const Codec &k : xc.b2b) {
+    HIPCHK(launch_crc32c_encode(d_index_ptr, (uint32_t)n, lo, len, k.at_start ? 1 : 0, s));
+    if (k.at_start) lo -= 4;
+    len += 4;
+  }
+  HIPCHK(hipMemcpyAsync(enc_lens, d_len, 8 * n, hipMemcpyDeviceToHost, s));
+  return ZGPU_OK;
+}
+
+extern "C" {
+
+int zgpu_encode_chunks(zgpu_chain *ch, uint32_t nd, const uint64_t *chunk_shape, const void *array,
+                       const uint64_t *array_shape, const zgpu_encode_desc *descs, uint64_t n, uint32_t flags,
+                       uint64_t *enc_lens, void *stream) {
+  ABI_GUARD_BEGIN
+  if (!ch || !chunk_shape || !array || !array_shape || (n && !descs))
+    return set_err(ZGPU_INVALID_ARGUMENT, "NULL argument");
+  if (nd == 0 || nd > ZGPU_MAX_DIMS) return set_err(ZGPU_INVALID_ARGUMENT, "ndim out of range");
+  if ((flags & (ZGPU_ENC_DEVICE | ZGPU_OUT_DEVICE)) != (ZGPU_ENC_DEVICE | ZGPU_OUT_DEVICE))
+    return set_err(ZGPU_INVALID_ARGUMENT, "encode: array and destinations must be device memory");
+  const Chain &c = *ch->chain;
+  for (uint64_t i = 0; i < n; i++)
     for (uint32_t d = 0; d < nd; d++)
       if (descs[i].chunk_start[d] >= array_shape[d])
         return set_err(ZGPU_INVALID_ARGUMENT, "encode: chunk origin outside the array");
-    h[i] = (uint64_t)descs[i].dst;
-    if (h[i] % 16) aligned = false;
-    for (uint32_t d = 0; d < nd; d++) h[n + i * nd + d] = descs[i].chunk_start[d];
-  }
-  P.aligned = aligned;
   zgpu_ctx *C = ch->ctx;
   std::lock_guard<std::mutex> lk(C->mu);
   HIPCHK(hipSetDevice(C->device));
   hipStream_t s = pick_stream(C, stream);
   if (!n) return ZGPU_OK;
-  uint64_t *d = (uint64_t *)C->dev_alloc(h.size() * 8);
+  std::vector<void *> owned;
+  int rc = 0;
   try {
-    HIPCHK(hipMemcpyAsync(d, h.data(), h.size() * 8, hipMemcpyHostToDevice, s));
-    HIPCHK(launch_encode_gather(d, d + n, (const uint8_t *)array, P, (uint32_t)n, s));
-    uint64_t lo = P.data_off, len = P.nelem * c.es;
-    for (const Codec &k : c.b2b) {
-      if (k.kind != CodecKind::Crc32c) continue;
-      HIPCHK(launch_crc32c_encode(d, (uint32_t)n, lo, len, k.at_start ? 1 : 0, s));
-      if (k.at_start) lo -= 4;
-      len += 4;
+    if (c.a2b.kind == CodecKind::Sharding) {
+      uint64_t *hl = (uint64_t *)C->host_alloc(8 * n);
+      rc = encode_sharded(C, c, nd, chunk_shape, array, array_shape, descs, n, hl, owned, s);
+      HIPCHK(hipStreamSynchronize(s));
+      if (!rc && enc_lens) std::memcpy(enc_lens, hl, 8 * n);
+      C->host_free(hl);
+    } else {
+      const int64_t enc_size = chain_fixed_encoded_size(c, [&] {
+        uint64_t e = 1;
+        for (uint32_t d = 0; d < nd; d++) e *= chunk_shape[d];
+        return e;
+      }());
+      if (enc_size < 0 && c.a2b.kind == CodecKind::Bytes)
+        rc = set_err(ZGPU_UNSUPPORTED, "encode: only transpose / bytes / numcodecs.shuffle (innermost, elementsize = "
+                                       "data type size) / crc32c, or sharding_indexed over such a chain, run on "
+                                       "the GPU write path");
+      for (uint64_t i = 0; i < n && !rc; i++)
+        if (!descs[i].dst || descs[i].dst_cap < (uint64_t)std::max<int64_t>(enc_size, 0))
+          rc = set_err(ZGPU_INVALID_ARGUMENT, "encode: destination missing or smaller than the encoded size");
+      if (!rc) {
+        std::vector<uint64_t> tab(n * (1 + nd));
+        for (uint64_t i = 0; i < n; i++) {
+          tab[i] = (uint64_t)descs[i].dst;
+          for (uint32_t d = 0; d < nd; d++) tab[n + i * nd + d] = descs[i].chunk_start[d];
+        }
+        rc = encode_fixed(C, c, nd, chunk_shape, array, array_shape, tab, n, owned, s);
+        HIPCHK(hipStreamSynchronize(s));
+        if (!rc && enc_lens)
+          for (uint64_t i = 0; i < n; i++) enc_lens[i] = (uint64_t)enc_size;
+      }
     }
-    HIPCHK(hipStreamSynchronize(s));
   } catch (...) {
     (void)hipStreamSynchronize(s);
-    C->dev_free(d);
+    for (void *p : owned) C->dev_free(p);
     throw;
   }
-  C->dev_free(d);
-  return ZGPU_OK;
+  for (void *p : owned) C->dev_free(p);
+  return rc;
   ABI_GUARD_END
+}
+
+int zgpu_encode_batch(zgpu_chain *ch, uint32_t nd, const uint64_t *chunk_shape, const void *array,
+                      const uint64_t *array_shape, const zgpu_encode_desc *descs, uint64_t n, uint32_t flags,
+                      void *hip_stream) {
+  if (ch && ch->chain->a2b.kind == CodecKind::Sharding)
+    return set_err(ZGPU_INVALID_ARGUMENT, "encode: sharding_indexed chunks have variable lengths: zgpu_encode_chunks");
+  return zgpu_encode_chunks(ch, nd, chunk_shape, array, array_shape, descs, n, flags, nullptr, hip_stream);
 }
 
 int zgpu_retrieve_array_subset_files(zgpu_chain *ch, uint32_t nd, const uint64_t *array_shape,
