@@ -165,7 +165,10 @@ uint64_t zgpu_plan_algorithmic_bytes(const zgpu_plan *plan);
 #define ZGPU_CTR_ENC_BYTES 0     /* encoded bytes read (resolved inner-chunk ranges of sharded items) */
 #define ZGPU_CTR_ZSTD_SERIAL 1   /* zstd items decoded by the serial one-wave fallback decoder     */
 #define ZGPU_CTR_ZSTD_PARALLEL 2 /* zstd items decoded by the block-parallel pipeline              */
-#define ZGPU_N_COUNTERS 3
+#define ZGPU_CTR_BLOSC_RERUN 3   /* 1 when a blosc input outgrew the stream-table layout recorded by
+                                    the plan's first execution and the execution was re-run with a
+                                    read-back layout (later executions are asynchronous otherwise) */
+#define ZGPU_N_COUNTERS 4
 uint32_t zgpu_plan_counters(const zgpu_plan *plan, uint64_t *out, uint32_t n);
 uint32_t zgpu_last_counters(uint64_t *out, uint32_t n);
 

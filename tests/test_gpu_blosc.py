@@ -175,3 +175,52 @@ def test_blosc_inside_sharding_vs_oracle(ctx, torch_cuda, cname):
     for start, sub in (([0, 0, 0], shape), ([5, 17, 3], [60, 40, 29])):
         exp = O.retrieve_array_subset(co, shape, cs, chunks, start, sub, nthreads=4)
         assert arr.retrieve_array_subset(start, sub).tobytes() == exp.tobytes(), (start, sub)
+
+
+@pytest.mark.parametrize("cname", ["lz4", "zstd", "blosclz"])
+def test_blosc_plan_cached_layout_and_rerun(ctx, torch_cuda, cname):
+    """A plan's first execution reads the blosc headers back and records the stream-table sizes; later
+    executions lay the table out on the device (no host round trip). Rewriting the device inputs in
+    place with frames of more blocks / streams (smaller blocksize, shuffle split) makes the recorded
+    layout too small: that execution is re-run with a read-back layout (ZGPU_CTR_BLOSC_RERUN = 1)
+    and is still bit-exact; a smaller layout afterwards fits the larger capacities (inert tails)."""
+    import ctypes as C
+    from zarrs_amd import CodecChain, make_desc
+    from zarrs_amd import _lib as L
+    rng = np.random.default_rng(3)
+    n, nchunk = 20000, 4
+    datas = [_data(rng, n, 2) for _ in range(nchunk)]
+    variants = []  # (blocksize, shuffle): few blocks -> many blocks and split streams -> few again
+    for bsz, sh in ((0, "noshuffle"), (1024, "shuffle"), (4096, "noshuffle")):
+        codecs = [{"name": "bytes", "configuration": {"endian": "little"}}, _blosc(cname, sh, 2, bsz)]
+        co = O.OracleChain.from_metadata(codecs, "uint16", 0, 1)
+        variants.append([co.encode(d) for d in datas])
+    cap = max(len(e) for v in variants for e in v)
+    bufs = [torch_cuda.zeros(cap, dtype=torch_cuda.uint8, device="cuda") for _ in range(nchunk)]
+    ch = CodecChain.from_metadata([{"name": "bytes", "configuration": {"endian": "little"}},
+                                   _blosc(cname, "shuffle", 2)], "uint16", 0, ctx)
+    descs = [make_desc(b, [n], out_start=[k * n]) for k, b in enumerate(bufs)]
+    arr = (L.ChunkDesc * nchunk)(*descs)
+    plan = C.c_void_p()
+    L.check(L.load().zgpu_plan_create(ch._h, 1, arr, nchunk, L.u64s([nchunk * n]), L.ENC_DEVICE | L.OUT_DEVICE,
+                                      C.byref(plan)))
+    out = torch_cuda.empty(nchunk * n, dtype=torch_cuda.int16, device="cuda")
+    st = (C.c_int32 * nchunk)()
+    ctr = (C.c_uint64 * L.N_COUNTERS)()
+    exp = np.concatenate(datas).view(np.int16)
+    try:
+        # (variant, expected rerun flag): first run reads back; same layout cached; grows -> rerun;
+        # shrinks -> fits; back to the first -> fits
+        for v, rerun in ((0, 0), (0, 0), (1, 1), (1, 0), (2, 0), (0, 0)):
+            for b, e in zip(bufs, variants[v]):
+                b.zero_()
+                b[: len(e)] = torch_cuda.frombuffer(bytearray(e), dtype=torch_cuda.uint8).cuda()
+            out.fill_(-1)
+            torch_cuda.cuda.synchronize()
+            L.check(L.load().zgpu_plan_execute(plan, out.data_ptr(), st, None))
+            assert list(st) == [0] * nchunk, v
+            assert np.array_equal(out.cpu().numpy(), exp), v
+            L.load().zgpu_plan_counters(plan, ctr, L.N_COUNTERS)
+            assert ctr[L.CTR_BLOSC_RERUN] == rerun, (v, list(ctr))
+    finally:
+        L.load().zgpu_plan_destroy(plan)

@@ -39,8 +39,8 @@ EXPORTS = [
     "zgpu_cache_retrieve_array_subset", "zgpu_retrieve_array_subset_dlpack", "zgpu_chain_encoded_bound",
     "zgpu_encode_chunks",
 ]
-CTR_ENC_BYTES, CTR_ZSTD_SERIAL, CTR_ZSTD_PARALLEL = range(3)
-N_COUNTERS = 3
+CTR_ENC_BYTES, CTR_ZSTD_SERIAL, CTR_ZSTD_PARALLEL, CTR_BLOSC_RERUN = range(4)
+N_COUNTERS = 4
 
 
 class ChunkDesc(C.Structure):

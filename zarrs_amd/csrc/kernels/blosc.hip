@@ -14,7 +14,9 @@
 //
 // GPU decomposition (one plan stage, items = the chain's leaf chunks):
 //   k_blosc_info     one thread per item: header checks, #blocks, #streams, compressor (read back
-//                    to the host to size the stream table)
+//                    to the host to size the stream table on a plan's first execution)
+//   k_blosc_layout   later executions: the table's layout as device prefix sums, checked against the
+//                    capacities the first execution recorded (no host round trip)
 //   k_blosc_streams  one wave per item: walks bstarts + split sizes in parallel over blocks, writes
 //                    one ZgItem per compressed stream (+ its kind) and one record per block
 //   zstd streams     the block-parallel zstd pipeline (launch_zstd) over the stream table
@@ -81,13 +83,68 @@ __global__ __launch_bounds__(64) void k_blosc_info(const ZgItem *items, uint32_t
   info[i] = r;
 }
 
+// The stream table's layout on the device (one workgroup): per-item {first stream, first block} as
+// exclusive prefix sums of BlInfo, checked against the capacities of a cached layout. Entries past
+// this execution's totals are made inert (skipped streams, empty blocks); on overflow every entry is,
+// *ovf is set and the host re-runs the plan with a read-back layout (plan_statuses).
+__global__ __launch_bounds__(1024) void k_blosc_layout(const BlInfo *info, uint32_t n_items, uint64_t *bases,
+                                                       BlCaps caps, uint32_t *sub_status, uint32_t *sub_kind,
+                                                       BlBlock *blocks, unsigned long long *ovf) {
+  __shared__ uint64_t ssub[1024], sblk[1024];
+  __shared__ uint32_t s_ne, s_kinds;
+  const uint32_t t = threadIdx.x;
+  if (t == 0) s_ne = 0, s_kinds = 0;
+  const uint32_t per = (n_items + 1023) / 1024, i0 = min(t * per, n_items), i1 = min(i0 + per, n_items);
+  uint64_t nsub = 0, nblk = 0;
+  uint32_t ne = 0, kinds = 0;
+  for (uint32_t i = i0; i < i1; i++) {
+    const BlInfo I = info[i];
+    if (I.comp == BL_COMP_SKIP) continue;
+    nsub += I.nsub;
+    nblk += I.nblk;
+    ne = max(ne, I.max_ne);
+    if (I.nsub) kinds |= I.comp == BL_COMP_ZSTD ? BL_HAS_ZSTD : I.comp == BL_COMP_LZ4 ? BL_HAS_LZ4
+                        : I.comp == BL_COMP_BLOSCLZ ? BL_HAS_BLOSCLZ : 0u;
+  }
+  ssub[t] = nsub;
+  sblk[t] = nblk;
+  __syncthreads();
+  if (ne) atomicMax(&s_ne, ne);
+  if (kinds) atomicOr(&s_kinds, kinds);
+  for (uint32_t off = 1; off < 1024; off <<= 1) {  // inclusive scans
+    const uint64_t a = t >= off ? ssub[t - off] : 0, b = t >= off ? sblk[t - off] : 0;
+    __syncthreads();
+    ssub[t] += a;
+    sblk[t] += b;
+    __syncthreads();
+  }
+  uint64_t bs = ssub[t] - nsub, bb = sblk[t] - nblk;
+  for (uint32_t i = i0; i < i1; i++) {
+    const BlInfo I = info[i];
+    bases[2 * i] = bs;
+    bases[2 * i + 1] = bb;
+    if (I.comp == BL_COMP_SKIP) continue;
+    bs += I.nsub;
+    bb += I.nblk;
+  }
+  const uint64_t tot_sub = ssub[1023], tot_blk = sblk[1023];
+  const bool over = tot_sub > caps.n_sub || tot_blk > caps.n_blk || s_ne > caps.max_ne || (s_kinds & ~caps.kinds);
+  if (over && t == 0) *ovf = 1ull;
+  for (uint64_t k = over ? t : tot_sub + t; k < caps.n_sub; k += 1024) {
+    sub_status[k] = BL_SKIP;
+    sub_kind[k] = BL_KIND_RAW;
+  }
+  for (uint64_t k = over ? t : tot_blk + t; k < caps.n_blk; k += 1024)
+    blocks[k] = BlBlock{0, 0, 0, 0, 0, 0, 0, 1, 1};
+}
+
 __global__ __launch_bounds__(64) void k_blosc_streams(ZgItem *items, uint32_t *status, const BlInfo *info,
                                                       const uint64_t *bases, ZgItem *subs, uint32_t *sub_status,
                                                       uint32_t *sub_kind, BlBlock *blocks, uint8_t *dst,
-                                                      uint64_t slot_bytes) {
+                                                      uint64_t slot_bytes, const unsigned long long *ovf) {
   const uint32_t item = blockIdx.x, lane = threadIdx.x;
   const BlInfo I = info[item];
-  if (I.comp == BL_COMP_SKIP || status[item]) return;
+  if (I.comp == BL_COMP_SKIP || status[item] || *ovf) return;
   const ZgItem it = items[item];
   const uint8_t *h = (const uint8_t *)it.src;
   const uint64_t sub0 = bases[2 * item], blk0 = bases[2 * item + 1];
@@ -413,11 +470,19 @@ hipError_t launch_blosc_info(const ZgItem *items, uint32_t *status, uint32_t n_i
   return hipGetLastError();
 }
 
+hipError_t launch_blosc_layout(const BlInfo *info, uint32_t n_items, uint64_t *bases, const BlCaps &caps,
+                               const BlDecode &D, hipStream_t s) {
+  if (!n_items) return hipSuccess;
+  hipLaunchKernelGGL(k_blosc_layout, dim3(1), dim3(1024), 0, s, info, n_items, bases, caps, D.sub_status, D.sub_kind,
+                     D.blocks, D.ovf);
+  return hipGetLastError();
+}
+
 hipError_t launch_blosc_decode(ZgItem *items, uint32_t *status, uint32_t n_items, const BlInfo *info,
                                const BlDecode &D, uint8_t *dst, uint64_t slot_bytes, hipStream_t s) {
   if (!n_items) return hipSuccess;
   hipLaunchKernelGGL(k_blosc_streams, dim3(n_items), dim3(64), 0, s, items, status, info, D.bases, D.subs,
-                     D.sub_status, D.sub_kind, D.blocks, dst, slot_bytes);
+                     D.sub_status, D.sub_kind, D.blocks, dst, slot_bytes, D.ovf);
   if (D.n_zstd) {
     hipError_t e = launch_zstd(D.subs, D.sub_status, (uint32_t)D.n_sub, D.tmp, D.sub_slot, D.zs, s);
     if (e != hipSuccess) return e;

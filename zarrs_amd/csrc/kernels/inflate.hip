@@ -16,7 +16,10 @@
 //    distances, each entry already holding the decoded meaning (literal byte, or length/distance base
 //    + extra-bit count). Longer codes (rare) take a canonical count/first slow path. Tables are built
 //    cooperatively by the 64 lanes (ballot ranks + parallel root fill).
-//  * Decoded symbols are recorded one per lane (up to 64 per batch), then executed in parallel:
+//  * Symbol decode: every lane decodes the whole symbol (code, extra bits, distance) that would start
+//    at its bit offset of a 64-bit lookahead window; a scalar walk chains the advances with one
+//    readlane per symbol, and the chained symbols are compacted into an LDS record array.
+//  * Decoded symbols (up to 64 per batch, one per lane) are then executed in parallel:
 //    a wave prefix sum places them, literals are written at once, each match is copied by all lanes
 //    (out[p+i] = out[p-d+(i mod d)], so overlapping copies need no serialisation), through a 16 KiB
 //    LDS ring that holds the recent output; sources older than the ring come from the flushed output
@@ -46,7 +49,7 @@ __device__ unsigned long long g_prof[8];
 namespace {
 
 #ifndef ZG_INFLATE_RING
-#define ZG_INFLATE_RING 4096
+#define ZG_INFLATE_RING 2048
 #endif
 // LDS ring of recent output (power of two). Small on purpose: LDS per wave sets how many streams a
 // CU decodes at once, and sources older than the ring are read back from the flushed output.
@@ -61,6 +64,8 @@ constexpr int LROOT = 10, DROOT = 8;
 // table entry: bits 0-3 code length (0 = longer than the root: slow path), 4-5 kind,
 // 6-9 extra bits, 16-31 value (literal byte / length base / distance base)
 constexpr uint32_t K_LIT = 0, K_LEN = 1, K_EOB = 2, K_BAD = 3;
+// lookahead stop flags (above the advance / output-length fields of a lane's symbol info)
+constexpr uint32_t F_EOB = 1u << 17, F_BAD = 1u << 18, F_SLOW = 1u << 19;
 
 __constant__ uint16_t c_len_base[29] = {3,  4,  5,  6,  7,  8,  9,  10, 11,  13,  15,  17,  19,  23, 27,
                                         31, 35, 43, 51, 59, 67, 83, 99, 115, 131, 163, 195, 227, 258};
@@ -91,13 +96,10 @@ struct Smem {
   uint16_t csorted[20];
   HuffMeta lm, dm, cm;
   uint32_t tmp[16];
+  uint32_t rec[64];  // the batch's symbols: literal byte, or (1<<31)|(dist<<9)|len
 };
 
 __device__ __forceinline__ uint32_t U(uint32_t x) { return __builtin_amdgcn_readfirstlane(x); }
-// lane k of v := x (x, k uniform)
-__device__ __forceinline__ uint32_t put_lane(uint32_t v, uint32_t x, uint32_t k) {
-  return __lane_id() == (int)k ? x : v;
-}
 __device__ __forceinline__ int lane_id() { return __lane_id(); }
 
 // ---------------------------------------------------------------------------------------------
@@ -156,15 +158,16 @@ __device__ __forceinline__ uint32_t win_word(const Bits &B, uint32_t k) {
   return k < 64 ? U(__builtin_amdgcn_readlane(B.win0, (int)k)) : U(__builtin_amdgcn_readlane(B.win1, (int)(k - 64)));
 }
 
-// The four aligned words w..w+3 (128 bits) as uniform values.
+// The five aligned words w..w+4 (160 bits) as uniform values.
 __device__ __forceinline__ void bits_words(Bits &B, uint32_t w, uint32_t &W0, uint32_t &W1, uint32_t &W2,
-                                           uint32_t &W3) {
+                                           uint32_t &W3, uint32_t &W4) {
   bits_advance_to(B, w);
   const uint32_t k = w - B.wcur;
   W0 = win_word(B, k);
   W1 = win_word(B, k + 1);
   W2 = win_word(B, k + 2);
   W3 = win_word(B, k + 3);
+  W4 = win_word(B, k + 4);
 }
 
 // Re-position the reader at an absolute (forward) bit offset without reloading the windows.
@@ -374,8 +377,11 @@ __device__ __forceinline__ void flush(const Smem &S, uint8_t *out, uint64_t cap,
 
 }  // namespace
 
+#ifndef ZG_INFLATE_WPE
+#define ZG_INFLATE_WPE 5
+#endif
 // One wave per item. aux[i] = {trailer CRC-32, trailer ISIZE}.
-__global__ __launch_bounds__(64) void k_gzip(ZgItem *items, uint32_t *status, uint8_t *dst, uint64_t slot_bytes,
+__global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(ZG_INFLATE_WPE, 8))) void k_gzip(ZgItem *items, uint32_t *status, uint8_t *dst, uint64_t slot_bytes,
                                              uint2 *aux) {
   __shared__ Smem S;
   PROF_DECL;
@@ -524,66 +530,79 @@ __global__ __launch_bounds__(64) void k_gzip(ZgItem *items, uint32_t *status, ui
     bool eob = false;
     while (!eob && !err) {
       PROF_T(t_dec);
-      uint32_t rec = 0;  // lane k's symbol: literal byte, or (1<<31)|(dist<<9)|len
       uint32_t cnt = 0, bytes = 0;
       uint64_t bp = B.consumed;  // absolute bit position of the next symbol
       while (cnt < 64 && bytes < BATCH_CAP && !eob && !err) {
-        // Lane-parallel lookahead: lane l looks both tables up at bit bp + l, so one LDS round trip
-        // serves every symbol that starts inside the next 64 bits; a scalar walk then chains them
-        // (readlane at the running offset) until a symbol no longer fits the window.
-        uint32_t W0, W1, W2, W3;
-        bits_words(B, (uint32_t)(bp >> 5), W0, W1, W2, W3);
+        // Lane-parallel lookahead: lane l decodes a whole symbol (literal/length code, length extra
+        // bits, distance code, distance extra bits: at most 36 bits with root-table codes) as if one
+        // started at bit bp + l. The scalar walk then only chains the advances (one readlane per
+        // symbol), and the symbols on the chain are compacted into the batch's record array.
+        uint32_t W0, W1, W2, W3, W4;
+        bits_words(B, (uint32_t)(bp >> 5), W0, W1, W2, W3, W4);
         const uint32_t bit = (uint32_t)(bp & 31) + (uint32_t)lane;
         const uint32_t wi = bit >> 5;
-        const uint32_t lo = wi == 0 ? W0 : (wi == 1 ? W1 : W2);
-        const uint32_t hi = wi == 0 ? W1 : (wi == 1 ? W2 : W3);
-        const uint32_t V = __builtin_amdgcn_alignbit(hi, lo, bit & 31);
-        const uint32_t E = S.ltab[V & ((1u << LROOT) - 1)];
-        const uint32_t D = S.dtab[V & ((1u << DROOT) - 1)];
-        uint32_t o = 0;
-        bool slow = false;
-        while (cnt < 64 && bytes < BATCH_CAP) {
-          const uint32_t e = __builtin_amdgcn_readlane(E, o);
-          const uint32_t L = e & 15;
-          if (L == 0) { slow = true; break; }  // code longer than the root table
-          const uint32_t kind = (e >> 4) & 3;
-          if (kind == K_LIT) {
-            rec = put_lane(rec, e >> 16, cnt);
-            cnt++;
-            bytes++;
-            o += L;
-            if (o > 63) break;
-            continue;
-          }
-          if (kind == K_EOB) { o += L; eob = true; break; }
-          if (kind == K_BAD) { err = ZG_CORRUPT_STREAM; break; }
-          const uint32_t lx = (e >> 6) & 15;
-          const uint32_t o1 = o + L, o2 = o1 + lx;
-          if (o2 > 63) break;  // the distance code starts beyond the window: next window
-          const uint32_t len = (e >> 16) + (__builtin_amdgcn_readlane(V, o1) & ((1u << lx) - 1));
-          const uint32_t de = __builtin_amdgcn_readlane(D, o2);
-          const uint32_t DL = de & 15;
-          if (DL == 0) { slow = true; break; }
-          if (((de >> 4) & 3) != K_LEN) { err = ZG_CORRUPT_STREAM; break; }
-          const uint32_t dx = (de >> 6) & 15, o3 = o2 + DL;
-          if (o3 > 63) break;
-          const uint32_t dist = (de >> 16) + (__builtin_amdgcn_readlane(V, o3) & ((1u << dx) - 1));
-          if (dist > pos + bytes) { err = ZG_CORRUPT_STREAM; break; }  // distance too far back
-          rec = put_lane(rec, 0x80000000u | (dist << 9) | len, cnt);
-          cnt++;
-          bytes += len;
-          o = o3 + dx;
-          if (o > 63) break;
+        const uint32_t a0 = wi == 0 ? W0 : (wi == 1 ? W1 : W2);
+        const uint32_t a1 = wi == 0 ? W1 : (wi == 1 ? W2 : W3);
+        const uint32_t a2 = wi == 0 ? W2 : (wi == 1 ? W3 : W4);
+        const uint32_t Vlo = __builtin_amdgcn_alignbit(a1, a0, bit & 31);
+        const uint32_t Vhi = __builtin_amdgcn_alignbit(a2, a1, bit & 31);
+        const uint64_t V = ((uint64_t)Vhi << 32) | Vlo;
+        const uint32_t E = S.ltab[Vlo & ((1u << LROOT) - 1)];
+        const uint32_t L = E & 15, kind = (E >> 4) & 3, lx = (E >> 6) & 15;
+        const uint32_t s1 = L + lx;  // <= 15
+        const uint32_t D = S.dtab[(Vlo >> s1) & ((1u << DROOT) - 1)];
+        const uint32_t DL = D & 15, dx = (D >> 6) & 15, s2 = s1 + DL;
+        // info: bits 0-7 advance in bits, 8-16 output bytes, 17+ stop flags
+        uint32_t info, rec;
+        if (kind == K_LIT) {
+          info = L | (1u << 8);
+          rec = E >> 16;
+        } else if (kind == K_LEN) {
+          const uint32_t len = (E >> 16) + ((Vlo >> L) & ((1u << lx) - 1));
+          const uint32_t dist = (D >> 16) + ((uint32_t)(V >> s2) & ((1u << dx) - 1));
+          info = (s2 + dx) | (len << 8);
+          rec = 0x80000000u | (dist << 9) | len;
+          if (DL == 0) info = F_SLOW;  // distance code longer than the root
+          else if (((D >> 4) & 3) != K_LEN) info = F_BAD;
+        } else {
+          info = kind == K_EOB ? (L | F_EOB) : F_BAD;
+          rec = 0;
         }
+        if (L == 0) info = F_SLOW;  // literal/length code longer than the root
+        uint64_t chain = 0;
+        uint32_t o = 0, n = 0;
+        bool slow = false;
+        while (o < 64 && cnt + n < 64 && bytes < BATCH_CAP) {
+          const uint32_t a = U(__builtin_amdgcn_readlane(info, o));
+          if (a >= F_EOB) {
+            if (a == (F_EOB | (a & 255))) {
+              o += a & 255;
+              eob = true;
+            } else if (a & F_BAD) {
+              err = ZG_CORRUPT_STREAM;
+            } else {
+              slow = true;
+            }
+            break;
+          }
+          chain |= 1ull << o;
+          n++;
+          bytes += a >> 8;
+          o += a & 255;
+        }
+        if ((chain >> lane) & 1) S.rec[cnt + __builtin_amdgcn_mbcnt_hi((uint32_t)(chain >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)chain, 0u))] = rec;
+        cnt += n;
         bp += o;
         if (slow && !err && cnt < 64 && bytes < BATCH_CAP) {
           // one symbol through the canonical slow path (codes longer than the root)
           bits_seek_in(B, bp);
           const uint32_t e = decode_sym(B, S.ltab, LROOT, S.lsorted, S.lm, 0);
           const uint32_t kind = (e >> 4) & 3;
+          uint32_t r = 0;
+          bool has = false;
           if (kind == K_LIT) {
-            rec = put_lane(rec, e >> 16, cnt);
-            cnt++;
+            r = e >> 16;
+            has = true;
             bytes++;
           } else if (kind == K_EOB) {
             eob = true;
@@ -602,11 +621,14 @@ __global__ __launch_bounds__(64) void k_gzip(ZgItem *items, uint32_t *status, ui
               const uint32_t dx = (de >> 6) & 15;
               const uint32_t dist = (de >> 16) + bits_peek(B, dx);
               bits_drop(B, dx);
-              if (dist > pos + bytes) err = ZG_CORRUPT_STREAM;
-              rec = put_lane(rec, 0x80000000u | (dist << 9) | len, cnt);
-              cnt++;
+              r = 0x80000000u | (dist << 9) | len;
+              has = true;
               bytes += len;
             }
+          }
+          if (has) {
+            if (lane == 0) S.rec[cnt] = r;
+            cnt++;
           }
           bp = B.consumed;
         }
@@ -618,7 +640,9 @@ __global__ __launch_bounds__(64) void k_gzip(ZgItem *items, uint32_t *status, ui
       // ---- execute the batch ----
       PROF_ADD(1, t_dec);
       PROF_T(t_exe);
+      __syncthreads();
       const bool mine = lane < (int)cnt;
+      const uint32_t rec = mine ? S.rec[lane] : 0u;
       const bool is_match = mine && (rec >> 31);
       const uint32_t ln = mine ? (is_match ? (rec & 511) : 1u) : 0u;
       uint32_t inc = ln;  // inclusive wave scan of output lengths
@@ -631,6 +655,7 @@ __global__ __launch_bounds__(64) void k_gzip(ZgItem *items, uint32_t *status, ui
       const uint64_t batch_end = pos + bytes;
       const uint32_t mlen = rec & 511, md = (rec >> 9) & 0xFFFF;
       const uint64_t msrc = mypos - md;
+      if (__ballot(is_match && md > mypos)) { err = ZG_CORRUPT_STREAM; break; }  // distance too far back
       // sources older than the ring are read back from the flushed output
       if (__ballot(is_match && msrc + RING < batch_end)) __threadfence_block();
       // Matches resolve in rounds: every pending match whose source lies entirely before the first

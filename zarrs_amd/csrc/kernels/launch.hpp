@@ -111,7 +111,8 @@ hipError_t launch_shard_encode(const uint64_t *starts, const uint8_t *array, con
                                const uint64_t *shard_dst, uint64_t *inner_off, uint64_t *index_ptr,
                                uint64_t *shard_len, uint32_t n_shards, hipStream_t s);
 
-// blosc (c-blosc 1.x frames): stream table built on the device, sized on the host from BlInfo
+// blosc (c-blosc 1.x frames): stream table built on the device, sized on the host from BlInfo (first
+// execution of a plan) or from the capacities that execution recorded (later executions)
 enum : uint32_t { BL_COMP_BLOSCLZ = 0, BL_COMP_LZ4 = 1, BL_COMP_ZSTD = 4, BL_COMP_MEMCPY = 0x100, BL_COMP_SKIP = 0xFFFFFFFFu };
 enum : uint32_t { BL_KIND_RAW = 0, BL_KIND_LZ4 = 1, BL_KIND_ZSTD = 4, BL_KIND_BLOSCLZ = 5 };
 struct BlInfo {     // per item (read back)
@@ -135,8 +136,19 @@ struct BlDecode {
   uint8_t *tmp;           // n_sub * sub_slot decoded streams
   uint64_t sub_slot;
   ZstdScratch zs;
-  uint64_t n_sub, n_blk, n_zstd, n_lz4, n_blosclz;
+  uint64_t n_sub, n_blk, n_zstd, n_lz4, n_blosclz;  // with a cached layout: capacities (n_* > 0 = launched)
+  unsigned long long *ovf;  // set by k_blosc_layout when a cached layout is too small (ctl counter)
 };
+// Capacities of a blosc stream table sized by an earlier execution of the same plan: the layout of
+// this execution is computed on the device (k_blosc_layout) and checked against them, so the stage
+// needs no host read-back. BL_KINDS_*: compressors the earlier execution launched decoders for.
+enum : uint32_t { BL_HAS_ZSTD = 1, BL_HAS_LZ4 = 2, BL_HAS_BLOSCLZ = 4 };
+struct BlCaps {
+  uint64_t n_sub, n_blk, max_ne;
+  uint32_t kinds;
+};
+hipError_t launch_blosc_layout(const BlInfo *info, uint32_t n_items, uint64_t *bases, const BlCaps &caps,
+                               const BlDecode &D, hipStream_t s);
 hipError_t launch_blosc_info(const ZgItem *items, uint32_t *status, uint32_t n_items, uint64_t slot_bytes,
                              BlInfo *info, hipStream_t s);
 hipError_t launch_blosc_decode(ZgItem *items, uint32_t *status, uint32_t n_items, const BlInfo *info,

@@ -1633,7 +1633,7 @@ __global__ __launch_bounds__(64) void k_zstd_blocks(const ZgItem *items, uint32_
 // offsets. The compressed literal section is staged in LDS first (sections over LIT_LDS read global).
 // -------------------------------------------------------------------------------------------------
 #ifndef ZG_LIT_LDS
-#define ZG_LIT_LDS (64 * 1024)
+#define ZG_LIT_LDS (16 * 1024)
 #endif
 constexpr uint32_t LIT_LDS = ZG_LIT_LDS;
 constexpr int32_t LIT_WARM = 128;
@@ -2007,9 +2007,10 @@ namespace {
 // parallelism to take here; it is taken in k_zstd_lits / k_zstd_blocks, and across items.)
 // -------------------------------------------------------------------------------------------------
 #ifndef ZG_XRING
-#define ZG_XRING 65536
+#define ZG_XRING 16384
 #endif
 constexpr uint32_t XRING = ZG_XRING, XRMASK = XRING - 1;
+static_assert((XRING & XRMASK) == 0 && XRING >= 2 * ZBATCH, "exec ring: a power of two holding two batches");
 #ifndef ZG_XSTAGE_V
 #define ZG_XSTAGE_V 512
 #endif
@@ -2078,7 +2079,9 @@ __device__ __forceinline__ void x_copy(ZXSmem &S, XOut &O, const uint8_t *src, u
   const uint32_t m = (uint32_t)(s0 & 15), mq = m >> 2, mr = m & 3;
   const zv4u *sa = (const zv4u *)(s0 & ~(uintptr_t)15);
   const uint64_t nch = (n - done) >> 4;
-  constexpr uint32_t R = 16, PC = 64 * R;  // chunks per piece: 16 KiB (one wave per CU: VGPRs are free)
+  // chunks per piece: up to 16 KiB, and at most half the ring (x_reserve keeps the unflushed part
+  // of the ring within half of it, so a piece never overwrites bytes that are not yet flushed)
+  constexpr uint32_t R = XRING / 2 / 16 / 64 < 16 ? XRING / 2 / 16 / 64 : 16, PC = 64 * R;
   for (uint64_t c0 = 0; c0 < nch; c0 += PC) {
     const uint32_t cn = (uint32_t)min<uint64_t>(PC, nch - c0);
     x_reserve(S, O, O.pos + 16ull * cn);

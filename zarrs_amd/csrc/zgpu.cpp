@@ -36,7 +36,9 @@ namespace {
 
 thread_local std::string g_last_error;
 // device counters in the plan's control block (u64 each, cleared per execute)
-enum { CTR_ENC_BYTES = 0, CTR_ZSTD_SERIAL = 1, CTR_ZSTD_PARALLEL = 2, CTR_N = 3 };
+enum { CTR_ENC_BYTES = 0, CTR_ZSTD_SERIAL = 1, CTR_ZSTD_PARALLEL = 2, CTR_BLOSC_RERUN = 3, CTR_N = 4 };
+// internal ctl slots (not reported): a cached blosc layout was outgrown (the execution is re-run)
+enum { CTR_BLOSC_OVF = 31 };
 thread_local uint64_t g_last_counters[CTR_N];
 // UnexpectedChunkDecodedSize detail of the last call's first DECODED_SIZE_MISMATCH descriptor
 struct SizeDetail {
@@ -190,7 +192,7 @@ struct zgpu_plan {
   };
   Grow bl_info, bl_bases, bl_subs, bl_sub_status, bl_sub_kind, bl_blocks, bl_tmp, bl_zblks, bl_znblk, bl_zmode,
       bl_zlit, bl_zseq;
-  uint8_t *bl_h = nullptr;  // pinned: BlInfo read-back, then the bases upload
+  uint8_t *bl_h = nullptr;  // pinned: BlInfo read-back (first execution)
   size_t bl_h_n = 0;
   void *grow(Grow &g, size_t bytes) {
     if (g.n < bytes) {
@@ -208,7 +210,10 @@ struct zgpu_plan {
   // host-input staging
   uint8_t *d_enc_stage = nullptr;
   uint64_t last_enc_bytes = 0;
-  uint64_t last_counters[CTR_N] = {0, 0, 0};
+  uint64_t last_counters[CTR_N] = {0, 0, 0, 0};
+  uint8_t *last_out = nullptr;  // output of the last enqueue (a blosc layout overflow re-runs into it)
+  BlCaps bl_caps{};             // blosc stream-table capacities recorded by the first execution
+  bool bl_caps_valid = false, bl_caps_seen = false;
 
   ~zgpu_plan() {
     if (!ctx) return;
@@ -517,49 +522,67 @@ static void plan_upload(zgpu_plan &P, hipStream_t us = nullptr) {
   }
 }
 
-// blosc stage: frame headers -> (host read-back) stream table sizes -> streams + blocks on the device
-// -> zstd / lz4 stream decode -> per-block gather + unshuffle into the item slots. The read-back makes
-// this stage synchronous with the host (the only stage that is).
+// blosc stage: frame headers -> stream table layout -> streams + blocks on the device -> zstd / lz4 /
+// blosclz stream decode -> per-block gather + unshuffle into the item slots. The first execution of a
+// plan reads the headers back to size the table (the one host round trip of any stage) and records
+// the sizes as capacities; later executions lay the table out on the device against them
+// (k_blosc_layout) and stay asynchronous. A later input that outgrows them is re-run by plan_statuses.
 static void blosc_stage(zgpu_plan &P, const Stage &st, hipStream_t s) {
   zgpu_ctx &C = *P.ctx;
   const uint32_t ni = (uint32_t)P.items.size();
   uint8_t *dst = P.d_pool[st.pool];
   BlInfo *info = (BlInfo *)P.grow(P.bl_info, ni * sizeof(BlInfo));
-  const size_t hbytes = std::max<size_t>(ni * sizeof(BlInfo), ni * 16);
-  if (P.bl_h_n < hbytes) {
-    C.host_free(P.bl_h);
-    P.bl_h = (uint8_t *)C.host_alloc(hbytes);
-    P.bl_h_n = hbytes;
-  }
   HIPCHK(launch_blosc_info(P.d_items, P.d_status, ni, P.slot_bytes, info, s));
-  HIPCHK(hipMemcpyAsync(P.bl_h, info, ni * sizeof(BlInfo), hipMemcpyDeviceToHost, s));
-  HIPCHK(hipStreamSynchronize(s));
-  std::vector<BlInfo> hi(ni);
-  std::memcpy(hi.data(), P.bl_h, ni * sizeof(BlInfo));
-  BlDecode D{};
-  uint64_t *bases = (uint64_t *)P.bl_h;
-  uint64_t max_ne = 0;
-  for (uint32_t i = 0; i < ni; i++) {
-    bases[2 * i] = D.n_sub;
-    bases[2 * i + 1] = D.n_blk;
-    if (hi[i].comp == BL_COMP_SKIP) continue;
-    D.n_sub += hi[i].nsub;
-    D.n_blk += hi[i].nblk;
-    if (hi[i].comp == BL_COMP_ZSTD) D.n_zstd += hi[i].nsub;
-    if (hi[i].comp == BL_COMP_LZ4) D.n_lz4 += hi[i].nsub;
-    if (hi[i].comp == BL_COMP_BLOSCLZ) D.n_blosclz += hi[i].nsub;
-    max_ne = std::max<uint64_t>(max_ne, hi[i].max_ne);
-  }
   uint64_t *d_bases = (uint64_t *)P.grow(P.bl_bases, ni * 16);
-  HIPCHK(hipMemcpyAsync(d_bases, bases, ni * 16, hipMemcpyHostToDevice, s));
+  BlDecode D{};
   D.bases = d_bases;
+  D.ovf = P.d_counter + CTR_BLOSC_OVF;
+  BlCaps &caps = P.bl_caps;
+  const bool cached = P.bl_caps_valid;
+  if (!cached) {
+    const size_t hbytes = ni * sizeof(BlInfo);
+    if (P.bl_h_n < hbytes) {
+      C.host_free(P.bl_h);
+      P.bl_h = (uint8_t *)C.host_alloc(hbytes);
+      P.bl_h_n = hbytes;
+    }
+    HIPCHK(hipMemcpyAsync(P.bl_h, info, ni * sizeof(BlInfo), hipMemcpyDeviceToHost, s));
+    HIPCHK(hipStreamSynchronize(s));
+    std::vector<BlInfo> hi(ni);
+    std::memcpy(hi.data(), P.bl_h, ni * sizeof(BlInfo));
+    BlCaps exact{0, 0, 0, 0};
+    for (uint32_t i = 0; i < ni; i++) {
+      if (hi[i].comp == BL_COMP_SKIP) continue;
+      exact.n_sub += hi[i].nsub;
+      exact.n_blk += hi[i].nblk;
+      if (hi[i].nsub)
+        exact.kinds |= hi[i].comp == BL_COMP_ZSTD ? BL_HAS_ZSTD : hi[i].comp == BL_COMP_LZ4 ? BL_HAS_LZ4
+                       : hi[i].comp == BL_COMP_BLOSCLZ ? BL_HAS_BLOSCLZ : 0u;
+      exact.max_ne = std::max<uint64_t>(exact.max_ne, hi[i].max_ne);
+    }
+    // capacities only grow (a plan whose inputs alternate between layouts settles on their maximum)
+    if (P.bl_caps_seen) {
+      caps.n_sub = std::max(caps.n_sub, exact.n_sub);
+      caps.n_blk = std::max(caps.n_blk, exact.n_blk);
+      caps.max_ne = std::max(caps.max_ne, exact.max_ne);
+      caps.kinds |= exact.kinds;
+    } else {
+      caps = exact;
+    }
+    P.bl_caps_seen = P.bl_caps_valid = true;
+  }
+  D.n_sub = caps.n_sub;
+  D.n_blk = caps.n_blk;
+  D.n_zstd = caps.kinds & BL_HAS_ZSTD;
+  D.n_lz4 = caps.kinds & BL_HAS_LZ4;
+  D.n_blosclz = caps.kinds & BL_HAS_BLOSCLZ;
   const uint64_t ns = std::max<uint64_t>(D.n_sub, 1);
   D.subs = (ZgItem *)P.grow(P.bl_subs, ns * sizeof(ZgItem));
   D.sub_status = (uint32_t *)P.grow(P.bl_sub_status, ns * 4);
   D.sub_kind = (uint32_t *)P.grow(P.bl_sub_kind, ns * 4);
   D.blocks = (BlBlock *)P.grow(P.bl_blocks, std::max<uint64_t>(D.n_blk, 1) * sizeof(BlBlock));
   if (D.n_zstd + D.n_lz4 + D.n_blosclz) {
-    D.sub_slot = (max_ne + 255) & ~(uint64_t)255;
+    D.sub_slot = (caps.max_ne + 255) & ~(uint64_t)255;
     D.tmp = (uint8_t *)P.grow(P.bl_tmp, D.n_sub * D.sub_slot);
   }
   if (D.n_zstd) {
@@ -573,12 +596,15 @@ static void blosc_stage(zgpu_plan &P, const Stage &st, hipStream_t s) {
     D.zs.counters = P.zs.counters;
     D.zs.force_serial = P.zs.force_serial;
   }
+  // the layout (bases, inert tails past this execution's totals) is always computed on the device
+  HIPCHK(launch_blosc_layout(info, ni, d_bases, caps, D, s));
   HIPCHK(launch_blosc_decode(P.d_items, P.d_status, ni, info, D, dst, P.slot_bytes, s));
 }
 
 // Enqueue the decode of an uploaded plan on stream s.
 static void plan_enqueue(zgpu_plan &P, uint8_t *out, hipStream_t s) {
   const uint32_t ni = (uint32_t)P.items.size();
+  P.last_out = out;
   HIPCHK(hipMemsetAsync(P.d_ctl, 0, P.ctl_bytes, s));
   if (!ni) return;
   // stages rewrite each item's {src,len} in place; a chain with none reads the uploaded table as is
@@ -650,6 +676,14 @@ static int plan_statuses(zgpu_plan &P, int32_t *status, hipStream_t s) {
   const size_t ni = P.items.size();
   HIPCHK(hipMemcpyAsync(P.h_ctl, P.d_ctl, P.ctl_bytes, hipMemcpyDeviceToHost, s));
   HIPCHK(hipStreamSynchronize(s));
+  if (((const uint64_t *)P.h_ctl)[CTR_BLOSC_OVF]) {
+    // the input outgrew the cached blosc layout: nothing was decoded; re-run with a read-back layout
+    P.bl_caps_valid = false;
+    plan_enqueue(P, P.last_out, s);
+    HIPCHK(hipMemcpyAsync(P.h_ctl, P.d_ctl, P.ctl_bytes, hipMemcpyDeviceToHost, s));
+    HIPCHK(hipStreamSynchronize(s));
+    ((uint64_t *)P.h_ctl)[CTR_BLOSC_RERUN] = 1;
+  }
   std::memcpy(P.last_counters, P.h_ctl, sizeof(P.last_counters));
   for (int k = 0; k < CTR_N; k++) g_last_counters[k] += P.last_counters[k];
   const uint32_t *st = (const uint32_t *)(P.h_ctl + 256);
