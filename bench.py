@@ -1014,6 +1014,16 @@ def main():
     cpu = W.cpu_baseline() if (rank == 0 and not args.no_cpu) else None
     traffic, traffic_note = None, "skipped (--no-pmc or N>1)"
     if rank == 0 and world == 1 and not args.no_pmc:
+        # the profiled child needs the HBM this process holds (C5: ~30 GB of frames, outputs and
+        # scratch): keep the line's fields, drop the workload's tensors and the zgpu context's pools
+        import gc
+        import types
+        W = types.SimpleNamespace(**{k: getattr(W, k) for k in ("scaling", "dtype", "data", "config", "kernel",
+                                                                 "pmc_regex") if hasattr(W, k)})
+        r["W"] = None
+        gc.collect()
+        args.ctx.close()
+        torch.cuda.empty_cache()
         traffic, traffic_note = pmc_traffic(args, W)
     if rank == 0:
         achieved = r["alg_bytes"] / (r["ev_ms"] * 1e-3) / 1e9
