@@ -944,11 +944,26 @@ def pmc_traffic(args, W):
                    "--output-format", "csv", "--", sys.executable, os.path.abspath(__file__), "--child",
                    "--workload", args.workload, "--steps", str(steps), "--warmup", str(warm), "--no-cpu",
                    "--grid", *map(str, args.grid), "--c5-scale", str(args.c5_scale)]
-            r = subprocess.run(cmd, stdout=subprocess.DEVNULL, stderr=subprocess.PIPE, timeout=600)
-            if r.returncode:
-                err = [ln for ln in r.stderr.decode(errors="replace").splitlines()
+            # the child's stderr goes to a file; a heartbeat on ours shows the pass is alive
+            elog = os.path.join(tmp, ctr + ".err")
+            t0 = time.time()
+            with open(elog, "wb") as ef:
+                proc = subprocess.Popen(cmd, stdout=subprocess.DEVNULL, stderr=ef)
+                while True:
+                    try:
+                        rc = proc.wait(timeout=20)
+                        break
+                    except subprocess.TimeoutExpired:
+                        print(f"[bench] rocprofv3 --pmc {ctr} pass running {time.time() - t0:.0f} s",
+                              file=sys.stderr, flush=True)
+                        if time.time() - t0 > 600:
+                            proc.kill()
+                            proc.wait()
+                            return None, f"rocprofv3 --pmc {ctr} timed out"
+            if rc:
+                err = [ln for ln in open(elog, errors="replace").read().splitlines()
                        if "simple_timer" not in ln and ln.strip()]
-                return None, f"rocprofv3 --pmc {ctr} rc={r.returncode}: {' | '.join(err[-6:])[-600:]}"
+                return None, f"rocprofv3 --pmc {ctr} rc={rc}: {' | '.join(err[-6:])[-600:]}"
             files = glob.glob(os.path.join(d, "**", "*counter_collection.csv"), recursive=True)
             import re
             rx = re.compile(regex)
