@@ -192,6 +192,22 @@ int zgpu_retrieve_array_subset(zgpu_chain *chain, uint32_t ndim, const uint64_t 
                                void *hip_stream);
 
 /*
+ * zgpu_retrieve_array_subset over several GPUs of one node from one process (one chain per device,
+ * each created on that device's context; same codecs and data type). The subset's chunk rows along
+ * axis 0 are cut into n_dev contiguous groups and decoded concurrently, device d taking group d
+ * (array_read_ops_common.rs:173-176: chunks are independent). Encoded chunks are host-resident
+ * (ZGPU_ENC_DEVICE is rejected): each device uploads its own over its own link. Host `out`: every
+ * device writes its rows straight into place. ZGPU_OUT_DEVICE: `out` is on chains[0]'s device; the
+ * other devices decode into their own HBM and copy their rows into `out` peer-to-peer (xGMI).
+ * Synchronous. Returns the first failing status in chunk (= device) order.
+ */
+int zgpu_retrieve_array_subset_multi(zgpu_chain *const *chains, uint32_t n_dev, uint32_t ndim,
+                                     const uint64_t *array_shape, const uint64_t *chunk_shape,
+                                     const void *const *chunk_ptrs, const uint64_t *chunk_lens,
+                                     const uint64_t *sel_start, const uint64_t *sel_shape, void *out,
+                                     uint32_t flags);
+
+/*
  * Encoded chunks in a filesystem store. One byte range of one file per descriptor:
  * path = FilesystemStore::key_to_fspath(key) (zarrs_filesystem/src/lib.rs:173-179); path NULL or a
  * file that does not exist = missing key -> fill value (lib.rs:339-343,428-430); len == UINT64_MAX

@@ -35,14 +35,30 @@ pub trait ArrayGpuExt {
         out: *mut c_void,
         hip_stream: *mut c_void,
     ) -> Result<(), ArrayError>;
+
+    /// Decode `subset` on several GPUs of this process (`devices`, HIP ordinals) into a new host
+    /// buffer: the subset's axis-0 chunk rows are cut into one contiguous group per device and every
+    /// device writes its rows straight into place (`zgpu_retrieve_array_subset_multi`).
+    ///
+    /// # Errors
+    /// Returns [`ArrayError`] as [`ArrayGpuExt::retrieve_array_subset_gpu`] does.
+    fn retrieve_array_subset_gpu_multi(&self, subset: &ArraySubset, devices: &[i32]) -> Result<Vec<u8>, ArrayError>;
 }
 
 fn gpu_chain<TStorage: ?Sized + ReadableStorageTraits + 'static>(array: &Array<TStorage>) -> Result<Chain, ArrayError> {
+    gpu_chain_on(array, crate::device())
+}
+
+fn gpu_chain_on<TStorage: ?Sized + ReadableStorageTraits + 'static>(
+    array: &Array<TStorage>,
+    device: std::ffi::c_int,
+) -> Result<Chain, ArrayError> {
     let ArrayMetadata::V3(meta) = array.metadata() else {
         return Err(CodecError::Other("zarrs_gpu: Zarr V2 arrays are read through the CPU path".into()).into());
     };
     let json = serde_json::to_string(&meta.codecs).map_err(|e| CodecError::Other(e.to_string()))?;
-    Chain::new(&json, array.data_type(), array.fill_value()).map_err(|e| CodecError::Other(e.to_string()).into())
+    Chain::new_on(&json, array.data_type(), array.fill_value(), device)
+        .map_err(|e| CodecError::Other(e.to_string()).into())
 }
 
 /// The encoded chunks a subset touches, as (pointer, length) tables over the whole chunk grid
@@ -102,13 +118,8 @@ unsafe fn gpu_retrieve<TStorage: ?Sized + ReadableStorageTraits + 'static>(
     let (chunk_shape, bufs, lins) = gpu_tables(array, subset)?;
     let n_grid: u64 = array.chunk_grid_shape().iter().product();
     let n_grid = usize::try_from(n_grid).map_err(|e| CodecError::Other(e.to_string()))?;
-    let mut ptrs: Vec<*const c_void> = vec![std::ptr::null(); n_grid];
-    let mut lens = vec![0u64; n_grid];
-    for (b, &lin) in bufs.iter().zip(&lins) {
-        // an empty object is present (not missing): give it a valid address
-        ptrs[lin as usize] = if b.is_empty() { EMPTY.as_ptr().cast() } else { b.as_ptr().cast() };
-        lens[lin as usize] = b.len() as u64;
-    }
+    // an empty object is present (not missing): it gets a valid address
+    let (ptrs, lens) = grid_tables(n_grid, &bufs, &lins);
     let (start, shape) = (subset.start(), subset.shape());
     // SAFETY: the tables, shapes and host chunk buffers outlive the synchronous call; `out` is the
     // caller's (host buffer, or a device buffer per this function's contract).
@@ -135,6 +146,17 @@ unsafe fn gpu_retrieve<TStorage: ?Sized + ReadableStorageTraits + 'static>(
 
 static EMPTY: [u8; 1] = [0];
 
+/// The pointer tables of [`gpu_retrieve`] over the whole chunk grid (NULL = missing chunk).
+fn grid_tables(n_grid: usize, bufs: &[Vec<u8>], lins: &[u64]) -> (Vec<*const c_void>, Vec<u64>) {
+    let mut ptrs: Vec<*const c_void> = vec![std::ptr::null(); n_grid];
+    let mut lens = vec![0u64; n_grid];
+    for (b, &lin) in bufs.iter().zip(lins) {
+        ptrs[lin as usize] = if b.is_empty() { EMPTY.as_ptr().cast() } else { b.as_ptr().cast() };
+        lens[lin as usize] = b.len() as u64;
+    }
+    (ptrs, lens)
+}
+
 impl<TStorage: ?Sized + ReadableStorageTraits + 'static> ArrayGpuExt for Array<TStorage> {
     fn retrieve_array_subset_gpu(&self, subset: &ArraySubset) -> Result<Vec<u8>, ArrayError> {
         let es = self
@@ -156,5 +178,45 @@ impl<TStorage: ?Sized + ReadableStorageTraits + 'static> ArrayGpuExt for Array<T
     ) -> Result<(), ArrayError> {
         // SAFETY: forwarded from this function's contract.
         unsafe { gpu_retrieve(self, subset, out, ffi::ZGPU_OUT_DEVICE, hip_stream) }
+    }
+
+    fn retrieve_array_subset_gpu_multi(&self, subset: &ArraySubset, devices: &[i32]) -> Result<Vec<u8>, ArrayError> {
+        let nd = self.dimensionality();
+        if nd == 0 || nd > ffi::ZGPU_MAX_DIMS || devices.is_empty() {
+            return Err(CodecError::Other("zarrs_gpu: unsupported dimensionality or no devices".into()).into());
+        }
+        let chains = devices.iter().map(|&d| gpu_chain_on(self, d)).collect::<Result<Vec<Chain>, ArrayError>>()?;
+        let handles: Vec<*mut ffi::zgpu_chain> = chains.iter().map(Chain::as_ptr).collect();
+        let es = self
+            .data_type()
+            .fixed_size()
+            .ok_or_else(|| CodecError::Other("zarrs_gpu: fixed-size data types only".into()))?;
+        let n = usize::try_from(subset.num_elements()).map_err(|e| CodecError::Other(e.to_string()))?;
+        let mut out = vec![0u8; n * es];
+        let (chunk_shape, bufs, lins) = gpu_tables(self, subset)?;
+        let n_grid: u64 = self.chunk_grid_shape().iter().product();
+        let n_grid = usize::try_from(n_grid).map_err(|e| CodecError::Other(e.to_string()))?;
+        let (ptrs, lens) = grid_tables(n_grid, &bufs, &lins);
+        let (start, shape) = (subset.start(), subset.shape());
+        // SAFETY: tables, shapes, host chunk buffers and the host output outlive the synchronous call.
+        let rc = unsafe {
+            ffi::zgpu_retrieve_array_subset_multi(
+                handles.as_ptr(),
+                u32::try_from(handles.len()).map_err(|e| CodecError::Other(e.to_string()))?,
+                nd as u32,
+                self.shape().as_ptr(),
+                chunk_shape.as_ptr(),
+                ptrs.as_ptr(),
+                lens.as_ptr(),
+                start.as_ptr(),
+                shape.as_ptr(),
+                out.as_mut_ptr().cast(),
+                0,
+            )
+        };
+        if rc != ffi::ZGPU_OK {
+            return Err(status_error(rc).into());
+        }
+        Ok(out)
     }
 }

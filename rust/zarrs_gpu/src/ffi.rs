@@ -98,4 +98,17 @@ unsafe extern "C" {
         hip_stream: *mut c_void,
     ) -> c_int;
     pub fn zgpu_last_size_mismatch(desc: *mut u64, len: *mut u64, expected_len: *mut u64) -> c_int;
+    pub fn zgpu_retrieve_array_subset_multi(
+        chains: *const *mut zgpu_chain,
+        n_dev: u32,
+        ndim: u32,
+        array_shape: *const u64,
+        chunk_shape: *const u64,
+        chunk_ptrs: *const *const c_void,
+        chunk_lens: *const u64,
+        sel_start: *const u64,
+        sel_shape: *const u64,
+        out: *mut c_void,
+        flags: u32,
+    ) -> c_int;
 }

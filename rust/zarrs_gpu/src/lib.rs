@@ -52,7 +52,7 @@ pub fn unregister(handle: &zarrs_codec::CodecRuntimeRegistryHandleV3) -> bool {
 }
 
 /// The HIP device the plugin decodes on: `ZARRS_GPU_DEVICE` (default 0).
-fn device() -> c_int {
+pub(crate) fn device() -> c_int {
     std::env::var("ZARRS_GPU_DEVICE").ok().and_then(|v| v.parse().ok()).unwrap_or(0)
 }
 
@@ -112,7 +112,17 @@ impl Drop for Chain {
 impl Chain {
     /// `codecs_json` is the Zarr V3 "codecs" array; the chain is bound to `data_type` / `fill_value`.
     pub(crate) fn new(codecs_json: &str, data_type: &DataType, fill_value: &FillValue) -> Result<Self, CodecCreateError> {
-        let ctx = context(device()).map_err(CodecCreateError::Other)?;
+        Self::new_on(codecs_json, data_type, fill_value, device())
+    }
+
+    /// As [`Chain::new`], on HIP device `dev` (its process-wide context).
+    pub(crate) fn new_on(
+        codecs_json: &str,
+        data_type: &DataType,
+        fill_value: &FillValue,
+        dev: c_int,
+    ) -> Result<Self, CodecCreateError> {
+        let ctx = context(dev).map_err(CodecCreateError::Other)?;
         let name = data_type
             .name(ZarrVersion::V3)
             .ok_or_else(|| CodecCreateError::Other("data type has no Zarr V3 name".into()))?;

@@ -50,3 +50,16 @@ fn gpu_sharding_plugin_matches_zarrs() {
     assert!(zarrs_gpu::unregister(&handle));
     assert!(!zarrs_gpu::unregister(&handle));
 }
+
+#[test]
+fn gpu_multi_device_read_matches_zarrs() {
+    // devices [0, 0] on a one-GPU machine: two contexts of one device still exercise the split
+    let store = Arc::new(MemoryStore::default());
+    let _ = write_array(store.clone());
+    let cpu: Array<MemoryStore> = Array::open(store.clone(), "/array").unwrap();
+    let subset = ArraySubset::new_with_ranges(&[3..61, 7..95]);
+    let expected: Vec<u16> = cpu.retrieve_array_subset(&subset).unwrap();
+    let raw = cpu.retrieve_array_subset_gpu_multi(&subset, &[0, 0]).unwrap();
+    let got: Vec<u16> = raw.chunks_exact(2).map(|b| u16::from_ne_bytes([b[0], b[1]])).collect();
+    assert_eq!(got, expected);
+}

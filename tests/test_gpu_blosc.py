@@ -188,11 +188,13 @@ def test_blosc_plan_cached_layout_and_rerun(ctx, torch_cuda, cname):
     from zarrs_amd import CodecChain, make_desc
     from zarrs_amd import _lib as L
     rng = np.random.default_rng(3)
-    n, nchunk = 20000, 4
+    n, nchunk = 1 << 18, 4
     datas = [_data(rng, n, 2) for _ in range(nchunk)]
-    variants = []  # (blocksize, shuffle): few blocks -> many blocks and split streams -> few again
-    for bsz, sh in ((0, "noshuffle"), (1024, "shuffle"), (4096, "noshuffle")):
-        codecs = [{"name": "bytes", "configuration": {"endian": "little"}}, _blosc(cname, sh, 2, bsz)]
+    # (shuffle, clevel) -> c-blosc's automatic blocksize: clevel 9 one 512 KiB block; clevel 1 8-16
+    # blocks of 32-64 KiB; clevel 5 two blocks (blosclz: a memcpyed frame)
+    variants = []
+    for sh, cl in (("noshuffle", 9), ("shuffle", 1), ("noshuffle", 5)):
+        codecs = [{"name": "bytes", "configuration": {"endian": "little"}}, _blosc(cname, sh, 2, clevel=cl)]
         co = O.OracleChain.from_metadata(codecs, "uint16", 0, 1)
         variants.append([co.encode(d) for d in datas])
     cap = max(len(e) for v in variants for e in v)

@@ -265,3 +265,52 @@ def test_tiled_transpose_paths(ctx, torch_cuda, dt, order, cs, shape):
         exp = O.retrieve_array_subset(co, shape, cs, chunks, start, sub, nthreads=4)
         got = arr.retrieve_array_subset(start, sub)
         assert got.tobytes() == exp.tobytes(), (start, sub)
+
+
+@pytest.mark.parametrize("out_dev", [False, True])
+def test_retrieve_array_subset_multi_device(ctx, torch_cuda, out_dev):
+    """zgpu_retrieve_array_subset_multi: the subset's axis-0 chunk rows cut over several contexts
+    (on this 1-GPU box: three contexts on device 0, so the partitioning, the per-device uploads, the
+    device-slab + peer-copy gather and the status order are exercised; the 8-GPU node runs the same
+    code with one context per device), vs the oracle. A corrupt chunk in the middle group is reported."""
+    from zarrs_amd import Array, Context, MemoryStore
+    codecs = [{"name": "transpose", "configuration": {"order": [2, 1, 0]}},
+              {"name": "bytes", "configuration": {"endian": "big"}},
+              {"name": "gzip", "configuration": {"level": 1}}, {"name": "crc32c"}]
+    rng = np.random.default_rng(21)
+    shape, cs = [70, 40, 33], [16, 16, 16]
+    a = np.round(rng.standard_normal(shape) * 50).astype(np.float32)
+    co = O.OracleChain.from_metadata(codecs, "float32", 0, 3)
+    chunks = _encode_grid(co, a, cs, drop={(1, 1, 1)})
+    ms = MemoryStore({"c/" + "/".join(map(str, k)): v for k, v in chunks.items()})
+    meta = {"shape": shape, "data_type": "float32", "fill_value": 0, "codecs": codecs,
+            "chunk_grid": {"name": "regular", "configuration": {"chunk_shape": cs}}}
+    arr = Array(ms, meta, ctx)
+    extra = [Context(0), Context(0)]
+    try:
+        for n_dev in (1, 2, 3):
+            for start, sub in (([0, 0, 0], shape), ([5, 3, 2], [60, 30, 31]), ([17, 0, 0], [5, 40, 33])):
+                exp = O.retrieve_array_subset(co, shape, cs, chunks, start, sub, nthreads=4)
+                if out_dev:
+                    out = torch_cuda.full(sub, -7.0, dtype=torch_cuda.float32, device="cuda")
+                else:
+                    out = np.full(sub, -7.0, np.float32)
+                arr.retrieve_array_subset_multi(start, sub, out, [ctx] + extra[: n_dev - 1])
+                got = out.cpu().numpy() if out_dev else out
+                assert got.tobytes() == exp.tobytes(), (n_dev, start, sub)
+        # a corrupt chunk in the middle group: its status, not a later one's
+        bad = dict(chunks)
+        k = (2, 0, 0)
+        b = bytearray(bad[k])
+        b[-1] ^= 0xFF  # its crc32c
+        bad[k] = bytes(b)
+        arr_bad = Array(MemoryStore({"c/" + "/".join(map(str, kk)): v for kk, v in bad.items()}), meta, ctx)
+        out = np.zeros(shape, np.float32)
+        from zarrs_amd import ZgpuError
+        from zarrs_amd import _lib as L
+        with pytest.raises(ZgpuError) as ei:
+            arr_bad.retrieve_array_subset_multi([0, 0, 0], shape, out, [ctx] + extra)
+        assert ei.value.status == L.INVALID_CHECKSUM
+    finally:
+        for c in extra:
+            c.close()

@@ -37,7 +37,7 @@ EXPORTS = [
     "zgpu_chain_encoded_size", "zgpu_encode_batch", "zgpu_plan_counters", "zgpu_last_counters",
     "zgpu_last_size_mismatch", "zgpu_cache_create", "zgpu_cache_destroy", "zgpu_cache_clear", "zgpu_cache_stats",
     "zgpu_cache_retrieve_array_subset", "zgpu_retrieve_array_subset_dlpack", "zgpu_chain_encoded_bound",
-    "zgpu_encode_chunks",
+    "zgpu_encode_chunks", "zgpu_retrieve_array_subset_multi",
 ]
 CTR_ENC_BYTES, CTR_ZSTD_SERIAL, CTR_ZSTD_PARALLEL, CTR_BLOSC_RERUN = range(4)
 N_COUNTERS = 4
@@ -137,6 +137,8 @@ def load() -> C.CDLL:
     L.zgpu_chain_encoded_bound.restype = C.c_int64
     L.zgpu_chain_encoded_bound.argtypes = [vp, u32, P64]
     L.zgpu_encode_chunks.argtypes = [vp, u32, P64, vp, P64, C.POINTER(EncodeDesc), u64, u32, P64, vp]
+    L.zgpu_retrieve_array_subset_multi.argtypes = [C.POINTER(vp), u32, u32, P64, P64, C.POINTER(vp), P64, P64, P64,
+                                                   vp, u32]
     L.zgpu_plan_counters.restype = u32
     L.zgpu_plan_counters.argtypes = [vp, P64, u32]
     L.zgpu_last_counters.restype = u32

@@ -131,6 +131,7 @@ class Array:
             self._sep, self._prefix = cfg.get("separator", "/"), "c" + cfg.get("separator", "/")
         else:
             self._sep, self._prefix = cfg.get("separator", "."), ""
+        self._validate = validate_checksums
         self.codecs = CodecChain.from_metadata(metadata["codecs"], self.data_type,
                                                metadata.get("fill_value", 0), ctx,
                                                validate_checksums)
@@ -206,6 +207,29 @@ class Array:
             self.codecs._h, self.ndim, L.u64s(self.shape), L.u64s(self.chunk_shape), ptrs, lens,
             L.u64s(start), L.u64s(shape), op, flags, default_stream(None, out, *keep))
         del keep
+        L.check(rc)
+
+    def retrieve_array_subset_multi(self, start, shape, out, contexts) -> None:
+        """The subset decoded by several GPUs of this process (zgpu_retrieve_array_subset_multi): one
+        chain per context in `contexts`, the subset's axis-0 chunk rows cut into one contiguous group
+        per device; a device `out` lives on contexts[0]'s device and receives the other devices'
+        rows peer-to-peer. Host-resident stores only (each device uploads its own chunks)."""
+        if self.store.device:
+            raise ValueError("multi-device reads take host-resident encoded chunks")
+        chains = [self.codecs if c is self.codecs.ctx else
+                  CodecChain.from_metadata(self.metadata["codecs"], self.data_type,
+                                           self.metadata.get("fill_value", 0), c, self._validate)
+                  for c in contexts]
+        hs = (C.c_void_p * len(chains))(*[ch._h.value for ch in chains])
+        ptrs, lens, keep = self._tables(start, shape)
+        odev, op = _out_ptr(out)
+        if odev:
+            import torch
+            torch.cuda.synchronize(out.device)  # the call has no stream: order torch's work first
+        rc = L.load().zgpu_retrieve_array_subset_multi(
+            hs, len(chains), self.ndim, L.u64s(self.shape), L.u64s(self.chunk_shape), ptrs, lens,
+            L.u64s(start), L.u64s(shape), op, L.OUT_DEVICE if odev else 0)
+        del keep, chains
         L.check(rc)
 
     def retrieve_array_subset_dlpack(self, start=None, shape=None, cache=None):

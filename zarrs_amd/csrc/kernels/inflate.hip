@@ -60,6 +60,15 @@ constexpr int FLUSH_MIN = RING / 4;  // flush the ring to the slot once this man
 // unflushed bytes stay below FLUSH_MIN + BATCH_CAP + 258 < RING: every source older than the ring
 // has been flushed
 constexpr int LROOT = 10, DROOT = 8;
+#ifndef ZG_INFLATE_XW
+#define ZG_INFLATE_XW 8  // > 0: in-ring matches up to this many bytes copy through aligned ring words
+#endif
+#ifndef ZG_INFLATE_BW
+#define ZG_INFLATE_BW 1  // window words by plain readlanes when they lie in one register window
+#endif
+#ifndef ZG_INFLATE_PJ
+#define ZG_INFLATE_PJ 1  // chain a window's symbols by pointer jumping (0: scalar walk)
+#endif
 
 // table entry: bits 0-3 code length (0 = longer than the root: slow path), 4-5 kind,
 // 6-9 extra bits, 16-31 value (literal byte / length base / distance base)
@@ -96,11 +105,27 @@ struct Smem {
   uint16_t csorted[20];
   HuffMeta lm, dm, cm;
   uint32_t tmp[16];
-  uint32_t rec[64];  // the batch's symbols: literal byte, or (1<<31)|(dist<<9)|len
+  uint32_t rec[64];   // the batch's symbols: literal byte, or (1<<31)|(dist<<9)|len
+  uint16_t roff[64];  // their output offsets in the batch
 };
 
 __device__ __forceinline__ uint32_t U(uint32_t x) { return __builtin_amdgcn_readfirstlane(x); }
 __device__ __forceinline__ int lane_id() { return __lane_id(); }
+// v of lane idx (idx >= 64: the sentinel 64), one ds_bpermute
+__device__ __forceinline__ uint32_t lane_gather(uint32_t v, uint32_t idx) {
+  const uint32_t g = (uint32_t)__builtin_amdgcn_ds_bpermute((int)(min(idx, 63u) << 2), (int)v);
+  return idx >= 64 ? 64u : g;
+}
+// inclusive wave64 prefix sum: row shifts within 16 lanes, then row broadcasts (DPP, no LDS)
+__device__ __forceinline__ uint32_t wave_incl_sum(uint32_t x) {
+  x += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0x111, 0xf, 0xf, false);  // row_shr:1
+  x += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0x112, 0xf, 0xf, false);  // row_shr:2
+  x += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0x114, 0xf, 0xf, false);  // row_shr:4
+  x += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0x118, 0xf, 0xf, false);  // row_shr:8
+  x += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0x142, 0xa, 0xf, false);  // row_bcast:15
+  x += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0x143, 0xc, 0xf, false);  // row_bcast:31
+  return x;
+}
 
 // ---------------------------------------------------------------------------------------------
 // Bit reader over aligned 32-bit words held in two per-lane register windows.
@@ -163,6 +188,16 @@ __device__ __forceinline__ void bits_words(Bits &B, uint32_t w, uint32_t &W0, ui
                                            uint32_t &W3, uint32_t &W4) {
   bits_advance_to(B, w);
   const uint32_t k = w - B.wcur;
+#if ZG_INFLATE_BW
+  if (k <= 59) {  // all five in the first window (the common case): five plain readlanes
+    W0 = U(__builtin_amdgcn_readlane(B.win0, (int)k));
+    W1 = U(__builtin_amdgcn_readlane(B.win0, (int)k + 1));
+    W2 = U(__builtin_amdgcn_readlane(B.win0, (int)k + 2));
+    W3 = U(__builtin_amdgcn_readlane(B.win0, (int)k + 3));
+    W4 = U(__builtin_amdgcn_readlane(B.win0, (int)k + 4));
+    return;
+  }
+#endif
   W0 = win_word(B, k);
   W1 = win_word(B, k + 1);
   W2 = win_word(B, k + 2);
@@ -569,6 +604,58 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(ZG_INFLATE_W
           rec = 0;
         }
         if (L == 0) info = F_SLOW;  // literal/length code longer than the root
+#if ZG_INFLATE_PJ
+        // Chain the window's symbols by pointer jumping, with no per-symbol scalar work: J_k(x) is
+        // the bit offset 2^k symbols after offset x (64: past the window, or after a stop symbol);
+        // lane t composes the J_k of the bits of t into p = the offset of the window's t-th symbol,
+        // then gathers that symbol. Output offsets are a wave prefix sum; the batch caps (64
+        // symbols, BATCH_CAP bytes) cut a prefix, as the scalar walk did.
+        bool slow = false;
+        uint32_t o = 0;
+        {
+          uint32_t J = info >= F_EOB ? 64u : min<uint32_t>((uint32_t)lane + (info & 255), 64u);
+          uint32_t p = (lane & 1) ? U(__builtin_amdgcn_readlane(J, 0)) : 0u;
+#pragma unroll
+          for (int k = 1; k < 6; k++) {
+            J = lane_gather(J, J);
+            const uint32_t q = lane_gather(J, p);
+            if ((lane >> k) & 1) p = q;
+          }
+          const uint32_t pi = min<uint32_t>(p, 63u);
+          const uint32_t info_t = (uint32_t)__builtin_amdgcn_ds_bpermute((int)(pi << 2), (int)info);
+          const uint32_t rec_t = (uint32_t)__builtin_amdgcn_ds_bpermute((int)(pi << 2), (int)rec);
+          const bool valid = p < 64 && info_t < F_EOB;
+          const uint32_t olen = valid ? info_t >> 8 : 0u;
+          const uint32_t incl = wave_incl_sum(olen), excl = incl - olen;
+          const bool take = valid && cnt + (uint32_t)lane < 64 && bytes + excl < BATCH_CAP;
+          const uint32_t m = (uint32_t)__builtin_popcountll(__ballot(take));
+          if (take) {
+            S.rec[cnt + lane] = rec_t;
+            S.roff[cnt + lane] = (uint16_t)(bytes + excl);
+          }
+          if (m) {
+            o = U(__builtin_amdgcn_readlane(p + (info_t & 255), (int)(m - 1)));
+            bytes += U(__builtin_amdgcn_readlane(incl, (int)(m - 1)));
+            cnt += m;
+          }
+          if (m < 64 && cnt < 64 && bytes < BATCH_CAP) {
+            const uint32_t pm = U(__builtin_amdgcn_readlane(p, (int)m));
+            if (pm < 64) {  // symbol m starts in the window and is not valid: a stop symbol
+              const uint32_t a = U(__builtin_amdgcn_readlane(info_t, (int)m));
+              o = pm;
+              if (a == (F_EOB | (a & 255))) {
+                o += a & 255;
+                eob = true;
+              } else if (a & F_BAD) {
+                err = ZG_CORRUPT_STREAM;
+              } else {
+                slow = true;
+              }
+            }
+          }
+        }
+        bp += o;
+#else
         uint64_t chain = 0;
         uint32_t o = 0, n = 0;
         bool slow = false;
@@ -593,12 +680,14 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(ZG_INFLATE_W
         if ((chain >> lane) & 1) S.rec[cnt + __builtin_amdgcn_mbcnt_hi((uint32_t)(chain >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)chain, 0u))] = rec;
         cnt += n;
         bp += o;
+#endif
         if (slow && !err && cnt < 64 && bytes < BATCH_CAP) {
           // one symbol through the canonical slow path (codes longer than the root)
           bits_seek_in(B, bp);
           const uint32_t e = decode_sym(B, S.ltab, LROOT, S.lsorted, S.lm, 0);
           const uint32_t kind = (e >> 4) & 3;
           uint32_t r = 0;
+          const uint32_t off0 = bytes;
           bool has = false;
           if (kind == K_LIT) {
             r = e >> 16;
@@ -627,7 +716,10 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(ZG_INFLATE_W
             }
           }
           if (has) {
-            if (lane == 0) S.rec[cnt] = r;
+            if (lane == 0) {
+              S.rec[cnt] = r;
+              S.roff[cnt] = (uint16_t)off0;
+            }
             cnt++;
           }
           bp = B.consumed;
@@ -644,6 +736,9 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(ZG_INFLATE_W
       const bool mine = lane < (int)cnt;
       const uint32_t rec = mine ? S.rec[lane] : 0u;
       const bool is_match = mine && (rec >> 31);
+#if ZG_INFLATE_PJ
+      const uint64_t mypos = pos + (mine ? S.roff[lane] : 0u);
+#else
       const uint32_t ln = mine ? (is_match ? (rec & 511) : 1u) : 0u;
       uint32_t inc = ln;  // inclusive wave scan of output lengths
       for (int off = 1; off < 64; off <<= 1) {
@@ -651,6 +746,7 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(ZG_INFLATE_W
         if (lane >= off) inc += t;
       }
       const uint64_t mypos = pos + inc - ln;
+#endif
       if (mine && !is_match) S.ring[mypos & RMASK] = (uint8_t)rec;
       const uint64_t batch_end = pos + bytes;
       const uint32_t mlen = rec & 511, md = (rec >> 9) & 0xFFFF;
@@ -685,8 +781,27 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(ZG_INFLATE_W
           continue;
         }
         const bool ready = pending && mlen <= 32 && (lane == first || msrc + mlen <= F);
+        const bool in_ring = msrc + RING >= batch_end;
+#if ZG_INFLATE_XW
+        if (ready && in_ring && md >= mlen && mlen <= ZG_INFLATE_XW) {
+          // a short source wholly in the ring, not overlapping the copy: aligned ring words (all
+          // loads in flight together), byte-aligned in registers
+          const uint32_t *rw = (const uint32_t *)S.ring;
+          const uint32_t a0 = (uint32_t)(msrc >> 2), sh = (uint32_t)(msrc & 3), nw = (sh + mlen + 3) >> 2;
+          uint32_t w[ZG_INFLATE_XW / 4 + 1];
+#pragma unroll
+          for (uint32_t j = 0; j <= ZG_INFLATE_XW / 4; j++) w[j] = j < nw ? rw[(a0 + j) & (RING / 4 - 1)] : 0u;
+#pragma unroll
+          for (uint32_t j = 0; j < ZG_INFLATE_XW / 4; j++) {
+            const uint32_t v = __builtin_amdgcn_alignbyte(w[j + 1], w[j], sh);
+#pragma unroll
+            for (uint32_t k = 0; k < 4; k++)
+              if (4 * j + k < mlen) S.ring[(mypos + 4 * j + k) & RMASK] = (uint8_t)(v >> (8 * k));
+          }
+          pending = false;
+        } else
+#endif
         if (ready) {
-          const bool in_ring = msrc + RING >= batch_end;
           for (uint32_t i0 = 0; i0 < mlen; i0 += 4) {
             uint8_t v[4];
 #pragma unroll

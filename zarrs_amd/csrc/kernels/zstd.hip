@@ -47,6 +47,12 @@ constexpr int ZBATCH = 4096;         // max output span of one sequence batch
 constexpr uint32_t ZBIG = 2048;      // sequences with a longer run are executed alone, chunked
 constexpr uint32_t BLOCK_MAX = 131072;
 constexpr uint32_t MAX_HUF_LOG = 12;
+// a block's Huffman decoding table in the literal scratch, right before its literals: 2^12 u16
+// entries + a 16-B header holding the table log (0: invalid description)
+constexpr uint32_t HUF_TAB = (1u << MAX_HUF_LOG) * 2 + 16;
+#ifndef ZG_HUF_SPLIT
+#define ZG_HUF_SPLIT 1  // Huffman tables built by k_zstd_huf (one wave per block) ahead of k_zstd_lits
+#endif
 // per-item decode mode chosen by k_zstd_scan
 constexpr uint32_t ZMODE_PARALLEL = 0, ZMODE_SERIAL = 1, ZMODE_SKIP = 2;
 
@@ -1170,18 +1176,17 @@ struct SeqX {
   uint16_t next;
   uint8_t nb, nbx;
 };
+#ifndef ZG_SEQ_ONE_FSE
+#define ZG_SEQ_ONE_FSE 1  // one FSE scratch table, folded into its SeqX table at once (0: three tables)
+#endif
 struct ZDecSmem {
-  union {
-    uint16_t huf[1 << MAX_HUF_LOG];
-    struct {
-      Fse ll[512], ml[512], of[256];
-    };
-  };
+#if ZG_SEQ_ONE_FSE
+  Fse fse[512];  // one FSE table at a time: built, then folded into its SeqX table
+#else
+  Fse ll[512], ml[512], of[256];
+#endif
   SeqX xl[512], xm[512], xo[256];
-  Fse wt[64];
   int16_t norm[64];
-  uint8_t weights[256];
-  uint16_t hsorted[256];
   uint32_t tmp[32];
 };
 
@@ -1328,6 +1333,9 @@ __global__ __launch_bounds__(64) void k_zstd_scan(const ZgItem *items, uint32_t 
           p += csize;
         }
         if (ltype != 0) {  // rle / huffman literals are materialised in the literal scratch
+#if ZG_HUF_SPLIT
+          if (ltype >= 2) lit_used = ((lit_used + 15) & ~(uint64_t)15) + HUF_TAB;  // the block's table
+#endif
           R.lit_buf = (uint32_t)lit_used;
           lit_used += regen;
           if (lit_used > lit_stride) { serial = true; break; }
@@ -1429,7 +1437,6 @@ __global__ __launch_bounds__(64) void k_zstd_blocks(const ZgItem *items, uint32_
     (void)ltype;
     (void)regen;
     (void)lit;
-    __syncthreads();  // Huffman table reads done: the FSE tables reuse its LDS
     // ---- sequences ----
     const uint32_t nseq = U(Bp->nseq);
     uint64_t sum_ll = 0, sum_ml = 0;
@@ -1441,7 +1448,11 @@ __global__ __launch_bounds__(64) void k_zstd_blocks(const ZgItem *items, uint32_
       uint32_t lg[3] = {0, 0, 0};
       for (int t = 0; t < 3 && !bad; t++) {
         const uint32_t mode = (tm >> (2 * t)) & 3, off = U(Bp->tab_off[t]);
+#if ZG_SEQ_ONE_FSE
+        Fse *T = S.fse;
+#else
         Fse *T = t == 0 ? S.ll : t == 1 ? S.of : S.ml;
+#endif
         const uint32_t maxs = t == 0 ? 35 : t == 1 ? 31 : 52, maxl = t == 0 ? 9 : t == 1 ? 8 : 9;
         if (mode == 0) {
           if (t == 0) { build_fse_default(T, c_ll_def, 36, 6, S.norm, S.tmp); lg[t] = 6; }
@@ -1458,27 +1469,24 @@ __global__ __launch_bounds__(64) void k_zstd_blocks(const ZgItem *items, uint32_
           build_fse(T, S.norm, ns, acc, S.tmp);
           lg[t] = acc;
         }
-      }
-      // value bases / extra bits folded into the decoding tables
-      if (!bad) {
+        // value bases / extra bits folded into the decoding table
         __syncthreads();
-        for (uint32_t u = lane; u < (1u << lg[0]); u += 64) {
-          const Fse e = S.ll[u];
-          const bool ok = e.sym <= 35;
-          S.xl[u] = SeqX{ok ? c_ll_base[e.sym] : 0u, e.base, e.nb, (uint8_t)(ok ? c_ll_bits[e.sym] : 0xFF)};
+        for (uint32_t u = lane; u < (1u << lg[t]); u += 64) {
+          const Fse e = T[u];
+          if (t == 0) {
+            const bool ok = e.sym <= 35;
+            S.xl[u] = SeqX{ok ? c_ll_base[e.sym] : 0u, e.base, e.nb, (uint8_t)(ok ? c_ll_bits[e.sym] : 0xFF)};
+          } else if (t == 1) {
+            const bool ok = e.sym <= 31;
+            S.xo[u] = SeqX{ok ? (1u << e.sym) : 0u, e.base, e.nb, (uint8_t)(ok ? e.sym : 0xFF)};
+          } else {
+            const bool ok = e.sym <= 52;
+            S.xm[u] = SeqX{ok ? c_ml_base[e.sym] : 0u, e.base, e.nb, (uint8_t)(ok ? c_ml_bits[e.sym] : 0xFF)};
+          }
         }
-        for (uint32_t u = lane; u < (1u << lg[2]); u += 64) {
-          const Fse e = S.ml[u];
-          const bool ok = e.sym <= 52;
-          S.xm[u] = SeqX{ok ? c_ml_base[e.sym] : 0u, e.base, e.nb, (uint8_t)(ok ? c_ml_bits[e.sym] : 0xFF)};
-        }
-        for (uint32_t u = lane; u < (1u << lg[1]); u += 64) {
-          const Fse e = S.of[u];
-          const bool ok = e.sym <= 31;
-          S.xo[u] = SeqX{ok ? (1u << e.sym) : 0u, e.base, e.nb, (uint8_t)(ok ? e.sym : 0xFF)};
-        }
-        __syncthreads();
+        if (ZG_SEQ_ONE_FSE) __syncthreads();  // the next table reuses S.fse
       }
+      if (!ZG_SEQ_ONE_FSE) __syncthreads();
       // Backward bit container in SGPRs: C holds bits [32 * lw, 32 * lw + have) of the aligned item
       // words, the next unread bit at bit 63; refilled a word at a time from the BitsBack register
       // window (readlane), so a field read is three scalar operations.
@@ -1638,6 +1646,10 @@ __global__ __launch_bounds__(64) void k_zstd_blocks(const ZgItem *items, uint32_
 constexpr uint32_t LIT_LDS = ZG_LIT_LDS;
 constexpr int32_t LIT_WARM = 128;
 constexpr uint32_t LIT_THREADS = 256;
+#ifndef ZG_LIT_WPE
+#define ZG_LIT_WPE 4  // waves per SIMD k_zstd_lits is compiled for (4: <= 128 VGPRs)
+#endif
+constexpr int LIT_STAGE_R = ZG_LIT_WPE >= 4 ? 4 : 8;  // 16-B staging loads in flight per thread
 
 struct ZLitSmem {
   uint16_t huf[1 << MAX_HUF_LOG];
@@ -1766,7 +1778,51 @@ __device__ bool lits_decode(ZLitSmem &S, const Wd &word, uint32_t nstreams, cons
   return true;
 }
 
-__global__ __launch_bounds__(LIT_THREADS) void k_zstd_lits(const ZgItem *items, uint32_t *status, const ZBlk *blks,
+#if ZG_HUF_SPLIT
+struct ZHufSmem {
+  uint16_t huf[1 << MAX_HUF_LOG];
+  Fse wt[64];
+  int16_t norm[64];
+  uint8_t weights[256];
+  uint16_t hsorted[256];
+  uint32_t tmp[32];
+};
+
+// One wave per Huffman-literal block record (block-major, like k_zstd_lits): parse the tree
+// description in effect and build the decoding table into the literal scratch ahead of the block's
+// literals. Kept out of k_zstd_lits: the table build needs ~110 more VGPRs than the decode, which
+// held the 256-lane literal decoder to 2 workgroups per CU while 3 of its 4 waves waited.
+__global__ __launch_bounds__(64) void k_zstd_huf(const ZgItem *items, const uint32_t *status, const ZBlk *blks,
+                                                 uint32_t blk_cap, const uint32_t *nblk, const uint32_t *zmode,
+                                                 uint32_t n_items, uint8_t *lit_scratch, uint64_t lit_stride) {
+  __shared__ __attribute__((aligned(16))) ZHufSmem S;
+  const uint32_t lane = threadIdx.x;
+  const uint64_t total = (uint64_t)n_items * blk_cap;
+  for (uint64_t g = blockIdx.x; g < total; g += gridDim.x) {
+    const uint32_t item = (uint32_t)(g % n_items), bi = (uint32_t)(g / n_items);  // block-major order
+    if (bi >= nblk[item] || zmode[item] != ZMODE_PARALLEL) continue;
+    const ZBlk *Bp = blks + (uint64_t)item * blk_cap + bi;
+    const uint32_t flags = Bp->flags;
+    if ((flags & 3) != ZB_CMP || ((flags >> 2) & 3) < 2) continue;
+    const ZgItem it = items[item];
+    const uint8_t *in = (const uint8_t *)it.src;
+    const uint32_t huf_off = Bp->huf_off;
+    uint8_t *tab = lit_scratch + (uint64_t)item * lit_stride + Bp->lit_buf - HUF_TAB;
+    __syncthreads();  // the previous record's LDS use is over
+    const In I{in, it.len};
+    uint32_t tl = 0;
+    const uint32_t ok = read_huffman<ZHufSmem, false>(I, huf_off, it.len - huf_off, S, tl, in, it.len);
+    __syncthreads();
+    if (ok) {
+      const uint32_t n16 = ((2u << tl) + 15) / 16;  // tables of 2^tl u16 entries (tl >= 1)
+      for (uint32_t v = lane; v < n16; v += 64) ((uint4 *)tab)[v] = ((const uint4 *)S.huf)[v];
+    }
+    if (lane == 0) *(uint32_t *)(tab + (HUF_TAB - 16)) = ok ? tl : 0u;
+  }
+}
+#endif
+
+__global__ __launch_bounds__(LIT_THREADS) __attribute__((amdgpu_waves_per_eu(ZG_LIT_WPE, 8))) void k_zstd_lits(const ZgItem *items, uint32_t *status, const ZBlk *blks,
                                                            uint32_t blk_cap, const uint32_t *nblk,
                                                            const uint32_t *zmode, uint32_t n_items,
                                                            uint8_t *lit_scratch, uint64_t lit_stride) {
@@ -1790,7 +1846,18 @@ __global__ __launch_bounds__(LIT_THREADS) void k_zstd_lits(const ZgItem *items, 
       for (uint32_t k = t; k < regen; k += LIT_THREADS) lit[k] = v;
       continue;
     }
-    const uint32_t huf_off = Bp->huf_off, lo0 = Bp->lit_off, lend = Bp->lit_end;
+    const uint32_t lo0 = Bp->lit_off, lend = Bp->lit_end;
+#if ZG_HUF_SPLIT
+    // the table k_zstd_huf built: 16-B loads, one per thread
+    const uint8_t *tab = lit - HUF_TAB;
+    const uint32_t tl = *(const uint32_t *)(tab + (HUF_TAB - 16));
+    if (tl) {
+      const uint32_t n16 = ((2u << tl) + 15) / 16;  // tables of 2^tl u16 entries (tl >= 1)
+      for (uint32_t v = t; v < n16; v += LIT_THREADS) ((uint4 *)S.huf)[v] = ((const uint4 *)tab)[v];
+    }
+    __syncthreads();
+#else
+    const uint32_t huf_off = Bp->huf_off;
     if (t < 64) {  // wave 0 builds the table
       const In I{in, it.len};
       uint32_t tl = 0;
@@ -1801,6 +1868,7 @@ __global__ __launch_bounds__(LIT_THREADS) void k_zstd_lits(const ZgItem *items, 
     }
     __syncthreads();
     const uint32_t tl = S.ctl[0];
+#endif
     bool bad = tl == 0;
     const uint32_t nstreams = (flags >> 4) & 1 ? 4 : 1;
     uint64_t s_lo[4] = {lo0, 0, 0, 0}, s_hi[4] = {lend, 0, 0, 0};
@@ -1840,13 +1908,13 @@ __global__ __launch_bounds__(LIT_THREADS) void k_zstd_lits(const ZgItem *items, 
     if (!bad) {
       const int64_t nw = wend - wbase;
       if (nw * 4 <= (int64_t)LIT_LDS) {
-        // 16-B loads, 8 per thread in flight before the first LDS write
+        // 16-B loads, LIT_STAGE_R per thread in flight before the first LDS write
         const int64_t a16 = wbase & ~(int64_t)3, n16 = (wend - a16 + 3) >> 2;
         const uint32_t sh = (uint32_t)(wbase - a16);  // words of the first vector before the section
-        for (int64_t v0 = 0; v0 < n16; v0 += 8 * LIT_THREADS) {
-          zv4u r[8];
+        for (int64_t v0 = 0; v0 < n16; v0 += LIT_STAGE_R * LIT_THREADS) {
+          zv4u r[LIT_STAGE_R];
 #pragma unroll
-          for (int q = 0; q < 8; q++) {
+          for (int q = 0; q < LIT_STAGE_R; q++) {
             const int64_t v = v0 + q * LIT_THREADS + t;
             if (v < n16) {
               const gu32 *src = (const gu32 *)(words + a16 + 4 * v);
@@ -1859,7 +1927,7 @@ __global__ __launch_bounds__(LIT_THREADS) void k_zstd_lits(const ZgItem *items, 
             }
           }
 #pragma unroll
-          for (int q = 0; q < 8; q++) {
+          for (int q = 0; q < LIT_STAGE_R; q++) {
             const int64_t v = v0 + q * LIT_THREADS + t;
             if (v < n16) {
               const uint32_t w4[4] = {r[q].x, r[q].y, r[q].z, r[q].w};
@@ -2836,7 +2904,9 @@ void zstd_scratch_layout(uint64_t slot_bytes, uint32_t &blk_cap, uint64_t &blk_b
                          uint64_t &seq_cap) {
   blk_cap = (uint32_t)std::min<uint64_t>(slot_bytes / 32768 + 64, 1u << 20);
   blk_bytes = sizeof(ZBlk);
-  lit_stride = std::max<uint64_t>(slot_bytes, BLOCK_MAX + 64);
+  // literals (<= the decoded size) + one Huffman table per block (HUF_TAB per >= 64 KiB of output on
+  // typical frames; frames of many tiny Huffman blocks overflow it and take the serial decoder)
+  lit_stride = std::max<uint64_t>(slot_bytes + slot_bytes / 8, BLOCK_MAX + 64 + 2 * HUF_TAB);
   lit_stride = (lit_stride + 255) & ~(uint64_t)255;
   seq_cap = slot_bytes / 4 + 1024;  // sequences per item (each decodes >= 3 bytes; typical >= 8)
 }
@@ -2858,6 +2928,10 @@ hipError_t launch_zstd(ZgItem *items, uint32_t *status, uint32_t n_items, uint8_
   }();
   const uint32_t grid = (uint32_t)std::min<uint64_t>(recs, g_cap);
   const uint32_t lgrid = (uint32_t)std::min<uint64_t>(recs, l_cap);
+#if ZG_HUF_SPLIT
+  hipLaunchKernelGGL(k_zstd_huf, dim3(grid), dim3(64), 0, s, items, status, blks, Z.blk_cap, Z.nblk, Z.mode, n_items,
+                     Z.lit, Z.lit_stride);
+#endif
   hipLaunchKernelGGL(k_zstd_lits, dim3(lgrid), dim3(LIT_THREADS), 0, s, items, status, blks, Z.blk_cap, Z.nblk,
                      Z.mode, n_items, Z.lit, Z.lit_stride);
   hipLaunchKernelGGL(k_zstd_blocks, dim3(grid), dim3(64), 0, s, items, status, blks, Z.blk_cap, Z.nblk, Z.mode,
