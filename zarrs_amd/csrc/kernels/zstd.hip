@@ -1647,7 +1647,7 @@ constexpr uint32_t LIT_LDS = ZG_LIT_LDS;
 constexpr int32_t LIT_WARM = 128;
 constexpr uint32_t LIT_THREADS = 256;
 #ifndef ZG_LIT_WPE
-#define ZG_LIT_WPE 4  // waves per SIMD k_zstd_lits is compiled for (4: <= 128 VGPRs)
+#define ZG_LIT_WPE 3  // waves per SIMD k_zstd_lits is compiled for (A/B: 3 beats 2 and 4 on C5)
 #endif
 constexpr int LIT_STAGE_R = ZG_LIT_WPE >= 4 ? 4 : 8;  // 16-B staging loads in flight per thread
 
@@ -2924,7 +2924,8 @@ hipError_t launch_zstd(ZgItem *items, uint32_t *status, uint32_t n_items, uint8_
   }();
   static const uint64_t l_cap = [] {
     const char *e = std::getenv("ZGPU_ZSTD_LGRID");
-    return e ? std::max<uint64_t>(1, std::strtoull(e, nullptr, 10)) : (uint64_t)256 * 2;
+    // one resident wave of workgroups: 256 CUs x ZG_LIT_WPE workgroups of 256 lanes (4 waves) each
+    return e ? std::max<uint64_t>(1, std::strtoull(e, nullptr, 10)) : (uint64_t)256 * ZG_LIT_WPE;
   }();
   const uint32_t grid = (uint32_t)std::min<uint64_t>(recs, g_cap);
   const uint32_t lgrid = (uint32_t)std::min<uint64_t>(recs, l_cap);
