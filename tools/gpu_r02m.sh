@@ -6,6 +6,9 @@ cd "$GRAFT_REPO_ROOT"
 export TMPDIR=/tmp
 O=gpurun_out/r02m
 mkdir -p $O
+echo "== gzip lab profile"
+timeout -k 10 120 zarrs_amd/lib_variants/gz/prof 15625 1 > $O/lab_prof.txt 2>&1 || { echo "rc=$?"; tail -3 $O/lab_prof.txt; exit 1; }
+grep -A8 k_gzip $O/lab_prof.txt
 echo "== pytest zstd paths"
 timeout -k 10 600 python -u -m pytest tests/test_gpu_codecs.py tests/test_gpu_c3c5.py tests/test_gpu_blosc.py tests/test_gpu_parity.py -q -m gpu -x --timeout 120 --timeout-method thread > $O/pytest.log 2>&1; rc=$?
 tail -3 $O/pytest.log; echo "pytest rc=$rc"

@@ -111,5 +111,8 @@ int main(int argc, char **argv) {
   const char *names[] = {"hdr+tables", "sym decode", "execute", "flush+sync", "total"};
   for (int i = 0; i < 5; i++)
     printf("  %-12s %6.1f%%  %.0f cycles/chunk\n", names[i], 100.0 * prof[i] / tot, (double)prof[i] / n);
+  if (prof[6])
+    printf("  per chunk: %.0f batches, %.1f symbols/batch, %.2f match rounds/batch\n", (double)prof[6] / n,
+           (double)prof[7] / prof[6], (double)prof[5] / prof[6]);
   return bad ? 1 : 0;
 }

@@ -35,15 +35,17 @@ namespace zgpu {
 // lab builds only (tools/lab): per-phase shader-clock totals, summed over waves
 __device__ unsigned long long g_prof[8];
 // per-wave accumulators (prof_acc[], declared by PROF_DECL), flushed once per wave by PROF_FLUSH
-#define PROF_DECL uint64_t prof_acc[5] = {0, 0, 0, 0, 0}
+#define PROF_DECL uint64_t prof_acc[8] = {0, 0, 0, 0, 0, 0, 0, 0}
 #define PROF_T(v) const uint64_t v = clock64()
 #define PROF_ADD(slot, t0) prof_acc[slot] += clock64() - (t0)
-#define PROF_FLUSH do { if (__lane_id() == 0) for (int k_ = 0; k_ < 5; k_++) atomicAdd(&g_prof[k_], (unsigned long long)prof_acc[k_]); } while (0)
+#define PROF_CNT(slot, n) prof_acc[slot] += (n)  // event counts: 5 match rounds, 6 batches, 7 symbols
+#define PROF_FLUSH do { if (__lane_id() == 0) for (int k_ = 0; k_ < 8; k_++) atomicAdd(&g_prof[k_], (unsigned long long)prof_acc[k_]); } while (0)
 #else
 #define PROF_DECL
 #define PROF_FLUSH
 #define PROF_T(v)
 #define PROF_ADD(slot, t0)
+#define PROF_CNT(slot, n)
 #endif
 
 namespace {
@@ -60,6 +62,9 @@ constexpr int FLUSH_MIN = RING / 4;  // flush the ring to the slot once this man
 // unflushed bytes stay below FLUSH_MIN + BATCH_CAP + 258 < RING: every source older than the ring
 // has been flushed
 constexpr int LROOT = 10, DROOT = 8;
+#ifndef ZG_INFLATE_XDEP
+#define ZG_INFLATE_XDEP 1  // matches resolve by exact dependencies (0: first-pending frontier)
+#endif
 #ifndef ZG_INFLATE_XW
 #define ZG_INFLATE_XW 8  // > 0: in-ring matches up to this many bytes copy through aligned ring words
 #endif
@@ -95,7 +100,10 @@ struct HuffMeta {  // canonical code description for the slow path
 };
 
 struct Smem {
-  uint8_t ring[RING];
+  union {  // the output ring, also read as aligned words (no generic-pointer cast of LDS)
+    uint8_t ring[RING];
+    uint32_t ring32[RING / 4];
+  };
   uint32_t ltab[1 << LROOT];
   uint32_t dtab[1 << DROOT];
   uint16_t lsorted[288];
@@ -107,6 +115,7 @@ struct Smem {
   uint32_t tmp[16];
   uint32_t rec[64];   // the batch's symbols: literal byte, or (1<<31)|(dist<<9)|len
   uint16_t roff[64];  // their output offsets in the batch
+  uint16_t rbeg[64], rend[64];  // output interval of each symbol in the batch (match dependencies)
 };
 
 __device__ __forceinline__ uint32_t U(uint32_t x) { return __builtin_amdgcn_readfirstlane(x); }
@@ -754,19 +763,43 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(ZG_INFLATE_W
       if (__ballot(is_match && md > mypos)) { err = ZG_CORRUPT_STREAM; break; }  // distance too far back
       // sources older than the ring are read back from the flushed output
       if (__ballot(is_match && msrc + RING < batch_end)) __threadfence_block();
-      // Matches resolve in rounds: every pending match whose source lies entirely before the first
-      // pending match (or that IS the first one) copies its bytes itself; dest byte i takes source
-      // byte msrc + (i mod d), which is always final, so a lane's copy has no inner dependency.
+#if ZG_INFLATE_XDEP
+      // Matches resolve in rounds by exact dependencies: a match waits only while the last symbol
+      // starting before the end of its source (found once per batch by a binary search over the
+      // symbols' output offsets) is a pending match whose output reaches into that source. A match
+      // reads at most min(len, dist) source bytes (dest byte i takes source byte i mod dist), all
+      // before its own output, so ready matches never depend on each other. Long ready matches are
+      // copied by the whole wave one after another, short ones by their own lane.
+      const int32_t s_rel = (int32_t)(msrc - pos);                   // source start, batch-relative
+      const int32_t e_rel = s_rel + (int32_t)min(mlen, md);          // source end
+      if (mine) S.rend[lane] = (uint16_t)(mypos - pos + (is_match ? mlen : 1u));
+      if (mine) S.rbeg[lane] = (uint16_t)(mypos - pos);
+      __syncthreads();
+      int32_t hi = -1;  // the last symbol that starts before e_rel
+      if (is_match && e_rel > 0) {
+        hi = 0;
+#pragma unroll
+        for (int32_t step = 32; step; step >>= 1)
+          if (hi + step < (int32_t)cnt && (int32_t)S.rbeg[hi + step] < e_rel) hi += step;
+      }
       bool pending = is_match;
       uint64_t pm;
+      PROF_CNT(6, 1);
+      PROF_CNT(7, cnt);
       while ((pm = __ballot(pending)) != 0) {
-        const int first = __builtin_ctzll(pm);
-        const uint32_t F_lo = __builtin_amdgcn_readlane((uint32_t)mypos, first);
-        const uint32_t F_hi = __builtin_amdgcn_readlane((uint32_t)(mypos >> 32), first);
-        const uint64_t F = ((uint64_t)F_hi << 32) | F_lo;
-        const uint32_t flen = __builtin_amdgcn_readlane(mlen, first);
-        if (flen > 32) {  // a long match: copied by the whole wave once it is the first pending
-          const uint32_t fd = __builtin_amdgcn_readlane(md, first);
+        PROF_CNT(5, 1);
+        bool ready = false;
+        if (pending) {
+          const uint64_t m = hi < 0 ? 0ull : pm & (hi >= 63 ? ~0ull : ((2ull << hi) - 1));
+          ready = m == 0 || (int32_t)S.rend[63 - __builtin_clzll(m)] <= s_rel;
+        }
+        const uint64_t lm = __ballot(ready && mlen > 32);
+        if (lm) {  // the first long ready match, by the whole wave (the others wait a round)
+          const int f = __builtin_ctzll(lm);
+          const uint32_t F_lo = __builtin_amdgcn_readlane((uint32_t)mypos, f);
+          const uint32_t F_hi = __builtin_amdgcn_readlane((uint32_t)(mypos >> 32), f);
+          const uint64_t F = ((uint64_t)F_hi << 32) | F_lo;
+          const uint32_t flen = __builtin_amdgcn_readlane(mlen, f), fd = __builtin_amdgcn_readlane(md, f);
           const float inv = 1.0f / (float)fd;
           for (uint32_t i = lane; i < flen; i += 64) {
             uint32_t q = (uint32_t)((float)i * inv);
@@ -777,20 +810,18 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(ZG_INFLATE_W
             const uint8_t v = (src + RING >= batch_end) ? S.ring[src & RMASK] : __builtin_nontemporal_load(out + src);
             S.ring[(F + i) & RMASK] = v;
           }
-          if (lane == first) pending = false;
-          continue;
         }
-        const bool ready = pending && mlen <= 32 && (lane == first || msrc + mlen <= F);
+        if (lm && lane == __builtin_ctzll(lm)) pending = false;
+        ready = ready && mlen <= 32;
         const bool in_ring = msrc + RING >= batch_end;
 #if ZG_INFLATE_XW
         if (ready && in_ring && md >= mlen && mlen <= ZG_INFLATE_XW) {
           // a short source wholly in the ring, not overlapping the copy: aligned ring words (all
           // loads in flight together), byte-aligned in registers
-          const uint32_t *rw = (const uint32_t *)S.ring;
           const uint32_t a0 = (uint32_t)(msrc >> 2), sh = (uint32_t)(msrc & 3), nw = (sh + mlen + 3) >> 2;
           uint32_t w[ZG_INFLATE_XW / 4 + 1];
 #pragma unroll
-          for (uint32_t j = 0; j <= ZG_INFLATE_XW / 4; j++) w[j] = j < nw ? rw[(a0 + j) & (RING / 4 - 1)] : 0u;
+          for (uint32_t j = 0; j <= ZG_INFLATE_XW / 4; j++) w[j] = j < nw ? S.ring32[(a0 + j) & (RING / 4 - 1)] : 0u;
 #pragma unroll
           for (uint32_t j = 0; j < ZG_INFLATE_XW / 4; j++) {
             const uint32_t v = __builtin_amdgcn_alignbyte(w[j + 1], w[j], sh);
@@ -818,6 +849,74 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(ZG_INFLATE_W
           pending = false;
         }
       }
+#else
+      // Matches resolve in rounds: every pending match whose source lies entirely before the first
+      // pending match (or that IS the first one) copies its bytes itself; dest byte i takes source
+      // byte msrc + (i mod d), which is always final, so a lane's copy has no inner dependency.
+      bool pending = is_match;
+      uint64_t pm;
+      PROF_CNT(6, 1);
+      PROF_CNT(7, cnt);
+      while ((pm = __ballot(pending)) != 0) {
+        PROF_CNT(5, 1);
+        const int first = __builtin_ctzll(pm);
+        const uint32_t F_lo = __builtin_amdgcn_readlane((uint32_t)mypos, first);
+        const uint32_t F_hi = __builtin_amdgcn_readlane((uint32_t)(mypos >> 32), first);
+        const uint64_t F = ((uint64_t)F_hi << 32) | F_lo;
+        const uint32_t flen = __builtin_amdgcn_readlane(mlen, first);
+        if (flen > 32) {  // a long match: copied by the whole wave once it is the first pending
+          const uint32_t fd = __builtin_amdgcn_readlane(md, first);
+          const float inv = 1.0f / (float)fd;
+          for (uint32_t i = lane; i < flen; i += 64) {
+            uint32_t q = (uint32_t)((float)i * inv);
+            int32_t rm = (int32_t)i - (int32_t)(q * fd);
+            if (rm < 0) rm += fd;
+            if (rm >= (int32_t)fd) rm -= fd;
+            const uint64_t src = F - fd + (uint32_t)rm;
+            const uint8_t v = (src + RING >= batch_end) ? S.ring[src & RMASK] : __builtin_nontemporal_load(out + src);
+            S.ring[(F + i) & RMASK] = v;
+          }
+          if (lane == first) pending = false;
+          continue;
+        }
+        const bool ready = pending && mlen <= 32 && (lane == first || msrc + mlen <= F);
+        const bool in_ring = msrc + RING >= batch_end;
+#if ZG_INFLATE_XW
+        if (ready && in_ring && md >= mlen && mlen <= ZG_INFLATE_XW) {
+          // a short source wholly in the ring, not overlapping the copy: aligned ring words (all
+          // loads in flight together), byte-aligned in registers
+          const uint32_t a0 = (uint32_t)(msrc >> 2), sh = (uint32_t)(msrc & 3), nw = (sh + mlen + 3) >> 2;
+          uint32_t w[ZG_INFLATE_XW / 4 + 1];
+#pragma unroll
+          for (uint32_t j = 0; j <= ZG_INFLATE_XW / 4; j++) w[j] = j < nw ? S.ring32[(a0 + j) & (RING / 4 - 1)] : 0u;
+#pragma unroll
+          for (uint32_t j = 0; j < ZG_INFLATE_XW / 4; j++) {
+            const uint32_t v = __builtin_amdgcn_alignbyte(w[j + 1], w[j], sh);
+#pragma unroll
+            for (uint32_t k = 0; k < 4; k++)
+              if (4 * j + k < mlen) S.ring[(mypos + 4 * j + k) & RMASK] = (uint8_t)(v >> (8 * k));
+          }
+          pending = false;
+        } else
+#endif
+        if (ready) {
+          for (uint32_t i0 = 0; i0 < mlen; i0 += 4) {
+            uint8_t v[4];
+#pragma unroll
+            for (int k = 0; k < 4; k++) {
+              const uint32_t i = i0 + k;
+              const uint32_t r = i < md ? i : i % md;
+              const uint64_t src = msrc + r;
+              v[k] = (i < mlen) ? (in_ring ? S.ring[src & RMASK] : __builtin_nontemporal_load(out + src)) : 0;
+            }
+#pragma unroll
+            for (int k = 0; k < 4; k++)
+              if (i0 + k < mlen) S.ring[(mypos + i0 + k) & RMASK] = v[k];
+          }
+          pending = false;
+        }
+      }
+#endif
       PROF_ADD(2, t_exe);
       PROF_T(t_fl);
       pos = batch_end;
