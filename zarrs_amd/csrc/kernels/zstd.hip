@@ -1650,6 +1650,15 @@ constexpr uint32_t LIT_THREADS = 256;
 #define ZG_LIT_WPE 3  // waves per SIMD k_zstd_lits is compiled for (A/B: 3 beats 2 and 4 on C5)
 #endif
 constexpr int LIT_STAGE_R = ZG_LIT_WPE >= 4 ? 4 : 8;  // 16-B staging loads in flight per thread
+#ifndef ZG_LIT_PACK
+#define ZG_LIT_PACK 1  // decoded literals stored ZG_LIT_PACK_B at a time
+#endif
+#ifndef ZG_LIT_PACK_B
+#define ZG_LIT_PACK_B 8
+#endif
+#ifndef ZG_LIT_GWIN
+#define ZG_LIT_GWIN 1  // literal sections beyond LIT_LDS read through a per-lane 16-B window
+#endif
 
 struct ZLitSmem {
   uint16_t huf[1 << MAX_HUF_LOG];
@@ -1683,6 +1692,15 @@ __device__ __forceinline__ uint32_t hl_run(HufLane &H, int32_t &p, int32_t stop,
                                            const Wd &word, uint8_t *out, uint32_t maxn) {
   uint32_t n = 0;
   const uint32_t sh = 64 - tl;
+#if ZG_LIT_PACK
+  // symbols are stored ZG_LIT_PACK_B at a time (aligned 8- or 16-B stores; bytes up to the first
+  // boundary and the tail singly): 256 lanes writing their own segments byte by byte made every byte
+  // a partial-line write-back (PMC: ~17x the literal bytes written)
+  constexpr uint32_t PB = ZG_LIT_PACK_B;
+  uint64_t acc = 0, acc1 = 0;
+  uint32_t k = 0;
+  const uint32_t head = WRITE ? (uint32_t)((PB - ((uintptr_t)out & (PB - 1))) & (PB - 1)) : 0u;
+#endif
   while (p > stop && n < maxn) {
     if (H.v <= 32) {
       H.C |= (uint64_t)word((H.lp >> 5) - 1) << (32 - H.v);
@@ -1694,11 +1712,55 @@ __device__ __forceinline__ uint32_t hl_run(HufLane &H, int32_t &p, int32_t stop,
     H.C <<= nb;
     H.v -= (int32_t)nb;
     p -= (int32_t)nb;
+#if ZG_LIT_PACK
+    if (WRITE) {
+      if (n < head) {
+        out[n] = (uint8_t)e;
+      } else {
+        if (PB == 16 && k >= 8) acc1 |= (uint64_t)(e & 255u) << (8 * (k - 8));
+        else acc |= (uint64_t)(e & 255u) << (8 * k);
+        if (++k == PB) {
+          if (PB == 16) {
+            *(uint4 *)(out + n - 15) = make_uint4((uint32_t)acc, (uint32_t)(acc >> 32), (uint32_t)acc1, (uint32_t)(acc1 >> 32));
+          } else {
+            *(uint64_t *)(out + n - 7) = acc;
+          }
+          acc = acc1 = 0;
+          k = 0;
+        }
+      }
+    }
+#else
     if (WRITE) out[n] = (uint8_t)e;
+#endif
     n++;
   }
+#if ZG_LIT_PACK
+  if (WRITE)
+    for (uint32_t i = 0; i < k; i++) out[n - k + i] = (uint8_t)((i < 8 ? acc : acc1) >> (8 * (i & 7)));
+#endif
   return n;
 }
+
+// Literal-section words read from global memory through a per-lane 16-B window: a lane walks its
+// segment backwards one word at a time, so one aligned 16-B load serves four words (scattered 4-B
+// loads of 256 lanes fetched ~10x the section bytes from HBM).
+struct GWord {
+  const gu32 *Wp;
+  int64_t lim;
+  mutable uintptr_t cb;  // address of the cached 16-B block (1: none)
+  mutable zv4u c;
+  __device__ __forceinline__ uint32_t operator()(int32_t k) const {
+    if (k < 0 || k >= lim) return 0u;
+    const uintptr_t a = (uintptr_t)(Wp + k), b = a & ~(uintptr_t)15;
+    if (b != cb) {
+      cb = b;
+      c = *(const __attribute__((address_space(1))) zv4u *)b;
+    }
+    const uint32_t i = (uint32_t)(a >> 2) & 3u;
+    return i == 0 ? c.x : i == 1 ? c.y : i == 2 ? c.z : c.w;
+  }
+};
 
 template <class Wd>
 __device__ bool lits_decode(ZLitSmem &S, const Wd &word, uint32_t nstreams, const int32_t *top, const int32_t *lob,
@@ -1946,7 +2008,11 @@ __global__ __launch_bounds__(LIT_THREADS) __attribute__((amdgpu_waves_per_eu(ZG_
       } else {
         const gu32 *Wp = (const gu32 *)(words + wbase);
         const int64_t lim = nwords_item - wbase;
+#if ZG_LIT_GWIN
+        const GWord word{Wp, lim, 1, zv4u{0, 0, 0, 0}};
+#else
         auto word = [Wp, lim](int32_t k) -> uint32_t { return (k >= 0 && k < lim) ? Wp[k] : 0u; };
+#endif
         ok = lits_decode(S, word, nstreams, top, lob, s_n, tl, lit, seg);
       }
     }
