@@ -215,7 +215,14 @@ __global__ __launch_bounds__(64) void k_blosc_streams(ZgItem *items, uint32_t *s
 // loads when the parse leaves it), literal runs are copied from the window by all lanes, and a
 // match is one round trip to the already written output (all lanes' loads in flight together).
 // ---------------------------------------------------------------------------------------------
-constexpr uint32_t LZW = 8192;
+#ifndef ZG_LZ_RING
+#define ZG_LZ_RING 4096  // bytes of recent output kept in LDS (0: matches read back from HBM only)
+#endif
+#ifndef ZG_LZW
+#define ZG_LZW (ZG_LZ_RING ? 4096 : 8192)
+#endif
+constexpr uint32_t LZW = ZG_LZW;
+constexpr uint32_t LZR = ZG_LZ_RING > 0 ? ZG_LZ_RING : 1, LZRM = LZR - 1;
 
 struct LzIn {
   const uint8_t *in;  // the stream
@@ -248,11 +255,14 @@ struct LzIn {
     }
     return w[k];
   }
-  // out[op .. op+len) = stream[ip .. ip+len), by all lanes (window bytes from LDS, the rest global)
-  __device__ __forceinline__ void copy(uint8_t *out, uint64_t op, uint64_t ip, uint64_t len) {
+  // out[op .. op+len) = stream[ip .. ip+len), by all lanes (window bytes from LDS, the rest global);
+  // ring (if any) receives the same bytes at op mod LZR
+  __device__ __forceinline__ void copy(uint8_t *out, uint64_t op, uint64_t ip, uint64_t len, uint8_t *ring) {
     for (uint64_t i = threadIdx.x; i < len; i += 64) {
       const uint64_t k = (uintptr_t)(in + ip + i) - a;
-      out[op + i] = k < LZW ? w[k] : in[ip + i];
+      const uint8_t v = k < LZW ? w[k] : in[ip + i];
+      out[op + i] = v;
+      if (ZG_LZ_RING) ring[(op + i) & LZRM] = v;
     }
   }
 };
@@ -262,13 +272,29 @@ struct LzIn {
 // hold bytes this wave stored since its last wait: wait for them first (workgroup scope = this CU's
 // L1, which the wave's own write-through stores keep coherent; an agent-scope fence would write back
 // / invalidate L2 across XCDs). Bytes below `safe` are known complete.
-__device__ __forceinline__ void lz_match(uint8_t *out, uint64_t op, uint64_t off, uint64_t ml, uint64_t &safe) {
+// With an LDS ring of the last LZR output bytes, a match whose source and copy fit in the ring
+// (off + ml <= LZR) reads the ring instead: no wait for the wave's own stores and no HBM round trip
+// (blosc streams of shuffled images match mostly a row or two back).
+__device__ __forceinline__ void lz_match(uint8_t *out, uint64_t op, uint64_t off, uint64_t ml, uint64_t &safe,
+                                         uint8_t *ring) {
+  if (ZG_LZ_RING && off + ml <= LZR) {
+    for (uint64_t i = threadIdx.x; i < ml; i += 64) {
+      const uint8_t v = ring[(op - off + (off >= ml ? i : i % off)) & LZRM];
+      ring[(op + i) & LZRM] = v;
+      out[op + i] = v;
+    }
+    return;
+  }
   if (op - off + (off < ml ? off : ml) > safe) {
     __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "workgroup");
     safe = op;
   }
   const uint8_t *src = out + op - off;
-  for (uint64_t i = threadIdx.x; i < ml; i += 64) out[op + i] = src[off >= ml ? i : i % off];
+  for (uint64_t i = threadIdx.x; i < ml; i += 64) {
+    const uint8_t v = src[off >= ml ? i : i % off];
+    out[op + i] = v;
+    if (ZG_LZ_RING) ring[(op + i) & LZRM] = v;
+  }
 }
 
 // LZ4 block format (lz4_Block_format.md): sequences {token, literal length, literals, offset u16,
@@ -276,6 +302,7 @@ __device__ __forceinline__ void lz_match(uint8_t *out, uint64_t op, uint64_t off
 __global__ __launch_bounds__(64) void k_lz4(ZgItem *subs, uint32_t *sub_status, const uint32_t *sub_kind,
                                             uint32_t n_sub, uint8_t *dst, uint64_t slot) {
   __shared__ __attribute__((aligned(16))) uint8_t win[LZW];
+  __shared__ uint8_t ring[LZR];
   const uint32_t s = blockIdx.x, lane = threadIdx.x;
   if (sub_kind[s] != BL_KIND_LZ4 || sub_status[s] != BL_SKIP) return;
   const ZgItem it = subs[s];
@@ -299,7 +326,7 @@ __global__ __launch_bounds__(64) void k_lz4(ZgItem *subs, uint32_t *sub_status, 
       if (err) break;
     }
     if (ip + ll > cs || op + ll > slot) { err = 1; break; }
-    I.copy(out, op, ip, ll);
+    I.copy(out, op, ip, ll, ring);
     ip += ll;
     op += ll;
     if (ip == cs) break;  // last sequence: literals only
@@ -319,7 +346,7 @@ __global__ __launch_bounds__(64) void k_lz4(ZgItem *subs, uint32_t *sub_status, 
     }
     ml += 4;
     if (op + ml > slot) { err = 1; break; }
-    lz_match(out, op, off, ml, safe);
+    lz_match(out, op, off, ml, safe, ring);
     op += ml;
   }
   if (lane == 0) {
@@ -338,6 +365,7 @@ __global__ __launch_bounds__(64) void k_lz4(ZgItem *subs, uint32_t *sub_status, 
 __global__ __launch_bounds__(64) void k_blosclz(ZgItem *subs, uint32_t *sub_status, const uint32_t *sub_kind,
                                                 uint32_t n_sub, uint8_t *dst, uint64_t slot) {
   __shared__ __attribute__((aligned(16))) uint8_t win[LZW];
+  __shared__ uint8_t ring[LZR];
   const uint32_t s = blockIdx.x, lane = threadIdx.x;
   if (sub_kind[s] != BL_KIND_BLOSCLZ || sub_status[s] != BL_SKIP) return;
   const ZgItem it = subs[s];
@@ -374,14 +402,14 @@ __global__ __launch_bounds__(64) void k_blosclz(ZgItem *subs, uint32_t *sub_stat
           ip += 2;
         }
         if (op + len > slot || dist > op) { err = 1; break; }
-        lz_match(out, op, dist, len, safe);
+        lz_match(out, op, dist, len, safe, ring);
         op += len;
         if (ip >= n) break;
         ctrl = I.b(ip++);
       } else {
         const uint64_t run = ctrl + 1;
         if (op + run > slot || ip + run > n) { err = 1; break; }
-        I.copy(out, op, ip, run);
+        I.copy(out, op, ip, run, ring);
         op += run;
         ip += run;
         if (ip >= n) break;
