@@ -65,7 +65,7 @@ def test_gzip_batch_vs_zlib(level):
     rng = np.random.default_rng(level)
     codecs = [BYTES_LE, {"name": "gzip", "configuration": {"level": level}}]
     n = 131072
-    kinds = ["random", "text", "smooth", "runs", "far"] * 8
+    kinds = ["random", "text", "smooth", "runs", "far", "periods"] * 8
     data = [_content(rng, n, k) for k in kinds]
     encs = []
     for d in data:
@@ -84,6 +84,38 @@ def test_gzip_batch_vs_zlib(level):
     got = out.cpu().numpy().reshape(len(encs), n)
     for i, d in enumerate(data):
         assert np.array_equal(got[i], d), (i, kinds[i])
+
+
+@pytest.mark.parametrize("strategy", ["stored", "fixed", "rle", "huffman_only", "filtered"])
+def test_gzip_block_types_vs_zlib(strategy):
+    """Every DEFLATE block type and symbol mix the decoder's paths distinguish: stored blocks (level
+    0), fixed-Huffman blocks (Z_FIXED), run-length matches at distance 1 (Z_RLE: overlapping copies,
+    long matches), literal-only dynamic blocks (Z_HUFFMAN_ONLY), and Z_FILTERED; varied content and
+    lengths, unaligned stream starts, one batch per strategy."""
+    from zarrs_amd import CodecChain, Context, make_desc
+    import torch
+    rng = np.random.default_rng(zlib.crc32(strategy.encode()))
+    level, strat = {"stored": (0, zlib.Z_DEFAULT_STRATEGY), "fixed": (6, zlib.Z_FIXED), "rle": (6, zlib.Z_RLE),
+                    "huffman_only": (6, zlib.Z_HUFFMAN_ONLY), "filtered": (6, zlib.Z_FILTERED)}[strategy]
+    kinds = ["random", "text", "smooth", "runs", "far", "periods"] * 3
+    sizes = [int(v) for v in rng.integers(1, 200000, len(kinds))]
+    n = max(sizes)
+    data = [_content(rng, max(sz, 200), k)[:sz] for sz, k in zip(sizes, kinds)]
+    encs = []
+    for d in data:
+        c = zlib.compressobj(level, zlib.DEFLATED, 31, 8, strat)
+        encs.append(c.compress(d.tobytes()) + c.flush())
+    blob = b"".join(encs)
+    dev = torch.frombuffer(bytearray(blob), dtype=torch.uint8).cuda()
+    ch = CodecChain.from_metadata([BYTES_LE, {"name": "gzip", "configuration": {"level": max(level, 1)}}], "uint8",
+                                  0, Context.default())
+    off = 0
+    for i, (d, e) in enumerate(zip(data, encs)):  # one decode per stream (each has its own length)
+        out = torch.zeros(len(d), dtype=torch.uint8, device="cuda")
+        st = ch.decode_batch([make_desc((dev.data_ptr() + off, len(e)), [len(d)])], out, [len(d)], enc_device=True)
+        off += len(e)
+        assert st == [0], (i, kinds[i], len(d))
+        assert np.array_equal(out.cpu().numpy(), d), (i, kinds[i], len(d))
 
 
 def test_gzip_header_fields_and_trailing_member():

@@ -2141,14 +2141,17 @@ namespace {
 // parallelism to take here; it is taken in k_zstd_lits / k_zstd_blocks, and across items.)
 // -------------------------------------------------------------------------------------------------
 #ifndef ZG_XRING
-#define ZG_XRING 16384
+#define ZG_XRING 8192
 #endif
 constexpr uint32_t XRING = ZG_XRING, XRMASK = XRING - 1;
 static_assert((XRING & XRMASK) == 0 && XRING >= 2 * ZBATCH, "exec ring: a power of two holding two batches");
 #ifndef ZG_XSTAGE_V
-#define ZG_XSTAGE_V 512
+#define ZG_XSTAGE_V 256
 #endif
 constexpr uint32_t XSTAGE_V = ZG_XSTAGE_V;  // staged far-source vectors (16 B) per batch
+#ifndef ZG_XWPE
+#define ZG_XWPE 2  // the executor is compiled for >= 2 waves/SIMD (VGPR + AGPR <= 256)
+#endif
 constexpr uint32_t XPL = 32;        // bytes of a short match its own lane copies (the rest: the wave)
 constexpr int XR_LIT = ZBATCH / 16 / 64 + 1, XR_FAR = XSTAGE_V / 64;
 
@@ -2744,7 +2747,7 @@ __global__ __launch_bounds__(256) void k_zstd_direct(const ZgItem *items, const 
   }
 }
 
-__global__ __launch_bounds__(64) void k_zstd_exec_item(ZgItem *items, uint32_t *status, const ZBlk *blks,
+__global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(ZG_XWPE, 8))) void k_zstd_exec_item(ZgItem *items, uint32_t *status, const ZBlk *blks,
                                                        uint32_t blk_cap, const uint32_t *nblk, const uint32_t *zmode,
                                                        uint8_t *dst, uint64_t slot_bytes, const uint8_t *lit_scratch,
                                                        uint64_t lit_stride, const uint32_t *seq_scratch,
