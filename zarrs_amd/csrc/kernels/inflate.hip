@@ -120,11 +120,6 @@ struct Smem {
 
 __device__ __forceinline__ uint32_t U(uint32_t x) { return __builtin_amdgcn_readfirstlane(x); }
 __device__ __forceinline__ int lane_id() { return __lane_id(); }
-// v of lane idx (idx >= 64: the sentinel 64), one ds_bpermute
-__device__ __forceinline__ uint32_t lane_gather(uint32_t v, uint32_t idx) {
-  const uint32_t g = (uint32_t)__builtin_amdgcn_ds_bpermute((int)(min(idx, 63u) << 2), (int)v);
-  return idx >= 64 ? 64u : g;
-}
 // inclusive wave64 prefix sum: row shifts within 16 lanes, then row broadcasts (DPP, no LDS)
 __device__ __forceinline__ uint32_t wave_incl_sum(uint32_t x) {
   x += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0x111, 0xf, 0xf, false);  // row_shr:1
@@ -622,18 +617,19 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(ZG_INFLATE_W
         bool slow = false;
         uint32_t o = 0;
         {
-          uint32_t J = info >= F_EOB ? 64u : min<uint32_t>((uint32_t)lane + (info & 255), 64u);
+          // symbol starts 0..62 of the window; lane 63 is the sink (J = 63 maps to itself), standing
+          // for "past the window" and "after a stop symbol", so the gathers need no range checks
+          uint32_t J = (lane == 63 || info >= F_EOB) ? 63u : min<uint32_t>((uint32_t)lane + (info & 255), 63u);
           uint32_t p = (lane & 1) ? U(__builtin_amdgcn_readlane(J, 0)) : 0u;
 #pragma unroll
           for (int k = 1; k < 6; k++) {
-            J = lane_gather(J, J);
-            const uint32_t q = lane_gather(J, p);
+            J = (uint32_t)__builtin_amdgcn_ds_bpermute((int)(J << 2), (int)J);
+            const uint32_t q = (uint32_t)__builtin_amdgcn_ds_bpermute((int)(p << 2), (int)J);
             if ((lane >> k) & 1) p = q;
           }
-          const uint32_t pi = min<uint32_t>(p, 63u);
-          const uint32_t info_t = (uint32_t)__builtin_amdgcn_ds_bpermute((int)(pi << 2), (int)info);
-          const uint32_t rec_t = (uint32_t)__builtin_amdgcn_ds_bpermute((int)(pi << 2), (int)rec);
-          const bool valid = p < 64 && info_t < F_EOB;
+          const uint32_t info_t = (uint32_t)__builtin_amdgcn_ds_bpermute((int)(p << 2), (int)info);
+          const uint32_t rec_t = (uint32_t)__builtin_amdgcn_ds_bpermute((int)(p << 2), (int)rec);
+          const bool valid = p < 63 && info_t < F_EOB;
           const uint32_t olen = valid ? info_t >> 8 : 0u;
           const uint32_t incl = wave_incl_sum(olen), excl = incl - olen;
           const bool take = valid && cnt + (uint32_t)lane < 64 && bytes + excl < BATCH_CAP;
@@ -649,7 +645,7 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(ZG_INFLATE_W
           }
           if (m < 64 && cnt < 64 && bytes < BATCH_CAP) {
             const uint32_t pm = U(__builtin_amdgcn_readlane(p, (int)m));
-            if (pm < 64) {  // symbol m starts in the window and is not valid: a stop symbol
+            if (pm < 63) {  // symbol m starts in the window and is not valid: a stop symbol
               const uint32_t a = U(__builtin_amdgcn_readlane(info_t, (int)m));
               o = pm;
               if (a == (F_EOB | (a & 255))) {
