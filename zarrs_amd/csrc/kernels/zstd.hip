@@ -1176,9 +1176,33 @@ struct SeqX {
   uint16_t next;
   uint8_t nb, nbx;
 };
+#ifndef ZG_BLK_WPE
+#define ZG_BLK_WPE 5  // waves per SIMD k_zstd_blocks is compiled for
+#endif
+#ifndef ZG_SEQ_PACK
+#define ZG_SEQ_PACK 1  // 4-byte sequence tables (below); 0: 8-byte SeqX
+#endif
 #ifndef ZG_SEQ_ONE_FSE
 #define ZG_SEQ_ONE_FSE 1  // one FSE scratch table, folded into its SeqX table at once (0: three tables)
 #endif
+#if ZG_SEQ_PACK
+// 4-byte sequence decoding entry: bits 0-8 next state base, 9-12 state bits, 13-17 value extra bits,
+// 18-23 code (LL/ML: index of its value base; OF: the offset code itself, value base 1 << code), bit
+// 31 a code outside the format. Everything the bit stream's order depends on (state and extra bit
+// counts) is in the entry; the LL/ML value base is a scalar constant load off that critical chain.
+// Each table is built as FSE entries in place (also 4 bytes) and repacked entry by entry, so the
+// three tables take 5 KiB of LDS (the 8-byte SeqX tables and their FSE scratch took 12 KiB): ~2x
+// the waves per CU for this latency-bound serial decoder.
+constexpr uint32_t SQ_BAD = 0x80000000u;
+__device__ __forceinline__ uint32_t sq_pack(uint32_t next, uint32_t nb, uint32_t nbx, uint32_t code) {
+  return next | (nb << 9) | (nbx << 13) | (code << 18);
+}
+struct ZDecSmem {
+  uint32_t xl[512], xm[512], xo[256];
+  int16_t norm[64];
+  uint32_t tmp[32];
+};
+#else
 struct ZDecSmem {
 #if ZG_SEQ_ONE_FSE
   Fse fse[512];  // one FSE table at a time: built, then folded into its SeqX table
@@ -1189,6 +1213,7 @@ struct ZDecSmem {
   int16_t norm[64];
   uint32_t tmp[32];
 };
+#endif
 
 
 
@@ -1411,7 +1436,7 @@ __global__ __launch_bounds__(64) void k_zstd_scan(const ZgItem *items, uint32_t 
 }
 
 // One wave per (item, block) record, grid-stride. Sequences land as {ll, ml, offset symbol}.
-__global__ __launch_bounds__(64) void k_zstd_blocks(const ZgItem *items, uint32_t *status, ZBlk *blks,
+__global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(ZG_BLK_WPE, 8))) void k_zstd_blocks(const ZgItem *items, uint32_t *status, ZBlk *blks,
                                                     uint32_t blk_cap, const uint32_t *nblk,
                                                     const uint32_t *zmode, uint32_t n_items, uint8_t *lit_scratch,
                                                     uint64_t lit_stride, uint32_t *seq_scratch, uint64_t seq_cap) {
@@ -1448,7 +1473,9 @@ __global__ __launch_bounds__(64) void k_zstd_blocks(const ZgItem *items, uint32_
       uint32_t lg[3] = {0, 0, 0};
       for (int t = 0; t < 3 && !bad; t++) {
         const uint32_t mode = (tm >> (2 * t)) & 3, off = U(Bp->tab_off[t]);
-#if ZG_SEQ_ONE_FSE
+#if ZG_SEQ_PACK
+        Fse *T = (Fse *)(t == 0 ? S.xl : t == 1 ? S.xo : S.xm);  // built in place, repacked below
+#elif ZG_SEQ_ONE_FSE
         Fse *T = S.fse;
 #else
         Fse *T = t == 0 ? S.ll : t == 1 ? S.of : S.ml;
@@ -1473,6 +1500,13 @@ __global__ __launch_bounds__(64) void k_zstd_blocks(const ZgItem *items, uint32_
         __syncthreads();
         for (uint32_t u = lane; u < (1u << lg[t]); u += 64) {
           const Fse e = T[u];
+#if ZG_SEQ_PACK
+          uint32_t x;
+          if (t == 0) x = e.sym <= 35 ? sq_pack(e.base, e.nb, c_ll_bits[e.sym], e.sym) : SQ_BAD;
+          else if (t == 1) x = e.sym <= 31 ? sq_pack(e.base, e.nb, e.sym, e.sym) : SQ_BAD;
+          else x = e.sym <= 52 ? sq_pack(e.base, e.nb, c_ml_bits[e.sym], e.sym) : SQ_BAD;
+          ((uint32_t *)T)[u] = x;  // same entry, same lane: in place
+#else
           if (t == 0) {
             const bool ok = e.sym <= 35;
             S.xl[u] = SeqX{ok ? c_ll_base[e.sym] : 0u, e.base, e.nb, (uint8_t)(ok ? c_ll_bits[e.sym] : 0xFF)};
@@ -1483,10 +1517,11 @@ __global__ __launch_bounds__(64) void k_zstd_blocks(const ZgItem *items, uint32_
             const bool ok = e.sym <= 52;
             S.xm[u] = SeqX{ok ? c_ml_base[e.sym] : 0u, e.base, e.nb, (uint8_t)(ok ? c_ml_bits[e.sym] : 0xFF)};
           }
+#endif
         }
-        if (ZG_SEQ_ONE_FSE) __syncthreads();  // the next table reuses S.fse
+        if (ZG_SEQ_ONE_FSE && !ZG_SEQ_PACK) __syncthreads();  // the next table reuses S.fse
       }
-      if (!ZG_SEQ_ONE_FSE) __syncthreads();
+      if (!ZG_SEQ_ONE_FSE || ZG_SEQ_PACK) __syncthreads();
       // Backward bit container in SGPRs: C holds bits [32 * lw, 32 * lw + have) of the aligned item
       // words, the next unread bit at bit 63; refilled a word at a time from the BitsBack register
       // window (readlane), so a field read is three scalar operations.
@@ -1523,10 +1558,29 @@ __global__ __launch_bounds__(64) void k_zstd_blocks(const ZgItem *items, uint32_
         uint32_t sml = rd(lg[2]);
         uint32_t *out = seq_scratch + ((uint64_t)item * seq_cap + U(Bp->seq_buf)) * 3;
         uint32_t remaining = nseq, done = 0;
+#if !ZG_SEQ_PACK
         const uint2 *XO = (const uint2 *)S.xo, *XM = (const uint2 *)S.xm, *XL = (const uint2 *)S.xl;
+#endif
         while (remaining && !bad) {
           uint32_t r_ll = 0, r_ml = 0, r_of = 0, cnt = 0;
           while (cnt < 64 && remaining) {
+#if ZG_SEQ_PACK
+            const uint32_t ow = U(S.xo[sof]), mw = U(S.xm[sml]), lwd = U(S.xl[sll]);
+            if ((ow | mw | lwd) & SQ_BAD) { bad = true; break; }
+            const uint32_t oc = (ow >> 18) & 63, mc = (mw >> 18) & 63, lc = (lwd >> 18) & 63;
+            refill();
+            const uint32_t ofv = (1u << oc) + rd(oc);
+            refill();
+            const uint32_t ml = c_ml_base[mc] + rd((mw >> 13) & 31);
+            const uint32_t ll = c_ll_base[lc] + rd((lwd >> 13) & 31);
+            remaining--;
+            if (remaining) {
+              refill();
+              sll = (lwd & 511) + rd((lwd >> 9) & 15);
+              sml = (mw & 511) + rd((mw >> 9) & 15);
+              sof = (ow & 511) + rd((ow >> 9) & 15);
+            }
+#else
             const uint2 eo = XO[sof], em = XM[sml], el = XL[sll];
             const uint32_t ob = U(eo.x), ow = U(eo.y), mb = U(em.x), mw = U(em.y), lb = U(el.x), lwd = U(el.y);
             if ((ow | mw | lwd) & 0x80000000u) { bad = true; break; }
@@ -1542,6 +1596,7 @@ __global__ __launch_bounds__(64) void k_zstd_blocks(const ZgItem *items, uint32_
               sml = (mw & 0xFFFF) + rd((mw >> 16) & 0xFF);
               sof = (ow & 0xFFFF) + rd((ow >> 16) & 0xFF);
             }
+#endif
             // repeat offsets, symbolically in the block's incoming rep state (RFC 8878 3.1.1.5)
             uint32_t off;
             if (ofv > 3) {
@@ -3004,7 +3059,9 @@ hipError_t launch_zstd(ZgItem *items, uint32_t *status, uint32_t n_items, uint8_
 #endif
   hipLaunchKernelGGL(k_zstd_lits, dim3(lgrid), dim3(LIT_THREADS), 0, s, items, status, blks, Z.blk_cap, Z.nblk,
                      Z.mode, n_items, Z.lit, Z.lit_stride);
-  hipLaunchKernelGGL(k_zstd_blocks, dim3(grid), dim3(64), 0, s, items, status, blks, Z.blk_cap, Z.nblk, Z.mode,
+  // one resident wave of the sequence decoder: 256 CUs x 4 SIMDs x ZG_BLK_WPE waves
+  const uint32_t bgrid = (uint32_t)std::min<uint64_t>(recs, std::max<uint64_t>(g_cap, (uint64_t)256 * 4 * ZG_BLK_WPE));
+  hipLaunchKernelGGL(k_zstd_blocks, dim3(bgrid), dim3(64), 0, s, items, status, blks, Z.blk_cap, Z.nblk, Z.mode,
                      n_items, Z.lit, Z.lit_stride, Z.seq, Z.seq_cap);
   hipLaunchKernelGGL(k_zstd_plan, dim3(n_items), dim3(64), 0, s, items, status, blks, Z.blk_cap, Z.nblk, Z.mode,
                      slot_bytes);
