@@ -1702,9 +1702,12 @@ constexpr uint32_t LIT_LDS = ZG_LIT_LDS;
 constexpr int32_t LIT_WARM = 128;
 constexpr uint32_t LIT_THREADS = 256;
 #ifndef ZG_LIT_WPE
-#define ZG_LIT_WPE 3  // waves per SIMD k_zstd_lits is compiled for (A/B: 3 beats 2 and 4 on C5)
+#define ZG_LIT_WPE 3  // min waves per SIMD k_zstd_lits is compiled for (A/B: 3 beats 2 and forced 4)
 #endif
 constexpr int LIT_STAGE_R = ZG_LIT_WPE >= 4 ? 4 : 8;  // 16-B staging loads in flight per thread
+#ifndef ZG_LIT_GRID_PER_CU
+#define ZG_LIT_GRID_PER_CU 4
+#endif
 #ifndef ZG_LIT_PACK
 #define ZG_LIT_PACK 1  // decoded literals stored ZG_LIT_PACK_B at a time
 #endif
@@ -1712,7 +1715,7 @@ constexpr int LIT_STAGE_R = ZG_LIT_WPE >= 4 ? 4 : 8;  // 16-B staging loads in f
 #define ZG_LIT_PACK_B 8
 #endif
 #ifndef ZG_LIT_GWIN
-#define ZG_LIT_GWIN 1  // literal sections beyond LIT_LDS read through a per-lane 16-B window
+#define ZG_LIT_GWIN 2  // literal sections beyond LIT_LDS: 1 per-lane 16-B window, 2 32-B + prefetch
 #endif
 
 struct ZLitSmem {
@@ -1797,9 +1800,43 @@ __device__ __forceinline__ uint32_t hl_run(HufLane &H, int32_t &p, int32_t stop,
   return n;
 }
 
-// Literal-section words read from global memory through a per-lane 16-B window: a lane walks its
-// segment backwards one word at a time, so one aligned 16-B load serves four words (scattered 4-B
-// loads of 256 lanes fetched ~10x the section bytes from HBM).
+// Literal-section words read from global memory through a per-lane window: a lane walks its segment
+// backwards one word at a time, so one aligned 32-B load serves eight words (scattered 4-B loads of
+// 256 lanes fetched ~10x the section bytes from HBM), and the next lower 32 B are already in flight
+// while the current ones are decoded (the decode otherwise waits a full HBM round trip every
+// 128 bits).
+struct GWordPF {
+  const gu32 *Wp;
+  int64_t lim;
+  mutable uintptr_t cb;       // address of the cached 32-B block (1: none)
+  mutable zv4u c0, c1;        // its words 0-3, 4-7
+  mutable zv4u n0, n1;        // the block below it (prefetched)
+  __device__ __forceinline__ static void ld(uintptr_t b, zv4u &x0, zv4u &x1) {
+    const __attribute__((address_space(1))) zv4u *q = (const __attribute__((address_space(1))) zv4u *)b;
+    x0 = q[0];
+    x1 = q[1];
+  }
+  __device__ __forceinline__ uint32_t operator()(int32_t k) const {
+    if (k < 0 || k >= lim) return 0u;
+    const uintptr_t a = (uintptr_t)(Wp + k), b = a & ~(uintptr_t)31;
+    if (b != cb) {
+      if (b + 32 == cb) {  // the next lower block: take the prefetched copy
+        c0 = n0;
+        c1 = n1;
+      } else {
+        ld(b, c0, c1);
+      }
+      cb = b;
+      // prefetch the block below, if it still holds words of the section (never before Wp's block)
+      if (b > ((uintptr_t)Wp & ~(uintptr_t)31)) ld(b - 32, n0, n1);
+    }
+    const uint32_t i = (uint32_t)(a >> 2) & 7u;
+    const zv4u h = i < 4 ? c0 : c1;
+    const uint32_t j = i & 3u;
+    return j == 0 ? h.x : j == 1 ? h.y : j == 2 ? h.z : h.w;
+  }
+};
+
 struct GWord {
   const gu32 *Wp;
   int64_t lim;
@@ -2063,7 +2100,9 @@ __global__ __launch_bounds__(LIT_THREADS) __attribute__((amdgpu_waves_per_eu(ZG_
       } else {
         const gu32 *Wp = (const gu32 *)(words + wbase);
         const int64_t lim = nwords_item - wbase;
-#if ZG_LIT_GWIN
+#if ZG_LIT_GWIN == 2
+        const GWordPF word{Wp, lim, 1, zv4u{0, 0, 0, 0}, zv4u{0, 0, 0, 0}, zv4u{0, 0, 0, 0}, zv4u{0, 0, 0, 0}};
+#elif ZG_LIT_GWIN
         const GWord word{Wp, lim, 1, zv4u{0, 0, 0, 0}};
 #else
         auto word = [Wp, lim](int32_t k) -> uint32_t { return (k >= 0 && k < lim) ? Wp[k] : 0u; };
@@ -3048,8 +3087,9 @@ hipError_t launch_zstd(ZgItem *items, uint32_t *status, uint32_t n_items, uint8_
   }();
   static const uint64_t l_cap = [] {
     const char *e = std::getenv("ZGPU_ZSTD_LGRID");
-    // one resident wave of workgroups: 256 CUs x ZG_LIT_WPE workgroups of 256 lanes (4 waves) each
-    return e ? std::max<uint64_t>(1, std::strtoull(e, nullptr, 10)) : (uint64_t)256 * ZG_LIT_WPE;
+    // one resident wave of workgroups: 256 CUs x ZG_LIT_GRID_PER_CU workgroups of 256 lanes each (the
+    // decoder compiles to 128 VGPRs: 4 workgroups per CU)
+    return e ? std::max<uint64_t>(1, std::strtoull(e, nullptr, 10)) : (uint64_t)256 * ZG_LIT_GRID_PER_CU;
   }();
   const uint32_t grid = (uint32_t)std::min<uint64_t>(recs, g_cap);
   const uint32_t lgrid = (uint32_t)std::min<uint64_t>(recs, l_cap);
