@@ -12,18 +12,25 @@
 //  * Bit reader: the compressed stream is read as aligned 32-bit words through two 256-byte register
 //    windows (one word per lane, one coalesced load each); a refill is a v_readlane, and the next
 //    window is loaded a full window ahead, so the decode loop never waits on HBM.
-//  * Huffman tables live in LDS: a 10-bit root table for literal/length and an 8-bit one for
+//  * Huffman tables live in LDS: a 9-bit root table for literal/length and an 8-bit one for
 //    distances, each entry already holding the decoded meaning (literal byte, or length/distance base
-//    + extra-bit count). Longer codes (rare) take a canonical count/first slow path. Tables are built
-//    cooperatively by the 64 lanes (ballot ranks + parallel root fill).
-//  * Symbol decode: every lane decodes the whole symbol (code, extra bits, distance) that would start
-//    at its bit offset of a 64-bit lookahead window; a scalar walk chains the advances with one
-//    readlane per symbol, and the chained symbols are compacted into an LDS record array.
+//    + extra-bit count); a root prefix of longer codes points to a second-level table indexed by the
+//    next bits (zlib's two-level scheme), so every code of real data decodes by table lookups (a code
+//    set whose subtables outgrow their LDS space takes a canonical count/first slow path for those
+//    prefixes). Tables are built cooperatively by the 64 lanes (ballot ranks, parallel root fill,
+//    subtables allocated by an LDS counter).
+//  * Symbol decode: every lane decodes, branch-free, the whole symbol (code, extra bits, distance)
+//    that would start at its bit offset of a 63-bit lookahead window; the window's symbols are
+//    chained by pointer jumping (ds_bpermute doublings, up to 16 symbols per window: C3 data has at
+//    most 11 per 64 bits) and compacted into an LDS record array.
 //  * Decoded symbols (up to 64 per batch, one per lane) are then executed in parallel:
-//    a wave prefix sum places them, literals are written at once, each match is copied by all lanes
-//    (out[p+i] = out[p-d+(i mod d)], so overlapping copies need no serialisation), through a 16 KiB
-//    LDS ring that holds the recent output; sources older than the ring come from the flushed output
-//    in HBM. Each batch is flushed to the item's slot with 16-byte stores.
+//    a wave prefix sum places them, literals are written at once, matches resolve in rounds by exact
+//    dependencies (a long match copied by all lanes: out[p+i] = out[p-d+(i mod d)], so overlapping
+//    copies need no serialisation), through a 2 KiB LDS ring that holds the recent output; sources
+//    older than the ring come from the flushed output in HBM. The ring is flushed to the item's slot
+//    with 16-byte stores.
+//  * LDS per stream is 8 KiB (ring 2 KiB, tables 4.6 KiB; the header scratch shares its space with
+//    the batch records) and the kernel is held at 96 VGPRs: 5 streams per SIMD.
 #include <hip/hip_runtime.h>
 
 #include "../common.hpp"
@@ -61,7 +68,23 @@ constexpr int BATCH_CAP = RING / 2;  // max output bytes decoded into one batch
 constexpr int FLUSH_MIN = RING / 4;  // flush the ring to the slot once this many bytes are pending
 // unflushed bytes stay below FLUSH_MIN + BATCH_CAP + 258 < RING: every source older than the ring
 // has been flushed
-constexpr int LROOT = 10, DROOT = 8;
+#ifndef ZG_INFLATE_LROOT
+#define ZG_INFLATE_LROOT 9
+#endif
+#ifndef ZG_INFLATE_LSUB
+#define ZG_INFLATE_LSUB 352
+#endif
+#ifndef ZG_INFLATE_DSUB
+#define ZG_INFLATE_DSUB 32
+#endif
+constexpr int LROOT = ZG_INFLATE_LROOT, DROOT = 8;
+// Second-level tables for codes longer than the root. zlib's bound for 286 symbols with a 9-bit
+// root is 852 entries in all (340 in subtables); distance subtables are sized for real data (C3
+// chunks need at most 16 entries with an 8-bit root): prefixes past the space take the slow path.
+constexpr int LSUB = ZG_INFLATE_LSUB, DSUB = ZG_INFLATE_DSUB;
+#ifndef ZG_INFLATE_SELECT
+#define ZG_INFLATE_SELECT 1  // lane symbol decode by selects instead of divergent branches
+#endif
 #ifndef ZG_INFLATE_XDEP
 #define ZG_INFLATE_XDEP 1  // matches resolve by exact dependencies (0: first-pending frontier)
 #endif
@@ -74,12 +97,18 @@ constexpr int LROOT = 10, DROOT = 8;
 #ifndef ZG_INFLATE_PJ
 #define ZG_INFLATE_PJ 1  // chain a window's symbols by pointer jumping (0: scalar walk)
 #endif
+#ifndef ZG_INFLATE_PJL
+#define ZG_INFLATE_PJL 3  // pointer-jumping doublings: a window chains up to 2^(PJL+1) symbols
+#endif
 
 // table entry: bits 0-3 code length (0 = longer than the root: slow path), 4-5 kind,
 // 6-9 extra bits, 16-31 value (literal byte / length base / distance base)
 constexpr uint32_t K_LIT = 0, K_LEN = 1, K_EOB = 2, K_BAD = 3;
 // lookahead stop flags (above the advance / output-length fields of a lane's symbol info)
 constexpr uint32_t F_EOB = 1u << 17, F_BAD = 1u << 18, F_SLOW = 1u << 19;
+// table entry with code length 0 and this bit: a subtable at index bits 16-31, indexed by the next
+// bits 6-9 bits of the stream; entries are then complete (code length = the whole code)
+constexpr uint32_t F_SUBT = 1u << 10;
 
 __constant__ uint16_t c_len_base[29] = {3,  4,  5,  6,  7,  8,  9,  10, 11,  13,  15,  17,  19,  23, 27,
                                         31, 35, 43, 51, 59, 67, 83, 99, 115, 131, 163, 195, 227, 258};
@@ -104,18 +133,23 @@ struct Smem {
     uint8_t ring[RING];
     uint32_t ring32[RING / 4];
   };
-  uint32_t ltab[1 << LROOT];
-  uint32_t dtab[1 << DROOT];
+  uint32_t ltab[(1 << LROOT) + LSUB];
+  uint32_t dtab[(1 << DROOT) + DSUB];
   uint16_t lsorted[288];
   uint16_t dsorted[32];
-  uint8_t lens[320];  // code lengths: 0..HLIT-1 literal/length, then distances
-  uint8_t clens[20];
-  uint16_t csorted[20];
   HuffMeta lm, dm, cm;
   uint32_t tmp[16];
-  uint32_t rec[64];   // the batch's symbols: literal byte, or (1<<31)|(dist<<9)|len
-  uint16_t roff[64];  // their output offsets in the batch
-  uint16_t rbeg[64], rend[64];  // output interval of each symbol in the batch (match dependencies)
+  union {
+    struct {  // a dynamic block header (decoded before the block's symbol batches)
+      uint8_t lens[320];  // code lengths: 0..HLIT-1 literal/length, then distances
+      uint8_t clens[20];
+      uint16_t csorted[20];
+    };
+    struct {  // a symbol batch
+      uint32_t rec[64];   // the batch's symbols: literal byte, or (1<<31)|(dist<<9)|len
+      uint16_t rbeg[64], rend[64];  // output interval of each symbol in the batch (match dependencies)
+    };
+  };
 };
 
 __device__ __forceinline__ uint32_t U(uint32_t x) { return __builtin_amdgcn_readfirstlane(x); }
@@ -253,8 +287,23 @@ __device__ __forceinline__ uint32_t rev_bits(uint32_t v, uint32_t n) { return __
 // 2 code-length codes (root 7 = max length: no slow path). Returns false on an invalid code set
 // (over-subscribed, or incomplete with more than one code: zlib inflate_table rules).
 // ---------------------------------------------------------------------------------------------
+// table entry for symbol `sym` of an alphabet (kind as in build_table) with code length L
+__device__ __forceinline__ uint32_t table_entry(int kind, uint32_t sym, uint32_t L) {
+  if (kind == 0) {
+    if (sym < 256) return (sym << 16) | (K_LIT << 4) | L;
+    if (sym == 256) return (K_EOB << 4) | L;
+    if (sym < 286) return ((uint32_t)c_len_base[sym - 257] << 16) | ((uint32_t)c_len_extra[sym - 257] << 6) | (K_LEN << 4) | L;
+    return (K_BAD << 4) | L;
+  }
+  if (kind == 1) {
+    if (sym < 30) return ((uint32_t)c_dist_base[sym] << 16) | ((uint32_t)c_dist_extra[sym] << 6) | (K_LEN << 4) | L;
+    return (K_BAD << 4) | L;
+  }
+  return (sym << 16) | L;
+}
+
 __device__ bool build_table(const uint8_t *lens, uint32_t n, uint32_t root, uint32_t *tab, uint16_t *sorted,
-                            HuffMeta &M, int kind, uint32_t *tmp) {
+                            HuffMeta &M, int kind, uint32_t *tmp, uint32_t sub_cap) {
   const int lane = lane_id();
   if (lane < 16) tmp[lane] = 0;
   __syncthreads();
@@ -295,6 +344,7 @@ __device__ bool build_table(const uint8_t *lens, uint32_t n, uint32_t root, uint
       off += cnt[l];
     }
     M.maxlen = (uint16_t)maxlen;
+    tmp[0] = 0;  // subtable allocation counter (the counts were read above)
   }
   __syncthreads();
   // sorted symbols (by length, then symbol) via ballot ranks
@@ -319,7 +369,9 @@ __device__ bool build_table(const uint8_t *lens, uint32_t n, uint32_t root, uint
     }
   }
   __syncthreads();
-  // root table fill: entry e <-> R-bit MSB-first prefix v = reverse(e)
+  // root table fill: entry e <-> R-bit MSB-first prefix v = reverse(e). A prefix of codes longer
+  // than the root gets a subtable of 2^sb entries (sb = its longest code - root), indexed by the next
+  // sb stream bits; subtables are allocated from tab[size..size+sub_cap) by an LDS counter (tmp[0]).
   const uint32_t size = 1u << root;
   for (uint32_t e = lane; e < size; e += 64) {
     const uint32_t v = rev_bits(e, root);
@@ -328,22 +380,36 @@ __device__ bool build_table(const uint8_t *lens, uint32_t n, uint32_t root, uint
     for (uint32_t L = 1; L <= root && L <= maxlen && !found; L++) {
       const uint32_t c = v >> (root - L);
       if (c - first[L] < cnt[L]) {
-        const uint32_t sym = sorted[M.offs[L] + c - first[L]];
+        entry = table_entry(kind, sorted[M.offs[L] + c - first[L]], L);
         found = true;
-        if (kind == 0) {
-          if (sym < 256) entry = (sym << 16) | (K_LIT << 4) | L;
-          else if (sym == 256) entry = (K_EOB << 4) | L;
-          else if (sym < 286) entry = ((uint32_t)c_len_base[sym - 257] << 16) | ((uint32_t)c_len_extra[sym - 257] << 6) | (K_LEN << 4) | L;
-          else entry = (K_BAD << 4) | L;
-        } else if (kind == 1) {
-          if (sym < 30) entry = ((uint32_t)c_dist_base[sym] << 16) | ((uint32_t)c_dist_extra[sym] << 6) | (K_LEN << 4) | L;
-          else entry = (K_BAD << 4) | L;
-        } else {
-          entry = (sym << 16) | L;
+      }
+    }
+    if (!found && maxlen > root) {
+      uint32_t sb = 0;
+      for (uint32_t L = root + 1; L <= maxlen; L++) {
+        const uint32_t lo = v << (L - root), hi = (v + 1) << (L - root);
+        if (cnt[L] && first[L] < hi && first[L] + cnt[L] > lo) sb = L - root;
+      }
+      if (sb) {
+        const uint32_t base = atomicAdd(&tmp[0], 1u << sb);
+        entry = 0;  // subtable space exhausted: the canonical slow path
+        if (base + (1u << sb) <= sub_cap) {
+          entry = ((size + base) << 16) | (sb << 6) | F_SUBT;
+          for (uint32_t x = 0; x < (1u << sb); x++) {
+            const uint32_t cf = (v << sb) | rev_bits(x, sb);  // MSB-first code of root + sb bits
+            uint32_t se = (K_BAD << 4) | 0xF;
+            for (uint32_t L = root + 1; L <= root + sb; L++) {
+              const uint32_t c = cf >> (root + sb - L);
+              if (c - first[L] < cnt[L]) {
+                se = table_entry(kind, sorted[M.offs[L] + c - first[L]], L);
+                break;
+              }
+            }
+            tab[size + base + x] = se;
+          }
         }
       }
     }
-    if (!found && maxlen > root) entry = 0;  // longer code: slow path
     tab[e] = entry;
   }
   __syncthreads();
@@ -398,6 +464,46 @@ __device__ __forceinline__ void build_fixed_lens(uint8_t *lens) {
     lens[s] = l;
   }
   __syncthreads();
+}
+
+// One lane's symbol at a 64-bit lookahead value V = Vhi:Vlo (the stream from the symbol's first
+// bit): literal/length code (+ subtable), length extra bits, distance code (+ subtable), distance
+// extra bits — at most 48 bits. info: bits 0-7 advance in bits, 8-16 output bytes, 17+ stop flags;
+// rec: the literal byte, or (1<<31)|(dist<<9)|len.
+__device__ __forceinline__ void lane_symbol(const Smem &S, uint32_t Vlo, uint32_t Vhi, uint32_t &info, uint32_t &rec) {
+  const uint64_t V = ((uint64_t)Vhi << 32) | Vlo;
+  uint32_t E = S.ltab[Vlo & ((1u << LROOT) - 1)];
+  if (E & F_SUBT) E = S.ltab[(E >> 16) + ((Vlo >> LROOT) & ((1u << ((E >> 6) & 15)) - 1))];
+  const uint32_t L = E & 15, kind = (E >> 4) & 3, lx = (E >> 6) & 15;
+  const uint32_t s1 = L + lx;  // <= 20
+  uint32_t D = S.dtab[(Vlo >> s1) & ((1u << DROOT) - 1)];
+  if (D & F_SUBT) D = S.dtab[(D >> 16) + ((uint32_t)(V >> (s1 + DROOT)) & ((1u << ((D >> 6) & 15)) - 1))];
+  const uint32_t DL = D & 15, dx = (D >> 6) & 15, s2 = s1 + DL;
+#if ZG_INFLATE_SELECT
+  // every kind computed, then selected (no divergent branches)
+  const uint32_t len = (E >> 16) + ((Vlo >> L) & ((1u << lx) - 1));
+  const uint32_t dist = (D >> 16) + ((uint32_t)(V >> s2) & ((1u << dx) - 1));
+  const uint32_t i_len = DL == 0 ? F_SLOW : (((D >> 4) & 3) != K_LEN ? F_BAD : ((s2 + dx) | (len << 8)));
+  const uint32_t i_oth = kind == K_EOB ? (L | F_EOB) : F_BAD;
+  info = kind == K_LIT ? (L | (1u << 8)) : (kind == K_LEN ? i_len : i_oth);
+  rec = kind == K_LIT ? (E >> 16) : (0x80000000u | (dist << 9) | len);
+#else
+  if (kind == K_LIT) {
+    info = L | (1u << 8);
+    rec = E >> 16;
+  } else if (kind == K_LEN) {
+    const uint32_t len = (E >> 16) + ((Vlo >> L) & ((1u << lx) - 1));
+    const uint32_t dist = (D >> 16) + ((uint32_t)(V >> s2) & ((1u << dx) - 1));
+    info = (s2 + dx) | (len << 8);
+    rec = 0x80000000u | (dist << 9) | len;
+    if (DL == 0) info = F_SLOW;  // distance code past the subtable space
+    else if (((D >> 4) & 3) != K_LEN) info = F_BAD;
+  } else {
+    info = kind == K_EOB ? (L | F_EOB) : F_BAD;
+    rec = 0;
+  }
+#endif
+  if (L == 0) info = F_SLOW;  // literal/length code past the subtable space
 }
 
 // Flush output bytes [from, to) (absolute positions) from the ring to the slot with 16-B stores.
@@ -517,7 +623,7 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(ZG_INFLATE_W
       if (lane == 0)
         for (int k = 0; k < 19; k++) S.clens[c_clen_order[k]] = (uint8_t)cl[k];
       __syncthreads();
-      if (!build_table(S.clens, 19, 7, S.ltab, S.csorted, S.cm, 2, S.tmp)) { err = ZG_CORRUPT_STREAM; break; }
+      if (!build_table(S.clens, 19, 7, S.ltab, S.csorted, S.cm, 2, S.tmp, 0)) { err = ZG_CORRUPT_STREAM; break; }
       // code lengths for literal/length + distance alphabets (ltab used as a 128-entry 7-bit table)
       uint32_t n = 0, prev = 0;
       const uint32_t total = hlit + hdist;
@@ -559,8 +665,8 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(ZG_INFLATE_W
       __syncthreads();
       if (U(S.lens[256]) == 0) { err = ZG_CORRUPT_STREAM; break; }  // missing end-of-block code
     }
-    if (!build_table(S.lens, 288, LROOT, S.ltab, S.lsorted, S.lm, 0, S.tmp)) { err = ZG_CORRUPT_STREAM; break; }
-    if (!build_table(S.lens + 288, 32, DROOT, S.dtab, S.dsorted, S.dm, 1, S.tmp)) { err = ZG_CORRUPT_STREAM; break; }
+    if (!build_table(S.lens, 288, LROOT, S.ltab, S.lsorted, S.lm, 0, S.tmp, LSUB)) { err = ZG_CORRUPT_STREAM; break; }
+    if (!build_table(S.lens + 288, 32, DROOT, S.dtab, S.dsorted, S.dm, 1, S.tmp, DSUB)) { err = ZG_CORRUPT_STREAM; break; }
     PROF_ADD(0, t_hdr);
     (void)hlit;
     (void)hdist;
@@ -583,31 +689,8 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(ZG_INFLATE_W
         const uint32_t a0 = wi == 0 ? W0 : (wi == 1 ? W1 : W2);
         const uint32_t a1 = wi == 0 ? W1 : (wi == 1 ? W2 : W3);
         const uint32_t a2 = wi == 0 ? W2 : (wi == 1 ? W3 : W4);
-        const uint32_t Vlo = __builtin_amdgcn_alignbit(a1, a0, bit & 31);
-        const uint32_t Vhi = __builtin_amdgcn_alignbit(a2, a1, bit & 31);
-        const uint64_t V = ((uint64_t)Vhi << 32) | Vlo;
-        const uint32_t E = S.ltab[Vlo & ((1u << LROOT) - 1)];
-        const uint32_t L = E & 15, kind = (E >> 4) & 3, lx = (E >> 6) & 15;
-        const uint32_t s1 = L + lx;  // <= 15
-        const uint32_t D = S.dtab[(Vlo >> s1) & ((1u << DROOT) - 1)];
-        const uint32_t DL = D & 15, dx = (D >> 6) & 15, s2 = s1 + DL;
-        // info: bits 0-7 advance in bits, 8-16 output bytes, 17+ stop flags
         uint32_t info, rec;
-        if (kind == K_LIT) {
-          info = L | (1u << 8);
-          rec = E >> 16;
-        } else if (kind == K_LEN) {
-          const uint32_t len = (E >> 16) + ((Vlo >> L) & ((1u << lx) - 1));
-          const uint32_t dist = (D >> 16) + ((uint32_t)(V >> s2) & ((1u << dx) - 1));
-          info = (s2 + dx) | (len << 8);
-          rec = 0x80000000u | (dist << 9) | len;
-          if (DL == 0) info = F_SLOW;  // distance code longer than the root
-          else if (((D >> 4) & 3) != K_LEN) info = F_BAD;
-        } else {
-          info = kind == K_EOB ? (L | F_EOB) : F_BAD;
-          rec = 0;
-        }
-        if (L == 0) info = F_SLOW;  // literal/length code longer than the root
+        lane_symbol(S, __builtin_amdgcn_alignbit(a1, a0, bit & 31), __builtin_amdgcn_alignbit(a2, a1, bit & 31), info, rec);
 #if ZG_INFLATE_PJ
         // Chain the window's symbols by pointer jumping, with no per-symbol scalar work: J_k(x) is
         // the bit offset 2^k symbols after offset x (64: past the window, or after a stop symbol);
@@ -622,28 +705,26 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(ZG_INFLATE_W
           uint32_t J = (lane == 63 || info >= F_EOB) ? 63u : min<uint32_t>((uint32_t)lane + (info & 255), 63u);
           uint32_t p = (lane & 1) ? U(__builtin_amdgcn_readlane(J, 0)) : 0u;
 #pragma unroll
-          for (int k = 1; k < 6; k++) {
+          for (int k = 1; k <= ZG_INFLATE_PJL; k++) {
             J = (uint32_t)__builtin_amdgcn_ds_bpermute((int)(J << 2), (int)J);
             const uint32_t q = (uint32_t)__builtin_amdgcn_ds_bpermute((int)(p << 2), (int)J);
             if ((lane >> k) & 1) p = q;
           }
           const uint32_t info_t = (uint32_t)__builtin_amdgcn_ds_bpermute((int)(p << 2), (int)info);
           const uint32_t rec_t = (uint32_t)__builtin_amdgcn_ds_bpermute((int)(p << 2), (int)rec);
-          const bool valid = p < 63 && info_t < F_EOB;
+          constexpr uint32_t NS = 2u << ZG_INFLATE_PJL;  // symbols a window can chain
+          const bool valid = p < 63 && info_t < F_EOB && (uint32_t)lane < NS;
           const uint32_t olen = valid ? info_t >> 8 : 0u;
           const uint32_t incl = wave_incl_sum(olen), excl = incl - olen;
           const bool take = valid && cnt + (uint32_t)lane < 64 && bytes + excl < BATCH_CAP;
           const uint32_t m = (uint32_t)__builtin_popcountll(__ballot(take));
-          if (take) {
-            S.rec[cnt + lane] = rec_t;
-            S.roff[cnt + lane] = (uint16_t)(bytes + excl);
-          }
+          if (take) S.rec[cnt + lane] = rec_t;
           if (m) {
             o = U(__builtin_amdgcn_readlane(p + (info_t & 255), (int)(m - 1)));
             bytes += U(__builtin_amdgcn_readlane(incl, (int)(m - 1)));
             cnt += m;
           }
-          if (m < 64 && cnt < 64 && bytes < BATCH_CAP) {
+          if (m < NS && cnt < 64 && bytes < BATCH_CAP) {
             const uint32_t pm = U(__builtin_amdgcn_readlane(p, (int)m));
             if (pm < 63) {  // symbol m starts in the window and is not valid: a stop symbol
               const uint32_t a = U(__builtin_amdgcn_readlane(info_t, (int)m));
@@ -692,7 +773,6 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(ZG_INFLATE_W
           const uint32_t e = decode_sym(B, S.ltab, LROOT, S.lsorted, S.lm, 0);
           const uint32_t kind = (e >> 4) & 3;
           uint32_t r = 0;
-          const uint32_t off0 = bytes;
           bool has = false;
           if (kind == K_LIT) {
             r = e >> 16;
@@ -721,10 +801,7 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(ZG_INFLATE_W
             }
           }
           if (has) {
-            if (lane == 0) {
-              S.rec[cnt] = r;
-              S.roff[cnt] = (uint16_t)off0;
-            }
+            if (lane == 0) S.rec[cnt] = r;
             cnt++;
           }
           bp = B.consumed;
@@ -741,17 +818,8 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(ZG_INFLATE_W
       const bool mine = lane < (int)cnt;
       const uint32_t rec = mine ? S.rec[lane] : 0u;
       const bool is_match = mine && (rec >> 31);
-#if ZG_INFLATE_PJ
-      const uint64_t mypos = pos + (mine ? S.roff[lane] : 0u);
-#else
       const uint32_t ln = mine ? (is_match ? (rec & 511) : 1u) : 0u;
-      uint32_t inc = ln;  // inclusive wave scan of output lengths
-      for (int off = 1; off < 64; off <<= 1) {
-        const uint32_t t = __shfl_up(inc, off, 64);
-        if (lane >= off) inc += t;
-      }
-      const uint64_t mypos = pos + inc - ln;
-#endif
+      const uint64_t mypos = pos + wave_incl_sum(ln) - ln;  // output offsets: a wave prefix sum
       if (mine && !is_match) S.ring[mypos & RMASK] = (uint8_t)rec;
       const uint64_t batch_end = pos + bytes;
       const uint32_t mlen = rec & 511, md = (rec >> 9) & 0xFFFF;
