@@ -1,6 +1,6 @@
 """GPU parity of the blosc codec against the reference's blosc fixtures
 (zstd + bitshuffle, written by zarrs and zarr-python) and the CPU oracle (c-blosc 1.21, the library
-zarrs' blosc-src binds) on seeded inputs: blosclz (c-blosc's default) / lz4 / lz4hc / zstd streams,
+zarrs' blosc-src binds) on seeded inputs: blosclz (c-blosc's default) / lz4 / lz4hc / zlib / zstd streams,
 byte shuffle / bitshuffle / none, typesizes 1-8, forced block sizes (split streams, leftover blocks,
 bitshuffle skipped for element counts that are not a multiple of 8), memcpyed frames, blosc inside
 sharding. Bit-exact."""
@@ -47,7 +47,7 @@ def _blosc(cname, shuffle, ts, blocksize=0, clevel=5):
 
 DT = {1: "uint8", 2: "uint16", 4: "float32", 8: "float64"}
 CASES = []
-for cname in ("lz4", "zstd", "lz4hc", "blosclz"):
+for cname in ("lz4", "zstd", "lz4hc", "blosclz", "zlib"):
     for sh in ("noshuffle", "shuffle", "bitshuffle"):
         for ts in (1, 2, 4, 8):
             CASES.append((cname, sh, ts))
@@ -105,12 +105,40 @@ def test_blosc_memcpyed_and_errors(ctx, torch_cuda):
     out = np.zeros(3000, np.float32)
     assert ch.decode_batch([make_desc(enc0, [3000])], out, [3000], enc_device=False) == [0]
     assert np.array_equal(out, a)
-    # zlib streams are not decoded on the GPU: UNSUPPORTED, loudly
-    codecs1 = [{"name": "bytes", "configuration": {"endian": "little"}}, _blosc("zlib", "shuffle", 4)]
-    enc1 = O.OracleChain.from_metadata(codecs1, "float32", 0, 1).encode(np.zeros(3000, np.float32) + 1)
+    # snappy streams (c-blosc compressor format 2; not in the host c-blosc) are not decoded on the
+    # GPU: UNSUPPORTED, loudly (a frame relabelled as snappy)
+    codecs1 = [{"name": "bytes", "configuration": {"endian": "little"}}, _blosc("lz4", "shuffle", 4)]
+    enc1 = bytearray(O.OracleChain.from_metadata(codecs1, "float32", 0, 1).encode(np.zeros(3000, np.float32) + 1))
+    assert not enc1[2] & 0x2
+    enc1[2] = (enc1[2] & 0x1F) | (2 << 5)
     with pytest.raises(ZgpuError) as ei:
-        ch.decode_batch([make_desc(enc1, [3000])], out, [3000], enc_device=False)
+        ch.decode_batch([make_desc(bytes(enc1), [3000])], out, [3000], enc_device=False)
     assert ei.value.status == L.UNSUPPORTED
+    # zlib streams: a flipped Adler-32 trailer byte / a corrupt zlib header -> CORRUPT_STREAM
+    codecs3 = [{"name": "bytes", "configuration": {"endian": "little"}}, _blosc("zlib", "shuffle", 4)]
+    z = np.round(rng.standard_normal(3000) * 10).astype(np.float32)
+    enc3 = bytearray(O.OracleChain.from_metadata(codecs3, "float32", 0, 1).encode(z))
+    assert not enc3[2] & 0x2 and enc3[2] >> 5 == 3
+    ch3 = CodecChain.from_metadata(codecs3, "float32", 0, ctx)
+    assert ch3.decode_batch([make_desc(bytes(enc3), [3000])], out, [3000], enc_device=False) == [0]
+    assert np.array_equal(out, z)
+    # the first block's first compressed (not stored) stream: {csize i32, zlib stream}
+    bsize = int.from_bytes(enc3[8:12], "little")
+    nsplit = 1 if enc3[2] & 0x10 else 4
+    p, tgt = int.from_bytes(enc3[16:20], "little"), None
+    for _ in range(nsplit):
+        cs = int.from_bytes(enc3[p:p + 4], "little")
+        if cs != bsize // nsplit:
+            tgt = (p + 4, cs)
+            break
+        p += 4 + cs
+    assert tgt is not None
+    for off in (tgt[0] + tgt[1] - 1, tgt[0]):  # last Adler-32 byte, CMF
+        bad3 = bytearray(enc3)
+        bad3[off] ^= 0x5A
+        with pytest.raises(ZgpuError) as ei:
+            ch3.decode_batch([make_desc(bytes(bad3), [3000])], out, [3000], enc_device=False)
+        assert ei.value.status == L.CORRUPT_STREAM
     # corrupt lz4 stream / truncated frame / wrong decoded size
     codecs2 = [{"name": "bytes", "configuration": {"endian": "little"}}, _blosc("lz4", "shuffle", 4)]
     b = np.round(rng.standard_normal(3000) * 10).astype(np.float32)

@@ -6,7 +6,7 @@
 //   16-B header {version, versionlz, flags, typesize, nbytes u32, blocksize u32, cbytes u32}
 //   flags: 0x1 byte shuffle, 0x2 memcpyed (raw payload after the header), 0x4 bitshuffle,
 //          0x10 blocks not split, bits 5-7 compressor format (0 blosclz, 1 lz4/lz4hc, 2 snappy,
-//          3 zlib, 4 zstd); blosclz, lz4/lz4hc and zstd decode here, snappy / zlib -> UNSUPPORTED
+//          3 zlib, 4 zstd); blosclz, lz4/lz4hc, zlib and zstd decode here, snappy -> UNSUPPORTED
 //   bstarts[nblocks] i32, then per block nsplit = (split && not the leftover block) ? typesize : 1
 //   streams of {csize i32, payload}; csize == neblock means stored.
 // A block's streams concatenate to the shuffled block, then unshuffle / bitunshuffle (format 2:
@@ -21,13 +21,14 @@
 //                    one ZgItem per compressed stream (+ its kind) and one record per block
 //   zstd streams     the block-parallel zstd pipeline (launch_zstd) over the stream table
 //   k_lz4, k_blosclz one wave per lz4 / blosclz stream (input staged through an LDS window)
+//   zlib streams     k_gzip's DEFLATE decoder with the RFC 1950 wrapper (inflate.hip), then the
+//                    Adler-32 trailer check (k_adler32_check, crc.hip)
 //   k_blosc_finish   one workgroup per block: gathers the block's streams and unshuffles /
 //                    bitunshuffles them into the item's output slot (fused: no extra pass)
 #include "launch.hpp"
 
 namespace zgpu {
 
-#define BL_SKIP 0x100u  // stream status: not a zstd stream (kept out of the zstd pipeline)
 
 __device__ __forceinline__ uint32_t ld_u32(const uint8_t *p) {
   return (uint32_t)p[0] | ((uint32_t)p[1] << 8) | ((uint32_t)p[2] << 16) | ((uint32_t)p[3] << 24);
@@ -65,7 +66,8 @@ __global__ __launch_bounds__(64) void k_blosc_info(const ZgItem *items, uint32_t
   } else if (!err && nbytes) {
     const uint32_t comp = flags >> 5;
     if (ts == 0 || bs == 0) err = ZG_CORRUPT_STREAM;
-    else if (comp != BL_COMP_LZ4 && comp != BL_COMP_ZSTD && comp != BL_COMP_BLOSCLZ) err = ZG_UNSUPPORTED;  // snappy/zlib
+    else if (comp != BL_COMP_LZ4 && comp != BL_COMP_ZSTD && comp != BL_COMP_BLOSCLZ && comp != BL_COMP_ZLIB)
+      err = ZG_UNSUPPORTED;  // snappy
     if (!err) {
       const uint32_t lo = nbytes % bs, nfull = nbytes / bs, nblk = nfull + (lo ? 1 : 0);
       const uint32_t nsplit = (flags & 0x10) ? 1 : ts;
@@ -104,7 +106,7 @@ __global__ __launch_bounds__(1024) void k_blosc_layout(const BlInfo *info, uint3
     nblk += I.nblk;
     ne = max(ne, I.max_ne);
     if (I.nsub) kinds |= I.comp == BL_COMP_ZSTD ? BL_HAS_ZSTD : I.comp == BL_COMP_LZ4 ? BL_HAS_LZ4
-                        : I.comp == BL_COMP_BLOSCLZ ? BL_HAS_BLOSCLZ : 0u;
+                        : I.comp == BL_COMP_BLOSCLZ ? BL_HAS_BLOSCLZ : I.comp == BL_COMP_ZLIB ? BL_HAS_ZLIB : 0u;
   }
   ssub[t] = nsub;
   sblk[t] = nblk;
@@ -188,6 +190,7 @@ __global__ __launch_bounds__(64) void k_blosc_streams(ZgItem *items, uint32_t *s
         sub_kind[s0 + j] = raw ? BL_KIND_RAW
                            : I.comp == BL_COMP_ZSTD ? BL_KIND_ZSTD
                            : I.comp == BL_COMP_LZ4  ? BL_KIND_LZ4
+                           : I.comp == BL_COMP_ZLIB ? BL_KIND_ZLIB
                                                     : BL_KIND_BLOSCLZ;
         sub_status[s0 + j] = (!raw && I.comp == BL_COMP_ZSTD) ? 0u : BL_SKIP;
         p += cs;
@@ -518,6 +521,11 @@ hipError_t launch_blosc_decode(ZgItem *items, uint32_t *status, uint32_t n_items
   if (D.n_lz4)
     hipLaunchKernelGGL(k_lz4, dim3((uint32_t)D.n_sub), dim3(64), 0, s, D.subs, D.sub_status, D.sub_kind,
                        (uint32_t)D.n_sub, D.tmp, D.sub_slot);
+  if (D.n_zlib) {
+    hipError_t e = launch_zlib_streams(D.subs, D.sub_status, D.sub_kind, (uint32_t)D.n_sub, D.tmp, D.sub_slot, D.zaux, s);
+    if (e == hipSuccess) e = launch_adler32_check(D.subs, D.sub_status, D.sub_kind, (uint32_t)D.n_sub, D.zaux, s);
+    if (e != hipSuccess) return e;
+  }
   if (D.n_blosclz)
     hipLaunchKernelGGL(k_blosclz, dim3((uint32_t)D.n_sub), dim3(64), 0, s, D.subs, D.sub_status, D.sub_kind,
                        (uint32_t)D.n_sub, D.tmp, D.sub_slot);

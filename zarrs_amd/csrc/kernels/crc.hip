@@ -210,6 +210,51 @@ hipError_t launch_crc32_check(const ZgItem *items, uint32_t *status, uint32_t n_
   return hipGetLastError();
 }
 
+// ------------------------------- Adler-32 (zlib trailer) ---------------------------------------
+// RFC 1950: s1 = 1 + sum b_j, s2 = sum of the running s1 = n + sum (n - j) b_j (mod 65521). Each
+// thread runs the serial recurrence over one contiguous segment [a, e) (A = sum b, B = sum (e - j) b),
+// reducing every NMAX bytes as zlib does; segments combine as s1 += A, s2 += B + (n - e) A.
+__global__ __launch_bounds__(CRC_THREADS) void k_adler32_check(const ZgItem *items, uint32_t *status,
+                                                               const uint32_t *kind, const uint2 *aux) {
+  constexpr uint32_t M = 65521, NMAX = 5552;
+  __shared__ uint32_t s1s[CRC_THREADS], s2s[CRC_THREADS];
+  const uint32_t i = blockIdx.x, t = threadIdx.x;
+  if (kind[i] != BL_KIND_ZLIB || status[i] != 0) return;
+  const ZgItem it = items[i];
+  const uint8_t *p = (const uint8_t *)it.src;
+  const uint64_t n = it.len, L = (n + CRC_THREADS - 1) / CRC_THREADS;
+  const uint64_t a = min<uint64_t>((uint64_t)t * L, n), e = min<uint64_t>(a + L, n);
+  uint32_t A = 0, B = 0;
+  for (uint64_t j = a; j < e;) {
+    const uint64_t k = min<uint64_t>(e, j + NMAX);
+    for (; j < k; j++) {
+      A += p[j];
+      B += A;
+    }
+    A %= M;
+    B %= M;
+  }
+  s1s[t] = A;
+  s2s[t] = (uint32_t)((B + (uint64_t)((n - e) % M) * A) % M);
+  __syncthreads();
+  if (t == 0) {
+    uint64_t s1 = 1, s2 = n % M;
+    for (uint32_t k = 0; k < CRC_THREADS; k++) {
+      s1 += s1s[k];
+      s2 += s2s[k];
+    }
+    const uint32_t adler = (uint32_t)((s2 % M) << 16) | (uint32_t)(s1 % M);
+    if (adler != aux[i].x) status[i] = ZG_CORRUPT_STREAM;
+  }
+}
+
+hipError_t launch_adler32_check(const ZgItem *subs, uint32_t *sub_status, const uint32_t *sub_kind, uint32_t n_sub,
+                                const uint2 *aux, hipStream_t s) {
+  if (!n_sub) return hipSuccess;
+  hipLaunchKernelGGL(k_adler32_check, dim3(n_sub), dim3(CRC_THREADS), 0, s, subs, sub_status, sub_kind, aux);
+  return hipGetLastError();
+}
+
 // ------------------------------- shard index --------------------------------------------------
 __global__ __launch_bounds__(CRC_THREADS) void k_shard_index(const ZgShard *shards, ZgIndexSpec spec,
                                                              uint64_t *index, uint32_t *shard_status) {

@@ -525,46 +525,62 @@ __device__ __forceinline__ void flush(const Smem &S, uint8_t *out, uint64_t cap,
 #ifndef ZG_INFLATE_WPE
 #define ZG_INFLATE_WPE 5
 #endif
-// One wave per item. aux[i] = {trailer CRC-32, trailer ISIZE}.
-__global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(ZG_INFLATE_WPE, 8))) void k_gzip(ZgItem *items, uint32_t *status, uint8_t *dst, uint64_t slot_bytes,
-                                             uint2 *aux) {
+// One wave per item. gzip (ZLIB = false, RFC 1952): aux[i] = {trailer CRC-32, trailer ISIZE}.
+// zlib (ZLIB = true, RFC 1950; blosc's zlib streams, c-blosc zlib_wrap_decompress = zlib uncompress):
+// only items whose kind is BL_KIND_ZLIB and status BL_SKIP; aux[i] = {Adler-32, 0}, status 0 on
+// success (the Adler-32 check follows in k_adler32_check).
+template <bool ZLIB>
+__global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(ZG_INFLATE_WPE, 8))) void k_gzip(
+    ZgItem *items, uint32_t *status, const uint32_t *kind, uint8_t *dst, uint64_t slot_bytes, uint2 *aux) {
   __shared__ Smem S;
   PROF_DECL;
   PROF_T(t_all);
   const uint32_t item = blockIdx.x;
+  if (ZLIB ? (kind[item] != BL_KIND_ZLIB || status[item] != BL_SKIP) : status[item] != 0) return;
   const ZgItem it = items[item];
-  if (status[item] || (it.flags & ZG_ITEM_FILL)) return;
+  if (it.flags & ZG_ITEM_FILL) return;
   const int lane = lane_id();
   uint8_t *out = dst + (uint64_t)item * slot_bytes;
   const uint64_t cap = slot_bytes;
   const uint8_t *in = (const uint8_t *)it.src;
   const uint64_t in_len = it.len;
   uint32_t err = 0;
-
-  // ---- RFC 1952 header (uniform byte reads) ----
-  uint64_t hp = 10;
-  if (in_len < 18) err = ZG_CORRUPT_STREAM;
-  uint32_t flg = 0;
-  if (!err) {
-    if (U(in[0]) != 0x1f || U(in[1]) != 0x8b || U(in[2]) != 8) err = ZG_CORRUPT_STREAM;
-    flg = U(in[3]);
-    if (flg & 0xE0) err = ZG_CORRUPT_STREAM;  // reserved flag bits
+  uint64_t hp;
+  if (ZLIB) {
+    // ---- RFC 1950 header: CM 8, CINFO <= 7, FCHECK, no preset dictionary (zlib: Z_NEED_DICT) ----
+    hp = 2;
+    if (in_len < 7) {
+      err = ZG_CORRUPT_STREAM;
+    } else {
+      const uint32_t cmf = U(in[0]), flg = U(in[1]);
+      if ((cmf & 15) != 8 || (cmf >> 4) > 7 || ((cmf << 8) | flg) % 31 != 0 || (flg & 0x20)) err = ZG_CORRUPT_STREAM;
+    }
+  } else {
+    // ---- RFC 1952 header (uniform byte reads) ----
+    hp = 10;
+    if (in_len < 18) err = ZG_CORRUPT_STREAM;
+    uint32_t flg = 0;
+    if (!err) {
+      if (U(in[0]) != 0x1f || U(in[1]) != 0x8b || U(in[2]) != 8) err = ZG_CORRUPT_STREAM;
+      flg = U(in[3]);
+      if (flg & 0xE0) err = ZG_CORRUPT_STREAM;  // reserved flag bits
+    }
+    if (!err && (flg & 4)) {  // FEXTRA
+      const uint32_t xlen = U(in[hp]) | (U(in[hp + 1]) << 8);  // hp + 2 <= 18 <= in_len
+      hp += 2 + xlen;
+      if (hp > in_len) err = ZG_CORRUPT_STREAM;
+    }
+    if (!err && (flg & 8)) {  // FNAME
+      while (hp < in_len && U(in[hp]) != 0) hp++;
+      hp++;
+    }
+    if (!err && (flg & 16)) {  // FCOMMENT
+      while (hp < in_len && U(in[hp]) != 0) hp++;
+      hp++;
+    }
+    if (!err && (flg & 2)) hp += 2;  // FHCRC
+    if (!err && hp + 8 > in_len) err = ZG_CORRUPT_STREAM;
   }
-  if (!err && (flg & 4)) {  // FEXTRA
-    const uint32_t xlen = U(in[hp]) | (U(in[hp + 1]) << 8);  // hp + 2 <= 18 <= in_len
-    hp += 2 + xlen;
-    if (hp > in_len) err = ZG_CORRUPT_STREAM;
-  }
-  if (!err && (flg & 8)) {  // FNAME
-    while (hp < in_len && U(in[hp]) != 0) hp++;
-    hp++;
-  }
-  if (!err && (flg & 16)) {  // FCOMMENT
-    while (hp < in_len && U(in[hp]) != 0) hp++;
-    hp++;
-  }
-  if (!err && (flg & 2)) hp += 2;  // FHCRC
-  if (!err && hp + 8 > in_len) err = ZG_CORRUPT_STREAM;
   if (err) {
     if (lane == 0) status[item] = err;
     return;
@@ -999,17 +1015,22 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(ZG_INFLATE_W
     flushed = pos;
   }
   if (!err) {
-    // trailer: byte-align, CRC-32 then ISIZE (little endian)
     const uint32_t r = (uint32_t)(B.consumed & 7);
     bits_drop(B, r ? 8 - r : 0);
     bits_refill(B);
-    const uint32_t crc_lo = bits_get(B, 16);
-    const uint32_t crc_hi = bits_get(B, 16);
-    const uint32_t isz_lo = bits_get(B, 16);
-    const uint32_t isz_hi = bits_get(B, 16);
-    const uint32_t crc = crc_lo | (crc_hi << 16), isz = isz_lo | (isz_hi << 16);
-    if (B.consumed > end_bits) err = ZG_CORRUPT_STREAM;
-    if (lane == 0 && !err) aux[item] = make_uint2(crc, isz);
+    if (ZLIB) {  // trailer: Adler-32, big endian
+      const uint32_t b0 = bits_get(B, 8), b1 = bits_get(B, 8), b2 = bits_get(B, 8), b3 = bits_get(B, 8);
+      if (B.consumed > end_bits) err = ZG_CORRUPT_STREAM;
+      if (lane == 0 && !err) aux[item] = make_uint2((b0 << 24) | (b1 << 16) | (b2 << 8) | b3, 0u);
+    } else {  // trailer: CRC-32 then ISIZE (little endian)
+      const uint32_t crc_lo = bits_get(B, 16);
+      const uint32_t crc_hi = bits_get(B, 16);
+      const uint32_t isz_lo = bits_get(B, 16);
+      const uint32_t isz_hi = bits_get(B, 16);
+      const uint32_t crc = crc_lo | (crc_hi << 16), isz = isz_lo | (isz_hi << 16);
+      if (B.consumed > end_bits) err = ZG_CORRUPT_STREAM;
+      if (lane == 0 && !err) aux[item] = make_uint2(crc, isz);
+    }
   }
   if (lane == 0) {
     if (err) {
@@ -1017,6 +1038,7 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(ZG_INFLATE_W
     } else {
       items[item].src = (uint64_t)out;
       items[item].len = pos;
+      if (ZLIB) status[item] = 0;
     }
   }
   PROF_ADD(4, t_all);
@@ -1026,7 +1048,14 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(ZG_INFLATE_W
 hipError_t launch_gzip(ZgItem *items, uint32_t *status, uint32_t n_items, uint8_t *dst, uint64_t slot_bytes,
                        uint2 *aux, hipStream_t s) {
   if (!n_items) return hipSuccess;
-  hipLaunchKernelGGL(k_gzip, dim3(n_items), dim3(64), 0, s, items, status, dst, slot_bytes, aux);
+  hipLaunchKernelGGL(k_gzip<false>, dim3(n_items), dim3(64), 0, s, items, status, nullptr, dst, slot_bytes, aux);
+  return hipGetLastError();
+}
+
+hipError_t launch_zlib_streams(ZgItem *subs, uint32_t *sub_status, const uint32_t *sub_kind, uint32_t n_sub,
+                               uint8_t *dst, uint64_t slot, uint2 *aux, hipStream_t s) {
+  if (!n_sub) return hipSuccess;
+  hipLaunchKernelGGL(k_gzip<true>, dim3(n_sub), dim3(64), 0, s, subs, sub_status, sub_kind, dst, slot, aux);
   return hipGetLastError();
 }
 

@@ -191,7 +191,7 @@ struct zgpu_plan {
     size_t n = 0;
   };
   Grow bl_info, bl_bases, bl_subs, bl_sub_status, bl_sub_kind, bl_blocks, bl_tmp, bl_zblks, bl_znblk, bl_zmode,
-      bl_zlit, bl_zseq;
+      bl_zlit, bl_zseq, bl_zaux;
   uint8_t *bl_h = nullptr;  // pinned: BlInfo read-back (first execution)
   size_t bl_h_n = 0;
   void *grow(Grow &g, size_t bytes) {
@@ -222,7 +222,7 @@ struct zgpu_plan {
                     d_enc_stage};
     for (void *b : bufs) ctx->dev_free(b);
     for (Grow *g : {&bl_info, &bl_bases, &bl_subs, &bl_sub_status, &bl_sub_kind, &bl_blocks, &bl_tmp, &bl_zblks,
-                    &bl_znblk, &bl_zmode, &bl_zlit, &bl_zseq})
+                    &bl_znblk, &bl_zmode, &bl_zlit, &bl_zseq, &bl_zaux})
       ctx->dev_free(g->p);
     ctx->host_free(bl_h);
     ctx->host_free(h_ctl);
@@ -557,7 +557,7 @@ static void blosc_stage(zgpu_plan &P, const Stage &st, hipStream_t s) {
       exact.n_blk += hi[i].nblk;
       if (hi[i].nsub)
         exact.kinds |= hi[i].comp == BL_COMP_ZSTD ? BL_HAS_ZSTD : hi[i].comp == BL_COMP_LZ4 ? BL_HAS_LZ4
-                       : hi[i].comp == BL_COMP_BLOSCLZ ? BL_HAS_BLOSCLZ : 0u;
+                       : hi[i].comp == BL_COMP_BLOSCLZ ? BL_HAS_BLOSCLZ : hi[i].comp == BL_COMP_ZLIB ? BL_HAS_ZLIB : 0u;
       exact.max_ne = std::max<uint64_t>(exact.max_ne, hi[i].max_ne);
     }
     // capacities only grow (a plan whose inputs alternate between layouts settles on their maximum)
@@ -576,15 +576,17 @@ static void blosc_stage(zgpu_plan &P, const Stage &st, hipStream_t s) {
   D.n_zstd = caps.kinds & BL_HAS_ZSTD;
   D.n_lz4 = caps.kinds & BL_HAS_LZ4;
   D.n_blosclz = caps.kinds & BL_HAS_BLOSCLZ;
+  D.n_zlib = caps.kinds & BL_HAS_ZLIB;
   const uint64_t ns = std::max<uint64_t>(D.n_sub, 1);
   D.subs = (ZgItem *)P.grow(P.bl_subs, ns * sizeof(ZgItem));
   D.sub_status = (uint32_t *)P.grow(P.bl_sub_status, ns * 4);
   D.sub_kind = (uint32_t *)P.grow(P.bl_sub_kind, ns * 4);
   D.blocks = (BlBlock *)P.grow(P.bl_blocks, std::max<uint64_t>(D.n_blk, 1) * sizeof(BlBlock));
-  if (D.n_zstd + D.n_lz4 + D.n_blosclz) {
+  if (D.n_zstd + D.n_lz4 + D.n_blosclz + D.n_zlib) {
     D.sub_slot = (caps.max_ne + 255) & ~(uint64_t)255;
     D.tmp = (uint8_t *)P.grow(P.bl_tmp, D.n_sub * D.sub_slot);
   }
+  if (D.n_zlib) D.zaux = (uint2 *)P.grow(P.bl_zaux, D.n_sub * sizeof(uint2));
   if (D.n_zstd) {
     uint64_t blk_bytes;
     zstd_scratch_layout(D.sub_slot, D.zs.blk_cap, blk_bytes, D.zs.lit_stride, D.zs.seq_cap);
