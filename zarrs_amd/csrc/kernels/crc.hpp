@@ -1,0 +1,150 @@
+// CRC-32 / CRC-32C helpers shared by crc.hip and inflate.hip (the gzip trailer check runs at the
+// end of k_gzip). Parallel CRC: each thread checksums a contiguous segment with slice-by-4 tables
+// held in LDS; the partial CRCs are merged with the GF(2) shift operator
+// crc(A||B) = crc(A) * x^(8|B|) mod P  xor  crc(B) (the zlib crc32_combine identity), using a table
+// of x^(2^k) mod P, in a log2(threads)-deep shuffle/LDS tree.
+#pragma once
+#include <hip/hip_runtime.h>
+
+#include <cstdint>
+
+namespace zgpu {
+
+constexpr uint32_t POLY_CRC32C = 0x82F63B78u;  // reflected Castagnoli (crc32c crate)
+constexpr uint32_t POLY_CRC32 = 0xEDB88320u;   // reflected IEEE (gzip trailer, RFC 1952)
+constexpr int CRC_THREADS = 256;
+
+struct CrcTables {
+  uint32_t t[4][256];  // slice-by-4
+  uint32_t x2n[32];    // x^(2^k) mod P
+};
+
+__device__ __forceinline__ uint32_t multmodp(uint32_t a, uint32_t b, uint32_t poly) {
+  uint32_t m = 1u << 31, p = 0;
+  for (;;) {
+    if (a & m) {
+      p ^= b;
+      if ((a & (m - 1)) == 0) break;
+    }
+    m >>= 1;
+    b = (b & 1) ? (b >> 1) ^ poly : b >> 1;
+  }
+  return p;
+}
+
+// x^(8*len) mod P
+__device__ __forceinline__ uint32_t x8nmodp(uint64_t len, const uint32_t *x2n, uint32_t poly) {
+  uint32_t p = 1u << 31;
+  uint32_t k = 3;
+  while (len) {
+    if (len & 1) p = multmodp(x2n[k & 31], p, poly);
+    len >>= 1;
+    k++;
+  }
+  return p;
+}
+
+__device__ __forceinline__ uint32_t crc_combine(uint32_t c1, uint32_t c2, uint64_t len2, const uint32_t *x2n,
+                                                uint32_t poly) {
+  if (len2 == 0) return c1;
+  return multmodp(x8nmodp(len2, x2n, poly), c1, poly) ^ c2;
+}
+
+__device__ inline void build_tables(CrcTables &T, uint32_t poly) {
+  for (uint32_t i = threadIdx.x; i < 256; i += blockDim.x) {
+    uint32_t c = i;
+    for (int k = 0; k < 8; k++) c = (c & 1) ? (c >> 1) ^ poly : c >> 1;
+    T.t[0][i] = c;
+  }
+  __syncthreads();
+  for (uint32_t i = threadIdx.x; i < 256; i += blockDim.x) {
+    uint32_t c = T.t[0][i];
+    for (int s = 1; s < 4; s++) {
+      c = (c >> 8) ^ T.t[0][c & 0xff];
+      T.t[s][i] = c;
+    }
+  }
+  if (threadIdx.x == 0) {
+    uint32_t p = 1u << 30;  // x^1
+    T.x2n[0] = p;
+    for (int n = 1; n < 32; n++) T.x2n[n] = p = multmodp(p, p, poly);
+  }
+  __syncthreads();
+}
+
+// Standard CRC (init/xorout 0xFFFFFFFF) of a short segment.
+__device__ __forceinline__ uint32_t crc_segment(const uint8_t *p, uint64_t n, const CrcTables &T) {
+  uint32_t c = 0xFFFFFFFFu;
+  while (n && ((uintptr_t)p & 3)) {
+    c = (c >> 8) ^ T.t[0][(c ^ *p++) & 0xff];
+    n--;
+  }
+  // 16-B vectors, the next two already in flight while one is folded in (a lane's segment is a
+  // serial chain: without the prefetch every vector waits a full memory round trip)
+  auto fold = [&](const uint4 v) {
+    const uint32_t w[4] = {v.x, v.y, v.z, v.w};
+#pragma unroll
+    for (int k = 0; k < 4; k++) {
+      const uint32_t x = c ^ w[k];
+      c = T.t[3][x & 0xff] ^ T.t[2][(x >> 8) & 0xff] ^ T.t[1][(x >> 16) & 0xff] ^ T.t[0][x >> 24];
+    }
+  };
+  if (n >= 16) {
+    const uint64_t nv = n >> 4;
+    uint4 v0 = *(const uint4 *)p, v1 = nv > 1 ? *(const uint4 *)(p + 16) : v0;
+    for (uint64_t k = 0; k < nv; k++) {
+      const uint4 v2 = k + 2 < nv ? *(const uint4 *)(p + 16 * (k + 2)) : v1;
+      fold(v0);
+      v0 = v1;
+      v1 = v2;
+    }
+    p += 16 * nv;
+    n -= 16 * nv;
+  }
+  while (n >= 4) {
+    const uint32_t x = c ^ *(const uint32_t *)p;
+    c = T.t[3][x & 0xff] ^ T.t[2][(x >> 8) & 0xff] ^ T.t[1][(x >> 16) & 0xff] ^ T.t[0][x >> 24];
+    p += 4;
+    n -= 4;
+  }
+  while (n--) c = (c >> 8) ^ T.t[0][(c ^ *p++) & 0xff];
+  return ~c;
+}
+
+// Workgroup-wide CRC of p[0..n): every thread returns the same value.
+__device__ inline uint32_t wg_crc(const uint8_t *p, uint64_t n, const CrcTables &T, uint32_t poly, uint64_t *s_len,
+                           uint32_t *s_crc) {
+  const uint32_t tid = threadIdx.x, nt = blockDim.x;
+  // segments aligned to 16 bytes so the inner loop runs on 16-B loads
+  uint64_t seg = (n + nt - 1) / nt;
+  seg = (seg + 15) & ~(uint64_t)15;
+  const uint64_t b0 = min<uint64_t>((uint64_t)tid * seg, n), b1 = min<uint64_t>(b0 + seg, n);
+  uint32_t c = crc_segment(p + b0, b1 - b0, T);
+  uint64_t l = b1 - b0;
+  // tree merge: lane pairs within the wave, then waves through LDS
+  for (int off = 1; off < 64; off <<= 1) {
+    const uint32_t c2 = __shfl_down(c, off, 64);
+    const uint64_t l2 = __shfl_down(l, off, 64);
+    if ((tid & 63) % (2 * off) == 0 && (tid & 63) + off < 64) {
+      c = crc_combine(c, c2, l2, T.x2n, poly);
+      l += l2;
+    }
+  }
+  const uint32_t nw = nt / 64;
+  if ((tid & 63) == 0) {
+    s_crc[tid / 64] = c;
+    s_len[tid / 64] = l;
+  }
+  __syncthreads();
+  if (tid == 0) {
+    uint32_t acc = s_crc[0];
+    for (uint32_t w = 1; w < nw; w++) acc = crc_combine(acc, s_crc[w], s_len[w], T.x2n, poly);
+    s_crc[0] = acc;
+  }
+  __syncthreads();
+  const uint32_t r = s_crc[0];
+  __syncthreads();
+  return r;
+}
+
+}  // namespace zgpu

@@ -51,14 +51,10 @@ hipError_t launch_item_resolve(ZgItem *items, uint32_t *status, uint32_t n_items
                                const uint64_t *index, const uint32_t *shard_status, uint64_t n_inner,
                                unsigned long long *enc_bytes, hipStream_t s);
 
-// gzip trailer check: CRC-32 (IEEE) and ISIZE of each item's inflated bytes vs aux[i] = {crc, isize}
-hipError_t launch_crc32_check(const ZgItem *items, uint32_t *status, uint32_t n_items, const uint2 *aux,
-                              hipStream_t s);
-
-// gzip (RFC 1952) member decode: header parse, DEFLATE inflate into dst slots, CRC-32 + ISIZE check.
-// On return items[i] points at its slot; aux[i] receives the trailer {crc32, isize} for launch_crc32_check.
+// gzip (RFC 1952) member decode: header parse, DEFLATE inflate into dst slots, trailer CRC-32 (IEEE)
+// + ISIZE check of the inflated bytes. On return items[i] points at its slot.
 hipError_t launch_gzip(ZgItem *items, uint32_t *status, uint32_t n_items, uint8_t *dst, uint64_t slot_bytes,
-                       uint2 *aux, hipStream_t s);
+                       hipStream_t s);
 // zstd (RFC 8878) frame decode into dst slots: block-parallel (scan, per-block entropy decode,
 // per-item execution) with the serial one-wave-per-item decoder as the fallback.
 struct ZstdScratch {

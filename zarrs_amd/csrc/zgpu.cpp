@@ -183,7 +183,6 @@ struct zgpu_plan {
   uint64_t *d_index = nullptr;
   uint32_t *d_shard_status = nullptr;
   uint8_t *d_pool[2] = {nullptr, nullptr};
-  uint2 *d_aux = nullptr;
   ZstdScratch zs{};  // block-parallel zstd scratch (allocated when the chain has zstd)
   // blosc stage scratch (grown on demand; the stream table is sized from the frame headers)
   struct Grow {
@@ -218,7 +217,7 @@ struct zgpu_plan {
   ~zgpu_plan() {
     if (!ctx) return;
     void *bufs[] = {d_items, d_items_init, d_geom, d_shards, d_index, d_shard_status,
-                    d_pool[0], d_pool[1], d_aux, zs.blks, zs.nblk, zs.mode, zs.lit, zs.seq, d_ctl,
+                    d_pool[0], d_pool[1], zs.blks, zs.nblk, zs.mode, zs.lit, zs.seq, d_ctl,
                     d_enc_stage};
     for (void *b : bufs) ctx->dev_free(b);
     for (Grow *g : {&bl_info, &bl_bases, &bl_subs, &bl_sub_status, &bl_sub_kind, &bl_blocks, &bl_tmp, &bl_zblks,
@@ -494,7 +493,6 @@ static void plan_upload(zgpu_plan &P, hipStream_t us = nullptr) {
     HIPCHK(hipMemcpyAsync(P.d_geom, P.geom.data(), P.geom.size() * 8, hipMemcpyHostToDevice, us));
     for (int k = 0; k < P.n_pools; k++) P.d_pool[k] = (uint8_t *)C.dev_alloc(ni * P.slot_bytes);
     for (const Stage &s : P.stages) {
-      if (s.kind == ST_GZIP && !P.d_aux) P.d_aux = (uint2 *)C.dev_alloc(ni * sizeof(uint2));
       if (s.kind == ST_ZSTD && !P.zs.blks) {
         uint64_t blk_bytes;
         zstd_scratch_layout(P.slot_bytes, P.zs.blk_cap, blk_bytes, P.zs.lit_stride, P.zs.seq_cap);
@@ -625,8 +623,7 @@ static void plan_enqueue(zgpu_plan &P, uint8_t *out, hipStream_t s) {
         HIPCHK(launch_crc32c_strip(P.d_items, P.d_status, ni, st.at_start, P.validate ? 1 : 0, s));
         break;
       case ST_GZIP:
-        HIPCHK(launch_gzip(P.d_items, P.d_status, ni, P.d_pool[st.pool], P.slot_bytes, P.d_aux, s));
-        HIPCHK(launch_crc32_check(P.d_items, P.d_status, ni, P.d_aux, s));
+        HIPCHK(launch_gzip(P.d_items, P.d_status, ni, P.d_pool[st.pool], P.slot_bytes, s));
         break;
       case ST_ZSTD:
         HIPCHK(launch_zstd(P.d_items, P.d_status, ni, P.d_pool[st.pool], P.slot_bytes, P.zs, s));
