@@ -816,9 +816,13 @@ def run_gpu(args, rank, world, dev):
     # the library launches on this stream; events are recorded on it. Independent parts (pyramid
     # levels) run concurrently, one stream each: part 0 (the largest level, the longest serial chain)
     # on `stream` at high priority, so its kernels take CUs first
-    stream = torch.cuda.Stream(dev, priority=-1) if len(lanes) > 1 else torch.cuda.Stream(dev)
+    prio = W.lane_priorities if hasattr(W, "lane_priorities") else [-1, -1] + [0] * max(0, len(lanes) - 2)
+    if args.lane_priorities:
+        prio = [int(x) for x in args.lane_priorities.split(",")]
+    prio = (prio + [0] * len(lanes))[:len(lanes)]
+    stream = torch.cuda.Stream(dev, priority=prio[0]) if len(lanes) > 1 else torch.cuda.Stream(dev)
     sp = C.c_void_p(stream.cuda_stream)
-    side = [torch.cuda.Stream(dev, priority=-1 if li < 2 else 0) for li in range(1, len(lanes))]
+    side = [torch.cuda.Stream(dev, priority=prio[li]) for li in range(1, len(lanes))]
     lane_sp = [sp] + [C.c_void_p(st.cuda_stream) for st in side]
     plan_sp = {pi: lane_sp[li] for li, ln in enumerate(lanes) for pi in ln}
 
@@ -943,7 +947,8 @@ def pmc_traffic(args, W):
             cmd = ["rocprofv3", "--pmc", ctr, "--kernel-include-regex", regex, "-d", d, "-o", "pmc",
                    "--output-format", "csv", "--", sys.executable, os.path.abspath(__file__), "--child",
                    "--workload", args.workload, "--steps", str(steps), "--warmup", str(warm), "--no-cpu",
-                   "--grid", *map(str, args.grid), "--c5-scale", str(args.c5_scale)]
+                   "--grid", *map(str, args.grid), "--c5-scale", str(args.c5_scale)] + \
+                  (["--lane-priorities", args.lane_priorities] if args.lane_priorities else [])
             # the child's stderr goes to a file; a heartbeat on ours shows the pass is alive
             elog = os.path.join(tmp, ctr + ".err")
             t0 = time.time()
@@ -1000,6 +1005,8 @@ def main():
     ap.add_argument("--no-cpu", action="store_true")
     ap.add_argument("--lane-times", action="store_true", help="print each stream lane's solo time (stderr)")
     ap.add_argument("--no-pmc", action="store_true", help="skip the rocprofv3 PMC traffic passes")
+    ap.add_argument("--lane-priorities", default="",
+                    help="comma-separated HIP stream priorities of the stream lanes (-1 high, 0 normal)")
     ap.add_argument("--serial-lanes", action="store_true",
                     help="run every plan on one stream (profiling: per-kernel durations without overlap)")
     ap.add_argument("--no-host-leg", dest="host_leg", action="store_false",

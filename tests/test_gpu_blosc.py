@@ -1,6 +1,7 @@
 """GPU parity of the blosc codec against the reference's blosc fixtures
 (zstd + bitshuffle, written by zarrs and zarr-python) and the CPU oracle (c-blosc 1.21, the library
-zarrs' blosc-src binds) on seeded inputs: blosclz (c-blosc's default) / lz4 / lz4hc / zlib / zstd streams,
+zarrs' blosc-src binds) on seeded inputs: blosclz (c-blosc's default) / lz4 / lz4hc / zlib / zstd streams
+(snappy: frames written by the test's own encoder, the host c-blosc has no snappy),
 byte shuffle / bitshuffle / none, typesizes 1-8, forced block sizes (split streams, leftover blocks,
 bitshuffle skipped for element counts that are not a multiple of 8), memcpyed frames, blosc inside
 sharding. Bit-exact."""
@@ -105,12 +106,11 @@ def test_blosc_memcpyed_and_errors(ctx, torch_cuda):
     out = np.zeros(3000, np.float32)
     assert ch.decode_batch([make_desc(enc0, [3000])], out, [3000], enc_device=False) == [0]
     assert np.array_equal(out, a)
-    # snappy streams (c-blosc compressor format 2; not in the host c-blosc) are not decoded on the
-    # GPU: UNSUPPORTED, loudly (a frame relabelled as snappy)
+    # compressor formats 5-7 are not defined by c-blosc 1.x: UNSUPPORTED, loudly (a relabelled frame)
     codecs1 = [{"name": "bytes", "configuration": {"endian": "little"}}, _blosc("lz4", "shuffle", 4)]
     enc1 = bytearray(O.OracleChain.from_metadata(codecs1, "float32", 0, 1).encode(np.zeros(3000, np.float32) + 1))
     assert not enc1[2] & 0x2
-    enc1[2] = (enc1[2] & 0x1F) | (2 << 5)
+    enc1[2] = (enc1[2] & 0x1F) | (5 << 5)
     with pytest.raises(ZgpuError) as ei:
         ch.decode_batch([make_desc(bytes(enc1), [3000])], out, [3000], enc_device=False)
     assert ei.value.status == L.UNSUPPORTED
@@ -254,3 +254,143 @@ def test_blosc_plan_cached_layout_and_rerun(ctx, torch_cuda, cname):
             assert ctr[L.CTR_BLOSC_RERUN] == rerun, (v, list(ctr))
     finally:
         L.load().zgpu_plan_destroy(plan)
+
+
+# ---- snappy streams (c-blosc compressor format 2) ------------------------------------------------
+# The host c-blosc is built without snappy, so these frames are written here: a small snappy encoder
+# (raw format, google/snappy format_description.txt) that emits every element form — inline and
+# 1-4-byte literal lengths, copies with 1-, 2- and 4-byte offsets, overlapping copies — inside c-blosc
+# 1.x frames (16-B header, bstarts, {csize, stream} per split; a stream whose compressed size would
+# reach the split's size is stored). Parity unpinned (no snappy library in the image): checked by
+# round trip against the encoded data.
+def _varint(v):
+    out = bytearray()
+    while True:
+        b = v & 127
+        v >>= 7
+        out.append(b | (128 if v else 0))
+        if not v:
+            return bytes(out)
+
+
+def _snappy_literal(out, lit, rng):
+    while lit:
+        n = len(lit) if len(lit) <= 200 else int(rng.integers(1, len(lit) + 1))
+        if n <= 60 and rng.random() < 0.7:
+            out.append((n - 1) << 2)
+        else:  # 60..63: the length - 1 in 1..4 little-endian bytes (any width that holds it is valid)
+            nb = max(1, ((n - 1).bit_length() + 7) // 8)
+            nb = min(4, nb + int(rng.integers(0, 2)))
+            out.append((59 + nb) << 2)
+            out += (n - 1).to_bytes(nb, "little")
+        out += lit[:n]
+        lit = lit[n:]
+
+
+def _snappy_copy(out, off, n, rng):
+    while n:
+        if 4 <= n <= 11 and off < 2048 and rng.random() < 0.6:
+            out.append(1 | ((n - 4) << 2) | ((off >> 8) << 5))
+            out.append(off & 255)
+            return
+        m = min(n, 64)
+        if n - m and n - m < 4:  # keep the remainder encodable (a copy of >= 1 byte is fine too)
+            m = n - 4 if n > 4 else n
+        if off < 65536 and rng.random() < 0.7:
+            out.append(2 | ((m - 1) << 2))
+            out += off.to_bytes(2, "little")
+        else:
+            out.append(3 | ((m - 1) << 2))
+            out += off.to_bytes(4, "little")
+        n -= m
+
+
+def _snappy_compress(data, rng):
+    out = bytearray(_varint(len(data)))
+    table, i, lit0, n = {}, 0, 0, len(data)
+    while i + 4 <= n:
+        key = data[i:i + 4]
+        j = table.get(key)
+        table[key] = i
+        if j is not None:
+            m = 4
+            while i + m < n and data[j + m] == data[i + m] and m < 300:
+                m += 1
+            _snappy_literal(out, data[lit0:i], rng)
+            _snappy_copy(out, i - j, m, rng)
+            i += m
+            lit0 = i
+        else:
+            i += 1
+    _snappy_literal(out, data[lit0:], rng)
+    return bytes(out)
+
+
+def _blosc_snappy_frame(data, ts, shuffle, blocksize, split, rng):
+    nbytes = len(data)
+    nblk = -(-nbytes // blocksize)
+    left = nbytes % blocksize
+    flags = (1 if shuffle else 0) | (0 if split else 0x10) | (2 << 5)
+    body, starts = bytearray(), []
+    hdr_len = 16 + 4 * nblk
+    for b in range(nblk):
+        src = data[b * blocksize:(b + 1) * blocksize]
+        bsize = len(src)
+        if shuffle and ts > 1:  # c-blosc shuffle: byte i of element j -> i * neb + j; the tail as is
+            neb = bsize // ts
+            a = np.frombuffer(src[:neb * ts], np.uint8).reshape(neb, ts).T.reshape(-1).tobytes()
+            src = a + src[neb * ts:]
+        nsplit = ts if (split and not (left and b == nblk - 1)) else 1
+        ne = bsize // nsplit
+        starts.append(hdr_len + len(body))
+        for j in range(nsplit):
+            part = src[j * ne:(j + 1) * ne]
+            z = _snappy_compress(part, rng)
+            if len(z) >= ne:
+                z = part  # stored
+            body += len(z).to_bytes(4, "little") + z
+    cbytes = hdr_len + len(body)
+    hdr = bytes([2, 1, flags, ts]) + nbytes.to_bytes(4, "little") + blocksize.to_bytes(4, "little") + \
+        cbytes.to_bytes(4, "little")
+    return hdr + b"".join(s.to_bytes(4, "little") for s in starts) + bytes(body)
+
+
+@pytest.mark.parametrize("ts,shuffle,split", [(1, False, False), (2, True, True), (4, True, False),
+                                              (4, False, True), (8, True, True)])
+def test_blosc_snappy_streams(ctx, torch_cuda, ts, shuffle, split):
+    from zarrs_amd import CodecChain, ZgpuError, make_desc
+    from zarrs_amd import _lib as L
+    rng = np.random.default_rng(ts * 11 + shuffle + 2 * split)
+    ch = CodecChain.from_metadata([{"name": "bytes", "configuration": {"endian": "little"}},
+                                   _blosc("snappy", "shuffle" if shuffle else "noshuffle", ts)], DT[ts], 0, ctx)
+    for n, bsz in ((1000, 4096), (40000, 8192), (30001, 4096), (70000, 65536)):
+        n -= n % 1 if ts == 1 else n % ts
+        descs, keep, exp = [], [], []
+        for k in range(3):
+            a = _data(rng, n // ts, ts)
+            if k == 1:  # long runs and a period past the 2-byte offsets (4-byte copies)
+                a = np.resize(np.repeat(a[: max(1, len(a) // 64)], 64), n // ts)
+            raw = a.tobytes()
+            enc = _blosc_snappy_frame(raw, ts, shuffle, bsz, split, rng)
+            d = torch_cuda.frombuffer(bytearray(enc), dtype=torch_cuda.uint8).cuda()
+            keep.append(d)
+            descs.append(make_desc(d, [n // ts], out_start=[k * (n // ts)]))
+            exp.append(a)
+        out = np.zeros(3 * (n // ts), DT[ts])
+        st = ch.decode_batch(descs, out, [3 * (n // ts)], enc_device=True)
+        assert st == [0] * 3, (n, bsz)
+        assert out.tobytes() == np.concatenate(exp).tobytes(), (n, bsz)
+    # a copy reaching before the stream start / a truncated stream -> CORRUPT_STREAM
+    a = _data(rng, 4096 // ts, ts)
+    enc = bytearray(_blosc_snappy_frame(a.tobytes(), ts, False, 4096, False, rng))
+    p = int.from_bytes(enc[16:20], "little")
+    cs = int.from_bytes(enc[p:p + 4], "little")
+    if cs != 4096:
+        z = bytearray(_varint(4096)) + bytes([2 | (3 << 2)]) + (9).to_bytes(2, "little")  # copy 4 at offset 9
+        bad = enc[:p] + len(z).to_bytes(4, "little") + z
+        bad[12:16] = len(bad).to_bytes(4, "little")
+        for e in (bytes(bad), bytes(enc[:p + 4 + cs // 2])):
+            with pytest.raises(ZgpuError) as ei:
+                ch.decode_batch([make_desc(e, [4096 // ts])], np.zeros(4096 // ts, DT[ts]), [4096 // ts],
+                                enc_device=False)
+            assert ei.value.status == L.CORRUPT_STREAM

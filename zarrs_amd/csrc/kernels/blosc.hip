@@ -6,7 +6,7 @@
 //   16-B header {version, versionlz, flags, typesize, nbytes u32, blocksize u32, cbytes u32}
 //   flags: 0x1 byte shuffle, 0x2 memcpyed (raw payload after the header), 0x4 bitshuffle,
 //          0x10 blocks not split, bits 5-7 compressor format (0 blosclz, 1 lz4/lz4hc, 2 snappy,
-//          3 zlib, 4 zstd); blosclz, lz4/lz4hc, zlib and zstd decode here, snappy -> UNSUPPORTED
+//          3 zlib, 4 zstd); every one of them decodes here (formats 5-7 -> UNSUPPORTED)
 //   bstarts[nblocks] i32, then per block nsplit = (split && not the leftover block) ? typesize : 1
 //   streams of {csize i32, payload}; csize == neblock means stored.
 // A block's streams concatenate to the shuffled block, then unshuffle / bitunshuffle (format 2:
@@ -20,7 +20,8 @@
 //   k_blosc_streams  one wave per item: walks bstarts + split sizes in parallel over blocks, writes
 //                    one ZgItem per compressed stream (+ its kind) and one record per block
 //   zstd streams     the block-parallel zstd pipeline (launch_zstd) over the stream table
-//   k_lz4, k_blosclz one wave per lz4 / blosclz stream (input staged through an LDS window)
+//   k_lz4, k_blosclz, k_snappy  one wave per lz4 / blosclz / snappy stream (input staged through
+//                    an LDS window, recent output in an LDS ring)
 //   zlib streams     k_gzip's DEFLATE decoder with the RFC 1950 wrapper (inflate.hip), then the
 //                    Adler-32 trailer check (k_adler32_check, crc.hip)
 //   k_blosc_finish   one workgroup per block: gathers the block's streams and unshuffles /
@@ -66,8 +67,7 @@ __global__ __launch_bounds__(64) void k_blosc_info(const ZgItem *items, uint32_t
   } else if (!err && nbytes) {
     const uint32_t comp = flags >> 5;
     if (ts == 0 || bs == 0) err = ZG_CORRUPT_STREAM;
-    else if (comp != BL_COMP_LZ4 && comp != BL_COMP_ZSTD && comp != BL_COMP_BLOSCLZ && comp != BL_COMP_ZLIB)
-      err = ZG_UNSUPPORTED;  // snappy
+    else if (comp > BL_COMP_ZSTD) err = ZG_UNSUPPORTED;  // formats 5-7 are not defined by c-blosc 1.x
     if (!err) {
       const uint32_t lo = nbytes % bs, nfull = nbytes / bs, nblk = nfull + (lo ? 1 : 0);
       const uint32_t nsplit = (flags & 0x10) ? 1 : ts;
@@ -106,7 +106,8 @@ __global__ __launch_bounds__(1024) void k_blosc_layout(const BlInfo *info, uint3
     nblk += I.nblk;
     ne = max(ne, I.max_ne);
     if (I.nsub) kinds |= I.comp == BL_COMP_ZSTD ? BL_HAS_ZSTD : I.comp == BL_COMP_LZ4 ? BL_HAS_LZ4
-                        : I.comp == BL_COMP_BLOSCLZ ? BL_HAS_BLOSCLZ : I.comp == BL_COMP_ZLIB ? BL_HAS_ZLIB : 0u;
+                        : I.comp == BL_COMP_BLOSCLZ ? BL_HAS_BLOSCLZ : I.comp == BL_COMP_ZLIB ? BL_HAS_ZLIB
+                        : I.comp == BL_COMP_SNAPPY ? BL_HAS_SNAPPY : 0u;
   }
   ssub[t] = nsub;
   sblk[t] = nblk;
@@ -191,6 +192,7 @@ __global__ __launch_bounds__(64) void k_blosc_streams(ZgItem *items, uint32_t *s
                            : I.comp == BL_COMP_ZSTD ? BL_KIND_ZSTD
                            : I.comp == BL_COMP_LZ4  ? BL_KIND_LZ4
                            : I.comp == BL_COMP_ZLIB ? BL_KIND_ZLIB
+                           : I.comp == BL_COMP_SNAPPY ? BL_KIND_SNAPPY
                                                     : BL_KIND_BLOSCLZ;
         sub_status[s0 + j] = (!raw && I.comp == BL_COMP_ZSTD) ? 0u : BL_SKIP;
         p += cs;
@@ -427,6 +429,81 @@ __global__ __launch_bounds__(64) void k_blosclz(ZgItem *subs, uint32_t *sub_stat
   }
 }
 
+// snappy (raw format, format_description.txt of google/snappy; c-blosc 1.21 snappy_wrap_decompress =
+// snappy_uncompress): a varint of the uncompressed length, then elements by the tag's low 2 bits —
+// 00 literal (length - 1 in the tag's upper 6 bits, or 60..63: in the next 1..4 bytes), 01 copy of
+// 4 + ((tag >> 2) & 7) bytes at an 11-bit offset ((tag >> 5) << 8 | next byte), 10 / 11 copy of
+// 1 + (tag >> 2) bytes at a 2 / 4-byte little-endian offset. Offset 0 or past the output is an error;
+// the output must be exactly the preamble's length and the input consumed exactly.
+__global__ __launch_bounds__(64) void k_snappy(ZgItem *subs, uint32_t *sub_status, const uint32_t *sub_kind,
+                                               uint32_t n_sub, uint8_t *dst, uint64_t slot) {
+  __shared__ __attribute__((aligned(16))) uint8_t win[LZW];
+  __shared__ uint8_t ring[LZR];
+  const uint32_t s = blockIdx.x, lane = threadIdx.x;
+  if (sub_kind[s] != BL_KIND_SNAPPY || sub_status[s] != BL_SKIP) return;
+  const ZgItem it = subs[s];
+  const uint64_t n = it.len;
+  LzIn I{(const uint8_t *)it.src, n, 0, win};
+  uint8_t *out = dst + (uint64_t)s * slot;
+  uint64_t ip = 0, op = 0, safe = 0, want = 0;
+  uint32_t err = 0;
+  if (n) I.fill(0);
+  // preamble: little-endian base-128 varint (<= 5 bytes, < 2^32)
+  for (uint32_t k = 0;; k++) {
+    if (ip >= n || k == 5) { err = 1; break; }
+    const uint32_t b = I.b(ip++);
+    want |= (uint64_t)(b & 127) << (7 * k);
+    if (!(b & 128)) break;
+  }
+  if (!err && (want > slot || want >> 32)) err = 1;
+  while (!err && ip < n) {
+    const uint32_t tag = I.b(ip++);
+    if ((tag & 3) == 0) {  // literal
+      uint64_t len = (tag >> 2) + 1;
+      if (len > 60) {
+        const uint32_t nb = (uint32_t)len - 60;  // 1..4 length bytes
+        if (ip + nb > n) { err = 1; break; }
+        uint64_t v = 0;
+        for (uint32_t k = 0; k < nb; k++) v |= (uint64_t)I.b(ip + k) << (8 * k);
+        ip += nb;
+        len = v + 1;
+      }
+      if (ip + len > n || op + len > want) { err = 1; break; }
+      I.copy(out, op, ip, len, ring);
+      ip += len;
+      op += len;
+    } else {
+      uint64_t len, off;
+      if ((tag & 3) == 1) {
+        if (ip + 1 > n) { err = 1; break; }
+        len = 4 + ((tag >> 2) & 7);
+        off = ((uint64_t)(tag >> 5) << 8) | I.b(ip);
+        ip += 1;
+      } else if ((tag & 3) == 2) {
+        if (ip + 2 > n) { err = 1; break; }
+        len = 1 + (tag >> 2);
+        off = I.b(ip) | (I.b(ip + 1) << 8);
+        ip += 2;
+      } else {
+        if (ip + 4 > n) { err = 1; break; }
+        len = 1 + (tag >> 2);
+        off = (uint64_t)I.b(ip) | ((uint64_t)I.b(ip + 1) << 8) | ((uint64_t)I.b(ip + 2) << 16) |
+              ((uint64_t)I.b(ip + 3) << 24);
+        ip += 4;
+      }
+      if (off == 0 || off > op || op + len > want) { err = 1; break; }
+      lz_match(out, op, off, len, safe, ring);
+      op += len;
+    }
+  }
+  if (!err && op != want) err = 1;
+  if (lane == 0) {
+    sub_status[s] = err ? ZG_CORRUPT_STREAM : 0u;
+    subs[s].src = (uint64_t)out;
+    subs[s].len = op;
+  }
+}
+
 // One workgroup per block: the block's streams (decoded, or stored in the frame) are the shuffled
 // block; unshuffle / bitunshuffle into the item's output slot.
 __global__ __launch_bounds__(256) void k_blosc_finish(const BlBlock *blocks, const ZgItem *subs,
@@ -526,6 +603,9 @@ hipError_t launch_blosc_decode(ZgItem *items, uint32_t *status, uint32_t n_items
     if (e == hipSuccess) e = launch_adler32_check(D.subs, D.sub_status, D.sub_kind, (uint32_t)D.n_sub, D.zaux, s);
     if (e != hipSuccess) return e;
   }
+  if (D.n_snappy)
+    hipLaunchKernelGGL(k_snappy, dim3((uint32_t)D.n_sub), dim3(64), 0, s, D.subs, D.sub_status, D.sub_kind,
+                       (uint32_t)D.n_sub, D.tmp, D.sub_slot);
   if (D.n_blosclz)
     hipLaunchKernelGGL(k_blosclz, dim3((uint32_t)D.n_sub), dim3(64), 0, s, D.subs, D.sub_status, D.sub_kind,
                        (uint32_t)D.n_sub, D.tmp, D.sub_slot);

@@ -109,10 +109,11 @@ hipError_t launch_shard_encode(const uint64_t *starts, const uint8_t *array, con
 
 // blosc (c-blosc 1.x frames): stream table built on the device, sized on the host from BlInfo (first
 // execution of a plan) or from the capacities that execution recorded (later executions)
-enum : uint32_t { BL_COMP_BLOSCLZ = 0, BL_COMP_LZ4 = 1, BL_COMP_ZLIB = 3, BL_COMP_ZSTD = 4, BL_COMP_MEMCPY = 0x100,
+enum : uint32_t { BL_COMP_BLOSCLZ = 0, BL_COMP_LZ4 = 1, BL_COMP_SNAPPY = 2, BL_COMP_ZLIB = 3, BL_COMP_ZSTD = 4, BL_COMP_MEMCPY = 0x100,
                   BL_COMP_SKIP = 0xFFFFFFFFu };
 #define BL_SKIP 0x100u  // stream status: not (yet) decoded by the zstd pipeline / a stream decoder
-enum : uint32_t { BL_KIND_RAW = 0, BL_KIND_LZ4 = 1, BL_KIND_ZLIB = 3, BL_KIND_ZSTD = 4, BL_KIND_BLOSCLZ = 5 };
+enum : uint32_t { BL_KIND_RAW = 0, BL_KIND_LZ4 = 1, BL_KIND_SNAPPY = 2, BL_KIND_ZLIB = 3, BL_KIND_ZSTD = 4,
+                  BL_KIND_BLOSCLZ = 5 };
 struct BlInfo {     // per item (read back)
   uint32_t nsub;    // compressed streams
   uint32_t nblk;    // blocks
@@ -134,14 +135,14 @@ struct BlDecode {
   uint8_t *tmp;           // n_sub * sub_slot decoded streams
   uint64_t sub_slot;
   ZstdScratch zs;
-  uint64_t n_sub, n_blk, n_zstd, n_lz4, n_blosclz, n_zlib;  // with a cached layout: capacities (n_* > 0 = launched)
+  uint64_t n_sub, n_blk, n_zstd, n_lz4, n_blosclz, n_zlib, n_snappy;  // with a cached layout: capacities (n_* > 0 = launched)
   uint2 *zaux;            // zlib streams: {Adler-32 trailer, -} per stream
   unsigned long long *ovf;  // set by k_blosc_layout when a cached layout is too small (ctl counter)
 };
 // Capacities of a blosc stream table sized by an earlier execution of the same plan: the layout of
 // this execution is computed on the device (k_blosc_layout) and checked against them, so the stage
 // needs no host read-back. BL_KINDS_*: compressors the earlier execution launched decoders for.
-enum : uint32_t { BL_HAS_ZSTD = 1, BL_HAS_LZ4 = 2, BL_HAS_BLOSCLZ = 4, BL_HAS_ZLIB = 8 };
+enum : uint32_t { BL_HAS_ZSTD = 1, BL_HAS_LZ4 = 2, BL_HAS_BLOSCLZ = 4, BL_HAS_ZLIB = 8, BL_HAS_SNAPPY = 16 };
 struct BlCaps {
   uint64_t n_sub, n_blk, max_ne;
   uint32_t kinds;

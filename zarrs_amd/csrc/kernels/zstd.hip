@@ -2128,7 +2128,10 @@ __device__ __forceinline__ bool x_direct_block(uint32_t flags, uint32_t nseq, ui
 // Executor segments: an item's blocks are cut where no later match reaches back before the cut (and
 // not inside a checksummed frame); each segment gets its own k_zstd_exec_item wave. Byte-shuffled
 // images cut at their byte planes (tools/lab/zstd_taint.cpp: no match crosses the plane boundary).
-constexpr uint32_t XSEG = 4;
+#ifndef ZG_XSEG
+#define ZG_XSEG 4
+#endif
+constexpr uint32_t XSEG = ZG_XSEG;  // executor segments per item (at most)
 
 __global__ __launch_bounds__(64) void k_zstd_plan(const ZgItem *items, uint32_t *status, ZBlk *blks,
                                                   uint32_t blk_cap, const uint32_t *nblk, const uint32_t *zmode,

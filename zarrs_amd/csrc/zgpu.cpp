@@ -555,7 +555,8 @@ static void blosc_stage(zgpu_plan &P, const Stage &st, hipStream_t s) {
       exact.n_blk += hi[i].nblk;
       if (hi[i].nsub)
         exact.kinds |= hi[i].comp == BL_COMP_ZSTD ? BL_HAS_ZSTD : hi[i].comp == BL_COMP_LZ4 ? BL_HAS_LZ4
-                       : hi[i].comp == BL_COMP_BLOSCLZ ? BL_HAS_BLOSCLZ : hi[i].comp == BL_COMP_ZLIB ? BL_HAS_ZLIB : 0u;
+                       : hi[i].comp == BL_COMP_BLOSCLZ ? BL_HAS_BLOSCLZ : hi[i].comp == BL_COMP_ZLIB ? BL_HAS_ZLIB
+                       : hi[i].comp == BL_COMP_SNAPPY ? BL_HAS_SNAPPY : 0u;
       exact.max_ne = std::max<uint64_t>(exact.max_ne, hi[i].max_ne);
     }
     // capacities only grow (a plan whose inputs alternate between layouts settles on their maximum)
@@ -575,12 +576,13 @@ static void blosc_stage(zgpu_plan &P, const Stage &st, hipStream_t s) {
   D.n_lz4 = caps.kinds & BL_HAS_LZ4;
   D.n_blosclz = caps.kinds & BL_HAS_BLOSCLZ;
   D.n_zlib = caps.kinds & BL_HAS_ZLIB;
+  D.n_snappy = caps.kinds & BL_HAS_SNAPPY;
   const uint64_t ns = std::max<uint64_t>(D.n_sub, 1);
   D.subs = (ZgItem *)P.grow(P.bl_subs, ns * sizeof(ZgItem));
   D.sub_status = (uint32_t *)P.grow(P.bl_sub_status, ns * 4);
   D.sub_kind = (uint32_t *)P.grow(P.bl_sub_kind, ns * 4);
   D.blocks = (BlBlock *)P.grow(P.bl_blocks, std::max<uint64_t>(D.n_blk, 1) * sizeof(BlBlock));
-  if (D.n_zstd + D.n_lz4 + D.n_blosclz + D.n_zlib) {
+  if (D.n_zstd + D.n_lz4 + D.n_blosclz + D.n_zlib + D.n_snappy) {
     D.sub_slot = (caps.max_ne + 255) & ~(uint64_t)255;
     D.tmp = (uint8_t *)P.grow(P.bl_tmp, D.n_sub * D.sub_slot);
   }
