@@ -803,8 +803,10 @@ def run_gpu(args, rank, world, dev):
             continue
         arr = (L.ChunkDesc * n)(*descs)
         plan = C.c_void_p()
+        # plans run concurrently on lanes of their own stay on their lane's stream (ZGPU_ONE_STREAM)
+        one = L.ONE_STREAM if len(getattr(W, "lanes", [[0]])) > 1 and not args.serial_lanes else 0
         L.check(lib.zgpu_plan_create(chain._h, len(out_shape), arr, n, L.u64s(out_shape),
-                                     L.ENC_DEVICE | L.OUT_DEVICE, C.byref(plan)))
+                                     L.ENC_DEVICE | L.OUT_DEVICE | one, C.byref(plan)))
         part_plan[pi] = len(plans)
         plans.append((plan, out, (C.c_int32 * n)()))
     # stream lanes: lists of plans executed in order on one stream; lanes run concurrently

@@ -86,6 +86,9 @@ enum {
 #define ZGPU_OUT_DEVICE 0x2u  /* out is a device pointer (else host memory)                    */
 #define ZGPU_NO_VALIDATE 0x4u /* override: CodecOptions::validate_checksums = false for the call */
 #define ZGPU_DIRECT_IO 0x8u   /* filesystem reads: FilesystemStoreOptions::direct_io (O_DIRECT)   */
+#define ZGPU_ONE_STREAM 0x10u /* every kernel of the call on hip_stream (no internal side stream,
+                                 e.g. zstd's sequence decoder beside its literal decoder): for callers
+                                 that run independent plans concurrently on streams of their own   */
 
 typedef struct zgpu_ctx zgpu_ctx;
 typedef struct zgpu_chain zgpu_chain;

@@ -23,6 +23,8 @@ pub const ZGPU_ENC_DEVICE: u32 = 0x1;
 pub const ZGPU_OUT_DEVICE: u32 = 0x2;
 pub const ZGPU_NO_VALIDATE: u32 = 0x4;
 pub const ZGPU_DIRECT_IO: u32 = 0x8;
+/// Every kernel of the call on the caller's stream (no internal side stream).
+pub const ZGPU_ONE_STREAM: u32 = 0x10;
 
 #[repr(C)]
 pub struct zgpu_ctx {

@@ -67,6 +67,10 @@ struct ZstdScratch {
   uint32_t blk_cap;
   uint32_t force_serial = 0;               // every item on the serial one-wave decoder (tests, ZGPU_ZSTD_FORCE_SERIAL)
   unsigned long long *counters = nullptr;  // [serial-fallback items, block-parallel items] (nullable)
+  // Fork for the sequence decoder (nullable: one stream): k_zstd_blocks needs only the scan, so it
+  // runs on `side` beside the Huffman literal kernels and joins before k_zstd_plan
+  hipStream_t side = nullptr;
+  hipEvent_t ev_fork = nullptr, ev_join = nullptr;
 };
 void zstd_scratch_layout(uint64_t slot_bytes, uint32_t &blk_cap, uint64_t &blk_bytes, uint64_t &lit_stride,
                          uint64_t &seq_cap);

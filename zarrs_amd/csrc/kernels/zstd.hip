@@ -3096,16 +3096,33 @@ hipError_t launch_zstd(ZgItem *items, uint32_t *status, uint32_t n_items, uint8_
   }();
   const uint32_t grid = (uint32_t)std::min<uint64_t>(recs, g_cap);
   const uint32_t lgrid = (uint32_t)std::min<uint64_t>(recs, l_cap);
+  // the sequence decoder reads only the scan's block records and writes its own fields of them (and
+  // the sequence scratch): with a side stream it runs beside the literal kernels
+  const bool fork = Z.side && Z.ev_fork && Z.ev_join;
+  hipStream_t sq = fork ? Z.side : s;
+  if (fork) {
+    hipError_t e = hipEventRecord(Z.ev_fork, s);
+    if (e == hipSuccess) e = hipStreamWaitEvent(Z.side, Z.ev_fork, 0);
+    if (e != hipSuccess) return e;
+  }
+  // one resident wave of the sequence decoder: 256 CUs x 4 SIMDs x ZG_BLK_WPE waves
+  const uint32_t bgrid = (uint32_t)std::min<uint64_t>(recs, std::max<uint64_t>(g_cap, (uint64_t)256 * 4 * ZG_BLK_WPE));
+  hipLaunchKernelGGL(k_zstd_blocks, dim3(bgrid), dim3(64), 0, sq, items, status, blks, Z.blk_cap, Z.nblk, Z.mode,
+                     n_items, Z.lit, Z.lit_stride, Z.seq, Z.seq_cap);
+  if (fork) {
+    hipError_t e = hipEventRecord(Z.ev_join, Z.side);
+    if (e != hipSuccess) return e;
+  }
 #if ZG_HUF_SPLIT
   hipLaunchKernelGGL(k_zstd_huf, dim3(grid), dim3(64), 0, s, items, status, blks, Z.blk_cap, Z.nblk, Z.mode, n_items,
                      Z.lit, Z.lit_stride);
 #endif
   hipLaunchKernelGGL(k_zstd_lits, dim3(lgrid), dim3(LIT_THREADS), 0, s, items, status, blks, Z.blk_cap, Z.nblk,
                      Z.mode, n_items, Z.lit, Z.lit_stride);
-  // one resident wave of the sequence decoder: 256 CUs x 4 SIMDs x ZG_BLK_WPE waves
-  const uint32_t bgrid = (uint32_t)std::min<uint64_t>(recs, std::max<uint64_t>(g_cap, (uint64_t)256 * 4 * ZG_BLK_WPE));
-  hipLaunchKernelGGL(k_zstd_blocks, dim3(bgrid), dim3(64), 0, s, items, status, blks, Z.blk_cap, Z.nblk, Z.mode,
-                     n_items, Z.lit, Z.lit_stride, Z.seq, Z.seq_cap);
+  if (fork) {
+    hipError_t e = hipStreamWaitEvent(s, Z.ev_join, 0);
+    if (e != hipSuccess) return e;
+  }
   hipLaunchKernelGGL(k_zstd_plan, dim3(n_items), dim3(64), 0, s, items, status, blks, Z.blk_cap, Z.nblk, Z.mode,
                      slot_bytes);
   hipLaunchKernelGGL(k_zstd_direct, dim3(grid), dim3(256), 0, s, items, status, blks, Z.blk_cap, Z.nblk, Z.mode,

@@ -184,6 +184,26 @@ struct zgpu_plan {
   uint32_t *d_shard_status = nullptr;
   uint8_t *d_pool[2] = {nullptr, nullptr};
   ZstdScratch zs{};  // block-parallel zstd scratch (allocated when the chain has zstd)
+  // side stream of the zstd sequence decoder (created on first use with the priority of the stream
+  // the plan first runs on; ZGPU_ZSTD_FORK=0 keeps one stream)
+  hipStream_t zside = nullptr;
+  hipEvent_t zev[2] = {nullptr, nullptr};
+  void zstd_fork(ZstdScratch &Z, hipStream_t s) {
+    static const bool on = [] {
+      const char *e = std::getenv("ZGPU_ZSTD_FORK");
+      return !e || std::atoi(e) != 0;
+    }();
+    if (!on || (flags & ZGPU_ONE_STREAM)) return;
+    if (!zside) {
+      int prio = 0;
+      if (s) (void)hipStreamGetPriority(s, &prio);
+      HIPCHK(hipStreamCreateWithPriority(&zside, hipStreamNonBlocking, prio));
+      for (hipEvent_t &e : zev) HIPCHK(hipEventCreateWithFlags(&e, hipEventDisableTiming));
+    }
+    Z.side = zside;
+    Z.ev_fork = zev[0];
+    Z.ev_join = zev[1];
+  }
   // blosc stage scratch (grown on demand; the stream table is sized from the frame headers)
   struct Grow {
     void *p = nullptr;
@@ -220,6 +240,12 @@ struct zgpu_plan {
                     d_pool[0], d_pool[1], zs.blks, zs.nblk, zs.mode, zs.lit, zs.seq, d_ctl,
                     d_enc_stage};
     for (void *b : bufs) ctx->dev_free(b);
+    if (zside) {
+      (void)hipStreamSynchronize(zside);
+      (void)hipStreamDestroy(zside);
+    }
+    for (hipEvent_t e : zev)
+      if (e) (void)hipEventDestroy(e);
     for (Grow *g : {&bl_info, &bl_bases, &bl_subs, &bl_sub_status, &bl_sub_kind, &bl_blocks, &bl_tmp, &bl_zblks,
                     &bl_znblk, &bl_zmode, &bl_zlit, &bl_zseq, &bl_zaux})
       ctx->dev_free(g->p);
@@ -597,6 +623,7 @@ static void blosc_stage(zgpu_plan &P, const Stage &st, hipStream_t s) {
     D.zs.seq = (uint32_t *)P.grow(P.bl_zseq, D.n_sub * D.zs.seq_cap * 12);
     D.zs.counters = P.zs.counters;
     D.zs.force_serial = P.zs.force_serial;
+    P.zstd_fork(D.zs, s);
   }
   // the layout (bases, inert tails past this execution's totals) is always computed on the device
   HIPCHK(launch_blosc_layout(info, ni, d_bases, caps, D, s));
@@ -628,6 +655,7 @@ static void plan_enqueue(zgpu_plan &P, uint8_t *out, hipStream_t s) {
         HIPCHK(launch_gzip(P.d_items, P.d_status, ni, P.d_pool[st.pool], P.slot_bytes, s));
         break;
       case ST_ZSTD:
+        P.zstd_fork(P.zs, s);
         HIPCHK(launch_zstd(P.d_items, P.d_status, ni, P.d_pool[st.pool], P.slot_bytes, P.zs, s));
         break;
       case ST_BLOSC:
