@@ -2131,11 +2131,19 @@ __device__ __forceinline__ bool x_direct_block(uint32_t flags, uint32_t nseq, ui
 #ifndef ZG_XSEG
 #define ZG_XSEG 4
 #endif
-constexpr uint32_t XSEG = ZG_XSEG;  // executor segments per item (at most)
+#ifndef ZG_XSEG_MAX
+#define ZG_XSEG_MAX 16
+#endif
+// executor segments per item (at most): ZG_XSEG, raised for batches of few items up to one resident
+// wave of executors (ZG_XSEG_WAVES = 256 CUs x 8 waves) and ZG_XSEG_MAX (launch_zstd)
+constexpr uint32_t XSEG = ZG_XSEG;
+#ifndef ZG_XSEG_WAVES
+#define ZG_XSEG_WAVES 2048
+#endif
 
 __global__ __launch_bounds__(64) void k_zstd_plan(const ZgItem *items, uint32_t *status, ZBlk *blks,
                                                   uint32_t blk_cap, const uint32_t *nblk, const uint32_t *zmode,
-                                                  uint64_t slot_bytes) {
+                                                  uint64_t slot_bytes, uint32_t xseg) {
   const uint32_t item = blockIdx.x;
   if (zmode[item] != ZMODE_PARALLEL || status[item]) return;
   const int lane = lane_id();
@@ -2184,7 +2192,7 @@ __global__ __launch_bounds__(64) void k_zstd_plan(const ZgItem *items, uint32_t 
   }
   if (!err) {
     // valid cuts (backward: the least source position of the matches from the block on), then up to
-    // XSEG - 1 of them chosen forward at equal shares of the estimated execution cost
+    // xseg - 1 of them chosen forward at equal shares of the estimated execution cost
     uint64_t smin = ~0ull, total_w = 0, vmask = 0;  // vmask: lane l holds the cuts at blocks 64 l ..
     bool ck = false;
     const bool cuts = nb <= 64 * 64;
@@ -2213,7 +2221,7 @@ __global__ __launch_bounds__(64) void k_zstd_plan(const ZgItem *items, uint32_t 
         const uint32_t flags = U(B[bi].flags), type = flags & 3, nsq = U(B[bi].nseq), osz = U(B[bi].out_size);
         const uint64_t vm = (uint64_t)U(__builtin_amdgcn_readlane((uint32_t)vmask, (int)(bi >> 6))) |
                             ((uint64_t)U(__builtin_amdgcn_readlane((uint32_t)(vmask >> 32), (int)(bi >> 6))) << 32);
-        if (((vm >> (bi & 63)) & 1) && k < XSEG && acc * XSEG >= total_w * k) {
+        if (((vm >> (bi & 63)) & 1) && k < xseg && acc * xseg >= total_w * k) {
           seg = 1;
           k++;
         }
@@ -2848,9 +2856,9 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(ZG_XWPE, 8))
                                                        uint32_t blk_cap, const uint32_t *nblk, const uint32_t *zmode,
                                                        uint8_t *dst, uint64_t slot_bytes, const uint8_t *lit_scratch,
                                                        uint64_t lit_stride, const uint32_t *seq_scratch,
-                                                       uint64_t seq_cap) {
+                                                       uint64_t seq_cap, uint32_t xseg) {
   __shared__ ZXSmem S;
-  const uint32_t item = blockIdx.x / XSEG, sg = blockIdx.x % XSEG;
+  const uint32_t item = blockIdx.x / xseg, sg = blockIdx.x % xseg;
   const int lane = lane_id();
   ZP_DECL;
   ZP_T(t_all);
@@ -3123,12 +3131,20 @@ hipError_t launch_zstd(ZgItem *items, uint32_t *status, uint32_t n_items, uint8_
     hipError_t e = hipStreamWaitEvent(s, Z.ev_join, 0);
     if (e != hipSuccess) return e;
   }
+  // executor segments per item: ZG_XSEG, more for batches of few items (up to one resident wave of
+  // executors); ZGPU_ZSTD_XSEG fixes it (tuning)
+  static const uint32_t xseg_env = [] {
+    const char *e = std::getenv("ZGPU_ZSTD_XSEG");
+    return e ? (uint32_t)std::min<unsigned long>(64, std::max<unsigned long>(1, std::strtoul(e, nullptr, 10))) : 0u;
+  }();
+  const uint32_t xseg = xseg_env ? xseg_env
+                                 : (uint32_t)std::min<uint64_t>(ZG_XSEG_MAX, std::max<uint64_t>(XSEG, ZG_XSEG_WAVES / n_items));
   hipLaunchKernelGGL(k_zstd_plan, dim3(n_items), dim3(64), 0, s, items, status, blks, Z.blk_cap, Z.nblk, Z.mode,
-                     slot_bytes);
+                     slot_bytes, xseg);
   hipLaunchKernelGGL(k_zstd_direct, dim3(grid), dim3(256), 0, s, items, status, blks, Z.blk_cap, Z.nblk, Z.mode,
                      n_items, dst, slot_bytes, Z.lit, Z.lit_stride);
-  hipLaunchKernelGGL(k_zstd_exec_item, dim3(n_items * XSEG), dim3(64), 0, s, items, status, blks, Z.blk_cap, Z.nblk, Z.mode,
-                     dst, slot_bytes, Z.lit, Z.lit_stride, Z.seq, Z.seq_cap);
+  hipLaunchKernelGGL(k_zstd_exec_item, dim3(n_items * xseg), dim3(64), 0, s, items, status, blks, Z.blk_cap, Z.nblk,
+                     Z.mode, dst, slot_bytes, Z.lit, Z.lit_stride, Z.seq, Z.seq_cap, xseg);
   hipLaunchKernelGGL(k_zstd, dim3(n_items), dim3(64), 0, s, items, status, dst, slot_bytes, Z.lit, Z.lit_stride,
                      Z.mode);
   return hipGetLastError();
