@@ -2131,15 +2131,10 @@ __device__ __forceinline__ bool x_direct_block(uint32_t flags, uint32_t nseq, ui
 #ifndef ZG_XSEG
 #define ZG_XSEG 4
 #endif
-#ifndef ZG_XSEG_MAX
-#define ZG_XSEG_MAX 16
-#endif
-// executor segments per item (at most): ZG_XSEG, raised for batches of few items up to one resident
-// wave of executors (ZG_XSEG_WAVES = 256 CUs x 8 waves) and ZG_XSEG_MAX (launch_zstd)
+// executor segments per item (at most; ZGPU_ZSTD_XSEG overrides it at run time). C5 A/B
+// (profiles/r02_c5_lanes_xseg_ab.txt): 8 or 16 per item, or more only for batches of few items,
+// measured equal or slower
 constexpr uint32_t XSEG = ZG_XSEG;
-#ifndef ZG_XSEG_WAVES
-#define ZG_XSEG_WAVES 2048
-#endif
 
 __global__ __launch_bounds__(64) void k_zstd_plan(const ZgItem *items, uint32_t *status, ZBlk *blks,
                                                   uint32_t blk_cap, const uint32_t *nblk, const uint32_t *zmode,
@@ -3131,14 +3126,12 @@ hipError_t launch_zstd(ZgItem *items, uint32_t *status, uint32_t n_items, uint8_
     hipError_t e = hipStreamWaitEvent(s, Z.ev_join, 0);
     if (e != hipSuccess) return e;
   }
-  // executor segments per item: ZG_XSEG, more for batches of few items (up to one resident wave of
-  // executors); ZGPU_ZSTD_XSEG fixes it (tuning)
+  // executor segments per item: ZG_XSEG (ZGPU_ZSTD_XSEG: tuning)
   static const uint32_t xseg_env = [] {
     const char *e = std::getenv("ZGPU_ZSTD_XSEG");
     return e ? (uint32_t)std::min<unsigned long>(64, std::max<unsigned long>(1, std::strtoul(e, nullptr, 10))) : 0u;
   }();
-  const uint32_t xseg = xseg_env ? xseg_env
-                                 : (uint32_t)std::min<uint64_t>(ZG_XSEG_MAX, std::max<uint64_t>(XSEG, ZG_XSEG_WAVES / n_items));
+  const uint32_t xseg = xseg_env ? xseg_env : XSEG;
   hipLaunchKernelGGL(k_zstd_plan, dim3(n_items), dim3(64), 0, s, items, status, blks, Z.blk_cap, Z.nblk, Z.mode,
                      slot_bytes, xseg);
   hipLaunchKernelGGL(k_zstd_direct, dim3(grid), dim3(256), 0, s, items, status, blks, Z.blk_cap, Z.nblk, Z.mode,
