@@ -89,6 +89,9 @@ constexpr int LSUB = ZG_INFLATE_LSUB, DSUB = ZG_INFLATE_DSUB;
 #ifndef ZG_INFLATE_XDEP
 #define ZG_INFLATE_XDEP 1  // matches resolve by exact dependencies (0: first-pending frontier)
 #endif
+#ifndef ZG_INFLATE_RANGE
+#define ZG_INFLATE_RANGE 1  // a match's readiness: pending mask vs the index range of its source
+#endif
 #ifndef ZG_INFLATE_XW
 #define ZG_INFLATE_XW 8  // > 0: in-ring matches up to this many bytes copy through aligned ring words
 #endif
@@ -861,6 +864,24 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(ZG_INFLATE_W
       // copied by the whole wave one after another, short ones by their own lane.
       const int32_t s_rel = (int32_t)(msrc - pos);                   // source start, batch-relative
       const int32_t e_rel = s_rel + (int32_t)min(mlen, md);          // source end
+#if ZG_INFLATE_RANGE
+      // The symbols whose output overlaps the source are an index range [lo, hi] (output offsets
+      // are monotonic): hi = the last symbol starting before e_rel, lo = the last starting at or
+      // before s_rel; both found by one interleaved binary search per batch. A round then tests
+      // the pending mask against the range, with no LDS read.
+      if (mine) S.rbeg[lane] = (uint16_t)(mypos - pos);
+      __syncthreads();
+      int32_t hi = -1, lo = 0;
+      if (is_match && e_rel > 0) {
+        hi = 0;
+#pragma unroll
+        for (int32_t step = 32; step; step >>= 1) {
+          if (hi + step < (int32_t)cnt && (int32_t)S.rbeg[hi + step] < e_rel) hi += step;
+          if (lo + step < (int32_t)cnt && (int32_t)S.rbeg[lo + step] <= s_rel) lo += step;
+        }
+      }
+      const uint64_t rmask = hi < 0 ? 0ull : (hi >= 63 ? ~0ull : ((2ull << hi) - 1)) & ~((1ull << lo) - 1);
+#else
       if (mine) S.rend[lane] = (uint16_t)(mypos - pos + (is_match ? mlen : 1u));
       if (mine) S.rbeg[lane] = (uint16_t)(mypos - pos);
       __syncthreads();
@@ -871,6 +892,7 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(ZG_INFLATE_W
         for (int32_t step = 32; step; step >>= 1)
           if (hi + step < (int32_t)cnt && (int32_t)S.rbeg[hi + step] < e_rel) hi += step;
       }
+#endif
       bool pending = is_match;
       uint64_t pm;
       PROF_CNT(6, 1);
@@ -879,8 +901,12 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(ZG_INFLATE_W
         PROF_CNT(5, 1);
         bool ready = false;
         if (pending) {
+#if ZG_INFLATE_RANGE
+          ready = (pm & rmask) == 0;
+#else
           const uint64_t m = hi < 0 ? 0ull : pm & (hi >= 63 ? ~0ull : ((2ull << hi) - 1));
           ready = m == 0 || (int32_t)S.rend[63 - __builtin_clzll(m)] <= s_rel;
+#endif
         }
         const uint64_t lm = __ballot(ready && mlen > 32);
         if (lm) {  // the first long ready match, by the whole wave (the others wait a round)
