@@ -115,6 +115,25 @@ CHAINS = {
                                               {"name": "bytes", "configuration": {"endian": "big"}}],
         "index_codecs": [{"name": "bytes", "configuration": {"endian": "big"}}, {"name": "crc32c"}],
         "index_location": "start"}}], "int32"),
+    # transpose codecs before sharding_indexed: the shard and its inner grid are in the transposed frame
+    "transpose_then_sharded": ([{"name": "transpose", "configuration": {"order": [1, 2, 0]}},
+                                {"name": "sharding_indexed", "configuration": {
+        "chunk_shape": [8, 8, 4], "codecs": [{"name": "bytes", "configuration": {"endian": "little"}},
+                                             {"name": "crc32c"}],
+        "index_codecs": [{"name": "bytes", "configuration": {"endian": "little"}}, {"name": "crc32c"}],
+        "index_location": "end"}}], "float32"),
+    "transpose_then_sharded_inner_transpose_gzip": ([{"name": "transpose", "configuration": {"order": [2, 0, 1]}},
+                                                     {"name": "sharding_indexed", "configuration": {
+        "chunk_shape": [8, 8, 16], "codecs": [{"name": "transpose", "configuration": {"order": [1, 2, 0]}},
+                                              {"name": "bytes", "configuration": {"endian": "big"}},
+                                              {"name": "gzip", "configuration": {"level": 1}}],
+        "index_codecs": [{"name": "bytes", "configuration": {"endian": "little"}}],
+        "index_location": "start"}}], "int16"),
+    "transpose_keep_inner_then_sharded": ([{"name": "transpose", "configuration": {"order": [1, 0, 2]}},
+                                           {"name": "sharding_indexed", "configuration": {
+        "chunk_shape": [8, 16, 8], "codecs": [{"name": "bytes", "configuration": {"endian": "big"}}],
+        "index_codecs": [{"name": "bytes", "configuration": {"endian": "little"}}, {"name": "crc32c"}],
+        "index_location": "end"}}], "float64"),
 }
 
 

@@ -327,8 +327,18 @@ static void plan_build(zgpu_plan &P, const zgpu_chunk_desc *descs) {
   const uint32_t nd = P.nd;
   P.item_desc_status.assign(P.n_desc, 0);
   const bool shard_chain = top.a2b.kind == CodecKind::Sharding;
+  // transpose codecs before sharding_indexed (codec_chain.rs:557-646: the sharding codec decodes the
+  // transposed array): the shard and its inner chunk grid live in the encoded frame, encoded axis a
+  // <-> decoded axis mo[a]; descriptors are mapped into that frame and the scatter writes through
+  // output strides permuted back
+  uint32_t mo[ZG_MAXD];
+  for (uint32_t a = 0; a < nd; a++) mo[a] = a;
+  bool outer_perm = false;
   if (shard_chain) {
-    if (!top.a2a.empty()) throw ChainError{ZGPU_UNSUPPORTED, "array->array codecs before sharding_indexed"};
+    for (const Codec &k : top.a2a)
+      if (k.order.size() != nd) throw ChainError{ZGPU_INVALID_ARGUMENT, "transpose order rank != array rank"};
+    composed_axes(top, nd, mo);
+    for (uint32_t a = 0; a < nd; a++) outer_perm = outer_perm || mo[a] != a;
     if (top.a2b.inner->a2b.kind == CodecKind::Sharding) throw ChainError{ZGPU_UNSUPPORTED, "nested sharding"};
     if (!top.b2b.empty()) throw ChainError{ZGPU_UNSUPPORTED, "bytes->bytes codecs after sharding_indexed"};
     if (top.a2b.inner_shape.size() != nd) throw ChainError{ZGPU_INVALID_ARGUMENT, "sharding chunk_shape rank"};
@@ -397,11 +407,19 @@ static void plan_build(zgpu_plan &P, const zgpu_chunk_desc *descs) {
       for (uint32_t d = 0; d < nd; d++) max_sel[d] = std::max(max_sel[d], D.sel_shape[d]);
       continue;
     }
-    // sharded descriptor: one item per intersecting inner chunk
+    // sharded descriptor: one item per intersecting inner chunk, in the sharding codec's (encoded)
+    // frame: axis a is decoded axis mo[a]
+    uint64_t c_sh[ZG_MAXD], c_ss[ZG_MAXD], c_sz[ZG_MAXD], c_os[ZG_MAXD];
+    for (uint32_t a = 0; a < nd; a++) {
+      c_sh[a] = D.chunk_shape[mo[a]];
+      c_ss[a] = D.sel_start[mo[a]];
+      c_sz[a] = D.sel_shape[mo[a]];
+      c_os[a] = D.out_start[mo[a]];
+    }
     n_inner = 1;
     for (uint32_t d = 0; d < nd; d++) {
-      if (D.chunk_shape[d] % leaf_shape[d]) ok = false;
-      cps[d] = D.chunk_shape[d] / leaf_shape[d];
+      if (c_sh[d] % leaf_shape[d]) ok = false;
+      cps[d] = c_sh[d] / leaf_shape[d];
       n_inner *= cps[d];
     }
     if (!ok) {  // calculate_chunks_per_shard error (sharding.rs:136-154)
@@ -417,8 +435,8 @@ static void plan_build(zgpu_plan &P, const zgpu_chunk_desc *descs) {
     P.shards.push_back(ZgShard{(uint64_t)D.enc, D.enc ? D.enc_len : 0});
     uint64_t lo[ZG_MAXD], hi[ZG_MAXD], idx[ZG_MAXD];
     for (uint32_t d = 0; d < nd; d++) {
-      lo[d] = D.sel_start[d] / leaf_shape[d];
-      hi[d] = (D.sel_start[d] + D.sel_shape[d] - 1) / leaf_shape[d] + 1;
+      lo[d] = c_ss[d] / leaf_shape[d];
+      hi[d] = (c_ss[d] + c_sz[d] - 1) / leaf_shape[d] + 1;
       idx[d] = lo[d];
     }
     for (;;) {
@@ -431,10 +449,10 @@ static void plan_build(zgpu_plan &P, const zgpu_chunk_desc *descs) {
       for (uint32_t d = 0; d < nd; d++) {
         lin = lin * cps[d] + idx[d];
         const uint64_t cs = idx[d] * leaf_shape[d], ce = cs + leaf_shape[d];
-        const uint64_t s0 = std::max(D.sel_start[d], cs), s1 = std::min(D.sel_start[d] + D.sel_shape[d], ce);
+        const uint64_t s0 = std::max(c_ss[d], cs), s1 = std::min(c_ss[d] + c_sz[d], ce);
         g[d] = s0 - cs;
         g[nd + d] = s1 - s0;
-        g[2 * nd + d] = D.out_start[d] + (s0 - D.sel_start[d]);
+        g[2 * nd + d] = c_os[d] + (s0 - c_ss[d]);
         max_sel[d] = std::max(max_sel[d], s1 - s0);
       }
       it.inner = (uint32_t)lin;
@@ -489,7 +507,7 @@ static void plan_build(zgpu_plan &P, const zgpu_chunk_desc *descs) {
   for (uint32_t a = 0; a < nd; a++) S.enc_stride[m[a]] = est[a];
   for (uint32_t d = 0; d < nd; d++) {
     S.chunk_shape[d] = leaf_shape[d];
-    S.out_stride[d] = out_strides[d];
+    S.out_stride[d] = out_strides[mo[d]];
   }
   S.tile_a = m[nd - 1];
   S.tile_b = ZG_MAXD;
@@ -497,7 +515,9 @@ static void plan_build(zgpu_plan &P, const zgpu_chunk_desc *descs) {
     if (d == S.tile_a) continue;
     if (S.tile_b == ZG_MAXD || S.enc_stride[d] <= S.enc_stride[S.tile_b]) S.tile_b = d;
   }
-  if (S.tile_a == nd - 1) {
+  if (outer_perm && S.out_stride[nd - 1] != 1) {
+    P.scatter_mode = SCATTER_GENERIC;  // the row / tile kernels write unit-stride output rows
+  } else if (S.tile_a == nd - 1) {
     P.scatter_mode = SCATTER_ROWS;
   } else if (!S.shuffle && (S.es == 1 || S.es == 2 || S.es == 4 || S.es == 8)) {
     P.scatter_mode = SCATTER_TILED;
