@@ -134,6 +134,27 @@ CHAINS = {
         "chunk_shape": [8, 16, 8], "codecs": [{"name": "bytes", "configuration": {"endian": "big"}}],
         "index_codecs": [{"name": "bytes", "configuration": {"endian": "little"}}, {"name": "crc32c"}],
         "index_location": "end"}}], "float64"),
+    # nested sharding: [16,32,32] shards of [8,16,16] middle shards of [4,8,8] (or [8,4,16]) leaves
+    "nested_sharded_crc": ([{"name": "sharding_indexed", "configuration": {
+        "chunk_shape": [8, 16, 16],
+        "codecs": [{"name": "sharding_indexed", "configuration": {
+            "chunk_shape": [4, 8, 8], "codecs": [{"name": "bytes", "configuration": {"endian": "little"}},
+                                                 {"name": "crc32c"}],
+            "index_codecs": [{"name": "bytes", "configuration": {"endian": "little"}}, {"name": "crc32c"}],
+            "index_location": "end"}}],
+        "index_codecs": [{"name": "bytes", "configuration": {"endian": "little"}}, {"name": "crc32c"}],
+        "index_location": "end"}}], "float32"),
+    "nested_sharded_zstd_transpose": ([{"name": "transpose", "configuration": {"order": [2, 0, 1]}},
+                                       {"name": "sharding_indexed", "configuration": {
+        "chunk_shape": [16, 8, 16],
+        "codecs": [{"name": "sharding_indexed", "configuration": {
+            "chunk_shape": [8, 4, 16], "codecs": [{"name": "transpose", "configuration": {"order": [1, 0, 2]}},
+                                                  {"name": "bytes", "configuration": {"endian": "big"}},
+                                                  {"name": "zstd", "configuration": {"level": 1, "checksum": False}}],
+            "index_codecs": [{"name": "bytes", "configuration": {"endian": "big"}}],
+            "index_location": "start"}}],
+        "index_codecs": [{"name": "bytes", "configuration": {"endian": "little"}}, {"name": "crc32c"}],
+        "index_location": "start"}}], "uint16"),
 }
 
 
@@ -333,3 +354,46 @@ def test_retrieve_array_subset_multi_device(ctx, torch_cuda, out_dev):
     finally:
         for c in extra:
             c.close()
+
+
+def test_nested_sharding_fill_and_errors(ctx, torch_cuda):
+    """Nested sharding: an all-fill middle shard (an empty outer index entry) decodes to the fill
+    value; a corrupt middle-shard index fails with INVALID_CHECKSUM (middle indexes are verified like
+    the outer one, SH:178-194); an out-of-range middle index entry fails with SHARD_INDEX_OOB."""
+    from zarrs_amd import CodecChain, ZgpuError, make_desc
+    from zarrs_amd import _lib as L
+    codecs, dt = CHAINS["nested_sharded_crc"]
+    shape = [16, 32, 32]
+    rng = np.random.default_rng(11)
+    a = (rng.standard_normal(shape) * 100).astype(np.float32)
+    a[8:16, 0:16, 16:32] = 3  # middle shard (1, 0, 1): all fill -> omitted by the encoder
+    a[0:4, 0:8, 0:8] = 3      # a leaf of middle shard (0, 0, 0): all fill -> omitted
+    co = O.OracleChain.from_metadata(codecs, dt, 3, 3)
+    enc = co.encode(a)
+    n1 = 8  # middle shards per shard
+    idx = np.frombuffer(enc[len(enc) - 4 - 16 * n1:len(enc) - 4], "<u8").reshape(n1, 2)
+    assert tuple(idx[5]) == (2**64 - 1, 2**64 - 1)  # (1, 0, 1) in C order
+    ch = CodecChain.from_metadata(codecs, dt, 3, ctx)
+    for start, sub in (([0, 0, 0], shape), ([3, 5, 7], [11, 20, 22])):
+        out = np.zeros(sub, np.float32)
+        desc = make_desc(enc, shape, sel_start=start, sel_shape=sub)
+        assert ch.decode_batch([desc], out, sub, enc_device=False) == [0]
+        exp = a[tuple(slice(s, s + n) for s, n in zip(start, sub))]
+        assert out.tobytes() == exp.tobytes(), (start, sub)
+    # middle shard 0: its own index (8 entries + crc32c) sits at its end
+    off, nb = (int(x) for x in idx[0])
+    bad = bytearray(enc)
+    bad[off + nb - 10] ^= 0x40
+    with pytest.raises(ZgpuError) as ei:
+        ch.decode_batch([make_desc(bytes(bad), shape)], np.zeros(shape, np.float32), shape, enc_device=False)
+    assert ei.value.status == L.INVALID_CHECKSUM
+    # an outer index entry pointing past the shard -> SHARD_INDEX_OOB (the outer index crc is
+    # recomputed so only the range is wrong)
+    import zlib  # noqa: F401  (crc32c comes from the oracle)
+    bad2 = bytearray(enc)
+    ib = len(enc) - 4 - 16 * n1
+    bad2[ib:ib + 8] = (len(enc) + 100).to_bytes(8, "little")
+    bad2[len(enc) - 4:] = O.crc32c(bytes(bad2[ib:len(enc) - 4])).to_bytes(4, "little")
+    with pytest.raises(ZgpuError) as ei:
+        ch.decode_batch([make_desc(bytes(bad2), shape)], np.zeros(shape, np.float32), shape, enc_device=False)
+    assert ei.value.status == L.SHARD_INDEX_OOB

@@ -104,11 +104,12 @@ hipError_t launch_adler32_check(const ZgItem *subs, uint32_t *sub_status, const 
 
 // ------------------------------- shard index --------------------------------------------------
 __global__ __launch_bounds__(CRC_THREADS) void k_shard_index(const ZgShard *shards, ZgIndexSpec spec,
-                                                             uint64_t *index, uint32_t *shard_status) {
+                                                             uint64_t *index, uint32_t *shard_status, int keep_err) {
   __shared__ CrcTables T;
   __shared__ uint64_t s_len[CRC_THREADS / 64];
   __shared__ uint32_t s_crc[CRC_THREADS / 64];
   const uint32_t sh = blockIdx.x;
+  if (keep_err && shard_status[sh]) return;
   const ZgShard S = shards[sh];
   uint64_t *dst = index + (uint64_t)sh * spec.n_inner * 2;
   if (S.ptr == 0) {  // missing shard: every inner chunk is empty (fill)
@@ -147,9 +148,27 @@ __global__ __launch_bounds__(CRC_THREADS) void k_shard_index(const ZgShard *shar
 }
 
 hipError_t launch_shard_index(const ZgShard *shards, uint32_t n_shards, const ZgIndexSpec &spec,
-                              uint64_t *index, uint32_t *shard_status, hipStream_t s) {
+                              uint64_t *index, uint32_t *shard_status, int keep_err, hipStream_t s) {
   if (!n_shards) return hipSuccess;
-  hipLaunchKernelGGL(k_shard_index, dim3(n_shards), dim3(CRC_THREADS), 0, s, shards, spec, index, shard_status);
+  hipLaunchKernelGGL(k_shard_index, dim3(n_shards), dim3(CRC_THREADS), 0, s, shards, spec, index, shard_status,
+                     keep_err);
+  return hipGetLastError();
+}
+
+__global__ void k_mid_shards(const ZgItem *mids, const uint32_t *mid_status, uint32_t n, ZgShard *shards,
+                             uint32_t *shard_status) {
+  const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= n) return;
+  const ZgItem m = mids[i];
+  const uint32_t st = mid_status[i];
+  shard_status[i] = st;
+  shards[i] = (st || (m.flags & ZG_ITEM_FILL)) ? ZgShard{0, 0} : ZgShard{m.src, m.len};
+}
+
+hipError_t launch_mid_shards(const ZgItem *mids, const uint32_t *mid_status, uint32_t n, ZgShard *shards,
+                             uint32_t *shard_status, hipStream_t s) {
+  if (!n) return hipSuccess;
+  hipLaunchKernelGGL(k_mid_shards, dim3((n + 255) / 256), dim3(256), 0, s, mids, mid_status, n, shards, shard_status);
   return hipGetLastError();
 }
 

@@ -45,8 +45,13 @@ struct ZgIndexSpec {
   uint32_t crc_at_start[4];
   uint32_t verify;       // validate_checksums
 };
+// keep_err: shards whose status is already non-zero keep it and are skipped (nested sharding's
+// middle level, whose statuses come from resolving them through the outer index)
 hipError_t launch_shard_index(const ZgShard *shards, uint32_t n_shards, const ZgIndexSpec &spec,
-                              uint64_t *index, uint32_t *shard_status, hipStream_t s);
+                              uint64_t *index, uint32_t *shard_status, int keep_err, hipStream_t s);
+// nested sharding: resolved middle-shard records -> a shard table ({0,0} when empty) + statuses
+hipError_t launch_mid_shards(const ZgItem *mids, const uint32_t *mid_status, uint32_t n, ZgShard *shards,
+                             uint32_t *shard_status, hipStream_t s);
 hipError_t launch_item_resolve(ZgItem *items, uint32_t *status, uint32_t n_items, const ZgShard *shards,
                                const uint64_t *index, const uint32_t *shard_status, uint64_t n_inner,
                                unsigned long long *enc_bytes, hipStream_t s);

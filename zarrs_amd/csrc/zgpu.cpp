@@ -38,7 +38,7 @@ thread_local std::string g_last_error;
 // device counters in the plan's control block (u64 each, cleared per execute)
 enum { CTR_ENC_BYTES = 0, CTR_ZSTD_SERIAL = 1, CTR_ZSTD_PARALLEL = 2, CTR_BLOSC_RERUN = 3, CTR_N = 4 };
 // internal ctl slots (not reported): a cached blosc layout was outgrown (the execution is re-run)
-enum { CTR_BLOSC_OVF = 31 };
+enum { CTR_BLOSC_OVF = 31, CTR_SCRATCH = 30 };  // not reported (device-side flags / sinks)
 thread_local uint64_t g_last_counters[CTR_N];
 // UnexpectedChunkDecodedSize detail of the last call's first DECODED_SIZE_MISMATCH descriptor
 struct SizeDetail {
@@ -170,8 +170,9 @@ struct zgpu_plan {
   ZgScatter scatter{};
   uint32_t scatter_mode = SCATTER_GENERIC;
   uint64_t scatter_units = 0;
-  bool sharded = false;
-  ZgIndexSpec ispec{};
+  bool sharded = false, nested = false;
+  ZgIndexSpec ispec{}, ispec2{};  // ispec2: the middle shards' index (nested sharding)
+  std::vector<ZgItem> mids;       // nested: one record per intersecting middle shard
   uint64_t slot_bytes = 0;
   int n_pools = 0;
   uint64_t alg_bytes_static = 0;  // decoded bytes written + (unsharded) encoded bytes + index bytes
@@ -182,6 +183,12 @@ struct zgpu_plan {
   ZgShard *d_shards = nullptr;
   uint64_t *d_index = nullptr;
   uint32_t *d_shard_status = nullptr;
+  // nested sharding: middle shard records (resolved through the outer index each execution), their
+  // status, the middle shards as a shard table, and their decoded indexes
+  ZgItem *d_mids = nullptr, *d_mids_init = nullptr;
+  uint32_t *d_mid_status = nullptr, *d_shard_status2 = nullptr;
+  ZgShard *d_mid_shards = nullptr;
+  uint64_t *d_index2 = nullptr;
   uint8_t *d_pool[2] = {nullptr, nullptr};
   ZstdScratch zs{};  // block-parallel zstd scratch (allocated when the chain has zstd)
   // side stream of the zstd sequence decoder (created on first use with the priority of the stream
@@ -236,7 +243,8 @@ struct zgpu_plan {
 
   ~zgpu_plan() {
     if (!ctx) return;
-    void *bufs[] = {d_items, d_items_init, d_geom, d_shards, d_index, d_shard_status,
+    void *bufs[] = {d_items, d_items_init, d_geom, d_shards, d_index, d_shard_status, d_mids, d_mids_init,
+                    d_mid_status, d_shard_status2, d_mid_shards, d_index2,
                     d_pool[0], d_pool[1], zs.blks, zs.nblk, zs.mode, zs.lit, zs.seq, d_ctl,
                     d_enc_stage};
     for (void *b : bufs) ctx->dev_free(b);
@@ -339,20 +347,42 @@ static void plan_build(zgpu_plan &P, const zgpu_chunk_desc *descs) {
       if (k.order.size() != nd) throw ChainError{ZGPU_INVALID_ARGUMENT, "transpose order rank != array rank"};
     composed_axes(top, nd, mo);
     for (uint32_t a = 0; a < nd; a++) outer_perm = outer_perm || mo[a] != a;
-    if (top.a2b.inner->a2b.kind == CodecKind::Sharding) throw ChainError{ZGPU_UNSUPPORTED, "nested sharding"};
     if (!top.b2b.empty()) throw ChainError{ZGPU_UNSUPPORTED, "bytes->bytes codecs after sharding_indexed"};
     if (top.a2b.inner_shape.size() != nd) throw ChainError{ZGPU_INVALID_ARGUMENT, "sharding chunk_shape rank"};
   }
-  const Chain &leaf = shard_chain ? *top.a2b.inner : top;
+  // nested sharding (sharding.rs:107-126 nested_local_subchunk_grids): the outer shard's subchunks
+  // are shards themselves ("middle" shards); their indexes are decoded on the device after the outer
+  // index resolves them, and the leaf chunks resolve through the middle indexes
+  const Chain *mid = nullptr;
+  if (shard_chain && top.a2b.inner->a2b.kind == CodecKind::Sharding) {
+    mid = top.a2b.inner.get();
+    if (!mid->a2a.empty() || !mid->b2b.empty())
+      throw ChainError{ZGPU_UNSUPPORTED, "codecs around a nested sharding_indexed"};
+    if (mid->a2b.inner->a2b.kind == CodecKind::Sharding)
+      throw ChainError{ZGPU_UNSUPPORTED, "sharding_indexed nested more than two deep"};
+    if (mid->a2b.inner_shape.size() != nd) throw ChainError{ZGPU_INVALID_ARGUMENT, "sharding chunk_shape rank"};
+  }
+  const Chain &leaf = shard_chain ? (mid ? *mid->a2b.inner : *top.a2b.inner) : top;
   P.leaf = &leaf;
   P.sharded = shard_chain;
+  P.nested = mid != nullptr;
   for (const Codec &k : leaf.a2a)
     if (k.order.size() != nd) throw ChainError{ZGPU_INVALID_ARGUMENT, "transpose order rank != array rank"};
 
   // leaf chunk shape
   uint64_t leaf_shape[ZG_MAXD];
+  uint64_t mid_shape[ZG_MAXD], cps2[ZG_MAXD], n_inner2 = 1;  // nested: middle shard shape, its subchunks
   if (shard_chain) {
-    for (uint32_t d = 0; d < nd; d++) leaf_shape[d] = top.a2b.inner_shape[d];
+    for (uint32_t d = 0; d < nd; d++) leaf_shape[d] = (mid ? mid->a2b.inner_shape : top.a2b.inner_shape)[d];
+    for (uint32_t d = 0; d < nd; d++) mid_shape[d] = top.a2b.inner_shape[d];
+    if (mid) {
+      for (uint32_t d = 0; d < nd; d++) {
+        if (!leaf_shape[d] || mid_shape[d] % leaf_shape[d])
+          throw ChainError{ZGPU_INVALID_ARGUMENT, "nested sharding: subchunk shape does not divide the shard"};
+        cps2[d] = mid_shape[d] / leaf_shape[d];
+        n_inner2 *= cps2[d];
+      }
+    }
   } else if (P.n_desc) {
     for (uint32_t d = 0; d < nd; d++) leaf_shape[d] = descs[0].chunk_shape[d];
   } else {
@@ -416,10 +446,12 @@ static void plan_build(zgpu_plan &P, const zgpu_chunk_desc *descs) {
       c_sz[a] = D.sel_shape[mo[a]];
       c_os[a] = D.out_start[mo[a]];
     }
+    // subchunks of the (outer) shard: the leaf chunks, or the middle shards when nested
+    const uint64_t *sub_shape = mid ? mid_shape : leaf_shape;
     n_inner = 1;
     for (uint32_t d = 0; d < nd; d++) {
-      if (c_sh[d] % leaf_shape[d]) ok = false;
-      cps[d] = c_sh[d] / leaf_shape[d];
+      if (c_sh[d] % sub_shape[d]) ok = false;
+      cps[d] = c_sh[d] / sub_shape[d];
       n_inner *= cps[d];
     }
     if (!ok) {  // calculate_chunks_per_shard error (sharding.rs:136-154)
@@ -434,30 +466,77 @@ static void plan_build(zgpu_plan &P, const zgpu_chunk_desc *descs) {
     const uint32_t shard_slot = (uint32_t)P.shards.size();
     P.shards.push_back(ZgShard{(uint64_t)D.enc, D.enc ? D.enc_len : 0});
     uint64_t lo[ZG_MAXD], hi[ZG_MAXD], idx[ZG_MAXD];
+    // one leaf item per intersecting leaf chunk; `sub` (nested: the middle shard, its index slot,
+    // its selection [m0, m1) and output origin mo0) or the outer shard itself
+    auto add_leaves = [&](uint32_t slot, const uint64_t *m0, const uint64_t *m1, const uint64_t *mo0,
+                          const uint64_t *grid) {
+      uint64_t llo[ZG_MAXD], lhi[ZG_MAXD], li[ZG_MAXD];
+      for (uint32_t d = 0; d < nd; d++) {
+        llo[d] = m0[d] / leaf_shape[d];
+        lhi[d] = (m1[d] - 1) / leaf_shape[d] + 1;
+        li[d] = llo[d];
+      }
+      for (;;) {
+        uint64_t lin = 0;
+        ZgItem it{};
+        it.desc = (uint32_t)i;
+        it.shard = slot;
+        it.flags = D.enc ? (ZG_ITEM_SHARDED | (full ? 0u : ZG_ITEM_PARTIAL)) : ZG_ITEM_FILL;
+        uint64_t g[3 * ZG_MAXD];
+        for (uint32_t d = 0; d < nd; d++) {
+          lin = lin * grid[d] + li[d];
+          const uint64_t cs = li[d] * leaf_shape[d], ce = cs + leaf_shape[d];
+          const uint64_t s0 = std::max(m0[d], cs), s1 = std::min(m1[d], ce);
+          g[d] = s0 - cs;
+          g[nd + d] = s1 - s0;
+          g[2 * nd + d] = mo0[d] + (s0 - m0[d]);
+          max_sel[d] = std::max(max_sel[d], s1 - s0);
+        }
+        it.inner = (uint32_t)lin;
+        P.items.push_back(it);
+        P.geom.insert(P.geom.end(), g, g + 3 * nd);
+        int d = (int)nd - 1;
+        for (; d >= 0; d--) {
+          if (++li[d] < lhi[d]) break;
+          li[d] = llo[d];
+        }
+        if (d < 0) break;
+      }
+    };
+    if (!mid) {
+      uint64_t m1[ZG_MAXD];
+      for (uint32_t d = 0; d < nd; d++) m1[d] = c_ss[d] + c_sz[d];
+      add_leaves(shard_slot, c_ss, m1, c_os, cps);
+      continue;
+    }
+    if (P.ispec2.n_inner && P.ispec2.n_inner != n_inner2) {
+      P.item_desc_status[i] = ZGPU_UNSUPPORTED;
+      continue;
+    }
+    P.ispec2.n_inner = n_inner2;
     for (uint32_t d = 0; d < nd; d++) {
-      lo[d] = c_ss[d] / leaf_shape[d];
-      hi[d] = (c_ss[d] + c_sz[d] - 1) / leaf_shape[d] + 1;
+      lo[d] = c_ss[d] / mid_shape[d];
+      hi[d] = (c_ss[d] + c_sz[d] - 1) / mid_shape[d] + 1;
       idx[d] = lo[d];
     }
-    for (;;) {
-      uint64_t lin = 0;
-      ZgItem it{};
-      it.desc = (uint32_t)i;
-      it.shard = shard_slot;
-      it.flags = D.enc ? (ZG_ITEM_SHARDED | (full ? 0u : ZG_ITEM_PARTIAL)) : ZG_ITEM_FILL;
-      uint64_t g[3 * ZG_MAXD];
+    for (;;) {  // every intersecting middle shard: an index slot, then its leaf chunks
+      uint64_t lin = 0, m0[ZG_MAXD], m1[ZG_MAXD], mo0[ZG_MAXD];
       for (uint32_t d = 0; d < nd; d++) {
         lin = lin * cps[d] + idx[d];
-        const uint64_t cs = idx[d] * leaf_shape[d], ce = cs + leaf_shape[d];
+        const uint64_t cs = idx[d] * mid_shape[d], ce = cs + mid_shape[d];
         const uint64_t s0 = std::max(c_ss[d], cs), s1 = std::min(c_ss[d] + c_sz[d], ce);
-        g[d] = s0 - cs;
-        g[nd + d] = s1 - s0;
-        g[2 * nd + d] = c_os[d] + (s0 - c_ss[d]);
-        max_sel[d] = std::max(max_sel[d], s1 - s0);
+        m0[d] = s0 - cs;
+        m1[d] = s1 - cs;
+        mo0[d] = c_os[d] + (s0 - c_ss[d]);
       }
-      it.inner = (uint32_t)lin;
-      P.items.push_back(it);
-      P.geom.insert(P.geom.end(), g, g + 3 * nd);
+      const uint32_t mslot = (uint32_t)P.mids.size();
+      ZgItem mi{};
+      mi.desc = (uint32_t)i;
+      mi.shard = shard_slot;
+      mi.inner = (uint32_t)lin;
+      mi.flags = D.enc ? ZG_ITEM_SHARDED : ZG_ITEM_FILL;
+      P.mids.push_back(mi);
+      add_leaves(mslot, m0, m1, mo0, cps2);
       int d = (int)nd - 1;
       for (; d >= 0; d--) {
         if (++idx[d] < hi[d]) break;
@@ -483,6 +562,23 @@ static void plan_build(zgpu_plan &P, const zgpu_chunk_desc *descs) {
     P.ispec.verify = P.validate;
     for (const ZgShard &sh : P.shards)
       if (sh.ptr) P.alg_bytes_static += P.ispec.index_bytes;
+    if (mid) {
+      const Chain &xc2 = *mid->a2b.index;
+      if (xc2.a2b.kind != CodecKind::Bytes || !xc2.a2a.empty())
+        throw ChainError{ZGPU_UNSUPPORTED, "index_codecs must be bytes (+crc32c)"};
+      for (const Codec &k : xc2.b2b)
+        if (k.kind != CodecKind::Crc32c) throw ChainError{ZGPU_UNSUPPORTED, "index_codecs must be bytes (+crc32c)"};
+      if (xc2.b2b.size() > 4) throw ChainError{ZGPU_UNSUPPORTED, "too many index crc32c codecs"};
+      P.ispec2.n_inner = n_inner2;
+      P.ispec2.index_bytes = (uint64_t)chain_fixed_encoded_size(xc2, n_inner2 * 2);
+      P.ispec2.at_start = mid->a2b.at_start;
+      P.ispec2.big_endian = xc2.a2b.big_endian;
+      P.ispec2.n_crc = (uint32_t)xc2.b2b.size();
+      for (size_t k = 0; k < xc2.b2b.size(); k++) P.ispec2.crc_at_start[k] = xc2.b2b[k].at_start;
+      P.ispec2.verify = P.validate;
+      for (const ZgItem &m : P.mids)
+        if (!(m.flags & ZG_ITEM_FILL)) P.alg_bytes_static += P.ispec2.index_bytes;
+    }
   }
 
   build_leaf_stages(P, leaf, nelem);
@@ -563,6 +659,16 @@ static void plan_upload(zgpu_plan &P, hipStream_t us = nullptr) {
     P.d_shard_status = (uint32_t *)C.dev_alloc(P.shards.size() * 4);
     HIPCHK(hipMemcpyAsync(P.d_shards, P.shards.data(), P.shards.size() * sizeof(ZgShard), hipMemcpyHostToDevice,
                           us));
+  }
+  if (!P.mids.empty()) {
+    const size_t nm = P.mids.size();
+    P.d_mids = (ZgItem *)C.dev_alloc(nm * sizeof(ZgItem));
+    P.d_mids_init = (ZgItem *)C.dev_alloc(nm * sizeof(ZgItem));
+    P.d_mid_status = (uint32_t *)C.dev_alloc(nm * 4);
+    P.d_shard_status2 = (uint32_t *)C.dev_alloc(nm * 4);
+    P.d_mid_shards = (ZgShard *)C.dev_alloc(nm * sizeof(ZgShard));
+    P.d_index2 = (uint64_t *)C.dev_alloc(nm * P.ispec2.n_inner * 16);
+    HIPCHK(hipMemcpyAsync(P.d_mids_init, P.mids.data(), nm * sizeof(ZgItem), hipMemcpyHostToDevice, us));
   }
 }
 
@@ -662,9 +768,23 @@ static void plan_enqueue(zgpu_plan &P, uint8_t *out, hipStream_t s) {
   if (mutates)
     HIPCHK(hipMemcpyAsync(P.d_items, P.d_items_init, ni * sizeof(ZgItem), hipMemcpyDeviceToDevice, s));
   if (P.sharded) {
-    HIPCHK(launch_shard_index(P.d_shards, (uint32_t)P.shards.size(), P.ispec, P.d_index, P.d_shard_status, s));
-    HIPCHK(launch_item_resolve(P.d_items, P.d_status, ni, P.d_shards, P.d_index, P.d_shard_status, P.ispec.n_inner,
-                               P.d_counter, s));
+    HIPCHK(launch_shard_index(P.d_shards, (uint32_t)P.shards.size(), P.ispec, P.d_index, P.d_shard_status, 0, s));
+    if (P.nested && !P.mids.empty()) {
+      // middle shards: resolved through the outer index, their indexes decoded, then the leaves
+      // resolve through them (a middle-shard error reaches every leaf of it via its status)
+      const uint32_t nm = (uint32_t)P.mids.size();
+      HIPCHK(hipMemcpyAsync(P.d_mids, P.d_mids_init, nm * sizeof(ZgItem), hipMemcpyDeviceToDevice, s));
+      HIPCHK(hipMemsetAsync(P.d_mid_status, 0, nm * 4, s));
+      HIPCHK(launch_item_resolve(P.d_mids, P.d_mid_status, nm, P.d_shards, P.d_index, P.d_shard_status,
+                                 P.ispec.n_inner, P.d_counter + CTR_SCRATCH, s));
+      HIPCHK(launch_mid_shards(P.d_mids, P.d_mid_status, nm, P.d_mid_shards, P.d_shard_status2, s));
+      HIPCHK(launch_shard_index(P.d_mid_shards, nm, P.ispec2, P.d_index2, P.d_shard_status2, 1, s));
+      HIPCHK(launch_item_resolve(P.d_items, P.d_status, ni, P.d_mid_shards, P.d_index2, P.d_shard_status2,
+                                 P.ispec2.n_inner, P.d_counter + CTR_ENC_BYTES, s));
+    } else if (!P.nested) {
+      HIPCHK(launch_item_resolve(P.d_items, P.d_status, ni, P.d_shards, P.d_index, P.d_shard_status, P.ispec.n_inner,
+                                 P.d_counter, s));
+    }
   }
   for (const Stage &st : P.stages) {
     switch (st.kind) {
