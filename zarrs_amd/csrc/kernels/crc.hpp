@@ -72,9 +72,9 @@ __device__ inline void build_tables(CrcTables &T, uint32_t poly) {
   __syncthreads();
 }
 
-// Standard CRC (init/xorout 0xFFFFFFFF) of a short segment.
-__device__ __forceinline__ uint32_t crc_segment(const uint8_t *p, uint64_t n, const CrcTables &T) {
-  uint32_t c = 0xFFFFFFFFu;
+// The running (pre-inversion) CRC state c advanced over p[0..n): crc_segment = ~crc_run(~0, ...), and
+// a segment split into pieces is one run over them.
+__device__ __forceinline__ uint32_t crc_run(uint32_t c, const uint8_t *p, uint64_t n, const CrcTables &T) {
   while (n && ((uintptr_t)p & 3)) {
     c = (c >> 8) ^ T.t[0][(c ^ *p++) & 0xff];
     n--;
@@ -108,19 +108,19 @@ __device__ __forceinline__ uint32_t crc_segment(const uint8_t *p, uint64_t n, co
     n -= 4;
   }
   while (n--) c = (c >> 8) ^ T.t[0][(c ^ *p++) & 0xff];
-  return ~c;
+  return c;
 }
 
-// Workgroup-wide CRC of p[0..n): every thread returns the same value.
-__device__ inline uint32_t wg_crc(const uint8_t *p, uint64_t n, const CrcTables &T, uint32_t poly, uint64_t *s_len,
-                           uint32_t *s_crc) {
+// Standard CRC (init/xorout 0xFFFFFFFF) of a short segment.
+__device__ __forceinline__ uint32_t crc_segment(const uint8_t *p, uint64_t n, const CrcTables &T) {
+  return ~crc_run(0xFFFFFFFFu, p, n, T);
+}
+
+// Workgroup-wide merge of each thread's CRC c of its contiguous segment of l bytes (segments in thread
+// order): every thread returns the CRC of the concatenation.
+__device__ inline uint32_t wg_crc_merge(uint32_t c, uint64_t l, const CrcTables &T, uint32_t poly, uint64_t *s_len,
+                                        uint32_t *s_crc) {
   const uint32_t tid = threadIdx.x, nt = blockDim.x;
-  // segments aligned to 16 bytes so the inner loop runs on 16-B loads
-  uint64_t seg = (n + nt - 1) / nt;
-  seg = (seg + 15) & ~(uint64_t)15;
-  const uint64_t b0 = min<uint64_t>((uint64_t)tid * seg, n), b1 = min<uint64_t>(b0 + seg, n);
-  uint32_t c = crc_segment(p + b0, b1 - b0, T);
-  uint64_t l = b1 - b0;
   // tree merge: lane pairs within the wave, then waves through LDS
   for (int off = 1; off < 64; off <<= 1) {
     const uint32_t c2 = __shfl_down(c, off, 64);
@@ -145,6 +145,17 @@ __device__ inline uint32_t wg_crc(const uint8_t *p, uint64_t n, const CrcTables 
   const uint32_t r = s_crc[0];
   __syncthreads();
   return r;
+}
+
+// Workgroup-wide CRC of p[0..n): every thread returns the same value.
+__device__ inline uint32_t wg_crc(const uint8_t *p, uint64_t n, const CrcTables &T, uint32_t poly, uint64_t *s_len,
+                                  uint32_t *s_crc) {
+  const uint32_t tid = threadIdx.x, nt = blockDim.x;
+  // segments aligned to 16 bytes so the inner loop runs on 16-B loads
+  uint64_t seg = (n + nt - 1) / nt;
+  seg = (seg + 15) & ~(uint64_t)15;
+  const uint64_t b0 = min<uint64_t>((uint64_t)tid * seg, n), b1 = min<uint64_t>(b0 + seg, n);
+  return wg_crc_merge(crc_segment(p + b0, b1 - b0, T), b1 - b0, T, poly, s_len, s_crc);
 }
 
 }  // namespace zgpu
