@@ -26,10 +26,10 @@
 //  * Decoded symbols (up to 64 per batch, one per lane) are then executed in parallel:
 //    a wave prefix sum places them, literals are written at once, matches resolve in rounds by exact
 //    dependencies (a long match copied by all lanes: out[p+i] = out[p-d+(i mod d)], so overlapping
-//    copies need no serialisation), through a 2 KiB LDS ring that holds the recent output; sources
+//    copies need no serialisation), through a 1 KiB LDS ring that holds the recent output; sources
 //    older than the ring come from the flushed output in HBM. The ring is flushed to the item's slot
 //    with 16-byte stores.
-//  * LDS per stream is 8 KiB (ring 2 KiB, tables 4.6 KiB; the header scratch shares its space with
+//  * LDS per stream is 7.0 KiB (ring 1 KiB, tables 4.6 KiB; the header scratch shares its space with
 //    the batch records) and the kernel is held at 96 VGPRs: 5 streams per SIMD.
 #include <hip/hip_runtime.h>
 
@@ -59,10 +59,12 @@ __device__ unsigned long long g_prof[8];
 namespace {
 
 #ifndef ZG_INFLATE_RING
-#define ZG_INFLATE_RING 2048
+#define ZG_INFLATE_RING 1024
 #endif
-// LDS ring of recent output (power of two). Small on purpose: LDS per wave sets how many streams a
-// CU decodes at once, and sources older than the ring are read back from the flushed output.
+// LDS ring of recent output (power of two). Small on purpose: sources older than the ring are read
+// back from the flushed output (L2-resident), and a 1 KiB ring (512-B batches, 256-B flushes)
+// measured faster than 2 KiB (42.5 -> 39.5 ms) and 512 B (40.5 ms) on C3 chunks at the same 5 waves
+// per SIMD (profiles/r02_gzip_lab_ring_ab.txt).
 constexpr int RING = ZG_INFLATE_RING;
 constexpr int RMASK = RING - 1;
 constexpr int BATCH_CAP = RING / 2;  // max output bytes decoded into one batch
