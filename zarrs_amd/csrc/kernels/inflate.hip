@@ -69,8 +69,10 @@ constexpr int RING = ZG_INFLATE_RING;
 constexpr int RMASK = RING - 1;
 constexpr int BATCH_CAP = RING / 2;  // max output bytes decoded into one batch
 constexpr int FLUSH_MIN = RING / 4;  // flush the ring to the slot once this many bytes are pending
-// unflushed bytes stay below FLUSH_MIN + BATCH_CAP + 258 < RING: every source older than the ring
-// has been flushed
+// Unflushed bytes never exceed the ring: fewer than FLUSH_MIN before a batch, and a batch takes
+// symbols while it holds fewer than BATCH_CAP bytes, the last one a match of at most 258. So every
+// source older than the ring has been flushed, and no unflushed byte is overwritten.
+static_assert((FLUSH_MIN - 1) + (BATCH_CAP - 1) + 258 <= RING, "gzip ring: unflushed bytes must fit it");
 #ifndef ZG_INFLATE_LROOT
 #define ZG_INFLATE_LROOT 9
 #endif
