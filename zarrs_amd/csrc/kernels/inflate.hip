@@ -67,8 +67,14 @@ namespace {
 // per SIMD (profiles/r02_gzip_lab_ring_ab.txt).
 constexpr int RING = ZG_INFLATE_RING;
 constexpr int RMASK = RING - 1;
-constexpr int BATCH_CAP = RING / 2;  // max output bytes decoded into one batch
-constexpr int FLUSH_MIN = RING / 4;  // flush the ring to the slot once this many bytes are pending
+#ifndef ZG_INFLATE_BATCH_CAP
+#define ZG_INFLATE_BATCH_CAP (RING / 2)
+#endif
+#ifndef ZG_INFLATE_FLUSH_MIN
+#define ZG_INFLATE_FLUSH_MIN (RING / 4)
+#endif
+constexpr int BATCH_CAP = ZG_INFLATE_BATCH_CAP;  // a batch takes symbols while it holds fewer bytes
+constexpr int FLUSH_MIN = ZG_INFLATE_FLUSH_MIN;  // flush the ring to the slot once this many are pending
 // Unflushed bytes never exceed the ring: fewer than FLUSH_MIN before a batch, and a batch takes
 // symbols while it holds fewer than BATCH_CAP bytes, the last one a match of at most 258. So every
 // source older than the ring has been flushed, and no unflushed byte is overwritten.
