@@ -14,6 +14,17 @@ constexpr uint32_t POLY_CRC32C = 0x82F63B78u;  // reflected Castagnoli (crc32c c
 constexpr uint32_t POLY_CRC32 = 0xEDB88320u;   // reflected IEEE (gzip trailer, RFC 1952)
 constexpr int CRC_THREADS = 256;
 
+static __constant__ uint32_t c_x2n_crc32c[32] = {
+    0x40000000u, 0x20000000u, 0x08000000u, 0x00800000u, 0x00008000u, 0x82F63B78u, 0x6EA2D55Cu, 0x18B8EA18u,
+    0x510AC59Au, 0xB82BE955u, 0xB8FDB1E7u, 0x88E56F72u, 0x74C360A4u, 0xE4172B16u, 0x0D65762Au, 0x35D73A62u,
+    0x28461564u, 0xBF455269u, 0xE2EA32DCu, 0xFE7740E6u, 0xF946610Bu, 0x3C204F8Fu, 0x538586E3u, 0x59726915u,
+    0x734D5309u, 0xBC1AC763u, 0x7D0722CCu, 0xD289CABEu, 0xE94CA9BCu, 0x05B74F3Fu, 0xA51E1F42u, 0x40000000u};
+static __constant__ uint32_t c_x2n_crc32[32] = {
+    0x40000000u, 0x20000000u, 0x08000000u, 0x00800000u, 0x00008000u, 0xEDB88320u, 0xB1E6B092u, 0xA06A2517u,
+    0xED627DAEu, 0x88D14467u, 0xD7BBFE6Au, 0xEC447F11u, 0x8E7EA170u, 0x6427800Eu, 0x4D47BAE0u, 0x09FE548Fu,
+    0x83852D0Fu, 0x30362F1Au, 0x7B5A9CC3u, 0x31FEC169u, 0x9FEC022Au, 0x6C8DEDC4u, 0x15D6874Du, 0x5FDE7A4Eu,
+    0xBAD90E37u, 0x2E4E5EEFu, 0x4EABA214u, 0xA8A472C0u, 0x429A969Eu, 0x148D302Au, 0xC40BA6D0u, 0xC4E22C3Cu};
+
 struct CrcTables {
   uint32_t t[4][256];  // slice-by-4
   uint32_t x2n[32];    // x^(2^k) mod P
@@ -64,11 +75,9 @@ __device__ inline void build_tables(CrcTables &T, uint32_t poly) {
       T.t[s][i] = c;
     }
   }
-  if (threadIdx.x == 0) {
-    uint32_t p = 1u << 30;  // x^1
-    T.x2n[0] = p;
-    for (int n = 1; n < 32; n++) T.x2n[n] = p = multmodp(p, p, poly);
-  }
+  // x^(2^k) mod P: precomputed (zlib's x2n_table for the IEEE polynomial; the same recurrence,
+  // p(0) = x^1, p(k+1) = p(k)^2 mod P, for Castagnoli) — thread 0 used to square 31 times per workgroup
+  if (threadIdx.x < 32) T.x2n[threadIdx.x] = poly == POLY_CRC32C ? c_x2n_crc32c[threadIdx.x] : c_x2n_crc32[threadIdx.x];
   __syncthreads();
 }
 
