@@ -84,6 +84,22 @@ def test_synthetic_golden(case):
                                              {"name": "gzip", "configuration": {"level": 1}}],
         "index_codecs": [{"name": "bytes", "configuration": {"endian": "little"}}, {"name": "crc32c"}],
         "index_location": "start"}}], "uint32"),
+    # transpose before sharding, and nested sharding (the GPU parity tests' expected values)
+    ([{"name": "transpose", "configuration": {"order": [1, 2, 0]}},
+      {"name": "sharding_indexed", "configuration": {
+          "chunk_shape": [3, 4, 2], "codecs": [{"name": "bytes", "configuration": {"endian": "little"}},
+                                               {"name": "crc32c"}],
+          "index_codecs": [{"name": "bytes", "configuration": {"endian": "little"}}, {"name": "crc32c"}],
+          "index_location": "end"}}], "float32"),
+    ([{"name": "sharding_indexed", "configuration": {
+        "chunk_shape": [2, 6, 4],
+        "codecs": [{"name": "sharding_indexed", "configuration": {
+            "chunk_shape": [2, 3, 2], "codecs": [{"name": "bytes", "configuration": {"endian": "big"}},
+                                                 {"name": "zstd", "configuration": {"level": 1, "checksum": False}}],
+            "index_codecs": [{"name": "bytes", "configuration": {"endian": "big"}}],
+            "index_location": "start"}}],
+        "index_codecs": [{"name": "bytes", "configuration": {"endian": "little"}}, {"name": "crc32c"}],
+        "index_location": "end"}}], "int32"),
 ])
 def test_oracle_roundtrip(codecs, dt):
     rng = np.random.default_rng(1)
