@@ -112,7 +112,7 @@ constexpr int LSUB = ZG_INFLATE_LSUB, DSUB = ZG_INFLATE_DSUB;
 #define ZG_INFLATE_PJ 1  // chain a window's symbols by pointer jumping (0: scalar walk)
 #endif
 #ifndef ZG_INFLATE_PJL
-#define ZG_INFLATE_PJL 3  // pointer-jumping doublings: a window chains up to 2^(PJL+1) symbols
+#define ZG_INFLATE_PJL 2  // pointer-jumping doublings: a window chains up to 2^(PJL+1) symbols
 #endif
 
 // table entry: bits 0-3 code length (0 = longer than the root: slow path), 4-5 kind,
