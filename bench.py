@@ -775,7 +775,14 @@ class BloscZstd(Blosc):
     CNAME = "zstd"
 
 
-WORKLOADS = {"c1": C1, "c2": C2, "c3": C3, "c5": C5, "blosc": Blosc, "blosc-zstd": BloscZstd}
+class BloscLZ(Blosc):
+    """Same volume, blosc{blosclz, clevel 5, shuffle}: c-blosc's default compressor, the one zarrs'
+    own blosc benchmark uses (zarrs/benches/codecs.rs:52)."""
+    CNAME = "blosclz"
+
+
+WORKLOADS = {"c1": C1, "c2": C2, "c3": C3, "c5": C5, "blosc": Blosc, "blosc-zstd": BloscZstd,
+             "blosc-blosclz": BloscLZ}
 
 
 def _time_reps(fn, seconds):
