@@ -536,6 +536,52 @@ __global__ __launch_bounds__(256) void k_blosc_finish(const BlBlock *blocks, con
     const uint32_t j = ne ? q / ne : 0;
     return ((const uint8_t *)src[j])[q - j * ne];
   };
+  if (B.mode == 1 && (ts == 2 || ts == 4) && ne && bsize % (16 * ts) == 0 && ((uintptr_t)out & 15) == 0) {
+    // u16 / u32 fast path: 16 elements per thread, a 16-B load from each byte plane and ts 16-B
+    // stores of the interleaved bytes (the generic loop below moves a byte per lane with two
+    // integer divisions); planes that are not 16-B aligned (stored streams inside the frame) fall
+    // through to the generic loop
+    const uint32_t neb = bsize / ts;
+    const uint4 *pl[4];
+    bool al = true;
+    for (uint32_t i = 0; i < ts; i++) {
+      const uint32_t q = i * neb, j = q / ne;
+      pl[i] = (const uint4 *)((const uint8_t *)src[j] + (q - j * ne));
+      al = al && ((uintptr_t)pl[i] & 15) == 0;
+    }
+    if (al) {
+      uint4 *o = (uint4 *)out;
+      for (uint32_t v = threadIdx.x; v < neb / 16; v += 256) {
+        if (ts == 2) {
+          const uint4 a = pl[0][v], b = pl[1][v];
+          const uint32_t aw[4] = {a.x, a.y, a.z, a.w}, bw[4] = {b.x, b.y, b.z, b.w};
+          uint32_t r[8];
+#pragma unroll
+          for (int k = 0; k < 4; k++) {
+            r[2 * k] = (aw[k] & 0xffu) | ((bw[k] & 0xffu) << 8) | ((aw[k] & 0xff00u) << 8) | ((bw[k] & 0xff00u) << 16);
+            r[2 * k + 1] = ((aw[k] >> 16) & 0xffu) | (((bw[k] >> 16) & 0xffu) << 8) | ((aw[k] >> 24) << 16) |
+                           ((bw[k] >> 24) << 24);
+          }
+          o[2 * v] = make_uint4(r[0], r[1], r[2], r[3]);
+          o[2 * v + 1] = make_uint4(r[4], r[5], r[6], r[7]);
+        } else {
+          const uint4 p0 = pl[0][v], p1 = pl[1][v], p2 = pl[2][v], p3 = pl[3][v];
+          const uint32_t w0[4] = {p0.x, p0.y, p0.z, p0.w}, w1[4] = {p1.x, p1.y, p1.z, p1.w},
+                         w2[4] = {p2.x, p2.y, p2.z, p2.w}, w3[4] = {p3.x, p3.y, p3.z, p3.w};
+#pragma unroll
+          for (int k = 0; k < 4; k++) {  // output word e of element group k: byte e of each plane
+            uint32_t r[4];
+#pragma unroll
+            for (int e = 0; e < 4; e++)
+              r[e] = ((w0[k] >> (8 * e)) & 0xffu) | (((w1[k] >> (8 * e)) & 0xffu) << 8) |
+                     (((w2[k] >> (8 * e)) & 0xffu) << 16) | (((w3[k] >> (8 * e)) & 0xffu) << 24);
+            o[4 * v + k] = make_uint4(r[0], r[1], r[2], r[3]);
+          }
+        }
+      }
+      return;
+    }
+  }
   if (B.mode == 1) {  // byte unshuffle (shuffle.c unshuffle_generic): dest[j*ts+i] = src[i*neb+j]
     const uint32_t neb = bsize / ts, body = neb * ts;
     for (uint32_t q = threadIdx.x; q < bsize; q += 256) {
