@@ -796,6 +796,18 @@ def _time_reps(fn, seconds):
 
 
 # ------------------------------------------------------------------------------------------------
+def world_info(world, dev):
+    """The process world this line was measured in: backend, size and every rank's device (gathered
+    over the process group at N > 1)."""
+    p = torch.cuda.get_device_properties(dev)
+    me = f"{p.name} (cuda:{dev.index}, pci {p.pci_domain_id:04x}:{p.pci_bus_id:02x}:{p.pci_device_id:02x})"
+    if world == 1:
+        return {"backend": None, "world_size": 1, "devices": [me]}
+    devs = [None] * world
+    torch.distributed.all_gather_object(devs, me)
+    return {"backend": torch.distributed.get_backend(), "world_size": world, "devices": devs}
+
+
 def run_gpu(args, rank, world, dev):
     from zarrs_amd import Context
     from zarrs_amd import _lib as L
@@ -927,7 +939,72 @@ def run_gpu(args, rank, world, dev):
         lib.zgpu_plan_destroy(plan)
     host = W.host_leg(sp) if (args.host_leg and rank == 0) else None
     return dict(W=W, elapsed=elapsed, ev_ms=ev_ms, alg_bytes=alg_bytes, ok=ok, batch_ms=batch_ms, host=host,
-                counters=counters)
+                counters=counters, world_info=world_info(world, dev))
+
+
+def secondary_legs(args, rank, world, dev, r_primary):
+    """The other §8(d) configs measured in the same run as the headline (C2): C3 (C4 at N > 1: the
+    subset's axis-0 slabs gathered to rank 0 over RCCL inside the step) and C5 at --secondary-c5-scale
+    (LPT chunk partition, plus the cross-GPU L0 subset gather at N > 1). Each leg: value, ms/step,
+    the roofline frac of its dominant kernel / step (HIP events, algorithmic bytes), decode(encode(x))
+    == x on device, and (rank 0, N = 1) a short CPU baseline of the oracle. No PMC passes here (their
+    traffic figures are in profiles/)."""
+    import copy
+    import gc
+    out = {}
+    r_primary["W"] = None
+    for name in [w for w in args.secondary.split(",") if w]:
+        if name not in WORKLOADS:
+            out[name] = {"error": "unknown workload"}
+            continue
+        t_leg = time.perf_counter()
+        a = copy.copy(args)
+        a.workload, a.steps, a.warmup = name, max(2, min(args.steps, 5)), 1
+        a.host_leg, a.cpu_seconds, a.c5_scale = False, 5.0, args.secondary_c5_scale
+        a.lane_priorities, a.serial_lanes, a.lane_times = "", False, False
+        gc.collect()
+        torch.cuda.empty_cache()
+        print(f"[bench] secondary leg {name} ...", file=sys.stderr, flush=True)
+        try:
+            r = run_gpu(a, rank, world, dev)
+        except Exception as e:  # noqa: BLE001 - a secondary leg never voids the headline line
+            out[name] = {"error": repr(e)[:300]}
+            continue
+        W = r["W"]
+        el = torch.tensor([r["elapsed"]], dtype=torch.float64, device=dev)
+        okt = torch.tensor([1 if r["ok"] else 0], dtype=torch.int32, device=dev)
+        if world > 1:
+            torch.distributed.all_reduce(el, op=torch.distributed.ReduceOp.MAX)
+            torch.distributed.all_reduce(okt, op=torch.distributed.ReduceOp.MIN)
+        t = float(el.item())
+        achieved = r["alg_bytes"] / (r["ev_ms"] * 1e-3) / 1e9
+        leg = {"metric": METRIC, "value": round(W.step_bytes * a.steps / t / 2 ** 30, 2), "unit": "GiB/s",
+               "n_gpus": world, "steps": a.steps, "warmup": a.warmup,
+               "ms_per_step": round(t / a.steps * 1e3, 3), "scaling": W.scaling, "dtype": W.dtype,
+               "config": W.config,
+               "roofline": {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                            "frac": round(achieved / HBM_PEAK_GBS, 4), "kernel": W.kernel,
+                            "alg_bytes_per_launch": r["alg_bytes"],
+                            "avg_launch_ms_hip_events": round(r["ev_ms"], 4),
+                            "traffic": None, "traffic_detail": "see profiles/ (PMC passes run for the headline only)"},
+               "roundtrip_ok": bool(okt.item())}
+        if r["counters"][L_CTR_ZSTD_SERIAL] or r["counters"][L_CTR_ZSTD_PARALLEL]:
+            leg["zstd_items_per_step"] = {"block_parallel": r["counters"][L_CTR_ZSTD_PARALLEL],
+                                          "serial_fallback": r["counters"][L_CTR_ZSTD_SERIAL]}
+        if rank == 0 and world == 1 and not args.no_cpu:
+            try:
+                leg["cpu_baseline"] = W.cpu_baseline()
+            except Exception as e:  # noqa: BLE001
+                leg["cpu_baseline"] = {"error": repr(e)[:300]}
+        leg["leg_seconds"] = round(time.perf_counter() - t_leg, 1)
+        out[name] = leg
+        r["W"] = W = None
+        a.ctx.close()
+        gc.collect()
+        torch.cuda.empty_cache()
+        if world > 1:
+            torch.distributed.barrier()
+    return out
 
 
 def pmc_traffic(args, W):
@@ -1001,6 +1078,33 @@ def pmc_traffic(args, W):
     return out, None
 
 
+def launcher_cmd(args, argv, port):
+    """torch.distributed.run over N local processes (one per GPU, rendezvous on 127.0.0.1), each
+    running this script with the same flags."""
+    return [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={args.gpus}",
+            "--master-addr", "127.0.0.1", "--master-port", str(port), os.path.abspath(__file__)] + \
+        [a for a in argv if a != "--dry-launch"]
+
+
+def launch_workers(args):
+    import socket
+    import subprocess
+    n_dev = torch.cuda.device_count()  # counts devices without initialising HIP (this image)
+    with socket.socket() as so:
+        so.bind(("127.0.0.1", 0))
+        port = so.getsockname()[1]
+    cmd = launcher_cmd(args, sys.argv[1:], port)
+    if args.dry_launch:
+        print(json.dumps({"launch": cmd, "visible_devices": n_dev}))
+        return 0
+    if n_dev < args.gpus:
+        print(f"bench.py: --gpus {args.gpus} but {n_dev} GPU(s) visible", file=sys.stderr)
+        return 2
+    env = dict(os.environ)
+    env.setdefault("HSA_ENABLE_IPC_MODE_LEGACY", "0")
+    return subprocess.call(cmd, env=env)
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -1021,9 +1125,27 @@ def main():
     ap.add_argument("--no-host-leg", dest="host_leg", action="store_false",
                     help="skip the PCIe-inclusive (host input/output) leg")
     ap.add_argument("--child", action="store_true", help=argparse.SUPPRESS)
+    ap.add_argument("--secondary", default="c3,c5",
+                    help="workloads measured after the headline and reported in its line's `secondary` object "
+                         "(comma-separated; '' for none)")
+    ap.add_argument("--secondary-c5-scale", type=int, default=2,
+                    help="C5 scale of the secondary leg (L0 y/x divided by this)")
+    ap.add_argument("--dry-launch", action="store_true",
+                    help="print the launcher command --gpus N > 1 would start, and exit (no GPU touched)")
     args = ap.parse_args()
 
-    world = int(os.environ.get("WORLD_SIZE", "1"))
+    if args.gpus < 1:
+        ap.error("--gpus must be >= 1")
+    env_world = os.environ.get("WORLD_SIZE")
+    if env_world is None and args.gpus > 1:
+        # N processes, one per GPU: started here as a child launcher BEFORE anything touches the GPU
+        # (this process never initialises HIP; it waits for the launcher and exits with its code)
+        return launch_workers(args)
+    world = int(env_world or "1")
+    if world != args.gpus:
+        print(f"bench.py: WORLD_SIZE={world} but --gpus {args.gpus}: refusing to report a line for a "
+              f"world the flags do not name", file=sys.stderr)
+        return 2
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
     if world > 1:
@@ -1072,16 +1194,21 @@ def main():
                          "avg_launch_ms_hip_events": round(r["ev_ms"], 4)},
             "cpu_baseline": cpu,
             "roundtrip_ok": bool(ok.item()),
+            "world": r["world_info"],
             "decode_batch_ms_incl_host_planning": round(r["batch_ms"], 3),
             "host_leg": r["host"],
         }
         if r["counters"][L_CTR_ZSTD_SERIAL] or r["counters"][L_CTR_ZSTD_PARALLEL]:
             line["zstd_items_per_step"] = {"block_parallel": r["counters"][L_CTR_ZSTD_PARALLEL],
                                            "serial_fallback": r["counters"][L_CTR_ZSTD_SERIAL]}
+    sec = secondary_legs(args, rank, world, dev, r) if args.secondary and not args.child else None
+    if rank == 0:
+        if sec:
+            line["secondary"] = sec
         print(json.dumps(line), flush=True)
     if world > 1:
         torch.distributed.destroy_process_group()
 
 
 if __name__ == "__main__":
-    main()
+    sys.exit(main() or 0)

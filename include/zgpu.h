@@ -106,8 +106,9 @@ const char *zgpu_version(void);
 /*
  * Parse and bind a codec chain.
  *  codecs_json : the Zarr V3 "codecs" JSON array (nested sharding_indexed configs included).
- *                Supported: transpose, bytes, sharding_indexed, crc32c (+numcodecs.crc32c),
- *                gzip, zstd, numcodecs.shuffle. Others -> ZGPU_UNSUPPORTED.
+ *                Supported: transpose, bytes, sharding_indexed (nested up to two levels),
+ *                crc32c (+numcodecs.crc32c), gzip, zstd, numcodecs.shuffle, blosc (blosclz, lz4,
+ *                lz4hc, zlib, snappy, zstd; shuffle / bitshuffle). Others -> ZGPU_UNSUPPORTED.
  *  data_type   : Zarr V3 data type name ("float32", "uint16", ...); fixed-size types only.
  *  fill        : native-endian fill value bytes (FillValue::as_ne_bytes), fill_len == dtype size.
  *  validate_checksums : CodecOptions::validate_checksums (zarrs default true, options.rs:24-33).
@@ -149,6 +150,13 @@ int zgpu_decode_batch(zgpu_chain *chain, uint32_t ndim, const zgpu_chunk_desc *d
  * (benchmarks, hipGraph capture): the descriptor table is planned and uploaded once.
  * zgpu_plan_execute enqueues the decode on the stream and, if status != NULL, waits and returns
  * per-chunk statuses; with status == NULL it returns immediately after enqueue.
+ * An asynchronous execute's output is valid only once zgpu_plan_status has returned for it: a blosc
+ * input that outgrows the stream-table layout the plan recorded on its first execution is detected
+ * on the device, nothing of it is decoded, and zgpu_plan_status re-runs the execution with a
+ * read-back layout (ZGPU_CTR_BLOSC_RERUN) before it returns the statuses. Likewise a plan whose last
+ * execution had no item for the serial zstd decoder skips that kernel; an input that needs it is
+ * re-run by zgpu_plan_status with the kernel launched. A hipGraph capture of zgpu_plan_execute
+ * therefore needs inputs whose blosc layout and zstd frame structure do not change between replays.
  */
 int zgpu_plan_create(zgpu_chain *chain, uint32_t ndim, const zgpu_chunk_desc *descs, uint64_t n,
                      const uint64_t *out_shape, uint32_t flags, zgpu_plan **out);

@@ -13,7 +13,7 @@ import torch.distributed as dist
 import torch.multiprocessing as mp
 
 import oracle as O
-from zarrs_amd.distributed import (chunk_boxes, gather_regions, gather_slabs, lpt_partition,
+from zarrs_amd.distributed import (_contiguous_in, chunk_boxes, gather_regions, gather_slabs, lpt_partition,
                                    retrieve_array_subset_distributed, slab_partition)
 
 CODECS = [{"name": "bytes", "configuration": {"endian": "little"}}, {"name": "crc32c"}]
@@ -102,6 +102,16 @@ def _worker(rank, world, port, q):
             res["c5_gather"] = bool(np.array_equal(got.numpy().view(np.uint16), lvl[1:7, 3:22, 5:35]))
         else:
             res["c5_gather"] = got is None
+        # a subset whose chunk boxes are contiguous runs of it: received in place (no packing)
+        sub0, subn = [1, 8, 16], [6, 8, 8]
+        boxes = [[] for _ in range(world)]
+        for idx, b0, bs in chunk_boxes(list(lvl.shape), cs, sub0, subn):
+            boxes[owner[idx]].append((b0, bs))
+        got = gather_regions(local, boxes, sub0, subn)
+        if rank == 0:
+            res["c5_gather_direct"] = bool(np.array_equal(got.numpy().view(np.uint16), lvl[1:7, 8:16, 16:24]))
+        else:
+            res["c5_gather_direct"] = got is None
         q.put((rank, res))
     finally:
         dist.destroy_process_group()
@@ -183,3 +193,11 @@ def test_chunk_boxes_cover_subset():
     boxes = chunk_boxes([10, 13], [4, 5], [3, 2], [6, 11])
     assert sum(bs[0] * bs[1] for _, _, bs in boxes) == 66
     assert [i for i, _, _ in boxes] == [(0, 0), (0, 1), (0, 2), (1, 0), (1, 1), (1, 2), (2, 0), (2, 1), (2, 2)]
+
+
+def test_contiguous_box_rule():
+    assert _contiguous_in([3, 8, 8], [6, 8, 8])
+    assert _contiguous_in([1, 1, 5], [6, 8, 8])
+    assert _contiguous_in([1, 3, 8], [6, 8, 8])
+    assert not _contiguous_in([1, 3, 7], [6, 8, 8])
+    assert not _contiguous_in([2, 4, 8], [6, 8, 8])

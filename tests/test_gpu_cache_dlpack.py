@@ -102,3 +102,22 @@ def test_cache_does_not_keep_failed_chunks(ctx):
     assert ei.value.status == 1
     assert ca.cache.stats()["entries"] == 2
     assert np.array_equal(ca.retrieve_array_subset([200], [100]), a[200:])
+
+
+def test_cache_call_level_error_is_not_cached(ctx):
+    """A chain the planner rejects before any chunk status exists (bytes->bytes codecs after
+    sharding_indexed: UNSUPPORTED) fails on every read through the cache; no slot is kept."""
+    from zarrs_amd import Array, ArrayCached, ChunkCacheDecodedLruSizeLimit, MemoryStore, ZgpuError
+    codecs = [{"name": "sharding_indexed", "configuration": {
+        "chunk_shape": [4], "codecs": [{"name": "bytes", "configuration": {"endian": "little"}}],
+        "index_codecs": [{"name": "bytes", "configuration": {"endian": "little"}}, {"name": "crc32c"}]}},
+        {"name": "crc32c"}]
+    meta = {"shape": [16], "data_type": "uint16", "fill_value": 0, "codecs": codecs,
+            "chunk_grid": {"name": "regular", "configuration": {"chunk_shape": [8]}}}
+    store = MemoryStore({"c/0": bytes(64), "c/1": bytes(64)})
+    ca = ArrayCached(Array(store, meta, ctx), ChunkCacheDecodedLruSizeLimit(1 << 20, ctx))
+    for _ in range(2):
+        with pytest.raises(ZgpuError) as ei:
+            ca.retrieve_array_subset()
+        assert ei.value.status == 6
+    assert ca.cache.stats()["entries"] == 0

@@ -253,3 +253,70 @@ def test_zstd_corruption_detected():
         ch.decode_batch(descs, out, [2 * n], enc_device=False)
     assert ei.value.status in (2, 4)  # CORRUPT_STREAM (or a size mismatch it causes)
     assert np.array_equal(out[n:], data[1])
+
+
+def _raw_block_frame(data: bytes, block: int) -> bytes:
+    """A zstd frame of raw blocks of `block` bytes (RFC 8878: single segment, 2-byte content size),
+    built by hand: more blocks than the block-parallel scratch holds send it to the serial decoder."""
+    import struct
+    n = len(data)
+    assert 256 <= n < 65536 + 256
+    out = bytearray(struct.pack("<IB", 0xFD2FB528, 0x60) + struct.pack("<H", n - 256))
+    for off in range(0, n, block):
+        part = data[off:off + block]
+        last = 1 if off + block >= n else 0
+        out += struct.pack("<I", last | (len(part) << 3))[:3] + part
+    return bytes(out)
+
+
+def _skippable(n: int) -> bytes:
+    import struct
+    return struct.pack("<II", 0x184D2A50, n - 8) + b"\0" * (n - 8)
+
+
+def test_plan_reruns_when_input_needs_the_serial_decoder():
+    """A plan whose executions had no item for the serial zstd decoder stops launching it; when the
+    input bytes change so that one item needs it, zgpu_plan_status re-runs the execution with the
+    kernel launched (both results exact, the serial counter reports the item)."""
+    import ctypes as C
+    import torch
+    from zarrs_amd import CodecChain, Context, make_desc
+    from zarrs_amd import _lib as L
+    lib = L.load()
+    rng = np.random.default_rng(11)
+    codecs = [BYTES_LE, {"name": "zstd", "configuration": {"level": 3, "checksum": False}}]
+    oc = O.OracleChain.from_metadata(codecs, "uint8", 0, 1)
+    n, k = 4096, 3
+    data = [_content(rng, n, "text") for _ in range(k)]
+    serial = _raw_block_frame(data[1].tobytes(), 40)  # 103 raw blocks > the 64-record scratch
+    encs = [oc.encode(d) for d in data]
+    L_item = max(len(serial), *[len(e) for e in encs]) + 16
+    pad = [e + _skippable(L_item - len(e)) for e in encs]
+    blob = torch.frombuffer(bytearray(b"".join(pad)), dtype=torch.uint8).cuda()
+    descs = [make_desc((blob.data_ptr() + i * L_item, L_item), [n], out_start=[i * n]) for i in range(k)]
+    ch = CodecChain.from_metadata(codecs, "uint8", 0, Context.default())
+    arr = (L.ChunkDesc * k)(*descs)
+    plan = C.c_void_p()
+    L.check(lib.zgpu_plan_create(ch._h, 1, arr, k, L.u64s([k * n]), L.ENC_DEVICE | L.OUT_DEVICE, C.byref(plan)))
+    try:
+        out = torch.zeros(k * n, dtype=torch.uint8, device="cuda")
+        st = (C.c_int32 * k)()
+        ctr = (C.c_uint64 * L.N_COUNTERS)()
+        for _ in range(2):  # all items on the block-parallel path; the second execution skips the fallback
+            out.zero_()
+            assert lib.zgpu_plan_execute(plan, out.data_ptr(), st, None) == 0
+            assert np.array_equal(out.cpu().numpy(), np.concatenate(data))
+            lib.zgpu_plan_counters(plan, ctr, L.N_COUNTERS)
+            assert ctr[1] == 0 and ctr[2] == k
+        # item 1 now holds the many-block frame (same padded length)
+        blob[L_item:2 * L_item] = torch.frombuffer(bytearray(serial + _skippable(L_item - len(serial))),
+                                                   dtype=torch.uint8).cuda()
+        out.zero_()
+        assert lib.zgpu_plan_execute(plan, out.data_ptr(), None, None) == 0  # asynchronous
+        assert lib.zgpu_plan_status(plan, st, None) == 0
+        assert list(st) == [0] * k
+        assert np.array_equal(out.cpu().numpy(), np.concatenate(data))
+        lib.zgpu_plan_counters(plan, ctr, L.N_COUNTERS)
+        assert ctr[1] == 1 and ctr[2] == k - 1
+    finally:
+        lib.zgpu_plan_destroy(plan)

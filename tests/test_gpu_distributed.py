@@ -1,0 +1,151 @@
+"""N>1 read paths with the HIP decode on every rank (configs C4 and C5's 8-GPU leg).
+
+Two ranks share the box's one GPU (device 0): each rank decodes its share through libzgpu (the HIP
+kernels, not the oracle) and the results are gathered to rank 0 over gloo, staged through host
+memory (RCCL cannot pair two ranks on one device; the exchange logic is the same code path that
+runs over RCCL/xGMI on an 8-GPU node). Rank 0 compares the gathered subset with the CPU oracle.
+
+  C4 pattern: C3's exact chain ([bytes, gzip 1, crc32c] inner chunks, [bytes, crc32c] index at the
+              end), subset split into axis-0 slabs, slabs gathered into rank 0's subset
+  C5 pattern: u16 [bytes, numcodecs.shuffle{2}, zstd{3}] chunks LPT-partitioned by encoded size,
+              each rank decodes its chunks into its own level array (one zgpu_decode_batch), one
+              cross-rank subset gathered with gather_regions (packed boxes and in-place boxes)
+"""
+import os
+import socket
+
+import numpy as np
+import pytest
+
+pytestmark = pytest.mark.gpu
+
+C3_CODECS = [{"name": "sharding_indexed", "configuration": {
+    "chunk_shape": [8, 8, 8],
+    "codecs": [{"name": "bytes", "configuration": {"endian": "little"}},
+               {"name": "gzip", "configuration": {"level": 1}}, {"name": "crc32c"}],
+    "index_codecs": [{"name": "bytes", "configuration": {"endian": "little"}}, {"name": "crc32c"}],
+    "index_location": "end"}}]
+C5_CODECS = [{"name": "bytes", "configuration": {"endian": "little"}},
+             {"name": "numcodecs.shuffle", "configuration": {"elementsize": 2}},
+             {"name": "zstd", "configuration": {"level": 3, "checksum": False}}]
+
+
+def _free_port():
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        return s.getsockname()[1]
+
+
+def _c3_array():
+    rng = np.random.default_rng(3)
+    z, y, x = np.meshgrid(np.arange(64), np.arange(48), np.arange(48), indexing="ij")
+    v = np.round((np.sin(0.05 * x) + np.cos(0.03 * y) + 0.5 * np.sin(0.07 * z)) * 256) / 256
+    return (v + rng.standard_normal(v.shape) / 256).astype(np.float32)
+
+
+def _c5_level():
+    rng = np.random.default_rng(42)
+    lvl = (100 + rng.poisson(50, (16, 96, 80))).astype(np.uint16)
+    lvl[2:12, 10:70, 8:60] += 3000
+    return lvl
+
+
+def _encode_chunks(co, a, cs):
+    out = {}
+    for idx in np.ndindex(*[-(-s // c) for s, c in zip(a.shape, cs)]):
+        blk = np.zeros(cs, a.dtype)
+        sl = tuple(slice(i * c, min((i + 1) * c, s)) for i, c, s in zip(idx, cs, a.shape))
+        blk[tuple(slice(0, n) for n in a[sl].shape)] = a[sl]
+        out[idx] = co.encode(blk)
+    return out
+
+
+def _worker(rank, world, port, q):
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    import torch
+    import torch.distributed as dist
+    import oracle as O
+    from zarrs_amd import Array, CodecChain, Context, DeviceStore, MemoryStore, make_desc
+    from zarrs_amd.distributed import chunk_boxes, gather_regions, lpt_partition, retrieve_array_subset_distributed
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    res = {}
+    try:
+        ctx = Context(0)
+        dev = torch.device("cuda", 0)
+        # ---- C4: sharded gzip+crc32c array, axis-0 slabs decoded on the GPU, gathered to rank 0
+        a = _c3_array()
+        shard = [16, 16, 16]
+        co = O.OracleChain.from_metadata(C3_CODECS, "float32", 0.0, 3)
+        shards = _encode_chunks(co, a, shard)
+        store = DeviceStore.from_store(MemoryStore({"c/" + "/".join(map(str, k)): v for k, v in shards.items()}))
+        meta = {"shape": list(a.shape), "data_type": "float32", "fill_value": 0.0, "codecs": C3_CODECS,
+                "chunk_grid": {"name": "regular", "configuration": {"chunk_shape": shard}}}
+        arr = Array(store, meta, ctx)
+        for name, (start, shape) in {"c4_even": ([5, 3, 7], [50, 40, 33]),
+                                     "c4_ragged": ([1, 0, 0], [63, 48, 48]),
+                                     "c4_thin": ([30, 2, 2], [3, 5, 40])}.items():
+            got = retrieve_array_subset_distributed(arr, start, shape, device=dev)
+            if rank == 0:
+                exp = O.retrieve_array_subset(co, list(a.shape), shard, shards, start, shape, nthreads=4)
+                res[name] = got is not None and got.is_cuda and got.cpu().numpy().tobytes() == exp.tobytes()
+            else:
+                res[name] = got is None
+        # ---- C5: zstd+shuffle u16 chunks LPT-partitioned, each rank decodes its own on the GPU
+        lvl = _c5_level()
+        cs = [8, 32, 32]
+        co5 = O.OracleChain.from_metadata(C5_CODECS, "uint16", 0, 3)
+        chunks = _encode_chunks(co5, lvl, cs)
+        keys = sorted(chunks)
+        parts = lpt_partition([len(chunks[k]) for k in keys], world)
+        owner = {keys[i]: r for r, p in enumerate(parts) for i in p}
+        chain = CodecChain.from_metadata(C5_CODECS, "uint16", 0, ctx)
+        local = torch.zeros(lvl.shape, dtype=torch.int16, device=dev)
+        bufs, descs = [], []
+        for k in keys:
+            if owner[k] != rank:
+                continue
+            st = [i * c for i, c in zip(k, cs)]
+            sel = [min(c, s - o) for c, s, o in zip(cs, lvl.shape, st)]
+            t = torch.frombuffer(bytearray(chunks[k]), dtype=torch.uint8).to(dev)
+            bufs.append(t)
+            descs.append(make_desc(t, cs, [0, 0, 0], sel, st))
+        status = chain.decode_batch(descs, local, list(lvl.shape), enc_device=True)
+        res["c5_decode_ok"] = all(v == 0 for v in status)
+        host = local.cpu()  # gloo: staged through host memory
+        for name, (sub0, subn) in {"c5_gather_packed": ([3, 20, 10], [10, 60, 65]),
+                                   "c5_gather_in_place": ([0, 32, 0], [16, 32, 80])}.items():
+            boxes = [[] for _ in range(world)]
+            for idx, b0, bs in chunk_boxes(list(lvl.shape), cs, sub0, subn):
+                boxes[owner[idx]].append((b0, bs))
+            res[name + "_spans_ranks"] = all(len(b) > 0 for b in boxes)
+            got = gather_regions(host, boxes, sub0, subn)
+            if rank == 0:
+                sl = tuple(slice(o, o + n) for o, n in zip(sub0, subn))
+                res[name] = bool(np.array_equal(got.numpy().view(np.uint16), lvl[sl]))
+            else:
+                res[name] = got is None
+        torch.cuda.synchronize()
+    except Exception as e:  # noqa: BLE001 - reported through the queue
+        res["error"] = repr(e)
+    finally:
+        q.put((rank, res))
+        dist.destroy_process_group()
+
+
+def test_two_ranks_hip_decode_and_gather():
+    import torch.multiprocessing as mp
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    world = 2
+    procs = [ctx.Process(target=_worker, args=(r, world, port, q)) for r in range(world)]
+    for p in procs:
+        p.start()
+    out = dict(q.get(timeout=100) for _ in range(world))
+    for p in procs:
+        p.join(timeout=30)
+        assert p.exitcode == 0
+    for r in range(world):
+        assert "error" not in out[r], out
+        assert out[r] and all(out[r].values()), out

@@ -123,7 +123,12 @@ class Array:
         self.store = store
         self.metadata = metadata
         self.shape = [int(s) for s in metadata["shape"]]
-        self.chunk_shape = [int(c) for c in metadata["chunk_grid"]["configuration"]["chunk_shape"]]
+        grid = metadata["chunk_grid"]
+        if grid.get("name") != "regular":
+            # the batched read plans one regular grid (zarrs/src/array/chunk_grid/regular.rs); the
+            # rectangular / rectilinear / regular_bounded grids would place chunks wrongly
+            raise L.ZgpuError(L.UNSUPPORTED, f"chunk grid {grid.get('name')!r}: only 'regular' grids are supported")
+        self.chunk_shape = [int(c) for c in grid["configuration"]["chunk_shape"]]
         self.data_type = metadata["data_type"]
         kenc = metadata.get("chunk_key_encoding", {"name": "default"})
         cfg = kenc.get("configuration", {}) or {}

@@ -50,8 +50,26 @@ struct zgpu_cache {
   std::list<uint64_t> lru;
   std::vector<uint64_t> free_slots;
   uint64_t hits = 0, misses = 0;
+  // "no chunk" entries hold no slot, so the byte capacity does not bound them: they are capped by
+  // count (sparse arrays would otherwise grow the map, and every eviction scan, without limit)
+  uint64_t n_slotless = 0;
+  uint64_t slotless_cap() const { return 4 * n_slots + 4096; }
+  void trim_slotless(const std::vector<uint64_t> &keep) {
+    if (n_slotless <= slotless_cap()) return;
+    std::unordered_map<uint64_t, char> in_read;
+    for (uint64_t lin : keep) in_read[lin] = 1;
+    for (auto it = lru.end(); it != lru.begin() && n_slotless > slotless_cap();) {
+      --it;
+      auto e = map.find(*it);
+      if (e->second.slot >= 0 || in_read.count(*it)) continue;
+      map.erase(e);
+      it = lru.erase(it);
+      n_slotless--;
+    }
+  }
 
   void reset() {
+    n_slotless = 0;
     map.clear();
     lru.clear();
     free_slots.clear();
@@ -121,6 +139,7 @@ void zgpu_cache_destroy(zgpu_cache *cache) {
 int zgpu_cache_clear(zgpu_cache *K) {
   if (!K) return fail(ZGPU_INVALID_ARGUMENT, "NULL argument");
   std::lock_guard<std::mutex> lk(K->mu);
+  K->n_slotless = 0;
   K->map.clear();
   K->lru.clear();
   K->free_slots.clear();
@@ -171,8 +190,10 @@ int zgpu_cache_retrieve_array_subset(zgpu_cache *K, zgpu_chain *ch, uint32_t nd,
     } else {  // missing key: cached as "no chunk" (fill value)
       K->lru.push_front(lin);
       K->map[lin] = zgpu_cache::Entry{-1, K->lru.begin()};
+      K->n_slotless++;
     }
   }
+  K->trim_slotless(lins);
   if (present > K->n_slots) {  // the read alone exceeds the capacity: decode it directly, cache nothing new
     return zgpu_retrieve_array_subset(ch, nd, array_shape, chunk_shape, chunk_ptrs, chunk_lens, sel_start, sel_shape,
                                       out, flags, hip_stream);
@@ -217,15 +238,22 @@ int zgpu_cache_retrieve_array_subset(zgpu_cache *K, zgpu_chain *ch, uint32_t nd,
     // every miss decoded into its slot in one batch: the pool is an array [n_slots * c0, c1, ...]
     std::vector<uint64_t> pshape(chunk_shape, chunk_shape + nd);
     pshape[0] *= K->n_slots;
-    std::vector<int32_t> st(md.size(), 0);
+    // -1: no status written (a call-level failure returns before the per-chunk statuses exist)
+    std::vector<int32_t> st(md.size(), -1);
+    // entries hold verified chunks (the header's promise): a caller's ZGPU_NO_VALIDATE does not reach
+    // the miss decode, so an entry never depends on which reader decoded it first
     rc = zgpu_decode_batch(ch, nd, md.data(), md.size(), K->pool, pshape.data(),
-                           (flags & (ZGPU_ENC_DEVICE | ZGPU_NO_VALIDATE)) | ZGPU_OUT_DEVICE, st.data(), hip_stream);
-    if (rc == ZGPU_HIP_ERROR || rc == ZGPU_INVALID_ARGUMENT) {
+                           (flags & ZGPU_ENC_DEVICE) | ZGPU_OUT_DEVICE, st.data(), hip_stream);
+    // a chunk is cached only with a written status of 0: a call-level error (HIP, argument, or a chain
+    // the planner rejects, e.g. UNSUPPORTED, before any status exists) leaves every slot undecoded
+    bool any_status = false;
+    for (int32_t v : st) any_status = any_status || v >= 0;
+    if (rc && !any_status) {
       for (int64_t sl : mslot) K->free_slots.push_back((uint64_t)sl);
       return rc;
     }
     for (size_t j = 0; j < need.size(); j++) {
-      if (st[j]) {  // not cached; the error is the call's
+      if (st[j] != 0) {  // not cached; the error is the call's
         K->free_slots.push_back((uint64_t)mslot[j]);
         continue;
       }

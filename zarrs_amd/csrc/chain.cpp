@@ -211,4 +211,22 @@ int64_t chain_fixed_encoded_size(const Chain &c, uint64_t nelem) {
   return n;
 }
 
+uint64_t gzip_bound(uint64_t n) { return n + 10 + 8 + (n + 7) / 8 + (n + 63) / 64 + 5; }
+
+// ZstdCodec::encoded_representation (zstd_codec.rs:132-147): header/trailer 4 + 14 + 4 bytes and a
+// 3-byte block header per 1000 bytes
+uint64_t zstd_bound(uint64_t n) { return n + 4 + 14 + 4 + 3 * ((n + 999) / 1000); }
+
+int64_t chain_encoded_bound(const Chain &c, uint64_t nelem) {
+  if (c.a2b.kind != CodecKind::Bytes) return -1;
+  uint64_t n = nelem * c.es;
+  for (const Codec &k : c.b2b) {
+    if (k.kind == CodecKind::Crc32c) n += 4;
+    else if (k.kind == CodecKind::Gzip) n = gzip_bound(n);
+    else if (k.kind == CodecKind::Zstd) n = zstd_bound(n);
+    else if (k.kind != CodecKind::Shuffle) return -1;
+  }
+  return (int64_t)n;
+}
+
 }  // namespace zgpu

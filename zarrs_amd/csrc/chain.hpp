@@ -54,4 +54,11 @@ std::shared_ptr<Chain> parse_chain(const Json &codecs, const std::string &data_t
 // (BytesRepresentation::FixedSize, sharding.rs:163-176).
 int64_t chain_fixed_encoded_size(const Chain &c, uint64_t nelem);
 
+// Upper bound of one chunk's encoded size for an array->bytes `bytes` chain (BytesRepresentation::
+// BoundedSize): crc32c +4, gzip as GzipCodec::encoded_representation (gzip_codec.rs:122-136, zlib's
+// deflateBound), zstd as ZstdCodec's (zstd_codec.rs:132-147); -1 if unbounded (e.g. blosc here).
+int64_t chain_encoded_bound(const Chain &c, uint64_t nelem);
+uint64_t gzip_bound(uint64_t n);
+uint64_t zstd_bound(uint64_t n);
+
 }  // namespace zgpu

@@ -4,6 +4,8 @@
 #include <string>
 #include <vector>
 
+#include <hip/hip_runtime.h>
+
 #include "../../include/zgpu.h"
 #include "chain.hpp"
 
@@ -15,6 +17,11 @@ zgpu_ctx *chain_ctx(const zgpu_chain *c);
 const Chain &chain_model(const zgpu_chain *c);
 bool chain_validates(const zgpu_chain *c);
 int ctx_device(const zgpu_ctx *c);
+// the context's caching device allocator (grow-only pools: a steady-state caller performs no
+// hipMalloc) and a second stream of its own for copies; both take the context lock
+void *ctx_dev_alloc(zgpu_ctx *c, size_t bytes);
+void ctx_dev_free(zgpu_ctx *c, void *p);
+hipStream_t ctx_copy_stream(zgpu_ctx *c);
 // array_read_ops_common.rs:20-109: subset -> one full/partial descriptor per intersecting chunk (C
 // order of the chunk grid), lins[k] = descriptor k's linear chunk-grid index. ZGPU_OK, -1 for an empty
 // subset, or an error status.

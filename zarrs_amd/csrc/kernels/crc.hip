@@ -218,6 +218,7 @@ __global__ __launch_bounds__(CRC_THREADS) void k_crc32c_encode(const uint64_t *d
   __shared__ CrcTables T;
   __shared__ uint64_t s_len[CRC_THREADS / 64];
   __shared__ uint32_t s_crc[CRC_THREADS / 64];
+  if (!dsts[blockIdx.x]) return;  // a shard whose layout failed (variable-length encode)
   uint8_t *p = (uint8_t *)dsts[blockIdx.x] + lo;
   build_tables(T, POLY_CRC32C);
   const uint32_t c = wg_crc(p, len, T, POLY_CRC32C, s_len, s_crc);

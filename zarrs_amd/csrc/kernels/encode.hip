@@ -350,10 +350,8 @@ __global__ __launch_bounds__(256) void k_shard_copy(const uint8_t *__restrict__ 
   }
 }
 
-hipError_t launch_shard_encode(const uint64_t *starts, const uint8_t *array, const ZgEncode &inner, uint32_t n_chunks,
-                               uint32_t *nonfill, const uint8_t *tmp, const ZgShardLayoutArgs &A,
-                               const uint64_t *shard_dst, uint64_t *inner_off, uint64_t *index_ptr,
-                               uint64_t *shard_len, uint32_t n_shards, hipStream_t s) {
+hipError_t launch_fill_check(const uint64_t *starts, const uint8_t *array, const ZgEncode &inner, uint32_t n_chunks,
+                             uint32_t *nonfill, hipStream_t s) {
   if (!n_chunks) return hipSuccess;
   switch (inner.es) {
     case 1: hipLaunchKernelGGL(k_fill_check<1>, dim3(n_chunks), dim3(256), 0, s, starts, array, inner, nonfill); break;
@@ -363,6 +361,16 @@ hipError_t launch_shard_encode(const uint64_t *starts, const uint8_t *array, con
     case 16: hipLaunchKernelGGL(k_fill_check<16>, dim3(n_chunks), dim3(256), 0, s, starts, array, inner, nonfill); break;
     default: return hipErrorInvalidValue;
   }
+  return hipGetLastError();
+}
+
+hipError_t launch_shard_encode(const uint64_t *starts, const uint8_t *array, const ZgEncode &inner, uint32_t n_chunks,
+                               uint32_t *nonfill, const uint8_t *tmp, const ZgShardLayoutArgs &A,
+                               const uint64_t *shard_dst, uint64_t *inner_off, uint64_t *index_ptr,
+                               uint64_t *shard_len, uint32_t n_shards, hipStream_t s) {
+  if (!n_chunks) return hipSuccess;
+  hipError_t e = launch_fill_check(starts, array, inner, n_chunks, nonfill, s);
+  if (e != hipSuccess) return e;
   const ZgShardLayout Lo{A.n_inner, A.E, A.E_pitch, A.index_bytes, A.pre, A.at_start, A.big_endian};
   hipLaunchKernelGGL(k_shard_layout, dim3(n_shards), dim3(256), 0, s, nonfill, Lo, shard_dst, inner_off, index_ptr,
                      shard_len);
@@ -398,7 +406,7 @@ hipError_t launch_encode_gather(const uint64_t *dsts, const uint64_t *starts, co
     }
     return hipSuccess;
   }
-  const uint32_t grid = (uint32_t)std::min<uint64_t>((total + 255) / 256, 256 * 64);
+  const uint32_t grid = (uint32_t)std::min<uint64_t>((total + 255) / 256, (uint64_t)device_cu_count() * 64);
   switch (P.es) {
     case 1: hipLaunchKernelGGL(k_encode_gather<1>, dim3(grid), dim3(256), 0, s, dsts, starts, array, P, total); break;
     case 2: hipLaunchKernelGGL(k_encode_gather<2>, dim3(grid), dim3(256), 0, s, dsts, starts, array, P, total); break;

@@ -20,6 +20,20 @@ inline uint64_t max_grid_blocks(uint32_t threads) {
   return m;
 }
 
+// Compute units of the current device (queried once per device; grids sized to the chip, not a
+// hard-coded 256).
+inline uint32_t device_cu_count() {
+  static uint32_t cache[64] = {0};
+  int dev = 0;
+  if (hipGetDevice(&dev) != hipSuccess || dev < 0 || dev >= 64) return 256;
+  if (!cache[dev]) {
+    int n = 0;
+    if (hipDeviceGetAttribute(&n, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || n <= 0) n = 256;
+    cache[dev] = (uint32_t)n;
+  }
+  return cache[dev];
+}
+
 enum ScatterMode : uint32_t { SCATTER_ROWS = 0, SCATTER_TILED = 1, SCATTER_GENERIC = 2 };
 // slabs (TILE x TILE tiles at consecutive values of ZgScatter::tile_b) per tiled-scatter block
 constexpr __host__ __device__ int tiled_slabs(uint32_t es) { return es == 8 ? 2 : 4; }
@@ -72,6 +86,12 @@ struct ZstdScratch {
   uint32_t blk_cap;
   uint32_t force_serial = 0;               // every item on the serial one-wave decoder (tests, ZGPU_ZSTD_FORCE_SERIAL)
   unsigned long long *counters = nullptr;  // [serial-fallback items, block-parallel items] (nullable)
+  // compacted serial-fallback items (nullable: the fallback then runs one wave per item): k_zstd_scan
+  // appends them, the fallback is a small persistent grid over the list, launched only when
+  // launch_serial (a plan whose last execution had no serial item skips it and re-runs on the flag)
+  uint32_t *ser_list = nullptr;
+  unsigned long long *ser_count = nullptr;
+  uint32_t launch_serial = 1;
   // Fork for the sequence decoder (nullable: one stream): k_zstd_blocks needs only the scan, so it
   // runs on `side` beside the Huffman literal kernels and joins before k_zstd_plan
   hipStream_t side = nullptr;
@@ -115,6 +135,32 @@ hipError_t launch_shard_encode(const uint64_t *starts, const uint8_t *array, con
                                uint32_t *nonfill, const uint8_t *tmp, const ZgShardLayoutArgs &A,
                                const uint64_t *shard_dst, uint64_t *inner_off, uint64_t *index_ptr,
                                uint64_t *shard_len, uint32_t n_shards, hipStream_t s);
+
+// ---- variable-length write path (compressing chains) ----
+// gzip member encode (deflate_enc.hip): item i's bytes -> a member written at slot i + GZE_HDR (the
+// headroom takes crc32c codecs located at the start), items rewritten to it. sym_scratch holds
+// gzip_encode_grid(n) * GZE_BLK_SYMS u32 symbol records.
+constexpr uint32_t GZE_BLK_SYMS = 16384;  // symbols per DEFLATE block
+constexpr uint64_t GZE_HDR = 62;          // member offset in a slot (its bit stream then starts word-aligned)
+uint32_t gzip_encode_grid(uint32_t n_items);
+hipError_t launch_gzip_encode(ZgItem *items, uint32_t *status, uint32_t n_items, uint8_t *slots, uint64_t slot_bytes,
+                              uint32_t *sym_scratch, int level, hipStream_t s);
+// crc32c of each item's bytes written after them (or before them with at_start: src moves back 4)
+hipError_t launch_crc32c_items(ZgItem *items, const uint32_t *status, uint32_t n, int at_start, hipStream_t s);
+// each item's bytes into dst[i] (capacity cap[i], else DECODED_SIZE_MISMATCH); lens[i] = length
+hipError_t launch_encode_place(const ZgItem *items, uint32_t *status, const uint64_t *dst, const uint64_t *cap,
+                               uint64_t *lens, uint32_t n, hipStream_t s);
+// fill check of every inner chunk (launch_shard_encode's first kernel)
+hipError_t launch_fill_check(const uint64_t *starts, const uint8_t *array, const ZgEncode &inner, uint32_t n_chunks,
+                             uint32_t *nonfill, hipStream_t s);
+// sharding_indexed layout over inner chunks of variable length (items, n_shards * n_inner of them);
+// A.E_pitch = a shard destination's capacity. shard_status: 0, 1 (an inner chunk failed), or
+// DECODED_SIZE_MISMATCH (capacity); a failed shard gets index_ptr 0 (the index crc launch skips it)
+hipError_t launch_shard_encode_var(const uint64_t *starts, const uint8_t *array, const ZgEncode &inner,
+                                   uint32_t n_chunks, uint32_t *nonfill, const ZgItem *items,
+                                   const uint32_t *item_status, const ZgShardLayoutArgs &A, const uint64_t *shard_dst,
+                                   uint64_t *inner_off, uint64_t *index_ptr, uint64_t *shard_len,
+                                   uint32_t *shard_status, uint32_t n_shards, hipStream_t s);
 
 // blosc (c-blosc 1.x frames): stream table built on the device, sized on the host from BlInfo (first
 // execution of a plan) or from the capacities that execution recorded (later executions)

@@ -717,14 +717,13 @@ __device__ void out_match(SM &S, Out &O, uint32_t d, uint64_t n) {
 
 }  // namespace
 
-// One wave per item. lit: per-item literal scratch (BLOCK_MAX + 64 bytes each).
-__global__ __launch_bounds__(64) void k_zstd(ZgItem *items, uint32_t *status, uint8_t *dst, uint64_t slot_bytes,
-                                             uint8_t *lit_scratch, uint64_t lit_stride, const uint32_t *zmode) {
-  __shared__ ZSmem S;
-  const uint32_t item = blockIdx.x;
+// The serial decoder: one wave decodes one item. lit: per-item literal scratch (BLOCK_MAX + 64 bytes
+// each).
+__device__ __attribute__((noinline)) void zstd_serial_item(ZSmem &S, uint32_t item, ZgItem *items, uint32_t *status,
+                                                           uint8_t *dst, uint64_t slot_bytes, uint8_t *lit_scratch,
+                                                           uint64_t lit_stride) {
   const ZgItem it = items[item];
   if (status[item] || (it.flags & ZG_ITEM_FILL)) return;
-  if (zmode && zmode[item] != ZMODE_SERIAL) return;  // decoded by the block-parallel path
   const int lane = lane_id();
   const uint8_t *in = (const uint8_t *)it.src;
   const In I{in, it.len};
@@ -1111,6 +1110,26 @@ __global__ __launch_bounds__(64) void k_zstd(ZgItem *items, uint32_t *status, ui
   }
 }
 
+// Serial fallback. ser_list == NULL: one wave per item, every item the scan marked ZMODE_SERIAL (the
+// standalone serial decoder, zmode NULL: all items). Otherwise a small persistent grid over the
+// items k_zstd_scan compacted into ser_list[0 .. *ser_count): with none, every wave exits at once.
+__global__ __launch_bounds__(64) void k_zstd(ZgItem *items, uint32_t *status, uint8_t *dst, uint64_t slot_bytes,
+                                             uint8_t *lit_scratch, uint64_t lit_stride, const uint32_t *zmode,
+                                             const uint32_t *ser_list, const unsigned long long *ser_count) {
+  __shared__ ZSmem S;
+  if (ser_list) {
+    const uint64_t n = *ser_count;
+    for (uint64_t k = blockIdx.x; k < n; k += gridDim.x) {
+      zstd_serial_item(S, ser_list[k], items, status, dst, slot_bytes, lit_scratch, lit_stride);
+      __syncthreads();
+    }
+    return;
+  }
+  const uint32_t item = blockIdx.x;
+  if (zmode && zmode[item] != ZMODE_SERIAL) return;  // decoded by the block-parallel path
+  zstd_serial_item(S, item, items, status, dst, slot_bytes, lit_scratch, lit_stride);
+}
+
 // =================================================================================================
 // Block-parallel path (items whose blocks fit the scratch; k_zstd above is the fallback).
 //
@@ -1229,7 +1248,8 @@ __device__ __forceinline__ uint32_t sym_eval(uint32_t x, uint32_t r0, uint32_t r
 __global__ __launch_bounds__(64) void k_zstd_scan(const ZgItem *items, uint32_t *status, ZBlk *blks,
                                                   uint32_t blk_cap, uint32_t *nblk, uint32_t *zmode,
                                                   uint64_t lit_stride, uint64_t seq_cap, uint32_t force_serial,
-                                                  unsigned long long *counters) {
+                                                  unsigned long long *counters, uint32_t *ser_list,
+                                                  unsigned long long *ser_count) {
   __shared__ ZScanSmem S;
   const uint32_t item = blockIdx.x;
   const ZgItem it = items[item];
@@ -1243,6 +1263,7 @@ __global__ __launch_bounds__(64) void k_zstd_scan(const ZgItem *items, uint32_t 
       nblk[item] = 0;
       zmode[item] = ZMODE_SERIAL;
       if (counters) atomicAdd(&counters[0], 1ull);
+      if (ser_list) ser_list[atomicAdd(ser_count, 1ull)] = item;
     }
     return;
   }
@@ -1432,6 +1453,7 @@ __global__ __launch_bounds__(64) void k_zstd_scan(const ZgItem *items, uint32_t 
     zmode[item] = serial ? ZMODE_SERIAL : (err ? ZMODE_SKIP : ZMODE_PARALLEL);
     if (err && !serial) status[item] = err;
     if (counters && (serial || !err)) atomicAdd(&counters[serial ? 0 : 1], 1ull);  // serial / block-parallel items
+    if (serial && ser_list) ser_list[atomicAdd(ser_count, 1ull)] = item;
   }
 }
 
@@ -3083,19 +3105,20 @@ hipError_t launch_zstd(ZgItem *items, uint32_t *status, uint32_t n_items, uint8_
                        const ZstdScratch &Z, hipStream_t s) {
   if (!n_items) return hipSuccess;
   ZBlk *blks = (ZBlk *)Z.blks;
+  const bool listed = Z.ser_list && Z.ser_count;
   hipLaunchKernelGGL(k_zstd_scan, dim3(n_items), dim3(64), 0, s, items, status, blks, Z.blk_cap, Z.nblk, Z.mode,
-                     Z.lit_stride, Z.seq_cap, Z.force_serial, Z.counters);
+                     Z.lit_stride, Z.seq_cap, Z.force_serial, Z.counters, listed ? Z.ser_list : nullptr,
+                     listed ? Z.ser_count : nullptr);
   const uint64_t recs = (uint64_t)n_items * Z.blk_cap;
   // grids of the record-strided entropy kernels (overridable for tuning: ZGPU_ZSTD_GRID, ZGPU_ZSTD_LGRID)
   static const uint64_t g_cap = [] {
     const char *e = std::getenv("ZGPU_ZSTD_GRID");
-    return e ? std::max<uint64_t>(1, std::strtoull(e, nullptr, 10)) : (uint64_t)256 * 16;
+    return e ? std::max<uint64_t>(1, std::strtoull(e, nullptr, 10)) : (uint64_t)device_cu_count() * 16;
   }();
   static const uint64_t l_cap = [] {
     const char *e = std::getenv("ZGPU_ZSTD_LGRID");
-    // one resident wave of workgroups: 256 CUs x ZG_LIT_GRID_PER_CU workgroups of 256 lanes each (the
-    // decoder compiles to 128 VGPRs: 4 workgroups per CU)
-    return e ? std::max<uint64_t>(1, std::strtoull(e, nullptr, 10)) : (uint64_t)256 * ZG_LIT_GRID_PER_CU;
+    // one resident wave of workgroups: the device's CUs x ZG_LIT_GRID_PER_CU workgroups of 256 lanes each
+    return e ? std::max<uint64_t>(1, std::strtoull(e, nullptr, 10)) : (uint64_t)device_cu_count() * ZG_LIT_GRID_PER_CU;
   }();
   const uint32_t grid = (uint32_t)std::min<uint64_t>(recs, g_cap);
   const uint32_t lgrid = (uint32_t)std::min<uint64_t>(recs, l_cap);
@@ -3108,8 +3131,9 @@ hipError_t launch_zstd(ZgItem *items, uint32_t *status, uint32_t n_items, uint8_
     if (e == hipSuccess) e = hipStreamWaitEvent(Z.side, Z.ev_fork, 0);
     if (e != hipSuccess) return e;
   }
-  // one resident wave of the sequence decoder: 256 CUs x 4 SIMDs x ZG_BLK_WPE waves
-  const uint32_t bgrid = (uint32_t)std::min<uint64_t>(recs, std::max<uint64_t>(g_cap, (uint64_t)256 * 4 * ZG_BLK_WPE));
+  // one resident wave of the sequence decoder: CUs x 4 SIMDs x ZG_BLK_WPE waves
+  const uint32_t bgrid =
+      (uint32_t)std::min<uint64_t>(recs, std::max<uint64_t>(g_cap, (uint64_t)device_cu_count() * 4 * ZG_BLK_WPE));
   hipLaunchKernelGGL(k_zstd_blocks, dim3(bgrid), dim3(64), 0, sq, items, status, blks, Z.blk_cap, Z.nblk, Z.mode,
                      n_items, Z.lit, Z.lit_stride, Z.seq, Z.seq_cap);
   if (fork) {
@@ -3138,8 +3162,15 @@ hipError_t launch_zstd(ZgItem *items, uint32_t *status, uint32_t n_items, uint8_
                      n_items, dst, slot_bytes, Z.lit, Z.lit_stride);
   hipLaunchKernelGGL(k_zstd_exec_item, dim3(n_items * xseg), dim3(64), 0, s, items, status, blks, Z.blk_cap, Z.nblk,
                      Z.mode, dst, slot_bytes, Z.lit, Z.lit_stride, Z.seq, Z.seq_cap, xseg);
-  hipLaunchKernelGGL(k_zstd, dim3(n_items), dim3(64), 0, s, items, status, dst, slot_bytes, Z.lit, Z.lit_stride,
-                     Z.mode);
+  if (!listed) {
+    hipLaunchKernelGGL(k_zstd, dim3(n_items), dim3(64), 0, s, items, status, dst, slot_bytes, Z.lit, Z.lit_stride,
+                       Z.mode, nullptr, nullptr);
+  } else if (Z.launch_serial) {
+    // the compacted serial items: a persistent grid of at most 4 waves per CU
+    const uint32_t sgrid = (uint32_t)std::min<uint64_t>(n_items, (uint64_t)device_cu_count() * 4);
+    hipLaunchKernelGGL(k_zstd, dim3(sgrid), dim3(64), 0, s, items, status, dst, slot_bytes, Z.lit, Z.lit_stride,
+                       Z.mode, Z.ser_list, Z.ser_count);
+  }
   return hipGetLastError();
 }
 

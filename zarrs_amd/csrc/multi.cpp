@@ -76,35 +76,39 @@ int zgpu_retrieve_array_subset_multi(zgpu_chain *const *chains, uint32_t n_dev, 
     }
     const bool dev_out = (flags & ZGPU_OUT_DEVICE) != 0;
     const int out_dev = ctx_device(chain_ctx(chains[0]));
+    // runs on its own host thread per device: every failure (HIP, allocation, exceptions) is recorded
+    // in the device's Part, never thrown across the thread boundary
     auto work = [&](uint32_t d) {
       Part &P = parts[d];
       if (!P.rows) return;
-      std::vector<uint64_t> s(sel_start, sel_start + nd), n(sel_shape, sel_shape + nd);
-      s[0] = sel_start[0] + P.row0;
-      n[0] = P.rows;
-      uint8_t *dst = (uint8_t *)out + P.row0 * row_bytes;
-      const int dev = ctx_device(chain_ctx(chains[d]));
+      zgpu_ctx *C = chain_ctx(chains[d]);
       void *scratch = nullptr;
-      hipStream_t st = nullptr;
-      if (dev_out && d != 0) {  // decode into this device's HBM, then one peer copy into `out`
-        if (hipSetDevice(dev) != hipSuccess || hipMalloc(&scratch, std::max<uint64_t>(P.rows * row_bytes, 1)) != hipSuccess) {
-          P.rc = ZGPU_HIP_ERROR;
-          P.err = "hipMalloc of the device slab failed";
-          return;
+      try {
+        std::vector<uint64_t> s(sel_start, sel_start + nd), n(sel_shape, sel_shape + nd);
+        s[0] = sel_start[0] + P.row0;
+        n[0] = P.rows;
+        uint8_t *dst = (uint8_t *)out + P.row0 * row_bytes;
+        const int dev = ctx_device(C);
+        if (dev_out && d != 0) {  // decode into this device's HBM (the context's pool), then one peer copy
+          scratch = ctx_dev_alloc(C, std::max<uint64_t>(P.rows * row_bytes, 1));
+          if (!scratch) {
+            P.rc = ZGPU_HIP_ERROR;
+            P.err = "allocation of the device slab failed";
+            return;
+          }
+          dst = (uint8_t *)scratch;
         }
-        dst = (uint8_t *)scratch;
-      }
-      P.rc = zgpu_retrieve_array_subset(chains[d], nd, array_shape, chunk_shape, chunk_ptrs, chunk_lens, s.data(),
-                                        n.data(), dst, flags, nullptr);
-      if (P.rc) P.err = zgpu_last_error(nullptr);
-      if (scratch) {
-        if (!P.rc) {
+        P.rc = zgpu_retrieve_array_subset(chains[d], nd, array_shape, chunk_shape, chunk_ptrs, chunk_lens, s.data(),
+                                          n.data(), dst, flags, nullptr);
+        if (P.rc) P.err = zgpu_last_error(nullptr);
+        if (scratch && !P.rc) {
           hipError_t e = hipSetDevice(dev);
           // the direct xGMI path for the copy below; without peer access the runtime still copies
           // (staged), so a refusal is not an error
           if (e == hipSuccess && dev != out_dev && hipDeviceEnablePeerAccess(out_dev, 0) != hipSuccess)
             (void)hipGetLastError();
-          if (e == hipSuccess) e = hipStreamCreateWithFlags(&st, hipStreamNonBlocking);
+          hipStream_t st = e == hipSuccess ? ctx_copy_stream(C) : nullptr;
+          if (e == hipSuccess && !st) e = hipErrorInvalidValue;
           if (e == hipSuccess)
             e = hipMemcpyPeerAsync((uint8_t *)out + P.row0 * row_bytes, out_dev, scratch, dev, P.rows * row_bytes, st);
           if (e == hipSuccess) e = hipStreamSynchronize(st);
@@ -112,11 +116,15 @@ int zgpu_retrieve_array_subset_multi(zgpu_chain *const *chains, uint32_t n_dev, 
             P.rc = ZGPU_HIP_ERROR;
             P.err = std::string("peer copy: ") + hipGetErrorString(e);
           }
-          if (st) (void)hipStreamDestroy(st);
         }
-        (void)hipSetDevice(dev);
-        (void)hipFree(scratch);
+      } catch (const std::exception &e) {
+        P.rc = ZGPU_HIP_ERROR;
+        P.err = e.what();
+      } catch (...) {
+        P.rc = ZGPU_HIP_ERROR;
+        P.err = "unknown exception";
       }
+      if (scratch) ctx_dev_free(C, scratch);
     };
     std::vector<std::thread> threads;
     for (uint32_t d = 1; d < n_dev; d++)

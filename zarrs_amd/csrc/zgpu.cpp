@@ -38,7 +38,7 @@ thread_local std::string g_last_error;
 // device counters in the plan's control block (u64 each, cleared per execute)
 enum { CTR_ENC_BYTES = 0, CTR_ZSTD_SERIAL = 1, CTR_ZSTD_PARALLEL = 2, CTR_BLOSC_RERUN = 3, CTR_N = 4 };
 // internal ctl slots (not reported): a cached blosc layout was outgrown (the execution is re-run)
-enum { CTR_BLOSC_OVF = 31, CTR_SCRATCH = 30 };  // not reported (device-side flags / sinks)
+enum { CTR_BLOSC_OVF = 31, CTR_SCRATCH = 30, CTR_ZSTD_NSER = 29 };  // not reported (device-side flags / sinks)
 thread_local uint64_t g_last_counters[CTR_N];
 // UnexpectedChunkDecodedSize detail of the last call's first DECODED_SIZE_MISMATCH descriptor
 struct SizeDetail {
@@ -217,7 +217,7 @@ struct zgpu_plan {
     size_t n = 0;
   };
   Grow bl_info, bl_bases, bl_subs, bl_sub_status, bl_sub_kind, bl_blocks, bl_tmp, bl_zblks, bl_znblk, bl_zmode,
-      bl_zlit, bl_zseq, bl_zaux;
+      bl_zlit, bl_zseq, bl_zaux, bl_zser;
   uint8_t *bl_h = nullptr;  // pinned: BlInfo read-back (first execution)
   size_t bl_h_n = 0;
   void *grow(Grow &g, size_t bytes) {
@@ -240,13 +240,17 @@ struct zgpu_plan {
   uint8_t *last_out = nullptr;  // output of the last enqueue (a blosc layout overflow re-runs into it)
   BlCaps bl_caps{};             // blosc stream-table capacities recorded by the first execution
   bool bl_caps_valid = false, bl_caps_seen = false;
+  // zstd serial fallback: skipped once an execution of this plan had no serial item (a later one that
+  // has some is re-run by plan_statuses with the fallback launched)
+  bool zstd_serial_off = false, zstd_serial_skipped = false;
+  uint32_t *d_zser = nullptr;
 
   ~zgpu_plan() {
     if (!ctx) return;
     void *bufs[] = {d_items, d_items_init, d_geom, d_shards, d_index, d_shard_status, d_mids, d_mids_init,
                     d_mid_status, d_shard_status2, d_mid_shards, d_index2,
                     d_pool[0], d_pool[1], zs.blks, zs.nblk, zs.mode, zs.lit, zs.seq, d_ctl,
-                    d_enc_stage};
+                    d_enc_stage, d_zser};
     for (void *b : bufs) ctx->dev_free(b);
     if (zside) {
       (void)hipStreamSynchronize(zside);
@@ -255,7 +259,7 @@ struct zgpu_plan {
     for (hipEvent_t e : zev)
       if (e) (void)hipEventDestroy(e);
     for (Grow *g : {&bl_info, &bl_bases, &bl_subs, &bl_sub_status, &bl_sub_kind, &bl_blocks, &bl_tmp, &bl_zblks,
-                    &bl_znblk, &bl_zmode, &bl_zlit, &bl_zseq, &bl_zaux})
+                    &bl_znblk, &bl_zmode, &bl_zlit, &bl_zseq, &bl_zaux, &bl_zser})
       ctx->dev_free(g->p);
     ctx->host_free(bl_h);
     ctx->host_free(h_ctl);
@@ -277,6 +281,28 @@ zgpu_ctx *zgpu::chain_ctx(const zgpu_chain *c) { return c->ctx; }
 const Chain &zgpu::chain_model(const zgpu_chain *c) { return *c->chain; }
 bool zgpu::chain_validates(const zgpu_chain *c) { return c->validate; }
 int zgpu::ctx_device(const zgpu_ctx *c) { return c->device; }
+void *zgpu::ctx_dev_alloc(zgpu_ctx *c, size_t bytes) {  // nullptr on failure
+  std::lock_guard<std::mutex> lk(c->mu);
+  try {
+    HIPCHK(hipSetDevice(c->device));
+    return c->dev_alloc(bytes);
+  } catch (const HipFail &) {
+    return nullptr;
+  }
+}
+void zgpu::ctx_dev_free(zgpu_ctx *c, void *p) {
+  std::lock_guard<std::mutex> lk(c->mu);
+  c->dev_free(p);
+}
+hipStream_t zgpu::ctx_copy_stream(zgpu_ctx *c) {  // nullptr on failure
+  std::lock_guard<std::mutex> lk(c->mu);
+  if (!c->copy[1] && (hipSetDevice(c->device) != hipSuccess ||
+                      hipStreamCreateWithFlags(&c->copy[1], hipStreamNonBlocking) != hipSuccess)) {
+    c->copy[1] = nullptr;
+    return nullptr;
+  }
+  return c->copy[1];
+}
 
 // composed permutation of all array->array codecs: encoded axis a <-> decoded axis m[a]
 static void composed_axes(const Chain &c, uint32_t nd, uint32_t *m) {
@@ -643,6 +669,8 @@ static void plan_upload(zgpu_plan &P, hipStream_t us = nullptr) {
         P.zs.mode = (uint32_t *)C.dev_alloc(ni * 4);
         P.zs.lit = (uint8_t *)C.dev_alloc(ni * P.zs.lit_stride);
         P.zs.seq = (uint32_t *)C.dev_alloc(ni * P.zs.seq_cap * 12);
+        P.d_zser = (uint32_t *)C.dev_alloc(ni * 4);
+        P.zs.ser_list = P.d_zser;
       }
     }
   }
@@ -652,6 +680,7 @@ static void plan_upload(zgpu_plan &P, hipStream_t us = nullptr) {
   P.d_counter = (unsigned long long *)P.d_ctl;
   P.d_status = (uint32_t *)(P.d_ctl + 256);
   P.zs.counters = P.d_counter + CTR_ZSTD_SERIAL;
+  P.zs.ser_count = P.d_counter + CTR_ZSTD_NSER;
   if (const char *e = std::getenv("ZGPU_ZSTD_FORCE_SERIAL")) P.zs.force_serial = std::atoi(e) != 0;
   if (!P.shards.empty()) {
     P.d_shards = (ZgShard *)C.dev_alloc(P.shards.size() * sizeof(ZgShard));
@@ -749,6 +778,9 @@ static void blosc_stage(zgpu_plan &P, const Stage &st, hipStream_t s) {
     D.zs.seq = (uint32_t *)P.grow(P.bl_zseq, D.n_sub * D.zs.seq_cap * 12);
     D.zs.counters = P.zs.counters;
     D.zs.force_serial = P.zs.force_serial;
+    D.zs.ser_list = (uint32_t *)P.grow(P.bl_zser, D.n_sub * 4);
+    D.zs.ser_count = P.zs.ser_count;
+    D.zs.launch_serial = P.zs.launch_serial;
     P.zstd_fork(D.zs, s);
   }
   // the layout (bases, inert tails past this execution's totals) is always computed on the device
@@ -762,6 +794,8 @@ static void plan_enqueue(zgpu_plan &P, uint8_t *out, hipStream_t s) {
   P.last_out = out;
   HIPCHK(hipMemsetAsync(P.d_ctl, 0, P.ctl_bytes, s));
   if (!ni) return;
+  P.zs.launch_serial = P.zstd_serial_off ? 0u : 1u;
+  P.zstd_serial_skipped = P.zstd_serial_off;
   // stages rewrite each item's {src,len} in place; a chain with none reads the uploaded table as is
   const bool mutates = P.sharded || !P.stages.empty();
   ZgItem *items = mutates ? P.d_items : P.d_items_init;
@@ -852,6 +886,17 @@ static int plan_statuses(zgpu_plan &P, int32_t *status, hipStream_t s) {
     HIPCHK(hipMemcpyAsync(P.h_ctl, P.d_ctl, P.ctl_bytes, hipMemcpyDeviceToHost, s));
     HIPCHK(hipStreamSynchronize(s));
     ((uint64_t *)P.h_ctl)[CTR_BLOSC_RERUN] = 1;
+  }
+  if (((const uint64_t *)P.h_ctl)[CTR_ZSTD_SERIAL]) {
+    if (P.zstd_serial_skipped) {
+      // this input has items for the serial zstd decoder, whose launch the plan skipped: re-run with it
+      P.zstd_serial_off = false;
+      plan_enqueue(P, P.last_out, s);
+      HIPCHK(hipMemcpyAsync(P.h_ctl, P.d_ctl, P.ctl_bytes, hipMemcpyDeviceToHost, s));
+      HIPCHK(hipStreamSynchronize(s));
+    }
+  } else if (((const uint64_t *)P.h_ctl)[CTR_ZSTD_PARALLEL]) {
+    P.zstd_serial_off = true;  // no serial item: later executions do not launch the fallback
   }
   std::memcpy(P.last_counters, P.h_ctl, sizeof(P.last_counters));
   for (int k = 0; k < CTR_N; k++) g_last_counters[k] += P.last_counters[k];
@@ -1505,13 +1550,18 @@ int64_t zgpu_chain_encoded_size(const zgpu_chain *ch, uint32_t nd, const uint64_
   return chain_fixed_encoded_size(*ch->chain, n);
 }
 
-// Upper bound of one chunk's encoded size: the fixed size, or for sharding_indexed over a fixed-size
-// inner chain every inner chunk present plus the index (ShardingCodec::encoded_shard_bounded_size,
-// sharding_codec.rs:924-945, BytesRepresentation::BoundedSize); -1 if unbounded.
+// Upper bound of one chunk's encoded size: the fixed size, a compressing chain's bounded size
+// (chain_encoded_bound), or for sharding_indexed every inner chunk at its bound plus the index
+// (ShardingCodec::encoded_shard_bounded_size, sharding_codec.rs:924-945, BytesRepresentation::
+// BoundedSize); -1 if unbounded.
 int64_t zgpu_chain_encoded_bound(const zgpu_chain *ch, uint32_t nd, const uint64_t *chunk_shape) {
   if (!ch || !chunk_shape || nd == 0 || nd > ZGPU_MAX_DIMS) return -1;
   const Chain &c = *ch->chain;
-  if (c.a2b.kind != CodecKind::Sharding) return zgpu_chain_encoded_size(ch, nd, chunk_shape);
+  if (c.a2b.kind != CodecKind::Sharding) {
+    uint64_t n = 1;
+    for (uint32_t d = 0; d < nd; d++) n *= chunk_shape[d];
+    return chain_encoded_bound(c, n);
+  }
   if (!c.a2a.empty() || !c.b2b.empty() || c.a2b.inner_shape.size() != nd) return -1;
   uint64_t n_inner = 1, inner_n = 1;
   for (uint32_t d = 0; d < nd; d++) {
@@ -1520,7 +1570,7 @@ int64_t zgpu_chain_encoded_bound(const zgpu_chain *ch, uint32_t nd, const uint64
     n_inner *= chunk_shape[d] / is;
     inner_n *= is;
   }
-  const int64_t E = chain_fixed_encoded_size(*c.a2b.inner, inner_n);
+  const int64_t E = chain_encoded_bound(*c.a2b.inner, inner_n);
   const int64_t X = chain_fixed_encoded_size(*c.a2b.index, n_inner * 2);
   if (E < 0 || X < 0) return -1;
   return (int64_t)n_inner * E + X;
@@ -1532,21 +1582,10 @@ int64_t zgpu_chain_encoded_bound(const zgpu_chain *ch, uint32_t nd, const uint64
 // into device buffers h_dst[i] (chunk origins h_starts[i*nd..]): one gather (transposes + endianness +
 // innermost shuffle, fill past the array edge), then one k_crc32c_encode launch per crc32c codec.
 // Enqueues only (no synchronisation); d_tab: device table of n dst pointers + n*nd origins.
-static int encode_fixed(zgpu_ctx *C, const Chain &c, uint32_t nd, const uint64_t *chunk_shape, const void *array,
-                        const uint64_t *array_shape, const std::vector<uint64_t> &h_tab, uint64_t n,
-                        std::vector<void *> &owned, hipStream_t s, ZgEncode *out_P = nullptr) {
-  if (c.a2b.kind != CodecKind::Bytes) return set_err(ZGPU_UNSUPPORTED, "encode: array->bytes codec must be bytes");
-  for (const Codec &k : c.a2a)
-    if (k.order.size() != nd) return set_err(ZGPU_INVALID_ARGUMENT, "transpose order rank != ndim");
-  bool shuffle = false;
-  int n_start = 0;
-  for (size_t i = 0; i < c.b2b.size(); i++) {
-    const Codec &k = c.b2b[i];
-    if (k.kind == CodecKind::Shuffle && i == 0 && k.elementsize == c.es) shuffle = true;
-    else if (k.kind == CodecKind::Crc32c) n_start += k.at_start ? 1 : 0;
-    else return set_err(ZGPU_UNSUPPORTED, "encode: only transpose / bytes / numcodecs.shuffle (innermost, "
-                                          "elementsize = data type size) / crc32c run on the GPU write path");
-  }
+// The gather's parameters: the chain's transposes, bytes endianness and (shuffle) an innermost
+// numcodecs.shuffle over the data type size, chunk data at data_off bytes into each destination.
+static ZgEncode encode_params(const Chain &c, uint32_t nd, const uint64_t *chunk_shape, const uint64_t *array_shape,
+                              bool shuffle, uint64_t data_off) {
   ZgEncode P{};
   P.nd = nd;
   P.es = c.es;
@@ -1555,7 +1594,7 @@ static int encode_fixed(zgpu_ctx *C, const Chain &c, uint32_t nd, const uint64_t
   P.shuffle = shuffle;
   P.nelem = 1;
   for (uint32_t d = 0; d < nd; d++) P.nelem *= chunk_shape[d];
-  P.data_off = 4ull * n_start;
+  P.data_off = data_off;
   uint32_t m[ZG_MAXD];
   composed_axes(c, nd, m);
   uint64_t stride = 1;
@@ -1584,6 +1623,26 @@ static int encode_fixed(zgpu_ctx *C, const Chain &c, uint32_t nd, const uint64_t
     }
   }
   std::memcpy(P.fill, c.fill, sizeof(P.fill));
+  P.aligned = 0;
+  return P;
+}
+
+static int encode_fixed(zgpu_ctx *C, const Chain &c, uint32_t nd, const uint64_t *chunk_shape, const void *array,
+                        const uint64_t *array_shape, const std::vector<uint64_t> &h_tab, uint64_t n,
+                        std::vector<void *> &owned, hipStream_t s, ZgEncode *out_P = nullptr) {
+  if (c.a2b.kind != CodecKind::Bytes) return set_err(ZGPU_UNSUPPORTED, "encode: array->bytes codec must be bytes");
+  for (const Codec &k : c.a2a)
+    if (k.order.size() != nd) return set_err(ZGPU_INVALID_ARGUMENT, "transpose order rank != ndim");
+  bool shuffle = false;
+  int n_start = 0;
+  for (size_t i = 0; i < c.b2b.size(); i++) {
+    const Codec &k = c.b2b[i];
+    if (k.kind == CodecKind::Shuffle && i == 0 && k.elementsize == c.es) shuffle = true;
+    else if (k.kind == CodecKind::Crc32c) n_start += k.at_start ? 1 : 0;
+    else return set_err(ZGPU_UNSUPPORTED, "encode: only transpose / bytes / numcodecs.shuffle (innermost, "
+                                          "elementsize = data type size) / crc32c / gzip run on the GPU write path");
+  }
+  ZgEncode P = encode_params(c, nd, chunk_shape, array_shape, shuffle, 4ull * n_start);
   bool aligned = (P.data_off % c.es) == 0;
   for (uint64_t i = 0; i < n; i++)
     if (h_tab[i] % 16) aligned = false;
@@ -1601,6 +1660,140 @@ static int encode_fixed(zgpu_ctx *C, const Chain &c, uint32_t nd, const uint64_t
     if (k.at_start) lo -= 4;
     len += 4;
   }
+  return ZGPU_OK;
+}
+
+static bool chain_compresses(const Chain &c) {
+  for (const Codec &k : c.b2b)
+    if (k.kind == CodecKind::Gzip || k.kind == CodecKind::Zstd || k.kind == CodecKind::Blosc) return true;
+  return false;
+}
+
+// CodecChain::encode (codec_chain.rs:528-555) of a chain with a compressor, for n chunks whose origins
+// are origins[i*nd..]: the gather (transposes, endianness, innermost shuffle) into 64 B-headroom
+// slots, then the bytes->bytes codecs in metadata order over the items {src, len}: crc32c appended /
+// prepended in place, gzip into the other slot pool (k_gzip_encode). Enqueues only; on return the
+// device item table and statuses describe every chunk's encoded bytes (inside scratch `owned`), and
+// *d_tab_out is the device table [n gather destinations | n*nd origins].
+static int encode_var(zgpu_ctx *C, const Chain &c, uint32_t nd, const uint64_t *chunk_shape, const void *array,
+                      const uint64_t *array_shape, const uint64_t *origins, uint64_t n, std::vector<void *> &owned,
+                      hipStream_t s, ZgItem **d_items_out, uint32_t **d_status_out, uint64_t **d_tab_out,
+                      ZgEncode *P_out) {
+  if (c.a2b.kind != CodecKind::Bytes) return set_err(ZGPU_UNSUPPORTED, "encode: array->bytes codec must be bytes");
+  for (const Codec &k : c.a2a)
+    if (k.order.size() != nd) return set_err(ZGPU_INVALID_ARGUMENT, "transpose order rank != ndim");
+  uint64_t nelem = 1;
+  for (uint32_t d = 0; d < nd; d++) nelem *= chunk_shape[d];
+  bool shuffle = false;
+  uint64_t size = nelem * c.es, max_size = size;
+  uint32_t n_crc = 0;
+  for (size_t i = 0; i < c.b2b.size(); i++) {
+    const Codec &k = c.b2b[i];
+    if (k.kind == CodecKind::Shuffle && i == 0 && k.elementsize == c.es) {
+      shuffle = true;
+    } else if (k.kind == CodecKind::Crc32c) {
+      size += 4;
+      n_crc++;
+    } else if (k.kind == CodecKind::Gzip) {
+      size = gzip_bound(size);
+    } else {
+      return set_err(ZGPU_UNSUPPORTED, "encode: only transpose / bytes / numcodecs.shuffle (innermost, elementsize = "
+                                       "data type size) / crc32c / gzip run on the GPU write path");
+    }
+    max_size = std::max(max_size, size);
+  }
+  if (n_crc > 14) return set_err(ZGPU_UNSUPPORTED, "encode: too many crc32c codecs");
+  constexpr uint64_t HR = 64;  // headroom in front of a slot's bytes (crc32c at the start)
+  const uint64_t pitch = (HR + max_size + 4 * n_crc + 16 + 255) & ~(uint64_t)255;
+  bool gz = false;
+  for (const Codec &k : c.b2b) gz = gz || k.kind == CodecKind::Gzip;
+  uint8_t *pool[2] = {(uint8_t *)C->dev_alloc(std::max<uint64_t>(n * pitch, 1)), nullptr};
+  owned.push_back(pool[0]);
+  if (gz) {
+    pool[1] = (uint8_t *)C->dev_alloc(std::max<uint64_t>(n * pitch, 1));
+    owned.push_back(pool[1]);
+  }
+  // gather into pool 0
+  std::vector<uint64_t> tab(n * (1 + nd));
+  for (uint64_t i = 0; i < n; i++) tab[i] = (uint64_t)(pool[0] + i * pitch + HR);
+  std::memcpy(tab.data() + n, origins, n * nd * 8);
+  uint64_t *d_tab = (uint64_t *)C->dev_alloc(std::max<size_t>(tab.size() * 8, 8));
+  owned.push_back(d_tab);
+  HIPCHK(hipMemcpyAsync(d_tab, tab.data(), tab.size() * 8, hipMemcpyHostToDevice, s));
+  ZgEncode P = encode_params(c, nd, chunk_shape, array_shape, shuffle, 0);
+  P.aligned = (c.es <= 16 && (HR % 16) == 0 && (pitch % 16) == 0) ? 1u : 0u;
+  if (n) HIPCHK(launch_encode_gather(d_tab, d_tab + n, (const uint8_t *)array, P, (uint32_t)n, s));
+  // items over the gathered chunks
+  std::vector<ZgItem> items(n);
+  for (uint64_t i = 0; i < n; i++) items[i] = ZgItem{tab[i], nelem * c.es, (uint32_t)i, 0, 0, 0};
+  ZgItem *d_items = (ZgItem *)C->dev_alloc(std::max<uint64_t>(n * sizeof(ZgItem), 1));
+  uint32_t *d_status = (uint32_t *)C->dev_alloc(std::max<uint64_t>(n * 4, 4));
+  owned.push_back(d_items);
+  owned.push_back(d_status);
+  HIPCHK(hipMemcpyAsync(d_items, items.data(), n * sizeof(ZgItem), hipMemcpyHostToDevice, s));
+  HIPCHK(hipMemsetAsync(d_status, 0, std::max<uint64_t>(n * 4, 4), s));
+  int cur = 0;
+  uint32_t *sym = nullptr;
+  for (size_t i = 0; i < c.b2b.size(); i++) {
+    const Codec &k = c.b2b[i];
+    if (k.kind == CodecKind::Crc32c) {
+      HIPCHK(launch_crc32c_items(d_items, d_status, (uint32_t)n, k.at_start ? 1 : 0, s));
+    } else if (k.kind == CodecKind::Gzip) {
+      if (!sym) {
+        sym = (uint32_t *)C->dev_alloc((uint64_t)gzip_encode_grid((uint32_t)std::max<uint64_t>(n, 1)) * GZE_BLK_SYMS * 4);
+        owned.push_back(sym);
+      }
+      cur ^= 1;
+      HIPCHK(launch_gzip_encode(d_items, d_status, (uint32_t)n, pool[cur], pitch, sym, k.level, s));
+    }
+  }
+  *d_items_out = d_items;
+  *d_status_out = d_status;
+  if (d_tab_out) *d_tab_out = d_tab;
+  if (P_out) *P_out = P;
+  return ZGPU_OK;
+}
+
+// first non-zero of n device statuses (read back synchronously), 0 if none
+static int first_status(const uint32_t *d_status, uint64_t n, hipStream_t s) {
+  std::vector<uint32_t> h(n);
+  if (n) HIPCHK(hipMemcpyAsync(h.data(), d_status, n * 4, hipMemcpyDeviceToHost, s));
+  HIPCHK(hipStreamSynchronize(s));
+  for (uint32_t v : h)
+    if (v) return (int)v;
+  return 0;
+}
+
+// a chain with a compressor, unsharded: encode_var, then every chunk copied to its destination
+static int encode_compressed(zgpu_ctx *C, const Chain &c, uint32_t nd, const uint64_t *chunk_shape, const void *array,
+                             const uint64_t *array_shape, const zgpu_encode_desc *descs, uint64_t n, uint64_t *enc_lens,
+                             std::vector<void *> &owned, hipStream_t s) {
+  uint64_t nelem = 1;
+  for (uint32_t d = 0; d < nd; d++) nelem *= chunk_shape[d];
+  const int64_t bound = chain_encoded_bound(c, nelem);
+  if (bound < 0) return set_err(ZGPU_UNSUPPORTED, "encode: the chain's encoded size is not bounded");
+  for (uint64_t i = 0; i < n; i++)
+    if (!descs[i].dst || descs[i].dst_cap < (uint64_t)bound)
+      return set_err(ZGPU_INVALID_ARGUMENT, "encode: destination missing or smaller than the encoded bound");
+  std::vector<uint64_t> org(n * nd), dc(2 * n);
+  for (uint64_t i = 0; i < n; i++) {
+    for (uint32_t d = 0; d < nd; d++) org[i * nd + d] = descs[i].chunk_start[d];
+    dc[i] = (uint64_t)descs[i].dst;
+    dc[n + i] = descs[i].dst_cap;
+  }
+  ZgItem *items = nullptr;
+  uint32_t *st = nullptr;
+  int rc = encode_var(C, c, nd, chunk_shape, array, array_shape, org.data(), n, owned, s, &items, &st, nullptr, nullptr);
+  if (rc) return rc;
+  uint64_t *d_dc = (uint64_t *)C->dev_alloc(8 * (3 * n));
+  owned.push_back(d_dc);
+  HIPCHK(hipMemcpyAsync(d_dc, dc.data(), 16 * n, hipMemcpyHostToDevice, s));
+  HIPCHK(launch_encode_place(items, st, d_dc, d_dc + n, d_dc + 2 * n, (uint32_t)n, s));
+  std::vector<uint64_t> lens(n);
+  HIPCHK(hipMemcpyAsync(lens.data(), d_dc + 2 * n, 8 * n, hipMemcpyDeviceToHost, s));
+  rc = first_status(st, n, s);
+  if (rc) return set_err(rc, std::string("encode: ") + zgpu_status_name(rc));
+  if (enc_lens) std::memcpy(enc_lens, lens.data(), 8 * n);
   return ZGPU_OK;
 }
 
@@ -1627,9 +1820,66 @@ static int encode_sharded(zgpu_ctx *C, const Chain &top, uint32_t nd, const uint
     n_inner *= cps[d];
     inner_n *= is;
   }
-  const int64_t E = chain_fixed_encoded_size(inner, inner_n);
-  if (E < 0) return set_err(ZGPU_UNSUPPORTED, "encode: the inner chain of sharding_indexed must be fixed-size");
   const int64_t X = chain_fixed_encoded_size(xc, n_inner * 2);
+  if (chain_compresses(inner)) {
+    // inner chunks of variable length: encode_var over all inner chunks of all shards, then the
+    // variable-length layout (C write order, all-fill inner chunks omitted) and the index crc32c
+    const int64_t EB = chain_encoded_bound(inner, inner_n);
+    if (EB < 0) return set_err(ZGPU_UNSUPPORTED, "encode: the inner chain's encoded size is not bounded");
+    const uint64_t bound = n_inner * (uint64_t)EB + (uint64_t)X;
+    uint64_t cap = UINT64_MAX;
+    for (uint64_t i = 0; i < n; i++) {
+      if (!descs[i].dst || descs[i].dst_cap < bound)
+        return set_err(ZGPU_INVALID_ARGUMENT, "encode: destination missing or smaller than the shard's bounded size");
+      cap = std::min(cap, descs[i].dst_cap);
+    }
+    const uint64_t n_chunks = n * n_inner;
+    std::vector<uint64_t> org(n_chunks * nd);
+    for (uint64_t i = 0; i < n; i++)
+      for (uint64_t k = 0; k < n_inner; k++) {
+        uint64_t rem = k;
+        for (int d = (int)nd - 1; d >= 0; d--) {
+          org[(i * n_inner + k) * nd + d] = descs[i].chunk_start[d] + (rem % cps[d]) * top.a2b.inner_shape[d];
+          rem /= cps[d];
+        }
+      }
+    ZgItem *items = nullptr;
+    uint32_t *st = nullptr;
+    uint64_t *d_tab = nullptr;
+    ZgEncode IP{};
+    int rc = encode_var(C, inner, nd, top.a2b.inner_shape.data(), array, array_shape, org.data(), n_chunks, owned, s,
+                        &items, &st, &d_tab, &IP);
+    if (rc) return rc;
+    uint64_t *d_sh = (uint64_t *)C->dev_alloc(8 * (3 * n + n_chunks));
+    uint32_t *d_nf = (uint32_t *)C->dev_alloc(4 * std::max<uint64_t>(n_chunks, 1) + 4 * n);
+    owned.push_back(d_sh);
+    owned.push_back(d_nf);
+    std::vector<uint64_t> hd(n);
+    for (uint64_t i = 0; i < n; i++) hd[i] = (uint64_t)descs[i].dst;
+    HIPCHK(hipMemcpyAsync(d_sh, hd.data(), 8 * n, hipMemcpyHostToDevice, s));
+    uint64_t *d_index_ptr = d_sh + n, *d_len = d_sh + 2 * n, *d_off = d_sh + 3 * n;
+    uint32_t *d_shst = d_nf + n_chunks;
+    int n_pre = 0;
+    for (const Codec &k : xc.b2b) n_pre += k.at_start ? 1 : 0;
+    ZgShardLayoutArgs A{n_inner, 0, cap, (uint64_t)X, 4ull * n_pre, top.a2b.at_start ? 1u : 0u,
+                        xc.a2b.big_endian ? 1u : 0u};
+    HIPCHK(launch_shard_encode_var(d_tab + n_chunks, (const uint8_t *)array, IP, (uint32_t)n_chunks, d_nf, items, st, A,
+                                   d_sh, d_off, d_index_ptr, d_len, d_shst, (uint32_t)n, s));
+    uint64_t lo = 4ull * n_pre, len = n_inner * 16;
+    for (const Codec &k : xc.b2b) {
+      HIPCHK(launch_crc32c_encode(d_index_ptr, (uint32_t)n, lo, len, k.at_start ? 1 : 0, s));
+      if (k.at_start) lo -= 4;
+      len += 4;
+    }
+    HIPCHK(hipMemcpyAsync(enc_lens, d_len, 8 * n, hipMemcpyDeviceToHost, s));
+    rc = first_status(st, n_chunks, s);
+    if (!rc) rc = first_status(d_shst, n, s);
+    if (rc) return set_err(rc == 1 ? ZGPU_HIP_ERROR : rc, std::string("encode: ") + zgpu_status_name(rc));
+    return ZGPU_OK;
+  }
+  const int64_t E = chain_fixed_encoded_size(inner, inner_n);
+  if (E < 0) return set_err(ZGPU_UNSUPPORTED, "encode: the inner chain of sharding_indexed must be fixed-size or "
+                                              "compressed by gzip");
   const uint64_t bound = n_inner * (uint64_t)E + (uint64_t)X;
   for (uint64_t i = 0; i < n; i++)
     if (!descs[i].dst || descs[i].dst_cap < bound)
@@ -1708,6 +1958,12 @@ int zgpu_encode_chunks(zgpu_chain *ch, uint32_t nd, const uint64_t *chunk_shape,
       HIPCHK(hipStreamSynchronize(s));
       if (!rc && enc_lens) std::memcpy(enc_lens, hl, 8 * n);
       C->host_free(hl);
+    } else if (chain_compresses(c)) {
+      uint64_t *hl = (uint64_t *)C->host_alloc(8 * n);
+      rc = encode_compressed(C, c, nd, chunk_shape, array, array_shape, descs, n, hl, owned, s);
+      HIPCHK(hipStreamSynchronize(s));
+      if (!rc && enc_lens) std::memcpy(enc_lens, hl, 8 * n);
+      C->host_free(hl);
     } else {
       const int64_t enc_size = chain_fixed_encoded_size(c, [&] {
         uint64_t e = 1;
@@ -1748,6 +2004,8 @@ int zgpu_encode_batch(zgpu_chain *ch, uint32_t nd, const uint64_t *chunk_shape, 
                       void *hip_stream) {
   if (ch && ch->chain->a2b.kind == CodecKind::Sharding)
     return set_err(ZGPU_INVALID_ARGUMENT, "encode: sharding_indexed chunks have variable lengths: zgpu_encode_chunks");
+  if (ch && chain_compresses(*ch->chain))
+    return set_err(ZGPU_INVALID_ARGUMENT, "encode: compressed chunks have variable lengths: zgpu_encode_chunks");
   return zgpu_encode_chunks(ch, nd, chunk_shape, array, array_shape, descs, n, flags, nullptr, hip_stream);
 }
 

@@ -13,8 +13,12 @@ read is partitioned and each rank decodes its share on its own GPU with no data-
                    its rows of the root's output (grouped send/recv: RCCL over xGMI on GPUs, gloo
                    on CPU), skipped at N=1
 
-  gather_regions   chunk-partitioned ranks (LPT): every rank's chunk boxes of one subset packed into a
-                   single message each and unpacked on the root
+  gather_regions   chunk-partitioned ranks (LPT): every rank's chunk boxes of one subset; boxes that are
+                   contiguous runs of the subset are received straight into place, the others are
+                   packed into one message per rank and unpacked on the root
+
+A process group whose backend cannot move device tensors (gloo) gets device data staged through
+host memory (tests put two ranks on one GPU that way; RCCL/xGMI moves HBM directly).
 
 retrieve_array_subset_distributed ties them together for a zarrs_amd.Array (or anything with the
 same retrieve_array_subset_into(start, shape, out) method).
@@ -126,6 +130,21 @@ def chunk_boxes(array_shape, chunk_shape, start, shape):
     return out
 
 
+def _host_staged(group) -> bool:
+    """True when the group's backend moves host tensors only (gloo): device data is staged."""
+    import torch.distributed as dist
+    return dist.is_initialized() and dist.get_backend(group) == "gloo"
+
+
+def _contiguous_in(bs, shape) -> bool:
+    """A box of shape `bs` inside a C-order array of shape `shape` is one contiguous run: after the
+    leading extent-1 axes, every axis but the first non-unit one spans the whole array."""
+    i = 0
+    while i < len(bs) - 1 and int(bs[i]) == 1:
+        i += 1
+    return all(int(b) == int(s) for b, s in zip(bs[i + 1:], shape[i + 1:]))
+
+
 def gather_regions(local, boxes_by_rank, sub_start, sub_shape, dst: int = 0, group=None, out=None):
     """Assemble an array subset on group rank `dst` from chunk-partitioned ranks (C5: chunks
     LPT-partitioned over the GPUs, one cross-GPU subset gathered). `local` is this
@@ -142,18 +161,34 @@ def gather_regions(local, boxes_by_rank, sub_start, sub_shape, dst: int = 0, gro
     def view(t, b0, bs, origin):
         sl = tuple(slice(a - o, a - o + n) for a, n, o in zip(b0, bs, origin))
         return t[sl]
+
+    def split(boxes):  # (packed boxes, boxes received in place): the same on sender and root
+        packed = [b for b in boxes if not _contiguous_in(b[1], sub_shape)]
+        direct = [b for b in boxes if _contiguous_in(b[1], sub_shape)]
+        return packed, direct
+
+    def numel(bs):
+        return int(torch.Size([int(x) for x in bs]).numel())
     zero = [0] * len(sub_start)
     if rank != dst:
-        mine = boxes_by_rank[rank]
-        n = sum(int(torch.Size(bs).numel()) for _, bs in mine)
+        packed, direct = split(boxes_by_rank[rank])
+        peer = dist.get_global_rank(group, dst) if group is not None else dst
+        n = sum(numel(bs) for _, bs in packed)
+        ops = []
         if n:
             flat = torch.empty(n, dtype=local.dtype, device=local.device)
             off = 0
-            for b0, bs in mine:
-                k = int(torch.Size(bs).numel())
+            for b0, bs in packed:
+                k = numel(bs)
                 flat.narrow(0, off, k).view(bs).copy_(view(local, b0, bs, zero))
                 off += k
-            dist.send(flat, dist.get_global_rank(group, dst) if group is not None else dst, group=group)
+            ops.append(dist.P2POp(dist.isend, flat, peer, group=group))
+        for b0, bs in direct:  # one message per box, landing in place on the root
+            if numel(bs):
+                ops.append(dist.P2POp(dist.isend, view(local, b0, bs, zero).contiguous(), peer, group=group))
+        if ops:
+            for w in dist.batch_isend_irecv(ops):
+                w.wait()
         return None
     if out is None:
         out = torch.empty([int(x) for x in sub_shape], dtype=local.dtype, device=local.device)
@@ -163,20 +198,23 @@ def gather_regions(local, boxes_by_rank, sub_start, sub_shape, dst: int = 0, gro
     for r in range(world):
         if r == dst:
             continue
-        n = sum(int(torch.Size(bs).numel()) for _, bs in boxes_by_rank[r])
-        if not n:
-            continue
-        flat = torch.empty(n, dtype=local.dtype, device=local.device)
-        bufs.append((r, flat))
-        ops.append(dist.P2POp(dist.irecv, flat, dist.get_global_rank(group, r) if group is not None else r,
-                              group=group))
+        packed, direct = split(boxes_by_rank[r])
+        g_r = dist.get_global_rank(group, r) if group is not None else r
+        n = sum(numel(bs) for _, bs in packed)
+        if n:
+            flat = torch.empty(n, dtype=local.dtype, device=local.device)
+            bufs.append((packed, flat))
+            ops.append(dist.P2POp(dist.irecv, flat, g_r, group=group))
+        for b0, bs in direct:
+            if numel(bs):
+                ops.append(dist.P2POp(dist.irecv, view(out, b0, bs, sub_start), g_r, group=group))
     if ops:
         for w in dist.batch_isend_irecv(ops):
             w.wait()
-    for r, flat in bufs:
+    for packed, flat in bufs:
         off = 0
-        for b0, bs in boxes_by_rank[r]:
-            k = int(torch.Size(bs).numel())
+        for b0, bs in packed:
+            k = numel(bs)
             view(out, b0, bs, sub_start).copy_(flat.narrow(0, off, k).view(bs))
             off += k
     return out
@@ -196,6 +234,14 @@ def retrieve_array_subset_distributed(array, start, shape, group=None, dst: int 
     if device is None:
         device = torch.device("cuda", torch.cuda.current_device()) if torch.cuda.is_available() else "cpu"
     tdtype = torch.from_numpy(np.zeros(1, dtype=array.dtype)).dtype
+    device = torch.device(device)
+    if device.type == "cuda" and world > 1 and _host_staged(group):
+        # gloo moves host tensors only: decode on the device, stage the slab through host memory
+        local = torch.empty(sh, dtype=tdtype, device=device)
+        if all(n > 0 for n in sh):
+            array.retrieve_array_subset_into(s, sh, local)
+        got = gather_slabs(local.cpu(), slabs, axis, dst, group)
+        return None if got is None else got.to(device)
     out = None
     if rank == dst and axis == 0:  # the root decodes its slab in place inside the gathered subset
         out = torch.empty([int(n) for n in shape], dtype=tdtype, device=device)
