@@ -459,7 +459,67 @@ class C3:
                           f"{threads} threads"}
 
     def host_leg(self, sp):
-        return None
+        return {"dropin_emulation": self.dropin_leg()}
+
+    def dropin_leg(self):
+        """The drop-in boundary's real call pattern (rust/zarrs_gpu with its sharding_indexed plugin
+        under zarrs' unchanged read path, array_read_ops_common.rs:173-176): zarrs calls the codec once
+        per shard from its rayon workers (here a pool of the host's threads), each call synchronous,
+        host bytes in and host bytes out, and copies the result into the output view. A fully covered
+        shard is one zgpu_decode_batch of the sharded chain (its index verified); a partial shard
+        reads its index (a suffix range), then only the intersecting inner chunks, decoded in one
+        zgpu_decode_batch of the inner chain with crc32c stripped, not verified (the plugin's
+        GpuShardPartialDecoder). Calls on one context are serialised by the library."""
+        from concurrent.futures import ThreadPoolExecutor
+        from zarrs_amd import _lib as L
+        from zarrs_amd import CodecChain, make_desc
+        S, I = self.SHARD, self.INNER
+        inner = CodecChain.from_metadata(self.CODECS[0]["configuration"]["codecs"], "float32", 0.0, self.args.ctx)
+        out = np.empty(self.shape, np.float32)
+        cps = S // I
+        n_idx = cps ** 3
+
+        def one(item):
+            (si, sj, sk), (_, host) = item
+            org = [si * S, sj * S, sk * S]
+            s0 = [max(a, o) for a, o in zip(self.start, org)]
+            s1 = [min(a + b, o + S) for a, b, o in zip(self.start, self.shape, org)]
+            sel = [b - a for a, b in zip(s0, s1)]
+            dst = tuple(slice(a - b, c - b) for a, c, b in zip(s0, s1, self.start))
+            if sel == [S] * 3:  # full shard: ShardingCodecBound::decode
+                buf = np.empty([S] * 3, np.float32)
+                self.chain.decode_batch([make_desc(host, [S] * 3)], buf, [S] * 3, enc_device=False)
+                out[dst] = buf
+                return
+            # partial: index by a suffix range, then the intersecting inner chunks' byte ranges
+            index = np.frombuffer(host[len(host) - (n_idx * 16 + 4):len(host) - 4].tobytes(), np.uint64).reshape(-1, 2)
+            lo = [(a - o) // I for a, o in zip(s0, org)]
+            hi = [(b - o - 1) // I + 1 for b, o in zip(s1, org)]
+            descs = []
+            for ci in range(lo[0], hi[0]):
+                for cj in range(lo[1], hi[1]):
+                    for ck in range(lo[2], hi[2]):
+                        off, ln = index[(ci * cps + cj) * cps + ck]
+                        c0 = [org[0] + ci * I, org[1] + cj * I, org[2] + ck * I]
+                        a0 = [max(a, c) for a, c in zip(s0, c0)]
+                        a1 = [min(b, c + I) for b, c in zip(s1, c0)]
+                        enc = None if off == 2 ** 64 - 1 else (host.ctypes.data + int(off), int(ln))
+                        descs.append(make_desc(enc, [I] * 3, [a - c for a, c in zip(a0, c0)],
+                                               [b - a for a, b in zip(a0, a1)], [a - b for a, b in zip(a0, s0)]))
+            buf = np.empty(sel, np.float32)
+            inner.decode_batch(descs, buf, sel, enc_device=False, validate_checksums=False)
+            out[dst] = buf
+
+        items = list(self.shards.items())
+        with ThreadPoolExecutor(_threads()) as ex:
+            list(ex.map(one, items))  # warm-up
+            ok = bool(np.array_equal(out, self.expected.cpu().numpy()))
+            times = _time_reps(lambda: list(ex.map(one, items)), 5.0)
+        t = float(np.median(times))
+        return {"GiBps": round(out.nbytes / t / 2 ** 30, 2), "ms": round(t * 1e3, 1), "threads": _threads(),
+                "roundtrip_ok": ok, "calls": len(items),
+                "note": "one synchronous host-in/host-out zgpu_decode_batch per shard from a thread pool (the "
+                        "Rust plugin's pattern under zarrs' rayon loop), result copied into the output"}
 
 
 # ------------------------------------------------------------------------------------------------

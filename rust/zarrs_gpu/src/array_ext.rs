@@ -14,7 +14,8 @@ use zarrs_storage::ReadableStorageTraits;
 
 use crate::{Chain, ffi, status_error};
 
-/// GPU reads of a Zarr V3 array with a regular chunk grid.
+/// GPU reads of a Zarr V3 array with a regular chunk grid (other grids are refused with a
+/// CodecError; zarrs' own read path handles them).
 pub trait ArrayGpuExt {
     /// Decode `subset` on the GPU into a new host buffer (C order, native-endian element bytes).
     ///
@@ -56,6 +57,15 @@ fn gpu_chain_on<TStorage: ?Sized + ReadableStorageTraits + 'static>(
     let ArrayMetadata::V3(meta) = array.metadata() else {
         return Err(CodecError::Other("zarrs_gpu: Zarr V2 arrays are read through the CPU path".into()).into());
     };
+    // the batched read lays chunks out on a regular grid (zarrs/src/array/chunk_grid/regular.rs); the
+    // rectangular / rectilinear / regular_bounded / repeat grids go through zarrs' own read path
+    if meta.chunk_grid.name() != "regular" {
+        return Err(CodecError::Other(format!(
+            "zarrs_gpu: chunk grid '{}' is not regular: read it through Array::retrieve_array_subset",
+            meta.chunk_grid.name()
+        ))
+        .into());
+    }
     let json = serde_json::to_string(&meta.codecs).map_err(|e| CodecError::Other(e.to_string()))?;
     Chain::new_on(&json, array.data_type(), array.fill_value(), device)
         .map_err(|e| CodecError::Other(e.to_string()).into())

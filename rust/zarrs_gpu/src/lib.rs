@@ -1,8 +1,11 @@
 //! `zarrs_gpu`: the MI355X chunk-decode pipeline (libzgpu.so, include/zgpu.h) behind zarrs' own
 //! codec plugin surface, so that `zarrs/src`'s array read path runs unchanged.
 //!
-//! Two entry points, both over the C ABI:
+//! Three entry points, all over the C ABI:
 //!
+//! * [`register_codecs`] adds per-codec runtime plugins for `bytes`, `transpose`, `crc32c`, `gzip`,
+//!   `zstd` and `numcodecs.shuffle` (codecs.rs): zarrs' unchanged per-chunk CodecChain then decodes
+//!   every stage on the GPU (one synchronous n = 1 zgpu_decode_batch per stage and chunk).
 //! * [`register`] adds a runtime codec plugin for `sharding_indexed`
 //!   (`zarrs_codec::register_codec_v3`, zarrs_codec/src/lib.rs:279-318; runtime plugins are matched
 //!   before the compile-time ones, lib.rs:385-414). A shard is the natural GPU batch: its
@@ -23,6 +26,7 @@
 //! from C++ (tests/c/abi_harness.cpp) and Python ctypes.
 
 mod array_ext;
+pub mod codecs;
 mod ffi;
 mod sharding;
 
@@ -49,6 +53,20 @@ pub fn register() -> zarrs_codec::CodecRuntimeRegistryHandleV3 {
 /// Unregister a plugin registered by [`register`].
 pub fn unregister(handle: &zarrs_codec::CodecRuntimeRegistryHandleV3) -> bool {
     zarrs_codec::unregister_codec_v3(handle)
+}
+
+/// Register the per-codec GPU plugins (`bytes`, `transpose`, `crc32c`, `gzip`, `zstd`,
+/// `numcodecs.shuffle`): one runtime plugin matching all their names, zarrs_codec/src/lib.rs:279-318.
+pub fn register_codecs() -> zarrs_codec::CodecRuntimeRegistryHandleV3 {
+    zarrs_codec::register_codec_v3(zarrs_codec::CodecRuntimePluginV3::new(
+        |name| codecs::GPU_CODEC_NAMES.contains(&name),
+        codecs::create,
+    ))
+}
+
+/// Both: [`register`] and [`register_codecs`] (the handles, for [`unregister`]).
+pub fn register_all() -> [zarrs_codec::CodecRuntimeRegistryHandleV3; 2] {
+    [register(), register_codecs()]
 }
 
 /// The HIP device the plugin decodes on: `ZARRS_GPU_DEVICE` (default 0).
@@ -202,6 +220,49 @@ impl Chain {
             return Err(status_error(rc));
         }
         Ok(out)
+    }
+}
+
+impl Chain {
+    /// One `zgpu_decode_batch` call over `descs` (host encoded bytes, host output of shape
+    /// `out_shape` in C order): the batched form every per-shard / per-chunk decode of the plugin
+    /// uses. `flags` may add ZGPU_NO_VALIDATE (partial-decoder semantics: crc32c stripped, not
+    /// verified). Returns the first failing descriptor's status as a [`CodecError`].
+    pub(crate) fn decode_descs(
+        &self,
+        descs: &[ffi::zgpu_chunk_desc],
+        out: &mut [u8],
+        out_shape: &[u64],
+        flags: u32,
+    ) -> Result<(), CodecError> {
+        let nd = out_shape.len();
+        if nd == 0 || nd > ffi::ZGPU_MAX_DIMS {
+            return Err(CodecError::Other(format!("zgpu: unsupported dimensionality {nd}")));
+        }
+        let need = out_shape.iter().product::<u64>() * self.element_size as u64;
+        if (out.len() as u64) < need {
+            return Err(CodecError::Other("zgpu: output buffer smaller than its shape".into()));
+        }
+        let mut status = vec![0i32; descs.len().max(1)];
+        // SAFETY: the descriptors point at host buffers the caller keeps alive for this synchronous
+        // call (flags carry no ZGPU_ENC_DEVICE / ZGPU_OUT_DEVICE), `out` holds the output shape.
+        let rc = unsafe {
+            ffi::zgpu_decode_batch(
+                self.as_ptr(),
+                nd as u32,
+                descs.as_ptr(),
+                descs.len() as u64,
+                out.as_mut_ptr().cast::<c_void>(),
+                out_shape.as_ptr(),
+                flags & ffi::ZGPU_NO_VALIDATE,
+                status.as_mut_ptr(),
+                std::ptr::null_mut(),
+            )
+        };
+        if rc != ffi::ZGPU_OK {
+            return Err(status_error(rc));
+        }
+        Ok(())
     }
 }
 

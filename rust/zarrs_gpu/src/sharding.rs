@@ -1,4 +1,6 @@
 //! GPU `sharding_indexed`: decode on the MI355X, everything else delegated to zarrs' ShardingCodec.
+//! Whole shards (decode / decode_into) are one zgpu_decode_batch of the sharded chain; the partial
+//! decoder reads the index and only the intersecting inner chunks by ranged reads, as zarrs does.
 //!
 //! Reference: zarrs/src/array/codec/array_to_bytes/sharding/sharding_codec.rs (ShardingCodec,
 //! ShardingCodecBound::{decode :378-518, decode_into :617-707}) and sharding_partial_decoder_sync.rs
@@ -11,6 +13,9 @@ use std::num::NonZeroU64;
 use std::sync::Arc;
 
 use zarrs::array::codec::ShardingCodec;
+use zarrs::array::{CodecChain, CodecChainBound, data_type};
+use zarrs_metadata_ext::codec::sharding::{ShardingCodecConfiguration, ShardingCodecConfigurationV1, ShardingIndexLocation};
+use zarrs_storage::byte_range::ByteRange;
 use zarrs_chunk_grid::{ChunkGridCreateError, Indexer};
 use zarrs_codec::{
     ArrayBytes, ArrayBytesRaw, ArrayCodecTraits, ArrayPartialDecoderNoSubchunkingTraits, ArrayPartialDecoderTraits,
@@ -25,7 +30,7 @@ use zarrs_metadata::v3::MetadataV3;
 use zarrs_plugin::ZarrVersion;
 use zarrs_storage::StorageError;
 
-use crate::Chain;
+use crate::{Chain, ffi};
 
 /// The unbound GPU `sharding_indexed` codec: zarrs' own ShardingCodec (for metadata, encoding and
 /// subchunk grids) plus the codec metadata the GPU chain is created from at bind time.
@@ -33,6 +38,7 @@ use crate::Chain;
 pub struct GpuShardingCodec {
     cpu: Arc<dyn UnboundArrayToBytesCodecTraits>,
     codecs_json: String,
+    config: ShardingCodecConfigurationV1,
 }
 
 zarrs_plugin::impl_extension_aliases!(GpuShardingCodec, v3: "sharding_indexed");
@@ -48,7 +54,9 @@ impl GpuShardingCodec {
         };
         // the GPU chain parses the same metadata: a one-codec "codecs" list
         let codecs_json = serde_json::to_string(&[metadata]).map_err(CodecCreateError::other)?;
-        Ok(Codec::ArrayToBytes(Arc::new(Self { cpu, codecs_json })))
+        let ShardingCodecConfiguration::V1(config) = metadata.to_typed_configuration::<ShardingCodecConfiguration>()
+            .map_err(|e| CodecCreateError::Other(e.to_string()))?;
+        Ok(Codec::ArrayToBytes(Arc::new(Self { cpu, codecs_json, config })))
     }
 }
 
@@ -76,7 +84,7 @@ impl UnboundArrayToBytesCodecTraits for GpuShardingCodec {
         opts: &CodecSpecificOptions,
     ) -> Result<Arc<dyn UnboundArrayToBytesCodecTraits>, CodecCreateError> {
         let cpu = self.cpu.clone().with_codec_specific_options(opts)?;
-        Ok(Arc::new(Self { cpu, codecs_json: self.codecs_json.clone() }))
+        Ok(Arc::new(Self { cpu, codecs_json: self.codecs_json.clone(), config: self.config.clone() }))
     }
 
     fn with_context(
@@ -86,7 +94,22 @@ impl UnboundArrayToBytesCodecTraits for GpuShardingCodec {
     ) -> Result<Arc<dyn ArrayToBytesCodecTraits>, CodecCreateError> {
         let cpu = self.cpu.with_context(data_type.clone(), fill_value.clone())?;
         let chain = Chain::new(&self.codecs_json, &data_type, &fill_value)?;
-        Ok(Arc::new(GpuShardingCodecBound { cpu, chain: Arc::new(chain), data_type, fill_value }))
+        // the inner chain alone (the partial decoder batches the intersecting inner chunks through
+        // it) and zarrs' own index chain, bound to uint64 / u64::MAX (sharding_codec.rs:266-268)
+        let inner_json = serde_json::to_string(&self.config.codecs).map_err(CodecCreateError::other)?;
+        let inner_chain = Chain::new(&inner_json, &data_type, &fill_value)?;
+        let index_chain = CodecChain::from_metadata(&self.config.index_codecs)?
+            .with_context(data_type::uint64(), FillValue::from(u64::MAX))?;
+        Ok(Arc::new(GpuShardingCodecBound {
+            cpu,
+            chain: Arc::new(chain),
+            inner_chain: Arc::new(inner_chain),
+            index_chain,
+            subchunk_shape: self.config.chunk_shape.iter().map(|c| c.get()).collect(),
+            index_location: self.config.index_location,
+            data_type,
+            fill_value,
+        }))
     }
 }
 
@@ -95,12 +118,65 @@ impl UnboundArrayToBytesCodecTraits for GpuShardingCodec {
 pub struct GpuShardingCodecBound {
     cpu: Arc<dyn ArrayToBytesCodecTraits>,
     chain: Arc<Chain>,
+    inner_chain: Arc<Chain>,
+    index_chain: Arc<CodecChainBound>,
+    subchunk_shape: Vec<u64>,
+    index_location: ShardingIndexLocation,
     data_type: DataType,
     fill_value: FillValue,
 }
 
 fn u64s(shape: &[NonZeroU64]) -> Vec<u64> {
     shape.iter().map(|s| s.get()).collect()
+}
+
+const OOB: &str = "The shard index references out-of-bounds bytes. The chunk may be corrupted.";
+
+impl GpuShardingCodecBound {
+    /// Inner chunks per shard along each axis (calculate_chunks_per_shard, sharding.rs:136-154).
+    fn chunks_per_shard(&self, shard_shape: &[u64]) -> Result<Vec<u64>, CodecError> {
+        if shard_shape.len() != self.subchunk_shape.len() {
+            return Err(CodecError::Other("sharding: shard / subchunk dimensionality mismatch".into()));
+        }
+        shard_shape
+            .iter()
+            .zip(&self.subchunk_shape)
+            .map(|(&s, &c)| {
+                if c == 0 || s % c != 0 {
+                    Err(CodecError::Other(format!("sharding: subchunk shape {c} does not divide shard shape {s}")))
+                } else {
+                    Ok(s / c)
+                }
+            })
+            .collect()
+    }
+
+    /// decode_shard_index_partial_decoder (sharding.rs:267-288): the encoded index by one ranged
+    /// read, decoded (and its crc32c verified) by zarrs' own index chain on the host: it is
+    /// 16 B per inner chunk, and the GPU work is the inner chunks. None: the shard does not exist.
+    fn read_index(
+        &self,
+        input: &dyn BytesPartialDecoderTraits,
+        shard_shape: &[u64],
+        options: &CodecOptions,
+    ) -> Result<Option<Vec<u64>>, CodecError> {
+        let cps = self.chunks_per_shard(shard_shape)?;
+        let mut index_shape: Vec<NonZeroU64> =
+            cps.iter().map(|&c| NonZeroU64::new(c).expect("positive")).collect();
+        index_shape.push(NonZeroU64::new(2).expect("two"));
+        let BytesRepresentation::FixedSize(index_size) = self.index_chain.encoded_representation(&index_shape)? else {
+            return Err(CodecError::Other("the array index cannot include a variable size output codec".into()));
+        };
+        let range = match self.index_location {
+            ShardingIndexLocation::Start => ByteRange::FromStart(0, Some(index_size)),
+            ShardingIndexLocation::End => ByteRange::Suffix(index_size),
+        };
+        let Some(encoded) = input.partial_decode(range, options)? else {
+            return Ok(None);
+        };
+        let decoded = self.index_chain.decode(encoded, &index_shape, options)?.into_fixed()?;
+        Ok(Some(decoded.chunks_exact(8).map(|b| u64::from_ne_bytes(b.try_into().expect("8 bytes"))).collect()))
+    }
 }
 
 impl ArrayCodecTraits for GpuShardingCodecBound {
@@ -174,13 +250,17 @@ impl ArrayToBytesCodecTraits for GpuShardingCodecBound {
         self.cpu.compact(bytes, shape, options)
     }
 
+    /// ShardingPartialDecoder::new (sharding_partial_decoder_sync.rs:47-74): only the shard index is
+    /// read here, by a suffix (index at the end) or prefix byte range (sharding.rs:196-207,267-288).
     fn partial_decoder(
         self: Arc<Self>,
         input_handle: Arc<dyn BytesPartialDecoderTraits>,
         shape: &[NonZeroU64],
-        _options: &CodecOptions,
+        options: &CodecOptions,
     ) -> Result<Arc<dyn ArrayPartialDecoderTraits>, CodecError> {
-        Ok(Arc::new(GpuShardPartialDecoder { input: input_handle, shape: u64s(shape), codec: self }))
+        let shape = u64s(shape);
+        let index = self.read_index(&*input_handle, &shape, options)?;
+        Ok(Arc::new(GpuShardPartialDecoder { input: input_handle, shape, codec: self, index }))
     }
 
     fn partial_encoder(
@@ -193,13 +273,89 @@ impl ArrayToBytesCodecTraits for GpuShardingCodecBound {
     }
 }
 
-/// ShardingPartialDecoder on the GPU: the shard's bytes are read once, and only the inner chunks that
-/// intersect the requested subset are decoded (crc32c stripped, not verified: crc32c_codec.rs:143-158),
-/// all in one zgpu_decode_batch call. A missing shard reads as the fill value (:329-333).
+/// ShardingPartialDecoder on the GPU (sharding_partial_decoder_sync.rs:34-400). Created with the
+/// shard index only (`index`, read by a ranged read: `None` = the shard does not exist). A partial
+/// decode reads the byte ranges of the inner chunks that intersect the subset with ONE
+/// `partial_decode_many` call (get_subchunk_partial_decoder's ByteIntervalPartialDecoder reads,
+/// :279-308, batched), and decodes all of them in ONE zgpu_decode_batch of the inner chain: each
+/// intersecting inner chunk is a descriptor whose selection is its overlap with the subset, decoded
+/// on the partial-decoder path (crc32c stripped, not verified: crc32c_codec.rs:143-158); empty inner
+/// chunks are fill-value descriptors (:380-381).
 struct GpuShardPartialDecoder {
     input: Arc<dyn BytesPartialDecoderTraits>,
     shape: Vec<u64>,
     codec: Arc<GpuShardingCodecBound>,
+    index: Option<Vec<u64>>,
+}
+
+impl GpuShardPartialDecoder {
+    fn decode_subset(&self, start: &[u64], shape: &[u64], options: &CodecOptions) -> Result<Vec<u8>, CodecError> {
+        let codec = &self.codec;
+        let es = codec.inner_chain.element_size;
+        let n: u64 = shape.iter().product();
+        let mut out = vec![0u8; usize::try_from(n).map_err(|e| CodecError::Other(e.to_string()))? * es];
+        let Some(index) = &self.index else {
+            // a missing shard reads as the fill value (:329-333)
+            let fill = codec.fill_value.as_ne_bytes();
+            out.chunks_exact_mut(es).for_each(|c| c.copy_from_slice(fill));
+            return Ok(out);
+        };
+        let cps = codec.chunks_per_shard(&self.shape)?;
+        let sub = &codec.subchunk_shape;
+        let nd = self.shape.len();
+        // the intersecting inner chunks, C order (chunks_in_array_subset of the shard's grid)
+        let lo: Vec<u64> = start.iter().zip(sub).map(|(s, c)| s / c).collect();
+        let hi: Vec<u64> = start.iter().zip(shape).zip(sub).map(|((s, n), c)| (s + n - 1) / c + 1).collect();
+        let mut descs = Vec::new();
+        let mut ranges = Vec::new();  // byte range of each present inner chunk, in descriptor order
+        let mut present = Vec::new(); // descriptor index of each range
+        let total: u64 = hi.iter().zip(&lo).map(|(h, l)| h - l).product();
+        for t in 0..total {
+            // C-order grid coordinates of the t-th intersecting inner chunk
+            let mut idx = vec![0u64; nd];
+            let mut rem = t;
+            for a in (0..nd).rev() {
+                let ext = hi[a] - lo[a];
+                idx[a] = lo[a] + rem % ext;
+                rem /= ext;
+            }
+            let lin = idx.iter().zip(&cps).fold(0u64, |acc, (i, c)| acc * c + i) as usize;
+            let (offset, size) = (index[2 * lin], index[2 * lin + 1]);
+            let mut d = ffi::zgpu_chunk_desc::default();
+            for a in 0..nd {
+                let c0 = idx[a] * sub[a];
+                let s0 = start[a].max(c0);
+                let s1 = (start[a] + shape[a]).min(c0 + sub[a]);
+                d.chunk_shape[a] = sub[a];
+                d.sel_start[a] = s0 - c0;
+                d.sel_shape[a] = s1 - s0;
+                d.out_start[a] = s0 - start[a];
+            }
+            if !(offset == u64::MAX && size == u64::MAX) {
+                let end = offset.checked_add(size).ok_or_else(|| CodecError::Other(OOB.into()))?;
+                ranges.push(ByteRange::new(offset..end));
+                present.push(descs.len());
+            }
+            descs.push(d);
+        }
+        // one batched ranged read of every present inner chunk
+        let bytes = if ranges.is_empty() {
+            Vec::new()
+        } else {
+            match self.input.partial_decode_many(Box::new(ranges.into_iter()), options) {
+                Ok(Some(b)) => b,
+                Ok(None) => return Err(CodecError::Other("zarrs_gpu: the shard disappeared during the read".into())),
+                Err(CodecError::InvalidByteRangeError(_)) => return Err(CodecError::Other(OOB.into())),
+                Err(e) => return Err(e),
+            }
+        };
+        for (b, &k) in bytes.iter().zip(&present) {
+            descs[k].enc = b.as_ptr().cast();
+            descs[k].enc_len = b.len() as u64;
+        }
+        codec.inner_chain.decode_descs(&descs, &mut out, shape, ffi::ZGPU_NO_VALIDATE)?;
+        Ok(out)
+    }
 }
 
 impl ArrayPartialDecoderNoSubchunkingTraits for GpuShardPartialDecoder {}
@@ -218,10 +374,6 @@ impl ArrayPartialDecoderTraits for GpuShardPartialDecoder {
     }
 
     fn partial_decode(&self, indexer: &dyn Indexer, options: &CodecOptions) -> Result<ArrayBytes<'_>, CodecError> {
-        let Some(encoded) = self.input.decode(options)? else {
-            return Ok(ArrayBytes::new_fill_value(&self.codec.data_type, indexer.len(), &self.codec.fill_value)?);
-        };
-        let chain = &self.codec.chain;
         if let Some(subset) = indexer.as_array_subset() {
             let (start, shape) = (subset.start(), subset.shape());
             let inside = start.len() == self.shape.len()
@@ -235,13 +387,13 @@ impl ArrayPartialDecoderTraits for GpuShardPartialDecoder {
             if shape.iter().any(|&n| n == 0) {
                 return Ok(ArrayBytes::new_flen(Cow::Owned(Vec::new())));
             }
-            let out = chain.decode_region(&encoded, &self.shape, &start, &shape, options.validate_checksums())?;
-            return Ok(ArrayBytes::new_flen(Cow::Owned(out)));
+            return Ok(ArrayBytes::new_flen(Cow::Owned(self.decode_subset(&start, &shape, options)?)));
         }
-        // arbitrary indexers: the whole shard decoded on the GPU, the indexed elements gathered here
+        // arbitrary indexers: the whole shard (every inner chunk, one batch), the indexed elements
+        // gathered here
         let zeros = vec![0u64; self.shape.len()];
-        let full = chain.decode_region(&encoded, &self.shape, &zeros, &self.shape, options.validate_checksums())?;
-        let es = chain.element_size;
+        let full = self.decode_subset(&zeros, &self.shape, options)?;
+        let es = self.codec.inner_chain.element_size;
         let mut out = Vec::with_capacity(usize::try_from(indexer.len()).unwrap_or(0) * es);
         for i in indexer.iter_linearised_indices(&self.shape)? {
             let o = usize::try_from(i).map_err(|e| CodecError::Other(e.to_string()))? * es;
@@ -251,6 +403,6 @@ impl ArrayPartialDecoderTraits for GpuShardPartialDecoder {
     }
 
     fn supports_partial_decode(&self) -> bool {
-        true
+        self.input.supports_partial_decode()
     }
 }

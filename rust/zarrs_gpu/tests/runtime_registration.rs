@@ -63,3 +63,59 @@ fn gpu_multi_device_read_matches_zarrs() {
     let got: Vec<u16> = raw.chunks_exact(2).map(|b| u16::from_ne_bytes([b[0], b[1]])).collect();
     assert_eq!(got, expected);
 }
+
+/// Unsharded arrays through zarrs' unchanged per-chunk read path with the per-codec GPU plugins
+/// registered (transpose + big-endian bytes: config C2's chain; bytes + shuffle + zstd: C5's;
+/// bytes + gzip + crc32c), against the same reads without them.
+#[test]
+fn gpu_per_codec_plugins_match_zarrs() {
+    let store = Arc::new(MemoryStore::default());
+    let chains = ["/c2", "/c5", "/gz"];
+    for path in &chains {
+        let mut b = ArrayBuilder::new(vec![40, 70, 33], vec![16, 32, 16], data_type::uint16(), 3u16);
+        match *path {
+            "/c2" => {
+                b.array_to_array_codecs(vec![Arc::new(codec::TransposeCodec::new(
+                    codec::TransposeOrder::new(&[2, 1, 0]).unwrap(),
+                ))])
+                .array_to_bytes_codec(Arc::new(codec::BytesCodec::big()));
+            }
+            "/c5" => {
+                b.bytes_to_bytes_codecs(vec![
+                    Arc::new(codec::ShuffleCodec::new(2)),
+                    Arc::new(codec::ZstdCodec::new(3, false)),
+                ]);
+            }
+            _ => {
+                b.bytes_to_bytes_codecs(vec![
+                    Arc::new(codec::GzipCodec::new(1).unwrap()),
+                    Arc::new(codec::Crc32cCodec::new()),
+                ]);
+            }
+        }
+        let array = b.build(store.clone(), path).unwrap();
+        array.store_metadata().unwrap();
+        let data: Vec<u16> = (0..40 * 70 * 33).map(|i| ((i * 7919) % 5003) as u16).collect();
+        array.store_array_subset(&array.subset_all(), &data).unwrap();
+    }
+    let subsets = [
+        ArraySubset::new_with_ranges(&[0..40, 0..70, 0..33]),
+        ArraySubset::new_with_ranges(&[3..37, 10..65, 5..30]),
+    ];
+    let expected: Vec<Vec<Vec<u16>>> = chains
+        .iter()
+        .map(|p| {
+            let a: Array<MemoryStore> = Array::open(store.clone(), p).unwrap();
+            subsets.iter().map(|s| a.retrieve_array_subset(s).unwrap()).collect()
+        })
+        .collect();
+    let handle = zarrs_gpu::register_codecs();
+    for (p, exp) in chains.iter().zip(&expected) {
+        let a: Array<MemoryStore> = Array::open(store.clone(), p).unwrap();
+        for (s, e) in subsets.iter().zip(exp) {
+            let got: Vec<u16> = a.retrieve_array_subset(s).unwrap();
+            assert_eq!(&got, e, "{p}");
+        }
+    }
+    assert!(zarrs_gpu::unregister(&handle));
+}

@@ -32,6 +32,7 @@ using namespace zgpu;
 
 struct zgpu_cache {
   zgpu_ctx *ctx = nullptr;
+  int device = 0;  // the context's device, kept so that destroying the cache never reads the context
   uint64_t capacity = 0;
   std::mutex mu;
   // geometry of the cached chunks (one array per cache, as an ArrayCached owns its cache)
@@ -99,7 +100,7 @@ int bind(zgpu_cache &K, const zgpu_chain *ch, uint32_t nd, const uint64_t *chunk
   K.slot_bytes = c.es;
   for (uint64_t s : cs) K.slot_bytes *= s;
   K.n_slots = K.slot_bytes ? K.capacity / K.slot_bytes : 0;
-  if (hipSetDevice(ctx_device(K.ctx)) != hipSuccess) return fail(ZGPU_HIP_ERROR, "hipSetDevice");
+  if (hipSetDevice(K.device) != hipSuccess) return fail(ZGPU_HIP_ERROR, "hipSetDevice");
   if (K.n_slots) {
     if (hipMalloc(&K.pool, K.n_slots * K.slot_bytes) != hipSuccess) {
       K.pool = nullptr;
@@ -125,6 +126,7 @@ int zgpu_cache_create(zgpu_ctx *ctx, uint64_t capacity_bytes, zgpu_cache **out) 
   if (!ctx || !out) return fail(ZGPU_INVALID_ARGUMENT, "NULL argument");
   auto K = std::make_unique<zgpu_cache>();
   K->ctx = ctx;
+  K->device = ctx_device(ctx);
   K->capacity = capacity_bytes;
   *out = K.release();
   return ZGPU_OK;
@@ -132,8 +134,10 @@ int zgpu_cache_create(zgpu_ctx *ctx, uint64_t capacity_bytes, zgpu_cache **out) 
 
 void zgpu_cache_destroy(zgpu_cache *cache) {
   if (!cache) return;
-  (void)hipSetDevice(ctx_device(cache->ctx));
+  // garbage-collected bindings may destroy the cache after its context: only the device id is used
+  if (hipSetDevice(cache->device) != hipSuccess) (void)hipGetLastError();
   delete cache;
+  (void)hipGetLastError();  // a failed free must not surface in the caller's next HIP error check
 }
 
 int zgpu_cache_clear(zgpu_cache *K) {

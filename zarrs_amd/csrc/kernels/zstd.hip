@@ -1739,6 +1739,11 @@ constexpr int LIT_STAGE_R = ZG_LIT_WPE >= 4 ? 4 : 8;  // 16-B staging loads in f
 #ifndef ZG_LIT_GWIN
 #define ZG_LIT_GWIN 2  // literal sections beyond LIT_LDS: 1 per-lane 16-B window, 2 32-B + prefetch
 #endif
+#ifndef ZG_LIT_STAGE
+#define ZG_LIT_STAGE 0  // 1: a lane's decoded literals leave through a 64-B LDS window, stored as whole
+                        // aligned 64-B pieces (4 x 16-B stores) instead of 8-B stores
+#endif
+constexpr uint32_t LIT_STG_PITCH = 80;  // bytes per lane window (64 + 16: 16-B aligned, banks spread)
 
 struct ZLitSmem {
   uint16_t huf[1 << MAX_HUF_LOG];
@@ -1751,6 +1756,9 @@ struct ZLitSmem {
   uint32_t cnt[LIT_THREADS], wsum[4];
   uint32_t ctl[4];  // table log, flags
   uint32_t lin[LIT_LDS / 4 + 8];
+#if ZG_LIT_STAGE
+  uint4 stg[LIT_THREADS * LIT_STG_PITCH / 16];  // per-lane 64-B output windows
+#endif
 };
 
 // backward bit container: C holds bits [lp, p) of the word array, bit p-1 at C bit 63
@@ -1769,7 +1777,7 @@ __device__ __forceinline__ void hl_init(HufLane &H, int32_t p, const Wd &word) {
 // decode symbols while p > stop (at most maxn); WRITE: out[k] = symbol k
 template <bool WRITE, class Wd>
 __device__ __forceinline__ uint32_t hl_run(HufLane &H, int32_t &p, int32_t stop, uint32_t tl, const uint16_t *huf,
-                                           const Wd &word, uint8_t *out, uint32_t maxn) {
+                                           const Wd &word, uint8_t *out, uint32_t maxn, uint4 *stg = nullptr) {
   uint32_t n = 0;
   const uint32_t sh = 64 - tl;
 #if ZG_LIT_PACK
@@ -1780,6 +1788,13 @@ __device__ __forceinline__ uint32_t hl_run(HufLane &H, int32_t &p, int32_t stop,
   uint64_t acc = 0, acc1 = 0;
   uint32_t k = 0;
   const uint32_t head = WRITE ? (uint32_t)((PB - ((uintptr_t)out & (PB - 1))) & (PB - 1)) : 0u;
+#if ZG_LIT_STAGE
+  // 8-B words from the first 64-B boundary on go to the lane's LDS window; a completed window leaves
+  // as four aligned 16-B stores (a whole half-line at once, no partial-line write-backs)
+  static_assert(!ZG_LIT_STAGE || ZG_LIT_PACK_B == 8, "literal staging packs 8-B words");
+  const uint32_t head64 = WRITE ? (uint32_t)((64 - ((uintptr_t)out & 63)) & 63) : 0u;
+  uint64_t *stg8 = (uint64_t *)stg;
+#endif
 #endif
   while (p > stop && n < maxn) {
     if (H.v <= 32) {
@@ -1803,7 +1818,24 @@ __device__ __forceinline__ uint32_t hl_run(HufLane &H, int32_t &p, int32_t stop,
           if (PB == 16) {
             *(uint4 *)(out + n - 15) = make_uint4((uint32_t)acc, (uint32_t)(acc >> 32), (uint32_t)acc1, (uint32_t)(acc1 >> 32));
           } else {
+#if ZG_LIT_STAGE
+            const uint32_t pos = n - 7;
+            if (pos < head64) {
+              *(uint64_t *)(out + pos) = acc;
+            } else {
+              const uint32_t r = (pos - head64) & 63;
+              stg8[r >> 3] = acc;
+              if (r == 56) {  // window complete: out + pos - 56 is 64-B aligned
+                uint4 *g = (uint4 *)(out + pos - 56);
+                g[0] = stg[0];
+                g[1] = stg[1];
+                g[2] = stg[2];
+                g[3] = stg[3];
+              }
+            }
+#else
             *(uint64_t *)(out + n - 7) = acc;
+#endif
           }
           acc = acc1 = 0;
           k = 0;
@@ -1816,6 +1848,13 @@ __device__ __forceinline__ uint32_t hl_run(HufLane &H, int32_t &p, int32_t stop,
     n++;
   }
 #if ZG_LIT_PACK
+#if ZG_LIT_STAGE
+  if (WRITE && n - k > head64) {  // the staged words of the last, incomplete window
+    const uint32_t done = n - k;  // bytes stored or staged as whole words
+    const uint32_t w0 = done - ((done - head64) & 63);
+    for (uint32_t q = w0; q < done; q += 8) *(uint64_t *)(out + q) = stg8[((q - head64) & 63) >> 3];
+  }
+#endif
   if (WRITE)
     for (uint32_t i = 0; i < k; i++) out[n - k + i] = (uint8_t)((i < 8 ? acc : acc1) >> (8 * (i & 7)));
 #endif
@@ -1949,7 +1988,11 @@ __device__ bool lits_decode(ZLitSmem &S, const Wd &word, uint32_t nstreams, cons
     HufLane H;
     int32_t p = S.entry[t];
     hl_init(H, p, word);
+#if ZG_LIT_STAGE
+    hl_run<true>(H, p, tj1, tl, S.huf, word, lit + (uint64_t)s * seg + off, c, &S.stg[t * (LIT_STG_PITCH / 16)]);
+#else
     hl_run<true>(H, p, tj1, tl, S.huf, word, lit + (uint64_t)s * seg + off, c);
+#endif
   }
   return true;
 }

@@ -16,6 +16,7 @@
 #include <cstdio>
 #include <cstdlib>
 #include <cstring>
+#include <condition_variable>
 #include <map>
 #include <memory>
 #include <mutex>
@@ -60,21 +61,59 @@ struct HipFail {
 }  // namespace
 
 // ------------------------------------------------------------------------------------------------
-// Context: one per GPU. Owns a stream and a caching device allocator (grow-only pools reused across
-// calls so a steady-state decode performs no hipMalloc).
+// Context: one per GPU. Owns a caching device allocator (grow-only pools reused across calls so a
+// steady-state decode performs no hipMalloc) and a small pool of "lanes" (a stream, two copy streams
+// and an ordering event): concurrent calls on one context each take a lane and run side by side on
+// the GPU (zarrs calls a codec from many rayon workers at once); a call that finds every lane busy
+// waits for one. ZGPU_CTX_LANES sets the pool size (default 4, the hardware queues of a process).
 // ------------------------------------------------------------------------------------------------
+struct Lane {
+  hipStream_t stream = nullptr;              // the call's stream when the caller passes none
+  hipStream_t copy[2] = {nullptr, nullptr};  // H2D / D2H streams of the pipelined host paths (lazy)
+  hipEvent_t order_ev = nullptr;              // legacy-stream -> lane-stream ordering (pick_stream)
+};
+
 struct zgpu_ctx {
   int device = 0;
-  hipStream_t stream = nullptr;
-  hipStream_t copy[2] = {nullptr, nullptr};  // H2D / D2H streams of the pipelined host path (lazy)
-  hipEvent_t order_ev = nullptr;              // legacy-stream -> context-stream ordering (pick_stream)
-  std::mutex mu;
+  std::mutex mu;  // the allocator pools
   std::multimap<size_t, void *> free_dev;  // size -> ptr
   std::map<void *, size_t> live_dev;
   std::multimap<size_t, void *> free_host;
   std::map<void *, size_t> live_host;
+  // lanes
+  std::mutex lane_mu;
+  std::condition_variable lane_cv;
+  std::vector<Lane *> lanes_all, lanes_free;
+  uint32_t max_lanes = 4;
+  hipStream_t peer = nullptr;  // peer copies of the multi-device read (lazy)
+
+  Lane *acquire_lane() {
+    std::unique_lock<std::mutex> lk(lane_mu);
+    while (lanes_free.empty()) {
+      if (lanes_all.size() < max_lanes) {
+        auto L = std::make_unique<Lane>();
+        HIPCHK(hipSetDevice(device));
+        HIPCHK(hipStreamCreateWithFlags(&L->stream, hipStreamNonBlocking));
+        lanes_all.push_back(L.get());
+        lanes_free.push_back(L.release());
+        break;
+      }
+      lane_cv.wait(lk);
+    }
+    Lane *L = lanes_free.back();
+    lanes_free.pop_back();
+    return L;
+  }
+  void release_lane(Lane *L) {
+    {
+      std::lock_guard<std::mutex> lk(lane_mu);
+      lanes_free.push_back(L);
+    }
+    lane_cv.notify_one();
+  }
 
   void *dev_alloc(size_t bytes) {
+    std::lock_guard<std::mutex> lk(mu);
     bytes = std::max<size_t>(256, (bytes + 255) & ~(size_t)255);
     auto it = free_dev.lower_bound(bytes);
     if (it != free_dev.end() && it->first <= bytes * 2 + (1u << 20)) {
@@ -95,12 +134,14 @@ struct zgpu_ctx {
   }
   void dev_free(void *p) {
     if (!p) return;
+    std::lock_guard<std::mutex> lk(mu);
     auto it = live_dev.find(p);
     if (it == live_dev.end()) return;
     free_dev.emplace(it->second, p);
     live_dev.erase(it);
   }
   void *host_alloc(size_t bytes) {
+    std::lock_guard<std::mutex> lk(mu);
     bytes = std::max<size_t>(4096, (bytes + 4095) & ~(size_t)4095);
     auto it = free_host.lower_bound(bytes);
     if (it != free_host.end() && it->first <= bytes * 2 + (1u << 20)) {
@@ -116,6 +157,7 @@ struct zgpu_ctx {
   }
   void host_free(void *p) {
     if (!p) return;
+    std::lock_guard<std::mutex> lk(mu);
     auto it = live_host.find(p);
     if (it == live_host.end()) return;
     free_host.emplace(it->second, p);
@@ -123,16 +165,32 @@ struct zgpu_ctx {
   }
   ~zgpu_ctx() {
     (void)hipSetDevice(device);
-    if (stream) (void)hipStreamSynchronize(stream);
+    for (Lane *L : lanes_all)
+      if (L->stream) (void)hipStreamSynchronize(L->stream);
     for (auto &kv : free_dev) (void)hipFree(kv.second);
     for (auto &kv : live_dev) (void)hipFree(kv.first);
     for (auto &kv : free_host) (void)hipHostFree(kv.second);
     for (auto &kv : live_host) (void)hipHostFree(kv.first);
-    if (stream) (void)hipStreamDestroy(stream);
-    if (order_ev) (void)hipEventDestroy(order_ev);
-    for (hipStream_t cs : copy)
-      if (cs) (void)hipStreamDestroy(cs);
+    for (Lane *L : lanes_all) {
+      if (L->stream) (void)hipStreamDestroy(L->stream);
+      if (L->order_ev) (void)hipEventDestroy(L->order_ev);
+      for (hipStream_t cs : L->copy)
+        if (cs) (void)hipStreamDestroy(cs);
+      delete L;
+    }
+    if (peer) (void)hipStreamDestroy(peer);
+    (void)hipGetLastError();  // teardown failures must not surface in the caller's next HIP error check
   }
+};
+
+// A call's lane for its whole duration (RAII).
+struct LaneScope {
+  zgpu_ctx *C;
+  Lane *L;
+  explicit LaneScope(zgpu_ctx *c) : C(c), L(c->acquire_lane()) {}
+  ~LaneScope() { C->release_lane(L); }
+  LaneScope(const LaneScope &) = delete;
+  LaneScope &operator=(const LaneScope &) = delete;
 };
 
 struct zgpu_chain {
@@ -154,6 +212,8 @@ struct Stage {
 
 struct zgpu_plan {
   zgpu_ctx *ctx = nullptr;
+  std::mutex mu;  // one execute / status at a time per plan
+  Lane own{};     // the plan's stream for executes without a caller stream (lazy)
   std::shared_ptr<Chain> chain;
   const Chain *leaf = nullptr;
   bool validate = true;
@@ -247,6 +307,11 @@ struct zgpu_plan {
 
   ~zgpu_plan() {
     if (!ctx) return;
+    if (own.stream) {
+      (void)hipStreamSynchronize(own.stream);
+      (void)hipStreamDestroy(own.stream);
+    }
+    if (own.order_ev) (void)hipEventDestroy(own.order_ev);
     void *bufs[] = {d_items, d_items_init, d_geom, d_shards, d_index, d_shard_status, d_mids, d_mids_init,
                     d_mid_status, d_shard_status2, d_mid_shards, d_index2,
                     d_pool[0], d_pool[1], zs.blks, zs.nblk, zs.mode, zs.lit, zs.seq, d_ctl,
@@ -282,7 +347,6 @@ const Chain &zgpu::chain_model(const zgpu_chain *c) { return *c->chain; }
 bool zgpu::chain_validates(const zgpu_chain *c) { return c->validate; }
 int zgpu::ctx_device(const zgpu_ctx *c) { return c->device; }
 void *zgpu::ctx_dev_alloc(zgpu_ctx *c, size_t bytes) {  // nullptr on failure
-  std::lock_guard<std::mutex> lk(c->mu);
   try {
     HIPCHK(hipSetDevice(c->device));
     return c->dev_alloc(bytes);
@@ -290,18 +354,15 @@ void *zgpu::ctx_dev_alloc(zgpu_ctx *c, size_t bytes) {  // nullptr on failure
     return nullptr;
   }
 }
-void zgpu::ctx_dev_free(zgpu_ctx *c, void *p) {
-  std::lock_guard<std::mutex> lk(c->mu);
-  c->dev_free(p);
-}
+void zgpu::ctx_dev_free(zgpu_ctx *c, void *p) { c->dev_free(p); }
 hipStream_t zgpu::ctx_copy_stream(zgpu_ctx *c) {  // nullptr on failure
-  std::lock_guard<std::mutex> lk(c->mu);
-  if (!c->copy[1] && (hipSetDevice(c->device) != hipSuccess ||
-                      hipStreamCreateWithFlags(&c->copy[1], hipStreamNonBlocking) != hipSuccess)) {
-    c->copy[1] = nullptr;
+  std::lock_guard<std::mutex> lk(c->lane_mu);
+  if (!c->peer && (hipSetDevice(c->device) != hipSuccess ||
+                   hipStreamCreateWithFlags(&c->peer, hipStreamNonBlocking) != hipSuccess)) {
+    c->peer = nullptr;
     return nullptr;
   }
-  return c->copy[1];
+  return c->peer;
 }
 
 // composed permutation of all array->array codecs: encoded axis a <-> decoded axis m[a]
@@ -649,9 +710,8 @@ static void plan_build(zgpu_plan &P, const zgpu_chunk_desc *descs) {
   P.scatter_units = P.items.empty() ? 0 : scatter_units_per_item(P.scatter_mode, S, max_sel);
 }
 
-static void plan_upload(zgpu_plan &P, hipStream_t us = nullptr) {
+static void plan_upload(zgpu_plan &P, hipStream_t us) {
   zgpu_ctx &C = *P.ctx;
-  if (!us) us = C.stream;
   const size_t ni = P.items.size();
   if (ni) {
     P.d_items = (ZgItem *)C.dev_alloc(ni * sizeof(ZgItem));
@@ -937,12 +997,19 @@ static zgpu_plan *plan_new(zgpu_chain *ch, uint32_t nd, const zgpu_chunk_desc *d
 // hip_stream NULL: the context's stream, ordered after all work already queued on the legacy
 // default stream (where torch's default stream and plain hipMemcpy/kernels land), so device buffers a
 // caller produced there are complete before the decode reads or writes them.
-static hipStream_t pick_stream(zgpu_ctx *c, void *s) {
+static hipStream_t pick_stream(Lane *L, void *s) {
   if (s) return (hipStream_t)s;
-  if (!c->order_ev) HIPCHK(hipEventCreateWithFlags(&c->order_ev, hipEventDisableTiming));
-  HIPCHK(hipEventRecord(c->order_ev, nullptr));
-  HIPCHK(hipStreamWaitEvent(c->stream, c->order_ev, 0));
-  return c->stream;
+  if (!L->order_ev) HIPCHK(hipEventCreateWithFlags(&L->order_ev, hipEventDisableTiming));
+  HIPCHK(hipEventRecord(L->order_ev, nullptr));
+  HIPCHK(hipStreamWaitEvent(L->stream, L->order_ev, 0));
+  return L->stream;
+}
+
+// a plan's own stream (executes without a caller stream: an asynchronous execute and its later
+// zgpu_plan_status must meet on one stream)
+static Lane *plan_lane(zgpu_plan &P) {
+  if (!P.own.stream) HIPCHK(hipStreamCreateWithFlags(&P.own.stream, hipStreamNonBlocking));
+  return &P.own;
 }
 
 // ------------------------------------------------------------------------------------------------
@@ -1034,7 +1101,8 @@ int zgpu_ctx_create(int dev, zgpu_ctx **out) {
   HIPCHK(hipSetDevice(dev));
   auto c = std::make_unique<zgpu_ctx>();
   c->device = dev;
-  HIPCHK(hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking));
+  if (const char *e = std::getenv("ZGPU_CTX_LANES")) c->max_lanes = (uint32_t)std::max(1, std::min(64, std::atoi(e)));
+  c->release_lane(c->acquire_lane());  // the first lane up front (stream creation errors surface here)
   *out = c.release();
   return ZGPU_OK;
   ABI_GUARD_END
@@ -1071,11 +1139,11 @@ int zgpu_plan_create(zgpu_chain *ch, uint32_t nd, const zgpu_chunk_desc *descs, 
   if (!ch || !out || !out_shape || (n && !descs)) return set_err(ZGPU_INVALID_ARGUMENT, "NULL argument");
   if (nd == 0 || nd > ZGPU_MAX_DIMS) return set_err(ZGPU_INVALID_ARGUMENT, "ndim out of range");
   if (!(flags & ZGPU_ENC_DEVICE)) return set_err(ZGPU_INVALID_ARGUMENT, "plans need device-resident inputs");
-  std::lock_guard<std::mutex> lk(ch->ctx->mu);
   HIPCHK(hipSetDevice(ch->ctx->device));
+  LaneScope ls(ch->ctx);
   std::unique_ptr<zgpu_plan> P(plan_new(ch, nd, descs, n, out_shape, flags));
-  plan_upload(*P);
-  HIPCHK(hipStreamSynchronize(ch->ctx->stream));
+  plan_upload(*P, ls.L->stream);
+  HIPCHK(hipStreamSynchronize(ls.L->stream));
   *out = P.release();
   return ZGPU_OK;
   ABI_GUARD_END
@@ -1084,9 +1152,9 @@ int zgpu_plan_create(zgpu_chain *ch, uint32_t nd, const zgpu_chunk_desc *descs, 
 int zgpu_plan_execute(zgpu_plan *P, void *out, int32_t *status, void *stream) {
   ABI_GUARD_BEGIN
   if (!P || !out) return set_err(ZGPU_INVALID_ARGUMENT, "NULL argument");
-  std::lock_guard<std::mutex> lk(P->ctx->mu);
+  std::lock_guard<std::mutex> lk(P->mu);
   HIPCHK(hipSetDevice(P->ctx->device));
-  hipStream_t s = pick_stream(P->ctx, stream);
+  hipStream_t s = pick_stream(plan_lane(*P), stream);
   reset_call_state();
   plan_enqueue(*P, (uint8_t *)out, s);
   if (!status) return ZGPU_OK;
@@ -1097,9 +1165,9 @@ int zgpu_plan_execute(zgpu_plan *P, void *out, int32_t *status, void *stream) {
 int zgpu_plan_status(zgpu_plan *P, int32_t *status, void *stream) {
   ABI_GUARD_BEGIN
   if (!P) return set_err(ZGPU_INVALID_ARGUMENT, "NULL argument");
-  std::lock_guard<std::mutex> lk(P->ctx->mu);
+  std::lock_guard<std::mutex> lk(P->mu);
   HIPCHK(hipSetDevice(P->ctx->device));
-  const int rc = plan_statuses(*P, status, pick_stream(P->ctx, stream));
+  const int rc = plan_statuses(*P, status, stream ? (hipStream_t)stream : plan_lane(*P)->stream);
   if (rc) set_err(rc, zgpu_status_name(rc));
   return rc;
   ABI_GUARD_END
@@ -1107,7 +1175,7 @@ int zgpu_plan_status(zgpu_plan *P, int32_t *status, void *stream) {
 
 void zgpu_plan_destroy(zgpu_plan *P) {
   if (!P) return;
-  std::lock_guard<std::mutex> lk(P->ctx->mu);
+  { std::lock_guard<std::mutex> lk(P->mu); }  // no execute of it still running on another thread
   delete P;
 }
 
@@ -1140,8 +1208,9 @@ uint32_t zgpu_last_counters(uint64_t *out, uint32_t n) {
 // (copy stream 0), decode (s) and D2H of its rows (copy stream 1) overlap with its neighbours' --
 // PCIe is full duplex, so the host-to-host rate approaches the one-direction bound instead of half
 // of it. Returns false (nothing done) when the batch does not cut into at least two sub-batches.
-static bool decode_pipelined(zgpu_chain *ch, uint32_t nd, const zgpu_chunk_desc *descs, uint64_t n, uint8_t *out,
-                             const uint64_t *out_shape, uint32_t flags, int32_t *status, hipStream_t s, int &rc) {
+static bool decode_pipelined(zgpu_chain *ch, Lane *LN, uint32_t nd, const zgpu_chunk_desc *descs, uint64_t n,
+                             uint8_t *out, const uint64_t *out_shape, uint32_t flags, int32_t *status, hipStream_t s,
+                             int &rc) {
   constexpr uint64_t K = 16;  // target sub-batches
   zgpu_ctx *C = ch->ctx;
   uint64_t row_bytes = ch->chain->es;
@@ -1167,7 +1236,7 @@ static bool decode_pipelined(zgpu_chain *ch, uint32_t nd, const zgpu_chunk_desc 
   if (groups.empty() || gr != groups.back().r1 || reach != out_shape[0]) return false;
   groups.push_back(Group{gb, n, gr, reach});
   if (groups.front().r0 != 0) return false;
-  for (hipStream_t &cs : C->copy)
+  for (hipStream_t &cs : LN->copy)
     if (!cs) HIPCHK(hipStreamCreateWithFlags(&cs, hipStreamNonBlocking));
   // encoded bytes: per sub-batch, address-sorted and merged ranges in one device staging buffer
   std::vector<size_t> range_of(n, SIZE_MAX);  // descriptor -> its merged range in its sub-batch
@@ -1209,8 +1278,8 @@ static bool decode_pipelined(zgpu_chain *ch, uint32_t nd, const zgpu_chunk_desc 
     for (size_t g = 0; g < groups.size(); g++) {
       const Group &G = groups[g];
       for (const HostRange &r : granges[g])
-        HIPCHK(hipMemcpyAsync(enc_dev + r.dev_off, r.src, r.len, hipMemcpyHostToDevice, C->copy[0]));
-      HIPCHK(hipEventRecord(ev[2 * g], C->copy[0]));
+        HIPCHK(hipMemcpyAsync(enc_dev + r.dev_off, r.src, r.len, hipMemcpyHostToDevice, LN->copy[0]));
+      HIPCHK(hipEventRecord(ev[2 * g], LN->copy[0]));
       std::vector<zgpu_chunk_desc> gd;
       gd.reserve(G.e - G.b);
       for (uint64_t k = G.b; k < G.e; k++) {
@@ -1230,9 +1299,9 @@ static bool decode_pipelined(zgpu_chain *ch, uint32_t nd, const zgpu_chunk_desc 
       HIPCHK(hipStreamWaitEvent(s, ev[2 * g], 0));
       plan_enqueue(*plans[g], dout, s);
       HIPCHK(hipEventRecord(ev[2 * g + 1], s));
-      HIPCHK(hipStreamWaitEvent(C->copy[1], ev[2 * g + 1], 0));
+      HIPCHK(hipStreamWaitEvent(LN->copy[1], ev[2 * g + 1], 0));
       HIPCHK(hipMemcpyAsync(out + G.r0 * row_bytes, dout + G.r0 * row_bytes, (G.r1 - G.r0) * row_bytes,
-                            hipMemcpyDeviceToHost, C->copy[1]));
+                            hipMemcpyDeviceToHost, LN->copy[1]));
     }
     std::vector<int32_t> all(n, 0);
     for (size_t g = 0; g < groups.size(); g++) {
@@ -1246,7 +1315,7 @@ static bool decode_pipelined(zgpu_chain *ch, uint32_t nd, const zgpu_chunk_desc 
       if (status) status[i] = all[i];
       if (!rc) rc = all[i];
     }
-    HIPCHK(hipStreamSynchronize(C->copy[1]));
+    HIPCHK(hipStreamSynchronize(LN->copy[1]));
   } catch (...) {
     (void)hipDeviceSynchronize();
     plans.clear();
@@ -1264,9 +1333,9 @@ int zgpu_decode_batch(zgpu_chain *ch, uint32_t nd, const zgpu_chunk_desc *descs,
   if (!ch || !out_shape || (n && !descs) || !out) return set_err(ZGPU_INVALID_ARGUMENT, "NULL argument");
   if (nd == 0 || nd > ZGPU_MAX_DIMS) return set_err(ZGPU_INVALID_ARGUMENT, "ndim out of range");
   zgpu_ctx *C = ch->ctx;
-  std::lock_guard<std::mutex> lk(C->mu);
   HIPCHK(hipSetDevice(C->device));
-  hipStream_t s = pick_stream(C, stream);
+  LaneScope ls(C);
+  hipStream_t s = pick_stream(ls.L, stream);
   reset_call_state();
   if (!(flags & ZGPU_ENC_DEVICE) && !(flags & ZGPU_OUT_DEVICE) && n >= 2) {
     // pinned host in and out, full coverage: the overlapped sub-batch pipeline
@@ -1283,7 +1352,7 @@ int zgpu_decode_batch(zgpu_chain *ch, uint32_t nd, const zgpu_chunk_desc *descs,
     }
     int rc = 0;
     if (pinned && covered == out_elems &&
-        decode_pipelined(ch, nd, descs, n, (uint8_t *)out, out_shape, flags, status, s, rc)) {
+        decode_pipelined(ch, ls.L, nd, descs, n, (uint8_t *)out, out_shape, flags, status, s, rc)) {
       if (rc) set_err(rc, zgpu_status_name(rc));
       return rc;
     }
@@ -1410,9 +1479,10 @@ int zgpu_decode_files(zgpu_chain *ch, uint32_t nd, const zgpu_chunk_desc *descs,
   if (!ch || !out_shape || (n && (!descs || !files)) || !out) return set_err(ZGPU_INVALID_ARGUMENT, "NULL argument");
   if (nd == 0 || nd > ZGPU_MAX_DIMS) return set_err(ZGPU_INVALID_ARGUMENT, "ndim out of range");
   zgpu_ctx *C = ch->ctx;
-  std::lock_guard<std::mutex> lk(C->mu);
   HIPCHK(hipSetDevice(C->device));
-  hipStream_t s = pick_stream(C, stream);
+  LaneScope ls(C);
+  Lane *LN = ls.L;
+  hipStream_t s = pick_stream(LN, stream);
   reset_call_state();
   const int threads = host_copy_threads();
   std::vector<FileRange> fr(n);
@@ -1457,14 +1527,14 @@ int zgpu_decode_files(zgpu_chain *ch, uint32_t nd, const zgpu_chunk_desc *descs,
   for (uint32_t d = 0; d < nd; d++) out_elems *= out_shape[d];
   const uint64_t out_bytes = out_elems * ch->chain->es;
   const bool host_out = !(flags & ZGPU_OUT_DEVICE);
-  for (hipStream_t &cs : C->copy)
+  for (hipStream_t &cs : LN->copy)
     if (!cs) HIPCHK(hipStreamCreateWithFlags(&cs, hipStreamNonBlocking));
   uint8_t *enc_dev = nullptr, *dout = (uint8_t *)out, *slab[2] = {nullptr, nullptr}, *pin_stage = nullptr;
   const uint64_t stage_slab = 64ull << 20;
   std::vector<hipEvent_t> ev(groups.size(), nullptr);
   std::vector<std::unique_ptr<zgpu_plan>> plans(groups.size());
   auto cleanup = [&]() {
-    (void)hipStreamSynchronize(C->copy[0]);
+    (void)hipStreamSynchronize(LN->copy[0]);
     (void)hipStreamSynchronize(s);
     plans.clear();
     for (hipEvent_t e : ev)
@@ -1502,8 +1572,8 @@ int zgpu_decode_files(zgpu_chain *ch, uint32_t nd, const zgpu_chunk_desc *descs,
         if (readable(i)) idx.push_back(i);
       err = fs_read_into(fr, idx, sl, threads);
       if (!err.empty()) throw ChainError{ZGPU_STORAGE_ERROR, err};
-      if (G.bytes) HIPCHK(hipMemcpyAsync(enc_dev + G.base, sl, G.bytes, hipMemcpyHostToDevice, C->copy[0]));
-      HIPCHK(hipEventRecord(ev[g], C->copy[0]));
+      if (G.bytes) HIPCHK(hipMemcpyAsync(enc_dev + G.base, sl, G.bytes, hipMemcpyHostToDevice, LN->copy[0]));
+      HIPCHK(hipEventRecord(ev[g], LN->copy[0]));
       std::vector<zgpu_chunk_desc> gd(descs + G.b, descs + G.e);
       for (uint64_t i = G.b; i < G.e; i++) {
         zgpu_chunk_desc &d = gd[i - G.b];
@@ -1945,9 +2015,9 @@ int zgpu_encode_chunks(zgpu_chain *ch, uint32_t nd, const uint64_t *chunk_shape,
       if (descs[i].chunk_start[d] >= array_shape[d])
         return set_err(ZGPU_INVALID_ARGUMENT, "encode: chunk origin outside the array");
   zgpu_ctx *C = ch->ctx;
-  std::lock_guard<std::mutex> lk(C->mu);
   HIPCHK(hipSetDevice(C->device));
-  hipStream_t s = pick_stream(C, stream);
+  LaneScope ls(C);
+  hipStream_t s = pick_stream(ls.L, stream);
   if (!n) return ZGPU_OK;
   std::vector<void *> owned;
   int rc = 0;
