@@ -737,11 +737,11 @@ class C5:
 # blosc
 # ------------------------------------------------------------------------------------------------
 class Blosc:
-    """u16 microscopy-style volume [256,1024,1024], chunks [64,256,256] (64 chunks of 8 MiB), codecs
+    """u16 microscopy-style volume [1024,2048,1024] (4 GiB), chunks [64,256,256] (512 chunks of 8 MiB), codecs
     [bytes, blosc{lz4, clevel 5, shuffle, typesize 2}] -- numcodecs' Blosc defaults, the most common
     compressor in existing OME-Zarr data. Chunks encoded on the host by c-blosc 1.21 (the oracle's
     library), decoded on the GPU from HBM; per-rank chunk partition, no collective."""
-    SHAPE, CHUNK = [256, 1024, 1024], [64, 256, 256]
+    SHAPE, CHUNK = [1024, 2048, 1024], [64, 256, 256]
     CNAME = "lz4"
     kernel = "blosc decode step (k_blosc_info/streams, stream decoders, k_blosc_finish, k_scatter_rows)"
     pmc_regex = "k_blosc|k_lz4|k_zstd|k_scatter"

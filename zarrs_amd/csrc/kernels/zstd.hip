@@ -21,6 +21,7 @@
 
 #include "../common.hpp"
 #include "launch.hpp"
+#include "xxh.hpp"
 
 #include <cstdlib>
 
@@ -521,70 +522,6 @@ __device__ __forceinline__ uint32_t lane_peek(LaneBits &L, uint32_t n) {
   }
   const uint32_t v = (uint32_t)(L.c64 >> (lo - (int64_t)L.ck * 32)) & ((1u << n) - 1);
   return v << shift_up;
-}
-
-// ---- XXH64 (content checksum), 4 lanes = the 4 accumulators ----
-constexpr uint64_t P1 = 11400714785074694791ull, P2 = 14029467366897019727ull, P3 = 1609587929392839161ull,
-                   P4 = 9650029242287828579ull, P5 = 2870177450012600261ull;
-__device__ __forceinline__ uint64_t rotl64(uint64_t x, int r) { return (x << r) | (x >> (64 - r)); }
-__device__ __forceinline__ uint64_t xround(uint64_t acc, uint64_t in) {
-  acc += in * P2;
-  acc = rotl64(acc, 31);
-  return acc * P1;
-}
-__device__ __forceinline__ uint64_t ld64(const uint8_t *p) {
-  uint64_t v = 0;
-  for (int i = 0; i < 8; i++) v |= (uint64_t)__builtin_nontemporal_load(p + i) << (8 * i);
-  return v;
-}
-__device__ uint64_t xxh64(const uint8_t *p, uint64_t len) {
-  const int lane = lane_id();
-  uint64_t h;
-  uint64_t off = 0;
-  if (len >= 32) {
-    uint64_t v = lane == 0 ? P1 + P2 : lane == 1 ? P2 : lane == 2 ? 0 : 0 - P1;
-    const uint64_t nst = len / 32;
-    if (lane < 4)
-      for (uint64_t s = 0; s < nst; s++) v = xround(v, ld64(p + s * 32 + lane * 8));
-    auto rl = [&](int l) -> uint64_t {
-      return (uint64_t)U(__builtin_amdgcn_readlane((uint32_t)v, l)) |
-             ((uint64_t)U(__builtin_amdgcn_readlane((uint32_t)(v >> 32), l)) << 32);
-    };
-    const uint64_t v1 = rl(0), v2 = rl(1), v3 = rl(2), v4 = rl(3);
-    h = rotl64(v1, 1) + rotl64(v2, 7) + rotl64(v3, 12) + rotl64(v4, 18);
-    const uint64_t vs[4] = {v1, v2, v3, v4};
-    for (int k = 0; k < 4; k++) {
-      h ^= xround(0, vs[k]);
-      h = h * P1 + P4;
-    }
-    off = nst * 32;
-  } else {
-    h = P5;
-  }
-  h += len;
-  while (off + 8 <= len) {
-    h ^= xround(0, U64(ld64(p + off)));
-    h = rotl64(h, 27) * P1 + P4;
-    off += 8;
-  }
-  if (off + 4 <= len) {
-    uint64_t w = 0;
-    for (int i = 0; i < 4; i++) w |= (uint64_t)U(__builtin_nontemporal_load(p + off + i)) << (8 * i);
-    h ^= w * P1;
-    h = rotl64(h, 23) * P2 + P3;
-    off += 4;
-  }
-  while (off < len) {
-    h ^= (uint64_t)U(__builtin_nontemporal_load(p + off)) * P5;
-    h = rotl64(h, 11) * P1;
-    off++;
-  }
-  h ^= h >> 33;
-  h *= P2;
-  h ^= h >> 29;
-  h *= P3;
-  h ^= h >> 32;
-  return h;
 }
 
 // ---- output engine: LDS ring + flush to the item slot ----
@@ -1743,7 +1680,9 @@ constexpr int LIT_STAGE_R = ZG_LIT_WPE >= 4 ? 4 : 8;  // 16-B staging loads in f
 #define ZG_LIT_STAGE 0  // 1: a lane's decoded literals leave through a 64-B LDS window, stored as whole
                         // aligned 64-B pieces (4 x 16-B stores) instead of 8-B stores
 #endif
+#if ZG_LIT_STAGE
 constexpr uint32_t LIT_STG_PITCH = 80;  // bytes per lane window (64 + 16: 16-B aligned, banks spread)
+#endif
 
 struct ZLitSmem {
   uint16_t huf[1 << MAX_HUF_LOG];

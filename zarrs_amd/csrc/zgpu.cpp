@@ -1736,7 +1736,7 @@ static int encode_fixed(zgpu_ctx *C, const Chain &c, uint32_t nd, const uint64_t
 static bool chain_compresses(const Chain &c) {
   for (const Codec &k : c.b2b)
     if (k.kind == CodecKind::Gzip || k.kind == CodecKind::Zstd || k.kind == CodecKind::Blosc) return true;
-  return false;
+  return false;  // (blosc is refused by encode_var: its encoder is not on the GPU)
 }
 
 // CodecChain::encode (codec_chain.rs:528-555) of a chain with a compressor, for n chunks whose origins
@@ -1766,17 +1766,19 @@ static int encode_var(zgpu_ctx *C, const Chain &c, uint32_t nd, const uint64_t *
       n_crc++;
     } else if (k.kind == CodecKind::Gzip) {
       size = gzip_bound(size);
+    } else if (k.kind == CodecKind::Zstd) {
+      size = zstd_bound(size);
     } else {
       return set_err(ZGPU_UNSUPPORTED, "encode: only transpose / bytes / numcodecs.shuffle (innermost, elementsize = "
-                                       "data type size) / crc32c / gzip run on the GPU write path");
+                                       "data type size) / crc32c / gzip / zstd run on the GPU write path");
     }
     max_size = std::max(max_size, size);
   }
   if (n_crc > 14) return set_err(ZGPU_UNSUPPORTED, "encode: too many crc32c codecs");
   constexpr uint64_t HR = 64;  // headroom in front of a slot's bytes (crc32c at the start)
   const uint64_t pitch = (HR + max_size + 4 * n_crc + 16 + 255) & ~(uint64_t)255;
-  bool gz = false;
-  for (const Codec &k : c.b2b) gz = gz || k.kind == CodecKind::Gzip;
+  bool gz = false;  // a compressor: its output goes to the other slot pool
+  for (const Codec &k : c.b2b) gz = gz || k.kind == CodecKind::Gzip || k.kind == CodecKind::Zstd;
   uint8_t *pool[2] = {(uint8_t *)C->dev_alloc(std::max<uint64_t>(n * pitch, 1)), nullptr};
   owned.push_back(pool[0]);
   if (gz) {
@@ -1804,6 +1806,7 @@ static int encode_var(zgpu_ctx *C, const Chain &c, uint32_t nd, const uint64_t *
   HIPCHK(hipMemsetAsync(d_status, 0, std::max<uint64_t>(n * 4, 4), s));
   int cur = 0;
   uint32_t *sym = nullptr;
+  uint8_t *zscr = nullptr;
   for (size_t i = 0; i < c.b2b.size(); i++) {
     const Codec &k = c.b2b[i];
     if (k.kind == CodecKind::Crc32c) {
@@ -1815,6 +1818,14 @@ static int encode_var(zgpu_ctx *C, const Chain &c, uint32_t nd, const uint64_t *
       }
       cur ^= 1;
       HIPCHK(launch_gzip_encode(d_items, d_status, (uint32_t)n, pool[cur], pitch, sym, k.level, s));
+    } else if (k.kind == CodecKind::Zstd) {
+      if (!zscr) {
+        zscr = (uint8_t *)C->dev_alloc((uint64_t)zstd_encode_grid((uint32_t)std::max<uint64_t>(n, 1)) *
+                                       zstd_encode_scratch());
+        owned.push_back(zscr);
+      }
+      cur ^= 1;
+      HIPCHK(launch_zstd_encode(d_items, d_status, (uint32_t)n, pool[cur], pitch, zscr, k.checksum ? 1 : 0, s));
     }
   }
   *d_items_out = d_items;
