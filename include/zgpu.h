@@ -26,10 +26,15 @@
  *                          323-470) feeding array_read_ops_array.rs:290-300, with the reads of
  *                          one sub-batch overlapped with the H2D copy and decode of the previous.
  *   zgpu_encode_batch   <- CodecChain::encode (codec_chain.rs:528-555), fixed-size chains
+ *   zgpu_encode_chunks  <- the same for variable-length chains: GzipCodec::encode (gzip_codec.rs:
+ *                          96-107), ZstdCodec::encode (zstd_codec.rs:100-111), crc32c around them, and
+ *                          ShardingCodecBound::encode_bounded (sharding_codec.rs:924-1085)
  *   status codes        <- CodecError variants (zarrs_codec/src/lib.rs:617-686), 1:1 (see below).
  *
- * Threading: every entry point is thread-safe; calls on one context are serialised internally
- * (they share the context's device scratch), calls on different contexts run concurrently.
+ * Threading: every entry point is thread-safe. Calls on one context run concurrently: each takes one
+ * of the context's lanes (stream + copy streams; ZGPU_CTX_LANES, default 4) for its duration and
+ * waits when all are busy; the context's pooled memory is shared under an allocator lock. A plan
+ * serialises its own executes.
  * Stream ordering: a call runs on the caller's hip_stream (device inputs/outputs must be ready in
  * that stream's order), or with hip_stream NULL on the context's own stream, which first waits for
  * all work queued so far on the legacy default stream.
@@ -256,7 +261,7 @@ int zgpu_retrieve_array_subset_files(zgpu_chain *chain, uint32_t ndim, const uin
  * Write path: CodecChain::encode (zarrs/src/array/codec/array_to_bytes/
  * codec_chain.rs:528-555) for fixed-size chains -- transpose, bytes (endianness), numcodecs.shuffle
  * (innermost, elementsize = data type size), crc32c (end or start, any number). Compressing codecs
- * return ZGPU_UNSUPPORTED; sharding_indexed goes through zgpu_encode_chunks (variable lengths).
+ * and sharding_indexed return ZGPU_UNSUPPORTED here: they go through zgpu_encode_chunks.
  * zgpu_chain_encoded_size: encoded bytes of one chunk of chunk_shape (BytesRepresentation::FixedSize),
  * -1 if the chain's encoded size is not fixed.
  * zgpu_encode_batch: encode the chunks whose origins are descs[i].chunk_start (in elements) of the
@@ -274,12 +279,19 @@ int zgpu_encode_batch(zgpu_chain *chain, uint32_t ndim, const uint64_t *chunk_sh
                       const uint64_t *array_shape, const zgpu_encode_desc *descs, uint64_t n, uint32_t flags,
                       void *hip_stream);
 /*
- * zgpu_encode_batch plus sharding_indexed over a fixed-size inner chain (ShardingCodecBound::
- * encode_bounded, sharding_codec.rs:924-1085, with SubchunkWriteOrder::C: inner chunks in C order of
- * the inner grid, an inner chunk equal to the fill value everywhere omitted, index bytes{endian} +
- * crc32c at the start or end). enc_lens[n] receives each chunk's encoded length (variable for shards);
- * descs[i].dst_cap must be >= zgpu_chain_encoded_bound. zgpu_chain_encoded_bound: the fixed size, or a
- * shard's bounded size (every inner chunk present + index), -1 if unbounded.
+ * zgpu_encode_batch plus the variable-length chains: gzip (one DEFLATE stream of dynamic-Huffman or
+ * stored blocks in a gzip member, k_gzip_encode), zstd (one single-segment frame, raw literals,
+ * predefined-FSE sequences, optional XXH64 content checksum, k_zstd_encode), crc32c around them,
+ * the fixed-size stages in front, and sharding_indexed over a fixed-size or compressing inner chain
+ * (ShardingCodecBound::encode_bounded, sharding_codec.rs:924-1085, with SubchunkWriteOrder::C: inner
+ * chunks in C order of the inner grid, an inner chunk equal to the fill value everywhere omitted,
+ * index bytes{endian} + crc32c at the start or end). The compressed bytes are valid streams that
+ * every gzip / zstd decoder reads back to the input; they are not byte-identical to zlib's or
+ * libzstd's output (the Zarr specification fixes the decoded bytes, not the encoder). blosc returns
+ * ZGPU_UNSUPPORTED. enc_lens[n] receives each chunk's encoded length; descs[i].dst_cap must be >=
+ * zgpu_chain_encoded_bound. zgpu_chain_encoded_bound: the fixed size, or the worst case
+ * (gzip_codec.rs:122-136, zstd_codec.rs:132-147; a shard: every inner chunk at its bound + index),
+ * -1 if unbounded.
  */
 int64_t zgpu_chain_encoded_bound(const zgpu_chain *chain, uint32_t ndim, const uint64_t *chunk_shape);
 int zgpu_encode_chunks(zgpu_chain *chain, uint32_t ndim, const uint64_t *chunk_shape, const void *array,

@@ -378,8 +378,8 @@ def test_zstd_encode_large_chunk_and_small_chunks(ctx, torch_cuda):
     co = O.OracleChain.from_metadata([B("little"), ZS], "uint8", 0, 1)
     ch = CodecChain.from_metadata([B("little"), ZS], "uint8", 0, ctx)
     rng = np.random.default_rng(5)
-    blk = rng.integers(0, 256, 70000, dtype=np.uint8)
-    big = np.concatenate([np.tile(blk, 40), np.zeros(1 << 20, np.uint8), rng.integers(0, 4, 300000, dtype=np.uint8)])
+    blk = rng.integers(0, 256, 3000, dtype=np.uint8)
+    big = np.concatenate([np.tile(blk, 933), np.zeros(1 << 20, np.uint8), rng.integers(0, 4, 300000, dtype=np.uint8)])
     n = len(big)
     x = torch_cuda.from_numpy(big).cuda()
     enc = ch.encode_chunks(x, [n], [[0]])

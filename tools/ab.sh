@@ -10,9 +10,13 @@ O=gpurun_out/$TAG
 mkdir -p "$O"
 for rep in 1 2; do
   for v in "$@"; do
-    lib=""; [ "$v" != base ] && lib=zarrs_amd/lib_variants/$v/libzgpu.so
-    ZGPU_LIB=$lib timeout -k 10 400 python -u bench.py --workload "$W" --no-cpu --no-pmc --no-host-leg --secondary= \
-      --steps "$N" --warmup 2 > "$O/$v.$rep.json" 2> "$O/$v.$rep.err" || { echo "$v rc=$?"; tail -5 "$O/$v.$rep.err"; exit 1; }
+    # a variant is a library under zarrs_amd/lib_variants/, or NAME=VALUE: the base library with that
+    # environment variable set
+    lib=""; ev=""
+    case "$v" in base) ;; *=*) ev=$v ;; *) lib=zarrs_amd/lib_variants/$v/libzgpu.so ;; esac
+    ( [ -n "$ev" ] && export "$ev"; ZGPU_LIB=$lib timeout -k 10 400 python -u bench.py --workload "$W" --no-cpu \
+      --no-pmc --no-host-leg --secondary= --steps "$N" --warmup 2 ) > "$O/$v.$rep.json" 2> "$O/$v.$rep.err" \
+      || { echo "$v rc=$?"; tail -5 "$O/$v.$rep.err"; exit 1; }
     python3 -c "import json,sys; d=json.load(open('$O/$v.$rep.json')); print('$v', $rep, d['value'], d['unit'], d['ms_per_step'], 'ms', 'ok' if d['roundtrip_ok'] else 'MISMATCH')"
   done
 done

@@ -5,8 +5,8 @@
 //
 // One 64-lane wave encodes one item, in superblocks of 64 zstd blocks of ZE_BLK input bytes:
 //   1. LZ77 over the superblock, 64 positions per step (the gzip encoder's scheme, deflate_enc.hip):
-//      per lane a 4-byte hash bucket candidate (u16 positions, 64 KiB window) and a match of up to 32
-//      bytes; the greedy parse is a scalar walk over the ballot of match-starting lanes, and a chosen
+//      per lane a 4-byte hash bucket candidate (u32 positions: the window is the whole frame, offsets
+//      below 2^29) and a match of up to 32 bytes; the greedy parse is a scalar walk over the ballot of match-starting lanes, and a chosen
 //      match that reached 32 bytes is extended by the whole wave (64 x 4 bytes per step). Matches never
 //      cross a block end. Chosen literals go to the block's literal scratch, matches to its sequence
 //      scratch (literal length, match length, offset), counted per block.
@@ -32,6 +32,7 @@ constexpr uint32_t ZE_SB = ZE_BLK * ZE_NB;   // superblock input bytes
 constexpr uint32_t ZE_SEQ = ZE_BLK / 4;      // sequences per block at most (matches >= 4 bytes)
 constexpr uint32_t ZE_BITW = 2048;           // bitstream scratch words per block (61 bits x 1024 seqs)
 constexpr uint32_t ZE_HBITS = 12, ZE_HSIZE = 1u << ZE_HBITS;
+constexpr uint32_t ZE_MAXOFF = (1u << 29) - 4;  // offset + 3 within the predefined OF table (codes <= 28)
 constexpr uint32_t ZE_CAP1 = 32;             // per-lane match search; longer chosen matches: the wave
 constexpr uint64_t ZE_SCRATCH = (uint64_t)ZE_SB + (uint64_t)ZE_NB * ZE_SEQ * 8 + (uint64_t)ZE_NB * ZE_BITW * 4;
 
@@ -67,7 +68,7 @@ struct PreTab {
 };
 
 struct ZeSmem {
-  uint16_t head[ZE_HSIZE];  // hash -> (position + 1) mod 2^16, 0 = empty
+  uint32_t head[ZE_HSIZE];  // hash -> position + 1 of the last 4-byte string with that hash, 0 = empty
   PreTab<6, 36> ll;
   PreTab<6, 53> ml;
   PreTab<5, 29> of;
@@ -232,7 +233,7 @@ __global__ __launch_bounds__(64) void k_zstd_encode(ZgItem *items, uint32_t *sta
     const uint32_t n = (uint32_t)it.len;
     uint8_t *out = slots + (uint64_t)item * slot_bytes + ZE_HDR;
     const uint64_t cap = slot_bytes - ZE_HDR - 8;
-    for (uint32_t k = lane; k < ZE_HSIZE / 2; k += 64) ((uint32_t *)S.head)[k] = 0;
+    for (uint32_t k = lane; k < ZE_HSIZE; k += 64) S.head[k] = 0;
     // frame header: magic, descriptor (single segment, content size, checksum flag), content size
     const uint32_t fcs_flag = n <= 255 ? 0u : n <= 65535 + 256 ? 1u : 2u;
     const uint32_t fcs_len = fcs_flag == 0 ? 1 : fcs_flag == 1 ? 2 : 4;
@@ -267,16 +268,11 @@ __global__ __launch_bounds__(64) void k_zstd_encode(ZgItem *items, uint32_t *sta
           const uint32_t h = (w4 * 0x9E3779B1u) >> (32 - ZE_HBITS);
           const uint32_t hvv = hv ? S.head[h] : 0u;
           WSYNC();
-          if (hv && ((p + 1) & 0xFFFF)) S.head[h] = (uint16_t)(p + 1);
+          if (hv) S.head[h] = p + 1;
           uint32_t mlen = 0, cand = 0;
           if (hvv && p >= skip && p + 4 <= b1) {
-            cand = (p & ~0xFFFFu) | (hvv - 1);
-            bool ok = true;
-            if (cand >= p) {
-              ok = p >= 65536u;
-              cand -= 65536u;
-            }
-            if (ok && ld4(in + cand) == w4) {
+            cand = hvv - 1;  // < p; the window is the whole frame (single segment)
+            if (p - cand <= ZE_MAXOFF && ld4(in + cand) == w4) {
               const uint32_t lim = min(ZE_CAP1, b1 - p);
               uint32_t k = 4;
               bool done = false;
