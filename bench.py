@@ -459,7 +459,58 @@ class C3:
                           f"{threads} threads"}
 
     def host_leg(self, sp):
-        return {"dropin_emulation": self.dropin_leg()}
+        return {"dropin_emulation": self.dropin_leg(), "encode": self.encode_leg()}
+
+    def encode_leg(self):
+        """Write path (SURVEY 8(f) rank 3): CodecChain::encode of the 64 whole shards this subset touches
+        (ShardingCodecBound::encode_bounded over [bytes, gzip 1, crc32c] inner chunks + the crc32c'd
+        index, sharding_codec.rs:924-1085) from a device-resident array, on the GPU (k_gzip_encode,
+        gzip_codec.rs:96-107): decoded GiB/s, the compressed size against the workload's own zlib-1
+        shards, a round trip through the GPU decoder, and the oracle's encoder (zlib deflate level 1,
+        one shard per host thread) on a 16-shard sample beside it."""
+        from concurrent.futures import ThreadPoolExecutor
+        from zarrs_amd import make_desc
+        sys.path.insert(0, os.path.join(ROOT, "oracle"))
+        import oracle as O
+        S = self.SHARD
+        keys = sorted(self.shards)
+        lo = [min(k[d] for k in keys) for d in range(3)]
+        shape = [(max(k[d] for k in keys) - lo[d] + 1) * S for d in range(3)]
+        host = np.empty(shape, np.float32)
+        _synth().synth_c3_values(_u64([l * S for l in lo]), _u64(shape), host.ctypes.data, _threads())
+        x = torch.from_numpy(host).to(self.dev)
+        starts = [[(k[d] - lo[d]) * S for d in range(3)] for k in keys]
+        enc = self.chain.encode_chunks(x, [S] * 3, starts)  # warm-up (pools, scratch)
+        torch.cuda.synchronize()
+
+        def run():
+            r = self.chain.encode_chunks(x, [S] * 3, starts)
+            torch.cuda.synchronize()
+            return r
+        times = _time_reps(run, 3.0)
+        enc = run()
+        gpu_bytes = sum(int(e.numel()) for e in enc)
+        zlib_bytes = sum(int(self.shards[k][1].nbytes) for k in keys)
+        out = torch.empty_like(x)
+        descs = [make_desc((e.data_ptr(), int(e.numel())), [S] * 3, out_start=st) for e, st in zip(enc, starts)]
+        ok = self.chain.decode_batch(descs, out, shape, enc_device=True) == [0] * len(keys)
+        ok = ok and bool(torch.equal(out.view(torch.int32), x.view(torch.int32)))
+        del out
+        t = float(np.median(times))
+        nbytes = host.nbytes
+        # CPU: the oracle's sharding encoder, 16 shards (one per thread)
+        co = O.OracleChain.from_metadata(self.CODECS, "float32", 0.0, 3)
+        sample = [np.ascontiguousarray(host[tuple(slice(a, a + S) for a in st)]) for st in starts[:16]]
+        threads = _threads()
+        with ThreadPoolExecutor(threads) as ex:
+            tc = float(np.median(_time_reps(lambda: list(ex.map(co.encode, sample)), 5.0)))
+        return {"GiBps": round(nbytes / t / 2 ** 30, 2), "ms": round(t * 1e3, 1), "shards": len(keys),
+                "decoded_bytes": nbytes, "encoded_bytes": gpu_bytes,
+                "size_vs_zlib1": round(gpu_bytes / zlib_bytes, 4), "roundtrip_ok": ok,
+                "cpu_oracle_GiBps": round(sum(b.nbytes for b in sample) / tc / 2 ** 30, 3), "cpu_threads": threads,
+                "note": "zgpu_encode_chunks of whole 256^3 shards from HBM (host-synchronous call incl. its result "
+                        "read-back); size_vs_zlib1 = GPU shard bytes / zlib-1 shard bytes (tools/synth); CPU: "
+                        "oracle encode (zlib deflate level 1 + crc32c + index), one shard per thread, 16 shards"}
 
     def dropin_leg(self):
         """The drop-in boundary's real call pattern (rust/zarrs_gpu with its sharding_indexed plugin
@@ -730,7 +781,56 @@ class C5:
                           f"oracle retrieve_array_subset per level (libzstd) with {threads} threads"}
 
     def host_leg(self, sp):
-        return None
+        return {"encode": self.encode_leg()}
+
+    def encode_leg(self):
+        """Write path (SURVEY 8(f) rank 3): CodecChain::encode of level 0's whole chunks ([32,512,512]
+        u16; 1024 chunks, 16 GiB at full scale) from HBM on the GPU (numcodecs.shuffle + k_zstd_encode: ZstdCodec::encode,
+        zstd_codec.rs:100-111): decoded GiB/s, the compressed size against the workload's libzstd
+        level-3 chunks, a round trip through the GPU decoder, and the oracle's encoder (libzstd level 3)
+        on 32 of those chunks, one per host thread, beside it."""
+        from concurrent.futures import ThreadPoolExecutor
+        from zarrs_amd import make_desc
+        sys.path.insert(0, os.path.join(ROOT, "oracle"))
+        import oracle as O
+        cs = self.CHUNKS[0]
+        x = self.expected[0]
+        l0 = [(i, idx) for i, (li, idx, _) in enumerate(self.all_chunks) if li == 0]
+        l0 = [(i, idx) for i, idx in l0
+              if all((k + 1) * c <= s_ for k, c, s_ in zip(idx, cs, x.shape))]  # whole chunks only
+        starts = [[k * c for k, c in zip(idx, cs)] for _, idx in l0]
+        self.chain.encode_chunks(x, cs, starts)  # warm-up
+        torch.cuda.synchronize()
+
+        def run():
+            r = self.chain.encode_chunks(x, cs, starts)
+            torch.cuda.synchronize()
+            return r
+        times = _time_reps(run, 3.0)
+        enc = run()
+        gpu_bytes = sum(int(e.numel()) for e in enc)
+        ref_bytes = sum(int(self.enc_host[i].nbytes) for i, _ in l0)
+        out = torch.zeros_like(x)
+        descs = [make_desc((e.data_ptr(), int(e.numel())), cs, out_start=st) for e, st in zip(enc, starts)]
+        ok = self.chain.decode_batch(descs, out, list(x.shape), enc_device=True) == [0] * len(l0)
+        for st in starts:
+            sl = tuple(slice(a, a + c) for a, c in zip(st, cs))
+            ok = ok and bool(torch.equal(out[sl], x[sl]))
+        del out, enc
+        t = float(np.median(times))
+        nbytes = len(l0) * int(np.prod(cs)) * 2
+        co = O.OracleChain.from_metadata(self.CODECS, "uint16", 0, 3)
+        sample = [self.all_chunks[i][2] for i, _ in l0[:32]]
+        threads = _threads()
+        with ThreadPoolExecutor(threads) as ex:
+            tc = float(np.median(_time_reps(lambda: list(ex.map(co.encode, sample)), 5.0)))
+        return {"GiBps": round(nbytes / t / 2 ** 30, 2), "ms": round(t * 1e3, 1), "chunks": len(l0),
+                "decoded_bytes": nbytes, "encoded_bytes": gpu_bytes,
+                "size_vs_libzstd3": round(gpu_bytes / ref_bytes, 4), "roundtrip_ok": ok,
+                "cpu_oracle_GiBps": round(sum(b.nbytes for b in sample) / tc / 2 ** 30, 3), "cpu_threads": threads,
+                "note": "zgpu_encode_chunks of whole L0 chunks from HBM (host-synchronous call incl. its result "
+                        "read-back); size_vs_libzstd3 = GPU bytes / libzstd level-3 bytes of the same chunks; "
+                        "CPU: oracle encode (shuffle + libzstd level 3), one chunk per thread, 32 chunks"}
 
 
 # ------------------------------------------------------------------------------------------------

@@ -157,6 +157,49 @@ def test_blosc_memcpyed_and_errors(ctx, torch_cuda):
     assert ei.value.status == L.DECODED_SIZE_MISMATCH
 
 
+@pytest.mark.parametrize("cname,shuffle,clevel", [("lz4", "shuffle", 5), ("blosclz", "shuffle", 9),
+                                                  ("zstd", "bitshuffle", 3), ("lz4", "noshuffle", 0),
+                                                  ("zlib", "shuffle", 1)])
+def test_blosc_direct_output_rows(ctx, torch_cuda, cname, shuffle, clevel):
+    """Whole chunks of a 3-D u16 array: blosc is the chain's last stage and the scatter would copy
+    the rows unchanged, so k_blosc_finish writes the unshuffled rows straight into the output
+    (ZG_ITEM_DIRECT, fast u16 path and the bitshuffle / memcpyed byte paths, forced small blocks);
+    a missing chunk still takes the scatter's fill, a partial subset the slot path. vs the oracle."""
+    from zarrs_amd import CodecChain, make_desc
+    rng = np.random.default_rng(len(cname) + clevel)
+    shape, cs = [4, 96, 512], [2, 48, 256]
+    z, y, x = np.meshgrid(*[np.arange(n) for n in shape], indexing="ij")
+    a = (500 + 300 * np.sin(y * 0.07) * np.cos(x * 0.05) + rng.integers(0, 40, shape)).astype(np.uint16)
+    for bsz in (0, 4096):
+        codecs = [{"name": "bytes", "configuration": {"endian": "little"}}, _blosc(cname, shuffle, 2, bsz, clevel)]
+        co = O.OracleChain.from_metadata(codecs, "uint16", 7, 1)
+        ch = CodecChain.from_metadata(codecs, "uint16", 7, ctx)
+        exp = a.copy()
+        descs, keep = [], []
+        for idx in np.ndindex(2, 2, 2):
+            sl = tuple(slice(i * c, (i + 1) * c) for i, c in zip(idx, cs))
+            o = [i * c for i, c in zip(idx, cs)]
+            if idx == (1, 1, 0):  # missing chunk: fill value
+                exp[sl] = 7
+                descs.append(make_desc((0, 0), cs, out_start=o))
+                continue
+            d = torch_cuda.frombuffer(bytearray(co.encode(np.ascontiguousarray(a[sl]))), dtype=torch_cuda.uint8).cuda()
+            keep.append(d)
+            descs.append(make_desc(d, cs, out_start=o))
+        out = torch_cuda.zeros(shape, dtype=torch_cuda.int16, device="cuda")
+        assert ch.decode_batch(descs, out, shape, enc_device=True) == [0] * 8
+        assert np.array_equal(out.cpu().numpy().view(np.uint16), exp), bsz
+        # a partial selection of every chunk: the slot + scatter path
+        sub = [make_desc((dd.enc, dd.enc_len), cs, sel_start=[1, 5, 16], sel_shape=[1, 40, 224],
+                         out_start=[i * 1, 0, 0]) for i, dd in enumerate(descs[:4])]
+        out2 = torch_cuda.zeros([4, 40, 224], dtype=torch_cuda.int16, device="cuda")
+        assert ch.decode_batch(sub, out2, [4, 40, 224], enc_device=True) == [0] * 4
+        for i in range(4):
+            idx = list(np.ndindex(2, 2, 2))[i]
+            src = exp[tuple(slice(j * c, (j + 1) * c) for j, c in zip(idx, cs))]
+            assert np.array_equal(out2[i].cpu().numpy().view(np.uint16), src[1, 5:45, 16:240]), (bsz, i)
+
+
 @pytest.mark.parametrize("clevel", [1, 5, 9])
 def test_blosclz_streams_vs_cblosc(ctx, torch_cuda, clevel):
     """blosclz (c-blosc's default compressor, the one zarrs benchmarks: benches/codecs.rs:52): long

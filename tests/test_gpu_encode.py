@@ -296,6 +296,37 @@ def test_gzip_encode_small_and_ragged_chunks(ctx, torch_cuda):
                 assert zlib.decompress(e.cpu().numpy().tobytes(), 31) == blk.tobytes(), (dt, n, st)
 
 
+def test_gzip_encode_huffman_length_limits(ctx, torch_cuda):
+    """Length-limited Huffman codes (zlib gen_bitlen: every node clamped to the limit counts as an
+    overflow, internal ones included): the code-length code at its 7-bit limit on the C3 inner chunk
+    where counting clamped leaves only left it over-subscribed (zlib: "invalid code lengths set";
+    the C3 synth volume at [0:32, 352:384, 1024:1056], tools/synth), and literal codes at the 15-bit
+    limit on bytes with Fibonacci-distributed frequencies (optimal depth ~24), through zlib."""
+    import ctypes as C
+    import os
+    import zlib
+    from zarrs_amd import CodecChain
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    syn = C.CDLL(os.path.join(root, "tools", "synth", "libsynth.so"))
+    P64 = C.POINTER(C.c_uint64)
+    syn.synth_c3_values.argtypes = [P64, P64, C.c_void_p, C.c_int]
+    u64 = lambda v: (C.c_uint64 * 3)(*v)  # noqa: E731
+    a = np.empty([32, 32, 32], np.float32)
+    syn.synth_c3_values(u64([0, 352, 1024]), u64([32, 32, 32]), a.ctypes.data, 4)
+    ch = CodecChain.from_metadata([B("little"), GZ], "float32", 0, ctx)
+    e = ch.encode_chunks(torch_cuda.from_numpy(a).cuda(), [32, 32, 32], [[0, 0, 0]])[0]
+    assert zlib.decompress(e.cpu().numpy().tobytes(), 31) == a.tobytes()
+    fib = [1, 1]
+    while len(fib) < 26:
+        fib.append(fib[-1] + fib[-2])
+    rng = np.random.default_rng(11)
+    b = rng.permutation(np.repeat(np.arange(26, dtype=np.uint8) * 7, fib))
+    chb = CodecChain.from_metadata([B("little"), GZ], "uint8", 0, ctx)
+    n = len(b)
+    e = chb.encode_chunks(torch_cuda.from_numpy(b).cuda(), [n], [[0]])[0]
+    assert zlib.decompress(e.cpu().numpy().tobytes(), 31) == b.tobytes()
+
+
 def test_sharding_gzip_encode_c3_chain(ctx, torch_cuda):
     """ShardingCodecBound::encode over SURVEY C3's exact inner chain ([bytes, gzip 1, crc32c], index
     [bytes, crc32c] at the end) on the GPU: shards decode through the oracle (zlib) and the GPU to

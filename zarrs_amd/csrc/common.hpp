@@ -16,6 +16,7 @@
 #define ZG_ITEM_FILL 0x1u     // write the fill value (missing chunk / empty inner chunk)
 #define ZG_ITEM_PARTIAL 0x2u  // partial-decoder path: crc32c strips without verifying
 #define ZG_ITEM_SHARDED 0x4u  // src/len resolved on device from the shard index
+#define ZG_ITEM_DIRECT 0x8u   // already written into the output by its last stage: the scatter skips it
 
 struct ZgItem {
   uint64_t src;    // device address of the current encoded bytes

@@ -144,7 +144,8 @@ __global__ __launch_bounds__(1024) void k_blosc_layout(const BlInfo *info, uint3
 __global__ __launch_bounds__(64) void k_blosc_streams(ZgItem *items, uint32_t *status, const BlInfo *info,
                                                       const uint64_t *bases, ZgItem *subs, uint32_t *sub_status,
                                                       uint32_t *sub_kind, BlBlock *blocks, uint8_t *dst,
-                                                      uint64_t slot_bytes, const unsigned long long *ovf) {
+                                                      uint64_t slot_bytes, const unsigned long long *ovf,
+                                                      uint32_t direct, uint64_t want, uint64_t row_bytes) {
   const uint32_t item = blockIdx.x, lane = threadIdx.x;
   const BlInfo I = info[item];
   if (I.comp == BL_COMP_SKIP || status[item] || *ovf) return;
@@ -152,6 +153,7 @@ __global__ __launch_bounds__(64) void k_blosc_streams(ZgItem *items, uint32_t *s
   const uint8_t *h = (const uint8_t *)it.src;
   const uint64_t sub0 = bases[2 * item], blk0 = bases[2 * item + 1];
   bool bad = false;
+  uint64_t blk_bytes = I.nbytes;  // the largest block
   if (I.comp == BL_COMP_MEMCPY) {
     if (lane == 0 && I.nblk) {
       subs[sub0] = ZgItem{it.src + 16, I.nbytes, item, 0, 0, 0};
@@ -163,6 +165,7 @@ __global__ __launch_bounds__(64) void k_blosc_streams(ZgItem *items, uint32_t *s
     const uint32_t flags = h[2], ts = h[3], bs = ld_u32(h + 8), cbytes = ld_u32(h + 12);
     const uint32_t lo = I.nbytes % bs, nsplit_full = (flags & 0x10) ? 1 : ts;
     const uint32_t mode = ((flags & 0x1) && ts > 1) ? 1u : (flags & 0x4) ? 2u : 0u;
+    blk_bytes = bs;
     for (uint32_t b = lane; b < I.nblk; b += 64) {
       const bool left = lo && b == I.nblk - 1;
       const uint32_t bsize = left ? lo : bs, nsplit = left ? 1 : nsplit_full, ne = bsize / nsplit;
@@ -209,6 +212,10 @@ __global__ __launch_bounds__(64) void k_blosc_streams(ZgItem *items, uint32_t *s
     } else {  // the item's decoded bytes will be in its slot (written by k_blosc_finish)
       items[item].src = (uint64_t)(dst + (uint64_t)item * slot_bytes);
       items[item].len = I.nbytes;
+      // or straight in the output rows (a size mismatch takes the slot path: the scatter reports it
+      // after the decode, as the chain's size check follows the codec's)
+      if (direct && I.nbytes == want && blk_bytes <= (uint64_t)(BL_DIRECT_ROWS - 2) * row_bytes)
+        items[item].flags = it.flags | ZG_ITEM_DIRECT;
     }
   }
 }
@@ -508,9 +515,12 @@ __global__ __launch_bounds__(64) void k_snappy(ZgItem *subs, uint32_t *sub_statu
 // block; unshuffle / bitunshuffle into the item's output slot.
 __global__ __launch_bounds__(256) void k_blosc_finish(const BlBlock *blocks, const ZgItem *subs,
                                                       const uint32_t *sub_status, const uint32_t *sub_kind,
-                                                      uint32_t *status, uint8_t *dst, uint64_t slot_bytes) {
+                                                      uint32_t *status, uint8_t *dst, uint64_t slot_bytes,
+                                                      const ZgItem *items, uint8_t *dout, const uint64_t *geom,
+                                                      ZgScatter sc) {
   const BlBlock B = blocks[blockIdx.x];
   __shared__ uint64_t src[256];
+  __shared__ uint64_t s_row[BL_DIRECT_ROWS];  // direct output: the output address of each row the block covers
   __shared__ uint32_t bad;
   if (threadIdx.x == 0) bad = status[B.item] ? 2u : 0u;  // one read: other blocks may set it meanwhile
   __syncthreads();
@@ -536,7 +546,33 @@ __global__ __launch_bounds__(256) void k_blosc_finish(const BlBlock *blocks, con
     const uint32_t j = ne ? q / ne : 0;
     return ((const uint8_t *)src[j])[q - j * ne];
   };
-  if (B.mode == 1 && (ts == 2 || ts == 4) && ne && bsize % (16 * ts) == 0 && ((uintptr_t)out & 15) == 0) {
+  // direct output: chunk byte c lives in row c / Lb (C order over the chunk's leading axes) at
+  // column c mod Lb; the block's rows are resolved once into s_row
+  const bool direct = dout && (items[B.item].flags & ZG_ITEM_DIRECT);
+  const uint32_t nd = sc.nd;
+  const uint32_t Lb = direct ? (uint32_t)(sc.chunk_shape[nd - 1] * sc.es) : 1u;
+  const uint32_t c0 = (uint32_t)B.out_off, r0 = c0 / Lb;
+  if (direct && bsize) {
+    const uint64_t *g = geom + (uint64_t)B.item * 3 * nd;  // sel_start (0) | sel_shape | out_start
+    const uint32_t nr = (c0 + bsize - 1) / Lb - r0 + 1;
+    for (uint32_t k = threadIdx.x; k < nr; k += 256) {
+      uint64_t r = r0 + k, e = g[2 * nd + nd - 1];
+      for (int d = (int)nd - 2; d >= 0; d--) {
+        const uint64_t ext = sc.chunk_shape[d], c = r % ext;
+        r /= ext;
+        e += (g[2 * nd + d] + c) * sc.out_stride[d];
+      }
+      s_row[k] = (uint64_t)dout + e * sc.es;
+    }
+    __syncthreads();
+  }
+  auto dptr = [&](uint32_t q) -> uint8_t * {  // destination of block byte q
+    if (!direct) return out + q;
+    const uint32_t c = c0 + q, r = c / Lb;
+    return (uint8_t *)s_row[r - r0] + (c - r * Lb);
+  };
+  if (B.mode == 1 && (ts == 2 || ts == 4) && ne && bsize % (16 * ts) == 0 && ((uintptr_t)out & 15) == 0 &&
+      (c0 & 15) == 0) {
     // u16 / u32 fast path: 16 elements per thread, a 16-B load from each byte plane and ts 16-B
     // stores of the interleaved bytes (the generic loop below moves a byte per lane with two
     // integer divisions); planes that are not 16-B aligned (stored streams inside the frame) fall
@@ -550,7 +586,8 @@ __global__ __launch_bounds__(256) void k_blosc_finish(const BlBlock *blocks, con
       al = al && ((uintptr_t)pl[i] & 15) == 0;
     }
     if (al) {
-      uint4 *o = (uint4 *)out;
+      // output vector k of the block (16 B, never across a row: rows are 16-B multiples)
+      auto o = [&](uint32_t k) -> uint4 & { return *(uint4 *)dptr(16 * k); };
       for (uint32_t v = threadIdx.x; v < neb / 16; v += 256) {
         if (ts == 2) {
           const uint4 a = pl[0][v], b = pl[1][v];
@@ -562,8 +599,8 @@ __global__ __launch_bounds__(256) void k_blosc_finish(const BlBlock *blocks, con
             r[2 * k + 1] = ((aw[k] >> 16) & 0xffu) | (((bw[k] >> 16) & 0xffu) << 8) | ((aw[k] >> 24) << 16) |
                            ((bw[k] >> 24) << 24);
           }
-          o[2 * v] = make_uint4(r[0], r[1], r[2], r[3]);
-          o[2 * v + 1] = make_uint4(r[4], r[5], r[6], r[7]);
+          o(2 * v) = make_uint4(r[0], r[1], r[2], r[3]);
+          o(2 * v + 1) = make_uint4(r[4], r[5], r[6], r[7]);
         } else {
           const uint4 p0 = pl[0][v], p1 = pl[1][v], p2 = pl[2][v], p3 = pl[3][v];
           const uint32_t w0[4] = {p0.x, p0.y, p0.z, p0.w}, w1[4] = {p1.x, p1.y, p1.z, p1.w},
@@ -575,7 +612,7 @@ __global__ __launch_bounds__(256) void k_blosc_finish(const BlBlock *blocks, con
             for (int e = 0; e < 4; e++)
               r[e] = ((w0[k] >> (8 * e)) & 0xffu) | (((w1[k] >> (8 * e)) & 0xffu) << 8) |
                      (((w2[k] >> (8 * e)) & 0xffu) << 16) | (((w3[k] >> (8 * e)) & 0xffu) << 24);
-            o[4 * v + k] = make_uint4(r[0], r[1], r[2], r[3]);
+            o(4 * v + k) = make_uint4(r[0], r[1], r[2], r[3]);
           }
         }
       }
@@ -592,7 +629,7 @@ __global__ __launch_bounds__(256) void k_blosc_finish(const BlBlock *blocks, con
       } else {
         v = in(q);
       }
-      out[q] = v;
+      *dptr(q) = v;
     }
   } else if (B.mode == 2 && bsize >= ts) {  // bitunshuffle (bshuf_untrans_bit_elem)
     const uint32_t size = bsize / ts;
@@ -609,10 +646,10 @@ __global__ __launch_bounds__(256) void k_blosc_finish(const BlBlock *blocks, con
       } else {
         v = in(q);
       }
-      out[q] = v;
+      *dptr(q) = v;
     }
   } else {
-    for (uint32_t q = threadIdx.x; q < bsize; q += 256) out[q] = in(q);
+    for (uint32_t q = threadIdx.x; q < bsize; q += 256) *dptr(q) = in(q);
   }
 }
 
@@ -635,8 +672,10 @@ hipError_t launch_blosc_layout(const BlInfo *info, uint32_t n_items, uint64_t *b
 hipError_t launch_blosc_decode(ZgItem *items, uint32_t *status, uint32_t n_items, const BlInfo *info,
                                const BlDecode &D, uint8_t *dst, uint64_t slot_bytes, hipStream_t s) {
   if (!n_items) return hipSuccess;
+  const uint32_t direct = D.dout ? 1u : 0u;
+  const uint64_t want = D.sc.nelem * D.sc.es, row_bytes = direct ? D.sc.chunk_shape[D.sc.nd - 1] * D.sc.es : 1;
   hipLaunchKernelGGL(k_blosc_streams, dim3(n_items), dim3(64), 0, s, items, status, info, D.bases, D.subs,
-                     D.sub_status, D.sub_kind, D.blocks, dst, slot_bytes, D.ovf);
+                     D.sub_status, D.sub_kind, D.blocks, dst, slot_bytes, D.ovf, direct, want, row_bytes);
   if (D.n_zstd) {
     hipError_t e = launch_zstd(D.subs, D.sub_status, (uint32_t)D.n_sub, D.tmp, D.sub_slot, D.zs, s);
     if (e != hipSuccess) return e;
@@ -657,7 +696,7 @@ hipError_t launch_blosc_decode(ZgItem *items, uint32_t *status, uint32_t n_items
                        (uint32_t)D.n_sub, D.tmp, D.sub_slot);
   if (D.n_blk)
     hipLaunchKernelGGL(k_blosc_finish, dim3((uint32_t)D.n_blk), dim3(256), 0, s, D.blocks, D.subs, D.sub_status,
-                       D.sub_kind, status, dst, slot_bytes);
+                       D.sub_kind, status, dst, slot_bytes, items, D.dout, D.geom, D.sc);
   return hipGetLastError();
 }
 

@@ -25,6 +25,7 @@
 
 #include "../common.hpp"
 #include "crc.hpp"
+#include "huff.hpp"
 #include "launch.hpp"
 
 namespace zgpu {
@@ -43,10 +44,7 @@ struct GzeSmem {
   uint32_t lfreq[288], dfreq[32], cfreq[20];
   uint32_t lcode[288], dcode[32], ccode[20];  // bit-reversed code | length << 16
   uint8_t llen[288], dlen[32], clen[20];
-  uint16_t sorted[288];
-  uint16_t parent[576];
-  uint32_t weight[288];
-  uint8_t depth[576];
+  HuffScratch hs;  // huff_lengths
   uint32_t blc[16], next[16];
   uint16_t rle[320];
   uint32_t bits[GZE_BB + 4];
@@ -105,86 +103,6 @@ __device__ __forceinline__ uint32_t wave_sum(uint32_t v) {
 __device__ __forceinline__ uint32_t wave_max(uint32_t v) {
   for (int o = 32; o > 0; o >>= 1) v = max(v, (uint32_t)__shfl_xor(v, o, 64));
   return v;
-}
-
-// Code lengths of a length-limited Huffman code for freq[0..n) (n <= 288) into lens (zlib trees.c
-// build_tree + gen_bitlen semantics: fewer than two used symbols are padded to two one-bit codes, so
-// every code is complete). Wave-cooperative; freq is only read.
-__device__ void huff_lengths(GzeSmem &S, const uint32_t *freq, uint32_t n, uint32_t maxlen, uint8_t *lens) {
-  const uint32_t lane = threadIdx.x;
-  uint32_t cnt = 0;
-  for (uint32_t s = lane; s < n; s += 64) {
-    lens[s] = 0;
-    cnt += freq[s] ? 1u : 0u;
-  }
-  const uint32_t m = wave_sum(cnt);
-  WSYNC();
-  if (m < 2) {
-    if (lane == 0) {
-      uint32_t a = n, b = n;
-      for (uint32_t s = 0; s < n; s++)
-        if (freq[s]) a = s;
-      if (a == n) a = 0;
-      b = a == 0 ? 1 : 0;
-      lens[a] = 1;
-      lens[b] = 1;
-    }
-    WSYNC();
-    return;
-  }
-  // ranks by (frequency, symbol): leaves in ascending order of weight
-  for (uint32_t s = lane; s < n; s += 64) {
-    const uint32_t f = freq[s];
-    if (!f) continue;
-    uint32_t r = 0;
-    for (uint32_t t = 0; t < n; t++) {
-      const uint32_t g = freq[t];
-      r += (g && (g < f || (g == f && t < s))) ? 1u : 0u;
-    }
-    S.sorted[r] = (uint16_t)s;
-  }
-  WSYNC();
-  if (lane == 0) {
-    // two-queue Huffman merge: leaves 0..m-1 (sorted), internal nodes m..2m-2 in creation order
-    uint32_t li = 0, ii = 0, ni = 0;
-    auto wt = [&](uint32_t node) { return node < m ? freq[S.sorted[node]] : S.weight[node - m]; };
-    for (uint32_t k = 0; k + 1 < m; k++) {
-      const uint32_t a = (li < m && (ii >= ni || wt(li) <= S.weight[ii])) ? li++ : m + ii++;
-      const uint32_t b = (li < m && (ii >= ni || wt(li) <= S.weight[ii])) ? li++ : m + ii++;
-      S.weight[ni] = wt(a) + wt(b);
-      S.parent[a] = (uint16_t)(m + ni);
-      S.parent[b] = (uint16_t)(m + ni);
-      ni++;
-    }
-    const uint32_t root = 2 * m - 2;
-    S.depth[root] = 0;
-    for (int node = (int)root - 1; node >= 0; node--) {
-      const uint32_t d = S.depth[S.parent[node]] + 1u;
-      S.depth[node] = (uint8_t)(d > 255 ? 255 : d);
-    }
-    for (uint32_t b = 0; b < 16; b++) S.blc[b] = 0;
-    int overflow = 0;
-    for (uint32_t i = 0; i < m; i++) {
-      uint32_t d = S.depth[i];
-      if (d > maxlen) {
-        d = maxlen;
-        overflow++;
-      }
-      S.blc[d]++;
-    }
-    while (overflow > 0) {  // zlib gen_bitlen: move leaves down until the counts fit the limit
-      uint32_t bits = maxlen - 1;
-      while (S.blc[bits] == 0) bits--;
-      S.blc[bits]--;
-      S.blc[bits + 1] += 2;
-      S.blc[maxlen]--;
-      overflow -= 2;
-    }
-    uint32_t idx = 0;  // the least frequent leaves take the longest codes
-    for (uint32_t len = maxlen; len >= 1; len--)
-      for (uint32_t c = 0; c < S.blc[len]; c++) lens[S.sorted[idx++]] = (uint8_t)len;
-  }
-  WSYNC();
 }
 
 // canonical codes (RFC 1951 3.2.2), stored bit-reversed | length << 16
@@ -315,8 +233,8 @@ __device__ void emit_block(GzeSmem &S, BitOut &B, const uint32_t *syms, uint32_t
   const uint32_t lane = threadIdx.x;
   if (lane == 0) S.lfreq[256] += 1;  // end of block
   WSYNC();
-  huff_lengths(S, S.lfreq, 286, 15, S.llen);
-  huff_lengths(S, S.dfreq, 30, 15, S.dlen);
+  huff_lengths(S.hs, S.lfreq, 286, 15, S.llen);
+  huff_lengths(S.hs, S.dfreq, 30, 15, S.dlen);
   huff_codes(S, S.llen, 286, S.lcode);
   huff_codes(S, S.dlen, 30, S.dcode);
   uint32_t hl = 0, hd = 0;
@@ -333,7 +251,7 @@ __device__ void emit_block(GzeSmem &S, BitOut &B, const uint32_t *syms, uint32_t
     rle_lengths(S, S.dlen, hdist);
   }
   WSYNC();
-  huff_lengths(S, S.cfreq, 19, 7, S.clen);
+  huff_lengths(S.hs, S.cfreq, 19, 7, S.clen);
   huff_codes(S, S.clen, 19, S.ccode);
   uint32_t hclen = 4;
   for (uint32_t i = 0; i < 19; i++)

@@ -200,7 +200,16 @@ struct BlDecode {
   uint64_t n_sub, n_blk, n_zstd, n_lz4, n_blosclz, n_zlib, n_snappy;  // with a cached layout: capacities (n_* > 0 = launched)
   uint2 *zaux;            // zlib streams: {Adler-32 trailer, -} per stream
   unsigned long long *ovf;  // set by k_blosc_layout when a cached layout is too small (ctl counter)
+  // Direct output (dout non-null): blosc is the last stage and the scatter would copy whole chunks'
+  // rows unchanged (rows kernel, no swap / shuffle / transpose, 16-B aligned rows; checked on the
+  // host). An item whose decoded size is right and whose blocks span at most BL_DIRECT_ROWS rows is
+  // marked ZG_ITEM_DIRECT by k_blosc_streams; k_blosc_finish then writes its unshuffled blocks
+  // straight into the output rows (geom: the plan's per-item geometry, sc: its scatter parameters).
+  uint8_t *dout;
+  const uint64_t *geom;
+  ZgScatter sc;
 };
+constexpr uint32_t BL_DIRECT_ROWS = 2048;  // rows per block (LDS row table of k_blosc_finish)
 // Capacities of a blosc stream table sized by an earlier execution of the same plan: the layout of
 // this execution is computed on the device (k_blosc_layout) and checked against them, so the stage
 // needs no host read-back. BL_KINDS_*: compressors the earlier execution launched decoders for.

@@ -88,7 +88,7 @@ __device__ __forceinline__ uint4 fill_elem(const ZgScatter &P) {
 // Validate the decoded byte count of a non-fill item; returns false if the item is dead.
 __device__ __forceinline__ bool item_live(const ZgItem &it, uint32_t *status, uint32_t i,
                                           const ZgScatter &P) {
-  if (status[i]) return false;
+  if (status[i] || (it.flags & ZG_ITEM_DIRECT)) return false;
   if (!(it.flags & ZG_ITEM_FILL) && it.len != P.nelem * P.es) {
     if (threadIdx.x == 0) status[i] = ZG_DECODED_SIZE_MISMATCH;
     return false;

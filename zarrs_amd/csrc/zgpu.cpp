@@ -300,6 +300,7 @@ struct zgpu_plan {
   uint8_t *last_out = nullptr;  // output of the last enqueue (a blosc layout overflow re-runs into it)
   BlCaps bl_caps{};             // blosc stream-table capacities recorded by the first execution
   bool bl_caps_valid = false, bl_caps_seen = false;
+  bool bl_direct = false;  // the blosc stage may write whole chunks straight into the output (BlDecode::dout)
   // zstd serial fallback: skipped once an execution of this plan had no serial item (a later one that
   // has some is re-run by plan_statuses with the fallback launched)
   bool zstd_serial_off = false, zstd_serial_skipped = false;
@@ -708,6 +709,25 @@ static void plan_build(zgpu_plan &P, const zgpu_chunk_desc *descs) {
     P.scatter_mode = SCATTER_GENERIC;
   }
   P.scatter_units = P.items.empty() ? 0 : scatter_units_per_item(P.scatter_mode, S, max_sel);
+
+  // blosc as the last stage feeding the rows scatter unchanged (no swap / shuffle / transpose), every
+  // decoded item a whole chunk on 16-B aligned output rows: k_blosc_finish writes the rows itself
+  if (!P.stages.empty() && P.stages.back().kind == ST_BLOSC && P.scatter_mode == SCATTER_ROWS && !S.swap &&
+      !S.shuffle && S.nelem > 0 && S.out_stride[nd - 1] == 1 && (S.chunk_shape[nd - 1] * S.es) % 16 == 0) {
+    bool ok = true;
+    uint64_t st = 1;
+    for (int a = (int)nd - 1; a >= 0 && ok; a--) {
+      ok = S.enc_stride[a] == st && (a == (int)nd - 1 || (S.out_stride[a] * S.es) % 16 == 0);
+      st *= S.chunk_shape[a];
+    }
+    for (size_t i = 0; i < P.items.size() && ok; i++) {
+      if (P.items[i].flags & ZG_ITEM_FILL) continue;
+      const uint64_t *g = P.geom.data() + i * 3 * nd;
+      for (uint32_t d = 0; d < nd && ok; d++) ok = g[d] == 0 && g[nd + d] == S.chunk_shape[d];
+      ok = ok && (g[2 * nd + nd - 1] * S.es) % 16 == 0;
+    }
+    P.bl_direct = ok && !std::getenv("ZGPU_BLOSC_NO_DIRECT");
+  }
 }
 
 static void plan_upload(zgpu_plan &P, hipStream_t us) {
@@ -766,7 +786,7 @@ static void plan_upload(zgpu_plan &P, hipStream_t us) {
 // plan reads the headers back to size the table (the one host round trip of any stage) and records
 // the sizes as capacities; later executions lay the table out on the device against them
 // (k_blosc_layout) and stay asynchronous. A later input that outgrows them is re-run by plan_statuses.
-static void blosc_stage(zgpu_plan &P, const Stage &st, hipStream_t s) {
+static void blosc_stage(zgpu_plan &P, const Stage &st, uint8_t *out, hipStream_t s) {
   zgpu_ctx &C = *P.ctx;
   const uint32_t ni = (uint32_t)P.items.size();
   uint8_t *dst = P.d_pool[st.pool];
@@ -775,6 +795,11 @@ static void blosc_stage(zgpu_plan &P, const Stage &st, hipStream_t s) {
   uint64_t *d_bases = (uint64_t *)P.grow(P.bl_bases, ni * 16);
   BlDecode D{};
   D.bases = d_bases;
+  if (P.bl_direct && ((uintptr_t)out & 15) == 0) {
+    D.dout = out;
+    D.geom = P.d_geom;
+    D.sc = P.scatter;
+  }
   D.ovf = P.d_counter + CTR_BLOSC_OVF;
   BlCaps &caps = P.bl_caps;
   const bool cached = P.bl_caps_valid;
@@ -893,7 +918,7 @@ static void plan_enqueue(zgpu_plan &P, uint8_t *out, hipStream_t s) {
         HIPCHK(launch_zstd(P.d_items, P.d_status, ni, P.d_pool[st.pool], P.slot_bytes, P.zs, s));
         break;
       case ST_BLOSC:
-        blosc_stage(P, st, s);
+        blosc_stage(P, st, out, s);
         break;
       case ST_UNSHUFFLE:
         HIPCHK(launch_unshuffle(P.d_items, P.d_status, ni, P.d_pool[st.pool], P.slot_bytes, st.elementsize, s));
