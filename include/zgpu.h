@@ -111,7 +111,8 @@ const char *zgpu_version(void);
 /*
  * Parse and bind a codec chain.
  *  codecs_json : the Zarr V3 "codecs" JSON array (nested sharding_indexed configs included).
- *                Supported: transpose, bytes, sharding_indexed (nested up to two levels),
+ *                Supported: transpose, bytes, sharding_indexed (nested to any depth, with codecs
+ *                around the inner shardings and bytes->bytes codecs after any of them),
  *                crc32c (+numcodecs.crc32c), gzip, zstd, numcodecs.shuffle, blosc (blosclz, lz4,
  *                lz4hc, zlib, snappy, zstd; shuffle / bitshuffle). Others -> ZGPU_UNSUPPORTED.
  *  data_type   : Zarr V3 data type name ("float32", "uint16", ...); fixed-size types only.
@@ -145,6 +146,13 @@ typedef struct {
  * status[n] (optional) receives each chunk's status. Returns the first non-zero chunk status
  * (zarrs' try_for_each semantics) or a call-level error. hip_stream NULL = context stream.
  * The call is synchronous with respect to the host (statuses are final on return).
+ * Any chain zgpu_chain_create accepts, and descriptors of different chunk shapes in one batch (e.g.
+ * a rectilinear grid), decode here: one fused launch sequence per chunk shape when the chain is
+ * "fused" (unsharded; or sharding_indexed, optionally behind transposes, with no bytes->bytes codec
+ * after it and at most one plain nested sharding_indexed inside), else composed from fused ones:
+ * whole-shard bytes->bytes codecs are decoded into device buffers first, and deeper or wrapped
+ * nested shards are resolved through their outer index (read back) into descriptors of the inner
+ * chain. A transpose before a sharding_indexed of the second kind -> ZGPU_UNSUPPORTED.
  */
 int zgpu_decode_batch(zgpu_chain *chain, uint32_t ndim, const zgpu_chunk_desc *descs,
                       uint64_t n, void *out, const uint64_t *out_shape, uint32_t flags,
@@ -152,7 +160,8 @@ int zgpu_decode_batch(zgpu_chain *chain, uint32_t ndim, const zgpu_chunk_desc *d
 
 /*
  * Prepared form of zgpu_decode_batch for device-resident inputs that are decoded repeatedly
- * (benchmarks, hipGraph capture): the descriptor table is planned and uploaded once.
+ * (benchmarks, hipGraph capture): the descriptor table is planned and uploaded once. Plans take
+ * fused chains and one chunk shape only (see zgpu_decode_batch); others -> ZGPU_UNSUPPORTED.
  * zgpu_plan_execute enqueues the decode on the stream and, if status != NULL, waits and returns
  * per-chunk statuses; with status == NULL it returns immediately after enqueue.
  * An asynchronous execute's output is valid only once zgpu_plan_status has returned for it: a blosc

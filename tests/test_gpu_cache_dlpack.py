@@ -105,13 +105,17 @@ def test_cache_does_not_keep_failed_chunks(ctx):
 
 
 def test_cache_call_level_error_is_not_cached(ctx):
-    """A chain the planner rejects before any chunk status exists (bytes->bytes codecs after
-    sharding_indexed: UNSUPPORTED) fails on every read through the cache; no slot is kept."""
+    """A chain the planner rejects before any chunk status exists (a transpose before a sharding
+    whose subchunks are shards with a checksum around them: UNSUPPORTED) fails on every read through
+    the cache; no slot is kept."""
     from zarrs_amd import Array, ArrayCached, ChunkCacheDecodedLruSizeLimit, MemoryStore, ZgpuError
-    codecs = [{"name": "sharding_indexed", "configuration": {
-        "chunk_shape": [4], "codecs": [{"name": "bytes", "configuration": {"endian": "little"}}],
-        "index_codecs": [{"name": "bytes", "configuration": {"endian": "little"}}, {"name": "crc32c"}]}},
-        {"name": "crc32c"}]
+    idx = [{"name": "bytes", "configuration": {"endian": "little"}}, {"name": "crc32c"}]
+    mid = {"name": "sharding_indexed", "configuration": {
+        "chunk_shape": [2], "codecs": [{"name": "bytes", "configuration": {"endian": "little"}}],
+        "index_codecs": idx}}
+    codecs = [{"name": "transpose", "configuration": {"order": [0]}},
+              {"name": "sharding_indexed", "configuration": {
+                  "chunk_shape": [4], "codecs": [mid, {"name": "crc32c"}], "index_codecs": idx}}]
     meta = {"shape": [16], "data_type": "uint16", "fill_value": 0, "codecs": codecs,
             "chunk_grid": {"name": "regular", "configuration": {"chunk_shape": [8]}}}
     store = MemoryStore({"c/0": bytes(64), "c/1": bytes(64)})

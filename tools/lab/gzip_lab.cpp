@@ -89,7 +89,7 @@ int main(int argc, char **argv) {
     CK(hipMemcpyToSymbol(HIP_SYMBOL(zgpu::g_prof), z, sizeof(z)));
 #endif
     CK(hipEventRecord(e0));
-    CK(zgpu::launch_gzip(d_items, d_status, n, d_out, slot, 0));
+    CK(zgpu::launch_gzip(d_items, d_status, n, d_out, slot, nullptr, 0));
     CK(hipEventRecord(e1));
     CK(hipEventSynchronize(e1));
     float ms; CK(hipEventElapsedTime(&ms, e0, e1));

@@ -33,6 +33,8 @@
 //    the batch records) and the kernel is held at 96 VGPRs: 5 streams per SIMD.
 #include <hip/hip_runtime.h>
 
+#include <cstdlib>
+
 #include "../common.hpp"
 #include "crc.hpp"
 #include "launch.hpp"
@@ -553,11 +555,12 @@ __device__ __forceinline__ void flush(const Smem &S, uint8_t *out, uint64_t cap,
 // success (the Adler-32 check follows in k_adler32_check).
 template <bool ZLIB>
 __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(ZG_INFLATE_WPE, 8))) void k_gzip(
-    ZgItem *items, uint32_t *status, const uint32_t *kind, uint8_t *dst, uint64_t slot_bytes, uint2 *aux) {
+    ZgItem *items, uint32_t *status, const uint32_t *kind, uint8_t *dst, uint64_t slot_bytes, uint2 *aux,
+    const uint32_t *order) {
   __shared__ Smem S;
   PROF_DECL;
   PROF_T(t_all);
-  const uint32_t item = blockIdx.x;
+  const uint32_t item = order ? order[blockIdx.x] : blockIdx.x;
   if (ZLIB ? (kind[item] != BL_KIND_ZLIB || status[item] != BL_SKIP) : status[item] != 0) return;
   const ZgItem it = items[item];
   if (it.flags & ZG_ITEM_FILL) return;
@@ -1100,17 +1103,62 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(ZG_INFLATE_W
   PROF_FLUSH;
 }
 
+// LPT order of a one-wave-per-stream launch: the items by descending encoded length, so the longest
+// streams are dispatched first and the launch's last round is made of the shortest ones (C3: 15,625
+// streams on 5,120 resident waves). One workgroup, a counting sort on 1024 length buckets; failed
+// and fill items go last.
+__global__ __launch_bounds__(1024) void k_order_by_len(const ZgItem *items, const uint32_t *status, uint32_t n,
+                                                       uint32_t *order) {
+  __shared__ uint32_t cnt[1024];
+  __shared__ uint32_t s_max;
+  const uint32_t t = threadIdx.x;
+  cnt[t] = 0;
+  if (t == 0) s_max = 0;
+  __syncthreads();
+  auto len_of = [&](uint32_t i) -> uint32_t {
+    const ZgItem it = items[i];
+    if (status[i] || (it.flags & ZG_ITEM_FILL)) return 0;
+    return it.len > 0xFFFFFFFFull ? 0xFFFFFFFFu : (uint32_t)it.len;
+  };
+  uint32_t m = 0;
+  for (uint32_t i = t; i < n; i += 1024) m = max(m, len_of(i));
+  atomicMax(&s_max, m);
+  __syncthreads();
+  uint32_t shift = 0;
+  while ((s_max >> shift) >= 1024) shift++;
+  for (uint32_t i = t; i < n; i += 1024) atomicAdd(&cnt[1023 - (len_of(i) >> shift)], 1u);
+  __syncthreads();
+  const uint32_t v = cnt[t];
+  for (uint32_t off = 1; off < 1024; off <<= 1) {  // inclusive scan (Hillis-Steele)
+    const uint32_t x = t >= off ? cnt[t - off] : 0;
+    __syncthreads();
+    cnt[t] += x;
+    __syncthreads();
+  }
+  cnt[t] -= v;  // exclusive: the bucket's first slot
+  __syncthreads();
+  for (uint32_t i = t; i < n; i += 1024) order[atomicAdd(&cnt[1023 - (len_of(i) >> shift)], 1u)] = i;
+}
+
 hipError_t launch_gzip(ZgItem *items, uint32_t *status, uint32_t n_items, uint8_t *dst, uint64_t slot_bytes,
-                       hipStream_t s) {
+                       uint32_t *order, hipStream_t s) {
   if (!n_items) return hipSuccess;
-  hipLaunchKernelGGL(k_gzip<false>, dim3(n_items), dim3(64), 0, s, items, status, nullptr, dst, slot_bytes, nullptr);
+  static const bool lpt = [] {
+    const char *e = std::getenv("ZGPU_GZIP_LPT");
+    return !e || std::atoi(e) != 0;
+  }();
+  if (!lpt || n_items < 2) order = nullptr;
+  if (order) hipLaunchKernelGGL(k_order_by_len, dim3(1), dim3(1024), 0, s, items, status, n_items, order);
+  hipLaunchKernelGGL(k_gzip<false>, dim3(n_items), dim3(64), 0, s, items, status, nullptr, dst, slot_bytes, nullptr,
+                     order);
   return hipGetLastError();
 }
 
 hipError_t launch_zlib_streams(ZgItem *subs, uint32_t *sub_status, const uint32_t *sub_kind, uint32_t n_sub,
                                uint8_t *dst, uint64_t slot, uint2 *aux, hipStream_t s) {
   if (!n_sub) return hipSuccess;
-  hipLaunchKernelGGL(k_gzip<true>, dim3(n_sub), dim3(64), 0, s, subs, sub_status, sub_kind, dst, slot, aux);
+  hipLaunchKernelGGL(k_gzip<true>, dim3(n_sub), dim3(64), 0, s, subs, sub_status, sub_kind, dst, slot, aux,
+                     nullptr);
   return hipGetLastError();
 }
 

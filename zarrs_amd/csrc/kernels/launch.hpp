@@ -72,8 +72,9 @@ hipError_t launch_item_resolve(ZgItem *items, uint32_t *status, uint32_t n_items
 
 // gzip (RFC 1952) member decode: header parse, DEFLATE inflate into dst slots, trailer CRC-32 (IEEE)
 // + ISIZE check of the inflated bytes. On return items[i] points at its slot.
+// order: n_items u32 of scratch for the LPT dispatch order (descending encoded length), or NULL
 hipError_t launch_gzip(ZgItem *items, uint32_t *status, uint32_t n_items, uint8_t *dst, uint64_t slot_bytes,
-                       hipStream_t s);
+                       uint32_t *order, hipStream_t s);
 // zstd (RFC 8878) frame decode into dst slots: block-parallel (scan, per-block entropy decode,
 // per-item execution) with the serial one-wave-per-item decoder as the fallback.
 struct ZstdScratch {
@@ -104,6 +105,10 @@ hipError_t launch_zstd(ZgItem *items, uint32_t *status, uint32_t n_items, uint8_
 // standalone unshuffle (when shuffle is not directly above the bytes codec)
 hipError_t launch_unshuffle(ZgItem *items, uint32_t *status, uint32_t n_items, uint8_t *dst, uint64_t slot_bytes,
                             uint32_t elementsize, hipStream_t s);
+// decoded-size hint per item of a whole-shard compressor stage (kernels/probe.hip); 0 = unknown
+enum : uint32_t { SIZE_HINT_GZIP = 0, SIZE_HINT_ZSTD = 1, SIZE_HINT_BLOSC = 2 };
+hipError_t launch_size_hint(const ZgItem *items, const uint32_t *status, uint32_t n, uint32_t kind, uint64_t *hint,
+                            hipStream_t s);
 
 // encode (write path): array -> encoded chunk layouts (transposes, endianness, innermost shuffle)
 struct ZgEncode {

@@ -305,6 +305,8 @@ struct zgpu_plan {
   // has some is re-run by plan_statuses with the fallback launched)
   bool zstd_serial_off = false, zstd_serial_skipped = false;
   uint32_t *d_zser = nullptr;
+  uint32_t *d_order = nullptr;  // gzip stage: LPT dispatch order of the items
+  bool no_scatter = false;  // a whole-shard predecode plan: its bytes->bytes stages only (decode_general)
 
   ~zgpu_plan() {
     if (!ctx) return;
@@ -316,7 +318,7 @@ struct zgpu_plan {
     void *bufs[] = {d_items, d_items_init, d_geom, d_shards, d_index, d_shard_status, d_mids, d_mids_init,
                     d_mid_status, d_shard_status2, d_mid_shards, d_index2,
                     d_pool[0], d_pool[1], zs.blks, zs.nblk, zs.mode, zs.lit, zs.seq, d_ctl,
-                    d_enc_stage, d_zser};
+                    d_enc_stage, d_zser, d_order};
     for (void *b : bufs) ctx->dev_free(b);
     if (zside) {
       (void)hipStreamSynchronize(zside);
@@ -416,6 +418,26 @@ static void build_leaf_stages(zgpu_plan &P, const Chain &leaf, uint64_t nelem) {
   }
   P.slot_bytes = (max_slot + 255) & ~(uint64_t)255;
   P.scatter.shuffle = fused_shuffle;
+}
+
+// ShardingIndex decode spec (sharding.rs:136-235, sharding_codec.rs:1262-1298): the index chain
+// must be bytes (+ crc32c), the only index_codecs zarrs' sharding writes and the GPU decodes.
+static ZgIndexSpec index_spec(const Codec &sharding, uint64_t n_inner, bool validate) {
+  const Chain &xc = *sharding.index;
+  if (xc.a2b.kind != CodecKind::Bytes || !xc.a2a.empty())
+    throw ChainError{ZGPU_UNSUPPORTED, "index_codecs must be bytes (+crc32c)"};
+  for (const Codec &k : xc.b2b)
+    if (k.kind != CodecKind::Crc32c) throw ChainError{ZGPU_UNSUPPORTED, "index_codecs must be bytes (+crc32c)"};
+  if (xc.b2b.size() > 4) throw ChainError{ZGPU_UNSUPPORTED, "too many index crc32c codecs"};
+  ZgIndexSpec S{};
+  S.n_inner = n_inner;
+  S.index_bytes = (uint64_t)chain_fixed_encoded_size(xc, n_inner * 2);
+  S.at_start = sharding.at_start;
+  S.big_endian = xc.a2b.big_endian;
+  S.n_crc = (uint32_t)xc.b2b.size();
+  for (size_t k = 0; k < xc.b2b.size(); k++) S.crc_at_start[k] = xc.b2b[k].at_start;
+  S.verify = validate;
+  return S;
 }
 
 static void plan_build(zgpu_plan &P, const zgpu_chunk_desc *descs) {
@@ -635,35 +657,11 @@ static void plan_build(zgpu_plan &P, const zgpu_chunk_desc *descs) {
   }
 
   if (shard_chain) {
-    const Chain &xc = *top.a2b.index;
-    if (xc.a2b.kind != CodecKind::Bytes || !xc.a2a.empty())
-      throw ChainError{ZGPU_UNSUPPORTED, "index_codecs must be bytes (+crc32c)"};
-    for (const Codec &k : xc.b2b)
-      if (k.kind != CodecKind::Crc32c) throw ChainError{ZGPU_UNSUPPORTED, "index_codecs must be bytes (+crc32c)"};
-    if (xc.b2b.size() > 4) throw ChainError{ZGPU_UNSUPPORTED, "too many index crc32c codecs"};
-    const int64_t isz = chain_fixed_encoded_size(xc, P.ispec.n_inner * 2);
-    P.ispec.index_bytes = (uint64_t)isz;
-    P.ispec.at_start = top.a2b.at_start;
-    P.ispec.big_endian = xc.a2b.big_endian;
-    P.ispec.n_crc = (uint32_t)xc.b2b.size();
-    for (size_t k = 0; k < xc.b2b.size(); k++) P.ispec.crc_at_start[k] = xc.b2b[k].at_start;
-    P.ispec.verify = P.validate;
+    P.ispec = index_spec(top.a2b, P.ispec.n_inner, P.validate);
     for (const ZgShard &sh : P.shards)
       if (sh.ptr) P.alg_bytes_static += P.ispec.index_bytes;
     if (mid) {
-      const Chain &xc2 = *mid->a2b.index;
-      if (xc2.a2b.kind != CodecKind::Bytes || !xc2.a2a.empty())
-        throw ChainError{ZGPU_UNSUPPORTED, "index_codecs must be bytes (+crc32c)"};
-      for (const Codec &k : xc2.b2b)
-        if (k.kind != CodecKind::Crc32c) throw ChainError{ZGPU_UNSUPPORTED, "index_codecs must be bytes (+crc32c)"};
-      if (xc2.b2b.size() > 4) throw ChainError{ZGPU_UNSUPPORTED, "too many index crc32c codecs"};
-      P.ispec2.n_inner = n_inner2;
-      P.ispec2.index_bytes = (uint64_t)chain_fixed_encoded_size(xc2, n_inner2 * 2);
-      P.ispec2.at_start = mid->a2b.at_start;
-      P.ispec2.big_endian = xc2.a2b.big_endian;
-      P.ispec2.n_crc = (uint32_t)xc2.b2b.size();
-      for (size_t k = 0; k < xc2.b2b.size(); k++) P.ispec2.crc_at_start[k] = xc2.b2b[k].at_start;
-      P.ispec2.verify = P.validate;
+      P.ispec2 = index_spec(mid->a2b, n_inner2, P.validate);
       for (const ZgItem &m : P.mids)
         if (!(m.flags & ZG_ITEM_FILL)) P.alg_bytes_static += P.ispec2.index_bytes;
     }
@@ -741,6 +739,7 @@ static void plan_upload(zgpu_plan &P, hipStream_t us) {
     HIPCHK(hipMemcpyAsync(P.d_geom, P.geom.data(), P.geom.size() * 8, hipMemcpyHostToDevice, us));
     for (int k = 0; k < P.n_pools; k++) P.d_pool[k] = (uint8_t *)C.dev_alloc(ni * P.slot_bytes);
     for (const Stage &s : P.stages) {
+      if (s.kind == ST_GZIP && !P.d_order) P.d_order = (uint32_t *)C.dev_alloc(ni * 4);
       if (s.kind == ST_ZSTD && !P.zs.blks) {
         uint64_t blk_bytes;
         zstd_scratch_layout(P.slot_bytes, P.zs.blk_cap, blk_bytes, P.zs.lit_stride, P.zs.seq_cap);
@@ -911,7 +910,7 @@ static void plan_enqueue(zgpu_plan &P, uint8_t *out, hipStream_t s) {
         HIPCHK(launch_crc32c_strip(P.d_items, P.d_status, ni, st.at_start, P.validate ? 1 : 0, s));
         break;
       case ST_GZIP:
-        HIPCHK(launch_gzip(P.d_items, P.d_status, ni, P.d_pool[st.pool], P.slot_bytes, s));
+        HIPCHK(launch_gzip(P.d_items, P.d_status, ni, P.d_pool[st.pool], P.slot_bytes, P.d_order, s));
         break;
       case ST_ZSTD:
         P.zstd_fork(P.zs, s);
@@ -925,7 +924,8 @@ static void plan_enqueue(zgpu_plan &P, uint8_t *out, hipStream_t s) {
         break;
     }
   }
-  HIPCHK(launch_scatter(items, P.d_geom, P.d_status, P.scatter, out, ni, P.scatter_mode, P.scatter_units, s));
+  if (!P.no_scatter)
+    HIPCHK(launch_scatter(items, P.d_geom, P.d_status, P.scatter, out, ni, P.scatter_mode, P.scatter_units, s));
 }
 
 // InvalidBytesLengthError{len, expected_len} of descriptor d's first mismatching leaf item: the item's
@@ -1005,18 +1005,23 @@ static int plan_statuses(zgpu_plan &P, int32_t *status, hipStream_t s) {
   return first;
 }
 
-static zgpu_plan *plan_new(zgpu_chain *ch, uint32_t nd, const zgpu_chunk_desc *descs, uint64_t n,
-                           const uint64_t *out_shape, uint32_t flags) {
+static zgpu_plan *plan_new(zgpu_ctx *ctx, const std::shared_ptr<Chain> &chain, bool validate, uint32_t nd,
+                           const zgpu_chunk_desc *descs, uint64_t n, const uint64_t *out_shape, uint32_t flags) {
   auto P = std::make_unique<zgpu_plan>();
-  P->ctx = ch->ctx;
-  P->chain = ch->chain;
-  P->validate = ch->validate && !(flags & ZGPU_NO_VALIDATE);
+  P->ctx = ctx;
+  P->chain = chain;
+  P->validate = validate && !(flags & ZGPU_NO_VALIDATE);
   P->nd = nd;
   P->n_desc = n;
   P->flags = flags;
   P->out_shape.assign(out_shape, out_shape + nd);
   plan_build(*P, descs);
   return P.release();
+}
+
+static zgpu_plan *plan_new(zgpu_chain *ch, uint32_t nd, const zgpu_chunk_desc *descs, uint64_t n,
+                           const uint64_t *out_shape, uint32_t flags) {
+  return plan_new(ch->ctx, ch->chain, ch->validate, nd, descs, n, out_shape, flags);
 }
 
 // hip_stream NULL: the context's stream, ordered after all work already queued on the legacy
@@ -1035,6 +1040,368 @@ static hipStream_t pick_stream(Lane *L, void *s) {
 static Lane *plan_lane(zgpu_plan &P) {
   if (!P.own.stream) HIPCHK(hipStreamCreateWithFlags(&P.own.stream, hipStreamNonBlocking));
   return &P.own;
+}
+
+// ------------------------------------------------------------------------------------------------
+// General decode: the chains and batches one fused plan does not take, composed from fused plans
+// (CodecChain composes any chain, codec_chain.rs:192-229, and zarrs decodes every chunk through its
+// own chain and shape):
+//  * descriptors of more than one chunk (shard) shape: one plan per shape, on one stream;
+//  * bytes->bytes codecs after sharding_indexed (a checksum or compressor over the whole shard): the
+//    shards go through those codecs first, stage by stage (the leaf-chunk kernels; slots sized from
+//    the streams' own size fields), then decode as plain shards;
+//  * sharding nested more than two deep, or codecs around a nested sharding_indexed: the outer shard
+//    indexes are decoded on the device and read back, and the intersecting middle shards become the
+//    descriptors of the inner chain (recursively, sharding.rs:107-126).
+// Synchronous (per-stage read-backs); per-descriptor statuses, first failing item of a descriptor.
+// ------------------------------------------------------------------------------------------------
+static bool fused_plannable(const Chain &top) {
+  if (top.a2b.kind != CodecKind::Sharding) return true;
+  if (!top.b2b.empty()) return false;
+  const Chain &mid = *top.a2b.inner;
+  if (mid.a2b.kind != CodecKind::Sharding) return true;
+  return mid.a2a.empty() && mid.b2b.empty() && mid.a2b.inner->a2b.kind != CodecKind::Sharding;
+}
+
+static bool same_shape(const zgpu_chunk_desc &a, const zgpu_chunk_desc &b, uint32_t nd) {
+  for (uint32_t d = 0; d < nd; d++)
+    if (a.chunk_shape[d] != b.chunk_shape[d]) return false;
+  return true;
+}
+
+static bool uniform_shapes(const zgpu_chunk_desc *descs, uint64_t n, uint32_t nd) {
+  for (uint64_t i = 1; i < n; i++)
+    if (!same_shape(descs[0], descs[i], nd)) return false;
+  return true;
+}
+
+static bool desc_geometry_ok(const zgpu_chunk_desc &D, uint32_t nd, const uint64_t *out_shape) {
+  for (uint32_t d = 0; d < nd; d++)
+    if (D.sel_start[d] + D.sel_shape[d] > D.chunk_shape[d] || D.out_start[d] + D.sel_shape[d] > out_shape[d])
+      return false;
+  return true;
+}
+
+static uint64_t sel_volume(const zgpu_chunk_desc &D, uint32_t nd) {
+  uint64_t v = 1;
+  for (uint32_t d = 0; d < nd; d++) v *= D.sel_shape[d];
+  return v;
+}
+
+static bool sel_full(const zgpu_chunk_desc &D, uint32_t nd) {
+  for (uint32_t d = 0; d < nd; d++)
+    if (D.sel_start[d] != 0 || D.sel_shape[d] != D.chunk_shape[d]) return false;
+  return true;
+}
+
+struct GeneralCall {
+  zgpu_ctx *C;
+  bool validate;
+  uint32_t nd;
+  uint8_t *out;  // device output array
+  const uint64_t *out_shape;
+  uint32_t flags;
+  hipStream_t s;
+  std::vector<std::unique_ptr<zgpu_plan>> keep;  // whole-shard decode slots, alive until the call ends
+};
+
+static void decode_general(GeneralCall &G, const std::shared_ptr<Chain> &chain, const zgpu_chunk_desc *descs,
+                           uint64_t n, int32_t *status);
+
+// Decode `sub` (sub-descriptor k belongs to caller descriptor owner[k]) and merge: a caller
+// descriptor keeps its first error.
+static void run_sub(GeneralCall &G, const std::shared_ptr<Chain> &chain, const std::vector<zgpu_chunk_desc> &sub,
+                    const std::vector<uint64_t> &owner, int32_t *status) {
+  if (sub.empty()) return;
+  std::vector<int32_t> st(sub.size(), 0);
+  const bool had_detail = g_size_detail.valid;
+  decode_general(G, chain, sub.data(), sub.size(), st.data());
+  if (!had_detail && g_size_detail.valid) g_size_detail.desc = owner[g_size_detail.desc];
+  for (size_t k = 0; k < sub.size(); k++)
+    if (st[k] && !status[owner[k]]) status[owner[k]] = st[k];
+}
+
+// One bytes->bytes codec applied to whole shards (items[i] = shard i's current bytes; ist[i] its
+// status): decoded by a stages-only plan whose slots hold the decoded shards. Compressors size the
+// slots from the streams (kernels/probe.hip); a gzip member longer than its ISIZE hint is re-run
+// with larger slots up to DEFLATE's 1032:1 bound.
+static void shard_stage(GeneralCall &G, const Codec &k, std::vector<ZgItem> &items, std::vector<int32_t> &ist) {
+  std::vector<uint32_t> todo;
+  for (uint32_t i = 0; i < items.size(); i++)
+    if (!ist[i]) todo.push_back(i);
+  if (todo.empty()) return;
+  Stage st{};
+  uint32_t hint_kind = UINT32_MAX;
+  switch (k.kind) {
+    case CodecKind::Crc32c: st.kind = ST_CRC32C; st.at_start = k.at_start; break;
+    case CodecKind::Gzip: st.kind = ST_GZIP; hint_kind = SIZE_HINT_GZIP; break;
+    case CodecKind::Zstd: st.kind = ST_ZSTD; hint_kind = SIZE_HINT_ZSTD; break;
+    case CodecKind::Blosc: st.kind = ST_BLOSC; hint_kind = SIZE_HINT_BLOSC; break;
+    case CodecKind::Shuffle: st.kind = ST_UNSHUFFLE; st.elementsize = k.elementsize; break;
+    default: throw ChainError{ZGPU_UNSUPPORTED, "codec '" + k.name + "' after sharding_indexed"};
+  }
+  uint64_t cap = 0;
+  if (st.kind == ST_UNSHUFFLE) {
+    for (uint32_t t : todo) cap = std::max(cap, items[t].len);
+  } else if (hint_kind != UINT32_MAX) {
+    const uint32_t nt = (uint32_t)todo.size();
+    std::vector<ZgItem> hi(nt);
+    for (uint32_t j = 0; j < nt; j++) hi[j] = items[todo[j]];
+    ZgItem *d_it = (ZgItem *)G.C->dev_alloc(nt * sizeof(ZgItem));
+    uint8_t *d_buf = (uint8_t *)G.C->dev_alloc(nt * 12);
+    std::vector<uint64_t> h(nt, 0);
+    hipError_t e = hipMemcpyAsync(d_it, hi.data(), nt * sizeof(ZgItem), hipMemcpyHostToDevice, G.s);
+    if (e == hipSuccess) e = hipMemsetAsync(d_buf + nt * 8, 0, nt * 4, G.s);
+    if (e == hipSuccess)
+      e = launch_size_hint(d_it, (const uint32_t *)(d_buf + nt * 8), nt, hint_kind, (uint64_t *)d_buf, G.s);
+    if (e == hipSuccess) e = hipMemcpyAsync(h.data(), d_buf, nt * 8, hipMemcpyDeviceToHost, G.s);
+    if (e == hipSuccess) e = hipStreamSynchronize(G.s);
+    G.C->dev_free(d_it);
+    G.C->dev_free(d_buf);
+    if (e != hipSuccess) throw HipFail{e, "whole-shard size hints"};
+    for (uint64_t v : h) cap = std::max(cap, v);
+  }
+  cap = std::max<uint64_t>(cap, 256);
+  for (;;) {
+    auto P = std::make_unique<zgpu_plan>();
+    P->ctx = G.C;
+    P->validate = G.validate;
+    P->nd = 1;
+    P->n_desc = todo.size();
+    P->flags = G.flags;
+    P->out_shape = {1};
+    P->item_desc_status.assign(todo.size(), 0);
+    for (size_t j = 0; j < todo.size(); j++) {
+      ZgItem it = items[todo[j]];
+      it.desc = (uint32_t)j;
+      P->items.push_back(it);
+    }
+    st.pool = 0;
+    P->stages = {st};
+    P->n_pools = st.kind == ST_CRC32C ? 0 : 1;
+    P->slot_bytes = (cap + 255) & ~(uint64_t)255;
+    P->no_scatter = true;
+    plan_upload(*P, G.s);
+    plan_enqueue(*P, nullptr, G.s);
+    std::vector<int32_t> s(todo.size(), 0);
+    const SizeDetail keep_detail = g_size_detail;
+    plan_statuses(*P, s.data(), G.s);
+    g_size_detail = keep_detail;  // a shard has no expected decoded size
+    std::vector<ZgItem> res(todo.size());
+    HIPCHK(hipMemcpyAsync(res.data(), P->d_items, todo.size() * sizeof(ZgItem), hipMemcpyDeviceToHost, G.s));
+    HIPCHK(hipStreamSynchronize(G.s));
+    std::vector<uint32_t> again;
+    uint64_t bound = 0;
+    for (size_t j = 0; j < todo.size(); j++) {
+      const uint32_t t = todo[j];
+      const uint64_t deflate_bound = items[t].len * 1032 + 1024;
+      if (s[j] == ZGPU_DECODED_SIZE_MISMATCH && st.kind == ST_GZIP && cap < deflate_bound) {
+        again.push_back(t);
+        bound = std::max(bound, deflate_bound);
+        continue;
+      }
+      ist[t] = s[j];
+      if (!s[j]) {
+        items[t].src = res[j].src;
+        items[t].len = res[j].len;
+      }
+    }
+    G.keep.push_back(std::move(P));
+    if (again.empty()) return;
+    cap = std::min(cap * 8, bound);
+    todo.swap(again);
+  }
+}
+
+// bytes->bytes codecs after sharding_indexed: decode every selected shard through them (reverse
+// order, codec_chain.rs:612-617), then read the decoded shards through the chain without them.
+static void predecode_shards(GeneralCall &G, const std::shared_ptr<Chain> &chain, const zgpu_chunk_desc *descs,
+                             uint64_t n, int32_t *status) {
+  const Chain &top = *chain;
+  const uint32_t nd = G.nd;
+  std::vector<ZgItem> items;
+  std::vector<uint64_t> owner;
+  for (uint64_t i = 0; i < n; i++) {
+    const zgpu_chunk_desc &D = descs[i];
+    if (!desc_geometry_ok(D, nd, G.out_shape)) {
+      status[i] = ZGPU_INVALID_ARGUMENT;
+      continue;
+    }
+    if (!D.enc || sel_volume(D, nd) == 0) continue;
+    ZgItem it{};
+    it.src = (uint64_t)D.enc;
+    it.len = D.enc_len;
+    it.desc = (uint32_t)items.size();
+    it.flags = sel_full(D, nd) ? 0u : ZG_ITEM_PARTIAL;  // a partial read strips crc32c unverified
+    items.push_back(it);
+    owner.push_back(i);
+  }
+  std::vector<int32_t> ist(items.size(), 0);
+  for (int k = (int)top.b2b.size() - 1; k >= 0; k--) shard_stage(G, top.b2b[k], items, ist);
+  auto bare = std::make_shared<Chain>(top);
+  bare->b2b.clear();
+  std::vector<zgpu_chunk_desc> sub;
+  std::vector<uint64_t> sub_owner;
+  size_t j = 0;
+  for (uint64_t i = 0; i < n; i++) {
+    if (status[i]) continue;
+    zgpu_chunk_desc D = descs[i];
+    if (j < owner.size() && owner[j] == i) {
+      const size_t t = j++;
+      if (ist[t]) {
+        status[i] = ist[t];
+        continue;
+      }
+      D.enc = (const void *)items[t].src;
+      D.enc_len = items[t].len;
+    }
+    sub.push_back(D);
+    sub_owner.push_back(i);
+  }
+  run_sub(G, bare, sub, sub_owner, status);
+}
+
+// A sharded chain whose subchunks are shards the fused plan cannot take (codecs around them, or
+// sharding below them again): the outer indexes decode on the device (k_shard_index, checksums
+// verified) and come back to the host, and every intersecting middle shard becomes a descriptor of
+// the inner chain (sharding_codec.rs:617-707 per subchunk; an empty one decodes to the fill value).
+static void nested_host(GeneralCall &G, const std::shared_ptr<Chain> &chain, const zgpu_chunk_desc *descs,
+                        uint64_t n, int32_t *status) {
+  const Chain &top = *chain;
+  const uint32_t nd = G.nd;
+  if (!top.a2a.empty())
+    throw ChainError{ZGPU_UNSUPPORTED, "transpose codecs before a sharding_indexed whose subchunks are shards "
+                                       "with codecs around them or nested sharding below them"};
+  const std::vector<uint64_t> &ms = top.a2b.inner_shape;
+  if (ms.size() != nd) throw ChainError{ZGPU_INVALID_ARGUMENT, "sharding chunk_shape rank"};
+  uint64_t cps[ZG_MAXD], n_inner = 0;
+  std::vector<ZgShard> shards;
+  std::vector<uint64_t> shard_of(n, UINT64_MAX);
+  for (uint64_t i = 0; i < n; i++) {
+    const zgpu_chunk_desc &D = descs[i];
+    bool ok = desc_geometry_ok(D, nd, G.out_shape);
+    uint64_t ni = 1;
+    for (uint32_t d = 0; d < nd && ok; d++) {
+      if (!ms[d] || D.chunk_shape[d] % ms[d]) ok = false;  // calculate_chunks_per_shard (sharding.rs:136-154)
+      else {
+        cps[d] = D.chunk_shape[d] / ms[d];
+        ni *= cps[d];
+      }
+    }
+    if (!ok) {
+      status[i] = ZGPU_INVALID_ARGUMENT;
+      continue;
+    }
+    n_inner = ni;  // one shard shape per call (decode_general groups by shape)
+    if (D.enc && sel_volume(D, nd)) {
+      shard_of[i] = shards.size();
+      shards.push_back(ZgShard{(uint64_t)D.enc, D.enc_len});
+    }
+  }
+  std::vector<uint64_t> index;
+  std::vector<uint32_t> sst;
+  if (!shards.empty()) {
+    const ZgIndexSpec spec = index_spec(top.a2b, n_inner, G.validate);
+    const size_t ns = shards.size();
+    index.resize(ns * n_inner * 2);
+    sst.resize(ns);
+    ZgShard *d_sh = (ZgShard *)G.C->dev_alloc(ns * sizeof(ZgShard));
+    uint64_t *d_idx = (uint64_t *)G.C->dev_alloc(index.size() * 8);
+    uint32_t *d_st = (uint32_t *)G.C->dev_alloc(ns * 4);
+    hipError_t e = hipMemcpyAsync(d_sh, shards.data(), ns * sizeof(ZgShard), hipMemcpyHostToDevice, G.s);
+    if (e == hipSuccess) e = launch_shard_index(d_sh, (uint32_t)ns, spec, d_idx, d_st, 0, G.s);
+    if (e == hipSuccess) e = hipMemcpyAsync(index.data(), d_idx, index.size() * 8, hipMemcpyDeviceToHost, G.s);
+    if (e == hipSuccess) e = hipMemcpyAsync(sst.data(), d_st, ns * 4, hipMemcpyDeviceToHost, G.s);
+    if (e == hipSuccess) e = hipStreamSynchronize(G.s);
+    G.C->dev_free(d_sh);
+    G.C->dev_free(d_idx);
+    G.C->dev_free(d_st);
+    if (e != hipSuccess) throw HipFail{e, "nested shard indexes"};
+  }
+  std::vector<zgpu_chunk_desc> sub;
+  std::vector<uint64_t> owner;
+  for (uint64_t i = 0; i < n; i++) {
+    const zgpu_chunk_desc &D = descs[i];
+    if (status[i] || sel_volume(D, nd) == 0) continue;
+    const uint64_t sh = shard_of[i];
+    if (sh != UINT64_MAX && sst[sh]) {
+      status[i] = (int32_t)sst[sh];
+      continue;
+    }
+    uint64_t lo[ZG_MAXD], hi[ZG_MAXD], idx[ZG_MAXD];
+    for (uint32_t d = 0; d < nd; d++) {
+      cps[d] = D.chunk_shape[d] / ms[d];
+      lo[d] = D.sel_start[d] / ms[d];
+      hi[d] = (D.sel_start[d] + D.sel_shape[d] - 1) / ms[d] + 1;
+      idx[d] = lo[d];
+    }
+    for (;;) {  // every intersecting middle shard, C order
+      zgpu_chunk_desc M{};
+      uint64_t lin = 0;
+      for (uint32_t d = 0; d < nd; d++) {
+        lin = lin * cps[d] + idx[d];
+        const uint64_t cs = idx[d] * ms[d], ce = cs + ms[d];
+        const uint64_t s0 = std::max(D.sel_start[d], cs), s1 = std::min(D.sel_start[d] + D.sel_shape[d], ce);
+        M.chunk_shape[d] = ms[d];
+        M.sel_start[d] = s0 - cs;
+        M.sel_shape[d] = s1 - s0;
+        M.out_start[d] = D.out_start[d] + (s0 - D.sel_start[d]);
+      }
+      bool oob = false;
+      if (sh != UINT64_MAX) {
+        const uint64_t off = index[(sh * n_inner + lin) * 2], size = index[(sh * n_inner + lin) * 2 + 1];
+        if (!(off == ~0ull && size == ~0ull)) {
+          if (off > D.enc_len || size > D.enc_len - off) oob = true;
+          M.enc = (const uint8_t *)D.enc + off;
+          M.enc_len = size;
+        }
+      }
+      if (oob) {  // sharding_codec.rs: an inner chunk outside the shard
+        status[i] = ZGPU_SHARD_INDEX_OOB;
+      } else {
+        sub.push_back(M);
+        owner.push_back(i);
+      }
+      int d = (int)nd - 1;
+      for (; d >= 0; d--) {
+        if (++idx[d] < hi[d]) break;
+        idx[d] = lo[d];
+      }
+      if (d < 0 || oob) break;
+    }
+  }
+  run_sub(G, top.a2b.inner, sub, owner, status);
+}
+
+static void decode_general(GeneralCall &G, const std::shared_ptr<Chain> &chain, const zgpu_chunk_desc *descs,
+                           uint64_t n, int32_t *status) {
+  for (uint64_t i = 0; i < n; i++) status[i] = 0;
+  if (!uniform_shapes(descs, n, G.nd)) {  // one plan per chunk shape
+    std::vector<char> done(n, 0);
+    for (uint64_t i = 0; i < n; i++) {
+      if (done[i]) continue;
+      std::vector<zgpu_chunk_desc> sub;
+      std::vector<uint64_t> owner;
+      for (uint64_t j = i; j < n; j++)
+        if (!done[j] && same_shape(descs[i], descs[j], G.nd)) {
+          sub.push_back(descs[j]);
+          owner.push_back(j);
+          done[j] = 1;
+        }
+      run_sub(G, chain, sub, owner, status);
+    }
+    return;
+  }
+  const Chain &top = *chain;
+  if (fused_plannable(top)) {
+    std::unique_ptr<zgpu_plan> P(plan_new(G.C, chain, G.validate, G.nd, descs, n, G.out_shape, G.flags));
+    plan_upload(*P, G.s);
+    plan_enqueue(*P, G.out, G.s);
+    plan_statuses(*P, status, G.s);
+    return;
+  }
+  if (!top.b2b.empty()) predecode_shards(G, chain, descs, n, status);
+  else nested_host(G, chain, descs, n, status);
 }
 
 // ------------------------------------------------------------------------------------------------
@@ -1362,7 +1729,8 @@ int zgpu_decode_batch(zgpu_chain *ch, uint32_t nd, const zgpu_chunk_desc *descs,
   LaneScope ls(C);
   hipStream_t s = pick_stream(ls.L, stream);
   reset_call_state();
-  if (!(flags & ZGPU_ENC_DEVICE) && !(flags & ZGPU_OUT_DEVICE) && n >= 2) {
+  const bool fused = fused_plannable(*ch->chain) && uniform_shapes(descs, n, nd);
+  if (!(flags & ZGPU_ENC_DEVICE) && !(flags & ZGPU_OUT_DEVICE) && n >= 2 && fused) {
     // pinned host in and out, full coverage: the overlapped sub-batch pipeline
     uint64_t out_elems = 1, covered = 0, out_b;
     for (uint32_t d = 0; d < nd; d++) out_elems *= out_shape[d];
@@ -1451,13 +1819,16 @@ int zgpu_decode_batch(zgpu_chain *ch, uint32_t nd, const zgpu_chunk_desc *descs,
     if (covered != out_elems)
       HIPCHK(h2d_bytes(dout, (const uint8_t *)out, out_bytes, stage(), slab, host_copy_threads(), s));
   }
-  std::unique_ptr<zgpu_plan> P;
   int rc = 0;
   try {
-    P.reset(plan_new(ch, nd, dd, n, out_shape, flags | ZGPU_ENC_DEVICE));
-    plan_upload(*P, s);
-    plan_enqueue(*P, dout, s);
-    rc = plan_statuses(*P, status, s);
+    GeneralCall G{C, ch->validate && !(flags & ZGPU_NO_VALIDATE), nd, dout, out_shape,
+                  flags | ZGPU_ENC_DEVICE | ZGPU_OUT_DEVICE, s, {}};
+    std::vector<int32_t> st(n, 0);
+    decode_general(G, ch->chain, dd, n, st.data());
+    for (uint64_t i = 0; i < n; i++) {
+      if (status) status[i] = st[i];
+      if (!rc) rc = st[i];
+    }
     if (host_out) HIPCHK(d2h_bytes((uint8_t *)out, dout, out_bytes, stage(), slab, host_copy_threads(), s));
   } catch (...) {
     if (host_out) C->dev_free(dout);
@@ -1468,7 +1839,6 @@ int zgpu_decode_batch(zgpu_chain *ch, uint32_t nd, const zgpu_chunk_desc *descs,
   if (host_out) C->dev_free(dout);
   C->dev_free(enc_stage);
   C->host_free(pin_stage);
-  P.reset();
   if (rc) set_err(rc, zgpu_status_name(rc));
   return rc;
   ABI_GUARD_END
@@ -1571,6 +1941,8 @@ int zgpu_decode_files(zgpu_chain *ch, uint32_t nd, const zgpu_chunk_desc *descs,
     C->host_free(pin_stage);
   };
   int rc = 0;
+  const bool fused = fused_plannable(*ch->chain) && uniform_shapes(descs, n, nd);
+  std::vector<int32_t> all(n, 0);
   try {
     enc_dev = (uint8_t *)C->dev_alloc(total ? total : 1);
     if (host_out) {
@@ -1610,14 +1982,20 @@ int zgpu_decode_files(zgpu_chain *ch, uint32_t nd, const zgpu_chunk_desc *descs,
           d.enc_len = 0;
         }
       }
+      if (!fused) {  // the general decode is synchronous: this group is done before the next is read
+        HIPCHK(hipStreamWaitEvent(s, ev[g], 0));
+        GeneralCall GC{C, ch->validate && !(flags & ZGPU_NO_VALIDATE), nd, dout, out_shape,
+                       flags | ZGPU_ENC_DEVICE | ZGPU_OUT_DEVICE, s, {}};
+        decode_general(GC, ch->chain, gd.data(), gd.size(), all.data() + G.b);
+        continue;
+      }
       plans[g].reset(plan_new(ch, nd, gd.data(), gd.size(), out_shape, flags | ZGPU_ENC_DEVICE | ZGPU_OUT_DEVICE));
       plan_upload(*plans[g], s);
       HIPCHK(hipStreamWaitEvent(s, ev[g], 0));
       plan_enqueue(*plans[g], dout, s);
     }
-    std::vector<int32_t> all(n, 0);
     for (size_t g = 0; g < groups.size(); g++)
-      plan_statuses(*plans[g], all.data() + groups[g].b, s);
+      if (plans[g]) plan_statuses(*plans[g], all.data() + groups[g].b, s);
     for (uint64_t i = 0; i < n; i++) {
       if (fr[i].bad_range) all[i] = ZGPU_INVALID_BYTE_RANGE;
       if (status) status[i] = all[i];
