@@ -128,7 +128,7 @@ int main(int argc, char **argv) {
   CK(hipMalloc(&Z.lit, n * Z.lit_stride));
   CK(hipMalloc(&Z.seq, n * Z.seq_cap * 12));
   constexpr int NK = 7;
-  const char *kn[NK] = {"scan", "lits", "blocks", "plan", "direct", "exec_item", "serial"};
+  const char *kn[NK] = {"scan", "blocks", "huf", "lits", "plan", "direct", "exec_item"};
   hipEvent_t ev[NK + 1];
   for (auto &evk : ev) CK(hipEventCreate(&evk));
   float best[NK];
@@ -139,34 +139,46 @@ int main(int argc, char **argv) {
     CK(hipMemcpyToSymbol(HIP_SYMBOL(zgpu::g_zprof), z, sizeof(z)));
   }
 #endif
-  for (int rep = 0; rep < 3; rep++) {
+#ifdef ZG_LIT_STATS
+  {
+    unsigned long long z[8] = {0};
+    CK(hipMemcpyToSymbol(HIP_SYMBOL(zgpu::g_litstats), z, sizeof(z)));
+  }
+#endif
+  int ncu = 256;
+  CK(hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, 0));
+  const int reps = getenv("LAB_REPS") ? atoi(getenv("LAB_REPS")) : 3;
+  for (int rep = 0; rep < reps; rep++) {
     CK(hipMemcpy(d_items, items.data(), n * sizeof(ZgItem), hipMemcpyHostToDevice));
     CK(hipMemset(d_status, 0, n * 4));
     CK(hipMemset(d_out, 0xA5, (size_t)n * chunk));
     zgpu::ZBlk *blks = (zgpu::ZBlk *)Z.blks;
-    const uint32_t grid = (uint32_t)std::min<uint64_t>((uint64_t)n * Z.blk_cap, 256 * 16);
+    const uint64_t recs = (uint64_t)n * Z.blk_cap;
+    const uint32_t grid = (uint32_t)std::min<uint64_t>(recs, (uint64_t)ncu * 16);
+    const uint32_t lgrid = (uint32_t)std::min<uint64_t>(recs, (uint64_t)ncu * ZG_LIT_GRID_PER_CU);
+    const uint32_t bgrid = (uint32_t)std::min<uint64_t>(recs, std::max<uint64_t>(grid, (uint64_t)ncu * 4 * ZG_BLK_WPE));
     CK(hipEventRecord(ev[0]));
     hipLaunchKernelGGL(zgpu::k_zstd_scan, dim3(n), dim3(64), 0, 0, d_items, d_status, blks, Z.blk_cap, Z.nblk, Z.mode,
-                       Z.lit_stride, Z.seq_cap);
+                       Z.lit_stride, Z.seq_cap, 0u, (unsigned long long *)nullptr, (uint32_t *)nullptr,
+                       (unsigned long long *)nullptr);
     CK(hipEventRecord(ev[1]));
-    hipLaunchKernelGGL(zgpu::k_zstd_lits, dim3(std::min<uint64_t>((uint64_t)n * Z.blk_cap, 512)),
-                       dim3(zgpu::LIT_THREADS), 0, 0, d_items, d_status, blks, Z.blk_cap, Z.nblk, Z.mode, (uint32_t)n,
-                       Z.lit, Z.lit_stride);
-    CK(hipEventRecord(ev[2]));
-    hipLaunchKernelGGL(zgpu::k_zstd_blocks, dim3(grid), dim3(64), 0, 0, d_items, d_status, blks, Z.blk_cap, Z.nblk,
+    hipLaunchKernelGGL(zgpu::k_zstd_blocks, dim3(bgrid), dim3(64), 0, 0, d_items, d_status, blks, Z.blk_cap, Z.nblk,
                        Z.mode, (uint32_t)n, Z.lit, Z.lit_stride, Z.seq, Z.seq_cap);
+    CK(hipEventRecord(ev[2]));
+    hipLaunchKernelGGL(zgpu::k_zstd_huf, dim3(grid), dim3(64), 0, 0, d_items, d_status, blks, Z.blk_cap, Z.nblk, Z.mode,
+                       (uint32_t)n, Z.lit, Z.lit_stride);
     CK(hipEventRecord(ev[3]));
-    hipLaunchKernelGGL(zgpu::k_zstd_plan, dim3(n), dim3(64), 0, 0, d_items, d_status, blks, Z.blk_cap, Z.nblk, Z.mode,
-                       chunk);
+    hipLaunchKernelGGL(zgpu::k_zstd_lits, dim3(lgrid), dim3(zgpu::LIT_THREADS), 0, 0, d_items, d_status, blks, Z.blk_cap,
+                       Z.nblk, Z.mode, (uint32_t)n, Z.lit, Z.lit_stride);
     CK(hipEventRecord(ev[4]));
+    hipLaunchKernelGGL(zgpu::k_zstd_plan, dim3(n), dim3(64), 0, 0, d_items, d_status, blks, Z.blk_cap, Z.nblk, Z.mode,
+                       chunk, zgpu::XSEG);
+    CK(hipEventRecord(ev[5]));
     hipLaunchKernelGGL(zgpu::k_zstd_direct, dim3(grid), dim3(256), 0, 0, d_items, d_status, blks, Z.blk_cap, Z.nblk,
                        Z.mode, (uint32_t)n, d_out, chunk, Z.lit, Z.lit_stride);
-    CK(hipEventRecord(ev[5]));
-    hipLaunchKernelGGL(zgpu::k_zstd_exec_item, dim3(n * zgpu::XSEG), dim3(64), 0, 0, d_items, d_status, blks, Z.blk_cap, Z.nblk,
-                       Z.mode, d_out, chunk, Z.lit, Z.lit_stride, Z.seq, Z.seq_cap);
     CK(hipEventRecord(ev[6]));
-    hipLaunchKernelGGL(zgpu::k_zstd, dim3(n), dim3(64), 0, 0, d_items, d_status, d_out, chunk, Z.lit, Z.lit_stride,
-                       Z.mode);
+    hipLaunchKernelGGL(zgpu::k_zstd_exec_item, dim3(n * zgpu::XSEG), dim3(64), 0, 0, d_items, d_status, blks,
+                       Z.blk_cap, Z.nblk, Z.mode, d_out, chunk, Z.lit, Z.lit_stride, Z.seq, Z.seq_cap, zgpu::XSEG);
     CK(hipEventRecord(ev[7]));
     CK(hipEventSynchronize(ev[7]));
     for (int k = 0; k < NK; k++) {
@@ -191,6 +203,14 @@ int main(int argc, char **argv) {
   for (int k = 0; k < NK; k++) tot += best[k];
   printf("blocks %llu (%.1f/chunk), mode[0]=%u, bad=%d\n", (unsigned long long)blocks, (double)blocks / n, mode[0], bad);
   for (int k = 0; k < NK; k++) printf("  %-12s %8.3f ms\n", kn[k], best[k]);
+#ifdef ZG_LIT_STATS
+  {
+    unsigned long long z[8];
+    CK(hipMemcpyFromSymbol(z, HIP_SYMBOL(zgpu::g_litstats), sizeof(z)));
+    printf("lit stats (all reps): huffman blocks %llu, blocks needing repair %llu, repair rounds %llu, lanes re-decoded %llu, "
+           "symbols %llu, warm-up symbols %llu, lanes %llu\n", z[0], z[1], z[2], z[3], z[4], z[5], z[6]);
+  }
+#endif
 #ifdef ZG_PROFILE
   {
     unsigned long long z[13];

@@ -1854,6 +1854,44 @@ struct GWord {
   }
 };
 
+#ifdef ZG_LIT_STATS
+// lab counters (tools/lab/zstd_lab.cpp): blocks, blocks with repairs, repair rounds, lanes re-decoded,
+// symbols, warm-up symbols, lanes
+__device__ unsigned long long g_litstats[8];
+#define LS_ADD(k, v) atomicAdd(&g_litstats[k], (unsigned long long)(v))
+#else
+#define LS_ADD(k, v) ((void)0)
+#endif
+
+// uncached word reads for the rare repair walks (the cached readers' state stays out of them)
+template <class Wd>
+__device__ __forceinline__ uint32_t word_raw(const Wd &w, int32_t k) { return w(k); }
+__device__ __forceinline__ uint32_t word_raw(const GWordPF &w, int32_t k) { return (k >= 0 && k < w.lim) ? w.Wp[k] : 0u; }
+__device__ __forceinline__ uint32_t word_raw(const GWord &w, int32_t k) { return (k >= 0 && k < w.lim) ? w.Wp[k] : 0u; }
+template <class Wd>
+struct RawWord {
+  const Wd &w;
+  __device__ __forceinline__ uint32_t operator()(int32_t k) const { return word_raw(w, k); }
+};
+
+// one symbol of a lane's chain (position p moves down by the code length)
+template <class Wd>
+__device__ __forceinline__ void hl_step(HufLane &H, int32_t &p, uint32_t tl, const uint16_t *huf, const Wd &word) {
+  if (H.v <= 32) {
+    H.C |= (uint64_t)word((H.lp >> 5) - 1) << (32 - H.v);
+    H.v += 32;
+    H.lp -= 32;
+  }
+  const uint32_t nb = huf[(uint32_t)(H.C >> (64 - tl))] >> 8;
+  H.C <<= nb;
+  H.v -= (int32_t)nb;
+  p -= (int32_t)nb;
+}
+
+#ifndef ZG_LIT_SYNC
+#define ZG_LIT_SYNC 1  // repair by sync-point search (0: re-decode the whole segment)
+#endif
+
 template <class Wd>
 __device__ bool lits_decode(ZLitSmem &S, const Wd &word, uint32_t nstreams, const int32_t *top, const int32_t *lob,
                             const uint32_t *nsym, uint32_t tl, uint8_t *lit, uint32_t seg) {
@@ -1866,14 +1904,18 @@ __device__ bool lits_decode(ZLitSmem &S, const Wd &word, uint32_t nstreams, cons
   const int64_t len = (int64_t)T0 - L0;
   const int32_t tj = T0 - (int32_t)(len * j / G), tj1 = T0 - (int32_t)(len * (j + 1) / G);
   const uint32_t maxn = NS + 1;  // a segment never holds more symbols than its stream
-  // pass 1: entry / exit / count
+  // pass 1: entry / exit / count (its own copy of a cached reader, dead after the pass)
   {
+    const Wd w1 = word;
     HufLane H;
     int32_t p = j == 0 ? T0 : min(T0, tj + LIT_WARM);
-    hl_init(H, p, word);
-    if (j) hl_run<false>(H, p, tj, tl, S.huf, word, nullptr, 0xFFFFFFFFu);
+    hl_init(H, p, w1);
+    if (j) {
+      const uint32_t wn = hl_run<false>(H, p, tj, tl, S.huf, w1, nullptr, 0xFFFFFFFFu);
+      LS_ADD(5, wn);
+    }
     S.entry[t] = p;
-    S.cnt[t] = hl_run<false>(H, p, tj1, tl, S.huf, word, nullptr, maxn);
+    S.cnt[t] = hl_run<false>(H, p, tj1, tl, S.huf, w1, nullptr, maxn);
     S.exit_[t] = p;
   }
   __syncthreads();
@@ -1886,15 +1928,59 @@ __device__ bool lits_decode(ZLitSmem &S, const Wd &word, uint32_t nstreams, cons
     int32_t ne = 0, nx = 0;
     uint32_t nc = 0;
     const bool fix = wrong && pred_ok;
+#ifdef ZG_LIT_STATS
+    if (fix) LS_ADD(3, 1);
+    if (t == 0 && round == 0) LS_ADD(0, 1);
+#endif
     if (fix) {
+#if ZG_LIT_SYNC
+      // The lane's own chain (from its warm-up entry) is wrong only until it meets the true chain
+      // (from the predecessor's exit): walk both, always stepping the one further up the stream,
+      // until they meet (the count differs by the symbols each took to get there; the exit is the
+      // lane's own) or the true chain leaves the segment without meeting it (its count and exit).
+      // Huffman chains meet within a few symbols, so a repair costs a few symbols, not a segment.
+      const RawWord<Wd> rw{word};
+      HufLane Ht, Hw;
+      int32_t pt = S.exit_[t - 1], pw = S.entry[t];
+      ne = pt;
+      hl_init(Ht, pt, rw);
+      hl_init(Hw, pw, rw);
+      uint32_t nt = 0, nw = 0;
+      for (;;) {
+        if (pt == pw) {
+          nc = S.cnt[t] - nw + nt;
+          nx = S.exit_[t];
+          break;
+        }
+        if (pt <= tj1 || nt > maxn || nw > maxn) {
+          nc = nt;
+          nx = pt;
+          break;
+        }
+        if (pt > pw) {
+          hl_step(Ht, pt, tl, S.huf, rw);
+          nt++;
+        } else {
+          hl_step(Hw, pw, tl, S.huf, rw);
+          nw++;
+        }
+      }
+#else
       HufLane H;
       int32_t p = S.exit_[t - 1];
       ne = p;
       hl_init(H, p, word);
       nc = hl_run<false>(H, p, tj1, tl, S.huf, word, nullptr, maxn);
       nx = p;
+#endif
     }
     if (__syncthreads_or(wrong) == 0) break;
+#ifdef ZG_LIT_STATS
+    if (t == 0) {
+      LS_ADD(2, 1);
+      if (round == 0) LS_ADD(1, 1);
+    }
+#endif
     if (fix) {
       S.entry[t] = ne;
       S.exit_[t] = nx;
@@ -1904,6 +1990,8 @@ __device__ bool lits_decode(ZLitSmem &S, const Wd &word, uint32_t nstreams, cons
   }
   // every lane right now; per-stream symbol count and exact end
   uint32_t c = S.cnt[t];
+  LS_ADD(4, c);
+  LS_ADD(6, 1);
   const uint32_t lane = lane_id();
   uint32_t incl = c;
   for (int o = 1; o < 64; o <<= 1) {
@@ -1924,13 +2012,14 @@ __device__ bool lits_decode(ZLitSmem &S, const Wd &word, uint32_t nstreams, cons
   if (__syncthreads_or(bad)) return false;
   // pass 2: decode again, writing
   if (c) {
+    const Wd w2 = word;
     HufLane H;
     int32_t p = S.entry[t];
-    hl_init(H, p, word);
+    hl_init(H, p, w2);
 #if ZG_LIT_STAGE
-    hl_run<true>(H, p, tj1, tl, S.huf, word, lit + (uint64_t)s * seg + off, c, &S.stg[t * (LIT_STG_PITCH / 16)]);
+    hl_run<true>(H, p, tj1, tl, S.huf, w2, lit + (uint64_t)s * seg + off, c, &S.stg[t * (LIT_STG_PITCH / 16)]);
 #else
-    hl_run<true>(H, p, tj1, tl, S.huf, word, lit + (uint64_t)s * seg + off, c);
+    hl_run<true>(H, p, tj1, tl, S.huf, w2, lit + (uint64_t)s * seg + off, c);
 #endif
   }
   return true;
