@@ -1658,7 +1658,10 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(ZG_BLK_WPE, 
 #define ZG_LIT_LDS (16 * 1024)
 #endif
 constexpr uint32_t LIT_LDS = ZG_LIT_LDS;
-constexpr int32_t LIT_WARM = 128;
+#ifndef ZG_LIT_WARM
+#define ZG_LIT_WARM 128
+#endif
+constexpr int32_t LIT_WARM = ZG_LIT_WARM;
 constexpr uint32_t LIT_THREADS = 256;
 #ifndef ZG_LIT_WPE
 #define ZG_LIT_WPE 3  // min waves per SIMD k_zstd_lits is compiled for (A/B: 3 beats 2 and forced 4)
