@@ -1,40 +1,50 @@
 // zstd (RFC 8878) frame ENCODER on gfx950: the write half of the zstd codec (ZstdCodec::encode,
 // zarrs/src/array/codec/bytes_to_bytes/zstd/zstd_codec.rs:100-111, zstd::bulk::Compressor). The output
 // is one single-segment frame any zstd decoder reads (libzstd, zstd-sys, k_zstd*); its bytes are not
-// libzstd's (match finding and block splitting are encoder choices).
+// libzstd's (match finding, block splitting and entropy tables are encoder choices).
 //
-// One 64-lane wave encodes one item, in superblocks of 64 zstd blocks of ZE_BLK input bytes:
+// One 64-lane wave encodes one item, in superblocks of ZE_NB zstd blocks of ZE_BLK (64 KiB) input:
 //   1. LZ77 over the superblock, 64 positions per step (the gzip encoder's scheme, deflate_enc.hip):
 //      per lane a 4-byte hash bucket candidate (u32 positions: the window is the whole frame, offsets
-//      below 2^29) and a match of up to 32 bytes; the greedy parse is a scalar walk over the ballot of match-starting lanes, and a chosen
-//      match that reached 32 bytes is extended by the whole wave (64 x 4 bytes per step). Matches never
-//      cross a block end. Chosen literals go to the block's literal scratch, matches to its sequence
-//      scratch (literal length, match length, offset), counted per block.
+//      below 2^29) and a match of up to 32 bytes; the greedy parse is a scalar walk over the ballot of
+//      match-starting lanes, and a chosen match that reached 32 bytes is extended by the whole wave
+//      (64 x 4 bytes per step). Matches never cross a block end. Chosen literals go to the block's
+//      literal scratch, matches to its sequence scratch (literal length, match length, offset).
 //   2. one lane per block: the block's sequences FSE-coded with the predefined distributions
 //      (Symbol_Compression_Modes 0: no table descriptions), the tANS state chain walked backwards from
-//      the last sequence as the format requires, into the lane's bitstream scratch; the block size from
-//      its raw literals section, sequences section and bitstream (a raw block when that is not smaller).
-//   3. the blocks' sizes prefix-summed over the wave, each lane writes its block (header, literals,
-//      sequences) at its offset; the frame header first, the XXH64 content checksum last when the
-//      codec asks for one.
+//      the last sequence as the format requires, into the lane's bitstream scratch.
+//   3. the wave writes the blocks in order: each block's literals become a Huffman-compressed
+//      literals section (RFC 8878 3.1.1.3.1 / 4.2.1: a length-limited code from the block's
+//      histogram, its tree description as FSE-compressed or 4-bit weights, 1 or 4 streams placed
+//      by a wave prefix sum of the code lengths through an LDS bit ring), an RLE section (one distinct
+//      byte) or raw literals, whichever is smallest; the block is written compressed (literals +
+//      sequences) or raw, whichever is smaller. The frame header first, the XXH64 content checksum
+//      last when the codec asks for one. 64 KiB blocks keep the decoder's per-block work (k_zstd_*:
+//      one Huffman table, one block record per block) to the libzstd frames' order of magnitude.
+// The literal-section format is pinned on the CPU by tests/zstd_huf_model.py (a Python restatement
+// of these steps whose frames libzstd decodes).
 #include <hip/hip_runtime.h>
 
 #include "../common.hpp"
+#include "huff.hpp"
 #include "launch.hpp"
 #include "xxh.hpp"
 
 namespace zgpu {
 namespace {
 
-constexpr uint32_t ZE_BLK = 4096;            // input bytes per zstd block
-constexpr uint32_t ZE_NB = 64;               // blocks per superblock (one per lane in phase 2)
+constexpr uint32_t ZE_BLK = 65536;           // input bytes per zstd block
+constexpr uint32_t ZE_NB = 8;                // blocks per superblock (one per lane in phase 2)
 constexpr uint32_t ZE_SB = ZE_BLK * ZE_NB;   // superblock input bytes
 constexpr uint32_t ZE_SEQ = ZE_BLK / 4;      // sequences per block at most (matches >= 4 bytes)
-constexpr uint32_t ZE_BITW = 2048;           // bitstream scratch words per block (61 bits x 1024 seqs)
+constexpr uint32_t ZE_BITW = ZE_SEQ * 77 / 32 + 16;  // bitstream scratch words per block (<= 77 bits a sequence)
 constexpr uint32_t ZE_HBITS = 12, ZE_HSIZE = 1u << ZE_HBITS;
 constexpr uint32_t ZE_MAXOFF = (1u << 29) - 4;  // offset + 3 within the predefined OF table (codes <= 28)
 constexpr uint32_t ZE_CAP1 = 32;             // per-lane match search; longer chosen matches: the wave
 constexpr uint64_t ZE_SCRATCH = (uint64_t)ZE_SB + (uint64_t)ZE_NB * ZE_SEQ * 8 + (uint64_t)ZE_NB * ZE_BITW * 4;
+constexpr uint32_t HUF_MAXBITS = 11;         // Max_Number_of_Bits of a literals code (RFC 8878 4.2.1)
+constexpr uint32_t HUF_WLOG = 6;             // accuracy log of the FSE-compressed weights
+constexpr uint32_t HR_WORDS = 512;           // LDS bit ring of a Huffman stream being written (>= 1024 x 11 bits)
 
 __constant__ int16_t c_ll_norm[36] = {4, 3, 2, 2, 2, 2, 2, 2, 2, 2, 2, 2, 2, 1, 1, 1, 2, 2,
                                       2, 2, 2, 2, 2, 2, 2, 3, 2, 1, 1, 1, 1, 1, -1, -1, -1, -1};
@@ -72,8 +82,23 @@ struct ZeSmem {
   PreTab<6, 36> ll;
   PreTab<6, 53> ml;
   PreTab<5, 29> of;
-  uint32_t nlit[ZE_NB], nseq[ZE_NB];
+  uint32_t nlit[ZE_NB], nseq[ZE_NB], sbytes[ZE_NB];
   uint32_t next[64];
+  // the literals section of the block being written
+  uint32_t hfreq[256];
+  uint32_t sfreq[4][256];  // per literal stream (4-stream sections)
+  uint8_t hlen[256];
+  uint16_t hcode[256];
+  HuffScratch hs;
+  uint32_t ring[HR_WORDS];
+  uint8_t hdesc[136];  // tree description (<= 1 + 128 bytes)
+  uint8_t wts[256];    // Huffman weights (tree description input)
+  uint32_t hmisc[8];
+  // FSE table of the weights (accuracy log 6, <= 13 symbols)
+  uint8_t wsym[64], wnb[64];
+  uint16_t wbase[64];
+  uint8_t wenc[13][64];
+  uint8_t wfirst[13];
 };
 
 #define WSYNC() __syncthreads()
@@ -207,6 +232,227 @@ __device__ uint32_t encode_seqs(ZeSmem &S, const uint64_t *seqs, uint32_t nseq, 
   return bytes;
 }
 
+struct BW8 {  // lane-serial forward bit writer into bytes, LSB first (k <= 24 bits a call)
+  uint8_t *out;
+  uint32_t n;
+  uint64_t acc;
+  uint32_t nb;
+  __device__ void put(uint32_t v, uint32_t k) {
+    acc |= (uint64_t)(v & ((1u << k) - 1u)) << nb;
+    nb += k;
+    while (nb >= 8) {
+      out[n++] = (uint8_t)acc;
+      acc >>= 8;
+      nb -= 8;
+    }
+  }
+  __device__ void close() {
+    if (nb) out[n++] = (uint8_t)acc;
+    acc = 0;
+    nb = 0;
+  }
+  __device__ void close_backward() {  // end mark of a backward-read stream: a 1 bit, zero padding
+    put(1, 1);
+    close();
+  }
+};
+
+// Normalised weight counts summing to 2^HUF_WLOG, every present symbol >= 1 (tests/zstd_huf_model.py
+// fse_normalize)
+__device__ void w_normalize(const uint32_t *counts, uint32_t nsym, int32_t *norm) {
+  uint32_t total = 0;
+  for (uint32_t s = 0; s < nsym; s++) total += counts[s];
+  int32_t sum = 0;
+  for (uint32_t s = 0; s < nsym; s++) {
+    norm[s] = counts[s] ? max(1, (int32_t)((counts[s] << HUF_WLOG) / total)) : 0;
+    sum += norm[s];
+  }
+  int32_t diff = (1 << HUF_WLOG) - sum;
+  while (diff) {
+    int32_t best = -1;
+    for (uint32_t t = 0; t < nsym; t++)
+      if ((diff > 0 || norm[t] > 1) && (best < 0 || norm[t] > norm[best])) best = (int32_t)t;
+    if (diff > 0) {
+      norm[best] += diff;
+      diff = 0;
+    } else {
+      const int32_t take = min(-diff, norm[best] - 1);
+      norm[best] -= take;
+      diff += take;
+    }
+  }
+}
+
+// FSE table description (RFC 8878 4.1.1; libzstd FSE_writeNCount; the model's fse_write_ncount)
+__device__ void w_ncount(const int32_t *norm, uint32_t nsym, BW8 &w) {
+  w.put(HUF_WLOG - 5, 4);
+  int32_t remaining = (1 << HUF_WLOG) + 1, threshold = 1 << HUF_WLOG, nbits = HUF_WLOG + 1;
+  uint32_t s = 0;
+  bool prev0 = false;
+  while (s < nsym && remaining > 1) {
+    if (prev0) {
+      uint32_t start = s;
+      while (s < nsym && norm[s] == 0) s++;
+      while (s >= start + 3) {
+        start += 3;
+        w.put(3, 2);
+      }
+      w.put(s - start, 2);
+    }
+    int32_t count = norm[s++];
+    const int32_t mx = (2 * threshold - 1) - remaining;
+    remaining -= count;
+    count += 1;
+    if (count >= threshold) count += mx;
+    w.put((uint32_t)count, (uint32_t)(nbits - (count < mx ? 1 : 0)));
+    prev0 = count == 1;
+    while (remaining < threshold) {
+      nbits--;
+      threshold >>= 1;
+    }
+  }
+  w.close();
+}
+
+// Huffman tree description of the code in S.hlen (lane 0; RFC 8878 4.2.1, libzstd HUF_writeCTable;
+// the model's huf_description): weights maxb + 1 - len of symbols 0..max_sym-1 (max_sym's is
+// implied), FSE-compressed when that is smaller, else 4-bit weights when max_sym <= 128. Returns the
+// description's length in S.hdesc, 0 when neither form applies.
+__device__ uint32_t huf_desc(ZeSmem &S, uint32_t maxb, uint32_t max_sym) {
+  uint32_t counts[13];
+  for (uint32_t k = 0; k < 13; k++) counts[k] = 0;
+  for (uint32_t s = 0; s < max_sym; s++) {
+    const uint32_t w = S.hlen[s] ? maxb + 1 - S.hlen[s] : 0u;
+    S.wts[s] = (uint8_t)w;
+    counts[w]++;
+  }
+  uint32_t distinct = 0, mxc = 0, last = 0;
+  for (uint32_t k = 0; k < 13; k++)
+    if (counts[k]) {
+      distinct++;
+      mxc = max(mxc, counts[k]);
+      last = k;
+    }
+  if (distinct > 1 && mxc < max_sym) {
+    int32_t norm[13];
+    const uint32_t nsym = last + 1;
+    w_normalize(counts, nsym, norm);
+    BW8 w{S.hdesc + 1, 0, 0, 0};
+    w_ncount(norm, nsym, w);
+    // the weights' FSE table (FSE_buildDTable's spread) and its encoding view
+    constexpr uint32_t size = 1u << HUF_WLOG, mask = size - 1, step = (size >> 1) + (size >> 3) + 3;
+    uint32_t pos = 0, nxt[13];
+    for (uint32_t s = 0; s < nsym; s++) {
+      for (int32_t i = 0; i < norm[s]; i++) {
+        S.wsym[pos] = (uint8_t)s;
+        pos = (pos + step) & mask;
+      }
+      nxt[s] = (uint32_t)norm[s];
+    }
+    for (uint32_t u = 0; u < size; u++) {
+      const uint32_t x = nxt[S.wsym[u]]++;
+      const uint32_t nb = HUF_WLOG - (31 - __builtin_clz(x));
+      S.wnb[u] = (uint8_t)nb;
+      S.wbase[u] = (uint16_t)((x << nb) - size);
+    }
+    for (uint32_t u = size; u-- > 0;) S.wfirst[S.wsym[u]] = (uint8_t)u;
+    for (uint32_t u = 0; u < size; u++)
+      for (uint32_t x = S.wbase[u]; x < S.wbase[u] + (1u << S.wnb[u]); x++) S.wenc[S.wsym[u]][x] = (uint8_t)u;
+    // two interleaved states (even / odd positions), the last two weights' states first
+    const uint32_t N = max_sym;
+    uint32_t X[2];
+    X[(N - 1) & 1] = S.wfirst[S.wts[N - 1]];
+    X[(N - 2) & 1] = S.wfirst[S.wts[N - 2]];
+    for (int32_t k = (int32_t)N - 3; k >= 0; k--) {
+      const uint32_t st = (uint32_t)k & 1u;
+      const uint32_t u = S.wenc[S.wts[k]][X[st]];
+      w.put(X[st] - S.wbase[u], S.wnb[u]);
+      X[st] = u;
+    }
+    w.put(X[1], HUF_WLOG);
+    w.put(X[0], HUF_WLOG);
+    w.close_backward();
+    const uint32_t comp = w.n;
+    if (comp > 1 && comp < max_sym / 2 && comp < 128) {
+      S.hdesc[0] = (uint8_t)comp;
+      return comp + 1;
+    }
+  }
+  if (max_sym <= 128) {
+    S.hdesc[0] = (uint8_t)(127 + max_sym);
+    for (uint32_t i = 0; i < max_sym; i += 2)
+      S.hdesc[1 + i / 2] = (uint8_t)((S.wts[i] << 4) | (i + 1 < max_sym ? S.wts[i + 1] : 0u));
+    return 1 + (max_sym + 1) / 2;
+  }
+  return 0;
+}
+
+// 16 bytes per lane per step, loads issued before use (byte loads of one step are independent, so
+// they are in flight together instead of one L2 round trip per byte)
+__device__ __forceinline__ void wave_copy(uint8_t *dst, const uint8_t *src, uint32_t n) {
+  const uint32_t lane = threadIdx.x;
+  for (uint32_t q0 = 16 * lane; q0 < n; q0 += 1024) {
+    uint8_t t[16];
+#pragma unroll
+    for (int k = 0; k < 16; k++) t[k] = q0 + k < n ? src[q0 + k] : 0;
+#pragma unroll
+    for (int k = 0; k < 16; k++)
+      if (q0 + k < n) dst[q0 + k] = t[k];
+  }
+}
+
+// One Huffman stream of the literals L[a, e) into dst, whose byte length is bits / 8 + 1: written
+// last literal first (the backward reader meets L[a] first). Steps of 1024 codes: lane t takes 16
+// consecutive write positions (one batch of byte loads), a wave prefix sum of the lanes' bit totals
+// places them, and each lane ORs its 16 codes into an LDS bit ring whose complete bytes go out after
+// every step.
+__device__ void huf_emit(ZeSmem &S, const uint8_t *L, uint32_t a, uint32_t e, uint8_t *dst) {
+  const uint32_t lane = threadIdx.x;
+  for (uint32_t k = lane; k < HR_WORDS; k += 64) S.ring[k] = 0;
+  WSYNC();
+  uint32_t base = 0, flushed = 0, cleared = 0;
+  const uint32_t m = e - a;
+  for (uint32_t c0 = 0; c0 < m; c0 += 1024) {
+    const uint32_t i0 = c0 + 16 * lane;  // write positions i0 .. i0 + 15: literals e-1-i
+    uint8_t v[16];
+#pragma unroll
+    for (int k = 0; k < 16; k++) v[k] = i0 + k < m ? L[e - 1 - (i0 + k)] : 0;
+    uint32_t mine = 0;
+#pragma unroll
+    for (int k = 0; k < 16; k++) mine += i0 + k < m ? S.hlen[v[k]] : 0u;
+    uint32_t incl = mine;
+    for (int o = 1; o < 64; o <<= 1) {
+      const uint32_t u = __shfl_up(incl, o, 64);
+      if ((int)lane >= o) incl += u;
+    }
+    const uint32_t tot = __shfl(incl, 63, 64);
+    uint32_t off = base + incl - mine;
+#pragma unroll
+    for (int k = 0; k < 16; k++) {
+      if (i0 + k >= m) break;
+      const uint32_t len = S.hlen[v[k]], code = S.hcode[v[k]];
+      const uint32_t w = (off >> 5) % HR_WORDS, sh = off & 31;
+      atomicOr(&S.ring[w], code << sh);
+      if (sh + len > 32) atomicOr(&S.ring[(w + 1) % HR_WORDS], code >> (32 - sh));
+      off += len;
+    }
+    base += tot;
+    WSYNC();
+    const uint32_t upto = base >> 3;  // complete bytes
+    for (uint32_t q = flushed + lane; q < upto; q += 64) dst[q] = (uint8_t)(S.ring[(q >> 2) % HR_WORDS] >> (8 * (q & 3)));
+    flushed = upto;
+    WSYNC();
+    for (uint32_t wd = cleared + lane; wd < (upto >> 2); wd += 64) S.ring[wd % HR_WORDS] = 0;
+    cleared = upto >> 2;
+    WSYNC();
+  }
+  if (lane == 0) atomicOr(&S.ring[(base >> 5) % HR_WORDS], 1u << (base & 31));  // end mark
+  WSYNC();
+  const uint32_t end = (base >> 3) + 1;
+  for (uint32_t q = flushed + lane; q < end; q += 64) dst[q] = (uint8_t)(S.ring[(q >> 2) % HR_WORDS] >> (8 * (q & 3)));
+  WSYNC();
+}
+
 }  // namespace
 
 // items[i] {src,len} -> one zstd frame in slot i at ZE_HDR (headroom for crc32c codecs at the start);
@@ -311,7 +557,7 @@ __global__ __launch_bounds__(64) void k_zstd_encode(ZgItem *items, uint32_t *sta
             const uint32_t pm = base + m;
             if (L == ZE_CAP1 && b1 - pm > ZE_CAP1) {
               const uint32_t cnd = (uint32_t)__builtin_amdgcn_readlane((int)cand, (int)m);
-              const uint32_t mlim = b1 - pm;
+              const uint32_t mlim = min(b1 - pm, 65535u);  // a sequence record holds 16-bit lengths
               for (uint32_t k0 = ZE_CAP1;; k0 += 256) {
                 const uint32_t k = k0 + 4 * lane;
                 uint32_t mis = 0xFFFFFFFFu;  // first mismatching offset this lane sees
@@ -373,66 +619,165 @@ __global__ __launch_bounds__(64) void k_zstd_encode(ZgItem *items, uint32_t *sta
         }
       }
       WSYNC();
-      // ---- 2. one lane per block: sequences bitstream and the block's size
-      uint32_t bsz = 0, kind = 0, nbytes = 0, nl = 0, ns = 0, blen = 0;
+      // ---- 2. one lane per block: the sequences' FSE bitstream
       if (lane < nblk) {
-        const uint32_t b0 = sb0 + lane * ZE_BLK;
-        blen = n ? min(ZE_BLK, n - b0) : 0;
-        nl = S.nlit[lane];
-        ns = S.nseq[lane];
-        nbytes = ns ? encode_seqs(S, seqs + lane * ZE_SEQ, ns, bits + lane * ZE_BITW) : 0;
-        const uint32_t shdr = ns == 0 ? 1 : ns < 128 ? 2 : ns < 0x7F00 ? 3 : 4;  // count (+ modes)
-        const uint32_t content = 3 + nl + shdr + nbytes;
-        kind = (ns && content < blen) ? 2u : 0u;  // compressed, else raw
-        bsz = 3 + (kind == 2 ? content : blen);
+        const uint32_t ns = S.nseq[lane];
+        S.sbytes[lane] = ns ? encode_seqs(S, seqs + lane * ZE_SEQ, ns, bits + lane * ZE_BITW) : 0u;
       }
-      uint32_t incl = bsz;
-      for (int o = 1; o < 64; o <<= 1) {
-        const uint32_t u = __shfl_up(incl, o, 64);
-        if ((int)lane >= o) incl += u;
-      }
-      const uint32_t total = __shfl(incl, 63, 64);
-      if (op + total > cap) ovf = true;
-      // ---- 3. every lane writes its block
-      if (!ovf && lane < nblk) {
-        uint8_t *o = out + op + (incl - bsz);
-        const bool last = sb0 + ZE_SB >= n && lane == nblk - 1;
-        const uint32_t bs = bsz - 3;
-        const uint32_t hdr = (last ? 1u : 0u) | (kind << 1) | (bs << 3);
-        o[0] = (uint8_t)hdr;
-        o[1] = (uint8_t)(hdr >> 8);
-        o[2] = (uint8_t)(hdr >> 16);
-        o += 3;
-        if (kind == 0) {
-          const uint8_t *src = in + sb0 + lane * ZE_BLK;
-          for (uint32_t q = 0; q < blen; q++) o[q] = src[q];
-        } else {
-          // raw literals section, 3-byte header (Size_Format 11: 20-bit Regenerated_Size)
-          o[0] = (uint8_t)((3u << 2) | ((nl & 0xF) << 4));
-          o[1] = (uint8_t)(nl >> 4);
-          o[2] = (uint8_t)(nl >> 12);
-          o += 3;
-          const uint8_t *bl = lits + lane * ZE_BLK;
-          for (uint32_t q = 0; q < nl; q++) o[q] = bl[q];
-          o += nl;
-          // sequences section: count, Symbol_Compression_Modes = 0 (predefined LL / OF / ML)
-          if (ns < 128) {
-            *o++ = (uint8_t)ns;
-          } else if (ns < 0x7F00) {
-            *o++ = (uint8_t)((ns >> 8) + 128);
-            *o++ = (uint8_t)ns;
-          } else {
-            *o++ = 0xFF;
-            *o++ = (uint8_t)(ns - 0x7F00);
-            *o++ = (uint8_t)((ns - 0x7F00) >> 8);
-          }
-          *o++ = 0;
-          const uint8_t *bw = (const uint8_t *)(bits + lane * ZE_BITW);
-          for (uint32_t q = 0; q < nbytes; q++) o[q] = bw[q];
-        }
-      }
-      op += total;
       WSYNC();
+      // ---- 3. the wave writes the blocks in order: literals section (Huffman / RLE / raw), sequences
+      for (uint32_t b = 0; b < nblk && !ovf; b++) {
+        const uint32_t b0 = sb0 + b * ZE_BLK;
+        const uint32_t blen = n ? min(ZE_BLK, n - b0) : 0u;
+        const uint32_t nl = S.nlit[b], ns = S.nseq[b], sbyt = S.sbytes[b];
+        const uint8_t *L = lits + b * ZE_BLK;
+        const bool last = sb0 + ZE_SB >= n && b == nblk - 1;
+        // histograms per literal stream (4-stream cut at seg4) and of the block
+        const uint32_t seg4 = (nl + 3) / 4;
+        for (uint32_t k = lane; k < 4 * 256; k += 64) (&S.sfreq[0][0])[k] = 0;
+        WSYNC();
+        for (uint32_t q0 = 16 * lane; q0 < nl; q0 += 1024) {
+          uint8_t v[16];
+#pragma unroll
+          for (int k = 0; k < 16; k++) v[k] = q0 + k < nl ? L[q0 + k] : 0;
+#pragma unroll
+          for (int k = 0; k < 16; k++) {
+            const uint32_t q = q0 + k;
+            if (q < nl) atomicAdd(&S.sfreq[(q >= seg4) + (q >= 2 * seg4) + (q >= 3 * seg4)][v[k]], 1u);
+          }
+        }
+        WSYNC();
+        uint32_t used = 0;
+        for (uint32_t k = lane; k < 256; k += 64) {
+          S.hfreq[k] = S.sfreq[0][k] + S.sfreq[1][k] + S.sfreq[2][k] + S.sfreq[3][k];
+          used += S.hfreq[k] ? 1u : 0u;
+        }
+        used = huff_wave_sum(used);
+        const uint32_t rh = nl <= 31 ? 1u : nl <= 4095 ? 2u : 3u;  // raw / RLE header (Size_Format)
+        uint32_t lsec = rh + nl, ltype = 0;
+        if (used == 1) {
+          lsec = rh + 1;
+          ltype = 1;
+        }
+        uint32_t dl = 0, nstr = 0, comp = 0, hh = 0, sf = 0, sb4[4] = {0, 0, 0, 0};
+#ifdef ZE_NO_HUF
+        if (false) {
+#else
+        if (used >= 2) {
+#endif
+          huff_lengths(S.hs, S.hfreq, 256, HUF_MAXBITS, S.hlen);
+          if (lane == 0) {
+            uint32_t maxb = 0, max_sym = 0;
+            for (uint32_t v = 0; v < 256; v++)
+              if (S.hlen[v]) {
+                maxb = max(maxb, (uint32_t)S.hlen[v]);
+                max_sym = v;
+              }
+            S.hmisc[0] = huf_desc(S, maxb, max_sym);
+            uint32_t val = 0;  // prefix codes: from the longest length up, in symbol order
+            for (uint32_t len = maxb; len >= 1; len--) {
+              for (uint32_t v = 0; v < 256; v++)
+                if (S.hlen[v] == len) S.hcode[v] = (uint16_t)val++;
+              val >>= 1;
+            }
+          }
+          WSYNC();
+          dl = S.hmisc[0];
+          if (dl) {
+            // stream bit counts from the stream histograms
+            uint32_t bs[4] = {0, 0, 0, 0};
+            for (uint32_t k = lane; k < 256; k += 64)
+              for (uint32_t t = 0; t < 4; t++) bs[t] += S.sfreq[t][k] * S.hlen[k];
+            for (uint32_t t = 0; t < 4; t++) bs[t] = huff_wave_sum(bs[t]);
+            nstr = 1;
+            sb4[0] = (bs[0] + bs[1] + bs[2] + bs[3]) / 8 + 1;
+            comp = dl + sb4[0];
+            if (nl > 1023 || comp > 1023) {
+              nstr = 4;
+              comp = dl + 6;
+              for (uint32_t t = 0; t < 4; t++) {
+                sb4[t] = bs[t] / 8 + 1;
+                comp += sb4[t];
+              }
+            }
+            sf = nstr == 1 ? 0u : (nl <= 1023 && comp <= 1023) ? 1u : (nl <= 16383 && comp <= 16383) ? 2u : 3u;
+            hh = sf <= 1 ? 3u : sf == 2 ? 4u : 5u;
+            if (hh + comp < lsec) {
+              lsec = hh + comp;
+              ltype = 2;
+            }
+          }
+        }
+        const uint32_t shdr = ns == 0 ? 1u : ns < 128 ? 2u : ns < 0x7F00 ? 3u : 4u;
+        const uint32_t content = lsec + shdr + sbyt;
+        const bool cmp = content < blen;
+        const uint32_t bsz = 3 + (cmp ? content : blen);
+        if (op + bsz > cap) {
+          ovf = true;
+          break;
+        }
+        uint8_t *o = out + op;
+#ifdef ZE_DEBUG
+        if (lane == 0)
+          printf("blk %u nl %u ns %u sbyt %u used %u lsec %u ltype %u content %u bsz %u op %llu cmp %d\n", b, nl, ns,
+                 sbyt, used, lsec, ltype, content, bsz, (unsigned long long)op, (int)cmp);
+#endif
+        if (lane == 0) {
+          const uint32_t hdr = (last ? 1u : 0u) | ((cmp ? 2u : 0u) << 1) | ((cmp ? content : blen) << 3);
+          o[0] = (uint8_t)hdr;
+          o[1] = (uint8_t)(hdr >> 8);
+          o[2] = (uint8_t)(hdr >> 16);
+        }
+        o += 3;
+        if (!cmp) {
+          wave_copy(o, in + b0, blen);
+        } else {
+          if (ltype < 2) {  // raw / RLE literals
+            if (lane == 0) {
+              const uint32_t h = rh == 1 ? (ltype | (nl << 3)) : rh == 2 ? (ltype | (1u << 2) | (nl << 4))
+                                                                       : (ltype | (3u << 2) | (nl << 4));
+              for (uint32_t k = 0; k < rh; k++) o[k] = (uint8_t)(h >> (8 * k));
+              if (ltype == 1) o[rh] = L[0];
+            }
+            if (ltype == 0) wave_copy(o + rh, L, nl);
+          } else {  // Huffman: header, tree description, jump table, streams
+            if (lane == 0) {
+              const uint64_t h = 2u | (sf << 2) | ((uint64_t)nl << 4) |
+                                 ((uint64_t)comp << (sf <= 1 ? 14 : sf == 2 ? 18 : 22));
+              for (uint32_t k = 0; k < hh; k++) o[k] = (uint8_t)(h >> (8 * k));
+              if (nstr == 4)
+                for (uint32_t t = 0; t < 3; t++) {
+                  o[hh + dl + 2 * t] = (uint8_t)sb4[t];
+                  o[hh + dl + 2 * t + 1] = (uint8_t)(sb4[t] >> 8);
+                }
+            }
+            for (uint32_t q = lane; q < dl; q += 64) o[hh + q] = S.hdesc[q];
+            uint8_t *st = o + hh + dl + (nstr == 4 ? 6 : 0);
+            const uint32_t seg = nstr == 4 ? (nl + 3) / 4 : nl;
+            for (uint32_t t = 0; t < nstr; t++) {
+              huf_emit(S, L, min(nl, t * seg), min(nl, (t + 1) * seg), st);
+              st += sb4[t];
+            }
+          }
+          uint8_t *q8 = o + lsec;
+          if (lane == 0) {  // Number_of_Sequences, Symbol_Compression_Modes = 0 (predefined LL / OF / ML)
+            if (ns < 128) {
+              q8[0] = (uint8_t)ns;
+            } else if (ns < 0x7F00) {
+              q8[0] = (uint8_t)((ns >> 8) + 128);
+              q8[1] = (uint8_t)ns;
+            } else {
+              q8[0] = 0xFF;
+              q8[1] = (uint8_t)(ns - 0x7F00);
+              q8[2] = (uint8_t)((ns - 0x7F00) >> 8);
+            }
+            if (ns) q8[shdr - 1] = 0;
+          }
+          wave_copy(q8 + shdr, (const uint8_t *)(bits + b * ZE_BITW), sbyt);
+        }
+        op += bsz;
+        WSYNC();
+      }
       if (n == 0) break;
     }
     if (checksum && !ovf) {
