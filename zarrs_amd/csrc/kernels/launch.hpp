@@ -150,13 +150,13 @@ constexpr uint64_t GZE_HDR = 62;          // member offset in a slot (its bit st
 uint32_t gzip_encode_grid(uint32_t n_items);
 hipError_t launch_gzip_encode(ZgItem *items, uint32_t *status, uint32_t n_items, uint8_t *slots, uint64_t slot_bytes,
                               uint32_t *sym_scratch, int level, hipStream_t s);
-// zstd frame encode (zstd_enc.hip): item i's bytes -> one single-segment frame at slot i + ZE_HDR, items
-// rewritten to it; scratch holds zstd_encode_grid(n) * zstd_encode_scratch() bytes
+// zstd frame encode (zstd_enc.hip): item i's bytes (at most max_len) -> one single-segment frame at
+// slot i + ZE_HDR, items rewritten to it; the work is cut into 1 MiB segments, one wave each.
+// scratch: zstd_encode_scratch(n_items, max_len) bytes
 constexpr uint64_t ZE_HDR = 64;
-uint64_t zstd_encode_scratch();
-uint32_t zstd_encode_grid(uint32_t n_items);
-hipError_t launch_zstd_encode(ZgItem *items, uint32_t *status, uint32_t n_items, uint8_t *slots, uint64_t slot_bytes,
-                              uint8_t *scratch, int checksum, hipStream_t s);
+uint64_t zstd_encode_scratch(uint32_t n_items, uint64_t max_len);
+hipError_t launch_zstd_encode(ZgItem *items, uint32_t *status, uint32_t n_items, uint64_t max_len, uint8_t *slots,
+                              uint64_t slot_bytes, uint8_t *scratch, int checksum, hipStream_t s);
 // crc32c of each item's bytes written after them (or before them with at_start: src moves back 4)
 hipError_t launch_crc32c_items(ZgItem *items, const uint32_t *status, uint32_t n, int at_start, hipStream_t s);
 // each item's bytes into dst[i] (capacity cap[i], else DECODED_SIZE_MISMATCH); lens[i] = length

@@ -1916,6 +1916,7 @@ __device__ bool lits_decode(ZLitSmem &S, const Wd &word, uint32_t nstreams, cons
     if (j) {
       const uint32_t wn = hl_run<false>(H, p, tj, tl, S.huf, w1, nullptr, 0xFFFFFFFFu);
       LS_ADD(5, wn);
+      (void)wn;
     }
     S.entry[t] = p;
     S.cnt[t] = hl_run<false>(H, p, tj1, tl, S.huf, w1, nullptr, maxn);

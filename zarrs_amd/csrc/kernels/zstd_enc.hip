@@ -455,10 +455,22 @@ __device__ void huf_emit(ZeSmem &S, const uint8_t *L, uint32_t a, uint32_t e, ui
 
 }  // namespace
 
-// items[i] {src,len} -> one zstd frame in slot i at ZE_HDR (headroom for crc32c codecs at the start);
-// items rewritten to it. scratch: zstd_encode_grid(n) * zstd_encode_scratch() bytes.
-__global__ __launch_bounds__(64) void k_zstd_encode(ZgItem *items, uint32_t *status, uint32_t n_items, uint8_t *slots,
-                                                    uint64_t slot_bytes, uint8_t *scratch, uint32_t checksum) {
+// Segment-parallel frame encode. An item is cut into segments of ZE_SEG input bytes (whole blocks);
+// every (item, segment) unit is one wave's work, so a few large chunks still fill the GPU. A
+// segment's blocks are independent of the other segments' encoding: every block carries its own
+// Huffman table and new offsets (no repeat codes), and its matches may reach back before the
+// segment (the input is all resident; the hash table is warmed up with the ZE_WARM bytes before it).
+//   k_zstd_encode_seg : unit u -> its blocks in unit scratch u (seg_len[u], ~0 on overflow)
+//   k_zstd_xxh        : XXH64 of each item (checksum chains only), before the items are rewritten
+//   k_zstd_frame      : unit u -> frame header (segment 0), its blocks copied after the previous
+//                       segments' bytes, the checksum and the item's {src,len} (last segment)
+constexpr uint32_t ZE_SEG = 2 * ZE_SB;                      // 1 MiB input per unit
+constexpr uint32_t ZE_SEGCAP = ZE_SEG + (ZE_SEG / ZE_BLK) * 3 + 256;  // a segment's blocks at most
+constexpr uint32_t ZE_WARM = 16384;
+
+__global__ __launch_bounds__(64) void k_zstd_encode_seg(const ZgItem *items, const uint32_t *status,
+                                                        uint32_t n_items, uint32_t ups, uint8_t *scratch,
+                                                        uint8_t *segout, uint32_t *seg_len) {
   __shared__ ZeSmem S;
   const uint32_t lane = threadIdx.x;
   uint8_t *scr = scratch + (uint64_t)blockIdx.x * ZE_SCRATCH;
@@ -468,39 +480,39 @@ __global__ __launch_bounds__(64) void k_zstd_encode(ZgItem *items, uint32_t *sta
   build_pre(S.ll, c_ll_norm, S.next);
   build_pre(S.ml, c_ml_norm, S.next);
   build_pre(S.of, c_of_norm, S.next);
-  for (uint32_t item = blockIdx.x; item < n_items; item += gridDim.x) {
+  const uint64_t n_units = (uint64_t)n_items * ups;
+  for (uint64_t u = blockIdx.x; u < n_units; u += gridDim.x) {
+    const uint32_t item = (uint32_t)(u / ups), seg = (uint32_t)(u % ups);
     if (status[item]) continue;
     const ZgItem it = items[item];
-    if (it.len >= 0xFFFFFFF0ull) {
-      if (lane == 0) status[item] = ZG_UNSUPPORTED;
-      continue;
-    }
+    if (it.len >= 0xFFFFFFF0ull) continue;  // k_zstd_frame reports it
     const uint8_t *in = (const uint8_t *)it.src;
     const uint32_t n = (uint32_t)it.len;
-    uint8_t *out = slots + (uint64_t)item * slot_bytes + ZE_HDR;
-    const uint64_t cap = slot_bytes - ZE_HDR - 8;
+    const uint32_t s0 = seg * ZE_SEG;
+    if (s0 >= n && !(n == 0 && seg == 0)) continue;
+    const uint32_t s1 = min(n, s0 + ZE_SEG);
+    uint8_t *out = segout + u * (uint64_t)ZE_SEGCAP;
+    const uint64_t cap = ZE_SEGCAP;
     for (uint32_t k = lane; k < ZE_HSIZE; k += 64) S.head[k] = 0;
-    // frame header: magic, descriptor (single segment, content size, checksum flag), content size
-    const uint32_t fcs_flag = n <= 255 ? 0u : n <= 65535 + 256 ? 1u : 2u;
-    const uint32_t fcs_len = fcs_flag == 0 ? 1 : fcs_flag == 1 ? 2 : 4;
-    const uint32_t fcs_val = fcs_flag == 1 ? n - 256 : n;
-    if (lane < 5 + fcs_len) {
-      uint8_t b;
-      if (lane < 4) b = (uint8_t)(0xFD2FB528u >> (8 * lane));
-      else if (lane == 4) b = (uint8_t)((fcs_flag << 6) | (1u << 5) | (checksum ? 4u : 0u));
-      else b = (uint8_t)(fcs_val >> (8 * (lane - 5)));
-      out[lane] = b;
-    }
-    uint64_t op = 5 + fcs_len;
-    bool ovf = false;
     WSYNC();
-    uint32_t skip = 0;
-    for (uint32_t sb0 = 0; sb0 < n || (n == 0 && sb0 == 0); sb0 += ZE_SB) {
-      const uint32_t sb_len = min(ZE_SB, n - sb0);
-      const uint32_t nblk = n ? (sb_len + ZE_BLK - 1) / ZE_BLK : 1;
+    // warm-up: the positions of the ZE_WARM bytes before the segment enter the hash table, in order
+    for (uint32_t p0 = s0 > ZE_WARM ? s0 - ZE_WARM : 0u; p0 < s0; p0 += 64) {
+      const uint32_t p = p0 + lane;
+      if (p < s0 && p + 4 <= n) {
+        const uint32_t h = (ld4(in + p) * 0x9E3779B1u) >> (32 - ZE_HBITS);
+        S.head[h] = p + 1;
+      }
+      WSYNC();
+    }
+    uint64_t op = 0;
+    bool ovf = false;
+    uint32_t skip = s0;
+    for (uint32_t sb0 = s0; sb0 < s1 || (s1 == s0 && sb0 == s0); sb0 += ZE_SB) {
+      const uint32_t sb_len = min(ZE_SB, s1 - sb0);
+      const uint32_t nblk = s1 > s0 ? (sb_len + ZE_BLK - 1) / ZE_BLK : 1;
       // ---- 1. LZ77 over the superblock's blocks
       for (uint32_t b = 0; b < nblk; b++) {
-        const uint32_t b0 = sb0 + b * ZE_BLK, b1 = min(b0 + ZE_BLK, n);
+        const uint32_t b0 = sb0 + b * ZE_BLK, b1 = min(b0 + ZE_BLK, s1);
         uint32_t nl = 0, ns = 0, carry = 0;  // literals / sequences so far; literals since the last match
         uint8_t *blit = lits + b * ZE_BLK;
         uint64_t *bseq = seqs + b * ZE_SEQ;
@@ -628,10 +640,10 @@ __global__ __launch_bounds__(64) void k_zstd_encode(ZgItem *items, uint32_t *sta
       // ---- 3. the wave writes the blocks in order: literals section (Huffman / RLE / raw), sequences
       for (uint32_t b = 0; b < nblk && !ovf; b++) {
         const uint32_t b0 = sb0 + b * ZE_BLK;
-        const uint32_t blen = n ? min(ZE_BLK, n - b0) : 0u;
+        const uint32_t blen = s1 > s0 ? min(ZE_BLK, s1 - b0) : 0u;
         const uint32_t nl = S.nlit[b], ns = S.nseq[b], sbyt = S.sbytes[b];
         const uint8_t *L = lits + b * ZE_BLK;
-        const bool last = sb0 + ZE_SB >= n && b == nblk - 1;
+        const bool last = s1 == n && sb0 + ZE_SB >= s1 && b == nblk - 1;
         // histograms per literal stream (4-stream cut at seg4) and of the block
         const uint32_t seg4 = (nl + 3) / 4;
         for (uint32_t k = lane; k < 4 * 256; k += 64) (&S.sfreq[0][0])[k] = 0;
@@ -778,36 +790,97 @@ __global__ __launch_bounds__(64) void k_zstd_encode(ZgItem *items, uint32_t *sta
         op += bsz;
         WSYNC();
       }
-      if (n == 0) break;
+      if (ovf || s1 == s0) break;
     }
-    if (checksum && !ovf) {
-      const uint64_t h = xxh64(in, n);
-      if (lane < 4) out[op + lane] = (uint8_t)(h >> (8 * lane));
-      op += 4;
-    }
-    if (lane == 0) {
-      if (ovf) {
-        status[item] = ZG_DECODED_SIZE_MISMATCH;
-      } else {
-        items[item].src = (uint64_t)out;
-        items[item].len = op;
-      }
-    }
+    if (lane == 0) seg_len[u] = ovf ? 0xFFFFFFFFu : (uint32_t)op;
     WSYNC();
   }
 }
 
-uint64_t zstd_encode_scratch() { return ZE_SCRATCH; }
-
-uint32_t zstd_encode_grid(uint32_t n_items) {
-  return (uint32_t)std::min<uint64_t>(n_items, (uint64_t)device_cu_count() * 4);
+__global__ __launch_bounds__(64) void k_zstd_xxh(const ZgItem *items, const uint32_t *status, uint32_t n_items,
+                                                 uint64_t *hash) {
+  for (uint32_t item = blockIdx.x; item < n_items; item += gridDim.x) {
+    if (status[item]) continue;
+    const ZgItem it = items[item];
+    const uint64_t h = xxh64((const uint8_t *)it.src, it.len);
+    if (threadIdx.x == 0) hash[item] = h;
+  }
 }
 
-hipError_t launch_zstd_encode(ZgItem *items, uint32_t *status, uint32_t n_items, uint8_t *slots, uint64_t slot_bytes,
-                              uint8_t *scratch, int checksum, hipStream_t s) {
+__global__ __launch_bounds__(64) void k_zstd_frame(ZgItem *items, uint32_t *status, uint32_t n_items, uint32_t ups,
+                                                   uint8_t *slots, uint64_t slot_bytes, const uint8_t *segout,
+                                                   const uint32_t *seg_len, const uint64_t *hash, uint32_t checksum) {
+  const uint32_t lane = threadIdx.x;
+  const uint64_t u = blockIdx.x;
+  const uint32_t item = (uint32_t)(u / ups), seg = (uint32_t)(u % ups);
+  if (status[item]) return;
+  const ZgItem it = items[item];
+  if (it.len >= 0xFFFFFFF0ull) {
+    if (seg == 0 && lane == 0) status[item] = ZG_UNSUPPORTED;
+    return;
+  }
+  const uint32_t n = (uint32_t)it.len;
+  const uint32_t nseg = n ? (n + ZE_SEG - 1) / ZE_SEG : 1u;
+  if (seg >= nseg) return;
+  // frame header: magic, descriptor (single segment, content size, checksum flag), content size
+  const uint32_t fcs_flag = n <= 255 ? 0u : n <= 65535 + 256 ? 1u : 2u;
+  const uint32_t fcs_len = fcs_flag == 0 ? 1 : fcs_flag == 1 ? 2 : 4;
+  const uint32_t fcs_val = fcs_flag == 1 ? n - 256 : n;
+  uint64_t before = 5 + fcs_len, total = 5 + fcs_len;
+  bool ovf = false;
+  for (uint32_t k = 0; k < nseg; k++) {
+    const uint32_t l = seg_len[(uint64_t)item * ups + k];
+    if (l == 0xFFFFFFFFu) ovf = true;
+    if (k < seg) before += l;
+    total += l;
+  }
+  if (checksum) total += 4;
+  const uint64_t cap = slot_bytes - ZE_HDR - 8;
+  if (ovf || total > cap) {
+    if (seg == 0 && lane == 0) status[item] = ZG_DECODED_SIZE_MISMATCH;
+    return;
+  }
+  uint8_t *out = slots + (uint64_t)item * slot_bytes + ZE_HDR;
+  if (seg == 0 && lane < 5 + fcs_len) {
+    uint8_t b;
+    if (lane < 4) b = (uint8_t)(0xFD2FB528u >> (8 * lane));
+    else if (lane == 4) b = (uint8_t)((fcs_flag << 6) | (1u << 5) | (checksum ? 4u : 0u));
+    else b = (uint8_t)(fcs_val >> (8 * (lane - 5)));
+    out[lane] = b;
+  }
+  wave_copy(out + before, segout + u * (uint64_t)ZE_SEGCAP, seg_len[u]);
+  if (seg == nseg - 1 && lane == 0) {
+    if (checksum) {
+      const uint64_t h = hash[item];
+      for (int k = 0; k < 4; k++) out[total - 4 + k] = (uint8_t)(h >> (8 * k));
+    }
+    items[item].src = (uint64_t)out;
+    items[item].len = total;
+  }
+}
+
+uint64_t zstd_encode_scratch(uint32_t n_items, uint64_t max_len) {
+  const uint64_t units = (uint64_t)n_items * ((max_len + ZE_SEG - 1) / ZE_SEG + (max_len == 0 ? 1 : 0));
+  const uint64_t grid = std::min<uint64_t>(std::max<uint64_t>(units, 1), (uint64_t)device_cu_count() * 4);
+  return grid * ZE_SCRATCH + units * (uint64_t)ZE_SEGCAP + units * 4 + (uint64_t)n_items * 8 + 256;
+}
+
+hipError_t launch_zstd_encode(ZgItem *items, uint32_t *status, uint32_t n_items, uint64_t max_len, uint8_t *slots,
+                              uint64_t slot_bytes, uint8_t *scratch, int checksum, hipStream_t s) {
   if (!n_items) return hipSuccess;
-  hipLaunchKernelGGL(k_zstd_encode, dim3(zstd_encode_grid(n_items)), dim3(64), 0, s, items, status, n_items, slots,
-                     slot_bytes, scratch, checksum ? 1u : 0u);
+  const uint32_t ups = (uint32_t)((max_len + ZE_SEG - 1) / ZE_SEG + (max_len == 0 ? 1 : 0));
+  const uint64_t units = (uint64_t)n_items * ups;
+  const uint32_t grid = (uint32_t)std::min<uint64_t>(units, (uint64_t)device_cu_count() * 4);
+  uint8_t *segout = scratch + (uint64_t)grid * ZE_SCRATCH;
+  uint32_t *seg_len = (uint32_t *)(segout + units * (uint64_t)ZE_SEGCAP);
+  uint64_t *hash = (uint64_t *)(((uintptr_t)(seg_len + units) + 7) & ~(uintptr_t)7);
+  hipLaunchKernelGGL(k_zstd_encode_seg, dim3(grid), dim3(64), 0, s, items, status, n_items, ups, scratch, segout,
+                     seg_len);
+  if (checksum)
+    hipLaunchKernelGGL(k_zstd_xxh, dim3(std::min<uint32_t>(n_items, device_cu_count() * 4)), dim3(64), 0, s, items,
+                       status, n_items, hash);
+  hipLaunchKernelGGL(k_zstd_frame, dim3((uint32_t)units), dim3(64), 0, s, items, status, n_items, ups, slots,
+                     slot_bytes, segout, seg_len, hash, checksum ? 1u : 0u);
   return hipGetLastError();
 }
 

@@ -2210,8 +2210,12 @@ static int encode_var(zgpu_ctx *C, const Chain &c, uint32_t nd, const uint64_t *
   int cur = 0;
   uint32_t *sym = nullptr;
   uint8_t *zscr = nullptr;
+  uint64_t in_size = nelem * c.es;  // the current stage's input bound
   for (size_t i = 0; i < c.b2b.size(); i++) {
     const Codec &k = c.b2b[i];
+    const uint64_t stage_in = in_size;
+    in_size = k.kind == CodecKind::Crc32c ? in_size + 4 : k.kind == CodecKind::Gzip ? gzip_bound(in_size)
+              : k.kind == CodecKind::Zstd ? zstd_bound(in_size) : in_size;
     if (k.kind == CodecKind::Crc32c) {
       HIPCHK(launch_crc32c_items(d_items, d_status, (uint32_t)n, k.at_start ? 1 : 0, s));
     } else if (k.kind == CodecKind::Gzip) {
@@ -2222,13 +2226,11 @@ static int encode_var(zgpu_ctx *C, const Chain &c, uint32_t nd, const uint64_t *
       cur ^= 1;
       HIPCHK(launch_gzip_encode(d_items, d_status, (uint32_t)n, pool[cur], pitch, sym, k.level, s));
     } else if (k.kind == CodecKind::Zstd) {
-      if (!zscr) {
-        zscr = (uint8_t *)C->dev_alloc((uint64_t)zstd_encode_grid((uint32_t)std::max<uint64_t>(n, 1)) *
-                                       zstd_encode_scratch());
-        owned.push_back(zscr);
-      }
+      zscr = (uint8_t *)C->dev_alloc(zstd_encode_scratch((uint32_t)n, stage_in));
+      owned.push_back(zscr);
       cur ^= 1;
-      HIPCHK(launch_zstd_encode(d_items, d_status, (uint32_t)n, pool[cur], pitch, zscr, k.checksum ? 1 : 0, s));
+      HIPCHK(launch_zstd_encode(d_items, d_status, (uint32_t)n, stage_in, pool[cur], pitch, zscr, k.checksum ? 1 : 0,
+                                s));
     }
   }
   *d_items_out = d_items;
