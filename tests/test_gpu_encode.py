@@ -424,10 +424,29 @@ def test_zstd_encode_large_chunk_and_small_chunks(ctx, torch_cuda):
             assert co.decode(e.cpu().numpy().tobytes(), [m]).tobytes() == a[i * m:(i + 1) * m].tobytes(), m
 
 
+def test_zstd_encode_many_segmented_chunks(ctx, torch_cuda):
+    """32 chunks of 16 MiB (16 one-wave segments each, 512 segment units): every frame, assembled
+    from its segments, decodes through libzstd. Half the chunks have an all-zero high byte plane
+    (RLE-literal blocks whose matches reach back across segment cuts)."""
+    from zarrs_amd import CodecChain
+    codecs = [B("little"), SHUF2, ZS]
+    co = O.OracleChain.from_metadata(codecs, "uint16", 0, 3)
+    ch = CodecChain.from_metadata(codecs, "uint16", 0, ctx)
+    g = torch_cuda.Generator(device="cuda").manual_seed(7)
+    x = torch_cuda.randint(0, 200, [32 * 32, 512, 512], device="cuda", generator=g, dtype=torch_cuda.int32)
+    x[16 * 32:] += 3000
+    x = x.to(torch_cuda.int16)
+    starts = [[i * 32, 0, 0] for i in range(32)]
+    enc = ch.encode_chunks(x, [32, 512, 512], starts)
+    for i, e in enumerate(enc):
+        d = co.decode(e.cpu().numpy().tobytes(), [32, 512, 512])
+        assert np.array_equal(d.view(np.int16), x[i * 32:(i + 1) * 32].cpu().numpy()), i
+
+
 def test_zstd_encode_ratio_vs_libzstd_level3(ctx, torch_cuda):
     """Compression of SURVEY C5-like data ([bytes, shuffle 2, zstd 3] u16) against libzstd level 3:
-    reported; the GPU frames use raw literals and predefined FSE tables (an encoder choice,
-    zstd_codec.rs:100-111), so they are larger."""
+    reported; the GPU frames use Huffman literals and predefined FSE sequence tables (an encoder
+    choice, zstd_codec.rs:100-111)."""
     from zarrs_amd import CodecChain
     codecs = [B("little"), SHUF2, ZS]
     co = O.OracleChain.from_metadata(codecs, "uint16", 0, 3)

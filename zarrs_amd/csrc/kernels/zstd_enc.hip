@@ -429,12 +429,13 @@ __device__ void huf_emit(ZeSmem &S, const uint8_t *L, uint32_t a, uint32_t e, ui
     uint32_t off = base + incl - mine;
 #pragma unroll
     for (int k = 0; k < 16; k++) {
-      if (i0 + k >= m) break;
-      const uint32_t len = S.hlen[v[k]], code = S.hcode[v[k]];
-      const uint32_t w = (off >> 5) % HR_WORDS, sh = off & 31;
-      atomicOr(&S.ring[w], code << sh);
-      if (sh + len > 32) atomicOr(&S.ring[(w + 1) % HR_WORDS], code >> (32 - sh));
-      off += len;
+      if (i0 + k < m) {
+        const uint32_t len = S.hlen[v[k]], code = S.hcode[v[k]];
+        const uint32_t w = (off >> 5) % HR_WORDS, sh = off & 31;
+        atomicOr(&S.ring[w], code << sh);
+        if (sh + len > 32) atomicOr(&S.ring[(w + 1) % HR_WORDS], code >> (32 - sh));
+        off += len;
+      }
     }
     base += tot;
     WSYNC();
@@ -463,7 +464,8 @@ __device__ void huf_emit(ZeSmem &S, const uint8_t *L, uint32_t a, uint32_t e, ui
 //   k_zstd_encode_seg : unit u -> its blocks in unit scratch u (seg_len[u], ~0 on overflow)
 //   k_zstd_xxh        : XXH64 of each item (checksum chains only), before the items are rewritten
 //   k_zstd_frame      : unit u -> frame header (segment 0), its blocks copied after the previous
-//                       segments' bytes, the checksum and the item's {src,len} (last segment)
+//                       segments' bytes, the checksum and the frame length (last segment)
+//   k_zstd_items      : the items rewritten to the frames (after every unit has read its item)
 constexpr uint32_t ZE_SEG = 2 * ZE_SB;                      // 1 MiB input per unit
 constexpr uint32_t ZE_SEGCAP = ZE_SEG + (ZE_SEG / ZE_BLK) * 3 + 256;  // a segment's blocks at most
 constexpr uint32_t ZE_WARM = 16384;
@@ -809,7 +811,8 @@ __global__ __launch_bounds__(64) void k_zstd_xxh(const ZgItem *items, const uint
 
 __global__ __launch_bounds__(64) void k_zstd_frame(ZgItem *items, uint32_t *status, uint32_t n_items, uint32_t ups,
                                                    uint8_t *slots, uint64_t slot_bytes, const uint8_t *segout,
-                                                   const uint32_t *seg_len, const uint64_t *hash, uint32_t checksum) {
+                                                   const uint32_t *seg_len, const uint64_t *hash, uint32_t checksum,
+                                                   uint64_t *ftot) {
   const uint32_t lane = threadIdx.x;
   const uint64_t u = blockIdx.x;
   const uint32_t item = (uint32_t)(u / ups), seg = (uint32_t)(u % ups);
@@ -854,15 +857,22 @@ __global__ __launch_bounds__(64) void k_zstd_frame(ZgItem *items, uint32_t *stat
       const uint64_t h = hash[item];
       for (int k = 0; k < 4; k++) out[total - 4 + k] = (uint8_t)(h >> (8 * k));
     }
-    items[item].src = (uint64_t)out;
-    items[item].len = total;
+    ftot[item] = total;  // the items are rewritten by k_zstd_items: the other segments still read them
   }
+}
+
+__global__ void k_zstd_items(ZgItem *items, const uint32_t *status, uint32_t n_items, uint8_t *slots,
+                             uint64_t slot_bytes, const uint64_t *ftot) {
+  const uint32_t item = blockIdx.x * blockDim.x + threadIdx.x;
+  if (item >= n_items || status[item]) return;
+  items[item].src = (uint64_t)(slots + (uint64_t)item * slot_bytes + ZE_HDR);
+  items[item].len = ftot[item];
 }
 
 uint64_t zstd_encode_scratch(uint32_t n_items, uint64_t max_len) {
   const uint64_t units = (uint64_t)n_items * ((max_len + ZE_SEG - 1) / ZE_SEG + (max_len == 0 ? 1 : 0));
   const uint64_t grid = std::min<uint64_t>(std::max<uint64_t>(units, 1), (uint64_t)device_cu_count() * 4);
-  return grid * ZE_SCRATCH + units * (uint64_t)ZE_SEGCAP + units * 4 + (uint64_t)n_items * 8 + 256;
+  return grid * ZE_SCRATCH + units * (uint64_t)ZE_SEGCAP + units * 4 + (uint64_t)n_items * 16 + 256;
 }
 
 hipError_t launch_zstd_encode(ZgItem *items, uint32_t *status, uint32_t n_items, uint64_t max_len, uint8_t *slots,
@@ -879,8 +889,11 @@ hipError_t launch_zstd_encode(ZgItem *items, uint32_t *status, uint32_t n_items,
   if (checksum)
     hipLaunchKernelGGL(k_zstd_xxh, dim3(std::min<uint32_t>(n_items, device_cu_count() * 4)), dim3(64), 0, s, items,
                        status, n_items, hash);
+  uint64_t *ftot = hash + n_items;
   hipLaunchKernelGGL(k_zstd_frame, dim3((uint32_t)units), dim3(64), 0, s, items, status, n_items, ups, slots,
-                     slot_bytes, segout, seg_len, hash, checksum ? 1u : 0u);
+                     slot_bytes, segout, seg_len, hash, checksum ? 1u : 0u, ftot);
+  hipLaunchKernelGGL(k_zstd_items, dim3((n_items + 255) / 256), dim3(256), 0, s, items, status, n_items, slots,
+                     slot_bytes, ftot);
   return hipGetLastError();
 }
 
