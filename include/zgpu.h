@@ -289,8 +289,9 @@ int zgpu_encode_batch(zgpu_chain *chain, uint32_t ndim, const uint64_t *chunk_sh
                       void *hip_stream);
 /*
  * zgpu_encode_batch plus the variable-length chains: gzip (one DEFLATE stream of dynamic-Huffman or
- * stored blocks in a gzip member, k_gzip_encode), zstd (one single-segment frame, raw literals,
- * predefined-FSE sequences, optional XXH64 content checksum, k_zstd_encode), crc32c around them,
+ * stored blocks in a gzip member, k_gzip_encode), zstd (one single-segment frame of 64 KiB blocks:
+ * Huffman / RLE / raw literals, predefined-FSE sequences, optional XXH64 content checksum; encoded in
+ * 1 MiB segments, one wave each, k_zstd_encode_seg + k_zstd_frame), crc32c around them,
  * the fixed-size stages in front, and sharding_indexed over a fixed-size or compressing inner chain
  * (ShardingCodecBound::encode_bounded, sharding_codec.rs:924-1085, with SubchunkWriteOrder::C: inner
  * chunks in C order of the inner grid, an inner chunk equal to the fill value everywhere omitted,

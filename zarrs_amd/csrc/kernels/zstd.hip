@@ -1683,8 +1683,16 @@ constexpr int LIT_STAGE_R = ZG_LIT_WPE >= 4 ? 4 : 8;  // 16-B staging loads in f
 #define ZG_LIT_STAGE 0  // 1: a lane's decoded literals leave through a 64-B LDS window, stored as whole
                         // aligned 64-B pieces (4 x 16-B stores) instead of 8-B stores
 #endif
+#ifndef ZG_LIT_STAGE_W
+#define ZG_LIT_STAGE_W 64  // staging window bytes per lane (32: one 32-B sector)
+#endif
+#ifndef ZG_LIT_STG_PITCH
+#define ZG_LIT_STG_PITCH (ZG_LIT_STAGE_W + 16)  // bytes per lane window (16-B aligned, banks spread)
+#endif
 #if ZG_LIT_STAGE
-constexpr uint32_t LIT_STG_PITCH = 80;  // bytes per lane window (64 + 16: 16-B aligned, banks spread)
+constexpr uint32_t LIT_STG_W = ZG_LIT_STAGE_W;
+constexpr uint32_t LIT_STG_PITCH = ZG_LIT_STG_PITCH;
+static_assert(LIT_STG_PITCH % 16 == 0 && LIT_STG_PITCH >= LIT_STG_W, "staging window pitch");
 #endif
 
 struct ZLitSmem {
@@ -1734,7 +1742,7 @@ __device__ __forceinline__ uint32_t hl_run(HufLane &H, int32_t &p, int32_t stop,
   // 8-B words from the first 64-B boundary on go to the lane's LDS window; a completed window leaves
   // as four aligned 16-B stores (a whole half-line at once, no partial-line write-backs)
   static_assert(!ZG_LIT_STAGE || ZG_LIT_PACK_B == 8, "literal staging packs 8-B words");
-  const uint32_t head64 = WRITE ? (uint32_t)((64 - ((uintptr_t)out & 63)) & 63) : 0u;
+  const uint32_t head64 = WRITE ? (uint32_t)((LIT_STG_W - ((uintptr_t)out & (LIT_STG_W - 1))) & (LIT_STG_W - 1)) : 0u;
   uint64_t *stg8 = (uint64_t *)stg;
 #endif
 #endif
@@ -1765,14 +1773,12 @@ __device__ __forceinline__ uint32_t hl_run(HufLane &H, int32_t &p, int32_t stop,
             if (pos < head64) {
               *(uint64_t *)(out + pos) = acc;
             } else {
-              const uint32_t r = (pos - head64) & 63;
+              const uint32_t r = (pos - head64) & (LIT_STG_W - 1);
               stg8[r >> 3] = acc;
-              if (r == 56) {  // window complete: out + pos - 56 is 64-B aligned
-                uint4 *g = (uint4 *)(out + pos - 56);
-                g[0] = stg[0];
-                g[1] = stg[1];
-                g[2] = stg[2];
-                g[3] = stg[3];
+              if (r == LIT_STG_W - 8) {  // window complete: out + pos - r is W-aligned
+                uint4 *g = (uint4 *)(out + pos - r);
+#pragma unroll
+                for (uint32_t q = 0; q < LIT_STG_W / 16; q++) g[q] = stg[q];
               }
             }
 #else
@@ -1793,8 +1799,8 @@ __device__ __forceinline__ uint32_t hl_run(HufLane &H, int32_t &p, int32_t stop,
 #if ZG_LIT_STAGE
   if (WRITE && n - k > head64) {  // the staged words of the last, incomplete window
     const uint32_t done = n - k;  // bytes stored or staged as whole words
-    const uint32_t w0 = done - ((done - head64) & 63);
-    for (uint32_t q = w0; q < done; q += 8) *(uint64_t *)(out + q) = stg8[((q - head64) & 63) >> 3];
+    const uint32_t w0 = done - ((done - head64) & (LIT_STG_W - 1));
+    for (uint32_t q = w0; q < done; q += 8) *(uint64_t *)(out + q) = stg8[((q - head64) & (LIT_STG_W - 1)) >> 3];
   }
 #endif
   if (WRITE)
