@@ -128,6 +128,20 @@ static Role create_codec(Codec &k, const Json *cfg, const std::string &dt, uint3
     k.level = l ? (int)l->as_int() : 5;
     const Json *t = cfg_get("typesize");
     k.elementsize = t && t->kind != Json::Null ? (uint32_t)t->as_int() : 0;
+    // shuffle: "noshuffle" / "shuffle" / "bitshuffle" (V3), 0 / 1 / 2 / -1 = auto (numcodecs: bit
+    // shuffle for 1-byte items, else byte shuffle)
+    if (const Json *sh = cfg_get("shuffle")) {
+      if (sh->kind == Json::Str) {
+        k.shuffle = sh->s == "noshuffle" ? 0 : sh->s == "shuffle" ? 1 : sh->s == "bitshuffle" ? 2 : -2;
+        if (k.shuffle == -2) throw ChainError{ZGPU_INVALID_ARGUMENT, "blosc: unknown shuffle '" + sh->s + "'"};
+      } else if (sh->kind != Json::Null) {
+        const int v = (int)sh->as_int();
+        k.shuffle = v == -1 ? (k.elementsize == 1 ? 2 : 1) : v;
+        if (k.shuffle < 0 || k.shuffle > 2) throw ChainError{ZGPU_INVALID_ARGUMENT, "blosc: shuffle out of range"};
+      }
+    }
+    const Json *bsz = cfg_get("blocksize");
+    k.blocksize = bsz && bsz->kind != Json::Null ? (uint64_t)bsz->as_int() : 0;
   } else if (k.name == "numcodecs.shuffle" || k.name == "shuffle") {
     k.kind = CodecKind::Shuffle;
     const Json *e = cfg_get("elementsize");
@@ -224,6 +238,7 @@ int64_t chain_encoded_bound(const Chain &c, uint64_t nelem) {
     if (k.kind == CodecKind::Crc32c) n += 4;
     else if (k.kind == CodecKind::Gzip) n = gzip_bound(n);
     else if (k.kind == CodecKind::Zstd) n = zstd_bound(n);
+    else if (k.kind == CodecKind::Blosc) n += 16;  // BLOSC_MAX_OVERHEAD (blosc_via_blosc_src.rs:80)
     else if (k.kind != CodecKind::Shuffle) return -1;
   }
   return (int64_t)n;

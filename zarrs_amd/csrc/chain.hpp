@@ -26,6 +26,8 @@ struct Codec {
   bool checksum = false;              // zstd
   uint32_t elementsize = 4;           // shuffle; blosc typesize
   std::string cname;                  // blosc compressor (decode reads the compressor from the header)
+  int shuffle = -1;                   // blosc: 0 noshuffle, 1 byte shuffle, 2 bitshuffle, -1 absent
+  uint64_t blocksize = 0;             // blosc: 0 = automatic
   std::vector<uint64_t> inner_shape;  // sharding
   std::shared_ptr<Chain> inner, index;
 };

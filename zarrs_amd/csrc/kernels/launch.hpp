@@ -236,4 +236,16 @@ hipError_t launch_blosc_info(const ZgItem *items, uint32_t *status, uint32_t n_i
 hipError_t launch_blosc_decode(ZgItem *items, uint32_t *status, uint32_t n_items, const BlInfo *info,
                                const BlDecode &D, uint8_t *dst, uint64_t slot_bytes, hipStream_t s);
 
+// blosc encode (blosc_enc.hip): item i's nbytes -> one c-blosc 1.x frame at slot i + BLE_HDR, items
+// rewritten to it. comp: BL_COMP_LZ4 (lz4 / lz4hc streams) or BL_COMP_ZSTD; shuffle 0 / 1 byte / 2 bit
+constexpr uint64_t BLE_HDR = 64;
+struct BloscEnc {
+  uint32_t comp, shuffle, ts, nsplit, nblk, spi;  // spi: streams per item
+  uint64_t nbytes, bs, ne_max;
+};
+BloscEnc blosc_enc_params(uint32_t comp, uint32_t shuffle, uint32_t ts, uint64_t nbytes, uint64_t blocksize);
+uint64_t blosc_encode_scratch(const BloscEnc &E, uint32_t n_items);
+hipError_t launch_blosc_encode(ZgItem *items, uint32_t *status, uint32_t n_items, const BloscEnc &E, uint8_t *slots,
+                               uint64_t slot_bytes, uint8_t *scratch, int zlevel, hipStream_t s);
+
 }  // namespace zgpu

@@ -467,12 +467,16 @@ __device__ void huf_emit(ZeSmem &S, const uint8_t *L, uint32_t a, uint32_t e, ui
 //                       segments' bytes, the checksum and the frame length (last segment)
 //   k_zstd_items      : the items rewritten to the frames (after every unit has read its item)
 constexpr uint32_t ZE_SEG = 2 * ZE_SB;                      // 1 MiB input per unit
-constexpr uint32_t ZE_SEGCAP = ZE_SEG + (ZE_SEG / ZE_BLK) * 3 + 256;  // a segment's blocks at most
+// a segment's blocks at most (raw blocks: the input + 3 bytes a block), for items of at most max_len
+__host__ __device__ inline uint64_t ze_segcap(uint64_t max_len) {
+  const uint64_t seg = max_len < ZE_SEG ? max_len : ZE_SEG;
+  return ((seg + ((seg + ZE_BLK - 1) / ZE_BLK + 1) * 3 + 256) + 255) & ~255ull;
+}
 constexpr uint32_t ZE_WARM = 16384;
 
 __global__ __launch_bounds__(64) void k_zstd_encode_seg(const ZgItem *items, const uint32_t *status,
                                                         uint32_t n_items, uint32_t ups, uint8_t *scratch,
-                                                        uint8_t *segout, uint32_t *seg_len) {
+                                                        uint8_t *segout, uint32_t *seg_len, uint64_t segcap) {
   __shared__ ZeSmem S;
   const uint32_t lane = threadIdx.x;
   uint8_t *scr = scratch + (uint64_t)blockIdx.x * ZE_SCRATCH;
@@ -493,8 +497,8 @@ __global__ __launch_bounds__(64) void k_zstd_encode_seg(const ZgItem *items, con
     const uint32_t s0 = seg * ZE_SEG;
     if (s0 >= n && !(n == 0 && seg == 0)) continue;
     const uint32_t s1 = min(n, s0 + ZE_SEG);
-    uint8_t *out = segout + u * (uint64_t)ZE_SEGCAP;
-    const uint64_t cap = ZE_SEGCAP;
+    uint8_t *out = segout + u * segcap;
+    const uint64_t cap = segcap;
     for (uint32_t k = lane; k < ZE_HSIZE; k += 64) S.head[k] = 0;
     WSYNC();
     // warm-up: the positions of the ZE_WARM bytes before the segment enter the hash table, in order
@@ -812,7 +816,7 @@ __global__ __launch_bounds__(64) void k_zstd_xxh(const ZgItem *items, const uint
 __global__ __launch_bounds__(64) void k_zstd_frame(ZgItem *items, uint32_t *status, uint32_t n_items, uint32_t ups,
                                                    uint8_t *slots, uint64_t slot_bytes, const uint8_t *segout,
                                                    const uint32_t *seg_len, const uint64_t *hash, uint32_t checksum,
-                                                   uint64_t *ftot) {
+                                                   uint64_t *ftot, uint64_t segcap) {
   const uint32_t lane = threadIdx.x;
   const uint64_t u = blockIdx.x;
   const uint32_t item = (uint32_t)(u / ups), seg = (uint32_t)(u % ups);
@@ -851,7 +855,7 @@ __global__ __launch_bounds__(64) void k_zstd_frame(ZgItem *items, uint32_t *stat
     else b = (uint8_t)(fcs_val >> (8 * (lane - 5)));
     out[lane] = b;
   }
-  wave_copy(out + before, segout + u * (uint64_t)ZE_SEGCAP, seg_len[u]);
+  wave_copy(out + before, segout + u * segcap, seg_len[u]);
   if (seg == nseg - 1 && lane == 0) {
     if (checksum) {
       const uint64_t h = hash[item];
@@ -872,7 +876,7 @@ __global__ void k_zstd_items(ZgItem *items, const uint32_t *status, uint32_t n_i
 uint64_t zstd_encode_scratch(uint32_t n_items, uint64_t max_len) {
   const uint64_t units = (uint64_t)n_items * ((max_len + ZE_SEG - 1) / ZE_SEG + (max_len == 0 ? 1 : 0));
   const uint64_t grid = std::min<uint64_t>(std::max<uint64_t>(units, 1), (uint64_t)device_cu_count() * 4);
-  return grid * ZE_SCRATCH + units * (uint64_t)ZE_SEGCAP + units * 4 + (uint64_t)n_items * 16 + 256;
+  return grid * ZE_SCRATCH + units * ze_segcap(max_len) + units * 4 + (uint64_t)n_items * 16 + 256;
 }
 
 hipError_t launch_zstd_encode(ZgItem *items, uint32_t *status, uint32_t n_items, uint64_t max_len, uint8_t *slots,
@@ -881,17 +885,18 @@ hipError_t launch_zstd_encode(ZgItem *items, uint32_t *status, uint32_t n_items,
   const uint32_t ups = (uint32_t)((max_len + ZE_SEG - 1) / ZE_SEG + (max_len == 0 ? 1 : 0));
   const uint64_t units = (uint64_t)n_items * ups;
   const uint32_t grid = (uint32_t)std::min<uint64_t>(units, (uint64_t)device_cu_count() * 4);
+  const uint64_t segcap = ze_segcap(max_len);
   uint8_t *segout = scratch + (uint64_t)grid * ZE_SCRATCH;
-  uint32_t *seg_len = (uint32_t *)(segout + units * (uint64_t)ZE_SEGCAP);
+  uint32_t *seg_len = (uint32_t *)(segout + units * segcap);
   uint64_t *hash = (uint64_t *)(((uintptr_t)(seg_len + units) + 7) & ~(uintptr_t)7);
   hipLaunchKernelGGL(k_zstd_encode_seg, dim3(grid), dim3(64), 0, s, items, status, n_items, ups, scratch, segout,
-                     seg_len);
+                     seg_len, segcap);
   if (checksum)
     hipLaunchKernelGGL(k_zstd_xxh, dim3(std::min<uint32_t>(n_items, device_cu_count() * 4)), dim3(64), 0, s, items,
                        status, n_items, hash);
   uint64_t *ftot = hash + n_items;
   hipLaunchKernelGGL(k_zstd_frame, dim3((uint32_t)units), dim3(64), 0, s, items, status, n_items, ups, slots,
-                     slot_bytes, segout, seg_len, hash, checksum ? 1u : 0u, ftot);
+                     slot_bytes, segout, seg_len, hash, checksum ? 1u : 0u, ftot, segcap);
   hipLaunchKernelGGL(k_zstd_items, dim3((n_items + 255) / 256), dim3(256), 0, s, items, status, n_items, slots,
                      slot_bytes, ftot);
   return hipGetLastError();

@@ -2171,9 +2171,11 @@ static int encode_var(zgpu_ctx *C, const Chain &c, uint32_t nd, const uint64_t *
       size = gzip_bound(size);
     } else if (k.kind == CodecKind::Zstd) {
       size = zstd_bound(size);
+    } else if (k.kind == CodecKind::Blosc) {
+      size += 16;
     } else {
       return set_err(ZGPU_UNSUPPORTED, "encode: only transpose / bytes / numcodecs.shuffle (innermost, elementsize = "
-                                       "data type size) / crc32c / gzip / zstd run on the GPU write path");
+                                       "data type size) / crc32c / gzip / zstd / blosc run on the GPU write path");
     }
     max_size = std::max(max_size, size);
   }
@@ -2181,7 +2183,8 @@ static int encode_var(zgpu_ctx *C, const Chain &c, uint32_t nd, const uint64_t *
   constexpr uint64_t HR = 64;  // headroom in front of a slot's bytes (crc32c at the start)
   const uint64_t pitch = (HR + max_size + 4 * n_crc + 16 + 255) & ~(uint64_t)255;
   bool gz = false;  // a compressor: its output goes to the other slot pool
-  for (const Codec &k : c.b2b) gz = gz || k.kind == CodecKind::Gzip || k.kind == CodecKind::Zstd;
+  for (const Codec &k : c.b2b)
+    gz = gz || k.kind == CodecKind::Gzip || k.kind == CodecKind::Zstd || k.kind == CodecKind::Blosc;
   uint8_t *pool[2] = {(uint8_t *)C->dev_alloc(std::max<uint64_t>(n * pitch, 1)), nullptr};
   owned.push_back(pool[0]);
   if (gz) {
@@ -2211,9 +2214,30 @@ static int encode_var(zgpu_ctx *C, const Chain &c, uint32_t nd, const uint64_t *
   uint32_t *sym = nullptr;
   uint8_t *zscr = nullptr;
   uint64_t in_size = nelem * c.es;  // the current stage's input bound
+  bool var_len = false;             // an earlier stage made the lengths variable
   for (size_t i = 0; i < c.b2b.size(); i++) {
     const Codec &k = c.b2b[i];
     const uint64_t stage_in = in_size;
+    if (k.kind == CodecKind::Blosc) {
+      // BloscCodec::encode (blosc_codec_via_blosc_src.rs:113-128): lz4 / lz4hc / zstd streams on the GPU
+      const uint32_t comp = (k.cname == "lz4" || k.cname == "lz4hc") ? (uint32_t)BL_COMP_LZ4
+                            : k.cname == "zstd"                       ? (uint32_t)BL_COMP_ZSTD
+                                                                      : UINT32_MAX;
+      if (comp == UINT32_MAX)
+        return set_err(ZGPU_UNSUPPORTED, "encode: blosc cname '" + k.cname + "' (the GPU writes lz4, lz4hc and zstd)");
+      if (var_len) return set_err(ZGPU_UNSUPPORTED, "encode: blosc after a variable-length codec");
+      const uint32_t ts = std::max<uint32_t>(1, k.elementsize);
+      const int sh = k.shuffle >= 0 ? k.shuffle : (k.elementsize > 0 ? 2 : 0);  // zarrs' default (:119-123)
+      const BloscEnc E = blosc_enc_params(comp, (uint32_t)sh, ts, stage_in, k.blocksize);
+      uint8_t *bscr = (uint8_t *)C->dev_alloc(blosc_encode_scratch(E, (uint32_t)n));
+      owned.push_back(bscr);
+      cur ^= 1;
+      HIPCHK(launch_blosc_encode(d_items, d_status, (uint32_t)n, E, pool[cur], pitch, bscr, k.level, s));
+      in_size += 16;
+      var_len = true;
+      continue;
+    }
+    if (k.kind == CodecKind::Gzip || k.kind == CodecKind::Zstd) var_len = true;
     in_size = k.kind == CodecKind::Crc32c ? in_size + 4 : k.kind == CodecKind::Gzip ? gzip_bound(in_size)
               : k.kind == CodecKind::Zstd ? zstd_bound(in_size) : in_size;
     if (k.kind == CodecKind::Crc32c) {
