@@ -927,8 +927,8 @@ class Blosc:
                           f"retrieve_array_subset (c-blosc 1.21 blosc_decompress_ctx) with {threads} threads"}
 
     def host_leg(self, sp):
-        if self.CNAME not in ("lz4", "lz4hc", "zstd"):
-            return None  # blosclz / zlib / snappy streams are not written on the GPU
+        if self.CNAME not in ("blosclz", "lz4", "lz4hc", "zstd"):
+            return None  # zlib / snappy streams are not written on the GPU
         return {"encode": self.encode_leg()}
 
     def encode_leg(self):

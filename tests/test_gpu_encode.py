@@ -108,9 +108,9 @@ def test_encode_round_trip_and_unsupported(ctx, torch_cuda):
     descs = [make_desc((e.data_ptr(), e.numel()), [64] * 3, out_start=s) for e, s in zip(enc, starts)]
     assert ch.decode_batch(descs, out, [128] * 3, enc_device=True) == [0] * 8
     assert torch_cuda.equal(out, x)
-    # blosc with a compressor the GPU does not write (blosclz) is refused loudly
+    # blosc with a compressor the GPU does not write (zlib) is refused loudly
     bl = CodecChain.from_metadata([B("little"), {"name": "blosc", "configuration": {
-        "cname": "blosclz", "clevel": 5, "shuffle": "shuffle", "typesize": 4, "blocksize": 0}}], "float32", 0, ctx)
+        "cname": "zlib", "clevel": 5, "shuffle": "shuffle", "typesize": 4, "blocksize": 0}}], "float32", 0, ctx)
     with pytest.raises(ZgpuError) as ei:
         bl.encode_chunks(x, [64, 64, 64], starts)
     assert ei.value.status == L.UNSUPPORTED
@@ -476,6 +476,8 @@ BLOSC_CHAINS = {
     "zstd_shuffle_f32": ([B("little"), BL("zstd", "shuffle", 4)], "float32"),
     "zstd_bitshuffle_blocks_f32": ([B("little"), BL("zstd", "bitshuffle", 4, blocksize=24000)], "float32"),
     "lz4_shuffle_crc_f32": ([B("little"), BL("lz4", "shuffle", 4), {"name": "crc32c"}], "float32"),
+    "blosclz_shuffle_f32": ([B("little"), BL("blosclz", "shuffle", 4)], "float32"),
+    "blosclz_noshuffle_blocks_f32": ([B("little"), BL("blosclz", "noshuffle", 4, blocksize=100000)], "float32"),
 }
 
 
@@ -534,11 +536,11 @@ def test_blosc_encode_u16_ratio_and_small_chunks(ctx, torch_cuda):
 
 
 def test_blosc_encode_unsupported_cnames(ctx, torch_cuda):
-    """blosclz, zlib and snappy streams are not written on the GPU: UNSUPPORTED, loudly."""
+    """zlib and snappy streams are not written on the GPU: UNSUPPORTED, loudly."""
     from zarrs_amd import CodecChain, ZgpuError
     from zarrs_amd import _lib as L
     x = torch_cuda.zeros([64], dtype=torch_cuda.float32, device="cuda")
-    for cname in ("blosclz", "zlib", "snappy"):
+    for cname in ("zlib", "snappy"):
         ch = CodecChain.from_metadata([B("little"), BL(cname, "shuffle", 4)], "float32", 0, ctx)
         with pytest.raises(ZgpuError) as ei:
             ch.encode_chunks(x, [64], [[0]])

@@ -7,10 +7,11 @@
 //   k_blosc_shuf_enc   one workgroup per (item, block): byte shuffle (shuffle.c shuffle_generic) or
 //                      bitshuffle (bshuf_trans_bit_elem; blocks whose element count is not a multiple
 //                      of 8 stay as they are, format 2) of the block into the staging buffer
-//   k_lz4_encode       one wave per stream: an LZ4 block (greedy LZ77, 64 positions a step, 4-byte
-//                      hash candidates in LDS, 64 KiB window; the last 5 bytes literals and no match
-//                      starting in the last 12, as the LZ4 block format requires), emitted only when
-//                      smaller than the stream
+//   k_lz4_encode       one wave per stream: an LZ4 block or a blosclz stream (greedy LZ77, 64
+//                      positions a step, 4-byte hash candidates in LDS, 64 / 72 KiB window; the last 5
+//                      bytes literals and no match starting in the last 12, as the LZ4 block format
+//                      requires and blosclz's decoder needs: it must end on a literal run), emitted
+//                      only when smaller than the stream
 //   zstd streams       k_zstd_encode_seg + k_zstd_frame over the stream table (zstd_enc.hip)
 //   k_blosc_layout_enc one thread per item: every stream's offset in the frame (stored streams
 //                      where compression did not help), a memcpyed frame when nothing is gained
@@ -27,6 +28,7 @@ namespace {
 constexpr uint32_t LZ4E_HBITS = 12, LZ4E_HSIZE = 1u << LZ4E_HBITS;
 constexpr uint32_t LZ4E_CAP1 = 32;        // per-lane match search; longer chosen matches: the wave
 constexpr uint32_t LZ4E_MAXOFF = 65535;   // 2-byte offsets
+constexpr uint32_t BLZ_MAXOFF = 8191 + 65536;  // blosclz: 13-bit near distances, 16-bit far ones above 8191
 constexpr uint32_t LZ4E_LAST = 5;         // LASTLITERALS
 constexpr uint32_t LZ4E_MFLIMIT = 12;     // no match starts in the last 12 bytes
 
@@ -43,6 +45,15 @@ __device__ __forceinline__ uint32_t ld4u(const uint8_t *p) {
 inline uint64_t zbound(uint64_t n) { return n + 4 + 14 + 4 + 3 * ((n + 999) / 1000); }
 
 __device__ __forceinline__ uint32_t lz4_extra(uint32_t v) { return v >= 15 ? (v - 15) / 255 + 1 : 0u; }
+
+// blosclz (c-blosc blosclz.c, the FastLZ level-2 format): literal runs of 1..32 bytes behind a
+// control byte run-1; a match: control (len-2) << 5 | distance-1 >> 8 (len 3..8; 7 << 5 and 255-terminated
+// extension bytes for longer ones), then the distance's low byte; distances above 8191 use the
+// reserved low byte 255 under high bits 31 and two big-endian bytes of distance - 8192.
+__device__ __forceinline__ uint32_t blz_match_size(uint32_t L, uint32_t dist) {
+  const uint32_t ext = L - 2 < 7 ? 0u : (L - 9) / 255 + 1;
+  return 1 + ext + 1 + (dist - 1 >= 8191 ? 2u : 0u);
+}
 
 // stream s of an item: (offset in the item, length)
 __device__ __forceinline__ void stream_range(const BloscEnc &E, uint32_t s, uint64_t &off, uint32_t &len) {
@@ -105,6 +116,7 @@ struct Lz4Smem {
 
 // One LZ4 block per stream: out_len[s] = compressed length, or ~0 when it would not be smaller
 // (stored). scratch per wave: 3 u32 per possible sequence (match start, length, offset).
+template <bool BLZ>
 __global__ __launch_bounds__(64) void k_lz4_encode(const uint32_t *status, uint32_t n_items, BloscEnc E,
                                                    const uint8_t *staging, uint8_t *outs, uint64_t out_pitch,
                                                    uint32_t *out_len, uint32_t *scratch, uint64_t seq_cap) {
@@ -137,7 +149,7 @@ __global__ __launch_bounds__(64) void k_lz4_encode(const uint32_t *status, uint3
       uint32_t mlen = 0, cand = 0;
       if (hvv && p >= skip && p < mlast) {
         cand = hvv - 1;
-        if (p - cand <= LZ4E_MAXOFF && ld4u(in + cand) == w4) {
+        if (p - cand <= (BLZ ? BLZ_MAXOFF : LZ4E_MAXOFF) && ld4u(in + cand) == w4) {
           const uint32_t lim = min(LZ4E_CAP1, m - LZ4E_LAST - p);
           uint32_t k = 4;
           while (k < lim && in[p + k] == in[cand + k]) k++;
@@ -192,11 +204,9 @@ __global__ __launch_bounds__(64) void k_lz4_encode(const uint32_t *status, uint3
     // sequence of literals only
     auto seq_size = [&](uint32_t k, uint32_t &lit0, uint32_t &ll) -> uint32_t {
       lit0 = k ? ms[k - 1] + ml[k - 1] : 0u;
-      if (k == ns) {
-        ll = m - lit0;
-        return 1 + lz4_extra(ll) + ll;
-      }
-      ll = ms[k] - lit0;
+      ll = (k == ns ? m : ms[k]) - lit0;
+      if (BLZ) return (ll + 31) / 32 + ll + (k == ns ? 0u : blz_match_size(ml[k], mo[k]));
+      if (k == ns) return 1 + lz4_extra(ll) + ll;
       return 1 + lz4_extra(ll) + ll + 2 + lz4_extra(ml[k] - 4);
     };
     uint32_t total = 0;
@@ -221,7 +231,36 @@ __global__ __launch_bounds__(64) void k_lz4_encode(const uint32_t *status, uint3
         if ((int)lane >= o) incl += u;
       }
       const uint32_t tot = __shfl(incl, 63, 64);
-      if (k <= ns) {
+      if (BLZ && k <= ns) {
+        uint8_t *o = out + obase + incl - sz;
+        for (uint32_t q = 0; q < ll; q += 32) {  // literal runs of <= 32 bytes
+          const uint32_t r = min(32u, ll - q);
+          *o++ = (uint8_t)(r - 1);
+          for (uint32_t t = 0; t < r; t++) o[t] = in[lit0 + q + t];
+          o += r;
+        }
+        if (k < ns) {
+          const uint32_t L = ml[k], d = mo[k] - 1;
+          const bool far = d >= 8191;
+          const uint32_t hi = far ? 31u : d >> 8;
+          if (L - 2 < 7) {
+            *o++ = (uint8_t)(((L - 2) << 5) | hi);
+          } else {
+            *o++ = (uint8_t)((7u << 5) | hi);
+            uint32_t r = L - 9;
+            for (; r >= 255; r -= 255) *o++ = 255;
+            *o++ = (uint8_t)r;
+          }
+          if (far) {
+            const uint32_t f = mo[k] - 8192;
+            *o++ = 255;
+            *o++ = (uint8_t)(f >> 8);
+            *o++ = (uint8_t)f;
+          } else {
+            *o++ = (uint8_t)d;
+          }
+        }
+      } else if (k <= ns) {
         uint8_t *o = out + obase + incl - sz;
         const uint32_t mm = k < ns ? ml[k] - 4 : 0u;
         *o++ = (uint8_t)((min(ll, 15u) << 4) | (k < ns ? min(mm, 15u) : 0u));
@@ -374,7 +413,8 @@ BloscEnc blosc_enc_params(uint32_t comp, uint32_t shuffle, uint32_t ts, uint64_t
   E.nblk = (uint32_t)(nbytes ? (nbytes + bs - 1) / bs : 0);
   // split the byte-shuffled planes into streams of their own (c-blosc's forward-compatible rule for
   // its LZ compressors); zstd streams stay whole
-  E.nsplit = (E.shuffle == 1 && comp == BL_COMP_LZ4 && E.ts <= 16 && bs % E.ts == 0) ? E.ts : 1u;
+  E.nsplit = (E.shuffle == 1 && (comp == BL_COMP_LZ4 || comp == BL_COMP_BLOSCLZ) && E.ts <= 16 && bs % E.ts == 0)
+                 ? E.ts : 1u;
   const uint32_t nfull = (uint32_t)(nbytes / bs);
   E.spi = nfull * E.nsplit + ((nbytes % bs) ? 1u : 0u);
   E.ne_max = std::max<uint64_t>(bs / E.nsplit, nbytes % bs);
@@ -386,7 +426,7 @@ uint64_t blosc_encode_scratch(const BloscEnc &E, uint32_t n_items) {
   uint64_t b = (uint64_t)n_items * E.nbytes + 256;      // staging
   b += ns * (8 + 8 + 4 + 4) + 1024;                       // soff, cptr, clen, zstatus
   b += (uint64_t)n_items * 8 + 256;                       // ftot
-  if (E.comp == BL_COMP_LZ4) {
+  if (E.comp == BL_COMP_LZ4 || E.comp == BL_COMP_BLOSCLZ) {
     const uint64_t grid = std::min<uint64_t>(std::max<uint64_t>(ns, 1), (uint64_t)device_cu_count() * 8);
     b += ns * ((E.ne_max + 255) & ~255ull);                // compressed streams
     b += grid * (E.ne_max / 4 + 2) * 12 + 256;             // sequence records
@@ -420,14 +460,18 @@ hipError_t launch_blosc_encode(ZgItem *items, uint32_t *status, uint32_t n_items
   const uint8_t *cdata = nullptr;
   uint64_t cpitch = 0;
   const uint64_t *cp = nullptr;
-  if (ns && E.comp == BL_COMP_LZ4) {
+  if (ns && (E.comp == BL_COMP_LZ4 || E.comp == BL_COMP_BLOSCLZ)) {
     cpitch = (E.ne_max + 255) & ~255ull;
     uint8_t *outs = take(ns * cpitch);
     const uint32_t grid = (uint32_t)std::min<uint64_t>(ns, (uint64_t)device_cu_count() * 8);
     const uint64_t seq_cap = E.ne_max / 4 + 2;
     uint32_t *seqs = (uint32_t *)take((uint64_t)grid * seq_cap * 12);
-    hipLaunchKernelGGL(k_lz4_encode, dim3(grid), dim3(64), 0, s, status, n_items, E, staging, outs, cpitch, clen,
-                       seqs, seq_cap);
+    if (E.comp == BL_COMP_BLOSCLZ)
+      hipLaunchKernelGGL(k_lz4_encode<true>, dim3(grid), dim3(64), 0, s, status, n_items, E, staging, outs, cpitch,
+                         clen, seqs, seq_cap);
+    else
+      hipLaunchKernelGGL(k_lz4_encode<false>, dim3(grid), dim3(64), 0, s, status, n_items, E, staging, outs, cpitch,
+                         clen, seqs, seq_cap);
     cdata = outs;
   } else if (ns) {
     const uint64_t zp = ((ZE_HDR + zbound(E.ne_max) + 64 + 255) & ~255ull);
