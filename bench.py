@@ -927,8 +927,8 @@ class Blosc:
                           f"retrieve_array_subset (c-blosc 1.21 blosc_decompress_ctx) with {threads} threads"}
 
     def host_leg(self, sp):
-        if self.CNAME not in ("blosclz", "lz4", "lz4hc", "zstd"):
-            return None  # zlib / snappy streams are not written on the GPU
+        if self.CNAME not in ("blosclz", "lz4", "lz4hc", "zlib", "zstd"):
+            return None  # snappy streams are not written on the GPU
         return {"encode": self.encode_leg()}
 
     def encode_leg(self):
@@ -988,8 +988,14 @@ class BloscLZ(Blosc):
     CNAME = "blosclz"
 
 
+class BloscZlib(Blosc):
+    """Same volume, blosc{zlib, clevel 5, shuffle}: DEFLATE streams (k_gzip's decoder in its RFC 1950
+    mode + k_adler32_check; the encoder's zlib mode)."""
+    CNAME = "zlib"
+
+
 WORKLOADS = {"c1": C1, "c2": C2, "c3": C3, "c5": C5, "blosc": Blosc, "blosc-zstd": BloscZstd,
-             "blosc-blosclz": BloscLZ}
+             "blosc-blosclz": BloscLZ, "blosc-zlib": BloscZlib}
 
 
 def _time_reps(fn, seconds):

@@ -478,13 +478,16 @@ BLOSC_CHAINS = {
     "lz4_shuffle_crc_f32": ([B("little"), BL("lz4", "shuffle", 4), {"name": "crc32c"}], "float32"),
     "blosclz_shuffle_f32": ([B("little"), BL("blosclz", "shuffle", 4)], "float32"),
     "blosclz_noshuffle_blocks_f32": ([B("little"), BL("blosclz", "noshuffle", 4, blocksize=100000)], "float32"),
+    "zlib_shuffle_f32": ([B("little"), BL("zlib", "shuffle", 4)], "float32"),
+    "zlib_bitshuffle_blocks_f32": ([B("little"), BL("zlib", "bitshuffle", 4, blocksize=24000)], "float32"),
+    "zlib_noshuffle_crc_f32": ([B("little"), BL("zlib", "noshuffle", 4), {"name": "crc32c"}], "float32"),
 }
 
 
 @pytest.mark.parametrize("name", sorted(BLOSC_CHAINS))
 def test_blosc_encode_decodes_with_c_blosc(ctx, torch_cuda, name):
-    """BloscCodec::encode on the GPU (blosc_enc.hip: shuffle / bitshuffle, lz4 or zstd streams,
-    stored streams and memcpyed frames where compression does not help): every frame decodes
+    """BloscCodec::encode on the GPU (blosc_enc.hip: shuffle / bitshuffle, blosclz / lz4 / zlib / zstd streams,
+    zlib / zstd / blosclz streams, stored streams and memcpyed frames where compression does not help): every frame decodes
     through the oracle (c-blosc 1.21, the library zarrs' blosc codec wraps) to the exact chunk, and
     back through the GPU decoder. Block sizes that leave a short last block exercise split and
     unsplit blocks and bitshuffle's unshuffled tail."""
@@ -536,11 +539,11 @@ def test_blosc_encode_u16_ratio_and_small_chunks(ctx, torch_cuda):
 
 
 def test_blosc_encode_unsupported_cnames(ctx, torch_cuda):
-    """zlib and snappy streams are not written on the GPU: UNSUPPORTED, loudly."""
+    """snappy streams are not written on the GPU: UNSUPPORTED, loudly."""
     from zarrs_amd import CodecChain, ZgpuError
     from zarrs_amd import _lib as L
     x = torch_cuda.zeros([64], dtype=torch_cuda.float32, device="cuda")
-    for cname in ("zlib", "snappy"):
+    for cname in ("snappy",):
         ch = CodecChain.from_metadata([B("little"), BL(cname, "shuffle", 4)], "float32", 0, ctx)
         with pytest.raises(ZgpuError) as ei:
             ch.encode_chunks(x, [64], [[0]])

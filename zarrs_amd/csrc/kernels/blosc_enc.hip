@@ -13,6 +13,7 @@
 //                      requires and blosclz's decoder needs: it must end on a literal run), emitted
 //                      only when smaller than the stream
 //   zstd streams       k_zstd_encode_seg + k_zstd_frame over the stream table (zstd_enc.hip)
+//   zlib streams       k_gzip_encode in its zlib mode over the stream table (deflate_enc.hip)
 //   k_blosc_layout_enc one thread per item: every stream's offset in the frame (stored streams
 //                      where compression did not help), a memcpyed frame when nothing is gained
 //   k_blosc_write_enc  one workgroup per stream: its {csize, payload} (the header and a block's
@@ -397,6 +398,10 @@ __global__ void k_blosc_zlens(const ZgItem *zitems, const uint32_t *zstatus, uin
   clen[sg] = ok ? (uint32_t)min<uint64_t>(zitems[sg].len, 0xFFFFFFFEull) : 0xFFFFFFFFu;
 }
 
+// a zlib stream's slot: the member offset, the stream and deflate's worst case (stored blocks: 5 bytes
+// per block of at most 16384 symbols), the trailer
+static uint64_t zlib_pitch(uint64_t n) { return (GZE_HDR + n + 5 * (n / 1024 + 2) + 64 + 255) & ~255ull; }
+
 BloscEnc blosc_enc_params(uint32_t comp, uint32_t shuffle, uint32_t ts, uint64_t nbytes, uint64_t blocksize) {
   BloscEnc E{};
   E.comp = comp;
@@ -430,6 +435,9 @@ uint64_t blosc_encode_scratch(const BloscEnc &E, uint32_t n_items) {
     const uint64_t grid = std::min<uint64_t>(std::max<uint64_t>(ns, 1), (uint64_t)device_cu_count() * 8);
     b += ns * ((E.ne_max + 255) & ~255ull);                // compressed streams
     b += grid * (E.ne_max / 4 + 2) * 12 + 256;             // sequence records
+  } else if (E.comp == BL_COMP_ZLIB) {
+    b += ns * zlib_pitch(E.ne_max) + ns * sizeof(ZgItem) + 256;
+    b += (uint64_t)gzip_encode_grid((uint32_t)std::max<uint64_t>(ns, 1)) * GZE_BLK_SYMS * 4 + 256;
   } else {
     const uint64_t zp = ((ZE_HDR + zbound(E.ne_max) + 64 + 255) & ~255ull);
     b += ns * zp + ns * sizeof(ZgItem) + 256;
@@ -441,7 +449,6 @@ uint64_t blosc_encode_scratch(const BloscEnc &E, uint32_t n_items) {
 hipError_t launch_blosc_encode(ZgItem *items, uint32_t *status, uint32_t n_items, const BloscEnc &E, uint8_t *slots,
                                uint64_t slot_bytes, uint8_t *scratch, int zlevel, hipStream_t s) {
   if (!n_items) return hipSuccess;
-  (void)zlevel;
   const uint64_t ns = (uint64_t)n_items * E.spi;
   uint8_t *p = scratch;
   auto take = [&](uint64_t bytes) {
@@ -473,6 +480,18 @@ hipError_t launch_blosc_encode(ZgItem *items, uint32_t *status, uint32_t n_items
       hipLaunchKernelGGL(k_lz4_encode<false>, dim3(grid), dim3(64), 0, s, status, n_items, E, staging, outs, cpitch,
                          clen, seqs, seq_cap);
     cdata = outs;
+  } else if (ns && E.comp == BL_COMP_ZLIB) {
+    const uint64_t zp = zlib_pitch(E.ne_max);
+    uint8_t *zslots = take(ns * zp);
+    ZgItem *zitems = (ZgItem *)take(ns * sizeof(ZgItem));
+    uint32_t *sym = (uint32_t *)take((uint64_t)gzip_encode_grid((uint32_t)ns) * GZE_BLK_SYMS * 4);
+    hipLaunchKernelGGL(k_blosc_zitems, dim3((uint32_t)((ns + 255) / 256)), dim3(256), 0, s, status, n_items, E,
+                       staging, zitems, zstatus);
+    hipError_t e = launch_gzip_encode(zitems, zstatus, (uint32_t)ns, zslots, zp, sym, zlevel, s, true);
+    if (e != hipSuccess) return e;
+    hipLaunchKernelGGL(k_blosc_zlens, dim3((uint32_t)((ns + 255) / 256)), dim3(256), 0, s, zitems, zstatus, ns, cptr,
+                       clen);
+    cp = cptr;
   } else if (ns) {
     const uint64_t zp = ((ZE_HDR + zbound(E.ne_max) + 64 + 255) & ~255ull);
     uint8_t *zslots = take(ns * zp);

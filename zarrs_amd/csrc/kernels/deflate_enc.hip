@@ -333,11 +333,48 @@ __device__ void emit_block(GzeSmem &S, BitOut &B, const uint32_t *syms, uint32_t
 
 }  // namespace
 
+// Adler-32 (RFC 1950) of in[0, n) on one wave: byte j adds b to s1 and (n - j) b to s2, so the lanes
+// sum coalesced dwords in any order and the wave adds their residues (s1 = 1 + sum, s2 = n + sum).
+__device__ uint32_t wave_adler32(const uint8_t *in, uint32_t n) {
+  constexpr uint32_t M = 65521;
+  const uint32_t lane = threadIdx.x;
+  uint64_t A = 0, Bs = 0;
+  uint32_t it = 0;
+  for (uint32_t base = 0; base < n; base += 256) {
+    const uint32_t j0 = base + 4 * lane;
+    if (j0 < n) {
+      const uint32_t w = j0 + 4 <= n ? ld4(in + j0) : 0u;
+#pragma unroll
+      for (uint32_t k = 0; k < 4; k++) {
+        const uint32_t j = j0 + k;
+        const uint32_t b = j0 + 4 <= n ? (w >> (8 * k)) & 0xff : (j < n ? in[j] : 0u);
+        A += b;
+        Bs += (uint64_t)(n - j) * b;
+      }
+    }
+    if (++it == 4096) {  // per lane <= 16384 bytes between reductions: Bs < 2^53
+      A %= M;
+      Bs %= M;
+      it = 0;
+    }
+  }
+  uint32_t a = (uint32_t)(A % M), b = (uint32_t)(Bs % M);
+#pragma unroll
+  for (int o = 32; o; o >>= 1) {
+    a += __shfl_xor(a, o, 64);
+    b += __shfl_xor(b, o, 64);
+  }
+  const uint32_t s1 = (1u + a) % M, s2 = (n % M + b) % M;
+  return (s2 << 16) | s1;
+}
+
 // items[i] {src,len} -> a gzip member in slot i at GZE_HDR; items rewritten to it. sym: grid * 16384
 // u32 symbol records (one block's worth per wave). xfl: the header's XFL byte (flate2: 4 for level <= 1,
-// 2 for level >= 9, else 0).
+// 2 for level >= 9, else 0). zhdr != 0: a zlib stream (RFC 1950) instead, CMF FLG = zhdr, at slot i +
+// GZE_HDR + 8 (the same bit stream position), with the Adler-32 trailer (blosc's zlib streams).
 __global__ __launch_bounds__(64) void k_gzip_encode(ZgItem *items, uint32_t *status, uint32_t n_items, uint8_t *slots,
-                                                    uint64_t slot_bytes, uint32_t *sym_scratch, uint32_t xfl) {
+                                                    uint64_t slot_bytes, uint32_t *sym_scratch, uint32_t xfl,
+                                                    uint32_t zhdr) {
   __shared__ GzeSmem S;
   const uint32_t lane = threadIdx.x;
   uint32_t *syms = sym_scratch + (uint64_t)blockIdx.x * GZE_BLK_SYMS;
@@ -351,15 +388,22 @@ __global__ __launch_bounds__(64) void k_gzip_encode(ZgItem *items, uint32_t *sta
     }
     const uint8_t *in = (const uint8_t *)it.src;
     const uint32_t n = (uint32_t)it.len;
-    // 1. CRC-32 of the input (tables in the hash table's space)
-    build_tables(S.crc, POLY_CRC32);
-    const uint32_t crc = wg_crc(in, n, S.crc, POLY_CRC32, S.s_len, S.s_crc);
+    // 1. CRC-32 of the input (tables in the hash table's space), or Adler-32 for zlib
+    uint32_t crc;
+    if (zhdr) {
+      crc = wave_adler32(in, n);
+    } else {
+      build_tables(S.crc, POLY_CRC32);
+      crc = wg_crc(in, n, S.crc, POLY_CRC32, S.s_len, S.s_crc);
+    }
     WSYNC();
     for (uint32_t k = lane; k < GZE_HSIZE / 2; k += 64) ((uint32_t *)S.head)[k] = 0;
     for (uint32_t s = lane; s < 288; s += 64) S.lfreq[s] = 0;
     if (lane < 32) S.dfreq[lane] = 0;
     for (uint32_t k = lane; k < GZE_BB + 4; k += 64) S.bits[k] = 0;
-    if (lane < 10)  // ID1 ID2 CM=deflate FLG=0 MTIME=0 XFL OS=255 (flate2's GzBuilder defaults)
+    if (zhdr) {
+      if (lane < 2) slot[GZE_HDR + 8 + lane] = (uint8_t)(lane == 0 ? zhdr >> 8 : zhdr);
+    } else if (lane < 10)  // ID1 ID2 CM=deflate FLG=0 MTIME=0 XFL OS=255 (flate2's GzBuilder defaults)
       slot[GZE_HDR + lane] = lane == 0 ? 0x1f : lane == 1 ? 0x8b : lane == 2 ? 8 : lane == 8 ? (uint8_t)xfl : lane == 9 ? 255 : 0;
     WSYNC();
     BitOut B{0, 0, (uint32_t *)(slot + GZE_HDR + 10), (uint32_t)((slot_bytes - GZE_HDR - 10) / 4), 0};
@@ -452,19 +496,23 @@ __global__ __launch_bounds__(64) void k_gzip_encode(ZgItem *items, uint32_t *sta
       put(S, B, 1, 2);
       put(S, B, 0, 7);
     }
-    // 4. trailer: CRC-32 and ISIZE, byte-aligned
+    // 4. trailer: CRC-32 and ISIZE, or the big-endian Adler-32; byte-aligned
     maybe_flush(S, B);
     B.bitpos = (B.bitpos + 7) & ~7u;
-    put(S, B, crc, 32);
-    put(S, B, n, 32);
+    if (zhdr) {
+      put(S, B, __builtin_bswap32(crc), 32);
+    } else {
+      put(S, B, crc, 32);
+      put(S, B, n, 32);
+    }
     const uint64_t total_bits = (uint64_t)B.outw * 32 + B.bitpos;
     flush(S, B, true);
     if (lane == 0) {
       if (B.ovf) {
         status[item] = ZG_DECODED_SIZE_MISMATCH;
       } else {
-        items[item].src = (uint64_t)(slot + GZE_HDR);
-        items[item].len = 10 + total_bits / 8;
+        items[item].src = (uint64_t)(slot + GZE_HDR + (zhdr ? 8 : 0));
+        items[item].len = (zhdr ? 2 : 10) + total_bits / 8;
       }
     }
     WSYNC();
@@ -476,11 +524,17 @@ uint32_t gzip_encode_grid(uint32_t n_items) {
 }
 
 hipError_t launch_gzip_encode(ZgItem *items, uint32_t *status, uint32_t n_items, uint8_t *slots, uint64_t slot_bytes,
-                              uint32_t *sym_scratch, int level, hipStream_t s) {
+                              uint32_t *sym_scratch, int level, hipStream_t s, bool zlib) {
   if (!n_items) return hipSuccess;
   const uint32_t xfl = level <= 1 ? 4u : level >= 9 ? 2u : 0u;
+  uint32_t zhdr = 0;
+  if (zlib) {  // CMF 0x78 (deflate, 32 KiB window), FLEVEL as zlib's deflate sets it, FCHECK
+    const uint32_t flevel = level < 0 ? 2u : level < 2 ? 0u : level < 6 ? 1u : level == 6 ? 2u : 3u;
+    zhdr = 0x7800u | (flevel << 6);
+    zhdr |= (31u - zhdr % 31u) % 31u;
+  }
   hipLaunchKernelGGL(k_gzip_encode, dim3(gzip_encode_grid(n_items)), dim3(64), 0, s, items, status, n_items, slots,
-                     slot_bytes, sym_scratch, xfl);
+                     slot_bytes, sym_scratch, xfl, zhdr);
   return hipGetLastError();
 }
 

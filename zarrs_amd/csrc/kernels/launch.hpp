@@ -144,12 +144,13 @@ hipError_t launch_shard_encode(const uint64_t *starts, const uint8_t *array, con
 // ---- variable-length write path (compressing chains) ----
 // gzip member encode (deflate_enc.hip): item i's bytes -> a member written at slot i + GZE_HDR (the
 // headroom takes crc32c codecs located at the start), items rewritten to it. sym_scratch holds
-// gzip_encode_grid(n) * GZE_BLK_SYMS u32 symbol records.
+// gzip_encode_grid(n) * GZE_BLK_SYMS u32 symbol records. zlib: a zlib stream (RFC 1950, Adler-32
+// trailer) at slot i + GZE_HDR + 8 instead of a gzip member (blosc's zlib streams).
 constexpr uint32_t GZE_BLK_SYMS = 16384;  // symbols per DEFLATE block
 constexpr uint64_t GZE_HDR = 62;          // member offset in a slot (its bit stream then starts word-aligned)
 uint32_t gzip_encode_grid(uint32_t n_items);
 hipError_t launch_gzip_encode(ZgItem *items, uint32_t *status, uint32_t n_items, uint8_t *slots, uint64_t slot_bytes,
-                              uint32_t *sym_scratch, int level, hipStream_t s);
+                              uint32_t *sym_scratch, int level, hipStream_t s, bool zlib = false);
 // zstd frame encode (zstd_enc.hip): item i's bytes (at most max_len) -> one single-segment frame at
 // slot i + ZE_HDR, items rewritten to it; the work is cut into 1 MiB segments, one wave each.
 // scratch: zstd_encode_scratch(n_items, max_len) bytes
@@ -237,7 +238,8 @@ hipError_t launch_blosc_decode(ZgItem *items, uint32_t *status, uint32_t n_items
                                const BlDecode &D, uint8_t *dst, uint64_t slot_bytes, hipStream_t s);
 
 // blosc encode (blosc_enc.hip): item i's nbytes -> one c-blosc 1.x frame at slot i + BLE_HDR, items
-// rewritten to it. comp: BL_COMP_LZ4 (lz4 / lz4hc streams) or BL_COMP_ZSTD; shuffle 0 / 1 byte / 2 bit
+// rewritten to it. comp: BL_COMP_BLOSCLZ, BL_COMP_LZ4 (lz4 / lz4hc streams), BL_COMP_ZLIB or BL_COMP_ZSTD;
+// shuffle 0 / 1 byte / 2 bit
 constexpr uint64_t BLE_HDR = 64;
 struct BloscEnc {
   uint32_t comp, shuffle, ts, nsplit, nblk, spi;  // spi: streams per item

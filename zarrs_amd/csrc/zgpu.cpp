@@ -2219,14 +2219,16 @@ static int encode_var(zgpu_ctx *C, const Chain &c, uint32_t nd, const uint64_t *
     const Codec &k = c.b2b[i];
     const uint64_t stage_in = in_size;
     if (k.kind == CodecKind::Blosc) {
-      // BloscCodec::encode (blosc_codec_via_blosc_src.rs:113-128): lz4 / lz4hc / zstd streams on the GPU
+      // BloscCodec::encode (blosc_codec_via_blosc_src.rs:113-128): blosclz / lz4 / lz4hc / zlib / zstd
+      // streams on the GPU
       const uint32_t comp = (k.cname == "lz4" || k.cname == "lz4hc") ? (uint32_t)BL_COMP_LZ4
                             : k.cname == "zstd"                       ? (uint32_t)BL_COMP_ZSTD
                             : k.cname == "blosclz"                    ? (uint32_t)BL_COMP_BLOSCLZ
+                            : k.cname == "zlib"                       ? (uint32_t)BL_COMP_ZLIB
                                                                       : UINT32_MAX;
       if (comp == UINT32_MAX)
-        return set_err(ZGPU_UNSUPPORTED,
-                       "encode: blosc cname '" + k.cname + "' (the GPU writes blosclz, lz4, lz4hc and zstd)");
+        return set_err(ZGPU_UNSUPPORTED, "encode: blosc cname '" + k.cname +
+                                             "' (the GPU writes blosclz, lz4, lz4hc, zlib and zstd)");
       if (var_len) return set_err(ZGPU_UNSUPPORTED, "encode: blosc after a variable-length codec");
       const uint32_t ts = std::max<uint32_t>(1, k.elementsize);
       const int sh = k.shuffle >= 0 ? k.shuffle : (k.elementsize > 0 ? 2 : 0);  // zarrs' default (:119-123)
