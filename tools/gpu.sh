@@ -45,7 +45,7 @@ for step in "$@"; do
         python3 bench.py --workload "$a" --no-cpu --no-pmc --no-host-leg --secondary= --steps 5 --warmup 1 "${F[@]}" \
         > "$O/$i.prof_$a.json" 2> "$O/$i.prof_$a.err" || { rc=$?; echo "rocprof rc=$rc"; tail -20 "$O/$i.prof_$a.err"; exit $rc; }
       cat "$O/$i.prof_$a.json"
-      f=$(ls "$O/$i.prof_$a"/*/run_kernel_stats.csv 2>/dev/null | head -1)
+      f=$(ls "$O/$i.prof_$a"/run_kernel_stats.csv "$O/$i.prof_$a"/*/run_kernel_stats.csv 2>/dev/null | head -1)
       [ -n "$f" ] && head -12 "$f" | cut -c1-200 ;;
     pmc)
       F=(${c//,/ })

@@ -230,8 +230,8 @@ __global__ __launch_bounds__(64) void k_blosc_streams(ZgItem *items, uint32_t *s
 #ifndef ZG_LZ_RING
 #define ZG_LZ_RING 4096  // bytes of recent output kept in LDS (0: matches read back from HBM only)
 #endif
-#ifndef ZG_LZW
-#define ZG_LZW (ZG_LZ_RING ? 4096 : 8192)
+#ifndef ZG_LZW  // input window: 1 KiB + the 4 KiB ring = 5 KiB per one-wave workgroup -> 8 waves per SIMD
+#define ZG_LZW (ZG_LZ_RING ? 1024 : 8192)  // (a 4 KiB window: 5 waves, lz4 43.1 -> 35.4 ms: r03s_blosc_lz_window_ab)
 #endif
 constexpr uint32_t LZW = ZG_LZW;
 constexpr uint32_t LZR = ZG_LZ_RING > 0 ? ZG_LZ_RING : 1, LZRM = LZR - 1;
@@ -575,22 +575,25 @@ __global__ __launch_bounds__(256) void k_blosc_finish(const BlBlock *blocks, con
       (c0 & 15) == 0) {
     // u16 / u32 fast path: 16 elements per thread, a 16-B load from each byte plane and ts 16-B
     // stores of the interleaved bytes (the generic loop below moves a byte per lane with two
-    // integer divisions); planes that are not 16-B aligned (stored streams inside the frame) fall
-    // through to the generic loop
+    // integer divisions). Planes stored inside the frame (incompressible byte planes, e.g. noise
+    // low bytes) sit at any address: unaligned 16-B global loads (gfx950 runs in unaligned mode)
     const uint32_t neb = bsize / ts;
-    const uint4 *pl[4];
-    bool al = true;
+    const uint8_t *pl[4];
     for (uint32_t i = 0; i < ts; i++) {
       const uint32_t q = i * neb, j = q / ne;
-      pl[i] = (const uint4 *)((const uint8_t *)src[j] + (q - j * ne));
-      al = al && ((uintptr_t)pl[i] & 15) == 0;
+      pl[i] = (const uint8_t *)src[j] + (q - j * ne);
     }
-    if (al) {
+    auto ldv = [&](uint32_t i, uint32_t v) -> uint4 {
+      uint4 r;
+      __builtin_memcpy(&r, pl[i] + 16ull * v, 16);
+      return r;
+    };
+    {
       // output vector k of the block (16 B, never across a row: rows are 16-B multiples)
       auto o = [&](uint32_t k) -> uint4 & { return *(uint4 *)dptr(16 * k); };
       for (uint32_t v = threadIdx.x; v < neb / 16; v += 256) {
         if (ts == 2) {
-          const uint4 a = pl[0][v], b = pl[1][v];
+          const uint4 a = ldv(0, v), b = ldv(1, v);
           const uint32_t aw[4] = {a.x, a.y, a.z, a.w}, bw[4] = {b.x, b.y, b.z, b.w};
           uint32_t r[8];
 #pragma unroll
@@ -602,7 +605,7 @@ __global__ __launch_bounds__(256) void k_blosc_finish(const BlBlock *blocks, con
           o(2 * v) = make_uint4(r[0], r[1], r[2], r[3]);
           o(2 * v + 1) = make_uint4(r[4], r[5], r[6], r[7]);
         } else {
-          const uint4 p0 = pl[0][v], p1 = pl[1][v], p2 = pl[2][v], p3 = pl[3][v];
+          const uint4 p0 = ldv(0, v), p1 = ldv(1, v), p2 = ldv(2, v), p3 = ldv(3, v);
           const uint32_t w0[4] = {p0.x, p0.y, p0.z, p0.w}, w1[4] = {p1.x, p1.y, p1.z, p1.w},
                          w2[4] = {p2.x, p2.y, p2.z, p2.w}, w3[4] = {p3.x, p3.y, p3.z, p3.w};
 #pragma unroll

@@ -58,31 +58,42 @@ hipError_t launch_crc32c_strip(ZgItem *items, uint32_t *status, uint32_t n_items
 }
 
 // ------------------------------- Adler-32 (zlib trailer) ---------------------------------------
-// RFC 1950: s1 = 1 + sum b_j, s2 = sum of the running s1 = n + sum (n - j) b_j (mod 65521). Each
-// thread runs the serial recurrence over one contiguous segment [a, e) (A = sum b, B = sum (e - j) b),
-// reducing every NMAX bytes as zlib does; segments combine as s1 += A, s2 += B + (n - e) A.
+// RFC 1950: s1 = 1 + sum b_j, s2 = sum of the running s1 = n + sum (n - j) b_j (mod 65521). Both sums
+// are linear in the bytes, so the threads take coalesced 4-byte words in any order (byte j adds b to A
+// and (n - j) b to B), reduce their residues every 4096 words, and the workgroup adds them.
 __global__ __launch_bounds__(CRC_THREADS) void k_adler32_check(const ZgItem *items, uint32_t *status,
                                                                const uint32_t *kind, const uint2 *aux) {
-  constexpr uint32_t M = 65521, NMAX = 5552;
+  constexpr uint32_t M = 65521;
   __shared__ uint32_t s1s[CRC_THREADS], s2s[CRC_THREADS];
   const uint32_t i = blockIdx.x, t = threadIdx.x;
   if (kind[i] != BL_KIND_ZLIB || status[i] != 0) return;
   const ZgItem it = items[i];
   const uint8_t *p = (const uint8_t *)it.src;
-  const uint64_t n = it.len, L = (n + CRC_THREADS - 1) / CRC_THREADS;
-  const uint64_t a = min<uint64_t>((uint64_t)t * L, n), e = min<uint64_t>(a + L, n);
-  uint32_t A = 0, B = 0;
-  for (uint64_t j = a; j < e;) {
-    const uint64_t k = min<uint64_t>(e, j + NMAX);
-    for (; j < k; j++) {
-      A += p[j];
-      B += A;
+  const uint64_t n = it.len;
+  uint64_t A = 0, B = 0;
+  uint32_t cnt = 0;
+  for (uint64_t j0 = 4ull * t; j0 < n; j0 += 4ull * CRC_THREADS) {
+    uint32_t w;
+    if (j0 + 4 <= n) {
+      __builtin_memcpy(&w, p + j0, 4);  // unaligned dword (gfx950 runs in unaligned mode)
+    } else {
+      w = 0;
+      for (uint32_t k = 0; j0 + k < n; k++) w |= (uint32_t)p[j0 + k] << (8 * k);
     }
-    A %= M;
-    B %= M;
+#pragma unroll
+    for (uint32_t k = 0; k < 4; k++) {  // bytes past n are 0 and add nothing
+      const uint32_t b = (w >> (8 * k)) & 0xffu;
+      A += b;
+      B += (n - j0 - k) * b;  // blosc streams are < 2^31 bytes
+    }
+    if (++cnt == 4096) {  // B < 4096 * 4 * 2^32 * 255 < 2^56 between reductions
+      A %= M;
+      B %= M;
+      cnt = 0;
+    }
   }
-  s1s[t] = A;
-  s2s[t] = (uint32_t)((B + (uint64_t)((n - e) % M) * A) % M);
+  s1s[t] = (uint32_t)(A % M);
+  s2s[t] = (uint32_t)(B % M);
   __syncthreads();
   if (t == 0) {
     uint64_t s1 = 1, s2 = n % M;
