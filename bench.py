@@ -843,13 +843,14 @@ class Blosc:
     library), decoded on the GPU from HBM; per-rank chunk partition, no collective."""
     SHAPE, CHUNK = [1024, 2048, 1024], [64, 256, 256]
     CNAME = "lz4"
+    SHUFFLE = "shuffle"
     kernel = "blosc decode step (k_blosc_info/streams, stream decoders, k_blosc_finish, k_scatter_rows)"
     pmc_regex = "k_blosc|k_lz4|k_zstd|k_scatter"
     dtype = "u16"
 
     def codecs(self):
         return [{"name": "bytes", "configuration": {"endian": "little"}},
-                {"name": "blosc", "configuration": {"cname": self.CNAME, "clevel": 5, "shuffle": "shuffle",
+                {"name": "blosc", "configuration": {"cname": self.CNAME, "clevel": 5, "shuffle": self.SHUFFLE,
                                                     "typesize": 2, "blocksize": 0}}]
 
     def __init__(self, args, rank, world, dev):
@@ -890,7 +891,8 @@ class Blosc:
         self.step_bytes = self.decoded_bytes * world
         enc_total = sum(len(e) for e in self.enc_host)
         self.config = {"workload": f"blosc: u16 volume {shape} per GPU, chunks {cs}, [bytes, blosc{{{self.CNAME}, "
-                                   "clevel 5, shuffle, typesize 2, blocksize auto}] (numcodecs Blosc defaults)",
+                                   f"clevel 5, {self.SHUFFLE}, typesize 2, blocksize auto}}]"
+                                   + (" (numcodecs Blosc defaults)" if self.SHUFFLE == "shuffle" else ""),
                        "chunks_per_gpu": len(idxs), "blosc_ratio": round(self.decoded_bytes / enc_total, 3),
                        "parallelism": f"chunk-partitioned x{world}"}
         self.data = ("synthetic (100 + 900|sin z cos y sin x| + sqrt-scaled N(0,1) noise, u16, seed 42; "
@@ -994,8 +996,15 @@ class BloscZlib(Blosc):
     CNAME = "zlib"
 
 
+class BloscBit(Blosc):
+    """Same volume, blosc{lz4, clevel 5, bitshuffle}: the bit-transposed layout (zarrs' BloscCodec
+    default shuffle when a typesize is set; k_blosc_finish's bit-transpose path)."""
+    SHUFFLE = "bitshuffle"
+
+
 WORKLOADS = {"c1": C1, "c2": C2, "c3": C3, "c5": C5, "blosc": Blosc, "blosc-zstd": BloscZstd,
-             "blosc-blosclz": BloscLZ, "blosc-zlib": BloscZlib}
+             "blosc-blosclz": BloscLZ, "blosc-zlib": BloscZlib,
+             "blosc-bitshuffle": BloscBit}
 
 
 def _time_reps(fn, seconds):

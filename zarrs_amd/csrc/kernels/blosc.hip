@@ -637,20 +637,51 @@ __global__ __launch_bounds__(256) void k_blosc_finish(const BlBlock *blocks, con
   } else if (B.mode == 2 && bsize >= ts) {  // bitunshuffle (bshuf_untrans_bit_elem)
     const uint32_t size = bsize / ts;
     const uint32_t n8 = (B.ver == 2) ? ((size % 8) ? 0u : size) : size - size % 8;
-    const uint32_t body = n8 * ts;
-    for (uint32_t q = threadIdx.x; q < bsize; q += 256) {
-      uint8_t v = 0;
-      if (q < body) {  // element j, byte b: bit k from bit-row b*8+k, column j
-        const uint32_t j = q / ts, b = q - j * ts;
-        for (uint32_t k = 0; k < 8; k++) {
-          const uint64_t bit = (uint64_t)(b * 8 + k) * n8 + j;
-          v |= (uint8_t)(((in((uint32_t)(bit >> 3)) >> (bit & 7)) & 1u) << k);
+    const uint32_t body = n8 * ts, rb = n8 / 8;  // rb: bytes per bit-row
+    // Element j, byte b, bit k is bit j of bit-row 8b + k. A thread takes 8 elements (column byte g
+    // of every row: coalesced across the threads) and per output byte b transposes the 8x8 bit
+    // matrix of rows 8b..8b+7 (three masked swaps of a u64).
+    const uint8_t *s0 = (const uint8_t *)src[0];
+    const bool one = B.nsplit == 1;
+    const bool vec = (ts == 2 || ts == 4) && !direct && ((uintptr_t)out & 15) == 0;
+    for (uint32_t g = threadIdx.x; g < rb; g += 256) {
+      auto row = [&](uint32_t r) -> uint64_t { return one ? s0[r * rb + g] : in(r * rb + g); };
+      uint32_t wd[8];
+      for (uint32_t b = 0; b < ts; b++) {
+        uint64_t x = 0;
+#pragma unroll
+        for (uint32_t k = 0; k < 8; k++) x |= row(8 * b + k) << (8 * k);
+        uint64_t t = (x ^ (x >> 7)) & 0x00AA00AA00AA00AAull;
+        x ^= t ^ (t << 7);
+        t = (x ^ (x >> 14)) & 0x0000CCCC0000CCCCull;
+        x ^= t ^ (t << 14);
+        t = (x ^ (x >> 28)) & 0x00000000F0F0F0F0ull;
+        x ^= t ^ (t << 28);  // byte m: bits of element 8g + m's byte b
+        if (vec) {
+          if (ts == 2) {
+#pragma unroll
+            for (uint32_t w = 0; w < 4; w++) {
+              const uint32_t lo = (uint32_t)(x >> (16 * w)) & 0xffu, hi = (uint32_t)(x >> (16 * w + 8)) & 0xffu;
+              wd[w] = b ? wd[w] | (lo << 8) | (hi << 24) : lo | (hi << 16);
+            }
+          } else {
+#pragma unroll
+            for (uint32_t m = 0; m < 8; m++) {
+              const uint32_t v = ((uint32_t)(x >> (8 * m)) & 0xffu) << (8 * b);
+              wd[m] = b ? wd[m] | v : v;
+            }
+          }
+        } else {
+          for (uint32_t m = 0; m < 8; m++) *dptr((8 * g + m) * ts + b) = (uint8_t)(x >> (8 * m));
         }
-      } else {
-        v = in(q);
       }
-      *dptr(q) = v;
+      if (vec) {
+        uint4 *o4 = (uint4 *)(out + 8ull * g * ts);
+        o4[0] = make_uint4(wd[0], wd[1], wd[2], wd[3]);
+        if (ts == 4) o4[1] = make_uint4(wd[4], wd[5], wd[6], wd[7]);
+      }
     }
+    for (uint32_t q = body + threadIdx.x; q < bsize; q += 256) *dptr(q) = in(q);
   } else {
     for (uint32_t q = threadIdx.x; q < bsize; q += 256) *dptr(q) = in(q);
   }
