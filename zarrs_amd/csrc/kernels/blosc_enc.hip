@@ -92,19 +92,26 @@ __global__ __launch_bounds__(256) void k_blosc_shuf_enc(const ZgItem *items, con
     }
   } else if (E.shuffle == 2 && bsize >= ts) {
     // bit-row r = b*8 + k holds bit k of byte b of every element; element count a multiple of 8
-    const uint32_t size = bsize / ts, n8 = (size % 8) ? 0u : size, body = n8 * ts;
-    for (uint32_t q = threadIdx.x; q < bsize; q += 256) {
-      uint8_t v = 0;
-      if (q < body) {
-        const uint64_t x = (uint64_t)q * 8;
-        const uint32_t r = (uint32_t)(x / n8), j0 = (uint32_t)(x - (uint64_t)r * n8);
-        const uint32_t bb = r >> 3, k = r & 7;
-        for (uint32_t t = 0; t < 8; t++) v |= (uint8_t)(((in[(uint64_t)(j0 + t) * ts + bb] >> k) & 1u) << t);
-      } else {
-        v = in[q];
+    // A thread takes 8 elements (8 ts contiguous input bytes) and per byte b transposes the 8x8 bit
+    // matrix (rows: the elements' byte b) into column byte g of bit-rows 8b..8b+7 (coalesced stores)
+    const uint32_t size = bsize / ts, n8 = (size % 8) ? 0u : size, body = n8 * ts, rb = n8 / 8;
+    for (uint32_t g = threadIdx.x; g < rb; g += 256) {
+      const uint8_t *e = in + 8ull * g * ts;
+      for (uint32_t bb = 0; bb < ts; bb++) {
+        uint64_t x = 0;
+#pragma unroll
+        for (uint32_t m = 0; m < 8; m++) x |= (uint64_t)e[m * ts + bb] << (8 * m);
+        uint64_t t = (x ^ (x >> 7)) & 0x00AA00AA00AA00AAull;
+        x ^= t ^ (t << 7);
+        t = (x ^ (x >> 14)) & 0x0000CCCC0000CCCCull;
+        x ^= t ^ (t << 14);
+        t = (x ^ (x >> 28)) & 0x00000000F0F0F0F0ull;
+        x ^= t ^ (t << 28);  // byte k: bit k of the 8 elements' byte bb
+#pragma unroll
+        for (uint32_t k = 0; k < 8; k++) out[(uint64_t)(8 * bb + k) * rb + g] = (uint8_t)(x >> (8 * k));
       }
-      out[q] = v;
     }
+    for (uint32_t q = body + threadIdx.x; q < bsize; q += 256) out[q] = in[q];
   } else {
     for (uint32_t q = threadIdx.x; q < bsize; q += 256) out[q] = in[q];
   }
