@@ -311,6 +311,130 @@ __device__ __forceinline__ void lz_match(uint8_t *out, uint64_t op, uint64_t off
 
 // LZ4 block format (lz4_Block_format.md): sequences {token, literal length, literals, offset u16,
 // match length}; the last sequence has literals only.
+#ifndef ZG_LZ4_LEAN
+#define ZG_LZ4_LEAN 1
+#endif
+#if ZG_LZ4_LEAN
+// The wave is issue-bound, not latency-bound, at 8 waves per SIMD (PMC on the 4 GiB blosc workload:
+// ~80 SALU + 42 VALU instructions per sequence, 27 % of wave time issuing with 8 waves sharing a
+// SIMD): positions are 32-bit (a blosc stream and its output are < 2 GiB), the window is addressed
+// by its stream offset, and a copy of at most 64 bytes (nearly all of them) is one predicated pass.
+__global__ __launch_bounds__(64) void k_lz4(ZgItem *subs, uint32_t *sub_status, const uint32_t *sub_kind,
+                                            uint32_t n_sub, uint8_t *dst, uint64_t slot) {
+  __shared__ __attribute__((aligned(16))) uint8_t win[LZW];
+  __shared__ uint8_t ring[LZR];
+  const uint32_t s = blockIdx.x, lane = threadIdx.x;
+  if (sub_kind[s] != BL_KIND_LZ4 || sub_status[s] != BL_SKIP) return;
+  const ZgItem it = subs[s];
+  const uint8_t *in = (const uint8_t *)it.src;
+  uint8_t *out = dst + (uint64_t)s * slot;
+  uint32_t err = it.len == 0 || it.len >= 0x7FFFFFFFull;
+  const uint32_t cs = err ? 0u : (uint32_t)it.len;
+  const uint32_t cap = (uint32_t)min<uint64_t>(slot, 0x7FFFFFFFull);
+  const uintptr_t base = (uintptr_t)in;
+  int32_t wo = 0;  // stream offset of win[0] (16-B aligned address; -15 .. 0 for the first window)
+  auto fill = [&](uint32_t p) {
+    __syncthreads();
+    const uintptr_t a = (base + p) & ~(uintptr_t)15;
+    wo = (int32_t)(int64_t)(a - base);
+    const uintptr_t hi = base + cs;
+    for (uint32_t v = lane; v < LZW / 16; v += 64) {
+      const uintptr_t qq = a + 16ull * v;
+      if (qq >= hi) break;
+      if (qq >= base && qq + 16 <= hi) {
+        *(uint4 *)(win + 16 * v) = *(const uint4 *)qq;
+      } else {
+        for (uint32_t k = 0; k < 16; k++)
+          if (qq + k >= base && qq + k < hi) win[16 * v + k] = *(const uint8_t *)(qq + k);
+      }
+    }
+    __syncthreads();
+  };
+  auto rd = [&](uint32_t p) -> uint32_t {
+    uint32_t k = p - (uint32_t)wo;
+    if (k >= LZW) {
+      fill(p);
+      k = p - (uint32_t)wo;
+    }
+    return win[k];
+  };
+  uint32_t ip = 0, op = 0, safe = 0;
+  if (!err) fill(0);
+  while (!err) {
+    if (ip >= cs) { err = 1; break; }
+    const uint32_t token = rd(ip++);
+    uint32_t ll = token >> 4;
+    if (ll == 15) {
+      uint32_t b;
+      do {
+        if (ip >= cs) { err = 1; break; }
+        b = rd(ip++);
+        ll += b;
+      } while (b == 255 && ll < 0x7FFFFFFFu);
+      if (err) break;
+    }
+    if (ll > cs - ip || ll > cap - op) { err = 1; break; }
+    for (uint32_t i = lane; i < ll; i += 64) {  // literals: the window, else the stream in HBM
+      const uint32_t q = ip + i, k = q - (uint32_t)wo;
+      const uint8_t v = k < LZW ? win[k] : in[q];
+      out[op + i] = v;
+      ring[(op + i) & LZRM] = v;
+    }
+    ip += ll;
+    op += ll;
+    if (ip == cs) break;  // last sequence: literals only
+    if (cs - ip < 2) { err = 1; break; }
+    const uint32_t off = rd(ip) | (rd(ip + 1) << 8);
+    ip += 2;
+    if (off == 0 || off > op) { err = 1; break; }
+    uint32_t ml = token & 15;
+    if (ml == 15) {
+      uint32_t b;
+      do {
+        if (ip >= cs) { err = 1; break; }
+        b = rd(ip++);
+        ml += b;
+      } while (b == 255 && ml < 0x7FFFFFFFu);
+      if (err) break;
+    }
+    ml += 4;
+    if (ml > cap - op) { err = 1; break; }
+    if (off + ml <= LZR) {  // source and copy in the ring
+      if (ml <= 64) {
+        if (lane < ml) {
+          const uint32_t j = off >= ml ? lane : lane % off;
+          const uint8_t v = ring[(op - off + j) & LZRM];
+          ring[(op + lane) & LZRM] = v;
+          out[op + lane] = v;
+        }
+      } else {
+        for (uint32_t i = lane; i < ml; i += 64) {
+          const uint8_t v = ring[(op - off + (off >= ml ? i : i % off)) & LZRM];
+          ring[(op + i) & LZRM] = v;
+          out[op + i] = v;
+        }
+      }
+    } else {  // a far source: the wave's own earlier output (wait for its stores first)
+      if (op - off + min(off, ml) > safe) {
+        __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "workgroup");
+        safe = op;
+      }
+      const uint8_t *src = out + (op - off);
+      for (uint32_t i = lane; i < ml; i += 64) {
+        const uint8_t v = src[off >= ml ? i : i % off];
+        out[op + i] = v;
+        ring[(op + i) & LZRM] = v;
+      }
+    }
+    op += ml;
+  }
+  if (lane == 0) {
+    sub_status[s] = err ? ZG_CORRUPT_STREAM : 0u;
+    subs[s].src = (uint64_t)out;
+    subs[s].len = op;
+  }
+}
+#else
 __global__ __launch_bounds__(64) void k_lz4(ZgItem *subs, uint32_t *sub_status, const uint32_t *sub_kind,
                                             uint32_t n_sub, uint8_t *dst, uint64_t slot) {
   __shared__ __attribute__((aligned(16))) uint8_t win[LZW];
@@ -367,6 +491,7 @@ __global__ __launch_bounds__(64) void k_lz4(ZgItem *subs, uint32_t *sub_status, 
     subs[s].len = op;
   }
 }
+#endif
 
 // blosclz (c-blosc 1.21 blosclz.c, blosclz_decompress; restated, checked against c-blosc in
 // tests/test_gpu_blosc.py): a FastLZ-style stream. The first control byte (low 5 bits) opens a
