@@ -221,189 +221,78 @@ __global__ __launch_bounds__(64) void k_blosc_streams(ZgItem *items, uint32_t *s
 }
 
 // ---------------------------------------------------------------------------------------------
-// Serial LZ77 stream decoders (lz4, blosclz), one wave per stream. The token parse is inherently
-// serial, so what bounds a wave is the latency of its dependent reads: every token / length / offset
-// byte comes from an LDS window of the compressed stream (LZW bytes, refilled with coalesced 16-B
-// loads when the parse leaves it), literal runs are copied from the window by all lanes, and a
-// match is one round trip to the already written output (all lanes' loads in flight together).
+// Serial LZ77 stream decoders (lz4, blosclz, snappy), one wave per stream. The token parse is
+// inherently serial. Every token / length / offset byte comes from an LDS window of the compressed
+// stream (LZW bytes, refilled with coalesced 16-B loads when the parse leaves it), literal runs are
+// copied from the window by all lanes, and a match is copied from an LDS ring of the last LZR output
+// bytes (or, further back, from the wave's own earlier output in HBM).
+// At 8 waves per SIMD the decoders are issue-bound, not latency-bound (PMC on the 4 GiB blosc lz4
+// workload: ~80 SALU + 42 VALU instructions per sequence, 27 % of wave time issuing, 8 waves sharing
+// a SIMD): positions are 32-bit (a blosc stream and its output are < 2 GiB), the window is addressed
+// by its stream offset, and a copy of at most 64 bytes (nearly all of them) is one predicated pass
+// (lz4 131.7 -> 151.2 GiB/s against 64-bit positions and loop copies).
 // ---------------------------------------------------------------------------------------------
 #ifndef ZG_LZ_RING
-#define ZG_LZ_RING 4096  // bytes of recent output kept in LDS (0: matches read back from HBM only)
+#define ZG_LZ_RING 4096  // bytes of recent output kept in LDS
 #endif
 #ifndef ZG_LZW  // input window: 1 KiB + the 4 KiB ring = 5 KiB per one-wave workgroup -> 8 waves per SIMD
-#define ZG_LZW (ZG_LZ_RING ? 1024 : 8192)  // (a 4 KiB window: 5 waves, lz4 43.1 -> 35.4 ms: r03s_blosc_lz_window_ab)
+#define ZG_LZW 1024     // (a 4 KiB window: 5 waves, lz4 43.1 -> 35.4 ms: r03s_blosc_lz_window_ab)
 #endif
 constexpr uint32_t LZW = ZG_LZW;
-constexpr uint32_t LZR = ZG_LZ_RING > 0 ? ZG_LZ_RING : 1, LZRM = LZR - 1;
+constexpr uint32_t LZR = ZG_LZ_RING, LZRM = LZR - 1;
+static_assert((LZR & LZRM) == 0 && LZR >= 64 && LZW % 1024 == 0, "lz ring / window sizes");
 
-struct LzIn {
-  const uint8_t *in;  // the stream
-  uint64_t n;         // its length
-  uintptr_t a;        // absolute address of window byte 0 (16-B aligned)
-  uint8_t *w;         // LDS window
+struct Lz32 {
+  uintptr_t base;  // the stream
+  uint32_t cs;     // its length (< 2^31)
+  int32_t wo;      // stream offset of win[0] (a 16-B aligned address: -15 .. 0 for the first window)
+  uint32_t safe;   // output below this is known written (the wave's stores waited for)
+  uint8_t *win, *ring, *out;
 
-  // load the window holding stream offset p (p < n); uniform across the wave
-  __device__ void fill(uint64_t p) {
+  // load the window holding stream offset p (uniform across the wave)
+  __device__ void fill(uint32_t p) {
     __syncthreads();
-    a = ((uintptr_t)(in + p)) & ~(uintptr_t)15;
-    const uintptr_t lo = (uintptr_t)in, hi = (uintptr_t)(in + n);
+    const uintptr_t a = (base + p) & ~(uintptr_t)15, hi = base + cs;
+    wo = (int32_t)(int64_t)(a - base);
     for (uint32_t v = threadIdx.x; v < LZW / 16; v += 64) {
       const uintptr_t q = a + 16ull * v;
       if (q >= hi) break;
-      if (q >= lo && q + 16 <= hi) {
-        *(uint4 *)(w + 16 * v) = *(const uint4 *)q;
+      if (q >= base && q + 16 <= hi) {
+        *(uint4 *)(win + 16 * v) = *(const uint4 *)q;
       } else {  // the stream's first / last partial vector: bytes inside it only
         for (uint32_t k = 0; k < 16; k++)
-          if (q + k >= lo && q + k < hi) w[16 * v + k] = *(const uint8_t *)(q + k);
+          if (q + k >= base && q + k < hi) win[16 * v + k] = *(const uint8_t *)(q + k);
       }
     }
     __syncthreads();
   }
-  __device__ __forceinline__ uint32_t b(uint64_t p) {
-    uint64_t k = (uintptr_t)(in + p) - a;
-    if (k >= LZW) {
-      fill(p);
-      k = (uintptr_t)(in + p) - a;
-    }
-    return w[k];
-  }
-  // out[op .. op+len) = stream[ip .. ip+len), by all lanes (window bytes from LDS, the rest global);
-  // ring (if any) receives the same bytes at op mod LZR
-  __device__ __forceinline__ void copy(uint8_t *out, uint64_t op, uint64_t ip, uint64_t len, uint8_t *ring) {
-    for (uint64_t i = threadIdx.x; i < len; i += 64) {
-      const uint64_t k = (uintptr_t)(in + ip + i) - a;
-      const uint8_t v = k < LZW ? w[k] : in[ip + i];
-      out[op + i] = v;
-      if (ZG_LZ_RING) ring[(op + i) & LZRM] = v;
-    }
-  }
-};
-
-// A match of length ml at distance off (off <= op): byte i is out[op - off + (i mod off)], which
-// precedes the match, so lanes never read what another lane of this copy writes. The source may
-// hold bytes this wave stored since its last wait: wait for them first (workgroup scope = this CU's
-// L1, which the wave's own write-through stores keep coherent; an agent-scope fence would write back
-// / invalidate L2 across XCDs). Bytes below `safe` are known complete.
-// With an LDS ring of the last LZR output bytes, a match whose source and copy fit in the ring
-// (off + ml <= LZR) reads the ring instead: no wait for the wave's own stores and no HBM round trip
-// (blosc streams of shuffled images match mostly a row or two back).
-__device__ __forceinline__ void lz_match(uint8_t *out, uint64_t op, uint64_t off, uint64_t ml, uint64_t &safe,
-                                         uint8_t *ring) {
-  if (ZG_LZ_RING && off + ml <= LZR) {
-    for (uint64_t i = threadIdx.x; i < ml; i += 64) {
-      const uint8_t v = ring[(op - off + (off >= ml ? i : i % off)) & LZRM];
-      ring[(op + i) & LZRM] = v;
-      out[op + i] = v;
-    }
-    return;
-  }
-  if (op - off + (off < ml ? off : ml) > safe) {
-    __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "workgroup");
-    safe = op;
-  }
-  const uint8_t *src = out + op - off;
-  for (uint64_t i = threadIdx.x; i < ml; i += 64) {
-    const uint8_t v = src[off >= ml ? i : i % off];
-    out[op + i] = v;
-    if (ZG_LZ_RING) ring[(op + i) & LZRM] = v;
-  }
-}
-
-// LZ4 block format (lz4_Block_format.md): sequences {token, literal length, literals, offset u16,
-// match length}; the last sequence has literals only.
-#ifndef ZG_LZ4_LEAN
-#define ZG_LZ4_LEAN 1
-#endif
-#if ZG_LZ4_LEAN
-// The wave is issue-bound, not latency-bound, at 8 waves per SIMD (PMC on the 4 GiB blosc workload:
-// ~80 SALU + 42 VALU instructions per sequence, 27 % of wave time issuing with 8 waves sharing a
-// SIMD): positions are 32-bit (a blosc stream and its output are < 2 GiB), the window is addressed
-// by its stream offset, and a copy of at most 64 bytes (nearly all of them) is one predicated pass.
-__global__ __launch_bounds__(64) void k_lz4(ZgItem *subs, uint32_t *sub_status, const uint32_t *sub_kind,
-                                            uint32_t n_sub, uint8_t *dst, uint64_t slot) {
-  __shared__ __attribute__((aligned(16))) uint8_t win[LZW];
-  __shared__ uint8_t ring[LZR];
-  const uint32_t s = blockIdx.x, lane = threadIdx.x;
-  if (sub_kind[s] != BL_KIND_LZ4 || sub_status[s] != BL_SKIP) return;
-  const ZgItem it = subs[s];
-  const uint8_t *in = (const uint8_t *)it.src;
-  uint8_t *out = dst + (uint64_t)s * slot;
-  uint32_t err = it.len == 0 || it.len >= 0x7FFFFFFFull;
-  const uint32_t cs = err ? 0u : (uint32_t)it.len;
-  const uint32_t cap = (uint32_t)min<uint64_t>(slot, 0x7FFFFFFFull);
-  const uintptr_t base = (uintptr_t)in;
-  int32_t wo = 0;  // stream offset of win[0] (16-B aligned address; -15 .. 0 for the first window)
-  auto fill = [&](uint32_t p) {
-    __syncthreads();
-    const uintptr_t a = (base + p) & ~(uintptr_t)15;
-    wo = (int32_t)(int64_t)(a - base);
-    const uintptr_t hi = base + cs;
-    for (uint32_t v = lane; v < LZW / 16; v += 64) {
-      const uintptr_t qq = a + 16ull * v;
-      if (qq >= hi) break;
-      if (qq >= base && qq + 16 <= hi) {
-        *(uint4 *)(win + 16 * v) = *(const uint4 *)qq;
-      } else {
-        for (uint32_t k = 0; k < 16; k++)
-          if (qq + k >= base && qq + k < hi) win[16 * v + k] = *(const uint8_t *)(qq + k);
-      }
-    }
-    __syncthreads();
-  };
-  auto rd = [&](uint32_t p) -> uint32_t {
+  __device__ __forceinline__ uint32_t rd(uint32_t p) {
     uint32_t k = p - (uint32_t)wo;
     if (k >= LZW) {
       fill(p);
       k = p - (uint32_t)wo;
     }
     return win[k];
-  };
-  uint32_t ip = 0, op = 0, safe = 0;
-  if (!err) fill(0);
-  while (!err) {
-    if (ip >= cs) { err = 1; break; }
-    const uint32_t token = rd(ip++);
-    uint32_t ll = token >> 4;
-    if (ll == 15) {
-      uint32_t b;
-      do {
-        if (ip >= cs) { err = 1; break; }
-        b = rd(ip++);
-        ll += b;
-      } while (b == 255 && ll < 0x7FFFFFFFu);
-      if (err) break;
-    }
-    if (ll > cs - ip || ll > cap - op) { err = 1; break; }
-    for (uint32_t i = lane; i < ll; i += 64) {  // literals: the window, else the stream in HBM
+  }
+  // out[op .. op+n) = stream[ip .. ip+n) (window bytes from LDS, the rest from HBM), and to the ring
+  __device__ __forceinline__ void lits(uint32_t op, uint32_t ip, uint32_t n) {
+    for (uint32_t i = threadIdx.x; i < n; i += 64) {
       const uint32_t q = ip + i, k = q - (uint32_t)wo;
-      const uint8_t v = k < LZW ? win[k] : in[q];
+      const uint8_t v = k < LZW ? win[k] : ((const uint8_t *)base)[q];
       out[op + i] = v;
       ring[(op + i) & LZRM] = v;
     }
-    ip += ll;
-    op += ll;
-    if (ip == cs) break;  // last sequence: literals only
-    if (cs - ip < 2) { err = 1; break; }
-    const uint32_t off = rd(ip) | (rd(ip + 1) << 8);
-    ip += 2;
-    if (off == 0 || off > op) { err = 1; break; }
-    uint32_t ml = token & 15;
-    if (ml == 15) {
-      uint32_t b;
-      do {
-        if (ip >= cs) { err = 1; break; }
-        b = rd(ip++);
-        ml += b;
-      } while (b == 255 && ml < 0x7FFFFFFFu);
-      if (err) break;
-    }
-    ml += 4;
-    if (ml > cap - op) { err = 1; break; }
-    if (off + ml <= LZR) {  // source and copy in the ring
+  }
+  // A match of length ml at distance off (1 <= off <= op): byte i is out[op - off + (i mod off)],
+  // which precedes the match, so lanes never read what another lane of this copy writes. From the
+  // ring when source and copy fit in it; else from HBM after waiting for the wave's own stores
+  // (workgroup scope = this CU's L1, which its write-through stores keep coherent).
+  __device__ __forceinline__ void match(uint32_t op, uint32_t off, uint32_t ml) {
+    const uint32_t lane = threadIdx.x;
+    if (off + ml <= LZR) {
       if (ml <= 64) {
         if (lane < ml) {
-          const uint32_t j = off >= ml ? lane : lane % off;
-          const uint8_t v = ring[(op - off + j) & LZRM];
+          const uint8_t v = ring[(op - off + (off >= ml ? lane : lane % off)) & LZRM];
           ring[(op + lane) & LZRM] = v;
           out[op + lane] = v;
         }
@@ -414,84 +303,86 @@ __global__ __launch_bounds__(64) void k_lz4(ZgItem *subs, uint32_t *sub_status, 
           out[op + i] = v;
         }
       }
-    } else {  // a far source: the wave's own earlier output (wait for its stores first)
-      if (op - off + min(off, ml) > safe) {
-        __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "workgroup");
-        safe = op;
-      }
-      const uint8_t *src = out + (op - off);
-      for (uint32_t i = lane; i < ml; i += 64) {
-        const uint8_t v = src[off >= ml ? i : i % off];
-        out[op + i] = v;
-        ring[(op + i) & LZRM] = v;
-      }
+      return;
     }
-    op += ml;
+    if (op - off + min(off, ml) > safe) {
+      __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "workgroup");
+      safe = op;
+    }
+    const uint8_t *src = out + (op - off);
+    for (uint32_t i = lane; i < ml; i += 64) {
+      const uint8_t v = src[off >= ml ? i : i % off];
+      out[op + i] = v;
+      ring[(op + i) & LZRM] = v;
+    }
   }
-  if (lane == 0) {
-    sub_status[s] = err ? ZG_CORRUPT_STREAM : 0u;
-    subs[s].src = (uint64_t)out;
-    subs[s].len = op;
+};
+
+// the decoder's setup: err when the stream is empty or too long for 32-bit positions
+#define LZ32_SETUP(KIND)                                                                       \
+  __shared__ __attribute__((aligned(16))) uint8_t win[LZW];                                  \
+  __shared__ uint8_t ring[LZR];                                                               \
+  const uint32_t s = blockIdx.x, lane = threadIdx.x;                                          \
+  if (sub_kind[s] != (KIND) || sub_status[s] != BL_SKIP) return;                              \
+  const ZgItem it = subs[s];                                                                  \
+  uint32_t err = it.len == 0 || it.len >= 0x7FFFFFFFull;                                      \
+  const uint32_t cs = err ? 0u : (uint32_t)it.len;                                            \
+  const uint32_t cap = (uint32_t)min<uint64_t>(slot, 0x7FFFFFFFull);                         \
+  Lz32 L{(uintptr_t)it.src, cs, 0, 0, win, ring, dst + (uint64_t)s * slot};                   \
+  if (!err) L.fill(0);                                                                        \
+  uint32_t ip = 0, op = 0
+
+#define LZ32_FINISH()                                  \
+  if (lane == 0) {                                     \
+    sub_status[s] = err ? ZG_CORRUPT_STREAM : 0u;      \
+    subs[s].src = (uint64_t)L.out;                     \
+    subs[s].len = op;                                  \
   }
-}
-#else
+
+// LZ4 block format (lz4_Block_format.md): sequences {token, literal length, literals, offset u16,
+// match length}; the last sequence has literals only.
 __global__ __launch_bounds__(64) void k_lz4(ZgItem *subs, uint32_t *sub_status, const uint32_t *sub_kind,
                                             uint32_t n_sub, uint8_t *dst, uint64_t slot) {
-  __shared__ __attribute__((aligned(16))) uint8_t win[LZW];
-  __shared__ uint8_t ring[LZR];
-  const uint32_t s = blockIdx.x, lane = threadIdx.x;
-  if (sub_kind[s] != BL_KIND_LZ4 || sub_status[s] != BL_SKIP) return;
-  const ZgItem it = subs[s];
-  const uint64_t cs = it.len;
-  LzIn I{(const uint8_t *)it.src, cs, 0, win};
-  uint8_t *out = dst + (uint64_t)s * slot;
-  uint64_t ip = 0, op = 0, safe = 0;
-  uint32_t err = 0;
-  if (cs) I.fill(0);
-  for (;;) {
+  LZ32_SETUP(BL_KIND_LZ4);
+  while (!err) {
     if (ip >= cs) { err = 1; break; }
-    const uint32_t token = I.b(ip++);
-    uint64_t ll = token >> 4;
+    const uint32_t token = L.rd(ip++);
+    uint32_t ll = token >> 4;
     if (ll == 15) {
       uint32_t b;
       do {
         if (ip >= cs) { err = 1; break; }
-        b = I.b(ip++);
+        b = L.rd(ip++);
         ll += b;
-      } while (b == 255);
+      } while (b == 255 && ll < 0x7FFFFFFFu);
       if (err) break;
     }
-    if (ip + ll > cs || op + ll > slot) { err = 1; break; }
-    I.copy(out, op, ip, ll, ring);
+    if (ll > cs - ip || ll > cap - op) { err = 1; break; }
+    L.lits(op, ip, ll);
     ip += ll;
     op += ll;
     if (ip == cs) break;  // last sequence: literals only
-    if (ip + 2 > cs) { err = 1; break; }
-    const uint64_t off = I.b(ip) | (I.b(ip + 1) << 8);
+    if (cs - ip < 2) { err = 1; break; }
+    const uint32_t off = L.rd(ip) | (L.rd(ip + 1) << 8);
     ip += 2;
     if (off == 0 || off > op) { err = 1; break; }
-    uint64_t ml = token & 15;
+    uint32_t ml = token & 15;
     if (ml == 15) {
       uint32_t b;
       do {
         if (ip >= cs) { err = 1; break; }
-        b = I.b(ip++);
+        b = L.rd(ip++);
         ml += b;
-      } while (b == 255);
+      } while (b == 255 && ml < 0x7FFFFFFFu);
       if (err) break;
     }
     ml += 4;
-    if (op + ml > slot) { err = 1; break; }
-    lz_match(out, op, off, ml, safe, ring);
+    if (ml > cap - op) { err = 1; break; }
+    L.match(op, off, ml);
     op += ml;
   }
-  if (lane == 0) {
-    sub_status[s] = err ? ZG_CORRUPT_STREAM : 0u;
-    subs[s].src = (uint64_t)out;
-    subs[s].len = op;
-  }
+  LZ32_FINISH();
 }
-#endif
 
 // blosclz (c-blosc 1.21 blosclz.c, blosclz_decompress; restated, checked against c-blosc in
 // tests/test_gpu_blosc.py): a FastLZ-style stream. The first control byte (low 5 bits) opens a
@@ -501,64 +392,46 @@ __global__ __launch_bounds__(64) void k_lz4(ZgItem *subs, uint32_t *sub_status, 
 // value + 8192 (MAX_DISTANCE 8191 + 1). The stream ends when its bytes are consumed.
 __global__ __launch_bounds__(64) void k_blosclz(ZgItem *subs, uint32_t *sub_status, const uint32_t *sub_kind,
                                                 uint32_t n_sub, uint8_t *dst, uint64_t slot) {
-  __shared__ __attribute__((aligned(16))) uint8_t win[LZW];
-  __shared__ uint8_t ring[LZR];
-  const uint32_t s = blockIdx.x, lane = threadIdx.x;
-  if (sub_kind[s] != BL_KIND_BLOSCLZ || sub_status[s] != BL_SKIP) return;
-  const ZgItem it = subs[s];
-  const uint64_t n = it.len;
-  LzIn I{(const uint8_t *)it.src, n, 0, win};
-  uint8_t *out = dst + (uint64_t)s * slot;
-  uint64_t ip = 0, op = 0, safe = 0;
-  uint32_t err = 0;
-  if (n) {
-    I.fill(0);
-    uint32_t ctrl = I.b(ip++) & 31u;
-    for (;;) {
-      if (ctrl >= 32) {
-        uint64_t len = (ctrl >> 5) - 1;
-        uint64_t ofs = (uint64_t)(ctrl & 31u) << 8;
-        uint32_t code;
-        if (len == 6) {
-          do {
-            if (ip + 1 >= n) { err = 1; break; }
-            code = I.b(ip++);
-            len += code;
-          } while (code == 255);
-          if (err) break;
-        } else if (ip + 1 >= n) {
-          err = 1;
-          break;
-        }
-        code = I.b(ip++);
-        len += 3;
-        uint64_t dist = ofs + code + 1;
-        if (code == 255 && ofs == (31u << 8)) {
-          if (ip + 1 >= n) { err = 1; break; }
-          dist = ((uint64_t)I.b(ip) << 8) + I.b(ip + 1) + 8192;
-          ip += 2;
-        }
-        if (op + len > slot || dist > op) { err = 1; break; }
-        lz_match(out, op, dist, len, safe, ring);
-        op += len;
-        if (ip >= n) break;
-        ctrl = I.b(ip++);
-      } else {
-        const uint64_t run = ctrl + 1;
-        if (op + run > slot || ip + run > n) { err = 1; break; }
-        I.copy(out, op, ip, run, ring);
-        op += run;
-        ip += run;
-        if (ip >= n) break;
-        ctrl = I.b(ip++);
+  LZ32_SETUP(BL_KIND_BLOSCLZ);
+  uint32_t ctrl = err ? 0u : L.rd(ip++) & 31u;
+  while (!err) {
+    if (ctrl >= 32) {
+      uint32_t len = (ctrl >> 5) - 1;
+      const uint32_t ofs = (ctrl & 31u) << 8;
+      uint32_t code;
+      if (len == 6) {
+        do {
+          if (cs - ip <= 1) { err = 1; break; }
+          code = L.rd(ip++);
+          len += code;
+        } while (code == 255 && len < 0x7FFFFFFFu);
+        if (err) break;
+      } else if (cs - ip <= 1) {
+        err = 1;
+        break;
       }
+      code = L.rd(ip++);
+      len += 3;
+      uint32_t dist = ofs + code + 1;
+      if (code == 255 && ofs == (31u << 8)) {
+        if (cs - ip <= 1) { err = 1; break; }
+        dist = (L.rd(ip) << 8) + L.rd(ip + 1) + 8192;
+        ip += 2;
+      }
+      if (len > cap - op || dist > op) { err = 1; break; }
+      L.match(op, dist, len);
+      op += len;
+    } else {
+      const uint32_t run = ctrl + 1;
+      if (run > cap - op || run > cs - ip) { err = 1; break; }
+      L.lits(op, ip, run);
+      op += run;
+      ip += run;
     }
+    if (ip >= cs) break;
+    ctrl = L.rd(ip++);
   }
-  if (lane == 0) {
-    sub_status[s] = err ? ZG_CORRUPT_STREAM : 0u;
-    subs[s].src = (uint64_t)out;
-    subs[s].len = op;
-  }
+  LZ32_FINISH();
 }
 
 // snappy (raw format, format_description.txt of google/snappy; c-blosc 1.21 snappy_wrap_decompress =
@@ -569,71 +442,60 @@ __global__ __launch_bounds__(64) void k_blosclz(ZgItem *subs, uint32_t *sub_stat
 // the output must be exactly the preamble's length and the input consumed exactly.
 __global__ __launch_bounds__(64) void k_snappy(ZgItem *subs, uint32_t *sub_status, const uint32_t *sub_kind,
                                                uint32_t n_sub, uint8_t *dst, uint64_t slot) {
-  __shared__ __attribute__((aligned(16))) uint8_t win[LZW];
-  __shared__ uint8_t ring[LZR];
-  const uint32_t s = blockIdx.x, lane = threadIdx.x;
-  if (sub_kind[s] != BL_KIND_SNAPPY || sub_status[s] != BL_SKIP) return;
-  const ZgItem it = subs[s];
-  const uint64_t n = it.len;
-  LzIn I{(const uint8_t *)it.src, n, 0, win};
-  uint8_t *out = dst + (uint64_t)s * slot;
-  uint64_t ip = 0, op = 0, safe = 0, want = 0;
-  uint32_t err = 0;
-  if (n) I.fill(0);
+  LZ32_SETUP(BL_KIND_SNAPPY);
+  uint64_t want = 0;
   // preamble: little-endian base-128 varint (<= 5 bytes, < 2^32)
-  for (uint32_t k = 0;; k++) {
-    if (ip >= n || k == 5) { err = 1; break; }
-    const uint32_t b = I.b(ip++);
+  for (uint32_t k = 0; !err; k++) {
+    if (ip >= cs || k == 5) { err = 1; break; }
+    const uint32_t b = L.rd(ip++);
     want |= (uint64_t)(b & 127) << (7 * k);
     if (!(b & 128)) break;
   }
-  if (!err && (want > slot || want >> 32)) err = 1;
-  while (!err && ip < n) {
-    const uint32_t tag = I.b(ip++);
+  if (!err && want > cap) err = 1;
+  const uint32_t w32 = (uint32_t)want;
+  while (!err && ip < cs) {
+    const uint32_t tag = L.rd(ip++);
     if ((tag & 3) == 0) {  // literal
       uint64_t len = (tag >> 2) + 1;
       if (len > 60) {
         const uint32_t nb = (uint32_t)len - 60;  // 1..4 length bytes
-        if (ip + nb > n) { err = 1; break; }
+        if (nb > cs - ip) { err = 1; break; }
         uint64_t v = 0;
-        for (uint32_t k = 0; k < nb; k++) v |= (uint64_t)I.b(ip + k) << (8 * k);
+        for (uint32_t k = 0; k < nb; k++) v |= (uint64_t)L.rd(ip + k) << (8 * k);
         ip += nb;
         len = v + 1;
       }
-      if (ip + len > n || op + len > want) { err = 1; break; }
-      I.copy(out, op, ip, len, ring);
-      ip += len;
-      op += len;
+      if (len > cs - ip || len > w32 - op) { err = 1; break; }
+      L.lits(op, ip, (uint32_t)len);
+      ip += (uint32_t)len;
+      op += (uint32_t)len;
     } else {
-      uint64_t len, off;
+      uint32_t len;
+      uint64_t off;
       if ((tag & 3) == 1) {
-        if (ip + 1 > n) { err = 1; break; }
+        if (cs - ip < 1) { err = 1; break; }
         len = 4 + ((tag >> 2) & 7);
-        off = ((uint64_t)(tag >> 5) << 8) | I.b(ip);
+        off = ((tag >> 5) << 8) | L.rd(ip);
         ip += 1;
       } else if ((tag & 3) == 2) {
-        if (ip + 2 > n) { err = 1; break; }
+        if (cs - ip < 2) { err = 1; break; }
         len = 1 + (tag >> 2);
-        off = I.b(ip) | (I.b(ip + 1) << 8);
+        off = L.rd(ip) | (L.rd(ip + 1) << 8);
         ip += 2;
       } else {
-        if (ip + 4 > n) { err = 1; break; }
+        if (cs - ip < 4) { err = 1; break; }
         len = 1 + (tag >> 2);
-        off = (uint64_t)I.b(ip) | ((uint64_t)I.b(ip + 1) << 8) | ((uint64_t)I.b(ip + 2) << 16) |
-              ((uint64_t)I.b(ip + 3) << 24);
+        off = (uint64_t)L.rd(ip) | ((uint64_t)L.rd(ip + 1) << 8) | ((uint64_t)L.rd(ip + 2) << 16) |
+              ((uint64_t)L.rd(ip + 3) << 24);
         ip += 4;
       }
-      if (off == 0 || off > op || op + len > want) { err = 1; break; }
-      lz_match(out, op, off, len, safe, ring);
+      if (off == 0 || off > op || len > w32 - op) { err = 1; break; }
+      L.match(op, (uint32_t)off, len);
       op += len;
     }
   }
-  if (!err && op != want) err = 1;
-  if (lane == 0) {
-    sub_status[s] = err ? ZG_CORRUPT_STREAM : 0u;
-    subs[s].src = (uint64_t)out;
-    subs[s].len = op;
-  }
+  if (!err && op != w32) err = 1;
+  LZ32_FINISH();
 }
 
 // One workgroup per block: the block's streams (decoded, or stored in the frame) are the shuffled
