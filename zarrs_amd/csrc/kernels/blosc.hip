@@ -384,6 +384,161 @@ __global__ __launch_bounds__(64) void k_lz4(ZgItem *subs, uint32_t *sub_status, 
   LZ32_FINISH();
 }
 
+// ---- several lz4 streams per wave ----
+// The one-stream-per-wave decoder spends ~155 instructions per sequence, most of them scalar parse
+// work, and a copy uses ~24 of 64 lanes. Here a wave decodes 64 / G streams at once, G lanes each:
+// the parse runs in vector registers (every group of G lanes holds its stream's uniform state), so
+// one instruction advances all the wave's streams; copies use the group's G lanes. Streams come
+// from a compacted list (k_lz_list) so no group idles on stored or other-kind streams.
+#ifndef ZG_LZM_G
+#define ZG_LZM_G 32
+#endif
+__global__ __launch_bounds__(1024) void k_lz_list(const uint32_t *sub_kind, const uint32_t *sub_status,
+                                                  uint32_t n_sub, uint32_t kind, uint32_t *list) {
+  __shared__ uint32_t wsum[16], s_base;
+  const uint32_t t = threadIdx.x, w = t >> 6, l = t & 63;
+  if (t == 0) s_base = 0;
+  __syncthreads();
+  for (uint32_t c = 0; c < n_sub; c += 1024) {
+    const uint32_t i = c + t;
+    const bool f = i < n_sub && sub_kind[i] == kind && sub_status[i] == BL_SKIP;
+    const uint64_t m = __ballot(f);
+    if (l == 0) wsum[w] = (uint32_t)__builtin_popcountll(m);
+    __syncthreads();
+    uint32_t off = s_base + (uint32_t)__builtin_popcountll(m & ((1ull << l) - 1));
+    for (uint32_t k = 0; k < w; k++) off += wsum[k];
+    if (f) list[1 + off] = i;
+    __syncthreads();
+    if (t == 0) {
+      uint32_t tot = 0;
+      for (uint32_t k = 0; k < 16; k++) tot += wsum[k];
+      s_base += tot;
+    }
+    __syncthreads();
+  }
+  if (t == 0) list[0] = s_base;
+}
+
+template <int G>
+__global__ __launch_bounds__(64) void k_lz4m(ZgItem *subs, uint32_t *sub_status, const uint32_t *list,
+                                             uint8_t *dst, uint64_t slot) {
+  constexpr uint32_t NG = 64 / G;
+  __shared__ __attribute__((aligned(16))) uint8_t win_all[NG][LZW];
+  __shared__ uint8_t ring_all[NG][LZR];
+  const uint32_t lane = threadIdx.x, g = lane / G, gl = lane % G;
+  const uint32_t k = blockIdx.x * NG + g, cnt = list[0];
+  if (blockIdx.x * NG >= cnt) return;  // the whole wave past the list
+  const bool have = k < cnt;
+  const uint32_t s = have ? list[1 + k] : 0u;
+  const ZgItem it = have ? subs[s] : ZgItem{0, 0, 0, 0, 0, 0};
+  uint8_t *win = win_all[g], *ring = ring_all[g];
+  const uintptr_t base = (uintptr_t)it.src;
+  uint32_t err = have && (it.len == 0 || it.len >= 0x7FFFFFFFull);
+  const uint32_t cs = (have && !err) ? (uint32_t)it.len : 0u;
+  const uint32_t cap = (uint32_t)min<uint64_t>(slot, 0x7FFFFFFFull);
+  uint8_t *out = dst + (uint64_t)s * slot;
+  int32_t wo = 0;
+  // the group's window holding stream offset p (p uniform in the group; called by whole groups)
+  auto fill = [&](uint32_t p) {
+    const uintptr_t a = (base + p) & ~(uintptr_t)15, hi = base + cs;
+    wo = (int32_t)(int64_t)(a - base);
+    for (uint32_t v = gl; v < LZW / 16; v += G) {
+      const uintptr_t q = a + 16ull * v;
+      if (q >= hi) break;
+      if (q >= base && q + 16 <= hi) {
+        *(uint4 *)(win + 16 * v) = *(const uint4 *)q;
+      } else {
+        for (uint32_t b = 0; b < 16; b++)
+          if (q + b >= base && q + b < hi) win[16 * v + b] = *(const uint8_t *)(q + b);
+      }
+    }
+  };
+  auto rd = [&](uint32_t p) -> uint32_t {
+    uint32_t kk = p - (uint32_t)wo;
+    if (kk >= LZW) {
+      fill(p);
+      kk = p - (uint32_t)wo;
+    }
+    return win[kk];
+  };
+  uint32_t ip = 0, op = 0, safe = 0;
+  bool act = have && !err;
+  if (act) fill(0);
+  while (__ballot(act)) {
+    if (act) {
+      uint32_t token = rd(ip++);
+      uint32_t ll = token >> 4;
+      if (ll == 15) {
+        uint32_t b;
+        do {
+          if (ip >= cs) { err = 1; break; }
+          b = rd(ip++);
+          ll += b;
+        } while (b == 255 && ll < 0x7FFFFFFFu);
+      }
+      if (!err && (ll > cs - ip || ll > cap - op)) err = 1;
+      if (!err) {
+        for (uint32_t i = gl; i < ll; i += G) {
+          const uint32_t q = ip + i, kk = q - (uint32_t)wo;
+          const uint8_t v = kk < LZW ? win[kk] : ((const uint8_t *)base)[q];
+          out[op + i] = v;
+          ring[(op + i) & LZRM] = v;
+        }
+        ip += ll;
+        op += ll;
+        if (ip == cs) {
+          act = false;  // last sequence: literals only
+        } else if (cs - ip < 2) {
+          err = 1;
+        } else {
+          const uint32_t off = rd(ip) | (rd(ip + 1) << 8);
+          ip += 2;
+          uint32_t ml = token & 15;
+          if (off == 0 || off > op) err = 1;
+          if (!err && ml == 15) {
+            uint32_t b;
+            do {
+              if (ip >= cs) { err = 1; break; }
+              b = rd(ip++);
+              ml += b;
+            } while (b == 255 && ml < 0x7FFFFFFFu);
+          }
+          ml += 4;
+          if (!err && ml > cap - op) err = 1;
+          if (!err && ip >= cs) err = 1;  // a stream ends with a literals-only sequence
+          if (!err) {
+            if (off + ml <= LZR) {
+              for (uint32_t i = gl; i < ml; i += G) {
+                const uint8_t v = ring[(op - off + (off >= ml ? i : i % off)) & LZRM];
+                ring[(op + i) & LZRM] = v;
+                out[op + i] = v;
+              }
+            } else {
+              if (op - off + min(off, ml) > safe) {
+                __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "workgroup");
+                safe = op;
+              }
+              const uint8_t *src = out + (op - off);
+              for (uint32_t i = gl; i < ml; i += G) {
+                const uint8_t v = src[off >= ml ? i : i % off];
+                out[op + i] = v;
+                ring[(op + i) & LZRM] = v;
+              }
+            }
+            op += ml;
+          }
+        }
+      }
+      if (err) act = false;
+    }
+  }
+  if (have && gl == 0) {
+    sub_status[s] = err ? ZG_CORRUPT_STREAM : 0u;
+    subs[s].src = (uint64_t)out;
+    subs[s].len = op;
+  }
+}
+
 // blosclz (c-blosc 1.21 blosclz.c, blosclz_decompress; restated, checked against c-blosc in
 // tests/test_gpu_blosc.py): a FastLZ-style stream. The first control byte (low 5 bits) opens a
 // literal run; a control byte c < 32 is a run of c + 1 literals; c >= 32 is a match of length
@@ -701,9 +856,16 @@ hipError_t launch_blosc_decode(ZgItem *items, uint32_t *status, uint32_t n_items
     hipError_t e = launch_zstd(D.subs, D.sub_status, (uint32_t)D.n_sub, D.tmp, D.sub_slot, D.zs, s);
     if (e != hipSuccess) return e;
   }
-  if (D.n_lz4)
+  if (D.n_lz4 && D.lz_list && ZG_LZM_G < 64) {
+    hipLaunchKernelGGL(k_lz_list, dim3(1), dim3(1024), 0, s, D.sub_kind, D.sub_status, (uint32_t)D.n_sub,
+                       (uint32_t)BL_KIND_LZ4, D.lz_list);
+    constexpr uint32_t NG = 64 / ZG_LZM_G;
+    hipLaunchKernelGGL(k_lz4m<ZG_LZM_G>, dim3((uint32_t)((D.n_sub + NG - 1) / NG)), dim3(64), 0, s, D.subs,
+                       D.sub_status, D.lz_list, D.tmp, D.sub_slot);
+  } else if (D.n_lz4) {
     hipLaunchKernelGGL(k_lz4, dim3((uint32_t)D.n_sub), dim3(64), 0, s, D.subs, D.sub_status, D.sub_kind,
                        (uint32_t)D.n_sub, D.tmp, D.sub_slot);
+  }
   if (D.n_zlib) {
     hipError_t e = launch_zlib_streams(D.subs, D.sub_status, D.sub_kind, (uint32_t)D.n_sub, D.tmp, D.sub_slot, D.zaux, s);
     if (e == hipSuccess) e = launch_adler32_check(D.subs, D.sub_status, D.sub_kind, (uint32_t)D.n_sub, D.zaux, s);

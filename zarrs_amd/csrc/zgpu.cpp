@@ -277,7 +277,7 @@ struct zgpu_plan {
     size_t n = 0;
   };
   Grow bl_info, bl_bases, bl_subs, bl_sub_status, bl_sub_kind, bl_blocks, bl_tmp, bl_zblks, bl_znblk, bl_zmode,
-      bl_zlit, bl_zseq, bl_zaux, bl_zser;
+      bl_zlit, bl_zseq, bl_zaux, bl_zser, bl_lzl;
   uint8_t *bl_h = nullptr;  // pinned: BlInfo read-back (first execution)
   size_t bl_h_n = 0;
   void *grow(Grow &g, size_t bytes) {
@@ -327,7 +327,7 @@ struct zgpu_plan {
     for (hipEvent_t e : zev)
       if (e) (void)hipEventDestroy(e);
     for (Grow *g : {&bl_info, &bl_bases, &bl_subs, &bl_sub_status, &bl_sub_kind, &bl_blocks, &bl_tmp, &bl_zblks,
-                    &bl_znblk, &bl_zmode, &bl_zlit, &bl_zseq, &bl_zaux, &bl_zser})
+                    &bl_znblk, &bl_zmode, &bl_zlit, &bl_zseq, &bl_zaux, &bl_zser, &bl_lzl})
       ctx->dev_free(g->p);
     ctx->host_free(bl_h);
     ctx->host_free(h_ctl);
@@ -852,6 +852,7 @@ static void blosc_stage(zgpu_plan &P, const Stage &st, uint8_t *out, hipStream_t
     D.tmp = (uint8_t *)P.grow(P.bl_tmp, D.n_sub * D.sub_slot);
   }
   if (D.n_zlib) D.zaux = (uint2 *)P.grow(P.bl_zaux, D.n_sub * sizeof(uint2));
+  D.lz_list = D.n_lz4 ? (uint32_t *)P.grow(P.bl_lzl, (D.n_sub + 1) * 4) : nullptr;
   if (D.n_zstd) {
     uint64_t blk_bytes;
     zstd_scratch_layout(D.sub_slot, D.zs.blk_cap, blk_bytes, D.zs.lit_stride, D.zs.seq_cap);
