@@ -419,27 +419,15 @@ __global__ __launch_bounds__(1024) void k_lz_list(const uint32_t *sub_kind, cons
   if (t == 0) list[0] = s_base;
 }
 
+// one stream's state in a group of G lanes (uniform within the group); methods are called by whole groups
 template <int G>
-__global__ __launch_bounds__(64) void k_lz4m(ZgItem *subs, uint32_t *sub_status, const uint32_t *list,
-                                             uint8_t *dst, uint64_t slot) {
-  constexpr uint32_t NG = 64 / G;
-  __shared__ __attribute__((aligned(16))) uint8_t win_all[NG][LZW];
-  __shared__ uint8_t ring_all[NG][LZR];
-  const uint32_t lane = threadIdx.x, g = lane / G, gl = lane % G;
-  const uint32_t k = blockIdx.x * NG + g, cnt = list[0];
-  if (blockIdx.x * NG >= cnt) return;  // the whole wave past the list
-  const bool have = k < cnt;
-  const uint32_t s = have ? list[1 + k] : 0u;
-  const ZgItem it = have ? subs[s] : ZgItem{0, 0, 0, 0, 0, 0};
-  uint8_t *win = win_all[g], *ring = ring_all[g];
-  const uintptr_t base = (uintptr_t)it.src;
-  uint32_t err = have && (it.len == 0 || it.len >= 0x7FFFFFFFull);
-  const uint32_t cs = (have && !err) ? (uint32_t)it.len : 0u;
-  const uint32_t cap = (uint32_t)min<uint64_t>(slot, 0x7FFFFFFFull);
-  uint8_t *out = dst + (uint64_t)s * slot;
-  int32_t wo = 0;
-  // the group's window holding stream offset p (p uniform in the group; called by whole groups)
-  auto fill = [&](uint32_t p) {
+struct LzG {
+  uintptr_t base;
+  uint32_t cs, gl, safe;
+  int32_t wo;
+  uint8_t *win, *ring, *out;
+
+  __device__ void fill(uint32_t p) {
     const uintptr_t a = (base + p) & ~(uintptr_t)15, hi = base + cs;
     wo = (int32_t)(int64_t)(a - base);
     for (uint32_t v = gl; v < LZW / 16; v += G) {
@@ -452,91 +440,178 @@ __global__ __launch_bounds__(64) void k_lz4m(ZgItem *subs, uint32_t *sub_status,
           if (q + b >= base && q + b < hi) win[16 * v + b] = *(const uint8_t *)(q + b);
       }
     }
-  };
-  auto rd = [&](uint32_t p) -> uint32_t {
+  }
+  __device__ __forceinline__ uint32_t rd(uint32_t p) {
     uint32_t kk = p - (uint32_t)wo;
     if (kk >= LZW) {
       fill(p);
       kk = p - (uint32_t)wo;
     }
     return win[kk];
-  };
-  uint32_t ip = 0, op = 0, safe = 0;
-  bool act = have && !err;
-  if (act) fill(0);
-  while (__ballot(act)) {
-    if (act) {
-      uint32_t token = rd(ip++);
-      uint32_t ll = token >> 4;
-      if (ll == 15) {
-        uint32_t b;
-        do {
-          if (ip >= cs) { err = 1; break; }
-          b = rd(ip++);
-          ll += b;
-        } while (b == 255 && ll < 0x7FFFFFFFu);
-      }
-      if (!err && (ll > cs - ip || ll > cap - op)) err = 1;
-      if (!err) {
-        for (uint32_t i = gl; i < ll; i += G) {
-          const uint32_t q = ip + i, kk = q - (uint32_t)wo;
-          const uint8_t v = kk < LZW ? win[kk] : ((const uint8_t *)base)[q];
-          out[op + i] = v;
-          ring[(op + i) & LZRM] = v;
-        }
-        ip += ll;
-        op += ll;
-        if (ip == cs) {
-          act = false;  // last sequence: literals only
-        } else if (cs - ip < 2) {
-          err = 1;
-        } else {
-          const uint32_t off = rd(ip) | (rd(ip + 1) << 8);
-          ip += 2;
-          uint32_t ml = token & 15;
-          if (off == 0 || off > op) err = 1;
-          if (!err && ml == 15) {
-            uint32_t b;
-            do {
-              if (ip >= cs) { err = 1; break; }
-              b = rd(ip++);
-              ml += b;
-            } while (b == 255 && ml < 0x7FFFFFFFu);
-          }
-          ml += 4;
-          if (!err && ml > cap - op) err = 1;
-          if (!err && ip >= cs) err = 1;  // a stream ends with a literals-only sequence
-          if (!err) {
-            if (off + ml <= LZR) {
-              for (uint32_t i = gl; i < ml; i += G) {
-                const uint8_t v = ring[(op - off + (off >= ml ? i : i % off)) & LZRM];
-                ring[(op + i) & LZRM] = v;
-                out[op + i] = v;
-              }
-            } else {
-              if (op - off + min(off, ml) > safe) {
-                __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "workgroup");
-                safe = op;
-              }
-              const uint8_t *src = out + (op - off);
-              for (uint32_t i = gl; i < ml; i += G) {
-                const uint8_t v = src[off >= ml ? i : i % off];
-                out[op + i] = v;
-                ring[(op + i) & LZRM] = v;
-              }
-            }
-            op += ml;
-          }
-        }
-      }
-      if (err) act = false;
+  }
+  __device__ __forceinline__ void lits(uint32_t op, uint32_t ip, uint32_t n) {
+    for (uint32_t i = gl; i < n; i += G) {
+      const uint32_t q = ip + i, kk = q - (uint32_t)wo;
+      const uint8_t v = kk < LZW ? win[kk] : ((const uint8_t *)base)[q];
+      out[op + i] = v;
+      ring[(op + i) & LZRM] = v;
     }
   }
-  if (have && gl == 0) {
-    sub_status[s] = err ? ZG_CORRUPT_STREAM : 0u;
-    subs[s].src = (uint64_t)out;
-    subs[s].len = op;
+  __device__ __forceinline__ void match(uint32_t op, uint32_t off, uint32_t ml) {
+    if (off + ml <= LZR) {
+      for (uint32_t i = gl; i < ml; i += G) {
+        const uint8_t v = ring[(op - off + (off >= ml ? i : i % off)) & LZRM];
+        ring[(op + i) & LZRM] = v;
+        out[op + i] = v;
+      }
+      return;
+    }
+    if (op - off + min(off, ml) > safe) {  // the wave's own stores of the source: wait for them
+      __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "workgroup");
+      safe = op;
+    }
+    const uint8_t *src = out + (op - off);
+    for (uint32_t i = gl; i < ml; i += G) {
+      const uint8_t v = src[off >= ml ? i : i % off];
+      out[op + i] = v;
+      ring[(op + i) & LZRM] = v;
+    }
   }
+};
+
+// group setup: stream k of the list for group g; act = the group has a stream to decode
+#define LZG_SETUP()                                                                            \
+  constexpr uint32_t NG = 64 / G;                                                              \
+  __shared__ __attribute__((aligned(16))) uint8_t win_all[NG][LZW];                           \
+  __shared__ uint8_t ring_all[NG][LZR];                                                        \
+  const uint32_t lane = threadIdx.x, g = lane / G;                                             \
+  const uint32_t k = blockIdx.x * NG + g, cnt = list[0];                                       \
+  if (blockIdx.x * NG >= cnt) return;                                                          \
+  const bool have = k < cnt;                                                                   \
+  const uint32_t s = have ? list[1 + k] : 0u;                                                  \
+  const ZgItem it = have ? subs[s] : ZgItem{0, 0, 0, 0, 0, 0};                                 \
+  uint32_t err = have && (it.len == 0 || it.len >= 0x7FFFFFFFull);                             \
+  const uint32_t cs = (have && !err) ? (uint32_t)it.len : 0u;                                  \
+  const uint32_t cap = (uint32_t)min<uint64_t>(slot, 0x7FFFFFFFull);                          \
+  LzG<G> L{(uintptr_t)it.src, cs, lane % G, 0, 0, win_all[g], ring_all[g], dst + (uint64_t)s * slot}; \
+  uint32_t ip = 0, op = 0;                                                                     \
+  bool act = have && !err;                                                                     \
+  if (act) L.fill(0)
+
+#define LZG_FINISH()                                   \
+  if (have && lane % G == 0) {                         \
+    sub_status[s] = err ? ZG_CORRUPT_STREAM : 0u;      \
+    subs[s].src = (uint64_t)L.out;                     \
+    subs[s].len = op;                                  \
+  }
+
+template <int G>
+__global__ __launch_bounds__(64) void k_lz4m(ZgItem *subs, uint32_t *sub_status, const uint32_t *list,
+                                             uint8_t *dst, uint64_t slot) {
+  LZG_SETUP();
+  while (__ballot(act)) {
+    if (!act) continue;
+    const uint32_t token = L.rd(ip++);
+    uint32_t ll = token >> 4;
+    if (ll == 15) {
+      uint32_t b;
+      do {
+        if (ip >= cs) { err = 1; break; }
+        b = L.rd(ip++);
+        ll += b;
+      } while (b == 255 && ll < 0x7FFFFFFFu);
+    }
+    if (!err && (ll > cs - ip || ll > cap - op)) err = 1;
+    if (!err) {
+      L.lits(op, ip, ll);
+      ip += ll;
+      op += ll;
+      if (ip == cs) {
+        act = false;  // last sequence: literals only
+      } else if (cs - ip < 2) {
+        err = 1;
+      } else {
+        const uint32_t off = L.rd(ip) | (L.rd(ip + 1) << 8);
+        ip += 2;
+        uint32_t ml = token & 15;
+        if (off == 0 || off > op) err = 1;
+        if (!err && ml == 15) {
+          uint32_t b;
+          do {
+            if (ip >= cs) { err = 1; break; }
+            b = L.rd(ip++);
+            ml += b;
+          } while (b == 255 && ml < 0x7FFFFFFFu);
+        }
+        ml += 4;
+        if (!err && (ml > cap - op || ip >= cs)) err = 1;  // a stream ends with a literals-only sequence
+        if (!err) {
+          L.match(op, off, ml);
+          op += ml;
+        }
+      }
+    }
+    if (err) act = false;
+  }
+  LZG_FINISH();
+}
+
+// blosclz (the format below, k_blosclz), several streams per wave
+template <int G>
+__global__ __launch_bounds__(64) void k_blosclzm(ZgItem *subs, uint32_t *sub_status, const uint32_t *list,
+                                                 uint8_t *dst, uint64_t slot) {
+  LZG_SETUP();
+  uint32_t ctrl = act ? L.rd(ip++) & 31u : 0u;
+  while (__ballot(act)) {
+    if (!act) continue;
+    if (ctrl >= 32) {
+      uint32_t len = (ctrl >> 5) - 1;
+      const uint32_t ofs = (ctrl & 31u) << 8;
+      uint32_t code = 0;
+      if (len == 6) {
+        do {
+          if (cs - ip <= 1) { err = 1; break; }
+          code = L.rd(ip++);
+          len += code;
+        } while (code == 255 && len < 0x7FFFFFFFu);
+      } else if (cs - ip <= 1) {
+        err = 1;
+      }
+      if (!err) {
+        code = L.rd(ip++);
+        len += 3;
+        uint32_t dist = ofs + code + 1;
+        if (code == 255 && ofs == (31u << 8)) {
+          if (cs - ip <= 1) {
+            err = 1;
+          } else {
+            dist = (L.rd(ip) << 8) + L.rd(ip + 1) + 8192;
+            ip += 2;
+          }
+        }
+        if (!err && (len > cap - op || dist > op)) err = 1;
+        if (!err) {
+          L.match(op, dist, len);
+          op += len;
+        }
+      }
+    } else {
+      const uint32_t run = ctrl + 1;
+      if (run > cap - op || run > cs - ip) {
+        err = 1;
+      } else {
+        L.lits(op, ip, run);
+        op += run;
+        ip += run;
+      }
+    }
+    if (err || ip >= cs) {
+      act = false;
+    } else {
+      ctrl = L.rd(ip++);
+    }
+  }
+  LZG_FINISH();
 }
 
 // blosclz (c-blosc 1.21 blosclz.c, blosclz_decompress; restated, checked against c-blosc in
@@ -874,9 +949,16 @@ hipError_t launch_blosc_decode(ZgItem *items, uint32_t *status, uint32_t n_items
   if (D.n_snappy)
     hipLaunchKernelGGL(k_snappy, dim3((uint32_t)D.n_sub), dim3(64), 0, s, D.subs, D.sub_status, D.sub_kind,
                        (uint32_t)D.n_sub, D.tmp, D.sub_slot);
-  if (D.n_blosclz)
+  if (D.n_blosclz && D.lz_list && ZG_LZM_G < 64) {
+    hipLaunchKernelGGL(k_lz_list, dim3(1), dim3(1024), 0, s, D.sub_kind, D.sub_status, (uint32_t)D.n_sub,
+                       (uint32_t)BL_KIND_BLOSCLZ, D.lz_list);
+    constexpr uint32_t NG = 64 / ZG_LZM_G;
+    hipLaunchKernelGGL(k_blosclzm<ZG_LZM_G>, dim3((uint32_t)((D.n_sub + NG - 1) / NG)), dim3(64), 0, s, D.subs,
+                       D.sub_status, D.lz_list, D.tmp, D.sub_slot);
+  } else if (D.n_blosclz) {
     hipLaunchKernelGGL(k_blosclz, dim3((uint32_t)D.n_sub), dim3(64), 0, s, D.subs, D.sub_status, D.sub_kind,
                        (uint32_t)D.n_sub, D.tmp, D.sub_slot);
+  }
   if (D.n_blk)
     hipLaunchKernelGGL(k_blosc_finish, dim3((uint32_t)D.n_blk), dim3(256), 0, s, D.blocks, D.subs, D.sub_status,
                        D.sub_kind, status, dst, slot_bytes, items, D.dout, D.geom, D.sc);

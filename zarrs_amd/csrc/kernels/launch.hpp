@@ -205,7 +205,7 @@ struct BlDecode {
   ZstdScratch zs;
   uint64_t n_sub, n_blk, n_zstd, n_lz4, n_blosclz, n_zlib, n_snappy;  // with a cached layout: capacities (n_* > 0 = launched)
   uint2 *zaux;            // zlib streams: {Adler-32 trailer, -} per stream
-  uint32_t *lz_list;      // lz4 streams: {count, stream indices} (k_lz_list), n_sub + 1 entries
+  uint32_t *lz_list;      // lz4 / blosclz streams: {count, stream indices} (k_lz_list), n_sub + 1 entries
   unsigned long long *ovf;  // set by k_blosc_layout when a cached layout is too small (ctl counter)
   // Direct output (dout non-null): blosc is the last stage and the scatter would copy whole chunks'
   // rows unchanged (rows kernel, no swap / shuffle / transpose, 16-B aligned rows; checked on the
