@@ -190,7 +190,9 @@ __global__ __launch_bounds__(64) void k_blosc_streams(ZgItem *items, uint32_t *s
           break;
         }
         const bool raw = (uint64_t)cs == ne;
-        subs[s0 + j] = ZgItem{it.src + (uint64_t)p, (uint64_t)cs, item, 0, 0, 0};
+        // bitshuffled blocks hold long literal runs and matches: decoded one stream per wave (BL_SUB_WIDE)
+        subs[s0 + j] = ZgItem{it.src + (uint64_t)p, (uint64_t)cs, item,
+                              (mode == 2 && I.comp != BL_COMP_ZSTD && I.comp != BL_COMP_ZLIB) ? BL_SUB_WIDE : 0u, 0, 0};
         sub_kind[s0 + j] = raw ? BL_KIND_RAW
                            : I.comp == BL_COMP_ZSTD ? BL_KIND_ZSTD
                            : I.comp == BL_COMP_LZ4  ? BL_KIND_LZ4
@@ -393,15 +395,17 @@ __global__ __launch_bounds__(64) void k_lz4(ZgItem *subs, uint32_t *sub_status, 
 #ifndef ZG_LZM_G
 #define ZG_LZM_G 32
 #endif
-__global__ __launch_bounds__(1024) void k_lz_list(const uint32_t *sub_kind, const uint32_t *sub_status,
-                                                  uint32_t n_sub, uint32_t kind, uint32_t *list) {
+__global__ __launch_bounds__(1024) void k_lz_list(const ZgItem *subs, const uint32_t *sub_kind,
+                                                  const uint32_t *sub_status, uint32_t n_sub, uint32_t kind,
+                                                  uint32_t wide, uint32_t *list) {
   __shared__ uint32_t wsum[16], s_base;
   const uint32_t t = threadIdx.x, w = t >> 6, l = t & 63;
   if (t == 0) s_base = 0;
   __syncthreads();
   for (uint32_t c = 0; c < n_sub; c += 1024) {
     const uint32_t i = c + t;
-    const bool f = i < n_sub && sub_kind[i] == kind && sub_status[i] == BL_SKIP;
+    const bool f = i < n_sub && sub_kind[i] == kind && sub_status[i] == BL_SKIP &&
+                   ((subs[i].flags & BL_SUB_WIDE) != 0) == (wide != 0);
     const uint64_t m = __ballot(f);
     if (l == 0) wsum[w] = (uint32_t)__builtin_popcountll(m);
     __syncthreads();
@@ -611,6 +615,86 @@ __global__ __launch_bounds__(64) void k_blosclzm(ZgItem *subs, uint32_t *sub_sta
       ctrl = L.rd(ip++);
     }
   }
+  LZG_FINISH();
+}
+
+// snappy (the format below, k_snappy), several streams per wave
+template <int G>
+__global__ __launch_bounds__(64) void k_snappym(ZgItem *subs, uint32_t *sub_status, const uint32_t *list,
+                                                uint8_t *dst, uint64_t slot) {
+  LZG_SETUP();
+  uint64_t want = 0;
+  // preamble: little-endian base-128 varint (<= 5 bytes, < 2^32)
+  for (uint32_t kk = 0; act; kk++) {
+    if (ip >= cs || kk == 5) { err = 1; break; }
+    const uint32_t b = L.rd(ip++);
+    want |= (uint64_t)(b & 127) << (7 * kk);
+    if (!(b & 128)) break;
+  }
+  if (act && !err && want > cap) err = 1;
+  if (err) act = false;
+  const uint32_t w32 = (uint32_t)want;
+  if (act && ip >= cs) act = false;  // no elements
+  while (__ballot(act)) {
+    if (!act) continue;
+    const uint32_t tag = L.rd(ip++);
+    if ((tag & 3) == 0) {  // literal
+      uint64_t len = (tag >> 2) + 1;
+      if (len > 60) {
+        const uint32_t nb = (uint32_t)len - 60;  // 1..4 length bytes
+        if (nb > cs - ip) {
+          err = 1;
+        } else {
+          uint64_t v = 0;
+          for (uint32_t q = 0; q < nb; q++) v |= (uint64_t)L.rd(ip + q) << (8 * q);
+          ip += nb;
+          len = v + 1;
+        }
+      }
+      if (!err && (len > cs - ip || len > w32 - op)) err = 1;
+      if (!err) {
+        L.lits(op, ip, (uint32_t)len);
+        ip += (uint32_t)len;
+        op += (uint32_t)len;
+      }
+    } else {
+      uint32_t len = 0;
+      uint64_t off = 0;
+      if ((tag & 3) == 1) {
+        if (cs - ip < 1) {
+          err = 1;
+        } else {
+          len = 4 + ((tag >> 2) & 7);
+          off = ((tag >> 5) << 8) | L.rd(ip);
+          ip += 1;
+        }
+      } else if ((tag & 3) == 2) {
+        if (cs - ip < 2) {
+          err = 1;
+        } else {
+          len = 1 + (tag >> 2);
+          off = L.rd(ip) | (L.rd(ip + 1) << 8);
+          ip += 2;
+        }
+      } else {
+        if (cs - ip < 4) {
+          err = 1;
+        } else {
+          len = 1 + (tag >> 2);
+          off = (uint64_t)L.rd(ip) | ((uint64_t)L.rd(ip + 1) << 8) | ((uint64_t)L.rd(ip + 2) << 16) |
+                ((uint64_t)L.rd(ip + 3) << 24);
+          ip += 4;
+        }
+      }
+      if (!err && (off == 0 || off > op || len > w32 - op)) err = 1;
+      if (!err) {
+        L.match(op, (uint32_t)off, len);
+        op += len;
+      }
+    }
+    if (err || ip >= cs) act = false;
+  }
+  if (have && !err && op != w32) err = 1;
   LZG_FINISH();
 }
 
@@ -932,11 +1016,16 @@ hipError_t launch_blosc_decode(ZgItem *items, uint32_t *status, uint32_t n_items
     if (e != hipSuccess) return e;
   }
   if (D.n_lz4 && D.lz_list && ZG_LZM_G < 64) {
-    hipLaunchKernelGGL(k_lz_list, dim3(1), dim3(1024), 0, s, D.sub_kind, D.sub_status, (uint32_t)D.n_sub,
-                       (uint32_t)BL_KIND_LZ4, D.lz_list);
+    uint32_t *wl = D.lz_list + D.n_sub + 1;  // the wide list
+    hipLaunchKernelGGL(k_lz_list, dim3(1), dim3(1024), 0, s, D.subs, D.sub_kind, D.sub_status, (uint32_t)D.n_sub,
+                       (uint32_t)BL_KIND_LZ4, 0u, D.lz_list);
+    hipLaunchKernelGGL(k_lz_list, dim3(1), dim3(1024), 0, s, D.subs, D.sub_kind, D.sub_status, (uint32_t)D.n_sub,
+                       (uint32_t)BL_KIND_LZ4, 1u, wl);
     constexpr uint32_t NG = 64 / ZG_LZM_G;
     hipLaunchKernelGGL(k_lz4m<ZG_LZM_G>, dim3((uint32_t)((D.n_sub + NG - 1) / NG)), dim3(64), 0, s, D.subs,
                        D.sub_status, D.lz_list, D.tmp, D.sub_slot);
+    hipLaunchKernelGGL(k_lz4m<64>, dim3((uint32_t)D.n_sub), dim3(64), 0, s, D.subs, D.sub_status, wl, D.tmp,
+                       D.sub_slot);
   } else if (D.n_lz4) {
     hipLaunchKernelGGL(k_lz4, dim3((uint32_t)D.n_sub), dim3(64), 0, s, D.subs, D.sub_status, D.sub_kind,
                        (uint32_t)D.n_sub, D.tmp, D.sub_slot);
@@ -946,15 +1035,32 @@ hipError_t launch_blosc_decode(ZgItem *items, uint32_t *status, uint32_t n_items
     if (e == hipSuccess) e = launch_adler32_check(D.subs, D.sub_status, D.sub_kind, (uint32_t)D.n_sub, D.zaux, s);
     if (e != hipSuccess) return e;
   }
-  if (D.n_snappy)
+  if (D.n_snappy && D.lz_list && ZG_LZM_G < 64) {
+    uint32_t *wl = D.lz_list + D.n_sub + 1;  // the wide list
+    hipLaunchKernelGGL(k_lz_list, dim3(1), dim3(1024), 0, s, D.subs, D.sub_kind, D.sub_status, (uint32_t)D.n_sub,
+                       (uint32_t)BL_KIND_SNAPPY, 0u, D.lz_list);
+    hipLaunchKernelGGL(k_lz_list, dim3(1), dim3(1024), 0, s, D.subs, D.sub_kind, D.sub_status, (uint32_t)D.n_sub,
+                       (uint32_t)BL_KIND_SNAPPY, 1u, wl);
+    constexpr uint32_t NG = 64 / ZG_LZM_G;
+    hipLaunchKernelGGL(k_snappym<ZG_LZM_G>, dim3((uint32_t)((D.n_sub + NG - 1) / NG)), dim3(64), 0, s, D.subs,
+                       D.sub_status, D.lz_list, D.tmp, D.sub_slot);
+    hipLaunchKernelGGL(k_snappym<64>, dim3((uint32_t)D.n_sub), dim3(64), 0, s, D.subs, D.sub_status, wl, D.tmp,
+                       D.sub_slot);
+  } else if (D.n_snappy) {
     hipLaunchKernelGGL(k_snappy, dim3((uint32_t)D.n_sub), dim3(64), 0, s, D.subs, D.sub_status, D.sub_kind,
                        (uint32_t)D.n_sub, D.tmp, D.sub_slot);
+  }
   if (D.n_blosclz && D.lz_list && ZG_LZM_G < 64) {
-    hipLaunchKernelGGL(k_lz_list, dim3(1), dim3(1024), 0, s, D.sub_kind, D.sub_status, (uint32_t)D.n_sub,
-                       (uint32_t)BL_KIND_BLOSCLZ, D.lz_list);
+    uint32_t *wl = D.lz_list + D.n_sub + 1;  // the wide list
+    hipLaunchKernelGGL(k_lz_list, dim3(1), dim3(1024), 0, s, D.subs, D.sub_kind, D.sub_status, (uint32_t)D.n_sub,
+                       (uint32_t)BL_KIND_BLOSCLZ, 0u, D.lz_list);
+    hipLaunchKernelGGL(k_lz_list, dim3(1), dim3(1024), 0, s, D.subs, D.sub_kind, D.sub_status, (uint32_t)D.n_sub,
+                       (uint32_t)BL_KIND_BLOSCLZ, 1u, wl);
     constexpr uint32_t NG = 64 / ZG_LZM_G;
     hipLaunchKernelGGL(k_blosclzm<ZG_LZM_G>, dim3((uint32_t)((D.n_sub + NG - 1) / NG)), dim3(64), 0, s, D.subs,
                        D.sub_status, D.lz_list, D.tmp, D.sub_slot);
+    hipLaunchKernelGGL(k_blosclzm<64>, dim3((uint32_t)D.n_sub), dim3(64), 0, s, D.subs, D.sub_status, wl, D.tmp,
+                       D.sub_slot);
   } else if (D.n_blosclz) {
     hipLaunchKernelGGL(k_blosclz, dim3((uint32_t)D.n_sub), dim3(64), 0, s, D.subs, D.sub_status, D.sub_kind,
                        (uint32_t)D.n_sub, D.tmp, D.sub_slot);

@@ -195,6 +195,7 @@ struct BlBlock {
   uint64_t out_off;  // in the item's decoded bytes
   uint32_t first_sub, nsplit, ne, mode, ts, ver;  // mode 0 none, 1 byte unshuffle, 2 bitunshuffle
 };
+constexpr uint32_t BL_SUB_WIDE = 0x80000000u;  // stream ZgItem flag: decode it with a whole wave
 struct BlDecode {
   const uint64_t *bases;  // per item {first stream, first block}
   ZgItem *subs;
@@ -205,7 +206,8 @@ struct BlDecode {
   ZstdScratch zs;
   uint64_t n_sub, n_blk, n_zstd, n_lz4, n_blosclz, n_zlib, n_snappy;  // with a cached layout: capacities (n_* > 0 = launched)
   uint2 *zaux;            // zlib streams: {Adler-32 trailer, -} per stream
-  uint32_t *lz_list;      // lz4 / blosclz streams: {count, stream indices} (k_lz_list), n_sub + 1 entries
+  uint32_t *lz_list;      // lz4 / blosclz / snappy streams: {count, stream indices} (k_lz_list), two lists of
+                          // n_sub + 1 entries: streams decoded two per wave, then bitshuffled ones (BL_SUB_WIDE)
   unsigned long long *ovf;  // set by k_blosc_layout when a cached layout is too small (ctl counter)
   // Direct output (dout non-null): blosc is the last stage and the scatter would copy whole chunks'
   // rows unchanged (rows kernel, no swap / shuffle / transpose, 16-B aligned rows; checked on the

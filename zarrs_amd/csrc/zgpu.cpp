@@ -852,7 +852,7 @@ static void blosc_stage(zgpu_plan &P, const Stage &st, uint8_t *out, hipStream_t
     D.tmp = (uint8_t *)P.grow(P.bl_tmp, D.n_sub * D.sub_slot);
   }
   if (D.n_zlib) D.zaux = (uint2 *)P.grow(P.bl_zaux, D.n_sub * sizeof(uint2));
-  D.lz_list = (D.n_lz4 || D.n_blosclz) ? (uint32_t *)P.grow(P.bl_lzl, (D.n_sub + 1) * 4) : nullptr;
+  D.lz_list = (D.n_lz4 || D.n_blosclz || D.n_snappy) ? (uint32_t *)P.grow(P.bl_lzl, 2 * (D.n_sub + 1) * 4) : nullptr;
   if (D.n_zstd) {
     uint64_t blk_bytes;
     zstd_scratch_layout(D.sub_slot, D.zs.blk_cap, blk_bytes, D.zs.lit_stride, D.zs.seq_cap);
