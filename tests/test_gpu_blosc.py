@@ -437,3 +437,60 @@ def test_blosc_snappy_streams(ctx, torch_cuda, ts, shuffle, split):
                 ch.decode_batch([make_desc(e, [4096 // ts])], np.zeros(4096 // ts, DT[ts]), [4096 // ts],
                                 enc_device=False)
             assert ei.value.status == L.CORRUPT_STREAM
+
+
+@pytest.mark.parametrize("cname,shuffle", [("lz4", "shuffle"), ("lz4", "bitshuffle"), ("blosclz", "shuffle"),
+                                           ("blosclz", "bitshuffle")])
+def test_blosc_lz_corrupt_stream_beside_good_ones(ctx, torch_cuda, cname, shuffle):
+    """Streams are decoded two per wave (k_lz4m / k_blosclzm, bitshuffled ones one per wave): a
+    stream that fails (a match before the output start) reports CORRUPT_STREAM for its own chunk
+    only, and the chunks decoded beside it in the same waves are exact (per-chunk statuses of
+    zgpu_decode_batch)."""
+    import ctypes as C
+    from zarrs_amd import CodecChain, make_desc
+    from zarrs_amd import _lib as L
+    from zarrs_amd.codec import default_stream
+    rng = np.random.default_rng(11)
+    n, nch, badk = 5000, 8, 3
+    codecs = [{"name": "bytes", "configuration": {"endian": "little"}}, _blosc(cname, shuffle, 4, 4096)]
+    co = O.OracleChain.from_metadata(codecs, "float32", 0, 1)
+    ch = CodecChain.from_metadata(codecs, "float32", 0, ctx)
+    data = [np.round(rng.standard_normal(n) * 10).astype(np.float32) for _ in range(nch)]
+    encs = [bytearray(co.encode(a)) for a in data]
+    e = encs[badk]
+    assert not e[2] & 0x2
+    nblk = (int.from_bytes(e[4:8], "little") + int.from_bytes(e[8:12], "little") - 1) // int.from_bytes(e[8:12], "little")
+    bsize = int.from_bytes(e[8:12], "little")
+    nsplit = 1 if e[2] & 0x10 else 4
+    hit = False
+    for b in range(nblk):  # the first compressed (not stored) stream of any full block
+        p = int.from_bytes(e[16 + 4 * b:20 + 4 * b], "little")
+        for _ in range(nsplit):
+            cs = int.from_bytes(e[p:p + 4], "little")
+            if cs != bsize // nsplit and not hit:
+                s0 = p + 4
+                if cname == "lz4":
+                    e[s0] = 0x0F  # no literals, then a match at output offset 0
+                else:
+                    r = (e[s0] & 31) + 1
+                    e[s0 + 1 + r] = 0xFF  # a match reaching 7937+ bytes back after <= 32 literals
+                hit = True
+            p += 4 + cs
+        if hit:
+            break
+    assert hit
+    keep = [torch_cuda.frombuffer(bytearray(x), dtype=torch_cuda.uint8).cuda() for x in encs]
+    descs = [make_desc(d, [n], out_start=[k * n]) for k, d in enumerate(keep)]
+    out = torch_cuda.zeros(nch * n, dtype=torch_cuda.float32, device="cuda")
+    arr = (L.ChunkDesc * nch)(*descs)
+    st = (C.c_int32 * nch)()
+    rc = L.load().zgpu_decode_batch(ch._h, 1, arr, nch, C.c_void_p(out.data_ptr()), L.u64s([nch * n]),
+                                    L.ENC_DEVICE | L.OUT_DEVICE, st, default_stream(None, out))
+    assert rc == L.CORRUPT_STREAM
+    got = out.cpu().numpy()
+    for k in range(nch):
+        if k == badk:
+            assert st[k] == L.CORRUPT_STREAM
+        else:
+            assert st[k] == 0, k
+            assert np.array_equal(got[k * n:(k + 1) * n], data[k]), k
