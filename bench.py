@@ -353,7 +353,10 @@ class C3:
                    {"name": "gzip", "configuration": {"level": 1}}, {"name": "crc32c"}],
         "index_codecs": [{"name": "bytes", "configuration": {"endian": "little"}}, {"name": "crc32c"}],
         "index_location": "end"}}]
-    kernel = "k_gzip"
+    # the roofline covers the step (k_shard_index, k_item_resolve, k_crc32c_strip, k_order_by_len,
+    # k_gzip ~96 %, k_scatter_rows); PMC counters summed over the step's dispatches
+    kernel = "C3 decode step (k_gzip ~96 % + k_shard_index/k_item_resolve/k_crc32c_strip/k_scatter_rows)"
+    pmc_regex = "zgpu::k_"
     dtype = "f32"
 
     def __init__(self, args, rank, world, dev):
@@ -398,9 +401,14 @@ class C3:
         syn.synth_c3_values(_u64(self.start), _u64(self.shape), exp.ctypes.data, nt)
         self.expected = torch.from_numpy(exp).to(dev)
         self.full = None
+        self.gather_s = []
         if world > 1 and rank == 0:  # the root decodes its slab in place inside the gathered subset
             self.full = torch.empty(self.SUB_SHAPE, dtype=torch.float32, device=dev)
             self.out = self.full.narrow(0, 0, self.shape[0])
+            ef = np.empty(self.SUB_SHAPE, np.float32)  # the whole subset: the root checks every slab
+            syn.synth_c3_values(_u64(self.SUB_START), _u64(self.SUB_SHAPE), ef.ctypes.data, nt)
+            self.expected_full = torch.from_numpy(ef).to(dev)
+            del ef
         else:
             self.out = torch.empty(self.shape, dtype=torch.float32, device=dev)
         self.out_shape = self.shape
@@ -424,13 +432,29 @@ class C3:
     def after_decode(self):
         if self.world > 1:  # C4: the requested subset spans GPUs -> one gather to the root
             from zarrs_amd.distributed import gather_slabs
+            torch.cuda.synchronize()
+            t0 = time.perf_counter()
             self.gathered = gather_slabs(self.out, self.slabs, dst=0, out=self.full)
+            torch.cuda.synchronize()
+            self.gather_s.append(time.perf_counter() - t0)
 
     def check(self) -> bool:
         ok = bool(torch.equal(self.out.view(torch.int32), self.expected.view(torch.int32)))
-        if self.gathered is not None:  # rank 0 holds the whole subset: its first slab is its own
-            ok = ok and bool(torch.equal(self.gathered[:self.shape[0]], self.out))
+        if self.gathered is not None:  # rank 0 holds the whole subset: every received slab is checked
+            from zarrs_amd.distributed import slab_mismatches
+            bad = slab_mismatches(self.gathered, self.expected_full, self.slabs)
+            if bad:
+                print(f"C4 check: slabs of ranks {bad} differ from the expected subset", file=sys.stderr)
+            ok = ok and not bad
         return ok
+
+    def gather_stats(self):
+        """The xGMI gather inside the step (N > 1): median wall time of the grouped P2P receives /
+        sends, and the bytes the root receives (every peer's slab)."""
+        if self.world == 1 or not self.gather_s:
+            return None
+        peer_bytes = sum(int(np.prod(sh)) * 4 for r, (_, sh) in enumerate(self.slabs) if r != 0)
+        return {"ms": float(np.median(self.gather_s)) * 1e3, "bytes_to_root": peer_bytes}
 
     def cpu_baseline(self):
         """The oracle's retrieve_array_subset of this rank's whole slab (the full C3 subset at N=1, all
@@ -516,31 +540,40 @@ class C3:
         """The drop-in boundary's real call pattern (rust/zarrs_gpu with its sharding_indexed plugin
         under zarrs' unchanged read path, array_read_ops_common.rs:173-176): zarrs calls the codec once
         per shard from its rayon workers (here a pool of the host's threads), each call synchronous,
-        host bytes in and host bytes out, and copies the result into the output view. A fully covered
-        shard is one zgpu_decode_batch of the sharded chain (its index verified); a partial shard
-        reads its index (a suffix range), then only the intersecting inner chunks, decoded in one
-        zgpu_decode_batch of the inner chain with crc32c stripped, not verified (the plugin's
-        GpuShardPartialDecoder). Calls on one context are serialised by the library."""
+        host bytes in and host bytes out. A fully covered shard is one decode of the sharded chain (its
+        index verified) into its window of the output array (ShardingCodecBound::decode_into,
+        sharding_codec.rs:617-707); a partial shard reads its index (a suffix range), then decodes only
+        the intersecting inner chunks through the inner chain, crc32c stripped, not verified (the
+        plugin's GpuShardPartialDecoder) into its window. Measured two ways: the plugin's calls with
+        ZGPU_COALESCE into their output windows (zgpu_decode_into: concurrent calls become one GPU
+        batch, rows placed straight into the array), and round 3's pattern (isolated calls into a
+        per-call buffer, copied into the array by the caller)."""
         from concurrent.futures import ThreadPoolExecutor
-        from zarrs_amd import _lib as L
         from zarrs_amd import CodecChain, make_desc
         S, I = self.SHARD, self.INNER
         inner = CodecChain.from_metadata(self.CODECS[0]["configuration"]["codecs"], "float32", 0.0, self.args.ctx)
         out = np.empty(self.shape, np.float32)
         cps = S // I
         n_idx = cps ** 3
+        expected = self.expected.cpu().numpy()
+        self.args.ctx.set_coalescing(window_us=200, max_calls=8)
 
-        def one(item):
+        def one(item, coalesce):
             (si, sj, sk), (_, host) = item
             org = [si * S, sj * S, sk * S]
             s0 = [max(a, o) for a, o in zip(self.start, org)]
             s1 = [min(a + b, o + S) for a, b, o in zip(self.start, self.shape, org)]
             sel = [b - a for a, b in zip(s0, s1)]
-            dst = tuple(slice(a - b, c - b) for a, c, b in zip(s0, s1, self.start))
-            if sel == [S] * 3:  # full shard: ShardingCodecBound::decode
-                buf = np.empty([S] * 3, np.float32)
-                self.chain.decode_batch([make_desc(host, [S] * 3)], buf, [S] * 3, enc_device=False)
-                out[dst] = buf
+            w0 = [a - b for a, b in zip(s0, self.start)]
+            dst = tuple(slice(a, a + n) for a, n in zip(w0, sel))
+            if sel == [S] * 3:  # full shard: ShardingCodecBound::decode_into
+                if coalesce:
+                    self.chain.decode_batch_into([make_desc(host, [S] * 3)], out, w0, sel, enc_device=False,
+                                                 coalesce=True)
+                else:
+                    buf = np.empty([S] * 3, np.float32)
+                    self.chain.decode_batch([make_desc(host, [S] * 3)], buf, [S] * 3, enc_device=False)
+                    out[dst] = buf
                 return
             # partial: index by a suffix range, then the intersecting inner chunks' byte ranges
             index = np.frombuffer(host[len(host) - (n_idx * 16 + 4):len(host) - 4].tobytes(), np.uint64).reshape(-1, 2)
@@ -557,21 +590,36 @@ class C3:
                         enc = None if off == 2 ** 64 - 1 else (host.ctypes.data + int(off), int(ln))
                         descs.append(make_desc(enc, [I] * 3, [a - c for a, c in zip(a0, c0)],
                                                [b - a for a, b in zip(a0, a1)], [a - b for a, b in zip(a0, s0)]))
-            buf = np.empty(sel, np.float32)
-            inner.decode_batch(descs, buf, sel, enc_device=False, validate_checksums=False)
-            out[dst] = buf
+            if coalesce:
+                inner.decode_batch_into(descs, out, w0, sel, enc_device=False, validate_checksums=False, coalesce=True)
+            else:
+                buf = np.empty(sel, np.float32)
+                inner.decode_batch(descs, buf, sel, enc_device=False, validate_checksums=False)
+                out[dst] = buf
 
         items = list(self.shards.items())
+        res = {"threads": _threads(), "calls": len(items)}
         with ThreadPoolExecutor(_threads()) as ex:
-            list(ex.map(one, items))  # warm-up
-            ok = bool(np.array_equal(out, self.expected.cpu().numpy()))
-            times = _time_reps(lambda: list(ex.map(one, items)), 5.0)
-        t = float(np.median(times))
-        return {"GiBps": round(out.nbytes / t / 2 ** 30, 2), "ms": round(t * 1e3, 1), "threads": _threads(),
-                "roundtrip_ok": ok, "calls": len(items),
-                "note": "one synchronous host-in/host-out zgpu_decode_batch per shard from a thread pool (the "
-                        "Rust plugin's pattern under zarrs' rayon loop), result copied into the output"}
-
+            for name, co in (("", True), ("uncoalesced_", False)):
+                out.fill(0)
+                list(ex.map(lambda it: one(it, co), items))  # warm-up
+                ok = bool(np.array_equal(out, expected))
+                st0 = self.args.ctx.coalescing_stats()
+                times = _time_reps(lambda: list(ex.map(lambda it: one(it, co), items)), 5.0)
+                st1 = self.args.ctx.coalescing_stats()
+                t = float(np.median(times))
+                res[name + "GiBps"] = round(out.nbytes / t / 2 ** 30, 2)
+                res[name + "ms"] = round(t * 1e3, 1)
+                res[name + "roundtrip_ok"] = ok
+                if co:
+                    nb = st1["batches"] - st0["batches"]
+                    res["coalesced_batches_per_pass"] = round(nb / len(times), 2)
+                    res["calls_per_batch"] = round((st1["calls"] - st0["calls"]) / max(1, nb), 2)
+        res["note"] = ("one synchronous host-in/host-out call per shard from a thread pool (the Rust plugin's pattern "
+                       "under zarrs' rayon loop); GiBps: ZGPU_COALESCE + zgpu_decode_into the output window "
+                       "(200 us collect window, <= 8 calls per batch); uncoalesced_GiBps: isolated "
+                       "zgpu_decode_batch calls into a per-call buffer copied into the output")
+        return res
 
 # ------------------------------------------------------------------------------------------------
 # C5
@@ -600,6 +648,12 @@ class C5:
         self.args, self.rank, self.world, self.dev = args, rank, world, dev
         sc = args.c5_scale
         shape0 = [self.L0[0], self.L0[1] // sc, self.L0[2] // sc]
+        self.chain = CodecChain.from_metadata(self.CODECS, "uint16", 0, args.ctx)
+        cache = getattr(args, "c5_cache", "")
+        if args.child and cache and os.path.exists(cache + ".json"):
+            # a rocprofv3 PMC pass: the parent's encoded frames, no data generation and no check
+            self._init_from_cache(cache, shape0, make_desc)
+            return
         syn = _synth()
         syn.synth_c5_level0.argtypes = [C.c_uint64] * 3 + [C.c_int] + [C.c_void_p] * 5 + [C.c_uint64, C.c_void_p,
                                                                                          C.c_int]
@@ -642,32 +696,61 @@ class C5:
         if syn.synth_shuffle_zstd_chunks(flat.ctypes.data, 2, offs.ctypes.data, lens.ctypes.data, n, 3, 0, nt,
                                          outs, olens):
             raise RuntimeError("zstd encode failed")
-        enc_sizes = [olens[i] for i in range(n)]
-        mine = lpt_partition(enc_sizes, world)[rank]
-        self.chain = CodecChain.from_metadata(self.CODECS, "uint16", 0, args.ctx)
-        self.outs = [torch.zeros(a.shape, dtype=torch.int16, device=dev) for a in levels]
-        self.expected = [torch.from_numpy(a.view(np.int16)).to(dev) for a in levels]
-        self.masks = [torch.zeros(a.shape, dtype=torch.bool, device=dev) for a in levels]
-        per_level = [[] for _ in levels]
+        enc_sizes = [int(olens[i]) for i in range(n)]
         # host copies of every encoded chunk (the CPU baseline decodes them all)
         self.enc_host = [np.ctypeslib.as_array((C.c_uint8 * olens[i]).from_address(outs[i])).copy()
                          for i in range(n)]
         for i in range(n):
             syn.synth_free(C.c_void_p(outs[i]))
+        self.levels_host = levels
+        self.all_chunks = chunks
+        self._setup(shape0, [list(a.shape) for a in levels], [(li, idx) for li, idx, _ in chunks], enc_sizes,
+                    make_desc, levels)
+
+    def _init_from_cache(self, path, shape0, make_desc):
+        meta = json.load(open(path + ".json"))
+        raw = np.fromfile(path + ".bin", dtype=np.uint8)
+        sizes = meta["enc_sizes"]
+        offs = np.concatenate([[0], np.cumsum(sizes)]).astype(np.int64)
+        self.enc_host = [raw[offs[i]:offs[i + 1]] for i in range(len(sizes))]
+        self.levels_host, self.all_chunks = None, None
+        self._setup(shape0, meta["level_shapes"], [(li, tuple(idx)) for li, idx in meta["chunks"]], sizes,
+                    make_desc, None)
+
+    def save_cache(self, path):
+        """The encoded frames and chunk table, for the rocprofv3 PMC passes' children (bench.py --child
+        --c5-cache): they profile the same frames without regenerating the pyramid."""
+        with open(path + ".bin", "wb") as f:
+            for e in self.enc_host:
+                f.write(memoryview(e))
+        json.dump({"level_shapes": self.level_shapes, "enc_sizes": self.enc_sizes,
+                   "chunks": [[li, list(idx)] for li, idx in self.chunk_meta]}, open(path + ".json", "w"))
+
+    def _setup(self, shape0, level_shapes, chunk_meta, enc_sizes, make_desc, levels):
+        from zarrs_amd.distributed import lpt_partition
+        dev, rank, world, sc = self.dev, self.rank, self.world, self.args.c5_scale
+        n = len(chunk_meta)
+        self.level_shapes, self.chunk_meta, self.enc_sizes = level_shapes, chunk_meta, enc_sizes
+        mine = lpt_partition(enc_sizes, world)[rank]
+        self.outs = [torch.zeros(s, dtype=torch.int16, device=dev) for s in level_shapes]
+        self.expected = None if levels is None else [torch.from_numpy(a.view(np.int16)).to(dev) for a in levels]
+        self.masks = [torch.zeros(s, dtype=torch.bool, device=dev) for s in level_shapes]
+        per_level = [[] for _ in level_shapes]
         mine = set(mine)
-        self.enc_bufs, enc_total, dec_total, all_bytes = [], 0, 0, 0
-        for i, (li, idx, blk) in enumerate(chunks):
-            cs, a = self.CHUNKS[li], levels[li]
+        self.enc_bufs, enc_total, dec_total, all_bytes, raw_bytes = [], 0, 0, 0, 0
+        for i, (li, idx) in enumerate(chunk_meta):
+            cs, shp = self.CHUNKS[li], level_shapes[li]
             start = [k * c for k, c in zip(idx, cs)]
-            sel = [min(c, s - st) for c, s, st in zip(cs, a.shape, start)]
+            sel = [min(c, s - st) for c, s, st in zip(cs, shp, start)]
             all_bytes += int(np.prod(sel)) * 2
+            raw_bytes += int(np.prod(cs)) * 2
             if i not in mine:
                 continue
             t = torch.from_numpy(self.enc_host[i]).to(dev)
             self.enc_bufs.append(t)
-            enc_total += olens[i]
+            enc_total += enc_sizes[i]
             dec_total += int(np.prod(sel)) * 2
-            per_level[li].append(make_desc((t.data_ptr(), olens[i]), cs, [0, 0, 0], sel, start))
+            per_level[li].append(make_desc((t.data_ptr(), enc_sizes[i]), cs, [0, 0, 0], sel, start))
             self.masks[li][tuple(slice(st, st + n_) for st, n_ in zip(start, sel))] = True
         # plans (chunk batches) and the streams they run on: the largest level is split in two halves
         # on streams of their own (its entropy-decode kernels are throughput-bound, its per-chunk
@@ -686,9 +769,7 @@ class C5:
         self.lanes = [ln for ln in self.lanes if ln]
         self.decoded_bytes = dec_total
         self.step_bytes = all_bytes
-        self.ratio = sum(int(x) for x in lens) / max(1, sum(enc_sizes))
-        self.levels_host = levels
-        self.all_chunks = chunks
+        self.ratio = raw_bytes / max(1, sum(enc_sizes))
         self.config = {"workload": f"C5: OME-Zarr-style u16 pyramid, 5 levels, L0 {shape0} (y/x scaled 1/{sc}), "
                                    "chunks [32,512,512] [64,256,256] [64,128,128] [64,64,64] [32,64,64], "
                                    "[bytes, numcodecs.shuffle{2}, zstd{3}]",
@@ -701,13 +782,14 @@ class C5:
         # N > 1: one cross-GPU L0 subset gathered to rank 0 in every step: the middle
         # [64, H/2, W/2] box of L0, whose chunks the LPT partition spreads over the ranks
         self.gathered = None
+        self.gather_s = []
         if world > 1:
             from zarrs_amd.distributed import chunk_boxes
             owner = {}
             for r, part in enumerate(lpt_partition(enc_sizes, world)):
                 for i in part:
                     owner[i] = r
-            lin0 = {idx: i for i, (li, idx, _) in enumerate(chunks) if li == 0}
+            lin0 = {idx: i for i, (li, idx) in enumerate(chunk_meta) if li == 0}
             self.g_start = [0, shape0[1] // 4, shape0[2] // 4]
             self.g_shape = [min(64, shape0[0]), shape0[1] // 2, shape0[2] // 2]
             self.g_boxes = [[] for _ in range(world)]
@@ -719,9 +801,21 @@ class C5:
     def after_decode(self):
         if self.world > 1:
             from zarrs_amd.distributed import gather_regions
+            torch.cuda.synchronize()
+            t0 = time.perf_counter()
             self.gathered = gather_regions(self.outs[0], self.g_boxes, self.g_start, self.g_shape)
+            torch.cuda.synchronize()
+            self.gather_s.append(time.perf_counter() - t0)
+
+    def gather_stats(self):
+        if self.world == 1 or not self.gather_s:
+            return None
+        peer_bytes = sum(int(np.prod(bs)) * 2 for r, boxes in enumerate(self.g_boxes) if r != 0 for _, bs in boxes)
+        return {"ms": float(np.median(self.gather_s)) * 1e3, "bytes_to_root": peer_bytes}
 
     def check(self) -> bool:
+        if self.expected is None:  # a PMC child on cached frames: the parent checked them
+            return True
         ok = True
         if self.gathered is not None:
             sl = tuple(slice(a, a + n) for a, n in zip(self.g_start, self.g_shape))
@@ -1160,17 +1254,39 @@ def run_gpu(args, rank, world, dev):
     for plan, _, _ in plans:
         lib.zgpu_plan_destroy(plan)
     host = W.host_leg(sp) if (args.host_leg and rank == 0) else None
+    gather = W.gather_stats() if hasattr(W, "gather_stats") else None
     return dict(W=W, elapsed=elapsed, ev_ms=ev_ms, alg_bytes=alg_bytes, ok=ok, batch_ms=batch_ms, host=host,
-                counters=counters, world_info=world_info(world, dev))
+                counters=counters, world_info=world_info(world, dev), gather=gather)
+
+
+XGMI_LINK_GBS = 153.0  # one MI355X xGMI link, per direction (/opt/skills/guides/MI355X_MICROARCH.md)
+
+
+def gather_report(r, world, dev):
+    """The gather to rank 0, reported apart from the decode: the max over ranks of
+    each rank's median gather time, the bytes rank 0 receives, and their rate against the direct
+    links into the root (one per peer, at most 7, 153 GB/s each)."""
+    if world == 1 or r.get("gather") is None:
+        return None
+    ms = torch.tensor([r["gather"]["ms"]], dtype=torch.float64, device=dev)
+    torch.distributed.all_reduce(ms, op=torch.distributed.ReduceOp.MAX)
+    t = float(ms.item())
+    nbytes = r["gather"]["bytes_to_root"]
+    peak = min(world - 1, 7) * XGMI_LINK_GBS
+    gbs = nbytes / (t * 1e-3) / 1e9 if t > 0 else 0.0
+    return {"gather_ms": round(t, 3), "bytes_to_root": nbytes, "xgmi_GBps": round(gbs, 1), "peak_GBps": peak,
+            "frac": round(gbs / peak, 4), "included_in_step": True,
+            "note": "grouped P2P receives into the root's output (RCCL over xGMI), timed inside the step"}
 
 
 def secondary_legs(args, rank, world, dev, r_primary):
     """The other §8(d) configs measured in the same run as the headline (C2): C3 (C4 at N > 1: the
     subset's axis-0 slabs gathered to rank 0 over RCCL inside the step) and C5 at --secondary-c5-scale
-    (LPT chunk partition, plus the cross-GPU L0 subset gather at N > 1). Each leg: value, ms/step,
-    the roofline frac of its dominant kernel / step (HIP events, algorithmic bytes), decode(encode(x))
-    == x on device, and (rank 0, N = 1) a short CPU baseline of the oracle. No PMC passes here (their
-    traffic figures are in profiles/)."""
+    (default 1: the full L0 [512,4096,4096]; LPT chunk partition, plus the cross-GPU L0 subset gather
+    at N > 1). Each leg: value, ms/step, the roofline frac of its step (HIP events, algorithmic bytes),
+    decode(encode(x)) == x on device, and (rank 0, N = 1) a short CPU baseline of the oracle, the
+    step's HBM traffic from two rocprofv3 PMC passes (C5's child profiles the parent's cached frames)
+    and, for C3, the drop-in boundary's per-shard call pattern (dropin_emulation)."""
     import copy
     import gc
     out = {}
@@ -1208,22 +1324,50 @@ def secondary_legs(args, rank, world, dev, r_primary):
                             "frac": round(achieved / HBM_PEAK_GBS, 4), "kernel": W.kernel,
                             "alg_bytes_per_launch": r["alg_bytes"],
                             "avg_launch_ms_hip_events": round(r["ev_ms"], 4),
-                            "traffic": None, "traffic_detail": "see profiles/ (PMC passes run for the headline only)"},
+                            "traffic": None, "traffic_detail": "skipped (--no-pmc or N>1)"},
                "roundtrip_ok": bool(okt.item())}
         if r["counters"][L_CTR_ZSTD_SERIAL] or r["counters"][L_CTR_ZSTD_PARALLEL]:
             leg["zstd_items_per_step"] = {"block_parallel": r["counters"][L_CTR_ZSTD_PARALLEL],
                                           "serial_fallback": r["counters"][L_CTR_ZSTD_SERIAL]}
+        g = gather_report(r, world, dev)
+        if g:
+            leg["gather"] = g
         if rank == 0 and world == 1 and not args.no_cpu:
             try:
                 leg["cpu_baseline"] = W.cpu_baseline()
             except Exception as e:  # noqa: BLE001
                 leg["cpu_baseline"] = {"error": repr(e)[:300]}
-        leg["leg_seconds"] = round(time.perf_counter() - t_leg, 1)
-        out[name] = leg
+        if name == "c3" and rank == 0 and world == 1 and args.host_leg:
+            try:  # the drop-in boundary's own rate (per-shard calls from a thread pool), same data
+                leg["dropin_emulation"] = W.dropin_leg()
+            except Exception as e:  # noqa: BLE001
+                leg["dropin_emulation"] = {"error": repr(e)[:300]}
+        pmc = rank == 0 and world == 1 and not args.no_pmc
+        cache = None
+        if pmc and hasattr(W, "save_cache"):
+            import tempfile
+            cache = os.path.join(tempfile.mkdtemp(prefix="zgpu_c5_", dir=os.environ.get("TMPDIR", "/tmp")), "frames")
+            W.save_cache(cache)
+        import types
+        meta = types.SimpleNamespace(**{k: getattr(W, k) for k in ("kernel", "pmc_regex") if hasattr(W, k)})
         r["W"] = W = None
         a.ctx.close()
         gc.collect()
         torch.cuda.empty_cache()
+        if pmc:  # HBM traffic of the leg's step: two rocprofv3 --pmc passes of a child on the same data
+            a.c5_cache = cache or ""
+            try:
+                traffic, note = pmc_traffic(a, meta)
+            finally:
+                if cache:
+                    import shutil
+                    shutil.rmtree(os.path.dirname(cache), ignore_errors=True)
+            leg["roofline"]["traffic"] = traffic["bytes"] if traffic else None
+            leg["roofline"]["traffic_detail"] = traffic or note
+            if traffic:
+                leg["roofline"]["traffic_over_alg"] = round(traffic["bytes"] / r["alg_bytes"], 3)
+        leg["leg_seconds"] = round(time.perf_counter() - t_leg, 1)
+        out[name] = leg
         if world > 1:
             torch.distributed.barrier()
     return out
@@ -1256,7 +1400,8 @@ def pmc_traffic(args, W):
                    "--output-format", "csv", "--", sys.executable, os.path.abspath(__file__), "--child",
                    "--workload", args.workload, "--steps", str(steps), "--warmup", str(warm), "--no-cpu",
                    "--grid", *map(str, args.grid), "--c5-scale", str(args.c5_scale)] + \
-                  (["--lane-priorities", args.lane_priorities] if args.lane_priorities else [])
+                  (["--lane-priorities", args.lane_priorities] if args.lane_priorities else []) + \
+                  (["--c5-cache", args.c5_cache] if getattr(args, "c5_cache", "") else [])
             # the child's stderr goes to a file; a heartbeat on ours shows the pass is alive
             elog = os.path.join(tmp, ctr + ".err")
             t0 = time.time()
@@ -1317,7 +1462,13 @@ def launch_workers(args):
         port = so.getsockname()[1]
     cmd = launcher_cmd(args, sys.argv[1:], port)
     if args.dry_launch:
-        print(json.dumps({"launch": cmd, "visible_devices": n_dev}))
+        print(json.dumps({"launch": cmd, "visible_devices": n_dev, "fields_at_n_gt_1": {
+            "value": "units all ranks processed per step / the max over ranks of the step time",
+            "roundtrip_ok": "MIN over ranks; the root checks EVERY received slab (C3/C4, slab_mismatches) and the "
+                            "gathered L0 box (C5) against the synthesised values, plus its own decode",
+            "gather": "gather_ms (max over ranks of the median in-step gather time), bytes_to_root, xgmi_GBps, "
+                      "peak_GBps = min(N-1, 7) x 153 GB/s direct links into the root, frac",
+            "world": "backend, world_size and every rank's device"}}))
         return 0
     if n_dev < args.gpus:
         print(f"bench.py: --gpus {args.gpus} but {n_dev} GPU(s) visible", file=sys.stderr)
@@ -1350,7 +1501,8 @@ def main():
     ap.add_argument("--secondary", default="c3,c5",
                     help="workloads measured after the headline and reported in its line's `secondary` object "
                          "(comma-separated; '' for none)")
-    ap.add_argument("--secondary-c5-scale", type=int, default=2,
+    ap.add_argument("--c5-cache", default="", help=argparse.SUPPRESS)
+    ap.add_argument("--secondary-c5-scale", type=int, default=1,
                     help="C5 scale of the secondary leg (L0 y/x divided by this)")
     ap.add_argument("--dry-launch", action="store_true",
                     help="print the launcher command --gpus N > 1 would start, and exit (no GPU touched)")
@@ -1386,6 +1538,7 @@ def main():
         torch.distributed.all_reduce(ok, op=torch.distributed.ReduceOp.MIN)
     t = float(elapsed.item())
     value = W.step_bytes * args.steps / t / 2 ** 30
+    gather = gather_report(r, world, dev)
     cpu = W.cpu_baseline() if (rank == 0 and not args.no_cpu) else None
     traffic, traffic_note = None, "skipped (--no-pmc or N>1)"
     if rank == 0 and world == 1 and not args.no_pmc:
@@ -1423,6 +1576,8 @@ def main():
         if r["counters"][L_CTR_ZSTD_SERIAL] or r["counters"][L_CTR_ZSTD_PARALLEL]:
             line["zstd_items_per_step"] = {"block_parallel": r["counters"][L_CTR_ZSTD_PARALLEL],
                                            "serial_fallback": r["counters"][L_CTR_ZSTD_SERIAL]}
+        if gather:
+            line["gather"] = gather
     sec = secondary_legs(args, rank, world, dev, r) if args.secondary and not args.child else None
     if rank == 0:
         if sec:

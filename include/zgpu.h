@@ -159,6 +159,50 @@ int zgpu_decode_batch(zgpu_chain *chain, uint32_t ndim, const zgpu_chunk_desc *d
                       int32_t *status, void *hip_stream);
 
 /*
+ * The output of a decode as a window of a larger C-order array: ArrayBytesDecodeIntoTarget /
+ * ArrayBytesFixedDisjointView (zarrs_codec/src/array_bytes_fixed_disjoint_view.rs:12-207, the
+ * target of CodecChainBound::decode_into, codec_chain.rs:592-646, and of
+ * ShardingCodecBound::decode_into, sharding_codec.rs:617-707): base points at element [0,...,0] of
+ * an array of array_shape; the view is the box [start, start + shape). Descriptors' out_start are
+ * relative to the view (as with zgpu_decode_batch's out_shape = shape). Bytes of the array outside
+ * the parts of the view the descriptors cover are never written.
+ */
+typedef struct {
+  void *base;
+  uint64_t array_shape[ZGPU_MAX_DIMS];
+  uint64_t start[ZGPU_MAX_DIMS];
+  uint64_t shape[ZGPU_MAX_DIMS];
+} zgpu_out_view;
+
+/* Concurrent-call coalescing (host inputs and host output only; ignored otherwise): calls carrying
+ * this flag on the same chain, with the same flags and ndim, that arrive within the context's
+ * collect window are decoded as ONE batch -- one packed H2D copy of their encoded bytes, one launch
+ * sequence over all their chunks, one D2H copy -- and each caller gets its own statuses, its own
+ * first-error return value and its own output window. This turns zarrs' per-shard decode_into calls
+ * from rayon workers (array_read_ops_common.rs:173-176, sharding_codec.rs:617-707) into GPU-sized
+ * batches without changing the read path. */
+#define ZGPU_COALESCE 0x20u
+
+/*
+ * zgpu_decode_batch into a window of a larger array (host or device, ZGPU_OUT_DEVICE). A device
+ * window is decoded in place (the scatter writes through the whole array's strides). A host window is
+ * decoded into HBM and copied back box-wise (only the window's bytes cross PCIe; rows are placed by
+ * host threads from pinned staging). Same statuses and return value as zgpu_decode_batch.
+ */
+int zgpu_decode_into(zgpu_chain *chain, uint32_t ndim, const zgpu_chunk_desc *descs, uint64_t n,
+                     const zgpu_out_view *view, uint32_t flags, int32_t *status, void *hip_stream);
+
+/*
+ * Coalescing policy of a context (ZGPU_COALESCE): a call waits at most window_us for other calls
+ * to join its batch; a batch closes early at max_calls calls or max_bytes encoded bytes. Defaults:
+ * 200 us, 8 calls, 1 GiB (env ZGPU_COALESCE_US / ZGPU_COALESCE_CALLS / ZGPU_COALESCE_BYTES).
+ * Batches of one context run concurrently on its lanes.
+ */
+int zgpu_ctx_set_coalescing(zgpu_ctx *ctx, uint32_t window_us, uint32_t max_calls, uint64_t max_bytes);
+/* Coalescing statistics of a context since its creation: batches executed and calls they carried. */
+int zgpu_ctx_coalescing_stats(const zgpu_ctx *ctx, uint64_t *batches, uint64_t *calls);
+
+/*
  * Prepared form of zgpu_decode_batch for device-resident inputs that are decoded repeatedly
  * (benchmarks, hipGraph capture): the descriptor table is planned and uploaded once. Plans take
  * fused chains and one chunk shape only (see zgpu_decode_batch); others -> ZGPU_UNSUPPORTED.

@@ -27,6 +27,8 @@ def test_gpus_n_launches_n_workers():
     # the workers get the same flags (so each asserts WORLD_SIZE == --gpus)
     tail = cmd[cmd.index(BENCH) + 1:]
     assert tail == ["--gpus", "4", "--workload", "c3", "--steps", "3"]
+    fields = json.loads(r.stdout.strip().splitlines()[-1])["fields_at_n_gt_1"]
+    assert {"roundtrip_ok", "gather", "value"} <= set(fields)
 
 
 def test_world_size_mismatch_refused():

@@ -14,6 +14,7 @@ import torch.multiprocessing as mp
 
 import oracle as O
 from zarrs_amd.distributed import (_contiguous_in, chunk_boxes, gather_regions, gather_slabs, lpt_partition,
+                                   slab_mismatches,
                                    retrieve_array_subset_distributed, slab_partition)
 
 CODECS = [{"name": "bytes", "configuration": {"endian": "little"}}, {"name": "crc32c"}]
@@ -139,6 +140,44 @@ def _subgroup_worker(rank, world, port, q):
         dist.destroy_process_group()
 
 
+def _verify_worker(rank, world, port, q):
+    """bench.py's N > 1 check (C3/C4): the root compares EVERY received slab with the expected subset,
+    not only its own, and the verdict (roundtrip_ok) is the MIN over ranks. Rank 1 corrupts one
+    element of its slab: the root names slab 1 and every rank sees roundtrip_ok false. Also a gather
+    into a non-contiguous root output (a transposed view), which is received through a temporary."""
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        res = {}
+        shape = [13, 7, 5]
+        full = torch.arange(int(np.prod(shape)), dtype=torch.float32).reshape(shape) * 0.25 - 3
+        slabs = slab_partition([0, 0, 0], shape, world)
+        for corrupt in (False, True):
+            s0, sh = slabs[rank]
+            local = full[s0[0]:s0[0] + sh[0]].clone()
+            if corrupt and rank == 1:
+                local[1, 2, 3] += 1.0
+            got = gather_slabs(local, slabs, dst=0)
+            ok = torch.tensor([1], dtype=torch.int32)
+            if rank == 0:
+                bad = slab_mismatches(got, full, slabs)
+                res[f"bad_{corrupt}"] = bad
+                ok[0] = 0 if bad else 1
+            dist.all_reduce(ok, op=dist.ReduceOp.MIN)
+            res[f"roundtrip_ok_{corrupt}"] = bool(ok.item())
+        # non-contiguous root output
+        s0, sh = slabs[rank]
+        local = full[s0[0]:s0[0] + sh[0]].clone()
+        out = torch.empty([shape[2], shape[1], shape[0]]).permute(2, 1, 0) if rank == 0 else None
+        got = gather_slabs(local, slabs, dst=0, out=out)
+        if rank == 0:
+            res["noncontig"] = got is out and bool(torch.equal(out, full))
+        q.put((rank, res))
+    finally:
+        dist.destroy_process_group()
+
+
 def _spawn(target, world):
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
@@ -201,3 +240,12 @@ def test_contiguous_box_rule():
     assert _contiguous_in([1, 3, 8], [6, 8, 8])
     assert not _contiguous_in([1, 3, 7], [6, 8, 8])
     assert not _contiguous_in([2, 4, 8], [6, 8, 8])
+
+
+def test_world3_root_verifies_every_slab():
+    out = _spawn(_verify_worker, 3)
+    assert out[0]["bad_False"] == [] and out[0]["bad_True"] == [1]
+    for r in range(3):
+        assert out[r]["roundtrip_ok_False"] is True
+        assert out[r]["roundtrip_ok_True"] is False
+    assert out[0]["noncontig"]

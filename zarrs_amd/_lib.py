@@ -27,6 +27,7 @@ OUT_DEVICE = 0x2
 ONE_STREAM = 0x10
 NO_VALIDATE = 0x4
 DIRECT_IO = 0x8
+COALESCE = 0x20
 WHOLE = (1 << 64) - 1  # zgpu_file_range.len: to the end of the file
 
 # every symbol include/zgpu.h declares (tests/test_abi.py checks the .so exports all of them)
@@ -38,7 +39,8 @@ EXPORTS = [
     "zgpu_chain_encoded_size", "zgpu_encode_batch", "zgpu_plan_counters", "zgpu_last_counters",
     "zgpu_last_size_mismatch", "zgpu_cache_create", "zgpu_cache_destroy", "zgpu_cache_clear", "zgpu_cache_stats",
     "zgpu_cache_retrieve_array_subset", "zgpu_retrieve_array_subset_dlpack", "zgpu_chain_encoded_bound",
-    "zgpu_encode_chunks", "zgpu_retrieve_array_subset_multi",
+    "zgpu_encode_chunks", "zgpu_retrieve_array_subset_multi", "zgpu_decode_into", "zgpu_ctx_set_coalescing",
+    "zgpu_ctx_coalescing_stats",
 ]
 CTR_ENC_BYTES, CTR_ZSTD_SERIAL, CTR_ZSTD_PARALLEL, CTR_BLOSC_RERUN = range(4)
 N_COUNTERS = 4
@@ -52,6 +54,16 @@ class ChunkDesc(C.Structure):
         ("sel_start", C.c_uint64 * MAX_DIMS),
         ("sel_shape", C.c_uint64 * MAX_DIMS),
         ("out_start", C.c_uint64 * MAX_DIMS),
+    ]
+
+
+class OutView(C.Structure):
+    """zgpu_out_view: the box [start, start + shape) of a C-order array of array_shape at base."""
+    _fields_ = [
+        ("base", C.c_void_p),
+        ("array_shape", C.c_uint64 * MAX_DIMS),
+        ("start", C.c_uint64 * MAX_DIMS),
+        ("shape", C.c_uint64 * MAX_DIMS),
     ]
 
 
@@ -120,6 +132,10 @@ def load() -> C.CDLL:
     L.zgpu_chain_element_size.argtypes = [vp]
     L.zgpu_decode_batch.argtypes = [vp, u32, C.POINTER(ChunkDesc), u64, vp, P64, u32,
                                     C.POINTER(C.c_int32), vp]
+    L.zgpu_decode_into.argtypes = [vp, u32, C.POINTER(ChunkDesc), u64, C.POINTER(OutView), u32,
+                                   C.POINTER(C.c_int32), vp]
+    L.zgpu_ctx_set_coalescing.argtypes = [vp, u32, u32, u64]
+    L.zgpu_ctx_coalescing_stats.argtypes = [vp, P64, P64]
     L.zgpu_plan_create.argtypes = [vp, u32, C.POINTER(ChunkDesc), u64, P64, u32, C.POINTER(vp)]
     L.zgpu_plan_execute.argtypes = [vp, vp, C.POINTER(C.c_int32), vp]
     L.zgpu_plan_status.argtypes = [vp, C.POINTER(C.c_int32), vp]

@@ -61,6 +61,15 @@ class Context:
             cls._default[device] = cls(device)
         return cls._default[device]
 
+    def set_coalescing(self, window_us: int = 200, max_calls: int = 8, max_bytes: int = 1 << 30):
+        """Collect window / batch caps of ZGPU_COALESCE calls on this context (zgpu_ctx_set_coalescing)."""
+        L.check(L.load().zgpu_ctx_set_coalescing(self._h, int(window_us), int(max_calls), int(max_bytes)))
+
+    def coalescing_stats(self) -> dict:
+        b, c = C.c_uint64(), C.c_uint64()
+        L.check(L.load().zgpu_ctx_coalescing_stats(self._h, C.byref(b), C.byref(c)))
+        return {"batches": b.value, "calls": c.value}
+
     def close(self):
         if getattr(self, "_h", None):
             L.load().zgpu_ctx_destroy(self._h)
@@ -173,6 +182,31 @@ class CodecChain:
         stream = default_stream(stream, out, *[getattr(d, "_keep", None) for d in descs])
         rc = L.load().zgpu_decode_batch(self._h, len(out_shape), arr, n, op, L.u64s(out_shape),
                                         flags, st, stream)
+        statuses = [st[i] for i in range(n)]
+        if rc:
+            raise L.ZgpuError(rc, L.last_error())
+        return statuses
+
+    def decode_batch_into(self, descs: Sequence[L.ChunkDesc], array, view_start, view_shape, enc_device: bool,
+                          validate_checksums: bool | None = None, coalesce: bool = False, stream=None) -> list:
+        """decode_into a window of a larger array (ArrayBytesFixedDisjointView; zgpu_decode_into):
+        `array` is the whole C-order output (numpy array or torch tensor), the window the box
+        [view_start, view_start + view_shape); descriptors' out_start are relative to the window.
+        coalesce: ZGPU_COALESCE (concurrent host-in/host-out calls share one GPU batch)."""
+        n = len(descs)
+        arr = (L.ChunkDesc * max(n, 1))(*descs)
+        arr._keep = [getattr(d, "_keep", None) for d in descs]
+        st = (C.c_int32 * max(n, 1))()
+        op, _, odev, _ = _ptr_len(array)
+        v = L.OutView()
+        v.base = op
+        for d, (a, s0, s1) in enumerate(zip(array.shape, view_start, view_shape)):
+            v.array_shape[d], v.start[d], v.shape[d] = int(a), int(s0), int(s1)
+        flags = (L.ENC_DEVICE if enc_device else 0) | (L.OUT_DEVICE if odev else 0) | (L.COALESCE if coalesce else 0)
+        if validate_checksums is False:
+            flags |= L.NO_VALIDATE
+        stream = default_stream(stream, array, *[getattr(d, "_keep", None) for d in descs])
+        rc = L.load().zgpu_decode_into(self._h, len(view_shape), arr, n, C.byref(v), flags, st, stream)
         statuses = [st[i] for i in range(n)]
         if rc:
             raise L.ZgpuError(rc, L.last_error())

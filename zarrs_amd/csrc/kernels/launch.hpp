@@ -43,6 +43,15 @@ hipError_t launch_scatter(const ZgItem *items, const uint64_t *geom, uint32_t *s
                           hipStream_t s);
 uint64_t scatter_units_per_item(uint32_t mode, const ZgScatter &P, const uint64_t *max_sel_shape);
 
+// Box copy between device arrays: run r (C order over the `outer` axes of `shape`) is run_bytes
+// contiguous bytes at src_base + sum(c_d * src_stride[d]) -> dst_base + sum(c_d * dst_stride[d]).
+struct ZgBoxCopy {
+  uint32_t outer, pad0;
+  uint64_t shape[ZG_MAXD], src_stride[ZG_MAXD], dst_stride[ZG_MAXD];
+  uint64_t src_base, dst_base, run_bytes, n_runs;
+};
+hipError_t launch_box_copy(const uint8_t *src, uint8_t *dst, const ZgBoxCopy &P, hipStream_t s);
+
 // crc32c (Castagnoli) verify + strip of a 4-byte LE checksum at the start or end of each item.
 // verify: 0 never, 1 unless the item is on the partial path.
 hipError_t launch_crc32c_strip(ZgItem *items, uint32_t *status, uint32_t n_items, int at_start, int verify,

@@ -489,3 +489,44 @@ uint64_t scatter_units_per_item(uint32_t mode, const ZgScatter &P, const uint64_
 }
 
 }  // namespace zgpu
+
+namespace zgpu {
+
+// Box copy between two device arrays (coalesced calls: a caller's window of the batch's stacked
+// output packed into its compact layout before the one D2H copy). One wave per contiguous run; 16-B
+// lanes when both runs and their length allow it, else 4-B, else bytes.
+__global__ __launch_bounds__(256) void k_box_copy(const uint8_t *__restrict__ src, uint8_t *__restrict__ dst,
+                                                   ZgBoxCopy P) {
+  const uint32_t lane = threadIdx.x & 63;
+  const uint64_t waves = (uint64_t)gridDim.x * (blockDim.x >> 6);
+  for (uint64_t r = (uint64_t)blockIdx.x * (blockDim.x >> 6) + (threadIdx.x >> 6); r < P.n_runs; r += waves) {
+    uint64_t k = r, so = 0, dof = 0;
+    for (int d = (int)P.outer - 1; d >= 0; d--) {
+      const uint64_t c = k % P.shape[d];
+      k /= P.shape[d];
+      so += c * P.src_stride[d];
+      dof += c * P.dst_stride[d];
+    }
+    const uint8_t *s = src + P.src_base + so;
+    uint8_t *t = dst + P.dst_base + dof;
+    const uint64_t n = P.run_bytes;
+    if ((((uintptr_t)s | (uintptr_t)t | n) & 15) == 0) {
+      for (uint64_t i = (uint64_t)lane * 16; i < n; i += 64 * 16)
+        *(uint4 *)(t + i) = *(const uint4 *)(s + i);
+    } else if ((((uintptr_t)s | (uintptr_t)t | n) & 3) == 0) {
+      for (uint64_t i = (uint64_t)lane * 4; i < n; i += 64 * 4)
+        *(uint32_t *)(t + i) = *(const uint32_t *)(s + i);
+    } else {
+      for (uint64_t i = lane; i < n; i += 64) t[i] = s[i];
+    }
+  }
+}
+
+hipError_t launch_box_copy(const uint8_t *src, uint8_t *dst, const ZgBoxCopy &P, hipStream_t s) {
+  if (!P.n_runs || !P.run_bytes) return hipSuccess;
+  const uint64_t blocks = std::min<uint64_t>((P.n_runs + 3) / 4, (uint64_t)device_cu_count() * 16);
+  hipLaunchKernelGGL(k_box_copy, dim3((uint32_t)blocks), dim3(256), 0, s, src, dst, P);
+  return hipGetLastError();
+}
+
+}  // namespace zgpu

@@ -150,4 +150,128 @@ hipError_t d2h_bytes(uint8_t *dst, const uint8_t *src, uint64_t n, uint8_t *stag
   return e;
 }
 
+// ------------------------------------------------------------------------------------------------
+// Boxes of a larger array (ArrayBytesFixedDisjointView, array_bytes_fixed_disjoint_view.rs:177-206:
+// one memcpy per contiguous run of the view's subset)
+// ------------------------------------------------------------------------------------------------
+bool box_is_whole(uint32_t nd, const uint64_t *array_shape, const uint64_t *start, const uint64_t *shape) {
+  for (uint32_t d = 0; d < nd; d++)
+    if (start[d] != 0 || shape[d] != array_shape[d]) return false;
+  return true;
+}
+
+BoxRuns box_runs(uint32_t nd, const uint64_t *array_shape, const uint64_t *start, const uint64_t *shape, uint32_t es) {
+  BoxRuns R;
+  uint64_t stride[8];
+  uint64_t s = es;
+  for (int d = (int)nd - 1; d >= 0; d--) {
+    stride[d] = s;
+    s *= array_shape[d];
+  }
+  for (uint32_t d = 0; d < nd; d++) R.base += start[d] * stride[d];
+  // the run: the innermost axis plus every outer axis the box spans whole, up to (and including) the
+  // first axis it does not
+  int j = (int)nd - 1;
+  uint64_t run = shape[j] * es;
+  while (j > 0 && shape[j] == array_shape[j]) {
+    j--;
+    run *= shape[j];
+  }
+  R.run_bytes = run;
+  R.outer = (uint32_t)j;
+  R.n_runs = 1;
+  for (int d = 0; d < j; d++) {
+    R.shape[d] = shape[d];
+    R.stride[d] = stride[d];
+    R.n_runs *= shape[d];
+  }
+  if (run == 0) R.n_runs = 0;
+  return R;
+}
+
+uint64_t BoxRuns::offset(uint64_t k) const {
+  uint64_t off = base;
+  for (int d = (int)outer - 1; d >= 0; d--) {
+    off += (k % shape[d]) * stride[d];
+    k /= shape[d];
+  }
+  return off;
+}
+
+void copy_box_runs(const BoxRuns &R, uint8_t *array, uint8_t *compact, uint64_t lo, uint64_t hi, bool to_array,
+                   int threads) {
+  if (hi <= lo || !R.run_bytes) return;
+  const uint64_t k0 = lo / R.run_bytes, k1 = (hi - 1) / R.run_bytes + 1;
+  auto work = [&](uint64_t a, uint64_t b) {
+    for (uint64_t k = a; k < b; k++) {
+      const uint64_t r0 = std::max(lo, k * R.run_bytes), r1 = std::min(hi, (k + 1) * R.run_bytes);
+      uint8_t *arr = array + R.offset(k) + (r0 - k * R.run_bytes);
+      uint8_t *cmp = compact + (r0 - lo);
+      if (to_array)
+        std::memcpy(arr, cmp, r1 - r0);
+      else
+        std::memcpy(cmp, arr, r1 - r0);
+    }
+  };
+  const uint64_t nk = k1 - k0;
+  if (threads <= 1 || hi - lo < (4u << 20) || nk < 2) {
+    work(k0, k1);
+    return;
+  }
+  const uint64_t nt = std::min<uint64_t>((uint64_t)threads, nk);
+  std::vector<std::thread> pool;
+  pool.reserve(nt);
+  for (uint64_t t = 0; t < nt; t++) pool.emplace_back(work, k0 + nk * t / nt, k0 + nk * (t + 1) / nt);
+  for (auto &th : pool) th.join();
+}
+
+hipError_t d2h_box(const BoxRuns &R, uint8_t *host_array, const uint8_t *dev_compact, uint8_t *stage,
+                   uint64_t slab_bytes, int threads, hipStream_t s) {
+  const uint64_t n = R.n_runs * R.run_bytes;
+  if (R.n_runs == 1) return d2h_bytes(host_array + R.base, dev_compact, n, stage, slab_bytes, threads, s);
+  hipError_t e;
+  hipEvent_t done[2] = {nullptr, nullptr};
+  for (int k = 0; k < 2; k++)
+    if ((e = hipEventCreateWithFlags(&done[k], hipEventDisableTiming)) != hipSuccess) return e;
+  const uint64_t nslabs = (n + slab_bytes - 1) / slab_bytes;
+  auto issue = [&](uint64_t k) {
+    const uint64_t o = k * slab_bytes, len = std::min(slab_bytes, n - o);
+    hipError_t r = hipMemcpyAsync(stage + (k & 1) * slab_bytes, dev_compact + o, len, hipMemcpyDeviceToHost, s);
+    if (r == hipSuccess) r = hipEventRecord(done[k & 1], s);
+    return r;
+  };
+  e = nslabs ? issue(0) : hipSuccess;
+  for (uint64_t k = 0; k < nslabs && e == hipSuccess; k++) {
+    if (k + 1 < nslabs && (e = issue(k + 1)) != hipSuccess) break;
+    if ((e = hipEventSynchronize(done[k & 1])) != hipSuccess) break;
+    const uint64_t o = k * slab_bytes, len = std::min(slab_bytes, n - o);
+    copy_box_runs(R, host_array, stage + (k & 1) * slab_bytes, o, o + len, true, threads);
+  }
+  for (int k = 0; k < 2; k++) (void)hipEventDestroy(done[k]);
+  return e;
+}
+
+hipError_t h2d_box(const BoxRuns &R, uint8_t *dev_compact, const uint8_t *host_array, uint8_t *stage,
+                   uint64_t slab_bytes, int threads, hipStream_t s) {
+  const uint64_t n = R.n_runs * R.run_bytes;
+  if (R.n_runs == 1) return h2d_bytes(dev_compact, host_array + R.base, n, stage, slab_bytes, threads, s);
+  hipError_t e = hipSuccess;
+  hipEvent_t done[2] = {nullptr, nullptr};
+  for (int k = 0; k < 2; k++)
+    if ((e = hipEventCreateWithFlags(&done[k], hipEventDisableTiming)) != hipSuccess) return e;
+  bool used[2] = {false, false};
+  for (uint64_t o = 0, k = 0; o < n && e == hipSuccess; o += slab_bytes, k++) {
+    const uint64_t len = std::min(slab_bytes, n - o);
+    if (used[k & 1] && (e = hipEventSynchronize(done[k & 1])) != hipSuccess) break;
+    uint8_t *buf = stage + (k & 1) * slab_bytes;
+    copy_box_runs(R, const_cast<uint8_t *>(host_array), buf, o, o + len, false, threads);
+    if ((e = hipMemcpyAsync(dev_compact + o, buf, len, hipMemcpyHostToDevice, s)) != hipSuccess) break;
+    e = hipEventRecord(done[k & 1], s);
+    used[k & 1] = true;
+  }
+  if (e == hipSuccess) e = hipStreamSynchronize(s);
+  for (int k = 0; k < 2; k++) (void)hipEventDestroy(done[k]);
+  return e;
+}
+
 }  // namespace zgpu

@@ -13,6 +13,7 @@
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
+#include <chrono>
 #include <cstdio>
 #include <cstdlib>
 #include <cstring>
@@ -67,6 +68,9 @@ struct HipFail {
 // the GPU (zarrs calls a codec from many rayon workers at once); a call that finds every lane busy
 // waits for one. ZGPU_CTX_LANES sets the pool size (default 4, the hardware queues of a process).
 // ------------------------------------------------------------------------------------------------
+struct Coalescer;
+static void delete_coalescer(Coalescer *co);
+
 struct Lane {
   hipStream_t stream = nullptr;              // the call's stream when the caller passes none
   hipStream_t copy[2] = {nullptr, nullptr};  // H2D / D2H streams of the pipelined host paths (lazy)
@@ -86,6 +90,7 @@ struct zgpu_ctx {
   std::vector<Lane *> lanes_all, lanes_free;
   uint32_t max_lanes = 4;
   hipStream_t peer = nullptr;  // peer copies of the multi-device read (lazy)
+  struct Coalescer *co = nullptr;  // ZGPU_COALESCE batching (lazy, under mu)
 
   Lane *acquire_lane() {
     std::unique_lock<std::mutex> lk(lane_mu);
@@ -179,6 +184,7 @@ struct zgpu_ctx {
       delete L;
     }
     if (peer) (void)hipStreamDestroy(peer);
+    delete_coalescer(co);
     (void)hipGetLastError();  // teardown failures must not surface in the caller's next HIP error check
   }
 };
@@ -1720,129 +1726,488 @@ static bool decode_pipelined(zgpu_chain *ch, Lane *LN, uint32_t nd, const zgpu_c
   return true;
 }
 
+}  // extern "C"
+
+// Host inputs -> one device staging buffer: chunks sorted by address and touching / overlapping ones
+// merged into ranges; pinned ranges are DMA'd directly (one copy per range), pageable ones through
+// the pinned staging slabs. local[i].enc is rewritten to descriptor i's device copy.
+struct HostStage {
+  zgpu_ctx *C;
+  uint8_t *enc = nullptr, *pin = nullptr;
+  static constexpr uint64_t slab = 64ull << 20;
+  explicit HostStage(zgpu_ctx *c) : C(c) {}
+  ~HostStage() {
+    C->dev_free(enc);
+    C->host_free(pin);
+  }
+  uint8_t *stage() {  // 2 slabs of pinned staging, only for pageable host buffers
+    if (!pin) pin = (uint8_t *)C->host_alloc(2 * slab);
+    return pin;
+  }
+  HostStage(const HostStage &) = delete;
+  HostStage &operator=(const HostStage &) = delete;
+};
+
+static void stage_host_inputs(HostStage &H, const zgpu_chunk_desc *descs, uint64_t n,
+                              std::vector<zgpu_chunk_desc> &local, hipStream_t s) {
+  local.assign(descs, descs + n);
+  std::vector<uint64_t> order;
+  for (uint64_t i = 0; i < n; i++)
+    if (descs[i].enc && descs[i].enc_len) order.push_back(i);
+  std::sort(order.begin(), order.end(),
+            [&](uint64_t a, uint64_t b) { return (uintptr_t)descs[a].enc < (uintptr_t)descs[b].enc; });
+  std::vector<HostRange> ranges;
+  std::vector<uint64_t> range_of(n, 0);
+  uint64_t total = 0;
+  for (uint64_t i : order) {
+    const uint8_t *p = (const uint8_t *)descs[i].enc;
+    if (!ranges.empty() && p <= ranges.back().src + ranges.back().len) {
+      HostRange &r = ranges.back();
+      const uint64_t end = std::max<uint64_t>((uint64_t)(p - r.src) + descs[i].enc_len, r.len);
+      total += end - r.len;
+      r.len = end;
+    } else {
+      total = (total + 255) & ~(uint64_t)255;
+      ranges.push_back(HostRange{p, descs[i].enc_len, total});
+      total += descs[i].enc_len;
+    }
+    range_of[i] = ranges.size() - 1;
+  }
+  if (!total) return;
+  H.enc = (uint8_t *)H.C->dev_alloc(total);
+  bool pinned = true;
+  for (const HostRange &r : ranges)
+    if (!host_is_pinned(r.src) || !host_is_pinned(r.src + r.len - 1)) {
+      pinned = false;
+      break;
+    }
+  HIPCHK(h2d_ranges(H.enc, ranges, pinned, pinned ? nullptr : H.stage(), HostStage::slab, host_copy_threads(), s));
+  for (uint64_t i : order) {
+    const HostRange &r = ranges[range_of[i]];
+    local[i].enc = H.enc + r.dev_off + ((const uint8_t *)descs[i].enc - r.src);
+  }
+}
+
+static uint64_t covered_volume(const zgpu_chunk_desc *descs, uint64_t n, uint32_t nd) {
+  uint64_t covered = 0;
+  for (uint64_t i = 0; i < n; i++) covered += sel_volume(descs[i], nd);
+  return covered;
+}
+
+static uint64_t volume(const uint64_t *shape, uint32_t nd) {
+  uint64_t v = 1;
+  for (uint32_t d = 0; d < nd; d++) v *= shape[d];
+  return v;
+}
+
+// Device-side decode of descriptors whose encoded bytes are on the device into dout (out_shape):
+// the general decode, per-descriptor statuses, first failing descriptor as the return value.
+static int decode_device(zgpu_chain *ch, uint32_t nd, const zgpu_chunk_desc *dd, uint64_t n, uint8_t *dout,
+                         const uint64_t *out_shape, uint32_t flags, int32_t *status, hipStream_t s) {
+  GeneralCall G{ch->ctx, ch->validate && !(flags & ZGPU_NO_VALIDATE), nd, dout, out_shape,
+                flags | ZGPU_ENC_DEVICE | ZGPU_OUT_DEVICE, s, {}};
+  std::vector<int32_t> st(n, 0);
+  decode_general(G, ch->chain, dd, n, st.data());
+  int rc = 0;
+  for (uint64_t i = 0; i < n; i++) {
+    if (status) status[i] = st[i];
+    if (!rc) rc = st[i];
+  }
+  return rc;
+}
+
+// zgpu_decode_batch / zgpu_decode_into on one lane (LN, stream s): every output form.
+static int decode_call(zgpu_chain *ch, Lane *LN, hipStream_t s, uint32_t nd, const zgpu_chunk_desc *descs, uint64_t n,
+                       const zgpu_out_view &V, uint32_t flags, int32_t *status) {
+  zgpu_ctx *C = ch->ctx;
+  const uint32_t es = ch->chain->es;
+  const bool whole = box_is_whole(nd, V.array_shape, V.start, V.shape);
+  const uint64_t out_elems = volume(V.shape, nd);
+  const bool fused = fused_plannable(*ch->chain) && uniform_shapes(descs, n, nd);
+  if (!(flags & ZGPU_ENC_DEVICE) && !(flags & ZGPU_OUT_DEVICE) && n >= 2 && fused && whole) {
+    // pinned host in and out, full coverage: the overlapped sub-batch pipeline
+    const uint64_t out_b = out_elems * es;
+    bool pinned = out_b && host_is_pinned(V.base) && host_is_pinned((const uint8_t *)V.base + out_b - 1);
+    for (uint64_t i = 0; i < n && pinned; i++) {
+      const uint8_t *e = (const uint8_t *)descs[i].enc;
+      if (e && descs[i].enc_len && (!host_is_pinned(e) || !host_is_pinned(e + descs[i].enc_len - 1))) pinned = false;
+    }
+    int rc = 0;
+    if (pinned && covered_volume(descs, n, nd) == out_elems &&
+        decode_pipelined(ch, LN, nd, descs, n, (uint8_t *)V.base, V.shape, flags, status, s, rc))
+      return rc;
+  }
+  HostStage H(C);
+  std::vector<zgpu_chunk_desc> local;
+  const zgpu_chunk_desc *dd = descs;
+  if (!(flags & ZGPU_ENC_DEVICE)) {
+    stage_host_inputs(H, descs, n, local, s);
+    dd = local.data();
+  }
+  if (flags & ZGPU_OUT_DEVICE) {
+    if (whole) return decode_device(ch, nd, dd, n, (uint8_t *)V.base, V.shape, flags, status, s);
+    // a window of a device array: decoded in place through the whole array's strides (descriptors
+    // shifted by the window origin; one outside its window fails alone, as it would against out_shape)
+    std::vector<zgpu_chunk_desc> sub;
+    std::vector<uint64_t> owner;
+    std::vector<int32_t> st(n, 0);
+    for (uint64_t i = 0; i < n; i++) {
+      if (!desc_geometry_ok(dd[i], nd, V.shape)) {
+        st[i] = ZGPU_INVALID_ARGUMENT;
+        continue;
+      }
+      zgpu_chunk_desc d = dd[i];
+      for (uint32_t k = 0; k < nd; k++) d.out_start[k] += V.start[k];
+      sub.push_back(d);
+      owner.push_back(i);
+    }
+    std::vector<int32_t> sst(sub.size(), 0);
+    decode_device(ch, nd, sub.data(), sub.size(), (uint8_t *)V.base, V.array_shape, flags, sst.data(), s);
+    if (g_size_detail.valid) g_size_detail.desc = owner[g_size_detail.desc];
+    for (size_t k = 0; k < sub.size(); k++) st[owner[k]] = sst[k];
+    int rc = 0;
+    for (uint64_t i = 0; i < n; i++) {
+      if (status) status[i] = st[i];
+      if (!rc) rc = st[i];
+    }
+    return rc;
+  }
+  // host output: decoded into a compact device copy of the window, copied back box-wise; parts of the
+  // window no descriptor covers keep the caller's bytes (the regions are disjoint,
+  // ArrayBytesFixedDisjointView, so equal volumes mean full coverage and no upload)
+  const uint64_t out_bytes = out_elems * es;
+  uint8_t *dout = (uint8_t *)C->dev_alloc(out_bytes ? out_bytes : 1);
+  const BoxRuns R = box_runs(nd, V.array_shape, V.start, V.shape, es);
+  int rc = 0;
+  try {
+    if (covered_volume(descs, n, nd) != out_elems)
+      HIPCHK(h2d_box(R, dout, (const uint8_t *)V.base, H.stage(), HostStage::slab, host_copy_threads(), s));
+    rc = decode_device(ch, nd, dd, n, dout, V.shape, flags, status, s);
+    HIPCHK(d2h_box(R, (uint8_t *)V.base, dout, H.stage(), HostStage::slab, host_copy_threads(), s));
+  } catch (...) {
+    C->dev_free(dout);
+    throw;
+  }
+  C->dev_free(dout);
+  return rc;
+}
+
+// ------------------------------------------------------------------------------------------------
+// Coalescing of concurrent host-in / host-out calls (ZGPU_COALESCE). zarrs' read path calls the codec
+// once per shard (or chunk) from each rayon worker (array_read_ops_common.rs:173-176,
+// sharding_codec.rs:617-707), and one shard's inner chunks fill a few percent of the GPU's decode
+// waves. Calls on one chain that arrive within the collect window become ONE batch: the first caller
+// (the batch's leader) waits for the window to close (or the batch to fill), stacks every caller's
+// window along axis 0 of one device output (trailing axes padded to the largest), uploads all
+// encoded bytes in one packed H2D, decodes everything in one launch sequence, packs the windows
+// compactly on the device (k_box_copy) and copies them back in one D2H into pinned memory. Every
+// caller then places its own window's rows into its host array (in parallel) and returns its own
+// statuses. Batches of one context run concurrently, each on a lane of its own.
+// ------------------------------------------------------------------------------------------------
+struct CoCall {
+  zgpu_chain *ch;
+  uint32_t nd;
+  const zgpu_chunk_desc *descs;
+  uint64_t n;
+  zgpu_out_view V;
+  uint32_t flags;
+  int32_t *status;
+  uint64_t enc_bytes = 0;
+  // results, set by the leader
+  bool done = false, call_error = false;  // call_error: the batch failed as a whole (rc, err)
+  int rc = 0;
+  std::string err;
+  SizeDetail sd;
+  uint64_t pack_off = 0;  // byte offset of this caller's compact window in the batch's host pack
+};
+
+struct CoBatch {
+  zgpu_ctx *C = nullptr;
+  std::vector<CoCall *> calls;
+  uint64_t bytes = 0;
+  bool closed = false;
+  std::condition_variable cv;
+  uint8_t *pack = nullptr;  // pinned: every caller's window, compact, back to back
+  ~CoBatch() {
+    if (pack) C->host_free(pack);
+  }
+};
+
+struct CoKey {
+  zgpu_chain *ch;
+  uint32_t flags, nd;
+  bool operator<(const CoKey &o) const {
+    return ch != o.ch ? ch < o.ch : flags != o.flags ? flags < o.flags : nd < o.nd;
+  }
+};
+
+struct Coalescer {
+  std::mutex mu;
+  std::map<CoKey, std::shared_ptr<CoBatch>> open;
+  uint32_t window_us = 200, max_calls = 8;
+  uint64_t max_bytes = 1ull << 30;
+  uint64_t batches = 0, calls = 0;
+};
+
+static Coalescer &coalescer(zgpu_ctx *C) {
+  std::lock_guard<std::mutex> lk(C->mu);
+  if (!C->co) {
+    C->co = new Coalescer();
+    if (const char *e = std::getenv("ZGPU_COALESCE_US")) C->co->window_us = (uint32_t)std::max(0, std::atoi(e));
+    if (const char *e = std::getenv("ZGPU_COALESCE_CALLS")) C->co->max_calls = (uint32_t)std::max(1, std::atoi(e));
+    if (const char *e = std::getenv("ZGPU_COALESCE_BYTES")) C->co->max_bytes = std::strtoull(e, nullptr, 10);
+  }
+  return *C->co;
+}
+
+// The leader's work: one decode of every caller's descriptors; fills each call's results and the
+// batch's host pack.
+static void co_run(CoBatch &B) {
+  zgpu_ctx *C = B.C;
+  CoCall &c0 = *B.calls[0];
+  zgpu_chain *ch = c0.ch;
+  const uint32_t nd = c0.nd, es = ch->chain->es;
+  HIPCHK(hipSetDevice(C->device));
+  LaneScope ls(C);
+  hipStream_t s = pick_stream(ls.L, nullptr);
+  // stacked output: caller k's window at rows [row0[k], row0[k] + V.shape[0]) of axis 0
+  uint64_t stacked[ZG_MAXD] = {0};
+  std::vector<uint64_t> row0(B.calls.size());
+  for (size_t k = 0; k < B.calls.size(); k++) {
+    const zgpu_out_view &V = B.calls[k]->V;
+    row0[k] = stacked[0];
+    stacked[0] += V.shape[0];
+    for (uint32_t d = 1; d < nd; d++) stacked[d] = std::max(stacked[d], V.shape[d]);
+  }
+  std::vector<zgpu_chunk_desc> all;
+  std::vector<std::pair<uint32_t, uint64_t>> owner;  // (call, descriptor)
+  std::vector<std::vector<int32_t>> st(B.calls.size());
+  for (size_t k = 0; k < B.calls.size(); k++) {
+    CoCall &c = *B.calls[k];
+    st[k].assign(c.n, 0);
+    for (uint64_t i = 0; i < c.n; i++) {
+      if (!desc_geometry_ok(c.descs[i], nd, c.V.shape)) {
+        st[k][i] = ZGPU_INVALID_ARGUMENT;
+        continue;
+      }
+      zgpu_chunk_desc d = c.descs[i];
+      d.out_start[0] += row0[k];
+      all.push_back(d);
+      owner.push_back({(uint32_t)k, i});
+    }
+  }
+  HostStage H(C);
+  std::vector<zgpu_chunk_desc> local;
+  stage_host_inputs(H, all.data(), all.size(), local, s);
+  uint64_t row_elems = 1;
+  for (uint32_t d = 1; d < nd; d++) row_elems *= stacked[d];
+  const uint64_t stacked_bytes = stacked[0] * row_elems * es;
+  uint64_t pack_bytes = 0;
+  for (CoCall *c : B.calls) {
+    c->pack_off = pack_bytes;
+    pack_bytes += volume(c->V.shape, nd) * es;
+  }
+  uint8_t *dout = (uint8_t *)C->dev_alloc(stacked_bytes ? stacked_bytes : 1);
+  uint8_t *dpack = nullptr;
+  try {
+    std::vector<int32_t> ast(all.size(), 0);
+    decode_device(ch, nd, local.data(), local.size(), dout, stacked, c0.flags, ast.data(), s);
+    const SizeDetail sd = g_size_detail;
+    for (size_t j = 0; j < all.size(); j++) st[owner[j].first][owner[j].second] = ast[j];
+    if (sd.valid && sd.desc < owner.size()) {
+      CoCall &c = *B.calls[owner[sd.desc].first];
+      c.sd = sd;
+      c.sd.desc = owner[sd.desc].second;
+    }
+    // pack: a window whose trailing extents are the stacked ones is already compact in place
+    bool compact = true;
+    for (CoCall *c : B.calls)
+      for (uint32_t d = 1; d < nd; d++)
+        if (c->V.shape[d] != stacked[d]) compact = false;
+    const uint8_t *src = dout;
+    if (!compact) {
+      dpack = (uint8_t *)C->dev_alloc(pack_bytes ? pack_bytes : 1);
+      for (size_t k = 0; k < B.calls.size(); k++) {
+        const zgpu_out_view &V = B.calls[k]->V;
+        uint64_t org[ZG_MAXD] = {0};
+        org[0] = row0[k];
+        const BoxRuns R = box_runs(nd, stacked, org, V.shape, es);
+        ZgBoxCopy P{};
+        P.outer = R.outer;
+        for (uint32_t d = 0; d < R.outer; d++) {
+          P.shape[d] = R.shape[d];
+          P.src_stride[d] = R.stride[d];
+        }
+        uint64_t cs = R.run_bytes;  // compact strides of the outer axes
+        for (int d = (int)R.outer - 1; d >= 0; d--) {
+          P.dst_stride[d] = cs;
+          cs *= R.shape[d];
+        }
+        P.src_base = R.base;
+        P.dst_base = B.calls[k]->pack_off;
+        P.run_bytes = R.run_bytes;
+        P.n_runs = R.n_runs;
+        HIPCHK(launch_box_copy(dout, dpack, P, s));
+      }
+      src = dpack;
+    }
+    B.pack = (uint8_t *)C->host_alloc(pack_bytes ? pack_bytes : 1);
+    if (pack_bytes) HIPCHK(hipMemcpyAsync(B.pack, src, pack_bytes, hipMemcpyDeviceToHost, s));
+    HIPCHK(hipStreamSynchronize(s));
+  } catch (...) {
+    C->dev_free(dout);
+    C->dev_free(dpack);
+    throw;
+  }
+  C->dev_free(dout);
+  C->dev_free(dpack);
+  for (size_t k = 0; k < B.calls.size(); k++) {
+    CoCall &c = *B.calls[k];
+    c.rc = 0;
+    for (uint64_t i = 0; i < c.n; i++) {
+      if (c.status) c.status[i] = st[k][i];
+      if (!c.rc) c.rc = st[k][i];
+    }
+  }
+}
+
+static int coalesced_call(zgpu_chain *ch, uint32_t nd, const zgpu_chunk_desc *descs, uint64_t n,
+                          const zgpu_out_view &V, uint32_t flags, int32_t *status) {
+  zgpu_ctx *C = ch->ctx;
+  Coalescer &K = coalescer(C);
+  CoCall me{ch, nd, descs, n, V, flags, status};
+  for (uint64_t i = 0; i < n; i++)
+    if (descs[i].enc) me.enc_bytes += descs[i].enc_len;
+  const CoKey key{ch, flags, nd};
+  std::shared_ptr<CoBatch> B;
+  bool leader = false;
+  std::unique_lock<std::mutex> lk(K.mu);
+  auto it = K.open.find(key);
+  if (it == K.open.end()) {
+    B = std::make_shared<CoBatch>();
+    B->C = C;
+    K.open[key] = B;
+    leader = true;
+  } else {
+    B = it->second;
+  }
+  B->calls.push_back(&me);
+  B->bytes += me.enc_bytes;
+  auto close = [&]() {
+    B->closed = true;
+    auto jt = K.open.find(key);
+    if (jt != K.open.end() && jt->second == B) K.open.erase(jt);
+  };
+  if (B->calls.size() >= K.max_calls || B->bytes >= K.max_bytes) {
+    close();
+    B->cv.notify_all();
+  }
+  if (leader) {
+    B->cv.wait_until(lk, std::chrono::steady_clock::now() + std::chrono::microseconds(K.window_us),
+                     [&] { return B->closed; });
+    if (!B->closed) close();
+    K.batches++;
+    K.calls += B->calls.size();
+    lk.unlock();
+    int rc = 0;
+    std::string err;
+    try {
+      co_run(*B);
+    } catch (const ChainError &e) {
+      rc = e.status;
+      err = e.msg;
+    } catch (const HipFail &e) {
+      rc = ZGPU_HIP_ERROR;
+      err = std::string(e.what) + ": " + hipGetErrorString(e.e);
+    } catch (const std::exception &e) {
+      rc = ZGPU_INVALID_ARGUMENT;
+      err = e.what();
+    }
+    lk.lock();
+    for (CoCall *c : B->calls) {
+      if (rc) {
+        c->rc = rc;
+        c->err = err;
+        c->call_error = true;
+        c->sd = SizeDetail{};
+      }
+      c->done = true;
+    }
+    B->cv.notify_all();
+  } else {
+    B->cv.wait(lk, [&] { return me.done; });
+  }
+  lk.unlock();
+  g_size_detail = me.sd;
+  if (me.call_error) return set_err(me.rc, me.err);
+  // this caller's window: its rows placed from the pinned pack by this caller's own thread (the
+  // batch's callers do this in parallel)
+  const BoxRuns R = box_runs(nd, V.array_shape, V.start, V.shape, ch->chain->es);
+  const uint64_t nb = R.n_runs * R.run_bytes;
+  copy_box_runs(R, (uint8_t *)V.base, B->pack + me.pack_off, 0, nb, true, 1);
+  if (me.rc) set_err(me.rc, zgpu_status_name(me.rc));
+  return me.rc;
+}
+
+static int decode_entry(zgpu_chain *ch, uint32_t nd, const zgpu_chunk_desc *descs, uint64_t n,
+                        const zgpu_out_view &V, uint32_t flags, int32_t *status, void *stream) {
+  zgpu_ctx *C = ch->ctx;
+  for (uint32_t d = 0; d < nd; d++)
+    if (V.start[d] + V.shape[d] > V.array_shape[d]) return set_err(ZGPU_INVALID_ARGUMENT, "view outside its array");
+  HIPCHK(hipSetDevice(C->device));
+  reset_call_state();
+  if ((flags & ZGPU_COALESCE) && !(flags & (ZGPU_ENC_DEVICE | ZGPU_OUT_DEVICE)) && n &&
+      covered_volume(descs, n, nd) == volume(V.shape, nd))
+    return coalesced_call(ch, nd, descs, n, V, flags & ~ZGPU_COALESCE, status);
+  LaneScope ls(C);
+  hipStream_t s = pick_stream(ls.L, stream);
+  const int rc = decode_call(ch, ls.L, s, nd, descs, n, V, flags & ~ZGPU_COALESCE, status);
+  if (rc) set_err(rc, zgpu_status_name(rc));
+  return rc;
+}
+
+static void delete_coalescer(Coalescer *co) { delete co; }
+
+extern "C" {
+
 int zgpu_decode_batch(zgpu_chain *ch, uint32_t nd, const zgpu_chunk_desc *descs, uint64_t n, void *out,
                       const uint64_t *out_shape, uint32_t flags, int32_t *status, void *stream) {
   ABI_GUARD_BEGIN
   if (!ch || !out_shape || (n && !descs) || !out) return set_err(ZGPU_INVALID_ARGUMENT, "NULL argument");
   if (nd == 0 || nd > ZGPU_MAX_DIMS) return set_err(ZGPU_INVALID_ARGUMENT, "ndim out of range");
-  zgpu_ctx *C = ch->ctx;
-  HIPCHK(hipSetDevice(C->device));
-  LaneScope ls(C);
-  hipStream_t s = pick_stream(ls.L, stream);
-  reset_call_state();
-  const bool fused = fused_plannable(*ch->chain) && uniform_shapes(descs, n, nd);
-  if (!(flags & ZGPU_ENC_DEVICE) && !(flags & ZGPU_OUT_DEVICE) && n >= 2 && fused) {
-    // pinned host in and out, full coverage: the overlapped sub-batch pipeline
-    uint64_t out_elems = 1, covered = 0, out_b;
-    for (uint32_t d = 0; d < nd; d++) out_elems *= out_shape[d];
-    out_b = out_elems * ch->chain->es;
-    bool pinned = out_b && host_is_pinned(out) && host_is_pinned((const uint8_t *)out + out_b - 1);
-    for (uint64_t i = 0; i < n && pinned; i++) {
-      uint64_t v = 1;
-      for (uint32_t d = 0; d < nd; d++) v *= descs[i].sel_shape[d];
-      covered += v;
-      const uint8_t *e = (const uint8_t *)descs[i].enc;
-      if (e && descs[i].enc_len && (!host_is_pinned(e) || !host_is_pinned(e + descs[i].enc_len - 1))) pinned = false;
-    }
-    int rc = 0;
-    if (pinned && covered == out_elems &&
-        decode_pipelined(ch, ls.L, nd, descs, n, (uint8_t *)out, out_shape, flags, status, s, rc)) {
-      if (rc) set_err(rc, zgpu_status_name(rc));
-      return rc;
-    }
-  }
-  std::vector<zgpu_chunk_desc> local;
-  const zgpu_chunk_desc *dd = descs;
-  uint8_t *enc_stage = nullptr;
-  const uint64_t slab = 64ull << 20;
-  uint8_t *pin_stage = nullptr;  // 2 slabs of pinned staging, only for pageable host buffers
-  auto stage = [&]() {
-    if (!pin_stage) pin_stage = (uint8_t *)C->host_alloc(2 * slab);
-    return pin_stage;
-  };
-  if (!(flags & ZGPU_ENC_DEVICE)) {
-    // host inputs: chunks sorted by address, touching/overlapping ones merged into ranges; pinned
-    // ranges are DMA'd directly (one copy per range), pageable ones through the staging slabs
-    local.assign(descs, descs + n);
-    std::vector<uint64_t> order;
-    for (uint64_t i = 0; i < n; i++)
-      if (descs[i].enc && descs[i].enc_len) order.push_back(i);
-    std::sort(order.begin(), order.end(),
-              [&](uint64_t a, uint64_t b) { return (uintptr_t)descs[a].enc < (uintptr_t)descs[b].enc; });
-    std::vector<HostRange> ranges;
-    std::vector<uint64_t> range_of(n, 0);
-    uint64_t total = 0;
-    for (uint64_t i : order) {
-      const uint8_t *p = (const uint8_t *)descs[i].enc;
-      if (!ranges.empty() && p <= ranges.back().src + ranges.back().len) {
-        HostRange &r = ranges.back();
-        const uint64_t end = std::max<uint64_t>((uint64_t)(p - r.src) + descs[i].enc_len, r.len);
-        total += end - r.len;
-        r.len = end;
-      } else {
-        total = (total + 255) & ~(uint64_t)255;
-        ranges.push_back(HostRange{p, descs[i].enc_len, total});
-        total += descs[i].enc_len;
-      }
-      range_of[i] = ranges.size() - 1;
-    }
-    if (total) {
-      enc_stage = (uint8_t *)C->dev_alloc(total);
-      bool pinned = true;
-      for (const HostRange &r : ranges)
-        if (!host_is_pinned(r.src) || !host_is_pinned(r.src + r.len - 1)) {
-          pinned = false;
-          break;
-        }
-      HIPCHK(h2d_ranges(enc_stage, ranges, pinned, pinned ? nullptr : stage(), slab, host_copy_threads(), s));
-      for (uint64_t i : order) {
-        const HostRange &r = ranges[range_of[i]];
-        local[i].enc = enc_stage + r.dev_off + ((const uint8_t *)descs[i].enc - r.src);
-      }
-    }
-    dd = local.data();
-  }
-  uint64_t out_elems = 1;
-  for (uint32_t d = 0; d < nd; d++) out_elems *= out_shape[d];
-  const uint64_t out_bytes = out_elems * ch->chain->es;
-  uint8_t *dout = (uint8_t *)out;
-  bool host_out = !(flags & ZGPU_OUT_DEVICE);
-  if (host_out) {
-    dout = (uint8_t *)C->dev_alloc(out_bytes ? out_bytes : 1);
-    // regions not covered by any descriptor keep the caller's bytes; the regions are disjoint
-    // (ArrayBytesFixedDisjointView contract), so equal volumes mean full coverage: no upload
-    uint64_t covered = 0;
-    for (uint64_t i = 0; i < n; i++) {
-      uint64_t v = 1;
-      for (uint32_t d = 0; d < nd; d++) v *= descs[i].sel_shape[d];
-      covered += v;
-    }
-    if (covered != out_elems)
-      HIPCHK(h2d_bytes(dout, (const uint8_t *)out, out_bytes, stage(), slab, host_copy_threads(), s));
-  }
-  int rc = 0;
-  try {
-    GeneralCall G{C, ch->validate && !(flags & ZGPU_NO_VALIDATE), nd, dout, out_shape,
-                  flags | ZGPU_ENC_DEVICE | ZGPU_OUT_DEVICE, s, {}};
-    std::vector<int32_t> st(n, 0);
-    decode_general(G, ch->chain, dd, n, st.data());
-    for (uint64_t i = 0; i < n; i++) {
-      if (status) status[i] = st[i];
-      if (!rc) rc = st[i];
-    }
-    if (host_out) HIPCHK(d2h_bytes((uint8_t *)out, dout, out_bytes, stage(), slab, host_copy_threads(), s));
-  } catch (...) {
-    if (host_out) C->dev_free(dout);
-    C->dev_free(enc_stage);
-    C->host_free(pin_stage);
-    throw;
-  }
-  if (host_out) C->dev_free(dout);
-  C->dev_free(enc_stage);
-  C->host_free(pin_stage);
-  if (rc) set_err(rc, zgpu_status_name(rc));
-  return rc;
+  zgpu_out_view V{};
+  V.base = out;
+  for (uint32_t d = 0; d < nd; d++) V.array_shape[d] = V.shape[d] = out_shape[d];
+  return decode_entry(ch, nd, descs, n, V, flags, status, stream);
   ABI_GUARD_END
+}
+
+int zgpu_decode_into(zgpu_chain *ch, uint32_t nd, const zgpu_chunk_desc *descs, uint64_t n, const zgpu_out_view *view,
+                     uint32_t flags, int32_t *status, void *stream) {
+  ABI_GUARD_BEGIN
+  if (!ch || !view || (n && !descs) || !view->base) return set_err(ZGPU_INVALID_ARGUMENT, "NULL argument");
+  if (nd == 0 || nd > ZGPU_MAX_DIMS) return set_err(ZGPU_INVALID_ARGUMENT, "ndim out of range");
+  return decode_entry(ch, nd, descs, n, *view, flags, status, stream);
+  ABI_GUARD_END
+}
+
+int zgpu_ctx_set_coalescing(zgpu_ctx *ctx, uint32_t window_us, uint32_t max_calls, uint64_t max_bytes) {
+  if (!ctx) return set_err(ZGPU_INVALID_ARGUMENT, "NULL argument");
+  Coalescer &K = coalescer(ctx);
+  std::lock_guard<std::mutex> lk(K.mu);
+  K.window_us = window_us;
+  K.max_calls = std::max<uint32_t>(1, max_calls);
+  K.max_bytes = max_bytes ? max_bytes : UINT64_MAX;
+  return ZGPU_OK;
+}
+
+int zgpu_ctx_coalescing_stats(const zgpu_ctx *ctx, uint64_t *batches, uint64_t *calls) {
+  if (!ctx) return set_err(ZGPU_INVALID_ARGUMENT, "NULL argument");
+  Coalescer &K = coalescer(const_cast<zgpu_ctx *>(ctx));
+  std::lock_guard<std::mutex> lk(K.mu);
+  if (batches) *batches = K.batches;
+  if (calls) *calls = K.calls;
+  return ZGPU_OK;
 }
 
 int zgpu_retrieve_array_subset(zgpu_chain *ch, uint32_t nd, const uint64_t *array_shape, const uint64_t *chunk_shape,

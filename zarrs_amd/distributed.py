@@ -80,6 +80,10 @@ def gather_slabs(local, slabs, axis: int = 0, dst: int = 0, group=None, out=None
             if local.numel():
                 dist.send(local.contiguous(), g_dst, group=group)
             return None
+        if out is not None and not out.is_contiguous():  # P2P receives need contiguous targets
+            got = gather_slabs(local, slabs, axis, dst, group)
+            out.copy_(got)
+            return out
         if out is None:
             shape = list(local.shape)
             shape[0] = sum(sh[0] for _, sh in slabs)
@@ -111,6 +115,23 @@ def gather_slabs(local, slabs, axis: int = 0, dst: int = 0, group=None, out=None
         return None
     parts = [b.narrow(axis, 0, sh[axis]) for b, (_, sh) in zip(bufs, slabs)]
     return torch.cat(parts, dim=axis)
+
+
+def slab_mismatches(gathered, expected, slabs, axis: int = 0):
+    """The ranks whose slab of a gathered subset differs from `expected` (bit for bit; the root's
+    check of every received slab, not only its own). Both tensors hold the whole subset."""
+    import torch
+    bad, row = [], 0
+    for r, (_, sh) in enumerate(slabs):
+        n = int(sh[axis])
+        a, b = gathered.narrow(axis, row, n), expected.narrow(axis, row, n)
+        row += n
+        if a.element_size() in (1, 2, 4, 8) and a.is_floating_point():
+            iv = {2: torch.int16, 4: torch.int32, 8: torch.int64}[a.element_size()]
+            a, b = a.contiguous().view(iv), b.contiguous().view(iv)
+        if not torch.equal(a, b):
+            bad.append(r)
+    return bad
 
 
 def chunk_boxes(array_shape, chunk_shape, start, shape):
@@ -190,6 +211,10 @@ def gather_regions(local, boxes_by_rank, sub_start, sub_shape, dst: int = 0, gro
             for w in dist.batch_isend_irecv(ops):
                 w.wait()
         return None
+    if out is not None and not out.is_contiguous():  # boxes are received in place: a contiguous target
+        got = gather_regions(local, boxes_by_rank, sub_start, sub_shape, dst, group)
+        out.copy_(got)
+        return out
     if out is None:
         out = torch.empty([int(x) for x in sub_shape], dtype=local.dtype, device=local.device)
     for b0, bs in boxes_by_rank[dst]:
