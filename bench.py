@@ -544,81 +544,105 @@ class C3:
         index verified) into its window of the output array (ShardingCodecBound::decode_into,
         sharding_codec.rs:617-707); a partial shard reads its index (a suffix range), then decodes only
         the intersecting inner chunks through the inner chain, crc32c stripped, not verified (the
-        plugin's GpuShardPartialDecoder) into its window. Measured two ways: the plugin's calls with
-        ZGPU_COALESCE into their output windows (zgpu_decode_into: concurrent calls become one GPU
-        batch, rows placed straight into the array), and round 3's pattern (isolated calls into a
-        per-call buffer, copied into the array by the caller)."""
+        plugin's GpuShardPartialDecoder) into its window. Each call's descriptor table is built before
+        the timed passes (the plugin builds it in native code; Python would time its own loops), so a
+        timed call is one zgpu_decode_into through ctypes, which releases the GIL. Measured two ways:
+        the plugin's calls with ZGPU_COALESCE into their output windows (concurrent calls become one
+        GPU batch, rows placed straight into the array), and isolated calls (no coalescing) into a
+        per-call buffer copied into the array by the caller (round 3's pattern)."""
         from concurrent.futures import ThreadPoolExecutor
+        from zarrs_amd import _lib as L
         from zarrs_amd import CodecChain, make_desc
+        lib = L.load()
         S, I = self.SHARD, self.INNER
         inner = CodecChain.from_metadata(self.CODECS[0]["configuration"]["codecs"], "float32", 0.0, self.args.ctx)
         out = np.empty(self.shape, np.float32)
         cps = S // I
         n_idx = cps ** 3
         expected = self.expected.cpu().numpy()
-        self.args.ctx.set_coalescing(window_us=200, max_calls=8)
 
-        def one(item, coalesce):
+        def prepare(item):
             (si, sj, sk), (_, host) = item
             org = [si * S, sj * S, sk * S]
             s0 = [max(a, o) for a, o in zip(self.start, org)]
             s1 = [min(a + b, o + S) for a, b, o in zip(self.start, self.shape, org)]
             sel = [b - a for a, b in zip(s0, s1)]
             w0 = [a - b for a, b in zip(s0, self.start)]
-            dst = tuple(slice(a, a + n) for a, n in zip(w0, sel))
             if sel == [S] * 3:  # full shard: ShardingCodecBound::decode_into
-                if coalesce:
-                    self.chain.decode_batch_into([make_desc(host, [S] * 3)], out, w0, sel, enc_device=False,
-                                                 coalesce=True)
-                else:
-                    buf = np.empty([S] * 3, np.float32)
-                    self.chain.decode_batch([make_desc(host, [S] * 3)], buf, [S] * 3, enc_device=False)
-                    out[dst] = buf
-                return
-            # partial: index by a suffix range, then the intersecting inner chunks' byte ranges
-            index = np.frombuffer(host[len(host) - (n_idx * 16 + 4):len(host) - 4].tobytes(), np.uint64).reshape(-1, 2)
-            lo = [(a - o) // I for a, o in zip(s0, org)]
-            hi = [(b - o - 1) // I + 1 for b, o in zip(s1, org)]
-            descs = []
-            for ci in range(lo[0], hi[0]):
-                for cj in range(lo[1], hi[1]):
-                    for ck in range(lo[2], hi[2]):
-                        off, ln = index[(ci * cps + cj) * cps + ck]
-                        c0 = [org[0] + ci * I, org[1] + cj * I, org[2] + ck * I]
-                        a0 = [max(a, c) for a, c in zip(s0, c0)]
-                        a1 = [min(b, c + I) for b, c in zip(s1, c0)]
-                        enc = None if off == 2 ** 64 - 1 else (host.ctypes.data + int(off), int(ln))
-                        descs.append(make_desc(enc, [I] * 3, [a - c for a, c in zip(a0, c0)],
-                                               [b - a for a, b in zip(a0, a1)], [a - b for a, b in zip(a0, s0)]))
-            if coalesce:
-                inner.decode_batch_into(descs, out, w0, sel, enc_device=False, validate_checksums=False, coalesce=True)
-            else:
-                buf = np.empty(sel, np.float32)
-                inner.decode_batch(descs, buf, sel, enc_device=False, validate_checksums=False)
-                out[dst] = buf
+                chain, descs, flags = self.chain, [make_desc((host.ctypes.data, host.nbytes), [S] * 3)], 0
+            else:  # partial: index by a suffix range, then the intersecting inner chunks' byte ranges
+                index = np.frombuffer(host[len(host) - (n_idx * 16 + 4):len(host) - 4].tobytes(),
+                                      np.uint64).reshape(-1, 2)
+                lo = [(a - o) // I for a, o in zip(s0, org)]
+                hi = [(b - o - 1) // I + 1 for b, o in zip(s1, org)]
+                descs = []
+                for ci in range(lo[0], hi[0]):
+                    for cj in range(lo[1], hi[1]):
+                        for ck in range(lo[2], hi[2]):
+                            off, ln = index[(ci * cps + cj) * cps + ck]
+                            c0 = [org[0] + ci * I, org[1] + cj * I, org[2] + ck * I]
+                            a0 = [max(a, c) for a, c in zip(s0, c0)]
+                            a1 = [min(b, c + I) for b, c in zip(s1, c0)]
+                            enc = None if off == 2 ** 64 - 1 else (host.ctypes.data + int(off), int(ln))
+                            descs.append(make_desc(enc, [I] * 3, [a - c for a, c in zip(a0, c0)],
+                                                   [b - a for a, b in zip(a0, a1)], [a - b for a, b in zip(a0, s0)]))
+                chain, flags = inner, L.NO_VALIDATE
+            arr = (L.ChunkDesc * len(descs))(*descs)
+            view = L.OutView()
+            view.base = out.ctypes.data
+            for d in range(3):
+                view.array_shape[d], view.start[d], view.shape[d] = self.shape[d], w0[d], sel[d]
+            buf = np.empty(sel, np.float32)
+            dst = tuple(slice(a, a + n) for a, n in zip(w0, sel))
+            return chain, arr, len(descs), view, flags, (C.c_int32 * len(descs))(), buf, dst, sel, host
 
-        items = list(self.shards.items())
-        res = {"threads": _threads(), "calls": len(items)}
+        calls = [prepare(it) for it in self.shards.items()]
+
+        def coalesced(c):
+            chain, arr, n, view, flags, st = c[:6]
+            rc = lib.zgpu_decode_into(chain._h, 3, arr, n, C.byref(view), flags | L.COALESCE, st, None)
+            if rc:
+                raise L.ZgpuError(rc, L.last_error())
+
+        def isolated(c):
+            chain, arr, n, _, flags, st, buf, dst, sel, _ = c
+            rc = lib.zgpu_decode_batch(chain._h, 3, arr, n, buf.ctypes.data, L.u64s(sel), flags, st, None)
+            if rc:
+                raise L.ZgpuError(rc, L.last_error())
+            out[dst] = buf
+
+        res = {"threads": _threads(), "calls": len(calls)}
+        sweep = [int(x) for x in str(getattr(self.args, "dropin_sweep", "") or "").split(",") if x]
+        best = None
         with ThreadPoolExecutor(_threads()) as ex:
-            for name, co in (("", True), ("uncoalesced_", False)):
+            def measure(fn, key):
                 out.fill(0)
-                list(ex.map(lambda it: one(it, co), items))  # warm-up
+                list(ex.map(fn, calls))  # warm-up (pools, scratch)
                 ok = bool(np.array_equal(out, expected))
                 st0 = self.args.ctx.coalescing_stats()
-                times = _time_reps(lambda: list(ex.map(lambda it: one(it, co), items)), 5.0)
+                times = _time_reps(lambda: list(ex.map(fn, calls)), 4.0)
                 st1 = self.args.ctx.coalescing_stats()
                 t = float(np.median(times))
-                res[name + "GiBps"] = round(out.nbytes / t / 2 ** 30, 2)
-                res[name + "ms"] = round(t * 1e3, 1)
-                res[name + "roundtrip_ok"] = ok
-                if co:
-                    nb = st1["batches"] - st0["batches"]
-                    res["coalesced_batches_per_pass"] = round(nb / len(times), 2)
-                    res["calls_per_batch"] = round((st1["calls"] - st0["calls"]) / max(1, nb), 2)
+                nb = st1["batches"] - st0["batches"]
+                return {"GiBps": round(out.nbytes / t / 2 ** 30, 2), "ms": round(t * 1e3, 1), "roundtrip_ok": ok,
+                        "batches_per_pass": round(nb / len(times), 2),
+                        "calls_per_batch": round((st1["calls"] - st0["calls"]) / max(1, nb), 2)}
+            for mc in sweep:
+                self.args.ctx.set_coalescing(window_us=200, max_calls=mc)
+                r = measure(coalesced, mc)
+                res.setdefault("sweep_max_calls", {})[str(mc)] = r
+            self.args.ctx.set_coalescing(window_us=200, max_calls=self.args.dropin_calls)
+            best = measure(coalesced, self.args.dropin_calls)
+            res.update(best)
+            res["max_calls_per_batch"] = self.args.dropin_calls
+            iso = measure(isolated, None)
+            res["uncoalesced_GiBps"], res["uncoalesced_ms"] = iso["GiBps"], iso["ms"]
+            res["uncoalesced_roundtrip_ok"] = iso["roundtrip_ok"]
         res["note"] = ("one synchronous host-in/host-out call per shard from a thread pool (the Rust plugin's pattern "
-                       "under zarrs' rayon loop); GiBps: ZGPU_COALESCE + zgpu_decode_into the output window "
-                       "(200 us collect window, <= 8 calls per batch); uncoalesced_GiBps: isolated "
-                       "zgpu_decode_batch calls into a per-call buffer copied into the output")
+                       "under zarrs' rayon loop), descriptor tables built before timing; GiBps: ZGPU_COALESCE + "
+                       "zgpu_decode_into the output window (200 us collect window, batches of <= max_calls_per_batch "
+                       "calls); uncoalesced_GiBps: isolated zgpu_decode_batch calls into a per-call buffer copied into "
+                       "the output")
         return res
 
 # ------------------------------------------------------------------------------------------------
@@ -1502,6 +1526,9 @@ def main():
                     help="workloads measured after the headline and reported in its line's `secondary` object "
                          "(comma-separated; '' for none)")
     ap.add_argument("--c5-cache", default="", help=argparse.SUPPRESS)
+    ap.add_argument("--dropin-calls", type=int, default=4,
+                    help="C3 drop-in leg: most calls one coalesced GPU batch takes (zgpu_ctx_set_coalescing)")
+    ap.add_argument("--dropin-sweep", default="", help="C3 drop-in leg: also measure these max_calls values (a,b,...)")
     ap.add_argument("--secondary-c5-scale", type=int, default=1,
                     help="C5 scale of the secondary leg (L0 y/x divided by this)")
     ap.add_argument("--dry-launch", action="store_true",

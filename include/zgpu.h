@@ -145,6 +145,9 @@ typedef struct {
  * Output regions of different descriptors must be disjoint (ArrayBytesFixedDisjointView).
  * status[n] (optional) receives each chunk's status. Returns the first non-zero chunk status
  * (zarrs' try_for_each semantics) or a call-level error. hip_stream NULL = context stream.
+ * A descriptor whose status is non-zero leaves its output region undefined (untouched, or partly
+ * written: e.g. a blosc chunk decoded straight into the output, some of whose blocks failed), as
+ * zarrs leaves a view whose decode_into failed; every other descriptor's region is complete.
  * The call is synchronous with respect to the host (statuses are final on return).
  * Any chain zgpu_chain_create accepts, and descriptors of different chunk shapes in one batch (e.g.
  * a rectilinear grid), decode here: one fused launch sequence per chunk shape when the chain is
@@ -152,7 +155,8 @@ typedef struct {
  * after it and at most one plain nested sharding_indexed inside), else composed from fused ones:
  * whole-shard bytes->bytes codecs are decoded into device buffers first, and deeper or wrapped
  * nested shards are resolved through their outer index (read back) into descriptors of the inner
- * chain. A transpose before a sharding_indexed of the second kind -> ZGPU_UNSUPPORTED.
+ * chain; transposes before a sharding_indexed of the second kind decode each selection in the
+ * encoded (transposed) frame first, then transpose and scatter it.
  */
 int zgpu_decode_batch(zgpu_chain *chain, uint32_t ndim, const zgpu_chunk_desc *descs,
                       uint64_t n, void *out, const uint64_t *out_shape, uint32_t flags,

@@ -53,7 +53,12 @@ pub fn create(metadata: &MetadataV3) -> Result<Codec, CodecCreateError> {
     };
     let meta_json = serde_json::to_string(metadata).map_err(CodecCreateError::other)?;
     Ok(match cpu {
-        Codec::BytesToBytes(cpu) => Codec::BytesToBytes(Arc::new(GpuBytesToBytes { cpu, meta_json, chain: OnceLock::new() })),
+        Codec::BytesToBytes(cpu) => Codec::BytesToBytes(Arc::new(GpuBytesToBytes {
+            cpu,
+            name: metadata.name().to_string(),
+            meta_json,
+            chain: OnceLock::new(),
+        })),
         Codec::ArrayToBytes(cpu) => Codec::ArrayToBytes(Arc::new(GpuBytes { cpu, meta_json })),
         Codec::ArrayToArray(cpu) => Codec::ArrayToArray(Arc::new(GpuTranspose { cpu, meta_json })),
         other => other,
@@ -71,8 +76,47 @@ const BYTES_LE: &str = r#"{"name":"bytes","configuration":{"endian":"little"}}"#
 #[derive(Debug)]
 pub struct GpuBytesToBytes {
     cpu: Arc<dyn BytesToBytesCodecTraits>,
+    name: String,
     meta_json: String,
     chain: OnceLock<Result<Chain, String>>,
+}
+
+/// The decoded length of a bytes->bytes codec's output when the chain only bounds it
+/// (BytesRepresentation::BoundedSize / UnboundedSize, e.g. crc32c after gzip in C3's inner chain):
+/// crc32c strips 4 bytes (crc32c_codec.rs:108-141; a shorter input decodes to the GPU's
+/// CRC_INPUT_TOO_SHORT), shuffle keeps the length (shuffle_codec.rs:109-129), gzip's trailer ISIZE
+/// (RFC 1952, modulo 2^32) and a zstd frame's content size (RFC 8878 frame header) are hints the GPU
+/// decode checks (DECODED_SIZE_MISMATCH when a stream lies: the caller then takes zarrs' codec).
+fn decoded_len_hint(name: &str, enc: &[u8]) -> Option<u64> {
+    match name {
+        "crc32c" => Some(enc.len().saturating_sub(4) as u64),
+        "numcodecs.shuffle" | "shuffle" => Some(enc.len() as u64),
+        "gzip" if enc.len() >= 18 => {
+            let t = &enc[enc.len() - 4..];
+            Some(u64::from(u32::from_le_bytes([t[0], t[1], t[2], t[3]])))
+        }
+        "zstd" if enc.len() >= 6 && enc[..4] == [0x28, 0xB5, 0x2F, 0xFD] => {
+            let fhd = enc[4];
+            let (fcs_flag, single, dict_flag) = (fhd >> 6, (fhd >> 5) & 1, fhd & 3);
+            let fcs_len = match fcs_flag {
+                0 => usize::from(single),
+                1 => 2,
+                2 => 4,
+                _ => 8,
+            };
+            if fcs_len == 0 {
+                return None;
+            }
+            let at = 5 + usize::from(single == 0) + [0usize, 1, 2, 4][usize::from(dict_flag)];
+            let f = enc.get(at..at + fcs_len)?;
+            let mut v = 0u64;
+            for (i, b) in f.iter().enumerate() {
+                v |= u64::from(*b) << (8 * i);
+            }
+            Some(if fcs_len == 2 { v + 256 } else { v })
+        }
+        _ => None,
+    }
 }
 
 impl GpuBytesToBytes {
@@ -109,7 +153,7 @@ impl BytesToBytesCodecTraits for GpuBytesToBytes {
         opts: &CodecSpecificOptions,
     ) -> Result<Arc<dyn BytesToBytesCodecTraits>, CodecCreateError> {
         let cpu = self.cpu.clone().with_codec_specific_options(opts)?;
-        Ok(Arc::new(Self { cpu, meta_json: self.meta_json.clone(), chain: OnceLock::new() }))
+        Ok(Arc::new(Self { cpu, name: self.name.clone(), meta_json: self.meta_json.clone(), chain: OnceLock::new() }))
     }
 
     fn recommended_concurrency(&self, decoded: &BytesRepresentation) -> Result<RecommendedConcurrency, CodecError> {
@@ -124,21 +168,32 @@ impl BytesToBytesCodecTraits for GpuBytesToBytes {
         self.cpu.encode(decoded, options)
     }
 
-    /// The GPU decode of a fixed-size decoded representation (crc32c verified per
-    /// `options.validate_checksums()`, gzip trailer / zstd frame checks always); zarrs' own codec
-    /// for a representation whose size is not known up front.
+    /// The GPU decode (crc32c verified per `options.validate_checksums()`, gzip trailer / zstd frame
+    /// checks always). A fixed-size decoded representation gives the length; otherwise (crc32c after a
+    /// compressor, as in C3's inner chain `[bytes, gzip, crc32c]`) it comes from the stream
+    /// (`decoded_len_hint`). zarrs' own codec only when no length is known (a zstd frame without a
+    /// content size) or a compressor's hint proves wrong.
     fn decode<'a>(
         &self,
         encoded: ArrayBytesRaw<'a>,
         decoded: &BytesRepresentation,
         options: &CodecOptions,
     ) -> Result<ArrayBytesRaw<'a>, CodecError> {
-        let BytesRepresentation::FixedSize(n) = *decoded else {
-            return self.cpu.decode(encoded, decoded, options);
+        let (n, hinted) = match *decoded {
+            BytesRepresentation::FixedSize(n) => (n, false),
+            _ => match decoded_len_hint(&self.name, &encoded) {
+                Some(n) => (n, true),
+                None => return self.cpu.decode(encoded, decoded, options),
+            },
         };
         let chain = self.chain()?;
-        let out = chain.decode_region(&encoded, &[n], &[0], &[n], options.validate_checksums())?;
-        Ok(Cow::Owned(out))
+        match chain.decode_region(&encoded, &[n], &[0], &[n], options.validate_checksums()) {
+            Ok(out) => Ok(Cow::Owned(out)),
+            Err(CodecError::UnexpectedChunkDecodedSize(_)) if hinted && !matches!(self.name.as_str(), "crc32c") => {
+                self.cpu.decode(encoded, decoded, options)
+            }
+            Err(e) => Err(e),
+        }
     }
 
     fn partial_decoder(

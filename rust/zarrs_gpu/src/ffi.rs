@@ -25,6 +25,8 @@ pub const ZGPU_NO_VALIDATE: u32 = 0x4;
 pub const ZGPU_DIRECT_IO: u32 = 0x8;
 /// Every kernel of the call on the caller's stream (no internal side stream).
 pub const ZGPU_ONE_STREAM: u32 = 0x10;
+/// Concurrent host-in/host-out calls on one chain share one GPU batch (zgpu.h ZGPU_COALESCE).
+pub const ZGPU_COALESCE: u32 = 0x20;
 
 #[repr(C)]
 pub struct zgpu_ctx {
@@ -59,6 +61,16 @@ impl Default for zgpu_chunk_desc {
     }
 }
 
+/// zgpu_out_view: the box [start, start + shape) of a C-order array of array_shape at base.
+#[repr(C)]
+#[derive(Clone, Copy)]
+pub struct zgpu_out_view {
+    pub base: *mut c_void,
+    pub array_shape: [u64; ZGPU_MAX_DIMS],
+    pub start: [u64; ZGPU_MAX_DIMS],
+    pub shape: [u64; ZGPU_MAX_DIMS],
+}
+
 unsafe extern "C" {
     pub fn zgpu_ctx_create(hip_device: c_int, out: *mut *mut zgpu_ctx) -> c_int;
     pub fn zgpu_ctx_destroy(ctx: *mut zgpu_ctx);
@@ -86,6 +98,17 @@ unsafe extern "C" {
         status: *mut i32,
         hip_stream: *mut c_void,
     ) -> c_int;
+    pub fn zgpu_decode_into(
+        chain: *mut zgpu_chain,
+        ndim: u32,
+        descs: *const zgpu_chunk_desc,
+        n: u64,
+        view: *const zgpu_out_view,
+        flags: u32,
+        status: *mut i32,
+        hip_stream: *mut c_void,
+    ) -> c_int;
+    pub fn zgpu_ctx_set_coalescing(ctx: *mut zgpu_ctx, window_us: u32, max_calls: u32, max_bytes: u64) -> c_int;
     pub fn zgpu_retrieve_array_subset(
         chain: *mut zgpu_chain,
         ndim: u32,

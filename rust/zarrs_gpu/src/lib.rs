@@ -200,7 +200,9 @@ impl Chain {
         let n: u64 = sel_shape.iter().product();
         let mut out = vec![0u8; usize::try_from(n).map_err(|e| CodecError::Other(e.to_string()))? * self.element_size];
         let mut status = 0i32;
-        let flags = if validate { 0 } else { ffi::ZGPU_NO_VALIDATE };
+        // ZGPU_COALESCE: this call joins the other rayon workers' concurrent calls on the chain in one
+        // GPU batch (zarrs decodes one shard per worker, array_read_ops_common.rs:173-176)
+        let flags = ffi::ZGPU_COALESCE | if validate { 0 } else { ffi::ZGPU_NO_VALIDATE };
         // SAFETY: the descriptor points at `encoded` (host memory, flags without ZGPU_ENC_DEVICE) and
         // `out` holds prod(sel_shape) elements; both outlive the synchronous call.
         let rc = unsafe {
@@ -254,7 +256,7 @@ impl Chain {
                 descs.len() as u64,
                 out.as_mut_ptr().cast::<c_void>(),
                 out_shape.as_ptr(),
-                flags & ffi::ZGPU_NO_VALIDATE,
+                flags & (ffi::ZGPU_NO_VALIDATE | ffi::ZGPU_COALESCE),
                 status.as_mut_ptr(),
                 std::ptr::null_mut(),
             )

@@ -18,11 +18,12 @@ use zarrs_metadata_ext::codec::sharding::{ShardingCodecConfiguration, ShardingCo
 use zarrs_storage::byte_range::ByteRange;
 use zarrs_chunk_grid::{ChunkGridCreateError, Indexer};
 use zarrs_codec::{
-    ArrayBytes, ArrayBytesRaw, ArrayCodecTraits, ArrayPartialDecoderNoSubchunkingTraits, ArrayPartialDecoderTraits,
+    ArrayBytes, ArrayBytesDecodeIntoTarget, ArrayBytesRaw, ArrayCodecTraits, ArrayPartialDecoderNoSubchunkingTraits, ArrayPartialDecoderTraits,
     ArrayPartialEncoderTraits, ArrayToBytesCodecSubchunkingTraits, ArrayToBytesCodecTraits, BytesPartialDecoderTraits,
     BytesPartialEncoderTraits, BytesRepresentation, ChunkGridDecoded, ChunkGridDecodedRef, Codec, CodecCreateError,
     CodecError, CodecMetadataOptions, CodecOptions, CodecSpecificOptions, CodecTraits, CodecTraitsV3,
     PartialDecoderCapability, PartialEncoderCapability, RecommendedConcurrency, UnboundArrayToBytesCodecTraits,
+    decode_into_array_bytes_target,
 };
 use zarrs_data_type::{DataType, FillValue};
 use zarrs_metadata::Configuration;
@@ -228,7 +229,7 @@ impl ArrayToBytesCodecTraits for GpuShardingCodecBound {
 
     /// ShardingCodecBound::decode: every inner chunk of the shard in one zgpu_decode_batch call
     /// (index decode + crc32c verify, inner chains, scatter into the shard), checksums verified per
-    /// `options.validate_checksums()`. The default `decode_into` copies the result into the view.
+    /// `options.validate_checksums()`, coalesced with concurrent calls (ZGPU_COALESCE).
     fn decode<'a>(
         &self,
         bytes: ArrayBytesRaw<'a>,
@@ -239,6 +240,43 @@ impl ArrayToBytesCodecTraits for GpuShardingCodecBound {
         let zeros = vec![0u64; shape.len()];
         let out = self.chain.decode_region(&bytes, &shape, &zeros, &shape, options.validate_checksums())?;
         Ok(ArrayBytes::new_flen(Cow::Owned(out)))
+    }
+
+    /// ShardingCodecBound::decode_into (sharding_codec.rs:617-707) into the caller's disjoint view
+    /// (the shard's place in the retrieve_array_subset output, array_read_ops_common.rs:150-176): the
+    /// shard's inner chunks are decoded in one GPU batch, coalesced (ZGPU_COALESCE) with the shards the
+    /// other rayon workers hand over at the same time, and the compact result is placed into the view
+    /// run by run (ArrayBytesFixedDisjointView::copy_from_slice, array_bytes_fixed_disjoint_view.rs:
+    /// 177-206). zarrs_codec exposes no raw pointer of a view, so the rows are placed here; a caller that
+    /// holds the raw output array (ArrayGpuExt) passes it to zgpu_decode_into, which places the rows
+    /// itself. Optional (masked) targets take the trait default.
+    fn decode_into(
+        &self,
+        bytes: ArrayBytesRaw<'_>,
+        shape: &[NonZeroU64],
+        output_target: ArrayBytesDecodeIntoTarget<'_>,
+        options: &CodecOptions,
+    ) -> Result<(), CodecError> {
+        match output_target {
+            ArrayBytesDecodeIntoTarget::Fixed(view) => {
+                let shape = u64s(shape);
+                let n: u64 = shape.iter().product();
+                if view.num_elements() != n {
+                    return Err(CodecError::Other(format!(
+                        "decode_into: the view holds {} elements, the shard {n}",
+                        view.num_elements()
+                    )));
+                }
+                let zeros = vec![0u64; shape.len()];
+                let out = self.chain.decode_region(&bytes, &shape, &zeros, &shape, options.validate_checksums())?;
+                view.copy_from_slice(&out)?;
+                Ok(())
+            }
+            target => {
+                let decoded = self.decode(bytes, shape, options)?;
+                decode_into_array_bytes_target(&decoded, target)
+            }
+        }
     }
 
     fn compact<'a>(
@@ -353,7 +391,8 @@ impl GpuShardPartialDecoder {
             descs[k].enc = b.as_ptr().cast();
             descs[k].enc_len = b.len() as u64;
         }
-        codec.inner_chain.decode_descs(&descs, &mut out, shape, ffi::ZGPU_NO_VALIDATE)?;
+        // coalesced with the partial shards other rayon workers decode at the same time
+        codec.inner_chain.decode_descs(&descs, &mut out, shape, ffi::ZGPU_NO_VALIDATE | ffi::ZGPU_COALESCE)?;
         Ok(out)
     }
 }

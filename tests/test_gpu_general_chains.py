@@ -32,6 +32,17 @@ CHAINS = {
                          {"name": "zstd", "configuration": {"level": 1}}],
     "around_nested": [sh([8, 16, 16], [{"name": "transpose", "configuration": {"order": [2, 1, 0]}},
                                         sh([4, 8, 8], LEAF), {"name": "crc32c"}])],
+    # transposes before a sharding the fused plan does not take: decoded in the encoded frame, then
+    # transposed and scattered (zgpu.cpp transposed_general)
+    "transpose_nested_zstd": [{"name": "transpose", "configuration": {"order": [2, 1, 0]}},
+                              sh([8, 16, 8], [sh([4, 8, 4], LEAF)]),
+                              {"name": "zstd", "configuration": {"level": 3, "checksum": False}}],
+    "transpose_deep3": [{"name": "transpose", "configuration": {"order": [1, 2, 0]}},
+                        {"name": "transpose", "configuration": {"order": [0, 2, 1]}},
+                        sh([16, 8, 16], [sh([8, 4, 8], [sh([4, 2, 4], LEAF)])])],
+    "transpose_around_nested": [{"name": "transpose", "configuration": {"order": [2, 0, 1]}},
+                                sh([16, 8, 16], [{"name": "transpose", "configuration": {"order": [1, 0, 2]}},
+                                                  sh([8, 4, 8], LEAF), {"name": "crc32c"}])],
 }
 SHAPE = [16, 32, 32]
 
@@ -183,3 +194,31 @@ def test_mixed_chunk_shapes_one_batch(ctx, torch_cuda, sharded):
     out = np.zeros([24, 24, 24], np.float32)
     assert ch.decode_batch(descs, out, [24, 24, 24], enc_device=True) == [0, 0]
     assert out.tobytes() == exp_out.tobytes() == full.tobytes()
+
+
+def test_whole_shard_gzip_isize_hint_retried_alone(ctx, torch_cuda):
+    """gzip's ISIZE (the decoded size mod 2^32, RFC 1952) only sizes the whole-shard slot: a member
+    whose ISIZE understates it outgrows the slot and is re-run alone with 8x larger slots until it
+    decodes; a member whose ISIZE then disagrees with its decoded size is corrupt (zlib and flate2
+    reject it too), while the shards beside it decode normally."""
+    from zarrs_amd import CodecChain, ZgpuError, make_desc
+    from zarrs_amd import _lib as L
+    codecs = CHAINS["shard_gzip"]
+    oc = O.OracleChain.from_metadata(codecs, "float32", 3, 3)
+    a0, a1 = _array(11), _array(12)
+    e0, e1 = oc.encode(a0), bytearray(oc.encode(a1))
+    e1[-4:] = (64).to_bytes(4, "little")  # ISIZE understated
+    with pytest.raises(O.OracleError) as oe:
+        oc.decode(bytes(e1), SHAPE)
+    ch = CodecChain.from_metadata(codecs, "float32", 3, ctx)
+    out = np.zeros([32, 32, 32], np.float32)
+    descs = [make_desc(e0, SHAPE, out_start=[0, 0, 0]), make_desc(bytes(e1), SHAPE, out_start=[16, 0, 0])]
+    with pytest.raises(ZgpuError) as ei:
+        ch.decode_batch(descs, out, [32, 32, 32], enc_device=False)
+    assert ei.value.status == oe.value.status == L.CORRUPT_STREAM
+    assert out[:16].tobytes() == a0.tobytes()
+    # both members with understated ISIZE hints but intact streams are not possible (the trailer holds
+    # ISIZE); a good member alone decodes from its own hint
+    out2 = np.zeros(SHAPE, np.float32)
+    assert ch.decode_batch([make_desc(e0, SHAPE)], out2, SHAPE, enc_device=False) == [0]
+    assert out2.tobytes() == a0.tobytes()

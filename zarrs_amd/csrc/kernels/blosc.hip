@@ -444,6 +444,12 @@ struct LzG {
           if (q + b >= base && q + b < hi) win[16 * v + b] = *(const uint8_t *)(q + b);
       }
     }
+    // The group's other lanes read these window bytes next (rd). A group lives inside one wave (G <=
+    // 64) and one wave's LDS operations complete in issue order, so no workgroup barrier is needed;
+    // the wavefront-scope fence keeps the compiler from moving those reads above the stores.
+    static_assert(G <= 64, "a stream's lane group must lie within one wave");
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    __builtin_amdgcn_wave_barrier();
   }
   __device__ __forceinline__ uint32_t rd(uint32_t p) {
     uint32_t kk = p - (uint32_t)wo;

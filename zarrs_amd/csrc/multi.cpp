@@ -89,11 +89,16 @@ int zgpu_retrieve_array_subset_multi(zgpu_chain *const *chains, uint32_t n_dev, 
         n[0] = P.rows;
         uint8_t *dst = (uint8_t *)out + P.row0 * row_bytes;
         const int dev = ctx_device(C);
-        if (dev_out && d != 0) {  // decode into this device's HBM (the context's pool), then one peer copy
-          scratch = ctx_dev_alloc(C, std::max<uint64_t>(P.rows * row_bytes, 1));
-          if (!scratch) {
+        if (dev_out && d != 0) {  // decode into a slab of this device's HBM, then one peer copy
+          // a one-off allocation (not the context's grow-only pool: a large read would otherwise keep
+          // rows * row_bytes of every secondary device reserved for the context's lifetime)
+          hipError_t e = hipSetDevice(dev);
+          if (e == hipSuccess) e = hipMalloc(&scratch, std::max<uint64_t>(P.rows * row_bytes, 1));
+          if (e != hipSuccess) {
+            (void)hipGetLastError();
+            scratch = nullptr;
             P.rc = ZGPU_HIP_ERROR;
-            P.err = "allocation of the device slab failed";
+            P.err = std::string("allocation of the device slab failed: ") + hipGetErrorString(e);
             return;
           }
           dst = (uint8_t *)scratch;
@@ -124,7 +129,7 @@ int zgpu_retrieve_array_subset_multi(zgpu_chain *const *chains, uint32_t n_dev, 
         P.rc = ZGPU_HIP_ERROR;
         P.err = "unknown exception";
       }
-      if (scratch) ctx_dev_free(C, scratch);
+      if (scratch && hipSetDevice(ctx_device(C)) == hipSuccess) (void)hipFree(scratch);
     };
     std::vector<std::thread> threads;
     for (uint32_t d = 1; d < n_dev; d++)

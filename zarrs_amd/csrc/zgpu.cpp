@@ -1101,6 +1101,27 @@ static bool sel_full(const zgpu_chunk_desc &D, uint32_t nd) {
   return true;
 }
 
+// The box [org, org + shape) of a device array (C order, array_shape) into dst + dst_off, compact
+// (k_box_copy: one wave per contiguous run).
+static void pack_box(const uint8_t *src, uint32_t nd, const uint64_t *array_shape, const uint64_t *org,
+                     const uint64_t *shape, uint32_t es, uint8_t *dst, uint64_t dst_off, hipStream_t s) {
+  const BoxRuns R = box_runs(nd, array_shape, org, shape, es);
+  ZgBoxCopy P{};
+  P.outer = R.outer;
+  uint64_t cs = R.run_bytes;  // compact strides of the outer axes
+  for (int d = (int)R.outer - 1; d >= 0; d--) {
+    P.shape[d] = R.shape[d];
+    P.src_stride[d] = R.stride[d];
+    P.dst_stride[d] = cs;
+    cs *= R.shape[d];
+  }
+  P.src_base = R.base;
+  P.dst_base = dst_off;
+  P.run_bytes = R.run_bytes;
+  P.n_runs = R.n_runs;
+  HIPCHK(launch_box_copy(src, dst, P, s));
+}
+
 struct GeneralCall {
   zgpu_ctx *C;
   bool validate;
@@ -1169,54 +1190,74 @@ static void shard_stage(GeneralCall &G, const Codec &k, std::vector<ZgItem> &ite
     for (uint64_t v : h) cap = std::max(cap, v);
   }
   cap = std::max<uint64_t>(cap, 256);
-  for (;;) {
+  // one stages-only plan over `set` with slots of `c` bytes; statuses in s, decoded items in res
+  auto run = [&](const std::vector<uint32_t> &set, uint64_t c, std::vector<int32_t> &s, std::vector<ZgItem> &res) {
     auto P = std::make_unique<zgpu_plan>();
     P->ctx = G.C;
     P->validate = G.validate;
     P->nd = 1;
-    P->n_desc = todo.size();
+    P->n_desc = set.size();
     P->flags = G.flags;
     P->out_shape = {1};
-    P->item_desc_status.assign(todo.size(), 0);
-    for (size_t j = 0; j < todo.size(); j++) {
-      ZgItem it = items[todo[j]];
+    P->item_desc_status.assign(set.size(), 0);
+    for (size_t j = 0; j < set.size(); j++) {
+      ZgItem it = items[set[j]];
       it.desc = (uint32_t)j;
       P->items.push_back(it);
     }
     st.pool = 0;
     P->stages = {st};
     P->n_pools = st.kind == ST_CRC32C ? 0 : 1;
-    P->slot_bytes = (cap + 255) & ~(uint64_t)255;
+    P->slot_bytes = (c + 255) & ~(uint64_t)255;
     P->no_scatter = true;
     plan_upload(*P, G.s);
     plan_enqueue(*P, nullptr, G.s);
-    std::vector<int32_t> s(todo.size(), 0);
+    s.assign(set.size(), 0);
     const SizeDetail keep_detail = g_size_detail;
     plan_statuses(*P, s.data(), G.s);
     g_size_detail = keep_detail;  // a shard has no expected decoded size
-    std::vector<ZgItem> res(todo.size());
-    HIPCHK(hipMemcpyAsync(res.data(), P->d_items, todo.size() * sizeof(ZgItem), hipMemcpyDeviceToHost, G.s));
+    res.resize(set.size());
+    HIPCHK(hipMemcpyAsync(res.data(), P->d_items, set.size() * sizeof(ZgItem), hipMemcpyDeviceToHost, G.s));
     HIPCHK(hipStreamSynchronize(G.s));
-    std::vector<uint32_t> again;
-    uint64_t bound = 0;
-    for (size_t j = 0; j < todo.size(); j++) {
-      const uint32_t t = todo[j];
-      const uint64_t deflate_bound = items[t].len * 1032 + 1024;
-      if (s[j] == ZGPU_DECODED_SIZE_MISMATCH && st.kind == ST_GZIP && cap < deflate_bound) {
-        again.push_back(t);
-        bound = std::max(bound, deflate_bound);
-        continue;
-      }
-      ist[t] = s[j];
-      if (!s[j]) {
-        items[t].src = res[j].src;
-        items[t].len = res[j].len;
+    if (std::find(s.begin(), s.end(), 0) != s.end()) G.keep.push_back(std::move(P));  // slots in use
+  };
+  // gzip's ISIZE is the decoded size modulo 2^32 (RFC 1952), only a hint: a member that outgrows its
+  // slot is re-run ALONE with 8x larger slots, up to DEFLATE's 1032:1 bound and the slot limit
+  // (ZGPU_SHARD_SLOT_LIMIT, default 64 GiB); past the limit it fails by itself with
+  // DECODED_SIZE_MISMATCH instead of sizing every retried shard's slot for the largest
+  static const uint64_t slot_limit = [] {
+    const char *e = std::getenv("ZGPU_SHARD_SLOT_LIMIT");
+    const uint64_t v = e ? std::strtoull(e, nullptr, 10) : 0;
+    return v ? v : (64ull << 30);
+  }();
+  std::vector<int32_t> s;
+  std::vector<ZgItem> res;
+  run(todo, std::min(cap, slot_limit), s, res);
+  auto settle = [&](uint32_t t, int32_t sj, const ZgItem &r) {
+    ist[t] = sj;
+    if (!sj) {
+      items[t].src = r.src;
+      items[t].len = r.len;
+    }
+  };
+  std::vector<uint32_t> again;
+  for (size_t j = 0; j < todo.size(); j++) {
+    const uint32_t t = todo[j];
+    const uint64_t bound = std::min(items[t].len * 1032 + 1024, slot_limit);
+    if (s[j] == ZGPU_DECODED_SIZE_MISMATCH && st.kind == ST_GZIP && cap < bound)
+      again.push_back(t);
+    else
+      settle(t, s[j], res[j]);
+  }
+  for (uint32_t t : again) {
+    const uint64_t bound = std::min(items[t].len * 1032 + 1024, slot_limit);
+    for (uint64_t c = std::min(cap * 8, bound);; c = std::min(c * 8, bound)) {
+      run({t}, c, s, res);
+      if (!(s[0] == ZGPU_DECODED_SIZE_MISMATCH && c < bound)) {
+        settle(t, s[0], res[0]);
+        break;
       }
     }
-    G.keep.push_back(std::move(P));
-    if (again.empty()) return;
-    cap = std::min(cap * 8, bound);
-    todo.swap(again);
   }
 }
 
@@ -1276,9 +1317,6 @@ static void nested_host(GeneralCall &G, const std::shared_ptr<Chain> &chain, con
                         uint64_t n, int32_t *status) {
   const Chain &top = *chain;
   const uint32_t nd = G.nd;
-  if (!top.a2a.empty())
-    throw ChainError{ZGPU_UNSUPPORTED, "transpose codecs before a sharding_indexed whose subchunks are shards "
-                                       "with codecs around them or nested sharding below them"};
   const std::vector<uint64_t> &ms = top.a2b.inner_shape;
   if (ms.size() != nd) throw ChainError{ZGPU_INVALID_ARGUMENT, "sharding chunk_shape rank"};
   uint64_t cps[ZG_MAXD], n_inner = 0;
@@ -1380,6 +1418,103 @@ static void nested_host(GeneralCall &G, const std::shared_ptr<Chain> &chain, con
   run_sub(G, top.a2b.inner, sub, owner, status);
 }
 
+// Transpose codecs before a sharding_indexed the fused plan does not take (bytes->bytes codecs after
+// it, or shards with codecs around them / nested deeper below it). zarrs decodes the sharding codec
+// on the encoded (transposed) shape, then the transposes (codec_chain.rs:592-646, transpose_codec.rs:
+// 264-281), and a partial read asks the sharding partial decoder for the selection's box in the
+// encoded frame (transpose_codec_partial.rs). Here every descriptor's selection is decoded by the
+// chain without its transposes, in the encoded frame, into its own box of a device buffer (boxes
+// stacked along axis 0); the boxes are packed compact (k_box_copy) and then decoded as the leaf chunks
+// of [transposes, bytes(native)], which transposes and scatters them into the output in one fused pass.
+static void transposed_general(GeneralCall &G, const std::shared_ptr<Chain> &chain, const zgpu_chunk_desc *descs,
+                               uint64_t n, int32_t *status) {
+  const Chain &top = *chain;
+  const uint32_t nd = G.nd, es = top.es;
+  uint32_t m[ZG_MAXD];
+  composed_axes(top, nd, m);  // encoded axis a <-> decoded axis m[a]
+  auto bare = std::make_shared<Chain>(top);
+  bare->a2a.clear();
+  auto tr = std::make_shared<Chain>(top);
+  tr->b2b.clear();
+  tr->a2b = Codec{};
+  tr->a2b.kind = CodecKind::Bytes;
+  tr->a2b.name = "bytes";
+  tr->a2b.big_endian = false;  // the decoded elements are native (little-endian) already
+  std::vector<zgpu_chunk_desc> enc_descs;
+  std::vector<uint64_t> owner, row0;
+  uint64_t stacked[ZG_MAXD] = {0};
+  for (uint64_t i = 0; i < n; i++) {
+    const zgpu_chunk_desc &D = descs[i];
+    if (!desc_geometry_ok(D, nd, G.out_shape)) {
+      status[i] = ZGPU_INVALID_ARGUMENT;
+      continue;
+    }
+    if (sel_volume(D, nd) == 0) continue;
+    zgpu_chunk_desc E = D;
+    for (uint32_t a = 0; a < nd; a++) {
+      E.chunk_shape[a] = D.chunk_shape[m[a]];
+      E.sel_start[a] = D.sel_start[m[a]];
+      E.sel_shape[a] = D.sel_shape[m[a]];
+      E.out_start[a] = 0;
+    }
+    E.out_start[0] = stacked[0];
+    row0.push_back(stacked[0]);
+    stacked[0] += E.sel_shape[0];
+    for (uint32_t a = 1; a < nd; a++) stacked[a] = std::max(stacked[a], E.sel_shape[a]);
+    enc_descs.push_back(E);
+    owner.push_back(i);
+  }
+  if (enc_descs.empty()) return;
+  uint64_t stacked_bytes = es;
+  for (uint32_t a = 0; a < nd; a++) stacked_bytes *= stacked[a];
+  uint64_t pack_bytes = 0;
+  std::vector<uint64_t> pack_off(enc_descs.size());
+  for (size_t k = 0; k < enc_descs.size(); k++) {
+    pack_off[k] = pack_bytes;
+    pack_bytes += sel_volume(enc_descs[k], nd) * es;
+  }
+  uint8_t *T = (uint8_t *)G.C->dev_alloc(stacked_bytes);
+  uint8_t *Pk = nullptr;
+  try {
+    // the encoded-frame boxes
+    GeneralCall G1{G.C, G.validate, nd, T, stacked, G.flags, G.s, {}};
+    std::vector<int32_t> st(enc_descs.size(), 0);
+    const bool had_detail = g_size_detail.valid;
+    decode_general(G1, bare, enc_descs.data(), enc_descs.size(), st.data());
+    if (!had_detail && g_size_detail.valid) g_size_detail.desc = owner[g_size_detail.desc];
+    Pk = (uint8_t *)G.C->dev_alloc(std::max<uint64_t>(pack_bytes, 1));
+    std::vector<zgpu_chunk_desc> leaf;
+    std::vector<uint64_t> leaf_owner;
+    for (size_t k = 0; k < enc_descs.size(); k++) {
+      const uint64_t i = owner[k];
+      if (st[k]) {
+        status[i] = st[k];
+        continue;
+      }
+      uint64_t org[ZG_MAXD] = {0};
+      org[0] = row0[k];
+      pack_box(T, nd, stacked, org, enc_descs[k].sel_shape, es, Pk, pack_off[k], G.s);
+      zgpu_chunk_desc L{};
+      L.enc = Pk + pack_off[k];
+      L.enc_len = sel_volume(enc_descs[k], nd) * es;
+      for (uint32_t a = 0; a < nd; a++) {
+        L.chunk_shape[a] = L.sel_shape[a] = descs[i].sel_shape[a];
+        L.sel_start[a] = 0;
+        L.out_start[a] = descs[i].out_start[a];
+      }
+      leaf.push_back(L);
+      leaf_owner.push_back(i);
+    }
+    run_sub(G, tr, leaf, leaf_owner, status);
+  } catch (...) {
+    G.C->dev_free(T);
+    G.C->dev_free(Pk);
+    throw;
+  }
+  G.C->dev_free(T);
+  G.C->dev_free(Pk);
+}
+
 static void decode_general(GeneralCall &G, const std::shared_ptr<Chain> &chain, const zgpu_chunk_desc *descs,
                            uint64_t n, int32_t *status) {
   for (uint64_t i = 0; i < n; i++) status[i] = 0;
@@ -1407,7 +1542,8 @@ static void decode_general(GeneralCall &G, const std::shared_ptr<Chain> &chain, 
     plan_statuses(*P, status, G.s);
     return;
   }
-  if (!top.b2b.empty()) predecode_shards(G, chain, descs, n, status);
+  if (!top.a2a.empty()) transposed_general(G, chain, descs, n, status);
+  else if (!top.b2b.empty()) predecode_shards(G, chain, descs, n, status);
   else nested_host(G, chain, descs, n, status);
 }
 
@@ -1949,6 +2085,20 @@ struct Coalescer {
   uint64_t batches = 0, calls = 0;
 };
 
+// ZGPU_TRACE=1: one stderr line per coalesced-batch phase (microseconds since the first trace)
+static void co_trace(const char *what, const void *batch, uint64_t a = 0, uint64_t b = 0) {
+  static const bool on = [] {
+    const char *e = std::getenv("ZGPU_TRACE");
+    return e && std::atoi(e) != 0;
+  }();
+  if (!on) return;
+  static const auto t0 = std::chrono::steady_clock::now();
+  const long long us =
+      std::chrono::duration_cast<std::chrono::microseconds>(std::chrono::steady_clock::now() - t0).count();
+  std::fprintf(stderr, "[zgpu-trace] %lld %s %p %llu %llu\n", us, what, batch, (unsigned long long)a,
+               (unsigned long long)b);
+}
+
 static Coalescer &coalescer(zgpu_ctx *C) {
   std::lock_guard<std::mutex> lk(C->mu);
   if (!C->co) {
@@ -1962,14 +2112,13 @@ static Coalescer &coalescer(zgpu_ctx *C) {
 
 // The leader's work: one decode of every caller's descriptors; fills each call's results and the
 // batch's host pack.
-static void co_run(CoBatch &B) {
+static void co_run(CoBatch &B, Lane *LN) {
   zgpu_ctx *C = B.C;
   CoCall &c0 = *B.calls[0];
   zgpu_chain *ch = c0.ch;
   const uint32_t nd = c0.nd, es = ch->chain->es;
   HIPCHK(hipSetDevice(C->device));
-  LaneScope ls(C);
-  hipStream_t s = pick_stream(ls.L, nullptr);
+  hipStream_t s = pick_stream(LN, nullptr);
   // stacked output: caller k's window at rows [row0[k], row0[k] + V.shape[0]) of axis 0
   uint64_t stacked[ZG_MAXD] = {0};
   std::vector<uint64_t> row0(B.calls.size());
@@ -1998,7 +2147,9 @@ static void co_run(CoBatch &B) {
   }
   HostStage H(C);
   std::vector<zgpu_chunk_desc> local;
+  co_trace("batch-start", &B, B.calls.size(), all.size());
   stage_host_inputs(H, all.data(), all.size(), local, s);
+  co_trace("h2d-done", &B);
   uint64_t row_elems = 1;
   for (uint32_t d = 1; d < nd; d++) row_elems *= stacked[d];
   const uint64_t stacked_bytes = stacked[0] * row_elems * es;
@@ -2012,6 +2163,7 @@ static void co_run(CoBatch &B) {
   try {
     std::vector<int32_t> ast(all.size(), 0);
     decode_device(ch, nd, local.data(), local.size(), dout, stacked, c0.flags, ast.data(), s);
+    co_trace("decode-done", &B);
     const SizeDetail sd = g_size_detail;
     for (size_t j = 0; j < all.size(); j++) st[owner[j].first][owner[j].second] = ast[j];
     if (sd.valid && sd.desc < owner.size()) {
@@ -2051,9 +2203,14 @@ static void co_run(CoBatch &B) {
       }
       src = dpack;
     }
-    B.pack = (uint8_t *)C->host_alloc(pack_bytes ? pack_bytes : 1);
+    // power-of-two size classes (>= 64 MiB): batches of varying size reuse pooled pinned buffers
+    // instead of page-locking new ones
+    uint64_t cls = 64ull << 20;
+    while (cls < pack_bytes) cls <<= 1;
+    B.pack = (uint8_t *)C->host_alloc(cls);
     if (pack_bytes) HIPCHK(hipMemcpyAsync(B.pack, src, pack_bytes, hipMemcpyDeviceToHost, s));
     HIPCHK(hipStreamSynchronize(s));
+    co_trace("d2h-done", &B, pack_bytes);
   } catch (...) {
     C->dev_free(dout);
     C->dev_free(dpack);
@@ -2093,6 +2250,7 @@ static int coalesced_call(zgpu_chain *ch, uint32_t nd, const zgpu_chunk_desc *de
   }
   B->calls.push_back(&me);
   B->bytes += me.enc_bytes;
+  co_trace(leader ? "arrive-lead" : "arrive-join", B.get(), me.enc_bytes);
   auto close = [&]() {
     B->closed = true;
     auto jt = K.open.find(key);
@@ -2103,16 +2261,28 @@ static int coalesced_call(zgpu_chain *ch, uint32_t nd, const zgpu_chunk_desc *de
     B->cv.notify_all();
   }
   if (leader) {
+    // the batch takes joiners for the collect window, and then for as long as its leader waits for a
+    // free lane: under load (every lane decoding an earlier batch) batches grow by themselves
     B->cv.wait_until(lk, std::chrono::steady_clock::now() + std::chrono::microseconds(K.window_us),
                      [&] { return B->closed; });
+    lk.unlock();
+    int rc = 0;
+    std::string err;
+    Lane *LN = nullptr;
+    try {
+      HIPCHK(hipSetDevice(C->device));
+      LN = C->acquire_lane();
+    } catch (const HipFail &e) {
+      rc = ZGPU_HIP_ERROR;
+      err = std::string(e.what) + ": " + hipGetErrorString(e.e);
+    }
+    lk.lock();
     if (!B->closed) close();
     K.batches++;
     K.calls += B->calls.size();
     lk.unlock();
-    int rc = 0;
-    std::string err;
-    try {
-      co_run(*B);
+    if (!rc) try {
+      co_run(*B, LN);
     } catch (const ChainError &e) {
       rc = e.status;
       err = e.msg;
@@ -2123,6 +2293,7 @@ static int coalesced_call(zgpu_chain *ch, uint32_t nd, const zgpu_chunk_desc *de
       rc = ZGPU_INVALID_ARGUMENT;
       err = e.what();
     }
+    if (LN) C->release_lane(LN);
     lk.lock();
     for (CoCall *c : B->calls) {
       if (rc) {
@@ -2145,6 +2316,7 @@ static int coalesced_call(zgpu_chain *ch, uint32_t nd, const zgpu_chunk_desc *de
   const BoxRuns R = box_runs(nd, V.array_shape, V.start, V.shape, ch->chain->es);
   const uint64_t nb = R.n_runs * R.run_bytes;
   copy_box_runs(R, (uint8_t *)V.base, B->pack + me.pack_off, 0, nb, true, 1);
+  co_trace("copied-out", B.get(), nb);
   if (me.rc) set_err(me.rc, zgpu_status_name(me.rc));
   return me.rc;
 }
