@@ -638,6 +638,12 @@ class C3:
             iso = measure(isolated, None)
             res["uncoalesced_GiBps"], res["uncoalesced_ms"] = iso["GiBps"], iso["ms"]
             res["uncoalesced_roundtrip_ok"] = iso["roundtrip_ok"]
+        # a rayon pool sized to a many-core host (zarrs' default: one worker per logical CPU) keeps
+        # every shard's call in flight at once; the calls mostly wait on the GPU
+        with ThreadPoolExecutor(len(calls)) as ex:
+            self.args.ctx.set_coalescing(window_us=200, max_calls=16)
+            wide = measure(coalesced, 16)
+            res["threads_one_per_shard"] = {"threads": len(calls), "max_calls_per_batch": 16, **wide}
         res["note"] = ("one synchronous host-in/host-out call per shard from a thread pool (the Rust plugin's pattern "
                        "under zarrs' rayon loop), descriptor tables built before timing; GiBps: ZGPU_COALESCE + "
                        "zgpu_decode_into the output window (200 us collect window, batches of <= max_calls_per_batch "

@@ -241,7 +241,9 @@ uint64_t zgpu_plan_algorithmic_bytes(const zgpu_plan *plan);
 #define ZGPU_CTR_BLOSC_RERUN 3   /* 1 when a blosc input outgrew the stream-table layout recorded by
                                     the plan's first execution and the execution was re-run with a
                                     read-back layout (later executions are asynchronous otherwise) */
-#define ZGPU_N_COUNTERS 4
+#define ZGPU_CTR_BLOSC_BLOCKS 4  /* blosc blocks decoded: a partial selection decodes only the blocks
+                                    covering the bytes it reads (blosc_partial_decoder.rs:33-60)     */
+#define ZGPU_N_COUNTERS 5
 uint32_t zgpu_plan_counters(const zgpu_plan *plan, uint64_t *out, uint32_t n);
 uint32_t zgpu_last_counters(uint64_t *out, uint32_t n);
 

@@ -494,3 +494,38 @@ def test_blosc_lz_corrupt_stream_beside_good_ones(ctx, torch_cuda, cname, shuffl
         else:
             assert st[k] == 0, k
             assert np.array_equal(got[k * n:(k + 1) * n], data[k]), k
+
+
+@pytest.mark.parametrize("cname,shuffle", [("lz4", "shuffle"), ("zstd", "bitshuffle"), ("blosclz", "noshuffle")])
+def test_blosc_partial_decodes_only_covering_blocks(ctx, torch_cuda, cname, shuffle):
+    """A partial selection of a blosc chunk decodes only the blocks that cover the bytes it reads, as
+    zarrs' blosc partial decoder does (blosc_partial_decoder.rs:33-60 -> blosc_decompress_bytes_partial,
+    c-blosc's blosc_getitem): ZGPU_CTR_BLOSC_BLOCKS counts the decoded blocks; the values equal the
+    oracle's."""
+    from zarrs_amd import CodecChain, make_desc
+    from zarrs_amd import _lib as L
+    codecs = [{"name": "bytes", "configuration": {"endian": "little"}}, _blosc(cname, shuffle, 4, blocksize=8192)]
+    co = O.OracleChain.from_metadata(codecs, "float32", 0, 3)
+    ch = CodecChain.from_metadata(codecs, "float32", 0, ctx)
+    rng = np.random.default_rng(5)
+    cs = [32, 32, 32]  # 128 KiB
+    x = np.arange(32, dtype=np.float32)
+    a = (np.round(rng.standard_normal(cs) * 2) + x[:, None, None] * 3 + x[None, :, None]).astype(np.float32)
+    enc = co.encode(a)
+    flags, bs = enc[2], int.from_bytes(enc[8:12], "little")  # c-blosc may round the requested block size
+    assert not flags & 2, "a compressed (not memcpyed) frame"
+    nblk = -(-a.nbytes // bs)
+    assert nblk >= 2
+    for hbm in (True, False):
+        src = torch_cuda.frombuffer(bytearray(enc), dtype=torch_cuda.uint8).cuda() if hbm else enc
+        for start, sub in (([0, 0, 0], cs), ([0, 0, 0], [2, 32, 32]), ([10, 5, 0], [2, 4, 32]), ([3, 0, 7], [9, 32, 3]),
+                           ([31, 31, 31], [1, 1, 1]), ([0, 0, 0], [32, 1, 1])):
+            out = np.zeros(sub, np.float32)
+            assert ch.decode_batch([make_desc(src, cs, start, sub)], out, sub, enc_device=hbm) == [0]
+            exp = co.decode(enc, cs)[tuple(slice(s, s + n) for s, n in zip(start, sub))]
+            assert out.tobytes() == exp.tobytes(), (start, sub)
+            # the blocks covering [first selected byte, last selected byte]
+            lo = 4 * sum(s * st for s, st in zip(start, (1024, 32, 1)))
+            hi = 4 * sum((s + n - 1) * st for s, n, st in zip(start, sub, (1024, 32, 1))) + 4
+            blocks = nblk if sub == cs else (hi - 1) // bs - lo // bs + 1
+            assert L.last_counters()["blosc_blocks"] == blocks, (start, sub, bs, L.last_counters())

@@ -108,9 +108,11 @@ def test_encode_round_trip_and_unsupported(ctx, torch_cuda):
     descs = [make_desc((e.data_ptr(), e.numel()), [64] * 3, out_start=s) for e, s in zip(enc, starts)]
     assert ch.decode_batch(descs, out, [128] * 3, enc_device=True) == [0] * 8
     assert torch_cuda.equal(out, x)
-    # blosc with a compressor the GPU does not write (snappy) is refused loudly
-    bl = CodecChain.from_metadata([B("little"), {"name": "blosc", "configuration": {
-        "cname": "snappy", "clevel": 5, "shuffle": "shuffle", "typesize": 4, "blocksize": 0}}], "float32", 0, ctx)
+    # blosc behind a variable-length codec (its frame needs a fixed typesize layout) is refused loudly
+    bl = CodecChain.from_metadata([B("little"), {"name": "gzip", "configuration": {"level": 1}},
+                                   {"name": "blosc", "configuration": {"cname": "lz4", "clevel": 5, "shuffle": "shuffle",
+                                                                       "typesize": 4, "blocksize": 0}}],
+                                  "float32", 0, ctx)
     with pytest.raises(ZgpuError) as ei:
         bl.encode_chunks(x, [64, 64, 64], starts)
     assert ei.value.status == L.UNSUPPORTED
@@ -538,13 +540,90 @@ def test_blosc_encode_u16_ratio_and_small_chunks(ctx, torch_cuda):
             assert co8.decode(e.cpu().numpy().tobytes(), [m]).tobytes() == v[i * m:(i + 1) * m].tobytes(), m
 
 
-def test_blosc_encode_unsupported_cnames(ctx, torch_cuda):
-    """snappy streams are not written on the GPU: UNSUPPORTED, loudly."""
-    from zarrs_amd import CodecChain, ZgpuError
-    from zarrs_amd import _lib as L
-    x = torch_cuda.zeros([64], dtype=torch_cuda.float32, device="cuda")
-    for cname in ("snappy",):
-        ch = CodecChain.from_metadata([B("little"), BL(cname, "shuffle", 4)], "float32", 0, ctx)
-        with pytest.raises(ZgpuError) as ei:
-            ch.encode_chunks(x, [64], [[0]])
-        assert ei.value.status == L.UNSUPPORTED
+def _snappy_decode(z: bytes) -> bytes:
+    """google/snappy format_description.txt (the same decoder tests/test_snappy_writer.py pins)."""
+    import test_snappy_writer as W
+    return W._snappy_decode(z)
+
+
+def _blosc_snappy_frame_decode(f: bytes) -> bytes:
+    """A c-blosc 1.x frame with snappy streams, decoded here (the host c-blosc has no snappy):
+    header, bstarts, per block its split streams ({csize, snappy stream} or stored when csize == the
+    stream's size), then byte- or bit-unshuffle (blosc.c blosc_d / shuffle.c)."""
+    import struct
+    ver, vlz, flags, ts = f[0], f[1], f[2], f[3]
+    nbytes, bsize, cbytes = struct.unpack_from("<3I", f, 4)
+    assert ver == 2 and cbytes == len(f)
+    if flags & 2:  # memcpyed
+        return bytes(f[16:16 + nbytes])
+    assert (flags >> 5) == 2, "snappy streams"
+    nblk = (nbytes + bsize - 1) // bsize
+    bstarts = struct.unpack_from("<%di" % nblk, f, 16)
+    out = bytearray()
+    for b in range(nblk):
+        bs = min(bsize, nbytes - b * bsize)
+        leftover = bs < bsize
+        nsplit = ts if (not (flags & 0x10) and not leftover) else 1
+        ne = bs // nsplit
+        p = bstarts[b]
+        blk = bytearray()
+        for _ in range(nsplit):
+            (cs,) = struct.unpack_from("<i", f, p)
+            p += 4
+            z = f[p:p + cs]
+            p += cs
+            blk += z if cs == ne else _snappy_decode(bytes(z))
+        assert len(blk) == bs
+        v = np.frombuffer(bytes(blk), np.uint8)
+        if flags & 1 and ts > 1:  # byte shuffle
+            neb = bs // ts
+            body = v[:neb * ts].reshape(ts, neb).T.reshape(-1)
+            v = np.concatenate([body, v[neb * ts:]])
+        elif flags & 4 and ts >= 1 and bs >= ts:  # bitshuffle (element count a multiple of 8)
+            n = bs // ts
+            if n % 8 == 0:
+                bits = np.unpackbits(v[:n * ts].reshape(8 * ts, n // 8), axis=1, bitorder="little")
+                v = np.packbits(bits.reshape(ts, 8, n).transpose(2, 0, 1), axis=2, bitorder="little").reshape(-1)
+                v = np.concatenate([v, np.frombuffer(bytes(blk), np.uint8)[n * ts:]])
+        out += v.tobytes()
+    return bytes(out)
+
+
+SNAPPY_CHAINS = {
+    "snappy_shuffle_f32": ([B("little"), BL("snappy", "shuffle", 4)], "float32"),
+    "snappy_noshuffle_blocks_f32": ([B("little"), BL("snappy", "noshuffle", 4, blocksize=10000)], "float32"),
+    "snappy_bitshuffle_f32": ([B("little"), BL("snappy", "bitshuffle", 4)], "float32"),
+    "snappy_shuffle_crc_u16": ([B("little"), BL("snappy", "shuffle", 2), {"name": "crc32c"}], "uint16"),
+}
+
+
+@pytest.mark.parametrize("name", sorted(SNAPPY_CHAINS))
+def test_blosc_snappy_encode(ctx, torch_cuda, name):
+    """BloscCodec::encode with snappy streams (blosc_via_blosc_src.rs:57 maps BloscCompressor::Snappy):
+    k_lz4_encode's LZ77 parse emitted as snappy elements (literals, 1- and 2-byte-offset copies,
+    long matches as several copies). Parity unpinned (no snappy library or fixture in the image):
+    every frame is decoded here from the format description and by the GPU decoder, to the exact
+    chunk."""
+    import struct
+    from zarrs_amd import CodecChain, make_desc
+    codecs, dt = SNAPPY_CHAINS[name]
+    ch = CodecChain.from_metadata(codecs, dt, 0, ctx)
+    crc = codecs[-1]["name"] == "crc32c"
+    cs = [32, 32, 32]
+    for kind, a in _contents([64, 64, 32]).items():
+        if dt == "uint16":
+            a = (a.view(np.uint32) & 0xFFFF).astype(np.uint16)
+        x = torch_cuda.from_numpy(a.view(np.int16) if dt == "uint16" else a).cuda()
+        starts = [[i, j, 0] for i in (0, 32) for j in (0, 32)]
+        enc = ch.encode_chunks(x, cs, starts)
+        for st, e in zip(starts, enc):
+            got = e.cpu().numpy().tobytes()
+            if crc:
+                assert struct.unpack("<I", got[-4:])[0] == O.crc32c(got[:-4])
+                got = got[:-4]
+            blk = np.ascontiguousarray(a[st[0]:st[0] + 32, st[1]:st[1] + 32, :])
+            assert _blosc_snappy_frame_decode(got) == blk.tobytes(), (name, kind, st)
+        out = torch_cuda.zeros_like(x)
+        descs = [make_desc((e.data_ptr(), e.numel()), cs, out_start=st) for e, st in zip(enc, starts)]
+        assert ch.decode_batch(descs, out, list(x.shape), enc_device=True) == [0] * len(enc)
+        assert torch_cuda.equal(out, x), (name, kind)

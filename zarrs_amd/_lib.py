@@ -42,8 +42,8 @@ EXPORTS = [
     "zgpu_encode_chunks", "zgpu_retrieve_array_subset_multi", "zgpu_decode_into", "zgpu_ctx_set_coalescing",
     "zgpu_ctx_coalescing_stats",
 ]
-CTR_ENC_BYTES, CTR_ZSTD_SERIAL, CTR_ZSTD_PARALLEL, CTR_BLOSC_RERUN = range(4)
-N_COUNTERS = 4
+CTR_ENC_BYTES, CTR_ZSTD_SERIAL, CTR_ZSTD_PARALLEL, CTR_BLOSC_RERUN, CTR_BLOSC_BLOCKS = range(5)
+N_COUNTERS = 5
 
 
 class ChunkDesc(C.Structure):
@@ -180,7 +180,8 @@ def last_counters() -> dict:
     """Device counters of this thread's last decode call (zgpu_last_counters)."""
     buf = (C.c_uint64 * N_COUNTERS)()
     load().zgpu_last_counters(buf, N_COUNTERS)
-    return {"enc_bytes": buf[0], "zstd_serial": buf[1], "zstd_parallel": buf[2]}
+    return {"enc_bytes": buf[0], "zstd_serial": buf[1], "zstd_parallel": buf[2], "blosc_rerun": buf[3],
+            "blosc_blocks": buf[4]}
 
 
 def last_size_mismatch():

@@ -145,10 +145,14 @@ __global__ __launch_bounds__(64) void k_blosc_streams(ZgItem *items, uint32_t *s
                                                       const uint64_t *bases, ZgItem *subs, uint32_t *sub_status,
                                                       uint32_t *sub_kind, BlBlock *blocks, uint8_t *dst,
                                                       uint64_t slot_bytes, const unsigned long long *ovf,
-                                                      uint32_t direct, uint64_t want, uint64_t row_bytes) {
+                                                      uint32_t direct, uint64_t want, uint64_t row_bytes,
+                                                      const uint64_t *need, unsigned long long *n_decoded) {
   const uint32_t item = blockIdx.x, lane = threadIdx.x;
   const BlInfo I = info[item];
   if (I.comp == BL_COMP_SKIP || status[item] || *ovf) return;
+  // the decoded bytes this item's selection reads (a partial read: only the blocks covering them)
+  const uint64_t nlo = need ? need[2 * item] : 0, nhi = need ? need[2 * item + 1] : UINT64_MAX;
+  uint32_t n_dec = 0;
   const ZgItem it = items[item];
   const uint8_t *h = (const uint8_t *)it.src;
   const uint64_t sub0 = bases[2 * item], blk0 = bases[2 * item + 1];
@@ -160,6 +164,7 @@ __global__ __launch_bounds__(64) void k_blosc_streams(ZgItem *items, uint32_t *s
       sub_status[sub0] = BL_SKIP;
       sub_kind[sub0] = BL_KIND_RAW;
       blocks[blk0] = BlBlock{item, I.nbytes, 0, (uint32_t)sub0, 1, I.nbytes, 0, 1, I.ver};
+      n_dec = 1;
     }
   } else {
     const uint32_t flags = h[2], ts = h[3], bs = ld_u32(h + 8), cbytes = ld_u32(h + 12);
@@ -175,6 +180,11 @@ __global__ __launch_bounds__(64) void k_blosc_streams(ZgItem *items, uint32_t *s
         sub_status[s0 + j] = BL_SKIP;
         sub_kind[s0 + j] = BL_KIND_RAW;
       }
+      if ((uint64_t)b * bs >= nhi || (uint64_t)b * bs + bsize <= nlo) {  // not read by the selection
+        blocks[blk0 + b] = BlBlock{item, 0u, (uint64_t)b * bs, (uint32_t)s0, 0u, ne, mode, ts, I.ver};
+        continue;
+      }
+      n_dec++;
       bool ok = true;
       int64_t p = (int32_t)ld_u32(h + 16 + 4ull * b);
       if (p < 16 + 4ll * I.nblk || p > (int64_t)cbytes || bsize % nsplit) ok = false;
@@ -208,6 +218,8 @@ __global__ __launch_bounds__(64) void k_blosc_streams(ZgItem *items, uint32_t *s
     }
   }
   bad = __any(bad);
+  for (int o = 32; o; o >>= 1) n_dec += __shfl_xor(n_dec, o, 64);
+  if (lane == 0 && n_decoded && n_dec) atomicAdd(n_decoded, (unsigned long long)n_dec);
   if (lane == 0) {
     if (bad) {
       set_status(&status[item], ZG_CORRUPT_STREAM);
@@ -1016,7 +1028,8 @@ hipError_t launch_blosc_decode(ZgItem *items, uint32_t *status, uint32_t n_items
   const uint32_t direct = D.dout ? 1u : 0u;
   const uint64_t want = D.sc.nelem * D.sc.es, row_bytes = direct ? D.sc.chunk_shape[D.sc.nd - 1] * D.sc.es : 1;
   hipLaunchKernelGGL(k_blosc_streams, dim3(n_items), dim3(64), 0, s, items, status, info, D.bases, D.subs,
-                     D.sub_status, D.sub_kind, D.blocks, dst, slot_bytes, D.ovf, direct, want, row_bytes);
+                     D.sub_status, D.sub_kind, D.blocks, dst, slot_bytes, D.ovf, direct, want, row_bytes, D.need,
+                     D.blocks_decoded);
   if (D.n_zstd) {
     hipError_t e = launch_zstd(D.subs, D.sub_status, (uint32_t)D.n_sub, D.tmp, D.sub_slot, D.zs, s);
     if (e != hipSuccess) return e;

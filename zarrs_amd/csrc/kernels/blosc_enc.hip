@@ -7,7 +7,7 @@
 //   k_blosc_shuf_enc   one workgroup per (item, block): byte shuffle (shuffle.c shuffle_generic) or
 //                      bitshuffle (bshuf_trans_bit_elem; blocks whose element count is not a multiple
 //                      of 8 stay as they are, format 2) of the block into the staging buffer
-//   k_lz4_encode       one wave per stream: an LZ4 block or a blosclz stream (greedy LZ77, 64
+//   k_lz4_encode       one wave per stream: an LZ4 block, a blosclz or a snappy stream (greedy LZ77, 64
 //                      positions a step, 4-byte hash candidates in LDS, 64 / 72 KiB window; the last 5
 //                      bytes literals and no match starting in the last 12, as the LZ4 block format
 //                      requires and blosclz's decoder needs: it must end on a literal run), emitted
@@ -54,6 +54,35 @@ __device__ __forceinline__ uint32_t lz4_extra(uint32_t v) { return v >= 15 ? (v 
 __device__ __forceinline__ uint32_t blz_match_size(uint32_t L, uint32_t dist) {
   const uint32_t ext = L - 2 < 7 ? 0u : (L - 9) / 255 + 1;
   return 1 + ext + 1 + (dist - 1 >= 8191 ? 2u : 0u);
+}
+
+// snappy (google/snappy format_description.txt, c-blosc's snappy_wrap_compress = snappy::RawCompress):
+// a varint of the stream's length, then elements: a literal (tag 00, length - 1 in the tag below 60,
+// else in 1..4 following bytes) and copies of at most 64 bytes (tag 01: length 4..11, offset < 2048,
+// two bytes; tag 10: length 1..64, a 2-byte offset); longer matches are several copies.
+constexpr int FMT_LZ4 = 0, FMT_BLZ = 1, FMT_SNAPPY = 2;
+__device__ __forceinline__ uint32_t sn_varint_size(uint32_t v) {
+  uint32_t n = 1;
+  while (v >= 128) {
+    v >>= 7;
+    n++;
+  }
+  return n;
+}
+__device__ __forceinline__ uint32_t sn_lit_size(uint32_t ll) {
+  if (!ll) return 0;
+  const uint32_t n = ll - 1;
+  return 1 + (n < 60 ? 0u : n < 256 ? 1u : n < 65536 ? 2u : n < (1u << 24) ? 3u : 4u) + ll;
+}
+__device__ __forceinline__ uint32_t sn_copy_piece(uint32_t L) { return L > 64 ? (L - 64 >= 4 ? 64u : 60u) : L; }
+__device__ __forceinline__ uint32_t sn_match_size(uint32_t L, uint32_t off) {
+  uint32_t n = 0;
+  while (L) {
+    const uint32_t c = sn_copy_piece(L);
+    n += (c >= 4 && c <= 11 && off < 2048) ? 2u : 3u;
+    L -= c;
+  }
+  return n;
 }
 
 // stream s of an item: (offset in the item, length)
@@ -122,9 +151,10 @@ struct Lz4Smem {
   uint32_t tot;
 };
 
-// One LZ4 block per stream: out_len[s] = compressed length, or ~0 when it would not be smaller
-// (stored). scratch per wave: 3 u32 per possible sequence (match start, length, offset).
-template <bool BLZ>
+// One LZ4 block, blosclz stream or snappy stream per stream (FMT): out_len[s] = compressed length, or
+// ~0 when it would not be smaller (stored). scratch per wave: 3 u32 per possible sequence (match
+// start, length, offset).
+template <int FMT>
 __global__ __launch_bounds__(64) void k_lz4_encode(const uint32_t *status, uint32_t n_items, BloscEnc E,
                                                    const uint8_t *staging, uint8_t *outs, uint64_t out_pitch,
                                                    uint32_t *out_len, uint32_t *scratch, uint64_t seq_cap) {
@@ -157,7 +187,7 @@ __global__ __launch_bounds__(64) void k_lz4_encode(const uint32_t *status, uint3
       uint32_t mlen = 0, cand = 0;
       if (hvv && p >= skip && p < mlast) {
         cand = hvv - 1;
-        if (p - cand <= (BLZ ? BLZ_MAXOFF : LZ4E_MAXOFF) && ld4u(in + cand) == w4) {
+        if (p - cand <= (FMT == FMT_BLZ ? BLZ_MAXOFF : LZ4E_MAXOFF) && ld4u(in + cand) == w4) {
           const uint32_t lim = min(LZ4E_CAP1, m - LZ4E_LAST - p);
           uint32_t k = 4;
           while (k < lim && in[p + k] == in[cand + k]) k++;
@@ -213,22 +243,30 @@ __global__ __launch_bounds__(64) void k_lz4_encode(const uint32_t *status, uint3
     auto seq_size = [&](uint32_t k, uint32_t &lit0, uint32_t &ll) -> uint32_t {
       lit0 = k ? ms[k - 1] + ml[k - 1] : 0u;
       ll = (k == ns ? m : ms[k]) - lit0;
-      if (BLZ) return (ll + 31) / 32 + ll + (k == ns ? 0u : blz_match_size(ml[k], mo[k]));
+      if (FMT == FMT_BLZ) return (ll + 31) / 32 + ll + (k == ns ? 0u : blz_match_size(ml[k], mo[k]));
+      if (FMT == FMT_SNAPPY) return sn_lit_size(ll) + (k == ns ? 0u : sn_match_size(ml[k], mo[k]));
       if (k == ns) return 1 + lz4_extra(ll) + ll;
       return 1 + lz4_extra(ll) + ll + 2 + lz4_extra(ml[k] - 4);
     };
+    const uint32_t pre = FMT == FMT_SNAPPY ? sn_varint_size(m) : 0u;  // snappy: the length preamble
     uint32_t total = 0;
     for (uint32_t k = lane; k <= ns; k += 64) {
       uint32_t a, b;
       total += seq_size(k, a, b);
     }
     for (int o = 32; o; o >>= 1) total += __shfl_xor(total, o, 64);
+    total += pre;
     if (total >= m) {  // stored
       if (lane == 0) out_len[sg] = 0xFFFFFFFFu;
       continue;
     }
     uint8_t *out = outs + sg * out_pitch;
-    uint32_t obase = 0;
+    uint32_t obase = pre;
+    if (FMT == FMT_SNAPPY && lane == 0) {
+      uint32_t v = m, q = 0;
+      for (; v >= 128; v >>= 7) out[q++] = (uint8_t)(v | 128);
+      out[q] = (uint8_t)v;
+    }
     for (uint32_t c0 = 0; c0 <= ns; c0 += 64) {
       const uint32_t k = c0 + lane;
       uint32_t sz = 0, lit0 = 0, ll = 0;
@@ -239,7 +277,37 @@ __global__ __launch_bounds__(64) void k_lz4_encode(const uint32_t *status, uint3
         if ((int)lane >= o) incl += u;
       }
       const uint32_t tot = __shfl(incl, 63, 64);
-      if (BLZ && k <= ns) {
+      if (FMT == FMT_SNAPPY && k <= ns) {
+        uint8_t *o = out + obase + incl - sz;
+        if (ll) {
+          const uint32_t n = ll - 1;
+          if (n < 60) {
+            *o++ = (uint8_t)(n << 2);
+          } else {
+            const uint32_t nb = n < 256 ? 1u : n < 65536 ? 2u : n < (1u << 24) ? 3u : 4u;
+            *o++ = (uint8_t)((59 + nb) << 2);
+            for (uint32_t q = 0; q < nb; q++) *o++ = (uint8_t)(n >> (8 * q));
+          }
+          for (uint32_t q = 0; q < ll; q++) o[q] = in[lit0 + q];
+          o += ll;
+        }
+        if (k < ns) {
+          uint32_t L = ml[k];
+          const uint32_t of = mo[k];
+          while (L) {
+            const uint32_t c = sn_copy_piece(L);
+            if (c >= 4 && c <= 11 && of < 2048) {
+              *o++ = (uint8_t)(1u | ((c - 4) << 2) | ((of >> 8) << 5));
+              *o++ = (uint8_t)of;
+            } else {
+              *o++ = (uint8_t)(2u | ((c - 1) << 2));
+              *o++ = (uint8_t)of;
+              *o++ = (uint8_t)(of >> 8);
+            }
+            L -= c;
+          }
+        }
+      } else if (FMT == FMT_BLZ && k <= ns) {
         uint8_t *o = out + obase + incl - sz;
         for (uint32_t q = 0; q < ll; q += 32) {  // literal runs of <= 32 bytes
           const uint32_t r = min(32u, ll - q);
@@ -425,7 +493,8 @@ BloscEnc blosc_enc_params(uint32_t comp, uint32_t shuffle, uint32_t ts, uint64_t
   E.nblk = (uint32_t)(nbytes ? (nbytes + bs - 1) / bs : 0);
   // split the byte-shuffled planes into streams of their own (c-blosc's forward-compatible rule for
   // its LZ compressors); zstd streams stay whole
-  E.nsplit = (E.shuffle == 1 && (comp == BL_COMP_LZ4 || comp == BL_COMP_BLOSCLZ) && E.ts <= 16 && bs % E.ts == 0)
+  E.nsplit = (E.shuffle == 1 && (comp == BL_COMP_LZ4 || comp == BL_COMP_BLOSCLZ || comp == BL_COMP_SNAPPY) &&
+              E.ts <= 16 && bs % E.ts == 0)
                  ? E.ts : 1u;
   const uint32_t nfull = (uint32_t)(nbytes / bs);
   E.spi = nfull * E.nsplit + ((nbytes % bs) ? 1u : 0u);
@@ -438,7 +507,7 @@ uint64_t blosc_encode_scratch(const BloscEnc &E, uint32_t n_items) {
   uint64_t b = (uint64_t)n_items * E.nbytes + 256;      // staging
   b += ns * (8 + 8 + 4 + 4) + 1024;                       // soff, cptr, clen, zstatus
   b += (uint64_t)n_items * 8 + 256;                       // ftot
-  if (E.comp == BL_COMP_LZ4 || E.comp == BL_COMP_BLOSCLZ) {
+  if (E.comp == BL_COMP_LZ4 || E.comp == BL_COMP_BLOSCLZ || E.comp == BL_COMP_SNAPPY) {
     const uint64_t grid = std::min<uint64_t>(std::max<uint64_t>(ns, 1), (uint64_t)device_cu_count() * 8);
     b += ns * ((E.ne_max + 255) & ~255ull);                // compressed streams
     b += grid * (E.ne_max / 4 + 2) * 12 + 256;             // sequence records
@@ -474,18 +543,21 @@ hipError_t launch_blosc_encode(ZgItem *items, uint32_t *status, uint32_t n_items
   const uint8_t *cdata = nullptr;
   uint64_t cpitch = 0;
   const uint64_t *cp = nullptr;
-  if (ns && (E.comp == BL_COMP_LZ4 || E.comp == BL_COMP_BLOSCLZ)) {
+  if (ns && (E.comp == BL_COMP_LZ4 || E.comp == BL_COMP_BLOSCLZ || E.comp == BL_COMP_SNAPPY)) {
     cpitch = (E.ne_max + 255) & ~255ull;
     uint8_t *outs = take(ns * cpitch);
     const uint32_t grid = (uint32_t)std::min<uint64_t>(ns, (uint64_t)device_cu_count() * 8);
     const uint64_t seq_cap = E.ne_max / 4 + 2;
     uint32_t *seqs = (uint32_t *)take((uint64_t)grid * seq_cap * 12);
     if (E.comp == BL_COMP_BLOSCLZ)
-      hipLaunchKernelGGL(k_lz4_encode<true>, dim3(grid), dim3(64), 0, s, status, n_items, E, staging, outs, cpitch,
-                         clen, seqs, seq_cap);
+      hipLaunchKernelGGL(k_lz4_encode<FMT_BLZ>, dim3(grid), dim3(64), 0, s, status, n_items, E, staging, outs,
+                         cpitch, clen, seqs, seq_cap);
+    else if (E.comp == BL_COMP_SNAPPY)
+      hipLaunchKernelGGL(k_lz4_encode<FMT_SNAPPY>, dim3(grid), dim3(64), 0, s, status, n_items, E, staging, outs,
+                         cpitch, clen, seqs, seq_cap);
     else
-      hipLaunchKernelGGL(k_lz4_encode<false>, dim3(grid), dim3(64), 0, s, status, n_items, E, staging, outs, cpitch,
-                         clen, seqs, seq_cap);
+      hipLaunchKernelGGL(k_lz4_encode<FMT_LZ4>, dim3(grid), dim3(64), 0, s, status, n_items, E, staging, outs,
+                         cpitch, clen, seqs, seq_cap);
     cdata = outs;
   } else if (ns && E.comp == BL_COMP_ZLIB) {
     const uint64_t zp = zlib_pitch(E.ne_max);

@@ -226,6 +226,10 @@ struct BlDecode {
   uint8_t *dout;
   const uint64_t *geom;
   ZgScatter sc;
+  // per item the decoded byte range [need[2i], need[2i+1]) its selection needs (nullable: all); blocks
+  // outside it are neither parsed nor decoded. blocks_decoded counts the decoded blocks (ctl counter)
+  const uint64_t *need;
+  unsigned long long *blocks_decoded;
 };
 constexpr uint32_t BL_DIRECT_ROWS = 2048;  // rows per block (LDS row table of k_blosc_finish)
 // Capacities of a blosc stream table sized by an earlier execution of the same plan: the layout of

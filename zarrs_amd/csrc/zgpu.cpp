@@ -38,7 +38,8 @@ namespace {
 
 thread_local std::string g_last_error;
 // device counters in the plan's control block (u64 each, cleared per execute)
-enum { CTR_ENC_BYTES = 0, CTR_ZSTD_SERIAL = 1, CTR_ZSTD_PARALLEL = 2, CTR_BLOSC_RERUN = 3, CTR_N = 4 };
+enum { CTR_ENC_BYTES = 0, CTR_ZSTD_SERIAL = 1, CTR_ZSTD_PARALLEL = 2, CTR_BLOSC_RERUN = 3, CTR_BLOSC_BLOCKS = 4,
+       CTR_N = 5 };
 // internal ctl slots (not reported): a cached blosc layout was outgrown (the execution is re-run)
 enum { CTR_BLOSC_OVF = 31, CTR_SCRATCH = 30, CTR_ZSTD_NSER = 29 };  // not reported (device-side flags / sinks)
 thread_local uint64_t g_last_counters[CTR_N];
@@ -302,11 +303,15 @@ struct zgpu_plan {
   // host-input staging
   uint8_t *d_enc_stage = nullptr;
   uint64_t last_enc_bytes = 0;
-  uint64_t last_counters[CTR_N] = {0, 0, 0, 0};
+  uint64_t last_counters[CTR_N] = {};
   uint8_t *last_out = nullptr;  // output of the last enqueue (a blosc layout overflow re-runs into it)
   BlCaps bl_caps{};             // blosc stream-table capacities recorded by the first execution
   bool bl_caps_valid = false, bl_caps_seen = false;
   bool bl_direct = false;  // the blosc stage may write whole chunks straight into the output (BlDecode::dout)
+  // blosc as the last stage: per item the decoded byte range its selection needs ([0, max) for whole
+  // chunks); blocks outside it are not decoded (blosc_decompress_bytes_partial)
+  std::vector<uint64_t> bl_need;
+  uint64_t *d_bl_need = nullptr;
   // zstd serial fallback: skipped once an execution of this plan had no serial item (a later one that
   // has some is re-run by plan_statuses with the fallback launched)
   bool zstd_serial_off = false, zstd_serial_skipped = false;
@@ -322,7 +327,7 @@ struct zgpu_plan {
     }
     if (own.order_ev) (void)hipEventDestroy(own.order_ev);
     void *bufs[] = {d_items, d_items_init, d_geom, d_shards, d_index, d_shard_status, d_mids, d_mids_init,
-                    d_mid_status, d_shard_status2, d_mid_shards, d_index2,
+                    d_mid_status, d_shard_status2, d_mid_shards, d_index2, d_bl_need,
                     d_pool[0], d_pool[1], zs.blks, zs.nblk, zs.mode, zs.lit, zs.seq, d_ctl,
                     d_enc_stage, d_zser, d_order};
     for (void *b : bufs) ctx->dev_free(b);
@@ -732,6 +737,32 @@ static void plan_build(zgpu_plan &P, const zgpu_chunk_desc *descs) {
     }
     P.bl_direct = ok && !std::getenv("ZGPU_BLOSC_NO_DIRECT");
   }
+  // blosc feeding the scatter directly (its decoded bytes are the chunk's encoded-layout elements; a
+  // fused unshuffle would interleave planes): a partial selection needs only the byte range between
+  // its first and last element in the encoded layout, so only the blocks that cover it are decoded,
+  // as the reference's blosc partial decoder does (blosc_partial_decoder.rs:33-60 ->
+  // blosc_decompress_bytes_partial, c-blosc's blosc_getitem)
+  if (!P.stages.empty() && P.stages.back().kind == ST_BLOSC && !S.shuffle && !std::getenv("ZGPU_BLOSC_NO_PARTIAL")) {
+    bool any = false;
+    P.bl_need.assign(2 * P.items.size(), 0);
+    for (size_t i = 0; i < P.items.size(); i++) {
+      P.bl_need[2 * i + 1] = UINT64_MAX;
+      if (!(P.items[i].flags & ZG_ITEM_PARTIAL)) continue;
+      const uint64_t *g = P.geom.data() + i * 3 * nd;
+      uint64_t lo = 0, hi = 0;
+      bool empty = false;
+      for (uint32_t d = 0; d < nd; d++) {
+        if (!g[nd + d]) empty = true;
+        lo += g[d] * S.enc_stride[d];
+        hi += (g[d] + g[nd + d] - 1) * S.enc_stride[d];
+      }
+      if (empty) continue;
+      P.bl_need[2 * i] = lo * S.es;
+      P.bl_need[2 * i + 1] = (hi + 1) * S.es;
+      any = true;
+    }
+    if (!any) P.bl_need.clear();
+  }
 }
 
 static void plan_upload(zgpu_plan &P, hipStream_t us) {
@@ -744,6 +775,10 @@ static void plan_upload(zgpu_plan &P, hipStream_t us) {
     HIPCHK(hipMemcpyAsync(P.d_items_init, P.items.data(), ni * sizeof(ZgItem), hipMemcpyHostToDevice, us));
     HIPCHK(hipMemcpyAsync(P.d_geom, P.geom.data(), P.geom.size() * 8, hipMemcpyHostToDevice, us));
     for (int k = 0; k < P.n_pools; k++) P.d_pool[k] = (uint8_t *)C.dev_alloc(ni * P.slot_bytes);
+    if (!P.bl_need.empty()) {
+      P.d_bl_need = (uint64_t *)C.dev_alloc(P.bl_need.size() * 8);
+      HIPCHK(hipMemcpyAsync(P.d_bl_need, P.bl_need.data(), P.bl_need.size() * 8, hipMemcpyHostToDevice, us));
+    }
     for (const Stage &s : P.stages) {
       if (s.kind == ST_GZIP && !P.d_order) P.d_order = (uint32_t *)C.dev_alloc(ni * 4);
       if (s.kind == ST_ZSTD && !P.zs.blks) {
@@ -806,6 +841,8 @@ static void blosc_stage(zgpu_plan &P, const Stage &st, uint8_t *out, hipStream_t
     D.sc = P.scatter;
   }
   D.ovf = P.d_counter + CTR_BLOSC_OVF;
+  D.need = P.d_bl_need;
+  D.blocks_decoded = P.d_counter + CTR_BLOSC_BLOCKS;
   BlCaps &caps = P.bl_caps;
   const bool cached = P.bl_caps_valid;
   if (!cached) {
@@ -2315,7 +2352,9 @@ static int coalesced_call(zgpu_chain *ch, uint32_t nd, const zgpu_chunk_desc *de
   // batch's callers do this in parallel)
   const BoxRuns R = box_runs(nd, V.array_shape, V.start, V.shape, ch->chain->es);
   const uint64_t nb = R.n_runs * R.run_bytes;
-  copy_box_runs(R, (uint8_t *)V.base, B->pack + me.pack_off, 0, nb, true, 1);
+  // the batch's callers place their rows concurrently; each takes its share of the copy threads
+  const int share = std::max<int>(1, host_copy_threads() / (int)std::max<size_t>(1, B->calls.size()));
+  copy_box_runs(R, (uint8_t *)V.base, B->pack + me.pack_off, 0, nb, true, std::min(share, 4));
   co_trace("copied-out", B.get(), nb);
   if (me.rc) set_err(me.rc, zgpu_status_name(me.rc));
   return me.rc;
@@ -2763,10 +2802,11 @@ static int encode_var(zgpu_ctx *C, const Chain &c, uint32_t nd, const uint64_t *
                             : k.cname == "zstd"                       ? (uint32_t)BL_COMP_ZSTD
                             : k.cname == "blosclz"                    ? (uint32_t)BL_COMP_BLOSCLZ
                             : k.cname == "zlib"                       ? (uint32_t)BL_COMP_ZLIB
+                            : k.cname == "snappy"                     ? (uint32_t)BL_COMP_SNAPPY
                                                                       : UINT32_MAX;
       if (comp == UINT32_MAX)
         return set_err(ZGPU_UNSUPPORTED, "encode: blosc cname '" + k.cname +
-                                             "' (the GPU writes blosclz, lz4, lz4hc, zlib and zstd)");
+                                             "' (the GPU writes blosclz, lz4, lz4hc, snappy, zlib and zstd)");
       if (var_len) return set_err(ZGPU_UNSUPPORTED, "encode: blosc after a variable-length codec");
       const uint32_t ts = std::max<uint32_t>(1, k.elementsize);
       const int sh = k.shuffle >= 0 ? k.shuffle : (k.elementsize > 0 ? 2 : 0);  // zarrs' default (:119-123)
