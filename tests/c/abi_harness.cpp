@@ -9,6 +9,7 @@
 #include <cstdio>
 #include <cstring>
 #include <string>
+#include <thread>
 #include <vector>
 
 #include "../../include/zgpu.h"
@@ -67,6 +68,8 @@ static void part1() {
   uint64_t ctr[ZGPU_N_COUNTERS];
   CHECK(zgpu_last_counters(ctr, ZGPU_N_COUNTERS) == ZGPU_N_COUNTERS);
   CHECK(zgpu_chain_encoded_size(nullptr, 1, nullptr) == -1);
+  CHECK(zgpu_decode_into(nullptr, 1, nullptr, 0, nullptr, 0, nullptr, nullptr) == ZGPU_INVALID_ARGUMENT);
+  CHECK(zgpu_ctx_set_coalescing(nullptr, 1, 1, 1) == ZGPU_INVALID_ARGUMENT);
 }
 
 static void part2(zgpu_ctx *ctx) {
@@ -161,6 +164,61 @@ static void part2(zgpu_ctx *ctx) {
   CHECK(zgpu_decode_batch(ch, 2, &sd, 1, po.data(), pshape, 0, st, nullptr) == ZGPU_OK);
   for (int y = 0; y < 2; y++)
     for (int x = 0; x < 3; x++) CHECK(po[y * 3 + x] == so[(y + 1) * 4 + x + 1]);
+
+  // decode_into a window of a larger host array ([6,9], window at [1,2] of shape [4,4]: the
+  // ArrayBytesFixedDisjointView a ShardingCodecBound::decode_into receives); bytes outside stay
+  sd.sel_start[0] = sd.sel_start[1] = 0;
+  sd.sel_shape[0] = sd.sel_shape[1] = 4;
+  std::vector<uint16_t> big_arr(6 * 9, 7777);
+  zgpu_out_view v;
+  std::memset(&v, 0, sizeof v);
+  v.base = big_arr.data();
+  v.array_shape[0] = 6;
+  v.array_shape[1] = 9;
+  v.start[0] = 1;
+  v.start[1] = 2;
+  v.shape[0] = v.shape[1] = 4;
+  CHECK(zgpu_decode_into(ch, 2, &sd, 1, &v, 0, st, nullptr) == ZGPU_OK);
+  for (int y = 0; y < 6; y++)
+    for (int x = 0; x < 9; x++) {
+      const bool in = y >= 1 && y < 5 && x >= 2 && x < 6;
+      CHECK(big_arr[y * 9 + x] == (in ? so[(y - 1) * 4 + (x - 2)] : 7777));
+    }
+  v.start[1] = 6;  // the window must lie inside its array
+  CHECK(zgpu_decode_into(ch, 2, &sd, 1, &v, 0, st, nullptr) == ZGPU_INVALID_ARGUMENT);
+
+  // ZGPU_COALESCE from 8 host threads, each its own window of one [8,16] array (two shards side by side
+  // per row of shards): every caller gets its own status; one caller's shard has a corrupt index crc
+  CHECK(zgpu_ctx_set_coalescing(ctx, 20000, 8, 0) == ZGPU_OK);
+  std::vector<uint8_t> bad = shard;
+  bad[bad.size() - 1] ^= 0x40;
+  std::vector<uint16_t> arr(16 * 8, 0);
+  int rc[8];
+  std::vector<std::thread> th;
+  for (int t = 0; t < 8; t++)
+    th.emplace_back([&, t] {
+      zgpu_chunk_desc d = desc(t == 5 ? bad.data() : shard.data(), shard.size(), {4, 4});
+      zgpu_out_view w;
+      std::memset(&w, 0, sizeof w);
+      w.base = arr.data();
+      w.array_shape[0] = 16;
+      w.array_shape[1] = 8;
+      w.start[0] = 4 * (t / 2);
+      w.start[1] = 4 * (t % 2);
+      w.shape[0] = w.shape[1] = 4;
+      int32_t s1 = -1;
+      rc[t] = zgpu_decode_into(ch, 2, &d, 1, &w, ZGPU_COALESCE, &s1, nullptr);
+    });
+  for (auto &x : th) x.join();
+  uint64_t batches = 0, calls = 0;
+  CHECK(zgpu_ctx_coalescing_stats(ctx, &batches, &calls) == ZGPU_OK);
+  CHECK(calls >= 8 && batches < calls);
+  for (int t = 0; t < 8; t++) {
+    CHECK(rc[t] == (t == 5 ? ZGPU_INVALID_CHECKSUM : ZGPU_OK));
+    if (t == 5) continue;
+    for (int y = 0; y < 4; y++)
+      for (int x = 0; x < 4; x++) CHECK(arr[(4 * (t / 2) + y) * 8 + 4 * (t % 2) + x] == so[y * 4 + x]);
+  }
   zgpu_chain_destroy(ch);
 }
 

@@ -1847,6 +1847,41 @@ struct GWordPF {
   }
 };
 
+// A 64-B window with the 64-B block below it prefetched (ZG_LIT_GWIN 3): a lane reads each 128-B line
+// of its segment in two pieces instead of four. 256 lanes per workgroup read 256 lines spread over a
+// section, and between a lane's pieces of one line L2 has usually evicted it, so every piece was a
+// fabric fetch of its own (C5 PMC: ~4x the compressed literal bytes fetched).
+struct GWordPF64 {
+  const gu32 *Wp;
+  int64_t lim;
+  mutable uintptr_t cb;  // address of the cached 64-B block (1: none)
+  mutable zv4u c[4];     // its words
+  mutable zv4u n[4];     // the block below it (prefetched)
+  __device__ __forceinline__ static void ld(uintptr_t b, zv4u *x) {
+    const __attribute__((address_space(1))) zv4u *q = (const __attribute__((address_space(1))) zv4u *)b;
+#pragma unroll
+    for (int i = 0; i < 4; i++) x[i] = q[i];
+  }
+  __device__ __forceinline__ uint32_t operator()(int32_t k) const {
+    if (k < 0 || k >= lim) return 0u;
+    const uintptr_t a = (uintptr_t)(Wp + k), b = a & ~(uintptr_t)63;
+    if (b != cb) {
+      if (b + 64 == cb) {
+#pragma unroll
+        for (int i = 0; i < 4; i++) c[i] = n[i];
+      } else {
+        ld(b, c);
+      }
+      cb = b;
+      if (b > ((uintptr_t)Wp & ~(uintptr_t)63)) ld(b - 64, n);
+    }
+    const uint32_t i = (uint32_t)(a >> 2) & 15u;
+    const zv4u h = (i >> 2) == 0 ? c[0] : (i >> 2) == 1 ? c[1] : (i >> 2) == 2 ? c[2] : c[3];
+    const uint32_t j = i & 3u;
+    return j == 0 ? h.x : j == 1 ? h.y : j == 2 ? h.z : h.w;
+  }
+};
+
 struct GWord {
   const gu32 *Wp;
   int64_t lim;
@@ -1877,6 +1912,7 @@ __device__ unsigned long long g_litstats[8];
 template <class Wd>
 __device__ __forceinline__ uint32_t word_raw(const Wd &w, int32_t k) { return w(k); }
 __device__ __forceinline__ uint32_t word_raw(const GWordPF &w, int32_t k) { return (k >= 0 && k < w.lim) ? w.Wp[k] : 0u; }
+__device__ __forceinline__ uint32_t word_raw(const GWordPF64 &w, int32_t k) { return (k >= 0 && k < w.lim) ? w.Wp[k] : 0u; }
 __device__ __forceinline__ uint32_t word_raw(const GWord &w, int32_t k) { return (k >= 0 && k < w.lim) ? w.Wp[k] : 0u; }
 template <class Wd>
 struct RawWord {
@@ -2204,7 +2240,9 @@ __global__ __launch_bounds__(LIT_THREADS) __attribute__((amdgpu_waves_per_eu(ZG_
       } else {
         const gu32 *Wp = (const gu32 *)(words + wbase);
         const int64_t lim = nwords_item - wbase;
-#if ZG_LIT_GWIN == 2
+#if ZG_LIT_GWIN == 3
+        GWordPF64 word{Wp, lim, 1, {}, {}};
+#elif ZG_LIT_GWIN == 2
         const GWordPF word{Wp, lim, 1, zv4u{0, 0, 0, 0}, zv4u{0, 0, 0, 0}, zv4u{0, 0, 0, 0}, zv4u{0, 0, 0, 0}};
 #elif ZG_LIT_GWIN
         const GWord word{Wp, lim, 1, zv4u{0, 0, 0, 0}};
