@@ -19,4 +19,6 @@ v = [float(r["Counter_Value"]) for f in glob.glob(sys.argv[1] + "/**/*counter_co
 print(sys.argv[1], "k_zstd_lits FETCH_SIZE KiB per step (raw counter):", sum(v) / 3)
 PY
 done
+timeout -k 10 200 ./labx/gzip_lab_prof 15625 > $O/gzip_lab_prof.txt 2>&1 || { echo "gzip_lab_prof failed"; tail -5 $O/gzip_lab_prof.txt; exit 1; }
+cat $O/gzip_lab_prof.txt
 echo done

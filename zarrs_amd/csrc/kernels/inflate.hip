@@ -543,6 +543,310 @@ __device__ __forceinline__ void flush(const Smem &S, uint8_t *out, uint64_t cap,
   }
 }
 
+#ifndef ZG_INFLATE_SEG
+#define ZG_INFLATE_SEG 1  // Huffman blocks: every lane decodes a region of the stream serially (k_gzip's seg path)
+#endif
+#ifndef ZG_INFLATE_SEGB
+#define ZG_INFLATE_SEGB 512  // bits of the stream per lane region
+#endif
+#ifndef ZG_INFLATE_OVL
+#define ZG_INFLATE_OVL 384  // a lane starts decoding this many bits before its region (chains converge)
+#endif
+#ifndef ZG_INFLATE_SEGCAP
+#define ZG_INFLATE_SEGCAP 96  // symbol records per lane region (a fuller region ends the round there)
+#endif
+#ifndef ZG_INFLATE_MAXREP
+#define ZG_INFLATE_MAXREP 8  // out-of-sync lanes re-decoded per round from their predecessor's exit
+#endif
+constexpr uint32_t SEGB = ZG_INFLATE_SEGB, OVL = ZG_INFLATE_OVL, SEGCAP = ZG_INFLATE_SEGCAP;
+static_assert(OVL <= SEGB && SEGB >= 64, "a lane starts inside its predecessor's region");
+constexpr uint32_t SG_END = 0, SG_EOB = 1, SG_BAD = 2, SG_SLOW = 3, SG_CAP = 4, SG_PAST = 5;
+
+// One lane's view of the aligned word stream: words wi..wi+2 (96 bits) in registers, the next one
+// loaded ahead; positions are absolute bits of the aligned stream (the Bits domain).
+struct LaneRd {
+  const uint32_t *base;
+  uint32_t nwords, wi, w0, w1, w2, pf;
+  __device__ __forceinline__ uint32_t ld(uint32_t k) const { return k < nwords ? base[k] : 0u; }
+  __device__ __forceinline__ void seek(uint64_t p) {
+    wi = (uint32_t)(p >> 5);
+    w0 = ld(wi);
+    w1 = ld(wi + 1);
+    w2 = ld(wi + 2);
+    pf = ld(wi + 3);
+  }
+  __device__ __forceinline__ void adv(uint64_t p) {  // forward to the word holding bit p
+    while ((uint32_t)(p >> 5) > wi) {
+      w0 = w1;
+      w1 = w2;
+      w2 = pf;
+      wi++;
+      pf = ld(wi + 3);
+    }
+  }
+  __device__ __forceinline__ void peek(uint64_t p, uint32_t &lo, uint32_t &hi) const {
+    const uint32_t o = (uint32_t)p & 31;
+    lo = __builtin_amdgcn_alignbit(w1, w0, o);
+    hi = __builtin_amdgcn_alignbit(w2, w1, o);
+  }
+};
+
+// One lane decodes serially from bit p (a symbol start of its chain) while p < s_end. Symbols starting
+// at or after s_own are its region's: their records go to rec[0..n) (at most SEGCAP), and mask marks
+// the region's first 64 bit positions that start a symbol. Returns why it stopped; p is then the
+// exit (SG_END: the first symbol start >= s_end), the bit after the end-of-block code (SG_EOB), or
+// the symbol it stopped at. A stop before its region (SG_PAST) leaves the lane out of sync.
+__device__ __forceinline__ uint32_t seg_decode(const Smem &S, LaneRd &R, uint64_t &p, uint64_t s_own,
+                                               uint64_t s_end, uint64_t end_bits, uint32_t *rec, uint32_t &n,
+                                               uint64_t &mask) {
+  n = 0;
+  mask = 0;
+  R.seek(p);
+  while (p < s_end) {
+    if (p >= end_bits) return SG_PAST;
+    R.adv(p);
+    uint32_t lo, hi, info, r;
+    R.peek(p, lo, hi);
+    lane_symbol(S, lo, hi, info, r);
+    const bool own = p >= s_own;
+    if (own && p - s_own < 64) mask |= 1ull << (uint32_t)(p - s_own);
+    if (info >= F_EOB) {
+      if (!own) return SG_PAST;
+      if (info == (F_EOB | (info & 255))) {
+        p += info & 255;
+        return SG_EOB;
+      }
+      return (info & F_BAD) ? SG_BAD : SG_SLOW;
+    }
+    if (own) {
+      if (n == SEGCAP) return SG_CAP;
+      rec[n++] = r;
+    }
+    p += info & 255;
+  }
+  return SG_END;
+}
+
+__device__ __forceinline__ uint64_t shfl_up64(uint64_t v) {
+  const uint32_t lo = (uint32_t)__shfl_up((int)(uint32_t)v, 1, 64), hi = (uint32_t)__shfl_up((int)(uint32_t)(v >> 32), 1, 64);
+  return ((uint64_t)hi << 32) | lo;
+}
+
+// Execute one batch of symbols: lane t < cnt holds symbol record rec_in (a literal byte, or
+// (1<<31)|(dist<<9)|len); `bytes` = the batch's output bytes (pos + bytes <= cap checked by the
+// caller). Literals are written at once, matches resolve in rounds by exact dependencies; the ring is
+// flushed to the slot once FLUSH_MIN bytes are pending. Returns false for a distance past the output
+// start (corrupt stream).
+#ifdef ZG_PROFILE
+#define XPROF(k, n) pa[k] += (n)
+#else
+#define XPROF(k, n)
+#endif
+__device__ __forceinline__ bool exec_batch(Smem &S, uint8_t *out, uint64_t cap, uint64_t &pos, uint64_t &flushed,
+                                           uint32_t cnt, uint32_t bytes, uint32_t rec_in, uint64_t *pa) {
+  (void)pa;
+  const int lane = lane_id();
+  __syncthreads();
+  const bool mine = lane < (int)cnt;
+  const uint32_t rec = mine ? rec_in : 0u;
+  const bool is_match = mine && (rec >> 31);
+  const uint32_t ln = mine ? (is_match ? (rec & 511) : 1u) : 0u;
+  const uint64_t mypos = pos + wave_incl_sum(ln) - ln;  // output offsets: a wave prefix sum
+  if (mine && !is_match) S.ring[mypos & RMASK] = (uint8_t)rec;
+  const uint64_t batch_end = pos + bytes;
+  const uint32_t mlen = rec & 511, md = (rec >> 9) & 0xFFFF;
+  const uint64_t msrc = mypos - md;
+  if (__ballot(is_match && md > mypos)) return false;  // distance too far back
+  // sources older than the ring are read back from the flushed output
+  if (__ballot(is_match && msrc + RING < batch_end)) __threadfence_block();
+#if ZG_INFLATE_XDEP
+  // Matches resolve in rounds by exact dependencies: a match waits only while the last symbol
+  // starting before the end of its source (found once per batch by a binary search over the
+  // symbols' output offsets) is a pending match whose output reaches into that source. A match
+  // reads at most min(len, dist) source bytes (dest byte i takes source byte i mod dist), all
+  // before its own output, so ready matches never depend on each other. Long ready matches are
+  // copied by the whole wave one after another, short ones by their own lane.
+  const int32_t s_rel = (int32_t)(msrc - pos);                   // source start, batch-relative
+  const int32_t e_rel = s_rel + (int32_t)min(mlen, md);          // source end
+#if ZG_INFLATE_RANGE
+  // The symbols whose output overlaps the source are an index range [lo, hi] (output offsets
+  // are monotonic): hi = the last symbol starting before e_rel, lo = the last starting at or
+  // before s_rel; both found by one interleaved binary search per batch. A round then tests
+  // the pending mask against the range, with no LDS read.
+  if (mine) S.rbeg[lane] = (uint16_t)(mypos - pos);
+  __syncthreads();
+  int32_t hi = -1, lo = 0;
+  if (is_match && e_rel > 0) {
+    hi = 0;
+#pragma unroll
+    for (int32_t step = 32; step; step >>= 1) {
+      if (hi + step < (int32_t)cnt && (int32_t)S.rbeg[hi + step] < e_rel) hi += step;
+      if (lo + step < (int32_t)cnt && (int32_t)S.rbeg[lo + step] <= s_rel) lo += step;
+    }
+  }
+  const uint64_t rmask = hi < 0 ? 0ull : (hi >= 63 ? ~0ull : ((2ull << hi) - 1)) & ~((1ull << lo) - 1);
+#else
+  if (mine) S.rend[lane] = (uint16_t)(mypos - pos + (is_match ? mlen : 1u));
+  if (mine) S.rbeg[lane] = (uint16_t)(mypos - pos);
+  __syncthreads();
+  int32_t hi = -1;  // the last symbol that starts before e_rel
+  if (is_match && e_rel > 0) {
+    hi = 0;
+#pragma unroll
+    for (int32_t step = 32; step; step >>= 1)
+      if (hi + step < (int32_t)cnt && (int32_t)S.rbeg[hi + step] < e_rel) hi += step;
+  }
+#endif
+  bool pending = is_match;
+  uint64_t pm;
+  XPROF(6, 1);
+  XPROF(7, cnt);
+  while ((pm = __ballot(pending)) != 0) {
+    XPROF(5, 1);
+    bool ready = false;
+    if (pending) {
+#if ZG_INFLATE_RANGE
+      ready = (pm & rmask) == 0;
+#else
+      const uint64_t m = hi < 0 ? 0ull : pm & (hi >= 63 ? ~0ull : ((2ull << hi) - 1));
+      ready = m == 0 || (int32_t)S.rend[63 - __builtin_clzll(m)] <= s_rel;
+#endif
+    }
+    const uint64_t lm = __ballot(ready && mlen > 32);
+    if (lm) {  // the first long ready match, by the whole wave (the others wait a round)
+      const int f = __builtin_ctzll(lm);
+      const uint32_t F_lo = __builtin_amdgcn_readlane((uint32_t)mypos, f);
+      const uint32_t F_hi = __builtin_amdgcn_readlane((uint32_t)(mypos >> 32), f);
+      const uint64_t F = ((uint64_t)F_hi << 32) | F_lo;
+      const uint32_t flen = __builtin_amdgcn_readlane(mlen, f), fd = __builtin_amdgcn_readlane(md, f);
+      const float inv = 1.0f / (float)fd;
+      for (uint32_t i = lane; i < flen; i += 64) {
+        uint32_t q = (uint32_t)((float)i * inv);
+        int32_t rm = (int32_t)i - (int32_t)(q * fd);
+        if (rm < 0) rm += fd;
+        if (rm >= (int32_t)fd) rm -= fd;
+        const uint64_t src = F - fd + (uint32_t)rm;
+        const uint8_t v = (src + RING >= batch_end) ? S.ring[src & RMASK] : __builtin_nontemporal_load(out + src);
+        S.ring[(F + i) & RMASK] = v;
+      }
+    }
+    if (lm && lane == __builtin_ctzll(lm)) pending = false;
+    ready = ready && mlen <= 32;
+    const bool in_ring = msrc + RING >= batch_end;
+#if ZG_INFLATE_XW
+    if (ready && in_ring && md >= mlen && mlen <= ZG_INFLATE_XW) {
+      // a short source wholly in the ring, not overlapping the copy: aligned ring words (all
+      // loads in flight together), byte-aligned in registers
+      const uint32_t a0 = (uint32_t)(msrc >> 2), sh = (uint32_t)(msrc & 3), nw = (sh + mlen + 3) >> 2;
+      uint32_t w[ZG_INFLATE_XW / 4 + 1];
+#pragma unroll
+      for (uint32_t j = 0; j <= ZG_INFLATE_XW / 4; j++) w[j] = j < nw ? S.ring32[(a0 + j) & (RING / 4 - 1)] : 0u;
+#pragma unroll
+      for (uint32_t j = 0; j < ZG_INFLATE_XW / 4; j++) {
+        const uint32_t v = __builtin_amdgcn_alignbyte(w[j + 1], w[j], sh);
+#pragma unroll
+        for (uint32_t k = 0; k < 4; k++)
+          if (4 * j + k < mlen) S.ring[(mypos + 4 * j + k) & RMASK] = (uint8_t)(v >> (8 * k));
+      }
+      pending = false;
+    } else
+#endif
+    if (ready) {
+      for (uint32_t i0 = 0; i0 < mlen; i0 += 4) {
+        uint8_t v[4];
+#pragma unroll
+        for (int k = 0; k < 4; k++) {
+          const uint32_t i = i0 + k;
+          const uint32_t r = i < md ? i : i % md;
+          const uint64_t src = msrc + r;
+          v[k] = (i < mlen) ? (in_ring ? S.ring[src & RMASK] : __builtin_nontemporal_load(out + src)) : 0;
+        }
+#pragma unroll
+        for (int k = 0; k < 4; k++)
+          if (i0 + k < mlen) S.ring[(mypos + i0 + k) & RMASK] = v[k];
+      }
+      pending = false;
+    }
+  }
+#else
+  // Matches resolve in rounds: every pending match whose source lies entirely before the first
+  // pending match (or that IS the first one) copies its bytes itself; dest byte i takes source
+  // byte msrc + (i mod d), which is always final, so a lane's copy has no inner dependency.
+  bool pending = is_match;
+  uint64_t pm;
+  XPROF(6, 1);
+  XPROF(7, cnt);
+  while ((pm = __ballot(pending)) != 0) {
+    XPROF(5, 1);
+    const int first = __builtin_ctzll(pm);
+    const uint32_t F_lo = __builtin_amdgcn_readlane((uint32_t)mypos, first);
+    const uint32_t F_hi = __builtin_amdgcn_readlane((uint32_t)(mypos >> 32), first);
+    const uint64_t F = ((uint64_t)F_hi << 32) | F_lo;
+    const uint32_t flen = __builtin_amdgcn_readlane(mlen, first);
+    if (flen > 32) {  // a long match: copied by the whole wave once it is the first pending
+      const uint32_t fd = __builtin_amdgcn_readlane(md, first);
+      const float inv = 1.0f / (float)fd;
+      for (uint32_t i = lane; i < flen; i += 64) {
+        uint32_t q = (uint32_t)((float)i * inv);
+        int32_t rm = (int32_t)i - (int32_t)(q * fd);
+        if (rm < 0) rm += fd;
+        if (rm >= (int32_t)fd) rm -= fd;
+        const uint64_t src = F - fd + (uint32_t)rm;
+        const uint8_t v = (src + RING >= batch_end) ? S.ring[src & RMASK] : __builtin_nontemporal_load(out + src);
+        S.ring[(F + i) & RMASK] = v;
+      }
+      if (lane == first) pending = false;
+      continue;
+    }
+    const bool ready = pending && mlen <= 32 && (lane == first || msrc + mlen <= F);
+    const bool in_ring = msrc + RING >= batch_end;
+#if ZG_INFLATE_XW
+    if (ready && in_ring && md >= mlen && mlen <= ZG_INFLATE_XW) {
+      // a short source wholly in the ring, not overlapping the copy: aligned ring words (all
+      // loads in flight together), byte-aligned in registers
+      const uint32_t a0 = (uint32_t)(msrc >> 2), sh = (uint32_t)(msrc & 3), nw = (sh + mlen + 3) >> 2;
+      uint32_t w[ZG_INFLATE_XW / 4 + 1];
+#pragma unroll
+      for (uint32_t j = 0; j <= ZG_INFLATE_XW / 4; j++) w[j] = j < nw ? S.ring32[(a0 + j) & (RING / 4 - 1)] : 0u;
+#pragma unroll
+      for (uint32_t j = 0; j < ZG_INFLATE_XW / 4; j++) {
+        const uint32_t v = __builtin_amdgcn_alignbyte(w[j + 1], w[j], sh);
+#pragma unroll
+        for (uint32_t k = 0; k < 4; k++)
+          if (4 * j + k < mlen) S.ring[(mypos + 4 * j + k) & RMASK] = (uint8_t)(v >> (8 * k));
+      }
+      pending = false;
+    } else
+#endif
+    if (ready) {
+      for (uint32_t i0 = 0; i0 < mlen; i0 += 4) {
+        uint8_t v[4];
+#pragma unroll
+        for (int k = 0; k < 4; k++) {
+          const uint32_t i = i0 + k;
+          const uint32_t r = i < md ? i : i % md;
+          const uint64_t src = msrc + r;
+          v[k] = (i < mlen) ? (in_ring ? S.ring[src & RMASK] : __builtin_nontemporal_load(out + src)) : 0;
+        }
+#pragma unroll
+        for (int k = 0; k < 4; k++)
+          if (i0 + k < mlen) S.ring[(mypos + i0 + k) & RMASK] = v[k];
+      }
+      pending = false;
+    }
+  }
+#endif
+  pos = batch_end;
+  if (pos - flushed >= FLUSH_MIN) {
+    __syncthreads();
+    flush(S, out, cap, flushed, pos);
+    flushed = pos;
+    __syncthreads();
+  }
+  return true;
+}
+#undef XPROF
+
 }  // namespace
 
 #ifndef ZG_INFLATE_WPE
@@ -556,8 +860,9 @@ __device__ __forceinline__ void flush(const Smem &S, uint8_t *out, uint64_t cap,
 template <bool ZLIB>
 __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(ZG_INFLATE_WPE, 8))) void k_gzip(
     ZgItem *items, uint32_t *status, const uint32_t *kind, uint8_t *dst, uint64_t slot_bytes, uint2 *aux,
-    const uint32_t *order) {
+    const uint32_t *order, uint32_t *seg_scr) {
   __shared__ Smem S;
+  __shared__ uint16_t seg_base[65], seg_skip[64];
   PROF_DECL;
   PROF_T(t_all);
   const uint32_t item = order ? order[blockIdx.x] : blockIdx.x;
@@ -712,8 +1017,124 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(ZG_INFLATE_W
     (void)hlit;
     (void)hdist;
 
-    // ---- symbol batches ----
     bool eob = false;
+#if ZG_INFLATE_SEG
+    // ---- segmented rounds: lane l decodes the stream region [r0 + l*SEGB, r0 + (l+1)*SEGB) serially,
+    // starting OVL bits early so that its chain has met the true one by then (Huffman codes
+    // self-synchronise); lane l is right once the true chain's exit from lane l-1's region is a
+    // symbol start on its own chain (else it re-decodes from that exit). The region records then
+    // run through the batch executor in order. A code past the subtable space ends the path (the
+    // lookahead loop below takes the rest of the block).
+    if (seg_scr) {
+      uint32_t *myrec = seg_scr + ((uint64_t)blockIdx.x * 64 + (uint32_t)lane) * SEGCAP;
+      LaneRd R{B.base, B.nwords, 0, 0, 0, 0, 0};
+      uint64_t r0 = B.consumed;
+      bool fallback = false;
+      while (!eob && !err && !fallback) {
+        PROF_T(t_sd);
+        const uint64_t s_own = r0 + (uint64_t)lane * SEGB, s_end = s_own + SEGB;
+        uint64_t p = lane ? s_own - OVL : r0;
+        uint32_t n;
+        uint64_t mask;
+        uint32_t st = seg_decode(S, R, p, s_own, s_end, end_bits, myrec, n, mask);
+        uint32_t skip = 0;
+        bool ok = lane == 0;
+        bool repaired = false;
+        // the valid prefix: lane l is right when lane l-1 is and ended at the end of its region at
+        // a symbol start of lane l's chain; out-of-sync lanes are re-decoded from that exit
+        for (int rep = 0;; rep++) {
+          const uint64_t e = shfl_up64(p);
+          const uint32_t stp = (uint32_t)__shfl_up((int)st, 1, 64);
+          if (lane && !repaired) {
+            const uint64_t d = e - s_own;
+            ok = stp == SG_END && e >= s_own && d < 64 && ((mask >> (uint32_t)d) & 1);
+            skip = ok ? (uint32_t)__builtin_popcountll(mask & ((1ull << (uint32_t)d) - 1)) : 0u;
+          }  // a repaired lane started at its predecessor's true exit: right (ok stays set)
+          const uint64_t bad = __ballot(!ok);
+          // every lane before the first bad one is right (the chain of checks)
+          const int j = bad ? __builtin_ctzll(bad) : 64;
+          if (j == 64) break;
+          const uint32_t stj = (uint32_t)__builtin_amdgcn_readlane((int)st, j - 1);
+          if (stj != SG_END || rep >= ZG_INFLATE_MAXREP) {
+            if (lane >= j) ok = false;
+            break;
+          }
+          if (lane == j) {  // re-decode from the true exit of lane j-1's region
+            p = e;
+            st = seg_decode(S, R, p, e, s_end, end_bits, myrec, n, mask);
+            skip = 0;
+            repaired = true;
+            ok = true;
+          }
+          // the lanes after j re-check against the updated exits; the earlier ones stay right
+          PROF_CNT(3, 1);
+        }
+        // the round ends at the last valid lane
+        const uint64_t vm = __ballot(ok);
+        const int J = (vm == ~0ull) ? 64 : __builtin_ctzll(~vm);
+        const uint32_t stl = (uint32_t)__builtin_amdgcn_readlane((int)st, J - 1);
+        const uint64_t pl = ((uint64_t)(uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)(p >> 32), J - 1) << 32) |
+                            (uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)p, J - 1);
+        // records of the valid lanes, in stream order
+        const uint32_t cnt_l = (lane < J) ? n - skip : 0u;
+        const uint32_t incl = wave_incl_sum(cnt_l);
+        seg_base[lane] = (uint16_t)(incl - cnt_l);
+        seg_skip[lane] = (uint16_t)skip;
+        if (lane == 63) seg_base[64] = (uint16_t)incl;
+        const uint32_t total = U(__builtin_amdgcn_readlane((int)incl, 63));
+        __threadfence_block();  // the records (global) and bases (LDS) before other lanes read them
+        __syncthreads();
+        PROF_ADD(1, t_sd);
+        PROF_T(t_sx);
+        for (uint32_t g = 0; g < total && !err;) {
+          const uint32_t idx = g + (uint32_t)lane;
+          uint32_t rec = 0, ln = 0;
+          if (idx < total) {
+            int k = 0;  // the lane region holding symbol idx: the last k with seg_base[k] <= idx
+#pragma unroll
+            for (int step = 32; step; step >>= 1)
+              if (k + step < 64 && seg_base[k + step] <= idx) k += step;
+            rec = seg_scr[((uint64_t)blockIdx.x * 64 + (uint32_t)k) * SEGCAP + seg_skip[k] + (idx - seg_base[k])];
+            ln = (rec >> 31) ? (rec & 511) : 1u;
+          }
+          const uint32_t inc = wave_incl_sum(ln);
+          const bool take = idx < total && inc - ln < (uint32_t)BATCH_CAP;
+          const uint64_t tm = __ballot(take);
+          const uint32_t bc = (uint32_t)__builtin_popcountll(tm);
+          const uint32_t bytes = U(__builtin_amdgcn_readlane((int)inc, (int)bc - 1));
+          if (pos + bytes > cap) {
+            err = ZG_DECODED_SIZE_MISMATCH;
+            break;
+          }
+          PROF_CNT(7, bc);
+          PROF_CNT(6, 1);
+#ifdef ZG_PROFILE
+          if (!exec_batch(S, out, cap, pos, flushed, bc, bytes, rec, prof_acc)) err = ZG_CORRUPT_STREAM;
+#else
+          if (!exec_batch(S, out, cap, pos, flushed, bc, bytes, rec, nullptr)) err = ZG_CORRUPT_STREAM;
+#endif
+          g += bc;
+        }
+        PROF_ADD(2, t_sx);
+        if (err) break;
+        if (stl == SG_EOB) {
+          eob = true;
+          bits_seek(B, pl);
+        } else if (stl == SG_END || stl == SG_CAP) {
+          r0 = pl;
+        } else if (stl == SG_SLOW) {
+          fallback = true;
+          bits_seek(B, pl);
+        } else {
+          err = ZG_CORRUPT_STREAM;
+        }
+        __syncthreads();
+      }
+      if (err) break;
+      if (!fallback) continue;  // the block is done (its end-of-block code consumed)
+    }
+#endif
+    // ---- symbol batches ----
     while (!eob && !err) {
       PROF_T(t_dec);
       uint32_t cnt = 0, bytes = 0;
@@ -856,205 +1277,12 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(ZG_INFLATE_W
       PROF_ADD(1, t_dec);
       PROF_T(t_exe);
       __syncthreads();
-      const bool mine = lane < (int)cnt;
-      const uint32_t rec = mine ? S.rec[lane] : 0u;
-      const bool is_match = mine && (rec >> 31);
-      const uint32_t ln = mine ? (is_match ? (rec & 511) : 1u) : 0u;
-      const uint64_t mypos = pos + wave_incl_sum(ln) - ln;  // output offsets: a wave prefix sum
-      if (mine && !is_match) S.ring[mypos & RMASK] = (uint8_t)rec;
-      const uint64_t batch_end = pos + bytes;
-      const uint32_t mlen = rec & 511, md = (rec >> 9) & 0xFFFF;
-      const uint64_t msrc = mypos - md;
-      if (__ballot(is_match && md > mypos)) { err = ZG_CORRUPT_STREAM; break; }  // distance too far back
-      // sources older than the ring are read back from the flushed output
-      if (__ballot(is_match && msrc + RING < batch_end)) __threadfence_block();
-#if ZG_INFLATE_XDEP
-      // Matches resolve in rounds by exact dependencies: a match waits only while the last symbol
-      // starting before the end of its source (found once per batch by a binary search over the
-      // symbols' output offsets) is a pending match whose output reaches into that source. A match
-      // reads at most min(len, dist) source bytes (dest byte i takes source byte i mod dist), all
-      // before its own output, so ready matches never depend on each other. Long ready matches are
-      // copied by the whole wave one after another, short ones by their own lane.
-      const int32_t s_rel = (int32_t)(msrc - pos);                   // source start, batch-relative
-      const int32_t e_rel = s_rel + (int32_t)min(mlen, md);          // source end
-#if ZG_INFLATE_RANGE
-      // The symbols whose output overlaps the source are an index range [lo, hi] (output offsets
-      // are monotonic): hi = the last symbol starting before e_rel, lo = the last starting at or
-      // before s_rel; both found by one interleaved binary search per batch. A round then tests
-      // the pending mask against the range, with no LDS read.
-      if (mine) S.rbeg[lane] = (uint16_t)(mypos - pos);
-      __syncthreads();
-      int32_t hi = -1, lo = 0;
-      if (is_match && e_rel > 0) {
-        hi = 0;
-#pragma unroll
-        for (int32_t step = 32; step; step >>= 1) {
-          if (hi + step < (int32_t)cnt && (int32_t)S.rbeg[hi + step] < e_rel) hi += step;
-          if (lo + step < (int32_t)cnt && (int32_t)S.rbeg[lo + step] <= s_rel) lo += step;
-        }
-      }
-      const uint64_t rmask = hi < 0 ? 0ull : (hi >= 63 ? ~0ull : ((2ull << hi) - 1)) & ~((1ull << lo) - 1);
+#ifdef ZG_PROFILE
+      if (!exec_batch(S, out, cap, pos, flushed, cnt, bytes, S.rec[lane], prof_acc)) { err = ZG_CORRUPT_STREAM; break; }
 #else
-      if (mine) S.rend[lane] = (uint16_t)(mypos - pos + (is_match ? mlen : 1u));
-      if (mine) S.rbeg[lane] = (uint16_t)(mypos - pos);
-      __syncthreads();
-      int32_t hi = -1;  // the last symbol that starts before e_rel
-      if (is_match && e_rel > 0) {
-        hi = 0;
-#pragma unroll
-        for (int32_t step = 32; step; step >>= 1)
-          if (hi + step < (int32_t)cnt && (int32_t)S.rbeg[hi + step] < e_rel) hi += step;
-      }
-#endif
-      bool pending = is_match;
-      uint64_t pm;
-      PROF_CNT(6, 1);
-      PROF_CNT(7, cnt);
-      while ((pm = __ballot(pending)) != 0) {
-        PROF_CNT(5, 1);
-        bool ready = false;
-        if (pending) {
-#if ZG_INFLATE_RANGE
-          ready = (pm & rmask) == 0;
-#else
-          const uint64_t m = hi < 0 ? 0ull : pm & (hi >= 63 ? ~0ull : ((2ull << hi) - 1));
-          ready = m == 0 || (int32_t)S.rend[63 - __builtin_clzll(m)] <= s_rel;
-#endif
-        }
-        const uint64_t lm = __ballot(ready && mlen > 32);
-        if (lm) {  // the first long ready match, by the whole wave (the others wait a round)
-          const int f = __builtin_ctzll(lm);
-          const uint32_t F_lo = __builtin_amdgcn_readlane((uint32_t)mypos, f);
-          const uint32_t F_hi = __builtin_amdgcn_readlane((uint32_t)(mypos >> 32), f);
-          const uint64_t F = ((uint64_t)F_hi << 32) | F_lo;
-          const uint32_t flen = __builtin_amdgcn_readlane(mlen, f), fd = __builtin_amdgcn_readlane(md, f);
-          const float inv = 1.0f / (float)fd;
-          for (uint32_t i = lane; i < flen; i += 64) {
-            uint32_t q = (uint32_t)((float)i * inv);
-            int32_t rm = (int32_t)i - (int32_t)(q * fd);
-            if (rm < 0) rm += fd;
-            if (rm >= (int32_t)fd) rm -= fd;
-            const uint64_t src = F - fd + (uint32_t)rm;
-            const uint8_t v = (src + RING >= batch_end) ? S.ring[src & RMASK] : __builtin_nontemporal_load(out + src);
-            S.ring[(F + i) & RMASK] = v;
-          }
-        }
-        if (lm && lane == __builtin_ctzll(lm)) pending = false;
-        ready = ready && mlen <= 32;
-        const bool in_ring = msrc + RING >= batch_end;
-#if ZG_INFLATE_XW
-        if (ready && in_ring && md >= mlen && mlen <= ZG_INFLATE_XW) {
-          // a short source wholly in the ring, not overlapping the copy: aligned ring words (all
-          // loads in flight together), byte-aligned in registers
-          const uint32_t a0 = (uint32_t)(msrc >> 2), sh = (uint32_t)(msrc & 3), nw = (sh + mlen + 3) >> 2;
-          uint32_t w[ZG_INFLATE_XW / 4 + 1];
-#pragma unroll
-          for (uint32_t j = 0; j <= ZG_INFLATE_XW / 4; j++) w[j] = j < nw ? S.ring32[(a0 + j) & (RING / 4 - 1)] : 0u;
-#pragma unroll
-          for (uint32_t j = 0; j < ZG_INFLATE_XW / 4; j++) {
-            const uint32_t v = __builtin_amdgcn_alignbyte(w[j + 1], w[j], sh);
-#pragma unroll
-            for (uint32_t k = 0; k < 4; k++)
-              if (4 * j + k < mlen) S.ring[(mypos + 4 * j + k) & RMASK] = (uint8_t)(v >> (8 * k));
-          }
-          pending = false;
-        } else
-#endif
-        if (ready) {
-          for (uint32_t i0 = 0; i0 < mlen; i0 += 4) {
-            uint8_t v[4];
-#pragma unroll
-            for (int k = 0; k < 4; k++) {
-              const uint32_t i = i0 + k;
-              const uint32_t r = i < md ? i : i % md;
-              const uint64_t src = msrc + r;
-              v[k] = (i < mlen) ? (in_ring ? S.ring[src & RMASK] : __builtin_nontemporal_load(out + src)) : 0;
-            }
-#pragma unroll
-            for (int k = 0; k < 4; k++)
-              if (i0 + k < mlen) S.ring[(mypos + i0 + k) & RMASK] = v[k];
-          }
-          pending = false;
-        }
-      }
-#else
-      // Matches resolve in rounds: every pending match whose source lies entirely before the first
-      // pending match (or that IS the first one) copies its bytes itself; dest byte i takes source
-      // byte msrc + (i mod d), which is always final, so a lane's copy has no inner dependency.
-      bool pending = is_match;
-      uint64_t pm;
-      PROF_CNT(6, 1);
-      PROF_CNT(7, cnt);
-      while ((pm = __ballot(pending)) != 0) {
-        PROF_CNT(5, 1);
-        const int first = __builtin_ctzll(pm);
-        const uint32_t F_lo = __builtin_amdgcn_readlane((uint32_t)mypos, first);
-        const uint32_t F_hi = __builtin_amdgcn_readlane((uint32_t)(mypos >> 32), first);
-        const uint64_t F = ((uint64_t)F_hi << 32) | F_lo;
-        const uint32_t flen = __builtin_amdgcn_readlane(mlen, first);
-        if (flen > 32) {  // a long match: copied by the whole wave once it is the first pending
-          const uint32_t fd = __builtin_amdgcn_readlane(md, first);
-          const float inv = 1.0f / (float)fd;
-          for (uint32_t i = lane; i < flen; i += 64) {
-            uint32_t q = (uint32_t)((float)i * inv);
-            int32_t rm = (int32_t)i - (int32_t)(q * fd);
-            if (rm < 0) rm += fd;
-            if (rm >= (int32_t)fd) rm -= fd;
-            const uint64_t src = F - fd + (uint32_t)rm;
-            const uint8_t v = (src + RING >= batch_end) ? S.ring[src & RMASK] : __builtin_nontemporal_load(out + src);
-            S.ring[(F + i) & RMASK] = v;
-          }
-          if (lane == first) pending = false;
-          continue;
-        }
-        const bool ready = pending && mlen <= 32 && (lane == first || msrc + mlen <= F);
-        const bool in_ring = msrc + RING >= batch_end;
-#if ZG_INFLATE_XW
-        if (ready && in_ring && md >= mlen && mlen <= ZG_INFLATE_XW) {
-          // a short source wholly in the ring, not overlapping the copy: aligned ring words (all
-          // loads in flight together), byte-aligned in registers
-          const uint32_t a0 = (uint32_t)(msrc >> 2), sh = (uint32_t)(msrc & 3), nw = (sh + mlen + 3) >> 2;
-          uint32_t w[ZG_INFLATE_XW / 4 + 1];
-#pragma unroll
-          for (uint32_t j = 0; j <= ZG_INFLATE_XW / 4; j++) w[j] = j < nw ? S.ring32[(a0 + j) & (RING / 4 - 1)] : 0u;
-#pragma unroll
-          for (uint32_t j = 0; j < ZG_INFLATE_XW / 4; j++) {
-            const uint32_t v = __builtin_amdgcn_alignbyte(w[j + 1], w[j], sh);
-#pragma unroll
-            for (uint32_t k = 0; k < 4; k++)
-              if (4 * j + k < mlen) S.ring[(mypos + 4 * j + k) & RMASK] = (uint8_t)(v >> (8 * k));
-          }
-          pending = false;
-        } else
-#endif
-        if (ready) {
-          for (uint32_t i0 = 0; i0 < mlen; i0 += 4) {
-            uint8_t v[4];
-#pragma unroll
-            for (int k = 0; k < 4; k++) {
-              const uint32_t i = i0 + k;
-              const uint32_t r = i < md ? i : i % md;
-              const uint64_t src = msrc + r;
-              v[k] = (i < mlen) ? (in_ring ? S.ring[src & RMASK] : __builtin_nontemporal_load(out + src)) : 0;
-            }
-#pragma unroll
-            for (int k = 0; k < 4; k++)
-              if (i0 + k < mlen) S.ring[(mypos + i0 + k) & RMASK] = v[k];
-          }
-          pending = false;
-        }
-      }
+      if (!exec_batch(S, out, cap, pos, flushed, cnt, bytes, S.rec[lane], nullptr)) { err = ZG_CORRUPT_STREAM; break; }
 #endif
       PROF_ADD(2, t_exe);
-      PROF_T(t_fl);
-      pos = batch_end;
-      if (pos - flushed >= FLUSH_MIN) {
-        __syncthreads();
-        flush(S, out, cap, flushed, pos);
-        flushed = pos;
-        __syncthreads();
-      }
-      PROF_ADD(3, t_fl);
     }
   }
   if (!err && flushed < pos) {
@@ -1140,17 +1368,26 @@ __global__ __launch_bounds__(1024) void k_order_by_len(const ZgItem *items, cons
   for (uint32_t i = t; i < n; i += 1024) order[atomicAdd(&cnt[1023 - (len_of(i) >> shift)], 1u)] = i;
 }
 
+uint64_t gzip_seg_scratch_bytes(uint32_t n_items) {
+  static const bool on = [] {
+    const char *e = std::getenv("ZGPU_GZIP_SEG");
+    return ZG_INFLATE_SEG && (!e || std::atoi(e) != 0);
+  }();
+  return on ? (uint64_t)n_items * 64 * SEGCAP * 4 : 0;
+}
+
 hipError_t launch_gzip(ZgItem *items, uint32_t *status, uint32_t n_items, uint8_t *dst, uint64_t slot_bytes,
-                       uint32_t *order, hipStream_t s) {
+                       uint32_t *order, uint32_t *seg_scr, hipStream_t s) {
   if (!n_items) return hipSuccess;
   static const bool lpt = [] {
     const char *e = std::getenv("ZGPU_GZIP_LPT");
     return !e || std::atoi(e) != 0;
   }();
   if (!lpt || n_items < 2) order = nullptr;
+  if (!gzip_seg_scratch_bytes(1)) seg_scr = nullptr;
   if (order) hipLaunchKernelGGL(k_order_by_len, dim3(1), dim3(1024), 0, s, items, status, n_items, order);
   hipLaunchKernelGGL(k_gzip<false>, dim3(n_items), dim3(64), 0, s, items, status, nullptr, dst, slot_bytes, nullptr,
-                     order);
+                     order, seg_scr);
   return hipGetLastError();
 }
 
@@ -1158,7 +1395,7 @@ hipError_t launch_zlib_streams(ZgItem *subs, uint32_t *sub_status, const uint32_
                                uint8_t *dst, uint64_t slot, uint2 *aux, hipStream_t s) {
   if (!n_sub) return hipSuccess;
   hipLaunchKernelGGL(k_gzip<true>, dim3(n_sub), dim3(64), 0, s, subs, sub_status, sub_kind, dst, slot, aux,
-                     nullptr);
+                     nullptr, nullptr);
   return hipGetLastError();
 }
 

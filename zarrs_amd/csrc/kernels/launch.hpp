@@ -82,8 +82,11 @@ hipError_t launch_item_resolve(ZgItem *items, uint32_t *status, uint32_t n_items
 // gzip (RFC 1952) member decode: header parse, DEFLATE inflate into dst slots, trailer CRC-32 (IEEE)
 // + ISIZE check of the inflated bytes. On return items[i] points at its slot.
 // order: n_items u32 of scratch for the LPT dispatch order (descending encoded length), or NULL
+// seg_scr: gzip_seg_scratch_bytes(n_items) of record scratch for the segmented symbol decode (NULL:
+// the lookahead decode); 0 bytes when that path is off (ZGPU_GZIP_SEG=0)
+uint64_t gzip_seg_scratch_bytes(uint32_t n_items);
 hipError_t launch_gzip(ZgItem *items, uint32_t *status, uint32_t n_items, uint8_t *dst, uint64_t slot_bytes,
-                       uint32_t *order, hipStream_t s);
+                       uint32_t *order, uint32_t *seg_scr, hipStream_t s);
 // zstd (RFC 8878) frame decode into dst slots: block-parallel (scan, per-block entropy decode,
 // per-item execution) with the serial one-wave-per-item decoder as the fallback.
 struct ZstdScratch {

@@ -317,6 +317,7 @@ struct zgpu_plan {
   bool zstd_serial_off = false, zstd_serial_skipped = false;
   uint32_t *d_zser = nullptr;
   uint32_t *d_order = nullptr;  // gzip stage: LPT dispatch order of the items
+  uint32_t *d_gz_seg = nullptr;  // gzip stage: symbol-record scratch of the segmented decode
   bool no_scatter = false;  // a whole-shard predecode plan: its bytes->bytes stages only (decode_general)
 
   ~zgpu_plan() {
@@ -329,7 +330,7 @@ struct zgpu_plan {
     void *bufs[] = {d_items, d_items_init, d_geom, d_shards, d_index, d_shard_status, d_mids, d_mids_init,
                     d_mid_status, d_shard_status2, d_mid_shards, d_index2, d_bl_need,
                     d_pool[0], d_pool[1], zs.blks, zs.nblk, zs.mode, zs.lit, zs.seq, d_ctl,
-                    d_enc_stage, d_zser, d_order};
+                    d_enc_stage, d_zser, d_order, d_gz_seg};
     for (void *b : bufs) ctx->dev_free(b);
     if (zside) {
       (void)hipStreamSynchronize(zside);
@@ -780,7 +781,10 @@ static void plan_upload(zgpu_plan &P, hipStream_t us) {
       HIPCHK(hipMemcpyAsync(P.d_bl_need, P.bl_need.data(), P.bl_need.size() * 8, hipMemcpyHostToDevice, us));
     }
     for (const Stage &s : P.stages) {
-      if (s.kind == ST_GZIP && !P.d_order) P.d_order = (uint32_t *)C.dev_alloc(ni * 4);
+      if (s.kind == ST_GZIP && !P.d_order) {
+        P.d_order = (uint32_t *)C.dev_alloc(ni * 4);
+        if (const uint64_t b = gzip_seg_scratch_bytes((uint32_t)ni)) P.d_gz_seg = (uint32_t *)C.dev_alloc(b);
+      }
       if (s.kind == ST_ZSTD && !P.zs.blks) {
         uint64_t blk_bytes;
         zstd_scratch_layout(P.slot_bytes, P.zs.blk_cap, blk_bytes, P.zs.lit_stride, P.zs.seq_cap);
@@ -954,7 +958,7 @@ static void plan_enqueue(zgpu_plan &P, uint8_t *out, hipStream_t s) {
         HIPCHK(launch_crc32c_strip(P.d_items, P.d_status, ni, st.at_start, P.validate ? 1 : 0, s));
         break;
       case ST_GZIP:
-        HIPCHK(launch_gzip(P.d_items, P.d_status, ni, P.d_pool[st.pool], P.slot_bytes, P.d_order, s));
+        HIPCHK(launch_gzip(P.d_items, P.d_status, ni, P.d_pool[st.pool], P.slot_bytes, P.d_order, P.d_gz_seg, s));
         break;
       case ST_ZSTD:
         P.zstd_fork(P.zs, s);
