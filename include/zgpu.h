@@ -349,8 +349,8 @@ int zgpu_encode_batch(zgpu_chain *chain, uint32_t ndim, const uint64_t *chunk_sh
  * every gzip / zstd decoder reads back to the input; they are not byte-identical to zlib's or
  * libzstd's output (the Zarr specification fixes the decoded bytes, not the encoder). blosc
  * (BloscCodec::encode, blosc_codec_via_blosc_src.rs:113-128) writes c-blosc 1.x frames with
- * blosclz, lz4 / lz4hc, zlib or zstd streams after a byte shuffle / bitshuffle (snappy:
- * ZGPU_UNSUPPORTED; frames any c-blosc 1.x decoder reads, not byte-identical to c-blosc's).
+ * blosclz, lz4 / lz4hc, snappy, zlib or zstd streams after a byte shuffle / bitshuffle (frames any
+ * c-blosc 1.x decoder reads, not byte-identical to c-blosc's).
  * enc_lens[n] receives each chunk's encoded length; descs[i].dst_cap must be >=
  * zgpu_chain_encoded_bound. zgpu_chain_encoded_bound: the fixed size, or the worst case
  * (gzip_codec.rs:122-136, zstd_codec.rs:132-147; a shard: every inner chunk at its bound + index),

@@ -15,6 +15,11 @@ for v in seg lookahead; do
   ZGPU_GZIP_SEG=$ev timeout -k 10 600 python -u bench.py --workload c3 --no-pmc --no-cpu --secondary= --steps 5 > $O/c3_$v.json 2> $O/c3_$v.err || { tail -5 $O/c3_$v.err; exit 1; }
   python3 -c "import json; d=json.load(open('$O/c3_$v.json')); e=d['host_leg']['dropin_emulation']; print('$v', d['value'], d['ms_per_step'], d['roundtrip_ok'], 'dropin', e['GiBps'], e['threads_one_per_shard']['GiBps'])"
 done
+for v in seg lookahead; do
+  ev=1; [ $v = lookahead ] && ev=0
+  ZGPU_GZIP_SEG=$ev timeout -k 10 600 python -u bench.py --workload blosc-zlib --no-pmc --no-cpu --no-host-leg --secondary= --steps 5 > $O/bz_$v.json 2> $O/bz_$v.err || { tail -5 $O/bz_$v.err; exit 1; }
+  python3 -c "import json; d=json.load(open('$O/bz_$v.json')); print('blosc-zlib $v', d['value'], d['ms_per_step'], d['roundtrip_ok'])"
+done
 for v in base gwin3; do
   lib=""; [ $v != base ] && lib=zarrs_amd/lib_variants/$v/libzgpu.so
   ZGPU_LIB=$lib timeout -k 10 400 python -u bench.py --workload c5 --c5-scale 2 --no-cpu --no-pmc --no-host-leg --secondary= --steps 5 --warmup 2 > $O/c5_$v.json 2> $O/c5_$v.err || { echo "$v failed"; tail -5 $O/c5_$v.err; exit 1; }

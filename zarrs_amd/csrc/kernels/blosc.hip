@@ -1050,7 +1050,7 @@ hipError_t launch_blosc_decode(ZgItem *items, uint32_t *status, uint32_t n_items
                        (uint32_t)D.n_sub, D.tmp, D.sub_slot);
   }
   if (D.n_zlib) {
-    hipError_t e = launch_zlib_streams(D.subs, D.sub_status, D.sub_kind, (uint32_t)D.n_sub, D.tmp, D.sub_slot, D.zaux, s);
+    hipError_t e = launch_zlib_streams(D.subs, D.sub_status, D.sub_kind, (uint32_t)D.n_sub, D.tmp, D.sub_slot, D.zaux, D.zseg, s);
     if (e == hipSuccess) e = launch_adler32_check(D.subs, D.sub_status, D.sub_kind, (uint32_t)D.n_sub, D.zaux, s);
     if (e != hipSuccess) return e;
   }

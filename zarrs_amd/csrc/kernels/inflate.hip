@@ -1392,10 +1392,11 @@ hipError_t launch_gzip(ZgItem *items, uint32_t *status, uint32_t n_items, uint8_
 }
 
 hipError_t launch_zlib_streams(ZgItem *subs, uint32_t *sub_status, const uint32_t *sub_kind, uint32_t n_sub,
-                               uint8_t *dst, uint64_t slot, uint2 *aux, hipStream_t s) {
+                               uint8_t *dst, uint64_t slot, uint2 *aux, uint32_t *seg_scr, hipStream_t s) {
   if (!n_sub) return hipSuccess;
+  if (!gzip_seg_scratch_bytes(1)) seg_scr = nullptr;
   hipLaunchKernelGGL(k_gzip<true>, dim3(n_sub), dim3(64), 0, s, subs, sub_status, sub_kind, dst, slot, aux,
-                     nullptr, nullptr);
+                     nullptr, seg_scr);
   return hipGetLastError();
 }
 

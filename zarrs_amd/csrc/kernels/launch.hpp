@@ -218,6 +218,7 @@ struct BlDecode {
   ZstdScratch zs;
   uint64_t n_sub, n_blk, n_zstd, n_lz4, n_blosclz, n_zlib, n_snappy;  // with a cached layout: capacities (n_* > 0 = launched)
   uint2 *zaux;            // zlib streams: {Adler-32 trailer, -} per stream
+  uint32_t *zseg;         // zlib streams: the segmented symbol decode's record scratch (nullable)
   uint32_t *lz_list;      // lz4 / blosclz / snappy streams: {count, stream indices} (k_lz_list), two lists of
                           // n_sub + 1 entries: streams decoded two per wave, then bitshuffled ones (BL_SUB_WIDE)
   unsigned long long *ovf;  // set by k_blosc_layout when a cached layout is too small (ctl counter)
@@ -246,7 +247,7 @@ struct BlCaps {
 // zlib (RFC 1950) streams of a blosc stream table: DEFLATE by the k_gzip machinery (streams whose
 // kind is BL_KIND_ZLIB and status BL_SKIP; status 0 on success), then the Adler-32 trailer check
 hipError_t launch_zlib_streams(ZgItem *subs, uint32_t *sub_status, const uint32_t *sub_kind, uint32_t n_sub,
-                               uint8_t *dst, uint64_t slot, uint2 *aux, hipStream_t s);
+                               uint8_t *dst, uint64_t slot, uint2 *aux, uint32_t *seg_scr, hipStream_t s);
 hipError_t launch_adler32_check(const ZgItem *subs, uint32_t *sub_status, const uint32_t *sub_kind, uint32_t n_sub,
                                 const uint2 *aux, hipStream_t s);
 hipError_t launch_blosc_layout(const BlInfo *info, uint32_t n_items, uint64_t *bases, const BlCaps &caps,

@@ -284,7 +284,7 @@ struct zgpu_plan {
     size_t n = 0;
   };
   Grow bl_info, bl_bases, bl_subs, bl_sub_status, bl_sub_kind, bl_blocks, bl_tmp, bl_zblks, bl_znblk, bl_zmode,
-      bl_zlit, bl_zseq, bl_zaux, bl_zser, bl_lzl;
+      bl_zlit, bl_zseq, bl_zaux, bl_zser, bl_lzl, bl_zseg;
   uint8_t *bl_h = nullptr;  // pinned: BlInfo read-back (first execution)
   size_t bl_h_n = 0;
   void *grow(Grow &g, size_t bytes) {
@@ -339,7 +339,7 @@ struct zgpu_plan {
     for (hipEvent_t e : zev)
       if (e) (void)hipEventDestroy(e);
     for (Grow *g : {&bl_info, &bl_bases, &bl_subs, &bl_sub_status, &bl_sub_kind, &bl_blocks, &bl_tmp, &bl_zblks,
-                    &bl_znblk, &bl_zmode, &bl_zlit, &bl_zseq, &bl_zaux, &bl_zser, &bl_lzl})
+                    &bl_znblk, &bl_zmode, &bl_zlit, &bl_zseq, &bl_zaux, &bl_zser, &bl_lzl, &bl_zseg})
       ctx->dev_free(g->p);
     ctx->host_free(bl_h);
     ctx->host_free(h_ctl);
@@ -898,7 +898,10 @@ static void blosc_stage(zgpu_plan &P, const Stage &st, uint8_t *out, hipStream_t
     D.sub_slot = (caps.max_ne + 255) & ~(uint64_t)255;
     D.tmp = (uint8_t *)P.grow(P.bl_tmp, D.n_sub * D.sub_slot);
   }
-  if (D.n_zlib) D.zaux = (uint2 *)P.grow(P.bl_zaux, D.n_sub * sizeof(uint2));
+  if (D.n_zlib) {
+    D.zaux = (uint2 *)P.grow(P.bl_zaux, D.n_sub * sizeof(uint2));
+    if (const uint64_t b = gzip_seg_scratch_bytes((uint32_t)D.n_sub)) D.zseg = (uint32_t *)P.grow(P.bl_zseg, b);
+  }
   D.lz_list = (D.n_lz4 || D.n_blosclz || D.n_snappy) ? (uint32_t *)P.grow(P.bl_lzl, 2 * (D.n_sub + 1) * 4) : nullptr;
   if (D.n_zstd) {
     uint64_t blk_bytes;
