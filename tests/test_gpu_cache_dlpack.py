@@ -105,17 +105,14 @@ def test_cache_does_not_keep_failed_chunks(ctx):
 
 
 def test_cache_call_level_error_is_not_cached(ctx):
-    """A chain the planner rejects before any chunk status exists (a transpose before a sharding
-    whose subchunks are shards with a checksum around them: UNSUPPORTED) fails on every read through
-    the cache; no slot is kept."""
+    """A chain the planner rejects before any chunk status exists (a shard index compressed with gzip:
+    the index must have a fixed encoded size, UNSUPPORTED) fails on every read through the cache; no
+    slot is kept."""
     from zarrs_amd import Array, ArrayCached, ChunkCacheDecodedLruSizeLimit, MemoryStore, ZgpuError
-    idx = [{"name": "bytes", "configuration": {"endian": "little"}}, {"name": "crc32c"}]
-    mid = {"name": "sharding_indexed", "configuration": {
-        "chunk_shape": [2], "codecs": [{"name": "bytes", "configuration": {"endian": "little"}}],
-        "index_codecs": idx}}
-    codecs = [{"name": "transpose", "configuration": {"order": [0]}},
-              {"name": "sharding_indexed", "configuration": {
-                  "chunk_shape": [4], "codecs": [mid, {"name": "crc32c"}], "index_codecs": idx}}]
+    idx = [{"name": "bytes", "configuration": {"endian": "little"}}, {"name": "gzip", "configuration": {"level": 1}}]
+    codecs = [{"name": "sharding_indexed", "configuration": {
+        "chunk_shape": [4], "codecs": [{"name": "bytes", "configuration": {"endian": "little"}}],
+        "index_codecs": idx}}]
     meta = {"shape": [16], "data_type": "uint16", "fill_value": 0, "codecs": codecs,
             "chunk_grid": {"name": "regular", "configuration": {"chunk_shape": [8]}}}
     store = MemoryStore({"c/0": bytes(64), "c/1": bytes(64)})

@@ -1690,6 +1690,12 @@ constexpr int LIT_STAGE_R = ZG_LIT_WPE >= 4 ? 4 : 8;  // 16-B staging loads in f
 #ifndef ZG_LIT_STG_PITCH
 #define ZG_LIT_STG_PITCH ZG_LIT_STAGE_W  // bytes per lane window (16-B aligned; 37 KB LDS: 4 workgroups/CU)
 #endif
+#ifndef ZG_LIT_ILP
+#define ZG_LIT_ILP 1  // Huffman chains per lane (2: a lane decodes two segments, interleaved)
+#endif
+static_assert(ZG_LIT_ILP == 1 || (ZG_LIT_ILP == 2 && ZG_LIT_STAGE && ZG_LIT_PACK && ZG_LIT_PACK_B == 8),
+              "two chains per lane need the staged 8-B literal writer");
+constexpr uint32_t LIT_SEGS = LIT_THREADS * ZG_LIT_ILP;  // segments per block record
 #if ZG_LIT_STAGE
 constexpr uint32_t LIT_STG_W = ZG_LIT_STAGE_W;
 constexpr uint32_t LIT_STG_PITCH = ZG_LIT_STG_PITCH;
@@ -1703,12 +1709,12 @@ struct ZLitSmem {
   uint8_t weights[256];
   uint16_t hsorted[256];
   uint32_t tmp[32];
-  int32_t entry[LIT_THREADS], exit_[LIT_THREADS];
-  uint32_t cnt[LIT_THREADS], wsum[4];
+  int32_t entry[LIT_SEGS], exit_[LIT_SEGS];
+  uint32_t cnt[LIT_SEGS], wsum[4 * ZG_LIT_ILP];
   uint32_t ctl[4];  // table log, flags
   uint32_t lin[LIT_LDS / 4 + 8];
 #if ZG_LIT_STAGE
-  uint4 stg[LIT_THREADS * LIT_STG_PITCH / 16];  // per-lane 64-B output windows
+  uint4 stg[LIT_SEGS * LIT_STG_PITCH / 16];  // per-segment output windows
 #endif
 };
 
@@ -2072,6 +2078,262 @@ __device__ bool lits_decode(ZLitSmem &S, const Wd &word, uint32_t nstreams, cons
   return true;
 }
 
+#if ZG_LIT_ILP == 2
+// Two chains per lane. A symbol step is one dependent LDS table read plus ~15 instructions; with
+// one chain per lane the wave waits out that read every symbol and the SIMD issues a third of its
+// cycles (4 waves each). A lane here owns segments t and t + LIT_THREADS of the record's 512 and
+// advances both every step, so two table reads are in flight per wave.
+
+// Writer of one chain's decoded literals (hl_run<true>'s packing): bytes up to the first 8-B
+// boundary singly, then 8-B words, from the first LIT_STG_W-aligned byte on through the segment's
+// LDS window as whole aligned LIT_STG_W-B pieces.
+struct LitPack {
+  uint8_t *out;
+  uint64_t *stg8;
+  uint64_t acc;
+  uint32_t k, n, head, head64;
+  __device__ __forceinline__ void init(uint8_t *o, uint4 *stg) {
+    out = o;
+    stg8 = (uint64_t *)stg;
+    acc = 0;
+    k = n = 0;
+    head = (uint32_t)((8 - ((uintptr_t)o & 7)) & 7);
+    head64 = (uint32_t)((LIT_STG_W - ((uintptr_t)o & (LIT_STG_W - 1))) & (LIT_STG_W - 1));
+  }
+  __device__ __forceinline__ void push(uint32_t e) {
+    if (n < head) {
+      out[n] = (uint8_t)e;
+    } else {
+      acc |= (uint64_t)(e & 255u) << (8 * k);
+      if (++k == 8) {
+        const uint32_t pos = n - 7;
+        if (pos < head64) {
+          *(uint64_t *)(out + pos) = acc;
+        } else {
+          const uint32_t r = (pos - head64) & (LIT_STG_W - 1);
+          stg8[r >> 3] = acc;
+          if (r == LIT_STG_W - 8) {  // window complete: out + pos - r is W-aligned
+            uint4 *g = (uint4 *)(out + pos - r);
+            const uint4 *w = (const uint4 *)stg8;
+#pragma unroll
+            for (uint32_t q = 0; q < LIT_STG_W / 16; q++) g[q] = w[q];
+          }
+        }
+        acc = 0;
+        k = 0;
+      }
+    }
+    n++;
+  }
+  __device__ __forceinline__ void finish() {
+    if (n - k > head64) {  // the staged words of the last, incomplete window
+      const uint32_t done = n - k;
+      const uint32_t w0 = done - ((done - head64) & (LIT_STG_W - 1));
+      for (uint32_t q = w0; q < done; q += 8) *(uint64_t *)(out + q) = stg8[((q - head64) & (LIT_STG_W - 1)) >> 3];
+    }
+    for (uint32_t i = 0; i < k; i++) out[n - k + i] = (uint8_t)(acc >> (8 * i));
+  }
+};
+
+// Advance two chains while p > stop and n < maxn, each on its own word reader; both table reads of
+// a step are issued before either is used.
+template <bool WRITE, class Wd>
+__device__ __forceinline__ void hl_run2(HufLane &H0, int32_t &p0, int32_t stop0, uint32_t &n0, uint32_t max0,
+                                        const Wd &w0, HufLane &H1, int32_t &p1, int32_t stop1, uint32_t &n1,
+                                        uint32_t max1, const Wd &w1, uint32_t tl, const uint16_t *huf, LitPack *P0,
+                                        LitPack *P1) {
+  const uint32_t sh = 64 - tl;
+  bool a0 = p0 > stop0 && n0 < max0, a1 = p1 > stop1 && n1 < max1;
+  while (a0 || a1) {
+    if (a0 && H0.v <= 32) {
+      H0.C |= (uint64_t)w0((H0.lp >> 5) - 1) << (32 - H0.v);
+      H0.v += 32;
+      H0.lp -= 32;
+    }
+    if (a1 && H1.v <= 32) {
+      H1.C |= (uint64_t)w1((H1.lp >> 5) - 1) << (32 - H1.v);
+      H1.v += 32;
+      H1.lp -= 32;
+    }
+    const uint32_t e0 = huf[(uint32_t)(H0.C >> sh)], e1 = huf[(uint32_t)(H1.C >> sh)];
+    if (a0) {
+      const uint32_t nb = e0 >> 8;
+      H0.C <<= nb;
+      H0.v -= (int32_t)nb;
+      p0 -= (int32_t)nb;
+      if (WRITE) P0->push(e0);
+      n0++;
+      a0 = p0 > stop0 && n0 < max0;
+    }
+    if (a1) {
+      const uint32_t nb = e1 >> 8;
+      H1.C <<= nb;
+      H1.v -= (int32_t)nb;
+      p1 -= (int32_t)nb;
+      if (WRITE) P1->push(e1);
+      n1++;
+      a1 = p1 > stop1 && n1 < max1;
+    }
+  }
+}
+
+__device__ __forceinline__ int32_t pick4(const int32_t *a, uint32_t s) {
+  return s == 0 ? a[0] : s == 1 ? a[1] : s == 2 ? a[2] : a[3];
+}
+__device__ __forceinline__ uint32_t pick4(const uint32_t *a, uint32_t s) {
+  return s == 0 ? a[0] : s == 1 ? a[1] : s == 2 ? a[2] : a[3];
+}
+
+// lits_decode with LIT_SEGS = 512 segments (same passes, repair rule and output layout).
+template <class Wd>
+__device__ bool lits_decode2(ZLitSmem &S, const Wd &word, uint32_t nstreams, const int32_t *top, const int32_t *lob,
+                             const uint32_t *nsym, uint32_t tl, uint8_t *lit, uint32_t seg) {
+  const uint32_t t = threadIdx.x;
+  const uint32_t G = LIT_SEGS / nstreams;  // segments per stream (a multiple of 64)
+  uint32_t gi[2], si[2], ji[2], NS[2];
+  int32_t T0[2], L0[2], tj[2], tj1[2];
+#pragma unroll
+  for (int c = 0; c < 2; c++) {
+    gi[c] = t + c * LIT_THREADS;
+    si[c] = gi[c] / G;
+    ji[c] = gi[c] % G;
+    T0[c] = pick4(top, si[c]);
+    L0[c] = pick4(lob, si[c]);
+    NS[c] = pick4(nsym, si[c]);
+    const int64_t len = (int64_t)T0[c] - L0[c];
+    tj[c] = T0[c] - (int32_t)(len * ji[c] / G);
+    tj1[c] = T0[c] - (int32_t)(len * (ji[c] + 1) / G);
+  }
+  // pass 1: entry / exit / count of both segments
+  {
+    const Wd wa = word, wb = word;
+    HufLane H0, H1;
+    int32_t p0 = ji[0] == 0 ? T0[0] : min(T0[0], tj[0] + LIT_WARM);
+    int32_t p1 = ji[1] == 0 ? T0[1] : min(T0[1], tj[1] + LIT_WARM);
+    hl_init(H0, p0, wa);
+    hl_init(H1, p1, wb);
+    uint32_t n0 = 0, n1 = 0;
+    hl_run2<false>(H0, p0, ji[0] ? tj[0] : p0, n0, 0xFFFFFFFFu, wa, H1, p1, ji[1] ? tj[1] : p1, n1, 0xFFFFFFFFu, wb,
+                   tl, S.huf, nullptr, nullptr);
+    LS_ADD(5, n0 + n1);
+    S.entry[gi[0]] = p0;
+    S.entry[gi[1]] = p1;
+    n0 = n1 = 0;
+    hl_run2<false>(H0, p0, tj1[0], n0, NS[0] + 1, wa, H1, p1, tj1[1], n1, NS[1] + 1, wb, tl, S.huf, nullptr, nullptr);
+    S.cnt[gi[0]] = n0;
+    S.cnt[gi[1]] = n1;
+    S.exit_[gi[0]] = p0;
+    S.exit_[gi[1]] = p1;
+  }
+  __syncthreads();
+  // repair rounds (lits_decode's rule, per segment)
+  for (uint32_t round = 0; round < G; round++) {
+    bool wrong[2], fix[2];
+    int32_t ne[2] = {0, 0}, nx[2] = {0, 0};
+    uint32_t nc[2] = {0, 0};
+#pragma unroll
+    for (int c = 0; c < 2; c++) {
+      const uint32_t g = gi[c], j = ji[c];
+      wrong[c] = j != 0 && S.entry[g] != S.exit_[g - 1];
+      fix[c] = wrong[c] && (j <= 1 || S.entry[g - 1] == S.exit_[g - 2]);
+    }
+    __syncthreads();
+    for (int c = 0; c < 2; c++) {
+      if (!fix[c]) continue;
+      const uint32_t g = gi[c];
+      const uint32_t maxn = NS[c] + 1;
+      const RawWord<Wd> rw{word};
+      HufLane Ht, Hw;
+      int32_t pt = S.exit_[g - 1], pw = S.entry[g];
+      ne[c] = pt;
+      hl_init(Ht, pt, rw);
+      hl_init(Hw, pw, rw);
+      uint32_t nt = 0, nw = 0;
+      for (;;) {
+        if (pt == pw) {
+          nc[c] = S.cnt[g] - nw + nt;
+          nx[c] = S.exit_[g];
+          break;
+        }
+        if (pt <= tj1[c] || nt > maxn || nw > maxn) {
+          nc[c] = nt;
+          nx[c] = pt;
+          break;
+        }
+        if (pt > pw) {
+          hl_step(Ht, pt, tl, S.huf, rw);
+          nt++;
+        } else {
+          hl_step(Hw, pw, tl, S.huf, rw);
+          nw++;
+        }
+      }
+    }
+    if (__syncthreads_or(wrong[0] || wrong[1]) == 0) break;
+#pragma unroll
+    for (int c = 0; c < 2; c++)
+      if (fix[c]) {
+        S.entry[gi[c]] = ne[c];
+        S.exit_[gi[c]] = nx[c];
+        S.cnt[gi[c]] = nc[c];
+      }
+    __syncthreads();
+  }
+  // prefix sums in segment order: wave-chain k = c * 4 + wave holds segments [64k, 64k + 64)
+  const uint32_t c0 = S.cnt[gi[0]], c1 = S.cnt[gi[1]];
+  LS_ADD(4, c0 + c1);
+  LS_ADD(6, 2);
+  const uint32_t lane = lane_id(), wave = t >> 6;
+  uint32_t i0 = c0, i1 = c1;
+  for (int o = 1; o < 64; o <<= 1) {
+    const uint32_t u0 = __shfl_up(i0, o, 64), u1 = __shfl_up(i1, o, 64);
+    if ((int)lane >= o) {
+      i0 += u0;
+      i1 += u1;
+    }
+  }
+  if (lane == 63) {
+    S.wsum[wave] = i0;
+    S.wsum[4 + wave] = i1;
+  }
+  __syncthreads();
+  auto pre = [&S](uint32_t k) {  // symbols in wave-chains before k
+    uint32_t b = 0;
+    for (uint32_t q = 0; q < k; q++) b += S.wsum[q];
+    return b;
+  };
+  uint32_t off[2];
+  bool bad = false;
+#pragma unroll
+  for (int c = 0; c < 2; c++) {
+    const uint32_t g = gi[c], j = ji[c], k = c * 4 + wave;
+    const uint32_t k0 = si[c] * G / 64, k1 = (si[c] + 1) * G / 64;  // the stream's wave-chains
+    const uint32_t sb = pre(k0);
+    off[c] = pre(k) + (c ? i1 - c1 : i0 - c0) - sb;
+    if (pre(k1) - sb != NS[c]) bad = true;
+    if (S.entry[g] != (j == 0 ? T0[c] : S.exit_[g - 1])) bad = true;
+    if (j == G - 1 && S.exit_[g] != L0[c]) bad = true;
+  }
+  if (__syncthreads_or(bad)) return false;
+  // pass 2: decode again, writing
+  if (c0 || c1) {
+    const Wd wa = word, wb = word;
+    HufLane H0, H1;
+    int32_t p0 = S.entry[gi[0]], p1 = S.entry[gi[1]];
+    hl_init(H0, p0, wa);
+    hl_init(H1, p1, wb);
+    LitPack P0, P1;
+    P0.init(lit + (uint64_t)si[0] * seg + off[0], &S.stg[gi[0] * (LIT_STG_PITCH / 16)]);
+    P1.init(lit + (uint64_t)si[1] * seg + off[1], &S.stg[gi[1] * (LIT_STG_PITCH / 16)]);
+    uint32_t n0 = 0, n1 = 0;
+    hl_run2<true>(H0, p0, tj1[0], n0, c0, wa, H1, p1, tj1[1], n1, c1, wb, tl, S.huf, &P0, &P1);
+    P0.finish();
+    P1.finish();
+  }
+  return true;
+}
+#endif
+
 #if ZG_HUF_SPLIT
 struct ZHufSmem {
   uint16_t huf[1 << MAX_HUF_LOG];
@@ -2116,6 +2378,11 @@ __global__ __launch_bounds__(64) void k_zstd_huf(const ZgItem *items, const uint
 }
 #endif
 
+#if ZG_LIT_ILP == 2
+#define ZG_LITS_DECODE lits_decode2
+#else
+#define ZG_LITS_DECODE lits_decode
+#endif
 __global__ __launch_bounds__(LIT_THREADS) __attribute__((amdgpu_waves_per_eu(ZG_LIT_WPE, 8))) void k_zstd_lits(const ZgItem *items, uint32_t *status, const ZBlk *blks,
                                                            uint32_t blk_cap, const uint32_t *nblk,
                                                            const uint32_t *zmode, uint32_t n_items,
@@ -2236,7 +2503,7 @@ __global__ __launch_bounds__(LIT_THREADS) __attribute__((amdgpu_waves_per_eu(ZG_
         __syncthreads();
         const int32_t n32 = (int32_t)nw;
         auto word = [n32](int32_t k) -> uint32_t { return (k >= 0 && k < n32) ? S.lin[k] : 0u; };
-        ok = lits_decode(S, word, nstreams, top, lob, s_n, tl, lit, seg);
+        ok = ZG_LITS_DECODE(S, word, nstreams, top, lob, s_n, tl, lit, seg);
       } else {
         const gu32 *Wp = (const gu32 *)(words + wbase);
         const int64_t lim = nwords_item - wbase;
@@ -2249,7 +2516,7 @@ __global__ __launch_bounds__(LIT_THREADS) __attribute__((amdgpu_waves_per_eu(ZG_
 #else
         auto word = [Wp, lim](int32_t k) -> uint32_t { return (k >= 0 && k < lim) ? Wp[k] : 0u; };
 #endif
-        ok = lits_decode(S, word, nstreams, top, lob, s_n, tl, lit, seg);
+        ok = ZG_LITS_DECODE(S, word, nstreams, top, lob, s_n, tl, lit, seg);
       }
     }
     if (!ok && t == 0) status[item] = ZG_CORRUPT_STREAM;
