@@ -32,7 +32,7 @@
  *   status codes        <- CodecError variants (zarrs_codec/src/lib.rs:617-686), 1:1 (see below).
  *
  * Threading: every entry point is thread-safe. Calls on one context run concurrently: each takes one
- * of the context's lanes (stream + copy streams; ZGPU_CTX_LANES, default 4) for its duration and
+ * of the context's lanes (stream + copy streams; ZGPU_CTX_LANES, default 8) for its duration and
  * waits when all are busy; the context's pooled memory is shared under an allocator lock. A plan
  * serialises its own executes.
  * Stream ordering: a call runs on the caller's hip_stream (device inputs/outputs must be ready in

@@ -495,7 +495,10 @@ namespace zgpu {
 // Box copy between two device arrays (coalesced calls: a caller's window of the batch's stacked
 // output packed into its compact layout before the one D2H copy). One wave per contiguous run; 16-B
 // lanes when both runs and their length allow it, else 4-B, else bytes.
-__global__ __launch_bounds__(256) void k_box_copy(const uint8_t *__restrict__ src, uint8_t *__restrict__ dst,
+// One-wave workgroups: the coalesced drop-in path launches this while other lanes' decodes hold the
+// CUs with long-running one-wave items, and a 4-wave workgroup waited for four free slots on one CU
+// (trace: 11 ms median for 30-60 MB packs).
+__global__ __launch_bounds__(64) void k_box_copy(const uint8_t *__restrict__ src, uint8_t *__restrict__ dst,
                                                    ZgBoxCopy P) {
   const uint32_t lane = threadIdx.x & 63;
   const uint64_t waves = (uint64_t)gridDim.x * (blockDim.x >> 6);
@@ -524,8 +527,8 @@ __global__ __launch_bounds__(256) void k_box_copy(const uint8_t *__restrict__ sr
 
 hipError_t launch_box_copy(const uint8_t *src, uint8_t *dst, const ZgBoxCopy &P, hipStream_t s) {
   if (!P.n_runs || !P.run_bytes) return hipSuccess;
-  const uint64_t blocks = std::min<uint64_t>((P.n_runs + 3) / 4, (uint64_t)device_cu_count() * 16);
-  hipLaunchKernelGGL(k_box_copy, dim3((uint32_t)blocks), dim3(256), 0, s, src, dst, P);
+  const uint64_t blocks = std::min<uint64_t>(P.n_runs, (uint64_t)device_cu_count() * 64);
+  hipLaunchKernelGGL(k_box_copy, dim3((uint32_t)blocks), dim3(64), 0, s, src, dst, P);
   return hipGetLastError();
 }
 

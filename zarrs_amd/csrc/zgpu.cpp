@@ -67,7 +67,8 @@ struct HipFail {
 // steady-state decode performs no hipMalloc) and a small pool of "lanes" (a stream, two copy streams
 // and an ordering event): concurrent calls on one context each take a lane and run side by side on
 // the GPU (zarrs calls a codec from many rayon workers at once); a call that finds every lane busy
-// waits for one. ZGPU_CTX_LANES sets the pool size (default 4, the hardware queues of a process).
+// waits for one. ZGPU_CTX_LANES sets the pool size (default 8: coalesced drop-in calls measured
+// 10.7 -> 11.6 GiB/s going from 4 to 8, profiles/r04o_dropin_lanes_ab.txt).
 // ------------------------------------------------------------------------------------------------
 struct Coalescer;
 static void delete_coalescer(Coalescer *co);
@@ -75,6 +76,7 @@ static void delete_coalescer(Coalescer *co);
 struct Lane {
   hipStream_t stream = nullptr;              // the call's stream when the caller passes none
   hipStream_t copy[2] = {nullptr, nullptr};  // H2D / D2H streams of the pipelined host paths (lazy)
+  hipStream_t out_hi = nullptr;               // high-priority stream of a coalesced batch's pack + D2H (lazy)
   hipEvent_t order_ev = nullptr;              // legacy-stream -> lane-stream ordering (pick_stream)
 };
 
@@ -89,7 +91,7 @@ struct zgpu_ctx {
   std::mutex lane_mu;
   std::condition_variable lane_cv;
   std::vector<Lane *> lanes_all, lanes_free;
-  uint32_t max_lanes = 4;
+  uint32_t max_lanes = 8;
   hipStream_t peer = nullptr;  // peer copies of the multi-device read (lazy)
   struct Coalescer *co = nullptr;  // ZGPU_COALESCE batching (lazy, under mu)
 
@@ -171,8 +173,10 @@ struct zgpu_ctx {
   }
   ~zgpu_ctx() {
     (void)hipSetDevice(device);
-    for (Lane *L : lanes_all)
+    for (Lane *L : lanes_all) {
       if (L->stream) (void)hipStreamSynchronize(L->stream);
+      if (L->out_hi) (void)hipStreamSynchronize(L->out_hi);
+    }
     for (auto &kv : free_dev) (void)hipFree(kv.second);
     for (auto &kv : live_dev) (void)hipFree(kv.first);
     for (auto &kv : free_host) (void)hipHostFree(kv.second);
@@ -180,6 +184,7 @@ struct zgpu_ctx {
     for (Lane *L : lanes_all) {
       if (L->stream) (void)hipStreamDestroy(L->stream);
       if (L->order_ev) (void)hipEventDestroy(L->order_ev);
+      if (L->out_hi) (void)hipStreamDestroy(L->out_hi);
       for (hipStream_t cs : L->copy)
         if (cs) (void)hipStreamDestroy(cs);
       delete L;
@@ -2108,6 +2113,7 @@ struct CoBatch {
   bool closed = false;
   std::condition_variable cv;
   uint8_t *pack = nullptr;  // pinned: every caller's window, compact, back to back
+  uint64_t id = 0;          // trace id
   ~CoBatch() {
     if (pack) C->host_free(pack);
   }
@@ -2126,21 +2132,24 @@ struct Coalescer {
   std::map<CoKey, std::shared_ptr<CoBatch>> open;
   uint32_t window_us = 200, max_calls = 8;
   uint64_t max_bytes = 1ull << 30;
-  uint64_t batches = 0, calls = 0;
+  uint64_t batches = 0, calls = 0, seq = 0;
 };
 
 // ZGPU_TRACE=1: one stderr line per coalesced-batch phase (microseconds since the first trace)
-static void co_trace(const char *what, const void *batch, uint64_t a = 0, uint64_t b = 0) {
+static bool co_tracing() {
   static const bool on = [] {
     const char *e = std::getenv("ZGPU_TRACE");
     return e && std::atoi(e) != 0;
   }();
-  if (!on) return;
+  return on;
+}
+static void co_trace(const char *what, uint64_t batch, uint64_t a = 0, uint64_t b = 0) {
+  if (!co_tracing()) return;
   static const auto t0 = std::chrono::steady_clock::now();
   const long long us =
       std::chrono::duration_cast<std::chrono::microseconds>(std::chrono::steady_clock::now() - t0).count();
-  std::fprintf(stderr, "[zgpu-trace] %lld %s %p %llu %llu\n", us, what, batch, (unsigned long long)a,
-               (unsigned long long)b);
+  std::fprintf(stderr, "[zgpu-trace] %lld %s %llu %llu %llu\n", us, what, (unsigned long long)batch,
+               (unsigned long long)a, (unsigned long long)b);
 }
 
 static Coalescer &coalescer(zgpu_ctx *C) {
@@ -2191,9 +2200,9 @@ static void co_run(CoBatch &B, Lane *LN) {
   }
   HostStage H(C);
   std::vector<zgpu_chunk_desc> local;
-  co_trace("batch-start", &B, B.calls.size(), all.size());
+  co_trace("batch-start", B.id, B.calls.size(), all.size());
   stage_host_inputs(H, all.data(), all.size(), local, s);
-  co_trace("h2d-done", &B);
+  co_trace("h2d-done", B.id);
   uint64_t row_elems = 1;
   for (uint32_t d = 1; d < nd; d++) row_elems *= stacked[d];
   const uint64_t stacked_bytes = stacked[0] * row_elems * es;
@@ -2207,13 +2216,29 @@ static void co_run(CoBatch &B, Lane *LN) {
   try {
     std::vector<int32_t> ast(all.size(), 0);
     decode_device(ch, nd, local.data(), local.size(), dout, stacked, c0.flags, ast.data(), s);
-    co_trace("decode-done", &B);
+    co_trace("decode-done", B.id);
     const SizeDetail sd = g_size_detail;
     for (size_t j = 0; j < all.size(); j++) st[owner[j].first][owner[j].second] = ast[j];
     if (sd.valid && sd.desc < owner.size()) {
       CoCall &c = *B.calls[owner[sd.desc].first];
       c.sd = sd;
       c.sd.desc = owner[sd.desc].second;
+    }
+    // The pack kernels and the D2H run on a high-priority stream: the other lanes' decodes hold the
+    // CUs with long-running waves, and a normal-priority pack kernel queued behind them waited for
+    // their slots (trace: 60 MB packs taking 20+ ms). ZGPU_CO_HIPRIO=0: the lane's own stream.
+    static const bool hiprio = [] {
+      const char *e = std::getenv("ZGPU_CO_HIPRIO");
+      return !e || std::atoi(e) != 0;
+    }();
+    if (hiprio) {
+      if (!LN->out_hi) {
+        int least = 0, greatest = 0;
+        HIPCHK(hipDeviceGetStreamPriorityRange(&least, &greatest));
+        HIPCHK(hipStreamCreateWithPriority(&LN->out_hi, hipStreamNonBlocking, greatest));
+      }
+      HIPCHK(hipStreamSynchronize(s));  // (decode_device has read its statuses back: a no-op)
+      s = LN->out_hi;
     }
     // pack: a window whose trailing extents are the stacked ones is already compact in place
     bool compact = true;
@@ -2249,12 +2274,17 @@ static void co_run(CoBatch &B, Lane *LN) {
     }
     // power-of-two size classes (>= 64 MiB): batches of varying size reuse pooled pinned buffers
     // instead of page-locking new ones
+    if (co_tracing()) {
+      HIPCHK(hipStreamSynchronize(s));
+      co_trace("packed", B.id, compact ? 0 : 1);
+    }
     uint64_t cls = 64ull << 20;
     while (cls < pack_bytes) cls <<= 1;
     B.pack = (uint8_t *)C->host_alloc(cls);
+    co_trace("pack-alloc", B.id);
     if (pack_bytes) HIPCHK(hipMemcpyAsync(B.pack, src, pack_bytes, hipMemcpyDeviceToHost, s));
     HIPCHK(hipStreamSynchronize(s));
-    co_trace("d2h-done", &B, pack_bytes);
+    co_trace("d2h-done", B.id, pack_bytes);
   } catch (...) {
     C->dev_free(dout);
     C->dev_free(dpack);
@@ -2272,10 +2302,79 @@ static void co_run(CoBatch &B, Lane *LN) {
   }
 }
 
+// A caller's encoded bytes copied into pinned memory by the caller's own thread before it joins a
+// batch: a batch's callers pack their inputs in parallel (each on its own thread, overlapping the
+// other lanes' GPU work) and the leader's upload is one DMA per contiguous range, instead of the
+// leader staging every caller's pageable bytes itself. Ranges (descriptors sorted by address, touching
+// ones merged) are placed back to back; local[i].enc points into the pinned copy. Returns nullptr
+// (local untouched) when there is nothing to copy or the bytes are pinned already.
+static uint8_t *pin_caller_inputs(zgpu_ctx *C, const zgpu_chunk_desc *descs, uint64_t n,
+                                  std::vector<zgpu_chunk_desc> &local) {
+  std::vector<uint64_t> order;
+  for (uint64_t i = 0; i < n; i++)
+    if (descs[i].enc && descs[i].enc_len) order.push_back(i);
+  if (order.empty()) return nullptr;
+  std::sort(order.begin(), order.end(),
+            [&](uint64_t a, uint64_t b) { return (uintptr_t)descs[a].enc < (uintptr_t)descs[b].enc; });
+  std::vector<HostRange> ranges;
+  std::vector<uint64_t> range_of(n, 0);
+  uint64_t total = 0;
+  for (uint64_t i : order) {
+    const uint8_t *p = (const uint8_t *)descs[i].enc;
+    if (!ranges.empty() && p <= ranges.back().src + ranges.back().len) {
+      HostRange &r = ranges.back();
+      const uint64_t end = std::max<uint64_t>((uint64_t)(p - r.src) + descs[i].enc_len, r.len);
+      total += end - r.len;
+      r.len = end;
+    } else {
+      ranges.push_back(HostRange{p, descs[i].enc_len, total});
+      total += descs[i].enc_len;
+    }
+    range_of[i] = ranges.size() - 1;
+  }
+  bool pinned = true;
+  for (const HostRange &r : ranges)
+    if (!host_is_pinned(r.src) || !host_is_pinned(r.src + r.len - 1)) {
+      pinned = false;
+      break;
+    }
+  if (pinned) return nullptr;
+  uint64_t cls = 4ull << 20;  // power-of-two classes: the pooled buffers are reused call after call
+  while (cls < total) cls <<= 1;
+  uint8_t *pin = (uint8_t *)C->host_alloc(cls);
+  std::vector<uint8_t *> d;
+  std::vector<const uint8_t *> sp;
+  std::vector<uint64_t> ln;
+  for (const HostRange &r : ranges) {
+    d.push_back(pin + r.dev_off);
+    sp.push_back(r.src);
+    ln.push_back(r.len);
+  }
+  parallel_memcpy(d, sp, ln, 2);
+  local.assign(descs, descs + n);
+  for (uint64_t i : order) {
+    const HostRange &r = ranges[range_of[i]];
+    local[i].enc = pin + r.dev_off + ((const uint8_t *)descs[i].enc - r.src);
+  }
+  return pin;
+}
+
 static int coalesced_call(zgpu_chain *ch, uint32_t nd, const zgpu_chunk_desc *descs, uint64_t n,
                           const zgpu_out_view &V, uint32_t flags, int32_t *status) {
   zgpu_ctx *C = ch->ctx;
   Coalescer &K = coalescer(C);
+  static const bool pin_in = [] {
+    const char *e = std::getenv("ZGPU_CO_PIN");
+    return !e || std::atoi(e) != 0;
+  }();
+  std::vector<zgpu_chunk_desc> pinned_descs;
+  struct PinGuard {
+    zgpu_ctx *C;
+    uint8_t *p;
+    ~PinGuard() { C->host_free(p); }
+  } pin{C, pin_in ? pin_caller_inputs(C, descs, n, pinned_descs) : nullptr};
+  co_trace("pinned", 0, pin.p ? 1 : 0);
+  if (pin.p) descs = pinned_descs.data();
   CoCall me{ch, nd, descs, n, V, flags, status};
   for (uint64_t i = 0; i < n; i++)
     if (descs[i].enc) me.enc_bytes += descs[i].enc_len;
@@ -2287,6 +2386,7 @@ static int coalesced_call(zgpu_chain *ch, uint32_t nd, const zgpu_chunk_desc *de
   if (it == K.open.end()) {
     B = std::make_shared<CoBatch>();
     B->C = C;
+    B->id = ++K.seq;
     K.open[key] = B;
     leader = true;
   } else {
@@ -2294,7 +2394,7 @@ static int coalesced_call(zgpu_chain *ch, uint32_t nd, const zgpu_chunk_desc *de
   }
   B->calls.push_back(&me);
   B->bytes += me.enc_bytes;
-  co_trace(leader ? "arrive-lead" : "arrive-join", B.get(), me.enc_bytes);
+  co_trace(leader ? "arrive-lead" : "arrive-join", B->id, me.enc_bytes);
   auto close = [&]() {
     B->closed = true;
     auto jt = K.open.find(key);
@@ -2320,6 +2420,7 @@ static int coalesced_call(zgpu_chain *ch, uint32_t nd, const zgpu_chunk_desc *de
       rc = ZGPU_HIP_ERROR;
       err = std::string(e.what) + ": " + hipGetErrorString(e.e);
     }
+    co_trace("lane", B->id);
     lk.lock();
     if (!B->closed) close();
     K.batches++;
@@ -2362,7 +2463,7 @@ static int coalesced_call(zgpu_chain *ch, uint32_t nd, const zgpu_chunk_desc *de
   // the batch's callers place their rows concurrently; each takes its share of the copy threads
   const int share = std::max<int>(1, host_copy_threads() / (int)std::max<size_t>(1, B->calls.size()));
   copy_box_runs(R, (uint8_t *)V.base, B->pack + me.pack_off, 0, nb, true, std::min(share, 4));
-  co_trace("copied-out", B.get(), nb);
+  co_trace("copied-out", B->id, nb);
   if (me.rc) set_err(me.rc, zgpu_status_name(me.rc));
   return me.rc;
 }
