@@ -203,6 +203,15 @@ int main(int argc, char **argv) {
   for (int k = 0; k < NK; k++) tot += best[k];
   printf("blocks %llu (%.1f/chunk), mode[0]=%u, bad=%d\n", (unsigned long long)blocks, (double)blocks / n, mode[0], bad);
   for (int k = 0; k < NK; k++) printf("  %-12s %8.3f ms\n", kn[k], best[k]);
+#ifdef ZG_LIT_PROF
+  {
+    unsigned long long z[8];
+    CK(hipMemcpyFromSymbol(z, HIP_SYMBOL(zgpu::g_litprof), sizeof(z)));
+    const double r = (double)(z[5] ? z[5] : 1);
+    printf("lits phases per record (s_memtime ticks, 100 MHz; all reps): pass1 %.0f repairs %.0f prefix %.0f pass2 %.0f | records %llu\n",
+           z[0] / r, z[1] / r, z[2] / r, z[3] / r, z[5]);
+  }
+#endif
 #ifdef ZG_LIT_STATS
   {
     unsigned long long z[8];

@@ -18,6 +18,7 @@
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
+#include <type_traits>
 
 #include "../common.hpp"
 #include "launch.hpp"
@@ -1677,7 +1678,8 @@ constexpr int LIT_STAGE_R = ZG_LIT_WPE >= 4 ? 4 : 8;  // 16-B staging loads in f
 #define ZG_LIT_PACK_B 8
 #endif
 #ifndef ZG_LIT_GWIN
-#define ZG_LIT_GWIN 2  // literal sections beyond LIT_LDS: 1 per-lane 16-B window, 2 32-B + prefetch
+#define ZG_LIT_GWIN 4  // literal sections beyond LIT_LDS: 1 per-lane 16-B window, 2 32-B + prefetch,
+                       // 3 64-B + prefetch, 4 GBlk (32-B blocks moved in lockstep rounds)
 #endif
 #ifndef ZG_LIT_STAGE
 #define ZG_LIT_STAGE 1  // 1: a lane's decoded literals leave through an LDS window, stored as whole
@@ -1731,6 +1733,267 @@ __device__ __forceinline__ void hl_init(HufLane &H, int32_t p, const Wd &word) {
   H.v = p - H.lp;  // (32, 64]
   H.C = V << (64 - H.v);
 }
+// word-reader hooks of hl_run: a plain reader always has the word; GBlk (below) has it only inside
+// its current block
+template <class Wd>
+__device__ __forceinline__ void wd_start(const Wd &, const HufLane &) {}
+
+// Literal-section words through a window of one 32-B block plus the block below it, moved in
+// lockstep (ZG_LIT_GWIN 4). The per-lane prefetching readers (GWordPF) let each lane switch blocks on
+// its own; but a wave's load counter is shared, so a lane switching blocks waited for every load the
+// other lanes had just issued (s_waitcnt vmcnt(0)), one memory round trip nearly every symbol step
+// (C5: ~2,000 cycles per step). Here a lane whose next word lies below its block stops; once every
+// lane of the wave has stopped or finished, the stopped lanes take the prefetched block (loaded one
+// round - ~40 symbols - earlier) and prefetch the next one. No load is waited for inside a round.
+struct GBlk {
+  const gu32 *Wp;
+  int64_t lim;
+  mutable uintptr_t cb;   // address of the current block
+  mutable zv4u a0, a1;    // block A
+  mutable zv4u b0, b1;    // block B
+  mutable uint32_t cur;   // 0: A is the current block and B the one below it; 1: the reverse
+  __device__ __forceinline__ static void ld(uintptr_t b, zv4u &x0, zv4u &x1) {
+    const __attribute__((address_space(1))) zv4u *q = (const __attribute__((address_space(1))) zv4u *)b;
+    x0 = q[0];
+    x1 = q[1];
+  }
+  __device__ __forceinline__ uintptr_t below(uintptr_t b) const {  // never before Wp's block
+    return b > ((uintptr_t)Wp & ~(uintptr_t)31) ? b - 32 : b;
+  }
+  __device__ __forceinline__ uint32_t operator()(int32_t k) const { return (k >= 0 && k < lim) ? Wp[k] : 0u; }
+  // window at the block of word k (the next word the lane reads), k clamped into the section
+  __device__ __forceinline__ void start(int32_t k) const {
+    const int32_t kc = k < 0 ? 0 : (k >= lim ? (int32_t)(lim - 1) : k);
+    cb = (uintptr_t)(Wp + kc) & ~(uintptr_t)31;
+    ld(cb, a0, a1);
+    cur = 0;
+  }
+  // A current again (hl_run's rounds alternate A and B in unrolled code, so no block is ever copied
+  // between registers in a round - a copy of a prefetched block is a wait for it)
+  __device__ __forceinline__ void norm() const {
+    if (cur) {
+      const zv4u t0 = a0, t1 = a1;
+      a0 = b0;
+      a1 = b1;
+      b0 = t0;
+      b1 = t1;
+      cur = 0;
+    }
+  }
+  // Straight-line (selects, no branches): written with ?: chains and short-circuit tests the
+  // compiler branched on every condition, and the symbol loop became ~50 scalar exec-mask
+  // instructions a step.
+  template <int P>
+  __device__ __forceinline__ bool get(int32_t k, uint32_t &w) const {
+    const bool inr = (k >= 0) & ((int64_t)k < lim);
+    const uintptr_t a = (uintptr_t)(Wp + k);
+    const bool inb = (uint32_t)((a ^ cb) >> 5) == 0u;  // same 32-B block (the low 32 bits decide:
+                                                        // k moves by words from inside cb's block)
+    const uint32_t i = (uint32_t)(a >> 2);
+    const zv4u lo = P ? b0 : a0, hi = P ? b1 : a1;
+    const bool h4 = (i & 4u) != 0u, h1 = (i & 1u) != 0u, h2 = (i & 2u) != 0u;
+    const uint32_t x0 = h4 ? hi.x : lo.x, x1 = h4 ? hi.y : lo.y, x2 = h4 ? hi.z : lo.z, x3 = h4 ? hi.w : lo.w;
+    const uint32_t y0 = h1 ? x1 : x0, y1 = h1 ? x3 : x2;
+    const uint32_t v = h2 ? y1 : y0;
+    w = (inr & inb) ? v : 0u;
+    return !inr | inb;
+  }
+  // start of a round reading block P: wait for everything issued before (the block itself was
+  // prefetched a round ago), then prefetch the block below into the other registers. The explicit
+  // wait comes first on purpose: left to the compiler, pass 2's stores (same counter, unordered
+  // against loads) and the merged paths of the lanes' exits got a vmcnt(0) placed after the
+  // prefetch, a wait for it. (gfx9 encoding: vmcnt 0, expcnt 7, lgkmcnt 15.)
+  template <int P>
+  __device__ __forceinline__ void pre() const {
+    __builtin_amdgcn_s_waitcnt(0x0F70);
+    if (P == 0) ld(below(cb), b0, b1);
+    else ld(below(cb), a0, a1);
+  }
+  // block P is used up: the block below (prefetched into the other registers) becomes current
+  __device__ __forceinline__ void adv() const { cb -= 32; }
+};
+__device__ __forceinline__ void wd_start(const GBlk &w, const HufLane &H) { w.start((H.lp >> 5) - 1); }
+template <class Wd>
+struct WdBlocks {
+  static constexpr bool value = false;
+};
+template <>
+struct WdBlocks<GBlk> {
+  static constexpr bool value = true;
+};
+template <int P, class Wd>
+__device__ __forceinline__ bool wd_get_p(const Wd &w, int32_t k, uint32_t &out) {
+  if constexpr (WdBlocks<Wd>::value) return w.template get<P>(k, out);
+  else {
+    out = w(k);
+    return true;
+  }
+}
+
+#ifndef ZG_LIT_BF
+#define ZG_LIT_BF 1  // 1: both passes' symbol loops in straight-line form (hl_count_bf / hl_write_bf)
+#endif
+// Pass 1's loop without branches inside a step: the refill is computed every step and applied under a
+// mask, and the loop has one exit (done, or blocked on a GBlk window). The scalar unit is shared by
+// the CU's four SIMDs, and the branchy form spent ~50 scalar (exec-mask) instructions per step for
+// ~45 vector ones.
+template <int P, class Wd>
+__device__ __forceinline__ uint32_t wd_getm(const Wd &w, int32_t k, bool &ok) {
+  if constexpr (WdBlocks<Wd>::value) {
+    uint32_t v;
+    ok = w.template get<P>(k, v);
+    return v;
+  } else {
+    ok = true;
+    return w(k);
+  }
+}
+template <class Wd>
+__device__ __forceinline__ uint32_t hl_count_bf(HufLane &H, int32_t &p, int32_t stop, uint32_t tl,
+                                                const uint16_t *huf, const Wd &word, uint32_t maxn) {
+  uint32_t n = 0;
+  const uint32_t sh = 64 - tl;
+  auto round = [&](auto par) -> bool {
+    constexpr int P = decltype(par)::value;
+    if constexpr (WdBlocks<Wd>::value) word.template pre<P>();
+    bool ok;
+    uint32_t wn = wd_getm<P>(word, (H.lp >> 5) - 1, ok);
+    bool go = (p > stop) & (n < maxn) & (ok | (H.v > 32));
+    while (go) {
+      const bool need = H.v <= 32;
+      const uint32_t wv = need ? wn : 0u;
+      H.C |= (uint64_t)wv << ((uint32_t)(32 - H.v) & 63u);
+      const int32_t add = need ? 32 : 0;
+      H.v += add;
+      H.lp -= add;
+      const uint32_t nb = huf[(uint32_t)(H.C >> sh)] >> 8;
+      H.C <<= nb;
+      H.v -= (int32_t)nb;
+      p -= (int32_t)nb;
+      n++;
+      wn = wd_getm<P>(word, (H.lp >> 5) - 1, ok);
+      go = (p > stop) & (n < maxn) & (ok | (H.v > 32));
+    }
+    return (p > stop) & (n < maxn);  // still running: stopped at the window's end
+  };
+  if constexpr (WdBlocks<Wd>::value) {
+    word.norm();
+    for (;;) {
+      if (!round(std::integral_constant<int, 0>{})) break;
+      word.adv();
+      if (!round(std::integral_constant<int, 1>{})) {
+        word.cur = 1;
+        break;
+      }
+      word.adv();
+    }
+  } else {
+    round(std::integral_constant<int, 0>{});
+  }
+  return n;
+}
+
+#if ZG_LIT_STAGE
+// Pass 2 in the same form: the symbols of a lane go into 8-B words of the output aligned to 8 B; a
+// completed word is the one branch of a step (every 8th symbol): the partial head word byte by byte,
+// words before the first LIT_STG_W-aligned byte as 8-B stores, the rest through the lane's LDS
+// window, stored as whole aligned LIT_STG_W-B pieces.
+struct LitWords {
+  uint8_t *wp;    // the current output word (8-B aligned)
+  uint8_t *win0;  // first LIT_STG_W-aligned address at or after the lane's first byte
+  uint64_t *stg8;
+  uint64_t acc;
+  uint32_t k, k0, staged;
+  bool first;     // the current word is the head word (bytes before k0 are not the lane's)
+  __device__ __forceinline__ void init(uint8_t *out, uint64_t *stg) {
+    k0 = (uint32_t)((uintptr_t)out & 7);
+    wp = out - k0;
+    win0 = (uint8_t *)(((uintptr_t)out + LIT_STG_W - 1) & ~(uintptr_t)(LIT_STG_W - 1));
+    stg8 = stg;
+    acc = 0;
+    k = k0;
+    staged = 0;
+    first = k0 != 0;
+  }
+  __device__ __forceinline__ void word_done() {
+    if (first) {
+      for (uint32_t i = k0; i < 8; i++) wp[i] = (uint8_t)(acc >> (8 * i));
+      first = false;
+    } else if (wp < win0) {
+      *(uint64_t *)wp = acc;
+    } else {
+      stg8[staged] = acc;
+      if (++staged == LIT_STG_W / 8) {
+#ifndef ZG_LIT_NOSTORE  // lab only: the cost of the window stores (output wrong)
+        uint4 *g = (uint4 *)(wp - (LIT_STG_W - 8));
+        const uint4 *w = (const uint4 *)stg8;
+#pragma unroll
+        for (uint32_t q = 0; q < LIT_STG_W / 16; q++) g[q] = w[q];
+#endif
+        staged = 0;
+      }
+    }
+    wp += 8;
+    acc = 0;
+    k = 0;
+  }
+  __device__ __forceinline__ void finish() {
+    for (uint32_t q = 0; q < staged; q++) *(uint64_t *)(wp - 8 * (staged - q)) = stg8[q];
+    for (uint32_t i = first ? k0 : 0u; i < k; i++) wp[i] = (uint8_t)(acc >> (8 * i));
+  }
+};
+
+template <class Wd>
+__device__ __forceinline__ void hl_write_bf(HufLane &H, int32_t &p, int32_t stop, uint32_t tl, const uint16_t *huf,
+                                            const Wd &word, uint8_t *out, uint32_t cnt, uint4 *stg) {
+  uint32_t n = 0;
+  const uint32_t sh = 64 - tl;
+  LitWords L;
+  L.init(out, (uint64_t *)stg);
+  auto round = [&](auto par) -> bool {
+    constexpr int P = decltype(par)::value;
+    if constexpr (WdBlocks<Wd>::value) word.template pre<P>();
+    bool ok;
+    uint32_t wn = wd_getm<P>(word, (H.lp >> 5) - 1, ok);
+    bool go = (p > stop) & (n < cnt) & (ok | (H.v > 32));
+    while (go) {
+      const bool need = H.v <= 32;
+      const uint32_t wv = need ? wn : 0u;
+      H.C |= (uint64_t)wv << ((uint32_t)(32 - H.v) & 63u);
+      const int32_t add = need ? 32 : 0;
+      H.v += add;
+      H.lp -= add;
+      const uint32_t e = huf[(uint32_t)(H.C >> sh)];
+      const uint32_t nb = e >> 8;
+      H.C <<= nb;
+      H.v -= (int32_t)nb;
+      p -= (int32_t)nb;
+      n++;
+      L.acc |= (uint64_t)(e & 255u) << (8 * L.k);
+      if (++L.k == 8) L.word_done();
+      wn = wd_getm<P>(word, (H.lp >> 5) - 1, ok);
+      go = (p > stop) & (n < cnt) & (ok | (H.v > 32));
+    }
+    return (p > stop) & (n < cnt);
+  };
+  if constexpr (WdBlocks<Wd>::value) {
+    word.norm();
+    for (;;) {
+      if (!round(std::integral_constant<int, 0>{})) break;
+      word.adv();
+      if (!round(std::integral_constant<int, 1>{})) {
+        word.cur = 1;
+        break;
+      }
+      word.adv();
+    }
+  } else {
+    round(std::integral_constant<int, 0>{});
+  }
+  L.finish();
+}
+#endif
+
 // decode symbols while p > stop (at most maxn); WRITE: out[k] = symbol k
 template <bool WRITE, class Wd>
 __device__ __forceinline__ uint32_t hl_run(HufLane &H, int32_t &p, int32_t stop, uint32_t tl, const uint16_t *huf,
@@ -1753,9 +2016,21 @@ __device__ __forceinline__ uint32_t hl_run(HufLane &H, int32_t &p, int32_t stop,
   uint64_t *stg8 = (uint64_t *)stg;
 #endif
 #endif
+  // Rounds: with a block-window reader (GBlk) a lane whose next word lies below its window stops
+  // until every lane of the wave has stopped or finished; the window then moves down one block.
+  // Other readers never stop: one round.
+  auto round = [&](auto par) -> bool {
+  constexpr int P = decltype(par)::value;
+  if constexpr (WdBlocks<Wd>::value) word.template pre<P>();
+  bool blk = false;
   while (p > stop && n < maxn) {
     if (H.v <= 32) {
-      H.C |= (uint64_t)word((H.lp >> 5) - 1) << (32 - H.v);
+      uint32_t w;
+      if (!wd_get_p<P>(word, (H.lp >> 5) - 1, w)) {
+        blk = true;
+        break;
+      }
+      H.C |= (uint64_t)w << (32 - H.v);
       H.v += 32;
       H.lp -= 32;
     }
@@ -1802,6 +2077,22 @@ __device__ __forceinline__ uint32_t hl_run(HufLane &H, int32_t &p, int32_t stop,
 #endif
     n++;
   }
+  return blk;
+  };
+  if constexpr (WdBlocks<Wd>::value) {
+    word.norm();
+    for (;;) {
+      if (!round(std::integral_constant<int, 0>{})) break;
+      word.adv();
+      if (!round(std::integral_constant<int, 1>{})) {
+        word.cur = 1;
+        break;
+      }
+      word.adv();
+    }
+  } else {
+    round(std::integral_constant<int, 0>{});
+  }
 #if ZG_LIT_PACK
 #if ZG_LIT_STAGE
   if (WRITE && n - k > head64) {  // the staged words of the last, incomplete window
@@ -1827,29 +2118,48 @@ struct GWordPF {
   mutable uintptr_t cb;       // address of the cached 32-B block (1: none)
   mutable zv4u c0, c1;        // its words 0-3, 4-7
   mutable zv4u n0, n1;        // the block below it (prefetched)
+  mutable uintptr_t nb;       // address of the block in n0/n1 (1: none)
+  mutable bool pf;            // the block below cb is still to be prefetched
   __device__ __forceinline__ static void ld(uintptr_t b, zv4u &x0, zv4u &x1) {
     const __attribute__((address_space(1))) zv4u *q = (const __attribute__((address_space(1))) zv4u *)b;
     x0 = q[0];
     x1 = q[1];
   }
+  // The prefetch is issued on the first call after a block switch, not at the switch: issued at the
+  // switch, next to the copy of the prefetched block into c0/c1, it made the compiler wait for the
+  // new loads at once (s_waitcnt vmcnt(0) before the block's first use, the prefetch's result moved
+  // between registers), so every switch paid a full memory round trip. Here the only load pending at
+  // a switch is the one issued seven words earlier.
+  // (The word is picked in each branch: picked after the merge, the compiler's wait for a switch's
+  // loads also covered the other branch's prefetch.)
+  __device__ __forceinline__ static uint32_t pick(const zv4u &x0, const zv4u &x1, uintptr_t a) {
+    const uint32_t i = (uint32_t)(a >> 2) & 7u;
+    const zv4u h = i < 4 ? x0 : x1;
+    const uint32_t j = i & 3u;
+    return j == 0 ? h.x : j == 1 ? h.y : j == 2 ? h.z : h.w;
+  }
   __device__ __forceinline__ uint32_t operator()(int32_t k) const {
     if (k < 0 || k >= lim) return 0u;
     const uintptr_t a = (uintptr_t)(Wp + k), b = a & ~(uintptr_t)31;
     if (b != cb) {
-      if (b + 32 == cb) {  // the next lower block: take the prefetched copy
+      if (b == nb) {  // the next lower block: take the prefetched copy
         c0 = n0;
         c1 = n1;
       } else {
         ld(b, c0, c1);
       }
       cb = b;
-      // prefetch the block below, if it still holds words of the section (never before Wp's block)
-      if (b > ((uintptr_t)Wp & ~(uintptr_t)31)) ld(b - 32, n0, n1);
+      nb = 1;
+      pf = b > ((uintptr_t)Wp & ~(uintptr_t)31);  // the block below still holds words of the section
+      return pick(c0, c1, a);
     }
-    const uint32_t i = (uint32_t)(a >> 2) & 7u;
-    const zv4u h = i < 4 ? c0 : c1;
-    const uint32_t j = i & 3u;
-    return j == 0 ? h.x : j == 1 ? h.y : j == 2 ? h.z : h.w;
+    const uint32_t w = pick(c0, c1, a);
+    if (pf) {
+      ld(b - 32, n0, n1);
+      nb = b - 32;
+      pf = false;
+    }
+    return w;
   }
 };
 
@@ -1913,6 +2223,16 @@ __device__ unsigned long long g_litstats[8];
 #else
 #define LS_ADD(k, v) ((void)0)
 #endif
+#ifdef ZG_LIT_PROF
+// lab phase clocks of k_zstd_lits (thread 0 of each workgroup, s_memtime ticks): pass 1, repairs,
+// prefix + checks, pass 2, staging of the section (LDS path), records
+__device__ unsigned long long g_litprof[8];
+#define LP_T(v) const uint64_t v = (threadIdx.x == 0) ? __builtin_amdgcn_s_memtime() : 0
+#define LP_ADD(k, a, b) do { if (threadIdx.x == 0) atomicAdd(&g_litprof[k], (unsigned long long)((b) - (a))); } while (0)
+#else
+#define LP_T(v) ((void)0)
+#define LP_ADD(k, a, b) ((void)0)
+#endif
 
 // uncached word reads for the rare repair walks (the cached readers' state stays out of them)
 template <class Wd>
@@ -1920,6 +2240,7 @@ __device__ __forceinline__ uint32_t word_raw(const Wd &w, int32_t k) { return w(
 __device__ __forceinline__ uint32_t word_raw(const GWordPF &w, int32_t k) { return (k >= 0 && k < w.lim) ? w.Wp[k] : 0u; }
 __device__ __forceinline__ uint32_t word_raw(const GWordPF64 &w, int32_t k) { return (k >= 0 && k < w.lim) ? w.Wp[k] : 0u; }
 __device__ __forceinline__ uint32_t word_raw(const GWord &w, int32_t k) { return (k >= 0 && k < w.lim) ? w.Wp[k] : 0u; }
+__device__ __forceinline__ uint32_t word_raw(const GBlk &w, int32_t k) { return w(k); }
 template <class Wd>
 struct RawWord {
   const Wd &w;
@@ -1956,12 +2277,23 @@ __device__ bool lits_decode(ZLitSmem &S, const Wd &word, uint32_t nstreams, cons
   const int64_t len = (int64_t)T0 - L0;
   const int32_t tj = T0 - (int32_t)(len * j / G), tj1 = T0 - (int32_t)(len * (j + 1) / G);
   const uint32_t maxn = NS + 1;  // a segment never holds more symbols than its stream
+  LP_T(tp0);
   // pass 1: entry / exit / count (its own copy of a cached reader, dead after the pass)
   {
     const Wd w1 = word;
     HufLane H;
     int32_t p = j == 0 ? T0 : min(T0, tj + LIT_WARM);
     hl_init(H, p, w1);
+    wd_start(w1, H);
+#if ZG_LIT_BF
+    if (j) {
+      const uint32_t wn = hl_count_bf(H, p, tj, tl, S.huf, w1, 0xFFFFFFFFu);
+      LS_ADD(5, wn);
+      (void)wn;
+    }
+    S.entry[t] = p;
+    S.cnt[t] = hl_count_bf(H, p, tj1, tl, S.huf, w1, maxn);
+#else
     if (j) {
       const uint32_t wn = hl_run<false>(H, p, tj, tl, S.huf, w1, nullptr, 0xFFFFFFFFu);
       LS_ADD(5, wn);
@@ -1969,9 +2301,12 @@ __device__ bool lits_decode(ZLitSmem &S, const Wd &word, uint32_t nstreams, cons
     }
     S.entry[t] = p;
     S.cnt[t] = hl_run<false>(H, p, tj1, tl, S.huf, w1, nullptr, maxn);
+#endif
     S.exit_[t] = p;
   }
   __syncthreads();
+  LP_T(tp1);
+  LP_ADD(0, tp0, tp1);
   // repair rounds: a lane whose entry is not its predecessor's exit re-decodes from that exit once
   // the predecessor is right (a lane is right when its entry is right)
   for (uint32_t round = 0; round < G; round++) {
@@ -2023,6 +2358,7 @@ __device__ bool lits_decode(ZLitSmem &S, const Wd &word, uint32_t nstreams, cons
       int32_t p = S.exit_[t - 1];
       ne = p;
       hl_init(H, p, word);
+      wd_start(word, H);
       nc = hl_run<false>(H, p, tj1, tl, S.huf, word, nullptr, maxn);
       nx = p;
 #endif
@@ -2041,6 +2377,8 @@ __device__ bool lits_decode(ZLitSmem &S, const Wd &word, uint32_t nstreams, cons
     }
     __syncthreads();
   }
+  LP_T(tp2);
+  LP_ADD(1, tp1, tp2);
   // every lane right now; per-stream symbol count and exact end
   uint32_t c = S.cnt[t];
   LS_ADD(4, c);
@@ -2063,18 +2401,29 @@ __device__ bool lits_decode(ZLitSmem &S, const Wd &word, uint32_t nstreams, cons
   bool bad = total != NS || S.entry[t] != (j == 0 ? T0 : S.exit_[t - 1]);
   if (j == G - 1 && S.exit_[t] != L0) bad = true;
   if (__syncthreads_or(bad)) return false;
+  LP_T(tp3);
+  LP_ADD(2, tp2, tp3);
   // pass 2: decode again, writing
   if (c) {
     const Wd w2 = word;
     HufLane H;
     int32_t p = S.entry[t];
     hl_init(H, p, w2);
-#if ZG_LIT_STAGE
+    wd_start(w2, H);
+#if ZG_LIT_STAGE && ZG_LIT_BF
+    hl_write_bf(H, p, tj1, tl, S.huf, w2, lit + (uint64_t)s * seg + off, c, &S.stg[t * (LIT_STG_PITCH / 16)]);
+#elif ZG_LIT_STAGE
     hl_run<true>(H, p, tj1, tl, S.huf, w2, lit + (uint64_t)s * seg + off, c, &S.stg[t * (LIT_STG_PITCH / 16)]);
 #else
     hl_run<true>(H, p, tj1, tl, S.huf, w2, lit + (uint64_t)s * seg + off, c);
 #endif
   }
+#ifdef ZG_LIT_PROF
+  __syncthreads();
+  LP_T(tp4);
+  LP_ADD(3, tp3, tp4);
+  LP_ADD(5, 0, 1);
+#endif
   return true;
 }
 
@@ -2502,15 +2851,21 @@ __global__ __launch_bounds__(LIT_THREADS) __attribute__((amdgpu_waves_per_eu(ZG_
         }
         __syncthreads();
         const int32_t n32 = (int32_t)nw;
-        auto word = [n32](int32_t k) -> uint32_t { return (k >= 0 && k < n32) ? S.lin[k] : 0u; };
+        auto word = [n32](int32_t k) -> uint32_t {
+          const bool in = (uint32_t)k < (uint32_t)n32;
+          const uint32_t v = S.lin[in ? k : 0];
+          return in ? v : 0u;
+        };
         ok = ZG_LITS_DECODE(S, word, nstreams, top, lob, s_n, tl, lit, seg);
       } else {
         const gu32 *Wp = (const gu32 *)(words + wbase);
         const int64_t lim = nwords_item - wbase;
-#if ZG_LIT_GWIN == 3
+#if ZG_LIT_GWIN == 4
+        const GBlk word{Wp, lim, 1, {}, {}, {}, {}, 0};
+#elif ZG_LIT_GWIN == 3
         GWordPF64 word{Wp, lim, 1, {}, {}};
 #elif ZG_LIT_GWIN == 2
-        const GWordPF word{Wp, lim, 1, zv4u{0, 0, 0, 0}, zv4u{0, 0, 0, 0}, zv4u{0, 0, 0, 0}, zv4u{0, 0, 0, 0}};
+        const GWordPF word{Wp, lim, 1, zv4u{0, 0, 0, 0}, zv4u{0, 0, 0, 0}, zv4u{0, 0, 0, 0}, zv4u{0, 0, 0, 0}, 1, false};
 #elif ZG_LIT_GWIN
         const GWord word{Wp, lim, 1, zv4u{0, 0, 0, 0}};
 #else
