@@ -1169,7 +1169,7 @@ def run_gpu(args, rank, world, dev):
         arr = (L.ChunkDesc * n)(*descs)
         plan = C.c_void_p()
         # plans run concurrently on lanes of their own stay on their lane's stream (ZGPU_ONE_STREAM)
-        one = L.ONE_STREAM if len(getattr(W, "lanes", [[0]])) > 1 and not args.serial_lanes else 0
+        one = L.ONE_STREAM if len(getattr(W, "lanes", [[0]])) > 1 and not args.serial_lanes and not args.fork else 0
         L.check(lib.zgpu_plan_create(chain._h, len(out_shape), arr, n, L.u64s(out_shape),
                                      L.ENC_DEVICE | L.OUT_DEVICE | one, C.byref(plan)))
         part_plan[pi] = len(plans)
@@ -1329,7 +1329,7 @@ def secondary_legs(args, rank, world, dev, r_primary):
         a = copy.copy(args)
         a.workload, a.steps, a.warmup = name, max(2, min(args.steps, 5)), 1
         a.host_leg, a.cpu_seconds, a.c5_scale = False, 5.0, args.secondary_c5_scale
-        a.lane_priorities, a.serial_lanes, a.lane_times = "", False, False
+        a.lane_priorities, a.serial_lanes, a.lane_times, a.fork = "", False, False, False
         gc.collect()
         torch.cuda.empty_cache()
         print(f"[bench] secondary leg {name} ...", file=sys.stderr, flush=True)
@@ -1523,6 +1523,7 @@ def main():
     ap.add_argument("--no-pmc", action="store_true", help="skip the rocprofv3 PMC traffic passes")
     ap.add_argument("--lane-priorities", default="",
                     help="comma-separated HIP stream priorities of the stream lanes (-1 high, 0 normal)")
+    ap.add_argument("--fork", action="store_true", help=argparse.SUPPRESS)  # A/B: concurrent plans keep their side streams
     ap.add_argument("--serial-lanes", action="store_true",
                     help="run every plan on one stream (profiling: per-kernel durations without overlap)")
     ap.add_argument("--no-host-leg", dest="host_leg", action="store_false",

@@ -148,6 +148,12 @@ int main(int argc, char **argv) {
   int ncu = 256;
   CK(hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, 0));
   const int reps = getenv("LAB_REPS") ? atoi(getenv("LAB_REPS")) : 3;
+  uint8_t *lit_rec = nullptr;  // literal record slots (ZG_LIT_REC; LAB_NOREC=1: none)
+  {
+    uint32_t wgs = 0;
+    const uint64_t rb = zgpu::zstd_lit_rec_bytes(wgs);
+    if (rb && !getenv("LAB_NOREC") && wgs >= (uint32_t)ncu * ZG_LIT_GRID_PER_CU) CK(hipMalloc(&lit_rec, rb));
+  }
   for (int rep = 0; rep < reps; rep++) {
     CK(hipMemcpy(d_items, items.data(), n * sizeof(ZgItem), hipMemcpyHostToDevice));
     CK(hipMemset(d_status, 0, n * 4));
@@ -169,7 +175,7 @@ int main(int argc, char **argv) {
                        (uint32_t)n, Z.lit, Z.lit_stride);
     CK(hipEventRecord(ev[3]));
     hipLaunchKernelGGL(zgpu::k_zstd_lits, dim3(lgrid), dim3(zgpu::LIT_THREADS), 0, 0, d_items, d_status, blks, Z.blk_cap,
-                       Z.nblk, Z.mode, (uint32_t)n, Z.lit, Z.lit_stride);
+                       Z.nblk, Z.mode, (uint32_t)n, Z.lit, Z.lit_stride, lit_rec);
     CK(hipEventRecord(ev[4]));
     hipLaunchKernelGGL(zgpu::k_zstd_plan, dim3(n), dim3(64), 0, 0, d_items, d_status, blks, Z.blk_cap, Z.nblk, Z.mode,
                        chunk, zgpu::XSEG);
@@ -217,7 +223,7 @@ int main(int argc, char **argv) {
     unsigned long long z[8];
     CK(hipMemcpyFromSymbol(z, HIP_SYMBOL(zgpu::g_litstats), sizeof(z)));
     printf("lit stats (all reps): huffman blocks %llu, blocks needing repair %llu, repair rounds %llu, lanes re-decoded %llu, "
-           "symbols %llu, warm-up symbols %llu, lanes %llu\n", z[0], z[1], z[2], z[3], z[4], z[5], z[6]);
+           "symbols %llu, warm-up symbols %llu, lanes %llu, lanes decoding twice %llu\n", z[0], z[1], z[2], z[3], z[4], z[5], z[6], z[7]);
   }
 #endif
 #ifdef ZG_PROFILE

@@ -109,7 +109,12 @@ struct ZstdScratch {
   // runs on `side` beside the Huffman literal kernels and joins before k_zstd_plan
   hipStream_t side = nullptr;
   hipEvent_t ev_fork = nullptr, ev_join = nullptr;
+  // literal record slots (k_zstd_lits pass 1 keeps its symbols; nullable: every lane decodes twice):
+  // zstd_lit_rec_bytes() bytes for lit_rec_wgs workgroups
+  uint8_t *lit_rec = nullptr;
+  uint32_t lit_rec_wgs = 0;
 };
+uint64_t zstd_lit_rec_bytes(uint32_t &wgs);
 void zstd_scratch_layout(uint64_t slot_bytes, uint32_t &blk_cap, uint64_t &blk_bytes, uint64_t &lit_stride,
                          uint64_t &seq_cap);
 hipError_t launch_zstd(ZgItem *items, uint32_t *status, uint32_t n_items, uint8_t *dst, uint64_t slot_bytes,

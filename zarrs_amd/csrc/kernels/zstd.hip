@@ -1656,7 +1656,7 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(ZG_BLK_WPE, 
 // offsets. The compressed literal section is staged in LDS first (sections over LIT_LDS read global).
 // -------------------------------------------------------------------------------------------------
 #ifndef ZG_LIT_LDS
-#define ZG_LIT_LDS (16 * 1024)
+#define ZG_LIT_LDS (8 * 1024)
 #endif
 constexpr uint32_t LIT_LDS = ZG_LIT_LDS;
 #ifndef ZG_LIT_WARM
@@ -1690,7 +1690,9 @@ constexpr int LIT_STAGE_R = ZG_LIT_WPE >= 4 ? 4 : 8;  // 16-B staging loads in f
                            // 2,994 -> 643 MB per launch on 64 C5 chunks, 1.2x the literal bytes)
 #endif
 #ifndef ZG_LIT_STG_PITCH
-#define ZG_LIT_STG_PITCH ZG_LIT_STAGE_W  // bytes per lane window (16-B aligned; 37 KB LDS: 4 workgroups/CU)
+#define ZG_LIT_STG_PITCH (2 * ZG_LIT_STAGE_W)  // bytes per lane: two windows (pass 1's record stores are
+                                               // deferred a round, below; with the 8 KiB section stage
+                                               // the workgroup keeps 37 KB of LDS: 4 per CU)
 #endif
 #ifndef ZG_LIT_ILP
 #define ZG_LIT_ILP 1  // Huffman chains per lane (2: a lane decodes two segments, interleaved)
@@ -1941,6 +1943,19 @@ struct LitWords {
     for (uint32_t q = 0; q < staged; q++) *(uint64_t *)(wp - 8 * (staged - q)) = stg8[q];
     for (uint32_t i = first ? k0 : 0u; i < k; i++) wp[i] = (uint8_t)(acc >> (8 * i));
   }
+  __device__ __forceinline__ void push_byte(uint32_t b) {
+    acc |= (uint64_t)(b & 255u) << (8 * k);
+    if (++k == 8) word_done();
+  }
+  // 8 bytes at once (the next 8 of the stream, byte 0 in the low bits)
+  __device__ __forceinline__ void push_word(uint64_t w) {
+    const uint32_t kk = k;
+    acc |= kk ? (w << (8 * kk)) : w;
+    const uint64_t hi = kk ? (w >> (64 - 8 * kk)) : 0ull;
+    word_done();
+    acc = hi;
+    k = kk;
+  }
 };
 
 template <class Wd>
@@ -1991,6 +2006,106 @@ __device__ __forceinline__ void hl_write_bf(HufLane &H, int32_t &p, int32_t stop
     round(std::integral_constant<int, 0>{});
   }
   L.finish();
+}
+#endif
+
+#ifndef ZG_LIT_REC
+#define ZG_LIT_REC 1  // pass 1 keeps its symbols in a per-lane record slot; pass 2 only copies (below)
+#endif
+// Record slot per lane: REC_OWN bytes of the lane's own chain (from its entry), then REC_RB bytes of
+// a repair's true-chain prefix. A lane whose symbols do not fit decodes again (pass 2) instead.
+constexpr uint32_t REC_OWN = 1024, REC_RB = 64, REC_SLOT = REC_OWN + REC_RB;
+static_assert(REC_OWN % 8 == 0 && REC_RB % 8 == 0, "record slot words");
+
+#if ZG_LIT_STAGE && ZG_LIT_BF
+// Pass 1 with records: hl_count_bf's loop, each symbol also packed into 8-B words of the lane's slot
+// (symbol i at slot[i]; only the first REC_OWN are kept).
+template <class Wd>
+__device__ __forceinline__ uint32_t hl_count_rec(HufLane &H, int32_t &p, int32_t stop, uint32_t tl,
+                                                 const uint16_t *huf, const Wd &word, uint32_t maxn, uint8_t *slot,
+                                                 uint64_t *stg8) {
+  // 8-B words through two LIT_STG_W-byte LDS windows of the lane (stg8), a completed window stored
+  // as whole 16-B pieces at the start of the next round: right after the round's wait for its
+  // prefetched block, so that no wait covers a store issued less than a round before it (one store
+  // per 8 symbols was 4x the store instructions, and each round start waited for the last ones).
+  constexpr uint32_t WW = LIT_STG_W / 8;  // words per window
+  uint32_t n = 0, pend = 0;               // completed windows not stored yet (0..2)
+  uint64_t acc = 0;
+  const uint32_t sh = 64 - tl;
+  auto store_win = [&](uint32_t wi) {     // window wi (slot bytes [W*wi, W*wi + W)) from its LDS half
+    uint4 *g = (uint4 *)(slot + (uint64_t)LIT_STG_W * wi);
+    const uint4 *w = (const uint4 *)(stg8 + (wi & 1u) * WW);
+#pragma unroll
+    for (uint32_t q = 0; q < LIT_STG_W / 16; q++) g[q] = w[q];
+  };
+  auto round = [&](auto par) -> bool {
+    constexpr int P = decltype(par)::value;
+    if constexpr (WdBlocks<Wd>::value) word.template pre<P>();
+    if (pend) {  // the windows completed in the last round
+      const uint32_t wn_ = n / LIT_STG_W;  // windows completed so far
+      if ((wn_ - pend + 1) * LIT_STG_W <= REC_OWN) store_win(wn_ - pend);
+      if (pend == 2 && wn_ * LIT_STG_W <= REC_OWN) store_win(wn_ - 1);
+      pend = 0;
+    }
+    bool ok;
+    uint32_t wn = wd_getm<P>(word, (H.lp >> 5) - 1, ok);
+    bool go = (p > stop) & (n < maxn) & (ok | (H.v > 32));
+    while (go) {
+      const bool need = H.v <= 32;
+      const uint32_t wv = need ? wn : 0u;
+      H.C |= (uint64_t)wv << ((uint32_t)(32 - H.v) & 63u);
+      const int32_t add = need ? 32 : 0;
+      H.v += add;
+      H.lp -= add;
+      const uint32_t e = huf[(uint32_t)(H.C >> sh)];
+      const uint32_t nb = e >> 8;
+      H.C <<= nb;
+      H.v -= (int32_t)nb;
+      p -= (int32_t)nb;
+      const uint32_t k = n & 7u;
+      acc |= (uint64_t)(e & 255u) << (8 * k);
+      if (k == 7u) {
+        const uint32_t wq = n >> 3;  // word index
+        stg8[wq & (2 * WW - 1)] = acc;
+        if ((wq & (WW - 1)) == WW - 1) {  // window wq / WW complete
+          if (pend == 1) {                // the other half still holds one: store it now (rare)
+            const uint32_t wi = wq / WW - 1;
+            if ((wi + 1) * LIT_STG_W <= REC_OWN) store_win(wi);
+          } else {
+            pend = 1;
+          }
+        }
+        acc = 0;
+      }
+      n++;
+      wn = wd_getm<P>(word, (H.lp >> 5) - 1, ok);
+      go = (p > stop) & (n < maxn) & (ok | (H.v > 32));
+    }
+    return (p > stop) & (n < maxn);
+  };
+  if constexpr (WdBlocks<Wd>::value) {
+    word.norm();
+    for (;;) {
+      if (!round(std::integral_constant<int, 0>{})) break;
+      word.adv();
+      if (!round(std::integral_constant<int, 1>{})) {
+        word.cur = 1;
+        break;
+      }
+      word.adv();
+    }
+  } else {
+    round(std::integral_constant<int, 0>{});
+  }
+  // the completed windows not stored yet, the last incomplete window's whole words, the partial word
+  const uint32_t wn_ = n / LIT_STG_W;
+  if (pend && wn_ * LIT_STG_W <= REC_OWN) store_win(wn_ - 1);
+  const uint32_t wdone = n >> 3, w0 = wdone & ~(uint32_t)(WW - 1);
+  if (n <= REC_OWN) {
+    for (uint32_t q = w0; q < wdone; q++) *(uint64_t *)(slot + 8 * q) = stg8[q & (2 * WW - 1)];
+    if (n & 7u) *(uint64_t *)(slot + (n & ~7u)) = acc;
+  }
+  return n;
 }
 #endif
 
@@ -2249,16 +2364,18 @@ struct RawWord {
 
 // one symbol of a lane's chain (position p moves down by the code length)
 template <class Wd>
-__device__ __forceinline__ void hl_step(HufLane &H, int32_t &p, uint32_t tl, const uint16_t *huf, const Wd &word) {
+__device__ __forceinline__ uint32_t hl_step(HufLane &H, int32_t &p, uint32_t tl, const uint16_t *huf, const Wd &word) {
   if (H.v <= 32) {
     H.C |= (uint64_t)word((H.lp >> 5) - 1) << (32 - H.v);
     H.v += 32;
     H.lp -= 32;
   }
-  const uint32_t nb = huf[(uint32_t)(H.C >> (64 - tl))] >> 8;
+  const uint32_t e = huf[(uint32_t)(H.C >> (64 - tl))];
+  const uint32_t nb = e >> 8;
   H.C <<= nb;
   H.v -= (int32_t)nb;
   p -= (int32_t)nb;
+  return e & 255u;
 }
 
 #ifndef ZG_LIT_SYNC
@@ -2267,7 +2384,7 @@ __device__ __forceinline__ void hl_step(HufLane &H, int32_t &p, uint32_t tl, con
 
 template <class Wd>
 __device__ bool lits_decode(ZLitSmem &S, const Wd &word, uint32_t nstreams, const int32_t *top, const int32_t *lob,
-                            const uint32_t *nsym, uint32_t tl, uint8_t *lit, uint32_t seg) {
+                            const uint32_t *nsym, uint32_t tl, uint8_t *lit, uint32_t seg, uint8_t *slot = nullptr) {
   const uint32_t t = threadIdx.x;
   const uint32_t G = LIT_THREADS / nstreams;
   const uint32_t s = t / G, j = t % G;
@@ -2292,7 +2409,12 @@ __device__ bool lits_decode(ZLitSmem &S, const Wd &word, uint32_t nstreams, cons
       (void)wn;
     }
     S.entry[t] = p;
+#if ZG_LIT_REC && ZG_LIT_STAGE
+    S.cnt[t] = slot ? hl_count_rec(H, p, tj1, tl, S.huf, w1, maxn, slot, (uint64_t *)&S.stg[t * (LIT_STG_PITCH / 16)])
+                    : hl_count_bf(H, p, tj1, tl, S.huf, w1, maxn);
+#else
     S.cnt[t] = hl_count_bf(H, p, tj1, tl, S.huf, w1, maxn);
+#endif
 #else
     if (j) {
       const uint32_t wn = hl_run<false>(H, p, tj, tl, S.huf, w1, nullptr, 0xFFFFFFFFu);
@@ -2307,6 +2429,12 @@ __device__ bool lits_decode(ZLitSmem &S, const Wd &word, uint32_t nstreams, cons
   __syncthreads();
   LP_T(tp1);
   LP_ADD(0, tp0, tp1);
+  // records: the lane's final symbols are rec_nt repair-prefix symbols (slot tail) followed by its own
+  // symbols [rec_nw, cnt_own) (none when the true chain left the segment without meeting the lane's)
+  const uint32_t cnt_own = S.cnt[t];
+  uint32_t rec_nw = 0, rec_nt = 0;
+  bool rec_full = false, rec_again = false, fixed_once = false;  // rec_again: fixed twice (a chain further up changed after
+                                             // the first fix): the records no longer describe it
   // repair rounds: a lane whose entry is not its predecessor's exit re-decodes from that exit once
   // the predecessor is right (a lane is right when its entry is right)
   for (uint32_t round = 0; round < G; round++) {
@@ -2334,6 +2462,7 @@ __device__ bool lits_decode(ZLitSmem &S, const Wd &word, uint32_t nstreams, cons
       hl_init(Ht, pt, rw);
       hl_init(Hw, pw, rw);
       uint32_t nt = 0, nw = 0;
+      bool full_now = false;
       for (;;) {
         if (pt == pw) {
           nc = S.cnt[t] - nw + nt;
@@ -2343,16 +2472,23 @@ __device__ bool lits_decode(ZLitSmem &S, const Wd &word, uint32_t nstreams, cons
         if (pt <= tj1 || nt > maxn || nw > maxn) {
           nc = nt;
           nx = pt;
+          full_now = true;
           break;
         }
         if (pt > pw) {
-          hl_step(Ht, pt, tl, S.huf, rw);
+          const uint32_t e = hl_step(Ht, pt, tl, S.huf, rw);
+          if (slot && nt < REC_RB) slot[REC_OWN + nt] = (uint8_t)e;
           nt++;
         } else {
           hl_step(Hw, pw, tl, S.huf, rw);
           nw++;
         }
       }
+      rec_again = rec_again || fixed_once;
+      fixed_once = true;
+      rec_full = full_now;
+      rec_nw = nw;
+      rec_nt = nt;
 #else
       HufLane H;
       int32_t p = S.exit_[t - 1];
@@ -2360,6 +2496,7 @@ __device__ bool lits_decode(ZLitSmem &S, const Wd &word, uint32_t nstreams, cons
       hl_init(H, p, word);
       wd_start(word, H);
       nc = hl_run<false>(H, p, tj1, tl, S.huf, word, nullptr, maxn);
+      rec_again = true;  // nothing recorded on this path: decode again
       nx = p;
 #endif
     }
@@ -2403,8 +2540,82 @@ __device__ bool lits_decode(ZLitSmem &S, const Wd &word, uint32_t nstreams, cons
   if (__syncthreads_or(bad)) return false;
   LP_T(tp3);
   LP_ADD(2, tp2, tp3);
+  bool redo = c != 0;  // pass 2 (decode again, writing) for this lane
+#if ZG_LIT_REC && ZG_LIT_STAGE && ZG_LIT_BF
+  // The lane's slot stores (pass 1, repairs) before its reads, and the CU's vector L1 invalidated:
+  // stores do not update lines the L1 already holds, and the slot's lines were read (and cached) by
+  // this lane's copy of the previous record - without the invalidate it read that record's bytes.
+  if (slot) {
+    __builtin_amdgcn_s_waitcnt(0);                      // the stores acknowledged (in L2)
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");  // buffer_inv: the L1 refetches
+  }
+  if (slot && c) {
+    // the recorded symbols, copied: fall back to pass 2 when a part did not fit its slot region
+    // c = the first npre true-chain symbols of a repair, then own symbols from rec_nw on. (Chains can
+    // meet below the segment's end, after the own chain's last symbol: then the segment is the true
+    // chain's first c symbols and nothing of the own chain.)
+    const uint32_t npre = min(rec_nt, c), n_own = c - npre;
+    const bool fits = !rec_again && npre <= REC_RB &&
+                      (n_own == 0 || (!rec_full && rec_nw + n_own == cnt_own && cnt_own <= REC_OWN));
+    if (fits) {
+      redo = false;
+      LitWords L;
+      L.init(lit + (uint64_t)s * seg + off, (uint64_t *)&S.stg[t * (LIT_STG_PITCH / 16)]);
+      for (uint32_t i = 0; i < npre; i++) L.push_byte(slot[REC_OWN + i]);
+      if (n_own) {
+        // own symbols [rec_nw, cnt_own): aligned 8-B slot words, funnel-shifted
+        const uint32_t a = rec_nw & 7u;
+        const uint64_t *sw = (const uint64_t *)(slot + (rec_nw & ~7u));
+        uint64_t cur = sw[0];
+        uint32_t i = 0;
+        // 64 bytes per group: the group's eight loads in flight together (one round trip, not eight)
+        for (; i + 64 <= n_own; i += 64) {
+          uint64_t w[8];
+#pragma unroll
+          for (int q = 0; q < 8; q++) w[q] = sw[(i >> 3) + 1 + q];
+#pragma unroll
+          for (int q = 0; q < 8; q++) {
+            L.push_word(a ? (cur >> (8 * a)) | (w[q] << (64 - 8 * a)) : cur);
+            cur = w[q];
+          }
+        }
+        for (; i + 8 <= n_own; i += 8) {
+          const uint64_t nxt = sw[(i >> 3) + 1];
+          L.push_word(a ? (cur >> (8 * a)) | (nxt << (64 - 8 * a)) : cur);
+          cur = nxt;
+        }
+        if (i < n_own) {
+          const uint64_t nxt = (a + (n_own - i) > 8) ? sw[(i >> 3) + 1] : 0ull;
+          const uint64_t w = a ? (cur >> (8 * a)) | (nxt << (64 - 8 * a)) : cur;
+          for (uint32_t q = 0; q < n_own - i; q++) L.push_byte((uint32_t)(w >> (8 * q)));
+        }
+      }
+      L.finish();
+    }
+  }
+  LS_ADD(7, redo ? 1 : 0);
+#ifdef ZG_LIT_REC_DEBUG  // lab: decode each copied lane again and report the first differing byte
+  if (slot && c && !redo) {
+    __builtin_amdgcn_s_waitcnt(0);
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+    const RawWord<Wd> rw{word};
+    HufLane Hd;
+    int32_t pd = S.entry[t];
+    hl_init(Hd, pd, rw);
+    const uint8_t *o = lit + (uint64_t)s * seg + off;
+    for (uint32_t i = 0; i < c; i++) {
+      const uint32_t e = hl_step(Hd, pd, tl, S.huf, rw);
+      if ((uint8_t)e != o[i]) {
+        printf("litrec: t %u s %u j %u c %u i %u exp %u got %u | cnt_own %u nw %u nt %u full %d entry %d exit %d tj %d tj1 %d\n",
+               t, s, j, c, i, e, (uint32_t)o[i], cnt_own, rec_nw, rec_nt, (int)rec_full, S.entry[t], S.exit_[t], tj, tj1);
+        break;
+      }
+    }
+  }
+#endif
+#endif
   // pass 2: decode again, writing
-  if (c) {
+  if (redo) {
     const Wd w2 = word;
     HufLane H;
     int32_t p = S.entry[t];
@@ -2728,16 +2939,20 @@ __global__ __launch_bounds__(64) void k_zstd_huf(const ZgItem *items, const uint
 #endif
 
 #if ZG_LIT_ILP == 2
-#define ZG_LITS_DECODE lits_decode2
+#define ZG_LITS_DECODE(...) lits_decode2(__VA_ARGS__)
 #else
-#define ZG_LITS_DECODE lits_decode
+#define ZG_LITS_DECODE(...) lits_decode(__VA_ARGS__, slot)
 #endif
 __global__ __launch_bounds__(LIT_THREADS) __attribute__((amdgpu_waves_per_eu(ZG_LIT_WPE, 8))) void k_zstd_lits(const ZgItem *items, uint32_t *status, const ZBlk *blks,
                                                            uint32_t blk_cap, const uint32_t *nblk,
                                                            const uint32_t *zmode, uint32_t n_items,
-                                                           uint8_t *lit_scratch, uint64_t lit_stride) {
+                                                           uint8_t *lit_scratch, uint64_t lit_stride,
+                                                           uint8_t *lit_rec) {
   __shared__ ZLitSmem S;
   const uint32_t t = threadIdx.x;
+  // this lane's record slot (ZG_LIT_REC; nullptr: every lane decodes twice)
+  uint8_t *const slot = lit_rec ? lit_rec + ((uint64_t)blockIdx.x * LIT_THREADS + t) * REC_SLOT : nullptr;
+  (void)slot;
   const uint64_t total = (uint64_t)n_items * blk_cap;
   for (uint64_t g = blockIdx.x; g < total; g += gridDim.x) {
     const uint32_t item = (uint32_t)(g % n_items), bi = (uint32_t)(g / n_items);  // block-major order
@@ -3834,6 +4049,18 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(ZG_XWPE, 8))
   }
 }
 
+uint64_t zstd_lit_rec_bytes(uint32_t &wgs) {
+  static const uint64_t cap = [] {
+    const char *e = std::getenv("ZGPU_ZSTD_LGRID");
+    return e ? std::max<uint64_t>(1, std::strtoull(e, nullptr, 10)) : (uint64_t)device_cu_count() * ZG_LIT_GRID_PER_CU;
+  }();
+  static const bool on = [] {
+    const char *e = std::getenv("ZGPU_ZSTD_LIT_REC");
+    return ZG_LIT_REC && (!e || std::atoi(e) != 0);
+  }();
+  wgs = on ? (uint32_t)cap : 0u;
+  return on ? cap * LIT_THREADS * REC_SLOT : 0ull;
+}
 void zstd_scratch_layout(uint64_t slot_bytes, uint32_t &blk_cap, uint64_t &blk_bytes, uint64_t &lit_stride,
                          uint64_t &seq_cap) {
   blk_cap = (uint32_t)std::min<uint64_t>(slot_bytes / 32768 + 64, 1u << 20);
@@ -3887,8 +4114,10 @@ hipError_t launch_zstd(ZgItem *items, uint32_t *status, uint32_t n_items, uint8_
   hipLaunchKernelGGL(k_zstd_huf, dim3(grid), dim3(64), 0, s, items, status, blks, Z.blk_cap, Z.nblk, Z.mode, n_items,
                      Z.lit, Z.lit_stride);
 #endif
+  // record slots: one per lane of the persistent grid (allocated for l_cap workgroups)
+  uint8_t *lit_rec = (ZG_LIT_REC && Z.lit_rec && lgrid <= Z.lit_rec_wgs) ? Z.lit_rec : nullptr;
   hipLaunchKernelGGL(k_zstd_lits, dim3(lgrid), dim3(LIT_THREADS), 0, s, items, status, blks, Z.blk_cap, Z.nblk,
-                     Z.mode, n_items, Z.lit, Z.lit_stride);
+                     Z.mode, n_items, Z.lit, Z.lit_stride, lit_rec);
   if (fork) {
     hipError_t e = hipStreamWaitEvent(s, Z.ev_join, 0);
     if (e != hipSuccess) return e;

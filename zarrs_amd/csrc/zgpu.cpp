@@ -289,7 +289,7 @@ struct zgpu_plan {
     size_t n = 0;
   };
   Grow bl_info, bl_bases, bl_subs, bl_sub_status, bl_sub_kind, bl_blocks, bl_tmp, bl_zblks, bl_znblk, bl_zmode,
-      bl_zlit, bl_zseq, bl_zaux, bl_zser, bl_lzl, bl_zseg;
+      bl_zlit, bl_zseq, bl_zaux, bl_zser, bl_lzl, bl_zseg, bl_zrec;
   uint8_t *bl_h = nullptr;  // pinned: BlInfo read-back (first execution)
   size_t bl_h_n = 0;
   void *grow(Grow &g, size_t bytes) {
@@ -335,7 +335,7 @@ struct zgpu_plan {
     void *bufs[] = {d_items, d_items_init, d_geom, d_shards, d_index, d_shard_status, d_mids, d_mids_init,
                     d_mid_status, d_shard_status2, d_mid_shards, d_index2, d_bl_need,
                     d_pool[0], d_pool[1], zs.blks, zs.nblk, zs.mode, zs.lit, zs.seq, d_ctl,
-                    d_enc_stage, d_zser, d_order, d_gz_seg};
+                    d_enc_stage, d_zser, d_order, d_gz_seg, zs.lit_rec};
     for (void *b : bufs) ctx->dev_free(b);
     if (zside) {
       (void)hipStreamSynchronize(zside);
@@ -344,7 +344,7 @@ struct zgpu_plan {
     for (hipEvent_t e : zev)
       if (e) (void)hipEventDestroy(e);
     for (Grow *g : {&bl_info, &bl_bases, &bl_subs, &bl_sub_status, &bl_sub_kind, &bl_blocks, &bl_tmp, &bl_zblks,
-                    &bl_znblk, &bl_zmode, &bl_zlit, &bl_zseq, &bl_zaux, &bl_zser, &bl_lzl, &bl_zseg})
+                    &bl_znblk, &bl_zmode, &bl_zlit, &bl_zseq, &bl_zaux, &bl_zser, &bl_lzl, &bl_zseg, &bl_zrec})
       ctx->dev_free(g->p);
     ctx->host_free(bl_h);
     ctx->host_free(h_ctl);
@@ -800,6 +800,7 @@ static void plan_upload(zgpu_plan &P, hipStream_t us) {
         P.zs.seq = (uint32_t *)C.dev_alloc(ni * P.zs.seq_cap * 12);
         P.d_zser = (uint32_t *)C.dev_alloc(ni * 4);
         P.zs.ser_list = P.d_zser;
+        if (const uint64_t rb = zstd_lit_rec_bytes(P.zs.lit_rec_wgs)) P.zs.lit_rec = (uint8_t *)C.dev_alloc(rb);
       }
     }
   }
@@ -919,6 +920,7 @@ static void blosc_stage(zgpu_plan &P, const Stage &st, uint8_t *out, hipStream_t
     D.zs.counters = P.zs.counters;
     D.zs.force_serial = P.zs.force_serial;
     D.zs.ser_list = (uint32_t *)P.grow(P.bl_zser, D.n_sub * 4);
+    if (const uint64_t rb = zstd_lit_rec_bytes(D.zs.lit_rec_wgs)) D.zs.lit_rec = (uint8_t *)P.grow(P.bl_zrec, rb);
     D.zs.ser_count = P.zs.ser_count;
     D.zs.launch_serial = P.zs.launch_serial;
     P.zstd_fork(D.zs, s);
