@@ -1139,6 +1139,9 @@ struct SeqX {
 #ifndef ZG_SEQ_PACK
 #define ZG_SEQ_PACK 1  // 4-byte sequence tables (below); 0: 8-byte SeqX
 #endif
+#ifndef ZG_SEQ_REP_SEL
+#define ZG_SEQ_REP_SEL 0  // 1: repeat-offset update as selects (lab A/B r04ae: blocks 3.60 -> 3.94-4.17 ms, off)
+#endif
 #ifndef ZG_SEQ_ONE_FSE
 #define ZG_SEQ_ONE_FSE 1  // one FSE scratch table, folded into its SeqX table at once (0: three tables)
 #endif
@@ -1558,6 +1561,19 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(ZG_BLK_WPE, 
             }
 #endif
             // repeat offsets, symbolically in the block's incoming rep state (RFC 8878 3.1.1.5)
+#if ZG_SEQ_REP_SEL
+            // as selects (the branchy form cost ~25 scalar instructions and four branches a sequence
+            // on a decoder bound by the CU's scalar unit): k = 0 new offset, else 1 + repeat index
+            const bool lit0 = ll == 0;
+            const uint32_t k = ofv > 3 ? 0u : ofv + (lit0 ? 1u : 0u);  // 1..4: repeat index 0..3
+            if (k == 0 && ((ofv - 3) & ZSYM)) { bad = true; break; }   // beyond any window we decode
+            const uint32_t off = k == 0 ? ofv - 3 : k == 1 ? r0 : k == 2 ? r1 : k == 3 ? r2 : sym_dec(r0);
+            const uint32_t n2 = (k == 0 || k >= 3) ? r1 : r2;  // rotations: every case but index 0/1 keeps r2
+            const uint32_t n1 = k == 1 ? r1 : r0;
+            r2 = n2;
+            r1 = n1;
+            r0 = off;
+#else
             uint32_t off;
             if (ofv > 3) {
               off = ofv - 3;
@@ -1575,6 +1591,7 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(ZG_BLK_WPE, 
                 off = sym_dec(r0); r2 = r1; r1 = r0; r0 = off;
               }
             }
+#endif
             if (lane == (int)cnt) { r_ll = ll; r_ml = ml; r_of = off; }
             sum_ll += ll;
             sum_ml += ml;
