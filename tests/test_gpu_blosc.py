@@ -529,3 +529,75 @@ def test_blosc_partial_decodes_only_covering_blocks(ctx, torch_cuda, cname, shuf
             hi = 4 * sum((s + n - 1) * st for s, n, st in zip(start, sub, (1024, 32, 1))) + 4
             blocks = nblk if sub == cs else (hi - 1) // bs - lo // bs + 1
             assert L.last_counters()["blosc_blocks"] == blocks, (start, sub, bs, L.last_counters())
+
+
+def _zstd_block_kinds(frame):
+    """(type, nseq) per block of one zstd frame (RFC 8878 3.1.1.2; nseq None for raw / rle)."""
+    fhd = frame[4]
+    single = (fhd >> 5) & 1
+    p = 5 + (0 if single else 1) + [0, 1, 2, 4][fhd & 3] + [1 if single else 0, 2, 4, 8][fhd >> 6]
+    out = []
+    while True:
+        h = frame[p] | frame[p + 1] << 8 | frame[p + 2] << 16
+        p += 3
+        t, sz = (h >> 1) & 3, h >> 3
+        nseq = None
+        if t == 2:
+            b = frame[p]
+            lt, sf = b & 3, (b >> 2) & 3
+            if lt < 2:
+                lh = [1, 2, 1, 3][sf]
+                regen = (b >> 3) if sf in (0, 2) else ((b >> 4) | (frame[p + 1] << 4) if sf == 1 else
+                                                       (b >> 4) | (frame[p + 1] << 4) | (frame[p + 2] << 12))
+                csz = regen if lt == 0 else 1
+            else:
+                lh = [3, 3, 4, 5][sf]
+                v = int.from_bytes(frame[p:p + lh], "little")
+                csz = v >> [14, 14, 18, 22][sf]
+            c0 = frame[p + lh + csz]
+            nseq = c0 if c0 < 128 else (((c0 - 128) << 8) + frame[p + lh + csz + 1] if c0 < 255 else 1 << 15)
+        out.append((t, nseq))
+        p += sz if t != 1 else 1
+        if h & 1:
+            return out
+
+
+def test_blosc_zstd_block_aliases_vs_oracle(ctx, torch_cuda):
+    """k_blosc_finish reads zstd blocks that need no execution where they lie (ZstdScratch::alias):
+    raw (noise) and rle (constant) byte planes, literal-only blocks, and raw blocks that a later
+    block's matches copy from (those must stay in the slot). Bytes vs the c-blosc oracle; the test
+    asserts the frames really hold each block kind."""
+    from zarrs_amd import CodecChain, make_desc
+    rng = np.random.default_rng(77)
+    n = 1 << 17  # u16 elements: one 256 KiB blosc block per chunk, two 128 KiB zstd blocks
+    cases = []
+    noise = rng.integers(0, 256, n, dtype=np.uint16)
+    cases.append(noise)  # low plane raw, high plane rle (0)
+    cases.append(noise | np.uint16(0x0700))  # rle 7
+    cases.append((noise % 180).astype(np.uint16))  # low plane literal-only (Huffman), high plane rle
+    cases.append(noise | (np.arange(n, dtype=np.uint16) // 512 % 5 << 8).astype(np.uint16))  # raw, then matches
+    half = rng.integers(0, 65536, n // 2, dtype=np.uint16)
+    cases.append(np.concatenate([half, half]))  # shuffled planes with a repeat (matches)
+    kinds = set()
+    for shuffle in ("shuffle", "noshuffle"):
+        codecs = [{"name": "bytes", "configuration": {"endian": "little"}}, _blosc("zstd", shuffle, 2, 0, 5)]
+        co = O.OracleChain.from_metadata(codecs, "uint16", 0, 1)
+        ch = CodecChain.from_metadata(codecs, "uint16", 0, ctx)
+        descs, keep = [], []
+        for k, a in enumerate(cases):
+            enc = bytes(co.encode(a))
+            nb = int.from_bytes(enc[8:12], "little")
+            for bi in range((2 * n + nb - 1) // nb):
+                s0 = int.from_bytes(enc[16 + 4 * bi:20 + 4 * bi], "little")
+                cs = int.from_bytes(enc[s0:s0 + 4], "little", signed=True)
+                if enc[2] & 0x10 and cs != nb:  # not split: one zstd frame per block
+                    kinds.update((shuffle,) + kb for kb in _zstd_block_kinds(enc[s0 + 4:s0 + 4 + cs]))
+            d = torch_cuda.frombuffer(bytearray(enc), dtype=torch_cuda.uint8).cuda()
+            keep.append(d)
+            descs.append(make_desc(d, [n], out_start=[k * n]))
+        out = np.zeros(len(cases) * n, np.uint16)
+        assert ch.decode_batch(descs, out, [len(cases) * n], enc_device=True) == [0] * len(cases)
+        assert out.tobytes() == np.concatenate(cases).tobytes(), shuffle
+    assert ("shuffle", 0, None) in kinds and ("shuffle", 1, None) in kinds, kinds  # raw and rle planes
+    assert ("shuffle", 2, 0) in kinds, kinds  # literal-only
+    assert ("noshuffle", 0, None) in kinds, kinds

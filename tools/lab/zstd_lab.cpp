@@ -178,10 +178,10 @@ int main(int argc, char **argv) {
                        Z.nblk, Z.mode, (uint32_t)n, Z.lit, Z.lit_stride, lit_rec);
     CK(hipEventRecord(ev[4]));
     hipLaunchKernelGGL(zgpu::k_zstd_plan, dim3(n), dim3(64), 0, 0, d_items, d_status, blks, Z.blk_cap, Z.nblk, Z.mode,
-                       chunk, zgpu::XSEG);
+                       chunk, zgpu::XSEG, (uint64_t *)nullptr, Z.lit, Z.lit_stride);
     CK(hipEventRecord(ev[5]));
     hipLaunchKernelGGL(zgpu::k_zstd_direct, dim3(grid), dim3(256), 0, 0, d_items, d_status, blks, Z.blk_cap, Z.nblk,
-                       Z.mode, (uint32_t)n, d_out, chunk, Z.lit, Z.lit_stride);
+                       Z.mode, (uint32_t)n, d_out, chunk, Z.lit, Z.lit_stride, (const uint64_t *)nullptr);
     CK(hipEventRecord(ev[6]));
     hipLaunchKernelGGL(zgpu::k_zstd_exec_item, dim3(n * zgpu::XSEG), dim3(64), 0, 0, d_items, d_status, blks,
                        Z.blk_cap, Z.nblk, Z.mode, d_out, chunk, Z.lit, Z.lit_stride, Z.seq, Z.seq_cap, zgpu::XSEG);

@@ -836,9 +836,13 @@ __global__ __launch_bounds__(256) void k_blosc_finish(const BlBlock *blocks, con
                                                       const uint32_t *sub_status, const uint32_t *sub_kind,
                                                       uint32_t *status, uint8_t *dst, uint64_t slot_bytes,
                                                       const ZgItem *items, uint8_t *dout, const uint64_t *geom,
-                                                      ZgScatter sc) {
+                                                      ZgScatter sc, const uint64_t *alias) {
   const BlBlock B = blocks[blockIdx.x];
   __shared__ uint64_t src[256];
+  // zstd blocks left where they are (ZstdScratch::alias): stream j's bytes [a_off, a_off + a_len) of
+  // entry r are at a_src[j][r] (or all one byte: ZALIAS_RLE)
+  __shared__ uint64_t a_src[256][ZALIAS];
+  __shared__ uint32_t a_off[256][ZALIAS], a_len[256][ZALIAS];
   __shared__ uint64_t s_row[BL_DIRECT_ROWS];  // direct output: the output address of each row the block covers
   __shared__ uint32_t bad;
   if (threadIdx.x == 0) bad = status[B.item] ? 2u : 0u;  // one read: other blocks may set it meanwhile
@@ -848,7 +852,18 @@ __global__ __launch_bounds__(256) void k_blosc_finish(const BlBlock *blocks, con
     const uint32_t s = B.first_sub + j;
     const ZgItem it = subs[s];
     if (sub_kind[s] != BL_KIND_RAW && (sub_status[s] != 0 || it.len != B.ne)) bad = 1;
-    if (j < 256) src[j] = it.src;
+    if (j < 256) {
+      src[j] = it.src;
+      const bool al = alias && sub_kind[s] == BL_KIND_ZSTD;
+      for (uint32_t r = 0; r < ZALIAS; r++) {
+        const uint64_t *a = alias + 3 * (ZALIAS * (uint64_t)s + r);
+        const uint64_t off = al ? a[1] : 0, len = al ? a[2] : 0;
+        const bool ok = len && off + len <= it.len;
+        a_src[j][r] = ok ? a[0] : 0ull;
+        a_off[j][r] = ok ? (uint32_t)off : 0u;
+        a_len[j][r] = ok ? (uint32_t)len : 0u;
+      }
+    }
   }
   __syncthreads();
   if (bad) {
@@ -862,9 +877,20 @@ __global__ __launch_bounds__(256) void k_blosc_finish(const BlBlock *blocks, con
   uint8_t *out = dst + (uint64_t)B.item * slot_bytes + B.out_off;
   const uint32_t ne = B.ne, ts = B.ts, bsize = B.bsize;
   auto in = [&](uint32_t q) -> uint8_t {
-    const uint32_t j = ne ? q / ne : 0;
-    return ((const uint8_t *)src[j])[q - j * ne];
+    const uint32_t j = ne ? q / ne : 0, l = q - j * ne;
+#pragma unroll
+    for (uint32_t r = 0; r < ZALIAS; r++) {
+      const uint32_t d = l - a_off[j][r];
+      if (d < a_len[j][r]) {
+        const uint64_t a = a_src[j][r];
+        return (a & ZALIAS_RLE) ? (uint8_t)a : ((const uint8_t *)a)[d];
+      }
+    }
+    return ((const uint8_t *)src[j])[l];
   };
+  bool aliased = false;
+  for (uint32_t j = 0; j < B.nsplit; j++)
+    for (uint32_t r = 0; r < ZALIAS; r++) aliased |= a_len[j][r] != 0;
   // direct output: chunk byte c lives in row c / Lb (C order over the chunk's leading axes) at
   // column c mod Lb; the block's rows are resolved once into s_row
   const bool direct = dout && (items[B.item].flags & ZG_ITEM_DIRECT);
@@ -890,19 +916,39 @@ __global__ __launch_bounds__(256) void k_blosc_finish(const BlBlock *blocks, con
     const uint32_t c = c0 + q, r = c / Lb;
     return (uint8_t *)s_row[r - r0] + (c - r * Lb);
   };
-  if (B.mode == 1 && (ts == 2 || ts == 4) && ne && bsize % (16 * ts) == 0 && ((uintptr_t)out & 15) == 0 &&
-      (c0 & 15) == 0) {
+  // byte plane i of a shuffled block: one pointer (or one byte value: bit i of rle) when the plane
+  // lies inside one aliased range of its stream or outside all of them
+  const uint8_t *pl[4];
+  uint32_t rle = 0, rle_v[4] = {0, 0, 0, 0};
+  bool planes = B.mode == 1 && (ts == 2 || ts == 4) && ne;
+  for (uint32_t i = 0; planes && i < ts; i++) {
+    const uint32_t neb = bsize / ts, q = i * neb, j = q / ne, l = q - j * ne;
+    pl[i] = (const uint8_t *)src[j] + l;
+    for (uint32_t r = 0; r < ZALIAS; r++) {
+      const uint32_t ao = a_off[j][r], al = a_len[j][r];
+      if (!al || l + neb <= ao || l >= ao + al) continue;  // disjoint
+      if (l < ao || l + neb > ao + al) {  // straddles the range: the byte loop
+        planes = false;
+        break;
+      }
+      const uint64_t a = a_src[j][r];
+      if (a & ZALIAS_RLE) {
+        rle |= 1u << i;
+        rle_v[i] = (uint32_t)(a & 255) * 0x01010101u;
+      } else {
+        pl[i] = (const uint8_t *)a + (l - ao);
+      }
+    }
+  }
+  if (planes && bsize % (16 * ts) == 0 && ((uintptr_t)out & 15) == 0 && (c0 & 15) == 0) {
     // u16 / u32 fast path: 16 elements per thread, a 16-B load from each byte plane and ts 16-B
     // stores of the interleaved bytes (the generic loop below moves a byte per lane with two
     // integer divisions). Planes stored inside the frame (incompressible byte planes, e.g. noise
-    // low bytes) sit at any address: unaligned 16-B global loads (gfx950 runs in unaligned mode)
+    // low bytes, or an aliased zstd block) sit at any address: unaligned 16-B global loads (gfx950
+    // runs in unaligned mode)
     const uint32_t neb = bsize / ts;
-    const uint8_t *pl[4];
-    for (uint32_t i = 0; i < ts; i++) {
-      const uint32_t q = i * neb, j = q / ne;
-      pl[i] = (const uint8_t *)src[j] + (q - j * ne);
-    }
     auto ldv = [&](uint32_t i, uint32_t v) -> uint4 {
+      if ((rle >> i) & 1) return make_uint4(rle_v[i], rle_v[i], rle_v[i], rle_v[i]);
       uint4 r;
       __builtin_memcpy(&r, pl[i] + 16ull * v, 16);
       return r;
@@ -961,7 +1007,7 @@ __global__ __launch_bounds__(256) void k_blosc_finish(const BlBlock *blocks, con
     // of every row: coalesced across the threads) and per output byte b transposes the 8x8 bit
     // matrix of rows 8b..8b+7 (three masked swaps of a u64).
     const uint8_t *s0 = (const uint8_t *)src[0];
-    const bool one = B.nsplit == 1;
+    const bool one = B.nsplit == 1 && !aliased;
     const bool vec = (ts == 2 || ts == 4) && !direct && ((uintptr_t)out & 15) == 0;
     for (uint32_t g = threadIdx.x; g < rb; g += 256) {
       auto row = [&](uint32_t r) -> uint64_t { return one ? s0[r * rb + g] : in(r * rb + g); };
@@ -1086,7 +1132,8 @@ hipError_t launch_blosc_decode(ZgItem *items, uint32_t *status, uint32_t n_items
   }
   if (D.n_blk)
     hipLaunchKernelGGL(k_blosc_finish, dim3((uint32_t)D.n_blk), dim3(256), 0, s, D.blocks, D.subs, D.sub_status,
-                       D.sub_kind, status, dst, slot_bytes, items, D.dout, D.geom, D.sc);
+                       D.sub_kind, status, dst, slot_bytes, items, D.dout, D.geom, D.sc,
+                       D.n_zstd ? D.zs.alias : nullptr);
   return hipGetLastError();
 }
 

@@ -113,7 +113,16 @@ struct ZstdScratch {
   // zstd_lit_rec_bytes() bytes for lit_rec_wgs workgroups
   uint8_t *lit_rec = nullptr;
   uint32_t lit_rec_wgs = 0;
+  // Block aliases (nullable; the blosc stage sets it: its consumer k_blosc_finish reads the decoded
+  // streams itself). Per item ZALIAS entries {src, off, len}: a block that needs no execution (raw,
+  // rle, or literals only), that no later match reads and no checksum covers, is left where its
+  // bytes already are (in the frame or the literal scratch; rle: src = ZALIAS_RLE | byte) and
+  // k_zstd_direct does not copy it into the slot: item bytes [off, off + len) are src[0 .. len).
+  // len = 0: none. Byte-shuffled blosc blocks of noisy data: the low-byte plane is a raw block.
+  uint64_t *alias = nullptr;
 };
+constexpr uint32_t ZALIAS = 2;
+constexpr uint64_t ZALIAS_RLE = 1ull << 63;
 uint64_t zstd_lit_rec_bytes(uint32_t &wgs);
 void zstd_scratch_layout(uint64_t slot_bytes, uint32_t &blk_cap, uint64_t &blk_bytes, uint64_t &lit_stride,
                          uint64_t &seq_cap);

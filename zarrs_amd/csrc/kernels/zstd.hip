@@ -3134,10 +3134,13 @@ constexpr uint32_t XSEG = ZG_XSEG;
 
 __global__ __launch_bounds__(64) void k_zstd_plan(const ZgItem *items, uint32_t *status, ZBlk *blks,
                                                   uint32_t blk_cap, const uint32_t *nblk, const uint32_t *zmode,
-                                                  uint64_t slot_bytes, uint32_t xseg) {
+                                                  uint64_t slot_bytes, uint32_t xseg, uint64_t *alias,
+                                                  const uint8_t *lit_scratch, uint64_t lit_stride) {
   const uint32_t item = blockIdx.x;
-  if (zmode[item] != ZMODE_PARALLEL || status[item]) return;
   const int lane = lane_id();
+  if (alias && lane == 0)
+    for (uint32_t r = 0; r < ZALIAS; r++) alias[3 * (ZALIAS * item + r) + 2] = 0;  // none
+  if (zmode[item] != ZMODE_PARALLEL || status[item]) return;
   ZBlk *B = blks + (uint64_t)item * blk_cap;
   const uint32_t nb = nblk[item];
   if (lane == 0 && nb) B[0].in_src = items[item].src;
@@ -3187,6 +3190,7 @@ __global__ __launch_bounds__(64) void k_zstd_plan(const ZgItem *items, uint32_t 
     uint64_t smin = ~0ull, total_w = 0, vmask = 0;  // vmask: lane l holds the cuts at blocks 64 l ..
     bool ck = false;
     const bool cuts = nb <= 64 * 64;
+    uint32_t al[ZALIAS] = {~0u, ~0u};  // aliased blocks (ZstdScratch::alias): the earliest candidates
     for (uint32_t bi = nb; cuts && bi-- > 0;) {
       const uint32_t flags = U(B[bi].flags), type = flags & 3, nsq = U(B[bi].nseq), osz = U(B[bi].out_size);
       if (flags & ZBF_LAST) ck = flags & ZBF_CK;
@@ -3199,6 +3203,12 @@ __global__ __launch_bounds__(64) void k_zstd_plan(const ZgItem *items, uint32_t 
         }
         const int64_t ms = (int64_t)off - reach;
         smin = min<uint64_t>(smin, ms < 0 ? 0ull : (uint64_t)ms);
+      }
+      // a block no later match reads (it has no matches itself) and no checksum covers
+      if (alias && !ck && x_direct_block(flags, nsq, osz) && smin >= off + osz &&
+          (type != ZB_CMP || U(B[bi].regen) == osz)) {
+        al[1] = al[0];
+        al[0] = bi;
       }
       const bool valid = bi > 0 && smin >= off && (!ck || (flags & ZBF_FIRST));
       total_w += (type == ZB_CMP ? 8ull * nsq : 0ull) + (x_direct_block(flags, nsq, osz) ? 0u : osz / 16);
@@ -3219,6 +3229,20 @@ __global__ __launch_bounds__(64) void k_zstd_plan(const ZgItem *items, uint32_t 
         acc += (type == ZB_CMP ? 8ull * nsq : 0ull) + (x_direct_block(flags, nsq, osz) ? 0u : osz / 16);
       }
       if (lane == 0) B[bi].seg = seg;
+    }
+    if (alias && lane == 0) {
+      const uint8_t *in = (const uint8_t *)items[item].src;
+      for (uint32_t r = 0; r < ZALIAS && al[r] != ~0u; r++) {
+        const ZBlk &L = B[al[r]];
+        const uint32_t fl = L.flags, ty = fl & 3;
+        const uint64_t src = ty == ZB_RLE ? ZALIAS_RLE | in[L.in_off]
+                             : ty == ZB_RAW ? (uint64_t)(in + L.in_off)
+                             : ((fl >> 2) & 3) == 0 ? (uint64_t)(in + L.lit_off)
+                                                    : (uint64_t)(lit_scratch + (uint64_t)item * lit_stride + L.lit_buf);
+        alias[3 * (ZALIAS * item + r)] = src;
+        alias[3 * (ZALIAS * item + r) + 1] = L.out_off;
+        alias[3 * (ZALIAS * item + r) + 2] = L.out_size;
+      }
     }
   }
   if (lane == 0 && err) status[item] = err;
@@ -3790,7 +3814,8 @@ __device__ __forceinline__ bool x_long_match(ZXSmem &S, XOut &O, uint64_t fstart
 __global__ __launch_bounds__(256) void k_zstd_direct(const ZgItem *items, const uint32_t *status, const ZBlk *blks,
                                                     uint32_t blk_cap, const uint32_t *nblk, const uint32_t *zmode,
                                                     uint32_t n_items, uint8_t *dst, uint64_t slot_bytes,
-                                                    const uint8_t *lit_scratch, uint64_t lit_stride) {
+                                                    const uint8_t *lit_scratch, uint64_t lit_stride,
+                                                    const uint64_t *alias) {
   const uint64_t recs = (uint64_t)n_items * blk_cap;
   const uint32_t tid = threadIdx.x;
   for (uint64_t rec = blockIdx.x; rec < recs; rec += gridDim.x) {
@@ -3800,6 +3825,12 @@ __global__ __launch_bounds__(256) void k_zstd_direct(const ZgItem *items, const 
     const uint32_t flags = b.flags, type = flags & 3, n = b.out_size;
     if (!x_direct_block(flags, b.nseq, n)) continue;
     if (type == ZB_CMP && b.regen != n) continue;  // corrupt: k_zstd_exec_item reports it
+    if (alias) {  // the consumer reads an aliased block where it is
+      const uint64_t *a = alias + 3 * ZALIAS * (uint64_t)item;
+      bool al = false;
+      for (uint32_t r = 0; r < ZALIAS; r++) al |= a[3 * r + 2] && a[3 * r + 1] == b.out_off;
+      if (al) continue;
+    }
     const uint8_t *in = (const uint8_t *)items[item].src;
     uint8_t *o = dst + (uint64_t)item * slot_bytes + b.out_off;
     if (type == ZB_RLE) {
@@ -4146,9 +4177,9 @@ hipError_t launch_zstd(ZgItem *items, uint32_t *status, uint32_t n_items, uint8_
   }();
   const uint32_t xseg = xseg_env ? xseg_env : XSEG;
   hipLaunchKernelGGL(k_zstd_plan, dim3(n_items), dim3(64), 0, s, items, status, blks, Z.blk_cap, Z.nblk, Z.mode,
-                     slot_bytes, xseg);
+                     slot_bytes, xseg, Z.alias, Z.lit, Z.lit_stride);
   hipLaunchKernelGGL(k_zstd_direct, dim3(grid), dim3(256), 0, s, items, status, blks, Z.blk_cap, Z.nblk, Z.mode,
-                     n_items, dst, slot_bytes, Z.lit, Z.lit_stride);
+                     n_items, dst, slot_bytes, Z.lit, Z.lit_stride, Z.alias);
   hipLaunchKernelGGL(k_zstd_exec_item, dim3(n_items * xseg), dim3(64), 0, s, items, status, blks, Z.blk_cap, Z.nblk,
                      Z.mode, dst, slot_bytes, Z.lit, Z.lit_stride, Z.seq, Z.seq_cap, xseg);
   if (!listed) {

@@ -289,7 +289,7 @@ struct zgpu_plan {
     size_t n = 0;
   };
   Grow bl_info, bl_bases, bl_subs, bl_sub_status, bl_sub_kind, bl_blocks, bl_tmp, bl_zblks, bl_znblk, bl_zmode,
-      bl_zlit, bl_zseq, bl_zaux, bl_zser, bl_lzl, bl_zseg, bl_zrec;
+      bl_zlit, bl_zseq, bl_zaux, bl_zser, bl_lzl, bl_zseg, bl_zrec, bl_zalias;
   uint8_t *bl_h = nullptr;  // pinned: BlInfo read-back (first execution)
   size_t bl_h_n = 0;
   void *grow(Grow &g, size_t bytes) {
@@ -344,7 +344,7 @@ struct zgpu_plan {
     for (hipEvent_t e : zev)
       if (e) (void)hipEventDestroy(e);
     for (Grow *g : {&bl_info, &bl_bases, &bl_subs, &bl_sub_status, &bl_sub_kind, &bl_blocks, &bl_tmp, &bl_zblks,
-                    &bl_znblk, &bl_zmode, &bl_zlit, &bl_zseq, &bl_zaux, &bl_zser, &bl_lzl, &bl_zseg, &bl_zrec})
+                    &bl_znblk, &bl_zmode, &bl_zlit, &bl_zseq, &bl_zaux, &bl_zser, &bl_lzl, &bl_zseg, &bl_zrec, &bl_zalias})
       ctx->dev_free(g->p);
     ctx->host_free(bl_h);
     ctx->host_free(h_ctl);
@@ -921,6 +921,12 @@ static void blosc_stage(zgpu_plan &P, const Stage &st, uint8_t *out, hipStream_t
     D.zs.force_serial = P.zs.force_serial;
     D.zs.ser_list = (uint32_t *)P.grow(P.bl_zser, D.n_sub * 4);
     if (const uint64_t rb = zstd_lit_rec_bytes(D.zs.lit_rec_wgs)) D.zs.lit_rec = (uint8_t *)P.grow(P.bl_zrec, rb);
+    // k_blosc_finish reads raw / rle / literal-only zstd blocks where they lie (ZGPU_BLOSC_ALIAS=0: off)
+    static const bool alias_on = [] {
+      const char *e = std::getenv("ZGPU_BLOSC_ALIAS");
+      return !e || std::atoi(e) != 0;
+    }();
+    D.zs.alias = alias_on ? (uint64_t *)P.grow(P.bl_zalias, D.n_sub * 3 * ZALIAS * 8) : nullptr;
     D.zs.ser_count = P.zs.ser_count;
     D.zs.launch_serial = P.zs.launch_serial;
     P.zstd_fork(D.zs, s);
