@@ -33,8 +33,11 @@ size_t ZSTD_compressBound(size_t srcSize);
 int main(int argc, char **argv) {
   setvbuf(stdout, NULL, _IOLBF, 0);
   const int n = argc > 1 ? atoi(argv[1]) : 64;
-  const uint64_t chunk = (argc > 2 ? atoll(argv[2]) : 16) << 20;  // bytes
-  const int level = argc > 3 ? atoi(argv[3]) : 3;
+  // argv[4] == "bz": the blosc-zstd bench's streams: 256 KiB byte-shuffled blocks (2 z-slices of a
+  // [64,256,256] chunk of the u16 volume [1024,2048,1024]) at zstd level 9 (c-blosc clevel 5)
+  const bool bz = argc > 4 && !strcmp(argv[4], "bz");
+  const uint64_t chunk = bz ? 262144ull : (uint64_t)(argc > 2 ? atoll(argv[2]) : 16) << 20;  // bytes
+  const int level = bz ? 9 : argc > 3 ? atoi(argv[3]) : 3;
   // argv[4] == "c5": chunks [32,512,512] of a bench-like C5 level 0 ([512,1024,1024], 64 blobs)
   // argv[4] == "c5l1": chunks [64,256,256] of the 2x2x2 mean of that level (8 MiB each)
   const bool l1 = argc > 4 && !strcmp(argv[4], "c5l1");
@@ -86,7 +89,16 @@ int main(int argc, char **argv) {
     std::normal_distribution<float> nd(0.f, 1.f);
     const uint64_t cnt = chunk / 2;
     std::vector<uint16_t> v(cnt);
-    for (uint64_t i = 0; i < cnt; i++) {
+    if (bz) {
+      const int ci = c / 32, b = c % 32;
+      const int z0 = 64 * ((ci / 32) % 16) + 2 * b, y0 = 256 * ((ci / 4) % 8), x0 = 256 * (ci % 4);
+      for (uint64_t i = 0; i < cnt; i++) {
+        const float z = (float)(z0 + (int)(i >> 16)), y = (float)(y0 + (int)((i >> 8) & 255)), x = (float)(x0 + (int)(i & 255));
+        const float m = 100.f + 900.f * fabsf(sinf(z * 0.05f) * cosf(y * 0.013f) * sinf(x * 0.021f));
+        v[i] = (uint16_t)fminf(fmaxf(m + nd(rng) * sqrtf(m), 0.f), 65535.f);
+      }
+    }
+    for (uint64_t i = 0; !bz && i < cnt; i++) {
       const float x = (float)(i % 512), y = (float)((i / 512) % 512);
       const float m = 100.f + 3000.f * expf(-((x - 200) * (x - 200) + (y - 300) * (y - 300)) / (2 * 40.f * 40.f));
       float val = rintf(m + sqrtf(m) * nd(rng));

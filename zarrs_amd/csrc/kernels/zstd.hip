@@ -3273,7 +3273,11 @@ constexpr uint32_t XSTAGE_V = ZG_XSTAGE_V;  // staged far-source vectors (16 B) 
 #ifndef ZG_XWPE
 #define ZG_XWPE 2  // the executor is compiled for >= 2 waves/SIMD (VGPR + AGPR <= 256)
 #endif
-constexpr uint32_t XPL = 32;        // bytes of a short match its own lane copies (the rest: the wave)
+#ifndef ZG_XPL
+#define ZG_XPL 32
+#endif
+constexpr uint32_t XPL = ZG_XPL;  // bytes of a short match its own lane copies (the rest: the wave)
+static_assert(XPL % 16 == 0 && XPL >= 16 && XPL <= 512, "XPL: 16-B pieces, at most a short match");
 constexpr int XR_LIT = ZBATCH / 16 / 64 + 1, XR_FAR = XSTAGE_V / 64;
 
 struct ZXSmem {
@@ -3608,9 +3612,8 @@ __device__ uint32_t x_resolve(ZXSmem &S, uint64_t ms, uint32_t d, uint32_t n, ui
         // groups of up to 8 pieces: all loads of a group, then its stores; a piece never starts
         // after n - 16 (the last one rewrites its neighbour's bytes with the same values)
         const uint32_t lim = n - 16;
-        {  // bytes from XPL = 128 on: the whole wave, below
-          const uint32_t g0 = 0;
-          const uint32_t np = min((n - g0 + 15) >> 4, XPL / 16);
+        for (uint32_t g0 = 0; g0 < min(n, XPL); g0 += 128) {  // bytes from XPL on: the whole wave, below
+          const uint32_t np = min((min(n, XPL) - g0 + 15) >> 4, 8u);
           zv4u v0, v1, v2, v3, v4, v5, v6, v7;
           v0 = ld16(sp + min(g0, lim));
           if (np > 1) v1 = ld16(sp + min(g0 + 16, lim));
