@@ -3274,10 +3274,14 @@ constexpr uint32_t XSTAGE_V = ZG_XSTAGE_V;  // staged far-source vectors (16 B) 
 #define ZG_XWPE 2  // the executor is compiled for >= 2 waves/SIMD (VGPR + AGPR <= 256)
 #endif
 #ifndef ZG_XPL
-#define ZG_XPL 32
+#define ZG_XPL 64
 #endif
 constexpr uint32_t XPL = ZG_XPL;  // bytes of a short match its own lane copies (the rest: the wave)
 static_assert(XPL % 16 == 0 && XPL >= 16 && XPL <= 512, "XPL: 16-B pieces, at most a short match");
+#ifndef ZG_XLI
+#define ZG_XLI 1
+#endif
+constexpr uint32_t XLI = ZG_XLI;  // long matches the wave copies per step (their loads together)
 constexpr int XR_LIT = ZBATCH / 16 / 64 + 1, XR_FAR = XSTAGE_V / 64;
 
 struct ZXSmem {
@@ -3655,22 +3659,46 @@ __device__ uint32_t x_resolve(ZXSmem &S, uint64_t ms, uint32_t d, uint32_t n, ui
       const uint8_t *lb = (const uint8_t *)&S;
       const uint32_t so = (uint32_t)(sp - lb), dof = (uint32_t)(dp - lb);
       uint64_t bm = __ballot(ready && ((splat && te > XPL) || (fast && !splat && n > XPL)));
+      // XLI matches per step: their loads issued together, then their stores (the sources of this
+      // round's matches are no destination of a pending match, so the order within a round is free)
       while (bm) {
-        const int i = __builtin_ctzll(bm);
-        bm &= bm - 1;
-        const uint32_t n_i = U(__builtin_amdgcn_readlane(n, i)), do_i = U(__builtin_amdgcn_readlane(dof, i));
-        const uint32_t te_i = U(__builtin_amdgcn_readlane(te, i));
-        if (te_i) {
-          const uint32_t L_i = U(__builtin_amdgcn_readlane(L, i));
-          const zv4u pv_i = zv4u{U(__builtin_amdgcn_readlane(pat[0], i)), U(__builtin_amdgcn_readlane(pat[1], i)),
-                                 U(__builtin_amdgcn_readlane(pat[2], i)), U(__builtin_amdgcn_readlane(pat[3], i))};
-          const uint32_t t = ((XPL + L_i - 1) / L_i + lane) * L_i;
-          if (t < te_i) st16((uint8_t *)lb + do_i + t, pv_i);
-        } else {
-          const uint32_t so_i = U(__builtin_amdgcn_readlane(so, i));
-          const uint32_t k = min(XPL + 16 * lane, n_i - 16);
-          if (XPL + 16 * lane < n_i) st16((uint8_t *)lb + do_i + k, ld16(lb + so_i + k));
+        int idx[XLI];
+        uint32_t c = 0;
+#pragma unroll
+        for (uint32_t u = 0; u < XLI; u++)
+          if (bm) {
+            idx[u] = __builtin_ctzll(bm);
+            bm &= bm - 1;
+            c++;
+          }
+        zv4u v[XLI];
+        uint32_t dk[XLI];
+        bool go[XLI];
+#pragma unroll
+        for (uint32_t u = 0; u < XLI; u++) {
+          go[u] = false;
+          if (u < c) {
+            const int i = idx[u];
+            const uint32_t n_i = U(__builtin_amdgcn_readlane(n, i)), do_i = U(__builtin_amdgcn_readlane(dof, i));
+            const uint32_t te_i = U(__builtin_amdgcn_readlane(te, i));
+            if (te_i) {
+              const uint32_t L_i = U(__builtin_amdgcn_readlane(L, i));
+              const zv4u pv_i = zv4u{U(__builtin_amdgcn_readlane(pat[0], i)), U(__builtin_amdgcn_readlane(pat[1], i)),
+                                     U(__builtin_amdgcn_readlane(pat[2], i)), U(__builtin_amdgcn_readlane(pat[3], i))};
+              const uint32_t t = ((XPL + L_i - 1) / L_i + lane) * L_i;
+              if (t < te_i) st16((uint8_t *)lb + do_i + t, pv_i);
+            } else {
+              const uint32_t so_i = U(__builtin_amdgcn_readlane(so, i));
+              const uint32_t k = min(XPL + 16 * lane, n_i - 16);
+              go[u] = XPL + 16 * lane < n_i;
+              if (go[u]) v[u] = ld16(lb + so_i + k);
+              dk[u] = do_i + k;
+            }
+          }
         }
+#pragma unroll
+        for (uint32_t u = 0; u < XLI; u++)
+          if (go[u]) st16((uint8_t *)lb + dk[u], v[u]);
       }
     }
     uint64_t sm = __ballot(ready && !fast);
