@@ -195,8 +195,12 @@ int main(int argc, char **argv) {
     hipLaunchKernelGGL(zgpu::k_zstd_direct, dim3(grid), dim3(256), 0, 0, d_items, d_status, blks, Z.blk_cap, Z.nblk,
                        Z.mode, (uint32_t)n, d_out, chunk, Z.lit, Z.lit_stride, (const uint64_t *)nullptr);
     CK(hipEventRecord(ev[6]));
-    hipLaunchKernelGGL(zgpu::k_zstd_exec_item, dim3(n * zgpu::XSEG), dim3(64), 0, 0, d_items, d_status, blks,
-                       Z.blk_cap, Z.nblk, Z.mode, d_out, chunk, Z.lit, Z.lit_stride, Z.seq, Z.seq_cap, zgpu::XSEG);
+    if (getenv("LAB_XDENSE"))
+      hipLaunchKernelGGL(zgpu::xdense::k_zstd_exec_item, dim3(n * zgpu::XSEG), dim3(64), 0, 0, d_items, d_status, blks,
+                         Z.blk_cap, Z.nblk, Z.mode, d_out, chunk, Z.lit, Z.lit_stride, Z.seq, Z.seq_cap, zgpu::XSEG);
+    else
+      hipLaunchKernelGGL(zgpu::xwide::k_zstd_exec_item, dim3(n * zgpu::XSEG), dim3(64), 0, 0, d_items, d_status, blks,
+                         Z.blk_cap, Z.nblk, Z.mode, d_out, chunk, Z.lit, Z.lit_stride, Z.seq, Z.seq_cap, zgpu::XSEG);
     CK(hipEventRecord(ev[7]));
     CK(hipEventSynchronize(ev[7]));
     for (int k = 0; k < NK; k++) {

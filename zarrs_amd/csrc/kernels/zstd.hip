@@ -3248,598 +3248,6 @@ __global__ __launch_bounds__(64) void k_zstd_plan(const ZgItem *items, uint32_t 
   if (lane == 0 && err) status[item] = err;
 }
 
-namespace {
-// -------------------------------------------------------------------------------------------------
-// k_zstd_exec_item: one wave per item executes its blocks in order from the decoded sequences and
-// literals. An 8 KiB LDS ring (ZG_XRING; 32 and 64 KiB rings measured no faster on C5's L1 frames)
-// holds the recent output; a match reaching further back reads output
-// this wave already flushed, staged into LDS per batch by 16-B loads issued together with the
-// batch's literal loads: one memory round trip per batch, not one per match. A batch is up to 64
-// sequences spanning <= ZBATCH bytes; its matches resolve in rounds: every pending match none of
-// whose source bytes is still to be written by another pending match is copied in the round.
-// (Matches crossing block boundaries are the rule in real data, e.g. byte-shuffled u16 images
-// whose high-byte plane is a chain of row- and plane-periodic copies, so there is no block-level
-// parallelism to take here; it is taken in k_zstd_lits / k_zstd_blocks, and across items.)
-// -------------------------------------------------------------------------------------------------
-#ifndef ZG_XRING
-#define ZG_XRING 8192
-#endif
-constexpr uint32_t XRING = ZG_XRING, XRMASK = XRING - 1;
-static_assert((XRING & XRMASK) == 0 && XRING >= 2 * ZBATCH, "exec ring: a power of two holding two batches");
-#ifndef ZG_XSTAGE_V
-#define ZG_XSTAGE_V 256
-#endif
-constexpr uint32_t XSTAGE_V = ZG_XSTAGE_V;  // staged far-source vectors (16 B) per batch
-#ifndef ZG_XWPE
-#define ZG_XWPE 2  // the executor is compiled for >= 2 waves/SIMD (VGPR + AGPR <= 256)
-#endif
-#ifndef ZG_XPL
-#define ZG_XPL 64
-#endif
-constexpr uint32_t XPL = ZG_XPL;  // bytes of a short match its own lane copies (the rest: the wave)
-static_assert(XPL % 16 == 0 && XPL >= 16 && XPL <= 512, "XPL: 16-B pieces, at most a short match");
-#ifndef ZG_XLI
-#define ZG_XLI 1
-#endif
-constexpr uint32_t XLI = ZG_XLI;  // long matches the wave copies per step (their loads together)
-constexpr int XR_LIT = ZBATCH / 16 / 64 + 1, XR_FAR = XSTAGE_V / 64;
-
-struct ZXSmem {
-  uint8_t ring[XRING];
-  zv4u stage[XSTAGE_V];
-  uint8_t lit_stage[ZBATCH + 32];  // the batch's literals at their 16-B phase in memory
-  uint8_t vown[XSTAGE_V];  // staged far vector -> the lane (match) it belongs to
-  uint32_t pfx_lit[64], pfx_out[64], pfx_nv[64], own_pv[64];
-  uint64_t own_v0[64];
-};
-
-struct XOut {
-  uint8_t *out;
-  uint64_t pos, flushed;
-  uint64_t rv;  // the ring holds no output below rv (a block written by k_zstd_direct precedes it)
-};
-
-__device__ __forceinline__ uint64_t rl64(uint64_t v, int i) {
-  return (uint64_t)U(__builtin_amdgcn_readlane((uint32_t)v, i)) |
-         ((uint64_t)U(__builtin_amdgcn_readlane((uint32_t)(v >> 32), i)) << 32);
-}
-
-// ring bytes [flushed, pos) -> the item slot
-__device__ __forceinline__ void x_flush(ZXSmem &S, XOut &O) {
-  __syncthreads();
-  const uint64_t from = O.flushed, to = O.pos;
-  const uint64_t a = min<uint64_t>((from + 15) & ~(uint64_t)15, to), b = max<uint64_t>(to & ~(uint64_t)15, a);
-  for (uint64_t p = from + lane_id(); p < a; p += 64) O.out[p] = S.ring[p & XRMASK];
-  for (uint64_t p = a + (uint64_t)lane_id() * 16; p < b; p += 64 * 16)
-    *(zv4u *)(O.out + p) = *(const zv4u *)&S.ring[p & XRMASK];
-  for (uint64_t p = b + lane_id(); p < to; p += 64) O.out[p] = S.ring[p & XRMASK];
-  O.flushed = to;
-  __syncthreads();
-}
-// before producing output up to wend: at most half the ring stays unflushed
-__device__ __forceinline__ void x_reserve(ZXSmem &S, XOut &O, uint64_t wend) {
-  if (wend - O.flushed > XRING / 2) x_flush(S, O);
-}
-// Sources below the bound are read from the slot: flushed, in whole 128-B lines (so no L1 line can
-// hold a byte written after the line was loaded). Sources at or above it are still in the ring and
-// are not overwritten by a batch ending at wend (<= ZBATCH past the current position).
-__device__ __forceinline__ uint64_t x_far_bound(const XOut &O, uint64_t wend) {
-  const uint64_t lim = max<uint64_t>(wend + ZBATCH > XRING ? wend + ZBATCH - XRING : 0, O.rv);  // rv: 128-B aligned
-  return min<uint64_t>(lim, O.flushed) & ~(uint64_t)127;
-}
-// n bytes of global memory into the ring at the output position, 16 KiB pieces (every load of a
-// piece in flight before its first LDS write)
-__device__ __forceinline__ void x_copy(ZXSmem &S, XOut &O, const uint8_t *src, uint64_t n) {
-  const int lane = lane_id();
-  if (!n) return;
-  // bytes up to the ring's next 16-B boundary, then 16-B chunks stored aligned (unaligned 16-B LDS
-  // accesses are replayed, cdna_hip_programming.md Guideline 17): every chunk's source is
-  // misaligned by the same m, so a chunk is two aligned global vectors and four byte-aligns
-  uint64_t done = min<uint64_t>(n, (16 - (O.pos & 15)) & 15);
-  if (done) {
-    x_reserve(S, O, O.pos + done);
-    if (lane < (int)done) S.ring[(O.pos + lane) & XRMASK] = src[lane];
-    O.pos += done;
-  }
-  const uintptr_t s0 = (uintptr_t)(src + done);
-  const uint32_t m = (uint32_t)(s0 & 15), mq = m >> 2, mr = m & 3;
-  const zv4u *sa = (const zv4u *)(s0 & ~(uintptr_t)15);
-  const uint64_t nch = (n - done) >> 4;
-  // chunks per piece: up to 16 KiB, and at most half the ring (x_reserve keeps the unflushed part
-  // of the ring within half of it, so a piece never overwrites bytes that are not yet flushed)
-  constexpr uint32_t R = XRING / 2 / 16 / 64 < 16 ? XRING / 2 / 16 / 64 : 16, PC = 64 * R;
-  for (uint64_t c0 = 0; c0 < nch; c0 += PC) {
-    const uint32_t cn = (uint32_t)min<uint64_t>(PC, nch - c0);
-    x_reserve(S, O, O.pos + 16ull * cn);
-    zv4u lo[R], hi[R];
-#pragma unroll
-    for (uint32_t r = 0; r < R; r++) {
-      const uint32_t i = lane + 64 * r;
-      if (i < cn) {
-        lo[r] = __builtin_nontemporal_load(sa + c0 + i);
-        hi[r] = m ? __builtin_nontemporal_load(sa + c0 + i + 1) : lo[r];
-      }
-    }
-#pragma unroll
-    for (uint32_t r = 0; r < R; r++) {
-      const uint32_t i = lane + 64 * r;
-      if (i < cn) {
-        const uint32_t w[8] = {lo[r].x, lo[r].y, lo[r].z, lo[r].w, hi[r].x, hi[r].y, hi[r].z, hi[r].w};
-        zv4u v;
-        // m is uniform: one branch taken by the whole wave
-        if (mq == 0) v = zv4u{__builtin_amdgcn_alignbyte(w[1], w[0], mr), __builtin_amdgcn_alignbyte(w[2], w[1], mr),
-                              __builtin_amdgcn_alignbyte(w[3], w[2], mr), __builtin_amdgcn_alignbyte(w[4], w[3], mr)};
-        else if (mq == 1) v = zv4u{__builtin_amdgcn_alignbyte(w[2], w[1], mr), __builtin_amdgcn_alignbyte(w[3], w[2], mr),
-                                   __builtin_amdgcn_alignbyte(w[4], w[3], mr), __builtin_amdgcn_alignbyte(w[5], w[4], mr)};
-        else if (mq == 2) v = zv4u{__builtin_amdgcn_alignbyte(w[3], w[2], mr), __builtin_amdgcn_alignbyte(w[4], w[3], mr),
-                                   __builtin_amdgcn_alignbyte(w[5], w[4], mr), __builtin_amdgcn_alignbyte(w[6], w[5], mr)};
-        else v = zv4u{__builtin_amdgcn_alignbyte(w[4], w[3], mr), __builtin_amdgcn_alignbyte(w[5], w[4], mr),
-                      __builtin_amdgcn_alignbyte(w[6], w[5], mr), __builtin_amdgcn_alignbyte(w[7], w[6], mr)};
-        *(zv4u *)&S.ring[(O.pos + 16ull * i) & XRMASK] = v;
-      }
-    }
-    O.pos += 16ull * cn;
-  }
-  done += 16 * nch;
-  const uint32_t tail = (uint32_t)(n - done);
-  if (tail) {
-    x_reserve(S, O, O.pos + tail);
-    if (lane < (int)tail) S.ring[(O.pos + lane) & XRMASK] = src[done + lane];
-    O.pos += tail;
-  }
-  __syncthreads();
-}
-__device__ __forceinline__ void x_fill(ZXSmem &S, XOut &O, uint8_t v, uint64_t n) {
-  for (uint64_t done = 0; done < n;) {
-    const uint64_t c = min<uint64_t>(n - done, ZBATCH);
-    x_reserve(S, O, O.pos + c);
-    for (uint64_t k = lane_id(); k < c; k += 64) S.ring[(O.pos + k) & XRMASK] = v;
-    O.pos += c;
-    done += c;
-  }
-  __syncthreads();
-}
-
-// The lanes with n > 0 hold matches {ms, d, n} (sources before ms). Stage their far parts (below fb)
-// and the batch's n_lit literals from lit, all loads in flight together. Returns false (nothing
-// staged) if the far parts exceed the stage. fe / sb: the lane's far end and stage byte offset.
-__device__ __forceinline__ bool x_stage(ZXSmem &S, const uint8_t *out, uint64_t fb, uint64_t ms, uint32_t d,
-                                        uint32_t n, const uint8_t *lit, uint32_t n_lit, uint64_t &fe, int64_t &sb) {
-  const int lane = lane_id();
-  const uint64_t src = ms - d;
-  const uint32_t cl = min(n, d);
-  fe = n ? min<uint64_t>(src + cl, fb) : 0;
-  const bool far = n && fe > src;
-  const uint64_t v0 = src >> 4;
-  const uint32_t nv = far ? (uint32_t)(((fe + 15) >> 4) - v0) : 0u;
-  uint32_t incl = nv;
-  for (int o = 1; o < 64; o <<= 1) {
-    const uint32_t u = __shfl_up(incl, o, 64);
-    if (lane >= o) incl += u;
-  }
-  const uint32_t total = U(__builtin_amdgcn_readlane(incl, 63));
-  if (total > XSTAGE_V) return false;
-  const uint32_t pv = incl - nv;
-  sb = (int64_t)pv * 16 - (int64_t)v0 * 16;
-  S.own_pv[lane] = pv;
-  S.own_v0[lane] = v0;
-  for (uint32_t j = 0; j < nv; j++) S.vown[pv + j] = (uint8_t)lane;  // stage vector -> its lane
-  __syncthreads();
-  const uintptr_t lbase = (uintptr_t)lit & ~(uintptr_t)15;
-  const uint32_t lhead = (uint32_t)((uintptr_t)lit - lbase);
-  const uint32_t lvec = n_lit ? (lhead + n_lit + 15) >> 4 : 0u;
-  zv4u lv[XR_LIT], fv[XR_FAR];
-#pragma unroll
-  for (int r = 0; r < XR_LIT; r++) {
-    const uint32_t idx = lane + 64 * r;
-    if (idx < lvec) lv[r] = __builtin_nontemporal_load((const zv4u *)(lbase + 16ull * idx));
-  }
-#pragma unroll
-  for (int r = 0; r < XR_FAR; r++) {
-    const uint32_t f = lane + 64 * r;
-    if (f < total) {
-      const uint32_t lo = S.vown[f];
-      fv[r] = *(const zv4u *)(out + 16 * (S.own_v0[lo] + (f - S.own_pv[lo])));
-    }
-  }
-#pragma unroll
-  for (int r = 0; r < XR_LIT; r++) {  // aligned as in memory: literal k is lit_stage[lhead + k]
-    const uint32_t idx = lane + 64 * r;
-    if (idx < lvec) *(zv4u *)&S.lit_stage[16 * idx] = lv[r];
-  }
-#pragma unroll
-  for (int r = 0; r < XR_FAR; r++) {
-    const uint32_t f = lane + 64 * r;
-    if (f < total) S.stage[f] = fv[r];
-  }
-  __syncthreads();
-  return true;
-}
-
-// unaligned 16-B LDS moves by value (an address-taken vector array would live in scratch)
-__device__ __forceinline__ zv4u ld16(const uint8_t *p) {
-  zv4u v;
-  __builtin_memcpy(&v, p, 16);
-  return v;
-}
-__device__ __forceinline__ void st16(uint8_t *p, zv4u v) { __builtin_memcpy(p, &v, 16); }
-
-// Gather e <= 16 bytes, byte j from source offset (r + j) mod d of s (stage below fe, else ring),
-// all loads issued before the first store, then store them at o.
-__device__ __forceinline__ void x_gather(ZXSmem &S, const uint8_t *stg, uint64_t o, uint64_t s, uint32_t r,
-                                         uint32_t d, uint32_t e, uint64_t fe, int64_t sb) {
-  uint32_t w[4] = {0, 0, 0, 0};
-  uint32_t rr = r;
-#pragma unroll
-  for (int j = 0; j < 16; j++) {
-    if ((uint32_t)j < e) {
-      const uint64_t q = s + rr;
-      const uint32_t v = q < fe ? stg[(int64_t)q + sb] : S.ring[q & XRMASK];
-      w[j >> 2] |= v << (8 * (j & 3));
-    }
-    rr = rr + 1 == d ? 0u : rr + 1;
-  }
-  if (e == 16 && (o & XRMASK) <= XRING - 16) {
-    st16(&S.ring[o & XRMASK], zv4u{w[0], w[1], w[2], w[3]});
-  } else {
-#pragma unroll
-    for (int j = 0; j < 16; j++)
-      if ((uint32_t)j < e) S.ring[(o + j) & XRMASK] = (uint8_t)(w[j >> 2] >> (8 * (j & 3)));
-  }
-}
-
-// Copy len <= 16 bytes whose source [q, q + len) is contiguous (no period wrap) and entirely before
-// the destination o: ring or stage (below fe) to ring, as one 16-B move or two overlapping 8-B / 4-B
-// moves; bytes only where a move would straddle the ring end or the stage / ring split.
-template <int W>
-__device__ __forceinline__ void x_mv(ZXSmem &S, const uint8_t *stg, uint64_t o, uint64_t q, uint64_t fe, int64_t sb) {
-  typedef __attribute__((ext_vector_type(W / 4))) unsigned int vt;
-  vt v;
-  if (q < fe) __builtin_memcpy(&v, stg + ((int64_t)q + sb), W);
-  else __builtin_memcpy(&v, &S.ring[q & XRMASK], W);
-  __builtin_memcpy(&S.ring[o & XRMASK], &v, W);
-}
-__device__ __forceinline__ void x_run(ZXSmem &S, const uint8_t *stg, uint64_t o, uint64_t q, uint32_t len, uint64_t fe,
-                                      int64_t sb) {
-  const uint32_t w = len >= 16 ? 16u : len >= 8 ? 8u : len >= 4 ? 4u : 0u;
-  const bool ok = w && (o & XRMASK) <= XRING - 16 && (q + len <= fe || (q >= fe && (q & XRMASK) <= XRING - 16));
-  if (ok) {
-    const uint64_t o2 = o + len - w, q2 = q + len - w;
-    if (w == 16) {
-      x_mv<16>(S, stg, o, q, fe, sb);
-    } else if (w == 8) {
-      x_mv<8>(S, stg, o, q, fe, sb);
-      x_mv<8>(S, stg, o2, q2, fe, sb);
-    } else {
-      x_mv<4>(S, stg, o, q, fe, sb);
-      x_mv<4>(S, stg, o2, q2, fe, sb);
-    }
-  } else {
-    x_gather(S, stg, o, q, 0, 0xFFFFFFFFu, len, fe, sb);
-  }
-}
-
-// Resolve the staged matches (see x_stage) in rounds. A round takes every pending match whose source
-// bytes outside itself overlap no pending match's destination (exact dependencies: the rounds are the
-// depth of the batch's copy chain, about half the count of a first-unresolved frontier on C5's
-// high-byte planes, tools/lab/zstd_taint.cpp). A short match (<= 512 bytes, not overlapping its source, source wholly in the stage or the ring) is copied by its
-// own lane: all its 16-byte pieces loaded, then stored (the last piece ends at the match end,
-// rewriting its neighbour's bytes with the same values). Other matches are copied by the whole wave,
-// one after another: byte k is byte (k mod d) of the first period [ms - d, ms - d + min(n, d)),
-// which precedes the match, so no lane reads what another writes. LDS operations of a wave complete
-// in issue order, so a round reads what the previous one wrote without waiting for it.
-__device__ uint32_t x_resolve(ZXSmem &S, uint64_t ms, uint32_t d, uint32_t n, uint64_t fe, int64_t sb,
-                              uint64_t *prof = nullptr) {
-  const int lane = lane_id();
-  const uint8_t *stg = (const uint8_t *)S.stage;
-  const uint64_t src = ms - d;
-  const uint32_t cl = min(n, d);
-  bool pending = n > 0;
-  // the short-match path: source and destination contiguous in one buffer each
-  const bool in_stage = src + n <= fe, in_ring = src >= fe && (src & XRMASK) + n <= XRING;
-  const bool dst_ok = (ms & XRMASK) + n <= XRING;
-  // period < 16 overlapping its own output: stores of the period repeated (see below)
-  const bool splat = n <= 512 && d < n && d < 16 && dst_ok &&
-                     (src + d <= fe || (src >= fe && (src & XRMASK) + d <= XRING));
-  const bool fast = splat || (n > 0 && n <= 512 && d >= n && dst_ok && (in_stage || in_ring));
-  const uint8_t *sp = in_stage ? stg + ((int64_t)src + sb) : &S.ring[src & XRMASK];
-  uint8_t *dp = &S.ring[ms & XRMASK];
-  // exact dependencies: the batch's matches whose destination overlaps the bytes this one reads
-  // from outside itself, [src, src + cl). Match starts ascend with the lane, so the first and last
-  // such match come from two binary searches over the lanes' starts (relative to lane 0's).
-  uint64_t dep = 0;
-  {
-    const uint64_t base0 = rl64(ms, 0);
-    const int32_t rm = (int32_t)(ms - base0), ra = (int32_t)(src - base0), rb = ra + (int32_t)cl - 1;
-    int ja = -1, jb = -1;
-#pragma unroll
-    for (int st = 64; st; st >>= 1) {
-      const int ca = ja + st, cb = jb + st;
-      const int32_t va = __shfl(rm, min(ca, 63), 64), vb = __shfl(rm, min(cb, 63), 64);
-      if (ca <= 63 && va <= ra) ja = ca;
-      if (cb <= 63 && vb <= rb) jb = cb;
-    }
-    const int32_t ea = __shfl(rm + (int32_t)n, max(ja, 0), 64);  // end of the match holding src
-    const int lo = ja < 0 ? 0 : (ea <= ra ? ja + 1 : ja);
-    if (pending && jb >= lo)
-      dep = (jb >= 63 ? ~0ull : ((2ull << jb) - 1)) & ~((1ull << lo) - 1);
-  }
-  uint32_t rounds = 0;
-  uint64_t pm;
-  while (true) {
-#ifdef ZG_PROFILE
-    const uint64_t cr = clock64();
-#endif
-    if ((pm = __ballot(pending)) == 0) break;
-    const bool ready = pending && !(pm & dep);
-#ifdef ZG_PROFILE
-    const uint64_t c0 = clock64();
-#endif
-    uint32_t L = 16, te = 0;
-    zv4u pat = zv4u{0, 0, 0, 0};
-    if (ready && splat) {
-      // period d < 16: P = the first 16 bytes of the periodic extension (the period doubled until
-      // it fills 16 bytes). With L = d * floor(16 / d), byte j of every 16-byte store at a multiple
-      // of L is byte j of P -- the bytes past L included, so consecutive stores overlap with equal
-      // values. The last < 16 bytes, from the next multiple of L, are P's first bytes, stored 8/4/2/1.
-      const uint8_t *pp = src + d <= fe ? stg + ((int64_t)src + sb) : &S.ring[src & XRMASK];
-      const zv4u v = ld16(pp);  // bytes past the period are garbage, masked off
-      unsigned __int128 P = ((unsigned __int128)(((uint64_t)v[3] << 32) | v[2]) << 64) | (((uint64_t)v[1] << 32) | v[0]);
-      P &= (((unsigned __int128)1) << (8 * d)) - 1;
-      for (uint32_t len = d; len < 16; len *= 2) P |= P << (8 * len);
-      const uint64_t p0 = (uint64_t)P, p1 = (uint64_t)(P >> 64);
-      const zv4u pv = zv4u{(uint32_t)p0, (uint32_t)(p0 >> 32), (uint32_t)p1, (uint32_t)(p1 >> 32)};
-      L = d * (16 / d);
-      pat = pv;
-      // te: the first multiple of L with te + 16 > n; this lane stores below XPL, the wave the rest
-      if (n >= 16) {
-        uint32_t q = (uint32_t)((float)(n - 16) * __builtin_amdgcn_rcpf((float)L));
-        if ((q + 1) * L + 16 <= n) q++;
-        if (q * L + 16 > n) q--;
-        te = (q + 1) * L;
-      }
-      for (uint32_t u = 0; u < min(te, XPL); u += L) st16(dp + u, pv);
-      const uint32_t t = te;
-      const uint32_t r = n - t;  // < 16, phase 0
-      uint32_t o = 0;
-      if (r & 8) { __builtin_memcpy(dp + t, &p0, 8); o = 8; }
-      const unsigned __int128 Q = P >> (8 * o);
-      const uint64_t q0 = (uint64_t)Q;
-      if (r & 4) { const uint32_t w = (uint32_t)q0; __builtin_memcpy(dp + t + o, &w, 4); }
-      const uint64_t q1 = (r & 4) ? q0 >> 32 : q0;
-      const uint32_t o2 = o + (r & 4);
-      if (r & 2) { const uint16_t w = (uint16_t)q1; __builtin_memcpy(dp + t + o2, &w, 2); }
-      const uint64_t q2 = (r & 2) ? q1 >> 16 : q1;
-      if (r & 1) dp[t + o2 + (r & 2)] = (uint8_t)q2;
-    } else if (ready && fast) {
-      if (n >= 16) {
-        // groups of up to 8 pieces: all loads of a group, then its stores; a piece never starts
-        // after n - 16 (the last one rewrites its neighbour's bytes with the same values)
-        const uint32_t lim = n - 16;
-        for (uint32_t g0 = 0; g0 < min(n, XPL); g0 += 128) {  // bytes from XPL on: the whole wave, below
-          const uint32_t np = min((min(n, XPL) - g0 + 15) >> 4, 8u);
-          zv4u v0, v1, v2, v3, v4, v5, v6, v7;
-          v0 = ld16(sp + min(g0, lim));
-          if (np > 1) v1 = ld16(sp + min(g0 + 16, lim));
-          if (np > 2) v2 = ld16(sp + min(g0 + 32, lim));
-          if (np > 3) v3 = ld16(sp + min(g0 + 48, lim));
-          if (np > 4) v4 = ld16(sp + min(g0 + 64, lim));
-          if (np > 5) v5 = ld16(sp + min(g0 + 80, lim));
-          if (np > 6) v6 = ld16(sp + min(g0 + 96, lim));
-          if (np > 7) v7 = ld16(sp + min(g0 + 112, lim));
-          st16(dp + min(g0, lim), v0);
-          if (np > 1) st16(dp + min(g0 + 16, lim), v1);
-          if (np > 2) st16(dp + min(g0 + 32, lim), v2);
-          if (np > 3) st16(dp + min(g0 + 48, lim), v3);
-          if (np > 4) st16(dp + min(g0 + 64, lim), v4);
-          if (np > 5) st16(dp + min(g0 + 80, lim), v5);
-          if (np > 6) st16(dp + min(g0 + 96, lim), v6);
-          if (np > 7) st16(dp + min(g0 + 112, lim), v7);
-        }
-      } else if (n >= 8) {
-        uint64_t a0, a1;
-        __builtin_memcpy(&a0, sp, 8);
-        __builtin_memcpy(&a1, sp + n - 8, 8);
-        __builtin_memcpy(dp, &a0, 8);
-        __builtin_memcpy(dp + n - 8, &a1, 8);
-      } else if (n >= 4) {
-        uint32_t a0, a1;
-        __builtin_memcpy(&a0, sp, 4);
-        __builtin_memcpy(&a1, sp + n - 4, 4);
-        __builtin_memcpy(dp, &a0, 4);
-        __builtin_memcpy(dp + n - 4, &a1, 4);
-      } else {
-        for (uint32_t j = 0; j < n; j++) dp[j] = sp[j];
-      }
-    }
-    // long matches past their first XPL bytes: the whole wave, one match after another -- a straight
-    // copy as one 16-B piece per lane (the last one ending at the match end), a period as its
-    // pattern stored at the multiples of L from the first one >= XPL up to te
-    {
-      const uint8_t *lb = (const uint8_t *)&S;
-      const uint32_t so = (uint32_t)(sp - lb), dof = (uint32_t)(dp - lb);
-      uint64_t bm = __ballot(ready && ((splat && te > XPL) || (fast && !splat && n > XPL)));
-      // XLI matches per step: their loads issued together, then their stores (the sources of this
-      // round's matches are no destination of a pending match, so the order within a round is free)
-      while (bm) {
-        int idx[XLI];
-        uint32_t c = 0;
-#pragma unroll
-        for (uint32_t u = 0; u < XLI; u++)
-          if (bm) {
-            idx[u] = __builtin_ctzll(bm);
-            bm &= bm - 1;
-            c++;
-          }
-        zv4u v[XLI];
-        uint32_t dk[XLI];
-        bool go[XLI];
-#pragma unroll
-        for (uint32_t u = 0; u < XLI; u++) {
-          go[u] = false;
-          if (u < c) {
-            const int i = idx[u];
-            const uint32_t n_i = U(__builtin_amdgcn_readlane(n, i)), do_i = U(__builtin_amdgcn_readlane(dof, i));
-            const uint32_t te_i = U(__builtin_amdgcn_readlane(te, i));
-            if (te_i) {
-              const uint32_t L_i = U(__builtin_amdgcn_readlane(L, i));
-              const zv4u pv_i = zv4u{U(__builtin_amdgcn_readlane(pat[0], i)), U(__builtin_amdgcn_readlane(pat[1], i)),
-                                     U(__builtin_amdgcn_readlane(pat[2], i)), U(__builtin_amdgcn_readlane(pat[3], i))};
-              const uint32_t t = ((XPL + L_i - 1) / L_i + lane) * L_i;
-              if (t < te_i) st16((uint8_t *)lb + do_i + t, pv_i);
-            } else {
-              const uint32_t so_i = U(__builtin_amdgcn_readlane(so, i));
-              const uint32_t k = min(XPL + 16 * lane, n_i - 16);
-              go[u] = XPL + 16 * lane < n_i;
-              if (go[u]) v[u] = ld16(lb + so_i + k);
-              dk[u] = do_i + k;
-            }
-          }
-        }
-#pragma unroll
-        for (uint32_t u = 0; u < XLI; u++)
-          if (go[u]) st16((uint8_t *)lb + dk[u], v[u]);
-      }
-    }
-    uint64_t sm = __ballot(ready && !fast);
-#ifdef ZG_PROFILE
-    const uint64_t c1 = clock64();
-    if (prof) {
-      prof[0] += c0 - cr;
-      prof[1] += c1 - c0;
-      prof[3] += 1;
-    }
-#endif
-    while (sm) {
-      const int i = __builtin_ctzll(sm);
-      sm &= sm - 1;
-      const uint64_t ms_i = rl64(ms, i), fe_i = rl64(fe, i);
-      const int64_t sb_i = (int64_t)rl64((uint64_t)sb, i);
-      uint32_t d_i = U(__builtin_amdgcn_readlane(d, i));
-      const uint32_t n_i = U(__builtin_amdgcn_readlane(n, i));
-      uint64_t s_i = ms_i - d_i;
-      const uint32_t k0 = 0;
-      const float inv = __builtin_amdgcn_rcpf((float)d_i);
-      for (uint32_t k = k0 + 16 * lane; k < n_i; k += 1024) {
-        const uint32_t kk = (n_i - k < 16 && n_i >= 16) ? n_i - 16 : k;
-        const uint32_t e = min(n_i - kk, 16u);
-        uint32_t r = kk;
-        if (kk >= d_i) {
-          const uint32_t q = (uint32_t)((float)kk * inv);
-          int32_t rr = (int32_t)kk - (int32_t)(q * d_i);
-          while (rr < 0) rr += d_i;
-          while (rr >= (int32_t)d_i) rr -= d_i;
-          r = (uint32_t)rr;
-        }
-        const uint64_t o = ms_i + kk;
-        if (r + e <= d_i) x_run(S, stg, o, s_i + r, e, fe_i, sb_i);
-        else x_gather(S, stg, o, s_i, r, d_i, e, fe_i, sb_i);  // the piece wraps the period
-      }
-      __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
-    }
-#ifdef ZG_PROFILE
-    if (prof) prof[2] += clock64() - c1;
-#endif
-    pending = pending && !ready;
-    __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
-    rounds++;
-  }
-  __syncthreads();
-  return rounds;
-}
-
-// n <= d bytes from ring position spos to ring position dpos = spos + d (the source precedes the
-// destination entirely): bytes up to dpos's 16-B boundary, then aligned 16-B stores, each built from
-// two aligned ring vectors with byte-aligns (the ring size is a multiple of 16: no vector wraps)
-__device__ __forceinline__ void x_ring_copy(ZXSmem &S, uint64_t dpos, uint64_t spos, uint32_t n) {
-  const int lane = lane_id();
-  const uint32_t head = min<uint32_t>(n, (uint32_t)((16 - (dpos & 15)) & 15));
-  if (lane < (int)head) S.ring[(dpos + lane) & XRMASK] = S.ring[(spos + lane) & XRMASK];
-  const uint64_t s1 = spos + head;
-  const uint32_t m = (uint32_t)(s1 & 15), mq = m >> 2, mr = m & 3;
-  const uint32_t nch = (n - head) >> 4;
-  for (uint32_t i = lane; i < nch; i += 64) {
-    const uint64_t sv = (s1 + 16ull * i) & ~(uint64_t)15;
-    const zv4u lo = *(const zv4u *)&S.ring[sv & XRMASK];
-    const zv4u hi = m ? *(const zv4u *)&S.ring[(sv + 16) & XRMASK] : lo;
-    const uint32_t w[8] = {lo.x, lo.y, lo.z, lo.w, hi.x, hi.y, hi.z, hi.w};
-    zv4u v;
-    if (mq == 0) v = zv4u{__builtin_amdgcn_alignbyte(w[1], w[0], mr), __builtin_amdgcn_alignbyte(w[2], w[1], mr),
-                          __builtin_amdgcn_alignbyte(w[3], w[2], mr), __builtin_amdgcn_alignbyte(w[4], w[3], mr)};
-    else if (mq == 1) v = zv4u{__builtin_amdgcn_alignbyte(w[2], w[1], mr), __builtin_amdgcn_alignbyte(w[3], w[2], mr),
-                               __builtin_amdgcn_alignbyte(w[4], w[3], mr), __builtin_amdgcn_alignbyte(w[5], w[4], mr)};
-    else if (mq == 2) v = zv4u{__builtin_amdgcn_alignbyte(w[3], w[2], mr), __builtin_amdgcn_alignbyte(w[4], w[3], mr),
-                               __builtin_amdgcn_alignbyte(w[5], w[4], mr), __builtin_amdgcn_alignbyte(w[6], w[5], mr)};
-    else v = zv4u{__builtin_amdgcn_alignbyte(w[4], w[3], mr), __builtin_amdgcn_alignbyte(w[5], w[4], mr),
-                  __builtin_amdgcn_alignbyte(w[6], w[5], mr), __builtin_amdgcn_alignbyte(w[7], w[6], mr)};
-    *(zv4u *)&S.ring[(dpos + head + 16ull * i) & XRMASK] = v;
-  }
-  const uint32_t t0 = head + 16 * nch, tail = n - t0;
-  if (lane < (int)tail) S.ring[(dpos + t0 + lane) & XRMASK] = S.ring[(spos + t0 + lane) & XRMASK];
-  __syncthreads();
-}
-
-// One long match (or one whose far part does not fit a batch); false if corrupt. Periods 1/2/4/8 are
-// pattern stores; other distances copy chunks whose source lies wholly before them: from the ring
-// (x_ring_copy) or, below the far bound, from the flushed output (x_copy).
-__device__ __forceinline__ bool x_long_match(ZXSmem &S, XOut &O, uint64_t fstart, uint32_t off, uint64_t ml, uint64_t bend) {
-  const int lane = lane_id();
-  const uint64_t p = O.pos;
-  if (off == 0 || off > p - fstart || p + ml > bend) return false;
-  if (off == 1 || off == 2 || off == 4 || off == 8) {
-    uint64_t pat = 0;
-    for (uint32_t j = 0; j < off; j++) {  // the period: from the slot where the ring holds nothing
-      const uint64_t q = p - off + j;
-      pat |= (uint64_t)(q >= O.rv ? S.ring[q & XRMASK] : O.out[q]) << (8 * j);
-    }
-    if (off == 1) pat *= 0x0101010101010101ull;
-    else if (off == 2) pat *= 0x0001000100010001ull;
-    else if (off == 4) pat |= pat << 32;
-    for (uint64_t c0 = 0; c0 < ml;) {
-      const uint32_t c = (uint32_t)min<uint64_t>(ZBATCH, ml - c0);
-      x_reserve(S, O, O.pos + c);
-      // byte k of the match is pat byte (k mod 8)
-      const uint32_t head = min<uint32_t>(c, (uint32_t)((16 - (O.pos & 15)) & 15));
-      if (lane < (int)head) S.ring[(O.pos + lane) & XRMASK] = (uint8_t)(pat >> (8 * ((c0 + lane) & 7)));
-      const uint32_t sh = 8 * ((c0 + head) & 7);
-      const uint64_t rp = sh ? (pat >> sh) | (pat << (64 - sh)) : pat;
-      const zv4u v = zv4u{(uint32_t)rp, (uint32_t)(rp >> 32), (uint32_t)rp, (uint32_t)(rp >> 32)};
-      const uint32_t nch = (c - head) >> 4;
-      for (uint32_t i = lane; i < nch; i += 64) *(zv4u *)&S.ring[(O.pos + head + 16ull * i) & XRMASK] = v;
-      const uint32_t t0 = head + 16 * nch, tail = c - t0;
-      if (lane < (int)tail) S.ring[(O.pos + t0 + lane) & XRMASK] = (uint8_t)(pat >> (8 * ((c0 + t0 + lane) & 7)));
-      __syncthreads();
-      O.pos += c;
-      c0 += c;
-    }
-    return true;
-  }
-  for (uint64_t c0 = 0; c0 < ml;) {
-    // copy from D bytes back, D the largest multiple of the distance not beyond the match start:
-    // the chunk's source is then contiguous, wholly before the chunk and final (chunks double
-    // until ZBATCH for short distances)
-    const uint64_t D = (uint64_t)off * ((c0 + off) / off);
-    const uint32_t c = (uint32_t)min<uint64_t>(min<uint64_t>(ZBATCH, ml - c0), D);
-    const uint64_t src = p + c0 - D;
-    x_reserve(S, O, p + c0 + c);
-    const uint64_t fb = x_far_bound(O, p + c0 + c);
-    if (src >= fb) {
-      x_ring_copy(S, p + c0, src, c);
-      O.pos = p + c0 + c;
-    } else if (src + c <= fb) {
-      x_copy(S, O, O.out + src, c);  // flushed, whole 128-B lines: no stale L1 line (x_far_bound)
-    } else {
-      const uint32_t c1 = (uint32_t)(fb - src);
-      x_copy(S, O, O.out + src, c1);
-      x_ring_copy(S, p + c0 + c1, src + c1, c - c1);
-      O.pos = p + c0 + c;
-    }
-    c0 += c;
-  }
-  return true;
-}
-
-}  // namespace
 
 
 __global__ __launch_bounds__(256) void k_zstd_direct(const ZgItem *items, const uint32_t *status, const ZBlk *blks,
@@ -3906,227 +3314,65 @@ __global__ __launch_bounds__(256) void k_zstd_direct(const ZgItem *items, const 
   }
 }
 
-__global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(ZG_XWPE, 8))) void k_zstd_exec_item(ZgItem *items, uint32_t *status, const ZBlk *blks,
-                                                       uint32_t blk_cap, const uint32_t *nblk, const uint32_t *zmode,
-                                                       uint8_t *dst, uint64_t slot_bytes, const uint8_t *lit_scratch,
-                                                       uint64_t lit_stride, const uint32_t *seq_scratch,
-                                                       uint64_t seq_cap, uint32_t xseg) {
-  __shared__ ZXSmem S;
-  const uint32_t item = blockIdx.x / xseg, sg = blockIdx.x % xseg;
-  const int lane = lane_id();
-  ZP_DECL;
-  ZP_T(t_all);
-  if (zmode[item] != ZMODE_PARALLEL || status[item]) return;
-  uint8_t *out = dst + (uint64_t)item * slot_bytes;
-  const ZBlk *B = blks + (uint64_t)item * blk_cap;
-  const uint32_t nb = nblk[item];
-  if (!nb) {  // no blocks: an empty output
-    if (sg == 0 && lane == 0) {
-      items[item].src = (uint64_t)out;
-      items[item].len = 0;
-    }
-    return;
-  }
-  // the input pointer from the plan's copy: the item record is rewritten by the last segment
-  const uint8_t *in = (const uint8_t *)U64(B[0].in_src);
-  // this wave's segment: blocks [b0, b1) between the sg-th and the next segment start (k_zstd_plan)
-  uint32_t b0 = nb, b1 = nb, count = 0;
-  for (uint32_t base = 0; base < nb && count <= sg + 1; base += 64) {
-    uint64_t m = __ballot(base + lane < nb && B[base + lane].seg);
-    while (m && count <= sg + 1) {
-      const uint32_t i = __builtin_ctzll(m);
-      m &= m - 1;
-      if (count == sg) b0 = base + i;
-      else if (count == sg + 1) b1 = base + i;
-      count++;
-    }
-  }
-  if (b0 >= nb) return;  // fewer segments
-  const uint64_t p0 = U(B[b0].out_off);
-  XOut O{out, p0, p0, p0};
-  uint32_t err = 0;
-  uint64_t fstart = U(B[b0].frame_off);
-  for (uint32_t bi = b0; bi < b1 && !err; bi++) {
-    const uint32_t flags = U(B[bi].flags), type = flags & 3;
-    const uint64_t bstart = U(B[bi].out_off);
-    const uint32_t bsize = U(B[bi].out_size);
-    if (flags & ZBF_FIRST) fstart = bstart;
-    if (bstart != O.pos) { err = ZG_CORRUPT_STREAM; break; }
-    const uint64_t bend = bstart + bsize;
-    ZP_T(t5);
-    if (x_direct_block(flags, U(B[bi].nseq), bsize)) {
-      // written by k_zstd_direct: everything before it to the slot, then the ring restarts at the
-      // block's last 128-B line boundary (sources below it are staged from the slot)
-      if (type == ZB_CMP && U(B[bi].regen) != bsize) { err = ZG_CORRUPT_STREAM; break; }
-      x_flush(S, O);
-      const uint64_t a = bend & ~(uint64_t)127;
-      for (uint64_t p = a + lane; p < bend; p += 64) S.ring[p & XRMASK] = out[p];
-      O.pos = O.flushed = bend;
-      O.rv = a;
-      __syncthreads();
-      ZP_ADD(5, t5);
-    } else if (type == ZB_RAW) {
-      x_copy(S, O, in + U(B[bi].in_off), bsize);
-      ZP_ADD(5, t5);
-    } else if (type == ZB_RLE) {
-      x_fill(S, O, (uint8_t)U(in[U(B[bi].in_off)]), bsize);
-      ZP_ADD(5, t5);
-    } else {
-      const uint32_t ltype = (flags >> 2) & 3, regen = U(B[bi].regen), nseq = U(B[bi].nseq);
-      const uint8_t *lsrc =
-          ltype == 0 ? in + U(B[bi].lit_off) : lit_scratch + (uint64_t)item * lit_stride + U(B[bi].lit_buf);
-      const uint32_t *seqs = seq_scratch + ((uint64_t)item * seq_cap + U(B[bi].seq_buf)) * 3;
-      const uint32_t ri0 = U(B[bi].rep_in[0]), ri1 = U(B[bi].rep_in[1]), ri2 = U(B[bi].rep_in[2]);
-      uint64_t litpos = 0;
-      uint32_t base = 0;
-      // the next batch's sequences are loaded while this batch executes
-      uint32_t nx_base = 0xFFFFFFFFu, nx_ll = 0, nx_ml = 0, nx_of = 0;
-      while (base < nseq && !err) {
-        ZP_T(th);
-        const uint32_t avail = min<uint32_t>(64, nseq - base);
-        const bool have = lane < (int)avail;
-        uint32_t r_ll = 0, r_ml = 0, r_of = 1;
-        if (nx_base == base) {
-          if (have) {
-            r_ll = nx_ll;
-            r_ml = nx_ml;
-            r_of = sym_eval(nx_of, ri0, ri1, ri2);
-          }
-        } else if (have) {
-          const uint32_t *q = seqs + (uint64_t)(base + lane) * 3;
-          r_ll = q[0];
-          r_ml = q[1];
-          r_of = sym_eval(q[2], ri0, ri1, ri2);
-        }
-        uint32_t a = r_ll, b = r_ll + r_ml;  // inclusive prefix sums (literals, output)
-        for (int o = 1; o < 64; o <<= 1) {
-          const uint32_t ta = __shfl_up(a, o, 64), tb = __shfl_up(b, o, 64);
-          if (lane >= o) { a += ta; b += tb; }
-        }
-        const uint64_t bigm = __ballot(have && (r_ll >= ZBIG || r_ml >= ZBIG));
-        const uint32_t fit = __builtin_popcountll(__ballot(have && b <= ZBATCH));
-        uint32_t cnt = min<uint32_t>(fit, bigm ? (uint32_t)__builtin_ctzll(bigm) : 64u);
-        const uint64_t out_base = O.pos;
-        bool staged = false;
-        uint64_t fe = 0;
-        int64_t sb = 0;
-        uint32_t span = 0, lspan = 0;
-        bool mine = false;
-        uint64_t mstart = 0;
-        uint32_t sml = 0;
-        if (cnt) {
-          span = U(__builtin_amdgcn_readlane(b, cnt - 1));
-          lspan = U(__builtin_amdgcn_readlane(a, cnt - 1));
-          if (out_base + span > bend || litpos + lspan > regen) { err = ZG_CORRUPT_STREAM; break; }
-          mine = lane < (int)cnt;
-          sml = mine ? r_ml : 0u;
-          mstart = out_base + b - sml;
-          if (__ballot(mine && sml && (r_of == 0 || (uint64_t)r_of > mstart - fstart))) {
-            err = ZG_CORRUPT_STREAM;
-            break;
-          }
-          ZP_T(ts);
-          x_reserve(S, O, out_base + span);
-          const uint64_t fb = x_far_bound(O, out_base + span);
-          staged = x_stage(S, O.out, fb, mstart, r_of, sml, lsrc + litpos, lspan, fe, sb);
-#ifdef ZG_PROFILE
-          zp_acc[12] += __ballot(mine && sml && fe > mstart - r_of) != 0;
+// -------------------------------------------------------------------------------------------------
+// k_zstd_exec_item (kernels/zstd_exec.inc) in two configurations, chosen per launch by launch_zstd:
+//   xwide  - 8 KiB ring, 4 KiB batches, 256 staged far vectors, 2 waves/SIMD (18.2 KiB LDS, 256
+//            VGPRs): fastest per wave; a grid of few waves per CU (C5-like batches of 16 MiB frames)
+//   xdense - 4 KiB ring, 2 KiB batches, 128 staged vectors, 4 waves/SIMD (9.9 KiB LDS, 128 VGPRs):
+//            twice the resident waves, for grids of many small frames (blosc's 256 KiB blocks)
+// -------------------------------------------------------------------------------------------------
+#ifndef ZG_XBATCH
+#define ZG_XBATCH 4096
 #endif
-          ZP_ADD(1, ts);
-        }
-#ifdef ZG_PROFILE
-        zp_acc[7] += 1;
+constexpr uint32_t XBATCH = ZG_XBATCH;  // max output span of one executor batch (ZBATCH: the serial decoder's)
+#ifndef ZG_XRING
+#define ZG_XRING 8192
 #endif
-        nx_base = base + (staged ? cnt : 1u);
-        if (nx_base < nseq && lane < (int)(nseq - nx_base)) {
-          const uint32_t *q = seqs + (uint64_t)(nx_base + lane) * 3;
-          nx_ll = q[0];
-          nx_ml = q[1];
-          nx_of = q[2];
-        }
-        if (!staged) {  // one sequence alone: its literal run, then its match in chunks
-          ZP_T(t4);
-          const uint32_t ll = U(__builtin_amdgcn_readlane(r_ll, 0)), ml = U(__builtin_amdgcn_readlane(r_ml, 0));
-          const uint32_t of = U(__builtin_amdgcn_readlane(r_of, 0));
-          if (litpos + ll > regen || O.pos + ll + ml > bend) { err = ZG_CORRUPT_STREAM; break; }
-          x_copy(S, O, lsrc + litpos, ll);
-          litpos += ll;
-          ZP_ADD(0, t4);
-          ZP_T(t4m);
-          if (ml && !x_long_match(S, O, fstart, of, ml, bend)) { err = ZG_CORRUPT_STREAM; break; }
-          ZP_ADD(2, t4m);
-#ifdef ZG_PROFILE
-          if (of < 16) zp_acc[7] += 1ull << 32;
+constexpr uint32_t XRING = ZG_XRING, XRMASK = XRING - 1;
+static_assert((XRING & XRMASK) == 0 && XRING >= 2 * XBATCH, "exec ring: a power of two holding two batches");
+#ifndef ZG_XSTAGE_V
+#define ZG_XSTAGE_V 256
 #endif
-          base += 1;
-          ZP_ADD(4, t4);
-          continue;
-        }
-        // literals of the batch into place: every lane moves its own run, 16 bytes at a time (loads
-        // of a group of four before its stores), bytes where the run wraps the ring
-        ZP_T(tl2);
-        if (mine && r_ll) {
-          const uint32_t ll = r_ll, o = (uint32_t)out_base + b - r_ml - ll;
-          const uint8_t *ls = S.lit_stage + (((uintptr_t)(lsrc + litpos)) & 15) + (a - ll);
-          if (ll >= 16 && (o & XRMASK) + ll <= XRING) {
-            uint8_t *dq = &S.ring[o & XRMASK];
-            for (uint32_t k0 = 0; k0 < ll; k0 += 64) {
-              const uint32_t lim = ll - 16;
-              const zv4u v0 = ld16(ls + min(k0, lim));
-              zv4u v1, v2, v3;
-              if (k0 + 16 < ll) v1 = ld16(ls + min(k0 + 16, lim));
-              if (k0 + 32 < ll) v2 = ld16(ls + min(k0 + 32, lim));
-              if (k0 + 48 < ll) v3 = ld16(ls + min(k0 + 48, lim));
-              st16(dq + min(k0, lim), v0);
-              if (k0 + 16 < ll) st16(dq + min(k0 + 16, lim), v1);
-              if (k0 + 32 < ll) st16(dq + min(k0 + 32, lim), v2);
-              if (k0 + 48 < ll) st16(dq + min(k0 + 48, lim), v3);
-            }
-          } else {
-            for (uint32_t k = 0; k < ll; k++) S.ring[(o + k) & XRMASK] = ls[k];
-          }
-        }
-        __syncthreads();
-        ZP_T(t3);
-#ifdef ZG_PROFILE
-        const uint32_t nr = x_resolve(S, mstart, r_of, sml, fe, sb, zp_acc + 8);
-#else
-        const uint32_t nr = x_resolve(S, mstart, r_of, sml, fe, sb);
+constexpr uint32_t XSTAGE_V = ZG_XSTAGE_V;  // staged far-source vectors (16 B) per batch
+#ifndef ZG_XWPE
+#define ZG_XWPE 2  // the executor is compiled for >= 2 waves/SIMD (VGPR + AGPR <= 256)
 #endif
-        ZP_ADD(3, t3);
-        (void)nr;
-        O.pos = out_base + span;
-        litpos += lspan;
-        base += cnt;
-      }
-      if (!err) {
-        ZP_T(t5b);
-        if (litpos > regen || O.pos + (regen - litpos) != bend) err = ZG_CORRUPT_STREAM;
-        else x_copy(S, O, lsrc + litpos, regen - litpos);
-        ZP_ADD(5, t5b);
-      }
-    }
-    if (!err && O.pos != bend) err = ZG_CORRUPT_STREAM;
-    if (!err && (flags & ZBF_LAST) && (flags & ZBF_CK)) {
-      x_flush(S, O);
-      __builtin_amdgcn_s_waitcnt(0);
-      __threadfence();
-      const uint64_t h = xxh64(out + fstart, O.pos - fstart);
-      if ((uint32_t)h != U(B[bi].ck)) err = ZG_CORRUPT_STREAM;
-    }
-  }
-  if (!err) x_flush(S, O);
-  ZP_ADD(6, t_all);
-  ZP_FLUSH;
-  if (lane == 0) {
-    if (err) {
-      status[item] = err;
-    } else if (b1 == nb) {  // the last segment
-      items[item].src = (uint64_t)out;
-      items[item].len = O.pos;
-    }
-  }
-}
+#ifndef ZG_XPL
+#define ZG_XPL 64
+#endif
+constexpr uint32_t XPL = ZG_XPL;  // bytes of a short match its own lane copies (the rest: the wave)
+static_assert(XPL % 16 == 0 && XPL >= 16 && XPL <= 512, "XPL: 16-B pieces, at most a short match");
+#ifndef ZG_XLI
+#define ZG_XLI 1
+#endif
+constexpr uint32_t XLI = ZG_XLI;  // long matches the wave copies per step (their loads together)
+namespace xwide {
+#define ZX_BATCH ZG_XBATCH
+#define ZX_RING ZG_XRING
+#define ZX_STAGE_V ZG_XSTAGE_V
+#define ZX_WPE ZG_XWPE
+#include "zstd_exec.inc"
+#undef ZX_BATCH
+#undef ZX_RING
+#undef ZX_STAGE_V
+#undef ZX_WPE
+}  // namespace xwide
+namespace xdense {
+#define ZX_BATCH 2048
+#define ZX_RING 4096
+#define ZX_STAGE_V 128
+#define ZX_WPE 4
+#include "zstd_exec.inc"
+#undef ZX_BATCH
+#undef ZX_RING
+#undef ZX_STAGE_V
+#undef ZX_WPE
+}  // namespace xdense
+// executor grids of at least this many waves (items x segments) per CU take xdense
+#ifndef ZG_XDENSE_WPC
+#define ZG_XDENSE_WPC 64
+#endif
+constexpr uint32_t XDENSE_WAVES_PER_CU = ZG_XDENSE_WPC;
 
 uint64_t zstd_lit_rec_bytes(uint32_t &wgs) {
   static const uint64_t cap = [] {
@@ -4211,8 +3457,19 @@ hipError_t launch_zstd(ZgItem *items, uint32_t *status, uint32_t n_items, uint8_
                      slot_bytes, xseg, Z.alias, Z.lit, Z.lit_stride);
   hipLaunchKernelGGL(k_zstd_direct, dim3(grid), dim3(256), 0, s, items, status, blks, Z.blk_cap, Z.nblk, Z.mode,
                      n_items, dst, slot_bytes, Z.lit, Z.lit_stride, Z.alias);
-  hipLaunchKernelGGL(k_zstd_exec_item, dim3(n_items * xseg), dim3(64), 0, s, items, status, blks, Z.blk_cap, Z.nblk,
-                     Z.mode, dst, slot_bytes, Z.lit, Z.lit_stride, Z.seq, Z.seq_cap, xseg);
+  // executor configuration: xdense when the grid has many waves per CU (ZGPU_ZSTD_XDENSE=0/1 forces one)
+  static const int xd_env = [] {
+    const char *e = std::getenv("ZGPU_ZSTD_XDENSE");
+    return e ? std::atoi(e) : -1;
+  }();
+  const bool dense = xd_env >= 0 ? xd_env != 0
+                                 : (uint64_t)n_items * xseg >= (uint64_t)device_cu_count() * XDENSE_WAVES_PER_CU;
+  if (dense)
+    hipLaunchKernelGGL(xdense::k_zstd_exec_item, dim3(n_items * xseg), dim3(64), 0, s, items, status, blks, Z.blk_cap,
+                       Z.nblk, Z.mode, dst, slot_bytes, Z.lit, Z.lit_stride, Z.seq, Z.seq_cap, xseg);
+  else
+    hipLaunchKernelGGL(xwide::k_zstd_exec_item, dim3(n_items * xseg), dim3(64), 0, s, items, status, blks, Z.blk_cap,
+                       Z.nblk, Z.mode, dst, slot_bytes, Z.lit, Z.lit_stride, Z.seq, Z.seq_cap, xseg);
   if (!listed) {
     hipLaunchKernelGGL(k_zstd, dim3(n_items), dim3(64), 0, s, items, status, dst, slot_bytes, Z.lit, Z.lit_stride,
                        Z.mode, nullptr, nullptr);
