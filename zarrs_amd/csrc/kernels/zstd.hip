@@ -3357,11 +3357,23 @@ namespace xwide {
 #undef ZX_STAGE_V
 #undef ZX_WPE
 }  // namespace xwide
+#ifndef ZG_XD_BATCH
+#define ZG_XD_BATCH 2048
+#endif
+#ifndef ZG_XD_RING
+#define ZG_XD_RING 4096
+#endif
+#ifndef ZG_XD_STAGE_V
+#define ZG_XD_STAGE_V 128
+#endif
+#ifndef ZG_XD_WPE
+#define ZG_XD_WPE 4
+#endif
 namespace xdense {
-#define ZX_BATCH 2048
-#define ZX_RING 4096
-#define ZX_STAGE_V 128
-#define ZX_WPE 4
+#define ZX_BATCH ZG_XD_BATCH
+#define ZX_RING ZG_XD_RING
+#define ZX_STAGE_V ZG_XD_STAGE_V
+#define ZX_WPE ZG_XD_WPE
 #include "zstd_exec.inc"
 #undef ZX_BATCH
 #undef ZX_RING
