@@ -601,3 +601,49 @@ def test_blosc_zstd_block_aliases_vs_oracle(ctx, torch_cuda):
     assert ("shuffle", 0, None) in kinds and ("shuffle", 1, None) in kinds, kinds  # raw and rle planes
     assert ("shuffle", 2, 0) in kinds, kinds  # literal-only
     assert ("noshuffle", 0, None) in kinds, kinds
+
+
+@pytest.mark.parametrize("knobs", [{"ZGPU_ZSTD_SPLIT_MIN": "1"}, {"ZGPU_ZSTD_XDENSE": "1"}, {"ZGPU_ZSTD_XDENSE": "0"},
+                                   {"ZGPU_BLOSC_ALIAS": "0"}, {"ZGPU_ZSTD_SPLIT_MIN": "1", "ZGPU_ZSTD_XDENSE": "1"}],
+                         ids=["split", "xdense", "xwide", "noalias", "split-xdense"])
+def test_blosc_zstd_pipeline_knobs_vs_oracle(ctx, torch_cuda, knobs):
+    """The zstd pipeline's run-time choices change no byte: two pipelined halves on a second stream
+    (forced for small batches by ZGPU_ZSTD_SPLIT_MIN), either executor configuration, and slot copies
+    instead of block aliases. A batch of shuffled u16 chunks (several blosc blocks each: raw, rle,
+    literal-only and sequence blocks) plus a corrupt one, vs the c-blosc oracle."""
+    import os
+    from zarrs_amd import CodecChain, make_desc
+    rng = np.random.default_rng(91)
+    n = 3 << 17  # three 256 KiB blosc blocks per chunk
+    codecs = [{"name": "bytes", "configuration": {"endian": "little"}}, _blosc("zstd", "shuffle", 2, 0, 5)]
+    co = O.OracleChain.from_metadata(codecs, "uint16", 0, 1)
+    x = np.arange(n)
+    chunks = [rng.integers(0, 256, n).astype(np.uint16),
+              (100 + 900 * np.abs(np.sin(x * 0.001)) + rng.standard_normal(n) * 8).astype(np.uint16),
+              (rng.integers(0, 256, n) % 180).astype(np.uint16),
+              np.tile(rng.integers(0, 65536, n // 3, dtype=np.uint16), 3),
+              (x // 700 % 9).astype(np.uint16)]
+    encs = [bytes(co.encode(a)) for a in chunks]
+    bad = bytearray(encs[1])
+    b1 = int.from_bytes(bad[20:24], "little")  # blosc block 1: 4-byte size, then its zstd frame
+    bad[b1 + 4] ^= 0x5A  # the frame's magic number
+    encs.append(bytes(bad))
+    saved = {k: os.environ.get(k) for k in knobs}
+    os.environ.update(knobs)
+    try:
+        ch = CodecChain.from_metadata(codecs, "uint16", 0, ctx)
+        descs, keep = [], []
+        for k, e in enumerate(encs):
+            d = torch_cuda.frombuffer(bytearray(e), dtype=torch_cuda.uint8).cuda()
+            keep.append(d)
+            descs.append(make_desc(d, [n], out_start=[k * n]))
+        out = np.zeros(len(encs) * n, np.uint16)
+        st = ch.decode_batch(descs, out, [len(encs) * n], enc_device=True)
+    finally:
+        for k, v in saved.items():
+            if v is None:
+                os.environ.pop(k, None)
+            else:
+                os.environ[k] = v
+    assert st[:5] == [0] * 5 and st[5] != 0, st
+    assert out[:5 * n].tobytes() == np.concatenate(chunks).tobytes()

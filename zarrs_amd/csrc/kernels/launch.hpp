@@ -120,6 +120,12 @@ struct ZstdScratch {
   // k_zstd_direct does not copy it into the slot: item bytes [off, off + len) are src[0 .. len).
   // len = 0: none. Byte-shuffled blosc blocks of noisy data: the low-byte plane is a raw block.
   uint64_t *alias = nullptr;
+  // Two halves (nullable s2: one pass): the second half of the items runs on stream s2, its entropy
+  // kernels after the first half's (ev_half), beside the first half's executor; the caller's stream
+  // waits for ev_done. Both halves share the side stream and the literal record slots (their literal
+  // kernels never overlap).
+  hipStream_t s2 = nullptr;
+  hipEvent_t ev_half = nullptr, ev_done = nullptr;
 };
 constexpr uint32_t ZALIAS = 2;
 constexpr uint64_t ZALIAS_RLE = 1ull << 63;

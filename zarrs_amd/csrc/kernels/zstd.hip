@@ -3385,6 +3385,8 @@ namespace xdense {
 #define ZG_XDENSE_WPC 64
 #endif
 constexpr uint32_t XDENSE_WAVES_PER_CU = ZG_XDENSE_WPC;
+// launch_zstd splits a batch into two pipelined halves (ZstdScratch::s2) from 2 x this many items
+constexpr uint32_t ZSPLIT_MIN = 1024;
 
 uint64_t zstd_lit_rec_bytes(uint32_t &wgs) {
   static const uint64_t cap = [] {
@@ -3408,8 +3410,10 @@ void zstd_scratch_layout(uint64_t slot_bytes, uint32_t &blk_cap, uint64_t &blk_b
   lit_stride = (lit_stride + 255) & ~(uint64_t)255;
   seq_cap = slot_bytes / 4 + 1024;  // sequences per item (each decodes >= 3 bytes; typical >= 8)
 }
-hipError_t launch_zstd(ZgItem *items, uint32_t *status, uint32_t n_items, uint8_t *dst, uint64_t slot_bytes,
-                       const ZstdScratch &Z, hipStream_t s) {
+// One pass of the block-parallel pipeline over n_items items on stream s; ev_entropy (nullable) is
+// recorded on s once the entropy kernels (and the side stream's sequence decode) are done.
+static hipError_t launch_zstd_pass(ZgItem *items, uint32_t *status, uint32_t n_items, uint8_t *dst,
+                                   uint64_t slot_bytes, const ZstdScratch &Z, hipStream_t s, hipEvent_t ev_entropy) {
   if (!n_items) return hipSuccess;
   ZBlk *blks = (ZBlk *)Z.blks;
   const bool listed = Z.ser_list && Z.ser_count;
@@ -3459,6 +3463,10 @@ hipError_t launch_zstd(ZgItem *items, uint32_t *status, uint32_t n_items, uint8_
     hipError_t e = hipStreamWaitEvent(s, Z.ev_join, 0);
     if (e != hipSuccess) return e;
   }
+  if (ev_entropy) {
+    hipError_t e = hipEventRecord(ev_entropy, s);
+    if (e != hipSuccess) return e;
+  }
   // executor segments per item: ZG_XSEG (ZGPU_ZSTD_XSEG: tuning)
   static const uint32_t xseg_env = [] {
     const char *e = std::getenv("ZGPU_ZSTD_XSEG");
@@ -3470,10 +3478,8 @@ hipError_t launch_zstd(ZgItem *items, uint32_t *status, uint32_t n_items, uint8_
   hipLaunchKernelGGL(k_zstd_direct, dim3(grid), dim3(256), 0, s, items, status, blks, Z.blk_cap, Z.nblk, Z.mode,
                      n_items, dst, slot_bytes, Z.lit, Z.lit_stride, Z.alias);
   // executor configuration: xdense when the grid has many waves per CU (ZGPU_ZSTD_XDENSE=0/1 forces one)
-  static const int xd_env = [] {
-    const char *e = std::getenv("ZGPU_ZSTD_XDENSE");
-    return e ? std::atoi(e) : -1;
-  }();
+  const char *xd_s = std::getenv("ZGPU_ZSTD_XDENSE");  // read per call (tests force both)
+  const int xd_env = xd_s ? std::atoi(xd_s) : -1;
   const bool dense = xd_env >= 0 ? xd_env != 0
                                  : (uint64_t)n_items * xseg >= (uint64_t)device_cu_count() * XDENSE_WAVES_PER_CU;
   if (dense)
@@ -3492,6 +3498,38 @@ hipError_t launch_zstd(ZgItem *items, uint32_t *status, uint32_t n_items, uint8_
                        Z.mode, Z.ser_list, Z.ser_count);
   }
   return hipGetLastError();
+}
+
+hipError_t launch_zstd(ZgItem *items, uint32_t *status, uint32_t n_items, uint8_t *dst, uint64_t slot_bytes,
+                       const ZstdScratch &Z, hipStream_t s) {
+  // read per call (tests switch these knobs between calls): ZGPU_ZSTD_SPLIT_MIN splits small batches
+  const char *sm = std::getenv("ZGPU_ZSTD_SPLIT_MIN");
+  const uint32_t split_min = sm ? (uint32_t)std::max<unsigned long>(1, std::strtoul(sm, nullptr, 10)) : ZSPLIT_MIN;
+  if (!Z.s2 || !Z.ev_half || !Z.ev_done || n_items < 2 * split_min)
+    return launch_zstd_pass(items, status, n_items, dst, slot_bytes, Z, s, nullptr);
+  // Two halves (ZstdScratch::s2): the second half's entropy kernels start once the first half's are
+  // done, so they run beside the first half's executor; the caller's stream joins the second half.
+  const uint32_t h = n_items / 2;
+  ZstdScratch A = Z;
+  A.s2 = nullptr;
+  hipError_t e = launch_zstd_pass(items, status, h, dst, slot_bytes, A, s, Z.ev_half);
+  if (e != hipSuccess) return e;
+  ZstdScratch B = Z;
+  B.s2 = nullptr;
+  B.blks = (uint8_t *)Z.blks + (uint64_t)h * Z.blk_cap * sizeof(ZBlk);
+  B.nblk = Z.nblk + h;
+  B.mode = Z.mode + h;
+  B.lit = Z.lit + (uint64_t)h * Z.lit_stride;
+  B.seq = Z.seq + (uint64_t)h * Z.seq_cap * 3;
+  B.alias = Z.alias ? Z.alias + (uint64_t)h * 3 * ZALIAS : nullptr;
+  B.ser_list = nullptr;  // the second half's serial fallback runs unlisted (one wave per item)
+  B.ser_count = nullptr;
+  if ((e = hipStreamWaitEvent(Z.s2, Z.ev_half, 0)) != hipSuccess) return e;
+  e = launch_zstd_pass(items + h, status + h, n_items - h, dst + (uint64_t)h * slot_bytes, slot_bytes, B, Z.s2,
+                       nullptr);
+  if (e != hipSuccess) return e;
+  if ((e = hipEventRecord(Z.ev_done, Z.s2)) != hipSuccess) return e;
+  return hipStreamWaitEvent(s, Z.ev_done, 0);
 }
 
 }  // namespace zgpu

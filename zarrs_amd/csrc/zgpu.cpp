@@ -283,6 +283,22 @@ struct zgpu_plan {
     Z.ev_fork = zev[0];
     Z.ev_join = zev[1];
   }
+  // zstd in two pipelined halves (ZstdScratch::s2; blosc stream tables of many frames). ZGPU_ZSTD_SPLIT=0: off
+  hipStream_t zs2 = nullptr;
+  hipEvent_t zev2[2] = {nullptr, nullptr};
+  void zstd_split(ZstdScratch &Z, hipStream_t s) {
+    const char *e = std::getenv("ZGPU_ZSTD_SPLIT");  // read per call (tests switch it)
+    if ((e && std::atoi(e) == 0) || !Z.side) return;
+    if (!zs2) {
+      int prio = 0;
+      if (s) (void)hipStreamGetPriority(s, &prio);
+      HIPCHK(hipStreamCreateWithPriority(&zs2, hipStreamNonBlocking, prio));
+      for (hipEvent_t &e : zev2) HIPCHK(hipEventCreateWithFlags(&e, hipEventDisableTiming));
+    }
+    Z.s2 = zs2;
+    Z.ev_half = zev2[0];
+    Z.ev_done = zev2[1];
+  }
   // blosc stage scratch (grown on demand; the stream table is sized from the frame headers)
   struct Grow {
     void *p = nullptr;
@@ -341,6 +357,12 @@ struct zgpu_plan {
       (void)hipStreamSynchronize(zside);
       (void)hipStreamDestroy(zside);
     }
+    if (zs2) {
+      (void)hipStreamSynchronize(zs2);
+      (void)hipStreamDestroy(zs2);
+    }
+    for (hipEvent_t e : zev2)
+      if (e) (void)hipEventDestroy(e);
     for (hipEvent_t e : zev)
       if (e) (void)hipEventDestroy(e);
     for (Grow *g : {&bl_info, &bl_bases, &bl_subs, &bl_sub_status, &bl_sub_kind, &bl_blocks, &bl_tmp, &bl_zblks,
@@ -922,14 +944,13 @@ static void blosc_stage(zgpu_plan &P, const Stage &st, uint8_t *out, hipStream_t
     D.zs.ser_list = (uint32_t *)P.grow(P.bl_zser, D.n_sub * 4);
     if (const uint64_t rb = zstd_lit_rec_bytes(D.zs.lit_rec_wgs)) D.zs.lit_rec = (uint8_t *)P.grow(P.bl_zrec, rb);
     // k_blosc_finish reads raw / rle / literal-only zstd blocks where they lie (ZGPU_BLOSC_ALIAS=0: off)
-    static const bool alias_on = [] {
-      const char *e = std::getenv("ZGPU_BLOSC_ALIAS");
-      return !e || std::atoi(e) != 0;
-    }();
+    const char *ae = std::getenv("ZGPU_BLOSC_ALIAS");  // read per call (tests switch it)
+    const bool alias_on = !ae || std::atoi(ae) != 0;
     D.zs.alias = alias_on ? (uint64_t *)P.grow(P.bl_zalias, D.n_sub * 3 * ZALIAS * 8) : nullptr;
     D.zs.ser_count = P.zs.ser_count;
     D.zs.launch_serial = P.zs.launch_serial;
     P.zstd_fork(D.zs, s);
+    P.zstd_split(D.zs, s);
   }
   // the layout (bases, inert tails past this execution's totals) is always computed on the device
   HIPCHK(launch_blosc_layout(info, ni, d_bases, caps, D, s));
