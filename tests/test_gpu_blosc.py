@@ -611,8 +611,11 @@ def test_blosc_zstd_pipeline_knobs_vs_oracle(ctx, torch_cuda, knobs):
     (forced for small batches by ZGPU_ZSTD_SPLIT_MIN), either executor configuration, and slot copies
     instead of block aliases. A batch of shuffled u16 chunks (several blosc blocks each: raw, rle,
     literal-only and sequence blocks) plus a corrupt one, vs the c-blosc oracle."""
+    import ctypes as C
     import os
     from zarrs_amd import CodecChain, make_desc
+    from zarrs_amd import _lib as L
+    from zarrs_amd.codec import default_stream
     rng = np.random.default_rng(91)
     n = 3 << 17  # three 256 KiB blosc blocks per chunk
     codecs = [{"name": "bytes", "configuration": {"endian": "little"}}, _blosc("zstd", "shuffle", 2, 0, 5)]
@@ -637,13 +640,18 @@ def test_blosc_zstd_pipeline_knobs_vs_oracle(ctx, torch_cuda, knobs):
             d = torch_cuda.frombuffer(bytearray(e), dtype=torch_cuda.uint8).cuda()
             keep.append(d)
             descs.append(make_desc(d, [n], out_start=[k * n]))
-        out = np.zeros(len(encs) * n, np.uint16)
-        st = ch.decode_batch(descs, out, [len(encs) * n], enc_device=True)
+        nch = len(encs)
+        out = torch_cuda.zeros(nch * n, dtype=torch_cuda.int16, device="cuda")
+        arr = (L.ChunkDesc * nch)(*descs)
+        stc = (C.c_int32 * nch)()
+        rc = L.load().zgpu_decode_batch(ch._h, 1, arr, nch, C.c_void_p(out.data_ptr()), L.u64s([nch * n]),
+                                        L.ENC_DEVICE | L.OUT_DEVICE, stc, default_stream(None, out))
+        st = list(stc)
     finally:
         for k, v in saved.items():
             if v is None:
                 os.environ.pop(k, None)
             else:
                 os.environ[k] = v
-    assert st[:5] == [0] * 5 and st[5] != 0, st
-    assert out[:5 * n].tobytes() == np.concatenate(chunks).tobytes()
+    assert rc == L.CORRUPT_STREAM and st[:5] == [0] * 5 and st[5] == L.CORRUPT_STREAM, (rc, st)
+    assert out.cpu().numpy()[:5 * n].tobytes() == np.concatenate(chunks).tobytes()
