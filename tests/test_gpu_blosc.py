@@ -603,12 +603,13 @@ def test_blosc_zstd_block_aliases_vs_oracle(ctx, torch_cuda):
     assert ("noshuffle", 0, None) in kinds, kinds
 
 
-@pytest.mark.parametrize("knobs", [{"ZGPU_ZSTD_SPLIT_MIN": "1"}, {"ZGPU_ZSTD_XDENSE": "1"}, {"ZGPU_ZSTD_XDENSE": "0"},
-                                   {"ZGPU_BLOSC_ALIAS": "0"}, {"ZGPU_ZSTD_SPLIT_MIN": "1", "ZGPU_ZSTD_XDENSE": "1"}],
+@pytest.mark.parametrize("knobs", [{"ZGPU_ZSTD_SPLIT": "1", "ZGPU_ZSTD_SPLIT_MIN": "1"}, {"ZGPU_ZSTD_XDENSE": "1"},
+                                   {"ZGPU_ZSTD_XDENSE": "0"}, {"ZGPU_BLOSC_ALIAS": "0"},
+                                   {"ZGPU_ZSTD_SPLIT": "1", "ZGPU_ZSTD_SPLIT_MIN": "1", "ZGPU_ZSTD_XDENSE": "1"}],
                          ids=["split", "xdense", "xwide", "noalias", "split-xdense"])
 def test_blosc_zstd_pipeline_knobs_vs_oracle(ctx, torch_cuda, knobs):
     """The zstd pipeline's run-time choices change no byte: two pipelined halves on a second stream
-    (forced for small batches by ZGPU_ZSTD_SPLIT_MIN), either executor configuration, and slot copies
+    (opt-in ZGPU_ZSTD_SPLIT, forced for small batches by ZGPU_ZSTD_SPLIT_MIN), either executor configuration, and slot copies
     instead of block aliases. A batch of shuffled u16 chunks (several blosc blocks each: raw, rle,
     literal-only and sequence blocks) plus a corrupt one, vs the c-blosc oracle."""
     import ctypes as C

@@ -283,12 +283,14 @@ struct zgpu_plan {
     Z.ev_fork = zev[0];
     Z.ev_join = zev[1];
   }
-  // zstd in two pipelined halves (ZstdScratch::s2; blosc stream tables of many frames). ZGPU_ZSTD_SPLIT=0: off
+  // zstd in two pipelined halves (ZstdScratch::s2; blosc stream tables of many frames): opt-in with
+  // ZGPU_ZSTD_SPLIT=1 (blosc-zstd bench 32.6 -> 35.6 ms with it: the halves' kernels contend more than
+  // they overlap, profiles/r04an_zstd_split_ab.txt)
   hipStream_t zs2 = nullptr;
   hipEvent_t zev2[2] = {nullptr, nullptr};
   void zstd_split(ZstdScratch &Z, hipStream_t s) {
     const char *e = std::getenv("ZGPU_ZSTD_SPLIT");  // read per call (tests switch it)
-    if ((e && std::atoi(e) == 0) || !Z.side) return;
+    if (!e || std::atoi(e) == 0 || !Z.side) return;
     if (!zs2) {
       int prio = 0;
       if (s) (void)hipStreamGetPriority(s, &prio);
