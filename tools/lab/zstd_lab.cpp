@@ -178,22 +178,23 @@ int main(int argc, char **argv) {
     CK(hipEventRecord(ev[0]));
     hipLaunchKernelGGL(zgpu::k_zstd_scan, dim3(n), dim3(64), 0, 0, d_items, d_status, blks, Z.blk_cap, Z.nblk, Z.mode,
                        Z.lit_stride, Z.seq_cap, 0u, (unsigned long long *)nullptr, (uint32_t *)nullptr,
-                       (unsigned long long *)nullptr);
+                       (unsigned long long *)nullptr, (unsigned long long *)nullptr);
     CK(hipEventRecord(ev[1]));
     hipLaunchKernelGGL(zgpu::k_zstd_blocks, dim3(bgrid), dim3(64), 0, 0, d_items, d_status, blks, Z.blk_cap, Z.nblk,
-                       Z.mode, (uint32_t)n, Z.lit, Z.lit_stride, Z.seq, Z.seq_cap);
+                       Z.mode, (uint32_t)n, Z.lit, Z.lit_stride, Z.seq, Z.seq_cap, (const unsigned long long *)nullptr);
     CK(hipEventRecord(ev[2]));
     hipLaunchKernelGGL(zgpu::k_zstd_huf, dim3(grid), dim3(64), 0, 0, d_items, d_status, blks, Z.blk_cap, Z.nblk, Z.mode,
-                       (uint32_t)n, Z.lit, Z.lit_stride);
+                       (uint32_t)n, Z.lit, Z.lit_stride, (const unsigned long long *)nullptr);
     CK(hipEventRecord(ev[3]));
     hipLaunchKernelGGL(zgpu::k_zstd_lits, dim3(lgrid), dim3(zgpu::LIT_THREADS), 0, 0, d_items, d_status, blks, Z.blk_cap,
-                       Z.nblk, Z.mode, (uint32_t)n, Z.lit, Z.lit_stride, lit_rec);
+                       Z.nblk, Z.mode, (uint32_t)n, Z.lit, Z.lit_stride, lit_rec, (const unsigned long long *)nullptr);
     CK(hipEventRecord(ev[4]));
     hipLaunchKernelGGL(zgpu::k_zstd_plan, dim3(n), dim3(64), 0, 0, d_items, d_status, blks, Z.blk_cap, Z.nblk, Z.mode,
                        chunk, zgpu::XSEG, (uint64_t *)nullptr, Z.lit, Z.lit_stride);
     CK(hipEventRecord(ev[5]));
     hipLaunchKernelGGL(zgpu::k_zstd_direct, dim3(grid), dim3(256), 0, 0, d_items, d_status, blks, Z.blk_cap, Z.nblk,
-                       Z.mode, (uint32_t)n, d_out, chunk, Z.lit, Z.lit_stride, (const uint64_t *)nullptr);
+                       Z.mode, (uint32_t)n, d_out, chunk, Z.lit, Z.lit_stride, (const uint64_t *)nullptr,
+                       (const unsigned long long *)nullptr);
     CK(hipEventRecord(ev[6]));
     if (getenv("LAB_XDENSE"))
       hipLaunchKernelGGL(zgpu::xdense::k_zstd_exec_item, dim3(n * zgpu::XSEG), dim3(64), 0, 0, d_items, d_status, blks,

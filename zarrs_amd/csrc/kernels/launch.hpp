@@ -126,6 +126,9 @@ struct ZstdScratch {
   // kernels never overlap).
   hipStream_t s2 = nullptr;
   hipEvent_t ev_half = nullptr, ev_done = nullptr;
+  // the batch's largest block count per item (nullable; zeroed before the call, k_zstd_scan's
+  // atomicMax): the record-strided kernels walk n_items x that many records, not x blk_cap
+  unsigned long long *max_nblk = nullptr;
 };
 constexpr uint32_t ZALIAS = 2;
 constexpr uint64_t ZALIAS_RLE = 1ull << 63;

@@ -1186,11 +1186,17 @@ __device__ __forceinline__ uint32_t sym_eval(uint32_t x, uint32_t r0, uint32_t r
 
 }  // namespace
 
+// Block records per item the record-strided kernels walk: blk_cap, or the batch's largest block count
+// (k_zstd_scan's atomicMax; a blosc table of 256 KiB frames has 2 of its 72 record slots in use)
+__device__ __forceinline__ uint64_t rec_blocks(uint32_t blk_cap, const unsigned long long *max_nblk) {
+  return max_nblk ? min<uint64_t>(blk_cap, *max_nblk) : blk_cap;
+}
+
 __global__ __launch_bounds__(64) void k_zstd_scan(const ZgItem *items, uint32_t *status, ZBlk *blks,
                                                   uint32_t blk_cap, uint32_t *nblk, uint32_t *zmode,
                                                   uint64_t lit_stride, uint64_t seq_cap, uint32_t force_serial,
                                                   unsigned long long *counters, uint32_t *ser_list,
-                                                  unsigned long long *ser_count) {
+                                                  unsigned long long *ser_count, unsigned long long *max_nblk) {
   __shared__ ZScanSmem S;
   const uint32_t item = blockIdx.x;
   const ZgItem it = items[item];
@@ -1395,6 +1401,7 @@ __global__ __launch_bounds__(64) void k_zstd_scan(const ZgItem *items, uint32_t 
     if (err && !serial) status[item] = err;
     if (counters && (serial || !err)) atomicAdd(&counters[serial ? 0 : 1], 1ull);  // serial / block-parallel items
     if (serial && ser_list) ser_list[atomicAdd(ser_count, 1ull)] = item;
+    if (max_nblk && !serial && !err) atomicMax(max_nblk, (unsigned long long)nb);
   }
 }
 
@@ -1402,10 +1409,11 @@ __global__ __launch_bounds__(64) void k_zstd_scan(const ZgItem *items, uint32_t 
 __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(ZG_BLK_WPE, 8))) void k_zstd_blocks(const ZgItem *items, uint32_t *status, ZBlk *blks,
                                                     uint32_t blk_cap, const uint32_t *nblk,
                                                     const uint32_t *zmode, uint32_t n_items, uint8_t *lit_scratch,
-                                                    uint64_t lit_stride, uint32_t *seq_scratch, uint64_t seq_cap) {
+                                                    uint64_t lit_stride, uint32_t *seq_scratch, uint64_t seq_cap,
+                                                    const unsigned long long *max_nblk) {
   __shared__ ZDecSmem S;
   const int lane = lane_id();
-  const uint64_t total = (uint64_t)n_items * blk_cap;
+  const uint64_t total = (uint64_t)n_items * rec_blocks(blk_cap, max_nblk);
   for (uint64_t g = blockIdx.x; g < total; g += gridDim.x) {
     // block-major record order: block bi of every item before block bi+1 of any, so that items
     // with few blocks (many small frames, e.g. blosc streams) spread over all workgroups
@@ -2927,10 +2935,11 @@ struct ZHufSmem {
 // held the 256-lane literal decoder to 2 workgroups per CU while 3 of its 4 waves waited.
 __global__ __launch_bounds__(64) void k_zstd_huf(const ZgItem *items, const uint32_t *status, const ZBlk *blks,
                                                  uint32_t blk_cap, const uint32_t *nblk, const uint32_t *zmode,
-                                                 uint32_t n_items, uint8_t *lit_scratch, uint64_t lit_stride) {
+                                                 uint32_t n_items, uint8_t *lit_scratch, uint64_t lit_stride,
+                                                 const unsigned long long *max_nblk) {
   __shared__ __attribute__((aligned(16))) ZHufSmem S;
   const uint32_t lane = threadIdx.x;
-  const uint64_t total = (uint64_t)n_items * blk_cap;
+  const uint64_t total = (uint64_t)n_items * rec_blocks(blk_cap, max_nblk);
   for (uint64_t g = blockIdx.x; g < total; g += gridDim.x) {
     const uint32_t item = (uint32_t)(g % n_items), bi = (uint32_t)(g / n_items);  // block-major order
     if (bi >= nblk[item] || zmode[item] != ZMODE_PARALLEL) continue;
@@ -2964,13 +2973,13 @@ __global__ __launch_bounds__(LIT_THREADS) __attribute__((amdgpu_waves_per_eu(ZG_
                                                            uint32_t blk_cap, const uint32_t *nblk,
                                                            const uint32_t *zmode, uint32_t n_items,
                                                            uint8_t *lit_scratch, uint64_t lit_stride,
-                                                           uint8_t *lit_rec) {
+                                                           uint8_t *lit_rec, const unsigned long long *max_nblk) {
   __shared__ ZLitSmem S;
   const uint32_t t = threadIdx.x;
   // this lane's record slot (ZG_LIT_REC; nullptr: every lane decodes twice)
   uint8_t *const slot = lit_rec ? lit_rec + ((uint64_t)blockIdx.x * LIT_THREADS + t) * REC_SLOT : nullptr;
   (void)slot;
-  const uint64_t total = (uint64_t)n_items * blk_cap;
+  const uint64_t total = (uint64_t)n_items * rec_blocks(blk_cap, max_nblk);
   for (uint64_t g = blockIdx.x; g < total; g += gridDim.x) {
     const uint32_t item = (uint32_t)(g % n_items), bi = (uint32_t)(g / n_items);  // block-major order
     if (bi >= nblk[item] || zmode[item] != ZMODE_PARALLEL) continue;
@@ -3254,8 +3263,8 @@ __global__ __launch_bounds__(256) void k_zstd_direct(const ZgItem *items, const 
                                                     uint32_t blk_cap, const uint32_t *nblk, const uint32_t *zmode,
                                                     uint32_t n_items, uint8_t *dst, uint64_t slot_bytes,
                                                     const uint8_t *lit_scratch, uint64_t lit_stride,
-                                                    const uint64_t *alias) {
-  const uint64_t recs = (uint64_t)n_items * blk_cap;
+                                                    const uint64_t *alias, const unsigned long long *max_nblk) {
+  const uint64_t recs = (uint64_t)n_items * rec_blocks(blk_cap, max_nblk);
   const uint32_t tid = threadIdx.x;
   for (uint64_t rec = blockIdx.x; rec < recs; rec += gridDim.x) {
     const uint32_t item = (uint32_t)(rec % n_items), bi = (uint32_t)(rec / n_items);  // block-major order
@@ -3419,7 +3428,7 @@ static hipError_t launch_zstd_pass(ZgItem *items, uint32_t *status, uint32_t n_i
   const bool listed = Z.ser_list && Z.ser_count;
   hipLaunchKernelGGL(k_zstd_scan, dim3(n_items), dim3(64), 0, s, items, status, blks, Z.blk_cap, Z.nblk, Z.mode,
                      Z.lit_stride, Z.seq_cap, Z.force_serial, Z.counters, listed ? Z.ser_list : nullptr,
-                     listed ? Z.ser_count : nullptr);
+                     listed ? Z.ser_count : nullptr, Z.max_nblk);
   const uint64_t recs = (uint64_t)n_items * Z.blk_cap;
   // grids of the record-strided entropy kernels (overridable for tuning: ZGPU_ZSTD_GRID, ZGPU_ZSTD_LGRID)
   static const uint64_t g_cap = [] {
@@ -3446,19 +3455,19 @@ static hipError_t launch_zstd_pass(ZgItem *items, uint32_t *status, uint32_t n_i
   const uint32_t bgrid =
       (uint32_t)std::min<uint64_t>(recs, std::max<uint64_t>(g_cap, (uint64_t)device_cu_count() * 4 * ZG_BLK_WPE));
   hipLaunchKernelGGL(k_zstd_blocks, dim3(bgrid), dim3(64), 0, sq, items, status, blks, Z.blk_cap, Z.nblk, Z.mode,
-                     n_items, Z.lit, Z.lit_stride, Z.seq, Z.seq_cap);
+                     n_items, Z.lit, Z.lit_stride, Z.seq, Z.seq_cap, Z.max_nblk);
   if (fork) {
     hipError_t e = hipEventRecord(Z.ev_join, Z.side);
     if (e != hipSuccess) return e;
   }
 #if ZG_HUF_SPLIT
   hipLaunchKernelGGL(k_zstd_huf, dim3(grid), dim3(64), 0, s, items, status, blks, Z.blk_cap, Z.nblk, Z.mode, n_items,
-                     Z.lit, Z.lit_stride);
+                     Z.lit, Z.lit_stride, Z.max_nblk);
 #endif
   // record slots: one per lane of the persistent grid (allocated for l_cap workgroups)
   uint8_t *lit_rec = (ZG_LIT_REC && Z.lit_rec && lgrid <= Z.lit_rec_wgs) ? Z.lit_rec : nullptr;
   hipLaunchKernelGGL(k_zstd_lits, dim3(lgrid), dim3(LIT_THREADS), 0, s, items, status, blks, Z.blk_cap, Z.nblk,
-                     Z.mode, n_items, Z.lit, Z.lit_stride, lit_rec);
+                     Z.mode, n_items, Z.lit, Z.lit_stride, lit_rec, Z.max_nblk);
   if (fork) {
     hipError_t e = hipStreamWaitEvent(s, Z.ev_join, 0);
     if (e != hipSuccess) return e;
@@ -3476,7 +3485,7 @@ static hipError_t launch_zstd_pass(ZgItem *items, uint32_t *status, uint32_t n_i
   hipLaunchKernelGGL(k_zstd_plan, dim3(n_items), dim3(64), 0, s, items, status, blks, Z.blk_cap, Z.nblk, Z.mode,
                      slot_bytes, xseg, Z.alias, Z.lit, Z.lit_stride);
   hipLaunchKernelGGL(k_zstd_direct, dim3(grid), dim3(256), 0, s, items, status, blks, Z.blk_cap, Z.nblk, Z.mode,
-                     n_items, dst, slot_bytes, Z.lit, Z.lit_stride, Z.alias);
+                     n_items, dst, slot_bytes, Z.lit, Z.lit_stride, Z.alias, Z.max_nblk);
   // executor configuration: xdense when the grid has many waves per CU (ZGPU_ZSTD_XDENSE=0/1 forces one)
   const char *xd_s = std::getenv("ZGPU_ZSTD_XDENSE");  // read per call (tests force both)
   const int xd_env = xd_s ? std::atoi(xd_s) : -1;

@@ -41,7 +41,7 @@ thread_local std::string g_last_error;
 enum { CTR_ENC_BYTES = 0, CTR_ZSTD_SERIAL = 1, CTR_ZSTD_PARALLEL = 2, CTR_BLOSC_RERUN = 3, CTR_BLOSC_BLOCKS = 4,
        CTR_N = 5 };
 // internal ctl slots (not reported): a cached blosc layout was outgrown (the execution is re-run)
-enum { CTR_BLOSC_OVF = 31, CTR_SCRATCH = 30, CTR_ZSTD_NSER = 29 };  // not reported (device-side flags / sinks)
+enum { CTR_BLOSC_OVF = 31, CTR_SCRATCH = 30, CTR_ZSTD_NSER = 29, CTR_ZSTD_MAXBLK = 28 };  // not reported (device-side flags / sinks)
 thread_local uint64_t g_last_counters[CTR_N];
 // UnexpectedChunkDecodedSize detail of the last call's first DECODED_SIZE_MISMATCH descriptor
 struct SizeDetail {
@@ -835,6 +835,7 @@ static void plan_upload(zgpu_plan &P, hipStream_t us) {
   P.d_status = (uint32_t *)(P.d_ctl + 256);
   P.zs.counters = P.d_counter + CTR_ZSTD_SERIAL;
   P.zs.ser_count = P.d_counter + CTR_ZSTD_NSER;
+  P.zs.max_nblk = P.d_counter + CTR_ZSTD_MAXBLK;
   if (const char *e = std::getenv("ZGPU_ZSTD_FORCE_SERIAL")) P.zs.force_serial = std::atoi(e) != 0;
   if (!P.shards.empty()) {
     P.d_shards = (ZgShard *)C.dev_alloc(P.shards.size() * sizeof(ZgShard));
@@ -942,6 +943,7 @@ static void blosc_stage(zgpu_plan &P, const Stage &st, uint8_t *out, hipStream_t
     D.zs.lit = (uint8_t *)P.grow(P.bl_zlit, D.n_sub * D.zs.lit_stride);
     D.zs.seq = (uint32_t *)P.grow(P.bl_zseq, D.n_sub * D.zs.seq_cap * 12);
     D.zs.counters = P.zs.counters;
+    D.zs.max_nblk = P.zs.max_nblk;
     D.zs.force_serial = P.zs.force_serial;
     D.zs.ser_list = (uint32_t *)P.grow(P.bl_zser, D.n_sub * 4);
     if (const uint64_t rb = zstd_lit_rec_bytes(D.zs.lit_rec_wgs)) D.zs.lit_rec = (uint8_t *)P.grow(P.bl_zrec, rb);
