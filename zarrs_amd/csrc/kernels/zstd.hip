@@ -1134,7 +1134,7 @@ struct SeqX {
   uint8_t nb, nbx;
 };
 #ifndef ZG_BLK_WPE
-#define ZG_BLK_WPE 5  // waves per SIMD k_zstd_blocks is compiled for
+#define ZG_BLK_WPE 6  // waves per SIMD k_zstd_blocks is compiled for
 #endif
 #ifndef ZG_SEQ_PACK
 #define ZG_SEQ_PACK 1  // 4-byte sequence tables (below); 0: 8-byte SeqX
