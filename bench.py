@@ -33,6 +33,13 @@ import time
 
 ROOT = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, ROOT)
+# HIP hardware queues per process, set before HIP starts (INTEGRATION.md "Drop-in tuning"): 8 lanes'
+# streams on HIP's default 4 queues serialise the drop-in leg's concurrent calls (10.6 GiB/s; 13.6
+# with 8 queues, the other legs unchanged: profiles/r04as_hw_queues_ab.txt). The benchmark's own
+# setting (ZGPU_BENCH_HW_QUEUES, default 8; 0 keeps the environment's) overrides the environment's.
+_hwq = os.environ.get("ZGPU_BENCH_HW_QUEUES", "8")
+if _hwq != "0":
+    os.environ["GPU_MAX_HW_QUEUES"] = str(min(32, max(1, int(_hwq))))
 
 import numpy as np  # noqa: E402
 import torch  # noqa: E402
