@@ -33,14 +33,9 @@ import time
 
 ROOT = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, ROOT)
-# HIP hardware queues per process, set before HIP starts (INTEGRATION.md "Drop-in tuning"): 8 lanes'
-# streams on HIP's default 4 queues serialise the drop-in leg's concurrent calls (10.6 GiB/s; 13.6
-# with 8 queues, the other legs unchanged: profiles/r04as_hw_queues_ab.txt). The benchmark's own
-# setting (ZGPU_BENCH_HW_QUEUES, default 8; 0 keeps the environment's) overrides the environment's.
-_hwq = os.environ.get("ZGPU_BENCH_HW_QUEUES", "8")
-if _hwq != "0":
-    os.environ["GPU_MAX_HW_QUEUES"] = str(min(32, max(1, int(_hwq))))
-
+# HIP runs with the environment's hardware-queue count (GPU_MAX_HW_QUEUES; HIP's default is 4): the
+# line records the value it ran with (`hip_env`). Round 4 forced 8 here for the drop-in leg; that is a
+# setting a zarrs user does not get, so the line is measured at the box's default.
 import numpy as np  # noqa: E402
 import torch  # noqa: E402
 
@@ -792,7 +787,7 @@ class C5:
         # plans (chunk batches) and the streams they run on: the largest level is split in two halves
         # on streams of their own (its entropy-decode kernels are throughput-bound, its per-chunk
         # sequence execution is not, so halving the batch shortens its chain), the next level on a
-        # third stream, the small levels one after another on a fourth (GPU_MAX_HW_QUEUES is 4)
+        # third stream, the small levels one after another on a fourth (HIP's default GPU_MAX_HW_QUEUES is 4)
         l0 = per_level[0]
         halves = lpt_partition([int(dsc.enc_len) for dsc in l0], 2)  # balanced by encoded size
         groups = [[l0[i] for i in hv] for hv in halves] + per_level[1:]
@@ -1613,6 +1608,7 @@ def main():
             "world": r["world_info"],
             "decode_batch_ms_incl_host_planning": round(r["batch_ms"], 3),
             "host_leg": r["host"],
+            "hip_env": {"GPU_MAX_HW_QUEUES": os.environ.get("GPU_MAX_HW_QUEUES", "unset (HIP default: 4)")},
         }
         if r["counters"][L_CTR_ZSTD_SERIAL] or r["counters"][L_CTR_ZSTD_PARALLEL]:
             line["zstd_items_per_step"] = {"block_parallel": r["counters"][L_CTR_ZSTD_PARALLEL],
@@ -1624,6 +1620,13 @@ def main():
         if sec:
             line["secondary"] = sec
         print(json.dumps(line), flush=True)
+    # explicit teardown before the interpreter's: the workload's tensors, then the context (plans were
+    # destroyed in run_gpu; chains keep their context alive until they go, zgpu_ctx_refcount)
+    r["W"] = None
+    import gc
+    gc.collect()
+    args.ctx.close()
+    torch.cuda.synchronize()
     if world > 1:
         torch.distributed.destroy_process_group()
 

@@ -99,9 +99,13 @@ typedef struct zgpu_ctx zgpu_ctx;
 typedef struct zgpu_chain zgpu_chain;
 typedef struct zgpu_plan zgpu_plan;
 
-/* One context per GPU: owns a HIP stream, device scratch and pinned staging. */
+/* One context per GPU: owns a HIP stream, device scratch and pinned staging. zgpu_ctx_destroy drops
+ * the caller's reference: chains, plans and caches created on the context hold references of their
+ * own, so the context is freed when the last of them is destroyed (any destruction order is safe). */
 int zgpu_ctx_create(int hip_device, zgpu_ctx **out);
 void zgpu_ctx_destroy(zgpu_ctx *ctx);
+/* Live references of a context (1 + its chains, plans and caches; diagnostics and tests). */
+int64_t zgpu_ctx_refcount(const zgpu_ctx *ctx);
 /* Last error message of the calling thread on this context ("" if none). */
 const char *zgpu_last_error(const zgpu_ctx *ctx);
 const char *zgpu_status_name(int status);

@@ -249,3 +249,15 @@ def test_world3_root_verifies_every_slab():
         assert out[r]["roundtrip_ok_False"] is True
         assert out[r]["roundtrip_ok_True"] is False
     assert out[0]["noncontig"]
+
+
+def test_slab_mismatches_one_byte_float():
+    """Floating dtypes compare bit for bit at every element size, 1-byte floats included."""
+    if not hasattr(torch, "float8_e4m3fn"):
+        pytest.skip("no float8 dtype in this torch")
+    full = torch.arange(24, dtype=torch.uint8).view(torch.float8_e4m3fn).reshape(6, 4)
+    slabs = slab_partition([0, 0], [6, 4], 2)
+    assert slab_mismatches(full.clone(), full, slabs) == []
+    bad = full.clone()
+    bad.view(torch.uint8)[4, 1] ^= 1
+    assert slab_mismatches(bad, full, slabs) == [1]

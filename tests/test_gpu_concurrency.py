@@ -52,6 +52,10 @@ def test_concurrent_calls_one_context(name):
                     out = torch.zeros(a.shape, dtype=torch.float32, device="cuda")
                     descs = [make_desc(e, cs, out_start=[i * 16, 0, k * 32]) for (i, k), e in encs.items()]
                     s = torch.cuda.Stream()
+                    # the inputs' H2D copies and the output's zero fill ran on this thread's current
+                    # stream: the decode's stream waits for them (a caller stream is not ordered
+                    # after other streams by the library, zgpu.h "Stream ordering")
+                    s.wait_stream(torch.cuda.current_stream())
                     with torch.cuda.stream(s):
                         st = ch.decode_batch(descs, out, list(a.shape), enc_device=True, stream=s.cuda_stream)
                     s.synchronize()

@@ -70,7 +70,14 @@ class Context:
         L.check(L.load().zgpu_ctx_coalescing_stats(self._h, C.byref(b), C.byref(c)))
         return {"batches": b.value, "calls": c.value}
 
+    def refcount(self) -> int:
+        """References the library holds on this context: 1 (this handle) + its live chains, plans and
+        caches (zgpu_ctx_refcount); 0 once closed."""
+        return int(L.load().zgpu_ctx_refcount(self._h)) if getattr(self, "_h", None) else 0
+
     def close(self):
+        """Drop this handle's reference (zgpu_ctx_destroy). Chains, plans and caches made on the
+        context keep it alive until they are destroyed too, in any order."""
         if getattr(self, "_h", None):
             L.load().zgpu_ctx_destroy(self._h)
             self._h = None

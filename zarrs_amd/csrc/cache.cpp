@@ -125,6 +125,7 @@ extern "C" {
 int zgpu_cache_create(zgpu_ctx *ctx, uint64_t capacity_bytes, zgpu_cache **out) {
   if (!ctx || !out) return fail(ZGPU_INVALID_ARGUMENT, "NULL argument");
   auto K = std::make_unique<zgpu_cache>();
+  ctx_ref(ctx);
   K->ctx = ctx;
   K->device = ctx_device(ctx);
   K->capacity = capacity_bytes;
@@ -134,10 +135,13 @@ int zgpu_cache_create(zgpu_ctx *ctx, uint64_t capacity_bytes, zgpu_cache **out) 
 
 void zgpu_cache_destroy(zgpu_cache *cache) {
   if (!cache) return;
-  // garbage-collected bindings may destroy the cache after its context: only the device id is used
+  // the cache holds a reference to its context: it is alive here whatever order a garbage-collected
+  // binding destroys them in
+  zgpu_ctx *ctx = cache->ctx;
   if (hipSetDevice(cache->device) != hipSuccess) (void)hipGetLastError();
   delete cache;
   (void)hipGetLastError();  // a failed free must not surface in the caller's next HIP error check
+  ctx_unref(ctx);
 }
 
 int zgpu_cache_clear(zgpu_cache *K) {

@@ -14,6 +14,9 @@ namespace zgpu {
 // set the calling thread's zgpu_last_error message; returns status
 int set_last_error(int status, const std::string &msg);
 zgpu_ctx *chain_ctx(const zgpu_chain *c);
+// context references (zgpu_ctx::refs): chains, plans and caches hold one each
+void ctx_ref(zgpu_ctx *c);
+void ctx_unref(zgpu_ctx *c);
 const Chain &chain_model(const zgpu_chain *c);
 bool chain_validates(const zgpu_chain *c);
 int ctx_device(const zgpu_ctx *c);

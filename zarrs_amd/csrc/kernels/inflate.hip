@@ -170,7 +170,11 @@ struct Smem {
     };
     struct {  // a symbol batch
       uint32_t rec[64];   // the batch's symbols: literal byte, or (1<<31)|(dist<<9)|len
-      uint16_t rbeg[64], rend[64];  // output interval of each symbol in the batch (match dependencies)
+      union {             // output interval of each symbol in the batch (match dependencies)
+        uint16_t rbeg[64];
+        uint4 rbeg4[8];   // eight 16-B segments of 8 entries (the pivot search)
+      };
+      uint16_t rend[64];
     };
   };
 };
@@ -555,6 +559,12 @@ __device__ __forceinline__ void flush(const Smem &S, uint8_t *out, uint64_t cap,
 #ifndef ZG_INFLATE_SEGCAP
 #define ZG_INFLATE_SEGCAP 96  // symbol records per lane region (a fuller region ends the round there)
 #endif
+#ifndef ZG_INFLATE_PIV
+#define ZG_INFLATE_PIV 1  // exec_batch: match source ranges by a two-level pivot search (no LDS search chain)
+#endif
+#ifndef ZG_INFLATE_XFETCH
+#define ZG_INFLATE_XFETCH 1  // executor batches: region lookup by ballots + records loaded a batch ahead
+#endif
 #ifndef ZG_INFLATE_MAXREP
 #define ZG_INFLATE_MAXREP 8  // out-of-sync lanes re-decoded per round from their predecessor's exit
 #endif
@@ -673,6 +683,37 @@ __device__ __forceinline__ bool exec_batch(Smem &S, uint8_t *out, uint64_t cap, 
   // are monotonic): hi = the last symbol starting before e_rel, lo = the last starting at or
   // before s_rel; both found by one interleaved binary search per batch. A round then tests
   // the pending mask against the range, with no LDS read.
+#if ZG_INFLATE_PIV
+  // Two-level search without a chain of dependent LDS reads: the entries 0, 8, .., 56 (uniform,
+  // by readlane) pick the 8-entry segment, one 16-B LDS read of that segment finishes it. Lanes
+  // past the batch hold 0xFFFF (above any query).
+  const uint32_t rv = mine ? (uint32_t)(mypos - pos) : 0xFFFFu;
+  S.rbeg[lane] = (uint16_t)rv;
+  int32_t piv[8];
+#pragma unroll
+  for (int k = 0; k < 8; k++) piv[k] = (int32_t)U(__builtin_amdgcn_readlane((int)rv, 8 * k));
+  __syncthreads();
+  int32_t hi = -1, lo = 0;
+  if (is_match && e_rel > 0) {
+    int32_t a = 0, b = 0;  // pivots < e_rel (>= 1: entry 0 is 0), pivots <= s_rel
+#pragma unroll
+    for (int k = 0; k < 8; k++) {
+      a += piv[k] < e_rel;
+      b += piv[k] <= s_rel;
+    }
+    const uint4 wa = S.rbeg4[a - 1];
+    const uint4 wb = S.rbeg4[b > 0 ? b - 1 : 0];
+    const uint32_t va[4] = {wa.x, wa.y, wa.z, wa.w}, vb[4] = {wb.x, wb.y, wb.z, wb.w};
+    int32_t ca = 0, cb = 0;
+#pragma unroll
+    for (int k = 0; k < 4; k++) {
+      ca += ((int32_t)(va[k] & 0xFFFF) < e_rel) + ((int32_t)(va[k] >> 16) < e_rel);
+      cb += ((int32_t)(vb[k] & 0xFFFF) <= s_rel) + ((int32_t)(vb[k] >> 16) <= s_rel);
+    }
+    hi = 8 * (a - 1) + ca - 1;
+    lo = b > 0 ? 8 * (b - 1) + cb - 1 : 0;
+  }
+#else
   if (mine) S.rbeg[lane] = (uint16_t)(mypos - pos);
   __syncthreads();
   int32_t hi = -1, lo = 0;
@@ -684,6 +725,7 @@ __device__ __forceinline__ bool exec_batch(Smem &S, uint8_t *out, uint64_t cap, 
       if (lo + step < (int32_t)cnt && (int32_t)S.rbeg[lo + step] <= s_rel) lo += step;
     }
   }
+#endif
   const uint64_t rmask = hi < 0 ? 0ull : (hi >= 63 ? ~0ull : ((2ull << hi) - 1)) & ~((1ull << lo) - 1);
 #else
   if (mine) S.rend[lane] = (uint16_t)(mypos - pos + (is_match ? mlen : 1u));
@@ -720,14 +762,23 @@ __device__ __forceinline__ bool exec_batch(Smem &S, uint8_t *out, uint64_t cap, 
       const uint64_t F = ((uint64_t)F_hi << 32) | F_lo;
       const uint32_t flen = __builtin_amdgcn_readlane(mlen, f), fd = __builtin_amdgcn_readlane(md, f);
       const float inv = 1.0f / (float)fd;
-      for (uint32_t i = lane; i < flen; i += 64) {
+      // every source byte lies before F (final): all loads (<= 5 per lane, len <= 258) are issued
+      // before the first store, one wait for all of them
+      uint8_t v[5];
+#pragma unroll
+      for (int j = 0; j < 5; j++) {
+        const uint32_t i = (uint32_t)lane + 64u * j;
         uint32_t q = (uint32_t)((float)i * inv);
         int32_t rm = (int32_t)i - (int32_t)(q * fd);
         if (rm < 0) rm += fd;
         if (rm >= (int32_t)fd) rm -= fd;
         const uint64_t src = F - fd + (uint32_t)rm;
-        const uint8_t v = (src + RING >= batch_end) ? S.ring[src & RMASK] : __builtin_nontemporal_load(out + src);
-        S.ring[(F + i) & RMASK] = v;
+        v[j] = i < flen ? ((src + RING >= batch_end) ? S.ring[src & RMASK] : __builtin_nontemporal_load(out + src)) : 0;
+      }
+#pragma unroll
+      for (int j = 0; j < 5; j++) {
+        const uint32_t i = (uint32_t)lane + 64u * j;
+        if (i < flen) S.ring[(F + i) & RMASK] = v[j];
       }
     }
     if (lm && lane == __builtin_ctzll(lm)) pending = false;
@@ -862,7 +913,9 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(ZG_INFLATE_W
     ZgItem *items, uint32_t *status, const uint32_t *kind, uint8_t *dst, uint64_t slot_bytes, uint2 *aux,
     const uint32_t *order, uint32_t *seg_scr) {
   __shared__ Smem S;
+#if !ZG_INFLATE_XFETCH
   __shared__ uint16_t seg_base[65], seg_skip[64];
+#endif
   PROF_DECL;
   PROF_T(t_all);
   const uint32_t item = order ? order[blockIdx.x] : blockIdx.x;
@@ -1075,13 +1128,50 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(ZG_INFLATE_W
         const uint32_t stl = (uint32_t)__builtin_amdgcn_readlane((int)st, J - 1);
         const uint64_t pl = ((uint64_t)(uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)(p >> 32), J - 1) << 32) |
                             (uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)p, J - 1);
-        // records of the valid lanes, in stream order
+        // records of the valid lanes, in stream order: lane l's region holds the round's symbols
+        // [rb_l, rb_l + cnt_l), its records start at word ro_l of the scratch
         const uint32_t cnt_l = (lane < J) ? n - skip : 0u;
         const uint32_t incl = wave_incl_sum(cnt_l);
+        const uint32_t total = U(__builtin_amdgcn_readlane((int)incl, 63));
+#if ZG_INFLATE_XFETCH
+        const uint32_t rb_l = incl - cnt_l;
+        const uint32_t ro_l = (uint32_t)lane * SEGCAP + skip;  // in this stream's 64 record slots
+        const uint32_t *wrec = seg_scr + (uint64_t)blockIdx.x * 64 * SEGCAP;
+        __threadfence_block();  // the records (global) before other lanes read them
+        __syncthreads();
+        PROF_ADD(1, t_sd);
+        PROF_T(t_sx);
+        // The batch starting at symbol g: lane t takes symbol g + t. Its region comes from ballots over
+        // the lane regions (the one holding g, then the few that start inside the batch: no LDS
+        // search), and a batch's records are loaded while the previous batch executes.
+        auto fetch = [&](uint32_t g) -> uint32_t {
+          const uint64_t has = __ballot(cnt_l != 0 && rb_l <= g);
+          const int k0 = has ? 63 - __builtin_clzll(has) : 0;
+          uint32_t rb = U(__builtin_amdgcn_readlane((int)rb_l, k0));
+          uint32_t ro = U(__builtin_amdgcn_readlane((int)ro_l, k0));
+          uint64_t st = __ballot(cnt_l != 0 && rb_l > g && rb_l < g + 64);
+          while (st) {  // the regions starting inside the batch, in stream order
+            const int k = __builtin_ctzll(st);
+            st &= st - 1;
+            const uint32_t b = U(__builtin_amdgcn_readlane((int)rb_l, k));
+            const uint32_t o = U(__builtin_amdgcn_readlane((int)ro_l, k));
+            if (g + (uint32_t)lane >= b) {
+              rb = b;
+              ro = o;
+            }
+          }
+          const uint32_t idx = g + (uint32_t)lane;
+          return idx < total ? wrec[ro + (idx - rb)] : 0u;
+        };
+        uint32_t rec_next = total ? fetch(0) : 0u;
+        for (uint32_t g = 0; g < total && !err;) {
+          const uint32_t idx = g + (uint32_t)lane;
+          const uint32_t rec = rec_next;
+          const uint32_t ln = idx < total ? ((rec >> 31) ? (rec & 511) : 1u) : 0u;
+#else
         seg_base[lane] = (uint16_t)(incl - cnt_l);
         seg_skip[lane] = (uint16_t)skip;
         if (lane == 63) seg_base[64] = (uint16_t)incl;
-        const uint32_t total = U(__builtin_amdgcn_readlane((int)incl, 63));
         __threadfence_block();  // the records (global) and bases (LDS) before other lanes read them
         __syncthreads();
         PROF_ADD(1, t_sd);
@@ -1097,6 +1187,7 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(ZG_INFLATE_W
             rec = seg_scr[((uint64_t)blockIdx.x * 64 + (uint32_t)k) * SEGCAP + seg_skip[k] + (idx - seg_base[k])];
             ln = (rec >> 31) ? (rec & 511) : 1u;
           }
+#endif
           const uint32_t inc = wave_incl_sum(ln);
           const bool take = idx < total && inc - ln < (uint32_t)BATCH_CAP;
           const uint64_t tm = __ballot(take);
@@ -1108,6 +1199,9 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(ZG_INFLATE_W
           }
           PROF_CNT(7, bc);
           PROF_CNT(6, 1);
+#if ZG_INFLATE_XFETCH
+          if (g + bc < total) rec_next = fetch(g + bc);  // in flight while this batch executes
+#endif
 #ifdef ZG_PROFILE
           if (!exec_batch(S, out, cap, pos, flushed, bc, bytes, rec, prof_acc)) err = ZG_CORRUPT_STREAM;
 #else

@@ -90,10 +90,15 @@ int zgpu_retrieve_array_subset_multi(zgpu_chain *const *chains, uint32_t n_dev, 
         uint8_t *dst = (uint8_t *)out + P.row0 * row_bytes;
         const int dev = ctx_device(C);
         if (dev_out && d != 0) {  // decode into a slab of this device's HBM, then one peer copy
-          // a one-off allocation (not the context's grow-only pool: a large read would otherwise keep
-          // rows * row_bytes of every secondary device reserved for the context's lifetime)
+          // a stream-ordered allocation on the context's copy stream (not the context's grow-only
+          // pool: a large read would otherwise keep rows * row_bytes of every secondary device reserved
+          // for the context's lifetime; not hipMalloc/hipFree either: hipFree synchronises the whole
+          // device, stalling the other lanes' decodes there)
           hipError_t e = hipSetDevice(dev);
-          if (e == hipSuccess) e = hipMalloc(&scratch, std::max<uint64_t>(P.rows * row_bytes, 1));
+          hipStream_t cs = e == hipSuccess ? ctx_copy_stream(C) : nullptr;
+          if (e == hipSuccess && !cs) e = hipErrorInvalidValue;
+          if (e == hipSuccess) e = hipMallocAsync(&scratch, std::max<uint64_t>(P.rows * row_bytes, 1), cs);
+          if (e == hipSuccess) e = hipStreamSynchronize(cs);  // the decode runs on another stream
           if (e != hipSuccess) {
             (void)hipGetLastError();
             scratch = nullptr;
@@ -129,7 +134,10 @@ int zgpu_retrieve_array_subset_multi(zgpu_chain *const *chains, uint32_t n_dev, 
         P.rc = ZGPU_HIP_ERROR;
         P.err = "unknown exception";
       }
-      if (scratch && hipSetDevice(ctx_device(C)) == hipSuccess) (void)hipFree(scratch);
+      if (scratch && hipSetDevice(ctx_device(C)) == hipSuccess) {
+        hipStream_t cs = ctx_copy_stream(C);  // ordered after the peer copy (synchronised above)
+        if (!cs || hipFreeAsync(scratch, cs) != hipSuccess) (void)hipGetLastError();
+      }
     };
     std::vector<std::thread> threads;
     for (uint32_t d = 1; d < n_dev; d++)

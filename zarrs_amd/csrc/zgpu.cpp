@@ -13,6 +13,7 @@
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
+#include <atomic>
 #include <chrono>
 #include <cstdio>
 #include <cstdlib>
@@ -82,6 +83,11 @@ struct Lane {
 
 struct zgpu_ctx {
   int device = 0;
+  // Lifetime: zgpu_ctx_destroy drops the caller's reference; every chain, plan and cache created on
+  // the context holds one more, so a context outlives the objects that use it in whatever order a
+  // garbage-collected binding destroys them. The last reference frees the context (no HIP call runs
+  // from a static destructor: the library has none).
+  std::atomic<int64_t> refs{1};
   std::mutex mu;  // the allocator pools
   std::multimap<size_t, void *> free_dev;  // size -> ptr
   std::map<void *, size_t> live_dev;
@@ -194,6 +200,13 @@ struct zgpu_ctx {
     (void)hipGetLastError();  // teardown failures must not surface in the caller's next HIP error check
   }
 };
+
+void zgpu::ctx_ref(zgpu_ctx *c) {
+  if (c) c->refs.fetch_add(1, std::memory_order_relaxed);
+}
+void zgpu::ctx_unref(zgpu_ctx *c) {
+  if (c && c->refs.fetch_sub(1, std::memory_order_acq_rel) == 1) delete c;
+}
 
 // A call's lane for its whole duration (RAII).
 struct LaneScope {
@@ -345,6 +358,10 @@ struct zgpu_plan {
 
   ~zgpu_plan() {
     if (!ctx) return;
+    struct Unref {
+      zgpu_ctx *c;
+      ~Unref() { ctx_unref(c); }
+    } unref{ctx};  // after every buffer below went back to the context's pools
     if (own.stream) {
       (void)hipStreamSynchronize(own.stream);
       (void)hipStreamDestroy(own.stream);
@@ -1097,6 +1114,7 @@ static int plan_statuses(zgpu_plan &P, int32_t *status, hipStream_t s) {
 static zgpu_plan *plan_new(zgpu_ctx *ctx, const std::shared_ptr<Chain> &chain, bool validate, uint32_t nd,
                            const zgpu_chunk_desc *descs, uint64_t n, const uint64_t *out_shape, uint32_t flags) {
   auto P = std::make_unique<zgpu_plan>();
+  ctx_ref(ctx);
   P->ctx = ctx;
   P->chain = chain;
   P->validate = validate && !(flags & ZGPU_NO_VALIDATE);
@@ -1275,6 +1293,7 @@ static void shard_stage(GeneralCall &G, const Codec &k, std::vector<ZgItem> &ite
   // one stages-only plan over `set` with slots of `c` bytes; statuses in s, decoded items in res
   auto run = [&](const std::vector<uint32_t> &set, uint64_t c, std::vector<int32_t> &s, std::vector<ZgItem> &res) {
     auto P = std::make_unique<zgpu_plan>();
+    ctx_ref(G.C);  // ~zgpu_plan drops it
     P->ctx = G.C;
     P->validate = G.validate;
     P->nd = 1;
@@ -1725,7 +1744,9 @@ int zgpu_ctx_create(int dev, zgpu_ctx **out) {
   ABI_GUARD_END
 }
 
-void zgpu_ctx_destroy(zgpu_ctx *c) { delete c; }
+void zgpu_ctx_destroy(zgpu_ctx *c) { ctx_unref(c); }
+
+int64_t zgpu_ctx_refcount(const zgpu_ctx *c) { return c ? c->refs.load() : 0; }
 
 int zgpu_chain_create(zgpu_ctx *ctx, const char *codecs_json, const char *data_type, const void *fill,
                       uint32_t fill_len, int validate, zgpu_chain **out) {
@@ -1738,15 +1759,21 @@ int zgpu_chain_create(zgpu_ctx *ctx, const char *codecs_json, const char *data_t
   if (fill) std::memcpy(f, fill, es);
   Json j = Json::parse(codecs_json);
   auto ch = std::make_unique<zgpu_chain>();
-  ch->ctx = ctx;
   ch->chain = parse_chain(j, data_type, f);
   ch->validate = validate != 0;
+  ctx_ref(ctx);
+  ch->ctx = ctx;
   *out = ch.release();
   return ZGPU_OK;
   ABI_GUARD_END
 }
 
-void zgpu_chain_destroy(zgpu_chain *c) { delete c; }
+void zgpu_chain_destroy(zgpu_chain *c) {
+  if (!c) return;
+  zgpu_ctx *ctx = c->ctx;
+  delete c;
+  ctx_unref(ctx);
+}
 
 uint32_t zgpu_chain_element_size(const zgpu_chain *c) { return c ? c->chain->es : 0; }
 
@@ -2166,6 +2193,7 @@ struct Coalescer {
   uint32_t window_us = 200, max_calls = 8;
   uint64_t max_bytes = 1ull << 30;
   uint64_t batches = 0, calls = 0, seq = 0;
+  uint64_t active = 0;  // coalescable calls inside coalesced_call (under mu)
 };
 
 // ZGPU_TRACE=1: one stderr line per coalesced-batch phase (microseconds since the first trace)
@@ -2415,6 +2443,7 @@ static int coalesced_call(zgpu_chain *ch, uint32_t nd, const zgpu_chunk_desc *de
   std::shared_ptr<CoBatch> B;
   bool leader = false;
   std::unique_lock<std::mutex> lk(K.mu);
+  K.active++;  // left below, once this call's batch is done (the lock is held there)
   auto it = K.open.find(key);
   if (it == K.open.end()) {
     B = std::make_shared<CoBatch>();
@@ -2439,9 +2468,12 @@ static int coalesced_call(zgpu_chain *ch, uint32_t nd, const zgpu_chunk_desc *de
   }
   if (leader) {
     // the batch takes joiners for the collect window, and then for as long as its leader waits for a
-    // free lane: under load (every lane decoding an earlier batch) batches grow by themselves
-    B->cv.wait_until(lk, std::chrono::steady_clock::now() + std::chrono::microseconds(K.window_us),
-                     [&] { return B->closed; });
+    // free lane: under load (every lane decoding an earlier batch) batches grow by themselves. A lone
+    // caller (no other coalescable call in flight on the context) does not wait: a single-threaded
+    // reader pays no collect window per chunk.
+    if (K.active > 1)
+      B->cv.wait_until(lk, std::chrono::steady_clock::now() + std::chrono::microseconds(K.window_us),
+                       [&] { return B->closed; });
     lk.unlock();
     int rc = 0;
     std::string err;
@@ -2486,6 +2518,7 @@ static int coalesced_call(zgpu_chain *ch, uint32_t nd, const zgpu_chunk_desc *de
   } else {
     B->cv.wait(lk, [&] { return me.done; });
   }
+  K.active--;
   lk.unlock();
   g_size_detail = me.sd;
   if (me.call_error) return set_err(me.rc, me.err);

@@ -127,7 +127,7 @@ def slab_mismatches(gathered, expected, slabs, axis: int = 0):
         a, b = gathered.narrow(axis, row, n), expected.narrow(axis, row, n)
         row += n
         if a.element_size() in (1, 2, 4, 8) and a.is_floating_point():
-            iv = {2: torch.int16, 4: torch.int32, 8: torch.int64}[a.element_size()]
+            iv = {1: torch.int8, 2: torch.int16, 4: torch.int32, 8: torch.int64}[a.element_size()]
             a, b = a.contiguous().view(iv), b.contiguous().view(iv)
         if not torch.equal(a, b):
             bad.append(r)
