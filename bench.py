@@ -416,6 +416,26 @@ class C3:
         self.out_shape = self.shape
         self.decoded_bytes = int(np.prod(self.shape)) * 4  # per rank per step
         self.parts = [(self.chain, self.descs, self.out, self.out_shape)]
+        if world > 1:
+            # C4: the slab is decoded in pieces of whole inner-chunk rows (32 array rows), one plan each,
+            # and every piece is sent to the root while the next one decodes (gather_slabs_overlapped)
+            from zarrs_amd.distributed import slab_pieces
+            self.pieces = slab_pieces(self.start, self.shape, self.INNER)
+            self.parts = []
+            for r0, n in self.pieces:
+                p0 = [self.start[0] + r0] + self.start[1:]
+                pd = []
+                for (si, sj, sk), (t, _) in self.shards.items():
+                    org = [si * S, sj * S, sk * S]
+                    s0 = [max(a, o) for a, o in zip(p0, org)]
+                    s1 = [min(a + b, o + S) for a, b, o in zip(p0, [n] + self.shape[1:], org)]
+                    if any(b <= a for a, b in zip(s0, s1)):
+                        continue
+                    pd.append(make_desc((t.data_ptr(), int(t.numel())), [S] * 3,
+                                        sel_start=[a - o for a, o in zip(s0, org)],
+                                        sel_shape=[b - a for a, b in zip(s0, s1)],
+                                        out_start=[a - b for a, b in zip(s0, p0)]))
+                self.parts.append((self.chain, pd, self.out.narrow(0, r0, n), [n] + self.shape[1:]))
         self.step_bytes = int(np.prod(self.SUB_SHAPE)) * 4  # the whole subset, all ranks
         self.gathered = None
         self.config = {"workload": "C3" + ("/C4" if world > 1 else "") +
@@ -431,14 +451,26 @@ class C3:
                      "written by tools/synth; decode(encode(x)) == x checked on device)")
         self.scaling = "strong"
 
+    def run_step(self, execute):
+        """C4 (N > 1): decode the slab piece by piece (execute(k) runs piece k's plan on the bench stream,
+        statuses read back) while the finished pieces travel to the root (RCCL isend / irecv straight into
+        place). gather_s records the step's exposed exchange: the time from this rank's last decode to
+        the completion of its sends (peers) or receives (root)."""
+        from zarrs_amd.distributed import gather_slabs_overlapped
+        done = []
+
+        def decode_piece(k, view):
+            assert view.data_ptr() == self.parts[k][2].data_ptr()
+            execute(k)
+            if k == len(self.parts) - 1:
+                done.append(time.perf_counter())
+        self.gathered = gather_slabs_overlapped(decode_piece, self.out, self.slabs, self.INNER, dst=0, out=self.full)
+        torch.cuda.synchronize()
+        if done:
+            self.gather_s.append(time.perf_counter() - done[0])
+
     def after_decode(self):
-        if self.world > 1:  # C4: the requested subset spans GPUs -> one gather to the root
-            from zarrs_amd.distributed import gather_slabs
-            torch.cuda.synchronize()
-            t0 = time.perf_counter()
-            self.gathered = gather_slabs(self.out, self.slabs, dst=0, out=self.full)
-            torch.cuda.synchronize()
-            self.gather_s.append(time.perf_counter() - t0)
+        pass
 
     def check(self) -> bool:
         ok = bool(torch.equal(self.out.view(torch.int32), self.expected.view(torch.int32)))
@@ -606,6 +638,19 @@ class C3:
             if rc:
                 raise L.ZgpuError(rc, L.last_error())
 
+        def plugin(c):  # the Rust plugin's decode_into: zgpu_decode_pinned, one copy into the view, release
+            chain, arr, n, _, flags, st, _, dst, sel, _ = c
+            data, res_h = C.c_void_p(), C.c_void_p()
+            rc = lib.zgpu_decode_pinned(chain._h, 3, arr, n, L.u64s(sel), flags | L.COALESCE, st, C.byref(data),
+                                        C.byref(res_h))
+            if rc:
+                raise L.ZgpuError(rc, L.last_error())
+            try:
+                nb = int(np.prod(sel)) * 4
+                out[dst] = np.ctypeslib.as_array((C.c_uint8 * nb).from_address(data.value)).view(np.float32).reshape(sel)
+            finally:
+                lib.zgpu_result_release(res_h)
+
         def isolated(c):
             chain, arr, n, _, flags, st, buf, dst, sel, _ = c
             rc = lib.zgpu_decode_batch(chain._h, 3, arr, n, buf.ctypes.data, L.u64s(sel), flags, st, None)
@@ -637,6 +682,9 @@ class C3:
             best = measure(coalesced, self.args.dropin_calls)
             res.update(best)
             res["max_calls_per_batch"] = self.args.dropin_calls
+            plug = measure(plugin, self.args.dropin_calls)
+            res["plugin_pattern_GiBps"], res["plugin_pattern_ms"] = plug["GiBps"], plug["ms"]
+            res["plugin_pattern_roundtrip_ok"] = plug["roundtrip_ok"]
             iso = measure(isolated, None)
             res["uncoalesced_GiBps"], res["uncoalesced_ms"] = iso["GiBps"], iso["ms"]
             res["uncoalesced_roundtrip_ok"] = iso["roundtrip_ok"]
@@ -646,11 +694,13 @@ class C3:
             self.args.ctx.set_coalescing(window_us=200, max_calls=16)
             wide = measure(coalesced, 16)
             res["threads_one_per_shard"] = {"threads": len(calls), "max_calls_per_batch": 16, **wide}
-        res["note"] = ("one synchronous host-in/host-out call per shard from a thread pool (the Rust plugin's pattern "
-                       "under zarrs' rayon loop), descriptor tables built before timing; GiBps: ZGPU_COALESCE + "
-                       "zgpu_decode_into the output window (200 us collect window, batches of <= max_calls_per_batch "
-                       "calls); uncoalesced_GiBps: isolated zgpu_decode_batch calls into a per-call buffer copied into "
-                       "the output")
+        res["note"] = ("one synchronous host-in/host-out call per shard from a thread pool (zarrs' rayon loop), "
+                       "descriptor tables built before timing; GiBps: ZGPU_COALESCE + zgpu_decode_into the output window "
+                       "(rows placed by the library: the C ABI's best case, what ArrayGpuExt-style callers holding the "
+                       "raw array get); plugin_pattern_GiBps: the Rust plugin's decode_into (zarrs' view exposes only "
+                       "copy_from_slice): ZGPU_COALESCE + zgpu_decode_pinned, one copy of the window into the array, "
+                       "zgpu_result_release; uncoalesced_GiBps: isolated zgpu_decode_batch calls into a per-call buffer "
+                       "copied into the output. Measured at the process's GPU_MAX_HW_QUEUES (hip_env)")
         return res
 
 # ------------------------------------------------------------------------------------------------
@@ -1213,9 +1263,20 @@ def run_gpu(args, rank, world, dev):
 
     pre = getattr(W, "pre_step", None)
 
+    def execute_part(pi):
+        plan, out, status = plans[part_plan[pi]]
+        rc = lib.zgpu_plan_execute(plan, out.data_ptr(), status, sp)
+        if rc:
+            raise RuntimeError(f"decode failed: {L.STATUS_NAMES[rc]} {L.last_error()}")
+
     def step():
         if pre:
             pre(sp)
+        if hasattr(W, "run_step") and world > 1:  # the workload drives its plans (C4: overlapped gather)
+            with torch.cuda.stream(stream):
+                W.run_step(execute_part)
+            W.after_decode()
+            return
         if len(plans) == 1:
             plan, out, status = plans[0]
             rc = lib.zgpu_plan_execute(plan, out.data_ptr(), status, sp)
@@ -1308,7 +1369,9 @@ def gather_report(r, world, dev):
     gbs = nbytes / (t * 1e-3) / 1e9 if t > 0 else 0.0
     return {"gather_ms": round(t, 3), "bytes_to_root": nbytes, "xgmi_GBps": round(gbs, 1), "peak_GBps": peak,
             "frac": round(gbs / peak, 4), "included_in_step": True,
-            "note": "grouped P2P receives into the root's output (RCCL over xGMI), timed inside the step"}
+            "note": "P2P receives straight into the root's output (RCCL over xGMI) inside the step; C3/C4: the "
+                    "slab is decoded in pieces of whole inner-chunk rows and each piece is sent while the next "
+                    "decodes, so gather_ms is only the exchange left after a rank's last piece (exposed time)"}
 
 
 def secondary_legs(args, rank, world, dev, r_primary):

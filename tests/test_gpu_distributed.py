@@ -149,3 +149,68 @@ def test_two_ranks_hip_decode_and_gather():
     for r in range(world):
         assert "error" not in out[r], out
         assert out[r] and all(out[r].values()), out
+
+
+def _overlap_worker(rank, world, port, q):
+    """C4 with the gather overlapped with the decode (gather_slabs_overlapped): each rank decodes its
+    axis-0 slab on the GPU in pieces of whole shard rows and sends each piece while the next decodes;
+    rank 0 receives every piece straight into place and checks EVERY slab against the oracle."""
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    import time
+    import torch
+    import torch.distributed as dist
+    import oracle as O
+    from zarrs_amd import Array, Context, DeviceStore, MemoryStore
+    from zarrs_amd.distributed import retrieve_array_subset_distributed, slab_mismatches, slab_partition
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    res = {}
+    try:
+        ctx = Context(0)
+        dev = torch.device("cuda", 0)
+        a = _c3_array()
+        shard = [16, 16, 16]
+        co = O.OracleChain.from_metadata(C3_CODECS, "float32", 0.0, 3)
+        shards = _encode_chunks(co, a, shard)
+        store = DeviceStore.from_store(MemoryStore({"c/" + "/".join(map(str, k)): v for k, v in shards.items()}))
+        meta = {"shape": list(a.shape), "data_type": "float32", "fill_value": 0.0, "codecs": C3_CODECS,
+                "chunk_grid": {"name": "regular", "configuration": {"chunk_shape": shard}}}
+        arr = Array(store, meta, ctx)
+        for name, (start, shape, rows) in {"shard_rows": ([5, 3, 7], [57, 40, 33], 16),
+                                          "inner_rows": ([1, 0, 0], [63, 48, 48], 8)}.items():
+            dist.barrier()
+            t0 = time.perf_counter()
+            got = retrieve_array_subset_distributed(arr, start, shape, device=dev, piece_rows=rows)
+            torch.cuda.synchronize()
+            res[name + "_ms"] = (time.perf_counter() - t0) * 1e3
+            if rank == 0:
+                exp = O.retrieve_array_subset(co, list(a.shape), shard, shards, start, shape, nthreads=4)
+                bad = slab_mismatches(got.cpu(), torch.from_numpy(exp), slab_partition(start, shape, world))
+                res[name] = got.is_cuda and not bad
+            else:
+                res[name] = got is None
+        torch.cuda.synchronize()
+    except Exception as e:  # noqa: BLE001 - reported through the queue
+        res["error"] = repr(e)
+    finally:
+        q.put((rank, res))
+        dist.destroy_process_group()
+
+
+def test_three_ranks_overlapped_gather_hip_decode():
+    import torch.multiprocessing as mp
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    world = 3
+    procs = [ctx.Process(target=_overlap_worker, args=(r, world, port, q)) for r in range(world)]
+    for p in procs:
+        p.start()
+    out = dict(q.get(timeout=100) for _ in range(world))
+    for p in procs:
+        p.join(timeout=30)
+        assert p.exitcode == 0
+    for r in range(world):
+        assert "error" not in out[r], out
+        assert all(v for k, v in out[r].items() if not k.endswith("_ms")), out
+    print({r: {k: round(v, 2) for k, v in out[r].items() if k.endswith("_ms")} for r in out})

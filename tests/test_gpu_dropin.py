@@ -286,3 +286,46 @@ def test_coalesce_flag_with_uncovered_window_takes_direct_path(ctx, data):
     assert np.array_equal(out[win], a[win])
     rest = (slice(o[0], o[0] + SH), slice(o[1], o[1] + SH), slice(o[2] + SH, o[2] + 2 * SH))
     assert np.all(out[rest] == SENTINEL)
+
+
+@pytest.mark.parametrize("coalesce", [False, True])
+def test_decode_pinned_plugin_pattern(ctx, data, coalesce):
+    """zgpu_decode_pinned (the Rust plugin's decode_into: the decoded window stays in library pinned
+    memory and the caller copies it once into its view) from 16 threads: full shards and partial
+    selections, one corrupt caller that gets its own INVALID_CHECKSUM and no data."""
+    from zarrs_amd import CodecChain, ZgpuError, make_desc
+    a, shards = data
+    ctx.set_coalescing(window_us=2000, max_calls=6)
+    ch = CodecChain.from_metadata(CODECS, "float32", 0.0, ctx)
+    inner = CodecChain.from_metadata(INNER_CODECS, "float32", 0.0, ctx)
+    out = np.full(SHAPE, SENTINEL, np.float32)
+    bad = (0, 1, 2)
+    src = dict(shards)
+    src[bad] = _corrupt(shards[bad], 5)
+    keys = sorted(src)
+    barrier = threading.Barrier(len(keys))
+
+    def one(key):
+        barrier.wait()
+        o = _origin(key)
+        try:
+            if sum(key) % 2:  # full shard: the sharded chain, index verified
+                return ch.decode_pinned_into([make_desc(src[key], [SH] * 3)], out, o, [SH] * 3, coalesce=coalesce)
+            return ch.decode_pinned_into([make_desc(src[key], [SH] * 3, [0, 0, 0], [SH, SH, 40])], out, o,
+                                         [SH, SH, 40], coalesce=coalesce)
+        except ZgpuError as e:
+            return e.status
+    with ThreadPoolExecutor(len(keys)) as ex:
+        res = dict(zip(keys, ex.map(one, keys)))
+    mask = np.ones(SHAPE, bool)
+    for key, v in res.items():
+        o = _origin(key)
+        full = sum(key) % 2 == 1
+        if key == bad and full:
+            assert v == 1, (key, v)
+            continue
+        assert v == [0], (key, v)
+        win = tuple(slice(s_, s_ + n_) for s_, n_ in zip(o, [SH] * 3 if full else [SH, SH, 40]))
+        assert np.array_equal(out[win], a[win]), key
+        mask[win] = False
+    assert np.all(out[mask] == SENTINEL)  # the corrupt caller's window and the unselected parts

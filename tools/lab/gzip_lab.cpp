@@ -5,6 +5,7 @@
 #include <hip/hip_runtime.h>
 #include <zlib.h>
 
+#include <algorithm>
 #include <cmath>
 #include <cstdio>
 #include <cstdlib>
@@ -58,6 +59,15 @@ int main(int argc, char **argv) {
     deflateEnd(&s);
     total += s.total_out;
   }
+  if (getenv("LAB_SAME")) {  // every chunk a copy of chunk LAB_SAME (content variance out of the timing)
+    const int src = atoi(getenv("LAB_SAME")) % n;
+    total = 0;
+    for (int c = 0; c < n; c++) {
+      enc[c] = enc[src];
+      memcpy(&dec[(size_t)c * E * E * E], &dec[(size_t)src * E * E * E], NB);
+      total += enc[c].size();
+    }
+  }
   printf("%d chunks, %.1f MiB encoded, ratio %.3f\n", n, total / 1048576.0, (double)n * NB / total);
   // pack encoded (256-B aligned) on device
   std::vector<uint64_t> off(n);
@@ -87,7 +97,7 @@ int main(int argc, char **argv) {
     CK(hipMemcpy(d_items, items.data(), n * sizeof(ZgItem), hipMemcpyHostToDevice));
     CK(hipMemset(d_status, 0, n * 4));
 #ifdef ZG_PROFILE
-    unsigned long long z[8] = {0};
+    unsigned long long z[16] = {0};
     CK(hipMemcpyToSymbol(HIP_SYMBOL(zgpu::g_prof), z, sizeof(z)));
 #endif
     CK(hipEventRecord(e0));
@@ -97,7 +107,29 @@ int main(int argc, char **argv) {
     float ms; CK(hipEventElapsedTime(&ms, e0, e1));
     if (ms < best) best = ms;
   }
-  unsigned long long prof[8] = {0, 0, 0, 0, 1, 0, 0, 0};
+  if (getenv("LAB_EACH")) {  // every stream alone: the per-stream latency distribution
+    std::vector<std::pair<float, int>> t(n);
+    for (int c = 0; c < n; c++) {
+      float b1 = 1e30f;
+      for (int rep = 0; rep < 2; rep++) {
+        CK(hipMemcpy(d_items + c, &items[c], sizeof(ZgItem), hipMemcpyHostToDevice));
+        CK(hipMemset(d_status + c, 0, 4));
+        CK(hipEventRecord(e0));
+        CK(zgpu::launch_gzip(d_items + c, d_status + c, 1, d_out + (size_t)c * slot, slot, nullptr, d_seg, 0));
+        CK(hipEventRecord(e1));
+        CK(hipEventSynchronize(e1));
+        float ms; CK(hipEventElapsedTime(&ms, e0, e1));
+        b1 = std::min(b1, ms);
+      }
+      t[c] = {b1, c};
+    }
+    std::sort(t.begin(), t.end());
+    printf("per-stream latency: min %.3f  p50 %.3f  p90 %.3f  p99 %.3f  max %.3f ms\n", t[0].first, t[n / 2].first,
+           t[n * 9 / 10].first, t[n * 99 / 100].first, t[n - 1].first);
+    for (int k = n - 1; k >= 0 && k >= n - 6; k--)
+      printf("  slow: chunk %d %.3f ms, %zu B encoded\n", t[k].second, t[k].first, enc[t[k].second].size());
+  }
+  unsigned long long prof[16] = {0, 0, 0, 0, 1};
 #ifdef ZG_PROFILE
   CK(hipMemcpyFromSymbol(prof, HIP_SYMBOL(zgpu::g_prof), sizeof(prof)));
 #endif
@@ -117,6 +149,13 @@ int main(int argc, char **argv) {
              (double)prof[i] / n);
     else
       printf("  %-12s %6.1f%%  %.0f cycles/chunk\n", names[i], 100.0 * prof[i] / tot, (double)prof[i] / n);
+  if (prof[12])
+    printf("  header detail: %.1f blocks/chunk; per chunk cycles: code lengths %.0f, litlen table %.0f, dist table %.0f, "
+           "trailer crc %.0f\n", (double)prof[12] / n, (double)prof[8] / n, (double)prof[9] / n, (double)prof[10] / n,
+           (double)prof[11] / n);
+  if (prof[13])
+    printf("  segmented decode: %.1f rounds/chunk, repair loop %.0f cycles/chunk\n", (double)prof[13] / n,
+           (double)prof[14] / n);
   if (prof[6])
     printf("  per chunk: %.0f batches, %.1f symbols/batch, %.2f match rounds/batch\n", (double)prof[6] / n,
            (double)prof[7] / prof[6], (double)prof[5] / prof[6]);

@@ -40,7 +40,7 @@ EXPORTS = [
     "zgpu_last_size_mismatch", "zgpu_cache_create", "zgpu_cache_destroy", "zgpu_cache_clear", "zgpu_cache_stats",
     "zgpu_cache_retrieve_array_subset", "zgpu_retrieve_array_subset_dlpack", "zgpu_chain_encoded_bound",
     "zgpu_encode_chunks", "zgpu_retrieve_array_subset_multi", "zgpu_decode_into", "zgpu_ctx_set_coalescing",
-    "zgpu_ctx_coalescing_stats", "zgpu_ctx_refcount",
+    "zgpu_ctx_coalescing_stats", "zgpu_ctx_refcount", "zgpu_decode_pinned", "zgpu_result_release",
 ]
 CTR_ENC_BYTES, CTR_ZSTD_SERIAL, CTR_ZSTD_PARALLEL, CTR_BLOSC_RERUN, CTR_BLOSC_BLOCKS = range(5)
 N_COUNTERS = 5
@@ -121,6 +121,10 @@ def load() -> C.CDLL:
     P64 = C.POINTER(C.c_uint64)
     L.zgpu_ctx_create.argtypes = [i32, C.POINTER(vp)]
     L.zgpu_ctx_destroy.argtypes = [vp]
+    L.zgpu_decode_pinned.argtypes = [vp, C.c_uint32, vp, C.c_uint64, vp, C.c_uint32, vp, C.POINTER(C.c_void_p),
+                                     C.POINTER(C.c_void_p)]
+    L.zgpu_result_release.argtypes = [vp]
+    L.zgpu_result_release.restype = None
     L.zgpu_ctx_refcount.argtypes = [vp]
     L.zgpu_ctx_refcount.restype = C.c_int64
     L.zgpu_last_error.restype = C.c_char_p

@@ -219,6 +219,33 @@ class CodecChain:
             raise L.ZgpuError(rc, L.last_error())
         return statuses
 
+    def decode_pinned_into(self, descs: Sequence[L.ChunkDesc], array: np.ndarray, view_start, view_shape,
+                           validate_checksums: bool | None = None, coalesce: bool = False) -> list:
+        """The codec plugin's decode_into (rust/zarrs_gpu): host inputs decoded by zgpu_decode_pinned into
+        library-owned pinned memory, then ONE copy of the compact window into the caller's view
+        (ArrayBytesFixedDisjointView::copy_from_slice, array_bytes_fixed_disjoint_view.rs:177-206; here
+        a numpy slice assignment), then zgpu_result_release. Descriptors' out_start are window-relative."""
+        n = len(descs)
+        arr = (L.ChunkDesc * max(n, 1))(*descs)
+        arr._keep = [getattr(d, "_keep", None) for d in descs]
+        st = (C.c_int32 * max(n, 1))()
+        flags = (L.COALESCE if coalesce else 0) | (L.NO_VALIDATE if validate_checksums is False else 0)
+        data, res = C.c_void_p(), C.c_void_p()
+        lib = L.load()
+        rc = lib.zgpu_decode_pinned(self._h, len(view_shape), arr, n, L.u64s(view_shape), flags, st, C.byref(data),
+                                    C.byref(res))
+        statuses = [st[i] for i in range(n)]
+        if rc:
+            raise L.ZgpuError(rc, L.last_error())
+        try:
+            count = int(np.prod(view_shape))
+            src = np.ctypeslib.as_array((C.c_uint8 * (count * self.dtype.itemsize)).from_address(data.value))
+            win = tuple(slice(int(a), int(a) + int(b)) for a, b in zip(view_start, view_shape))
+            array[win] = src.view(array.dtype).reshape([int(x) for x in view_shape])
+        finally:
+            lib.zgpu_result_release(res)
+        return statuses
+
     # ---- per-chunk forms (degenerate batches) ------------------------------------------------
     def decode(self, encoded, shape) -> np.ndarray:
         out = np.empty([int(s) for s in shape], dtype=self.dtype)

@@ -43,13 +43,13 @@ namespace zgpu {
 
 #ifdef ZG_PROFILE
 // lab builds only (tools/lab): per-phase shader-clock totals, summed over waves
-__device__ unsigned long long g_prof[8];
+__device__ unsigned long long g_prof[16];
 // per-wave accumulators (prof_acc[], declared by PROF_DECL), flushed once per wave by PROF_FLUSH
-#define PROF_DECL uint64_t prof_acc[8] = {0, 0, 0, 0, 0, 0, 0, 0}
+#define PROF_DECL uint64_t prof_acc[16] = {0}
 #define PROF_T(v) const uint64_t v = clock64()
 #define PROF_ADD(slot, t0) prof_acc[slot] += clock64() - (t0)
 #define PROF_CNT(slot, n) prof_acc[slot] += (n)  // event counts: 5 match rounds, 6 batches, 7 symbols
-#define PROF_FLUSH do { if (__lane_id() == 0) for (int k_ = 0; k_ < 8; k_++) atomicAdd(&g_prof[k_], (unsigned long long)prof_acc[k_]); } while (0)
+#define PROF_FLUSH do { if (__lane_id() == 0) for (int k_ = 0; k_ < 16; k_++) atomicAdd(&g_prof[k_], (unsigned long long)prof_acc[k_]); } while (0)
 #else
 #define PROF_DECL
 #define PROF_FLUSH
@@ -158,6 +158,7 @@ struct Smem {
   };
   uint64_t crc_len[1];
   uint32_t crc_val[1];
+  uint8_t sink[4];  // the executor's discarded byte stores (branch-free short copies)
   uint16_t lsorted[288];
   uint16_t dsorted[32];
   HuffMeta lm, dm, cm;
@@ -374,25 +375,23 @@ __device__ bool build_table(const uint8_t *lens, uint32_t n, uint32_t root, uint
     tmp[0] = 0;  // subtable allocation counter (the counts were read above)
   }
   __syncthreads();
-  // sorted symbols (by length, then symbol) via ballot ranks
-  uint32_t base[16];
-  {
-    uint32_t off = 0;
-    for (int l = 0; l < 16; l++) {
-      base[l] = off;
-      off += (l ? cnt[l] : 0);
-    }
+  // sorted symbols (by length, then symbol) via ballot ranks. The per-length offsets and codes are
+  // read from M in LDS (uniform addresses): private arrays indexed by a loop variable would live in
+  // scratch memory (one scratch round trip per access; 17 % of k_gzip's time went to table builds)
+  uint32_t lv[5];  // n <= 320 lengths: five per lane
+#pragma unroll
+  for (int j = 0; j < 5; j++) {
+    const uint32_t s = 64u * j + (uint32_t)lane;
+    lv[j] = s < n ? lens[s] : 0u;
   }
-  for (uint32_t s0 = 0; s0 < n; s0 += 64) {
-    const uint32_t s = s0 + lane;
-    const uint32_t l = s < n ? lens[s] : 0;
-    for (int L = 1; L <= (int)maxlen; L++) {
-      const uint64_t m = __ballot(l == (uint32_t)L);
-      if (l == (uint32_t)L) {
-        const uint32_t rank = __builtin_popcountll(m & ((1ull << lane) - 1));
-        sorted[base[L] + rank] = (uint16_t)s;
-      }
-      base[L] += __builtin_popcountll(m);
+  for (uint32_t L = 1; L <= maxlen; L++) {
+    uint32_t b = U(M.offs[L]);
+#pragma unroll
+    for (int j = 0; j < 5; j++) {
+      if (64u * j >= n) break;
+      const uint64_t m = __ballot(lv[j] == L);
+      if (lv[j] == L) sorted[b + __builtin_popcountll(m & ((1ull << lane) - 1))] = (uint16_t)(64u * j + lane);
+      b += __builtin_popcountll(m);
     }
   }
   __syncthreads();
@@ -405,17 +404,17 @@ __device__ bool build_table(const uint8_t *lens, uint32_t n, uint32_t root, uint
     uint32_t entry = (K_BAD << 4) | 0xF;  // invalid code marker (len 15 so it is consumed; flagged bad)
     bool found = false;
     for (uint32_t L = 1; L <= root && L <= maxlen && !found; L++) {
-      const uint32_t c = v >> (root - L);
-      if (c - first[L] < cnt[L]) {
-        entry = table_entry(kind, sorted[M.offs[L] + c - first[L]], L);
+      const uint32_t c = v >> (root - L), f = M.first[L];
+      if (c - f < M.count[L]) {
+        entry = table_entry(kind, sorted[M.offs[L] + c - f], L);
         found = true;
       }
     }
     if (!found && maxlen > root) {
       uint32_t sb = 0;
       for (uint32_t L = root + 1; L <= maxlen; L++) {
-        const uint32_t lo = v << (L - root), hi = (v + 1) << (L - root);
-        if (cnt[L] && first[L] < hi && first[L] + cnt[L] > lo) sb = L - root;
+        const uint32_t lo = v << (L - root), hi = (v + 1) << (L - root), f = M.first[L], k = M.count[L];
+        if (k && f < hi && f + k > lo) sb = L - root;
       }
       if (sb) {
         const uint32_t base = atomicAdd(&tmp[0], 1u << sb);
@@ -426,9 +425,9 @@ __device__ bool build_table(const uint8_t *lens, uint32_t n, uint32_t root, uint
             const uint32_t cf = (v << sb) | rev_bits(x, sb);  // MSB-first code of root + sb bits
             uint32_t se = (K_BAD << 4) | 0xF;
             for (uint32_t L = root + 1; L <= root + sb; L++) {
-              const uint32_t c = cf >> (root + sb - L);
-              if (c - first[L] < cnt[L]) {
-                se = table_entry(kind, sorted[M.offs[L] + c - first[L]], L);
+              const uint32_t c = cf >> (root + sb - L), f = M.first[L];
+              if (c - f < M.count[L]) {
+                se = table_entry(kind, sorted[M.offs[L] + c - f], L);
                 break;
               }
             }
@@ -437,7 +436,7 @@ __device__ bool build_table(const uint8_t *lens, uint32_t n, uint32_t root, uint
         }
       }
     }
-    tab[e] = entry;
+  tab[e] = entry;
   }
   __syncthreads();
   return true;
@@ -747,7 +746,9 @@ __device__ __forceinline__ bool exec_batch(Smem &S, uint8_t *out, uint64_t cap, 
     XPROF(5, 1);
     bool ready = false;
     if (pending) {
-#if ZG_INFLATE_RANGE
+#if ZG_EXP_ONEROUND  // lab experiment only (wrong output): every match ready in the first round
+      ready = true;
+#elif ZG_INFLATE_RANGE
       ready = (pm & rmask) == 0;
 #else
       const uint64_t m = hi < 0 ? 0ull : pm & (hi >= 63 ? ~0ull : ((2ull << hi) - 1));
@@ -784,7 +785,26 @@ __device__ __forceinline__ bool exec_batch(Smem &S, uint8_t *out, uint64_t cap, 
     if (lm && lane == __builtin_ctzll(lm)) pending = false;
     ready = ready && mlen <= 32;
     const bool in_ring = msrc + RING >= batch_end;
-#if ZG_INFLATE_XW
+#if ZG_INFLATE_XW == 8
+    if (ready && in_ring && mlen <= 8) {
+      // a short match whose source is in the ring (99 % of C3's): the 8 bytes from the source start
+      // as two byte-aligned words of three aligned ring reads, byte k of the copy = source byte
+      // k mod d (an overlapping copy repeats its period); 8 unconditional byte stores, the ones past
+      // the match's length into a sink byte (no exec-mask branches)
+      const uint32_t a0 = (uint32_t)(msrc >> 2), sh = (uint32_t)(msrc & 3);
+      const uint32_t w0 = S.ring32[a0 & (RING / 4 - 1)], w1 = S.ring32[(a0 + 1) & (RING / 4 - 1)],
+                     w2 = S.ring32[(a0 + 2) & (RING / 4 - 1)];
+      const uint64_t V = ((uint64_t)__builtin_amdgcn_alignbyte(w2, w1, sh) << 32) | __builtin_amdgcn_alignbyte(w1, w0, sh);
+      uint32_t r = 0;
+#pragma unroll
+      for (uint32_t k = 0; k < 8; k++) {
+        uint8_t *dst = k < mlen ? &S.ring[(mypos + k) & RMASK] : &S.sink[0];
+        *dst = (uint8_t)(V >> (8 * r));
+        r = r + 1 == md ? 0u : r + 1;
+      }
+      pending = false;
+    } else
+#elif ZG_INFLATE_XW
     if (ready && in_ring && md >= mlen && mlen <= ZG_INFLATE_XW) {
       // a short source wholly in the ring, not overlapping the copy: aligned ring words (all
       // loads in flight together), byte-aligned in registers
@@ -803,14 +823,16 @@ __device__ __forceinline__ bool exec_batch(Smem &S, uint8_t *out, uint64_t cap, 
     } else
 #endif
     if (ready) {
+      // byte i of the copy takes source byte i mod d: the remainder advanced per byte (no division)
+      uint32_t r = 0;
       for (uint32_t i0 = 0; i0 < mlen; i0 += 4) {
         uint8_t v[4];
 #pragma unroll
         for (int k = 0; k < 4; k++) {
           const uint32_t i = i0 + k;
-          const uint32_t r = i < md ? i : i % md;
           const uint64_t src = msrc + r;
           v[k] = (i < mlen) ? (in_ring ? S.ring[src & RMASK] : __builtin_nontemporal_load(out + src)) : 0;
+          r = r + 1 == md ? 0u : r + 1;
         }
 #pragma unroll
         for (int k = 0; k < 4; k++)
@@ -851,7 +873,26 @@ __device__ __forceinline__ bool exec_batch(Smem &S, uint8_t *out, uint64_t cap, 
     }
     const bool ready = pending && mlen <= 32 && (lane == first || msrc + mlen <= F);
     const bool in_ring = msrc + RING >= batch_end;
-#if ZG_INFLATE_XW
+#if ZG_INFLATE_XW == 8
+    if (ready && in_ring && mlen <= 8) {
+      // a short match whose source is in the ring (99 % of C3's): the 8 bytes from the source start
+      // as two byte-aligned words of three aligned ring reads, byte k of the copy = source byte
+      // k mod d (an overlapping copy repeats its period); 8 unconditional byte stores, the ones past
+      // the match's length into a sink byte (no exec-mask branches)
+      const uint32_t a0 = (uint32_t)(msrc >> 2), sh = (uint32_t)(msrc & 3);
+      const uint32_t w0 = S.ring32[a0 & (RING / 4 - 1)], w1 = S.ring32[(a0 + 1) & (RING / 4 - 1)],
+                     w2 = S.ring32[(a0 + 2) & (RING / 4 - 1)];
+      const uint64_t V = ((uint64_t)__builtin_amdgcn_alignbyte(w2, w1, sh) << 32) | __builtin_amdgcn_alignbyte(w1, w0, sh);
+      uint32_t r = 0;
+#pragma unroll
+      for (uint32_t k = 0; k < 8; k++) {
+        uint8_t *dst = k < mlen ? &S.ring[(mypos + k) & RMASK] : &S.sink[0];
+        *dst = (uint8_t)(V >> (8 * r));
+        r = r + 1 == md ? 0u : r + 1;
+      }
+      pending = false;
+    } else
+#elif ZG_INFLATE_XW
     if (ready && in_ring && md >= mlen && mlen <= ZG_INFLATE_XW) {
       // a short source wholly in the ring, not overlapping the copy: aligned ring words (all
       // loads in flight together), byte-aligned in registers
@@ -870,14 +911,16 @@ __device__ __forceinline__ bool exec_batch(Smem &S, uint8_t *out, uint64_t cap, 
     } else
 #endif
     if (ready) {
+      // byte i of the copy takes source byte i mod d: the remainder advanced per byte (no division)
+      uint32_t r = 0;
       for (uint32_t i0 = 0; i0 < mlen; i0 += 4) {
         uint8_t v[4];
 #pragma unroll
         for (int k = 0; k < 4; k++) {
           const uint32_t i = i0 + k;
-          const uint32_t r = i < md ? i : i % md;
           const uint64_t src = msrc + r;
           v[k] = (i < mlen) ? (in_ring ? S.ring[src & RMASK] : __builtin_nontemporal_load(out + src)) : 0;
+          r = r + 1 == md ? 0u : r + 1;
         }
 #pragma unroll
         for (int k = 0; k < 4; k++)
@@ -1012,15 +1055,17 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(ZG_INFLATE_W
     if (type == 1) {
       build_fixed_lens(S.lens);
     } else {  // ---- dynamic header ----
+      PROF_T(t_cl);
       hlit = bits_get(B, 5) + 257;
       hdist = bits_get(B, 5) + 1;
       const uint32_t hclen = bits_get(B, 4) + 4;
       if (hlit > 286 || hdist > 30) { err = ZG_CORRUPT_STREAM; break; }
-      uint32_t cl[19];
-      for (int k = 0; k < 19; k++) cl[k] = 0;
-      for (uint32_t k = 0; k < hclen; k++) cl[k] = bits_get(B, 3);
-      if (lane == 0)
-        for (int k = 0; k < 19; k++) S.clens[c_clen_order[k]] = (uint8_t)cl[k];
+      if (lane < 20) S.clens[lane] = 0;
+      __syncthreads();
+      for (uint32_t k = 0; k < hclen; k++) {  // (a private array indexed by k would live in scratch)
+        const uint32_t v = bits_get(B, 3);
+        if (lane == 0) S.clens[c_clen_order[k]] = (uint8_t)v;
+      }
       __syncthreads();
       if (!build_table(S.clens, 19, 7, S.ltab, S.csorted, S.cm, 2, S.tmp, 0)) { err = ZG_CORRUPT_STREAM; break; }
       // code lengths for literal/length + distance alphabets (ltab used as a 128-entry 7-bit table)
@@ -1063,9 +1108,15 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(ZG_INFLATE_W
       }
       __syncthreads();
       if (U(S.lens[256]) == 0) { err = ZG_CORRUPT_STREAM; break; }  // missing end-of-block code
+      PROF_ADD(8, t_cl);
     }
+    PROF_T(t_lt);
     if (!build_table(S.lens, 288, LROOT, S.ltab, S.lsorted, S.lm, 0, S.tmp, LSUB)) { err = ZG_CORRUPT_STREAM; break; }
+    PROF_ADD(9, t_lt);
+    PROF_T(t_dt);
     if (!build_table(S.lens + 288, 32, DROOT, S.dtab, S.dsorted, S.dm, 1, S.tmp, DSUB)) { err = ZG_CORRUPT_STREAM; break; }
+    PROF_ADD(10, t_dt);
+    PROF_CNT(12, 1);  // blocks
     PROF_ADD(0, t_hdr);
     (void)hlit;
     (void)hdist;
@@ -1090,6 +1141,8 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(ZG_INFLATE_W
         uint32_t n;
         uint64_t mask;
         uint32_t st = seg_decode(S, R, p, s_own, s_end, end_bits, myrec, n, mask);
+        PROF_CNT(13, 1);  // rounds
+        PROF_T(t_rep);
         uint32_t skip = 0;
         bool ok = lane == 0;
         bool repaired = false;
@@ -1122,6 +1175,7 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(ZG_INFLATE_W
           // the lanes after j re-check against the updated exits; the earlier ones stay right
           PROF_CNT(3, 1);
         }
+        PROF_ADD(14, t_rep);
         // the round ends at the last valid lane
         const uint64_t vm = __ballot(ok);
         const int J = (vm == ~0ull) ? 64 : __builtin_ctzll(~vm);
@@ -1202,7 +1256,10 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(ZG_INFLATE_W
 #if ZG_INFLATE_XFETCH
           if (g + bc < total) rec_next = fetch(g + bc);  // in flight while this batch executes
 #endif
-#ifdef ZG_PROFILE
+#if ZG_EXP_NOEXEC  // lab experiment only (wrong output): records fetched and batched, not executed
+          pos += bytes;
+          if (__ballot(rec == 0xFFFFFFFFu)) err = ZG_CORRUPT_STREAM;
+#elif defined(ZG_PROFILE)
           if (!exec_batch(S, out, cap, pos, flushed, bc, bytes, rec, prof_acc)) err = ZG_CORRUPT_STREAM;
 #else
           if (!exec_batch(S, out, cap, pos, flushed, bc, bytes, rec, nullptr)) err = ZG_CORRUPT_STREAM;
@@ -1406,8 +1463,10 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(ZG_INFLATE_W
         // second kernel re-reading every decoded byte.
         __threadfence_block();
         __syncthreads();
+        PROF_T(t_crc);
         build_tables(S.crc, POLY_CRC32);
         const uint32_t c = wg_crc(out, pos, S.crc, POLY_CRC32, S.crc_len, S.crc_val);
+        PROF_ADD(11, t_crc);
         if (c != crc || isz != (uint32_t)pos) err = ZG_CORRUPT_STREAM;
       }
     }

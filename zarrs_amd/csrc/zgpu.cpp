@@ -2420,8 +2420,22 @@ static uint8_t *pin_caller_inputs(zgpu_ctx *C, const zgpu_chunk_desc *descs, uin
   return pin;
 }
 
+// zgpu_decode_pinned's result: a pooled pinned buffer of the context, or a slice of a coalesced
+// batch's pack (the batch, and with it the pack, lives until every caller released its result)
+struct zgpu_result {
+  zgpu_ctx *ctx = nullptr;
+  uint8_t *own = nullptr;             // pooled pinned buffer (uncoalesced call)
+  std::shared_ptr<CoBatch> batch;     // coalesced call: the batch holding the pack
+  ~zgpu_result() {
+    if (own) ctx->host_free(own);
+    batch.reset();
+    ctx_unref(ctx);
+  }
+};
+
 static int coalesced_call(zgpu_chain *ch, uint32_t nd, const zgpu_chunk_desc *descs, uint64_t n,
-                          const zgpu_out_view &V, uint32_t flags, int32_t *status) {
+                          const zgpu_out_view &V, uint32_t flags, int32_t *status,
+                          zgpu_result **keep = nullptr, const void **keep_data = nullptr) {
   zgpu_ctx *C = ch->ctx;
   Coalescer &K = coalescer(C);
   static const bool pin_in = [] {
@@ -2522,6 +2536,16 @@ static int coalesced_call(zgpu_chain *ch, uint32_t nd, const zgpu_chunk_desc *de
   lk.unlock();
   g_size_detail = me.sd;
   if (me.call_error) return set_err(me.rc, me.err);
+  if (keep) {  // zgpu_decode_pinned: the caller copies its compact window out of the pack itself
+    auto *R = new zgpu_result();
+    ctx_ref(C);
+    R->ctx = C;
+    R->batch = B;
+    *keep = R;
+    *keep_data = B->pack + me.pack_off;
+    if (me.rc) set_err(me.rc, zgpu_status_name(me.rc));
+    return me.rc;
+  }
   // this caller's window: its rows placed from the pinned pack by this caller's own thread (the
   // batch's callers do this in parallel)
   const BoxRuns R = box_runs(nd, V.array_shape, V.start, V.shape, ch->chain->es);
@@ -2554,6 +2578,56 @@ static int decode_entry(zgpu_chain *ch, uint32_t nd, const zgpu_chunk_desc *desc
 static void delete_coalescer(Coalescer *co) { delete co; }
 
 extern "C" {
+
+int zgpu_decode_pinned(zgpu_chain *ch, uint32_t nd, const zgpu_chunk_desc *descs, uint64_t n, const uint64_t *out_shape,
+                       uint32_t flags, int32_t *status, const void **data, zgpu_result **result) {
+  ABI_GUARD_BEGIN
+  if (data) *data = nullptr;
+  if (result) *result = nullptr;
+  if (!ch || !out_shape || (n && !descs) || !data || !result) return set_err(ZGPU_INVALID_ARGUMENT, "NULL argument");
+  if (nd == 0 || nd > ZGPU_MAX_DIMS) return set_err(ZGPU_INVALID_ARGUMENT, "ndim out of range");
+  if (flags & (ZGPU_ENC_DEVICE | ZGPU_OUT_DEVICE))
+    return set_err(ZGPU_INVALID_ARGUMENT, "zgpu_decode_pinned takes host inputs and returns host memory");
+  zgpu_ctx *C = ch->ctx;
+  HIPCHK(hipSetDevice(C->device));
+  reset_call_state();
+  const uint64_t bytes = volume(out_shape, nd) * ch->chain->es;
+  if ((flags & ZGPU_COALESCE) && n && covered_volume(descs, n, nd) == volume(out_shape, nd)) {
+    zgpu_out_view V{};
+    V.base = nullptr;  // never written: the result stays in the pack
+    for (uint32_t d = 0; d < nd; d++) V.array_shape[d] = V.shape[d] = out_shape[d];
+    zgpu_result *R = nullptr;
+    const void *p = nullptr;
+    const int rc = coalesced_call(ch, nd, descs, n, V, flags & ~ZGPU_COALESCE, status, &R, &p);
+    if (rc) {
+      delete R;
+      return rc;
+    }
+    *result = R;
+    *data = p;
+    return ZGPU_OK;
+  }
+  // one call: its own pooled pinned buffer (pinned host output takes the overlapped D2H paths)
+  std::unique_ptr<zgpu_result> R(new zgpu_result());
+  ctx_ref(C);
+  R->ctx = C;
+  R->own = (uint8_t *)C->host_alloc(bytes ? bytes : 1);
+  zgpu_out_view V{};
+  V.base = R->own;
+  for (uint32_t d = 0; d < nd; d++) V.array_shape[d] = V.shape[d] = out_shape[d];
+  if (covered_volume(descs, n, nd) != volume(out_shape, nd) && bytes)  // parts no descriptor covers: zero
+    std::memset(R->own, 0, bytes);
+  LaneScope ls(C);
+  hipStream_t s = pick_stream(ls.L, nullptr);
+  const int rc = decode_call(ch, ls.L, s, nd, descs, n, V, flags & ~ZGPU_COALESCE, status);
+  if (rc) return set_err(rc, zgpu_status_name(rc));
+  *data = R->own;
+  *result = R.release();
+  return ZGPU_OK;
+  ABI_GUARD_END
+}
+
+void zgpu_result_release(zgpu_result *r) { delete r; }
 
 int zgpu_decode_batch(zgpu_chain *ch, uint32_t nd, const zgpu_chunk_desc *descs, uint64_t n, void *out,
                       const uint64_t *out_shape, uint32_t flags, int32_t *status, void *stream) {

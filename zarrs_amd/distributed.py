@@ -13,6 +13,8 @@ read is partitioned and each rank decodes its share on its own GPU with no data-
                    its rows of the root's output (grouped send/recv: RCCL over xGMI on GPUs, gloo
                    on CPU), skipped at N=1
 
+  gather_slabs_overlapped  the same exchange overlapped with the decode: slabs decoded in pieces of
+                   whole chunk rows, each piece sent while the next one decodes (C4)
   gather_regions   chunk-partitioned ranks (LPT): every rank's chunk boxes of one subset; boxes that are
                    contiguous runs of the subset are received straight into place, the others are
                    packed into one message per rank and unpacked on the root
@@ -115,6 +117,75 @@ def gather_slabs(local, slabs, axis: int = 0, dst: int = 0, group=None, out=None
         return None
     parts = [b.narrow(axis, 0, sh[axis]) for b, (_, sh) in zip(bufs, slabs)]
     return torch.cat(parts, dim=axis)
+
+
+def slab_pieces(slab_start, slab_shape, piece_rows: int, axis: int = 0):
+    """A slab cut along `axis` at array-coordinate multiples of `piece_rows` (the chunk or inner-chunk
+    extent: a piece's decode touches only its own chunk rows, so no chunk is decoded twice inside a
+    rank): [(row offset within the slab, rows)], in order."""
+    s0, n = int(slab_start[axis]), int(slab_shape[axis])
+    out, r = [], s0
+    while r < s0 + n:
+        e = min(s0 + n, (r // piece_rows + 1) * piece_rows)
+        out.append((r - s0, e - r))
+        r = e
+    return out
+
+
+def gather_slabs_overlapped(decode_piece, local, slabs, piece_rows: int, dst: int = 0, group=None, out=None):
+    """gather_slabs with the exchange overlapped with the decode (C4): every rank's slab is
+    decoded piece by piece (slab_pieces), and a peer sends each piece to the root as soon as it is
+    decoded, while its next piece decodes -- over RCCL the send is queued on the communicator's stream
+    behind the decode already on the caller's stream, so the xGMI transfer of piece k runs beside the
+    kernels of piece k+1. The root posts every receive first (straight into place in `out`) and then
+    decodes its own pieces into its rows. decode_piece(k, view) decodes piece k of this rank's slab into
+    `view` (its rows of `local`, or of the root's `out`). Axis 0 only. Returns the subset on dst."""
+    import torch
+    import torch.distributed as dist
+    world = len(slabs)
+    rank = dist.get_rank(group) if world > 1 else 0
+    pieces = [slab_pieces(s, sh, piece_rows) for s, sh in slabs]
+    if world == 1:
+        for k, (r0, n) in enumerate(pieces[0]):
+            decode_piece(k, local.narrow(0, r0, n))
+        return local
+    staged = _host_staged(group) and local.is_cuda  # gloo: device pieces staged through host memory
+    g_dst = dist.get_global_rank(group, dst) if group is not None else dst
+    if rank != dst:
+        works = []
+        for k, (r0, n) in enumerate(pieces[rank]):
+            part = local.narrow(0, r0, n)
+            decode_piece(k, part)
+            if part.numel():
+                t = part.cpu() if staged else part  # (the staging copy waits for the decode)
+                works.append((dist.isend(t, g_dst, group=group), t))
+        for w, _ in works:
+            w.wait()
+        return None
+    if out is None:
+        shape = list(local.shape)
+        shape[0] = sum(sh[0] for _, sh in slabs)
+        out = torch.empty(shape, dtype=local.dtype, device=local.device)
+    recvs, row, own = [], 0, 0
+    for r, (_, sh) in enumerate(slabs):
+        if r == dst:
+            own = row
+        else:
+            g_r = dist.get_global_rank(group, r) if group is not None else r
+            for r0, n in pieces[r]:
+                tgt = out.narrow(0, row + r0, n)
+                if not tgt.numel():
+                    continue
+                buf = torch.empty(tgt.shape, dtype=tgt.dtype) if staged else tgt
+                recvs.append((dist.irecv(buf, g_r, group=group), buf, tgt))
+        row += sh[0]
+    for k, (r0, n) in enumerate(pieces[dst]):
+        decode_piece(k, out.narrow(0, own + r0, n))
+    for w, buf, tgt in recvs:
+        w.wait()
+        if buf is not tgt:
+            tgt.copy_(buf)
+    return out
 
 
 def slab_mismatches(gathered, expected, slabs, axis: int = 0):
@@ -246,9 +317,12 @@ def gather_regions(local, boxes_by_rank, sub_start, sub_shape, dst: int = 0, gro
 
 
 def retrieve_array_subset_distributed(array, start, shape, group=None, dst: int = 0, axis: int = 0,
-                                      device=None):
+                                      device=None, piece_rows: int | None = None):
     """Array::retrieve_array_subset over all ranks of `group`: this rank decodes its slab on its own
-    device, then the slabs are gathered to `dst` (the assembled subset there, None elsewhere)."""
+    device, then the slabs are gathered to `dst` (the assembled subset there, None elsewhere).
+    piece_rows (axis 0): decode and send the slab in pieces of that many array rows (the chunk extent
+    along axis 0, or a multiple), the sends overlapping the next piece's decode
+    (gather_slabs_overlapped)."""
     import numpy as np
     import torch
     import torch.distributed as dist
@@ -260,6 +334,20 @@ def retrieve_array_subset_distributed(array, start, shape, group=None, dst: int 
         device = torch.device("cuda", torch.cuda.current_device()) if torch.cuda.is_available() else "cpu"
     tdtype = torch.from_numpy(np.zeros(1, dtype=array.dtype)).dtype
     device = torch.device(device)
+    if piece_rows and axis == 0:
+        pieces = slab_pieces(s, sh, piece_rows)
+
+        def decode_piece(k, view):
+            r0, n = pieces[k]
+            if n and all(x > 0 for x in sh):
+                array.retrieve_array_subset_into([s[0] + r0] + list(s[1:]), [n] + list(sh[1:]), view)
+        out = None
+        if rank == dst:  # the root's pieces decode in place inside the gathered subset
+            out = torch.empty([int(n) for n in shape], dtype=tdtype, device=device)
+            local = out.narrow(0, sum(slabs[r][1][0] for r in range(rank)), sh[0])
+        else:
+            local = torch.empty(sh, dtype=tdtype, device=device)
+        return gather_slabs_overlapped(decode_piece, local, slabs, piece_rows, dst, group, out=out)
     if device.type == "cuda" and world > 1 and _host_staged(group):
         # gloo moves host tensors only: decode on the device, stage the slab through host memory
         local = torch.empty(sh, dtype=tdtype, device=device)
