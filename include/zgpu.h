@@ -201,6 +201,23 @@ int zgpu_decode_into(zgpu_chain *chain, uint32_t ndim, const zgpu_chunk_desc *de
                      const zgpu_out_view *view, uint32_t flags, int32_t *status, void *hip_stream);
 
 /*
+ * zgpu_decode_batch with host inputs whose decoded output stays in library-owned pinned memory:
+ * *data points at the C-order window of shape out_shape (prod(out_shape) * element size bytes),
+ * valid until zgpu_result_release(*result). For callers that can only COPY into their target, as a
+ * zarrs codec plugin must (ArrayBytesFixedDisjointView exposes copy_from_slice and no pointer,
+ * zarrs_codec/src/array_bytes_fixed_disjoint_view.rs:177-206): decoding into a caller buffer and
+ * then copying that into the view would cross host memory twice. ZGPU_COALESCE applies as for
+ * zgpu_decode_batch (the pointer then lies inside the batch's pack, shared with its other callers).
+ * On a failure *data is NULL and *result NULL. Host inputs only (ZGPU_ENC_DEVICE / ZGPU_OUT_DEVICE
+ * -> ZGPU_INVALID_ARGUMENT).
+ */
+typedef struct zgpu_result zgpu_result;
+int zgpu_decode_pinned(zgpu_chain *chain, uint32_t ndim, const zgpu_chunk_desc *descs, uint64_t n,
+                       const uint64_t *out_shape, uint32_t flags, int32_t *status, const void **data,
+                       zgpu_result **result);
+void zgpu_result_release(zgpu_result *result);
+
+/*
  * Coalescing policy of a context (ZGPU_COALESCE): a call waits at most window_us for other calls
  * to join its batch; a batch closes early at max_calls calls or max_bytes encoded bytes. Defaults:
  * 200 us, 8 calls, 1 GiB (env ZGPU_COALESCE_US / ZGPU_COALESCE_CALLS / ZGPU_COALESCE_BYTES).
@@ -247,7 +264,9 @@ uint64_t zgpu_plan_algorithmic_bytes(const zgpu_plan *plan);
                                     read-back layout (later executions are asynchronous otherwise) */
 #define ZGPU_CTR_BLOSC_BLOCKS 4  /* blosc blocks decoded: a partial selection decodes only the blocks
                                     covering the bytes it reads (blosc_partial_decoder.rs:33-60)     */
-#define ZGPU_N_COUNTERS 5
+#define ZGPU_CTR_ITEMS 5         /* leaf items the call planned: chunks, or inner chunks of shards that meet
+                                    the selection (each decoded, or filled when empty)                 */
+#define ZGPU_N_COUNTERS 6
 uint32_t zgpu_plan_counters(const zgpu_plan *plan, uint64_t *out, uint32_t n);
 uint32_t zgpu_last_counters(uint64_t *out, uint32_t n);
 
@@ -361,6 +380,12 @@ int zgpu_encode_batch(zgpu_chain *chain, uint32_t ndim, const uint64_t *chunk_sh
  * -1 if unbounded.
  */
 int64_t zgpu_chain_encoded_bound(const zgpu_chain *chain, uint32_t ndim, const uint64_t *chunk_shape);
+/* One chunk (or shard) of chunk_shape from host bytes (C order), encoded on the GPU as
+ * zgpu_encode_chunks does; *enc / *enc_len: the encoded bytes in library-owned pinned memory, valid
+ * until zgpu_result_release(*result) -- the codec plugin's CodecChain::encode /
+ * ShardingCodecBound::encode (sharding_codec.rs:351-376), which must return owned host bytes. */
+int zgpu_encode_pinned(zgpu_chain *chain, uint32_t ndim, const uint64_t *chunk_shape, const void *decoded,
+                       const void **enc, uint64_t *enc_len, zgpu_result **result);
 int zgpu_encode_chunks(zgpu_chain *chain, uint32_t ndim, const uint64_t *chunk_shape, const void *array,
                        const uint64_t *array_shape, const zgpu_encode_desc *descs, uint64_t n, uint32_t flags,
                        uint64_t *enc_lens, void *hip_stream);

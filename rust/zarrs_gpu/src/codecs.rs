@@ -6,16 +6,20 @@
 //! whose `decode` is the GPU's and whose metadata, representation, encode and partial-encode behaviour
 //! is zarrs' own codec, which the plugin wraps.
 //!
-//! Each decode is one synchronous `zgpu_decode_batch` of a one-codec chain (n = 1, host bytes in,
-//! host bytes out). A per-codec plugin cannot fuse a chain's stages or batch chunks: every stage is
-//! a PCIe round trip. The batched paths (the `sharding_indexed` plugin, ArrayGpuExt) are the fast
-//! ones; these plugins make the GPU a drop-in for arrays read through zarrs' per-chunk path.
+//! Each decode is one synchronous `zgpu_decode_pinned` of a one-codec chain (n = 1, host bytes in,
+//! the decoded bytes copied once out of pinned memory), coalesced with the calls other rayon workers
+//! make at the same time (ZGPU_COALESCE: one H2D, one launch sequence, one D2H per batch). A
+//! per-codec plugin cannot fuse a chain's stages: every GPU stage is a PCIe round trip, so by default
+//! only the entropy stages (gzip, zstd, blosc: GPU_ENTROPY_CODEC_NAMES) are registered and zarrs'
+//! own bytes / transpose / crc32c / shuffle run on the host around them (bench.py's
+//! `secondary.c5.dropin_emulation` measures that split on C5). The batched paths (the
+//! `sharding_indexed` plugin, ArrayGpuExt) remain the fast ones.
 
 use std::borrow::Cow;
 use std::num::NonZeroU64;
 use std::sync::{Arc, OnceLock};
 
-use zarrs::array::codec::{BytesCodec, Crc32cCodec, GzipCodec, ShuffleCodec, TransposeCodec, ZstdCodec};
+use zarrs::array::codec::{BloscCodec, BytesCodec, Crc32cCodec, GzipCodec, ShuffleCodec, TransposeCodec, ZstdCodec};
 use zarrs_chunk_grid::ChunkGridCreateError;
 use zarrs_codec::{
     ArrayBytes, ArrayBytesRaw, ArrayCodecTraits, ArrayPartialDecoderTraits, ArrayPartialEncoderTraits,
@@ -33,8 +37,17 @@ use zarrs_plugin::ZarrVersion;
 
 use crate::Chain;
 
-/// Names the per-codec plugins register (the v3 names zarrs registers for these codecs).
-pub const GPU_CODEC_NAMES: [&str; 7] = ["bytes", "transpose", "crc32c", "gzip", "zstd", "numcodecs.shuffle", "shuffle"];
+/// Names every per-codec plugin answers to (the v3 names zarrs registers for these codecs).
+pub const GPU_CODEC_NAMES: [&str; 8] =
+    ["bytes", "transpose", "crc32c", "gzip", "zstd", "blosc", "numcodecs.shuffle", "shuffle"];
+
+/// The codecs [`crate::register_codecs`] sends to the GPU by default: the entropy stages, whose
+/// decode is worth a PCIe round trip per chunk (an inflate or zstd decode runs ~1 GB/s per host
+/// core; the GPU's batched decode is two orders faster and a coalesced call moves only the
+/// compressed bytes in and the decoded bytes out). `bytes`, `transpose`, `crc32c` and
+/// `numcodecs.shuffle` run near memory speed on the host, where a hop to the GPU and back costs more
+/// than the stage: they stay zarrs' own unless [`crate::register_codecs_all`] asks for them.
+pub const GPU_ENTROPY_CODEC_NAMES: [&str; 3] = ["gzip", "zstd", "blosc"];
 
 /// The runtime-plugin create function of the per-codec plugins: zarrs' own codec is created from the
 /// metadata (never through the registry, which would find this plugin again) and wrapped.
@@ -48,6 +61,7 @@ pub fn create(metadata: &MetadataV3) -> Result<Codec, CodecCreateError> {
         "crc32c" => <Crc32cCodec as CodecTraitsV3>::create(metadata)?,
         "gzip" => <GzipCodec as CodecTraitsV3>::create(metadata)?,
         "zstd" => <ZstdCodec as CodecTraitsV3>::create(metadata)?,
+        "blosc" => <BloscCodec as CodecTraitsV3>::create(metadata)?,
         "numcodecs.shuffle" | "shuffle" => <ShuffleCodec as CodecTraitsV3>::create(metadata)?,
         other => return Err(CodecCreateError::Other(format!("zarrs_gpu: no GPU plugin for codec {other}"))),
     };

@@ -36,6 +36,25 @@ pub struct zgpu_ctx {
 pub struct zgpu_chain {
     _opaque: [u8; 0],
 }
+/// Library-owned pinned bytes of zgpu_decode_pinned / zgpu_encode_pinned (released by
+/// zgpu_result_release).
+#[repr(C)]
+pub struct zgpu_result {
+    _opaque: [u8; 0],
+}
+
+/// zgpu_last_counters index: leaf items (chunks / inner chunks) the calling thread's last call planned.
+pub const ZGPU_CTR_ITEMS: usize = 5;
+pub const ZGPU_N_COUNTERS: usize = 6;
+
+/// zgpu_encode_desc: one chunk of a device-resident array encoded into `dst`.
+#[repr(C)]
+#[derive(Clone, Copy)]
+pub struct zgpu_encode_desc {
+    pub dst: *mut c_void,
+    pub dst_cap: u64,
+    pub chunk_start: [u64; ZGPU_MAX_DIMS],
+}
 
 #[repr(C)]
 #[derive(Clone, Copy)]
@@ -123,6 +142,28 @@ unsafe extern "C" {
         hip_stream: *mut c_void,
     ) -> c_int;
     pub fn zgpu_last_size_mismatch(desc: *mut u64, len: *mut u64, expected_len: *mut u64) -> c_int;
+    pub fn zgpu_last_counters(out: *mut u64, n: u32) -> u32;
+    pub fn zgpu_decode_pinned(
+        chain: *mut zgpu_chain,
+        ndim: u32,
+        descs: *const zgpu_chunk_desc,
+        n: u64,
+        out_shape: *const u64,
+        flags: u32,
+        status: *mut i32,
+        data: *mut *const c_void,
+        result: *mut *mut zgpu_result,
+    ) -> c_int;
+    pub fn zgpu_encode_pinned(
+        chain: *mut zgpu_chain,
+        ndim: u32,
+        chunk_shape: *const u64,
+        decoded: *const c_void,
+        enc: *mut *const c_void,
+        enc_len: *mut u64,
+        result: *mut *mut zgpu_result,
+    ) -> c_int;
+    pub fn zgpu_result_release(result: *mut zgpu_result);
     pub fn zgpu_retrieve_array_subset_multi(
         chains: *const *mut zgpu_chain,
         n_dev: u32,

@@ -3,9 +3,10 @@
 //!
 //! Three entry points, all over the C ABI:
 //!
-//! * [`register_codecs`] adds per-codec runtime plugins for `bytes`, `transpose`, `crc32c`, `gzip`,
-//!   `zstd` and `numcodecs.shuffle` (codecs.rs): zarrs' unchanged per-chunk CodecChain then decodes
-//!   every stage on the GPU (one synchronous n = 1 zgpu_decode_batch per stage and chunk).
+//! * [`register_codecs`] adds per-codec runtime plugins for the entropy stages `gzip`, `zstd` and
+//!   `blosc` (codecs.rs): zarrs' unchanged per-chunk CodecChain then decodes them on the GPU (one
+//!   coalesced zgpu_decode_pinned per chunk) and runs its own `bytes` / `transpose` / `crc32c` /
+//!   `numcodecs.shuffle` on the host ([`register_codecs_all`] puts every stage on the GPU).
 //! * [`register`] adds a runtime codec plugin for `sharding_indexed`
 //!   (`zarrs_codec::register_codec_v3`, zarrs_codec/src/lib.rs:279-318; runtime plugins are matched
 //!   before the compile-time ones, lib.rs:385-414). A shard is the natural GPU batch: its
@@ -55,9 +56,20 @@ pub fn unregister(handle: &zarrs_codec::CodecRuntimeRegistryHandleV3) -> bool {
     zarrs_codec::unregister_codec_v3(handle)
 }
 
-/// Register the per-codec GPU plugins (`bytes`, `transpose`, `crc32c`, `gzip`, `zstd`,
-/// `numcodecs.shuffle`): one runtime plugin matching all their names, zarrs_codec/src/lib.rs:279-318.
+/// Register the per-codec GPU plugins of the entropy stages (`gzip`, `zstd`, `blosc`:
+/// [`codecs::GPU_ENTROPY_CODEC_NAMES`]): one runtime plugin matching their names,
+/// zarrs_codec/src/lib.rs:279-318. zarrs' own codecs keep the near-memory-speed stages.
 pub fn register_codecs() -> zarrs_codec::CodecRuntimeRegistryHandleV3 {
+    zarrs_codec::register_codec_v3(zarrs_codec::CodecRuntimePluginV3::new(
+        |name| codecs::GPU_ENTROPY_CODEC_NAMES.contains(&name),
+        codecs::create,
+    ))
+}
+
+/// Register a per-codec GPU plugin for every stage (`bytes`, `transpose`, `crc32c`, `gzip`, `zstd`,
+/// `blosc`, `numcodecs.shuffle`): each stage of zarrs' per-chunk chain then decodes on the GPU, one
+/// PCIe round trip per stage.
+pub fn register_codecs_all() -> zarrs_codec::CodecRuntimeRegistryHandleV3 {
     zarrs_codec::register_codec_v3(zarrs_codec::CodecRuntimePluginV3::new(
         |name| codecs::GPU_CODEC_NAMES.contains(&name),
         codecs::create,
@@ -197,32 +209,88 @@ impl Chain {
         d.chunk_shape[..nd].copy_from_slice(chunk_shape);
         d.sel_start[..nd].copy_from_slice(sel_start);
         d.sel_shape[..nd].copy_from_slice(sel_shape);
-        let n: u64 = sel_shape.iter().product();
-        let mut out = vec![0u8; usize::try_from(n).map_err(|e| CodecError::Other(e.to_string()))? * self.element_size];
-        let mut status = 0i32;
         // ZGPU_COALESCE: this call joins the other rayon workers' concurrent calls on the chain in one
-        // GPU batch (zarrs decodes one shard per worker, array_read_ops_common.rs:173-176)
+        // GPU batch (zarrs decodes one shard per worker, array_read_ops_common.rs:173-176); a lone caller
+        // does not wait for the collect window (the library sees no other call in flight)
         let flags = ffi::ZGPU_COALESCE | if validate { 0 } else { ffi::ZGPU_NO_VALIDATE };
-        // SAFETY: the descriptor points at `encoded` (host memory, flags without ZGPU_ENC_DEVICE) and
-        // `out` holds prod(sel_shape) elements; both outlive the synchronous call.
+        Ok(self.decode_pinned(&[d], sel_shape, flags)?.as_slice().to_vec())
+    }
+}
+
+impl Chain {
+    /// zgpu_decode_pinned over `descs` (host encoded bytes): the C-order output of `out_shape` left in
+    /// library pinned memory, for ONE copy into the caller's target (a zarrs view can only be written
+    /// by `copy_from_slice`, array_bytes_fixed_disjoint_view.rs:177-206). `flags`: ZGPU_NO_VALIDATE
+    /// (partial-decoder semantics), ZGPU_COALESCE (join concurrent calls in one GPU batch).
+    pub(crate) fn decode_pinned(
+        &self,
+        descs: &[ffi::zgpu_chunk_desc],
+        out_shape: &[u64],
+        flags: u32,
+    ) -> Result<Pinned, CodecError> {
+        let nd = out_shape.len();
+        if nd == 0 || nd > ffi::ZGPU_MAX_DIMS {
+            return Err(CodecError::Other(format!("zgpu: unsupported dimensionality {nd}")));
+        }
+        let len = usize::try_from(out_shape.iter().product::<u64>() * self.element_size as u64)
+            .map_err(|e| CodecError::Other(e.to_string()))?;
+        let mut status = vec![0i32; descs.len().max(1)];
+        let mut data: *const c_void = std::ptr::null();
+        let mut res: *mut ffi::zgpu_result = std::ptr::null_mut();
+        // SAFETY: the descriptors point at host buffers the caller keeps alive for this synchronous call;
+        // out-pointers to locals.
         let rc = unsafe {
-            ffi::zgpu_decode_batch(
+            ffi::zgpu_decode_pinned(
                 self.as_ptr(),
                 nd as u32,
-                &d,
-                1,
-                out.as_mut_ptr().cast::<c_void>(),
-                sel_shape.as_ptr(),
-                flags,
-                &mut status,
-                std::ptr::null_mut(),
+                descs.as_ptr(),
+                descs.len() as u64,
+                out_shape.as_ptr(),
+                flags & (ffi::ZGPU_NO_VALIDATE | ffi::ZGPU_COALESCE),
+                status.as_mut_ptr(),
+                &mut data,
+                &mut res,
             )
         };
         if rc != ffi::ZGPU_OK {
             return Err(status_error(rc));
         }
-        Ok(out)
+        let res = NonNull::new(res).ok_or_else(|| CodecError::Other("zgpu_decode_pinned returned no result".into()))?;
+        Ok(Pinned { ptr: data.cast(), len, res })
     }
+
+    /// zgpu_encode_pinned: one chunk (or shard) of `chunk_shape` from host bytes, encoded on the GPU.
+    pub(crate) fn encode_pinned(&self, decoded: &[u8], chunk_shape: &[u64]) -> Result<Pinned, CodecError> {
+        let nd = chunk_shape.len();
+        let need = chunk_shape.iter().product::<u64>() * self.element_size as u64;
+        if nd == 0 || nd > ffi::ZGPU_MAX_DIMS || decoded.len() as u64 != need {
+            return Err(CodecError::Other(format!(
+                "zgpu encode: {} bytes for a chunk of {chunk_shape:?} ({need} expected)",
+                decoded.len()
+            )));
+        }
+        let mut enc: *const c_void = std::ptr::null();
+        let mut len = 0u64;
+        let mut res: *mut ffi::zgpu_result = std::ptr::null_mut();
+        // SAFETY: `decoded` holds the chunk's bytes for this synchronous call; out-pointers to locals.
+        let rc = unsafe {
+            ffi::zgpu_encode_pinned(self.as_ptr(), nd as u32, chunk_shape.as_ptr(), decoded.as_ptr().cast(), &mut enc,
+                                    &mut len, &mut res)
+        };
+        if rc != ffi::ZGPU_OK {
+            return Err(status_error(rc));
+        }
+        let res = NonNull::new(res).ok_or_else(|| CodecError::Other("zgpu_encode_pinned returned no result".into()))?;
+        Ok(Pinned { ptr: enc.cast(), len: usize::try_from(len).map_err(|e| CodecError::Other(e.to_string()))?, res })
+    }
+}
+
+/// Leaf items (chunks / inner chunks) the calling thread's last zgpu call planned (ZGPU_CTR_ITEMS).
+pub fn last_call_items() -> u64 {
+    let mut c = [0u64; ffi::ZGPU_N_COUNTERS];
+    // SAFETY: a buffer of ZGPU_N_COUNTERS values.
+    unsafe { ffi::zgpu_last_counters(c.as_mut_ptr(), ffi::ZGPU_N_COUNTERS as u32) };
+    c[ffi::ZGPU_CTR_ITEMS]
 }
 
 impl Chain {

@@ -9,6 +9,7 @@
 
 use std::any::Any;
 use std::borrow::Cow;
+use std::collections::HashMap;
 use std::num::NonZeroU64;
 use std::sync::Arc;
 
@@ -16,12 +17,13 @@ use zarrs::array::codec::ShardingCodec;
 use zarrs::array::{CodecChain, CodecChainBound, data_type};
 use zarrs_metadata_ext::codec::sharding::{ShardingCodecConfiguration, ShardingCodecConfigurationV1, ShardingIndexLocation};
 use zarrs_storage::byte_range::ByteRange;
-use zarrs_chunk_grid::{ChunkGridCreateError, Indexer};
+use zarrs_chunk_grid::{ChunkGridCreateError, Indexer, IndexerError};
 use zarrs_codec::{
     ArrayBytes, ArrayBytesDecodeIntoTarget, ArrayBytesRaw, ArrayCodecTraits, ArrayPartialDecoderNoSubchunkingTraits, ArrayPartialDecoderTraits,
     ArrayPartialEncoderTraits, ArrayToBytesCodecSubchunkingTraits, ArrayToBytesCodecTraits, BytesPartialDecoderTraits,
     BytesPartialEncoderTraits, BytesRepresentation, ChunkGridDecoded, ChunkGridDecodedRef, Codec, CodecCreateError,
     CodecError, CodecMetadataOptions, CodecOptions, CodecSpecificOptions, CodecTraits, CodecTraitsV3,
+    InvalidNumberOfElementsError,
     PartialDecoderCapability, PartialEncoderCapability, RecommendedConcurrency, UnboundArrayToBytesCodecTraits,
     decode_into_array_bytes_target,
 };
@@ -31,7 +33,7 @@ use zarrs_metadata::v3::MetadataV3;
 use zarrs_plugin::ZarrVersion;
 use zarrs_storage::StorageError;
 
-use crate::{Chain, ffi};
+use crate::{Chain, Pinned, ffi};
 
 /// The unbound GPU `sharding_indexed` codec: zarrs' own ShardingCodec (for metadata, encoding and
 /// subchunk grids) plus the codec metadata the GPU chain is created from at bind time.
@@ -217,13 +219,26 @@ impl ArrayToBytesCodecTraits for GpuShardingCodecBound {
         self.cpu.encoded_representation(shape)
     }
 
-    /// The write path stays zarrs' (ShardingCodecBound::encode, sharding_codec.rs:351-376).
+    /// ShardingCodecBound::encode (sharding_codec.rs:351-376) on the GPU: the shard's inner chunks
+    /// encoded by zgpu_encode_pinned (inner chains of fixed-size stages, gzip, zstd, blosc, crc32c; an
+    /// inner chunk equal to the fill value everywhere omitted; the index encoded with its chain), the
+    /// bytes copied once into the returned buffer. Chains the GPU write path does not take (and
+    /// variable-size data types) stay with zarrs' own encoder.
     fn encode<'a>(
         &self,
         bytes: ArrayBytes<'a>,
         shape: &[NonZeroU64],
         options: &CodecOptions,
     ) -> Result<ArrayBytesRaw<'a>, CodecError> {
+        if self.data_type.fixed_size().is_some() {
+            if let ArrayBytes::Fixed(raw) = &bytes {
+                match self.chain.encode_pinned(raw, &u64s(shape)) {
+                    Ok(enc) => return Ok(Cow::Owned(enc.as_slice().to_vec())),
+                    Err(CodecError::Other(msg)) if msg.contains("UNSUPPORTED") => {}
+                    Err(e) => return Err(e),
+                }
+            }
+        }
         self.cpu.encode(bytes, shape, options)
     }
 
@@ -267,9 +282,17 @@ impl ArrayToBytesCodecTraits for GpuShardingCodecBound {
                         view.num_elements()
                     )));
                 }
-                let zeros = vec![0u64; shape.len()];
-                let out = self.chain.decode_region(&bytes, &shape, &zeros, &shape, options.validate_checksums())?;
-                view.copy_from_slice(&out)?;
+                let nd = shape.len();
+                if nd == 0 || nd > ffi::ZGPU_MAX_DIMS {
+                    return Err(CodecError::Other(format!("zgpu: unsupported dimensionality {nd}")));
+                }
+                let mut d = ffi::zgpu_chunk_desc { enc: bytes.as_ptr().cast(), enc_len: bytes.len() as u64, ..Default::default() };
+                d.chunk_shape[..nd].copy_from_slice(&shape);
+                d.sel_shape[..nd].copy_from_slice(&shape);
+                let flags = ffi::ZGPU_COALESCE | if options.validate_checksums() { 0 } else { ffi::ZGPU_NO_VALIDATE };
+                // the decoded shard stays in library pinned memory: one copy into the view, no Vec
+                let decoded = self.chain.decode_pinned(&[d], &shape, flags)?;
+                view.copy_from_slice(decoded.as_slice())?;
                 Ok(())
             }
             target => {
@@ -327,17 +350,51 @@ struct GpuShardPartialDecoder {
 }
 
 impl GpuShardPartialDecoder {
-    fn decode_subset(&self, start: &[u64], shape: &[u64], options: &CodecOptions) -> Result<Vec<u8>, CodecError> {
-        let codec = &self.codec;
-        let es = codec.inner_chain.element_size;
-        let n: u64 = shape.iter().product();
-        let mut out = vec![0u8; usize::try_from(n).map_err(|e| CodecError::Other(e.to_string()))? * es];
-        let Some(index) = &self.index else {
-            // a missing shard reads as the fill value (:329-333)
-            let fill = codec.fill_value.as_ne_bytes();
-            out.chunks_exact_mut(es).for_each(|c| c.copy_from_slice(fill));
-            return Ok(out);
+    /// The shard index entry of inner chunk `lin` (C order of the inner grid): None = empty.
+    fn entry(index: &[u64], lin: usize) -> Result<Option<ByteRange>, CodecError> {
+        let (offset, size) = (index[2 * lin], index[2 * lin + 1]);
+        if offset == u64::MAX && size == u64::MAX {
+            return Ok(None);
+        }
+        let end = offset.checked_add(size).ok_or_else(|| CodecError::Other(OOB.into()))?;
+        Ok(Some(ByteRange::new(offset..end)))
+    }
+
+    /// One batched ranged read of every present inner chunk (get_subchunk_partial_decoder's
+    /// ByteIntervalPartialDecoder reads, :279-308): the bytes, and each descriptor's pointer set.
+    fn read_inner(
+        &self,
+        ranges: Vec<ByteRange>,
+        present: &[usize],
+        descs: &mut [ffi::zgpu_chunk_desc],
+        options: &CodecOptions,
+    ) -> Result<Vec<Vec<u8>>, CodecError> {
+        if ranges.is_empty() {
+            return Ok(Vec::new());
+        }
+        let bytes: Vec<Vec<u8>> = match self.input.partial_decode_many(Box::new(ranges.into_iter()), options) {
+            Ok(Some(b)) => b.into_iter().map(|x| x.into_owned()).collect(),
+            Ok(None) => return Err(CodecError::Other("zarrs_gpu: the shard disappeared during the read".into())),
+            Err(CodecError::InvalidByteRangeError(_)) => return Err(CodecError::Other(OOB.into())),
+            Err(e) => return Err(e),
         };
+        for (b, &k) in bytes.iter().zip(present) {
+            descs[k].enc = b.as_ptr().cast();
+            descs[k].enc_len = b.len() as u64;
+        }
+        Ok(bytes)
+    }
+
+    /// partial_decode_fixed_array_subset_into (sharding_partial_decoder_sync.rs:311-400): the inner
+    /// chunks intersecting [start, start + shape), each a descriptor whose selection is its overlap
+    /// (crc32c stripped, not verified: crc32c_codec.rs:143-158; empty inner chunks are fill
+    /// descriptors, :380-381), decoded in ONE coalesced zgpu_decode_pinned of the inner chain. None: the
+    /// shard does not exist (the caller fills, :329-333).
+    fn decode_subset_pinned(&self, start: &[u64], shape: &[u64], options: &CodecOptions) -> Result<Option<Pinned>, CodecError> {
+        let Some(index) = &self.index else {
+            return Ok(None);
+        };
+        let codec = &self.codec;
         let cps = codec.chunks_per_shard(&self.shape)?;
         let sub = &codec.subchunk_shape;
         let nd = self.shape.len();
@@ -345,7 +402,7 @@ impl GpuShardPartialDecoder {
         let lo: Vec<u64> = start.iter().zip(sub).map(|(s, c)| s / c).collect();
         let hi: Vec<u64> = start.iter().zip(shape).zip(sub).map(|((s, n), c)| (s + n - 1) / c + 1).collect();
         let mut descs = Vec::new();
-        let mut ranges = Vec::new();  // byte range of each present inner chunk, in descriptor order
+        let mut ranges = Vec::new(); // byte range of each present inner chunk, in descriptor order
         let mut present = Vec::new(); // descriptor index of each range
         let total: u64 = hi.iter().zip(&lo).map(|(h, l)| h - l).product();
         for t in 0..total {
@@ -358,7 +415,6 @@ impl GpuShardPartialDecoder {
                 rem /= ext;
             }
             let lin = idx.iter().zip(&cps).fold(0u64, |acc, (i, c)| acc * c + i) as usize;
-            let (offset, size) = (index[2 * lin], index[2 * lin + 1]);
             let mut d = ffi::zgpu_chunk_desc::default();
             for a in 0..nd {
                 let c0 = idx[a] * sub[a];
@@ -369,31 +425,104 @@ impl GpuShardPartialDecoder {
                 d.sel_shape[a] = s1 - s0;
                 d.out_start[a] = s0 - start[a];
             }
-            if !(offset == u64::MAX && size == u64::MAX) {
-                let end = offset.checked_add(size).ok_or_else(|| CodecError::Other(OOB.into()))?;
-                ranges.push(ByteRange::new(offset..end));
+            if let Some(r) = Self::entry(index, lin)? {
+                ranges.push(r);
                 present.push(descs.len());
             }
             descs.push(d);
         }
-        // one batched ranged read of every present inner chunk
-        let bytes = if ranges.is_empty() {
-            Vec::new()
-        } else {
-            match self.input.partial_decode_many(Box::new(ranges.into_iter()), options) {
-                Ok(Some(b)) => b,
-                Ok(None) => return Err(CodecError::Other("zarrs_gpu: the shard disappeared during the read".into())),
-                Err(CodecError::InvalidByteRangeError(_)) => return Err(CodecError::Other(OOB.into())),
-                Err(e) => return Err(e),
-            }
-        };
-        for (b, &k) in bytes.iter().zip(&present) {
-            descs[k].enc = b.as_ptr().cast();
-            descs[k].enc_len = b.len() as u64;
-        }
+        let _bytes = self.read_inner(ranges, &present, &mut descs, options)?;
         // coalesced with the partial shards other rayon workers decode at the same time
-        codec.inner_chain.decode_descs(&descs, &mut out, shape, ffi::ZGPU_NO_VALIDATE | ffi::ZGPU_COALESCE)?;
+        Ok(Some(codec.inner_chain.decode_pinned(&descs, shape, ffi::ZGPU_NO_VALIDATE | ffi::ZGPU_COALESCE)?))
+    }
+
+    fn fill_bytes(&self, n: u64) -> Result<Vec<u8>, CodecError> {
+        let es = self.codec.inner_chain.element_size;
+        let mut out = vec![0u8; usize::try_from(n).map_err(|e| CodecError::Other(e.to_string()))? * es];
+        let fill = self.codec.fill_value.as_ne_bytes();
+        out.chunks_exact_mut(es).for_each(|c| c.copy_from_slice(fill));
         Ok(out)
+    }
+
+    /// partial_decode_fixed_indexer (sharding_partial_decoder_sync.rs:492-560) for indexers that are
+    /// not an array subset: only the inner chunks the indices touch are decoded -- each once (the
+    /// reference's per-chunk decoder cache), all of them in ONE zgpu_decode_pinned whose output stacks
+    /// them along axis 0 -- and the indexed elements gathered from the pinned result in indexer order.
+    fn decode_indexer(&self, indexer: &dyn Indexer, options: &CodecOptions) -> Result<Vec<u8>, CodecError> {
+        let codec = &self.codec;
+        let es = codec.inner_chain.element_size;
+        let cps = codec.chunks_per_shard(&self.shape)?;
+        let sub = &codec.subchunk_shape;
+        let nd = self.shape.len();
+        let chunk_elems: u64 = sub.iter().product();
+        let mut slot: HashMap<u64, usize> = HashMap::new();
+        let mut order: Vec<u64> = Vec::new(); // touched inner chunks, first-touch order
+        let mut elems: Vec<(usize, u64)> = Vec::new(); // (slot, element offset inside the inner chunk)
+        for indices in indexer.iter_indices() {
+            if indices.len() != nd {
+                return Err(IndexerError::new_incompatible_dimensionality(indices.len(), nd).into());
+            }
+            let ci: Vec<u64> = indices.iter().zip(sub).map(|(&i, &c)| i / c).collect();
+            if ci.iter().zip(&cps).any(|(a, b)| a >= b) {
+                return Err(IndexerError::new_oob(ci, cps.clone()).into());
+            }
+            let lin = ci.iter().zip(&cps).fold(0u64, |acc, (i, c)| acc * c + i);
+            let k = *slot.entry(lin).or_insert_with(|| {
+                order.push(lin);
+                order.len() - 1
+            });
+            let within = indices.iter().zip(sub).fold(0u64, |acc, (&i, &c)| acc * c + i % c);
+            elems.push((k, within));
+        }
+        let Some(index) = &self.index else {
+            return self.fill_bytes(elems.len() as u64);
+        };
+        let mut descs = Vec::with_capacity(order.len());
+        let mut ranges = Vec::new();
+        let mut present = Vec::new();
+        for (k, &lin) in order.iter().enumerate() {
+            let mut d = ffi::zgpu_chunk_desc::default();
+            d.chunk_shape[..nd].copy_from_slice(sub);
+            d.sel_shape[..nd].copy_from_slice(sub);
+            d.out_start[0] = k as u64 * sub[0];
+            if let Some(r) = Self::entry(index, usize::try_from(lin).map_err(|e| CodecError::Other(e.to_string()))?)? {
+                ranges.push(r);
+                present.push(descs.len());
+            }
+            descs.push(d);
+        }
+        let _bytes = self.read_inner(ranges, &present, &mut descs, options)?;
+        let mut stacked = sub.clone();
+        stacked[0] *= order.len().max(1) as u64;
+        let decoded = codec.inner_chain.decode_pinned(&descs, &stacked, ffi::ZGPU_NO_VALIDATE | ffi::ZGPU_COALESCE)?;
+        let src = decoded.as_slice();
+        let mut out = Vec::with_capacity(elems.len() * es);
+        for (k, within) in elems {
+            let o = usize::try_from(k as u64 * chunk_elems + within).map_err(|e| CodecError::Other(e.to_string()))? * es;
+            out.extend_from_slice(&src[o..o + es]);
+        }
+        Ok(out)
+    }
+
+    /// The reference's checks before any decode (sharding_partial_decoder_sync.rs:118-131).
+    fn check(&self, indexer: &dyn Indexer) -> Result<(), CodecError> {
+        if indexer.dimensionality() != self.shape.len() {
+            return Err(IndexerError::new_incompatible_dimensionality(indexer.dimensionality(), self.shape.len()).into());
+        }
+        if self.codec.data_type.is_optional() {
+            return Err(CodecError::UnsupportedDataType(self.codec.data_type.clone(), "sharding_indexed".to_string()));
+        }
+        Ok(())
+    }
+
+    fn subset_inside(&self, start: &[u64], shape: &[u64]) -> Result<(), CodecError> {
+        let inside = start.len() == self.shape.len()
+            && start.iter().zip(shape.iter()).zip(&self.shape).all(|((s, n), e)| s + n <= *e);
+        if inside {
+            Ok(())
+        } else {
+            Err(CodecError::Other(format!("subset {start:?} + {shape:?} is out of the bounds of the shard {:?}", self.shape)))
+        }
     }
 }
 
@@ -413,32 +542,55 @@ impl ArrayPartialDecoderTraits for GpuShardPartialDecoder {
     }
 
     fn partial_decode(&self, indexer: &dyn Indexer, options: &CodecOptions) -> Result<ArrayBytes<'_>, CodecError> {
+        self.check(indexer)?;
         if let Some(subset) = indexer.as_array_subset() {
             let (start, shape) = (subset.start(), subset.shape());
-            let inside = start.len() == self.shape.len()
-                && start.iter().zip(shape.iter()).zip(&self.shape).all(|((s, n), e)| s + n <= *e);
-            if !inside {
-                return Err(CodecError::Other(format!(
-                    "subset {start:?} + {shape:?} is out of the bounds of the shard {:?}",
-                    self.shape
-                )));
-            }
-            if shape.iter().any(|&n| n == 0) {
+            self.subset_inside(&start, &shape)?;
+            let n: u64 = shape.iter().product();
+            if n == 0 {
                 return Ok(ArrayBytes::new_flen(Cow::Owned(Vec::new())));
             }
-            return Ok(ArrayBytes::new_flen(Cow::Owned(self.decode_subset(&start, &shape, options)?)));
+            let out = match self.decode_subset_pinned(&start, &shape, options)? {
+                Some(p) => p.as_slice().to_vec(),
+                None => self.fill_bytes(n)?, // a missing shard reads as the fill value (:329-333)
+            };
+            return Ok(ArrayBytes::new_flen(Cow::Owned(out)));
         }
-        // arbitrary indexers: the whole shard (every inner chunk, one batch), the indexed elements
-        // gathered here
-        let zeros = vec![0u64; self.shape.len()];
-        let full = self.decode_subset(&zeros, &self.shape, options)?;
-        let es = self.codec.inner_chain.element_size;
-        let mut out = Vec::with_capacity(usize::try_from(indexer.len()).unwrap_or(0) * es);
-        for i in indexer.iter_linearised_indices(&self.shape)? {
-            let o = usize::try_from(i).map_err(|e| CodecError::Other(e.to_string()))? * es;
-            out.extend_from_slice(&full[o..o + es]);
+        Ok(ArrayBytes::new_flen(Cow::Owned(self.decode_indexer(indexer, options)?)))
+    }
+
+    /// ShardingPartialDecoder::partial_decode_into (sharding_partial_decoder_sync.rs:241-272): an array
+    /// subset into a fixed-size view is decoded into library pinned memory and copied into the view
+    /// once (copy_from_slice: no intermediate Vec); a missing shard fills the view. Other indexers and
+    /// targets decode, then copy (decode_into_array_bytes_target), as the reference does.
+    fn partial_decode_into(
+        &self,
+        indexer: &dyn Indexer,
+        output_target: ArrayBytesDecodeIntoTarget<'_>,
+        options: &CodecOptions,
+    ) -> Result<(), CodecError> {
+        if indexer.len() != output_target.num_elements() {
+            return Err(InvalidNumberOfElementsError::new(indexer.len(), output_target.num_elements()).into());
         }
-        Ok(ArrayBytes::new_flen(Cow::Owned(out)))
+        self.check(indexer)?;
+        match (indexer.as_array_subset(), output_target) {
+            (Some(subset), ArrayBytesDecodeIntoTarget::Fixed(view)) => {
+                let (start, shape) = (subset.start(), subset.shape());
+                self.subset_inside(&start, &shape)?;
+                if shape.iter().product::<u64>() == 0 {
+                    return Ok(());
+                }
+                match self.decode_subset_pinned(&start, &shape, options)? {
+                    Some(decoded) => view.copy_from_slice(decoded.as_slice())?,
+                    None => view.fill(self.codec.fill_value.as_ne_bytes())?,
+                }
+                Ok(())
+            }
+            (_, target) => {
+                let decoded = self.partial_decode(indexer, options)?;
+                decode_into_array_bytes_target(&decoded, target)
+            }
+        }
     }
 
     fn supports_partial_decode(&self) -> bool {

@@ -109,13 +109,16 @@ fn gpu_per_codec_plugins_match_zarrs() {
             subsets.iter().map(|s| a.retrieve_array_subset(s).unwrap()).collect()
         })
         .collect();
-    let handle = zarrs_gpu::register_codecs();
-    for (p, exp) in chains.iter().zip(&expected) {
-        let a: Array<MemoryStore> = Array::open(store.clone(), p).unwrap();
-        for (s, e) in subsets.iter().zip(exp) {
-            let got: Vec<u16> = a.retrieve_array_subset(s).unwrap();
-            assert_eq!(&got, e, "{p}");
+    // the entropy stages on the GPU (the default), then every stage
+    for register in [zarrs_gpu::register_codecs, zarrs_gpu::register_codecs_all] {
+        let handle = register();
+        for (p, exp) in chains.iter().zip(&expected) {
+            let a: Array<MemoryStore> = Array::open(store.clone(), p).unwrap();
+            for (s, e) in subsets.iter().zip(exp) {
+                let got: Vec<u16> = a.retrieve_array_subset(s).unwrap();
+                assert_eq!(&got, e, "{p}");
+            }
         }
+        assert!(zarrs_gpu::unregister(&handle));
     }
-    assert!(zarrs_gpu::unregister(&handle));
 }

@@ -41,9 +41,10 @@ EXPORTS = [
     "zgpu_cache_retrieve_array_subset", "zgpu_retrieve_array_subset_dlpack", "zgpu_chain_encoded_bound",
     "zgpu_encode_chunks", "zgpu_retrieve_array_subset_multi", "zgpu_decode_into", "zgpu_ctx_set_coalescing",
     "zgpu_ctx_coalescing_stats", "zgpu_ctx_refcount", "zgpu_decode_pinned", "zgpu_result_release",
+    "zgpu_encode_pinned",
 ]
-CTR_ENC_BYTES, CTR_ZSTD_SERIAL, CTR_ZSTD_PARALLEL, CTR_BLOSC_RERUN, CTR_BLOSC_BLOCKS = range(5)
-N_COUNTERS = 5
+CTR_ENC_BYTES, CTR_ZSTD_SERIAL, CTR_ZSTD_PARALLEL, CTR_BLOSC_RERUN, CTR_BLOSC_BLOCKS, CTR_ITEMS = range(6)
+N_COUNTERS = 6
 
 
 class ChunkDesc(C.Structure):
@@ -124,6 +125,8 @@ def load() -> C.CDLL:
     L.zgpu_decode_pinned.argtypes = [vp, C.c_uint32, vp, C.c_uint64, vp, C.c_uint32, vp, C.POINTER(C.c_void_p),
                                      C.POINTER(C.c_void_p)]
     L.zgpu_result_release.argtypes = [vp]
+    L.zgpu_encode_pinned.argtypes = [vp, C.c_uint32, vp, vp, C.POINTER(C.c_void_p), C.POINTER(C.c_uint64),
+                                     C.POINTER(C.c_void_p)]
     L.zgpu_result_release.restype = None
     L.zgpu_ctx_refcount.argtypes = [vp]
     L.zgpu_ctx_refcount.restype = C.c_int64

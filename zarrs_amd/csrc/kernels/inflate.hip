@@ -419,26 +419,33 @@ __device__ bool build_table(const uint8_t *lens, uint32_t n, uint32_t root, uint
       if (sb) {
         const uint32_t base = atomicAdd(&tmp[0], 1u << sb);
         entry = 0;  // subtable space exhausted: the canonical slow path
-        if (base + (1u << sb) <= sub_cap) {
-          entry = ((size + base) << 16) | (sb << 6) | F_SUBT;
-          for (uint32_t x = 0; x < (1u << sb); x++) {
-            const uint32_t cf = (v << sb) | rev_bits(x, sb);  // MSB-first code of root + sb bits
-            uint32_t se = (K_BAD << 4) | 0xF;
-            for (uint32_t L = root + 1; L <= root + sb; L++) {
-              const uint32_t c = cf >> (root + sb - L), f = M.first[L];
-              if (c - f < M.count[L]) {
-                se = table_entry(kind, sorted[M.offs[L] + c - f], L);
-                break;
-              }
-            }
-            tab[size + base + x] = se;
-          }
-        }
+        if (base + (1u << sb) <= sub_cap) entry = ((size + base) << 16) | (sb << 6) | F_SUBT;
       }
     }
-  tab[e] = entry;
+    tab[e] = entry;
   }
   __syncthreads();
+  if (maxlen > root) {
+    // Subtables, filled by symbol (zlib's replication) with all lanes: first every allocated entry
+    // invalid (an incomplete code's holes), then each code longer than the root writes its entries:
+    // with d = L - root bits past the prefix, the entries x = rev(last d code bits) + j * 2^d of its
+    // prefix's subtable. (Filling by entry took one lane 2^sb canonical searches in a row.)
+    const uint32_t used = min(U(tmp[0]), sub_cap);
+    for (uint32_t x = lane; x < used; x += 64) tab[size + x] = (K_BAD << 4) | 0xF;
+    __syncthreads();
+    const uint32_t i0 = U(M.offs[root + 1]), i1 = U(M.offs[maxlen]) + U(M.count[maxlen]);
+    for (uint32_t i = i0 + lane; i < i1; i += 64) {
+      const uint32_t sym = sorted[i], L = lens[sym];
+      const uint32_t code = M.first[L] + (i - M.offs[L]);  // MSB-first, L bits
+      const uint32_t d = L - root;
+      const uint32_t pe = tab[rev_bits(code >> d, root)];
+      if (!(pe & F_SUBT)) continue;  // its prefix took the slow path (no subtable space)
+      const uint32_t sb = (pe >> 6) & 15, sbase = pe >> 16;
+      const uint32_t ent = table_entry(kind, sym, L);
+      for (uint32_t x = rev_bits(code & ((1u << d) - 1), d); x < (1u << sb); x += 1u << d) tab[sbase + x] = ent;
+    }
+    __syncthreads();
+  }
   return true;
 }
 
@@ -558,6 +565,9 @@ __device__ __forceinline__ void flush(const Smem &S, uint8_t *out, uint64_t cap,
 #ifndef ZG_INFLATE_SEGCAP
 #define ZG_INFLATE_SEGCAP 96  // symbol records per lane region (a fuller region ends the round there)
 #endif
+#ifndef ZG_INFLATE_PCL
+#define ZG_INFLATE_PCL 1  // dynamic-header code lengths decoded lane-parallel (pointer-jumped windows)
+#endif
 #ifndef ZG_INFLATE_PIV
 #define ZG_INFLATE_PIV 1  // exec_batch: match source ranges by a two-level pivot search (no LDS search chain)
 #endif
@@ -573,9 +583,12 @@ constexpr uint32_t SG_END = 0, SG_EOB = 1, SG_BAD = 2, SG_SLOW = 3, SG_CAP = 4, 
 
 // One lane's view of the aligned word stream: words wi..wi+2 (96 bits) in registers, the next one
 // loaded ahead; positions are absolute bits of the aligned stream (the Bits domain).
+#ifndef ZG_INFLATE_LPF
+#define ZG_INFLATE_LPF 4  // words a lane's reader loads ahead of the three it decodes from (1..4)
+#endif
 struct LaneRd {
   const uint32_t *base;
-  uint32_t nwords, wi, w0, w1, w2, pf;
+  uint32_t nwords, wi, w0, w1, w2, pf, pf1, pf2, pf3;
   __device__ __forceinline__ uint32_t ld(uint32_t k) const { return k < nwords ? base[k] : 0u; }
   __device__ __forceinline__ void seek(uint64_t p) {
     wi = (uint32_t)(p >> 5);
@@ -583,14 +596,27 @@ struct LaneRd {
     w1 = ld(wi + 1);
     w2 = ld(wi + 2);
     pf = ld(wi + 3);
+    if (ZG_INFLATE_LPF > 1) pf1 = ld(wi + 4);
+    if (ZG_INFLATE_LPF > 2) pf2 = ld(wi + 5);
+    if (ZG_INFLATE_LPF > 3) pf3 = ld(wi + 6);
   }
-  __device__ __forceinline__ void adv(uint64_t p) {  // forward to the word holding bit p
+  // forward to the word holding bit p; the word ZG_INFLATE_LPF past the decode window is loaded
+  // then, so a load has ~LPF * 32 bits of decoding (a few symbols each) to arrive: the lanes' regions
+  // lie 64 B apart, every load of the wave touches 64 lines, and 3 words ahead stalled on HBM
+  __device__ __forceinline__ void adv(uint64_t p) {
     while ((uint32_t)(p >> 5) > wi) {
       w0 = w1;
       w1 = w2;
       w2 = pf;
+      if (ZG_INFLATE_LPF > 1) pf = pf1;
+      if (ZG_INFLATE_LPF > 2) pf1 = pf2;
+      if (ZG_INFLATE_LPF > 3) pf2 = pf3;
       wi++;
-      pf = ld(wi + 3);
+      const uint32_t nx = ld(wi + 2 + ZG_INFLATE_LPF);
+      if (ZG_INFLATE_LPF == 1) pf = nx;
+      else if (ZG_INFLATE_LPF == 2) pf1 = nx;
+      else if (ZG_INFLATE_LPF == 3) pf2 = nx;
+      else pf3 = nx;
     }
   }
   __device__ __forceinline__ void peek(uint64_t p, uint32_t &lo, uint32_t &hi) const {
@@ -1071,6 +1097,87 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(ZG_INFLATE_W
       // code lengths for literal/length + distance alphabets (ltab used as a 128-entry 7-bit table)
       uint32_t n = 0, prev = 0;
       const uint32_t total = hlit + hdist;
+#if ZG_INFLATE_PCL
+      // Lane-parallel, as the lookahead symbol decode: lane l decodes the code-length symbol (code +
+      // repeat bits, <= 14 bits) that would start at bit bp + l of a 63-bit window, the window's
+      // symbols are chained by pointer jumping, their runs placed by a prefix sum and written at
+      // once; a repeat-previous code (16) takes the value of the last explicit length before it
+      // (a ballot mask, not a scan). ~10 windows per header instead of ~150 dependent steps.
+      {
+        uint64_t bp = B.consumed;
+        bool have = false;  // a length was decoded before (16 needs one: zlib "invalid bit length repeat")
+        while (n < total && !err) {
+          uint32_t W0, W1, W2, W3, W4;
+          bits_words(B, (uint32_t)(bp >> 5), W0, W1, W2, W3, W4);
+          const uint32_t bit = (uint32_t)(bp & 31) + (uint32_t)lane;
+          const uint32_t wi = bit >> 5;
+          const uint32_t a0 = wi == 0 ? W0 : (wi == 1 ? W1 : W2);
+          const uint32_t a1 = wi == 0 ? W1 : (wi == 1 ? W2 : W3);
+          const uint32_t a2 = wi == 0 ? W2 : (wi == 1 ? W3 : W4);
+          const uint32_t lo = __builtin_amdgcn_alignbit(a1, a0, bit & 31), hi = __builtin_amdgcn_alignbit(a2, a1, bit & 31);
+          const uint32_t e = S.ltab[lo & 127];
+          const uint32_t L = e & 15, sym = e >> 16;
+          const uint32_t xb = sym == 16 ? 2u : (sym == 17 ? 3u : (sym == 18 ? 7u : 0u));
+          const uint32_t xv = (uint32_t)((((uint64_t)hi << 32) | lo) >> L) & ((1u << xb) - 1u);
+          const uint32_t adv = L + xb;
+          const uint32_t rep = sym < 16 ? 1u : (sym == 18 ? 11u : 3u) + xv;
+          // pointer jumping: p = the offset of this lane's (t-th) symbol in the window
+          uint32_t J = lane == 63 ? 63u : min<uint32_t>((uint32_t)lane + adv, 63u);
+          uint32_t p = (lane & 1) ? U(__builtin_amdgcn_readlane(J, 0)) : 0u;
+#pragma unroll
+          for (int k = 1; k <= 4; k++) {
+            J = (uint32_t)__builtin_amdgcn_ds_bpermute((int)(J << 2), (int)J);
+            const uint32_t q = (uint32_t)__builtin_amdgcn_ds_bpermute((int)(p << 2), (int)J);
+            if ((lane >> k) & 1) p = q;
+          }
+          const uint32_t sym_t = (uint32_t)__builtin_amdgcn_ds_bpermute((int)(p << 2), (int)sym);
+          const uint32_t rep_t = (uint32_t)__builtin_amdgcn_ds_bpermute((int)(p << 2), (int)rep);
+          const uint32_t adv_t = (uint32_t)__builtin_amdgcn_ds_bpermute((int)(p << 2), (int)adv);
+          const bool valid = p < 63 && lane < 32;
+          const uint32_t r = valid ? rep_t : 0u;
+          const uint32_t incl = wave_incl_sum(r), excl = incl - r;
+          const bool take = valid && excl < total - n;
+          const uint64_t tm = __ballot(take);
+          const uint32_t m = (uint32_t)__builtin_popcountll(tm);
+          if (!m) {  // no symbol fits the window: a corrupt stream
+            err = ZG_CORRUPT_STREAM;
+            break;
+          }
+          // the value a symbol writes: its length (< 16), 0 (17, 18), or the last explicit one (16)
+          const uint64_t expl = __ballot(take && sym_t != 16);
+          const uint64_t upto = expl & (lane == 63 ? ~0ull : ((2ull << lane) - 1));
+          const int src = upto ? 63 - __builtin_clzll(upto) : -1;
+          const uint32_t own = sym_t < 16 ? sym_t : 0u;
+          const uint32_t from = (uint32_t)__builtin_amdgcn_ds_bpermute((int)((src < 0 ? 0 : src) << 2), (int)own);
+          if (__ballot(take && sym_t == 16 && src < 0 && !have)) {
+            err = ZG_CORRUPT_STREAM;
+            break;
+          }
+          const uint32_t val = src < 0 ? prev : from;
+          const uint32_t last = m - 1;
+          const uint32_t n_new = n + U(__builtin_amdgcn_readlane(incl, (int)last));
+          if (n_new > total) {  // a run past the last length
+            err = ZG_CORRUPT_STREAM;
+            break;
+          }
+          if (take)
+            for (uint32_t k = 0; k < r; k++) {
+              const uint32_t si = n + excl + k;
+              S.lens[si < hlit ? si : 288 + (si - hlit)] = (uint8_t)val;
+            }
+          if (expl) {
+            const int hs = 63 - __builtin_clzll(expl);
+            prev = U(__builtin_amdgcn_readlane(own, hs));
+          }
+          have = true;
+          n = n_new;
+          bp += U(__builtin_amdgcn_readlane(p, (int)last)) + U(__builtin_amdgcn_readlane(adv_t, (int)last));
+          if (bp > end_bits) err = ZG_CORRUPT_STREAM;
+        }
+        if (!err) bits_seek_in(B, bp);
+        __syncthreads();
+      }
+#else
       while (n < total) {
         bits_refill(B);
         const uint32_t e = U(S.ltab[bits_peek(B, 7)]);
@@ -1101,6 +1208,7 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(ZG_INFLATE_W
         }
         n += rep;
       }
+#endif
       if (err) break;
       // zero the unused tails so the table builders see exactly hlit / hdist symbols
       for (uint32_t s = lane; s < 320; s += 64) {
@@ -1131,7 +1239,7 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(ZG_INFLATE_W
     // lookahead loop below takes the rest of the block).
     if (seg_scr) {
       uint32_t *myrec = seg_scr + ((uint64_t)blockIdx.x * 64 + (uint32_t)lane) * SEGCAP;
-      LaneRd R{B.base, B.nwords, 0, 0, 0, 0, 0};
+      LaneRd R{B.base, B.nwords, 0, 0, 0, 0, 0, 0, 0, 0};
       uint64_t r0 = B.consumed;
       bool fallback = false;
       while (!eob && !err && !fallback) {

@@ -40,7 +40,7 @@ namespace {
 thread_local std::string g_last_error;
 // device counters in the plan's control block (u64 each, cleared per execute)
 enum { CTR_ENC_BYTES = 0, CTR_ZSTD_SERIAL = 1, CTR_ZSTD_PARALLEL = 2, CTR_BLOSC_RERUN = 3, CTR_BLOSC_BLOCKS = 4,
-       CTR_N = 5 };
+       CTR_ITEMS = 5, CTR_N = 6 };  // CTR_ITEMS is host-side (the plan's leaf items)
 // internal ctl slots (not reported): a cached blosc layout was outgrown (the execution is re-run)
 enum { CTR_BLOSC_OVF = 31, CTR_SCRATCH = 30, CTR_ZSTD_NSER = 29, CTR_ZSTD_MAXBLK = 28 };  // not reported (device-side flags / sinks)
 thread_local uint64_t g_last_counters[CTR_N];
@@ -1090,6 +1090,7 @@ static int plan_statuses(zgpu_plan &P, int32_t *status, hipStream_t s) {
     P.zstd_serial_off = true;  // no serial item: later executions do not launch the fallback
   }
   std::memcpy(P.last_counters, P.h_ctl, sizeof(P.last_counters));
+  P.last_counters[CTR_ITEMS] = ni;
   for (int k = 0; k < CTR_N; k++) g_last_counters[k] += P.last_counters[k];
   const uint32_t *st = (const uint32_t *)(P.h_ctl + 256);
   P.last_enc_bytes = P.last_counters[CTR_ENC_BYTES];
@@ -3336,6 +3337,63 @@ int zgpu_encode_chunks(zgpu_chain *ch, uint32_t nd, const uint64_t *chunk_shape,
   }
   for (void *p : owned) C->dev_free(p);
   return rc;
+  ABI_GUARD_END
+}
+
+// One chunk (or shard) from host bytes, encoded on the GPU, the encoded bytes left in pooled pinned
+// memory for the caller to copy (the plugin's CodecChain::encode / ShardingCodecBound::encode).
+int zgpu_encode_pinned(zgpu_chain *ch, uint32_t nd, const uint64_t *chunk_shape, const void *decoded,
+                       const void **enc, uint64_t *enc_len, zgpu_result **result) {
+  ABI_GUARD_BEGIN
+  if (enc) *enc = nullptr;
+  if (result) *result = nullptr;
+  if (!ch || !chunk_shape || !decoded || !enc || !enc_len || !result)
+    return set_err(ZGPU_INVALID_ARGUMENT, "NULL argument");
+  if (nd == 0 || nd > ZGPU_MAX_DIMS) return set_err(ZGPU_INVALID_ARGUMENT, "ndim out of range");
+  zgpu_ctx *C = ch->ctx;
+  HIPCHK(hipSetDevice(C->device));
+  const int64_t bound = zgpu_chain_encoded_bound(ch, nd, chunk_shape);
+  if (bound < 0) return set_err(ZGPU_UNSUPPORTED, "encode: the chain's encoded size is not bounded");
+  const uint64_t nbytes = volume(chunk_shape, nd) * ch->chain->es;
+  uint8_t *d_in = (uint8_t *)C->dev_alloc(nbytes ? nbytes : 1);
+  uint8_t *d_out = (uint8_t *)C->dev_alloc(bound ? (uint64_t)bound : 1);
+  std::unique_ptr<zgpu_result> R(new zgpu_result());
+  ctx_ref(C);
+  R->ctx = C;
+  int rc = 0;
+  try {
+    hipStream_t s;
+    {
+      LaneScope ls(C);
+      s = pick_stream(ls.L, nullptr);
+      HIPCHK(hipMemcpyAsync(d_in, decoded, nbytes, hipMemcpyHostToDevice, s));
+      HIPCHK(hipStreamSynchronize(s));
+    }
+    zgpu_encode_desc D{};
+    D.dst = d_out;
+    D.dst_cap = (uint64_t)bound;
+    uint64_t len = 0;
+    rc = zgpu_encode_chunks(ch, nd, chunk_shape, d_in, chunk_shape, &D, 1, ZGPU_ENC_DEVICE | ZGPU_OUT_DEVICE, &len,
+                            nullptr);
+    if (!rc) {
+      R->own = (uint8_t *)C->host_alloc(len ? len : 1);
+      LaneScope ls(C);
+      s = pick_stream(ls.L, nullptr);
+      HIPCHK(hipMemcpyAsync(R->own, d_out, len, hipMemcpyDeviceToHost, s));
+      HIPCHK(hipStreamSynchronize(s));
+      *enc = R->own;
+      *enc_len = len;
+    }
+  } catch (...) {
+    C->dev_free(d_in);
+    C->dev_free(d_out);
+    throw;
+  }
+  C->dev_free(d_in);
+  C->dev_free(d_out);
+  if (rc) return rc;
+  *result = R.release();
+  return ZGPU_OK;
   ABI_GUARD_END
 }
 
