@@ -588,6 +588,8 @@ class C3:
         from zarrs_amd import _lib as L
         from zarrs_amd import CodecChain, make_desc
         lib = L.load()
+        torch.cuda.empty_cache()
+        self.args.ctx.release_cached()
         S, I = self.SHARD, self.INNER
         inner = CodecChain.from_metadata(self.CODECS[0]["configuration"]["codecs"], "float32", 0.0, self.args.ctx)
         out = np.empty(self.shape, np.float32)
@@ -678,7 +680,8 @@ class C3:
                 self.args.ctx.set_coalescing(window_us=200, max_calls=mc)
                 r = measure(coalesced, mc)
                 res.setdefault("sweep_max_calls", {})[str(mc)] = r
-            self.args.ctx.set_coalescing(window_us=200, max_calls=self.args.dropin_calls)
+            self.args.ctx.set_coalescing(window_us=getattr(self.args, "dropin_window_us", 200),
+                                         max_calls=self.args.dropin_calls)
             best = measure(coalesced, self.args.dropin_calls)
             res.update(best)
             res["max_calls_per_batch"] = self.args.dropin_calls
@@ -957,7 +960,76 @@ class C5:
                           f"oracle retrieve_array_subset per level (libzstd) with {threads} threads"}
 
     def host_leg(self, sp):
-        return {"encode": self.encode_leg()}
+        return {"encode": self.encode_leg(), "dropin_emulation": self.dropin_leg()}
+
+    def dropin_leg(self):
+        """zarrs' unchanged per-chunk read path with the per-codec GPU plugins (rust/zarrs_gpu
+        register_codecs: the entropy stage on the GPU, zarrs' own CPU codecs around it). CodecChain::
+        decode_into (codec_chain.rs:592-646) of a [bytes, numcodecs.shuffle{2}, zstd] chunk calls, per
+        chunk, from a rayon worker: ZstdCodec::decode -> the plugin: one coalesced zgpu_decode_pinned of
+        the host frame, copied into a new Vec; ShuffleCodec::decode (shuffle_codec.rs:109-129) on the
+        CPU into a new Vec; BytesCodec (little endian: passthrough) decode_into the array's view
+        (array_bytes_fixed_disjoint_view.rs:177-206). Emulated for every chunk of the pyramid from a
+        pool of the host's threads (numpy copies release the GIL); value = the pyramid's decoded
+        bytes / pass time, the same unit as the leg's cpu_baseline."""
+        from concurrent.futures import ThreadPoolExecutor
+        from zarrs_amd import _lib as L
+        from zarrs_amd import CodecChain, make_desc
+        lib = L.load()
+        zs_meta = self.CODECS[2]
+        chain = CodecChain.from_metadata([self.CODECS[0], zs_meta], "uint8", 0, self.args.ctx)
+        outs = [np.empty(s_, np.uint16) for s_ in self.level_shapes]
+        calls = []
+        for i, (li, idx) in enumerate(self.chunk_meta):
+            cs = self.CHUNKS[li]
+            nb = int(np.prod(cs)) * 2
+            enc = self.enc_host[i]
+            d = (L.ChunkDesc * 1)(make_desc((enc.ctypes.data, enc.nbytes), [nb]))
+            start = [k * c for k, c in zip(idx, cs)]
+            sel = [min(c, s_ - st) for c, s_, st in zip(cs, self.level_shapes[li], start)]
+            dst = tuple(slice(a, a + n_) for a, n_ in zip(start, sel))
+            calls.append((d, nb, cs, li, dst, tuple(slice(0, n_) for n_ in sel), enc))
+
+        def one(c):
+            d, nb, cs, li, dst, src_sel, _ = c
+            st = (C.c_int32 * 1)()
+            data, res_h = C.c_void_p(), C.c_void_p()
+            rc = lib.zgpu_decode_pinned(chain._h, 1, d, 1, L.u64s([nb]), L.COALESCE, st, C.byref(data), C.byref(res_h))
+            if rc:
+                raise L.ZgpuError(rc, L.last_error())
+            try:  # the plugin's decode returns an owned Vec: one copy out of the pinned result
+                zs = np.ctypeslib.as_array((C.c_uint8 * nb).from_address(data.value)).copy()
+            finally:
+                lib.zgpu_result_release(res_h)
+            # ShuffleCodec::decode (elementsize 2): dec[j*2 + i] = enc[i*count + j], into a new buffer
+            count = nb // 2
+            dec = np.empty((count, 2), np.uint8)
+            dec[:, 0] = zs[:count]
+            dec[:, 1] = zs[count:]
+            # BytesCodec decode_into the array's view (little endian: the bytes as they are)
+            outs[li][dst] = dec.view(np.uint16).reshape(cs)[src_sel]
+
+        threads = _threads()
+        self.args.ctx.set_coalescing(window_us=200, max_calls=8)
+        # the encode leg left torch's cache and the context's pools full: the per-call batches need room
+        torch.cuda.empty_cache()
+        self.args.ctx.release_cached()
+        with ThreadPoolExecutor(threads) as ex:
+            list(ex.map(one, calls))  # warm-up (pools, pinned buffers)
+            ok = all(np.array_equal(o, a) for o, a in zip(outs, self.levels_host))
+            st0 = self.args.ctx.coalescing_stats()
+            times = _time_reps(lambda: list(ex.map(one, calls)), 4.0)
+            st1 = self.args.ctx.coalescing_stats()
+        t = float(np.median(times))
+        nb_ = st1["batches"] - st0["batches"]
+        return {"GiBps": round(self.step_bytes / t / 2 ** 30, 2), "ms": round(t * 1e3, 1), "roundtrip_ok": ok,
+                "threads": threads, "calls": len(calls), "batches_per_pass": round(nb_ / len(times), 1),
+                "calls_per_batch": round((st1["calls"] - st0["calls"]) / max(1, nb_), 2),
+                "hip_env_GPU_MAX_HW_QUEUES": os.environ.get("GPU_MAX_HW_QUEUES", "unset (HIP default: 4)"),
+                "note": "per-chunk CodecChain::decode_into with the per-codec GPU plugins (zstd on the GPU through "
+                        "a coalesced zgpu_decode_pinned + one copy into a Vec; shuffle and bytes on the CPU, numpy "
+                        "standing in for zarrs' loops), one call per chunk from a thread pool; compare with the "
+                        "leg's cpu_baseline (the whole chain on the CPU)"}
 
     def encode_leg(self):
         """Write path (SURVEY 8(f) rank 3): CodecChain::encode of level 0's whole chunks ([32,512,512]
@@ -1432,8 +1504,8 @@ def secondary_legs(args, rank, world, dev, r_primary):
                 leg["cpu_baseline"] = W.cpu_baseline()
             except Exception as e:  # noqa: BLE001
                 leg["cpu_baseline"] = {"error": repr(e)[:300]}
-        if name == "c3" and rank == 0 and world == 1 and args.host_leg:
-            try:  # the drop-in boundary's own rate (per-shard calls from a thread pool), same data
+        if name in ("c3", "c5") and rank == 0 and world == 1 and args.host_leg:
+            try:  # the drop-in boundary's own rate (zarrs' per-shard / per-chunk calls from a thread pool)
                 leg["dropin_emulation"] = W.dropin_leg()
             except Exception as e:  # noqa: BLE001
                 leg["dropin_emulation"] = {"error": repr(e)[:300]}

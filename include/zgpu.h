@@ -106,6 +106,9 @@ int zgpu_ctx_create(int hip_device, zgpu_ctx **out);
 void zgpu_ctx_destroy(zgpu_ctx *ctx);
 /* Live references of a context (1 + its chains, plans and caches; diagnostics and tests). */
 int64_t zgpu_ctx_refcount(const zgpu_ctx *ctx);
+/* Return the context's cached free device and pinned buffers to HIP (buffers in use stay). The
+ * device pool also trims itself past ZGPU_POOL_CAP_MB (default 16 GiB) of free blocks. */
+int zgpu_ctx_release_cached(zgpu_ctx *ctx);
 /* Last error message of the calling thread on this context ("" if none). */
 const char *zgpu_last_error(const zgpu_ctx *ctx);
 const char *zgpu_status_name(int status);

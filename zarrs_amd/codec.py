@@ -75,6 +75,11 @@ class Context:
         caches (zgpu_ctx_refcount); 0 once closed."""
         return int(L.load().zgpu_ctx_refcount(self._h)) if getattr(self, "_h", None) else 0
 
+    def release_cached(self):
+        """Return the context's cached free device / pinned buffers to HIP (zgpu_ctx_release_cached)."""
+        if getattr(self, "_h", None):
+            L.check(L.load().zgpu_ctx_release_cached(self._h))
+
     def close(self):
         """Drop this handle's reference (zgpu_ctx_destroy). Chains, plans and caches made on the
         context keep it alive until they are destroyed too, in any order."""

@@ -81,6 +81,29 @@ struct Lane {
   hipEvent_t order_ev = nullptr;              // legacy-stream -> lane-stream ordering (pick_stream)
 };
 
+// A lane's stream. HIP maps streams onto GPU_MAX_HW_QUEUES hardware queues (4 by default), and
+// kernels of different streams sharing a queue run one after the other: 8 lanes (plus their pack
+// streams) on 4 queues serialised the drop-in's concurrent calls. A stream with a CU mask gets a
+// hardware queue of its own; with every CU in the mask (ZGPU_LANE_QUEUES=1) it is an ordinary stream
+// otherwise.
+static hipError_t lane_stream_create(hipStream_t *s) {
+  static const bool own = [] {
+    const char *e = std::getenv("ZGPU_LANE_QUEUES");
+    return e && std::atoi(e) != 0;
+  }();
+  if (own) {
+    int ncu = 0;
+    if (hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, 0) == hipSuccess && ncu > 0) {
+      std::vector<uint32_t> mask((ncu + 31) / 32, ~0u);
+      if (ncu % 32) mask.back() = (1u << (ncu % 32)) - 1;
+      const hipError_t e = hipExtStreamCreateWithCUMask(s, (uint32_t)mask.size(), mask.data());
+      if (e == hipSuccess) return e;
+      (void)hipGetLastError();
+    }
+  }
+  return hipStreamCreateWithFlags(s, hipStreamNonBlocking);
+}
+
 struct zgpu_ctx {
   int device = 0;
   // Lifetime: zgpu_ctx_destroy drops the caller's reference; every chain, plan and cache created on
@@ -107,7 +130,7 @@ struct zgpu_ctx {
       if (lanes_all.size() < max_lanes) {
         auto L = std::make_unique<Lane>();
         HIPCHK(hipSetDevice(device));
-        HIPCHK(hipStreamCreateWithFlags(&L->stream, hipStreamNonBlocking));
+        HIPCHK(lane_stream_create(&L->stream));
         lanes_all.push_back(L.get());
         lanes_free.push_back(L.release());
         break;
@@ -126,21 +149,44 @@ struct zgpu_ctx {
     lane_cv.notify_one();
   }
 
+  // Device pool: sizes rounded up to classes (1/8 of a power of two above 1 MiB: <= 12.5 % slack) so
+  // that buffers of batches of varying size are reused instead of accumulating; the free blocks are
+  // capped (ZGPU_POOL_CAP_MB, default 16 GiB: the largest are returned to HIP beyond it). Without the
+  // cap, thousands of concurrent per-chunk calls (the codec plugin's pattern) of varying batch sizes
+  // grew the pool until the device had no memory left for a kernel's scratch.
+  size_t free_dev_bytes = 0;
+  size_t pool_cap = (size_t)16 << 30;
+  static size_t size_class(size_t b) {
+    b = std::max<size_t>(256, (b + 255) & ~(size_t)255);
+    if (b <= (1u << 20)) return b;
+    size_t p = (size_t)1 << (63 - __builtin_clzll(b - 1));  // largest power of two < b
+    const size_t step = p / 8;
+    return (b + step - 1) / step * step;
+  }
+  void trim_free_locked(size_t keep) {
+    while (free_dev_bytes > keep && !free_dev.empty()) {
+      auto it = std::prev(free_dev.end());  // the largest free block
+      (void)hipFree(it->second);
+      free_dev_bytes -= it->first;
+      free_dev.erase(it);
+    }
+  }
   void *dev_alloc(size_t bytes) {
     std::lock_guard<std::mutex> lk(mu);
-    bytes = std::max<size_t>(256, (bytes + 255) & ~(size_t)255);
+    bytes = size_class(bytes);
     auto it = free_dev.lower_bound(bytes);
-    if (it != free_dev.end() && it->first <= bytes * 2 + (1u << 20)) {
+    if (it != free_dev.end() && it->first <= bytes + bytes / 4 + (1u << 20)) {
       void *p = it->second;
       live_dev[p] = it->first;
+      free_dev_bytes -= it->first;
       free_dev.erase(it);
       return p;
     }
     void *p = nullptr;
     hipError_t e = hipMalloc(&p, bytes);
     if (e != hipSuccess) {  // release the cache and retry once
-      for (auto &kv : free_dev) (void)hipFree(kv.second);
-      free_dev.clear();
+      (void)hipGetLastError();
+      trim_free_locked(0);
       HIPCHK(hipMalloc(&p, bytes));
     }
     live_dev[p] = bytes;
@@ -152,7 +198,9 @@ struct zgpu_ctx {
     auto it = live_dev.find(p);
     if (it == live_dev.end()) return;
     free_dev.emplace(it->second, p);
+    free_dev_bytes += it->second;
     live_dev.erase(it);
+    if (free_dev_bytes > pool_cap) trim_free_locked(pool_cap / 2);
   }
   void *host_alloc(size_t bytes) {
     std::lock_guard<std::mutex> lk(mu);
@@ -1739,6 +1787,7 @@ int zgpu_ctx_create(int dev, zgpu_ctx **out) {
   auto c = std::make_unique<zgpu_ctx>();
   c->device = dev;
   if (const char *e = std::getenv("ZGPU_CTX_LANES")) c->max_lanes = (uint32_t)std::max(1, std::min(64, std::atoi(e)));
+  if (const char *e = std::getenv("ZGPU_POOL_CAP_MB")) c->pool_cap = (size_t)std::max(64, std::atoi(e)) << 20;
   c->release_lane(c->acquire_lane());  // the first lane up front (stream creation errors surface here)
   *out = c.release();
   return ZGPU_OK;
@@ -1748,6 +1797,17 @@ int zgpu_ctx_create(int dev, zgpu_ctx **out) {
 void zgpu_ctx_destroy(zgpu_ctx *c) { ctx_unref(c); }
 
 int64_t zgpu_ctx_refcount(const zgpu_ctx *c) { return c ? c->refs.load() : 0; }
+
+int zgpu_ctx_release_cached(zgpu_ctx *c) {
+  if (!c) return set_err(ZGPU_INVALID_ARGUMENT, "NULL argument");
+  std::lock_guard<std::mutex> lk(c->mu);
+  if (hipSetDevice(c->device) != hipSuccess) (void)hipGetLastError();
+  c->trim_free_locked(0);
+  for (auto &kv : c->free_host) (void)hipHostFree(kv.second);
+  c->free_host.clear();
+  (void)hipGetLastError();
+  return ZGPU_OK;
+}
 
 int zgpu_chain_create(zgpu_ctx *ctx, const char *codecs_json, const char *data_type, const void *fill,
                       uint32_t fill_len, int validate, zgpu_chain **out) {
