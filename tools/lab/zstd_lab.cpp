@@ -55,8 +55,10 @@ int main(int argc, char **argv) {
     synth_c5_level0(512, 1024, 1024, 64, cz, cy, cx, sg, amp, 42, lvl.data(), 16);
   }
   std::vector<std::vector<uint8_t>> dec(n), enc(n);
+  // c5 modes: chunks past the 64 distinct ones repeat them (throughput at scale)
+  const int ndist = c5 ? std::min(n, 64) : n;
 #pragma omp parallel for
-  for (int c = 0; c < n; c++) {
+  for (int c = 0; c < ndist; c++) {
     if (c5) {
       const int ncz = l1 ? 64 : 32, ncy = l1 ? 256 : 512;
       const int z0 = (c / 4) * ncz, y0 = ((c / 2) % 2) * ncy, x0 = (c % 2) * ncy;
@@ -114,6 +116,10 @@ int main(int argc, char **argv) {
     enc[c].resize(r);
     ZSTD_freeCCtx(cc);
   }
+  for (int c = ndist; c < n; c++) {
+    dec[c] = dec[c % ndist];
+    enc[c] = enc[c % ndist];
+  }
   uint64_t total = 0;
   std::vector<uint64_t> off(n);
   for (int c = 0; c < n; c++) { off[c] = total; total += (enc[c].size() + 255) & ~255ull; }
@@ -139,12 +145,20 @@ int main(int argc, char **argv) {
   CK(hipMalloc(&Z.mode, n * 4));
   CK(hipMalloc(&Z.lit, n * Z.lit_stride));
   CK(hipMalloc(&Z.seq, n * Z.seq_cap * 12));
+
   constexpr int NK = 7;
   const char *kn[NK] = {"scan", "blocks", "huf", "lits", "plan", "direct", "exec_item"};
   hipEvent_t ev[NK + 1];
   for (auto &evk : ev) CK(hipEventCreate(&evk));
+
   float best[NK];
   for (auto &bk : best) bk = 1e30f;
+#ifdef ZG_SQ_PROFILE
+  {
+    unsigned long long z[20] = {0};
+    CK(hipMemcpyToSymbol(HIP_SYMBOL(zgpu::g_sqprof), z, sizeof(z)));
+  }
+#endif
 #ifdef ZG_PROFILE
   {
     unsigned long long z[13] = {0};
@@ -180,8 +194,19 @@ int main(int argc, char **argv) {
                        Z.lit_stride, Z.seq_cap, 0u, (unsigned long long *)nullptr, (uint32_t *)nullptr,
                        (unsigned long long *)nullptr, (unsigned long long *)nullptr);
     CK(hipEventRecord(ev[1]));
-    hipLaunchKernelGGL(zgpu::k_zstd_blocks, dim3(bgrid), dim3(64), 0, 0, d_items, d_status, blks, Z.blk_cap, Z.nblk,
-                       Z.mode, (uint32_t)n, Z.lit, Z.lit_stride, Z.seq, Z.seq_cap, (const unsigned long long *)nullptr);
+    const int seqm = getenv("LAB_SEQLG") ? atoi(getenv("LAB_SEQLG")) : 1;
+    if (seqm == 1) {  // the lane-group sequence decoder, as launch_zstd_pass
+      const uint64_t per_cu =
+          std::max<uint64_t>(1, (160u << 10) / ((sizeof(zgpu::ZDecLgSmem<ZG_SEQ_G>) + 1023) & ~size_t(1023)));
+      const uint32_t lg_grid =
+          (uint32_t)std::min<uint64_t>((recs + ZG_SEQ_G - 1) / ZG_SEQ_G, (uint64_t)ncu * per_cu);
+      hipLaunchKernelGGL(zgpu::k_zstd_blocks_lg<ZG_SEQ_G>, dim3(lg_grid), dim3(64), 0, 0, d_items, d_status, blks,
+                         Z.blk_cap, Z.nblk, Z.mode, (uint32_t)n, Z.seq, Z.seq_cap, (const unsigned long long *)nullptr);
+    } else {
+      hipLaunchKernelGGL(zgpu::k_zstd_blocks, dim3(bgrid), dim3(64), 0, 0, d_items, d_status, blks, Z.blk_cap,
+                         Z.nblk, Z.mode, (uint32_t)n, Z.lit, Z.lit_stride, Z.seq, Z.seq_cap,
+                         (const unsigned long long *)nullptr);
+    }
     CK(hipEventRecord(ev[2]));
     hipLaunchKernelGGL(zgpu::k_zstd_huf, dim3(grid), dim3(64), 0, 0, d_items, d_status, blks, Z.blk_cap, Z.nblk, Z.mode,
                        (uint32_t)n, Z.lit, Z.lit_stride, (const unsigned long long *)nullptr);
@@ -209,6 +234,7 @@ int main(int argc, char **argv) {
       CK(hipEventElapsedTime(&ms, ev[k], ev[k + 1]));
       best[k] = std::min(best[k], ms);
     }
+
   }
   std::vector<uint32_t> st(n), nblk(n), mode(n);
   CK(hipMemcpy(st.data(), d_status, n * 4, hipMemcpyDeviceToHost));
@@ -257,6 +283,19 @@ int main(int argc, char **argv) {
     printf("resolve per frame (Mticks): ready %.2f fast copies %.2f slow copies %.2f | rounds %.0f\n", z[8] / per / 1e6,
            z[9] / per / 1e6, z[10] / per / 1e6, (double)z[11] / per);
     printf("batches with far sources per frame: %.0f\n", z[12] / per);
+  }
+#endif
+#ifdef ZG_SQ_PROFILE
+  {
+    unsigned long long z[20];
+    CK(hipMemcpyFromSymbol(z, HIP_SYMBOL(zgpu::g_sqprof), sizeof(z)));
+    for (int t = 0; t < 3; t++)
+      printf("table %s modes (predefined / rle / fse / repeat): %llu %llu %llu %llu\n", t == 0 ? "LL" : t == 1 ? "OF" : "ML",
+             z[8 + 4 * t] / reps, z[9 + 4 * t] / reps, z[10 + 4 * t] / reps, z[11 + 4 * t] / reps);
+    const double nb = z[3] ? (double)z[3] : 1.0;
+    printf("sequences: %.0f blocks with sequences, %.1f sequences/block, records visited %llu, epochs %llu | per block "
+           "(clocks, wave sums): tables %.0f decode %.0f | per sequence: decode %.1f\n", nb / reps, z[2] / nb,
+           z[5] / reps, z[4] / reps, z[0] / nb, z[1] / nb, z[1] / (double)(z[2] ? z[2] : 1));
   }
 #endif
   printf("total %.3f ms -> %.2f GB/s decoded\n", tot, (double)n * chunk / tot / 1e6);

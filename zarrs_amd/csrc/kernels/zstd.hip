@@ -41,6 +41,16 @@ __device__ unsigned long long g_zprof[13];
 #define ZP_ADD(slot, t0)
 #define ZP_FLUSH
 #endif
+#ifdef ZG_SQ_PROFILE
+// lab-only sequence-decoder profile: [0] table-build clocks, [1] decode clocks, [2] sequences,
+// [3] blocks with sequences, [4] epochs (lane-group decoder), [5] records visited
+__device__ unsigned long long g_sqprof[20];  // [8 + 4 t + mode]: table modes (LL, OF, ML) in the scan
+#define SQP_T(v) const uint64_t v = clock64()
+#define SQP_ADD(slot, x) do { if (__lane_id() == 0) atomicAdd(&g_sqprof[slot], (unsigned long long)(x)); } while (0)
+#else
+#define SQP_T(v)
+#define SQP_ADD(slot, x) do { } while (0)
+#endif
 
 namespace {
 
@@ -288,51 +298,84 @@ __device__ uint32_t read_ncount(IN &I, uint64_t off, uint64_t avail, int16_t *no
   return (uint32_t)bytes;
 }
 
-// Build an FSE decoding table from normalized counts (FSE_buildDTable).
+// Build an FSE decoding table from normalized counts (FSE_buildDTable semantics, RFC 8878 4.1.1),
+// all 64 lanes of the wave at once (lane s owns symbol s; nsym <= 64). The spread visits positions
+// p_i = i * step & mask, skipping those above the low-probability region; the k-th visited position
+// takes the symbol whose cumulative count range holds k, so each lane places its share of i directly
+// (a prefix count of valid i, a 6-step binary search of the cumulative counts). A position's state
+// counter is its symbol's count plus the symbol's earlier occurrences in table order: per 64
+// positions, the lanes holding one symbol find each other with 6 ballots (symbol bits). The old
+// scalar form walked the table twice, one LDS round trip per position (~0.1 ms per table).
+// `norm` is consumed: it holds the per-symbol running counters afterwards.
 template <bool WS = false>
-__device__ void build_fse(Fse *T, const int16_t *norm, uint32_t nsym, uint32_t acc_log, uint32_t *tmp) {
+__device__ void build_fse(Fse *T, int16_t *norm, uint32_t nsym, uint32_t acc_log, uint32_t *tmp) {
+  (void)tmp;
   const uint32_t size = 1u << acc_log, mask = size - 1;
   const int lane = lane_id();
-  // low-probability (-1) symbols at the top, then spread the others
-  uint32_t high = size - 1;
-  for (uint32_t s = 0; s < nsym; s++) {
-    if (U((uint32_t)(int32_t)norm[s]) == 0xFFFFFFFFu) {
-      if (lane == 0) {
-        T[high].sym = (uint8_t)s;
-      }
-      high--;
-    }
+  const uint64_t lt = (1ull << lane) - 1;
+  const int32_t c = lane < (int)nsym ? (int32_t)norm[lane] : 0;
+  const uint64_t lowm = __ballot(c == -1);
+  const uint32_t nlow = (uint32_t)__popcll(lowm);
+  const uint32_t high = size - 1 - nlow;
+  if (c == -1) T[size - 1 - (uint32_t)__popcll(lowm & lt)].sym = (uint8_t)lane;  // the top, in symbol order
+  // cumulative counts: start_s (exclusive); past nsym a value no k reaches
+  const uint32_t cnt = c > 0 ? (uint32_t)c : 0u;
+  uint32_t inc = cnt;
+  for (int o = 1; o < 64; o <<= 1) {
+    const uint32_t t = __shfl_up(inc, o, 64);
+    if (lane >= o) inc += t;
   }
+  const uint32_t start = lane < (int)nsym ? inc - cnt : 0xFFFFu;
   const uint32_t step = (size >> 1) + (size >> 3) + 3;
-  uint32_t pos = 0;
-  for (uint32_t s = 0; s < nsym; s++) {
-    const int32_t c = (int32_t)U((uint32_t)(int32_t)norm[s]);
-    for (int32_t i = 0; i < c; i++) {
-      if (lane == 0) T[pos].sym = (uint8_t)s;
-      do {
-        pos = (pos + step) & mask;
-      } while (pos > high);
+  const uint32_t per = (size + 63) >> 6, i0 = (uint32_t)lane * per;
+  uint32_t nv = 0;
+  for (uint32_t j = 0; j < per; j++) {
+    const uint32_t i = i0 + j;
+    nv += (i < size && ((i * step) & mask) <= high) ? 1u : 0u;
+  }
+  uint32_t kx = nv;
+  for (int o = 1; o < 64; o <<= 1) {
+    const uint32_t t = __shfl_up(kx, o, 64);
+    if (lane >= o) kx += t;
+  }
+  uint32_t k = kx - nv;  // rank of this lane's first valid i
+  for (uint32_t j = 0; j < per; j++) {
+    const uint32_t i = i0 + j, pos = (i * step) & mask;
+    const bool v = i < size && pos <= high;
+    uint32_t sl = 0;
+    for (int st = 32; st; st >>= 1) {
+      const uint32_t sv = (uint32_t)__shfl((int)start, (int)(sl + st), 64);
+      if (sv <= k) sl += st;
+    }
+    if (v) {
+      T[pos].sym = (uint8_t)sl;
+      k++;
     }
   }
+  if (lane < (int)nsym) norm[lane] = (int16_t)(c == -1 ? 1 : c);
   zsync<WS>();
-  // state info: lane s owns symbol s (nsym <= 64); symbols' next-state counters start at norm[s]
-  // (1 for -1 symbols) and advance in increasing table position.
-  uint32_t next = 0;
-  if (lane < (int)nsym) {
-    const int32_t c = norm[lane];
-    next = c == -1 ? 1u : (uint32_t)c;
-  }
-  for (uint32_t u = 0; u < size; u++) {
-    const uint32_t s = T[u].sym;
-    if ((uint32_t)lane == s) {
-      const uint32_t nb = acc_log - highbit(next);
+  for (uint32_t b = 0; b < size; b += 64) {
+    const uint32_t u = b + (uint32_t)lane;
+    const bool v = u < size;
+    const uint32_t s = v ? (uint32_t)T[u].sym : 0u;
+    uint64_t peer = __ballot(v);
+#pragma unroll
+    for (int bit = 0; bit < 6; bit++) {
+      const bool on = (s >> bit) & 1;
+      const uint64_t bb = __ballot(v && on);
+      peer &= on ? bb : ~bb;
+    }
+    const uint32_t rank = (uint32_t)__popcll(peer & lt), pc = (uint32_t)__popcll(peer);
+    const uint32_t nx = v ? (uint32_t)(uint16_t)norm[s] : 0u, jn = nx + rank;
+    zsync<WS>();
+    if (v && rank == 0) norm[s] = (int16_t)(nx + pc);
+    if (v) {
+      const uint32_t nb = acc_log - highbit(jn);
       T[u].nb = (uint8_t)nb;
-      T[u].base = (uint16_t)((next << nb) - size);
-      next++;
+      T[u].base = (uint16_t)((jn << nb) - size);
     }
+    zsync<WS>();
   }
-  zsync<WS>();
-  (void)tmp;
 }
 
 template <bool WS = false>
@@ -347,7 +390,7 @@ __device__ void build_fse_rle(Fse *T, uint32_t sym) {
 
 template <bool WS = false>
 __device__ void build_fse_default(Fse *T, const int16_t *def, uint32_t nsym, uint32_t acc_log, int16_t *norm,
-                                  uint32_t *tmp) {
+                                  uint32_t *tmp) {  // norm: scratch
   for (uint32_t s = lane_id(); s < nsym; s += 64) norm[s] = def[s];
   zsync<WS>();
   build_fse<WS>(T, norm, nsym, acc_log, tmp);
@@ -1369,6 +1412,9 @@ __global__ __launch_bounds__(64) void k_zstd_scan(const ZgItem *items, uint32_t 
             }
           }
           if (!ok) SFAIL(ZG_CORRUPT_STREAM);
+#ifdef ZG_SQ_PROFILE
+          if (lane == 0) for (int t = 0; t < 3; t++) atomicAdd(&g_sqprof[8 + t * 4 + mm[t]], 1ull);
+#endif
           R.tab_mode = tmode[0] | (tmode[1] << 2) | (tmode[2] << 4);
           R.tab_off[0] = toff[0];
           R.tab_off[1] = toff[1];
@@ -1439,7 +1485,9 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(ZG_BLK_WPE, 
     uint32_t r0 = ZSYM | (0u << 24), r1 = ZSYM | (1u << 24), r2 = ZSYM | (2u << 24);
     int32_t reach_c = INT32_MIN;
     uint32_t reach_m0 = ~0u, reach_m1 = ~0u, reach_m2 = ~0u;
+    SQP_ADD(5, 1);
     if (!bad && nseq) {
+      SQP_T(sq_t0);
       const uint32_t tm = U(Bp->tab_mode);
       uint32_t lg[3] = {0, 0, 0};
       for (int t = 0; t < 3 && !bad; t++) {
@@ -1461,7 +1509,7 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(ZG_BLK_WPE, 
           lg[t] = 0;
         } else {
           uint32_t acc, ns;
-          In Ic = I;
+          InW Ic(in, it.len);  // the description through a register window, not a load per byte
           if (!read_ncount(Ic, off, it.len - off, S.norm, maxs, maxl, acc, ns)) { bad = true; break; }
           __syncthreads();
           build_fse(T, S.norm, ns, acc, S.tmp);
@@ -1493,6 +1541,8 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(ZG_BLK_WPE, 
         if (ZG_SEQ_ONE_FSE && !ZG_SEQ_PACK) __syncthreads();  // the next table reuses S.fse
       }
       if (!ZG_SEQ_ONE_FSE || ZG_SEQ_PACK) __syncthreads();
+      SQP_T(sq_t1);
+      SQP_ADD(0, sq_t1 - sq_t0);
       // Backward bit container in SGPRs: C holds bits [32 * lw, 32 * lw + have) of the aligned item
       // words, the next unread bit at bit 63; refilled a word at a time from the BitsBack register
       // window (readlane), so a field read is three scalar operations.
@@ -1649,6 +1699,10 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(ZG_BLK_WPE, 
         // the stream must end exactly on its first bit
         if (!bad && (int64_t)lw * 32 + have != R.lo_bit) bad = true;
       }
+      SQP_T(sq_t2);
+      SQP_ADD(1, sq_t2 - sq_t1);
+      SQP_ADD(2, nseq);
+      SQP_ADD(3, 1);
     }
     if (!bad && sum_ll > regen) bad = true;
     if (!bad && regen + sum_ml > BLOCK_MAX) bad = true;  // a block decodes to at most 128 KiB
@@ -1666,6 +1720,289 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(ZG_BLK_WPE, 
         Bp->rep_out[2] = r2;
       }
     }
+  }
+}
+
+// -------------------------------------------------------------------------------------------------
+// Lane-group sequence decoder (ZGPU_ZSTD_SEQ=1, default): ZG_SEQ_G blocks per wave, one lane each.
+// k_zstd_blocks above runs one block per wave as wave-uniform scalar code (~120 scalar instructions a
+// sequence), and the CU's one scalar unit, shared by the ~20 waves resident on it, bounded the
+// whole decoder. Here the serial FSE chain of a block runs in one lane's vector registers, so one
+// vector instruction advances ZG_SEQ_G blocks and four SIMDs share the work: each lane has its own
+// backward bit container (refilled from a 4-word prefetch queue of its block's stream), its three
+// states, its repeat offsets (symbolic, as above) and its block's three tables, built into its own
+// slot of LDS by the whole wave before the decode (5 KiB per block). Output and record fields are
+// those of k_zstd_blocks.
+#ifndef ZG_SEQ_G
+#define ZG_SEQ_G 4
+#endif
+#ifndef ZG_SEQ_WN
+#define ZG_SEQ_WN 128  // staged stream words per block and epoch
+#endif
+template <int G>
+struct ZDecLgSmem {
+  uint32_t xl[G][512], xm[G][512], xo[G][256];
+  uint32_t win[G][ZG_SEQ_WN];
+  uint32_t llb[36], mlb[53];
+  int16_t norm[64];
+  uint32_t tmp[32];
+};
+
+#ifndef ZG_SEQ_WPE
+#define ZG_SEQ_WPE 1  // lane-group decoder: minimum waves per SIMD the register allocation must allow
+#endif
+template <int G>
+__global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(ZG_SEQ_WPE, 8))) void k_zstd_blocks_lg(const ZgItem *items, uint32_t *status, ZBlk *blks,
+                                                       uint32_t blk_cap, const uint32_t *nblk, const uint32_t *zmode,
+                                                       uint32_t n_items, uint32_t *seq_scratch, uint64_t seq_cap,
+                                                       const unsigned long long *max_nblk) {
+  __shared__ ZDecLgSmem<G> S;
+  const int lane = lane_id();
+  for (int k = lane; k < 53; k += 64) {
+    if (k < 36) S.llb[k] = c_ll_base[k];
+    S.mlb[k] = c_ml_base[k];
+  }
+  const uint64_t total = (uint64_t)n_items * rec_blocks(blk_cap, max_nblk);
+  for (uint64_t g0 = (uint64_t)blockIdx.x * G; g0 < total; g0 += (uint64_t)gridDim.x * G) {
+    SQP_T(sq_t0);
+    SQP_ADD(5, G);
+    // ---- the wave builds the tables of its G records, one record at a time; lane k keeps record
+    // k's fields (block-major record order, as k_zstd_blocks)
+    bool mine = false, bad = false;
+    ZBlk *Bp = nullptr;
+    uint32_t item = 0, nseq = 0, regen = 0, lg0 = 0, lg1 = 0, lg2 = 0, seq_off = 0, seq_end = 0, seq_buf = 0;
+    for (int k = 0; k < G; k++) {
+      const uint64_t g = g0 + k;
+      if (g >= total) break;
+      const uint32_t it_k = (uint32_t)(g % n_items), bi = (uint32_t)(g / n_items);
+      if (bi >= nblk[it_k] || zmode[it_k] != ZMODE_PARALLEL) continue;
+      ZBlk *B = blks + (uint64_t)it_k * blk_cap + bi;
+      const uint32_t flags = U(B->flags);
+      if ((flags & 3) != ZB_CMP) continue;
+      const ZgItem it = items[it_k];
+      const In I{(const uint8_t *)it.src, it.len};
+      const uint32_t ns_k = U(B->nseq);
+      bool bad_k = false;
+      uint32_t lg[3] = {0, 0, 0};
+      if (ns_k) {
+        const uint32_t tm = U(B->tab_mode);
+        __syncthreads();  // the previous use of norm / tmp is done
+        for (int t = 0; t < 3 && !bad_k; t++) {
+          const uint32_t mode = (tm >> (2 * t)) & 3, off = U(B->tab_off[t]);
+          Fse *T = (Fse *)(t == 0 ? S.xl[k] : t == 1 ? S.xo[k] : S.xm[k]);  // built in place, repacked below
+          const uint32_t maxs = t == 0 ? 35 : t == 1 ? 31 : 52, maxl = t == 0 ? 9 : t == 1 ? 8 : 9;
+          if (mode == 0) {
+            if (t == 0) { build_fse_default(T, c_ll_def, 36, 6, S.norm, S.tmp); lg[t] = 6; }
+            else if (t == 1) { build_fse_default(T, c_of_def, 29, 5, S.norm, S.tmp); lg[t] = 5; }
+            else { build_fse_default(T, c_ml_def, 53, 6, S.norm, S.tmp); lg[t] = 6; }
+          } else if (mode == 1) {
+            build_fse_rle(T, I.b(off));
+            lg[t] = 0;
+          } else {
+            uint32_t acc, ns;
+            InW Ic((const uint8_t *)it.src, it.len);
+            if (!read_ncount(Ic, off, it.len - off, S.norm, maxs, maxl, acc, ns)) { bad_k = true; break; }
+            __syncthreads();
+            build_fse(T, S.norm, ns, acc, S.tmp);
+            lg[t] = acc;
+          }
+          __syncthreads();
+          for (uint32_t u = lane; u < (1u << lg[t]); u += 64) {
+            const Fse e = T[u];
+            uint32_t x;
+            if (t == 0) x = e.sym <= 35 ? sq_pack(e.base, e.nb, c_ll_bits[e.sym], e.sym) : SQ_BAD;
+            else if (t == 1) x = e.sym <= 31 ? sq_pack(e.base, e.nb, e.sym, e.sym) : SQ_BAD;
+            else x = e.sym <= 52 ? sq_pack(e.base, e.nb, c_ml_bits[e.sym], e.sym) : SQ_BAD;
+            ((uint32_t *)T)[u] = x;
+          }
+        }
+      }
+      if (lane == k) {
+        mine = true;
+        bad = bad_k;
+        Bp = B;
+        item = it_k;
+        nseq = ns_k;
+        regen = U(B->regen);
+        lg0 = lg[0];
+        lg1 = lg[1];
+        lg2 = lg[2];
+        seq_off = U(B->seq_off);
+        seq_end = U(B->seq_end);
+        seq_buf = U(B->seq_buf);
+      }
+    }
+    __syncthreads();
+    // ---- every lane decodes its own block's sequences, in epochs: the wave stages the next ZG_SEQ_WN
+    // words of each lane's stream into LDS (one coalesced load per lane and block, one wait), then
+    // each lane decodes until fewer than three staged words remain below its position (a sequence
+    // takes at most three refills). No global load inside the decode loop, so the sequence stores
+    // are never waited on, and a sequence's three table reads and three word reads issue together.
+    uint64_t sum_ll = 0, sum_ml = 0;
+    uint32_t r0 = ZSYM | (0u << 24), r1 = ZSYM | (1u << 24), r2 = ZSYM | (2u << 24);
+    int32_t reach_c = INT32_MIN;
+    uint32_t reach_m0 = ~0u, reach_m1 = ~0u, reach_m2 = ~0u;
+    const uint32_t *words = nullptr;
+    int32_t nwords = 0, lw = 0, have = 0, lo_w = 0;
+    int64_t lo_bit = 0;
+    uint64_t C = 0;
+    bool act = false;
+    uint32_t sll = 0, sof = 0, sml = 0, n = 0;
+    uint32_t *out = nullptr;
+    if (mine && !bad && nseq) {
+      const ZgItem it = items[item];
+      const uint8_t *in = (const uint8_t *)it.src;
+      const uintptr_t mis = (uintptr_t)in & 3;
+      words = (const uint32_t *)((uintptr_t)in - mis);
+      nwords = (int32_t)((it.len + mis + 3) / 4);
+      const uint32_t last = seq_end > seq_off ? in[seq_end - 1] : 0u;
+      if (last == 0) {
+        bad = true;
+      } else {
+        const int64_t p0 = (int64_t)(seq_end - 1 + mis) * 8 + highbit(last);
+        lo_bit = (int64_t)(seq_off + mis) * 8;
+        lw = (int32_t)((p0 - 1) >> 5) - 1;
+        have = (int32_t)(p0 - 32 * (int64_t)lw);  // (32, 64]
+        auto ld = [&](int32_t k) -> uint32_t { return (k >= 0 && k < nwords) ? words[k] : 0u; };
+        C = (((uint64_t)ld(lw + 1) << 32) | ld(lw)) << (64 - have);
+        act = true;
+        out = seq_scratch + ((uint64_t)item * seq_cap + seq_buf) * 3;
+      }
+    }
+    bool first = true;
+    SQP_T(sq_t1);
+    SQP_ADD(0, sq_t1 - sq_t0);
+#ifdef ZG_SQ_PROFILE
+    if (mine && nseq) {
+      atomicAdd(&g_sqprof[2], (unsigned long long)nseq);
+      atomicAdd(&g_sqprof[3], 1ull);
+    }
+#endif
+    while (__any(act)) {
+      SQP_ADD(4, 1);
+      // stage words [lw - WN, lw) of every active lane's stream: lane k's window is S.win[k]
+      lo_w = lw - ZG_SEQ_WN;
+#pragma unroll
+      for (int k = 0; k < G; k++) {
+        const bool ak = __builtin_amdgcn_readlane((int)act, k) != 0;
+        if (!ak) continue;
+        const uint64_t wp = ((uint64_t)(uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)(uintptr_t)words, k)) |
+                            ((uint64_t)(uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)((uintptr_t)words >> 32), k) << 32);
+        const int32_t nw = __builtin_amdgcn_readlane(nwords, k), b = __builtin_amdgcn_readlane(lo_w, k);
+        const uint32_t *W = (const uint32_t *)(uintptr_t)wp;
+        for (int i = lane; i < ZG_SEQ_WN; i += 64) {
+          const int32_t w = b + i;
+          S.win[k][i] = (w >= 0 && w < nw) ? W[w] : 0u;
+        }
+      }
+      __syncthreads();
+      if (act && first) {  // the three initial states
+        first = false;
+        // the container holds > 32 bits, at most 9 + 8 read before the refill
+        sll = (uint32_t)((C >> 1) >> (63 - lg0));
+        C <<= lg0;
+        have -= (int32_t)lg0;
+        sof = (uint32_t)((C >> 1) >> (63 - lg1));
+        C <<= lg1;
+        have -= (int32_t)lg1;
+        if (have <= 32) {
+          lw--;
+          C |= (uint64_t)S.win[lane][lw - lo_w] << (32 - have);
+          have += 32;
+        }
+        sml = (uint32_t)((C >> 1) >> (63 - lg2));
+        C <<= lg2;
+        have -= (int32_t)lg2;
+      }
+      const uint32_t k = (uint32_t)lane;
+      while (act && lw - 3 >= lo_w) {
+        // everything this sequence can read: its three table entries and the next three words
+        const uint32_t ow = S.xo[k][sof], mw = S.xm[k][sml], lwd = S.xl[k][sll];
+        uint32_t w1 = S.win[k][lw - 1 - lo_w], w2 = S.win[k][lw - 2 - lo_w], w3 = S.win[k][lw - 3 - lo_w];
+        if ((ow | mw | lwd) & SQ_BAD) { bad = true; act = false; break; }
+        auto refill = [&]() {
+          const bool nd = have <= 32;
+          C |= nd ? (uint64_t)w1 << (32 - have) : 0ull;
+          have += nd ? 32 : 0;
+          lw -= nd ? 1 : 0;
+          w1 = nd ? w2 : w1;
+          w2 = nd ? w3 : w2;
+        };
+        auto rd = [&](uint32_t nb) -> uint32_t {  // nb <= 31 bits
+          const uint32_t v = (uint32_t)((C >> 1) >> (63 - nb));
+          C <<= nb;
+          have -= (int32_t)nb;
+          return v;
+        };
+        const uint32_t oc = (ow >> 18) & 63, mc = (mw >> 18) & 63, lc = (lwd >> 18) & 63;
+        refill();
+        const uint32_t ofv = (1u << oc) + rd(oc);
+        refill();
+        const uint32_t ml = S.mlb[mc] + rd((mw >> 13) & 31);
+        const uint32_t ll = S.llb[lc] + rd((lwd >> 13) & 31);
+        n++;
+        if (n < nseq) {
+          refill();
+          sll = (lwd & 511) + rd((lwd >> 9) & 15);
+          sml = (mw & 511) + rd((mw >> 9) & 15);
+          sof = (ow & 511) + rd((ow >> 9) & 15);
+        }
+        // repeat offsets, symbolically in the block's incoming rep state (RFC 8878 3.1.1.5), as
+        // selects: kk = 0 a new offset, else 1 + repeat index
+        const uint32_t kk = ofv > 3 ? 0u : ofv + (ll == 0 ? 1u : 0u);
+        if (kk == 0 && ((ofv - 3) & ZSYM)) { bad = true; act = false; break; }  // beyond any window we decode
+        const uint32_t s3 = (r0 & ZSYM) ? r0 + 1 : r0 - 1;
+        uint32_t off = ofv - 3;
+        off = kk == 1 ? r0 : off;
+        off = kk == 2 ? r1 : off;
+        off = kk == 3 ? r2 : off;
+        off = kk == 4 ? s3 : off;
+        const uint32_t n2 = (kk == 0 || kk >= 3) ? r1 : r2;
+        const uint32_t n1 = kk == 1 ? r1 : r0;
+        r2 = n2;
+        r1 = n1;
+        r0 = off;
+        // how far the match reaches back from the block start (exact, per match)
+        const int32_t p = (int32_t)(sum_ll + sum_ml + ll);
+        const bool isc = !(off & ZSYM);
+        const uint32_t slot = (off >> 24) & 3, mv = (off & 0xFFFFFF) + (uint32_t)p;
+        reach_c = isc ? max(reach_c, (int32_t)off - p) : reach_c;
+        reach_m0 = (!isc && slot == 0) ? min(reach_m0, mv) : reach_m0;
+        reach_m1 = (!isc && slot == 1) ? min(reach_m1, mv) : reach_m1;
+        reach_m2 = (!isc && slot >= 2) ? min(reach_m2, mv) : reach_m2;
+        sum_ll += ll;
+        sum_ml += ml;
+        uint32_t *o = out + (uint64_t)(n - 1) * 3;
+        o[0] = ll;
+        o[1] = ml;
+        o[2] = off;
+        if (n == nseq) {
+          act = false;
+          // the stream must end exactly on its first bit
+          if ((int64_t)lw * 32 + have != lo_bit) bad = true;
+        }
+      }
+      __syncthreads();  // this epoch's window reads are done before the next staging
+    }
+    SQP_T(sq_t2);
+    SQP_ADD(1, sq_t2 - sq_t1);
+    if (mine) {
+      if (!bad && sum_ll > regen) bad = true;
+      if (!bad && regen + sum_ml > BLOCK_MAX) bad = true;  // a block decodes to at most 128 KiB
+      if (bad) {
+        status[item] = ZG_CORRUPT_STREAM;
+      } else {
+        Bp->out_size = (uint32_t)(regen + sum_ml);
+        Bp->reach_c = reach_c;
+        Bp->reach_m[0] = reach_m0;
+        Bp->reach_m[1] = reach_m1;
+        Bp->reach_m[2] = reach_m2;
+        Bp->rep_out[0] = r0;
+        Bp->rep_out[1] = r1;
+        Bp->rep_out[2] = r2;
+      }
+    }
+    __syncthreads();  // the tables are rebuilt for the next records
   }
 }
 
@@ -3454,8 +3791,22 @@ static hipError_t launch_zstd_pass(ZgItem *items, uint32_t *status, uint32_t n_i
   // one resident wave of the sequence decoder: CUs x 4 SIMDs x ZG_BLK_WPE waves
   const uint32_t bgrid =
       (uint32_t)std::min<uint64_t>(recs, std::max<uint64_t>(g_cap, (uint64_t)device_cu_count() * 4 * ZG_BLK_WPE));
-  hipLaunchKernelGGL(k_zstd_blocks, dim3(bgrid), dim3(64), 0, sq, items, status, blks, Z.blk_cap, Z.nblk, Z.mode,
-                     n_items, Z.lit, Z.lit_stride, Z.seq, Z.seq_cap, Z.max_nblk);
+  // sequence decoder: 1 lane groups (k_zstd_blocks_lg, default), 0 one wave per block (k_zstd_blocks)
+  static const int seq_mode = [] {
+    const char *e = std::getenv("ZGPU_ZSTD_SEQ");
+    return e ? std::atoi(e) : 1;
+  }();
+  if (seq_mode == 1) {
+    // one resident wave of the lane-group decoder: its LDS (5 KiB per block) sets the waves per CU
+    const uint64_t per_cu = std::max<uint64_t>(1, (160u << 10) / ((sizeof(ZDecLgSmem<ZG_SEQ_G>) + 1023) & ~size_t(1023)));
+    const uint64_t lrecs = (recs + ZG_SEQ_G - 1) / ZG_SEQ_G;
+    const uint32_t lg_grid = (uint32_t)std::min<uint64_t>(lrecs, (uint64_t)device_cu_count() * per_cu);
+    hipLaunchKernelGGL(k_zstd_blocks_lg<ZG_SEQ_G>, dim3(lg_grid), dim3(64), 0, sq, items, status, blks, Z.blk_cap,
+                       Z.nblk, Z.mode, n_items, Z.seq, Z.seq_cap, Z.max_nblk);
+  } else {
+    hipLaunchKernelGGL(k_zstd_blocks, dim3(bgrid), dim3(64), 0, sq, items, status, blks, Z.blk_cap, Z.nblk, Z.mode,
+                       n_items, Z.lit, Z.lit_stride, Z.seq, Z.seq_cap, Z.max_nblk);
+  }
   if (fork) {
     hipError_t e = hipEventRecord(Z.ev_join, Z.side);
     if (e != hipSuccess) return e;
