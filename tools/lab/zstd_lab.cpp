@@ -219,7 +219,7 @@ int main(int argc, char **argv) {
     CK(hipEventRecord(ev[5]));
     hipLaunchKernelGGL(zgpu::k_zstd_direct, dim3(grid), dim3(256), 0, 0, d_items, d_status, blks, Z.blk_cap, Z.nblk,
                        Z.mode, (uint32_t)n, d_out, chunk, Z.lit, Z.lit_stride, (const uint64_t *)nullptr,
-                       (const unsigned long long *)nullptr);
+                       (const unsigned long long *)nullptr, 0);
     CK(hipEventRecord(ev[6]));
     if (getenv("LAB_XDENSE"))
       hipLaunchKernelGGL(zgpu::xdense::k_zstd_exec_item, dim3(n * zgpu::XSEG), dim3(64), 0, 0, d_items, d_status, blks,

@@ -3300,6 +3300,27 @@ __global__ __launch_bounds__(64) void k_zstd_huf(const ZgItem *items, const uint
   }
 }
 #endif
+// Blocks whose output is their literals alone (raw, rle, or compressed without sequences) depend on
+// nothing before them: k_zstd_direct writes them into the slot with the whole GPU ahead of the
+// per-item execution, which only flushes up to them and steps over (at least XDIRECT bytes: a
+// shorter block costs the executor less than the restart of its ring).
+constexpr uint32_t XDIRECT = 4096;
+__device__ __forceinline__ bool x_direct_block(uint32_t flags, uint32_t nseq, uint32_t out_size) {
+  const uint32_t type = flags & 3;
+  return out_size >= XDIRECT && (type == ZB_RAW || type == ZB_RLE || (type == ZB_CMP && nseq == 0));
+}
+
+// A compressed block without sequences is its literals: when k_zstd_plan has run before the literal
+// decoder (one stream, no aliases: launch_zstd_pass), k_zstd_lits writes them straight into the slot
+// at the block's output offset and k_zstd_direct leaves the block alone - the literal scratch round
+// trip (written by the literal decoder, read and written again by the direct copy) was 17.7 GB of
+// C5's 149 GB per step. The predicate both kernels apply:
+__device__ __forceinline__ bool lits_in_slot(uint32_t flags, uint32_t nseq, uint32_t regen, uint32_t out_size,
+                                             uint32_t out_off, uint64_t slot_bytes) {
+  return (flags & 3) == ZB_CMP && ((flags >> 2) & 3) != 0 && nseq == 0 && regen == out_size && out_size >= XDIRECT &&
+         (uint64_t)out_off + out_size <= slot_bytes;
+}
+
 
 #if ZG_LIT_ILP == 2
 #define ZG_LITS_DECODE(...) lits_decode2(__VA_ARGS__)
@@ -3310,7 +3331,8 @@ __global__ __launch_bounds__(LIT_THREADS) __attribute__((amdgpu_waves_per_eu(ZG_
                                                            uint32_t blk_cap, const uint32_t *nblk,
                                                            const uint32_t *zmode, uint32_t n_items,
                                                            uint8_t *lit_scratch, uint64_t lit_stride,
-                                                           uint8_t *lit_rec, const unsigned long long *max_nblk) {
+                                                           uint8_t *lit_rec, const unsigned long long *max_nblk,
+                                                           uint8_t *dst = nullptr, uint64_t slot_bytes = 0) {
   __shared__ ZLitSmem S;
   const uint32_t t = threadIdx.x;
   // this lane's record slot (ZG_LIT_REC; nullptr: every lane decodes twice)
@@ -3327,7 +3349,10 @@ __global__ __launch_bounds__(LIT_THREADS) __attribute__((amdgpu_waves_per_eu(ZG_
     const ZgItem it = items[item];
     const uint8_t *in = (const uint8_t *)it.src;
     const uint32_t regen = Bp->regen;
-    uint8_t *lit = lit_scratch + (uint64_t)item * lit_stride + Bp->lit_buf;
+    uint8_t *const lit_s = lit_scratch + (uint64_t)item * lit_stride + Bp->lit_buf;
+    uint8_t *lit = lit_s;
+    if (dst && status[item] == 0 && lits_in_slot(flags, Bp->nseq, regen, Bp->out_size, Bp->out_off, slot_bytes))
+      lit = dst + (uint64_t)item * slot_bytes + Bp->out_off;
     __syncthreads();  // the previous record's LDS use is over
     if (ltype == 1) {  // RLE literals
       const uint8_t v = in[Bp->lit_off];
@@ -3337,7 +3362,7 @@ __global__ __launch_bounds__(LIT_THREADS) __attribute__((amdgpu_waves_per_eu(ZG_
     const uint32_t lo0 = Bp->lit_off, lend = Bp->lit_end;
 #if ZG_HUF_SPLIT
     // the table k_zstd_huf built: 16-B loads, one per thread
-    const uint8_t *tab = lit - HUF_TAB;
+    const uint8_t *tab = lit_s - HUF_TAB;
     const uint32_t tl = *(const uint32_t *)(tab + (HUF_TAB - 16));
     if (tl) {
       const uint32_t n16 = ((2u << tl) + 15) / 16;  // tables of 2^tl u16 entries (tl >= 1)
@@ -3457,16 +3482,6 @@ __global__ __launch_bounds__(LIT_THREADS) __attribute__((amdgpu_waves_per_eu(ZG_
 }
 
 // One wave per item: output offsets, incoming rep offsets, frame size checks.
-// Blocks whose output is their literals alone (raw, rle, or compressed without sequences) depend on
-// nothing before them: k_zstd_direct writes them into the slot with the whole GPU ahead of the
-// per-item execution, which only flushes up to them and steps over (at least XDIRECT bytes: a
-// shorter block costs the executor less than the restart of its ring).
-constexpr uint32_t XDIRECT = 4096;
-__device__ __forceinline__ bool x_direct_block(uint32_t flags, uint32_t nseq, uint32_t out_size) {
-  const uint32_t type = flags & 3;
-  return out_size >= XDIRECT && (type == ZB_RAW || type == ZB_RLE || (type == ZB_CMP && nseq == 0));
-}
-
 // Executor segments: an item's blocks are cut where no later match reaches back before the cut (and
 // not inside a checksummed frame); each segment gets its own k_zstd_exec_item wave. Byte-shuffled
 // images cut at their byte planes (tools/lab/zstd_taint.cpp: no match crosses the plane boundary).
@@ -3600,7 +3615,8 @@ __global__ __launch_bounds__(256) void k_zstd_direct(const ZgItem *items, const 
                                                     uint32_t blk_cap, const uint32_t *nblk, const uint32_t *zmode,
                                                     uint32_t n_items, uint8_t *dst, uint64_t slot_bytes,
                                                     const uint8_t *lit_scratch, uint64_t lit_stride,
-                                                    const uint64_t *alias, const unsigned long long *max_nblk) {
+                                                    const uint64_t *alias, const unsigned long long *max_nblk,
+                                                    int lits_direct) {
   const uint64_t recs = (uint64_t)n_items * rec_blocks(blk_cap, max_nblk);
   const uint32_t tid = threadIdx.x;
   for (uint64_t rec = blockIdx.x; rec < recs; rec += gridDim.x) {
@@ -3610,6 +3626,7 @@ __global__ __launch_bounds__(256) void k_zstd_direct(const ZgItem *items, const 
     const uint32_t flags = b.flags, type = flags & 3, n = b.out_size;
     if (!x_direct_block(flags, b.nseq, n)) continue;
     if (type == ZB_CMP && b.regen != n) continue;  // corrupt: k_zstd_exec_item reports it
+    if (lits_direct && lits_in_slot(flags, b.nseq, b.regen, n, b.out_off, slot_bytes)) continue;  // k_zstd_lits wrote it
     if (alias) {  // the consumer reads an aliased block where it is
       const uint64_t *a = alias + 3 * ZALIAS * (uint64_t)item;
       bool al = false;
@@ -3783,6 +3800,20 @@ static hipError_t launch_zstd_pass(ZgItem *items, uint32_t *status, uint32_t n_i
   // the sequence scratch): with a side stream it runs beside the literal kernels
   const bool fork = Z.side && Z.ev_fork && Z.ev_join;
   hipStream_t sq = fork ? Z.side : s;
+  // literal-only blocks decoded straight into the slot (lits_in_slot): needs k_zstd_plan's output
+  // offsets before the literal decoder, i.e. the sequence decoder on the same stream, and no aliases
+  static const bool lit_direct_env = [] {
+    const char *e = std::getenv("ZGPU_ZSTD_LITDIRECT");
+    return !e || std::atoi(e) != 0;
+  }();
+  const bool lit_direct = lit_direct_env && !fork && !Z.alias;
+  // executor segments per item: ZG_XSEG (ZGPU_ZSTD_XSEG: tuning)
+  static const uint32_t xseg_env = [] {
+    const char *e = std::getenv("ZGPU_ZSTD_XSEG");
+    return e ? (uint32_t)std::min<unsigned long>(64, std::max<unsigned long>(1, std::strtoul(e, nullptr, 10))) : 0u;
+  }();
+  const uint32_t xseg = xseg_env ? xseg_env : XSEG;
+
   if (fork) {
     hipError_t e = hipEventRecord(Z.ev_fork, s);
     if (e == hipSuccess) e = hipStreamWaitEvent(Z.side, Z.ev_fork, 0);
@@ -3811,6 +3842,9 @@ static hipError_t launch_zstd_pass(ZgItem *items, uint32_t *status, uint32_t n_i
     hipError_t e = hipEventRecord(Z.ev_join, Z.side);
     if (e != hipSuccess) return e;
   }
+  if (lit_direct)  // output offsets first: the literal decoder writes literal-only blocks into the slot
+    hipLaunchKernelGGL(k_zstd_plan, dim3(n_items), dim3(64), 0, s, items, status, blks, Z.blk_cap, Z.nblk, Z.mode,
+                       slot_bytes, xseg, Z.alias, Z.lit, Z.lit_stride);
 #if ZG_HUF_SPLIT
   hipLaunchKernelGGL(k_zstd_huf, dim3(grid), dim3(64), 0, s, items, status, blks, Z.blk_cap, Z.nblk, Z.mode, n_items,
                      Z.lit, Z.lit_stride, Z.max_nblk);
@@ -3818,7 +3852,7 @@ static hipError_t launch_zstd_pass(ZgItem *items, uint32_t *status, uint32_t n_i
   // record slots: one per lane of the persistent grid (allocated for l_cap workgroups)
   uint8_t *lit_rec = (ZG_LIT_REC && Z.lit_rec && lgrid <= Z.lit_rec_wgs) ? Z.lit_rec : nullptr;
   hipLaunchKernelGGL(k_zstd_lits, dim3(lgrid), dim3(LIT_THREADS), 0, s, items, status, blks, Z.blk_cap, Z.nblk,
-                     Z.mode, n_items, Z.lit, Z.lit_stride, lit_rec, Z.max_nblk);
+                     Z.mode, n_items, Z.lit, Z.lit_stride, lit_rec, Z.max_nblk, lit_direct ? dst : nullptr, slot_bytes);
   if (fork) {
     hipError_t e = hipStreamWaitEvent(s, Z.ev_join, 0);
     if (e != hipSuccess) return e;
@@ -3827,16 +3861,11 @@ static hipError_t launch_zstd_pass(ZgItem *items, uint32_t *status, uint32_t n_i
     hipError_t e = hipEventRecord(ev_entropy, s);
     if (e != hipSuccess) return e;
   }
-  // executor segments per item: ZG_XSEG (ZGPU_ZSTD_XSEG: tuning)
-  static const uint32_t xseg_env = [] {
-    const char *e = std::getenv("ZGPU_ZSTD_XSEG");
-    return e ? (uint32_t)std::min<unsigned long>(64, std::max<unsigned long>(1, std::strtoul(e, nullptr, 10))) : 0u;
-  }();
-  const uint32_t xseg = xseg_env ? xseg_env : XSEG;
-  hipLaunchKernelGGL(k_zstd_plan, dim3(n_items), dim3(64), 0, s, items, status, blks, Z.blk_cap, Z.nblk, Z.mode,
-                     slot_bytes, xseg, Z.alias, Z.lit, Z.lit_stride);
+  if (!lit_direct)
+    hipLaunchKernelGGL(k_zstd_plan, dim3(n_items), dim3(64), 0, s, items, status, blks, Z.blk_cap, Z.nblk, Z.mode,
+                       slot_bytes, xseg, Z.alias, Z.lit, Z.lit_stride);
   hipLaunchKernelGGL(k_zstd_direct, dim3(grid), dim3(256), 0, s, items, status, blks, Z.blk_cap, Z.nblk, Z.mode,
-                     n_items, dst, slot_bytes, Z.lit, Z.lit_stride, Z.alias, Z.max_nblk);
+                     n_items, dst, slot_bytes, Z.lit, Z.lit_stride, Z.alias, Z.max_nblk, lit_direct ? 1 : 0);
   // executor configuration: xdense when the grid has many waves per CU (ZGPU_ZSTD_XDENSE=0/1 forces one)
   const char *xd_s = std::getenv("ZGPU_ZSTD_XDENSE");  // read per call (tests force both)
   const int xd_env = xd_s ? std::atoi(xd_s) : -1;
