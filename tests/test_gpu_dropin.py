@@ -162,6 +162,32 @@ def _coalesced_full(ctx, data, bad_key=None, threads=16):
     return a, out, res
 
 
+def test_lone_coalesced_caller_does_not_wait_the_window(ctx, data):
+    """A coalesced call with no other call in flight closes its batch at once (the collect window is
+    for concurrent callers): with a 300 ms window a lone shard call must not take 300 ms."""
+    import time
+    from zarrs_amd import CodecChain, make_desc
+    a, shards = data
+    ch = CodecChain.from_metadata(CODECS, "float32", 0.0, ctx)
+    out = np.full(SHAPE, SENTINEL, np.float32)
+    key = (0, 1, 3)
+    o = _origin(key)
+    call = lambda co: ch.decode_batch_into([make_desc(shards[key], [SH] * 3)], out, o, [SH] * 3,  # noqa: E731
+                                           enc_device=False, coalesce=co)
+    call(False)  # warm the chain's plan and pools
+    ctx.set_coalescing(window_us=300000, max_calls=16)
+    try:
+        t0 = time.perf_counter()
+        st = call(True)
+        dt = time.perf_counter() - t0
+    finally:
+        ctx.set_coalescing(window_us=200, max_calls=8)
+    assert st == [0]
+    win = tuple(slice(s, s + SH) for s in o)
+    assert np.array_equal(out[win], a[win])
+    assert dt < 0.15, dt
+
+
 def test_coalesced_full_shards(ctx, data):
     ctx.set_coalescing(window_us=50000, max_calls=16)
     before = ctx.coalescing_stats()
