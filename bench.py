@@ -1544,7 +1544,8 @@ def pmc_traffic(args, W):
     """HBM traffic of the dominant kernel from rocprofv3 PMC counters, in two separate passes
     (FETCH_SIZE and WRITE_SIZE cannot share one pass on gfx950), corrected as
     /opt/skills/guides/MI355X_MICROARCH.md (HBM) prescribes: counters are in KiB; FETCH_SIZE counts
-    exactly half the bytes of a wide (16 B/lane) coalesced streaming read on gfx950 -> x2; WRITE_SIZE
+    exactly half the bytes of a wide (16 B/lane) coalesced streaming read on gfx950 -> x2 (and, measured
+    with tools/lab/fetch_calib.hip, of 4- and 8-B coalesced and per-lane segment reads too); WRITE_SIZE
     is exact for 16-B streaming stores. Runs bench.py itself as a child under rocprofv3. A workload
     whose step is a kernel pipeline (W.pmc_regex, e.g. C5) reports the sum over one step's dispatches;
     otherwise the average per launch of W.kernel."""
@@ -1607,8 +1608,9 @@ def pmc_traffic(args, W):
            "per": "step (all dispatches matching " + regex + ")" if per_step else "launch of " + regex,
            "source": "rocprofv3 --pmc FETCH_SIZE / WRITE_SIZE passes (KiB; FETCH x2 on gfx950)"}
     if per_step:
-        out["note"] = ("the x2 FETCH correction is calibrated for 16-B/lane streaming reads only; the entropy "
-                       "kernels also read with narrower loads (uncalibrated), so fetch_bytes may be overstated")
+        out["note"] = ("the x2 FETCH correction, which the guide calibrates for 16-B/lane streaming reads, was "
+                       "calibrated here for the entropy kernels' narrower loads too (4/8-B coalesced and per-lane "
+                       "segment reads also report half: profiles/r05/r05cal_pmc_calibration_and_crc_fold_ab.txt)")
     return out, None
 
 
