@@ -1672,7 +1672,7 @@ def main():
                     help="workloads measured after the headline and reported in its line's `secondary` object "
                          "(comma-separated; '' for none)")
     ap.add_argument("--c5-cache", default="", help=argparse.SUPPRESS)
-    ap.add_argument("--dropin-calls", type=int, default=4,
+    ap.add_argument("--dropin-calls", type=int, default=8,
                     help="C3 drop-in leg: most calls one coalesced GPU batch takes (zgpu_ctx_set_coalescing)")
     ap.add_argument("--dropin-sweep", default="", help="C3 drop-in leg: also measure these max_calls values (a,b,...)")
     ap.add_argument("--secondary-c5-scale", type=int, default=1,

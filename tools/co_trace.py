@@ -29,8 +29,9 @@ for k in ("wait", "setup", "h2d", "decode", "d2h", "pack", "alloc", "copy", "cop
 span = (min(r["t0"] for r in rows), max(r["end"] for r in rows))
 busy = sum(b - a for a, b in (r["busy"] for r in rows))
 print(f"span {(span[1] - span[0]) / 1e3:.1f} ms, lane-busy {busy / 1e3:.1f} ms = {busy / (span[1] - span[0]):.2f} lanes on average")
-for boxed in (0, 1):
+for boxed in (0, 1, 2):
     v = [r for r in rows if r["boxed"] == boxed]
     if v:
-        print(f"  {'box-copied' if boxed else 'compact'} batches {len(v)}: pack median {st.median(r['pack'] for r in v) / 1e3:.2f} ms, "
+        name = ("compact", "box-copied (kernel)", "rect-copied (3-D DMA)")[boxed]
+        print(f"  {name} batches {len(v)}: pack median {st.median(r['pack'] for r in v) / 1e3:.2f} ms, "
               f"D2H median {st.median(r['copy'] for r in v) / 1e3:.2f} ms")

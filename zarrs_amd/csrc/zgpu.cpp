@@ -2255,6 +2255,12 @@ struct Coalescer {
   uint64_t max_bytes = 1ull << 30;
   uint64_t batches = 0, calls = 0, seq = 0;
   uint64_t active = 0;  // coalescable calls inside coalesced_call (under mu)
+  // Batches decoding at once (under mu): a leader waits for a slot while its batch keeps taking
+  // joiners. Each batch is a synchronous H2D -> decode -> D2H chain on its lane; with more of them than
+  // the process's HIP hardware queues (4 by default) their kernels queue behind each other, and a few
+  // larger batches fill the GPU better (drop-in sweep, profiles/r05/r05d8_dropin_rect_pack_inflight_cap.txt).
+  uint32_t max_inflight = 3, inflight = 0;
+  std::condition_variable slot_cv;
 };
 
 // ZGPU_TRACE=1: one stderr line per coalesced-batch phase (microseconds since the first trace)
@@ -2281,6 +2287,7 @@ static Coalescer &coalescer(zgpu_ctx *C) {
     if (const char *e = std::getenv("ZGPU_COALESCE_US")) C->co->window_us = (uint32_t)std::max(0, std::atoi(e));
     if (const char *e = std::getenv("ZGPU_COALESCE_CALLS")) C->co->max_calls = (uint32_t)std::max(1, std::atoi(e));
     if (const char *e = std::getenv("ZGPU_COALESCE_BYTES")) C->co->max_bytes = std::strtoull(e, nullptr, 10);
+    if (const char *e = std::getenv("ZGPU_CO_INFLIGHT")) C->co->max_inflight = (uint32_t)std::max(1, std::atoi(e));
   }
   return *C->co;
 }
@@ -2367,14 +2374,53 @@ static void co_run(CoBatch &B, Lane *LN) {
     for (CoCall *c : B.calls)
       for (uint32_t d = 1; d < nd; d++)
         if (c->V.shape[d] != stacked[d]) compact = false;
-    const uint8_t *src = dout;
+    std::vector<BoxRuns> boxes;
+    bool rect = false;  // every window a 3-D box: packed by the copy engines, no kernel
     if (!compact) {
-      dpack = (uint8_t *)C->dev_alloc(pack_bytes ? pack_bytes : 1);
+      static const bool rect_on = [] {
+        const char *e = std::getenv("ZGPU_CO_PACK_RECT");
+        return !e || std::atoi(e) != 0;
+      }();
+      rect = rect_on;
       for (size_t k = 0; k < B.calls.size(); k++) {
-        const zgpu_out_view &V = B.calls[k]->V;
         uint64_t org[ZG_MAXD] = {0};
         org[0] = row0[k];
-        const BoxRuns R = box_runs(nd, stacked, org, V.shape, es);
+        boxes.push_back(box_runs(nd, stacked, org, B.calls[k]->V.shape, es));
+        if (boxes.back().outer > 2) rect = false;
+      }
+    }
+    // power-of-two size classes (>= 64 MiB): batches of varying size reuse pooled pinned buffers
+    // instead of page-locking new ones
+    if (compact || rect) co_trace("packed", B.id, compact ? 0 : 2);
+    uint64_t cls = 64ull << 20;
+    while (cls < pack_bytes) cls <<= 1;
+    B.pack = (uint8_t *)C->host_alloc(cls);
+    co_trace("pack-alloc", B.id);
+    if (compact) {
+      if (pack_bytes) HIPCHK(hipMemcpyAsync(B.pack, dout, pack_bytes, hipMemcpyDeviceToHost, s));
+    } else if (rect) {
+      // Each caller's window straight from the stacked output into its place in the pinned pack as
+      // one pitched 3-D copy (DMA): a box-copy kernel queued while other lanes' decode waves hold the
+      // CUs waited for their slots (trace: pack median 5 ms at 8 lanes, 20 ms at 2 lanes with bigger
+      // batches), and the copy engines need none.
+      for (size_t k = 0; k < B.calls.size(); k++) {
+        const BoxRuns &R = boxes[k];
+        if (!R.n_runs) continue;
+        const uint64_t w = R.run_bytes;
+        const uint64_t h = R.outer >= 1 ? R.shape[R.outer - 1] : 1, depth = R.outer >= 2 ? R.shape[0] : 1;
+        const uint64_t pitch = R.outer >= 1 ? R.stride[R.outer - 1] : w;
+        const uint64_t sy = R.outer >= 2 ? R.stride[0] / pitch : h;
+        hipMemcpy3DParms p3{};
+        p3.srcPtr = make_hipPitchedPtr(dout + R.base, pitch, w, sy);
+        p3.dstPtr = make_hipPitchedPtr(B.pack + B.calls[k]->pack_off, w, w, h);
+        p3.extent = make_hipExtent(w, h, depth);
+        p3.kind = hipMemcpyDeviceToHost;
+        HIPCHK(hipMemcpy3DAsync(&p3, s));
+      }
+    } else {
+      dpack = (uint8_t *)C->dev_alloc(pack_bytes ? pack_bytes : 1);
+      for (size_t k = 0; k < B.calls.size(); k++) {
+        const BoxRuns &R = boxes[k];
         ZgBoxCopy P{};
         P.outer = R.outer;
         for (uint32_t d = 0; d < R.outer; d++) {
@@ -2392,19 +2438,12 @@ static void co_run(CoBatch &B, Lane *LN) {
         P.n_runs = R.n_runs;
         HIPCHK(launch_box_copy(dout, dpack, P, s));
       }
-      src = dpack;
+      if (co_tracing()) {
+        HIPCHK(hipStreamSynchronize(s));
+        co_trace("packed", B.id, 1);
+      }
+      if (pack_bytes) HIPCHK(hipMemcpyAsync(B.pack, dpack, pack_bytes, hipMemcpyDeviceToHost, s));
     }
-    // power-of-two size classes (>= 64 MiB): batches of varying size reuse pooled pinned buffers
-    // instead of page-locking new ones
-    if (co_tracing()) {
-      HIPCHK(hipStreamSynchronize(s));
-      co_trace("packed", B.id, compact ? 0 : 1);
-    }
-    uint64_t cls = 64ull << 20;
-    while (cls < pack_bytes) cls <<= 1;
-    B.pack = (uint8_t *)C->host_alloc(cls);
-    co_trace("pack-alloc", B.id);
-    if (pack_bytes) HIPCHK(hipMemcpyAsync(B.pack, src, pack_bytes, hipMemcpyDeviceToHost, s));
     HIPCHK(hipStreamSynchronize(s));
     co_trace("d2h-done", B.id, pack_bytes);
   } catch (...) {
@@ -2549,6 +2588,8 @@ static int coalesced_call(zgpu_chain *ch, uint32_t nd, const zgpu_chunk_desc *de
     if (K.active > 1)
       B->cv.wait_until(lk, std::chrono::steady_clock::now() + std::chrono::microseconds(K.window_us),
                        [&] { return B->closed; });
+    K.slot_cv.wait(lk, [&] { return K.inflight < K.max_inflight; });
+    K.inflight++;
     lk.unlock();
     int rc = 0;
     std::string err;
@@ -2580,6 +2621,8 @@ static int coalesced_call(zgpu_chain *ch, uint32_t nd, const zgpu_chunk_desc *de
     }
     if (LN) C->release_lane(LN);
     lk.lock();
+    K.inflight--;
+    K.slot_cv.notify_one();
     for (CoCall *c : B->calls) {
       if (rc) {
         c->rc = rc;
