@@ -154,8 +154,8 @@ int main(int argc, char **argv) {
            "trailer crc %.0f\n", (double)prof[12] / n, (double)prof[8] / n, (double)prof[9] / n, (double)prof[10] / n,
            (double)prof[11] / n);
   if (prof[13])
-    printf("  segmented decode: %.1f rounds/chunk, repair loop %.0f cycles/chunk\n", (double)prof[13] / n,
-           (double)prof[14] / n);
+    printf("  segmented decode: %.1f rounds/chunk, repair loop %.0f cycles/chunk, slow-path fallbacks %.2f/chunk\n",
+           (double)prof[13] / n, (double)prof[14] / n, (double)prof[15] / n);
   if (prof[6])
     printf("  per chunk: %.0f batches, %.1f symbols/batch, %.2f match rounds/batch\n", (double)prof[6] / n,
            (double)prof[7] / prof[6], (double)prof[5] / prof[6]);

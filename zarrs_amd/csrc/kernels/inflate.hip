@@ -34,6 +34,7 @@
 #include <hip/hip_runtime.h>
 
 #include <cstdlib>
+#include <type_traits>
 
 #include "../common.hpp"
 #include "crc.hpp"
@@ -156,8 +157,6 @@ struct Smem {
     };
     CrcTables crc;  // after the last block: the gzip trailer's CRC-32 of the decoded stream
   };
-  uint64_t crc_len[1];
-  uint32_t crc_val[1];
   uint8_t sink[4];  // the executor's discarded byte stores (branch-free short copies)
   uint16_t lsorted[288];
   uint16_t dsorted[32];
@@ -180,8 +179,33 @@ struct Smem {
   };
 };
 
+// The pipelined latency mode (k_gzip<false, true>): wave 0 decodes the symbol regions of round r+1
+// while wave 1 executes round r's records. Its own batch intervals (Smem's share their space with the
+// block header wave 0 parses meanwhile) and the hand-off: per message slot the message, the round's
+// symbol count and each decoder lane's region (first symbol, record offset, count), and the output
+// state the waves pass back and forth when wave 0 writes output itself (stored blocks, the canonical
+// slow path, the stream's end).
+constexpr uint32_t P_END = 0, P_ROUND = 1, P_SYNC = 2;
+struct SmemP : Smem {
+  union {
+    uint16_t rbeg[64];
+    uint4 rbeg4[8];
+  };
+  uint16_t rend[64];
+  uint32_t p_msg[2], p_total[2], p_err;
+  uint64_t p_pos, p_flushed;
+  uint32_t p_rb[2][64], p_ro[2][64], p_cnt[2][64];
+};
+
 __device__ __forceinline__ uint32_t U(uint32_t x) { return __builtin_amdgcn_readfirstlane(x); }
 __device__ __forceinline__ int lane_id() { return __lane_id(); }
+// Syncs inside k_gzip are wave syncs: its workgroup is one wave (throughput mode) or two waves with
+// roles of their own (k_gzip<.., true>, the pipelined latency mode), whose only workgroup barriers
+// are the hand-offs between them. In a one-wave workgroup this is what __syncthreads() was.
+__device__ __forceinline__ void wsync() {
+  __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "workgroup");
+  __builtin_amdgcn_wave_barrier();
+}
 // inclusive wave64 prefix sum: row shifts within 16 lanes, then row broadcasts (DPP, no LDS)
 __device__ __forceinline__ uint32_t wave_incl_sum(uint32_t x) {
   x += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0x111, 0xf, 0xf, false);  // row_shr:1
@@ -334,12 +358,12 @@ __device__ bool build_table(const uint8_t *lens, uint32_t n, uint32_t root, uint
                             HuffMeta &M, int kind, uint32_t *tmp, uint32_t sub_cap) {
   const int lane = lane_id();
   if (lane < 16) tmp[lane] = 0;
-  __syncthreads();
+  wsync();
   for (uint32_t s = lane; s < n; s += 64) {
     const uint32_t l = lens[s];
     if (l) atomicAdd(&tmp[l], 1u);
   }
-  __syncthreads();
+  wsync();
   // uniform: counts, validity, first codes, offsets
   uint32_t cnt[16];
   for (int l = 0; l < 16; l++) cnt[l] = U(tmp[l]);
@@ -374,7 +398,7 @@ __device__ bool build_table(const uint8_t *lens, uint32_t n, uint32_t root, uint
     M.maxlen = (uint16_t)maxlen;
     tmp[0] = 0;  // subtable allocation counter (the counts were read above)
   }
-  __syncthreads();
+  wsync();
   // sorted symbols (by length, then symbol) via ballot ranks. The per-length offsets and codes are
   // read from M in LDS (uniform addresses): private arrays indexed by a loop variable would live in
   // scratch memory (one scratch round trip per access; 17 % of k_gzip's time went to table builds)
@@ -394,7 +418,7 @@ __device__ bool build_table(const uint8_t *lens, uint32_t n, uint32_t root, uint
       b += __builtin_popcountll(m);
     }
   }
-  __syncthreads();
+  wsync();
   // root table fill: entry e <-> R-bit MSB-first prefix v = reverse(e). A prefix of codes longer
   // than the root gets a subtable of 2^sb entries (sb = its longest code - root), indexed by the next
   // sb stream bits; subtables are allocated from tab[size..size+sub_cap) by an LDS counter (tmp[0]).
@@ -424,7 +448,7 @@ __device__ bool build_table(const uint8_t *lens, uint32_t n, uint32_t root, uint
     }
     tab[e] = entry;
   }
-  __syncthreads();
+  wsync();
   if (maxlen > root) {
     // Subtables, filled by symbol (zlib's replication) with all lanes: first every allocated entry
     // invalid (an incomplete code's holes), then each code longer than the root writes its entries:
@@ -432,7 +456,7 @@ __device__ bool build_table(const uint8_t *lens, uint32_t n, uint32_t root, uint
     // prefix's subtable. (Filling by entry took one lane 2^sb canonical searches in a row.)
     const uint32_t used = min(U(tmp[0]), sub_cap);
     for (uint32_t x = lane; x < used; x += 64) tab[size + x] = (K_BAD << 4) | 0xF;
-    __syncthreads();
+    wsync();
     const uint32_t i0 = U(M.offs[root + 1]), i1 = U(M.offs[maxlen]) + U(M.count[maxlen]);
     for (uint32_t i = i0 + lane; i < i1; i += 64) {
       const uint32_t sym = sorted[i], L = lens[sym];
@@ -444,7 +468,7 @@ __device__ bool build_table(const uint8_t *lens, uint32_t n, uint32_t root, uint
       const uint32_t ent = table_entry(kind, sym, L);
       for (uint32_t x = rev_bits(code & ((1u << d) - 1), d); x < (1u << sb); x += 1u << d) tab[sbase + x] = ent;
     }
-    __syncthreads();
+    wsync();
   }
   return true;
 }
@@ -496,7 +520,7 @@ __device__ __forceinline__ void build_fixed_lens(uint8_t *lens) {
     else l = 5;  // 30 distance codes (+2 invalid) of length 5, stored at 288..319
     lens[s] = l;
   }
-  __syncthreads();
+  wsync();
 }
 
 // One lane's symbol at a 64-bit lookahead value V = Vhi:Vlo (the stream from the symbol's first
@@ -539,8 +563,98 @@ __device__ __forceinline__ void lane_symbol(const Smem &S, uint32_t Vlo, uint32_
   if (L == 0) info = F_SLOW;  // literal/length code past the subtable space
 }
 
+// A code longer than its table's root whose prefix got no subtable space (a stream whose code set
+// outgrows LSUB / DSUB): this lane walks the canonical code from root + 1 (the HuffMeta counts and
+// the sorted symbols build_table keeps), so the segmented decode goes on instead of handing the rest
+// of the block to the one-symbol-at-a-time path (one such block made a shard's slowest stream ~60 %
+// slower). Returns a table entry (code length in bits 0-3) or a K_BAD one.
+__device__ __forceinline__ uint32_t lane_canon(uint64_t bits, const uint32_t *tab, uint32_t root, const uint16_t *sorted,
+                                            const HuffMeta &M, int kind) {
+  uint32_t E = tab[(uint32_t)bits & ((1u << root) - 1)];
+  if (E & F_SUBT) E = tab[(E >> 16) + ((uint32_t)(bits >> root) & ((1u << ((E >> 6) & 15)) - 1))];
+  if (E & 15) return E;
+  uint32_t v = rev_bits((uint32_t)bits & ((1u << root) - 1), root), L = root, sym = 0xFFFF;
+  uint64_t b = bits >> root;
+  const uint32_t maxlen = M.maxlen;
+  while (L < maxlen) {
+    L++;
+    v = (v << 1) | (uint32_t)(b & 1);
+    b >>= 1;
+    const uint32_t first = M.first[L], cnt = M.count[L];
+    if (v - first < cnt) {
+      sym = sorted[M.offs[L] + v - first];
+      break;
+    }
+  }
+  return sym == 0xFFFF ? ((K_BAD << 4) | 15) : table_entry(kind, sym, L);
+}
+__device__ __forceinline__ void lane_symbol_slow(const Smem &S, uint64_t V, uint32_t &info, uint32_t &rec) {
+  const uint32_t E = lane_canon(V, S.ltab, LROOT, S.lsorted, S.lm, 0);
+  const uint32_t L = E & 15, kind = (E >> 4) & 3, lx = (E >> 6) & 15;
+  rec = 0;
+  if (kind == K_LIT) {
+    info = L | (1u << 8);
+    rec = E >> 16;
+  } else if (kind == K_EOB) {
+    info = L | F_EOB;
+  } else if (kind == K_LEN) {
+    const uint32_t len = (E >> 16) + ((uint32_t)(V >> L) & ((1u << lx) - 1));
+    const uint32_t s1 = L + lx;
+    const uint32_t D = lane_canon(V >> s1, S.dtab, DROOT, S.dsorted, S.dm, 1);
+    const uint32_t DL = D & 15, dx = (D >> 6) & 15;
+    if (((D >> 4) & 3) != K_LEN) {
+      info = F_BAD;
+    } else {
+      const uint32_t dist = (D >> 16) + ((uint32_t)(V >> (s1 + DL)) & ((1u << dx) - 1));
+      info = (s1 + DL + dx) | (len << 8);
+      rec = 0x80000000u | (dist << 9) | len;
+    }
+  } else {
+    info = F_BAD;
+  }
+}
+
 // Flush output bytes [from, to) (absolute positions) from the ring to the slot with 16-B stores.
 // Words straddling `to` are rewritten by the next flush.
+// The gzip trailer's CRC-32 by one wave (crc.hpp's helpers index by threadIdx / blockDim, and in the
+// pipelined kernel the second wave has left by then): slice-by-4 tables in LDS, 64 lane segments
+// merged by the GF(2) shift tree.
+__device__ inline void wave_crc_tables(CrcTables &T, uint32_t poly) {
+  const uint32_t l = (uint32_t)lane_id();
+  for (uint32_t i = l; i < 256; i += 64) {
+    uint32_t c = i;
+    for (int k = 0; k < 8; k++) c = (c & 1) ? (c >> 1) ^ poly : c >> 1;
+    T.t[0][i] = c;
+  }
+  wsync();
+  for (uint32_t i = l; i < 256; i += 64) {
+    uint32_t c = T.t[0][i];
+    for (int k = 1; k < 4; k++) {
+      c = (c >> 8) ^ T.t[0][c & 0xff];
+      T.t[k][i] = c;
+    }
+  }
+  if (l < 32) T.x2n[l] = poly == POLY_CRC32C ? c_x2n_crc32c[l] : c_x2n_crc32[l];
+  wsync();
+}
+__device__ inline uint32_t wave_crc(const uint8_t *p, uint64_t n, const CrcTables &T, uint32_t poly) {
+  const uint32_t l = (uint32_t)lane_id();
+  uint64_t seg = (n + 63) / 64;
+  seg = (seg + 15) & ~(uint64_t)15;  // 16-B aligned segments: the inner loop runs on 16-B loads
+  const uint64_t b0 = min<uint64_t>((uint64_t)l * seg, n), b1 = min<uint64_t>(b0 + seg, n);
+  uint32_t c = crc_segment(p + b0, b1 - b0, T);
+  uint64_t len = b1 - b0;
+  for (int off = 1; off < 64; off <<= 1) {
+    const uint32_t c2 = __shfl_down(c, off, 64);
+    const uint64_t l2 = __shfl_down(len, off, 64);
+    if (l % (2 * off) == 0 && l + off < 64) {
+      c = crc_combine(c, c2, l2, T.x2n, poly);
+      len += l2;
+    }
+  }
+  return U(__shfl(c, 0, 64));
+}
+
 __device__ __forceinline__ void flush(const Smem &S, uint8_t *out, uint64_t cap, uint64_t from, uint64_t to) {
   const uint64_t a = from & ~(uint64_t)15, b = (to + 15) & ~(uint64_t)15;
   for (uint64_t p = a + (uint64_t)lane_id() * 16; p < b; p += 64 * 16) {
@@ -643,6 +757,7 @@ __device__ __forceinline__ uint32_t seg_decode(const Smem &S, LaneRd &R, uint64_
     uint32_t lo, hi, info, r;
     R.peek(p, lo, hi);
     lane_symbol(S, lo, hi, info, r);
+    if (info == F_SLOW) lane_symbol_slow(S, ((uint64_t)hi << 32) | lo, info, r);
     const bool own = p >= s_own;
     if (own && p - s_own < 64) mask |= 1ull << (uint32_t)(p - s_own);
     if (info >= F_EOB) {
@@ -677,11 +792,12 @@ __device__ __forceinline__ uint64_t shfl_up64(uint64_t v) {
 #else
 #define XPROF(k, n)
 #endif
-__device__ __forceinline__ bool exec_batch(Smem &S, uint8_t *out, uint64_t cap, uint64_t &pos, uint64_t &flushed,
+template <class SM>
+__device__ __forceinline__ bool exec_batch(SM &S, uint8_t *out, uint64_t cap, uint64_t &pos, uint64_t &flushed,
                                            uint32_t cnt, uint32_t bytes, uint32_t rec_in, uint64_t *pa) {
   (void)pa;
   const int lane = lane_id();
-  __syncthreads();
+  wsync();
   const bool mine = lane < (int)cnt;
   const uint32_t rec = mine ? rec_in : 0u;
   const bool is_match = mine && (rec >> 31);
@@ -717,7 +833,7 @@ __device__ __forceinline__ bool exec_batch(Smem &S, uint8_t *out, uint64_t cap, 
   int32_t piv[8];
 #pragma unroll
   for (int k = 0; k < 8; k++) piv[k] = (int32_t)U(__builtin_amdgcn_readlane((int)rv, 8 * k));
-  __syncthreads();
+  wsync();
   int32_t hi = -1, lo = 0;
   if (is_match && e_rel > 0) {
     int32_t a = 0, b = 0;  // pivots < e_rel (>= 1: entry 0 is 0), pivots <= s_rel
@@ -740,7 +856,7 @@ __device__ __forceinline__ bool exec_batch(Smem &S, uint8_t *out, uint64_t cap, 
   }
 #else
   if (mine) S.rbeg[lane] = (uint16_t)(mypos - pos);
-  __syncthreads();
+  wsync();
   int32_t hi = -1, lo = 0;
   if (is_match && e_rel > 0) {
     hi = 0;
@@ -755,7 +871,7 @@ __device__ __forceinline__ bool exec_batch(Smem &S, uint8_t *out, uint64_t cap, 
 #else
   if (mine) S.rend[lane] = (uint16_t)(mypos - pos + (is_match ? mlen : 1u));
   if (mine) S.rbeg[lane] = (uint16_t)(mypos - pos);
-  __syncthreads();
+  wsync();
   int32_t hi = -1;  // the last symbol that starts before e_rel
   if (is_match && e_rel > 0) {
     hi = 0;
@@ -958,10 +1074,10 @@ __device__ __forceinline__ bool exec_batch(Smem &S, uint8_t *out, uint64_t cap, 
 #endif
   pos = batch_end;
   if (pos - flushed >= FLUSH_MIN) {
-    __syncthreads();
+    wsync();
     flush(S, out, cap, flushed, pos);
     flushed = pos;
-    __syncthreads();
+    wsync();
   }
   return true;
 }
@@ -977,11 +1093,12 @@ __device__ __forceinline__ bool exec_batch(Smem &S, uint8_t *out, uint64_t cap, 
 // zlib (ZLIB = true, RFC 1950; blosc's zlib streams, c-blosc zlib_wrap_decompress = zlib uncompress):
 // only items whose kind is BL_KIND_ZLIB and status BL_SKIP; aux[i] = {Adler-32, 0}, status 0 on
 // success (the Adler-32 check follows in k_adler32_check).
-template <bool ZLIB>
-__global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(ZG_INFLATE_WPE, 8))) void k_gzip(
+template <bool ZLIB, bool PIPE = false>
+__global__ __launch_bounds__(PIPE ? 128 : 64) __attribute__((amdgpu_waves_per_eu(ZG_INFLATE_WPE, 8))) void k_gzip(
     ZgItem *items, uint32_t *status, const uint32_t *kind, uint8_t *dst, uint64_t slot_bytes, uint2 *aux,
     const uint32_t *order, uint32_t *seg_scr) {
-  __shared__ Smem S;
+  static_assert(!(ZLIB && PIPE), "the pipelined mode is for gzip streams");
+  __shared__ std::conditional_t<PIPE, SmemP, Smem> S;
 #if !ZG_INFLATE_XFETCH
   __shared__ uint16_t seg_base[65], seg_skip[64];
 #endif
@@ -1049,12 +1166,116 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(ZG_INFLATE_W
   uint64_t pos = 0;        // output bytes produced (absolute)
   uint64_t flushed = 0;    // output bytes flushed to the slot
   bool last = false;
+  // pipelined mode: the message protocol (every message one workgroup barrier; a sync takes two more)
+  uint32_t pm = 0;    // messages wave 0 has posted
+  bool held = false;  // wave 0 holds the output state (between dsync and drelease)
+  auto post = [&](uint32_t msg) {
+    if constexpr (PIPE) {
+      if (lane == 0) S.p_msg[pm & 1] = msg;
+      __threadfence_block();
+      __syncthreads();
+      pm++;
+    }
+  };
+  auto dsync = [&]() {  // take the output state from wave 1 (it finishes its round first)
+    if constexpr (PIPE) {
+      post(P_SYNC);
+      __syncthreads();  // wave 1 has written it
+      pos = S.p_pos;
+      flushed = S.p_flushed;
+      if (!err) err = S.p_err;
+      held = true;
+    }
+  };
+  auto drelease = [&]() {  // hand it back
+    if constexpr (PIPE) {
+      if (lane == 0) {
+        S.p_pos = pos;
+        S.p_flushed = flushed;
+        S.p_err = err;
+      }
+      __threadfence_block();
+      __syncthreads();
+      held = false;
+    }
+  };
+  if constexpr (PIPE) {
+    if (threadIdx.x == 0) S.p_msg[0] = S.p_msg[1] = P_END;
+    __syncthreads();
+    if (threadIdx.x >= 64) {
+      // ---- wave 1: the executor of wave 0's rounds ----
+      uint64_t xpos = 0, xfl = 0;
+      uint32_t xerr = 0;
+      const uint32_t *rbase = seg_scr + (uint64_t)blockIdx.x * 2 * 64 * SEGCAP;
+      for (uint32_t m = 0;; m++) {
+        __syncthreads();  // wave 0's next message
+        const uint32_t slot = m & 1, msg = S.p_msg[slot];
+        if (msg == P_END) break;
+        if (msg == P_SYNC) {
+          if (lane == 0) {
+            S.p_pos = xpos;
+            S.p_flushed = xfl;
+            S.p_err = xerr;
+          }
+          __threadfence_block();
+          __syncthreads();  // wave 0 takes the output state
+          __syncthreads();  // and hands it back
+          xpos = S.p_pos;
+          xfl = S.p_flushed;
+          xerr = S.p_err;
+          continue;
+        }
+        if (xerr) continue;
+        const uint32_t total = S.p_total[slot];
+        const uint32_t rb_l = S.p_rb[slot][lane], ro_l = S.p_ro[slot][lane], cnt_l = S.p_cnt[slot][lane];
+        const uint32_t *wrec = rbase + (uint64_t)slot * 64 * SEGCAP;
+        auto fetch = [&](uint32_t g) -> uint32_t {
+          const uint64_t has = __ballot(cnt_l != 0 && rb_l <= g);
+          const int k0 = has ? 63 - __builtin_clzll(has) : 0;
+          uint32_t rb = U(__builtin_amdgcn_readlane((int)rb_l, k0));
+          uint32_t ro = U(__builtin_amdgcn_readlane((int)ro_l, k0));
+          uint64_t st = __ballot(cnt_l != 0 && rb_l > g && rb_l < g + 64);
+          while (st) {
+            const int k = __builtin_ctzll(st);
+            st &= st - 1;
+            const uint32_t b = U(__builtin_amdgcn_readlane((int)rb_l, k));
+            const uint32_t o = U(__builtin_amdgcn_readlane((int)ro_l, k));
+            if (g + (uint32_t)lane >= b) {
+              rb = b;
+              ro = o;
+            }
+          }
+          const uint32_t idx = g + (uint32_t)lane;
+          return idx < total ? wrec[ro + (idx - rb)] : 0u;
+        };
+        uint32_t rec_next = total ? fetch(0) : 0u;
+        for (uint32_t g = 0; g < total && !xerr;) {
+          const uint32_t idx = g + (uint32_t)lane;
+          const uint32_t rec = rec_next;
+          const uint32_t ln = idx < total ? ((rec >> 31) ? (rec & 511) : 1u) : 0u;
+          const uint32_t inc = wave_incl_sum(ln);
+          const bool take = idx < total && inc - ln < (uint32_t)BATCH_CAP;
+          const uint32_t bc = (uint32_t)__builtin_popcountll(__ballot(take));
+          const uint32_t bytes = U(__builtin_amdgcn_readlane((int)inc, (int)bc - 1));
+          if (xpos + bytes > cap) {
+            xerr = ZG_DECODED_SIZE_MISMATCH;
+            break;
+          }
+          if (g + bc < total) rec_next = fetch(g + bc);  // in flight while this batch executes
+          if (!exec_batch(S, out, cap, xpos, xfl, bc, bytes, rec, nullptr)) xerr = ZG_CORRUPT_STREAM;
+          g += bc;
+        }
+      }
+      return;
+    }
+  }
   while (!last && !err) {
     PROF_T(t_hdr);
     bits_refill(B);
     last = bits_get(B, 1);
     const uint32_t type = bits_get(B, 2);
     if (type == 0) {  // ---- stored block ----
+      if (PIPE && !held) dsync();  // wave 0 writes the block's bytes itself
       const uint32_t r = (uint32_t)(B.consumed & 7);
       bits_drop(B, r ? 8 - r : 0);  // to a byte boundary (nb is a multiple of 8 here)
       bits_refill(B);
@@ -1066,14 +1287,15 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(ZG_INFLATE_W
       for (uint32_t done = 0; done < ln;) {
         const uint32_t n = min<uint32_t>(ln - done, BATCH_CAP);
         for (uint32_t k = lane; k < n; k += 64) S.ring[(pos + k) & RMASK] = in[byte0 + done + k];
-        __syncthreads();
+        wsync();
         flush(S, out, cap, flushed, pos + n);
         pos += n;
         flushed = pos;
         done += n;
-        __syncthreads();
+        wsync();
       }
       bits_seek(B, (byte0 + ln + mis) * 8);
+      if (PIPE) drelease();
       continue;
     }
     if (type == 3) { err = ZG_CORRUPT_STREAM; break; }
@@ -1087,12 +1309,12 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(ZG_INFLATE_W
       const uint32_t hclen = bits_get(B, 4) + 4;
       if (hlit > 286 || hdist > 30) { err = ZG_CORRUPT_STREAM; break; }
       if (lane < 20) S.clens[lane] = 0;
-      __syncthreads();
+      wsync();
       for (uint32_t k = 0; k < hclen; k++) {  // (a private array indexed by k would live in scratch)
         const uint32_t v = bits_get(B, 3);
         if (lane == 0) S.clens[c_clen_order[k]] = (uint8_t)v;
       }
-      __syncthreads();
+      wsync();
       if (!build_table(S.clens, 19, 7, S.ltab, S.csorted, S.cm, 2, S.tmp, 0)) { err = ZG_CORRUPT_STREAM; break; }
       // code lengths for literal/length + distance alphabets (ltab used as a 128-entry 7-bit table)
       uint32_t n = 0, prev = 0;
@@ -1175,7 +1397,7 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(ZG_INFLATE_W
           if (bp > end_bits) err = ZG_CORRUPT_STREAM;
         }
         if (!err) bits_seek_in(B, bp);
-        __syncthreads();
+        wsync();
       }
 #else
       while (n < total) {
@@ -1214,7 +1436,7 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(ZG_INFLATE_W
       for (uint32_t s = lane; s < 320; s += 64) {
         if ((s >= hlit && s < 288) || s >= 288 + hdist) S.lens[s] = 0;
       }
-      __syncthreads();
+      wsync();
       if (U(S.lens[256]) == 0) { err = ZG_CORRUPT_STREAM; break; }  // missing end-of-block code
       PROF_ADD(8, t_cl);
     }
@@ -1238,11 +1460,14 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(ZG_INFLATE_W
     // run through the batch executor in order. A code past the subtable space ends the path (the
     // lookahead loop below takes the rest of the block).
     if (seg_scr) {
-      uint32_t *myrec = seg_scr + ((uint64_t)blockIdx.x * 64 + (uint32_t)lane) * SEGCAP;
+      if (PIPE && held) drelease();  // wave 1 executes this block's rounds
       LaneRd R{B.base, B.nwords, 0, 0, 0, 0, 0, 0, 0, 0};
       uint64_t r0 = B.consumed;
       bool fallback = false;
       while (!eob && !err && !fallback) {
+        // this round's record slots (pipelined: the message slot's half of the stream's two)
+        uint32_t *myrec = seg_scr + ((uint64_t)blockIdx.x * (PIPE ? 128 : 64) + (PIPE ? (pm & 1) * 64 : 0) +
+                                     (uint32_t)lane) * SEGCAP;
         PROF_T(t_sd);
         const uint64_t s_own = r0 + (uint64_t)lane * SEGB, s_end = s_own + SEGB;
         uint64_t p = lane ? s_own - OVL : r0;
@@ -1298,9 +1523,18 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(ZG_INFLATE_W
 #if ZG_INFLATE_XFETCH
         const uint32_t rb_l = incl - cnt_l;
         const uint32_t ro_l = (uint32_t)lane * SEGCAP + skip;  // in this stream's 64 record slots
+        if constexpr (PIPE) {
+          // hand the round to wave 1 and decode the next one meanwhile
+          const uint32_t slot = pm & 1;
+          S.p_rb[slot][lane] = rb_l;
+          S.p_ro[slot][lane] = ro_l;
+          S.p_cnt[slot][lane] = cnt_l;
+          if (lane == 0) S.p_total[slot] = total;
+          post(P_ROUND);
+        }
         const uint32_t *wrec = seg_scr + (uint64_t)blockIdx.x * 64 * SEGCAP;
         __threadfence_block();  // the records (global) before other lanes read them
-        __syncthreads();
+        wsync();
         PROF_ADD(1, t_sd);
         PROF_T(t_sx);
         // The batch starting at symbol g: lane t takes symbol g + t. Its region comes from ballots over
@@ -1325,8 +1559,8 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(ZG_INFLATE_W
           const uint32_t idx = g + (uint32_t)lane;
           return idx < total ? wrec[ro + (idx - rb)] : 0u;
         };
-        uint32_t rec_next = total ? fetch(0) : 0u;
-        for (uint32_t g = 0; g < total && !err;) {
+        uint32_t rec_next = (!PIPE && total) ? fetch(0) : 0u;
+        for (uint32_t g = 0; !PIPE && g < total && !err;) {
           const uint32_t idx = g + (uint32_t)lane;
           const uint32_t rec = rec_next;
           const uint32_t ln = idx < total ? ((rec >> 31) ? (rec & 511) : 1u) : 0u;
@@ -1335,7 +1569,7 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(ZG_INFLATE_W
         seg_skip[lane] = (uint16_t)skip;
         if (lane == 63) seg_base[64] = (uint16_t)incl;
         __threadfence_block();  // the records (global) and bases (LDS) before other lanes read them
-        __syncthreads();
+        wsync();
         PROF_ADD(1, t_sd);
         PROF_T(t_sx);
         for (uint32_t g = 0; g < total && !err;) {
@@ -1383,17 +1617,19 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(ZG_INFLATE_W
           r0 = pl;
         } else if (stl == SG_SLOW) {
           fallback = true;
+          PROF_CNT(15, 1);  // blocks finished by the canonical slow path
           bits_seek(B, pl);
         } else {
           err = ZG_CORRUPT_STREAM;
         }
-        __syncthreads();
+        wsync();
       }
       if (err) break;
       if (!fallback) continue;  // the block is done (its end-of-block code consumed)
     }
 #endif
     // ---- symbol batches ----
+    if (PIPE && !eob && !err && !held) dsync();  // wave 0 executes these batches itself
     while (!eob && !err) {
       PROF_T(t_dec);
       uint32_t cnt = 0, bytes = 0;
@@ -1535,7 +1771,7 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(ZG_INFLATE_W
       // ---- execute the batch ----
       PROF_ADD(1, t_dec);
       PROF_T(t_exe);
-      __syncthreads();
+      wsync();
 #ifdef ZG_PROFILE
       if (!exec_batch(S, out, cap, pos, flushed, cnt, bytes, S.rec[lane], prof_acc)) { err = ZG_CORRUPT_STREAM; break; }
 #else
@@ -1544,8 +1780,13 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(ZG_INFLATE_W
       PROF_ADD(2, t_exe);
     }
   }
+  if constexpr (PIPE) {  // the output state back from wave 1, which then leaves
+    if (!held) dsync();
+    drelease();
+    post(P_END);
+  }
   if (!err && flushed < pos) {
-    __syncthreads();
+    wsync();
     flush(S, out, cap, flushed, pos);
     flushed = pos;
   }
@@ -1570,10 +1811,10 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(ZG_INFLATE_W
         // lanes, 2 KiB segments of a C3 chunk each: ~0.3 % of the stream's decode time, and no
         // second kernel re-reading every decoded byte.
         __threadfence_block();
-        __syncthreads();
+        wsync();
         PROF_T(t_crc);
-        build_tables(S.crc, POLY_CRC32);
-        const uint32_t c = wg_crc(out, pos, S.crc, POLY_CRC32, S.crc_len, S.crc_val);
+        wave_crc_tables(S.crc, POLY_CRC32);
+        const uint32_t c = wave_crc(out, pos, S.crc, POLY_CRC32);
         PROF_ADD(11, t_crc);
         if (c != crc || isz != (uint32_t)pos) err = ZG_CORRUPT_STREAM;
       }
@@ -1629,12 +1870,25 @@ __global__ __launch_bounds__(1024) void k_order_by_len(const ZgItem *items, cons
   for (uint32_t i = t; i < n; i += 1024) order[atomicAdd(&cnt[1023 - (len_of(i) >> shift)], 1u)] = i;
 }
 
+// Batches of at most this many streams take the pipelined kernel (ZGPU_GZIP_PIPE_MAX; 0: never): a
+// stream then costs two waves, one decoding the next round while the other executes this one, so its
+// latency is the longer of the two instead of their sum - the time of a lone shard call.
+uint32_t gzip_pipe_max() {
+  static const uint32_t v = [] {
+    const char *e = std::getenv("ZGPU_GZIP_PIPE_MAX");
+    return e ? (uint32_t)std::strtoul(e, nullptr, 10) : 2048u;
+  }();
+  return v;
+}
+
 uint64_t gzip_seg_scratch_bytes(uint32_t n_items) {
   static const bool on = [] {
     const char *e = std::getenv("ZGPU_GZIP_SEG");
     return ZG_INFLATE_SEG && (!e || std::atoi(e) != 0);
   }();
-  return on ? (uint64_t)n_items * 64 * SEGCAP * 4 : 0;
+  // the pipelined kernel double-buffers a stream's record slots
+  const uint64_t slots = (uint64_t)n_items + std::min<uint64_t>(n_items, gzip_pipe_max());
+  return on ? slots * 64 * SEGCAP * 4 : 0;
 }
 
 hipError_t launch_gzip(ZgItem *items, uint32_t *status, uint32_t n_items, uint8_t *dst, uint64_t slot_bytes,
@@ -1647,8 +1901,12 @@ hipError_t launch_gzip(ZgItem *items, uint32_t *status, uint32_t n_items, uint8_
   if (!lpt || n_items < 2) order = nullptr;
   if (!gzip_seg_scratch_bytes(1)) seg_scr = nullptr;
   if (order) hipLaunchKernelGGL(k_order_by_len, dim3(1), dim3(1024), 0, s, items, status, n_items, order);
-  hipLaunchKernelGGL(k_gzip<false>, dim3(n_items), dim3(64), 0, s, items, status, nullptr, dst, slot_bytes, nullptr,
-                     order, seg_scr);
+  if (seg_scr && n_items <= gzip_pipe_max())  // few streams: the pipelined latency mode (two waves each)
+    hipLaunchKernelGGL((k_gzip<false, true>), dim3(n_items), dim3(128), 0, s, items, status, nullptr, dst, slot_bytes,
+                       nullptr, order, seg_scr);
+  else
+    hipLaunchKernelGGL(k_gzip<false>, dim3(n_items), dim3(64), 0, s, items, status, nullptr, dst, slot_bytes, nullptr,
+                       order, seg_scr);
   return hipGetLastError();
 }
 
