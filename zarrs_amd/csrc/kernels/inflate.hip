@@ -1094,7 +1094,7 @@ __device__ __forceinline__ bool exec_batch(SM &S, uint8_t *out, uint64_t cap, ui
 // only items whose kind is BL_KIND_ZLIB and status BL_SKIP; aux[i] = {Adler-32, 0}, status 0 on
 // success (the Adler-32 check follows in k_adler32_check).
 template <bool ZLIB, bool PIPE = false>
-__global__ __launch_bounds__(PIPE ? 128 : 64) __attribute__((amdgpu_waves_per_eu(ZG_INFLATE_WPE, 8))) void k_gzip(
+__global__ __launch_bounds__(PIPE ? 128 : 64) __attribute__((amdgpu_waves_per_eu(PIPE ? 4 : ZG_INFLATE_WPE, 8))) void k_gzip(
     ZgItem *items, uint32_t *status, const uint32_t *kind, uint8_t *dst, uint64_t slot_bytes, uint2 *aux,
     const uint32_t *order, uint32_t *seg_scr) {
   static_assert(!(ZLIB && PIPE), "the pipelined mode is for gzip streams");
