@@ -1469,6 +1469,7 @@ def secondary_legs(args, rank, world, dev, r_primary):
         a.lane_priorities, a.serial_lanes, a.lane_times, a.fork = "", False, False, False
         gc.collect()
         torch.cuda.empty_cache()
+        args.ctx.release_cached()  # the previous leg's pooled device / pinned blocks back to the driver
         print(f"[bench] secondary leg {name} ...", file=sys.stderr, flush=True)
         try:
             r = run_gpu(a, rank, world, dev)
