@@ -92,9 +92,14 @@ def ctx():
     return Context(0)
 
 
+@pytest.mark.parametrize("gzip_kernel", ["pipelined", "one_wave"])
 @pytest.mark.parametrize("store", ["hbm", "host"])
-def test_c3_chain_full_and_partial(ctx, c3, store):
+def test_c3_chain_full_and_partial(ctx, c3, store, gzip_kernel, monkeypatch):
+    """Both k_gzip kernels: batches of <= 2048 streams take the two-wave pipelined one unless
+    ZGPU_GZIP_PIPE_MAX (read per launch) lowers the threshold; 0 forces the one-wave kernel."""
     from zarrs_amd import ZgpuError
+    if gzip_kernel == "one_wave":
+        monkeypatch.setenv("ZGPU_GZIP_PIPE_MAX", "0")
     a, co, shards = c3
     arr = _array(shards, ctx, store)
     # the whole array: shard (1,1,0) is fully covered -> its corrupted inner crc32c is verified

@@ -1873,12 +1873,12 @@ __global__ __launch_bounds__(1024) void k_order_by_len(const ZgItem *items, cons
 // Batches of at most this many streams take the pipelined kernel (ZGPU_GZIP_PIPE_MAX; 0: never): a
 // stream then costs two waves, one decoding the next round while the other executes this one, so its
 // latency is the longer of the two instead of their sum - the time of a lone shard call.
+// The record scratch is always sized for GZIP_PIPE_CAP; the environment (read per launch: tests run
+// both kernels in one process) can only lower the threshold.
+constexpr uint32_t GZIP_PIPE_CAP = 2048;
 uint32_t gzip_pipe_max() {
-  static const uint32_t v = [] {
-    const char *e = std::getenv("ZGPU_GZIP_PIPE_MAX");
-    return e ? (uint32_t)std::strtoul(e, nullptr, 10) : 2048u;
-  }();
-  return v;
+  const char *e = std::getenv("ZGPU_GZIP_PIPE_MAX");
+  return e ? (uint32_t)std::min<unsigned long>(std::strtoul(e, nullptr, 10), GZIP_PIPE_CAP) : GZIP_PIPE_CAP;
 }
 
 uint64_t gzip_seg_scratch_bytes(uint32_t n_items) {
@@ -1887,7 +1887,7 @@ uint64_t gzip_seg_scratch_bytes(uint32_t n_items) {
     return ZG_INFLATE_SEG && (!e || std::atoi(e) != 0);
   }();
   // the pipelined kernel double-buffers a stream's record slots
-  const uint64_t slots = (uint64_t)n_items + std::min<uint64_t>(n_items, gzip_pipe_max());
+  const uint64_t slots = (uint64_t)n_items + std::min<uint64_t>(n_items, GZIP_PIPE_CAP);
   return on ? slots * 64 * SEGCAP * 4 : 0;
 }
 
