@@ -195,6 +195,8 @@ struct SmemP : Smem {
   uint32_t p_msg[2], p_total[2], p_err;
   uint64_t p_pos, p_flushed;
   uint32_t p_rb[2][64], p_ro[2][64], p_cnt[2][64];
+  uint32_t p_crc_bad;  // wave 1's CRC-32C check of the stream (crc_tail 1) failed
+  CrcTables c32c;      // its tables (the Huffman tables' space is wave 0's meanwhile)
 };
 
 __device__ __forceinline__ uint32_t U(uint32_t x) { return __builtin_amdgcn_readfirstlane(x); }
@@ -1096,7 +1098,7 @@ __device__ __forceinline__ bool exec_batch(SM &S, uint8_t *out, uint64_t cap, ui
 template <bool ZLIB, bool PIPE = false>
 __global__ __launch_bounds__(PIPE ? 128 : 64) __attribute__((amdgpu_waves_per_eu(PIPE ? 4 : ZG_INFLATE_WPE, 8))) void k_gzip(
     ZgItem *items, uint32_t *status, const uint32_t *kind, uint8_t *dst, uint64_t slot_bytes, uint2 *aux,
-    const uint32_t *order, uint32_t *seg_scr) {
+    const uint32_t *order, uint32_t *seg_scr, int crc_tail) {
   static_assert(!(ZLIB && PIPE), "the pipelined mode is for gzip streams");
   __shared__ std::conditional_t<PIPE, SmemP, Smem> S;
 #if !ZG_INFLATE_XFETCH
@@ -1112,7 +1114,17 @@ __global__ __launch_bounds__(PIPE ? 128 : 64) __attribute__((amdgpu_waves_per_eu
   uint8_t *out = dst + (uint64_t)item * slot_bytes;
   const uint64_t cap = slot_bytes;
   const uint8_t *in = (const uint8_t *)it.src;
-  const uint64_t in_len = it.len;
+  uint64_t in_len = it.len;
+  // The crc32c codec after gzip (C3's inner chain [bytes, gzip, crc32c]; crc32c_codec.rs:108-141)
+  // folded into the pipelined kernel: the stream's last 4 bytes are its CRC-32C, which wave 1 checks
+  // while wave 0 parses the first block header (crc_tail 1; 2: stripped, not verified).
+  if (PIPE && crc_tail) {
+    if (in_len < 4) {
+      if (lane == 0) status[item] = ZG_CRC_INPUT_TOO_SHORT;
+      return;
+    }
+    in_len -= 4;
+  }
   uint32_t err = 0;
   uint64_t hp;
   if (ZLIB) {
@@ -1200,10 +1212,20 @@ __global__ __launch_bounds__(PIPE ? 128 : 64) __attribute__((amdgpu_waves_per_eu
     }
   };
   if constexpr (PIPE) {
-    if (threadIdx.x == 0) S.p_msg[0] = S.p_msg[1] = P_END;
+    if (threadIdx.x == 0) {
+      S.p_msg[0] = S.p_msg[1] = P_END;
+      S.p_crc_bad = 0;
+    }
     __syncthreads();
     if (threadIdx.x >= 64) {
-      // ---- wave 1: the executor of wave 0's rounds ----
+      // ---- wave 1: the stream's CRC-32C, then the executor of wave 0's rounds ----
+      if (crc_tail == 1 && !(it.flags & ZG_ITEM_PARTIAL)) {
+        wave_crc_tables(S.c32c, POLY_CRC32C);
+        const uint32_t c = wave_crc(in, in_len, S.c32c, POLY_CRC32C);
+        const uint32_t st = U(in[in_len]) | (U(in[in_len + 1]) << 8) | (U(in[in_len + 2]) << 16) |
+                            (U(in[in_len + 3]) << 24);
+        if (lane == 0 && c != st) S.p_crc_bad = 1;
+      }
       uint64_t xpos = 0, xfl = 0;
       uint32_t xerr = 0;
       const uint32_t *rbase = seg_scr + (uint64_t)blockIdx.x * 2 * 64 * SEGCAP;
@@ -1784,6 +1806,7 @@ __global__ __launch_bounds__(PIPE ? 128 : 64) __attribute__((amdgpu_waves_per_eu
     if (!held) dsync();
     drelease();
     post(P_END);
+    if (S.p_crc_bad) err = ZG_INVALID_CHECKSUM;  // the crc32c stage fails first, as in the chain order
   }
   if (!err && flushed < pos) {
     wsync();
@@ -1892,7 +1915,7 @@ uint64_t gzip_seg_scratch_bytes(uint32_t n_items) {
 }
 
 hipError_t launch_gzip(ZgItem *items, uint32_t *status, uint32_t n_items, uint8_t *dst, uint64_t slot_bytes,
-                       uint32_t *order, uint32_t *seg_scr, hipStream_t s) {
+                       uint32_t *order, uint32_t *seg_scr, hipStream_t s, int crc_tail) {
   if (!n_items) return hipSuccess;
   static const bool lpt = [] {
     const char *e = std::getenv("ZGPU_GZIP_LPT");
@@ -1900,13 +1923,20 @@ hipError_t launch_gzip(ZgItem *items, uint32_t *status, uint32_t n_items, uint8_
   }();
   if (!lpt || n_items < 2) order = nullptr;
   if (!gzip_seg_scratch_bytes(1)) seg_scr = nullptr;
+  const bool pipe = seg_scr && n_items <= gzip_pipe_max();  // few streams: the pipelined latency mode
+  // a trailing crc32c: checked inside the pipelined kernel (its second wave is idle at the start), by
+  // k_crc32c_strip ahead of the one-wave kernel (inside it the check cost more HBM traffic: r05cal)
+  if (crc_tail && !pipe) {
+    const hipError_t e = launch_crc32c_strip(items, status, n_items, 0, crc_tail == 1 ? 1 : 0, s);
+    if (e != hipSuccess) return e;
+  }
   if (order) hipLaunchKernelGGL(k_order_by_len, dim3(1), dim3(1024), 0, s, items, status, n_items, order);
-  if (seg_scr && n_items <= gzip_pipe_max())  // few streams: the pipelined latency mode (two waves each)
+  if (pipe)
     hipLaunchKernelGGL((k_gzip<false, true>), dim3(n_items), dim3(128), 0, s, items, status, nullptr, dst, slot_bytes,
-                       nullptr, order, seg_scr);
+                       nullptr, order, seg_scr, crc_tail);
   else
     hipLaunchKernelGGL(k_gzip<false>, dim3(n_items), dim3(64), 0, s, items, status, nullptr, dst, slot_bytes, nullptr,
-                       order, seg_scr);
+                       order, seg_scr, 0);
   return hipGetLastError();
 }
 
@@ -1915,7 +1945,7 @@ hipError_t launch_zlib_streams(ZgItem *subs, uint32_t *sub_status, const uint32_
   if (!n_sub) return hipSuccess;
   if (!gzip_seg_scratch_bytes(1)) seg_scr = nullptr;
   hipLaunchKernelGGL(k_gzip<true>, dim3(n_sub), dim3(64), 0, s, subs, sub_status, sub_kind, dst, slot, aux,
-                     nullptr, seg_scr);
+                     nullptr, seg_scr, 0);
   return hipGetLastError();
 }
 

@@ -1058,13 +1058,21 @@ static void plan_enqueue(zgpu_plan &P, uint8_t *out, hipStream_t s) {
                                  P.d_counter, s));
     }
   }
-  for (const Stage &st : P.stages) {
+  int crc_tail = 0;  // a trailing crc32c stage handed to the next gzip stage (launch_gzip places it)
+  for (size_t si = 0; si < P.stages.size(); si++) {
+    const Stage &st = P.stages[si];
     switch (st.kind) {
       case ST_CRC32C:
+        if (!st.at_start && si + 1 < P.stages.size() && P.stages[si + 1].kind == ST_GZIP && P.d_gz_seg) {
+          crc_tail = P.validate ? 1 : 2;
+          break;
+        }
         HIPCHK(launch_crc32c_strip(P.d_items, P.d_status, ni, st.at_start, P.validate ? 1 : 0, s));
         break;
       case ST_GZIP:
-        HIPCHK(launch_gzip(P.d_items, P.d_status, ni, P.d_pool[st.pool], P.slot_bytes, P.d_order, P.d_gz_seg, s));
+        HIPCHK(launch_gzip(P.d_items, P.d_status, ni, P.d_pool[st.pool], P.slot_bytes, P.d_order, P.d_gz_seg, s,
+                           crc_tail));
+        crc_tail = 0;
         break;
       case ST_ZSTD:
         P.zstd_fork(P.zs, s);
