@@ -1,26 +1,25 @@
-"""Timeline of the last step of a multi-stream rocprofv3 kernel trace (C5's four lanes): per stream,
-each kernel's start / end in ms from the step's first launch. Usage: c5_timeline.py trace.csv [n_last]"""
+"""Timeline of the last bench step in a rocprofv3 kernel trace (bench.py --workload c5 under
+`tools/gpu.sh prof:c5`): every zgpu kernel of the step with its stream, start and end (ms from the
+step's first dispatch) - which plan's kernels make the step's critical path."""
 import csv
 import sys
 
-rows = [r for r in csv.DictReader(open(sys.argv[1])) if "zgpu" in r["Kernel_Name"]]
+rows = [r for r in csv.DictReader(open(sys.argv[1])) if "zgpu::" in r["Kernel_Name"]]
 rows.sort(key=lambda r: int(r["Start_Timestamp"]))
-n_last = int(sys.argv[2]) if len(sys.argv) > 2 else 0
-# the last step: launches after the largest gap between consecutive kernel starts in the last 300
-tail = rows[-300:]
-gaps = [(int(b["Start_Timestamp"]) - int(a["End_Timestamp"]), i + 1) for i, (a, b) in enumerate(zip(tail, tail[1:]))]
-cut = max(gaps)[1] if not n_last else len(tail) - n_last
-step = tail[cut:]
-t0 = min(int(r["Start_Timestamp"]) for r in step)
-key = "Stream_Id" if "Stream_Id" in step[0] else "Queue_Id"
-by = {}
+# argv[2]: the step's start (ms after the trace's first zgpu dispatch; the scans of one step start
+# together), argv[3]: its length bound (ms)
+at, span = float(sys.argv[2]), float(sys.argv[3]) if len(sys.argv) > 3 else 150.0
+T = int(rows[0]["Start_Timestamp"])
+step = [r for r in rows if at <= (int(r["Start_Timestamp"]) - T) / 1e6 < at + span]
+t0 = int(step[0]["Start_Timestamp"])
+end = max(int(r["End_Timestamp"]) for r in step)
+print(f"step: {len(step)} zgpu dispatches, {(end - t0) / 1e6:.2f} ms")
+busy = {}
 for r in step:
-    by.setdefault(r[key], []).append(r)
-end_all = max(int(r["End_Timestamp"]) for r in step)
-print(f"step: {len(step)} launches, {(end_all - t0) / 1e6:.2f} ms")
-for s, rs in sorted(by.items(), key=lambda kv: int(kv[1][0]["Start_Timestamp"])):
-    print(f"-- {key} {s}: ends at {(max(int(r['End_Timestamp']) for r in rs) - t0) / 1e6:.2f} ms")
-    for r in rs:
-        k = r["Kernel_Name"].split("(")[0].replace("zgpu::", "").replace("void ", "")
-        a, b = (int(r["Start_Timestamp"]) - t0) / 1e6, (int(r["End_Timestamp"]) - t0) / 1e6
-        print(f"   {k:28s} {a:8.2f} -> {b:8.2f}  ({b - a:7.2f} ms)")
+    s, e = (int(r["Start_Timestamp"]) - t0) / 1e6, (int(r["End_Timestamp"]) - t0) / 1e6
+    name = r["Kernel_Name"].split("(")[0].replace("zgpu::", "")
+    q = r["Stream_Id"]
+    busy[q] = busy.get(q, 0) + e - s
+    print(f"  stream {q:>3}  {name:<28} grid {int(r['Grid_Size_X']):>8}  {s:8.2f} -> {e:8.2f}  ({e - s:7.2f} ms)")
+for q, b in sorted(busy.items()):
+    print(f"stream {q}: kernels busy {b:.2f} ms")

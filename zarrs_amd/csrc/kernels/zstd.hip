@@ -3486,11 +3486,11 @@ __global__ __launch_bounds__(LIT_THREADS) __attribute__((amdgpu_waves_per_eu(ZG_
 // not inside a checksummed frame); each segment gets its own k_zstd_exec_item wave. Byte-shuffled
 // images cut at their byte planes (tools/lab/zstd_taint.cpp: no match crosses the plane boundary).
 #ifndef ZG_XSEG
-#define ZG_XSEG 4
+#define ZG_XSEG 3
 #endif
-// executor segments per item (at most; ZGPU_ZSTD_XSEG overrides it at run time). C5 A/B
-// (profiles/r02_c5_lanes_xseg_ab.txt): 8 or 16 per item, or more only for batches of few items,
-// measured equal or slower
+// executor segments per item (at most; ZGPU_ZSTD_XSEG overrides it at run time). With the
+// segment-major executor grid (zstd_exec.inc), 2, 3, 4 and 8 measure within 1 % on C5 and
+// blosc-zstd, 3 best on both (profiles/r05/r05xs_zstd_exec_segment_major_xcd_ab.txt)
 constexpr uint32_t XSEG = ZG_XSEG;
 
 __global__ __launch_bounds__(64) void k_zstd_plan(const ZgItem *items, uint32_t *status, ZBlk *blks,
