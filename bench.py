@@ -852,6 +852,9 @@ class C5:
                 lane_of.append(min(gi, 3))
         self.lanes = [[p for p, l in enumerate(lane_of) if l == k] for k in range(4)]
         self.lanes = [ln for ln in self.lanes if ln]
+        # L1 and the small levels decode their literals first (ZGPU_ZSTD_LITS_FIRST), while the L0
+        # halves decode sequences: C5 88.2-88.5 -> 87.0-87.4 ms (profiles/r05/r05lf_zstd_lits_first_ab.txt)
+        self.lits_first_parts = [p for p, l in enumerate(lane_of) if l >= 2]
         self.decoded_bytes = dec_total
         self.step_bytes = all_bytes
         self.ratio = raw_bytes / max(1, sum(enc_sizes))
@@ -1286,6 +1289,9 @@ def run_gpu(args, rank, world, dev):
     lib = L.load()
     plans = []  # one prepared plan per part (e.g. per pyramid level: one chunk shape per plan)
     part_plan = {}
+    lits_first = set(getattr(W, "lits_first_parts", []))
+    if args.lits_first is not None:
+        lits_first = {int(x) for x in args.lits_first.split(",") if x.strip()}
     for pi, (chain, descs, out, out_shape) in enumerate(W.parts):
         n = len(descs)
         if not n:
@@ -1294,8 +1300,10 @@ def run_gpu(args, rank, world, dev):
         plan = C.c_void_p()
         # plans run concurrently on lanes of their own stay on their lane's stream (ZGPU_ONE_STREAM)
         one = L.ONE_STREAM if len(getattr(W, "lanes", [[0]])) > 1 and not args.serial_lanes and not args.fork else 0
+        # zstd plans that decode their literals before their sequences (ZGPU_ZSTD_LITS_FIRST)
+        lf = L.ZSTD_LITS_FIRST if one and pi in lits_first else 0
         L.check(lib.zgpu_plan_create(chain._h, len(out_shape), arr, n, L.u64s(out_shape),
-                                     L.ENC_DEVICE | L.OUT_DEVICE | one, C.byref(plan)))
+                                     L.ENC_DEVICE | L.OUT_DEVICE | one | lf, C.byref(plan)))
         part_plan[pi] = len(plans)
         plans.append((plan, out, (C.c_int32 * n)()))
     # stream lanes: lists of plans executed in order on one stream; lanes run concurrently
@@ -1467,6 +1475,7 @@ def secondary_legs(args, rank, world, dev, r_primary):
         a.workload, a.steps, a.warmup = name, max(2, min(args.steps, 5)), 1
         a.host_leg, a.cpu_seconds, a.c5_scale = False, 5.0, args.secondary_c5_scale
         a.lane_priorities, a.serial_lanes, a.lane_times, a.fork = "", False, False, False
+        a.lits_first = None
         gc.collect()
         torch.cuda.empty_cache()
         args.ctx.release_cached()  # the previous leg's pooled device / pinned blocks back to the driver
@@ -1663,6 +1672,9 @@ def main():
     ap.add_argument("--no-pmc", action="store_true", help="skip the rocprofv3 PMC traffic passes")
     ap.add_argument("--lane-priorities", default="",
                     help="comma-separated HIP stream priorities of the stream lanes (-1 high, 0 normal)")
+    ap.add_argument("--lits-first", default=None,
+                    help="comma-separated parts whose zstd plans decode literals before sequences (ZGPU_ZSTD_LITS_FIRST; "
+                         "default: the workload's choice, '' for none)")
     ap.add_argument("--fork", action="store_true", help=argparse.SUPPRESS)  # A/B: concurrent plans keep their side streams
     ap.add_argument("--serial-lanes", action="store_true",
                     help="run every plan on one stream (profiling: per-kernel durations without overlap)")

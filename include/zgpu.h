@@ -94,6 +94,11 @@ enum {
 #define ZGPU_ONE_STREAM 0x10u /* every kernel of the call on hip_stream (no internal side stream,
                                  e.g. zstd's sequence decoder beside its literal decoder): for callers
                                  that run independent plans concurrently on streams of their own   */
+#define ZGPU_ZSTD_LITS_FIRST 0x40u /* zstd, with ZGPU_ONE_STREAM: the plan decodes its Huffman literals
+                                 before its sequences. For callers overlapping plans on streams of
+                                 their own: a plan whose executor ends the overlap gets its literals
+                                 (throughput-bound) done while the other plans decode sequences
+                                 (latency-bound). Output identical either way.                     */
 
 typedef struct zgpu_ctx zgpu_ctx;
 typedef struct zgpu_chain zgpu_chain;

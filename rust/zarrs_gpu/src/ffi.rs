@@ -25,6 +25,8 @@ pub const ZGPU_NO_VALIDATE: u32 = 0x4;
 pub const ZGPU_DIRECT_IO: u32 = 0x8;
 /// Every kernel of the call on the caller's stream (no internal side stream).
 pub const ZGPU_ONE_STREAM: u32 = 0x10;
+/// With ZGPU_ONE_STREAM: a zstd stage decodes its literals before its sequences (zgpu.h).
+pub const ZGPU_ZSTD_LITS_FIRST: u32 = 0x40;
 /// Concurrent host-in/host-out calls on one chain share one GPU batch (zgpu.h ZGPU_COALESCE).
 pub const ZGPU_COALESCE: u32 = 0x20;
 

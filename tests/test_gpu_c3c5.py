@@ -160,10 +160,12 @@ C5_CODECS = [BYTES_LE, {"name": "numcodecs.shuffle", "configuration": {"elements
              {"name": "zstd", "configuration": {"level": 3, "checksum": False}}]
 
 
-@pytest.mark.parametrize("force_serial", [False, True], ids=["block_parallel", "serial_fallback"])
-def test_c5_16mib_frames(ctx, force_serial):
+@pytest.mark.parametrize("force_serial,lits_first", [(False, False), (True, False), (False, True)],
+                         ids=["block_parallel", "serial_fallback", "lits_first_one_stream"])
+def test_c5_16mib_frames(ctx, force_serial, lits_first):
     """Full-size C5 L0 chunks (16 MiB shuffled-u16 zstd frames): bit-exact vs libzstd through the oracle,
-    and the path taken is the one asked for (device counters of the call)."""
+    and the path taken is the one asked for (device counters of the call). lits_first: one stream, the
+    Huffman literals decoded before the sequences (ZGPU_ONE_STREAM | ZGPU_ZSTD_LITS_FIRST)."""
     import torch
     from zarrs_amd import CodecChain, make_desc
     from zarrs_amd import _lib as L
@@ -180,7 +182,8 @@ def test_c5_16mib_frames(ctx, force_serial):
     old = os.environ.get("ZGPU_ZSTD_FORCE_SERIAL")
     os.environ["ZGPU_ZSTD_FORCE_SERIAL"] = "1" if force_serial else "0"
     try:
-        st = ch.decode_batch(descs, out, [96, 512, 512], enc_device=True)
+        extra = (L.ONE_STREAM | L.ZSTD_LITS_FIRST) if lits_first else 0
+        st = ch.decode_batch(descs, out, [96, 512, 512], enc_device=True, flags=extra)
         ctr = L.last_counters()
     finally:
         if old is None:

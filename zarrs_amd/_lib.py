@@ -25,6 +25,7 @@ OK, INVALID_CHECKSUM, DECODED_SIZE_MISMATCH, SHARD_INDEX_OOB, CORRUPT_STREAM, IN
 ENC_DEVICE = 0x1
 OUT_DEVICE = 0x2
 ONE_STREAM = 0x10
+ZSTD_LITS_FIRST = 0x40
 NO_VALIDATE = 0x4
 DIRECT_IO = 0x8
 COALESCE = 0x20

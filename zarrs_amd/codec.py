@@ -180,15 +180,16 @@ class CodecChain:
 
     # ---- batched entry point -------------------------------------------------------------
     def decode_batch(self, descs: Sequence[L.ChunkDesc], out, out_shape, enc_device: bool,
-                     validate_checksums: bool | None = None, stream=None) -> list:
+                     validate_checksums: bool | None = None, stream=None, flags: int = 0) -> list:
         """Decode many chunks into `out` (numpy array or torch tensor); returns per-chunk statuses
-        and raises ZgpuError with the first failing status (try_for_each semantics)."""
+        and raises ZgpuError with the first failing status (try_for_each semantics). `flags`: extra
+        ZGPU_* decode flags (e.g. ONE_STREAM | ZSTD_LITS_FIRST)."""
         n = len(descs)
         arr = (L.ChunkDesc * max(n, 1))(*descs)
         arr._keep = [getattr(d, "_keep", None) for d in descs]
         st = (C.c_int32 * max(n, 1))()
         op, _, odev, _ = _ptr_len(out)
-        flags = (L.ENC_DEVICE if enc_device else 0) | (L.OUT_DEVICE if odev else 0)
+        flags |= (L.ENC_DEVICE if enc_device else 0) | (L.OUT_DEVICE if odev else 0)
         if validate_checksums is False:
             flags |= L.NO_VALIDATE
         stream = default_stream(stream, out, *[getattr(d, "_keep", None) for d in descs])

@@ -109,6 +109,9 @@ struct ZstdScratch {
   // runs on `side` beside the Huffman literal kernels and joins before k_zstd_plan
   hipStream_t side = nullptr;
   hipEvent_t ev_fork = nullptr, ev_join = nullptr;
+  // one stream only: Huffman literals before the sequences (ZGPU_ZSTD_LITS_FIRST; the literal decoder
+  // then writes literal-only blocks to the scratch, as k_zstd_plan has not placed them yet)
+  uint32_t lits_first = 0;
   // literal record slots (k_zstd_lits pass 1 keeps its symbols; nullable: every lane decodes twice):
   // zstd_lit_rec_bytes() bytes for lit_rec_wgs workgroups
   uint8_t *lit_rec = nullptr;

@@ -3806,7 +3806,8 @@ static hipError_t launch_zstd_pass(ZgItem *items, uint32_t *status, uint32_t n_i
     const char *e = std::getenv("ZGPU_ZSTD_LITDIRECT");
     return !e || std::atoi(e) != 0;
   }();
-  const bool lit_direct = lit_direct_env && !fork && !Z.alias;
+  const bool lits_first = Z.lits_first && !fork;
+  const bool lit_direct = lit_direct_env && !fork && !Z.alias && !lits_first;
   // executor segments per item: ZG_XSEG (ZGPU_ZSTD_XSEG: tuning)
   static const uint32_t xseg_env = [] {
     const char *e = std::getenv("ZGPU_ZSTD_XSEG");
@@ -3827,17 +3828,20 @@ static hipError_t launch_zstd_pass(ZgItem *items, uint32_t *status, uint32_t n_i
     const char *e = std::getenv("ZGPU_ZSTD_SEQ");
     return e ? std::atoi(e) : 1;
   }();
-  if (seq_mode == 1) {
-    // one resident wave of the lane-group decoder: its LDS (5 KiB per block) sets the waves per CU
-    const uint64_t per_cu = std::max<uint64_t>(1, (160u << 10) / ((sizeof(ZDecLgSmem<ZG_SEQ_G>) + 1023) & ~size_t(1023)));
-    const uint64_t lrecs = (recs + ZG_SEQ_G - 1) / ZG_SEQ_G;
-    const uint32_t lg_grid = (uint32_t)std::min<uint64_t>(lrecs, (uint64_t)device_cu_count() * per_cu);
-    hipLaunchKernelGGL(k_zstd_blocks_lg<ZG_SEQ_G>, dim3(lg_grid), dim3(64), 0, sq, items, status, blks, Z.blk_cap,
-                       Z.nblk, Z.mode, n_items, Z.seq, Z.seq_cap, Z.max_nblk);
-  } else {
-    hipLaunchKernelGGL(k_zstd_blocks, dim3(bgrid), dim3(64), 0, sq, items, status, blks, Z.blk_cap, Z.nblk, Z.mode,
-                       n_items, Z.lit, Z.lit_stride, Z.seq, Z.seq_cap, Z.max_nblk);
-  }
+  auto launch_seq = [&] {
+    if (seq_mode == 1) {
+      // one resident wave of the lane-group decoder: its LDS (5 KiB per block) sets the waves per CU
+      const uint64_t per_cu = std::max<uint64_t>(1, (160u << 10) / ((sizeof(ZDecLgSmem<ZG_SEQ_G>) + 1023) & ~size_t(1023)));
+      const uint64_t lrecs = (recs + ZG_SEQ_G - 1) / ZG_SEQ_G;
+      const uint32_t lg_grid = (uint32_t)std::min<uint64_t>(lrecs, (uint64_t)device_cu_count() * per_cu);
+      hipLaunchKernelGGL(k_zstd_blocks_lg<ZG_SEQ_G>, dim3(lg_grid), dim3(64), 0, sq, items, status, blks, Z.blk_cap,
+                         Z.nblk, Z.mode, n_items, Z.seq, Z.seq_cap, Z.max_nblk);
+    } else {
+      hipLaunchKernelGGL(k_zstd_blocks, dim3(bgrid), dim3(64), 0, sq, items, status, blks, Z.blk_cap, Z.nblk, Z.mode,
+                         n_items, Z.lit, Z.lit_stride, Z.seq, Z.seq_cap, Z.max_nblk);
+    }
+  };
+  if (!lits_first) launch_seq();
   if (fork) {
     hipError_t e = hipEventRecord(Z.ev_join, Z.side);
     if (e != hipSuccess) return e;
@@ -3853,6 +3857,7 @@ static hipError_t launch_zstd_pass(ZgItem *items, uint32_t *status, uint32_t n_i
   uint8_t *lit_rec = (ZG_LIT_REC && Z.lit_rec && lgrid <= Z.lit_rec_wgs) ? Z.lit_rec : nullptr;
   hipLaunchKernelGGL(k_zstd_lits, dim3(lgrid), dim3(LIT_THREADS), 0, s, items, status, blks, Z.blk_cap, Z.nblk,
                      Z.mode, n_items, Z.lit, Z.lit_stride, lit_rec, Z.max_nblk, lit_direct ? dst : nullptr, slot_bytes);
+  if (lits_first) launch_seq();  // same stream: after the literal decoder
   if (fork) {
     hipError_t e = hipStreamWaitEvent(s, Z.ev_join, 0);
     if (e != hipSuccess) return e;

@@ -1076,6 +1076,7 @@ static void plan_enqueue(zgpu_plan &P, uint8_t *out, hipStream_t s) {
         break;
       case ST_ZSTD:
         P.zstd_fork(P.zs, s);
+        P.zs.lits_first = (P.flags & ZGPU_ZSTD_LITS_FIRST) && !P.zs.side ? 1u : 0u;
         HIPCHK(launch_zstd(P.d_items, P.d_status, ni, P.d_pool[st.pool], P.slot_bytes, P.zs, s));
         break;
       case ST_BLOSC:
