@@ -20,7 +20,7 @@ if [ "$2" = bz ]; then  # blosc-zstd: executor segments 4 vs 3 (vs 2 with "bz3")
   exit 0
 fi
 if [ "$2" = lf ]; then  # C5: parts whose plans decode literals before sequences (0,1 L0 halves, 2 L1, 3-5 L2-L4)
-  for r in a b; do for x in none 2 2,3,4,5 3,4,5 0,1; do
+  for r in a b; do for x in ${3:-none 2 2,3,4,5 3,4,5 0,1}; do
     v=$x; [ $x = none ] && v=
     run lf$x$r ZGPU_NONE=1 --lits-first=$v || exit 1
   done; done
