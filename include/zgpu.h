@@ -114,6 +114,10 @@ int64_t zgpu_ctx_refcount(const zgpu_ctx *ctx);
 /* Return the context's cached free device and pinned buffers to HIP (buffers in use stay). The
  * device pool also trims itself past ZGPU_POOL_CAP_MB (default 16 GiB) of free blocks. */
 int zgpu_ctx_release_cached(zgpu_ctx *ctx);
+/* The context's pooled memory in bytes (diagnostics and tests; any pointer may be NULL): device
+ * blocks in use and cached free, pinned host blocks in use and cached free. */
+int zgpu_ctx_pool_stats(const zgpu_ctx *ctx, uint64_t *dev_live, uint64_t *dev_free, uint64_t *host_live,
+                        uint64_t *host_free);
 /* Last error message of the calling thread on this context ("" if none). */
 const char *zgpu_last_error(const zgpu_ctx *ctx);
 const char *zgpu_status_name(int status);

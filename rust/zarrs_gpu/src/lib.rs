@@ -217,6 +217,38 @@ impl Chain {
     }
 }
 
+/// Library-owned pinned bytes handed back by `zgpu_decode_pinned` / `zgpu_encode_pinned` (a coalesced
+/// batch's pack buffer or a pooled pinned block). Dropping it returns the block with
+/// `zgpu_result_release`, so a pack shared by several callers is recycled once its last holder drops.
+pub(crate) struct Pinned {
+    ptr: *const u8,
+    len: usize,
+    res: NonNull<ffi::zgpu_result>,
+}
+
+// SAFETY: the bytes are immutable once the call returned, and zgpu_result_release is thread-safe
+// (the library counts a pack's holders under its own lock).
+unsafe impl Send for Pinned {}
+unsafe impl Sync for Pinned {}
+
+impl Pinned {
+    /// The result bytes (empty for a zero-length result or a null data pointer).
+    pub(crate) fn as_slice(&self) -> &[u8] {
+        if self.len == 0 || self.ptr.is_null() {
+            return &[];
+        }
+        // SAFETY: the library guarantees `len` readable bytes at `ptr` until zgpu_result_release.
+        unsafe { std::slice::from_raw_parts(self.ptr, self.len) }
+    }
+}
+
+impl Drop for Pinned {
+    fn drop(&mut self) {
+        // SAFETY: `res` came from a successful zgpu_*_pinned call and is released exactly once here.
+        unsafe { ffi::zgpu_result_release(self.res.as_ptr()) };
+    }
+}
+
 impl Chain {
     /// zgpu_decode_pinned over `descs` (host encoded bytes): the C-order output of `out_shape` left in
     /// library pinned memory, for ONE copy into the caller's target (a zarrs view can only be written
@@ -260,7 +292,9 @@ impl Chain {
     }
 
     /// zgpu_encode_pinned: one chunk (or shard) of `chunk_shape` from host bytes, encoded on the GPU.
-    pub(crate) fn encode_pinned(&self, decoded: &[u8], chunk_shape: &[u64]) -> Result<Pinned, CodecError> {
+    /// `Ok(None)`: the library's write path does not take this chain (ZGPU_UNSUPPORTED); the caller
+    /// falls back to zarrs' own encoder.
+    pub(crate) fn encode_pinned(&self, decoded: &[u8], chunk_shape: &[u64]) -> Result<Option<Pinned>, CodecError> {
         let nd = chunk_shape.len();
         let need = chunk_shape.iter().product::<u64>() * self.element_size as u64;
         if nd == 0 || nd > ffi::ZGPU_MAX_DIMS || decoded.len() as u64 != need {
@@ -277,11 +311,15 @@ impl Chain {
             ffi::zgpu_encode_pinned(self.as_ptr(), nd as u32, chunk_shape.as_ptr(), decoded.as_ptr().cast(), &mut enc,
                                     &mut len, &mut res)
         };
+        if rc == ffi::ZGPU_UNSUPPORTED {
+            return Ok(None);
+        }
         if rc != ffi::ZGPU_OK {
             return Err(status_error(rc));
         }
         let res = NonNull::new(res).ok_or_else(|| CodecError::Other("zgpu_encode_pinned returned no result".into()))?;
-        Ok(Pinned { ptr: enc.cast(), len: usize::try_from(len).map_err(|e| CodecError::Other(e.to_string()))?, res })
+        let len = usize::try_from(len).map_err(|e| CodecError::Other(e.to_string()))?;
+        Ok(Some(Pinned { ptr: enc.cast(), len, res }))
     }
 }
 

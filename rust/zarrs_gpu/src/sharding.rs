@@ -230,12 +230,14 @@ impl ArrayToBytesCodecTraits for GpuShardingCodecBound {
         shape: &[NonZeroU64],
         options: &CodecOptions,
     ) -> Result<ArrayBytesRaw<'a>, CodecError> {
+        // the reference's length check first (sharding_codec.rs:357-359): a wrong-length input is
+        // InvalidBytesLength whichever encoder would have run
+        let num_elements = shape.iter().map(|d| d.get()).product::<u64>();
+        bytes.validate(num_elements, &self.data_type)?;
         if self.data_type.fixed_size().is_some() {
             if let ArrayBytes::Fixed(raw) = &bytes {
-                match self.chain.encode_pinned(raw, &u64s(shape)) {
-                    Ok(enc) => return Ok(Cow::Owned(enc.as_slice().to_vec())),
-                    Err(CodecError::Other(msg)) if msg.contains("UNSUPPORTED") => {}
-                    Err(e) => return Err(e),
+                if let Some(enc) = self.chain.encode_pinned(raw, &u64s(shape))? {
+                    return Ok(Cow::Owned(enc.as_slice().to_vec()));
                 }
             }
         }

@@ -132,6 +132,13 @@ def test_c3_chain_full_and_partial(ctx, c3, store, gzip_kernel, monkeypatch):
         arr.retrieve_array_subset([256, 256, 0], [SHARD] * 3)
     assert ei.value.status == 1
     nov = _array(shards, ctx, store, validate=False)
+    # the lone shard (512 streams: the pipelined kernel's latency mode unless forced off) without
+    # validation: its corrupt inner crc32c is stripped, not checked (crc32c_codec.rs:108-141)
+    got = nov.retrieve_array_subset([256, 256, 0], [SHARD] * 3)
+    exp = O.retrieve_array_subset(co, [N] * 3, [SHARD] * 3, shards, [256, 256, 0], [SHARD] * 3, nthreads=8,
+                                  validate_checksums=False)
+    assert got.tobytes() == exp.tobytes()
+    assert np.array_equal(got, a[256:, 256:, :256])
     exp = O.retrieve_array_subset(co, [N] * 3, [SHARD] * 3, shards, [0] * 3, [N] * 3, nthreads=8,
                                   validate_checksums=False)
     got = nov.retrieve_array_subset()
@@ -139,6 +146,41 @@ def test_c3_chain_full_and_partial(ctx, c3, store, gzip_kernel, monkeypatch):
     exp_a = a.copy()
     exp_a[0:32, 0:32, 256 + 160:256 + 192] = 0
     assert np.array_equal(got, exp_a)
+
+
+@pytest.mark.parametrize("gzip_kernel", ["pipelined", "one_wave"])
+def test_c3_corrupt_gzip_header_checksum_first(ctx, c3, gzip_kernel, monkeypatch):
+    """A corrupt gzip header inside an inner chunk: the chain decodes crc32c before gzip, so with the
+    stored CRC-32C left as it was the full path reports INVALID_CHECKSUM (crc32c_codec.rs:108-141) on
+    both gzip kernels (the pipelined one folds the check in); with the CRC-32C recomputed over the
+    corrupt stream the gzip decoder's CORRUPT_STREAM (gzip_codec.rs:110-120); the partial path strips
+    the CRC-32C unverified and reports CORRUPT_STREAM either way."""
+    from zarrs_amd import ZgpuError
+    if gzip_kernel == "one_wave":
+        monkeypatch.setenv("ZGPU_GZIP_PIPE_MAX", "0")
+    a, co, shards = c3
+    n_inner = (SHARD // INNER) ** 3
+    key = (0, 1, 0)
+    idx = _index(shards[key], n_inner)
+    off, nb = idx[6], idx[7]  # inner chunk 3
+    for fix_crc, full_status in ((False, 1), (True, 4)):
+        bad = bytearray(shards[key])
+        bad[off] ^= 0xFF  # gzip ID1 0x1f
+        if fix_crc:
+            bad[off + nb - 4:off + nb] = struct.pack("<I", O.crc32c(bytes(bad[off:off + nb - 4])))
+        sh = dict(shards)
+        sh[key] = bytes(bad)
+        arr = _array(sh, ctx, "hbm")
+        start = [0, SHARD, 0]
+        with pytest.raises(ZgpuError) as ei:
+            arr.retrieve_array_subset(start, [SHARD] * 3)
+        assert ei.value.status == full_status, (fix_crc, ei.value.status)
+        with pytest.raises(O.OracleError) as eo:
+            O.retrieve_array_subset(co, [N] * 3, [SHARD] * 3, sh, start, [SHARD] * 3, nthreads=8)
+        assert eo.value.status == full_status
+        with pytest.raises(ZgpuError) as ei:  # partial: crc stripped, the gzip header fails
+            arr.retrieve_array_subset([0, SHARD, 0], [SHARD - 1, SHARD, SHARD])
+        assert ei.value.status == 4
 
 
 def _c5_chunk(seed, shape=(32, 512, 512)):
@@ -160,13 +202,17 @@ C5_CODECS = [BYTES_LE, {"name": "numcodecs.shuffle", "configuration": {"elements
              {"name": "zstd", "configuration": {"level": 3, "checksum": False}}]
 
 
-@pytest.mark.parametrize("force_serial,lits_first", [(False, False), (True, False), (False, True)],
-                         ids=["block_parallel", "serial_fallback", "lits_first_one_stream"])
-def test_c5_16mib_frames(ctx, force_serial, lits_first):
+@pytest.mark.parametrize("force_serial,lits_first,xwin", [(False, False, 1), (False, False, 0), (True, False, 1),
+                                                          (False, True, 1), (False, True, 0)],
+                         ids=["block_parallel", "block_parallel_wave_exec", "serial_fallback",
+                              "lits_first_one_stream", "lits_first_wave_exec"])
+def test_c5_16mib_frames(ctx, force_serial, lits_first, xwin, monkeypatch):
     """Full-size C5 L0 chunks (16 MiB shuffled-u16 zstd frames): bit-exact vs libzstd through the oracle,
     and the path taken is the one asked for (device counters of the call). lits_first: one stream, the
-    Huffman literals decoded before the sequences (ZGPU_ONE_STREAM | ZGPU_ZSTD_LITS_FIRST)."""
+    Huffman literals decoded before the sequences (ZGPU_ONE_STREAM | ZGPU_ZSTD_LITS_FIRST). xwin: the
+    windowed workgroup executor (k_zstd_exec_win, default) or the per-segment wave executor."""
     import torch
+    monkeypatch.setenv("ZGPU_ZSTD_XWIN", str(xwin))
     from zarrs_amd import CodecChain, make_desc
     from zarrs_amd import _lib as L
     co = O.OracleChain.from_metadata(C5_CODECS, "uint16", 0, 3)

@@ -124,3 +124,50 @@ def test_clean_interpreter_exit(case, tmp_path):
     p = subprocess.run([sys.executable, "-c", src], capture_output=True, text=True, timeout=110)
     assert p.returncode == 0, f"rc={p.returncode}\n{p.stderr[-2000:]}"
     assert p.stdout.strip().endswith("done")
+
+
+C5_CODECS = [{"name": "bytes", "configuration": {"endian": "little"}},
+             {"name": "numcodecs.shuffle", "configuration": {"elementsize": 2}},
+             {"name": "zstd", "configuration": {"level": 3, "checksum": False}}]
+
+
+def test_pinned_calls_keep_pools_bounded(monkeypatch):
+    """200 zgpu_decode_pinned calls of varying batch and chunk sizes (the per-codec plugin's pattern that
+    exhausted device memory in the round-5 C5 drop-in leg): every result bit-exact, the device and pinned
+    pools' free blocks within their caps (ZGPU_POOL_CAP_MB / ZGPU_PINNED_CAP_MB, read at context
+    creation), and the blocks in use back to the same level after every call (zgpu_ctx_pool_stats)."""
+    from zarrs_amd import CodecChain, Context, make_desc
+    monkeypatch.setenv("ZGPU_POOL_CAP_MB", "256")
+    monkeypatch.setenv("ZGPU_PINNED_CAP_MB", "128")
+    ctx = Context(0)
+    chain = CodecChain.from_metadata(C5_CODECS, "uint16", 0, ctx)
+    co = O.OracleChain.from_metadata(C5_CODECS, "uint16", 0, 3)
+    rng = np.random.default_rng(11)
+    lives, frees, hfrees, hlives = [], [], [], []
+    for i in range(200):
+        n, rows = 1 + (i * 7) % 8, 1 + (i * 13) % 48
+        base = rng.integers(0, 64, size=(1, 64, 64), dtype=np.uint16)
+        chunks = [(base + rng.integers(0, 3, size=(rows, 64, 64), dtype=np.uint16) * (k + 1)).astype(np.uint16)
+                  for k in range(n)]
+        encs = [co.encode(c) for c in chunks]
+        descs = [make_desc(np.frombuffer(e, np.uint8), [rows, 64, 64], out_start=[k * rows, 0, 0])
+                 for k, e in enumerate(encs)]
+        out = np.empty((n * rows, 64, 64), np.uint16)
+        st = chain.decode_pinned_into(descs, out, [0, 0, 0], [n * rows, 64, 64], coalesce=(i % 2 == 0))
+        assert st == [0] * n, (i, st)
+        assert np.array_equal(out, np.concatenate(chunks)), i
+        s = ctx.pool_stats()
+        lives.append(s["dev_live"])
+        frees.append(s["dev_free"])
+        hlives.append(s["host_live"])
+        hfrees.append(s["host_free"])
+    assert max(frees) <= 256 << 20, max(frees)
+    assert max(hfrees) <= 128 << 20, max(hfrees)
+    # nothing accumulates in use: the second half of the calls holds no more than the first half did
+    assert max(lives[100:]) <= max(lives[:100]), (max(lives[:100]), max(lives[100:]))
+    assert max(hlives[100:]) <= max(hlives[:100]), (max(hlives[:100]), max(hlives[100:]))
+    ctx.release_cached()
+    s = ctx.pool_stats()
+    assert s["dev_free"] == 0 and s["host_free"] == 0, s
+    del chain
+    ctx.close()

@@ -11,6 +11,8 @@
 #   serial:W[:FLAGS]     the same with every plan on one stream (--serial-lanes: per-kernel split)
 #   pmc:W:CTR[:FLAGS]    one rocprofv3 --pmc pass (a single counter) of bench.py --workload W
 #   torchrun:N[:FLAGS]   bench.py --gpus N through torch.distributed.run (N processes)
+#   lab:BIN:ARGS[:ENV]   tools/labbin/BIN with ARGS (comma-separated) and ENV (NAME=VALUE, comma-separated)
+#   py:SCRIPT[:ARGS]     python3 SCRIPT with ARGS (comma-separated), e.g. a tools/*.py measurement
 # Everything lands in gpurun_out/<tag>/ (step-numbered files).
 set -o pipefail
 cd "$GRAFT_REPO_ROOT" || exit 1
@@ -58,6 +60,16 @@ for step in "$@"; do
         --master-port 29517 bench.py --gpus "$a" --no-pmc --no-host-leg "${F[@]}" > "$O/$i.torchrun.json" \
         2> "$O/$i.torchrun.err" || { rc=$?; echo "torchrun rc=$rc"; tail -20 "$O/$i.torchrun.err"; exit $rc; }
       tail -1 "$O/$i.torchrun.json" ;;
+    lab)
+      A=(${b//,/ }); E=(${c//,/ })
+      env "${E[@]}" timeout -k 10 300 "tools/labbin/$a" "${A[@]}" > "$O/$i.lab_$a.txt" 2>&1 \
+        || { rc=$?; echo "lab rc=$rc"; tail -20 "$O/$i.lab_$a.txt"; exit $rc; }
+      cat "$O/$i.lab_$a.txt" ;;
+    py)
+      A=(${b//,/ })
+      timeout -k 10 600 python3 -u "$a" "${A[@]}" > "$O/$i.py.txt" 2>&1 \
+        || { rc=$?; echo "py rc=$rc"; tail -30 "$O/$i.py.txt"; exit $rc; }
+      tail -40 "$O/$i.py.txt" ;;
     *) echo "unknown step $step"; exit 2 ;;
   esac
 done

@@ -56,7 +56,7 @@ int main(int argc, char **argv) {
   }
   std::vector<std::vector<uint8_t>> dec(n), enc(n);
   // c5 modes: chunks past the 64 distinct ones repeat them (throughput at scale)
-  const int ndist = c5 ? std::min(n, 64) : n;
+  const int ndist = l1 ? std::min(n, 16) : c5 ? std::min(n, 64) : n;  // c5l1: the level holds 16 chunks
 #pragma omp parallel for
   for (int c = 0; c < ndist; c++) {
     if (c5) {
@@ -159,6 +159,12 @@ int main(int argc, char **argv) {
     CK(hipMemcpyToSymbol(HIP_SYMBOL(zgpu::g_sqprof), z, sizeof(z)));
   }
 #endif
+#ifdef ZG_XWIN_PROF
+  {
+    unsigned long long z[8] = {0};
+    CK(hipMemcpyToSymbol(HIP_SYMBOL(zgpu::xwin::g_xwprof), z, sizeof(z)));
+  }
+#endif
 #ifdef ZG_PROFILE
   {
     unsigned long long z[13] = {0};
@@ -214,19 +220,26 @@ int main(int argc, char **argv) {
     hipLaunchKernelGGL(zgpu::k_zstd_lits, dim3(lgrid), dim3(zgpu::LIT_THREADS), 0, 0, d_items, d_status, blks, Z.blk_cap,
                        Z.nblk, Z.mode, (uint32_t)n, Z.lit, Z.lit_stride, lit_rec, (const unsigned long long *)nullptr);
     CK(hipEventRecord(ev[4]));
+    // executor: LAB_EXEC=win (k_zstd_exec_win, the default), wide, dense; LAB_XSEG segments per item
+    const char *lx = getenv("LAB_EXEC");
+    const int xk = !lx || !strcmp(lx, "win") ? 2 : !strcmp(lx, "dense") ? 1 : 0;
+    const uint32_t xseg = getenv("LAB_XSEG") ? (uint32_t)atoi(getenv("LAB_XSEG")) : xk == 2 ? zgpu::XSEG_WIN : zgpu::XSEG;
     hipLaunchKernelGGL(zgpu::k_zstd_plan, dim3(n), dim3(64), 0, 0, d_items, d_status, blks, Z.blk_cap, Z.nblk, Z.mode,
-                       chunk, zgpu::XSEG, (uint64_t *)nullptr, Z.lit, Z.lit_stride);
+                       chunk, xseg, (uint64_t *)nullptr, Z.lit, Z.lit_stride);
     CK(hipEventRecord(ev[5]));
     hipLaunchKernelGGL(zgpu::k_zstd_direct, dim3(grid), dim3(256), 0, 0, d_items, d_status, blks, Z.blk_cap, Z.nblk,
                        Z.mode, (uint32_t)n, d_out, chunk, Z.lit, Z.lit_stride, (const uint64_t *)nullptr,
                        (const unsigned long long *)nullptr, 0);
     CK(hipEventRecord(ev[6]));
-    if (getenv("LAB_XDENSE"))
-      hipLaunchKernelGGL(zgpu::xdense::k_zstd_exec_item, dim3(n * zgpu::XSEG), dim3(64), 0, 0, d_items, d_status, blks,
-                         Z.blk_cap, Z.nblk, Z.mode, d_out, chunk, Z.lit, Z.lit_stride, Z.seq, Z.seq_cap, zgpu::XSEG);
+    if (xk == 2)
+      hipLaunchKernelGGL(zgpu::k_zstd_exec_win, dim3(n * xseg), dim3(zgpu::xwin::THREADS), 0, 0, d_items, d_status,
+                         blks, Z.blk_cap, Z.nblk, Z.mode, d_out, chunk, Z.lit, Z.lit_stride, Z.seq, Z.seq_cap, xseg);
+    else if (xk == 1)
+      hipLaunchKernelGGL(zgpu::xdense::k_zstd_exec_item, dim3(n * xseg), dim3(64), 0, 0, d_items, d_status, blks,
+                         Z.blk_cap, Z.nblk, Z.mode, d_out, chunk, Z.lit, Z.lit_stride, Z.seq, Z.seq_cap, xseg);
     else
-      hipLaunchKernelGGL(zgpu::xwide::k_zstd_exec_item, dim3(n * zgpu::XSEG), dim3(64), 0, 0, d_items, d_status, blks,
-                         Z.blk_cap, Z.nblk, Z.mode, d_out, chunk, Z.lit, Z.lit_stride, Z.seq, Z.seq_cap, zgpu::XSEG);
+      hipLaunchKernelGGL(zgpu::xwide::k_zstd_exec_item, dim3(n * xseg), dim3(64), 0, 0, d_items, d_status, blks,
+                         Z.blk_cap, Z.nblk, Z.mode, d_out, chunk, Z.lit, Z.lit_stride, Z.seq, Z.seq_cap, xseg);
     CK(hipEventRecord(ev[7]));
     CK(hipEventSynchronize(ev[7]));
     for (int k = 0; k < NK; k++) {
@@ -245,7 +258,15 @@ int main(int argc, char **argv) {
   uint64_t blocks = 0;
   for (int c = 0; c < n; c++) {
     CK(hipMemcpy(out.data(), d_out + (uint64_t)c * chunk, chunk, hipMemcpyDeviceToHost));
-    if (st[c] || memcmp(out.data(), dec[c].data(), chunk)) bad++;
+    if (st[c] || memcmp(out.data(), dec[c].data(), chunk)) {
+      if (bad < 4) {
+        uint64_t k = 0;
+        while (k < chunk && out[k] == dec[c][k]) k++;
+        printf("chunk %d: status %u, first mismatch at %llu (got %u want %u)\n", c, st[c], (unsigned long long)k,
+               k < chunk ? out[k] : 0, k < chunk ? dec[c][k] : 0);
+      }
+      bad++;
+    }
     blocks += nblk[c];
   }
   double tot = 0;
@@ -283,6 +304,15 @@ int main(int argc, char **argv) {
     printf("resolve per frame (Mticks): ready %.2f fast copies %.2f slow copies %.2f | rounds %.0f\n", z[8] / per / 1e6,
            z[9] / per / 1e6, z[10] / per / 1e6, (double)z[11] / per);
     printf("batches with far sources per frame: %.0f\n", z[12] / per);
+  }
+#endif
+#ifdef ZG_XWIN_PROF
+  {
+    unsigned long long z[8];
+    CK(hipMemcpyFromSymbol(z, HIP_SYMBOL(zgpu::xwin::g_xwprof), sizeof(z)));
+    const double w = z[6] ? (double)z[6] : 1.0;
+    printf("exec_win per window (clocks, workgroup thread 0): table %.0f rows %.0f expand %.0f rounds %.0f output %.0f | "
+           "windows %llu (all reps), rounds/window %.2f\n", z[0] / w, z[1] / w, z[2] / w, z[3] / w, z[4] / w, z[6], z[7] / w);
   }
 #endif
 #ifdef ZG_SQ_PROFILE

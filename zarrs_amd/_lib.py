@@ -42,7 +42,7 @@ EXPORTS = [
     "zgpu_cache_retrieve_array_subset", "zgpu_retrieve_array_subset_dlpack", "zgpu_chain_encoded_bound",
     "zgpu_encode_chunks", "zgpu_retrieve_array_subset_multi", "zgpu_decode_into", "zgpu_ctx_set_coalescing",
     "zgpu_ctx_coalescing_stats", "zgpu_ctx_refcount", "zgpu_decode_pinned", "zgpu_result_release",
-    "zgpu_encode_pinned", "zgpu_ctx_release_cached",
+    "zgpu_encode_pinned", "zgpu_ctx_release_cached", "zgpu_ctx_pool_stats",
 ]
 CTR_ENC_BYTES, CTR_ZSTD_SERIAL, CTR_ZSTD_PARALLEL, CTR_BLOSC_RERUN, CTR_BLOSC_BLOCKS, CTR_ITEMS = range(6)
 N_COUNTERS = 6
@@ -130,6 +130,7 @@ def load() -> C.CDLL:
                                      C.POINTER(C.c_void_p)]
     L.zgpu_result_release.restype = None
     L.zgpu_ctx_release_cached.argtypes = [vp]
+    L.zgpu_ctx_pool_stats.argtypes = [vp, P64, P64, P64, P64]
     L.zgpu_ctx_refcount.argtypes = [vp]
     L.zgpu_ctx_refcount.restype = C.c_int64
     L.zgpu_last_error.restype = C.c_char_p

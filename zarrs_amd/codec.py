@@ -80,6 +80,13 @@ class Context:
         if getattr(self, "_h", None):
             L.check(L.load().zgpu_ctx_release_cached(self._h))
 
+    def pool_stats(self) -> dict:
+        """The context's pooled memory in bytes (zgpu_ctx_pool_stats): device blocks in use / cached
+        free, pinned host blocks in use / cached free."""
+        v = [C.c_uint64() for _ in range(4)]
+        L.check(L.load().zgpu_ctx_pool_stats(self._h, *[C.byref(x) for x in v]))
+        return dict(zip(("dev_live", "dev_free", "host_live", "host_free"), (x.value for x in v)))
+
     def close(self):
         """Drop this handle's reference (zgpu_ctx_destroy). Chains, plans and caches made on the
         context keep it alive until they are destroyed too, in any order."""

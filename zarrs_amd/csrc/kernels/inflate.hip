@@ -1163,7 +1163,20 @@ __global__ __launch_bounds__(PIPE ? 128 : 64) __attribute__((amdgpu_waves_per_eu
     if (!err && hp + 8 > in_len) err = ZG_CORRUPT_STREAM;
   }
   if (err) {
-    if (lane == 0) status[item] = err;
+    if constexpr (PIPE) {
+      // the chain decodes crc32c before gzip (crc32c_codec.rs:108-141): a stream whose CRC-32C fails
+      // is INVALID_CHECKSUM even when its gzip header is corrupt too, as with k_crc32c_strip. Wave 0
+      // checks it here (wave 1 has not split off yet and returns).
+      if (crc_tail == 1 && !(it.flags & ZG_ITEM_PARTIAL)) {
+        if (threadIdx.x >= 64) return;
+        wave_crc_tables(S.c32c, POLY_CRC32C);
+        const uint32_t c = wave_crc(in, in_len, S.c32c, POLY_CRC32C);
+        const uint32_t st = U(in[in_len]) | (U(in[in_len + 1]) << 8) | (U(in[in_len + 2]) << 16) |
+                            (U(in[in_len + 3]) << 24);
+        if (c != st) err = ZG_INVALID_CHECKSUM;
+      }
+    }
+    if (lane == 0 && threadIdx.x < 64) status[item] = err;
     return;
   }
 

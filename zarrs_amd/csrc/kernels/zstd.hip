@@ -3743,6 +3743,14 @@ namespace xdense {
 #undef ZX_STAGE_V
 #undef ZX_WPE
 }  // namespace xdense
+// k_zstd_exec_win (kernels/zstd_xwin.inc): one 512-thread workgroup per segment, 32 KiB windows
+// resolved in parallel by pointer jumping in LDS; the default executor (ZGPU_ZSTD_XWIN=0: the wave
+// executors above)
+#include "zstd_xwin.inc"
+#ifndef ZG_XSEG_WIN
+#define ZG_XSEG_WIN 8
+#endif
+constexpr uint32_t XSEG_WIN = ZG_XSEG_WIN;  // executor segments per item (at most) for k_zstd_exec_win
 // executor grids of at least this many waves (items x segments) per CU take xdense
 #ifndef ZG_XDENSE_WPC
 #define ZG_XDENSE_WPC 64
@@ -3813,7 +3821,10 @@ static hipError_t launch_zstd_pass(ZgItem *items, uint32_t *status, uint32_t n_i
     const char *e = std::getenv("ZGPU_ZSTD_XSEG");
     return e ? (uint32_t)std::min<unsigned long>(64, std::max<unsigned long>(1, std::strtoul(e, nullptr, 10))) : 0u;
   }();
-  const uint32_t xseg = xseg_env ? xseg_env : XSEG;
+  // executor: the windowed workgroup executor unless ZGPU_ZSTD_XWIN=0 (read per call: tests run both)
+  const char *xw_s = std::getenv("ZGPU_ZSTD_XWIN");
+  const bool xwin_on = !xw_s || std::atoi(xw_s) != 0;
+  const uint32_t xseg = xseg_env ? xseg_env : xwin_on ? XSEG_WIN : XSEG;
 
   if (fork) {
     hipError_t e = hipEventRecord(Z.ev_fork, s);
@@ -3876,7 +3887,10 @@ static hipError_t launch_zstd_pass(ZgItem *items, uint32_t *status, uint32_t n_i
   const int xd_env = xd_s ? std::atoi(xd_s) : -1;
   const bool dense = xd_env >= 0 ? xd_env != 0
                                  : (uint64_t)n_items * xseg >= (uint64_t)device_cu_count() * XDENSE_WAVES_PER_CU;
-  if (dense)
+  if (xwin_on)
+    hipLaunchKernelGGL(k_zstd_exec_win, dim3(n_items * xseg), dim3(xwin::THREADS), 0, s, items, status, blks,
+                       Z.blk_cap, Z.nblk, Z.mode, dst, slot_bytes, Z.lit, Z.lit_stride, Z.seq, Z.seq_cap, xseg);
+  else if (dense)
     hipLaunchKernelGGL(xdense::k_zstd_exec_item, dim3(n_items * xseg), dim3(64), 0, s, items, status, blks, Z.blk_cap,
                        Z.nblk, Z.mode, dst, slot_bytes, Z.lit, Z.lit_stride, Z.seq, Z.seq_cap, xseg);
   else

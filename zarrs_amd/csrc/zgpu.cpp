@@ -202,18 +202,36 @@ struct zgpu_ctx {
     live_dev.erase(it);
     if (free_dev_bytes > pool_cap) trim_free_locked(pool_cap / 2);
   }
+  // Pinned host pool: the same size classes, free blocks capped at ZGPU_PINNED_CAP_MB (default 4 GiB;
+  // the largest go back to HIP beyond it) -- per-chunk pinned results of varying size otherwise
+  // accumulate a free block per distinct size
+  size_t free_host_bytes = 0;
+  size_t host_cap = (size_t)4 << 30;
+  void trim_host_locked(size_t keep) {
+    while (free_host_bytes > keep && !free_host.empty()) {
+      auto it = std::prev(free_host.end());
+      (void)hipHostFree(it->second);
+      free_host_bytes -= it->first;
+      free_host.erase(it);
+    }
+  }
   void *host_alloc(size_t bytes) {
     std::lock_guard<std::mutex> lk(mu);
-    bytes = std::max<size_t>(4096, (bytes + 4095) & ~(size_t)4095);
+    bytes = std::max<size_t>(4096, size_class((bytes + 4095) & ~(size_t)4095));
     auto it = free_host.lower_bound(bytes);
-    if (it != free_host.end() && it->first <= bytes * 2 + (1u << 20)) {
+    if (it != free_host.end() && it->first <= bytes + bytes / 4 + (1u << 20)) {
       void *p = it->second;
       live_host[p] = it->first;
+      free_host_bytes -= it->first;
       free_host.erase(it);
       return p;
     }
     void *p = nullptr;
-    HIPCHK(hipHostMalloc(&p, bytes, hipHostMallocDefault));
+    if (hipHostMalloc(&p, bytes, hipHostMallocDefault) != hipSuccess) {  // release the cache and retry once
+      (void)hipGetLastError();
+      trim_host_locked(0);
+      HIPCHK(hipHostMalloc(&p, bytes, hipHostMallocDefault));
+    }
     live_host[p] = bytes;
     return p;
   }
@@ -223,7 +241,9 @@ struct zgpu_ctx {
     auto it = live_host.find(p);
     if (it == live_host.end()) return;
     free_host.emplace(it->second, p);
+    free_host_bytes += it->second;
     live_host.erase(it);
+    if (free_host_bytes > host_cap) trim_host_locked(host_cap / 2);
   }
   ~zgpu_ctx() {
     (void)hipSetDevice(device);
@@ -1797,6 +1817,7 @@ int zgpu_ctx_create(int dev, zgpu_ctx **out) {
   c->device = dev;
   if (const char *e = std::getenv("ZGPU_CTX_LANES")) c->max_lanes = (uint32_t)std::max(1, std::min(64, std::atoi(e)));
   if (const char *e = std::getenv("ZGPU_POOL_CAP_MB")) c->pool_cap = (size_t)std::max(64, std::atoi(e)) << 20;
+  if (const char *e = std::getenv("ZGPU_PINNED_CAP_MB")) c->host_cap = (size_t)std::max(64, std::atoi(e)) << 20;
   c->release_lane(c->acquire_lane());  // the first lane up front (stream creation errors surface here)
   *out = c.release();
   return ZGPU_OK;
@@ -1807,13 +1828,28 @@ void zgpu_ctx_destroy(zgpu_ctx *c) { ctx_unref(c); }
 
 int64_t zgpu_ctx_refcount(const zgpu_ctx *c) { return c ? c->refs.load() : 0; }
 
+int zgpu_ctx_pool_stats(const zgpu_ctx *c, uint64_t *dev_live, uint64_t *dev_free, uint64_t *host_live,
+                        uint64_t *host_free) {
+  if (!c) return set_err(ZGPU_INVALID_ARGUMENT, "NULL argument");
+  zgpu_ctx *m = const_cast<zgpu_ctx *>(c);  // the allocator lock only
+  std::lock_guard<std::mutex> lk(m->mu);
+  uint64_t dl = 0, hl = 0, hf = 0;
+  for (const auto &kv : c->live_dev) dl += kv.second;
+  for (const auto &kv : c->live_host) hl += kv.second;
+  hf = c->free_host_bytes;
+  if (dev_live) *dev_live = dl;
+  if (dev_free) *dev_free = c->free_dev_bytes;
+  if (host_live) *host_live = hl;
+  if (host_free) *host_free = hf;
+  return ZGPU_OK;
+}
+
 int zgpu_ctx_release_cached(zgpu_ctx *c) {
   if (!c) return set_err(ZGPU_INVALID_ARGUMENT, "NULL argument");
   std::lock_guard<std::mutex> lk(c->mu);
   if (hipSetDevice(c->device) != hipSuccess) (void)hipGetLastError();
   c->trim_free_locked(0);
-  for (auto &kv : c->free_host) (void)hipHostFree(kv.second);
-  c->free_host.clear();
+  c->trim_host_locked(0);
   (void)hipGetLastError();
   return ZGPU_OK;
 }
