@@ -161,7 +161,7 @@ int main(int argc, char **argv) {
 #endif
 #ifdef ZG_XWIN_PROF
   {
-    unsigned long long z[8] = {0};
+    unsigned long long z[16] = {0};
     CK(hipMemcpyToSymbol(HIP_SYMBOL(zgpu::xwin::g_xwprof), z, sizeof(z)));
   }
 #endif
@@ -308,9 +308,12 @@ int main(int argc, char **argv) {
 #endif
 #ifdef ZG_XWIN_PROF
   {
-    unsigned long long z[8];
+    unsigned long long z[16];
     CK(hipMemcpyFromSymbol(z, HIP_SYMBOL(zgpu::xwin::g_xwprof), sizeof(z)));
     const double w = z[6] ? (double)z[6] : 1.0;
+    printf("exec_win per window: pointer cells %.0f literal loads %.0f far loads %.0f | classify clocks %.0f | wave-0 "
+           "round steps %.2f, wave-0 round clocks (no barrier) %.0f\n", z[8] / w, z[9] / w, z[10] / w, z[5] / w, z[11] / w,
+           z[12] / w);
     printf("exec_win per window (clocks, workgroup thread 0): table %.0f rows %.0f expand %.0f rounds %.0f output %.0f | "
            "windows %llu (all reps), rounds/window %.2f\n", z[0] / w, z[1] / w, z[2] / w, z[3] / w, z[4] / w, z[6], z[7] / w);
   }

@@ -176,6 +176,36 @@ struct InW {
   }
 };
 
+// ---- per-lane forward byte access (k_zstd_scan's block parse: one lane per block) ----
+struct InL {
+  const uint32_t *words;
+  uint64_t n, nwords;
+  uint32_t mis;
+  __device__ InL(const uint8_t *p, uint64_t n_) : n(n_) {
+    mis = (uint32_t)((uintptr_t)p & 3);
+    words = (const uint32_t *)((uintptr_t)p - mis);
+    nwords = (n_ + mis + 3) / 4;
+  }
+  __device__ __forceinline__ uint32_t w(uint64_t k) const { return k < nwords ? words[k] : 0u; }
+  __device__ __forceinline__ uint32_t b(uint64_t i) const {
+    if (i >= n) return 0u;
+    return (w((i + mis) >> 2) >> (8 * ((i + mis) & 3))) & 0xFFu;
+  }
+  __device__ __forceinline__ uint64_t le40(uint64_t i) const {  // zero past the item
+    if (i + 5 > n) {
+      uint64_t v = 0;
+      for (uint32_t k = 0; k < 5; k++) v |= (uint64_t)b(i + k) << (8 * k);
+      return v;
+    }
+    const uint64_t k = (i + mis) >> 2;
+    const uint64_t v = (uint64_t)w(k) | ((uint64_t)w(k + 1) << 32);
+    return (v >> (8 * ((i + mis) & 3))) & 0xFFFFFFFFFFull;
+  }
+  __device__ __forceinline__ uint32_t le16(uint64_t i) const { return (uint32_t)le40(i) & 0xFFFFu; }
+  __device__ __forceinline__ uint32_t le24(uint64_t i) const { return (uint32_t)le40(i) & 0xFFFFFFu; }
+  __device__ __forceinline__ uint32_t le32(uint64_t i) const { return (uint32_t)le40(i); }
+};
+
 // ---- uniform backward bit reader over [lo, hi) bytes of the item input ----
 // Bits are numbered as in a little-endian integer of the aligned item buffer; the stream's data
 // bits are [lo_bit, top) where top is just below the padding marker of byte hi-1.
@@ -238,7 +268,8 @@ __device__ __forceinline__ bool bb_overflow(const BitsBack &R) { return R.cur < 
 
 // ---- FSE ----
 // Parse an FSE table description (FSE_readNCount semantics). Returns bytes consumed, 0 on error.
-template <class IN>
+// STORE = false: only the description's size (k_zstd_scan's per-lane block parse; norm unused).
+template <class IN, bool STORE = true>
 __device__ uint32_t read_ncount(IN &I, uint64_t off, uint64_t avail, int16_t *norm, uint32_t max_sym,
                                 uint32_t max_log, uint32_t &acc_log, uint32_t &nsym) {
   uint64_t bit = 0;
@@ -255,7 +286,8 @@ __device__ uint32_t read_ncount(IN &I, uint64_t off, uint64_t avail, int16_t *no
   int nbBits = acc_log + 1;
   uint32_t s = 0;
   bool prev0 = false;
-  for (uint32_t k = 0; k <= max_sym; k++) norm[k] = 0;
+  if constexpr (STORE)
+    for (uint32_t k = 0; k <= max_sym; k++) norm[k] = 0;
   while (remaining > 1 && s <= max_sym) {
     if (prev0) {
       uint32_t rep;
@@ -283,7 +315,8 @@ __device__ uint32_t read_ncount(IN &I, uint64_t off, uint64_t avail, int16_t *no
     count--;
     remaining -= count < 0 ? -count : count;
     if (s > max_sym) return 0;
-    norm[s++] = (int16_t)count;
+    if constexpr (STORE) norm[s] = (int16_t)count;
+    s++;
     prev0 = (count == 0);
     if (remaining < threshold) {
       if (remaining <= 1) break;
@@ -1235,13 +1268,14 @@ __device__ __forceinline__ uint64_t rec_blocks(uint32_t blk_cap, const unsigned 
   return max_nblk ? min<uint64_t>(blk_cap, *max_nblk) : blk_cap;
 }
 
-__global__ __launch_bounds__(64) void k_zstd_scan(const ZgItem *items, uint32_t *status, ZBlk *blks,
-                                                  uint32_t blk_cap, uint32_t *nblk, uint32_t *zmode,
-                                                  uint64_t lit_stride, uint64_t seq_cap, uint32_t force_serial,
-                                                  unsigned long long *counters, uint32_t *ser_list,
-                                                  unsigned long long *ser_count, unsigned long long *max_nblk) {
-  __shared__ ZScanSmem S;
-  const uint32_t item = blockIdx.x;
+// The uniform one-wave frame walk: every block header and section header in order, one register
+// window load per position. k_zstd_scan below takes it for frames of more blocks than its LDS holds.
+__device__ __attribute__((noinline)) void scan_uniform(ZScanSmem &S, uint32_t item, const ZgItem *items,
+                                                        uint32_t *status, ZBlk *blks, uint32_t blk_cap,
+                                                        uint32_t *nblk, uint32_t *zmode, uint64_t lit_stride,
+                                                        uint64_t seq_cap, uint32_t force_serial,
+                                                        unsigned long long *counters, uint32_t *ser_list,
+                                                        unsigned long long *ser_count, unsigned long long *max_nblk) {
   const ZgItem it = items[item];
   const int lane = lane_id();
   if (status[item] || (it.flags & ZG_ITEM_FILL)) {
@@ -1443,6 +1477,303 @@ __global__ __launch_bounds__(64) void k_zstd_scan(const ZgItem *items, uint32_t 
   if (!err && !serial && !any_frame) err = ZG_CORRUPT_STREAM;
   if (lane == 0) {
     nblk[item] = serial ? 0u : nb;
+    zmode[item] = serial ? ZMODE_SERIAL : (err ? ZMODE_SKIP : ZMODE_PARALLEL);
+    if (err && !serial) status[item] = err;
+    if (counters && (serial || !err)) atomicAdd(&counters[serial ? 0 : 1], 1ull);  // serial / block-parallel items
+    if (serial && ser_list) ser_list[atomicAdd(ser_count, 1ull)] = item;
+    if (max_nblk && !serial && !err) atomicMax(max_nblk, (unsigned long long)nb);
+  }
+}
+
+// k_zstd_scan: one wave per item, in three passes over the frame. (A) a uniform walk of the frame and
+// block headers alone -- one dependent load per block (the next header is bsize bytes on), recorded in
+// LDS; (B) every compressed block's literal / sequence section headers and FSE table descriptions
+// parsed by its own lane (per-lane loads: 64 blocks at once); (C) a uniform pass over the LDS records in
+// block order: treeless literals and repeat table modes resolved to the block that defined them, the
+// literal / sequence scratch offsets, the first error or scratch overflow. The one-walk form took
+// ~22 us per 128 KiB block of a C5 frame (dependent header reads in series: 2.8 ms a frame).
+#ifndef ZG_SCAN_LDS_BLOCKS
+#define ZG_SCAN_LDS_BLOCKS 144
+#endif
+constexpr uint32_t SCAN_LB = ZG_SCAN_LDS_BLOCKS;
+struct ZScan2Smem {
+  ZBlk R[SCAN_LB];
+  uint32_t err[SCAN_LB];
+};
+constexpr uint32_t TREE_NONE = 0xFFFFFFFFu;
+
+__global__ __launch_bounds__(64) void k_zstd_scan(const ZgItem *items, uint32_t *status, ZBlk *blks,
+                                                  uint32_t blk_cap, uint32_t *nblk, uint32_t *zmode,
+                                                  uint64_t lit_stride, uint64_t seq_cap, uint32_t force_serial,
+                                                  unsigned long long *counters, uint32_t *ser_list,
+                                                  unsigned long long *ser_count, unsigned long long *max_nblk) {
+  __shared__ ZScanSmem S;
+  __shared__ ZScan2Smem Q;
+  const uint32_t item = blockIdx.x;
+  const ZgItem it = items[item];
+  const int lane = lane_id();
+  if (status[item] || (it.flags & ZG_ITEM_FILL)) {
+    if (lane == 0) { nblk[item] = 0; zmode[item] = ZMODE_SKIP; }
+    return;
+  }
+  if (it.len >= 0xFFFFFFF0ull || force_serial) {  // 32-bit record offsets: decode such items serially
+    if (lane == 0) {
+      nblk[item] = 0;
+      zmode[item] = ZMODE_SERIAL;
+      if (counters) atomicAdd(&counters[0], 1ull);
+      if (ser_list) ser_list[atomicAdd(ser_count, 1ull)] = item;
+    }
+    return;
+  }
+  const uint8_t *in = (const uint8_t *)it.src;
+  InW I(in, it.len);
+  // ---- (A) frame and block headers ----
+  uint32_t nb = 0, err = 0;
+  bool serial = false, any_frame = false, full = false;
+  uint64_t ip = 0;
+#define SFAIL(code) { err = (code); break; }
+  while (!err && !serial && !full && ip < it.len) {
+    const uint32_t magic = I.le32(ip);
+    if (ip + 4 > it.len) SFAIL(ZG_CORRUPT_STREAM);
+    if ((magic & 0xFFFFFFF0u) == 0x184D2A50u) {  // skippable frame
+      if (ip + 8 > it.len) SFAIL(ZG_CORRUPT_STREAM);
+      ip += 8 + (uint64_t)I.le32(ip + 4);
+      if (ip > it.len) SFAIL(ZG_CORRUPT_STREAM);
+      continue;
+    }
+    if (magic != 0xFD2FB528u) SFAIL(ZG_CORRUPT_STREAM);
+    ip += 4;
+    any_frame = true;
+    const uint32_t fhd = I.b(ip++);
+    const uint32_t fcs_flag = fhd >> 6, single = (fhd >> 5) & 1, has_ck = (fhd >> 2) & 1, did_flag = fhd & 3;
+    if (fhd & 8) SFAIL(ZG_CORRUPT_STREAM);
+    if (!single) ip++;
+    const uint32_t did_sz = did_flag == 3 ? 4 : did_flag;
+    uint32_t did = 0;
+    for (uint32_t k = 0; k < did_sz; k++) did |= I.b(ip + k) << (8 * k);
+    ip += did_sz;
+    if (did != 0) SFAIL(ZG_CORRUPT_STREAM);
+    const uint32_t fcs_sz = fcs_flag == 0 ? (single ? 1 : 0) : (fcs_flag == 1 ? 2 : fcs_flag == 2 ? 4 : 8);
+    uint64_t fcs = 0;
+    for (uint32_t k = 0; k < fcs_sz; k++) fcs |= (uint64_t)I.b(ip + k) << (8 * k);
+    if (fcs_sz == 2) fcs += 256;
+    ip += fcs_sz;
+    if (ip > it.len) SFAIL(ZG_CORRUPT_STREAM);
+    bool first = true, last = false;
+    while (!last && !err) {
+      if (nb == blk_cap) { serial = true; break; }
+      if (nb == SCAN_LB) { full = true; break; }
+      if (ip + 3 > it.len) SFAIL(ZG_CORRUPT_STREAM);
+      const uint32_t bh = I.le24(ip);
+      ip += 3;
+      last = bh & 1;
+      const uint32_t btype = (bh >> 1) & 3, bsize = bh >> 3;
+      if (btype == 3) SFAIL(ZG_CORRUPT_STREAM);
+      ZBlk R{};
+      R.flags = btype | (first ? ZBF_FIRST : 0u) | (last ? ZBF_LAST : 0u);
+      if (first && fcs_sz) { R.flags |= ZBF_FCS; R.fcs = fcs; }
+      first = false;
+      R.in_off = (uint32_t)ip;
+      if (btype == 0) {
+        if (ip + bsize > it.len) SFAIL(ZG_CORRUPT_STREAM);
+        R.in_size = bsize;
+        R.out_size = bsize;
+        ip += bsize;
+      } else if (btype == 1) {
+        if (ip + 1 > it.len) SFAIL(ZG_CORRUPT_STREAM);
+        R.in_size = 1;
+        R.out_size = bsize;
+        ip += 1;
+      } else {
+        if (bsize > BLOCK_MAX || ip + bsize > it.len) SFAIL(ZG_CORRUPT_STREAM);
+        R.in_size = bsize;
+        ip += bsize;
+      }
+      if (last && has_ck) {
+        if (ip + 4 > it.len) SFAIL(ZG_CORRUPT_STREAM);
+        R.flags |= ZBF_CK;
+        R.ck = I.le32(ip);
+        ip += 4;
+      }
+      if (lane == 0) Q.R[nb] = R;
+      nb++;
+    }
+  }
+#undef SFAIL
+  if (full) {  // more blocks than the LDS records hold: the one-walk form
+    scan_uniform(S, item, items, status, blks, blk_cap, nblk, zmode, lit_stride, seq_cap, force_serial, counters,
+                 ser_list, ser_count, max_nblk);
+    return;
+  }
+  __syncthreads();
+  // ---- (B) compressed blocks' sections, one lane per block ----
+  {
+    const InL L(in, it.len);
+    for (uint32_t bi = lane; bi < nb; bi += 64) {
+      ZBlk &R = Q.R[bi];
+      uint32_t e = 0;
+      if ((R.flags & 3) == ZB_CMP) {
+        do {
+          const uint64_t bend = (uint64_t)R.in_off + R.in_size;
+          uint64_t p = R.in_off;
+          const uint32_t b0 = L.b(p);
+          const uint32_t ltype = b0 & 3, sfmt = (b0 >> 2) & 3;
+          uint32_t regen = 0, csize = 0, lhdr = 0, four = 0;
+          if (ltype <= 1) {
+            if (sfmt == 0 || sfmt == 2) { regen = b0 >> 3; lhdr = 1; }
+            else if (sfmt == 1) { regen = (b0 >> 4) | (L.b(p + 1) << 4); lhdr = 2; }
+            else { regen = (b0 >> 4) | (L.b(p + 1) << 4) | (L.b(p + 2) << 12); lhdr = 3; }
+          } else {
+            four = sfmt == 0 ? 0 : 1;
+            if (sfmt <= 1) { const uint32_t v = L.le24(p); regen = (v >> 4) & 0x3FF; csize = (v >> 14) & 0x3FF; lhdr = 3; }
+            else if (sfmt == 2) { const uint32_t v = L.le32(p); regen = (v >> 4) & 0x3FFF; csize = (v >> 18) & 0x3FFF; lhdr = 4; }
+            else {
+              const uint64_t v = L.le40(p);
+              regen = (uint32_t)(v >> 4) & 0x3FFFF; csize = (uint32_t)(v >> 22) & 0x3FFFF; lhdr = 5;
+            }
+          }
+          if (regen > BLOCK_MAX) { e = ZG_CORRUPT_STREAM; break; }
+          p += lhdr;
+          R.flags |= (ltype << 2) | (four << 4);
+          R.regen = regen;
+          R.huf_off = TREE_NONE;
+          if (ltype == 0) {
+            if (p + regen > bend) { e = ZG_CORRUPT_STREAM; break; }
+            R.lit_off = (uint32_t)p;
+            R.lit_end = (uint32_t)(p + regen);
+            p += regen;
+          } else if (ltype == 1) {
+            if (p + 1 > bend) { e = ZG_CORRUPT_STREAM; break; }
+            R.lit_off = (uint32_t)p;
+            p += 1;
+          } else {
+            if (p + csize > bend) { e = ZG_CORRUPT_STREAM; break; }
+            uint64_t q = p;
+            if (ltype == 2) {  // tree description: FSE-compressed weights (hb < 128) or 4-bit weights
+              const uint32_t hb = L.b(q);
+              const uint32_t tsz = hb < 128 ? 1 + hb : 1 + (hb - 127 + 1) / 2;
+              if (hb == 0 || tsz > csize) { e = ZG_CORRUPT_STREAM; break; }
+              R.huf_off = (uint32_t)q;  // this block's own tree
+              q += tsz;
+            }
+            R.lit_off = (uint32_t)q;
+            R.lit_end = (uint32_t)(p + csize);
+            p += csize;
+          }
+          if (p >= bend) { e = ZG_CORRUPT_STREAM; break; }
+          uint32_t nseq = 0;
+          const uint32_t c0 = L.b(p);
+          if (c0 < 128) { nseq = c0; p += 1; }
+          else if (c0 < 255) { nseq = ((c0 - 128) << 8) + L.b(p + 1); p += 2; }
+          else { nseq = L.le16(p + 1) + 0x7F00; p += 3; }
+          R.nseq = nseq;
+          if (nseq) {
+            if (p >= bend) { e = ZG_CORRUPT_STREAM; break; }
+            const uint32_t modes = L.b(p++);
+            if (modes & 3) { e = ZG_CORRUPT_STREAM; break; }
+            const uint32_t mm[3] = {modes >> 6, (modes >> 4) & 3, (modes >> 2) & 3};  // LL, OF, ML
+            uint32_t raw = 0;
+            for (int t = 0; t < 3 && !e; t++) {
+              const uint32_t maxs = t == 0 ? 35 : t == 1 ? 31 : 52, maxl = t == 0 ? 9 : t == 1 ? 8 : 9;
+              raw |= mm[t] << (2 * t);  // 3: repeat, resolved in (C)
+              R.tab_off[t] = 0;
+              if (mm[t] == 1) {
+                if (p >= bend || L.b(p) > maxs) { e = ZG_CORRUPT_STREAM; break; }
+                R.tab_off[t] = (uint32_t)p;
+                p += 1;
+              } else if (mm[t] == 2) {
+                uint32_t acc, ns;
+                const uint32_t used = read_ncount<const InL, false>(L, p, bend - p, nullptr, maxs, maxl, acc, ns);
+                if (!used) { e = ZG_CORRUPT_STREAM; break; }
+                R.tab_off[t] = (uint32_t)p;
+                p += used;
+              }
+            }
+            if (e) break;
+            R.tab_mode = raw;
+            R.seq_off = (uint32_t)p;
+            R.seq_end = (uint32_t)bend;
+          } else if (p != bend) {
+            e = ZG_CORRUPT_STREAM;
+            break;
+          }
+        } while (false);
+      }
+      Q.err[bi] = e;
+    }
+  }
+  __syncthreads();
+  // ---- (C) in block order: tree / table references, scratch offsets, the first error or overflow ----
+  uint32_t nbv = nb;
+  if (!serial && !err) {
+    uint64_t lit_used = 0, seq_used = 0;
+    uint32_t huf_src = TREE_NONE, tmode[3] = {3, 3, 3}, toff[3] = {0, 0, 0};  // 3 = no table yet
+    for (uint32_t bi = 0; bi < nb; bi++) {
+      ZBlk &R = Q.R[bi];
+      const uint32_t flags = U(R.flags);
+      if (flags & ZBF_FIRST) {  // a new frame: no tree, no tables
+        huf_src = TREE_NONE;
+        tmode[0] = tmode[1] = tmode[2] = 3;
+      }
+      if ((flags & 3) != ZB_CMP) continue;
+      if (U(Q.err[bi])) { err = ZG_CORRUPT_STREAM; nbv = bi; break; }
+      const uint32_t ltype = (flags >> 2) & 3, regen = U(R.regen), nseq = U(R.nseq);
+      uint32_t huf = 0;
+      if (ltype == 2) huf_src = huf = U(R.huf_off);
+      else if (ltype == 3) {
+        if (huf_src == TREE_NONE) { err = ZG_CORRUPT_STREAM; nbv = bi; break; }  // treeless without a tree
+        huf = huf_src;
+      }
+      uint32_t lit_buf = 0;
+      if (ltype != 0) {  // rle / huffman literals are materialised in the literal scratch
+#if ZG_HUF_SPLIT
+        if (ltype >= 2) lit_used = ((lit_used + 15) & ~(uint64_t)15) + HUF_TAB;  // the block's table
+#endif
+        lit_buf = (uint32_t)lit_used;
+        lit_used += regen;
+        if (lit_used > lit_stride) { serial = true; break; }
+      }
+      uint32_t tab_mode = 0, seq_buf = 0;
+      if (nseq) {
+        const uint32_t raw = U(R.tab_mode);
+        bool ok = true;
+        for (int t = 0; t < 3; t++) {
+          const uint32_t m = (raw >> (2 * t)) & 3;
+          if (m == 3) {
+            if (tmode[t] == 3) ok = false;  // repeat mode without a previous table
+          } else {
+            tmode[t] = m;
+            toff[t] = U(R.tab_off[t]);
+          }
+        }
+        if (!ok) { err = ZG_CORRUPT_STREAM; nbv = bi; break; }
+        tab_mode = tmode[0] | (tmode[1] << 2) | (tmode[2] << 4);
+        seq_buf = (uint32_t)seq_used;
+        seq_used += nseq;
+        if (seq_used > seq_cap) { serial = true; break; }
+      }
+      if (lane == 0) {
+        R.huf_off = huf;
+        R.lit_buf = lit_buf;
+        R.tab_mode = tab_mode;
+        if (nseq) {
+          R.tab_off[0] = toff[0];
+          R.tab_off[1] = toff[1];
+          R.tab_off[2] = toff[2];
+        }
+        R.seq_buf = seq_buf;
+      }
+    }
+  }
+  if (!err && !serial && !any_frame) err = ZG_CORRUPT_STREAM;
+  __syncthreads();
+  // ---- (D) the records, one lane per block ----
+  if (!serial && !err) {
+    ZBlk *B = blks + (uint64_t)item * blk_cap;
+    for (uint32_t bi = lane; bi < nb; bi += 64) B[bi] = Q.R[bi];
+  }
+  if (lane == 0) {
+    nblk[item] = serial ? 0u : nbv;
     zmode[item] = serial ? ZMODE_SERIAL : (err ? ZMODE_SKIP : ZMODE_PARALLEL);
     if (err && !serial) status[item] = err;
     if (counters && (serial || !err)) atomicAdd(&counters[serial ? 0 : 1], 1ull);  // serial / block-parallel items
@@ -3751,6 +4082,9 @@ namespace xdense {
 #define ZG_XSEG_WIN 8
 #endif
 constexpr uint32_t XSEG_WIN = ZG_XSEG_WIN;  // executor segments per item (at most) for k_zstd_exec_win
+#ifndef ZG_XWIN_MAX_WPC
+#define ZG_XWIN_MAX_WPC 4
+#endif
 // executor grids of at least this many waves (items x segments) per CU take xdense
 #ifndef ZG_XDENSE_WPC
 #define ZG_XDENSE_WPC 64
@@ -3821,9 +4155,16 @@ static hipError_t launch_zstd_pass(ZgItem *items, uint32_t *status, uint32_t n_i
     const char *e = std::getenv("ZGPU_ZSTD_XSEG");
     return e ? (uint32_t)std::min<unsigned long>(64, std::max<unsigned long>(1, std::strtoul(e, nullptr, 10))) : 0u;
   }();
-  // executor: the windowed workgroup executor unless ZGPU_ZSTD_XWIN=0 (read per call: tests run both)
+  // executor: the windowed workgroup executor for batches the wave executor would leave mostly idle
+  // (fewer than ZG_XWIN_MAX_WPC of its waves per CU: lone frames, per-chunk calls, C5's L1 and small
+  // levels); the wave executor for batches that fill the GPU with waves (C5's L0 halves, blosc-zstd),
+  // where the window executor's whole-CU workgroups measured slower beside the other lanes' entropy
+  // kernels (C5 100 vs 91-94 ms with it everywhere, profiles/r06/r06h_*). ZGPU_ZSTD_XWIN=0/1 forces
+  // one (read per call: tests run both).
   const char *xw_s = std::getenv("ZGPU_ZSTD_XWIN");
-  const bool xwin_on = !xw_s || std::atoi(xw_s) != 0;
+  const int xw_env = xw_s ? std::atoi(xw_s) : -1;
+  const bool xwin_on = xw_env >= 0 ? xw_env != 0
+                                   : (uint64_t)n_items * XSEG < (uint64_t)device_cu_count() * ZG_XWIN_MAX_WPC;
   const uint32_t xseg = xseg_env ? xseg_env : xwin_on ? XSEG_WIN : XSEG;
 
   if (fork) {
