@@ -145,6 +145,11 @@ int main(int argc, char **argv) {
   CK(hipMalloc(&Z.mode, n * 4));
   CK(hipMalloc(&Z.lit, n * Z.lit_stride));
   CK(hipMalloc(&Z.seq, n * Z.seq_cap * 12));
+  if (getenv("LAB_EXEC") && !strcmp(getenv("LAB_EXEC"), "par")) {
+    CK(hipMalloc(&Z.ext, 2 * (uint64_t)n * chunk * 4));
+    CK(hipMalloc(&Z.ext_cnt, zgpu::ZEXT_ROUNDS * 8));
+    Z.ext_items = n;
+  }
 
   constexpr int NK = 7;
   const char *kn[NK] = {"scan", "blocks", "huf", "lits", "plan", "direct", "exec_item"};
@@ -222,7 +227,7 @@ int main(int argc, char **argv) {
     CK(hipEventRecord(ev[4]));
     // executor: LAB_EXEC=win (k_zstd_exec_win, the default), wide, dense; LAB_XSEG segments per item
     const char *lx = getenv("LAB_EXEC");
-    const int xk = !lx || !strcmp(lx, "win") ? 2 : !strcmp(lx, "dense") ? 1 : 0;
+    const int xk = !lx || !strcmp(lx, "win") ? 2 : !strcmp(lx, "par") ? 3 : !strcmp(lx, "dense") ? 1 : 0;
     const uint32_t xseg = getenv("LAB_XSEG") ? (uint32_t)atoi(getenv("LAB_XSEG")) : xk == 2 ? zgpu::XSEG_WIN : zgpu::XSEG;
     hipLaunchKernelGGL(zgpu::k_zstd_plan, dim3(n), dim3(64), 0, 0, d_items, d_status, blks, Z.blk_cap, Z.nblk, Z.mode,
                        chunk, xseg, (uint64_t *)nullptr, Z.lit, Z.lit_stride);
@@ -231,9 +236,28 @@ int main(int argc, char **argv) {
                        Z.mode, (uint32_t)n, d_out, chunk, Z.lit, Z.lit_stride, (const uint64_t *)nullptr,
                        (const unsigned long long *)nullptr, 0);
     CK(hipEventRecord(ev[6]));
-    if (xk == 2)
-      hipLaunchKernelGGL(zgpu::k_zstd_exec_win, dim3(n * xseg), dim3(zgpu::xwin::THREADS), 0, 0, d_items, d_status,
-                         blks, Z.blk_cap, Z.nblk, Z.mode, d_out, chunk, Z.lit, Z.lit_stride, Z.seq, Z.seq_cap, xseg);
+    if (xk == 3) {  // the latency mode, as launch_zstd_pass runs it
+      const uint64_t tot = (uint64_t)n * chunk;
+      CK(hipMemsetAsync(Z.ext, 0xFF, tot * 4, 0));
+      CK(hipMemsetAsync(Z.ext_cnt, 0, zgpu::ZEXT_ROUNDS * 8, 0));
+      hipLaunchKernelGGL(zgpu::k_zstd_exec_win<true>, dim3(ncu), dim3(zgpu::xwin::THREADS), 0, 0, d_items, d_status,
+                         blks, Z.blk_cap, Z.nblk, Z.mode, d_out, chunk, Z.lit, Z.lit_stride, Z.seq, Z.seq_cap,
+                         (uint32_t)n, Z.ext, (const unsigned long long *)nullptr);
+      uint32_t rounds = 2;
+      while (rounds < zgpu::ZEXT_ROUNDS && (1ull << (rounds - 2)) < chunk / 1024 + 1) rounds++;
+      const uint32_t g2 = (uint32_t)std::min<uint64_t>((tot / 4 + 255) / 256, (uint64_t)ncu * 16);
+      uint32_t *ea = Z.ext, *eb = Z.ext + tot;
+      for (uint32_t r = 0; r < rounds; r++) {
+        hipLaunchKernelGGL(zgpu::k_zstd_ext_round, dim3(g2), dim3(256), 0, 0, ea, eb, d_out, chunk, tot,
+                           r ? Z.ext_cnt + r - 1 : (const unsigned long long *)nullptr, Z.ext_cnt + r);
+        std::swap(ea, eb);
+      }
+      hipLaunchKernelGGL(zgpu::k_zstd_par_finish, dim3(n), dim3(64), 0, 0, d_items, d_status, blks, Z.blk_cap, Z.nblk,
+                         Z.mode, d_out, chunk);
+    } else if (xk == 2)
+      hipLaunchKernelGGL(zgpu::k_zstd_exec_win<false>, dim3(n * xseg), dim3(zgpu::xwin::THREADS), 0, 0, d_items,
+                         d_status, blks, Z.blk_cap, Z.nblk, Z.mode, d_out, chunk, Z.lit, Z.lit_stride, Z.seq, Z.seq_cap,
+                         xseg, (uint32_t *)nullptr, (const unsigned long long *)nullptr);
     else if (xk == 1)
       hipLaunchKernelGGL(zgpu::xdense::k_zstd_exec_item, dim3(n * xseg), dim3(64), 0, 0, d_items, d_status, blks,
                          Z.blk_cap, Z.nblk, Z.mode, d_out, chunk, Z.lit, Z.lit_stride, Z.seq, Z.seq_cap, xseg);
@@ -331,6 +355,13 @@ int main(int argc, char **argv) {
            z[5] / reps, z[4] / reps, z[0] / nb, z[1] / nb, z[1] / (double)(z[2] ? z[2] : 1));
   }
 #endif
+  if (Z.ext_cnt) {
+    unsigned long long c[zgpu::ZEXT_ROUNDS];
+    CK(hipMemcpy(c, Z.ext_cnt, sizeof(c), hipMemcpyDeviceToHost));
+    printf("ext references left after each round:");
+    for (uint32_t r = 0; r < 16; r++) printf(" %llu", c[r]);
+    printf("\n");
+  }
   printf("total %.3f ms -> %.2f GB/s decoded\n", tot, (double)n * chunk / tot / 1e6);
   return bad ? 1 : 0;
 }

@@ -132,8 +132,16 @@ struct ZstdScratch {
   // the batch's largest block count per item (nullable; zeroed before the call, k_zstd_scan's
   // atomicMax): the record-strided kernels walk n_items x that many records, not x blk_cap
   unsigned long long *max_nblk = nullptr;
+  // Latency mode of the window executor (nullable: off): two ext arrays of ext_items * slot u32 each
+  // (the external references of k_zstd_exec_win<true>) and ZEXT_ROUNDS round counters
+  uint32_t *ext = nullptr;
+  unsigned long long *ext_cnt = nullptr;
+  uint64_t ext_items = 0;
 };
 constexpr uint32_t ZALIAS = 2;
+// latency mode: batches of at most this many decoded bytes (n_items x slot) get the ext arrays
+constexpr uint64_t ZPAR_MAX_BYTES = 128ull << 20;
+constexpr uint32_t ZEXT_ROUNDS = 24;
 constexpr uint64_t ZALIAS_RLE = 1ull << 63;
 uint64_t zstd_lit_rec_bytes(uint32_t &wgs);
 void zstd_scratch_layout(uint64_t slot_bytes, uint32_t &blk_cap, uint64_t &blk_bytes, uint64_t &lit_stride,

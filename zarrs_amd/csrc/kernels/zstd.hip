@@ -4228,9 +4228,35 @@ static hipError_t launch_zstd_pass(ZgItem *items, uint32_t *status, uint32_t n_i
   const int xd_env = xd_s ? std::atoi(xd_s) : -1;
   const bool dense = xd_env >= 0 ? xd_env != 0
                                  : (uint64_t)n_items * xseg >= (uint64_t)device_cu_count() * XDENSE_WAVES_PER_CU;
-  if (xwin_on)
-    hipLaunchKernelGGL(k_zstd_exec_win, dim3(n_items * xseg), dim3(xwin::THREADS), 0, s, items, status, blks,
-                       Z.blk_cap, Z.nblk, Z.mode, dst, slot_bytes, Z.lit, Z.lit_stride, Z.seq, Z.seq_cap, xseg);
+  // latency mode (ZGPU_ZSTD_XPAR=0 off; read per call): batches the plan gave ext arrays
+  const char *xp_s = std::getenv("ZGPU_ZSTD_XPAR");
+  const bool par = xwin_on && Z.ext && Z.ext_cnt && n_items <= Z.ext_items && (!xp_s || std::atoi(xp_s) != 0);
+  if (par) {
+    const uint64_t tot = (uint64_t)n_items * slot_bytes;
+    hipError_t e = hipMemsetAsync(Z.ext, 0xFF, tot * 4, s);
+    if (e == hipSuccess) e = hipMemsetAsync(Z.ext_cnt, 0, ZEXT_ROUNDS * 8, s);
+    if (e != hipSuccess) return e;
+    hipLaunchKernelGGL(k_zstd_exec_win<true>, dim3(device_cu_count()), dim3(xwin::THREADS), 0, s, items, status,
+                       blks, Z.blk_cap, Z.nblk, Z.mode, dst, slot_bytes, Z.lit, Z.lit_stride, Z.seq, Z.seq_cap,
+                       n_items, Z.ext, Z.max_nblk);
+    // rounds: a reference hops back at least one window range (or one table's sub-window, >= 1 KiB on
+    // real data) per step, so log2 of the slot's KiB + 2 rounds; a round after the last reference
+    // returns at once
+    uint32_t rounds = 2;
+    while (rounds < ZEXT_ROUNDS && (1ull << (rounds - 2)) < slot_bytes / 1024 + 1) rounds++;
+    const uint32_t g2 = (uint32_t)std::min<uint64_t>((tot / 4 + 255) / 256, (uint64_t)device_cu_count() * 16);
+    uint32_t *ea = Z.ext, *eb = Z.ext + tot;
+    for (uint32_t r = 0; r < rounds; r++) {
+      hipLaunchKernelGGL(k_zstd_ext_round, dim3(g2), dim3(256), 0, s, ea, eb, dst, slot_bytes, tot,
+                         r ? Z.ext_cnt + r - 1 : (const unsigned long long *)nullptr, Z.ext_cnt + r);
+      std::swap(ea, eb);
+    }
+    hipLaunchKernelGGL(k_zstd_par_finish, dim3(n_items), dim3(64), 0, s, items, status, blks, Z.blk_cap, Z.nblk, Z.mode,
+                       dst, slot_bytes);
+  } else if (xwin_on)
+    hipLaunchKernelGGL(k_zstd_exec_win<false>, dim3(n_items * xseg), dim3(xwin::THREADS), 0, s, items, status, blks,
+                       Z.blk_cap, Z.nblk, Z.mode, dst, slot_bytes, Z.lit, Z.lit_stride, Z.seq, Z.seq_cap, xseg,
+                       (uint32_t *)nullptr, (const unsigned long long *)nullptr);
   else if (dense)
     hipLaunchKernelGGL(xdense::k_zstd_exec_item, dim3(n_items * xseg), dim3(64), 0, s, items, status, blks, Z.blk_cap,
                        Z.nblk, Z.mode, dst, slot_bytes, Z.lit, Z.lit_stride, Z.seq, Z.seq_cap, xseg);

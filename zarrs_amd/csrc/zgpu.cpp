@@ -438,7 +438,7 @@ struct zgpu_plan {
     void *bufs[] = {d_items, d_items_init, d_geom, d_shards, d_index, d_shard_status, d_mids, d_mids_init,
                     d_mid_status, d_shard_status2, d_mid_shards, d_index2, d_bl_need,
                     d_pool[0], d_pool[1], zs.blks, zs.nblk, zs.mode, zs.lit, zs.seq, d_ctl,
-                    d_enc_stage, d_zser, d_order, d_gz_seg, zs.lit_rec};
+                    d_enc_stage, d_zser, d_order, d_gz_seg, zs.lit_rec, zs.ext, zs.ext_cnt};
     for (void *b : bufs) ctx->dev_free(b);
     if (zside) {
       (void)hipStreamSynchronize(zside);
@@ -910,6 +910,11 @@ static void plan_upload(zgpu_plan &P, hipStream_t us) {
         P.d_zser = (uint32_t *)C.dev_alloc(ni * 4);
         P.zs.ser_list = P.d_zser;
         if (const uint64_t rb = zstd_lit_rec_bytes(P.zs.lit_rec_wgs)) P.zs.lit_rec = (uint8_t *)C.dev_alloc(rb);
+        if (ni * P.slot_bytes <= ZPAR_MAX_BYTES) {  // the window executor's latency mode (few frames)
+          P.zs.ext = (uint32_t *)C.dev_alloc(2 * ni * P.slot_bytes * 4);
+          P.zs.ext_cnt = (unsigned long long *)C.dev_alloc(ZEXT_ROUNDS * 8);
+          P.zs.ext_items = ni;
+        }
       }
     }
   }
