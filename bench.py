@@ -58,7 +58,20 @@ def _synth():
     L.synth_gzip_crc_shard.argtypes = [C.c_void_p, C.c_uint64, P64, P64, C.c_int, C.c_int,
                                        C.POINTER(C.c_void_p), P64]
     L.synth_free.argtypes = [C.c_void_p]
+    L.synth_unshuffle.argtypes = [C.c_void_p, C.c_void_p, C.c_uint64, C.c_uint64]
+    L.synth_unshuffle.restype = None
     return L
+
+
+def _emulated_rank(args, rank, world):
+    """--emulate-rank R/N (one process, one GPU): the step decodes rank R's share of an N-GPU run (C3:
+    its axis-0 slab, C5: its LPT chunk part) with the single-GPU code path -- for profiling a rank's
+    step (the rank_share legs time every rank this way from their own plans)."""
+    spec = getattr(args, "emulate_rank", "")
+    if not spec or world > 1:
+        return rank, world
+    r, n = (int(x) for x in spec.split("/"))
+    return r, n
 
 
 def _u64(v):
@@ -347,6 +360,11 @@ class C1:
 # ------------------------------------------------------------------------------------------------
 class C3:
     SHARD, INNER = 256, 32
+    # C4: rows per piece of a rank's slab (one plan each; a piece's send overlaps the next piece's
+    # decode). Inner-chunk rows (32) made each piece a latency-bound k_gzip launch of its own: a 96-row
+    # slab took 12.7-13.1 ms against 18.4 for the whole subset on one GPU (profiles/r06/r06m_*); the
+    # whole slab in one plan (1 << 30: one piece) decodes its ~2.3 k streams in one launch
+    C4_PIECE_ROWS = 1 << 30
     ARRAY = [2048, 2048, 2048]
     SUB_START, SUB_SHAPE = [200, 300, 1000], [768, 768, 768]
     CODECS = [{"name": "sharding_indexed", "configuration": {
@@ -367,8 +385,9 @@ class C3:
         from zarrs_amd.distributed import slab_partition
         S = self.SHARD
         # this rank's axis-0 slab of the subset (array coordinates)
-        self.slabs = slab_partition(self.SUB_START, self.SUB_SHAPE, world)
-        self.start, self.shape = self.slabs[rank]
+        er, ew = _emulated_rank(args, rank, world)
+        self.slabs = slab_partition(self.SUB_START, self.SUB_SHAPE, ew)
+        self.start, self.shape = self.slabs[er]
         syn = _synth()
         self.chain = CodecChain.from_metadata(self.CODECS, "float32", 0.0, args.ctx)
         lo = [s // S for s in self.start]
@@ -420,7 +439,7 @@ class C3:
             # C4: the slab is decoded in pieces of whole inner-chunk rows (32 array rows), one plan each,
             # and every piece is sent to the root while the next one decodes (gather_slabs_overlapped)
             from zarrs_amd.distributed import slab_pieces
-            self.pieces = slab_pieces(self.start, self.shape, self.INNER)
+            self.pieces = slab_pieces(self.start, self.shape, self.C4_PIECE_ROWS)
             self.parts = []
             for r0, n in self.pieces:
                 p0 = [self.start[0] + r0] + self.start[1:]
@@ -437,6 +456,8 @@ class C3:
                                         out_start=[a - b for a, b in zip(s0, p0)]))
                 self.parts.append((self.chain, pd, self.out.narrow(0, r0, n), [n] + self.shape[1:]))
         self.step_bytes = int(np.prod(self.SUB_SHAPE)) * 4  # the whole subset, all ranks
+        if getattr(args, "emulate_rank", ""):
+            self.step_bytes = self.decoded_bytes
         self.gathered = None
         self.config = {"workload": "C3" + ("/C4" if world > 1 else "") +
                                    ": sharded [2048]^3 f32, 256^3 shards / 32^3 inner chunks, "
@@ -451,6 +472,58 @@ class C3:
                      "written by tools/synth; decode(encode(x)) == x checked on device)")
         self.scaling = "strong"
 
+    def rank_share(self, n1_ms):
+        """SURVEY §8(e) C4 at N = 8, predicted on this GPU: rank r's axis-0 slab of the subset
+        (slab_partition, as --gpus 8 cuts it) decoded alone as the N = 8 step decodes it (C4_PIECE_ROWS
+        pieces, one plan each, statuses read after each), for every r; a piece's send overlaps the next
+        piece's decode, so the exposed exchange is the last piece over one xGMI link. The other piece
+        size is measured beside it (`alt`: 32-row pieces, i.e. inner-chunk rows, or the whole slab)."""
+        from zarrs_amd import make_desc
+        from zarrs_amd.distributed import slab_partition, slab_pieces
+        N, S = RANK_SHARE_N, self.SHARD
+        slabs = slab_partition(self.SUB_START, self.SUB_SHAPE, N)
+
+        def measure(piece_rows):
+            rank_ms, last_piece = [], 0
+            for r in range(N):
+                start, shape = slabs[r]
+                buf = torch.empty(shape, dtype=torch.float32, device=self.dev)
+                groups = []
+                for r0, n in slab_pieces(start, shape, piece_rows):
+                    p0 = [start[0] + r0] + list(start[1:])
+                    pd = []
+                    for (si, sj, sk), (t, _) in self.shards.items():
+                        org = [si * S, sj * S, sk * S]
+                        s0 = [max(a, o) for a, o in zip(p0, org)]
+                        s1 = [min(a + b, o + S) for a, b, o in zip(p0, [n] + list(shape[1:]), org)]
+                        if any(b <= a for a, b in zip(s0, s1)):
+                            continue
+                        pd.append(make_desc((t.data_ptr(), int(t.numel())), [S] * 3,
+                                            sel_start=[a - o for a, o in zip(s0, org)],
+                                            sel_shape=[b - a for a, b in zip(s0, s1)],
+                                            out_start=[a - b for a, b in zip(s0, p0)]))
+                    groups.append((self.chain, pd, buf.narrow(0, r0, n), [n] + list(shape[1:])))
+                    last_piece = max(last_piece, int(np.prod([n] + list(shape[1:]))) * 4)
+                rank_ms.append(_time_plan_groups(self.args.ctx, groups, [list(range(len(groups)))], set(),
+                                                 self.dev, status_each=True))
+                del buf
+            return rank_ms, last_piece / (XGMI_LINK_GBS * 1e9) * 1e3
+
+        gb = int(np.prod(self.SUB_SHAPE)) * 4 * (N - 1) // N
+        rank_ms, gms = measure(self.C4_PIECE_ROWS)
+        rep = rank_share_report(rank_ms, n1_ms, self.step_bytes, gb, gms,
+                                f"each rank's axis-0 slab decoded alone on this GPU in the N = 8 step's "
+                                f"pieces ({self.C4_PIECE_ROWS if self.C4_PIECE_ROWS < 1 << 20 else 'whole slab'} "
+                                "rows, one plan each; 5 reps, median); a piece's send overlaps the next piece's "
+                                f"decode, so the last piece's send is exposed (at {XGMI_LINK_GBS:.0f} GB/s); "
+                                "the slowest rank sets the step")
+        alt_rows = self.INNER if self.C4_PIECE_ROWS != self.INNER else 1 << 30
+        alt_ms, alt_g = measure(alt_rows)
+        rep["alt"] = {"piece_rows": alt_rows if alt_rows < 1 << 20 else "whole slab",
+                      "max_rank_ms": round(max(alt_ms), 3), "gather_ms_model": round(alt_g, 3),
+                      "predicted_speedup_vs_n1": round(n1_ms / (max(alt_ms) + alt_g), 3)}
+        return rep
+
     def run_step(self, execute):
         """C4 (N > 1): decode the slab piece by piece (execute(k) runs piece k's plan on the bench stream,
         statuses read back) while the finished pieces travel to the root (RCCL isend / irecv straight into
@@ -464,7 +537,8 @@ class C3:
             execute(k)
             if k == len(self.parts) - 1:
                 done.append(time.perf_counter())
-        self.gathered = gather_slabs_overlapped(decode_piece, self.out, self.slabs, self.INNER, dst=0, out=self.full)
+        self.gathered = gather_slabs_overlapped(decode_piece, self.out, self.slabs, self.C4_PIECE_ROWS, dst=0,
+                                                out=self.full)
         torch.cuda.synchronize()
         if done:
             self.gather_s.append(time.perf_counter() - done[0])
@@ -816,7 +890,8 @@ class C5:
         dev, rank, world, sc = self.dev, self.rank, self.world, self.args.c5_scale
         n = len(chunk_meta)
         self.level_shapes, self.chunk_meta, self.enc_sizes = level_shapes, chunk_meta, enc_sizes
-        mine = lpt_partition(enc_sizes, world)[rank]
+        er, ew = _emulated_rank(self.args, rank, world)
+        mine = lpt_partition(enc_sizes, ew)[er]
         self.outs = [torch.zeros(s, dtype=torch.int16, device=dev) for s in level_shapes]
         self.expected = None if levels is None else [torch.from_numpy(a.view(np.int16)).to(dev) for a in levels]
         self.masks = [torch.zeros(s, dtype=torch.bool, device=dev) for s in level_shapes]
@@ -857,7 +932,7 @@ class C5:
         # latency-bound sequence decoding: C5 88.2-88.5 -> 83.2 ms (profiles/r05/r05lf_zstd_lits_first_ab.txt)
         self.lits_first_parts = [p for p, l in enumerate(lane_of) if l in (0, 3)]
         self.decoded_bytes = dec_total
-        self.step_bytes = all_bytes
+        self.step_bytes = dec_total if getattr(self.args, "emulate_rank", "") else all_bytes
         self.ratio = raw_bytes / max(1, sum(enc_sizes))
         self.config = {"workload": f"C5: OME-Zarr-style u16 pyramid, 5 levels, L0 {shape0} (y/x scaled 1/{sc}), "
                                    "chunks [32,512,512] [64,256,256] [64,128,128] [64,64,64] [32,64,64], "
@@ -886,6 +961,49 @@ class C5:
                 self.g_boxes[owner[lin0[idx]]].append((b0, bs))
             self.config["gather"] = {"l0_subset_start": self.g_start, "l0_subset_shape": self.g_shape,
                                      "bytes": int(np.prod(self.g_shape)) * 2}
+
+    def rank_share(self, n1_ms):
+        """SURVEY §8(e) C5 at N = 8, predicted on this GPU: rank r's LPT share of the pyramid
+        (lpt_partition over encoded sizes, as --gpus 8 assigns it) decoded alone with the N = 8 run's
+        plan and lane layout (its L0 chunks in two halves, L1, the small levels; literals-first parts),
+        for every r; the L0 subset gather priced at the root's 7 direct xGMI links."""
+        from zarrs_amd import make_desc
+        from zarrs_amd.distributed import lpt_partition
+        N = RANK_SHARE_N
+        parts = lpt_partition(self.enc_sizes, N)
+        if len(self.enc_bufs) != len(self.chunk_meta):
+            raise RuntimeError("rank share needs every chunk resident (N = 1)")
+        rank_ms = []
+        for r in range(N):
+            per_level = [[] for _ in self.level_shapes]
+            for i in sorted(parts[r]):
+                li, idx = self.chunk_meta[i]
+                cs, shp = self.CHUNKS[li], self.level_shapes[li]
+                start = [k * c for k, c in zip(idx, cs)]
+                sel = [min(c, s_ - st) for c, s_, st in zip(cs, shp, start)]
+                per_level[li].append(make_desc((self.enc_bufs[i].data_ptr(), self.enc_sizes[i]), cs, [0, 0, 0],
+                                               sel, start))
+            l0 = per_level[0]
+            halves = lpt_partition([int(d.enc_len) for d in l0], 2)
+            groups_d = [[l0[i] for i in hv] for hv in halves] + per_level[1:]
+            outs_g = [self.outs[0], self.outs[0]] + self.outs[1:]
+            groups, lane_of = [], []
+            for gi, (d, o) in enumerate(zip(groups_d, outs_g)):
+                if d:
+                    groups.append((self.chain, d, o, list(o.shape)))
+                    lane_of.append(min(gi, 3))
+            lanes = [[g for g, l in enumerate(lane_of) if l == k] for k in range(4)]
+            lanes = [ln for ln in lanes if ln]
+            lf = {g for g, l in enumerate(lane_of) if l in (0, 3)}
+            rank_ms.append(_time_plan_groups(self.args.ctx, groups, lanes, lf, self.dev))
+        s0 = self.level_shapes[0]
+        g_shape = [min(64, s0[0]), s0[1] // 2, s0[2] // 2]
+        gb = int(np.prod(g_shape)) * 2 * (N - 1) // N
+        gms = gb / ((N - 1) * XGMI_LINK_GBS * 1e9) * 1e3
+        return rank_share_report(rank_ms, n1_ms, self.step_bytes, gb, gms,
+                                 "each rank's LPT chunk share decoded alone on this GPU (its plans on the N = 8 "
+                                 "lane layout, 5 reps, median); the L0 subset gather (7/8 of it to rank 0) at "
+                                 f"7 x {XGMI_LINK_GBS:.0f} GB/s; the slowest rank sets the step")
 
     def after_decode(self):
         if self.world > 1:
@@ -980,6 +1098,7 @@ class C5:
         from zarrs_amd import _lib as L
         from zarrs_amd import CodecChain, make_desc
         lib = L.load()
+        syn = _synth()
         zs_meta = self.CODECS[2]
         chain = CodecChain.from_metadata([self.CODECS[0], zs_meta], "uint8", 0, self.args.ctx)
         outs = [np.empty(s_, np.uint16) for s_ in self.level_shapes]
@@ -1006,10 +1125,9 @@ class C5:
             finally:
                 lib.zgpu_result_release(res_h)
             # ShuffleCodec::decode (elementsize 2): dec[j*2 + i] = enc[i*count + j], into a new buffer
-            count = nb // 2
-            dec = np.empty((count, 2), np.uint8)
-            dec[:, 0] = zs[:count]
-            dec[:, 1] = zs[count:]
+            # (zarrs' loop compiled natively: tools/synth synth_unshuffle; ctypes drops the GIL)
+            dec = np.empty(nb, np.uint8)
+            syn.synth_unshuffle(zs.ctypes.data, dec.ctypes.data, nb, 2)
             # BytesCodec decode_into the array's view (little endian: the bytes as they are)
             outs[li][dst] = dec.view(np.uint16).reshape(cs)[src_sel]
 
@@ -1026,14 +1144,30 @@ class C5:
             st1 = self.args.ctx.coalescing_stats()
         t = float(np.median(times))
         nb_ = st1["batches"] - st0["batches"]
+        # one call alone (the latency a lone rayon worker sees): an L0 chunk's frame from host memory,
+        # decoded into pinned memory, median of 10 (the plugin's zgpu_decode_pinned, no copies after it)
+        lone = []
+        d0, nb0 = calls[0][0], calls[0][1]
+        for _ in range(11):
+            st = (C.c_int32 * 1)()
+            data, res_h = C.c_void_p(), C.c_void_p()
+            t0 = time.perf_counter()
+            rc = lib.zgpu_decode_pinned(chain._h, 1, d0, 1, L.u64s([nb0]), L.COALESCE, st, C.byref(data),
+                                        C.byref(res_h))
+            lone.append(time.perf_counter() - t0)
+            if rc:
+                raise L.ZgpuError(rc, L.last_error())
+            lib.zgpu_result_release(res_h)
         return {"GiBps": round(self.step_bytes / t / 2 ** 30, 2), "ms": round(t * 1e3, 1), "roundtrip_ok": ok,
+                "lone_frame_call_ms": round(float(np.median(lone[1:])) * 1e3, 3), "lone_frame_bytes": nb0,
                 "threads": threads, "calls": len(calls), "batches_per_pass": round(nb_ / len(times), 1),
                 "calls_per_batch": round((st1["calls"] - st0["calls"]) / max(1, nb_), 2),
                 "hip_env_GPU_MAX_HW_QUEUES": os.environ.get("GPU_MAX_HW_QUEUES", "unset (HIP default: 4)"),
                 "note": "per-chunk CodecChain::decode_into with the per-codec GPU plugins (zstd on the GPU through "
-                        "a coalesced zgpu_decode_pinned + one copy into a Vec; shuffle and bytes on the CPU, numpy "
-                        "standing in for zarrs' loops), one call per chunk from a thread pool; compare with the "
-                        "leg's cpu_baseline (the whole chain on the CPU)"}
+                        "a coalesced zgpu_decode_pinned + one copy into a Vec; shuffle on the CPU by zarrs' loop "
+                        "compiled in C (tools/synth synth_unshuffle), bytes as a numpy copy into the array), one call "
+                        "per chunk from a thread pool; compare with the leg's cpu_baseline (the whole chain on the "
+                        "CPU)"}
 
     def encode_leg(self):
         """Write path (SURVEY 8(f) rank 3): CodecChain::encode of level 0's whole chunks ([32,512,512]
@@ -1267,6 +1401,80 @@ def _time_reps(fn, seconds):
         fn()
         times.append(time.perf_counter() - t0)
     return times
+
+
+RANK_SHARE_N = 8
+
+
+def _time_plan_groups(ctx, groups, lanes, lits_first, dev, reps=5, status_each=False):
+    """Median wall ms of one decode of `groups` ((chain, descs, out tensor, out_shape) per plan) laid out
+    as a step is: `lanes` lists of group indices, each lane's plans in order on a stream of its own, the
+    lanes concurrent (ZGPU_ONE_STREAM; ZGPU_ZSTD_LITS_FIRST for the groups in `lits_first`). Statuses
+    are read back once after the timing and must be 0 (status_each: every plan's statuses read back
+    after it, as C4's piece-wise decode does)."""
+    from zarrs_amd import _lib as L
+    lib = L.load()
+    plans = []
+    multi = len(lanes) > 1
+    for gi, (chain, descs, out, out_shape) in enumerate(groups):
+        n = len(descs)
+        arr = (L.ChunkDesc * n)(*descs)
+        plan = C.c_void_p()
+        flags = L.ENC_DEVICE | L.OUT_DEVICE | (L.ONE_STREAM if multi else 0) | \
+            (L.ZSTD_LITS_FIRST if multi and gi in lits_first else 0)
+        L.check(lib.zgpu_plan_create(chain._h, len(out_shape), arr, n, L.u64s(out_shape), flags, C.byref(plan)))
+        plans.append((plan, out, (C.c_int32 * n)()))
+    streams = [torch.cuda.Stream(dev) for _ in lanes]
+    sps = [C.c_void_p(st.cuda_stream) for st in streams]
+
+    def once():
+        main = torch.cuda.current_stream(dev)
+        ev = torch.cuda.Event()
+        ev.record(main)
+        for li, ln in enumerate(lanes):
+            streams[li].wait_event(ev)
+            for gi in ln:
+                plan, out, st = plans[gi]
+                rc = lib.zgpu_plan_execute(plan, out.data_ptr(), st if status_each else None, sps[li])
+                if rc:
+                    raise RuntimeError(f"decode failed: {L.STATUS_NAMES[rc]} {L.last_error()}")
+        for st in streams:
+            done = torch.cuda.Event()
+            done.record(st)
+            main.wait_event(done)
+        torch.cuda.synchronize(dev)
+    try:
+        once()
+        once()
+        ts = []
+        for _ in range(reps):
+            t0 = time.perf_counter()
+            once()
+            ts.append(time.perf_counter() - t0)
+        for li, ln in enumerate(lanes):
+            for gi in ln:
+                plan, _, st = plans[gi]
+                rc = lib.zgpu_plan_status(plan, st, sps[li])
+                if rc or any(st[k] for k in range(len(st))):
+                    raise RuntimeError(f"rank share decode failed: {L.STATUS_NAMES[rc]}")
+        return float(np.median(ts)) * 1e3
+    finally:
+        for plan, _, _ in plans:
+            lib.zgpu_plan_destroy(plan)
+
+
+def rank_share_report(rank_ms, n1_ms, step_bytes, gather_bytes, gather_ms, note):
+    """The N = RANK_SHARE_N prediction from one GPU: each rank's share of the step decoded alone (the
+    same kernels, plans and lane layout as that rank runs), the exchange priced at the root's direct xGMI
+    links, aggregate = the step's bytes over the slowest rank's time."""
+    worst = max(rank_ms)
+    t = worst + gather_ms
+    return {"ranks": RANK_SHARE_N, "rank_ms": [round(x, 3) for x in rank_ms], "max_rank_ms": round(worst, 3),
+            "rank_of_max": int(np.argmax(rank_ms)), "gather_bytes_to_root": gather_bytes,
+            "gather_ms_model": round(gather_ms, 3), "n1_ms": round(n1_ms, 3),
+            "predicted_step_ms": round(t, 3), "predicted_speedup_vs_n1": round(n1_ms / t, 3),
+            "predicted_value_GiBps": round(step_bytes / (t * 1e-3) / 2 ** 30, 2),
+            "status": "predicted, unmeasured on 8 GPUs", "note": note}
 
 
 # ------------------------------------------------------------------------------------------------
@@ -1520,6 +1728,11 @@ def secondary_legs(args, rank, world, dev, r_primary):
                 leg["dropin_emulation"] = W.dropin_leg()
             except Exception as e:  # noqa: BLE001
                 leg["dropin_emulation"] = {"error": repr(e)[:300]}
+        if name in ("c3", "c5") and rank == 0 and world == 1 and args.rank_share:
+            try:  # one rank's share at N = 8 on this GPU (C4: the slabs; C5: the LPT parts)
+                leg["c4_rank_share" if name == "c3" else "c5_rank_share"] = W.rank_share(t / a.steps * 1e3)
+            except Exception as e:  # noqa: BLE001
+                leg["rank_share"] = {"error": repr(e)[:300]}
         pmc = rank == 0 and world == 1 and not args.no_pmc
         cache = None
         if pmc and hasattr(W, "save_cache"):
@@ -1679,6 +1892,10 @@ def main():
     ap.add_argument("--fork", action="store_true", help=argparse.SUPPRESS)  # A/B: concurrent plans keep their side streams
     ap.add_argument("--serial-lanes", action="store_true",
                     help="run every plan on one stream (profiling: per-kernel durations without overlap)")
+    ap.add_argument("--emulate-rank", default="", help="R/N: decode rank R's share of an N-GPU C3/C5 run "
+                    "on this one GPU (profiling; the line then covers that share only)")
+    ap.add_argument("--no-rank-share", dest="rank_share", action="store_false",
+                    help="skip the C3/C5 legs' predicted N = 8 rank shares (SURVEY 8(e))")
     ap.add_argument("--no-host-leg", dest="host_leg", action="store_false",
                     help="skip the PCIe-inclusive (host input/output) leg")
     ap.add_argument("--child", action="store_true", help=argparse.SUPPRESS)
@@ -1727,6 +1944,12 @@ def main():
     value = W.step_bytes * args.steps / t / 2 ** 30
     gather = gather_report(r, world, dev)
     cpu = W.cpu_baseline() if (rank == 0 and not args.no_cpu) else None
+    share = None
+    if args.workload in ("c3", "c5") and world == 1 and args.rank_share and not args.emulate_rank:
+        try:  # one rank's share at N = 8 on this GPU
+            share = W.rank_share(t / args.steps * 1e3)
+        except Exception as e:  # noqa: BLE001
+            share = {"error": repr(e)[:300]}
     traffic, traffic_note = None, "skipped (--no-pmc or N>1)"
     if rank == 0 and world == 1 and not args.no_pmc:
         # the profiled child needs the HBM this process holds (C5: ~30 GB of frames, outputs and
@@ -1766,6 +1989,8 @@ def main():
                                            "serial_fallback": r["counters"][L_CTR_ZSTD_SERIAL]}
         if gather:
             line["gather"] = gather
+        if share:
+            line["c4_rank_share" if args.workload == "c3" else "c5_rank_share"] = share
     sec = secondary_legs(args, rank, world, dev, r) if args.secondary and not args.child else None
     if rank == 0:
         if sec:

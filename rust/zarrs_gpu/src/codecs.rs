@@ -10,10 +10,11 @@
 //! the decoded bytes copied once out of pinned memory), coalesced with the calls other rayon workers
 //! make at the same time (ZGPU_COALESCE: one H2D, one launch sequence, one D2H per batch). A
 //! per-codec plugin cannot fuse a chain's stages: every GPU stage is a PCIe round trip, so by default
-//! only the entropy stages (gzip, zstd, blosc: GPU_ENTROPY_CODEC_NAMES) are registered and zarrs'
-//! own bytes / transpose / crc32c / shuffle run on the host around them (bench.py's
-//! `secondary.c5.dropin_emulation` measures that split on C5). The batched paths (the
-//! `sharding_indexed` plugin, ArrayGpuExt) remain the fast ones.
+//! only the entropy stages gzip and blosc (GPU_ENTROPY_CODEC_NAMES) are registered and zarrs' own
+//! bytes / transpose / crc32c / shuffle run on the host around them; per-chunk zstd is opt-in
+//! (GPU_ZSTD_CODEC_NAMES: bench.py's `secondary.c5.dropin_emulation` measures that split on C5 and
+//! finds the host side alone as slow as zarrs' CPU zstd). The batched paths (the `sharding_indexed`
+//! plugin, ArrayGpuExt) remain the fast ones.
 
 use std::borrow::Cow;
 use std::num::NonZeroU64;
@@ -41,13 +42,24 @@ use crate::Chain;
 pub const GPU_CODEC_NAMES: [&str; 8] =
     ["bytes", "transpose", "crc32c", "gzip", "zstd", "blosc", "numcodecs.shuffle", "shuffle"];
 
-/// The codecs [`crate::register_codecs`] sends to the GPU by default: the entropy stages, whose
-/// decode is worth a PCIe round trip per chunk (an inflate or zstd decode runs ~1 GB/s per host
-/// core; the GPU's batched decode is two orders faster and a coalesced call moves only the
-/// compressed bytes in and the decoded bytes out). `bytes`, `transpose`, `crc32c` and
-/// `numcodecs.shuffle` run near memory speed on the host, where a hop to the GPU and back costs more
-/// than the stage: they stay zarrs' own unless [`crate::register_codecs_all`] asks for them.
-pub const GPU_ENTROPY_CODEC_NAMES: [&str; 3] = ["gzip", "zstd", "blosc"];
+/// The codecs [`crate::register_codecs`] sends to the GPU by default: the entropy stages whose
+/// per-chunk decode is worth a PCIe round trip (an inflate runs ~0.3 GB/s per host core; the GPU's
+/// coalesced call moves only the compressed bytes in and the decoded bytes out). `bytes`,
+/// `transpose`, `crc32c` and `numcodecs.shuffle` run near memory speed on the host, where a hop to
+/// the GPU and back costs more than the stage: they stay zarrs' own unless
+/// [`crate::register_codecs_all`] asks for them.
+///
+/// `zstd` is not among them: a lone 16 MiB C5 frame decodes in 3.3 ms through the plugin's call
+/// (the window executor's latency mode), but zarrs' per-codec chain then copies the result out of
+/// pinned memory, unshuffles and places it on the host, and that host work alone is about the CPU
+/// codec's whole per-chunk cost (libzstd ~1.5 GB/s per core): C5 read per chunk through the plugin
+/// runs at 10.1 GiB/s against 28.7 on 16 host threads (bench.py `secondary.c5.dropin_emulation`,
+/// profiles/r06/). Opt in with [`GPU_ZSTD_CODEC_NAMES`] and [`crate::register_codecs_named`]; the
+/// batched paths (ArrayGpuExt: 216 GiB/s from HBM on C5) are the ones for zstd arrays.
+pub const GPU_ENTROPY_CODEC_NAMES: [&str; 2] = ["gzip", "blosc"];
+
+/// The per-chunk zstd plugin (opt-in, see [`GPU_ENTROPY_CODEC_NAMES`]).
+pub const GPU_ZSTD_CODEC_NAMES: [&str; 1] = ["zstd"];
 
 /// The runtime-plugin create function of the per-codec plugins: zarrs' own codec is created from the
 /// metadata (never through the registry, which would find this plugin again) and wrapped.

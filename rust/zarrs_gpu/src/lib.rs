@@ -3,10 +3,11 @@
 //!
 //! Three entry points, all over the C ABI:
 //!
-//! * [`register_codecs`] adds per-codec runtime plugins for the entropy stages `gzip`, `zstd` and
-//!   `blosc` (codecs.rs): zarrs' unchanged per-chunk CodecChain then decodes them on the GPU (one
-//!   coalesced zgpu_decode_pinned per chunk) and runs its own `bytes` / `transpose` / `crc32c` /
-//!   `numcodecs.shuffle` on the host ([`register_codecs_all`] puts every stage on the GPU).
+//! * [`register_codecs`] adds per-codec runtime plugins for the entropy stages `gzip` and `blosc`
+//!   (codecs.rs): zarrs' unchanged per-chunk CodecChain then decodes them on the GPU (one coalesced
+//!   zgpu_decode_pinned per chunk) and runs its own `bytes` / `transpose` / `crc32c` /
+//!   `numcodecs.shuffle` / `zstd` on the host ([`register_codecs_named`] opts zstd in,
+//!   [`register_codecs_all`] puts every stage on the GPU).
 //! * [`register`] adds a runtime codec plugin for `sharding_indexed`
 //!   (`zarrs_codec::register_codec_v3`, zarrs_codec/src/lib.rs:279-318; runtime plugins are matched
 //!   before the compile-time ones, lib.rs:385-414). A shard is the natural GPU batch: its
@@ -56,12 +57,20 @@ pub fn unregister(handle: &zarrs_codec::CodecRuntimeRegistryHandleV3) -> bool {
     zarrs_codec::unregister_codec_v3(handle)
 }
 
-/// Register the per-codec GPU plugins of the entropy stages (`gzip`, `zstd`, `blosc`:
-/// [`codecs::GPU_ENTROPY_CODEC_NAMES`]): one runtime plugin matching their names,
-/// zarrs_codec/src/lib.rs:279-318. zarrs' own codecs keep the near-memory-speed stages.
+/// Register the per-codec GPU plugins of the entropy stages worth a per-chunk PCIe round trip
+/// (`gzip`, `blosc`: [`codecs::GPU_ENTROPY_CODEC_NAMES`]): one runtime plugin matching their names,
+/// zarrs_codec/src/lib.rs:279-318. zarrs' own codecs keep the near-memory-speed stages, and zstd
+/// (see [`codecs::GPU_ENTROPY_CODEC_NAMES`] for the measurement; opt in with
+/// [`register_codecs_named`]).
 pub fn register_codecs() -> zarrs_codec::CodecRuntimeRegistryHandleV3 {
+    register_codecs_named(&codecs::GPU_ENTROPY_CODEC_NAMES)
+}
+
+/// Register the per-codec GPU plugins of the codecs `names` (a subset of
+/// [`codecs::GPU_CODEC_NAMES`]), e.g. `&["gzip", "blosc", "zstd"]`.
+pub fn register_codecs_named(names: &'static [&'static str]) -> zarrs_codec::CodecRuntimeRegistryHandleV3 {
     zarrs_codec::register_codec_v3(zarrs_codec::CodecRuntimePluginV3::new(
-        |name| codecs::GPU_ENTROPY_CODEC_NAMES.contains(&name),
+        move |name| names.contains(&name) && codecs::GPU_CODEC_NAMES.contains(&name),
         codecs::create,
     ))
 }

@@ -4,8 +4,9 @@
 # Steps run in order, each under its own time limit; the session stops at the first failure.
 #   test[:EXPR]          pytest -m gpu (-k EXPR when given)
 #   smoke                __graft_entry__.smoke()
-#   bench:W[:FLAGS]      bench.py --workload W, the full line (CPU baseline, PMC passes, host leg);
-#                        FLAGS: extra bench flags, comma-separated (e.g. bench:c5:--c5-scale,2)
+#   bench:W[:FLAGS[:ENV]] bench.py --workload W, the full line (CPU baseline, PMC passes, host leg);
+#                        FLAGS: extra bench flags, comma-separated (e.g. bench:c5:--c5-scale,2); ENV:
+#                        NAME=VALUE settings, comma-separated
 #   quick:W[:FLAGS]      bench.py --workload W without PMC passes / host leg, short CPU baseline
 #   prof:W[:FLAGS]       rocprofv3 --kernel-trace --stats of bench.py --workload W (5 steps)
 #   serial:W[:FLAGS]     the same with every plan on one stream (--serial-lanes: per-kernel split)
@@ -37,8 +38,8 @@ for step in "$@"; do
         || { rc=$?; echo "smoke rc=$rc"; tail -20 "$O/$i.smoke.log"; exit $rc; }
       tail -1 "$O/$i.smoke.log" ;;
     bench|quick)
-      F=(${b//,/ }); [ "$kind" = quick ] && F+=(--no-pmc --no-host-leg --cpu-seconds 5 --secondary=)
-      timeout -k 10 900 python -u bench.py --workload "$a" "${F[@]}" > "$O/$i.bench_$a.json" 2> "$O/$i.bench_$a.err" \
+      F=(${b//,/ }); E=(${c//,/ }); [ "$kind" = quick ] && F+=(--no-pmc --no-host-leg --cpu-seconds 5 --secondary=)
+      env "${E[@]}" timeout -k 10 900 python -u bench.py --workload "$a" "${F[@]}" > "$O/$i.bench_$a.json" 2> "$O/$i.bench_$a.err" \
         || { rc=$?; echo "bench rc=$rc"; tail -20 "$O/$i.bench_$a.err"; exit $rc; }
       cat "$O/$i.bench_$a.json" ;;
     prof|serial)

@@ -338,3 +338,20 @@ void synth_c5_level0(uint64_t nz, uint64_t ny, uint64_t nx, int nblobs, const fl
   }
   for (int t = 0; t < nthreads; t++) pthread_join(th[t], NULL);
 }
+
+// The drop-in emulation's stand-in for zarrs' CPU shuffle codec (bench.py C5 dropin_leg): the loop of
+// zarrs/src/array/codec/bytes_to_bytes/shuffle/shuffle_codec.rs:109-129 compiled natively, as zarrs'
+// Rust loop is (numpy's strided column copies are several times slower than either).
+void synth_unshuffle(const uint8_t *enc, uint8_t *dec, uint64_t n, uint64_t es) {
+  const uint64_t count = n / es;
+  if (es == 2) {
+    const uint8_t *lo = enc, *hi = enc + count;
+    for (uint64_t j = 0; j < count; j++) {
+      dec[2 * j] = lo[j];
+      dec[2 * j + 1] = hi[j];
+    }
+    return;
+  }
+  for (uint64_t i = 0; i < es; i++)
+    for (uint64_t j = 0; j < count; j++) dec[j * es + i] = enc[i * count + j];
+}

@@ -135,7 +135,10 @@ int zgpu_retrieve_array_subset_multi(zgpu_chain *const *chains, uint32_t n_dev, 
         P.err = "unknown exception";
       }
       if (scratch && hipSetDevice(ctx_device(C)) == hipSuccess) {
-        hipStream_t cs = ctx_copy_stream(C);  // ordered after the peer copy (synchronised above)
+        // ordered after the peer copy (synchronised above). After a failure the decode may still have
+        // kernels writing the slab on its lane stream: wait for the device before the pool reuses it
+        if (P.rc) (void)hipDeviceSynchronize();
+        hipStream_t cs = ctx_copy_stream(C);
         if (!cs || hipFreeAsync(scratch, cs) != hipSuccess) (void)hipGetLastError();
       }
     };

@@ -85,15 +85,17 @@ struct Lane {
 // kernels of different streams sharing a queue run one after the other: 8 lanes (plus their pack
 // streams) on 4 queues serialised the drop-in's concurrent calls. A stream with a CU mask gets a
 // hardware queue of its own; with every CU in the mask (ZGPU_LANE_QUEUES=1) it is an ordinary stream
-// otherwise.
-static hipError_t lane_stream_create(hipStream_t *s) {
+// otherwise. HIP creates CU-masked streams as blocking streams (ordered against the legacy null stream,
+// unlike the non-blocking lanes they replace), and has no flags argument for them: with
+// ZGPU_LANE_QUEUES=1, work a caller queues on the null stream serialises with the lanes.
+static hipError_t lane_stream_create(hipStream_t *s, int device) {
   static const bool own = [] {
     const char *e = std::getenv("ZGPU_LANE_QUEUES");
     return e && std::atoi(e) != 0;
   }();
   if (own) {
     int ncu = 0;
-    if (hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, 0) == hipSuccess && ncu > 0) {
+    if (hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, device) == hipSuccess && ncu > 0) {
       std::vector<uint32_t> mask((ncu + 31) / 32, ~0u);
       if (ncu % 32) mask.back() = (1u << (ncu % 32)) - 1;
       const hipError_t e = hipExtStreamCreateWithCUMask(s, (uint32_t)mask.size(), mask.data());
@@ -130,7 +132,7 @@ struct zgpu_ctx {
       if (lanes_all.size() < max_lanes) {
         auto L = std::make_unique<Lane>();
         HIPCHK(hipSetDevice(device));
-        HIPCHK(lane_stream_create(&L->stream));
+        HIPCHK(lane_stream_create(&L->stream, device));
         lanes_all.push_back(L.get());
         lanes_free.push_back(L.release());
         break;
@@ -910,7 +912,11 @@ static void plan_upload(zgpu_plan &P, hipStream_t us) {
         P.d_zser = (uint32_t *)C.dev_alloc(ni * 4);
         P.zs.ser_list = P.d_zser;
         if (const uint64_t rb = zstd_lit_rec_bytes(P.zs.lit_rec_wgs)) P.zs.lit_rec = (uint8_t *)C.dev_alloc(rb);
-        if (ni * P.slot_bytes <= ZPAR_MAX_BYTES) {  // the window executor's latency mode (few frames)
+        static const uint64_t par_max = [] {  // ZGPU_ZSTD_XPAR_MB: the latency mode's batch limit (tuning)
+          const char *e = std::getenv("ZGPU_ZSTD_XPAR_MB");
+          return e ? (uint64_t)std::strtoull(e, nullptr, 10) << 20 : ZPAR_MAX_BYTES;
+        }();
+        if (ni * P.slot_bytes <= par_max) {  // the window executor's latency mode (few frames)
           P.zs.ext = (uint32_t *)C.dev_alloc(2 * ni * P.slot_bytes * 4);
           P.zs.ext_cnt = (unsigned long long *)C.dev_alloc(ZEXT_ROUNDS * 8);
           P.zs.ext_items = ni;
