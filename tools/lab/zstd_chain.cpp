@@ -32,24 +32,23 @@ int main(int argc, char **argv) {
   }
   std::vector<uint16_t> lvl((size_t)512 * 1024 * 1024);
   synth_c5_level0(512, 1024, 1024, 64, cz, cy, cx, sg, amp, 42, lvl.data(), 8);
-  const int ncz = level ? 64 : 32, ncy = level ? 256 : 512;
-  const int z0 = (c / 4) * ncz, y0 = ((c / 2) % 2) * ncy, x0 = (c % 2) * ncy;
+  // level L: the 2^L mean of L0 ([512,1024,1024] here); chunk shapes as bench C5
+  const int czs[5] = {32, 64, 64, 64, 32}, cys[5] = {512, 256, 128, 64, 64};
+  const int ncz = czs[level], ncy = cys[level], f = 1 << level;
+  const int gz = (512 / f) / ncz, gy = (1024 / f) / ncy;
+  const int z0 = (c / (gy * gy)) % gz * ncz, y0 = (c / gy) % gy * ncy, x0 = c % gy * ncy;
   const uint64_t cnt = (uint64_t)ncz * ncy * ncy, N = 2 * cnt;
   std::vector<uint8_t> d(N);
   uint64_t i = 0;
   for (int z = 0; z < ncz; z++)
     for (int y = 0; y < ncy; y++)
       for (int x = 0; x < ncy; x++, i++) {
-        uint32_t v;
-        if (!level) {
-          v = lvl[((uint64_t)(z0 + z) * 1024 + (y0 + y)) * 1024 + (x0 + x)];
-        } else {
-          uint32_t sum = 0;
-          for (int k = 0; k < 8; k++)
-            sum += lvl[((uint64_t)(2 * (z0 + z) + (k >> 2)) * 1024 + (2 * (y0 + y) + ((k >> 1) & 1))) * 1024 +
-                       (2 * (x0 + x) + (k & 1))];
-          v = sum / 8;
-        }
+        uint64_t sum = 0;
+        for (int a = 0; a < f; a++)
+          for (int b = 0; b < f; b++)
+            for (int e = 0; e < f; e++)
+              sum += lvl[((uint64_t)((z0 + z) * f + a) * 1024 + ((y0 + y) * f + b)) * 1024 + ((x0 + x) * f + e)];
+        const uint32_t v = (uint32_t)(sum / ((uint64_t)f * f * f));
         d[i] = (uint8_t)v; d[cnt + i] = (uint8_t)(v >> 8);
       }
   ZSTD_CCtx *cc = ZSTD_createCCtx();
@@ -129,6 +128,14 @@ int main(int argc, char **argv) {
     }
   }
   printf("match-granular resolution rounds (whole frame): %u\n", maxr);
+  {  // sequences per 128 KiB block (by the sequence's start)
+    std::vector<uint32_t> per(N / BLK + 1, 0);
+    uint64_t q = 0;
+    for (size_t k = 0; k < ns; k++) { per[q / BLK]++; q += s[k].litLength + s[k].matchLength; }
+    uint32_t mx = 0; uint64_t tot = 0;
+    for (uint32_t v : per) { mx = std::max(mx, v); tot += v; }
+    printf("sequences per 128 KiB block: mean %.0f max %u (blocks %zu)\n", (double)tot / per.size(), mx, per.size());
+  }
   // windowed pointer doubling (the k_zstd_exec_win model): windows of W bytes in order; a match byte
   // whose (period-reduced) source lies before the window takes the final value, else it points into
   // the window; synchronous doubling rounds until every cell holds a value
