@@ -2,7 +2,7 @@
 # One parameterised GPU-box session, run from this container through gpurun:
 #   gpurun --timeout T -- bash tools/gpu.sh <tag> <step> [<step> ...]
 # Steps run in order, each under its own time limit; the session stops at the first failure.
-#   test[:EXPR]          pytest -m gpu (-k EXPR when given)
+#   test[:EXPR[:ENV]]    pytest -m gpu (-k EXPR when given; ENV: NAME=VALUE settings, comma-separated)
 #   smoke                __graft_entry__.smoke()
 #   bench:W[:FLAGS[:ENV]] bench.py --workload W, the full line (CPU baseline, PMC passes, host leg);
 #                        FLAGS: extra bench flags, comma-separated (e.g. bench:c5:--c5-scale,2); ENV:
@@ -28,8 +28,8 @@ for step in "$@"; do
   echo "== [$i] $step"
   case "$kind" in
     test)
-      K=(); [ -n "$a" ] && K=(-k "$a")
-      timeout -k 10 600 python -u -m pytest tests -q -m gpu -x --timeout 120 --timeout-method thread "${K[@]}" \
+      K=(); [ -n "$a" ] && K=(-k "$a"); E=(${b//,/ })
+      env "${E[@]}" timeout -k 10 600 python -u -m pytest tests -q -m gpu -x --timeout 120 --timeout-method thread "${K[@]}" \
         > "$O/$i.pytest.log" 2>&1; rc=$?
       tail -3 "$O/$i.pytest.log"
       [ $rc -ne 0 ] && { echo "pytest rc=$rc"; tail -40 "$O/$i.pytest.log"; exit $rc; } ;;

@@ -36,12 +36,17 @@ int main(int argc, char **argv) {
   // argv[4] == "bz": the blosc-zstd bench's streams: 256 KiB byte-shuffled blocks (2 z-slices of a
   // [64,256,256] chunk of the u16 volume [1024,2048,1024]) at zstd level 9 (c-blosc clevel 5)
   const bool bz = argc > 4 && !strcmp(argv[4], "bz");
-  const uint64_t chunk = bz ? 262144ull : (uint64_t)(argc > 2 ? atoll(argv[2]) : 16) << 20;  // bytes
+  // argv[4] == "c5lL", L = 0..4: chunks of bench C5's level L (the 2^L mean of level 0), as bench.py
+  // cuts them: [32,512,512], [64,256,256], [64,128,128], [64,64,64], [32,64,64] (argv[2] ignored)
+  const int clev = argc > 4 && !strncmp(argv[4], "c5l", 3) ? atoi(argv[4] + 3) : !(argc > 4 && !strcmp(argv[4], "c5")) ? -1 : 0;
+  const int czs[5] = {32, 64, 64, 64, 32}, cys[5] = {512, 256, 128, 64, 64};
+  const uint64_t chunk = bz ? 262144ull
+                         : clev >= 0 ? 2ull * czs[clev] * cys[clev] * cys[clev]
+                                     : (uint64_t)(argc > 2 ? atoll(argv[2]) : 16) << 20;  // bytes
   const int level = bz ? 9 : argc > 3 ? atoi(argv[3]) : 3;
   // argv[4] == "c5": chunks [32,512,512] of a bench-like C5 level 0 ([512,1024,1024], 64 blobs)
   // argv[4] == "c5l1": chunks [64,256,256] of the 2x2x2 mean of that level (8 MiB each)
-  const bool l1 = argc > 4 && !strcmp(argv[4], "c5l1");
-  const bool c5 = l1 || (argc > 4 && !strcmp(argv[4], "c5"));
+  const bool c5 = clev >= 0;
   std::vector<uint16_t> lvl;
   if (c5) {
     std::mt19937_64 g(42);
@@ -56,27 +61,25 @@ int main(int argc, char **argv) {
   }
   std::vector<std::vector<uint8_t>> dec(n), enc(n);
   // c5 modes: chunks past the 64 distinct ones repeat them (throughput at scale)
-  const int ndist = l1 ? std::min(n, 16) : c5 ? std::min(n, 64) : n;  // c5l1: the level holds 16 chunks
+  const int gz = c5 ? (512 >> clev) / czs[clev] : 1, gy = c5 ? (1024 >> clev) / cys[clev] : 1;
+  const int ndist = c5 ? std::min(n, gz * gy * gy) : n;  // the chunks the level holds
 #pragma omp parallel for
   for (int c = 0; c < ndist; c++) {
     if (c5) {
-      const int ncz = l1 ? 64 : 32, ncy = l1 ? 256 : 512;
-      const int z0 = (c / 4) * ncz, y0 = ((c / 2) % 2) * ncy, x0 = (c % 2) * ncy;
+      const int ncz = czs[clev], ncy = cys[clev], f = 1 << clev;
+      const int z0 = (c / (gy * gy)) % gz * ncz, y0 = (c / gy) % gy * ncy, x0 = c % gy * ncy;
       const uint64_t cnt = (uint64_t)ncz * ncy * ncy;
       dec[c].resize(2 * cnt);
       uint64_t i = 0;
       for (int z = 0; z < ncz; z++)
         for (int y = 0; y < ncy; y++)
           for (int x = 0; x < ncy; x++, i++) {
-            uint32_t v = 0;
-            if (!l1) {
-              v = lvl[((uint64_t)(z0 + z) * 1024 + (y0 + y)) * 1024 + (x0 + x)];
-            } else {
-              for (int k = 0; k < 8; k++)
-                v += lvl[((uint64_t)(2 * (z0 + z) + (k >> 2)) * 1024 + (2 * (y0 + y) + ((k >> 1) & 1))) * 1024 +
-                         (2 * (x0 + x) + (k & 1))];
-              v /= 8;
-            }
+            uint64_t sum = 0;
+            for (int a = 0; a < f; a++)
+              for (int b = 0; b < f; b++)
+                for (int e = 0; e < f; e++)
+                  sum += lvl[((uint64_t)((z0 + z) * f + a) * 1024 + ((y0 + y) * f + b)) * 1024 + ((x0 + x) * f + e)];
+            const uint32_t v = (uint32_t)(sum / ((uint64_t)f * f * f));
             dec[c][i] = (uint8_t)v;
             dec[c][cnt + i] = (uint8_t)(v >> 8);
           }

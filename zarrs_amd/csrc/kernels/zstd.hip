@@ -1218,6 +1218,9 @@ struct SeqX {
 #ifndef ZG_SEQ_REP_SEL
 #define ZG_SEQ_REP_SEL 0  // 1: repeat-offset update as selects (lab A/B r04ae: blocks 3.60 -> 3.94-4.17 ms, off)
 #endif
+#ifndef ZG_SEQ_SPLIT
+#define ZG_SEQ_SPLIT 1  // k_zstd_blocks walks only the FSE state chain; fields and reps per 64-batch by lanes
+#endif
 #ifndef ZG_SEQ_ONE_FSE
 #define ZG_SEQ_ONE_FSE 1  // one FSE scratch table, folded into its SeqX table at once (0: three tables)
 #endif
@@ -1880,6 +1883,171 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(ZG_BLK_WPE, 
       BitsBack R;
       if (!bad && !bb_init(R, in, it.len, U(Bp->seq_off), U(Bp->seq_end))) bad = true;
       if (!bad) {
+#if ZG_SEQ_SPLIT && ZG_SEQ_PACK
+        // Split decoder. The serial part is only the FSE state chain: three table entries give every
+        // bit count of the sequence, so the next three states are read positionally (one 64-bit
+        // window read below the sequence's extra bits) while the entries and the bit position are
+        // parked in lane cnt. Every 64 sequences the lanes extract their own extra-bit fields (three
+        // item words each), and the batch's repeat offsets are resolved by an inclusive scan of
+        // rep-state transforms: a sequence maps the incoming (r0, r1, r2) to three values that are
+        // literal offsets or ZSYM | slot << 24 | minus references to the incoming ones (the block's
+        // symbolic reps, above), and transforms compose slot by slot. The container decoder below
+        // (ZG_SEQ_SPLIT=0) spent ~120 scalar instructions a sequence on the one chain.
+        // Positions are 32-bit, relative to word kb0 of the item (a little below the stream start). The
+        // chain reads its 64-bit windows by readlane from wcur = words [wb, wb + 64); wnext = words
+        // [wb - 60, wb + 4) is loaded one slide ahead, so a slide (every 60 words) waits for nothing.
+        const int32_t kb0 = (int32_t)(R.lo_bit >> 5) - 8;
+        const int32_t lo_r = (int32_t)(R.lo_bit - (int64_t)kb0 * 32);
+        int32_t Pr = (int32_t)(R.cur - (int64_t)kb0 * 32);  // bits not read: the next bit read is Pr - 1
+        int32_t wb = ((Pr - 1) >> 5) - 61;
+        uint32_t wcur = ldw(R, kb0 + wb + lane), wnext = ldw(R, kb0 + wb - 60 + lane);
+        auto bits64 = [&](int32_t q) -> uint64_t {  // stream bits from q up (q at most 3 words below the last)
+          int32_t d = (q >> 5) - wb;
+          if (__builtin_expect(d < 0, 0)) {
+            wcur = wnext;
+            wb -= 60;
+            d += 60;
+            wnext = ldw(R, kb0 + wb - 60 + lane);
+          }
+          const uint32_t lo = U(__builtin_amdgcn_readlane(wcur, d)), hi = U(__builtin_amdgcn_readlane(wcur, d + 1));
+          return ((((uint64_t)hi) << 32) | lo) >> (q & 31);
+        };
+        uint32_t sll, sof, sml;
+        {
+          const int32_t q = Pr - (int32_t)(lg[0] + lg[1] + lg[2]);
+          const uint64_t w = bits64(q);
+          sml = (uint32_t)w & ((1u << lg[2]) - 1);
+          sof = (uint32_t)(w >> lg[2]) & ((1u << lg[1]) - 1);
+          sll = (uint32_t)(w >> (lg[2] + lg[1])) & ((1u << lg[0]) - 1);
+          Pr = q;
+        }
+        uint32_t *out = seq_scratch + ((uint64_t)item * seq_cap + U(Bp->seq_buf)) * 3;
+        auto compose = [](uint32_t x, uint32_t a0, uint32_t a1, uint32_t a2) -> uint32_t {
+          if (!(x & ZSYM)) return x;
+          const uint32_t sl = (x >> 24) & 3, m = x & 0xFFFFFF, v = sl == 0 ? a0 : sl == 1 ? a1 : a2;
+          return (v & ZSYM) ? v + m : v - m;
+        };
+        uint32_t done = 0;
+        while (done < nseq && !bad) {
+          const uint32_t nb = min(64u, nseq - done);
+          int32_t r_p = 0;
+          uint32_t r_o = 0, r_m = 0, r_l = 0, bad_acc = 0;
+          // straight-line chain: no branch but the loop's and the rare slide (a code outside the
+          // format is caught after the batch; its entry's fields are zero, so the chain stays in the tables)
+          for (uint32_t cnt = 0; cnt < nb; cnt++) {
+            const uint32_t ow = U(S.xo[sof]), mw = U(S.xm[sml]), lwd = U(S.xl[sll]);
+            bad_acc |= ow | mw | lwd;
+            const bool here = lane == (int)cnt;
+            r_p = here ? Pr : r_p;
+            r_o = here ? ow : r_o;
+            r_m = here ? mw : r_m;
+            r_l = here ? lwd : r_l;
+            const int32_t p3 = Pr - (int32_t)(((ow >> 13) & 31) + ((mw >> 13) & 31) + ((lwd >> 13) & 31));
+            const uint32_t nl = (lwd >> 9) & 15, nm = (mw >> 9) & 15, no = (ow >> 9) & 15;
+            const int32_t q = p3 - (int32_t)(nl + nm + no);
+            const uint64_t w = bits64(q);
+            sof = (ow & 511) + ((uint32_t)w & ((1u << no) - 1));
+            sml = (mw & 511) + ((uint32_t)(w >> no) & ((1u << nm) - 1));
+            sll = (lwd & 511) + ((uint32_t)(w >> (no + nm)) & ((1u << nl) - 1));
+            Pr = done + cnt + 1 < nseq ? q : p3;  // the last sequence reads no state update
+          }
+          if (bad_acc & SQ_BAD) { bad = true; break; }
+          // lane l: sequence done + l's fields, from the three item words holding its extra bits
+          const bool mine = lane < (int)nb;
+          uint32_t ll = 0, ml = 0, ofv = 0;
+          if (mine) {
+            const uint32_t oc = (r_o >> 13) & 31, mb = (r_m >> 13) & 31, lb = (r_l >> 13) & 31;
+            const int32_t p0 = r_p, p3 = p0 - (int32_t)(oc + mb + lb);
+            const int32_t k0 = p3 >> 5;
+            const uint32_t w0 = ldw(R, kb0 + k0), w1 = ldw(R, kb0 + k0 + 1), w2 = ldw(R, kb0 + k0 + 2);
+            const uint32_t mbs = c_ml_base[(r_m >> 18) & 63], lbs = c_ll_base[(r_l >> 18) & 63];
+            const int32_t base = k0 * 32;
+            auto ext = [&](int32_t q, uint32_t n) -> uint32_t {  // n <= 31; q + n - base <= 94
+              const uint32_t r = (uint32_t)(q - base), j = r >> 5;
+              const uint64_t v = j == 0 ? (((uint64_t)w1 << 32) | w0) : j == 1 ? (((uint64_t)w2 << 32) | w1) : (uint64_t)w2;
+              return (uint32_t)(v >> (r & 31)) & ((1u << n) - 1);
+            };
+            ofv = (1u << oc) + ext(p0 - (int32_t)oc, oc);
+            ml = mbs + ext(p0 - (int32_t)(oc + mb), mb);
+            ll = lbs + ext(p3, lb);
+          }
+          // the sequence's rep-state transform; lanes past cnt hold the identity
+          const uint32_t I0 = ZSYM, I1 = ZSYM | (1u << 24), I2 = ZSYM | (2u << 24);
+          uint32_t t0, t1, t2;
+          bool lbad = false;
+          if (ofv > 3) {
+            t0 = ofv - 3;
+            lbad = (t0 & ZSYM) != 0;  // beyond any window we decode
+            t1 = I0;
+            t2 = I1;
+          } else {
+            const uint32_t idx = ofv - 1 + (ll == 0 ? 1u : 0u);  // 0..3 (ofv 1..3), 0 off the batch
+            t0 = idx == 0 ? I0 : idx == 1 ? I1 : idx == 2 ? I2 : I0 + 1;
+            t1 = idx == 0 ? I1 : I0;
+            t2 = idx <= 1 ? I2 : I1;
+          }
+          if (__any(lbad)) { bad = true; break; }
+          uint32_t inc = ll + ml, incl = ll;
+          for (int o = 1; o < 64; o <<= 1) {
+            const uint32_t a0 = __shfl_up(t0, o, 64), a1 = __shfl_up(t1, o, 64), a2 = __shfl_up(t2, o, 64);
+            const uint32_t u = __shfl_up(inc, o, 64), ul = __shfl_up(incl, o, 64);
+            if (lane >= o) {
+              const uint32_t c0 = compose(t0, a0, a1, a2), c1 = compose(t1, a0, a1, a2), c2 = compose(t2, a0, a1, a2);
+              t0 = c0;
+              t1 = c1;
+              t2 = c2;
+              inc += u;
+              incl += ul;
+            }
+          }
+          const uint32_t off = compose(t0, r0, r1, r2);
+          {
+            const uint32_t n1 = compose(t1, r0, r1, r2), n2 = compose(t2, r0, r1, r2);
+            r0 = __shfl(off, 63, 64);
+            r1 = __shfl(n1, 63, 64);
+            r2 = __shfl(n2, 63, 64);
+          }
+          {  // the batch's reach back from the block start (exact, per match)
+            const int32_t p = (int32_t)(sum_ll + sum_ml + inc - ml);  // this lane's match start
+            int32_t rc = INT32_MIN;
+            uint32_t m0 = ~0u, m1 = ~0u, m2 = ~0u;
+            if (mine && ml) {
+              if (!(off & ZSYM)) {
+                rc = (int32_t)off - p;
+              } else {
+                const uint32_t slot = (off >> 24) & 3, mv = (off & 0xFFFFFF) + (uint32_t)p;
+                if (slot == 0) m0 = mv;
+                else if (slot == 1) m1 = mv;
+                else m2 = mv;
+              }
+            }
+            for (int o = 32; o; o >>= 1) {
+              rc = max(rc, __shfl_xor(rc, o, 64));
+              m0 = min(m0, __shfl_xor(m0, o, 64));
+              m1 = min(m1, __shfl_xor(m1, o, 64));
+              m2 = min(m2, __shfl_xor(m2, o, 64));
+            }
+            reach_c = max(reach_c, rc);
+            reach_m0 = min(reach_m0, m0);
+            reach_m1 = min(reach_m1, m1);
+            reach_m2 = min(reach_m2, m2);
+          }
+          {
+            const uint32_t tot = __shfl(inc, 63, 64), totl = __shfl(incl, 63, 64);
+            sum_ll += totl;
+            sum_ml += tot - totl;
+          }
+          if (mine) {
+            uint32_t *o = out + (uint64_t)(done + lane) * 3;
+            o[0] = ll;
+            o[1] = ml;
+            o[2] = off;
+          }
+          done += nb;
+        }
+        // the stream must end exactly on its first bit
+        if (!bad && Pr != lo_r) bad = true;
+#else
         auto word = [&](int32_t k) -> uint32_t {
           if (k < R.wb - 16) {  // slide the window pair down, prefetching the next lower window
             R.wb -= 64;
@@ -2029,6 +2197,7 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(ZG_BLK_WPE, 
         }
         // the stream must end exactly on its first bit
         if (!bad && (int64_t)lw * 32 + have != R.lo_bit) bad = true;
+#endif
       }
       SQP_T(sq_t2);
       SQP_ADD(1, sq_t2 - sq_t1);
@@ -2069,6 +2238,9 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(ZG_BLK_WPE, 
 #endif
 #ifndef ZG_SEQ_WN
 #define ZG_SEQ_WN 128  // staged stream words per block and epoch
+#endif
+#ifndef ZG_SEQ_POS
+#define ZG_SEQ_POS 0  // 1: positional field reader (lab r06p: blocks 5.01 -> 5.74 ms at 64 L0 chunks, off)
 #endif
 template <int G>
 struct ZDecLgSmem {
@@ -2175,7 +2347,7 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(ZG_SEQ_WPE, 
     uint32_t reach_m0 = ~0u, reach_m1 = ~0u, reach_m2 = ~0u;
     const uint32_t *words = nullptr;
     int32_t nwords = 0, lw = 0, have = 0, lo_w = 0;
-    int64_t lo_bit = 0;
+    int64_t lo_bit = 0, P = 0;  // P (ZG_SEQ_POS): stream bits not read yet; the next bit read is P - 1
     uint64_t C = 0;
     bool act = false;
     uint32_t sll = 0, sof = 0, sml = 0, n = 0;
@@ -2192,6 +2364,7 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(ZG_SEQ_WPE, 
       } else {
         const int64_t p0 = (int64_t)(seq_end - 1 + mis) * 8 + highbit(last);
         lo_bit = (int64_t)(seq_off + mis) * 8;
+        P = p0;
         lw = (int32_t)((p0 - 1) >> 5) - 1;
         have = (int32_t)(p0 - 32 * (int64_t)lw);  // (32, 64]
         auto ld = [&](int32_t k) -> uint32_t { return (k >= 0 && k < nwords) ? words[k] : 0u; };
@@ -2212,7 +2385,8 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(ZG_SEQ_WPE, 
     while (__any(act)) {
       SQP_ADD(4, 1);
       // stage words [lw - WN, lw) of every active lane's stream: lane k's window is S.win[k]
-      lo_w = lw - ZG_SEQ_WN;
+      // (positional reader: [kt + 1 - WN, kt + 1), kt the word holding bit P - 1)
+      lo_w = ZG_SEQ_POS ? (int32_t)((P - 1) >> 5) + 1 - ZG_SEQ_WN : lw - ZG_SEQ_WN;
 #pragma unroll
       for (int k = 0; k < G; k++) {
         const bool ak = __builtin_amdgcn_readlane((int)act, k) != 0;
@@ -2227,6 +2401,99 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(ZG_SEQ_WPE, 
         }
       }
       __syncthreads();
+#if ZG_SEQ_POS
+      // Positional reader: a field of nb bits is stream bits [P - nb, P). A sequence reads at most
+      // 31 + 16 + 16 + 9 + 9 + 8 = 89 bits, i.e. words kt = (P - 1) >> 5 down to kt - 3: they are read
+      // from the staged window with the three table entries, in one LDS round; the six field
+      // positions follow from the entries' bit counts, and the fields are funnel-shifted out of those
+      // four words independently (the 64-bit container's refill / shift chain serialised them).
+      const uint32_t k = (uint32_t)lane;
+      auto win4 = [&](int32_t kt, uint32_t &q0, uint32_t &q1, uint32_t &q2, uint32_t &q3) {
+        const uint32_t *wk = &S.win[k][kt - 3 - lo_w];
+        q0 = wk[0];
+        q1 = wk[1];
+        q2 = wk[2];
+        q3 = wk[3];
+      };
+      // bits [q, q + nb) of the stream, nb <= 31, from words base/32 .. base/32 + 3
+      auto ext = [](int64_t q, uint32_t nb, int64_t base, uint32_t q0, uint32_t q1, uint32_t q2, uint32_t q3) -> uint32_t {
+        const uint32_t r = (uint32_t)(q - base), j = r >> 5, sh = r & 31;
+        const uint32_t lo = j == 0 ? q0 : j == 1 ? q1 : j == 2 ? q2 : q3;
+        const uint32_t hi = j == 0 ? q1 : j == 1 ? q2 : j == 2 ? q3 : 0u;
+        return (uint32_t)((((uint64_t)hi << 32) | lo) >> sh) & ((1u << nb) - 1);
+      };
+      if (act && first) {  // the three initial states (at most 9 + 8 + 9 bits)
+        first = false;
+        const int32_t kt = (int32_t)((P - 1) >> 5);
+        uint32_t q0, q1, q2, q3;
+        win4(kt, q0, q1, q2, q3);
+        const int64_t base = (int64_t)(kt - 3) * 32;
+        sll = ext(P - lg0, lg0, base, q0, q1, q2, q3);
+        P -= lg0;
+        sof = ext(P - lg1, lg1, base, q0, q1, q2, q3);
+        P -= lg1;
+        sml = ext(P - lg2, lg2, base, q0, q1, q2, q3);
+        P -= lg2;
+      }
+      while (act) {
+        const int32_t kt = (int32_t)((P - 1) >> 5);
+        if (kt - 3 < lo_w) break;  // the next epoch stages the words below
+        const uint32_t ow = S.xo[k][sof], mw = S.xm[k][sml], lwd = S.xl[k][sll];
+        uint32_t q0, q1, q2, q3;
+        win4(kt, q0, q1, q2, q3);
+        if ((ow | mw | lwd) & SQ_BAD) { bad = true; act = false; break; }
+        const int64_t base = (int64_t)(kt - 3) * 32;
+        const uint32_t oc = (ow >> 18) & 63, mc = (mw >> 18) & 63, lc = (lwd >> 18) & 63;
+        const uint32_t mbits = (mw >> 13) & 31, lbits = (lwd >> 13) & 31;
+        const int64_t P1 = P - oc, P2 = P1 - mbits, P3 = P2 - lbits;
+        const uint32_t ofv = (1u << oc) + ext(P1, oc, base, q0, q1, q2, q3);
+        const uint32_t ml = S.mlb[mc] + ext(P2, mbits, base, q0, q1, q2, q3);
+        const uint32_t ll = S.llb[lc] + ext(P3, lbits, base, q0, q1, q2, q3);
+        n++;
+        P = P3;
+        if (n < nseq) {
+          const uint32_t nl = (lwd >> 9) & 15, nm = (mw >> 9) & 15, no = (ow >> 9) & 15;
+          const int64_t P4 = P3 - nl, P5 = P4 - nm, P6 = P5 - no;
+          sll = (lwd & 511) + ext(P4, nl, base, q0, q1, q2, q3);
+          sml = (mw & 511) + ext(P5, nm, base, q0, q1, q2, q3);
+          sof = (ow & 511) + ext(P6, no, base, q0, q1, q2, q3);
+          P = P6;
+        }
+        // repeat offsets, symbolically in the block's incoming rep state (RFC 8878 3.1.1.5), as
+        // selects: kk = 0 a new offset, else 1 + repeat index
+        const uint32_t kk = ofv > 3 ? 0u : ofv + (ll == 0 ? 1u : 0u);
+        if (kk == 0 && ((ofv - 3) & ZSYM)) { bad = true; act = false; break; }  // beyond any window we decode
+        const uint32_t s3 = (r0 & ZSYM) ? r0 + 1 : r0 - 1;
+        uint32_t off = ofv - 3;
+        off = kk == 1 ? r0 : off;
+        off = kk == 2 ? r1 : off;
+        off = kk == 3 ? r2 : off;
+        off = kk == 4 ? s3 : off;
+        const uint32_t n2 = (kk == 0 || kk >= 3) ? r1 : r2;
+        const uint32_t n1 = kk == 1 ? r1 : r0;
+        r2 = n2;
+        r1 = n1;
+        r0 = off;
+        // how far the match reaches back from the block start (exact, per match)
+        const int32_t p = (int32_t)(sum_ll + sum_ml + ll);
+        const bool isc = !(off & ZSYM);
+        const uint32_t slot = (off >> 24) & 3, mv = (off & 0xFFFFFF) + (uint32_t)p;
+        reach_c = isc ? max(reach_c, (int32_t)off - p) : reach_c;
+        reach_m0 = (!isc && slot == 0) ? min(reach_m0, mv) : reach_m0;
+        reach_m1 = (!isc && slot == 1) ? min(reach_m1, mv) : reach_m1;
+        reach_m2 = (!isc && slot >= 2) ? min(reach_m2, mv) : reach_m2;
+        sum_ll += ll;
+        sum_ml += ml;
+        uint32_t *o = out + (uint64_t)(n - 1) * 3;
+        o[0] = ll;
+        o[1] = ml;
+        o[2] = off;
+        if (n == nseq) {
+          act = false;
+          if (P != lo_bit) bad = true;  // the stream must end exactly on its first bit
+        }
+      }
+#else
       if (act && first) {  // the three initial states
         first = false;
         // the container holds > 32 bits, at most 9 + 8 read before the refill
@@ -2313,6 +2580,7 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(ZG_SEQ_WPE, 
           if ((int64_t)lw * 32 + have != lo_bit) bad = true;
         }
       }
+#endif
       __syncthreads();  // this epoch's window reads are done before the next staging
     }
     SQP_T(sq_t2);
