@@ -4443,16 +4443,16 @@ static hipError_t launch_zstd_pass(ZgItem *items, uint32_t *status, uint32_t n_i
   // one resident wave of the sequence decoder: CUs x 4 SIMDs x ZG_BLK_WPE waves
   const uint32_t bgrid =
       (uint32_t)std::min<uint64_t>(recs, std::max<uint64_t>(g_cap, (uint64_t)device_cu_count() * 4 * ZG_BLK_WPE));
-  // sequence decoder: 1 lane groups (k_zstd_blocks_lg: batches), 0 one wave per block (k_zstd_blocks:
-  // the latency mode's few frames, lone C5 frame 1.15 -> 0.71 ms, profiles/r06/r06l_*); ZGPU_ZSTD_SEQ
-  // forces one
+  // sequence decoder: 0 one wave per block (k_zstd_blocks, the split chain decoder: lab 64 L0 chunks
+  // 1.63 ms against the lane groups' 5.0, C5 82.0 -> 74.7 ms, profiles/r06/r06pqr_*), 1 lane groups
+  // (k_zstd_blocks_lg, the round-5 default); ZGPU_ZSTD_SEQ forces one
   const char *xp_s = std::getenv("ZGPU_ZSTD_XPAR");
   const bool par = xwin_on && Z.ext && Z.ext_cnt && n_items <= Z.ext_items && (!xp_s || std::atoi(xp_s) != 0);
   static const int seq_env = [] {
     const char *e = std::getenv("ZGPU_ZSTD_SEQ");
     return e ? std::atoi(e) : -1;
   }();
-  const int seq_mode = seq_env >= 0 ? seq_env : par ? 0 : 1;
+  const int seq_mode = seq_env >= 0 ? seq_env : 0;
   auto launch_seq = [&] {
     if (seq_mode == 1) {
       // one resident wave of the lane-group decoder: its LDS (5 KiB per block) sets the waves per CU
