@@ -4431,8 +4431,9 @@ static hipError_t launch_zstd_pass(ZgItem *items, uint32_t *status, uint32_t n_i
   // one (read per call: tests run both).
   const char *xw_s = std::getenv("ZGPU_ZSTD_XWIN");
   const int xw_env = xw_s ? std::atoi(xw_s) : -1;
-  const bool xwin_on = xw_env >= 0 ? xw_env != 0
-                                   : (uint64_t)n_items * XSEG < (uint64_t)device_cu_count() * ZG_XWIN_MAX_WPC;
+  const char *xwpc_s = std::getenv("ZGPU_ZSTD_XWIN_WPC");  // the threshold's waves per CU (A/B)
+  const uint64_t xwpc = xwpc_s ? (uint64_t)std::atoi(xwpc_s) : ZG_XWIN_MAX_WPC;
+  const bool xwin_on = xw_env >= 0 ? xw_env != 0 : (uint64_t)n_items * XSEG < (uint64_t)device_cu_count() * xwpc;
   const uint32_t xseg = xseg_env ? xseg_env : xwin_on ? XSEG_WIN : XSEG;
 
   if (fork) {
