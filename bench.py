@@ -931,6 +931,8 @@ class C5:
         # while the second L0 half and L1 decode sequences, so throughput-bound literal work overlaps
         # latency-bound sequence decoding: C5 88.2-88.5 -> 83.2 ms (profiles/r05/r05lf_zstd_lits_first_ab.txt)
         self.lits_first_parts = [p for p, l in enumerate(lane_of) if l in (0, 3)]
+        # the same levels as one library plan group (zgpu_group, the default; --bench-lanes: the lanes above)
+        self.level_parts = [(self.chain, d, o, list(o.shape)) for d, o in zip(per_level, self.outs) if d]
         self.decoded_bytes = dec_total
         self.step_bytes = dec_total if getattr(self.args, "emulate_rank", "") else all_bytes
         self.ratio = raw_bytes / max(1, sum(enc_sizes))
@@ -983,6 +985,10 @@ class C5:
                 sel = [min(c, s_ - st) for c, s_, st in zip(cs, shp, start)]
                 per_level[li].append(make_desc((self.enc_bufs[i].data_ptr(), self.enc_sizes[i]), cs, [0, 0, 0],
                                                sel, start))
+            if not getattr(self.args, "bench_lanes", False):  # the library plan group, as the step runs it
+                rank_ms.append(_time_group([(self.chain, d, list(o.shape)) for d, o in zip(per_level, self.outs) if d],
+                                           [o for d, o in zip(per_level, self.outs) if d], self.dev))
+                continue
             l0 = per_level[0]
             halves = lpt_partition([int(d.enc_len) for d in l0], 2)
             groups_d = [[l0[i] for i in hv] for hv in halves] + per_level[1:]
@@ -1001,8 +1007,9 @@ class C5:
         gb = int(np.prod(g_shape)) * 2 * (N - 1) // N
         gms = gb / ((N - 1) * XGMI_LINK_GBS * 1e9) * 1e3
         return rank_share_report(rank_ms, n1_ms, self.step_bytes, gb, gms,
-                                 "each rank's LPT chunk share decoded alone on this GPU (its plans on the N = 8 "
-                                 "lane layout, 5 reps, median); the L0 subset gather (7/8 of it to rank 0) at "
+                                 "each rank's LPT chunk share decoded alone on this GPU (its levels as the N = 8 "
+                                 "run decodes them: one library plan group, or --bench-lanes' lanes; 5 reps, "
+                                 "median); the L0 subset gather (7/8 of it to rank 0) at "
                                  f"7 x {XGMI_LINK_GBS:.0f} GB/s; the slowest rank sets the step")
 
     def after_decode(self):
@@ -1463,6 +1470,28 @@ def _time_plan_groups(ctx, groups, lanes, lits_first, dev, reps=5, status_each=F
             lib.zgpu_plan_destroy(plan)
 
 
+def _time_group(parts, outs, dev, reps=5):
+    """Median wall ms of one decode of `parts` ((chain, descs, out_shape) per part) as ONE library plan
+    group (zgpu_group) into `outs`; statuses read back after the timing must be 0."""
+    from zarrs_amd import PlanGroup
+    g = PlanGroup(parts)
+    try:
+        main = torch.cuda.current_stream(dev)
+        for _ in range(2):
+            g.execute(outs, stream=main.cuda_stream, wait=True)
+        ts = []
+        for _ in range(reps):
+            t0 = time.perf_counter()
+            g.execute(outs, stream=main.cuda_stream, wait=False)
+            torch.cuda.synchronize(dev)
+            ts.append(time.perf_counter() - t0)
+        if any(g.wait()):
+            raise RuntimeError("rank share decode failed")
+        return float(np.median(ts)) * 1e3
+    finally:
+        g.close()
+
+
 def rank_share_report(rank_ms, n1_ms, step_bytes, gather_bytes, gather_ms, note):
     """The N = RANK_SHARE_N prediction from one GPU: each rank's share of the step decoded alone (the
     same kernels, plans and lane layout as that rank runs), the exchange priced at the root's direct xGMI
@@ -1501,7 +1530,17 @@ def run_gpu(args, rank, world, dev):
     lits_first = set(getattr(W, "lits_first_parts", []))
     if args.lits_first is not None:
         lits_first = {int(x) for x in args.lits_first.split(",") if x.strip()}
-    for pi, (chain, descs, out, out_shape) in enumerate(W.parts):
+    # independent parts (pyramid levels) as ONE library plan group (zgpu_group: the library lays them out
+    # on streams of its own); --bench-lanes (and the profiling / A/B options) keep the bench-side lanes
+    group = None
+    if getattr(W, "level_parts", None) and not (args.bench_lanes or args.serial_lanes or args.fork or
+                                                args.lits_first is not None or args.lane_priorities):
+        from zarrs_amd import PlanGroup
+        group = PlanGroup([(c, d, shp) for c, d, _, shp in W.level_parts])
+        group_outs = [o for _, _, o, _ in W.level_parts]
+        W.config["plan_layout"] = {"kind": "library plan group (zgpu_group)",
+                                   "plans_lane_part_litsfirst": group.layout()}
+    for pi, (chain, descs, out, out_shape) in enumerate([] if group else W.parts):
         n = len(descs)
         if not n:
             continue
@@ -1535,6 +1574,9 @@ def run_gpu(args, rank, world, dev):
     plan_sp = {pi: lane_sp[li] for li, ln in enumerate(lanes) for pi in ln}
 
     def enqueue_all():
+        if group:
+            group.execute(group_outs, stream=sp.value, wait=False)
+            return
         start = torch.cuda.Event()
         start.record(stream)
         for st in side:
@@ -1566,7 +1608,11 @@ def run_gpu(args, rank, world, dev):
                 W.run_step(execute_part)
             W.after_decode()
             return
-        if len(plans) == 1:
+        if group:
+            enqueue_all()
+            group.wait()
+            rc = 0
+        elif len(plans) == 1:
             plan, out, status = plans[0]
             rc = lib.zgpu_plan_execute(plan, out.data_ptr(), status, sp)
         else:
@@ -1605,6 +1651,8 @@ def run_gpu(args, rank, world, dev):
     if args.child:  # rocprofv3 --pmc pass: only the dispatches matter
         for plan, _, _ in plans:
             lib.zgpu_plan_destroy(plan)
+        if group:
+            group.close()
         return None
     # Device time of one decode launch sequence, HIP events on the stream the library launches on;
     # enqueue-only executes (status=NULL), back to back.
@@ -1619,7 +1667,8 @@ def run_gpu(args, rank, world, dev):
     torch.cuda.synchronize()
     ev_ms = ev0.elapsed_time(ev1) / args.steps
     alg_bytes = sum(lib.zgpu_plan_algorithmic_bytes(plan) for plan, _, _ in plans) + getattr(W, "extra_alg_bytes", 0)
-    counters = [0] * L.N_COUNTERS
+    alg_bytes += group.algorithmic_bytes() if group else 0
+    counters = group.counters() if group else [0] * L.N_COUNTERS
     for plan, _, _ in plans:  # device counters of each plan's last execute (statuses read in step())
         buf = (C.c_uint64 * L.N_COUNTERS)()
         lib.zgpu_plan_counters(plan, buf, L.N_COUNTERS)
@@ -1635,6 +1684,8 @@ def run_gpu(args, rank, world, dev):
     batch_ms = (time.perf_counter() - t1) / reps * 1e3
     for plan, _, _ in plans:
         lib.zgpu_plan_destroy(plan)
+    if group:
+        group.close()
     host = W.host_leg(sp) if (args.host_leg and rank == 0) else None
     gather = W.gather_stats() if hasattr(W, "gather_stats") else None
     return dict(W=W, elapsed=elapsed, ev_ms=ev_ms, alg_bytes=alg_bytes, ok=ok, batch_ms=batch_ms, host=host,
@@ -1685,6 +1736,7 @@ def secondary_legs(args, rank, world, dev, r_primary):
         a.host_leg, a.cpu_seconds, a.c5_scale = False, 5.0, args.secondary_c5_scale
         a.lane_priorities, a.serial_lanes, a.lane_times, a.fork = "", False, False, False
         a.lits_first = None
+        a.bench_lanes = args.bench_lanes
         gc.collect()
         torch.cuda.empty_cache()
         args.ctx.release_cached()  # the previous leg's pooled device / pinned blocks back to the driver
@@ -1883,6 +1935,8 @@ def main():
     ap.add_argument("--c5-scale", type=int, default=1, help="C5: divide the L0 y/x extents by this (1: the full [512,4096,4096] L0)")
     ap.add_argument("--no-cpu", action="store_true")
     ap.add_argument("--lane-times", action="store_true", help="print each stream lane's solo time (stderr)")
+    ap.add_argument("--bench-lanes", action="store_true",
+                    help="C5: the bench-side stream lanes (round 5) instead of the library plan group (A/B)")
     ap.add_argument("--no-pmc", action="store_true", help="skip the rocprofv3 PMC traffic passes")
     ap.add_argument("--lane-priorities", default="",
                     help="comma-separated HIP stream priorities of the stream lanes (-1 high, 0 normal)")

@@ -265,6 +265,34 @@ void zgpu_plan_destroy(zgpu_plan *plan);
  * written), the figure bench.py prices the roofline with. */
 uint64_t zgpu_plan_algorithmic_bytes(const zgpu_plan *plan);
 
+/*
+ * Plan group: one decode over the independent parts of a batch, each part one chunk shape and one
+ * output (the levels of a multiscale pyramid; zarrs runs one rayon loop per array,
+ * array_read_ops_common.rs:111-179). The group creates the parts' plans and places them on streams of
+ * its own (at most ZGPU_GROUP_LANES, default 4 = HIP's default hardware queues): a part with at least
+ * 1/(4 x lanes) of the group's encoded bytes gets a lane, the smaller parts share one lane (largest
+ * first), the lanes left over go to the largest part, split into pieces of balanced encoded bytes; zstd
+ * literals-first on the largest part's first piece and on the small-part lane (group.cpp). Part p has
+ * n_descs[p] descriptors descs[p] decoded with chains[p] into an output of out_shapes[p] (ndim dims);
+ * flags as zgpu_plan_create (ZGPU_ENC_DEVICE required). zgpu_group_execute enqueues every part behind
+ * the work already on hip_stream (NULL: the legacy default stream) and makes hip_stream wait for all
+ * of them; outs[p] is part p's output. status (NULL: asynchronous, read with zgpu_group_status)
+ * receives the per-descriptor statuses, concatenated in part order; the return value is the first
+ * non-zero one.
+ */
+typedef struct zgpu_group zgpu_group;
+int zgpu_group_create(zgpu_chain *const *chains, uint32_t ndim, uint32_t n_parts, const zgpu_chunk_desc *const *descs,
+                      const uint64_t *n_descs, const uint64_t *const *out_shapes, uint32_t flags, zgpu_group **out);
+int zgpu_group_execute(zgpu_group *group, void *const *outs, int32_t *status, void *hip_stream);
+int zgpu_group_status(zgpu_group *group, int32_t *status, void *hip_stream);
+/* The group's plans: returns how many; for the first n, their lane, part and literals-first flag. */
+uint32_t zgpu_group_layout(const zgpu_group *group, uint32_t *lane_of, uint32_t *part_of, uint32_t *lits_first,
+                           uint32_t n);
+uint64_t zgpu_group_algorithmic_bytes(const zgpu_group *group);
+/* zgpu_plan_counters summed over the group's plans (after zgpu_group_status). */
+uint32_t zgpu_group_counters(const zgpu_group *group, uint64_t *out, uint32_t n);
+void zgpu_group_destroy(zgpu_group *group);
+
 /* Device counters of a plan's last execute (after its statuses were read) or of the calling
  * thread's last decode call (zgpu_decode_batch / zgpu_decode_files / zgpu_retrieve_*), summed over
  * its sub-batches. Writes min(n, ZGPU_N_COUNTERS) values, returns how many were written. */

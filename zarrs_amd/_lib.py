@@ -43,6 +43,8 @@ EXPORTS = [
     "zgpu_encode_chunks", "zgpu_retrieve_array_subset_multi", "zgpu_decode_into", "zgpu_ctx_set_coalescing",
     "zgpu_ctx_coalescing_stats", "zgpu_ctx_refcount", "zgpu_decode_pinned", "zgpu_result_release",
     "zgpu_encode_pinned", "zgpu_ctx_release_cached", "zgpu_ctx_pool_stats",
+    "zgpu_group_create", "zgpu_group_execute", "zgpu_group_status", "zgpu_group_layout",
+    "zgpu_group_algorithmic_bytes", "zgpu_group_counters", "zgpu_group_destroy",
 ]
 CTR_ENC_BYTES, CTR_ZSTD_SERIAL, CTR_ZSTD_PARALLEL, CTR_BLOSC_RERUN, CTR_BLOSC_BLOCKS, CTR_ITEMS = range(6)
 N_COUNTERS = 6
@@ -154,6 +156,17 @@ def load() -> C.CDLL:
     L.zgpu_plan_destroy.argtypes = [vp]
     L.zgpu_plan_algorithmic_bytes.restype = u64
     L.zgpu_plan_algorithmic_bytes.argtypes = [vp]
+    L.zgpu_group_create.argtypes = [C.POINTER(vp), u32, u32, C.POINTER(C.POINTER(ChunkDesc)), P64, C.POINTER(P64),
+                                    u32, C.POINTER(vp)]
+    L.zgpu_group_execute.argtypes = [vp, C.POINTER(vp), C.POINTER(C.c_int32), vp]
+    L.zgpu_group_status.argtypes = [vp, C.POINTER(C.c_int32), vp]
+    L.zgpu_group_layout.restype = u32
+    L.zgpu_group_layout.argtypes = [vp, C.POINTER(u32), C.POINTER(u32), C.POINTER(u32), u32]
+    L.zgpu_group_algorithmic_bytes.restype = u64
+    L.zgpu_group_algorithmic_bytes.argtypes = [vp]
+    L.zgpu_group_counters.restype = u32
+    L.zgpu_group_counters.argtypes = [vp, P64, u32]
+    L.zgpu_group_destroy.argtypes = [vp]
     L.zgpu_retrieve_array_subset.argtypes = [vp, u32, P64, P64, C.POINTER(vp), P64, P64, P64, vp,
                                              u32, vp]
     L.zgpu_decode_files.argtypes = [vp, u32, C.POINTER(ChunkDesc), C.POINTER(FileRange), u64, vp, P64,

@@ -312,3 +312,69 @@ class CodecChain:
         self.decode_batch([make_desc(encoded, shape, subset_start, subset_shape)], out,
                           list(subset_shape), dev)
         return out
+
+
+class PlanGroup:
+    """zgpu_group: independent parts of one batch (each part one chunk shape and one output, e.g. the
+    levels of a multiscale pyramid) decoded by one call; the library lays the parts out on streams of
+    its own and picks each plan's literals-first order (group.cpp). `parts`: (chain, descs,
+    out_shape) per part, descriptors with device-resident encoded bytes; `execute(outs)` decodes part
+    p into outs[p] (device tensors) behind `stream` (default: torch's current stream of outs[0])."""
+
+    def __init__(self, parts, flags: int = 0):
+        lib = L.load()
+        self.n_parts = len(parts)
+        self.chains = [c for c, _, _ in parts]
+        nd = len(parts[0][2])
+        self._arrs = [(L.ChunkDesc * max(len(d), 1))(*d) for _, d, _ in parts]
+        self.n_descs = [len(d) for _, d, _ in parts]
+        chains = (C.c_void_p * self.n_parts)(*[c._h for c in self.chains])
+        dptrs = (C.POINTER(L.ChunkDesc) * self.n_parts)(*[C.cast(a, C.POINTER(L.ChunkDesc)) for a in self._arrs])
+        ns = (C.c_uint64 * self.n_parts)(*self.n_descs)
+        self._shapes = [L.u64s(s) for _, _, s in parts]
+        shp = (C.POINTER(C.c_uint64) * self.n_parts)(*[C.cast(s, C.POINTER(C.c_uint64)) for s in self._shapes])
+        h = C.c_void_p()
+        L.check(lib.zgpu_group_create(chains, nd, self.n_parts, dptrs, ns, shp,
+                                      flags | L.ENC_DEVICE | L.OUT_DEVICE, C.byref(h)))
+        self._h = h
+        self.status = (C.c_int32 * max(1, sum(self.n_descs)))()
+
+    def layout(self) -> list:
+        """[(lane, part, literals_first)] of the group's plans."""
+        lib = L.load()
+        n = lib.zgpu_group_layout(self._h, None, None, None, 0)
+        lane, part, lf = (C.c_uint32 * max(n, 1))(), (C.c_uint32 * max(n, 1))(), (C.c_uint32 * max(n, 1))()
+        lib.zgpu_group_layout(self._h, lane, part, lf, n)
+        return [(lane[i], part[i], bool(lf[i])) for i in range(n)]
+
+    def algorithmic_bytes(self) -> int:
+        return int(L.load().zgpu_group_algorithmic_bytes(self._h))
+
+    def counters(self) -> list:
+        buf = (C.c_uint64 * L.N_COUNTERS)()
+        n = L.load().zgpu_group_counters(self._h, buf, L.N_COUNTERS)
+        return list(buf[:n])
+
+    def execute(self, outs, stream=None, wait: bool = True) -> list | None:
+        """Enqueue the decode; with wait, read back the per-descriptor statuses (concatenated in part
+        order) and raise ZgpuError with the first failing one."""
+        lib = L.load()
+        ptrs = (C.c_void_p * self.n_parts)(*[_ptr_len(o)[0] for o in outs])
+        s = default_stream(stream, *outs)
+        L.check(lib.zgpu_group_execute(self._h, ptrs, self.status if wait else None, s))
+        return list(self.status[: sum(self.n_descs)]) if wait else None
+
+    def wait(self, stream=None) -> list:
+        L.check(L.load().zgpu_group_status(self._h, self.status, stream))
+        return list(self.status[: sum(self.n_descs)])
+
+    def close(self):
+        if getattr(self, "_h", None):
+            L.load().zgpu_group_destroy(self._h)
+            self._h = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
