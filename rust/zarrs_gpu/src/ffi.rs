@@ -44,6 +44,11 @@ pub struct zgpu_chain {
 pub struct zgpu_result {
     _opaque: [u8; 0],
 }
+/// A plan group (`zgpu_group_create`): the independent parts of one batch decoded by one call.
+#[repr(C)]
+pub struct zgpu_group {
+    _opaque: [u8; 0],
+}
 
 /// zgpu_last_counters index: leaf items (chunks / inner chunks) the calling thread's last call planned.
 pub const ZGPU_CTR_ITEMS: usize = 5;
@@ -166,6 +171,24 @@ unsafe extern "C" {
         result: *mut *mut zgpu_result,
     ) -> c_int;
     pub fn zgpu_result_release(result: *mut zgpu_result);
+    pub fn zgpu_group_create(
+        chains: *const *mut zgpu_chain,
+        ndim: u32,
+        n_parts: u32,
+        descs: *const *const zgpu_chunk_desc,
+        n_descs: *const u64,
+        out_shapes: *const *const u64,
+        flags: u32,
+        out: *mut *mut zgpu_group,
+    ) -> c_int;
+    pub fn zgpu_group_execute(
+        group: *mut zgpu_group,
+        outs: *const *mut c_void,
+        status: *mut i32,
+        hip_stream: *mut c_void,
+    ) -> c_int;
+    pub fn zgpu_group_status(group: *mut zgpu_group, status: *mut i32, hip_stream: *mut c_void) -> c_int;
+    pub fn zgpu_group_destroy(group: *mut zgpu_group);
     pub fn zgpu_retrieve_array_subset_multi(
         chains: *const *mut zgpu_chain,
         n_dev: u32,
