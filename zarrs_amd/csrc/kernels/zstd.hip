@@ -1904,6 +1904,9 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(ZG_BLK_WPE, 
         auto bits64 = [&](int32_t q) -> uint64_t {  // stream bits from q up (q at most 3 words below the last)
           int32_t d = (q >> 5) - wb;
           if (__builtin_expect(d < 0, 0)) {
+            // keeps the copy inside the branch: hoisted above it, the copy read wnext on every sequence
+            // and so waited for its load right after each slide
+            asm volatile("" : "+v"(wnext));
             wcur = wnext;
             wb -= 60;
             d += 60;
@@ -1930,28 +1933,34 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(ZG_BLK_WPE, 
         uint32_t done = 0;
         while (done < nseq && !bad) {
           const uint32_t nb = min(64u, nseq - done);
-          int32_t r_p = 0;
-          uint32_t r_o = 0, r_m = 0, r_l = 0, bad_acc = 0;
-          // straight-line chain: no branch but the loop's and the rare slide (a code outside the
-          // format is caught after the batch; its entry's fields are zero, so the chain stays in the tables)
+          int32_t r_p = 0, p3 = Pr;
+          uint32_t r_o = 0, r_m = 0, r_l = 0;
+          // straight-line chain: no branch but the loop's and the rare slide. A code outside the format
+          // is caught by the lanes after the batch (its entry's fields are zero, so the chain stays in
+          // the tables); each sequence's entries and position go to lane cnt by v_writelane.
           for (uint32_t cnt = 0; cnt < nb; cnt++) {
             const uint32_t ow = U(S.xo[sof]), mw = U(S.xm[sml]), lwd = U(S.xl[sll]);
-            bad_acc |= ow | mw | lwd;
-            const bool here = lane == (int)cnt;
-            r_p = here ? Pr : r_p;
-            r_o = here ? ow : r_o;
-            r_m = here ? mw : r_m;
-            r_l = here ? lwd : r_l;
-            const int32_t p3 = Pr - (int32_t)(((ow >> 13) & 31) + ((mw >> 13) & 31) + ((lwd >> 13) & 31));
+            // (the lane select goes through m0: gfx9 writelane reads one SGPR besides m0)
+            asm volatile(
+                "s_mov_b32 m0, %4\n\t"
+                "v_writelane_b32 %0, %5, m0\n\t"
+                "v_writelane_b32 %1, %6, m0\n\t"
+                "v_writelane_b32 %2, %7, m0\n\t"
+                "v_writelane_b32 %3, %8, m0"
+                : "+v"(r_p), "+v"(r_o), "+v"(r_m), "+v"(r_l)
+                : "s"(cnt), "s"(Pr), "s"(ow), "s"(mw), "s"(lwd)
+                : "m0");
+            p3 = Pr - (int32_t)(((ow >> 13) & 31) + ((mw >> 13) & 31) + ((lwd >> 13) & 31));
             const uint32_t nl = (lwd >> 9) & 15, nm = (mw >> 9) & 15, no = (ow >> 9) & 15;
             const int32_t q = p3 - (int32_t)(nl + nm + no);
             const uint64_t w = bits64(q);
             sof = (ow & 511) + ((uint32_t)w & ((1u << no) - 1));
             sml = (mw & 511) + ((uint32_t)(w >> no) & ((1u << nm) - 1));
             sll = (lwd & 511) + ((uint32_t)(w >> (no + nm)) & ((1u << nl) - 1));
-            Pr = done + cnt + 1 < nseq ? q : p3;  // the last sequence reads no state update
+            Pr = q;
           }
-          if (bad_acc & SQ_BAD) { bad = true; break; }
+          if (done + nb == nseq) Pr = p3;  // the block's last sequence reads no state update
+          if (__any(lane < (int)nb && ((r_o | r_m | r_l) & SQ_BAD))) { bad = true; break; }
           // lane l: sequence done + l's fields, from the three item words holding its extra bits
           const bool mine = lane < (int)nb;
           uint32_t ll = 0, ml = 0, ofv = 0;
