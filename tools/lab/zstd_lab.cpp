@@ -356,6 +356,8 @@ int main(int argc, char **argv) {
     printf("sequences: %.0f blocks with sequences, %.1f sequences/block, records visited %llu, epochs %llu | per block "
            "(clocks, wave sums): tables %.0f decode %.0f | per sequence: decode %.1f\n", nb / reps, z[2] / nb,
            z[5] / reps, z[4] / reps, z[0] / nb, z[1] / nb, z[1] / (double)(z[2] ? z[2] : 1));
+    printf("tables (k_zstd_blocks, per block with sequences): FSE descriptions parsed %.0f clocks, built %.0f clocks\n",
+           z[6] / nb, z[7] / nb);
   }
 #endif
   if (Z.ext_cnt) {

@@ -1843,10 +1843,15 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(ZG_BLK_WPE, 
           lg[t] = 0;
         } else {
           uint32_t acc, ns;
+          SQP_T(nc0);
           InW Ic(in, it.len);  // the description through a register window, not a load per byte
           if (!read_ncount(Ic, off, it.len - off, S.norm, maxs, maxl, acc, ns)) { bad = true; break; }
           __syncthreads();
+          SQP_T(nc1);
           build_fse(T, S.norm, ns, acc, S.tmp);
+          SQP_T(nc2);
+          SQP_ADD(6, nc1 - nc0);
+          SQP_ADD(7, nc2 - nc1);
           lg[t] = acc;
         }
         // value bases / extra bits folded into the decoding table
@@ -4450,9 +4455,16 @@ static hipError_t launch_zstd_pass(ZgItem *items, uint32_t *status, uint32_t n_i
     if (e == hipSuccess) e = hipStreamWaitEvent(Z.side, Z.ev_fork, 0);
     if (e != hipSuccess) return e;
   }
-  // one resident wave of the sequence decoder: CUs x 4 SIMDs x ZG_BLK_WPE waves
-  const uint32_t bgrid =
-      (uint32_t)std::min<uint64_t>(recs, std::max<uint64_t>(g_cap, (uint64_t)device_cu_count() * 4 * ZG_BLK_WPE));
+  // one resident wave of the sequence decoder: CUs x 4 SIMDs x ZG_BLK_WPE waves (ZGPU_ZSTD_BLK_WPE: fewer,
+  // leaving CU slots to concurrent plans' kernels; A/B)
+  static const uint64_t blk_wpe = [] {
+    const char *e = std::getenv("ZGPU_ZSTD_BLK_WPE");
+    const int v = e ? std::atoi(e) : 0;
+    return (uint64_t)(v > 0 && v <= ZG_BLK_WPE ? v : 0);
+  }();
+  const uint32_t bgrid = (uint32_t)std::min<uint64_t>(
+      recs, blk_wpe ? (uint64_t)device_cu_count() * 4 * blk_wpe
+                    : std::max<uint64_t>(g_cap, (uint64_t)device_cu_count() * 4 * ZG_BLK_WPE));
   // sequence decoder: 0 one wave per block (k_zstd_blocks, the split chain decoder: lab 64 L0 chunks
   // 1.63 ms against the lane groups' 5.0, C5 82.0 -> 74.7 ms, profiles/r06/r06pqr_*), 1 lane groups
   // (k_zstd_blocks_lg, the round-5 default); ZGPU_ZSTD_SEQ forces one
