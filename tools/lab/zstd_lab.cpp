@@ -148,6 +148,7 @@ int main(int argc, char **argv) {
   CK(hipMalloc(&Z.mode, n * 4));
   CK(hipMalloc(&Z.lit, n * Z.lit_stride));
   CK(hipMalloc(&Z.seq, n * Z.seq_cap * 12));
+  if (!getenv("LAB_NONORM")) CK(hipMalloc(&Z.norm, n * (uint64_t)Z.blk_cap * zgpu::zstd_norm_bytes()));
   if (getenv("LAB_EXEC") && !strcmp(getenv("LAB_EXEC"), "par")) {
     CK(hipMalloc(&Z.ext, 2 * (uint64_t)n * chunk * 4));
     CK(hipMalloc(&Z.ext_cnt, zgpu::ZEXT_ROUNDS * 8));
@@ -206,7 +207,7 @@ int main(int argc, char **argv) {
     CK(hipEventRecord(ev[0]));
     hipLaunchKernelGGL(zgpu::k_zstd_scan, dim3(n), dim3(64), 0, 0, d_items, d_status, blks, Z.blk_cap, Z.nblk, Z.mode,
                        Z.lit_stride, Z.seq_cap, 0u, (unsigned long long *)nullptr, (uint32_t *)nullptr,
-                       (unsigned long long *)nullptr, (unsigned long long *)nullptr);
+                       (unsigned long long *)nullptr, (unsigned long long *)nullptr, Z.norm);
     CK(hipEventRecord(ev[1]));
     const int seqm = getenv("LAB_SEQLG") ? atoi(getenv("LAB_SEQLG")) : 1;
     if (seqm == 1) {  // the lane-group sequence decoder, as launch_zstd_pass
@@ -219,7 +220,7 @@ int main(int argc, char **argv) {
     } else {
       hipLaunchKernelGGL(zgpu::k_zstd_blocks, dim3(bgrid), dim3(64), 0, 0, d_items, d_status, blks, Z.blk_cap,
                          Z.nblk, Z.mode, (uint32_t)n, Z.lit, Z.lit_stride, Z.seq, Z.seq_cap,
-                         (const unsigned long long *)nullptr);
+                         (const unsigned long long *)nullptr, Z.norm);
     }
     CK(hipEventRecord(ev[2]));
     hipLaunchKernelGGL(zgpu::k_zstd_huf, dim3(grid), dim3(64), 0, 0, d_items, d_status, blks, Z.blk_cap, Z.nblk, Z.mode,

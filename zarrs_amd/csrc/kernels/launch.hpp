@@ -97,6 +97,7 @@ struct ZstdScratch {
   uint32_t *seq;         // n_items * seq_cap sequences of 3 u32
   uint64_t seq_cap;
   uint32_t blk_cap;
+  int16_t *norm = nullptr;  // n_items * blk_cap * zstd_norm_bytes(): FSE counts the scan parsed (nullable)
   uint32_t force_serial = 0;               // every item on the serial one-wave decoder (tests, ZGPU_ZSTD_FORCE_SERIAL)
   unsigned long long *counters = nullptr;  // [serial-fallback items, block-parallel items] (nullable)
   // compacted serial-fallback items (nullable: the fallback then runs one wave per item): k_zstd_scan
@@ -144,6 +145,8 @@ constexpr uint64_t ZPAR_MAX_BYTES = 128ull << 20;
 constexpr uint32_t ZEXT_ROUNDS = 24;
 constexpr uint64_t ZALIAS_RLE = 1ull << 63;
 uint64_t zstd_lit_rec_bytes(uint32_t &wgs);
+// bytes of FSE-count scratch per block record (ZstdScratch::norm)
+uint64_t zstd_norm_bytes();
 void zstd_scratch_layout(uint64_t slot_bytes, uint32_t &blk_cap, uint64_t &blk_bytes, uint64_t &lit_stride,
                          uint64_t &seq_cap);
 hipError_t launch_zstd(ZgItem *items, uint32_t *status, uint32_t n_items, uint8_t *dst, uint64_t slot_bytes,

@@ -1168,6 +1168,9 @@ namespace {
 constexpr uint32_t ZB_RAW = 0, ZB_RLE = 1, ZB_CMP = 2;
 constexpr uint32_t ZBF_FIRST = 1u << 8, ZBF_LAST = 1u << 9, ZBF_FCS = 1u << 10, ZBF_CK = 1u << 11;
 constexpr uint32_t ZSYM = 0x80000000u;      // symbolic offset: ZSYM | slot << 24 | minus
+// normalized-count scratch: per block record 3 tables x 64 int16 (counts of symbols 0..52; [62] the
+// accuracy log, [63] the symbol count)
+constexpr uint32_t ZNORM = 3 * 64;
 
 struct ZBlk {
   uint32_t flags;             // bits 0-1 block type, 2-3 literal type, 4 four streams, ZBF_*
@@ -1179,6 +1182,8 @@ struct ZBlk {
   uint32_t nseq, seq_off, seq_end;  // sequence bitstream
   uint32_t tab_off[3];        // LL / OF / ML table source (rle: symbol byte; fse: NCount)
   uint32_t tab_mode;          // 2 bits per table: 0 predefined, 1 rle, 2 fse
+  uint32_t norm_src[3];       // fse: 1 + the block whose description k_zstd_scan parsed into the normalized
+                              // count scratch (ZNORM per block), 0: none (k_zstd_blocks parses tab_off)
   uint32_t lit_buf;           // literal scratch offset (huffman / rle literals)
   uint32_t seq_buf;           // first sequence in the item's sequence scratch
   uint32_t ck;                // frame checksum (last block of a frame with one)
@@ -1509,7 +1514,8 @@ __global__ __launch_bounds__(64) void k_zstd_scan(const ZgItem *items, uint32_t 
                                                   uint32_t blk_cap, uint32_t *nblk, uint32_t *zmode,
                                                   uint64_t lit_stride, uint64_t seq_cap, uint32_t force_serial,
                                                   unsigned long long *counters, uint32_t *ser_list,
-                                                  unsigned long long *ser_count, unsigned long long *max_nblk) {
+                                                  unsigned long long *ser_count, unsigned long long *max_nblk,
+                                                  int16_t *norms) {
   __shared__ ZScanSmem S;
   __shared__ ZScan2Smem Q;
   const uint32_t item = blockIdx.x;
@@ -1685,8 +1691,15 @@ __global__ __launch_bounds__(64) void k_zstd_scan(const ZgItem *items, uint32_t 
                 R.tab_off[t] = (uint32_t)p;
                 p += 1;
               } else if (mm[t] == 2) {
-                uint32_t acc, ns;
-                const uint32_t used = read_ncount<const InL, false>(L, p, bend - p, nullptr, maxs, maxl, acc, ns);
+                uint32_t acc, ns, used;
+                if (norms) {  // the counts kept for k_zstd_blocks (it then skips the serial parse)
+                  int16_t *nr = norms + ((uint64_t)item * blk_cap + bi) * ZNORM + t * 64;
+                  used = read_ncount<const InL, true>(L, p, bend - p, nr, maxs, maxl, acc, ns);
+                  nr[62] = (int16_t)acc;
+                  nr[63] = (int16_t)ns;
+                } else {
+                  used = read_ncount<const InL, false>(L, p, bend - p, nullptr, maxs, maxl, acc, ns);
+                }
                 if (!used) { e = ZG_CORRUPT_STREAM; break; }
                 R.tab_off[t] = (uint32_t)p;
                 p += used;
@@ -1711,6 +1724,7 @@ __global__ __launch_bounds__(64) void k_zstd_scan(const ZgItem *items, uint32_t 
   if (!serial && !err) {
     uint64_t lit_used = 0, seq_used = 0;
     uint32_t huf_src = TREE_NONE, tmode[3] = {3, 3, 3}, toff[3] = {0, 0, 0};  // 3 = no table yet
+    uint32_t tsrc[3] = {0, 0, 0};  // 1 + the block that defined each table (its counts in `norms`)
     for (uint32_t bi = 0; bi < nb; bi++) {
       ZBlk &R = Q.R[bi];
       const uint32_t flags = U(R.flags);
@@ -1747,6 +1761,7 @@ __global__ __launch_bounds__(64) void k_zstd_scan(const ZgItem *items, uint32_t 
           } else {
             tmode[t] = m;
             toff[t] = U(R.tab_off[t]);
+            tsrc[t] = (m == 2 && norms) ? bi + 1 : 0u;
           }
         }
         if (!ok) { err = ZG_CORRUPT_STREAM; nbv = bi; break; }
@@ -1763,6 +1778,9 @@ __global__ __launch_bounds__(64) void k_zstd_scan(const ZgItem *items, uint32_t 
           R.tab_off[0] = toff[0];
           R.tab_off[1] = toff[1];
           R.tab_off[2] = toff[2];
+          R.norm_src[0] = tsrc[0];
+          R.norm_src[1] = tsrc[1];
+          R.norm_src[2] = tsrc[2];
         }
         R.seq_buf = seq_buf;
       }
@@ -1790,7 +1808,7 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(ZG_BLK_WPE, 
                                                     uint32_t blk_cap, const uint32_t *nblk,
                                                     const uint32_t *zmode, uint32_t n_items, uint8_t *lit_scratch,
                                                     uint64_t lit_stride, uint32_t *seq_scratch, uint64_t seq_cap,
-                                                    const unsigned long long *max_nblk) {
+                                                    const unsigned long long *max_nblk, const int16_t *norms) {
   __shared__ ZDecSmem S;
   const int lane = lane_id();
   const uint64_t total = (uint64_t)n_items * rec_blocks(blk_cap, max_nblk);
@@ -1844,8 +1862,17 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(ZG_BLK_WPE, 
         } else {
           uint32_t acc, ns;
           SQP_T(nc0);
-          InW Ic(in, it.len);  // the description through a register window, not a load per byte
-          if (!read_ncount(Ic, off, it.len - off, S.norm, maxs, maxl, acc, ns)) { bad = true; break; }
+          const uint32_t nsrc = U(Bp->norm_src[t]);
+          if (norms && nsrc) {  // counts the scan parsed (its lanes, one block each, in parallel)
+            const int16_t *nr = norms + ((uint64_t)item * blk_cap + (nsrc - 1)) * ZNORM + t * 64;
+            const int16_t v = nr[lane];
+            acc = (uint32_t)nr[62];
+            ns = (uint32_t)nr[63];
+            S.norm[lane] = v;
+          } else {
+            InW Ic(in, it.len);  // the description through a register window, not a load per byte
+            if (!read_ncount(Ic, off, it.len - off, S.norm, maxs, maxl, acc, ns)) { bad = true; break; }
+          }
           __syncthreads();
           SQP_T(nc1);
           build_fse(T, S.norm, ns, acc, S.tmp);
@@ -4387,6 +4414,7 @@ uint64_t zstd_lit_rec_bytes(uint32_t &wgs) {
   wgs = on ? (uint32_t)cap : 0u;
   return on ? cap * LIT_THREADS * REC_SLOT : 0ull;
 }
+uint64_t zstd_norm_bytes() { return ZNORM * sizeof(int16_t); }
 void zstd_scratch_layout(uint64_t slot_bytes, uint32_t &blk_cap, uint64_t &blk_bytes, uint64_t &lit_stride,
                          uint64_t &seq_cap) {
   blk_cap = (uint32_t)std::min<uint64_t>(slot_bytes / 32768 + 64, 1u << 20);
@@ -4406,7 +4434,7 @@ static hipError_t launch_zstd_pass(ZgItem *items, uint32_t *status, uint32_t n_i
   const bool listed = Z.ser_list && Z.ser_count;
   hipLaunchKernelGGL(k_zstd_scan, dim3(n_items), dim3(64), 0, s, items, status, blks, Z.blk_cap, Z.nblk, Z.mode,
                      Z.lit_stride, Z.seq_cap, Z.force_serial, Z.counters, listed ? Z.ser_list : nullptr,
-                     listed ? Z.ser_count : nullptr, Z.max_nblk);
+                     listed ? Z.ser_count : nullptr, Z.max_nblk, Z.norm);
   const uint64_t recs = (uint64_t)n_items * Z.blk_cap;
   // grids of the record-strided entropy kernels (overridable for tuning: ZGPU_ZSTD_GRID, ZGPU_ZSTD_LGRID)
   static const uint64_t g_cap = [] {
@@ -4485,7 +4513,7 @@ static hipError_t launch_zstd_pass(ZgItem *items, uint32_t *status, uint32_t n_i
                          Z.nblk, Z.mode, n_items, Z.seq, Z.seq_cap, Z.max_nblk);
     } else {
       hipLaunchKernelGGL(k_zstd_blocks, dim3(bgrid), dim3(64), 0, sq, items, status, blks, Z.blk_cap, Z.nblk, Z.mode,
-                         n_items, Z.lit, Z.lit_stride, Z.seq, Z.seq_cap, Z.max_nblk);
+                         n_items, Z.lit, Z.lit_stride, Z.seq, Z.seq_cap, Z.max_nblk, Z.norm);
     }
   };
   if (!lits_first) launch_seq();

@@ -390,7 +390,7 @@ struct zgpu_plan {
     size_t n = 0;
   };
   Grow bl_info, bl_bases, bl_subs, bl_sub_status, bl_sub_kind, bl_blocks, bl_tmp, bl_zblks, bl_znblk, bl_zmode,
-      bl_zlit, bl_zseq, bl_zaux, bl_zser, bl_lzl, bl_zseg, bl_zrec, bl_zalias;
+      bl_zlit, bl_zseq, bl_zaux, bl_zser, bl_lzl, bl_zseg, bl_zrec, bl_zalias, bl_znorm;
   uint8_t *bl_h = nullptr;  // pinned: BlInfo read-back (first execution)
   size_t bl_h_n = 0;
   void *grow(Grow &g, size_t bytes) {
@@ -440,7 +440,7 @@ struct zgpu_plan {
     void *bufs[] = {d_items, d_items_init, d_geom, d_shards, d_index, d_shard_status, d_mids, d_mids_init,
                     d_mid_status, d_shard_status2, d_mid_shards, d_index2, d_bl_need,
                     d_pool[0], d_pool[1], zs.blks, zs.nblk, zs.mode, zs.lit, zs.seq, d_ctl,
-                    d_enc_stage, d_zser, d_order, d_gz_seg, zs.lit_rec, zs.ext, zs.ext_cnt};
+                    d_enc_stage, d_zser, d_order, d_gz_seg, zs.lit_rec, zs.ext, zs.ext_cnt, zs.norm};
     for (void *b : bufs) ctx->dev_free(b);
     if (zside) {
       (void)hipStreamSynchronize(zside);
@@ -455,7 +455,8 @@ struct zgpu_plan {
     for (hipEvent_t e : zev)
       if (e) (void)hipEventDestroy(e);
     for (Grow *g : {&bl_info, &bl_bases, &bl_subs, &bl_sub_status, &bl_sub_kind, &bl_blocks, &bl_tmp, &bl_zblks,
-                    &bl_znblk, &bl_zmode, &bl_zlit, &bl_zseq, &bl_zaux, &bl_zser, &bl_lzl, &bl_zseg, &bl_zrec, &bl_zalias})
+                    &bl_znblk, &bl_zmode, &bl_zlit, &bl_zseq, &bl_zaux, &bl_zser, &bl_lzl, &bl_zseg, &bl_zrec, &bl_zalias,
+                    &bl_znorm})
       ctx->dev_free(g->p);
     ctx->host_free(bl_h);
     ctx->host_free(h_ctl);
@@ -905,6 +906,7 @@ static void plan_upload(zgpu_plan &P, hipStream_t us) {
         uint64_t blk_bytes;
         zstd_scratch_layout(P.slot_bytes, P.zs.blk_cap, blk_bytes, P.zs.lit_stride, P.zs.seq_cap);
         P.zs.blks = C.dev_alloc(ni * (uint64_t)P.zs.blk_cap * blk_bytes);
+        P.zs.norm = (int16_t *)C.dev_alloc(ni * (uint64_t)P.zs.blk_cap * zstd_norm_bytes());
         P.zs.nblk = (uint32_t *)C.dev_alloc(ni * 4);
         P.zs.mode = (uint32_t *)C.dev_alloc(ni * 4);
         P.zs.lit = (uint8_t *)C.dev_alloc(ni * P.zs.lit_stride);
@@ -1034,6 +1036,7 @@ static void blosc_stage(zgpu_plan &P, const Stage &st, uint8_t *out, hipStream_t
     uint64_t blk_bytes;
     zstd_scratch_layout(D.sub_slot, D.zs.blk_cap, blk_bytes, D.zs.lit_stride, D.zs.seq_cap);
     D.zs.blks = P.grow(P.bl_zblks, D.n_sub * (uint64_t)D.zs.blk_cap * blk_bytes);
+    D.zs.norm = (int16_t *)P.grow(P.bl_znorm, D.n_sub * (uint64_t)D.zs.blk_cap * zstd_norm_bytes());
     D.zs.nblk = (uint32_t *)P.grow(P.bl_znblk, D.n_sub * 4);
     D.zs.mode = (uint32_t *)P.grow(P.bl_zmode, D.n_sub * 4);
     D.zs.lit = (uint8_t *)P.grow(P.bl_zlit, D.n_sub * D.zs.lit_stride);
