@@ -4126,11 +4126,14 @@ __global__ __launch_bounds__(LIT_THREADS) __attribute__((amdgpu_waves_per_eu(ZG_
 // not inside a checksummed frame); each segment gets its own k_zstd_exec_item wave. Byte-shuffled
 // images cut at their byte planes (tools/lab/zstd_taint.cpp: no match crosses the plane boundary).
 #ifndef ZG_XSEG
-#define ZG_XSEG 3
+#define ZG_XSEG 12
 #endif
-// executor segments per item (at most; ZGPU_ZSTD_XSEG overrides it at run time). With the
-// segment-major executor grid (zstd_exec.inc), 2, 3, 4 and 8 measure within 1 % on C5 and
-// blosc-zstd, 3 best on both (profiles/r05/r05xs_zstd_exec_segment_major_xcd_ab.txt)
+// executor segments per item of the wave executor (at most; ZGPU_ZSTD_XSEG overrides it for both
+// executors, ZGPU_ZSTD_XSEG_WIDE for this one). Round 5 measured 2, 3, 4 and 8 within 1 % with 3 best
+// (profiles/r05/r05xs_zstd_exec_segment_major_xcd_ab.txt); with round 6's faster sequence decoder
+// and the plan group the L0 executors end the C5 step, and more segments shorten them: C5 73.2 (3),
+// 72.5 (8), 70.8 (12), 71.3 (16), 103 (32) ms (profiles/r06/r06zfg_*); blosc-zstd's 2-block frames
+// cut into 2 at most either way
 constexpr uint32_t XSEG = ZG_XSEG;
 
 __global__ __launch_bounds__(64) void k_zstd_plan(const ZgItem *items, uint32_t *status, ZBlk *blks,
@@ -4476,7 +4479,17 @@ static hipError_t launch_zstd_pass(ZgItem *items, uint32_t *status, uint32_t n_i
   const char *xwpc_s = std::getenv("ZGPU_ZSTD_XWIN_WPC");  // the threshold's waves per CU (A/B)
   const uint64_t xwpc = xwpc_s ? (uint64_t)std::atoi(xwpc_s) : ZG_XWIN_MAX_WPC;
   const bool xwin_on = xw_env >= 0 ? xw_env != 0 : (uint64_t)n_items * XSEG < (uint64_t)device_cu_count() * xwpc;
-  const uint32_t xseg = xseg_env ? xseg_env : xwin_on ? XSEG_WIN : XSEG;
+  static const uint32_t xseg_wide_env = [] {  // A/B: the wave executor's segments only
+    const char *e = std::getenv("ZGPU_ZSTD_XSEG_WIDE");
+    return e ? (uint32_t)std::min<unsigned long>(64, std::max<unsigned long>(1, std::strtoul(e, nullptr, 10))) : 0u;
+  }();
+  static const uint32_t xseg_win_env = [] {  // A/B: the window executor's segments only
+    const char *e = std::getenv("ZGPU_ZSTD_XSEG_WIN");
+    return e ? (uint32_t)std::min<unsigned long>(64, std::max<unsigned long>(1, std::strtoul(e, nullptr, 10))) : 0u;
+  }();
+  const uint32_t xseg = xseg_env               ? xseg_env
+                        : xwin_on              ? (xseg_win_env ? xseg_win_env : XSEG_WIN)
+                                               : (xseg_wide_env ? xseg_wide_env : XSEG);
 
   if (fork) {
     hipError_t e = hipEventRecord(Z.ev_fork, s);
