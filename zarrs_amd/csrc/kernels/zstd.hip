@@ -4478,7 +4478,9 @@ static hipError_t launch_zstd_pass(ZgItem *items, uint32_t *status, uint32_t n_i
   const int xw_env = xw_s ? std::atoi(xw_s) : -1;
   const char *xwpc_s = std::getenv("ZGPU_ZSTD_XWIN_WPC");  // the threshold's waves per CU (A/B)
   const uint64_t xwpc = xwpc_s ? (uint64_t)std::atoi(xwpc_s) : ZG_XWIN_MAX_WPC;
-  const bool xwin_on = xw_env >= 0 ? xw_env != 0 : (uint64_t)n_items * XSEG < (uint64_t)device_cu_count() * xwpc;
+  // (the threshold counts 3 waves per item, round 5's segment count: C5's L1 and small levels take the
+  // window executor, its L0 halves the wave executor)
+  const bool xwin_on = xw_env >= 0 ? xw_env != 0 : (uint64_t)n_items * 3 < (uint64_t)device_cu_count() * xwpc;
   static const uint32_t xseg_wide_env = [] {  // A/B: the wave executor's segments only
     const char *e = std::getenv("ZGPU_ZSTD_XSEG_WIDE");
     return e ? (uint32_t)std::min<unsigned long>(64, std::max<unsigned long>(1, std::strtoul(e, nullptr, 10))) : 0u;
