@@ -126,7 +126,10 @@ int zgpu_group_create(zgpu_chain *const *chains, uint32_t nd, uint32_t n_parts, 
     }
     const uint32_t n_lanes_min = (uint32_t)big.size() + (small.empty() ? 0u : 1u);
     const uint32_t extra = live.size() > 1 && max_lanes > n_lanes_min ? max_lanes - n_lanes_min : 0u;
-    const uint32_t lf_mask = env_u32("ZGPU_GROUP_LITS_FIRST", ~0u);  // lanes decoding literals first (A/B)
+    const uint32_t lf_mask = env_u32("ZGPU_GROUP_LITS_FIRST", ~0u);  // lanes allowed literals-first (A/B)
+    const char *lf_force_s = std::getenv("ZGPU_GROUP_LF_FORCE");     // A/B: lane i literals-first iff bit i
+    const bool lf_forced = lf_force_s && *lf_force_s;
+    const uint32_t lf_force = lf_forced ? (uint32_t)std::strtoul(lf_force_s, nullptr, 0) : 0u;
     const bool multi = n_lanes_min + extra > 1;
     auto add_piece = [&](uint32_t part, const std::vector<uint64_t> &which, uint32_t lane, bool lits_first) -> int {
       std::vector<zgpu_chunk_desc> d;
@@ -134,6 +137,7 @@ int zgpu_group_create(zgpu_chain *const *chains, uint32_t nd, uint32_t n_parts, 
       zgpu_group::Piece pc;
       pc.part = part;
       pc.lane = lane;
+      if (lf_forced) lits_first = (lf_force >> lane) & 1u;
       pc.lits_first = lits_first ? 1u : 0u;
       for (uint64_t i : which) {
         d.push_back(descs[part][i]);
