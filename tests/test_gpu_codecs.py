@@ -216,6 +216,26 @@ def test_zstd_multiblock_frames(level):
         assert np.array_equal(got[i], d), (i, kinds[i])
 
 
+@pytest.mark.parametrize("level", [3, 9])
+def test_zstd_frames_beyond_the_scan_lds(level):
+    """20 MiB frames: 160 blocks, more than k_zstd_scan's three-pass path holds in LDS (144 block
+    records), so the frame is walked by the uniform scan and the sequence decoder parses the FSE table
+    descriptions itself (no scan-parsed counts for these blocks); bit-exact vs libzstd."""
+    rng = np.random.default_rng(300 + level)
+    codecs = [BYTES_LE, {"name": "zstd", "configuration": {"level": level, "checksum": True}}]
+    oc = O.OracleChain.from_metadata(codecs, "uint8", 0, 1)
+    n = 20 << 20
+    z = np.arange(n // 2, dtype=np.float32)
+    u16 = np.clip(100 + 3000 * np.exp(-((z % 65536) - 30000) ** 2 / 2e7) + rng.normal(0, 10, n // 2), 0,
+                  65535).astype(np.uint16)
+    data = [_content(rng, n, "text"), np.concatenate([u16.view(np.uint8)[0::2], u16.view(np.uint8)[1::2]])]
+    encs = [oc.encode(d) for d in data]
+    st, got = _zstd_batch(codecs, encs, n)
+    assert st == [0] * len(encs)
+    for i, d in enumerate(data):
+        assert np.array_equal(got[i], d), i
+
+
 def test_zstd_concatenated_and_skippable_frames():
     """Several frames (and a skippable frame) in one chunk decode to the concatenation
     (zstd bulk decompress semantics, zstd_codec.rs:113-130)."""
