@@ -92,12 +92,16 @@ def ctx():
     return Context(0)
 
 
+@pytest.mark.parametrize("gz_direct", ["1", "0"], ids=["direct_rows", "slot_scatter"])
 @pytest.mark.parametrize("gzip_kernel", ["pipelined", "one_wave"])
 @pytest.mark.parametrize("store", ["hbm", "host"])
-def test_c3_chain_full_and_partial(ctx, c3, store, gzip_kernel, monkeypatch):
+def test_c3_chain_full_and_partial(ctx, c3, store, gzip_kernel, gz_direct, monkeypatch):
     """Both k_gzip kernels: batches of <= 2048 streams take the two-wave pipelined one unless
-    ZGPU_GZIP_PIPE_MAX (read per launch) lowers the threshold; 0 forces the one-wave kernel."""
+    ZGPU_GZIP_PIPE_MAX (read per launch) lowers the threshold; 0 forces the one-wave kernel.
+    gz_direct: whole inner chunks written into the output rows by k_gzip (ZGPU_GZIP_DIRECT, read per
+    plan) or through the slot and the rows scatter."""
     from zarrs_amd import ZgpuError
+    monkeypatch.setenv("ZGPU_GZIP_DIRECT", gz_direct)
     if gzip_kernel == "one_wave":
         monkeypatch.setenv("ZGPU_GZIP_PIPE_MAX", "0")
     a, co, shards = c3

@@ -51,6 +51,20 @@ struct ZgScatter {
   uint8_t fill[16];
 };
 
+// k_gzip writing whole chunks straight into the output rows (the gzip stage last before a rows scatter
+// with no swap / shuffle / transpose): an item whose selection is its whole chunk and whose output
+// rows are 16-B aligned is decoded into the array, flagged ZG_ITEM_DIRECT, and the scatter skips it.
+// Chunk byte p lives in row p >> lbs (C order over the leading axes) at column p & (2^lbs - 1).
+struct GzDirect {
+  uint8_t *dout;         // output array; nullptr: every item decodes into its slot
+  const uint64_t *geom;  // per item: sel_start | sel_shape | out_start (ZG_MAXD-free: 3 * nd)
+  uint64_t want;         // decoded bytes of a whole chunk
+  uint64_t cshape[4];    // chunk shape
+  uint64_t ostr[4];      // output byte stride of each axis
+  uint32_t nd;           // <= 3 (axis 1 of a 3-d chunk has a power-of-two extent); byte strides < 4 GiB
+  uint32_t lbs;          // log2 of the row bytes (chunk_shape[nd-1] * es, >= 16)
+};
+
 // device status codes (== zgpu.h)
 #define ZG_OK 0u
 #define ZG_INVALID_CHECKSUM 1u

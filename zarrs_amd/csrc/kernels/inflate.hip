@@ -657,14 +657,72 @@ __device__ inline uint32_t wave_crc(const uint8_t *p, uint64_t n, const CrcTable
   return U(__shfl(c, 0, 64));
 }
 
-__device__ __forceinline__ void flush(const Smem &S, uint8_t *out, uint64_t cap, uint64_t from, uint64_t to) {
+// Where decoded byte p of a stream lives: its slot (base + p), or, for a direct item (GzDirect), the
+// output array: row p >> lbs of the chunk, whose index splits over the row axes innermost first
+// (extent 2^sh[k] each, the outermost unbounded), at column p & (2^lbs - 1). 16-B pieces never
+// straddle a row (rows are multiples of 16 bytes on 16-B aligned addresses).
+#ifndef ZG_GZ_DIRECT_READS
+#define ZG_GZ_DIRECT_READS 0  // 1: a direct item lives only in the array (sources older than the ring read
+                              // back from its rows, no slot copy); 0: the slot is written too (A/B)
+#endif
+struct OutMap {
+  uint8_t *slot;  // the item's slot: always written (sources older than the ring are read back from it)
+  uint8_t *base;
+  uint32_t o0, o1;  // output byte stride of the inner and the outer row axis (nd 3; nd 2: o0 only)
+  uint32_t cfg;     // bit 31: direct; bits 0-7: lbs; bits 8-15: log2 of the inner row axis' extent
+  uint32_t want;    // the chunk's bytes: a stream decoding longer writes only its slot past them
+  __device__ __forceinline__ uint8_t *at(uint64_t p) const {
+    const uint32_t lbs = cfg & 255, sh = (cfg >> 8) & 255;
+    const uint32_t r = (uint32_t)(p >> lbs);
+    return base + (p & ((1ull << lbs) - 1)) + (uint64_t)(r & ((1u << sh) - 1u)) * o0 + (uint64_t)(r >> sh) * o1;
+  }
+  __device__ __forceinline__ const uint8_t *rd(uint64_t p) const {  // a source byte older than the ring
+    return (ZG_GZ_DIRECT_READS && (cfg >> 31) && p < want) ? at(p) : slot + p;
+  }
+};
+
+#if ZG_GZ_DIRECT_READS
+// The CRC of decoded bytes [0, n) of a direct item: wave_crc's lane segments, each run over its row pieces.
+__device__ inline uint32_t wave_crc_map(const OutMap &O, uint64_t n, const CrcTables &T, uint32_t poly) {
+  if (!(O.cfg >> 31) || n > O.want) return wave_crc(O.slot, n, T, poly);
+  const uint32_t l = (uint32_t)lane_id(), lbs = O.cfg & 255;
+  uint64_t seg = (n + 63) / 64;
+  seg = (seg + 15) & ~(uint64_t)15;
+  const uint64_t b0 = min<uint64_t>((uint64_t)l * seg, n), b1 = min<uint64_t>(b0 + seg, n);
+  uint32_t c = 0xFFFFFFFFu;
+  for (uint64_t q = b0; q < b1;) {
+    const uint64_t e = min<uint64_t>(b1, ((q >> lbs) + 1) << lbs);
+    c = crc_run(c, O.at(q), e - q, T);
+    q = e;
+  }
+  c = ~c;
+  uint64_t len = b1 - b0;
+  for (int off = 1; off < 64; off <<= 1) {
+    const uint32_t c2 = __shfl_down(c, off, 64);
+    const uint64_t l2 = __shfl_down(len, off, 64);
+    if (l % (2 * off) == 0 && l + off < 64) {
+      c = crc_combine(c, c2, l2, T.x2n, poly);
+      len += l2;
+    }
+  }
+  return U(__shfl(c, 0, 64));
+}
+#endif
+
+__device__ __forceinline__ void flush(const Smem &S, const OutMap &O, uint64_t cap, uint64_t from, uint64_t to) {
   const uint64_t a = from & ~(uint64_t)15, b = (to + 15) & ~(uint64_t)15;
   for (uint64_t p = a + (uint64_t)lane_id() * 16; p < b; p += 64 * 16) {
     if (p + 16 <= cap) {
       const uint4 v = *(const uint4 *)&S.ring[p & RMASK];
-      *(uint4 *)(out + p) = v;
+      const bool d = (O.cfg >> 31) && p < O.want;  // want is a multiple of 16
+      if (!ZG_GZ_DIRECT_READS || !d) *(uint4 *)(O.slot + p) = v;
+      if (d) *(uint4 *)O.at(p) = v;
     } else {
-      for (uint64_t q = p; q < cap && q < p + 16; q++) out[q] = S.ring[q & RMASK];
+      for (uint64_t q = p; q < cap && q < p + 16; q++) {
+        const bool d = (O.cfg >> 31) && q < O.want;
+        if (!ZG_GZ_DIRECT_READS || !d) O.slot[q] = S.ring[q & RMASK];
+        if (d) *O.at(q) = S.ring[q & RMASK];
+      }
     }
   }
 }
@@ -795,7 +853,7 @@ __device__ __forceinline__ uint64_t shfl_up64(uint64_t v) {
 #define XPROF(k, n)
 #endif
 template <class SM>
-__device__ __forceinline__ bool exec_batch(SM &S, uint8_t *out, uint64_t cap, uint64_t &pos, uint64_t &flushed,
+__device__ __forceinline__ bool exec_batch(SM &S, const OutMap &O, uint64_t cap, uint64_t &pos, uint64_t &flushed,
                                            uint32_t cnt, uint32_t bytes, uint32_t rec_in, uint64_t *pa) {
   (void)pa;
   const int lane = lane_id();
@@ -918,7 +976,7 @@ __device__ __forceinline__ bool exec_batch(SM &S, uint8_t *out, uint64_t cap, ui
         if (rm < 0) rm += fd;
         if (rm >= (int32_t)fd) rm -= fd;
         const uint64_t src = F - fd + (uint32_t)rm;
-        v[j] = i < flen ? ((src + RING >= batch_end) ? S.ring[src & RMASK] : __builtin_nontemporal_load(out + src)) : 0;
+        v[j] = i < flen ? ((src + RING >= batch_end) ? S.ring[src & RMASK] : __builtin_nontemporal_load(O.rd(src))) : 0;
       }
 #pragma unroll
       for (int j = 0; j < 5; j++) {
@@ -975,7 +1033,7 @@ __device__ __forceinline__ bool exec_batch(SM &S, uint8_t *out, uint64_t cap, ui
         for (int k = 0; k < 4; k++) {
           const uint32_t i = i0 + k;
           const uint64_t src = msrc + r;
-          v[k] = (i < mlen) ? (in_ring ? S.ring[src & RMASK] : __builtin_nontemporal_load(out + src)) : 0;
+          v[k] = (i < mlen) ? (in_ring ? S.ring[src & RMASK] : __builtin_nontemporal_load(O.rd(src))) : 0;
           r = r + 1 == md ? 0u : r + 1;
         }
 #pragma unroll
@@ -1009,7 +1067,7 @@ __device__ __forceinline__ bool exec_batch(SM &S, uint8_t *out, uint64_t cap, ui
         if (rm < 0) rm += fd;
         if (rm >= (int32_t)fd) rm -= fd;
         const uint64_t src = F - fd + (uint32_t)rm;
-        const uint8_t v = (src + RING >= batch_end) ? S.ring[src & RMASK] : __builtin_nontemporal_load(out + src);
+        const uint8_t v = (src + RING >= batch_end) ? S.ring[src & RMASK] : __builtin_nontemporal_load(O.rd(src));
         S.ring[(F + i) & RMASK] = v;
       }
       if (lane == first) pending = false;
@@ -1063,7 +1121,7 @@ __device__ __forceinline__ bool exec_batch(SM &S, uint8_t *out, uint64_t cap, ui
         for (int k = 0; k < 4; k++) {
           const uint32_t i = i0 + k;
           const uint64_t src = msrc + r;
-          v[k] = (i < mlen) ? (in_ring ? S.ring[src & RMASK] : __builtin_nontemporal_load(out + src)) : 0;
+          v[k] = (i < mlen) ? (in_ring ? S.ring[src & RMASK] : __builtin_nontemporal_load(O.rd(src))) : 0;
           r = r + 1 == md ? 0u : r + 1;
         }
 #pragma unroll
@@ -1077,7 +1135,7 @@ __device__ __forceinline__ bool exec_batch(SM &S, uint8_t *out, uint64_t cap, ui
   pos = batch_end;
   if (pos - flushed >= FLUSH_MIN) {
     wsync();
-    flush(S, out, cap, flushed, pos);
+    flush(S, O, cap, flushed, pos);
     flushed = pos;
     wsync();
   }
@@ -1098,7 +1156,7 @@ __device__ __forceinline__ bool exec_batch(SM &S, uint8_t *out, uint64_t cap, ui
 template <bool ZLIB, bool PIPE = false>
 __global__ __launch_bounds__(PIPE ? 128 : 64) __attribute__((amdgpu_waves_per_eu(PIPE ? 4 : ZG_INFLATE_WPE, 8))) void k_gzip(
     ZgItem *items, uint32_t *status, const uint32_t *kind, uint8_t *dst, uint64_t slot_bytes, uint2 *aux,
-    const uint32_t *order, uint32_t *seg_scr, int crc_tail) {
+    const uint32_t *order, uint32_t *seg_scr, int crc_tail, GzDirect gd) {
   static_assert(!(ZLIB && PIPE), "the pipelined mode is for gzip streams");
   __shared__ std::conditional_t<PIPE, SmemP, Smem> S;
 #if !ZG_INFLATE_XFETCH
@@ -1113,6 +1171,31 @@ __global__ __launch_bounds__(PIPE ? 128 : 64) __attribute__((amdgpu_waves_per_eu
   const int lane = lane_id();
   uint8_t *out = dst + (uint64_t)item * slot_bytes;
   const uint64_t cap = slot_bytes;
+  OutMap O;
+  O.slot = O.base = out;
+  O.cfg = O.want = 0;
+  O.o0 = O.o1 = 0;
+  if (!ZLIB && gd.dout && !(it.flags & ZG_ITEM_PARTIAL)) {
+    // a whole chunk on 16-B aligned output rows: decoded straight into the array (GzDirect)
+    const uint32_t nd = gd.nd;
+    const uint64_t *g = gd.geom + (uint64_t)item * 3 * nd;
+    bool whole = true;
+    uint64_t off = 0;
+    for (uint32_t d = 0; d < nd; d++) {
+      whole = whole && g[d] == 0 && g[nd + d] == gd.cshape[d];
+      off += g[2 * nd + d] * gd.ostr[d];
+    }
+    uint8_t *b = gd.dout + off;
+    if (whole && ((uintptr_t)b & 15) == 0) {
+      // rows: nd 1 one row; nd 2 row index r -> r * ostr[0]; nd 3 (r mod n1) * ostr[1] + (r / n1) * ostr[0]
+      O.base = b;
+      const uint32_t sh = nd == 3 ? (uint32_t)__builtin_ctzll(gd.cshape[1]) : 31u;
+      O.o0 = nd == 3 ? (uint32_t)gd.ostr[1] : nd == 2 ? (uint32_t)gd.ostr[0] : 0u;
+      O.o1 = nd == 3 ? (uint32_t)gd.ostr[0] : 0u;
+      O.cfg = 0x80000000u | gd.lbs | (sh << 8);
+      O.want = (uint32_t)gd.want;
+    }
+  }
   const uint8_t *in = (const uint8_t *)it.src;
   uint64_t in_len = it.len;
   // The crc32c codec after gzip (C3's inner chain [bytes, gzip, crc32c]; crc32c_codec.rs:108-141)
@@ -1297,7 +1380,7 @@ __global__ __launch_bounds__(PIPE ? 128 : 64) __attribute__((amdgpu_waves_per_eu
             break;
           }
           if (g + bc < total) rec_next = fetch(g + bc);  // in flight while this batch executes
-          if (!exec_batch(S, out, cap, xpos, xfl, bc, bytes, rec, nullptr)) xerr = ZG_CORRUPT_STREAM;
+          if (!exec_batch(S, O, cap, xpos, xfl, bc, bytes, rec, nullptr)) xerr = ZG_CORRUPT_STREAM;
           g += bc;
         }
       }
@@ -1323,7 +1406,7 @@ __global__ __launch_bounds__(PIPE ? 128 : 64) __attribute__((amdgpu_waves_per_eu
         const uint32_t n = min<uint32_t>(ln - done, BATCH_CAP);
         for (uint32_t k = lane; k < n; k += 64) S.ring[(pos + k) & RMASK] = in[byte0 + done + k];
         wsync();
-        flush(S, out, cap, flushed, pos + n);
+        flush(S, O, cap, flushed, pos + n);
         pos += n;
         flushed = pos;
         done += n;
@@ -1637,9 +1720,9 @@ __global__ __launch_bounds__(PIPE ? 128 : 64) __attribute__((amdgpu_waves_per_eu
           pos += bytes;
           if (__ballot(rec == 0xFFFFFFFFu)) err = ZG_CORRUPT_STREAM;
 #elif defined(ZG_PROFILE)
-          if (!exec_batch(S, out, cap, pos, flushed, bc, bytes, rec, prof_acc)) err = ZG_CORRUPT_STREAM;
+          if (!exec_batch(S, O, cap, pos, flushed, bc, bytes, rec, prof_acc)) err = ZG_CORRUPT_STREAM;
 #else
-          if (!exec_batch(S, out, cap, pos, flushed, bc, bytes, rec, nullptr)) err = ZG_CORRUPT_STREAM;
+          if (!exec_batch(S, O, cap, pos, flushed, bc, bytes, rec, nullptr)) err = ZG_CORRUPT_STREAM;
 #endif
           g += bc;
         }
@@ -1808,9 +1891,9 @@ __global__ __launch_bounds__(PIPE ? 128 : 64) __attribute__((amdgpu_waves_per_eu
       PROF_T(t_exe);
       wsync();
 #ifdef ZG_PROFILE
-      if (!exec_batch(S, out, cap, pos, flushed, cnt, bytes, S.rec[lane], prof_acc)) { err = ZG_CORRUPT_STREAM; break; }
+      if (!exec_batch(S, O, cap, pos, flushed, cnt, bytes, S.rec[lane], prof_acc)) { err = ZG_CORRUPT_STREAM; break; }
 #else
-      if (!exec_batch(S, out, cap, pos, flushed, cnt, bytes, S.rec[lane], nullptr)) { err = ZG_CORRUPT_STREAM; break; }
+      if (!exec_batch(S, O, cap, pos, flushed, cnt, bytes, S.rec[lane], nullptr)) { err = ZG_CORRUPT_STREAM; break; }
 #endif
       PROF_ADD(2, t_exe);
     }
@@ -1823,7 +1906,7 @@ __global__ __launch_bounds__(PIPE ? 128 : 64) __attribute__((amdgpu_waves_per_eu
   }
   if (!err && flushed < pos) {
     wsync();
-    flush(S, out, cap, flushed, pos);
+    flush(S, O, cap, flushed, pos);
     flushed = pos;
   }
   if (!err) {
@@ -1850,7 +1933,11 @@ __global__ __launch_bounds__(PIPE ? 128 : 64) __attribute__((amdgpu_waves_per_eu
         wsync();
         PROF_T(t_crc);
         wave_crc_tables(S.crc, POLY_CRC32);
+#if ZG_GZ_DIRECT_READS
+        const uint32_t c = wave_crc_map(O, pos, S.crc, POLY_CRC32);
+#else
         const uint32_t c = wave_crc(out, pos, S.crc, POLY_CRC32);
+#endif
         PROF_ADD(11, t_crc);
         if (c != crc || isz != (uint32_t)pos) err = ZG_CORRUPT_STREAM;
       }
@@ -1863,6 +1950,10 @@ __global__ __launch_bounds__(PIPE ? 128 : 64) __attribute__((amdgpu_waves_per_eu
       items[item].src = (uint64_t)out;
       items[item].len = pos;
       if (ZLIB) status[item] = 0;
+      if (O.cfg >> 31) {  // in the array already: the scatter skips it (its size check is made here)
+        if (pos != O.want) status[item] = ZG_DECODED_SIZE_MISMATCH;
+        else items[item].flags = it.flags | ZG_ITEM_DIRECT;
+      }
     }
   }
   PROF_ADD(4, t_all);
@@ -1928,7 +2019,8 @@ uint64_t gzip_seg_scratch_bytes(uint32_t n_items) {
 }
 
 hipError_t launch_gzip(ZgItem *items, uint32_t *status, uint32_t n_items, uint8_t *dst, uint64_t slot_bytes,
-                       uint32_t *order, uint32_t *seg_scr, hipStream_t s, int crc_tail) {
+                       uint32_t *order, uint32_t *seg_scr, hipStream_t s, int crc_tail, const GzDirect *direct) {
+  const GzDirect gd = direct ? *direct : GzDirect{};
   if (!n_items) return hipSuccess;
   static const bool lpt = [] {
     const char *e = std::getenv("ZGPU_GZIP_LPT");
@@ -1946,10 +2038,10 @@ hipError_t launch_gzip(ZgItem *items, uint32_t *status, uint32_t n_items, uint8_
   if (order) hipLaunchKernelGGL(k_order_by_len, dim3(1), dim3(1024), 0, s, items, status, n_items, order);
   if (pipe)
     hipLaunchKernelGGL((k_gzip<false, true>), dim3(n_items), dim3(128), 0, s, items, status, nullptr, dst, slot_bytes,
-                       nullptr, order, seg_scr, crc_tail);
+                       nullptr, order, seg_scr, crc_tail, gd);
   else
     hipLaunchKernelGGL(k_gzip<false>, dim3(n_items), dim3(64), 0, s, items, status, nullptr, dst, slot_bytes, nullptr,
-                       order, seg_scr, 0);
+                       order, seg_scr, 0, gd);
   return hipGetLastError();
 }
 
@@ -1958,7 +2050,7 @@ hipError_t launch_zlib_streams(ZgItem *subs, uint32_t *sub_status, const uint32_
   if (!n_sub) return hipSuccess;
   if (!gzip_seg_scratch_bytes(1)) seg_scr = nullptr;
   hipLaunchKernelGGL(k_gzip<true>, dim3(n_sub), dim3(64), 0, s, subs, sub_status, sub_kind, dst, slot, aux,
-                     nullptr, seg_scr, 0);
+                     nullptr, seg_scr, 0, GzDirect{});
   return hipGetLastError();
 }
 

@@ -86,7 +86,8 @@ hipError_t launch_item_resolve(ZgItem *items, uint32_t *status, uint32_t n_items
 // the lookahead decode); 0 bytes when that path is off (ZGPU_GZIP_SEG=0)
 uint64_t gzip_seg_scratch_bytes(uint32_t n_items);
 hipError_t launch_gzip(ZgItem *items, uint32_t *status, uint32_t n_items, uint8_t *dst, uint64_t slot_bytes,
-                       uint32_t *order, uint32_t *seg_scr, hipStream_t s, int crc_tail = 0);
+                       uint32_t *order, uint32_t *seg_scr, hipStream_t s, int crc_tail = 0,
+                       const GzDirect *direct = nullptr);  // direct: whole chunks into the output rows
 // zstd (RFC 8878) frame decode into dst slots: block-parallel (scan, per-block entropy decode,
 // per-item execution) with the serial one-wave-per-item decoder as the fallback.
 struct ZstdScratch {

@@ -414,6 +414,8 @@ struct zgpu_plan {
   BlCaps bl_caps{};             // blosc stream-table capacities recorded by the first execution
   bool bl_caps_valid = false, bl_caps_seen = false;
   bool bl_direct = false;  // the blosc stage may write whole chunks straight into the output (BlDecode::dout)
+  bool gz_direct = false;  // the gzip stage may write whole chunks straight into the output (GzDirect)
+  GzDirect gz{};
   // blosc as the last stage: per item the decoded byte range its selection needs ([0, max) for whole
   // chunks); blocks outside it are not decoded (blosc_decompress_bytes_partial)
   std::vector<uint64_t> bl_need;
@@ -855,6 +857,35 @@ static void plan_build(zgpu_plan &P, const zgpu_chunk_desc *descs) {
     }
     P.bl_direct = ok && !std::getenv("ZGPU_BLOSC_NO_DIRECT");
   }
+  // gzip as the last stage feeding the rows scatter unchanged (no swap / shuffle / transpose), rows of a
+  // power-of-two multiple of 16 bytes, the row axes but the outermost of power-of-two extent: k_gzip
+  // writes the items whose selection is their whole chunk into the output rows itself and the scatter
+  // takes only the others (C3: the subset's 12,167 interior inner chunks of 15,625). ZGPU_GZIP_DIRECT=0: off.
+  {
+    const char *gz_env = std::getenv("ZGPU_GZIP_DIRECT");  // read per plan (an A/B knob)
+    const bool gz_on = !gz_env || std::atoi(gz_env) != 0;
+    const uint64_t Lb = S.chunk_shape[nd - 1] * S.es;
+    bool ok = gz_on && !P.stages.empty() && P.stages.back().kind == ST_GZIP && P.scatter_mode == SCATTER_ROWS &&
+              !S.swap && !S.shuffle && S.nelem > 0 && nd >= 1 && nd <= 3 && S.out_stride[nd - 1] == 1 && Lb >= 16 &&
+              (nd < 2 || S.out_stride[0] * S.es < (1ull << 32)) && S.nelem * S.es < (1ull << 32) &&
+              (Lb & (Lb - 1)) == 0;
+    uint64_t st = 1;
+    for (int a = (int)nd - 1; a >= 0 && ok; a--) {
+      ok = S.enc_stride[a] == st && (a == (int)nd - 1 || (S.out_stride[a] * S.es) % 16 == 0) &&
+           (a == 0 || a == (int)nd - 1 || (S.chunk_shape[a] & (S.chunk_shape[a] - 1)) == 0);
+      st *= S.chunk_shape[a];
+    }
+    P.gz_direct = ok;
+    if (ok) {
+      P.gz.want = S.nelem * S.es;
+      P.gz.nd = nd;
+      P.gz.lbs = (uint32_t)__builtin_ctzll(Lb);
+      for (uint32_t d = 0; d < nd; d++) {
+        P.gz.cshape[d] = S.chunk_shape[d];
+        P.gz.ostr[d] = S.out_stride[d] * S.es;
+      }
+    }
+  }
   // blosc feeding the scatter directly (its decoded bytes are the chunk's encoded-layout elements; a
   // fused unshuffle would interleave planes): a partial selection needs only the byte range between
   // its first and last element in the encoded layout, so only the blocks that cover it are decoded,
@@ -1103,9 +1134,15 @@ static void plan_enqueue(zgpu_plan &P, uint8_t *out, hipStream_t s) {
         }
         HIPCHK(launch_crc32c_strip(P.d_items, P.d_status, ni, st.at_start, P.validate ? 1 : 0, s));
         break;
-      case ST_GZIP:
+      case ST_GZIP: {
+        GzDirect gd = P.gz;
+        const bool direct = P.gz_direct && si + 1 == P.stages.size() && !P.no_scatter && out &&
+                            ((uintptr_t)out & 15) == 0;
+        gd.dout = direct ? out : nullptr;
+        gd.geom = P.d_geom;
         HIPCHK(launch_gzip(P.d_items, P.d_status, ni, P.d_pool[st.pool], P.slot_bytes, P.d_order, P.d_gz_seg, s,
-                           crc_tail));
+                           crc_tail, direct ? &gd : nullptr));
+      }
         crc_tail = 0;
         break;
       case ST_ZSTD:
