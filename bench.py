@@ -65,7 +65,7 @@ def _synth():
 
 def _emulated_rank(args, rank, world):
     """--emulate-rank R/N (one process, one GPU): the step decodes rank R's share of an N-GPU run (C3:
-    its axis-0 slab, C5: its LPT chunk part) with the single-GPU code path -- for profiling a rank's
+    its stream-balanced inner-chunk lines, C5: its LPT chunk part) with the single-GPU code path -- for profiling a rank's
     step (the rank_share legs time every rank this way from their own plans)."""
     spec = getattr(args, "emulate_rank", "")
     if not spec or world > 1:
@@ -360,11 +360,6 @@ class C1:
 # ------------------------------------------------------------------------------------------------
 class C3:
     SHARD, INNER = 256, 32
-    # C4: rows per piece of a rank's slab (one plan each; a piece's send overlaps the next piece's
-    # decode). Inner-chunk rows (32) made each piece a latency-bound k_gzip launch of its own: a 96-row
-    # slab took 12.7-13.1 ms against 18.4 for the whole subset on one GPU (profiles/r06/r06m_*); the
-    # whole slab in one plan (1 << 30: one piece) decodes its ~2.3 k streams in one launch
-    C4_PIECE_ROWS = 1 << 30
     ARRAY = [2048, 2048, 2048]
     SUB_START, SUB_SHAPE = [200, 300, 1000], [768, 768, 768]
     CODECS = [{"name": "sharding_indexed", "configuration": {
@@ -382,11 +377,20 @@ class C3:
     def __init__(self, args, rank, world, dev):
         from zarrs_amd import CodecChain, make_desc
         self.args, self.rank, self.world, self.dev = args, rank, world, dev
-        from zarrs_amd.distributed import slab_partition
+        from zarrs_amd.distributed import chunk_line_partition, slab_partition
         S = self.SHARD
-        # this rank's axis-0 slab of the subset (array coordinates)
         er, ew = _emulated_rank(args, rank, world)
-        self.slabs = slab_partition(self.SUB_START, self.SUB_SHAPE, ew)
+        if ew > 1:
+            # C4: the subset's inner-chunk lines (axis-0 x axis-1 inner chunks) cut into stream-balanced runs
+            # (chunk_line_partition: <= 3 boxes per rank, 1,950-1,975 inner chunks each at N = 8, inside the
+            # pipelined gzip kernel's 2,048; axis-0 slabs cut through inner-chunk rows and gave a rank 2,500);
+            # a rank decodes its boxes into its slab, the rows they span (array coordinates)
+            self.boxes_by_rank = chunk_line_partition(self.SUB_START, self.SUB_SHAPE, [self.INNER] * 3, ew)
+            self.slabs = [self._box_slab(b) for b in self.boxes_by_rank]
+        else:
+            self.slabs = slab_partition(self.SUB_START, self.SUB_SHAPE, ew)
+            self.boxes_by_rank = [[sl] for sl in self.slabs]
+        self.boxes = self.boxes_by_rank[er]
         self.start, self.shape = self.slabs[er]
         syn = _synth()
         self.chain = CodecChain.from_metadata(self.CODECS, "float32", 0.0, args.ctx)
@@ -409,12 +413,7 @@ class C3:
                     t = torch.from_numpy(host).to(dev)
                     self.shards[(si, sj, sk)] = (t, host)
                     enc_total += n.value
-                    s0 = [max(a, o) for a, o in zip(self.start, org)]
-                    s1 = [min(a + b, o + S) for a, b, o in zip(self.start, self.shape, org)]
-                    self.descs.append(make_desc((t.data_ptr(), n.value), [S] * 3,
-                                                sel_start=[a - o for a, o in zip(s0, org)],
-                                                sel_shape=[b - a for a, b in zip(s0, s1)],
-                                                out_start=[a - b for a, b in zip(s0, self.start)]))
+        self.descs = self._box_descs(self.boxes, self.start)
         self.enc_total = enc_total
         n_sh = len(self.shards)
         self.ratio = n_sh * S ** 3 * 4 / enc_total
@@ -423,9 +422,9 @@ class C3:
         self.expected = torch.from_numpy(exp).to(dev)
         self.full = None
         self.gather_s = []
-        if world > 1 and rank == 0:  # the root decodes its slab in place inside the gathered subset
+        if world > 1 and rank == 0:  # the root decodes its boxes in place inside the gathered subset
             self.full = torch.empty(self.SUB_SHAPE, dtype=torch.float32, device=dev)
-            self.out = self.full.narrow(0, 0, self.shape[0])
+            self.out = self.full.narrow(0, self.start[0] - self.SUB_START[0], self.shape[0])
             ef = np.empty(self.SUB_SHAPE, np.float32)  # the whole subset: the root checks every slab
             syn.synth_c3_values(_u64(self.SUB_START), _u64(self.SUB_SHAPE), ef.ctypes.data, nt)
             self.expected_full = torch.from_numpy(ef).to(dev)
@@ -433,28 +432,9 @@ class C3:
         else:
             self.out = torch.empty(self.shape, dtype=torch.float32, device=dev)
         self.out_shape = self.shape
-        self.decoded_bytes = int(np.prod(self.shape)) * 4  # per rank per step
+        self.decoded_bytes = sum(int(np.prod(bs)) for _, bs in self.boxes) * 4  # per rank per step
+        # one plan: at N > 1 the rank's boxes in one launch (C4), sent to the root once decoded
         self.parts = [(self.chain, self.descs, self.out, self.out_shape)]
-        if world > 1:
-            # C4: the slab is decoded in pieces of whole inner-chunk rows (32 array rows), one plan each,
-            # and every piece is sent to the root while the next one decodes (gather_slabs_overlapped)
-            from zarrs_amd.distributed import slab_pieces
-            self.pieces = slab_pieces(self.start, self.shape, self.C4_PIECE_ROWS)
-            self.parts = []
-            for r0, n in self.pieces:
-                p0 = [self.start[0] + r0] + self.start[1:]
-                pd = []
-                for (si, sj, sk), (t, _) in self.shards.items():
-                    org = [si * S, sj * S, sk * S]
-                    s0 = [max(a, o) for a, o in zip(p0, org)]
-                    s1 = [min(a + b, o + S) for a, b, o in zip(p0, [n] + self.shape[1:], org)]
-                    if any(b <= a for a, b in zip(s0, s1)):
-                        continue
-                    pd.append(make_desc((t.data_ptr(), int(t.numel())), [S] * 3,
-                                        sel_start=[a - o for a, o in zip(s0, org)],
-                                        sel_shape=[b - a for a, b in zip(s0, s1)],
-                                        out_start=[a - b for a, b in zip(s0, p0)]))
-                self.parts.append((self.chain, pd, self.out.narrow(0, r0, n), [n] + self.shape[1:]))
         self.step_bytes = int(np.prod(self.SUB_SHAPE)) * 4  # the whole subset, all ranks
         if getattr(args, "emulate_rank", ""):
             self.step_bytes = self.decoded_bytes
@@ -466,102 +446,117 @@ class C3:
                        "shards_touched_per_gpu": n_sh, "subset_shape": self.SUB_SHAPE,
                        "slab_per_gpu": self.shape, "gzip_ratio": round(self.ratio, 3),
                        "encoded_bytes_resident_per_gpu": enc_total,
-                       "parallelism": f"axis-0 slabs x{world}" + (", peers' slabs received straight into rank 0's "
-                                                                   "output over RCCL in the step" if world > 1 else "")}
+                       "parallelism": ("axis-0 slabs x1" if world == 1 else
+                                       f"stream-balanced inner-chunk lines x{world} (<= 3 boxes per rank), peers' "
+                                       "boxes sent to rank 0 over RCCL in the step (whole-row boxes received in "
+                                       "place)")}
+        if world > 1:
+            self.config["boxes_this_gpu"] = [[list(b0), list(bs)] for b0, bs in self.boxes]
         self.data = ("synthetic (round(256*(sin(.05x)+cos(.03y)+.5sin(.07z))+N(0,1))/256 f32, shards "
                      "written by tools/synth; decode(encode(x)) == x checked on device)")
         self.scaling = "strong"
 
-    def rank_share(self, n1_ms):
-        """SURVEY §8(e) C4 at N = 8, predicted on this GPU: rank r's axis-0 slab of the subset
-        (slab_partition, as --gpus 8 cuts it) decoded alone as the N = 8 step decodes it (C4_PIECE_ROWS
-        pieces, one plan each, statuses read after each), for every r; a piece's send overlaps the next
-        piece's decode, so the exposed exchange is the last piece over one xGMI link. The other piece
-        size is measured beside it (`alt`: 32-row pieces, i.e. inner-chunk rows, or the whole slab)."""
-        from zarrs_amd import make_desc
-        from zarrs_amd.distributed import slab_partition, slab_pieces
-        N, S = RANK_SHARE_N, self.SHARD
-        slabs = slab_partition(self.SUB_START, self.SUB_SHAPE, N)
+    def _box_slab(self, boxes):
+        """The slab (rows of the subset, whole on the other axes) that a rank's boxes span."""
+        r0 = min(b0[0] for b0, _ in boxes)
+        r1 = max(b0[0] + bs[0] for b0, bs in boxes)
+        return [r0] + list(self.SUB_START[1:]), [r1 - r0] + list(self.SUB_SHAPE[1:])
 
-        def measure(piece_rows):
-            rank_ms, last_piece = [], 0
-            for r in range(N):
-                start, shape = slabs[r]
+    def _box_descs(self, boxes, origin):
+        """Chunk descriptors of the shards' parts inside `boxes` (array coordinates), placed relative to
+        `origin` (the output's first element)."""
+        from zarrs_amd import make_desc
+        S = self.SHARD
+        pd = []
+        for b0, bs in boxes:
+            for (si, sj, sk), (t, _) in self.shards.items():
+                org = [si * S, sj * S, sk * S]
+                s0 = [max(a, o) for a, o in zip(b0, org)]
+                s1 = [min(a + n, o + S) for a, n, o in zip(b0, bs, org)]
+                if any(b <= a for a, b in zip(s0, s1)):
+                    continue
+                pd.append(make_desc((t.data_ptr(), int(t.numel())), [S] * 3,
+                                    sel_start=[a - o for a, o in zip(s0, org)],
+                                    sel_shape=[b - a for a, b in zip(s0, s1)],
+                                    out_start=[a - o for a, o in zip(s0, origin)]))
+        return pd
+
+    def rank_share(self, n1_ms):
+        """SURVEY §8(e) C4 at N = 8, predicted on this GPU: rank r's share of the subset (its stream-
+        balanced inner-chunk lines, chunk_line_partition, as --gpus 8 cuts it) decoded alone as the N = 8
+        step decodes it (its boxes in one plan into its slab, statuses read back), for every r; its boxes
+        then travel to the root over one xGMI link, beside the other peers' on theirs (the exposed exchange:
+        the largest rank share at one link's rate). The axis-0 slabs of rounds 5-6 are measured beside it
+        (`alt`: 2,500 inner chunks per rank, the one-wave gzip kernel)."""
+        from zarrs_amd.distributed import chunk_line_partition, slab_partition
+        N = RANK_SHARE_N
+
+        def measure(boxes_by_rank):
+            rank_ms, biggest = [], 0
+            for boxes in boxes_by_rank:
+                start, shape = self._box_slab(boxes)
                 buf = torch.empty(shape, dtype=torch.float32, device=self.dev)
-                groups = []
-                for r0, n in slab_pieces(start, shape, piece_rows):
-                    p0 = [start[0] + r0] + list(start[1:])
-                    pd = []
-                    for (si, sj, sk), (t, _) in self.shards.items():
-                        org = [si * S, sj * S, sk * S]
-                        s0 = [max(a, o) for a, o in zip(p0, org)]
-                        s1 = [min(a + b, o + S) for a, b, o in zip(p0, [n] + list(shape[1:]), org)]
-                        if any(b <= a for a, b in zip(s0, s1)):
-                            continue
-                        pd.append(make_desc((t.data_ptr(), int(t.numel())), [S] * 3,
-                                            sel_start=[a - o for a, o in zip(s0, org)],
-                                            sel_shape=[b - a for a, b in zip(s0, s1)],
-                                            out_start=[a - b for a, b in zip(s0, p0)]))
-                    groups.append((self.chain, pd, buf.narrow(0, r0, n), [n] + list(shape[1:])))
-                    last_piece = max(last_piece, int(np.prod([n] + list(shape[1:]))) * 4)
-                rank_ms.append(_time_plan_groups(self.args.ctx, groups, [list(range(len(groups)))], set(),
-                                                 self.dev, status_each=True))
+                groups = [(self.chain, self._box_descs(boxes, start), buf, shape)]
+                rank_ms.append(_time_plan_groups(self.args.ctx, groups, [[0]], set(), self.dev, status_each=True))
+                biggest = max(biggest, sum(int(np.prod(bs)) for _, bs in boxes) * 4)
                 del buf
-            return rank_ms, last_piece / (XGMI_LINK_GBS * 1e9) * 1e3
+            return rank_ms, biggest / (XGMI_LINK_GBS * 1e9) * 1e3
 
         gb = int(np.prod(self.SUB_SHAPE)) * 4 * (N - 1) // N
-        rank_ms, gms = measure(self.C4_PIECE_ROWS)
+        rank_ms, gms = measure(chunk_line_partition(self.SUB_START, self.SUB_SHAPE, [self.INNER] * 3, N))
         rep = rank_share_report(rank_ms, n1_ms, self.step_bytes, gb, gms,
-                                f"each rank's axis-0 slab decoded alone on this GPU in the N = 8 step's "
-                                f"pieces ({self.C4_PIECE_ROWS if self.C4_PIECE_ROWS < 1 << 20 else 'whole slab'} "
-                                "rows, one plan each; 5 reps, median); a piece's send overlaps the next piece's "
-                                f"decode, so the last piece's send is exposed (at {XGMI_LINK_GBS:.0f} GB/s); "
-                                "the slowest rank sets the step")
-        alt_rows = self.INNER if self.C4_PIECE_ROWS != self.INNER else 1 << 30
-        alt_ms, alt_g = measure(alt_rows)
-        rep["alt"] = {"piece_rows": alt_rows if alt_rows < 1 << 20 else "whole slab",
+                                "each rank's stream-balanced inner-chunk lines (chunk_line_partition: <= 3 boxes, "
+                                "1,950-1,975 inner chunks) decoded alone on this GPU in one plan, as the N = 8 step "
+                                "does (5 reps, median); its boxes then go to the root over one xGMI link (at "
+                                f"{XGMI_LINK_GBS:.0f} GB/s) beside the other peers'; the slowest rank sets the step")
+        alt_ms, alt_g = measure([[sl] for sl in slab_partition(self.SUB_START, self.SUB_SHAPE, N)])
+        rep["alt"] = {"partition": "axis-0 slabs (rounds 5-6)",
                       "max_rank_ms": round(max(alt_ms), 3), "gather_ms_model": round(alt_g, 3),
                       "predicted_speedup_vs_n1": round(n1_ms / (max(alt_ms) + alt_g), 3)}
         return rep
 
     def run_step(self, execute):
-        """C4 (N > 1): decode the slab piece by piece (execute(k) runs piece k's plan on the bench stream,
-        statuses read back) while the finished pieces travel to the root (RCCL isend / irecv straight into
-        place). gather_s records the step's exposed exchange: the time from this rank's last decode to
-        the completion of its sends (peers) or receives (root)."""
-        from zarrs_amd.distributed import gather_slabs_overlapped
-        done = []
-
-        def decode_piece(k, view):
-            assert view.data_ptr() == self.parts[k][2].data_ptr()
-            execute(k)
-            if k == len(self.parts) - 1:
-                done.append(time.perf_counter())
-        self.gathered = gather_slabs_overlapped(decode_piece, self.out, self.slabs, self.C4_PIECE_ROWS, dst=0,
-                                                out=self.full)
+        """C4 (N > 1): decode this rank's boxes (one plan on the bench stream, statuses read back), then
+        send them to the root (RCCL point-to-point; whole-row boxes land in place, the others packed
+        into one message per peer: gather_regions). gather_s records the step's exchange: the time from
+        this rank's decode to the completion of its sends (peers) or receives (root)."""
+        from zarrs_amd.distributed import gather_regions
+        execute(0)
+        t0 = time.perf_counter()
+        rel = [[([a - o for a, o in zip(b0, self.SUB_START)], bs) for b0, bs in boxes] for boxes in self.boxes_by_rank]
+        self.gathered = gather_regions(self.out, rel, [0, 0, 0], self.SUB_SHAPE, dst=0, out=self.full,
+                                       local_origin=[a - o for a, o in zip(self.start, self.SUB_START)])
         torch.cuda.synchronize()
-        if done:
-            self.gather_s.append(time.perf_counter() - done[0])
+        self.gather_s.append(time.perf_counter() - t0)
 
     def after_decode(self):
         pass
 
+    def _box_views(self, t, origin, boxes):
+        return [t[tuple(slice(a - o, a - o + n) for a, o, n in zip(b0, origin, bs))] for b0, bs in boxes]
+
     def check(self) -> bool:
-        ok = bool(torch.equal(self.out.view(torch.int32), self.expected.view(torch.int32)))
-        if self.gathered is not None:  # rank 0 holds the whole subset: every received slab is checked
-            from zarrs_amd.distributed import slab_mismatches
-            bad = slab_mismatches(self.gathered, self.expected_full, self.slabs)
+        # this rank's boxes (its slab holds other ranks' boxes too, which it does not write)
+        ok = all(bool(torch.equal(g.contiguous().view(torch.int32), e.contiguous().view(torch.int32)))
+                 for g, e in zip(self._box_views(self.out, self.start, self.boxes),
+                                 self._box_views(self.expected, self.start, self.boxes)))
+        if self.gathered is not None:  # rank 0 holds the whole subset: every rank's boxes are checked
+            bad = [r for r, boxes in enumerate(self.boxes_by_rank)
+                   if not all(bool(torch.equal(g.contiguous().view(torch.int32), e.contiguous().view(torch.int32)))
+                              for g, e in zip(self._box_views(self.gathered, self.SUB_START, boxes),
+                                              self._box_views(self.expected_full, self.SUB_START, boxes)))]
             if bad:
-                print(f"C4 check: slabs of ranks {bad} differ from the expected subset", file=sys.stderr)
+                print(f"C4 check: boxes of ranks {bad} differ from the expected subset", file=sys.stderr)
             ok = ok and not bad
         return ok
 
     def gather_stats(self):
         """The xGMI gather inside the step (N > 1): median wall time of the grouped P2P receives /
-        sends, and the bytes the root receives (every peer's slab)."""
+        sends, and the bytes the root receives (every peer's boxes)."""
         if self.world == 1 or not self.gather_s:
             return None
-        peer_bytes = sum(int(np.prod(sh)) * 4 for r, (_, sh) in enumerate(self.slabs) if r != 0)
+        peer_bytes = sum(int(np.prod(bs)) * 4 for r, boxes in enumerate(self.boxes_by_rank) if r != 0
+                         for _, bs in boxes)
         return {"ms": float(np.median(self.gather_s)) * 1e3, "bytes_to_root": peer_bytes}
 
     def cpu_baseline(self):

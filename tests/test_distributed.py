@@ -13,7 +13,8 @@ import torch.distributed as dist
 import torch.multiprocessing as mp
 
 import oracle as O
-from zarrs_amd.distributed import (_contiguous_in, chunk_boxes, gather_regions, gather_slabs, lpt_partition,
+from zarrs_amd.distributed import (_contiguous_in, chunk_boxes, chunk_line_partition, gather_regions, gather_slabs,
+                                   lpt_partition,
                                    slab_mismatches, slab_pieces,
                                    retrieve_array_subset_distributed, slab_partition)
 
@@ -113,6 +114,25 @@ def _worker(rank, world, port, q):
             res["c5_gather_direct"] = bool(np.array_equal(got.numpy().view(np.uint16), lvl[1:7, 8:16, 16:24]))
         else:
             res["c5_gather_direct"] = got is None
+        # C4 pattern (bench.py at N > 1): stream-balanced chunk lines, each rank decoding its boxes into
+        # its slab (the rows its boxes span; the root's slab is a view of the gathered subset), the boxes
+        # gathered with the slab as local's origin
+        sub0, subn = [2, 1, 0], [33, 10, 5]
+        parts = chunk_line_partition(sub0, subn, arr.cs, world)
+        rel = [[([x - o for x, o in zip(b0, sub0)], bs) for b0, bs in boxes] for boxes in parts]
+        mine = rel[rank]
+        r0 = min(b0[0] for b0, _ in mine)
+        r1 = max(b0[0] + bs[0] for b0, bs in mine)
+        full = torch.zeros(subn, dtype=torch.float32) if rank == 0 else None
+        slab = full.narrow(0, r0, r1 - r0) if rank == 0 else torch.full([r1 - r0] + subn[1:], -1.0)
+        for b0, bs in mine:
+            arr.retrieve_array_subset_into([x + o for x, o in zip(b0, sub0)], bs,
+                                           slab[b0[0] - r0:b0[0] - r0 + bs[0], b0[1]:b0[1] + bs[1], b0[2]:b0[2] + bs[2]])
+        got = gather_regions(slab, rel, [0, 0, 0], subn, out=full, local_origin=[r0, 0, 0])
+        if rank == 0:
+            res["c4_lines_gather"] = bool(np.array_equal(got.numpy(), a[2:35, 1:11, 0:5]))
+        else:
+            res["c4_lines_gather"] = got is None
         q.put((rank, res))
     finally:
         dist.destroy_process_group()
@@ -304,3 +324,36 @@ def test_overlapped_slab_gather(world):
     out = _spawn(_overlap_worker, world)
     for r, res in out.items():
         assert all(res.values()), (r, res)
+
+
+@pytest.mark.parametrize("world", [1, 2, 3, 8, 13])
+def test_chunk_line_partition_balanced_and_exact(world):
+    """C4's partition: every voxel of the subset in exactly one rank's boxes, at most three boxes per
+    rank, chunk counts per rank within one chunk line of each other, no chunk split between ranks."""
+    start, shape, cs = [200, 300, 1000], [768, 768, 768], [32, 32, 32]
+    parts = chunk_line_partition(start, shape, cs, world)
+    assert len(parts) == world
+    cover = np.zeros([25, 25], np.int32)  # chunk lines (axis-0 chunk, axis-1 chunk) of the subset
+    vol = 0
+    owner = {}
+    for r, boxes in enumerate(parts):
+        assert len(boxes) <= 3
+        for b0, bs in boxes:
+            assert b0[2] == start[2] and bs[2] == shape[2]
+            vol += int(np.prod(bs))
+            for ci in range(b0[0] // 32, (b0[0] + bs[0] - 1) // 32 + 1):
+                for cj in range(b0[1] // 32, (b0[1] + bs[1] - 1) // 32 + 1):
+                    cover[ci - 6, cj - 9] += 1
+                    assert owner.setdefault((ci, cj), r) == r
+    assert vol == int(np.prod(shape))
+    assert (cover == 1).all()
+    counts = [sum(1 for v in owner.values() if v == r) for r in range(world)]
+    assert max(counts) - min(counts) <= 1
+    # small and 2-d subsets; a 1-d subset falls back to slabs
+    parts = chunk_line_partition([3, 1], [10, 7], [4, 3], 3)
+    got = np.zeros([10, 7], np.int32)
+    for boxes in parts:
+        for b0, bs in boxes:
+            got[b0[0] - 3:b0[0] - 3 + bs[0], b0[1] - 1:b0[1] - 1 + bs[1]] += 1
+    assert (got == 1).all()
+    assert chunk_line_partition([5], [10], [4], 2) == [[([5], [5])], [([10], [5])]]

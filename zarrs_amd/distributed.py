@@ -47,6 +47,46 @@ def slab_partition(start: Sequence[int], shape: Sequence[int], world: int, axis:
     return out
 
 
+def chunk_line_partition(start: Sequence[int], shape: Sequence[int], chunk_shape: Sequence[int], world: int):
+    """Stream-balanced partition of an array subset over `world` ranks (C4): the subset's
+    chunk lines -- (chunk row, chunk column) pairs along axes 0 and 1, each spanning the subset on the
+    other axes -- in C order, cut into `world` contiguous runs whose counts differ by at most one. A rank
+    decodes the chunks of its lines only, so every chunk is decoded by exactly one rank and every rank
+    gets the same number of chunks (+- one line) -- unlike axis-0 slabs, whose boundaries cut through
+    chunk rows (the chunks there decoded by two ranks) and whose chunk counts step by whole rows.
+    Returns [[(box_start, box_shape), ...] per rank] in array coordinates: at most three boxes per rank
+    (a partial chunk row, whole chunk rows, a partial chunk row); 1-d subsets fall back to slabs."""
+    start, shape, cs = [int(x) for x in start], [int(x) for x in shape], [int(x) for x in chunk_shape]
+    nd = len(shape)
+    if nd < 2 or any(n == 0 for n in shape):
+        return [[(s, sh)] if all(n > 0 for n in sh) else [] for s, sh in slab_partition(start, shape, world)]
+    lo = [s // c for s, c in zip(start, cs)]
+    hi = [(s + n - 1) // c + 1 for s, n, c in zip(start, shape, cs)]
+    nr, ny = hi[0] - lo[0], hi[1] - lo[1]
+    total = nr * ny
+    out = []
+    for r in range(world):
+        l0, l1 = r * total // world, (r + 1) * total // world
+        boxes = []  # [b0, b1] per box, merged along axis 1 within a chunk row, then along axis 0
+        for ln in range(l0, l1):
+            ci, cj = lo[0] + ln // ny, lo[1] + ln % ny
+            b0 = [max(start[0], ci * cs[0]), max(start[1], cj * cs[1])] + start[2:]
+            b1 = [min(start[0] + shape[0], (ci + 1) * cs[0]), min(start[1] + shape[1], (cj + 1) * cs[1])] + \
+                 [a + n for a, n in zip(start[2:], shape[2:])]
+            if boxes and boxes[-1][0][0] == b0[0] and boxes[-1][1][1] == b0[1]:
+                boxes[-1][1][1] = b1[1]
+            else:
+                boxes.append([b0, b1])
+        merged = []
+        for b0, b1 in boxes:
+            if merged and merged[-1][1][0] == b0[0] and merged[-1][0][1:] == b0[1:] and merged[-1][1][1:] == b1[1:]:
+                merged[-1][1][0] = b1[0]
+            else:
+                merged.append([list(b0), list(b1)])
+        out.append([(b0, [e - b for b, e in zip(b0, b1)]) for b0, b1 in merged])
+    return out
+
+
 def lpt_partition(costs: Sequence[int], world: int):
     """Greedy LPT: items sorted by cost (ties by index) go to the least-loaded rank.
     Returns [[item indices] per rank], each list in ascending index order (deterministic)."""
@@ -237,14 +277,16 @@ def _contiguous_in(bs, shape) -> bool:
     return all(int(b) == int(s) for b, s in zip(bs[i + 1:], shape[i + 1:]))
 
 
-def gather_regions(local, boxes_by_rank, sub_start, sub_shape, dst: int = 0, group=None, out=None):
+def gather_regions(local, boxes_by_rank, sub_start, sub_shape, dst: int = 0, group=None, out=None,
+                   local_origin=None):
     """Assemble an array subset on group rank `dst` from chunk-partitioned ranks (C5: chunks
     LPT-partitioned over the GPUs, one cross-GPU subset gathered). `local` is this
     rank's copy of the whole array holding the chunks it decoded; boxes_by_rank[r] lists the
     (start, shape) array boxes rank r contributes. Each peer packs its boxes into one contiguous
     buffer and sends it with a single point-to-point message; the root receives every peer's buffer
     (grouped receives, all links at once) and unpacks the boxes into the subset. Returns the subset
-    on dst and None elsewhere."""
+    on dst and None elsewhere. local_origin: the coordinates of local's first element (default the
+    origin: local is the whole array; C4 passes its rank's slab)."""
     import torch
     import torch.distributed as dist
     world = len(boxes_by_rank)
@@ -261,7 +303,7 @@ def gather_regions(local, boxes_by_rank, sub_start, sub_shape, dst: int = 0, gro
 
     def numel(bs):
         return int(torch.Size([int(x) for x in bs]).numel())
-    zero = [0] * len(sub_start)
+    zero = [0] * len(sub_start) if local_origin is None else [int(x) for x in local_origin]
     if rank != dst:
         packed, direct = split(boxes_by_rank[rank])
         peer = dist.get_global_rank(group, dst) if group is not None else dst
@@ -283,13 +325,15 @@ def gather_regions(local, boxes_by_rank, sub_start, sub_shape, dst: int = 0, gro
                 w.wait()
         return None
     if out is not None and not out.is_contiguous():  # boxes are received in place: a contiguous target
-        got = gather_regions(local, boxes_by_rank, sub_start, sub_shape, dst, group)
+        got = gather_regions(local, boxes_by_rank, sub_start, sub_shape, dst, group, local_origin=local_origin)
         out.copy_(got)
         return out
     if out is None:
         out = torch.empty([int(x) for x in sub_shape], dtype=local.dtype, device=local.device)
     for b0, bs in boxes_by_rank[dst]:
-        view(out, b0, bs, sub_start).copy_(view(local, b0, bs, zero))
+        o, l_ = view(out, b0, bs, sub_start), view(local, b0, bs, zero)
+        if o.data_ptr() != l_.data_ptr() or o.stride() != l_.stride():  # the root decoded in place: no copy
+            o.copy_(l_)
     ops, bufs = [], []
     for r in range(world):
         if r == dst:
