@@ -49,6 +49,15 @@ class OracleArray:
         got = O.retrieve_array_subset(self.co, self.shape, self.cs, self.chunks, start, shape)
         out.copy_(torch.from_numpy(got))
 
+    @property
+    def read_chunk_shape(self):
+        return self.cs
+
+    def retrieve_boxes_into(self, boxes, out, origin):
+        for b0, bs in boxes:
+            got = O.retrieve_array_subset(self.co, self.shape, self.cs, self.chunks, b0, bs)
+            out[tuple(slice(a - o, a - o + n) for a, o, n in zip(b0, origin, bs))].copy_(torch.from_numpy(got))
+
 
 def _free_port():
     with socket.socket() as s:
@@ -66,15 +75,18 @@ def _worker(rank, world, port, q):
         res = {}
         for name, (start, shape) in {"even": ([2, 1, 0], [20, 9, 5]), "ragged": ([3, 0, 1], [31, 11, 3]),
                                      "tiny": ([5, 5, 2], [1, 2, 2])}.items():
+            lines = retrieve_array_subset_distributed(arr, start, shape, device="cpu", partition="lines")
             got = retrieve_array_subset_distributed(arr, start, shape, device="cpu")
             if rank == 0:
                 sl = tuple(slice(s, s + n) for s, n in zip(start, shape))
                 res[name] = bool(np.array_equal(got.numpy(), a[sl]))
+                res[name + "_lines"] = bool(np.array_equal(lines.numpy(), a[sl]))
                 # the root's slab was decoded in place, inside the returned subset (no temporary)
                 own = arr.outs[-1] if arr.outs else None
                 res[name + "_inplace"] = own is None or own.data_ptr() == got.data_ptr()
             else:
                 res[name] = got is None
+                res[name + "_lines"] = lines is None
         # C5 pattern: u16 chunks [bytes, shuffle 2, zstd 3] LPT-partitioned by encoded size; every rank
         # decodes its chunks into its own level array; one subset spanning ranks gathered to rank 0
         rng = np.random.default_rng(42)

@@ -6,7 +6,9 @@ memory (RCCL cannot pair two ranks on one device; the exchange logic is the same
 runs over RCCL/xGMI on an 8-GPU node). Rank 0 compares the gathered subset with the CPU oracle.
 
   C4 pattern: C3's exact chain ([bytes, gzip 1, crc32c] inner chunks, [bytes, crc32c] index at the
-              end), subset split into axis-0 slabs, slabs gathered into rank 0's subset
+              end), subset split into axis-0 slabs, slabs gathered into rank 0's subset; and split
+              into stream-balanced inner-chunk lines (partition="lines", each rank's boxes decoded
+              as one batch by Array.retrieve_boxes_into), boxes gathered with gather_regions
   C5 pattern: u16 [bytes, numcodecs.shuffle{2}, zstd{3}] chunks LPT-partitioned by encoded size,
               each rank decodes its chunks into its own level array (one zgpu_decode_batch), one
               cross-rank subset gathered with gather_regions (packed boxes and in-place boxes)
@@ -86,11 +88,16 @@ def _worker(rank, world, port, q):
                                      "c4_ragged": ([1, 0, 0], [63, 48, 48]),
                                      "c4_thin": ([30, 2, 2], [3, 5, 40])}.items():
             got = retrieve_array_subset_distributed(arr, start, shape, device=dev)
+            lines = retrieve_array_subset_distributed(arr, start, shape, device=dev, partition="lines")
             if rank == 0:
                 exp = O.retrieve_array_subset(co, list(a.shape), shard, shards, start, shape, nthreads=4)
                 res[name] = got is not None and got.is_cuda and got.cpu().numpy().tobytes() == exp.tobytes()
+                # bench.py's C4 cut: stream-balanced inner-chunk lines, each rank's boxes in one batch
+                res[name + "_lines"] = (lines is not None and lines.is_cuda and
+                                        lines.cpu().numpy().tobytes() == exp.tobytes())
             else:
                 res[name] = got is None
+                res[name + "_lines"] = lines is None
         # ---- C5: zstd+shuffle u16 chunks LPT-partitioned, each rank decodes its own on the GPU
         lvl = _c5_level()
         cs = [8, 32, 32]
@@ -214,3 +221,37 @@ def test_three_ranks_overlapped_gather_hip_decode():
         assert "error" not in out[r], out
         assert all(v for k, v in out[r].items() if not k.endswith("_ms")), out
     print({r: {k: round(v, 2) for k, v in out[r].items() if k.endswith("_ms")} for r in out})
+
+
+def test_retrieve_boxes_into_one_batch():
+    """Array.retrieve_boxes_into: a rank's chunk_line_partition boxes decoded as one batch into its slab
+    (the HIP decode), equal to the oracle inside the boxes and untouched (sentinel) outside them; an
+    absent shard reads as the fill value."""
+    import torch
+    import oracle as O
+    from zarrs_amd import Array, Context, DeviceStore, MemoryStore
+    from zarrs_amd.distributed import chunk_line_partition
+    a = _c3_array()
+    shard = [16, 16, 16]
+    co = O.OracleChain.from_metadata(C3_CODECS, "float32", 0.0, 3)
+    shards = _encode_chunks(co, a, shard)
+    del shards[(1, 1, 1)]  # absent: the fill value
+    a[16:32, 16:32, 16:32] = 0
+    meta = {"shape": list(a.shape), "data_type": "float32", "fill_value": 0.0, "codecs": C3_CODECS,
+            "chunk_grid": {"name": "regular", "configuration": {"chunk_shape": shard}}}
+    arr = Array(DeviceStore.from_store(MemoryStore({"c/" + "/".join(map(str, k)): v for k, v in shards.items()})),
+                meta, Context(0))
+    assert arr.read_chunk_shape == [8, 8, 8]
+    start, shape = [3, 5, 1], [50, 40, 45]
+    for boxes in chunk_line_partition(start, shape, arr.read_chunk_shape, 3):
+        r0 = min(b0[0] for b0, _ in boxes)
+        r1 = max(b0[0] + bs[0] for b0, bs in boxes)
+        origin = [r0] + start[1:]
+        out = torch.full([r1 - r0] + shape[1:], -7.0, device="cuda")
+        arr.retrieve_boxes_into(boxes, out, origin)
+        got = out.cpu().numpy()
+        exp = np.full(got.shape, -7.0, np.float32)
+        for b0, bs in boxes:
+            sl = tuple(slice(x - o, x - o + n) for x, o, n in zip(b0, origin, bs))
+            exp[sl] = a[tuple(slice(x, x + n) for x, n in zip(b0, bs))]
+        assert got.tobytes() == exp.tobytes()

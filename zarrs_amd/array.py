@@ -214,6 +214,55 @@ class Array:
         del keep
         L.check(rc)
 
+    @property
+    def read_chunk_shape(self):
+        """The decode granule: a sharded array's inner chunk shape (sharding_indexed's chunk_shape), else
+        its chunk shape."""
+        c0 = self.metadata["codecs"][0] if self.metadata.get("codecs") else {}
+        if c0.get("name") == "sharding_indexed":
+            return [int(c) for c in c0["configuration"]["chunk_shape"]]
+        return list(self.chunk_shape)
+
+    def retrieve_boxes_into(self, boxes, out, origin) -> None:
+        """Several boxes of the array decoded as ONE batch (one plan: every box's chunks in one launch per
+        stage) into `out`, whose first element is array coordinate `origin`; elements of `out` outside
+        the boxes are not written. A distributed rank's share (chunk_line_partition's <= 3 boxes) decodes
+        in one latency instead of one per box. Stores read by path (FilesystemStore) take one
+        retrieve_array_subset_into per box."""
+        from .codec import make_desc
+        boxes = [([int(a) for a in b0], [int(n) for n in bs]) for b0, bs in boxes]
+        boxes = [(b0, bs) for b0, bs in boxes if all(n > 0 for n in bs)]
+        if not boxes:
+            return
+        if isinstance(self.store, FilesystemStore):
+            for b0, bs in boxes:
+                v = out[tuple(slice(a - o, a - o + n) for a, o, n in zip(b0, origin, bs))]
+                self.retrieve_array_subset_into(b0, bs, v)
+            return
+        descs, keep = [], []
+        for b0, bs in boxes:
+            ranges = [range(a // c, (a + n - 1) // c + 1) for a, n, c in zip(b0, bs, self.chunk_shape)]
+            for idx in itertools.product(*ranges):
+                org = [i * c for i, c in zip(idx, self.chunk_shape)]
+                s0 = [max(a, o) for a, o in zip(b0, org)]
+                s1 = [min(a + n, o + c) for a, n, o, c in zip(b0, bs, org, self.chunk_shape)]
+                v = self.store.get(self.chunk_key(idx))
+                if v is None:
+                    enc = (0, 0)
+                elif self.store.device:
+                    keep.append(v)
+                    enc = (v.data_ptr(), v.numel())
+                else:
+                    b = np.frombuffer(v, dtype=np.uint8) if len(v) else np.zeros(1, np.uint8)
+                    keep.append(b)
+                    enc = (b.ctypes.data, len(v))
+                descs.append(make_desc(enc, self.chunk_shape, sel_start=[a - o for a, o in zip(s0, org)],
+                                       sel_shape=[e - a for a, e in zip(s0, s1)],
+                                       out_start=[a - o for a, o in zip(s0, origin)]))
+        self.codecs.decode_batch(descs, out, list(out.shape), enc_device=bool(self.store.device),
+                                 validate_checksums=self._validate)
+        del keep
+
     def retrieve_array_subset_multi(self, start, shape, out, contexts) -> None:
         """The subset decoded by several GPUs of this process (zgpu_retrieve_array_subset_multi): one
         chain per context in `contexts`, the subset's axis-0 chunk rows cut into one contiguous group

@@ -360,24 +360,61 @@ def gather_regions(local, boxes_by_rank, sub_start, sub_shape, dst: int = 0, gro
     return out
 
 
+def _retrieve_lines_distributed(array, start, shape, group, dst, device, tdtype, world, rank):
+    """retrieve_array_subset_distributed(partition="lines"): this rank's chunk_line_partition boxes of
+    the subset (the array's read granule: a sharded array's inner chunks) decoded as one batch into
+    its slab (the root's: a view of the gathered subset), then gathered with gather_regions."""
+    import torch
+    parts = chunk_line_partition(start, shape, array.read_chunk_shape, world)
+    mine = parts[rank]
+    rel = [[([a - o for a, o in zip(b0, start)], bs) for b0, bs in boxes] for boxes in parts]
+    if mine:
+        r0 = min(b0[0] for b0, _ in mine)
+        r1 = max(b0[0] + bs[0] for b0, bs in mine)
+    else:
+        r0 = r1 = int(start[0])
+    slab0 = [r0] + [int(s) for s in start[1:]]
+    slab_shape = [r1 - r0] + [int(n) for n in shape[1:]]
+    staged = device.type == "cuda" and world > 1 and _host_staged(group)
+    out = None
+    if rank == dst and not staged:  # the root decodes its boxes in place inside the gathered subset
+        out = torch.empty([int(n) for n in shape], dtype=tdtype, device=device)
+        local = out.narrow(0, r0 - int(start[0]), r1 - r0)
+    else:
+        local = torch.empty(slab_shape, dtype=tdtype, device=device)
+    if mine:
+        array.retrieve_boxes_into(mine, local, slab0)
+    origin = [a - o for a, o in zip(slab0, start)]
+    if staged:  # gloo moves host tensors only: the slab staged through host memory
+        got = gather_regions(local.cpu(), rel, [0] * len(shape), shape, dst, group, local_origin=origin)
+        return None if got is None else got.to(device)
+    return gather_regions(local, rel, [0] * len(shape), shape, dst, group, out=out, local_origin=origin)
+
+
 def retrieve_array_subset_distributed(array, start, shape, group=None, dst: int = 0, axis: int = 0,
-                                      device=None, piece_rows: int | None = None):
+                                      device=None, piece_rows: int | None = None, partition: str = "slabs"):
     """Array::retrieve_array_subset over all ranks of `group`: this rank decodes its slab on its own
     device, then the slabs are gathered to `dst` (the assembled subset there, None elsewhere).
     piece_rows (axis 0): decode and send the slab in pieces of that many array rows (the chunk extent
     along axis 0, or a multiple), the sends overlapping the next piece's decode
-    (gather_slabs_overlapped)."""
+    (gather_slabs_overlapped). partition="lines": each rank decodes its stream-balanced chunk lines
+    (chunk_line_partition over the array's read granule, <= 3 boxes, one batch) instead of a slab --
+    every chunk decoded by exactly one rank (bench.py's C4)."""
     import numpy as np
     import torch
     import torch.distributed as dist
     world = dist.get_world_size(group) if dist.is_initialized() else 1
     rank = dist.get_rank(group) if dist.is_initialized() else 0
-    slabs = slab_partition(start, shape, world, axis)
-    s, sh = slabs[rank]
     if device is None:
         device = torch.device("cuda", torch.cuda.current_device()) if torch.cuda.is_available() else "cpu"
     tdtype = torch.from_numpy(np.zeros(1, dtype=array.dtype)).dtype
     device = torch.device(device)
+    if partition == "lines" and world > 1 and len(shape) >= 2:
+        return _retrieve_lines_distributed(array, start, shape, group, dst, device, tdtype, world, rank)
+    if partition not in ("slabs", "lines"):
+        raise ValueError(f"partition {partition!r}: 'slabs' or 'lines'")
+    slabs = slab_partition(start, shape, world, axis)
+    s, sh = slabs[rank]
     if piece_rows and axis == 0:
         pieces = slab_pieces(s, sh, piece_rows)
 
