@@ -43,7 +43,7 @@ struct ZgScatter {
   uint32_t tile_a;    // decoded axis that is innermost in the encoded layout (tiled kernel)
   uint32_t tile_b;    // tiled kernel: axis batched TJ slabs per block (smallest encoded stride
                       // among the other axes: adjacent slabs are adjacent encoded rows); ZG_MAXD = none
-  uint32_t pad0;
+  uint32_t pad0;      // u16 unshuffle A/B (ZGPU_UNSHUFFLE_WIDE): 0 8-B plane loads, 1 / 2 16-B (nt / plain)
   uint64_t chunk_shape[ZG_MAXD];  // leaf decoded shape
   uint64_t enc_stride[ZG_MAXD];   // encoded linear stride (elements) of each decoded axis
   uint64_t out_stride[ZG_MAXD];   // output array C strides (elements)

@@ -96,6 +96,11 @@ __device__ __forceinline__ bool item_live(const ZgItem &it, uint32_t *status, ui
   return true;
 }
 
+__device__ __forceinline__ void store16(bool nt, uint8_t *d, uint4 v) {
+  if (nt) nt_store16(d, v);
+  else *(uint4 *)d = v;
+}
+
 // ---------------------------------------------------------------------------------------------
 // Rows: block = (item, group of ROWS rows). Row offsets are computed once per row into LDS.
 // ---------------------------------------------------------------------------------------------
@@ -178,6 +183,55 @@ __global__ __launch_bounds__(SCATTER_THREADS) void k_scatter_rows(
     for (uint32_t r = 0; r < nr && vec_ok; r++)
       vec_ok = (((s_src[r] - it.src) / es) % epv) == 0 && (s_dst[r] & 15) == 0;
     (void)s0;
+    if (vec_ok && es == 2 && P.pad0) {
+      // A/B (ZGPU_UNSHUFFLE_WIDE=1: non-temporal loads, 2: plain loads; off by default): u16 rows of
+      // whole 16-element units on 16-B aligned plane offsets, each unit one 16-B load per plane and
+      // two 16-B stores, two units per thread in flight. C5 with non-temporal loads: 71.8 ms against
+      // 70.8-71.1 with the 8-B plane loads below (profiles/r06/r06us_c5_unshuffle_wide_ab.txt)
+      bool wide = (L % 16) == 0 && (P.nelem % 16) == 0;
+      for (uint32_t r = 0; r < nr && wide; r++) wide = (((s_src[r] - it.src) / 2) % 16) == 0;
+      if (wide) {
+        const uint32_t upr = (uint32_t)(L / 16);
+        const uint32_t tot = nr * upr;
+        const uint8_t *base = (const uint8_t *)it.src;
+        for (uint32_t u0 = threadIdx.x; u0 < tot; u0 += 2 * SCATTER_THREADS) {
+          uint4 a[2], b[2];
+#pragma unroll
+          for (int q = 0; q < 2; q++) {
+            const uint32_t u = u0 + q * SCATTER_THREADS;
+            if (u < tot) {
+              const uint32_t r = u / upr, c = u % upr;
+              const uint64_t e0 = (s_src[r] - it.src) / 2 + (uint64_t)c * 16;
+              if (P.pad0 == 1) {
+                a[q] = nt_load16(base + e0);
+                b[q] = nt_load16(base + P.nelem + e0);
+              } else {
+                a[q] = *(const uint4 *)(base + e0);
+                b[q] = *(const uint4 *)(base + P.nelem + e0);
+              }
+            }
+          }
+#pragma unroll
+          for (int q = 0; q < 2; q++) {
+            const uint32_t u = u0 + q * SCATTER_THREADS;
+            if (u < tot) {
+              const uint32_t r = u / upr, c = u % upr;
+              const uint4 lo = swap ? b[q] : a[q], hi = swap ? a[q] : b[q];
+              uint8_t *d = (uint8_t *)(s_dst[r] + (uint64_t)c * 32);
+              store16(P.pad0 == 1, d, make_uint4(__builtin_amdgcn_perm(hi.x, lo.x, 0x05010400u),
+                                       __builtin_amdgcn_perm(hi.x, lo.x, 0x07030602u),
+                                       __builtin_amdgcn_perm(hi.y, lo.y, 0x05010400u),
+                                       __builtin_amdgcn_perm(hi.y, lo.y, 0x07030602u)));
+              store16(P.pad0 == 1, d + 16, make_uint4(__builtin_amdgcn_perm(hi.z, lo.z, 0x05010400u),
+                                            __builtin_amdgcn_perm(hi.z, lo.z, 0x07030602u),
+                                            __builtin_amdgcn_perm(hi.w, lo.w, 0x05010400u),
+                                            __builtin_amdgcn_perm(hi.w, lo.w, 0x07030602u)));
+            }
+          }
+        }
+        return;
+      }
+    }
     if (vec_ok) {
       const uint32_t vpr = (uint32_t)(L / epv);
       const uint32_t total = nr * vpr;

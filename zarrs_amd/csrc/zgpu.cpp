@@ -549,6 +549,10 @@ static void build_leaf_stages(zgpu_plan &P, const Chain &leaf, uint64_t nelem) {
   }
   P.slot_bytes = (max_slot + 255) & ~(uint64_t)255;
   P.scatter.shuffle = fused_shuffle;
+  {
+    const char *e = std::getenv("ZGPU_UNSHUFFLE_WIDE");  // A/B knob: 1 / 2 the 16-B unshuffle (scatter.hip)
+    P.scatter.pad0 = e ? (uint32_t)std::max(0, std::min(2, std::atoi(e))) : 0u;
+  }
 }
 
 // ShardingIndex decode spec (sharding.rs:136-235, sharding_codec.rs:1262-1298): the index chain
