@@ -457,7 +457,9 @@ class C3:
         self.scaling = "strong"
 
     def _box_slab(self, boxes):
-        """The slab (rows of the subset, whole on the other axes) that a rank's boxes span."""
+        """The slab (rows of the subset, whole on the other axes) that a rank's boxes span (empty: none)."""
+        if not boxes:
+            return list(self.SUB_START), [0] + list(self.SUB_SHAPE[1:])
         r0 = min(b0[0] for b0, _ in boxes)
         r1 = max(b0[0] + bs[0] for b0, bs in boxes)
         return [r0] + list(self.SUB_START[1:]), [r1 - r0] + list(self.SUB_SHAPE[1:])
