@@ -50,6 +50,48 @@ __global__ __launch_bounds__(CRC_THREADS) void k_crc32c_strip(ZgItem *items, uin
   }
 }
 
+// The trailing crc32c of C3's inner chain verified beside the one-wave k_gzip (which strips the 4 bytes
+// itself, crc_tail 3) on a side stream: reads a snapshot of the items and statuses taken before the
+// fork (k_gzip rewrites both), writes only bad[i]. k_crc32c_merge, after the join, makes a failed
+// checksum the item's status whatever k_gzip reported (the chain decodes crc32c first,
+// crc32c_codec.rs:108-141).
+__global__ __launch_bounds__(CRC_THREADS) void k_crc32c_check(const ZgItem *items, const uint32_t *status,
+                                                              uint32_t *bad) {
+  __shared__ CrcTables T;
+  __shared__ uint64_t s_len[CRC_THREADS / 64];
+  __shared__ uint32_t s_crc[CRC_THREADS / 64];
+  const uint32_t i = blockIdx.x;
+  const ZgItem it = items[i];
+  if (threadIdx.x == 0) bad[i] = 0;
+  if (status[i] || (it.flags & (ZG_ITEM_FILL | ZG_ITEM_PARTIAL)) || it.len < 4) return;
+  const uint8_t *data = (const uint8_t *)it.src;
+  const uint8_t *stored = data + it.len - 4;
+  build_tables(T, POLY_CRC32C);
+  const uint32_t c = wg_crc(data, it.len - 4, T, POLY_CRC32C, s_len, s_crc);
+  if (threadIdx.x == 0) {
+    const uint32_t st = stored[0] | stored[1] << 8 | stored[2] << 16 | (uint32_t)stored[3] << 24;
+    bad[i] = st != c;
+  }
+}
+
+__global__ void k_crc32c_merge(uint32_t *status, const uint32_t *bad, uint32_t n) {
+  const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i < n && bad[i]) status[i] = ZG_INVALID_CHECKSUM;
+}
+
+hipError_t launch_crc32c_check(const ZgItem *items, const uint32_t *status, uint32_t *bad, uint32_t n_items,
+                               hipStream_t s) {
+  if (!n_items) return hipSuccess;
+  hipLaunchKernelGGL(k_crc32c_check, dim3(n_items), dim3(CRC_THREADS), 0, s, items, status, bad);
+  return hipGetLastError();
+}
+
+hipError_t launch_crc32c_merge(uint32_t *status, const uint32_t *bad, uint32_t n_items, hipStream_t s) {
+  if (!n_items) return hipSuccess;
+  hipLaunchKernelGGL(k_crc32c_merge, dim3((n_items + 255) / 256), dim3(256), 0, s, status, bad, n_items);
+  return hipGetLastError();
+}
+
 hipError_t launch_crc32c_strip(ZgItem *items, uint32_t *status, uint32_t n_items, int at_start, int verify,
                                hipStream_t s) {
   if (!n_items) return hipSuccess;

@@ -1201,7 +1201,7 @@ __global__ __launch_bounds__(PIPE ? 128 : 64) __attribute__((amdgpu_waves_per_eu
   // The crc32c codec after gzip (C3's inner chain [bytes, gzip, crc32c]; crc32c_codec.rs:108-141)
   // folded into the pipelined kernel: the stream's last 4 bytes are its CRC-32C, which wave 1 checks
   // while wave 0 parses the first block header (crc_tail 1; 2: stripped, not verified).
-  if (PIPE && crc_tail) {
+  if ((PIPE || crc_tail == 3) && crc_tail) {  // crc_tail 3 (one-wave kernel): stripped, verified beside it
     if (in_len < 4) {
       if (lane == 0) status[item] = ZG_CRC_INPUT_TOO_SHORT;
       return;
@@ -2019,7 +2019,8 @@ uint64_t gzip_seg_scratch_bytes(uint32_t n_items) {
 }
 
 hipError_t launch_gzip(ZgItem *items, uint32_t *status, uint32_t n_items, uint8_t *dst, uint64_t slot_bytes,
-                       uint32_t *order, uint32_t *seg_scr, hipStream_t s, int crc_tail, const GzDirect *direct) {
+                       uint32_t *order, uint32_t *seg_scr, hipStream_t s, int crc_tail, const GzDirect *direct,
+                       const GzCrcFork *crc_fork) {
   const GzDirect gd = direct ? *direct : GzDirect{};
   if (!n_items) return hipSuccess;
   static const bool lpt = [] {
@@ -2031,9 +2032,30 @@ hipError_t launch_gzip(ZgItem *items, uint32_t *status, uint32_t n_items, uint8_
   const bool pipe = seg_scr && n_items <= gzip_pipe_max();  // few streams: the pipelined latency mode
   // a trailing crc32c: checked inside the pipelined kernel (its second wave is idle at the start), by
   // k_crc32c_strip ahead of the one-wave kernel (inside it the check cost more HBM traffic: r05cal)
+  int tail_mode = 0;  // what the one-wave kernel does with the trailing crc32c (3: strips it itself)
+  bool merge = false;
   if (crc_tail && !pipe) {
-    const hipError_t e = launch_crc32c_strip(items, status, n_items, 0, crc_tail == 1 ? 1 : 0, s);
-    if (e != hipSuccess) return e;
+    if (crc_fork) {
+      // verified on the side stream while k_gzip decodes (the check is HBM-bound, the decode latency-
+      // bound); a stripped-unverified tail (crc_tail 2) needs no check at all
+      tail_mode = 3;
+      if (crc_tail == 1) {
+        hipError_t e = hipMemcpyAsync(crc_fork->snap_items, items, (size_t)n_items * sizeof(ZgItem),
+                                      hipMemcpyDeviceToDevice, s);
+        if (e == hipSuccess)
+          e = hipMemcpyAsync(crc_fork->snap_status, status, (size_t)n_items * 4, hipMemcpyDeviceToDevice, s);
+        if (e == hipSuccess) e = hipEventRecord(crc_fork->ev_fork, s);
+        if (e == hipSuccess) e = hipStreamWaitEvent(crc_fork->side, crc_fork->ev_fork, 0);
+        if (e == hipSuccess)
+          e = launch_crc32c_check(crc_fork->snap_items, crc_fork->snap_status, crc_fork->bad, n_items, crc_fork->side);
+        if (e == hipSuccess) e = hipEventRecord(crc_fork->ev_join, crc_fork->side);
+        if (e != hipSuccess) return e;
+        merge = true;
+      }
+    } else {
+      const hipError_t e = launch_crc32c_strip(items, status, n_items, 0, crc_tail == 1 ? 1 : 0, s);
+      if (e != hipSuccess) return e;
+    }
   }
   if (order) hipLaunchKernelGGL(k_order_by_len, dim3(1), dim3(1024), 0, s, items, status, n_items, order);
   if (pipe)
@@ -2041,7 +2063,13 @@ hipError_t launch_gzip(ZgItem *items, uint32_t *status, uint32_t n_items, uint8_
                        nullptr, order, seg_scr, crc_tail, gd);
   else
     hipLaunchKernelGGL(k_gzip<false>, dim3(n_items), dim3(64), 0, s, items, status, nullptr, dst, slot_bytes, nullptr,
-                       order, seg_scr, 0, gd);
+                       order, seg_scr, tail_mode, gd);
+  if (merge) {
+    hipError_t e = hipGetLastError();
+    if (e == hipSuccess) e = hipStreamWaitEvent(s, crc_fork->ev_join, 0);
+    if (e == hipSuccess) e = launch_crc32c_merge(status, crc_fork->bad, n_items, s);
+    if (e != hipSuccess) return e;
+  }
   return hipGetLastError();
 }
 

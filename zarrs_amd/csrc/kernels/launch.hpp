@@ -85,9 +85,21 @@ hipError_t launch_item_resolve(ZgItem *items, uint32_t *status, uint32_t n_items
 // seg_scr: gzip_seg_scratch_bytes(n_items) of record scratch for the segmented symbol decode (NULL:
 // the lookahead decode); 0 bytes when that path is off (ZGPU_GZIP_SEG=0)
 uint64_t gzip_seg_scratch_bytes(uint32_t n_items);
+// A trailing crc32c verified on a side stream beside the one-wave gzip kernel (GzCrcFork; nullptr: by
+// k_crc32c_strip ahead of it): snapshots of n_items items and statuses, n_items flags.
+struct GzCrcFork {
+  hipStream_t side;
+  hipEvent_t ev_fork, ev_join;
+  ZgItem *snap_items;
+  uint32_t *snap_status, *bad;
+};
+hipError_t launch_crc32c_check(const ZgItem *items, const uint32_t *status, uint32_t *bad, uint32_t n_items,
+                               hipStream_t s);
+hipError_t launch_crc32c_merge(uint32_t *status, const uint32_t *bad, uint32_t n_items, hipStream_t s);
 hipError_t launch_gzip(ZgItem *items, uint32_t *status, uint32_t n_items, uint8_t *dst, uint64_t slot_bytes,
                        uint32_t *order, uint32_t *seg_scr, hipStream_t s, int crc_tail = 0,
-                       const GzDirect *direct = nullptr);  // direct: whole chunks into the output rows
+                       const GzDirect *direct = nullptr,  // direct: whole chunks into the output rows
+                       const GzCrcFork *crc_fork = nullptr);
 // zstd (RFC 8878) frame decode into dst slots: block-parallel (scan, per-block entropy decode,
 // per-item execution) with the serial one-wave-per-item decoder as the fallback.
 struct ZstdScratch {

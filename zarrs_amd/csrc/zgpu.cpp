@@ -390,7 +390,7 @@ struct zgpu_plan {
     size_t n = 0;
   };
   Grow bl_info, bl_bases, bl_subs, bl_sub_status, bl_sub_kind, bl_blocks, bl_tmp, bl_zblks, bl_znblk, bl_zmode,
-      bl_zlit, bl_zseq, bl_zaux, bl_zser, bl_lzl, bl_zseg, bl_zrec, bl_zalias, bl_znorm;
+      bl_zlit, bl_zseq, bl_zaux, bl_zser, bl_lzl, bl_zseg, bl_zrec, bl_zalias, bl_znorm, gz_crc;
   uint8_t *bl_h = nullptr;  // pinned: BlInfo read-back (first execution)
   size_t bl_h_n = 0;
   void *grow(Grow &g, size_t bytes) {
@@ -458,7 +458,7 @@ struct zgpu_plan {
       if (e) (void)hipEventDestroy(e);
     for (Grow *g : {&bl_info, &bl_bases, &bl_subs, &bl_sub_status, &bl_sub_kind, &bl_blocks, &bl_tmp, &bl_zblks,
                     &bl_znblk, &bl_zmode, &bl_zlit, &bl_zseq, &bl_zaux, &bl_zser, &bl_lzl, &bl_zseg, &bl_zrec, &bl_zalias,
-                    &bl_znorm})
+                    &bl_znorm, &gz_crc})
       ctx->dev_free(g->p);
     ctx->host_free(bl_h);
     ctx->host_free(h_ctl);
@@ -1144,8 +1144,28 @@ static void plan_enqueue(zgpu_plan &P, uint8_t *out, hipStream_t s) {
                             ((uintptr_t)out & 15) == 0;
         gd.dout = direct ? out : nullptr;
         gd.geom = P.d_geom;
+        // A/B (ZGPU_GZIP_CRC_FORK=1): the trailing crc32c checked on the plan's side stream beside the
+        // one-wave kernel instead of by k_crc32c_strip ahead of it. It loses on C3 (18.11-18.18 ms against
+        // 17.75-17.83 on one box, profiles/r06/r06cf_c3_gzip_crc_fork_ab.txt): the check's workgroups take
+        // CU slots from the latency-bound decode
+        GzCrcFork cf{};
+        const char *fe = std::getenv("ZGPU_GZIP_CRC_FORK");
+        const bool fork = crc_tail == 1 && fe && std::atoi(fe) != 0 && !(P.flags & ZGPU_ONE_STREAM);
+        if (fork) {
+          P.zstd_fork(P.zs, s);  // creates the plan's side stream and events (one compressor per chain)
+        }
+        if (fork && P.zside) {
+          const size_t nb = (size_t)ni * (sizeof(ZgItem) + 8);
+          uint8_t *scr = (uint8_t *)P.grow(P.gz_crc, nb);
+          cf.side = P.zside;
+          cf.ev_fork = P.zev[0];
+          cf.ev_join = P.zev[1];
+          cf.snap_items = (ZgItem *)scr;
+          cf.snap_status = (uint32_t *)(scr + (size_t)ni * sizeof(ZgItem));
+          cf.bad = cf.snap_status + ni;
+        }
         HIPCHK(launch_gzip(P.d_items, P.d_status, ni, P.d_pool[st.pool], P.slot_bytes, P.d_order, P.d_gz_seg, s,
-                           crc_tail, direct ? &gd : nullptr));
+                           crc_tail, direct ? &gd : nullptr, cf.side ? &cf : nullptr));
       }
         crc_tail = 0;
         break;
