@@ -152,7 +152,7 @@ def test_c3_chain_full_and_partial(ctx, c3, store, gzip_kernel, gz_direct, monke
     assert np.array_equal(got, exp_a)
 
 
-@pytest.mark.parametrize("gzip_kernel", ["pipelined", "one_wave"])
+@pytest.mark.parametrize("gzip_kernel", ["pipelined", "one_wave", "one_wave_crc_fork"])
 def test_c3_corrupt_gzip_header_checksum_first(ctx, c3, gzip_kernel, monkeypatch):
     """A corrupt gzip header inside an inner chunk: the chain decodes crc32c before gzip, so with the
     stored CRC-32C left as it was the full path reports INVALID_CHECKSUM (crc32c_codec.rs:108-141) on
@@ -160,8 +160,10 @@ def test_c3_corrupt_gzip_header_checksum_first(ctx, c3, gzip_kernel, monkeypatch
     corrupt stream the gzip decoder's CORRUPT_STREAM (gzip_codec.rs:110-120); the partial path strips
     the CRC-32C unverified and reports CORRUPT_STREAM either way."""
     from zarrs_amd import ZgpuError
-    if gzip_kernel == "one_wave":
+    if gzip_kernel.startswith("one_wave"):
         monkeypatch.setenv("ZGPU_GZIP_PIPE_MAX", "0")
+    if gzip_kernel == "one_wave_crc_fork":  # the check on a side stream beside the decode (opt-in A/B)
+        monkeypatch.setenv("ZGPU_GZIP_CRC_FORK", "1")
     a, co, shards = c3
     n_inner = (SHARD // INNER) ** 3
     key = (0, 1, 0)
