@@ -252,6 +252,11 @@ class Array:
                 elif self.store.device:
                     keep.append(v)
                     enc = (v.data_ptr(), v.numel())
+                    if not v.numel():  # an empty object is still present: give it a valid address (_tables)
+                        import torch
+                        t = torch.empty(1, dtype=torch.uint8, device=v.device)
+                        keep.append(t)
+                        enc = (t.data_ptr(), 0)
                 else:
                     b = np.frombuffer(v, dtype=np.uint8) if len(v) else np.zeros(1, np.uint8)
                     keep.append(b)
