@@ -40,7 +40,8 @@ constexpr __host__ __device__ int tiled_slabs(uint32_t es) { return es == 8 ? 2 
 
 hipError_t launch_scatter(const ZgItem *items, const uint64_t *geom, uint32_t *status, const ZgScatter &P,
                           uint8_t *out, uint32_t n_items, uint32_t mode, uint64_t units_per_item,
-                          hipStream_t s);
+                          hipStream_t s, uint32_t *live_scratch = nullptr);  // (n_items + 1) u32: rows mode
+                                                                            // over the items not yet written
 uint64_t scatter_units_per_item(uint32_t mode, const ZgScatter &P, const uint64_t *max_sel_shape);
 
 // Box copy between device arrays: run r (C order over the `outer` axes of `shape`) is run_bytes

@@ -107,12 +107,10 @@ __device__ __forceinline__ void store16(bool nt, uint8_t *d, uint4 v) {
 constexpr int ROWS_PER_BLOCK = 64;
 constexpr int SCATTER_THREADS = 256;
 
-__global__ __launch_bounds__(SCATTER_THREADS) void k_scatter_rows(
-    const ZgItem *__restrict__ items, const uint64_t *__restrict__ geom, uint32_t *__restrict__ status,
-    ZgScatter P, uint8_t *__restrict__ out, uint32_t blocks_per_item, uint64_t block_base) {
-  const uint64_t bid = block_base + blockIdx.x;
-  const uint32_t item = (uint32_t)(bid / blocks_per_item);
-  const uint32_t blk = (uint32_t)(bid % blocks_per_item);
+// One (item, group of ROWS_PER_BLOCK rows) unit of the rows scatter; every early exit is block-uniform.
+__device__ __forceinline__ void rows_unit(const ZgItem *__restrict__ items, const uint64_t *__restrict__ geom,
+                                          uint32_t *__restrict__ status, const ZgScatter &P,
+                                          uint8_t *__restrict__ out, uint32_t item, uint32_t blk) {
   const ZgItem it = items[item];
   if (!item_live(it, status, item, P)) return;
   const uint32_t nd = P.nd;
@@ -298,6 +296,34 @@ __global__ __launch_bounds__(SCATTER_THREADS) void k_scatter_rows(
       x = load_elem((const uint8_t *)(s_src[r] + c * es), es, P.comp, swap);
     }
     store_elem((uint8_t *)(s_dst[r] + c * es), x, es);
+  }
+}
+
+__global__ __launch_bounds__(SCATTER_THREADS) void k_scatter_rows(
+    const ZgItem *__restrict__ items, const uint64_t *__restrict__ geom, uint32_t *__restrict__ status,
+    ZgScatter P, uint8_t *__restrict__ out, uint32_t blocks_per_item, uint64_t block_base) {
+  const uint64_t bid = block_base + blockIdx.x;
+  rows_unit(items, geom, status, P, out, (uint32_t)(bid / blocks_per_item), (uint32_t)(bid % blocks_per_item));
+}
+
+// The items still to scatter after a stage that wrote most of them into the output itself
+// (ZG_ITEM_DIRECT: k_gzip's whole chunks): k_live_items lists them, and a grid of a few blocks per CU
+// walks their units -- a full grid spent most of its time dispatching blocks that only exit (C3: 195 k
+// of 250 k).
+__global__ void k_live_items(const ZgItem *__restrict__ items, const uint32_t *__restrict__ status, uint32_t n,
+                             uint32_t *__restrict__ list, uint32_t *__restrict__ count) {
+  const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i < n && !status[i] && !(items[i].flags & ZG_ITEM_DIRECT)) list[atomicAdd(count, 1u)] = i;
+}
+
+__global__ __launch_bounds__(SCATTER_THREADS) void k_scatter_rows_list(
+    const ZgItem *__restrict__ items, const uint64_t *__restrict__ geom, uint32_t *__restrict__ status,
+    ZgScatter P, uint8_t *__restrict__ out, uint32_t blocks_per_item, const uint32_t *__restrict__ list,
+    const uint32_t *__restrict__ count) {
+  const uint64_t total = (uint64_t)*count * blocks_per_item;
+  for (uint64_t w = blockIdx.x; w < total; w += gridDim.x) {
+    __syncthreads();  // the previous unit's row tables are no longer read
+    rows_unit(items, geom, status, P, out, list[w / blocks_per_item], (uint32_t)(w % blocks_per_item));
   }
 }
 
@@ -489,9 +515,23 @@ __global__ __launch_bounds__(SCATTER_THREADS) void k_scatter_generic(
 // ---------------------------------------------------------------------------------------------
 hipError_t launch_scatter(const ZgItem *items, const uint64_t *geom, uint32_t *status, const ZgScatter &P,
                           uint8_t *out, uint32_t n_items, uint32_t mode, uint64_t units_per_item,
-                          hipStream_t s) {
+                          hipStream_t s, uint32_t *live_scratch) {
   if (n_items == 0 || units_per_item == 0) return hipSuccess;
   if (units_per_item > 0xFFFFFFFFull) return hipErrorInvalidConfiguration;
+  if (live_scratch && mode == SCATTER_ROWS) {  // [count | list of n_items]
+    hipError_t e = hipMemsetAsync(live_scratch, 0, 4, s);
+    if (e != hipSuccess) return e;
+    hipLaunchKernelGGL(k_live_items, dim3((n_items + 255) / 256), dim3(256), 0, s, items, status, n_items,
+                       live_scratch + 1, live_scratch);
+    int dev = 0, ncu = 0;
+    if (hipGetDevice(&dev) != hipSuccess || hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, dev) !=
+                                                 hipSuccess || ncu <= 0)
+      ncu = 256;
+    const uint64_t g = std::min<uint64_t>((uint64_t)n_items * units_per_item, (uint64_t)ncu * 8);
+    hipLaunchKernelGGL(k_scatter_rows_list, dim3((uint32_t)g), dim3(SCATTER_THREADS), 0, s, items, geom, status, P,
+                       out, (uint32_t)units_per_item, live_scratch + 1, live_scratch);
+    return hipGetLastError();
+  }
   const uint64_t total = (uint64_t)n_items * units_per_item;
   const uint32_t u = (uint32_t)units_per_item;
   // gridDim.x * blockDim.x must stay below 2^32: launch the block range in slices

@@ -390,7 +390,7 @@ struct zgpu_plan {
     size_t n = 0;
   };
   Grow bl_info, bl_bases, bl_subs, bl_sub_status, bl_sub_kind, bl_blocks, bl_tmp, bl_zblks, bl_znblk, bl_zmode,
-      bl_zlit, bl_zseq, bl_zaux, bl_zser, bl_lzl, bl_zseg, bl_zrec, bl_zalias, bl_znorm, gz_crc;
+      bl_zlit, bl_zseq, bl_zaux, bl_zser, bl_lzl, bl_zseg, bl_zrec, bl_zalias, bl_znorm, gz_crc, live_list;
   uint8_t *bl_h = nullptr;  // pinned: BlInfo read-back (first execution)
   size_t bl_h_n = 0;
   void *grow(Grow &g, size_t bytes) {
@@ -458,7 +458,7 @@ struct zgpu_plan {
       if (e) (void)hipEventDestroy(e);
     for (Grow *g : {&bl_info, &bl_bases, &bl_subs, &bl_sub_status, &bl_sub_kind, &bl_blocks, &bl_tmp, &bl_zblks,
                     &bl_znblk, &bl_zmode, &bl_zlit, &bl_zseq, &bl_zaux, &bl_zser, &bl_lzl, &bl_zseg, &bl_zrec, &bl_zalias,
-                    &bl_znorm, &gz_crc})
+                    &bl_znorm, &gz_crc, &live_list})
       ctx->dev_free(g->p);
     ctx->host_free(bl_h);
     ctx->host_free(h_ctl);
@@ -1128,6 +1128,7 @@ static void plan_enqueue(zgpu_plan &P, uint8_t *out, hipStream_t s) {
     }
   }
   int crc_tail = 0;  // a trailing crc32c stage handed to the next gzip stage (launch_gzip places it)
+  bool wrote_direct = false;  // a stage wrote whole items into the output (the scatter lists the rest)
   for (size_t si = 0; si < P.stages.size(); si++) {
     const Stage &st = P.stages[si];
     switch (st.kind) {
@@ -1166,6 +1167,7 @@ static void plan_enqueue(zgpu_plan &P, uint8_t *out, hipStream_t s) {
         }
         HIPCHK(launch_gzip(P.d_items, P.d_status, ni, P.d_pool[st.pool], P.slot_bytes, P.d_order, P.d_gz_seg, s,
                            crc_tail, direct ? &gd : nullptr, cf.side ? &cf : nullptr));
+        wrote_direct = wrote_direct || direct;
       }
         crc_tail = 0;
         break;
@@ -1182,8 +1184,15 @@ static void plan_enqueue(zgpu_plan &P, uint8_t *out, hipStream_t s) {
         break;
     }
   }
-  if (!P.no_scatter)
-    HIPCHK(launch_scatter(items, P.d_geom, P.d_status, P.scatter, out, ni, P.scatter_mode, P.scatter_units, s));
+  if (!P.no_scatter) {
+    // after the gzip direct rows most items are in the output already: the rows scatter walks a list of
+    // the others (ZGPU_SCATTER_LIST=1; default: the full grid, every written item's blocks exiting at once)
+    const char *le = std::getenv("ZGPU_SCATTER_LIST");
+    uint32_t *live = nullptr;
+    if (wrote_direct && le && std::atoi(le) != 0)
+      live = (uint32_t *)P.grow(P.live_list, ((size_t)ni + 1) * 4);
+    HIPCHK(launch_scatter(items, P.d_geom, P.d_status, P.scatter, out, ni, P.scatter_mode, P.scatter_units, s, live));
+  }
 }
 
 // InvalidBytesLengthError{len, expected_len} of descriptor d's first mismatching leaf item: the item's
