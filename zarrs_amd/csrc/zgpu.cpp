@@ -1185,8 +1185,9 @@ static void plan_enqueue(zgpu_plan &P, uint8_t *out, hipStream_t s) {
     }
   }
   if (!P.no_scatter) {
-    // after the gzip direct rows most items are in the output already: the rows scatter walks a list of
-    // the others (ZGPU_SCATTER_LIST=1; default: the full grid, every written item's blocks exiting at once)
+    // A/B (ZGPU_SCATTER_LIST=1): after the gzip direct rows, the rows scatter over a device-built list
+    // of the items still to write instead of the full grid whose written items' blocks exit at once;
+    // it lost on C3 (18.22-18.33 vs 17.87-17.94 ms, profiles/r06/r06sl_c3_scatter_list_ab.txt)
     const char *le = std::getenv("ZGPU_SCATTER_LIST");
     uint32_t *live = nullptr;
     if (wrote_direct && le && std::atoi(le) != 0)
